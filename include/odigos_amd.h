@@ -1,0 +1,263 @@
+/*
+ * odigos_amd.h — C ABI of the MI355X span-processing engine.
+ *
+ * This is the drop-in boundary for the three gateway trace processors of the
+ * Odigos collector (reference: damemi/odigos @ 2026-02-13):
+ *
+ *   odigossampling       collector/processors/odigossamplingprocessor
+ *   odigosurltemplate    collector/processors/odigosurltemplateprocessor
+ *   odigostrafficmetrics collector/processors/odigostrafficmetrics
+ *
+ * In the reference each processor is a Go processor.Factory whose
+ * processorhelper.ProcessTracesFunc walks a ptrace.Traces
+ * (odigossamplingprocessor/processor.go:16-21, odigosurltemplateprocessor/
+ * processor.go:71-96, odigostrafficmetrics/processor.go:71-84).  A cgo shim
+ * that keeps the Go Factory / Config / mapstructure tags columnarises each
+ * batch into the struct-of-arrays described by ose_columns, calls
+ * ose_process*, and applies the results (RemoveIf, PutStr, SetName, counter
+ * Add).  See INTEGRATION.md for the shim.
+ *
+ * Conventions: every entry point returns 0 on success or a negative
+ * errno-style code (OSE_E*); nothing throws across the ABI; the message of the
+ * last failure on the calling thread is returned by ose_last_error().  All
+ * entry points are re-entrant; one engine may be used from many threads
+ * (each call takes its own HIP stream and workspace from a pool).
+ */
+#ifndef ODIGOS_AMD_H
+#define ODIGOS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OSE_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------- */
+#define OSE_OK        0
+#define OSE_EINVAL  (-22) /* bad argument / invalid config (Validate error) */
+#define OSE_ENOMEM  (-12) /* host or device allocation failed               */
+#define OSE_ENOTSUP (-95) /* config uses a feature the engine cannot run     */
+#define OSE_EDEVICE (-5)  /* HIP runtime error, or no MI355X visible         */
+#define OSE_ERANGE  (-34) /* batch exceeds a 32-bit arena/offset limit       */
+#define OSE_ETIMEDOUT (-110) /* an in-kernel bounded spin gave up            */
+
+#define OSE_NONE 0xFFFFFFFFu   /* "no value" for interned-id columns */
+
+/* ---- OTLP enums (ptrace.SpanKind / ptrace.StatusCode values) -------- */
+#define OSE_KIND_UNSPECIFIED 0
+#define OSE_KIND_INTERNAL    1
+#define OSE_KIND_SERVER      2
+#define OSE_KIND_CLIENT      3
+#define OSE_KIND_PRODUCER    4
+#define OSE_KIND_CONSUMER    5
+#define OSE_STATUS_UNSET 0
+#define OSE_STATUS_OK    1
+#define OSE_STATUS_ERROR 2
+
+/* ---- per-span url_flags (columnarised by the shim) ------------------
+ * Mirrors what odigosurltemplateprocessor/processor.go reads from the span
+ * attribute map:
+ *   HAS_METHOD      getHttpMethod found http.request.method or http.method
+ *                   (processor.go:98-111)
+ *   TGT_*           state of the target attribute (http.route for SERVER,
+ *                   url.template for CLIENT) as read by enhanceSpan
+ *                   (processor.go:235-252)
+ *   NAME_EQ_METHOD  span.Name() == AsString(method) (updateHttpSpanName,
+ *                   processor.go:214-233)
+ *   PATH_*          which source calculateTemplatedUrlFromAttr uses
+ *                   (processor.go:113-147, 188-212): RAW = url.path, or the
+ *                   Path of url.full/http.url after net/url.Parse on the host;
+ *                   TARGET = http.target, the engine cuts at the first '?';
+ *                   NONE = no source, or url.Parse failed.                     */
+#define OSE_URL_HAS_METHOD      0x01u
+#define OSE_URL_TGT_MASK        0x06u
+#define OSE_URL_TGT_ABSENT      0x00u
+#define OSE_URL_TGT_STR_EMPTY   0x02u
+#define OSE_URL_TGT_STR         0x04u
+#define OSE_URL_TGT_NONSTR      0x06u
+#define OSE_URL_NAME_EQ_METHOD  0x08u
+#define OSE_URL_PATH_MASK       0x30u
+#define OSE_URL_PATH_NONE       0x00u
+#define OSE_URL_PATH_RAW        0x10u
+#define OSE_URL_PATH_TARGET     0x20u
+
+/* ---- per-span url_out (results) ------------------------------------ */
+#define OSE_OUT_SET_ATTR 0x01u  /* attr.PutStr(target, tmpl)             */
+#define OSE_OUT_RENAME   0x02u  /* span.SetName(method + " " + tmpl)     */
+
+/* ---- stage mask ------------------------------------------------------ */
+#define OSE_STAGE_SAMPLE   0x1u  /* odigossampling       */
+#define OSE_STAGE_TEMPLATE 0x2u  /* odigosurltemplate    */
+#define OSE_STAGE_SIZE     0x4u  /* odigostrafficmetrics */
+
+/* ---- grouping of spans into "traces" for odigossampling --------------
+ * TRACE_ID: spans sharing a 128-bit trace_id form one trace (the contract
+ *   groupbytrace establishes upstream, sampling_controller.go:193-220).
+ * BATCH: the whole batch is one trace, exactly as RuleEngine.ShouldSample
+ *   treats one ConsumeTraces call (rule_engine.go:55-83).                   */
+#define OSE_GROUP_TRACE_ID 0u
+#define OSE_GROUP_BATCH    1u
+
+/* ---- injected randomness ---------------------------------------------
+ * The reference draws rand.Float64() from Go's auto-seeded global source
+ * (rule_engine.go:68,79; odigostrafficmetrics/processor.go:72), which is not
+ * reproducible.  The engine instead uses, per trace,
+ *   u = (splitmix64(tid_hi ^ rotl64(tid_lo, 29) ^ seed) >> 11) * 2^-53
+ * and keeps the trace iff u*100 < ratio; the traffic gate uses traffic_u
+ * (one draw per batch = per ConsumeTraces call).                          */
+typedef struct ose_rand {
+  uint64_t seed;
+  double traffic_u;   /* in [0,1); the traffic stage runs iff traffic_u < sampling_ratio */
+} ose_rand;
+
+typedef struct ose_strref {
+  uint32_t off;   /* byte offset into the arena */
+  uint32_t len;   /* byte length                */
+} ose_strref;
+
+/* ---- columnar batch ----------------------------------------------------
+ * Spans are in pdata traversal order (ResourceSpans -> ScopeSpans -> Span),
+ * so `resource` and `scope` are non-decreasing.  A pointer may be NULL when
+ * no requested stage reads it.  For ose_process_device every pointer is a
+ * device pointer; for ose_process they point into an ose_batch.            */
+typedef struct ose_columns {
+  uint64_t n_spans;
+  uint32_t n_resources;
+  uint32_t n_scopes;
+  uint32_t n_attrsets;      /* traffic-metrics attribute sets (res_attrset range) */
+  uint32_t _pad;
+  uint64_t arena_bytes;
+  const uint8_t* arena;     /* all string bytes referenced by ose_strref columns */
+
+  /* per span */
+  const uint64_t* trace_id;   /* [2*n]: {hi, lo}: bytes 0..7 and 8..15, big-endian */
+  const uint64_t* start_ns;   /* StartTimestamp */
+  const uint64_t* end_ns;     /* EndTimestamp */
+  const uint8_t* status;      /* Status().Code() */
+  const uint8_t* kind;        /* Kind() */
+  const uint32_t* resource;   /* index of the span's ResourceSpans */
+  const uint32_t* scope;      /* index of the span's ScopeSpans */
+  const uint8_t* url_flags;   /* OSE_URL_* */
+  const ose_strref* path;     /* url path bytes per url_flags PATH_* */
+  const ose_strref* route;    /* AsString(http.route) before templating; len 0 if absent */
+  const uint32_t* span_size;  /* wire size of the Span message before mutation */
+  const uint32_t* name_len;   /* len(span.Name()) before mutation */
+
+  /* per resource */
+  const uint32_t* res_svc;      /* ose_engine_service_id(AsString(service.name)) or OSE_NONE */
+  const uint32_t* res_svc_str;  /* same, only if service.name is ValueTypeStr, else OSE_NONE */
+  const uint8_t* res_url_ok;    /* include/exclude PropertiesMatcher verdict (filtermatcher.go) */
+  const uint32_t* res_attrset;  /* interned attributeSetFromResource (processor.go:60-69) */
+  const uint32_t* res_size;     /* ResourceSpans bytes excluding its scope_spans fields */
+
+  /* per scope */
+  const uint32_t* scope_size;   /* ScopeSpans bytes excluding its spans fields */
+} ose_columns;
+
+/* ---- results -----------------------------------------------------------
+ * Any pointer may be NULL when its stage is not requested.                 */
+typedef struct ose_outputs {
+  /* odigossampling */
+  uint8_t* keep;              /* [n_spans] 1 if the span's trace is sampled */
+  uint32_t* trace_count;      /* [1] number of traces found (optional) */
+  uint32_t* trace_first_span; /* [n_spans cap] first span of each trace (optional) */
+  uint8_t* trace_keep;        /* [n_spans cap] decision per trace (optional) */
+  uint8_t* trace_level;       /* [n_spans cap] 0..2 satisfied level, 3 fallback, 4 none */
+  double* trace_ratio;        /* [n_spans cap] ratio drawn against (100 when level 4) */
+
+  /* odigosurltemplate */
+  uint8_t* url_out;           /* [n_spans] OSE_OUT_* */
+  ose_strref* tmpl;           /* [n_spans] template (valid where url_out != 0) */
+  uint8_t* tmpl_arena;        /* output bytes */
+  uint64_t tmpl_arena_cap;
+  uint64_t* tmpl_arena_used;  /* [1] bytes written */
+
+  /* odigostrafficmetrics (ADDED to, so counters accumulate across calls) */
+  int64_t* attrset_bytes;     /* [n_attrsets] otelcol_odigos_trace_data_size */
+  int64_t* accepted_spans;    /* [1] otelcol_odigos_accepted_spans */
+  uint64_t* res_bytes;        /* [n_resources] ResourceSpansSize after mutation (optional) */
+
+  /* device-side failure bits OR-ed in by the kernels (ose_process_device
+   * only; the caller zeroes it and checks after synchronising):
+   * 1 = in-kernel bounded spin gave up, 2 = tmpl_arena_cap too small */
+  uint32_t* device_status;
+} ose_outputs;
+
+typedef struct ose_engine ose_engine;
+typedef struct ose_batch ose_batch;
+
+/* Replaces the three processor.Factory.CreateTraces paths
+ * (odigossamplingprocessor/factory.go:29-45 -> config.go:17-80 Validate;
+ *  odigosurltemplateprocessor/factory.go:31-44 -> processor.go:27-69;
+ *  odigostrafficmetrics/factory.go:34-47 -> processor.go:31-58).
+ * cfg_json: {"odigossampling": {...}, "odigosurltemplate": {...},
+ *            "odigostrafficmetrics": {...}} with the mapstructure keys of the
+ * Go Config structs; absent sections are absent processors.  Validates
+ * exactly as the Go Validate() does (same messages) and compiles every user
+ * regexp to a DFA; a regexp the DFA compiler cannot express is OSE_ENOTSUP
+ * (there is no host fallback).                                              */
+int ose_engine_create(const char* cfg_json, ose_engine** out);
+void ose_engine_destroy(ose_engine* eng);
+
+/* Interned id of a service name referenced by a sampling rule, or OSE_NONE.
+ * The shim uses it to fill res_svc / res_svc_str (rule_engine callers compare
+ * service.name by equality only: latency.go:55, servicename.go:40).        */
+uint32_t ose_engine_service_id(const ose_engine* eng, const char* name, size_t len);
+
+/* Static per-engine facts the shim needs (OSE_STAGE_* bitmask of configured
+ * processors; max output bytes per input path byte for tmpl_arena sizing). */
+typedef struct ose_engine_info {
+  uint32_t stages;
+  uint32_t max_template_name;   /* longest "{name}" body the templater can emit */
+  int64_t inverse_sampling;     /* odigostrafficmetrics int64(1/sampling_ratio) */
+  double traffic_sampling_ratio;
+} ose_engine_info;
+int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info);
+
+/* Pinned host staging: the engine owns the memory (cgo: no Go pointers are
+ * retained).  dims->n_spans, n_resources, n_scopes, n_attrsets and
+ * arena_bytes size the buffers; the returned columns/outputs point into
+ * pinned memory the shim fills / reads.                                     */
+int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out);
+ose_columns* ose_batch_columns(ose_batch* b);
+ose_outputs* ose_batch_outputs(ose_batch* b);
+void ose_batch_release(ose_batch* b);
+
+/* Synchronous: H2D of the batch, stages in `stage_mask`, D2H of results.
+ * Replaces one ProcessTracesFunc call of each selected processor, run in
+ * gateway pipeline order sample -> template -> size
+ * (common/pipelinegen/config_builder.go:215-229).                           */
+int ose_process(ose_engine* eng, ose_batch* b, uint32_t stage_mask,
+                uint32_t group_mode, const ose_rand* rnd);
+
+/* Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream):
+ * columns/outputs are device pointers already resident in HBM.  This is the
+ * entry point the benchmark times.                                          */
+int ose_process_device(ose_engine* eng, const ose_columns* cols,
+                       const ose_outputs* outs, uint32_t stage_mask,
+                       uint32_t group_mode, const ose_rand* rnd, void* hip_stream);
+
+/* Workspace pre-sizing for ose_process_device (so the timed call performs no
+ * allocation and can be captured into a hipGraph).                          */
+int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes);
+
+/* Per-kernel device time, measured with hipEvents recorded on the stream
+ * each kernel is launched on (diagnostics and bench.py; off by default).
+ * ose_profile_read writes {"<kernel>": {"launches": n, "ms": total}, ...}
+ * and resets the counters; it synchronises the recorded events.           */
+int ose_profile_enable(ose_engine* eng, int on);
+int ose_profile_read(ose_engine* eng, char* json, size_t cap);
+
+/* Message of the last failure on this thread ("" if none). */
+const char* ose_last_error(void);
+
+/* Runtime facts for diagnostics: device name, gfx arch, CU count. */
+int ose_device_info(char* buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ODIGOS_AMD_H */

@@ -1,0 +1,182 @@
+"""Device-resident columnar batches for ``ose_process_device``.
+
+PyTorch is used only as the HBM allocator / stream / copy engine: every
+column is a flat ``torch.uint8`` tensor whose data pointer is handed to the
+C ABI.  Also wraps the seeded synthetic generator (libosegen.so).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+from . import native
+
+# element size and the dimension each column is indexed by
+COLUMN_LAYOUT = {
+    "arena": ("arena", 1),
+    "trace_id": ("span", 16), "start_ns": ("span", 8), "end_ns": ("span", 8), "status": ("span", 1),
+    "kind": ("span", 1), "resource": ("span", 4), "scope": ("span", 4), "url_flags": ("span", 1),
+    "path": ("span", 8), "route": ("span", 8), "span_size": ("span", 4), "name_len": ("span", 4),
+    "res_svc": ("res", 4), "res_svc_str": ("res", 4), "res_url_ok": ("res", 1), "res_attrset": ("res", 4),
+    "res_size": ("res", 4), "scope_size": ("scope", 4),
+}
+OUTPUT_LAYOUT = {
+    "keep": ("span", 1), "trace_count": ("one", 4), "trace_first_span": ("span", 4), "trace_keep": ("span", 1),
+    "trace_level": ("span", 1), "trace_ratio": ("span", 8), "url_out": ("span", 1), "tmpl": ("span", 8),
+    "attrset_bytes": ("attrset", 8), "accepted_spans": ("one", 8), "res_bytes": ("res", 8),
+    "device_status": ("one", 16),
+}
+
+
+def _count(cols, dim: str) -> int:
+    return {"span": cols.n_spans, "res": cols.n_resources, "scope": cols.n_scopes, "arena": cols.arena_bytes,
+            "attrset": cols.n_attrsets, "one": 1}[dim]
+
+
+def host_array(ptr: int, nbytes: int) -> np.ndarray:
+    if nbytes == 0 or not ptr:
+        return np.zeros(0, dtype=np.uint8)
+    return np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(ptr))
+
+
+class Generator:
+    """Seeded synthetic batch (odigos_amd/csrc/gen_batch.cpp)."""
+    LIB = Path(__file__).resolve().parent / "_lib" / "libosegen.so"
+    _L = None
+
+    def __init__(self, workload: str, seed: int, n_spans: int, threads: int = 8, shuffle: bool = False):
+        if Generator._L is None:
+            L = C.CDLL(str(self.LIB))
+            L.osegen_create.restype = C.c_void_p
+            L.osegen_create.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int]
+            L.osegen_columns.restype = C.POINTER(native.Columns)
+            L.osegen_columns.argtypes = [C.c_void_p]
+            L.osegen_free.argtypes = [C.c_void_p]
+            Generator._L = L
+        self.h = Generator._L.osegen_create(workload.encode(), seed, n_spans, threads, int(shuffle))
+        self.cols = Generator._L.osegen_columns(self.h).contents
+        self.workload = workload
+
+    def array(self, field: str) -> np.ndarray:
+        dim, size = COLUMN_LAYOUT[field]
+        n = _count(self.cols, dim) * size
+        if field == "arena":
+            n = (n + 15) // 16 * 16 + 16
+        return host_array(getattr(self.cols, field), n)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            Generator._L.osegen_free(self.h)
+            self.h = None
+
+
+class HostOutputs:
+    """Host output buffers (numpy) for the oracle."""
+
+    def __init__(self, cols: native.Columns, tmpl_cap: int | None = None):
+        self.bufs = {}
+        self.outs = native.Outputs()
+        for name, (dim, size) in OUTPUT_LAYOUT.items():
+            a = np.zeros(max(_count(cols, dim) * size, 16), dtype=np.uint8)
+            self.bufs[name] = a
+            setattr(self.outs, name, a.ctypes.data)
+        cap = tmpl_cap if tmpl_cap is not None else int(2 * cols.arena_bytes + 16 * cols.n_spans + 4096)
+        self.bufs["tmpl_arena"] = np.zeros(cap + 16, dtype=np.uint8)
+        self.outs.tmpl_arena = self.bufs["tmpl_arena"].ctypes.data
+        self.outs.tmpl_arena_cap = cap
+        self.used = np.zeros(1, dtype=np.uint64)
+        self.outs.tmpl_arena_used = self.used.ctypes.data
+
+    def view(self, name, dtype):
+        return self.bufs[name].view(dtype)
+
+
+class DeviceBatch:
+    """Columns + outputs resident in HBM (torch uint8 tensors)."""
+
+    def __init__(self, host_cols: native.Columns, device="cuda", tmpl_cap: int | None = None, fields=None):
+        import torch
+        self.torch = torch
+        self.cols = native.Columns()
+        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes"):
+            setattr(self.cols, f, getattr(host_cols, f))
+        self.t = {}
+        for name, (dim, size) in COLUMN_LAYOUT.items():
+            if fields is not None and name not in fields:
+                continue
+            n = _count(host_cols, dim) * size
+            if name == "arena":
+                n = (n + 15) // 16 * 16 + 16
+            src = host_array(getattr(host_cols, name), n)
+            t = torch.zeros(max(n, 16) + 16, dtype=torch.uint8, device=device)
+            if n:
+                t[:n].copy_(torch.from_numpy(src))
+            self.t[name] = t
+            setattr(self.cols, name, t.data_ptr())
+        self.outs = native.Outputs()
+        self.o = {}
+        for name, (dim, size) in OUTPUT_LAYOUT.items():
+            n = max(_count(host_cols, dim) * size, 16)
+            t = torch.zeros(n + 16, dtype=torch.uint8, device=device)
+            self.o[name] = t
+            setattr(self.outs, name, t.data_ptr())
+        cap = tmpl_cap if tmpl_cap is not None else int(2 * host_cols.arena_bytes + 16 * host_cols.n_spans + 4096)
+        self.o["tmpl_arena"] = torch.zeros(cap + 16, dtype=torch.uint8, device=device)
+        self.outs.tmpl_arena = self.o["tmpl_arena"].data_ptr()
+        self.outs.tmpl_arena_cap = cap
+        self.o["used"] = torch.zeros(2, dtype=torch.int64, device=device)
+        self.outs.tmpl_arena_used = self.o["used"].data_ptr()
+
+    def out_numpy(self, name: str, dtype=np.uint8) -> np.ndarray:
+        return self.o[name].cpu().numpy().view(dtype)
+
+    def used(self) -> int:
+        return int(self.o["used"][0].item())
+
+
+class Engine:
+    """ose_engine handle (product path: raises if the HIP library cannot run)."""
+
+    def __init__(self, cfg: dict):
+        from .host import dumps
+        self.L = native.lib()
+        h = C.c_void_p()
+        native.check(self.L.ose_engine_create(dumps(cfg).encode(), C.byref(h)))
+        self.h = h
+
+    def info(self) -> native.EngineInfo:
+        i = native.EngineInfo()
+        native.check(self.L.ose_engine_get_info(self.h, C.byref(i)))
+        return i
+
+    def service_id(self, name: str) -> int:
+        b = name.encode()
+        return self.L.ose_engine_service_id(self.h, b, len(b))
+
+    def reserve(self, n_spans: int, arena_bytes: int = 0):
+        native.check(self.L.ose_reserve(self.h, n_spans, arena_bytes))
+
+    def process_device(self, db: DeviceBatch, stages: int, group_mode: int = native.GROUP_TRACE_ID,
+                       seed: int = 0, traffic_u: float = 0.0, stream=None):
+        rnd = native.Rand(seed, traffic_u)
+        s = None if stream is None else C.c_void_p(stream)
+        native.check(self.L.ose_process_device(self.h, C.byref(db.cols), C.byref(db.outs), stages, group_mode,
+                                               C.byref(rnd), s))
+
+    def profile(self, on: bool = True):
+        native.check(self.L.ose_profile_enable(self.h, int(on)))
+
+    def profile_read(self) -> dict:
+        import json
+        buf = C.create_string_buffer(1 << 16)
+        native.check(self.L.ose_profile_read(self.h, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ose_engine_destroy(self.h)
+            self.h = None
+
+    __del__ = close

@@ -1,0 +1,474 @@
+// engine.cpp — the C ABI (include/odigos_amd.h): config decoding/validation,
+// compilation of the read-only device tables, workspaces, kernel launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <map>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/odigos_amd.h"
+#include "config.hpp"
+#include "devcfg.hpp"
+#include "engine_internal.hpp"
+#include "kernels.hpp"
+#include "regex_dfa.hpp"
+
+namespace ose {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) return fail(OSE_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+
+// ---------------- blob builder ----------------
+struct Blob {
+  std::vector<uint8_t> b;
+  uint32_t align() {
+    while (b.size() % 16) b.push_back(0);
+    return (uint32_t)b.size();
+  }
+  template <typename T>
+  uint32_t put(const T* p, size_t n) {
+    uint32_t off = align();
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(p);
+    b.insert(b.end(), s, s + n * sizeof(T));
+    return off;
+  }
+  template <typename T>
+  T* at(uint32_t off) { return reinterpret_cast<T*>(b.data() + off); }
+};
+
+uint32_t put_dfa(Blob& bl, const Dfa& d) {
+  DfaDev h{};
+  h.nclasses = d.nclasses;
+  h.nstates = d.nstates;
+  h.start = d.start;
+  h.match = d.match;
+  h.hi_n = (uint32_t)d.hi_lo.size();
+  std::memcpy(h.ascii, d.ascii_class, 128);
+  uint32_t off = bl.put(&h, 1);
+  std::vector<uint32_t> hr;
+  for (size_t k = 0; k < d.hi_lo.size(); k++) { hr.push_back(d.hi_lo[k]); hr.push_back(d.hi_hi[k]); hr.push_back(d.hi_cls[k]); }
+  uint32_t hoff = bl.put(hr.data(), hr.size());
+  uint32_t toff = bl.put(d.trans.data(), d.trans.size());
+  uint32_t aoff = bl.put(d.accept_end.data(), d.accept_end.size());
+  DfaDev* hp = bl.at<DfaDev>(off);
+  hp->hi_off = hoff;
+  hp->trans_off = toff;
+  hp->acc_off = aoff;
+  return off;
+}
+
+}  // namespace
+
+// odigosurltemplate tables: newUrlTemplateProcessor (processor.go:27-69)
+// groups rules by segment count keeping config order; custom ids default
+// their name to "id".
+int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32_t& max_name) {
+  Blob bl;
+  UrlCfgDev h{};
+  bl.put(&h, 1);
+  std::string bytes;
+  std::vector<NameDev> names;
+  auto add_text = [&](const std::string& s) {
+    NameDev n{(uint32_t)bytes.size(), (uint32_t)s.size()};
+    bytes += s;
+    return n;
+  };
+  names.push_back(add_text("id"));
+  names.push_back(add_text("date"));
+  names.push_back(add_text("email"));
+  std::vector<Dfa> dfas;
+  auto compile = [&](const std::string& rx, int32_t& idx) -> int {
+    Dfa d;
+    std::string err;
+    RegexStatus st = compile_dfa(rx, d, err);
+    if (st == RegexStatus::Syntax) return fail(OSE_EINVAL, err);
+    if (st != RegexStatus::Ok) return fail(OSE_ENOTSUP, "regexp not supported by the DFA compiler: " + err);
+    idx = (int32_t)dfas.size();
+    dfas.push_back(std::move(d));
+    return 0;
+  };
+  std::vector<UrlCustomDev> custom;
+  for (auto& ci : c.custom_ids) {
+    UrlCustomDev cd{};
+    int rc = compile(ci.regexp, cd.dfa);
+    if (rc) return rc;
+    cd.name = (uint32_t)names.size();
+    names.push_back(add_text(ci.template_name.empty() ? "id" : ci.template_name));
+    custom.push_back(cd);
+  }
+  struct ParsedRule { uint32_t nseg; size_t order; std::vector<RuleSegment> segs; };
+  std::vector<ParsedRule> rules;
+  for (size_t k = 0; k < c.templatization_rules.size(); k++) {
+    ParsedRule pr;
+    std::string e = parse_user_rule(c.templatization_rules[k], pr.segs);
+    if (!e.empty()) return fail(OSE_EINVAL, e);
+    pr.nseg = (uint32_t)pr.segs.size();
+    pr.order = k;
+    if (pr.nseg > kMaxRuleLen) return fail(OSE_ENOTSUP, "templatization rule has more than 64 segments");
+    rules.push_back(std::move(pr));
+  }
+  std::stable_sort(rules.begin(), rules.end(), [](const ParsedRule& a, const ParsedRule& b) { return a.nseg < b.nseg; });
+  std::vector<uint32_t> by_len(kMaxRuleLen + 2, 0);
+  std::vector<UrlRuleDev> rdev;
+  std::vector<UrlRuleSegDev> sdev;
+  uint32_t max_nseg = 0;
+  for (auto& r : rules) {
+    rdev.push_back(UrlRuleDev{r.nseg, (uint32_t)sdev.size()});
+    max_nseg = std::max(max_nseg, r.nseg);
+    for (auto& s : r.segs) {
+      UrlRuleSegDev sd{};
+      sd.dfa = -1;
+      switch (s.kind) {
+        case SegKind::Static: sd.kind = kRuleStatic; break;
+        case SegKind::Wildcard: sd.kind = kRuleWildcard; break;
+        case SegKind::Template: sd.kind = kRuleTemplate; break;
+        case SegKind::Regex: sd.kind = kRuleRegex; break;
+      }
+      NameDev t = add_text(s.text);
+      sd.text_off = t.off;
+      sd.text_len = t.len;
+      if (s.has_regexp) {
+        int rc = compile(s.regexp, sd.dfa);
+        if (rc) return rc;
+      }
+      sdev.push_back(sd);
+    }
+  }
+  // by_len[n] = first rule with nseg >= n
+  for (uint32_t n = 0; n <= kMaxRuleLen + 1; n++) {
+    uint32_t k = 0;
+    while (k < rules.size() && rules[k].nseg < n) k++;
+    by_len[n] = k;
+  }
+  max_name = 0;
+  for (auto& n : names) max_name = std::max(max_name, n.len);
+  h.n_custom = (uint32_t)custom.size();
+  h.n_rules = (uint32_t)rdev.size();
+  h.n_names = (uint32_t)names.size();
+  h.n_dfa = (uint32_t)dfas.size();
+  h.max_rule_nseg = max_nseg;
+  h.max_name_len = max_name;
+  h.rules_by_len_off = bl.put(by_len.data(), by_len.size());
+  h.rules_off = bl.put(rdev.data(), rdev.size());
+  h.segs_off = bl.put(sdev.data(), sdev.size());
+  h.custom_off = bl.put(custom.data(), custom.size());
+  h.names_off = bl.put(names.data(), names.size());
+  std::vector<uint32_t> dfa_offs;
+  for (auto& d : dfas) dfa_offs.push_back(put_dfa(bl, d));
+  h.dfa_off = bl.put(dfa_offs.data(), dfa_offs.size());
+  h.bytes_off = bl.put(bytes.data(), bytes.size());
+  bl.align();
+  bl.b.resize(bl.b.size() + 16, 0);
+  h.total_bytes = (uint32_t)bl.b.size();
+  std::memcpy(bl.b.data(), &h, sizeof h);
+  out = std::move(bl.b);
+  return 0;
+}
+
+// ---------------- engine ----------------
+Engine::~Engine() {
+  for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+  for (auto ev : event_pool) (void)hipEventDestroy(ev);
+  if (url_blob_dev) (void)hipFree(url_blob_dev);
+  if (sampling_blob_dev) (void)hipFree(sampling_blob_dev);
+  for (auto* w : pool) {
+    if (w->dev) (void)hipFree(w->dev);
+    if (w->stream) (void)hipStreamDestroy(w->stream);
+    delete w;
+  }
+}
+
+hipEvent_t Engine::take_event() {
+  if (!event_pool.empty()) {
+    hipEvent_t ev = event_pool.back();
+    event_pool.pop_back();
+    return ev;
+  }
+  hipEvent_t ev = nullptr;
+  (void)hipEventCreate(&ev);
+  return ev;
+}
+void Engine::prof_begin(const char* name, hipStream_t st, Timed& t) {
+  if (!profiling) return;
+  std::lock_guard<std::mutex> g(mu);
+  t.name = name;
+  t.a = take_event();
+  t.b = take_event();
+  (void)hipEventRecord(t.a, st);
+}
+void Engine::prof_end(Timed& t, hipStream_t st) {
+  if (!profiling || !t.a) return;
+  (void)hipEventRecord(t.b, st);
+  std::lock_guard<std::mutex> g(mu);
+  timed.push_back(t);
+}
+
+Workspace* Engine::acquire_ws() {
+  std::lock_guard<std::mutex> g(mu);
+  if (!free_ws.empty()) {
+    Workspace* w = free_ws.back();
+    free_ws.pop_back();
+    return w;
+  }
+  Workspace* w = new Workspace();
+  pool.push_back(w);
+  return w;
+}
+void Engine::release_ws(Workspace* w) {
+  std::lock_guard<std::mutex> g(mu);
+  free_ws.push_back(w);
+}
+
+int Workspace::reserve(size_t bytes) {
+  if (bytes <= cap) return 0;
+  if (dev) HIP_TRY(hipFree(dev));
+  dev = nullptr;
+  cap = 0;
+  size_t want = std::max<size_t>(bytes, 1 << 20);
+  HIP_TRY(hipMalloc(&dev, want));
+  cap = want;
+  return 0;
+}
+
+int ensure_device() {
+  static int status = 1;   // 1 = unknown
+  static std::mutex m;
+  std::lock_guard<std::mutex> g(m);
+  if (status == 1) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    status = (e == hipSuccess && n > 0) ? 0 : OSE_EDEVICE;
+  }
+  if (status) return fail(OSE_EDEVICE, "no HIP device visible: the odigos_amd engine runs only on an MI355X (gfx950)");
+  return 0;
+}
+
+int upload(const std::vector<uint8_t>& host, uint8_t** dev) {
+  HIP_TRY(hipMalloc(dev, host.size()));
+  HIP_TRY(hipMemcpy(*dev, host.data(), host.size(), hipMemcpyHostToDevice));
+  return 0;
+}
+
+// Workspace layout for one call (byte offsets), see run_stages.
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws) {
+  if (!e->has_url) return fail(OSE_EINVAL, "odigosurltemplate is not configured on this engine");
+  if (!c->url_flags || !c->kind || !c->path || !c->arena || !o->url_out || !o->tmpl || !o->tmpl_arena)
+    return fail(OSE_EINVAL, "TEMPLATE stage needs url_flags, kind, path, arena, url_out, tmpl, tmpl_arena");
+  if (e->url_needs_resource && (!c->resource || !c->res_url_ok))
+    return fail(OSE_EINVAL, "include/exclude configured: resource and res_url_ok columns are required");
+  if (o->tmpl_arena_cap > 0xFFFFFFFFull) return fail(OSE_ERANGE, "tmpl_arena_cap exceeds the 32-bit offset range");
+  uint64_t n = c->n_spans;
+  uint32_t tiles = (uint32_t)((n + kUrlTile - 1) / kUrlTile);
+  size_t off_status = 64;
+  size_t need = align_up(off_status + (size_t)tiles * 8, 256);
+  int rc = ws->reserve(need);
+  if (rc) return rc;
+  uint8_t* base = static_cast<uint8_t*>(ws->dev);
+  HIP_TRY(hipMemsetAsync(base, 0, off_status + (size_t)tiles * 8, st));
+  UrlKernelArgs a{};
+  a.n_spans = n;
+  a.n_tiles = tiles;
+  a.arena = c->arena;
+  a.url_flags = c->url_flags;
+  a.kind = c->kind;
+  a.resource = c->resource;
+  a.res_url_ok = e->url_needs_resource ? c->res_url_ok : nullptr;
+  a.path = c->path;
+  a.url_out = o->url_out;
+  a.tmpl = o->tmpl;
+  a.out_arena = o->tmpl_arena;
+  a.out_cap = o->tmpl_arena_cap;
+  a.cfg = e->url_blob_dev;
+  a.tile_counter = reinterpret_cast<uint32_t*>(base);
+  a.error = o->device_status ? o->device_status : reinterpret_cast<uint32_t*>(base + 8);
+  a.used = o->tmpl_arena_used;
+  a.tile_status = reinterpret_cast<uint64_t*>(base + off_status);
+  if (n == 0) {
+    if (o->tmpl_arena_used) HIP_TRY(hipMemsetAsync(o->tmpl_arena_used, 0, 8, st));
+    return 0;
+  }
+  Engine::Timed tm{};
+  e->prof_begin("url_template_kernel", st, tm);
+  launch_url_template(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  return 0;
+}
+
+int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
+               const ose_rand* rnd, hipStream_t st) {
+  if (!c || !o) return fail(OSE_EINVAL, "columns and outputs are required");
+  if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE)) return fail(OSE_EINVAL, "unknown stage bit");
+  (void)group_mode;
+  (void)rnd;
+  if (mask & OSE_STAGE_SAMPLE) return fail(OSE_ENOTSUP, "SAMPLE stage not built yet");
+  if (mask & OSE_STAGE_SIZE) return fail(OSE_ENOTSUP, "SIZE stage not built yet");
+  Workspace* ws = e->acquire_ws();
+  int rc = 0;
+  if (mask & OSE_STAGE_TEMPLATE) rc = run_url(e, c, o, st, ws);
+  e->release_ws(ws);
+  return rc;
+}
+
+}  // namespace ose
+
+using namespace ose;
+
+extern "C" {
+
+const char* ose_last_error(void) { return g_last_error.c_str(); }
+
+int ose_engine_create(const char* cfg_json, ose_engine** out) {
+  if (!out) return fail(OSE_EINVAL, "out is NULL");
+  *out = nullptr;
+  Json root;
+  try {
+    root = parse_json(cfg_json ? cfg_json : "{}");
+  } catch (const std::exception& ex) {
+    return fail(OSE_EINVAL, ex.what());
+  }
+  if (!root.is_obj()) return fail(OSE_EINVAL, "config must be a JSON object");
+  auto* e = new Engine();
+  std::string err;
+  if (const Json* j = root.get("odigosurltemplate")) {
+    err = decode_url_config(*j, e->url);
+    if (!err.empty()) { delete e; return fail(OSE_EINVAL, err); }
+    e->has_url = true;
+    e->url_needs_resource = e->url.include.has_value() || e->url.exclude.has_value();
+  }
+  if (const Json* j = root.get("odigossampling")) {
+    err = decode_sampling_config(*j, e->sampling);
+    if (!err.empty()) { delete e; return fail(OSE_EINVAL, err); }
+    e->has_sampling = true;
+  }
+  if (const Json* j = root.get("odigostrafficmetrics")) {
+    err = decode_traffic_config(*j, e->traffic);
+    if (!err.empty()) { delete e; return fail(OSE_EINVAL, err); }
+    e->has_traffic = true;
+    // newThroughputMeasurementProcessor (processor.go:31-36)
+    e->inverse = e->traffic.sampling_ratio != 0 ? (int64_t)(1.0 / e->traffic.sampling_ratio) : 0;
+  }
+  if (e->has_url) {
+    int rc = build_url_blob(e->url, e->url_blob_host, e->max_name);
+    if (rc) { delete e; return rc; }
+  }
+  int rc = e->build_sampling_tables();
+  if (rc) { delete e; return rc; }
+  rc = ensure_device();
+  if (rc) { delete e; return rc; }
+  if (e->has_url) {
+    rc = upload(e->url_blob_host, &e->url_blob_dev);
+    if (rc) { delete e; return rc; }
+  }
+  *out = reinterpret_cast<ose_engine*>(e);
+  return 0;
+}
+
+void ose_engine_destroy(ose_engine* eng) { delete reinterpret_cast<Engine*>(eng); }
+
+uint32_t ose_engine_service_id(const ose_engine* eng, const char* name, size_t len) {
+  if (!eng || !name) return OSE_NONE;
+  const Engine* e = reinterpret_cast<const Engine*>(eng);
+  auto it = e->service_ids.find(std::string(name, len));
+  return it == e->service_ids.end() ? OSE_NONE : it->second;
+}
+
+int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info) {
+  if (!eng || !info) return fail(OSE_EINVAL, "NULL argument");
+  const Engine* e = reinterpret_cast<const Engine*>(eng);
+  info->stages = (e->has_sampling ? OSE_STAGE_SAMPLE : 0) | (e->has_url ? OSE_STAGE_TEMPLATE : 0) |
+                 (e->has_traffic ? OSE_STAGE_SIZE : 0);
+  info->max_template_name = e->max_name;
+  info->inverse_sampling = e->inverse;
+  info->traffic_sampling_ratio = e->traffic.sampling_ratio;
+  return 0;
+}
+
+int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
+  if (!eng) return fail(OSE_EINVAL, "NULL engine");
+  (void)arena_bytes;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  Workspace* ws = e->acquire_ws();
+  int rc = ws->reserve(e->workspace_bytes(n_spans));
+  e->release_ws(ws);
+  return rc;
+}
+
+int ose_process_device(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, uint32_t stage_mask,
+                       uint32_t group_mode, const ose_rand* rnd, void* hip_stream) {
+  if (!eng) return fail(OSE_EINVAL, "NULL engine");
+  return run_stages(reinterpret_cast<Engine*>(eng), cols, outs, stage_mask, group_mode, rnd,
+                    static_cast<hipStream_t>(hip_stream));
+}
+
+int ose_profile_enable(ose_engine* eng, int on) {
+  if (!eng) return fail(OSE_EINVAL, "NULL engine");
+  reinterpret_cast<Engine*>(eng)->profiling = on != 0;
+  return 0;
+}
+
+int ose_profile_read(ose_engine* eng, char* json, size_t cap) {
+  if (!eng || !json) return fail(OSE_EINVAL, "NULL argument");
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::vector<Engine::Timed> ts;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    ts.swap(e->timed);
+  }
+  std::map<std::string, std::pair<uint64_t, double>> acc;
+  for (auto& t : ts) {
+    HIP_TRY(hipEventSynchronize(t.b));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, t.a, t.b));
+    auto& a = acc[t.name];
+    a.first++;
+    a.second += ms;
+  }
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    for (auto& t : ts) { e->event_pool.push_back(t.a); e->event_pool.push_back(t.b); }
+  }
+  std::string s = "{";
+  for (auto& kv : acc) {
+    if (s.size() > 1) s += ",";
+    char buf[256];
+    snprintf(buf, sizeof buf, "\"%s\":{\"launches\":%llu,\"ms\":%.6f}", kv.first.c_str(),
+             (unsigned long long)kv.second.first, kv.second.second);
+    s += buf;
+  }
+  s += "}";
+  if (s.size() + 1 > cap) return fail(OSE_ERANGE, "profile buffer too small");
+  std::memcpy(json, s.c_str(), s.size() + 1);
+  return 0;
+}
+
+int ose_device_info(char* buf, size_t cap) {
+  if (!buf || cap == 0) return fail(OSE_EINVAL, "NULL buffer");
+  int rc = ensure_device();
+  if (rc) { snprintf(buf, cap, "no device"); return rc; }
+  hipDeviceProp_t p;
+  HIP_TRY(hipGetDeviceProperties(&p, 0));
+  snprintf(buf, cap, "%s arch=%s CUs=%d HBM=%.1fGB", p.name, p.gcnArchName, p.multiProcessorCount,
+           (double)p.totalGlobalMem / 1e9);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// engine_internal.hpp — the engine object behind the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/odigos_amd.h"
+#include "config.hpp"
+
+namespace ose {
+
+int fail(int code, const std::string& msg);
+int ensure_device();
+
+// Device scratch for one in-flight call (look-back status words, sort
+// buffers, partial records).  Engines keep a pool so concurrent callers never
+// share one.
+struct Workspace {
+  void* dev = nullptr;
+  size_t cap = 0;
+  hipStream_t stream = nullptr;   // used by ose_process (host batches)
+  int reserve(size_t bytes);
+};
+
+struct Engine {
+  UrlTemplateConfig url;
+  SamplingConfig sampling;
+  TrafficMetricsConfig traffic;
+  bool has_url = false, has_sampling = false, has_traffic = false;
+  bool url_needs_resource = false;
+  int64_t inverse = 1;
+  uint32_t max_name = 5;
+
+  std::vector<uint8_t> url_blob_host;
+  uint8_t* url_blob_dev = nullptr;
+  std::vector<uint8_t> sampling_blob_host;
+  uint8_t* sampling_blob_dev = nullptr;
+  std::unordered_map<std::string, uint32_t> service_ids;
+
+  std::mutex mu;
+  std::vector<Workspace*> pool, free_ws;
+
+  // ose_profile_*: (kernel name, start, stop) per launch
+  bool profiling = false;
+  struct Timed { const char* name; hipEvent_t a, b; };
+  std::vector<Timed> timed;
+  std::vector<hipEvent_t> event_pool;
+  hipEvent_t take_event();
+  void prof_begin(const char* name, hipStream_t st, Timed& t);
+  void prof_end(Timed& t, hipStream_t st);
+
+  ~Engine();
+  Workspace* acquire_ws();
+  void release_ws(Workspace* w);
+  int build_sampling_tables();
+  size_t workspace_bytes(uint64_t n_spans) const;
+};
+
+int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
+               const ose_rand* rnd, hipStream_t st);
+
+}  // namespace ose

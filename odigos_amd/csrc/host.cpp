@@ -1,0 +1,570 @@
+// host.cpp — see host.hpp.  Columnarisation mirrors what each reference
+// function reads from pdata; Apply mirrors what it writes.
+#include "host.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <set>
+
+#include "urlparse.hpp"
+
+namespace ose {
+
+std::map<std::string, uint32_t> intern_services(const SamplingConfig& c) {
+  std::map<std::string, uint32_t> m;
+  auto add = [&](const std::string& s) { if (!m.count(s)) m.emplace(s, (uint32_t)m.size()); };
+  for (auto* lvl : {&c.global_rules, &c.service_rules, &c.endpoint_rules})
+    for (auto& r : *lvl) {
+      if (r.rtype == RuleType::HttpLatency) add(r.latency.service_name);
+      if (r.rtype == RuleType::ServiceName) add(r.service.service_name);
+      if (r.rtype == RuleType::SpanAttribute) add(r.attr.service_name);
+    }
+  return m;
+}
+
+void HostBatch::bind() {
+  cols.arena = arena.data();
+  cols.trace_id = trace_id.data();
+  cols.start_ns = start.data();
+  cols.end_ns = end.data();
+  cols.status = status.data();
+  cols.kind = kind.data();
+  cols.resource = resource.data();
+  cols.scope = scope.data();
+  cols.url_flags = url_flags.data();
+  cols.path = path.data();
+  cols.route = route.data();
+  cols.span_size = span_size.data();
+  cols.name_len = name_len.data();
+  cols.res_svc = res_svc.data();
+  cols.res_svc_str = res_svc_str.data();
+  cols.res_url_ok = res_url_ok.data();
+  cols.res_attrset = res_attrset.data();
+  cols.res_size = res_size.data();
+  cols.scope_size = scope_size.data();
+  outs.keep = keep.data();
+  outs.trace_count = trace_count.data();
+  outs.trace_first_span = trace_first_span.data();
+  outs.trace_keep = trace_keep.data();
+  outs.trace_level = trace_level.data();
+  outs.trace_ratio = trace_ratio.data();
+  outs.url_out = url_out.data();
+  outs.tmpl = tmpl.data();
+  outs.tmpl_arena = tmpl_arena.data();
+  outs.tmpl_arena_cap = tmpl_arena.size() - 16;
+  outs.tmpl_arena_used = tmpl_used.data();
+  outs.attrset_bytes = attrset_bytes.data();
+  outs.accepted_spans = accepted.data();
+  outs.res_bytes = res_bytes.data();
+  outs.device_status = device_status.data();
+}
+
+namespace {
+
+const char* kProcType[] = {"odigossampling", "odigosurltemplate", "odigostrafficmetrics", "pipeline"};
+
+// resourceToWorkloadStringRepresentation (filtermatcher.go:30-84)
+bool workload_key(const AttrMap& attrs, std::string& key) {
+  const Value* ns = attrs.Get("k8s.namespace.name");
+  if (!ns || ns->type != Value::TStr) return false;
+  struct { const char* attr; const char* kind; } order[] = {
+      {"k8s.deployment.name", "deployment"}, {"k8s.statefulset.name", "statefulset"}, {"k8s.daemonset.name", "daemonset"}};
+  for (auto& o : order) {
+    const Value* v = attrs.Get(o.attr);
+    if (!v) continue;
+    if (v->type != Value::TStr) return false;
+    key = ns->s + "/" + o.kind + "/" + v->s;
+    return true;
+  }
+  return false;
+}
+std::set<std::string> workload_set(const MatchProperties& mp) {
+  std::set<std::string> s;
+  for (auto& w : mp.k8s_workloads) {
+    std::string k = w.kind;
+    for (auto& c : k) c = (char)std::tolower((unsigned char)c);
+    s.insert(w.namespace_ + "/" + k + "/" + w.name);   // k8sWorkloadToStringRepresentation (:21-24)
+  }
+  return s;
+}
+
+}  // namespace
+
+TracesProcessor::TracesProcessor(ProcKind k, const Json& cfg) : kind_(k), cfg_json_(cfg) {
+  Json c = cfg.is_null() ? Json::object() : cfg;
+  switch (k) {
+    case ProcKind::Sampling: err_ = decode_sampling_config(c, sampling_); has_sampling_ = true; break;
+    case ProcKind::UrlTemplate: err_ = decode_url_config(c, url_); has_url_ = true; break;
+    case ProcKind::TrafficMetrics: err_ = decode_traffic_config(c, traffic_); has_traffic_ = true; break;
+    case ProcKind::Pipeline:
+      if (const Json* j = c.get("odigossampling")) { err_ = decode_sampling_config(*j, sampling_); has_sampling_ = true; }
+      if (err_.empty()) if (const Json* j = c.get("odigosurltemplate")) { err_ = decode_url_config(*j, url_); has_url_ = true; }
+      if (err_.empty()) if (const Json* j = c.get("odigostrafficmetrics")) { err_ = decode_traffic_config(*j, traffic_); has_traffic_ = true; }
+      group_mode = OSE_GROUP_TRACE_ID;
+      break;
+  }
+  if (has_sampling_) services_ = intern_services(sampling_);
+  if (err_.empty() && has_url_) {
+    // newUrlTemplateProcessor errors (rule parsing, custom id regexps) are
+    // create-time errors too (factory.go:37-40); decode_url_config covers them.
+  }
+}
+
+TracesProcessor::~TracesProcessor() {
+  if (eng_) ose_engine_destroy(eng_);
+}
+
+uint32_t TracesProcessor::stages() const {
+  return (has_sampling_ ? OSE_STAGE_SAMPLE : 0) | (has_url_ ? OSE_STAGE_TEMPLATE : 0) | (has_traffic_ ? OSE_STAGE_SIZE : 0);
+}
+
+int TracesProcessor::ensure_engine() {
+  if (eng_) return 0;
+  Json root = Json::object();
+  if (kind_ == ProcKind::Pipeline) root = cfg_json_;
+  else root.set(kProcType[(int)kind_], cfg_json_.is_null() ? Json::object() : cfg_json_);
+  std::string s;
+  dump_json(s, root);
+  return ose_engine_create(s.c_str(), &eng_);
+}
+
+double TracesProcessor::next_uniform() {
+  // splitmix64 stream -> [0,1)
+  uint64_t z = (seed_ += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  draws_++;
+  return (double)(z >> 11) * 0x1.0p-53;
+}
+
+std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const {
+  auto hb = std::make_unique<HostBatch>();
+  hb->td = td;
+  const Traces& t = hb->td;
+  ProtoSizer sizer;
+  std::set<std::string> excl, incl;
+  if (url_.exclude) excl = workload_set(*url_.exclude);
+  if (url_.include) incl = workload_set(*url_.include);
+  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> attrset_ids;
+  std::string arena;
+  auto add_str = [&](const std::string& s) {
+    ose_strref r{(uint32_t)arena.size(), (uint32_t)s.size()};
+    arena += s;
+    return r;
+  };
+  uint32_t scope_idx = 0;
+  for (size_t ri = 0; ri < t.resource_spans.size(); ri++) {
+    const ResourceSpans& rs = t.resource_spans[ri];
+    const AttrMap& ra = rs.resource_attrs;
+    // service ids (latency.go:51-56 AsString; servicename.go:38-42 Str)
+    uint32_t svc = OSE_NONE, svc_str = OSE_NONE;
+    if (const Value* v = ra.Get("service.name")) {
+      auto it = services_.find(v->AsString());
+      if (it != services_.end()) svc = it->second;
+      if (v->type == Value::TStr && it != services_.end()) svc_str = it->second;
+    }
+    hb->res_svc.push_back(svc);
+    hb->res_svc_str.push_back(svc_str);
+    // include/exclude (processor.go:76-85)
+    bool ok = true;
+    if (url_.exclude || url_.include) {
+      std::string key;
+      bool has_key = workload_key(ra, key);
+      if (url_.exclude && has_key && excl.count(key)) ok = false;
+      if (url_.include && !(has_key && incl.count(key))) ok = false;
+    }
+    hb->res_url_ok.push_back(ok ? 1 : 0);
+    // attributeSetFromResource (odigostrafficmetrics/processor.go:60-69)
+    std::map<std::string, std::string> set;   // attribute.NewSet: sorted, last value wins
+    for (auto& k : traffic_.res_attributes_keys)
+      if (const Value* v = ra.Get(k)) set[k] = v->Str();
+    std::vector<std::pair<std::string, std::string>> key(set.begin(), set.end());
+    auto it = attrset_ids.find(key);
+    if (it == attrset_ids.end()) {
+      it = attrset_ids.emplace(key, (uint32_t)hb->attrsets.size()).first;
+      hb->attrsets.push_back(key);
+    }
+    hb->res_attrset.push_back(it->second);
+    hb->res_size.push_back((uint32_t)sizer.resource_fixed(rs));
+    for (auto& ss : rs.scope_spans) {
+      hb->scope_size.push_back((uint32_t)sizer.scope_fixed(ss));
+      for (auto& sp : ss.spans) {
+        uint64_t hi = 0, lo = 0;
+        for (int k = 0; k < 8; k++) { hi = hi << 8 | sp.trace_id[k]; lo = lo << 8 | sp.trace_id[8 + k]; }
+        hb->trace_id.push_back(hi);
+        hb->trace_id.push_back(lo);
+        hb->start.push_back(sp.start);
+        hb->end.push_back(sp.end);
+        hb->status.push_back((uint8_t)sp.status_code);
+        hb->kind.push_back((uint8_t)std::min<int32_t>(std::max<int32_t>(sp.kind, 0), 255));
+        hb->resource.push_back((uint32_t)ri);
+        hb->scope.push_back(scope_idx);
+        hb->span_size.push_back((uint32_t)sizer.span(sp));
+        hb->name_len.push_back((uint32_t)sp.name.size());
+        const AttrMap& a = sp.attrs;
+        // sampling: AsString(http.route) (latency.go:64-68)
+        const Value* route = a.Get("http.route");
+        hb->route.push_back(route ? add_str(route->AsString()) : ose_strref{0, 0});
+        // urltemplate (processor.go:98-147, 235-287)
+        uint8_t f = 0;
+        ose_strref pref{0, 0};
+        const Value* m = a.Get("http.request.method");
+        if (!m) m = a.Get("http.method");
+        if (m) {
+          f |= OSE_URL_HAS_METHOD;
+          std::string method = m->AsString();
+          if (sp.name == method) f |= OSE_URL_NAME_EQ_METHOD;
+          const char* tkey = sp.kind == OSE_KIND_CLIENT ? "url.template" : "http.route";
+          if (const Value* tv = a.Get(tkey)) {
+            if (tv->type != Value::TStr) f |= OSE_URL_TGT_NONSTR;
+            else f |= tv->s.empty() ? OSE_URL_TGT_STR_EMPTY : OSE_URL_TGT_STR;
+          }
+          if (const Value* p = a.Get("url.path")) {
+            f |= OSE_URL_PATH_RAW;
+            pref = add_str(p->AsString());
+          } else if (const Value* p = a.Get("http.target")) {
+            f |= OSE_URL_PATH_TARGET;
+            pref = add_str(p->AsString());
+          } else {
+            const Value* fu = a.Get("url.full");
+            if (!fu) fu = a.Get("http.url");
+            std::string path;
+            if (fu && go_url_parse_path(fu->AsString(), path)) {
+              f |= OSE_URL_PATH_RAW;
+              pref = add_str(path);
+            }
+          }
+        }
+        hb->url_flags.push_back(f);
+        hb->path.push_back(pref);
+      }
+      scope_idx++;
+    }
+  }
+  size_t n = hb->kind.size();
+  hb->arena.assign(arena.begin(), arena.end());
+  hb->arena.resize(((arena.size() + 15) / 16) * 16 + 16, 0);
+  hb->cols.n_spans = n;
+  hb->cols.n_resources = (uint32_t)t.resource_spans.size();
+  hb->cols.n_scopes = scope_idx;
+  hb->cols.n_attrsets = (uint32_t)hb->attrsets.size();
+  hb->cols.arena_bytes = arena.size();
+  // outputs (vectors never empty so data() is non-null)
+  size_t nn = std::max<size_t>(n, 1);
+  hb->keep.assign(nn, 0);
+  hb->trace_keep.assign(nn, 0);
+  hb->trace_level.assign(nn, 0);
+  hb->trace_ratio.assign(nn, 0);
+  hb->trace_first_span.assign(nn, 0);
+  hb->trace_count.assign(1, 0);
+  hb->url_out.assign(nn, 0);
+  hb->tmpl.assign(nn, ose_strref{0, 0});
+  // capacity bound: every output byte comes from a path byte, a separator or a name
+  size_t cap = 16 + arena.size() * 2;
+  uint32_t maxname = 5;
+  for (auto& c : url_.custom_ids) maxname = std::max<uint32_t>(maxname, (uint32_t)c.template_name.size());
+  for (auto& r : url_.templatization_rules) maxname = std::max<uint32_t>(maxname, (uint32_t)r.size());
+  for (size_t i = 0; i < n; i++) cap += 2 + (size_t)(hb->path[i].len + 1) * (maxname + 3);
+  hb->tmpl_arena.assign(cap + 16, 0);
+  hb->attrset_bytes.assign(std::max<size_t>(hb->attrsets.size(), 1), 0);
+  hb->accepted.assign(1, 0);
+  hb->res_bytes.assign(std::max<size_t>(hb->res_svc.size(), 1), 0);
+  hb->tmpl_used.assign(1, 0);
+  hb->device_status.assign(4, 0);
+  for (auto* v : {&hb->res_svc, &hb->res_svc_str, &hb->res_attrset, &hb->res_size, &hb->scope_size,
+                  &hb->resource, &hb->scope, &hb->span_size, &hb->name_len})
+    if (v->empty()) v->push_back(0);
+  for (auto* v : {&hb->status, &hb->kind, &hb->url_flags, &hb->res_url_ok})
+    if (v->empty()) v->push_back(0);
+  for (auto* v : {&hb->trace_id, &hb->start, &hb->end})
+    if (v->empty()) v->push_back(0);
+  if (hb->path.empty()) hb->path.push_back(ose_strref{0, 0});
+  if (hb->route.empty()) hb->route.push_back(ose_strref{0, 0});
+  hb->bind();
+  return hb;
+}
+
+void TracesProcessor::Apply(HostBatch& hb, Traces& td) {
+  const uint32_t st = stages();
+  const ose_outputs& o = hb.outs;
+  // odigossampling: drop the spans of unsampled traces.  With one trace per
+  // call (OSE_GROUP_BATCH) this is exactly ResourceSpans().RemoveIf(true)
+  // (processor.go:23-25); per trace_id, emptied scopes/resources go too.
+  std::vector<uint8_t> keep;
+  if (st & OSE_STAGE_SAMPLE) keep.assign(o.keep, o.keep + hb.cols.n_spans);
+  size_t i = 0;
+  for (auto& rs : td.resource_spans) {
+    for (auto& ss : rs.scope_spans) {
+      for (auto& sp : ss.spans) {
+        bool kept = keep.empty() || keep[i];
+        if (kept && (st & OSE_STAGE_TEMPLATE) && o.url_out[i]) {
+          std::string tmpl(reinterpret_cast<const char*>(o.tmpl_arena) + o.tmpl[i].off, o.tmpl[i].len);
+          if (o.url_out[i] & OSE_OUT_SET_ATTR)
+            sp.attrs.PutStr(sp.kind == OSE_KIND_CLIENT ? "url.template" : "http.route", tmpl);   // processor.go:259
+          if (o.url_out[i] & OSE_OUT_RENAME) {
+            const Value* m = sp.attrs.Get("http.request.method");
+            if (!m) m = sp.attrs.Get("http.method");
+            sp.name = (m ? m->AsString() : std::string()) + " " + tmpl;   // processor.go:230-232
+          }
+        }
+        i++;
+      }
+    }
+  }
+  if (!keep.empty()) {
+    if (group_mode == OSE_GROUP_BATCH) {
+      if (hb.cols.n_spans > 0 && !keep[0]) td.resource_spans.clear();
+    } else {
+      size_t k = 0;
+      std::vector<ResourceSpans> rout;
+      for (auto& rs : td.resource_spans) {
+        bool had = false;
+        std::vector<ScopeSpans> sout;
+        for (auto& ss : rs.scope_spans) {
+          bool shad = !ss.spans.empty();
+          had |= shad;
+          std::vector<Span> kept;
+          for (auto& sp : ss.spans) { if (keep[k]) kept.push_back(std::move(sp)); k++; }
+          ss.spans = std::move(kept);
+          if (!shad || !ss.spans.empty()) sout.push_back(std::move(ss));
+        }
+        rs.scope_spans = std::move(sout);
+        if (!had || !rs.scope_spans.empty()) rout.push_back(std::move(rs));
+      }
+      td.resource_spans = std::move(rout);
+    }
+  }
+  if (st & OSE_STAGE_SIZE) {
+    for (size_t a = 0; a < hb.attrsets.size(); a++)
+      if (o.attrset_bytes[a]) data_size_[hb.attrsets[a]] += o.attrset_bytes[a];
+    accepted_spans_ += o.accepted_spans[0];
+  }
+}
+
+int TracesProcessor::ProcessTraces(Traces& td) {
+  int rc = ensure_engine();
+  if (rc) return rc;
+  auto hb = Columnarize(td);
+  ose_rand rnd{seed_ ^ (draws_ * 0x9E3779B97F4A7C15ull), 0.0};
+  if (has_traffic_) rnd.traffic_u = next_uniform();   // rand.Float64() per call (processor.go:72)
+  ose_columns dims = hb->cols;
+  ose_batch* b = nullptr;
+  rc = ose_batch_acquire(eng_, &dims, &b);
+  if (rc) return rc;
+  ose_columns* c = ose_batch_columns(b);
+  ose_outputs* o = ose_batch_outputs(b);
+  const uint64_t n = hb->cols.n_spans;
+  const uint32_t R = hb->cols.n_resources, S = hb->cols.n_scopes, A = hb->cols.n_attrsets;
+  auto cp = [](const void* dst, const void* src, size_t bytes) {
+    if (bytes) std::memcpy(const_cast<void*>(dst), src, bytes);
+  };
+  cp(c->arena, hb->cols.arena, hb->cols.arena_bytes);
+  cp(c->trace_id, hb->cols.trace_id, 16 * n);
+  cp(c->start_ns, hb->cols.start_ns, 8 * n);
+  cp(c->end_ns, hb->cols.end_ns, 8 * n);
+  cp(c->status, hb->cols.status, n);
+  cp(c->kind, hb->cols.kind, n);
+  cp(c->resource, hb->cols.resource, 4 * n);
+  cp(c->scope, hb->cols.scope, 4 * n);
+  cp(c->url_flags, hb->cols.url_flags, n);
+  cp(c->path, hb->cols.path, 8 * n);
+  cp(c->route, hb->cols.route, 8 * n);
+  cp(c->span_size, hb->cols.span_size, 4 * n);
+  cp(c->name_len, hb->cols.name_len, 4 * n);
+  cp(c->res_svc, hb->cols.res_svc, 4 * R);
+  cp(c->res_svc_str, hb->cols.res_svc_str, 4 * R);
+  cp(c->res_url_ok, hb->cols.res_url_ok, R);
+  cp(c->res_attrset, hb->cols.res_attrset, 4 * R);
+  cp(c->res_size, hb->cols.res_size, 4 * R);
+  cp(c->scope_size, hb->cols.scope_size, 4 * S);
+  std::memset(o->attrset_bytes, 0, 8 * (size_t)A);
+  std::memset(o->accepted_spans, 0, 8);
+  rc = ose_process(eng_, b, stages(), group_mode, &rnd);
+  if (rc) { ose_batch_release(b); return rc; }
+  // read back into the host batch and apply
+  cp(hb->outs.keep, o->keep, n);
+  cp(hb->outs.url_out, o->url_out, n);
+  cp(hb->outs.tmpl, o->tmpl, 8 * n);
+  uint64_t used = *o->tmpl_arena_used;
+  if (used + 16 > hb->tmpl_arena.size()) { hb->tmpl_arena.resize(used + 16); hb->bind(); }
+  cp(hb->outs.tmpl_arena, o->tmpl_arena, used);
+  cp(hb->outs.attrset_bytes, o->attrset_bytes, 8 * (size_t)A);
+  cp(hb->outs.accepted_spans, o->accepted_spans, 8);
+  ose_batch_release(b);
+  Apply(*hb, td);
+  return 0;
+}
+
+std::string TracesProcessor::MetricsJson() const {
+  Json root = Json::object();
+  Json pts = Json::array();
+  for (auto& kv : data_size_) {
+    Json p = Json::object();
+    Json at = Json::object();
+    for (auto& a : kv.first) at.set(a.first, Json::str(a.second));
+    p.set("attributes", std::move(at));
+    p.set("value", Json::number(std::to_string(kv.second)));
+    pts.push(std::move(p));
+  }
+  root.set("otelcol_odigos_trace_data_size", std::move(pts));
+  root.set("otelcol_odigos_accepted_spans", Json::number(std::to_string(accepted_spans_)));
+  std::string s;
+  dump_json(s, root);
+  return s;
+}
+
+}  // namespace ose
+
+// ---------------- C API for the host layer (tests, smoke) ----------------
+using namespace ose;
+
+namespace {
+thread_local std::string g_host_err;
+char* dup_cstr(const std::string& s) {
+  char* p = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(p, s.data(), s.size());
+  p[s.size()] = 0;
+  return p;
+}
+std::string dump_traces(const Traces& t) {
+  std::string s;
+  dump_json(s, traces_to_json(t));
+  return s;
+}
+}  // namespace
+
+extern "C" {
+
+const char* osehost_last_error(void) { return g_host_err.c_str(); }
+
+// Factory.CreateTraces for "odigossampling" | "odigosurltemplate" |
+// "odigostrafficmetrics" | "pipeline" (all three, gateway order).  NULL on a
+// config error (message in osehost_last_error).
+void* osehost_processor_create(const char* type, const char* cfg_json) {
+  ProcKind k;
+  std::string t = type ? type : "";
+  if (t == "odigossampling") k = ProcKind::Sampling;
+  else if (t == "odigosurltemplate") k = ProcKind::UrlTemplate;
+  else if (t == "odigostrafficmetrics") k = ProcKind::TrafficMetrics;
+  else if (t == "pipeline") k = ProcKind::Pipeline;
+  else { g_host_err = "unknown processor type: " + t; return nullptr; }
+  Json cfg;
+  try {
+    cfg = parse_json(cfg_json && *cfg_json ? cfg_json : "{}");
+  } catch (const std::exception& e) {
+    g_host_err = e.what();
+    return nullptr;
+  }
+  auto* p = new TracesProcessor(k, cfg);
+  if (!p->error().empty()) { g_host_err = p->error(); delete p; return nullptr; }
+  return p;
+}
+
+void osehost_processor_destroy(void* p) { delete static_cast<TracesProcessor*>(p); }
+
+void osehost_processor_set(void* p, uint64_t seed, uint32_t group_mode) {
+  auto* tp = static_cast<TracesProcessor*>(p);
+  tp->set_seed(seed);
+  tp->group_mode = group_mode;
+}
+
+// ConsumeTraces on the device path.  Returns 0 and the processed traces as
+// OTLP/JSON in *out (free with osehost_free), or an OSE_E* code.
+int osehost_consume(void* p, const char* traces_json, char** out) {
+  auto* tp = static_cast<TracesProcessor*>(p);
+  Traces td;
+  try {
+    td = traces_from_json(parse_json(traces_json));
+  } catch (const std::exception& e) {
+    g_host_err = e.what();
+    return OSE_EINVAL;
+  }
+  int rc = tp->ProcessTraces(td);
+  if (rc) { g_host_err = ose_last_error(); return rc; }
+  if (out) *out = dup_cstr(dump_traces(td));
+  return 0;
+}
+
+// Test seam: the host half of ConsumeTraces without the device.
+void* osehost_columnarize(void* p, const char* traces_json) {
+  auto* tp = static_cast<TracesProcessor*>(p);
+  try {
+    return tp->Columnarize(traces_from_json(parse_json(traces_json))).release();
+  } catch (const std::exception& e) {
+    g_host_err = e.what();
+    return nullptr;
+  }
+}
+ose_columns* osehost_batch_columns(void* hb) { return &static_cast<HostBatch*>(hb)->cols; }
+ose_outputs* osehost_batch_outputs(void* hb) { return &static_cast<HostBatch*>(hb)->outs; }
+int osehost_apply(void* p, void* hb, char** out) {
+  auto* tp = static_cast<TracesProcessor*>(p);
+  auto* b = static_cast<HostBatch*>(hb);
+  Traces td = b->td;
+  tp->Apply(*b, td);
+  if (out) *out = dup_cstr(dump_traces(td));
+  return 0;
+}
+void osehost_batch_free(void* hb) { delete static_cast<HostBatch*>(hb); }
+
+char* osehost_metrics_json(void* p) { return dup_cstr(static_cast<TracesProcessor*>(p)->MetricsJson()); }
+// Traces round trip through the pdata model (fixture sanity)
+char* osehost_roundtrip(const char* traces_json) {
+  try {
+    return dup_cstr(dump_traces(traces_from_json(parse_json(traces_json))));
+  } catch (const std::exception& e) {
+    g_host_err = e.what();
+    return nullptr;
+  }
+}
+// ptrace.ProtoMarshaler.ResourceSpansSize for every resource of a batch
+int osehost_resource_sizes(const char* traces_json, int gogo, uint64_t* out, size_t cap) {
+  try {
+    Traces t = traces_from_json(parse_json(traces_json));
+    ProtoSizer s;
+    s.gogo = gogo != 0;
+    for (size_t k = 0; k < t.resource_spans.size() && k < cap; k++) out[k] = s.resource_spans(t.resource_spans[k]);
+    return (int)t.resource_spans.size();
+  } catch (const std::exception& e) {
+    g_host_err = e.what();
+    return -1;
+  }
+}
+char* osehost_as_string(const char* value_json) {   // pcommon.Value.AsString of an OTLP/JSON AnyValue
+  try {
+    Json j = parse_json(value_json);
+    Json wrapper = Json::object();
+    Json attrs = Json::array();
+    Json kv = Json::object();
+    kv.set("key", Json::str("k"));
+    kv.set("value", j);
+    attrs.push(kv);
+    Json res = Json::object();
+    res.set("attributes", attrs);
+    Json rs = Json::object();
+    rs.set("resource", res);
+    Json rss = Json::array();
+    rss.push(rs);
+    wrapper.set("resourceSpans", rss);
+    Traces t = traces_from_json(wrapper);
+    return dup_cstr(t.resource_spans[0].resource_attrs.kv[0].second.AsString());
+  } catch (const std::exception& e) {
+    g_host_err = e.what();
+    return nullptr;
+  }
+}
+void osehost_free(char* s) { std::free(s); }
+
+}  // extern "C"
+
+// ---- test seam: the product regex->DFA compiler evaluated on the host ----
+#include "regex_dfa.hpp"
+extern "C" int osehost_regex_match(const char* pattern, const char* s, size_t n) {
+  ose::Dfa d;
+  std::string err;
+  ose::RegexStatus st = ose::compile_dfa(pattern, d, err);
+  if (st == ose::RegexStatus::Syntax) { g_host_err = err; return -1; }
+  if (st != ose::RegexStatus::Ok) { g_host_err = err; return -2; }
+  return ose::dfa_match(d, reinterpret_cast<const uint8_t*>(s), n) ? 1 : 0;
+}

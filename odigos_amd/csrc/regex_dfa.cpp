@@ -1,0 +1,758 @@
+// regex_dfa.cpp — Go RE2-syntax regexp -> DFA (see regex_dfa.hpp).
+#include "regex_dfa.hpp"
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <set>
+
+namespace ose {
+namespace {
+
+constexpr uint32_t kRuneMax = 0x10FFFF;
+constexpr uint32_t kRuneError = 0xFFFD;
+
+using Ranges = std::vector<std::pair<uint32_t, uint32_t>>;
+
+// unicode/utf8.DecodeRune: invalid -> (U+FFFD, 1)
+uint32_t decode(const uint8_t* s, size_t n, int& w) {
+  uint8_t c = s[0];
+  if (c < 0x80) { w = 1; return c; }
+  int need;
+  uint32_t r;
+  uint8_t lo = 0x80, hi = 0xBF;
+  if (c >= 0xC2 && c <= 0xDF) { need = 1; r = c & 0x1F; }
+  else if (c == 0xE0) { need = 2; r = c & 0x0F; lo = 0xA0; }
+  else if (c >= 0xE1 && c <= 0xEC) { need = 2; r = c & 0x0F; }
+  else if (c == 0xED) { need = 2; r = c & 0x0F; hi = 0x9F; }
+  else if (c >= 0xEE && c <= 0xEF) { need = 2; r = c & 0x0F; }
+  else if (c == 0xF0) { need = 3; r = c & 0x07; lo = 0x90; }
+  else if (c >= 0xF1 && c <= 0xF3) { need = 3; r = c & 0x07; }
+  else if (c == 0xF4) { need = 3; r = c & 0x07; hi = 0x8F; }
+  else { w = 1; return kRuneError; }
+  if ((size_t)need >= n) { w = 1; return kRuneError; }
+  for (int i = 1; i <= need; i++) {
+    uint8_t b = s[i];
+    if (b < (i == 1 ? lo : 0x80) || b > (i == 1 ? hi : 0xBF)) { w = 1; return kRuneError; }
+    r = (r << 6) | (b & 0x3F);
+  }
+  w = need + 1;
+  return r;
+}
+
+void normalize(Ranges& r) {
+  std::sort(r.begin(), r.end());
+  Ranges o;
+  for (auto& x : r) {
+    if (!o.empty() && x.first <= o.back().second + 1) o.back().second = std::max(o.back().second, x.second);
+    else o.push_back(x);
+  }
+  r.swap(o);
+}
+Ranges negate(Ranges r) {
+  normalize(r);
+  Ranges o;
+  uint32_t next = 0;
+  for (auto& x : r) {
+    if (x.first > next) o.push_back({next, x.first - 1});
+    next = x.second + 1;
+  }
+  if (next <= kRuneMax) o.push_back({next, kRuneMax});
+  return o;
+}
+// unicode.SimpleFold restricted to ASCII-letter orbits: {k,K,U+212A}, {s,S,U+017F}
+void fold(Ranges& r) {
+  Ranges add;
+  for (auto& x : r) {
+    for (uint32_t c = x.first; c <= x.second && c < 0x80; c++) {
+      if (c >= 'a' && c <= 'z') add.push_back({c - 32, c - 32});
+      if (c >= 'A' && c <= 'Z') add.push_back({c + 32, c + 32});
+      if (c == 'k' || c == 'K') add.push_back({0x212A, 0x212A});
+      if (c == 's' || c == 'S') add.push_back({0x17F, 0x17F});
+    }
+    if (x.first <= 0x212A && 0x212A <= x.second) { add.push_back({'k', 'k'}); add.push_back({'K', 'K'}); }
+    if (x.first <= 0x17F && 0x17F <= x.second) { add.push_back({'s', 's'}); add.push_back({'S', 'S'}); }
+  }
+  r.insert(r.end(), add.begin(), add.end());
+  normalize(r);
+}
+
+enum EmptyOp : uint8_t { kBOL = 1, kEOL = 2, kBOT = 4, kEOT = 8, kWB = 16, kNWB = 32 };
+
+struct Node {
+  enum Kind { Empty, Chars, Assert, Cat, Alt, Rep } kind = Empty;
+  Ranges chars;
+  uint8_t op = 0;
+  std::vector<std::unique_ptr<Node>> sub;
+  int min = 0, max = 0;  // max -1 = unbounded
+};
+using NodeP = std::unique_ptr<Node>;
+
+struct ParseError {
+  RegexStatus st;
+  std::string msg;
+};
+
+class Parser {
+ public:
+  explicit Parser(const std::string& p) : s_(p) {}
+  NodeP parse() {
+    NodeP n = alt();
+    if (i_ < s_.size()) throw ParseError{RegexStatus::Syntax, "unexpected ): `" + s_ + "`"};
+    return n;
+  }
+
+ private:
+  const std::string& s_;
+  size_t i_ = 0;
+  bool fi_ = false, fm_ = false, fs_ = false;
+  int depth_ = 0;
+
+  [[noreturn]] void syntax(const std::string& m) { throw ParseError{RegexStatus::Syntax, m}; }
+  [[noreturn]] void unsupported(const std::string& m) { throw ParseError{RegexStatus::Unsupported, m}; }
+  bool eof() const { return i_ >= s_.size(); }
+  uint32_t rune(int& w) const { return decode((const uint8_t*)s_.data() + i_, s_.size() - i_, w); }
+
+  NodeP chars(Ranges r, bool neg) {
+    normalize(r);
+    if (fi_) fold(r);
+    if (neg) r = negate(r);
+    auto n = std::make_unique<Node>();
+    n->kind = Node::Chars;
+    n->chars = std::move(r);
+    return n;
+  }
+  // regexp/syntax appendGroup: under (?i) the group is folded, then negated
+  void perl(Ranges& r, char k, bool neg) const {
+    Ranges t;
+    if (k == 'd') t = {{'0', '9'}};
+    else if (k == 's') t = {{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}};
+    else t = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+    if (fi_) fold(t);
+    if (neg) t = negate(t);
+    r.insert(r.end(), t.begin(), t.end());
+  }
+  // Folding is only implemented for ASCII orbits ({k,K,U+212A}, {s,S,U+017F},
+  // letter pairs).  A set whose non-ASCII part is empty, only U+017F/U+212A,
+  // or everything but those two is closed under every other orbit.
+  static bool fold_safe(Ranges r) {
+    normalize(r);
+    Ranges na;
+    for (auto& x : r) if (x.second >= 0x80) na.push_back({std::max<uint32_t>(x.first, 0x80), x.second});
+    if (na.empty()) return true;
+    auto specials_only = [](const Ranges& s) {
+      for (auto& x : s) if (x.first != x.second || (x.first != 0x17F && x.first != 0x212A)) return false;
+      return true;
+    };
+    if (specials_only(na)) return true;
+    Ranges comp;
+    uint32_t next = 0x80;
+    for (auto& x : na) { if (x.first > next) comp.push_back({next, x.first - 1}); next = x.second + 1; }
+    if (next <= kRuneMax) comp.push_back({next, kRuneMax});
+    return specials_only(comp);
+  }
+  static bool alnum(uint32_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+  static bool hexd(char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
+  static uint32_t hexv(char c) { return c <= '9' ? c - '0' : ((c | 0x20) - 'a' + 10); }
+
+  // escape after '\'; kind: 0 rune, 1 perl class (perl,neg), 2 empty op
+  int escape(uint32_t& r, char& pk, bool& pneg, uint8_t& op, bool in_class) {
+    if (eof()) syntax("trailing backslash at end of expression");
+    int w;
+    uint32_t c = rune(w);
+    i_ += w;
+    if (c < 0x80 && !alnum(c)) { r = c; return 0; }
+    switch (c) {
+      case 'd': case 's': case 'w': pk = (char)c; pneg = false; return 1;
+      case 'D': case 'S': case 'W': pk = (char)(c + 32); pneg = true; return 1;
+      case 'a': r = 7; return 0;
+      case 'f': r = 12; return 0;
+      case 'n': r = 10; return 0;
+      case 'r': r = 13; return 0;
+      case 't': r = 9; return 0;
+      case 'v': r = 11; return 0;
+      case 'b': if (!in_class) { op = kWB; return 2; } break;
+      case 'B': if (!in_class) { op = kNWB; return 2; } break;
+      case 'A': if (!in_class) { op = kBOT; return 2; } break;
+      case 'z': if (!in_class) { op = kEOT; return 2; } break;
+      case 'p': case 'P': unsupported("unsupported: Unicode class \\p");
+      case 'Q': unsupported("unsupported: \\Q...\\E");
+      case '1': case '2': case '3': case '4': case '5': case '6': case '7':
+        if (eof() || s_[i_] < '0' || s_[i_] > '7') break;
+        [[fallthrough]];
+      case '0': {
+        uint32_t v = c - '0';
+        for (int k = 1; k < 3 && !eof() && s_[i_] >= '0' && s_[i_] <= '7'; k++) v = v * 8 + (s_[i_++] - '0');
+        r = v;
+        return 0;
+      }
+      case 'x': {
+        if (eof()) break;
+        if (s_[i_] == '{') {
+          size_t j = i_ + 1;
+          uint32_t v = 0;
+          int nd = 0;
+          while (j < s_.size() && hexd(s_[j]) && v <= kRuneMax) { v = v * 16 + hexv(s_[j]); j++; nd++; }
+          if (nd == 0 || j >= s_.size() || s_[j] != '}' || v > kRuneMax) break;
+          i_ = j + 1;
+          r = v;
+          return 0;
+        }
+        if (i_ + 2 > s_.size() || !hexd(s_[i_]) || !hexd(s_[i_ + 1])) break;
+        r = hexv(s_[i_]) * 16 + hexv(s_[i_ + 1]);
+        i_ += 2;
+        return 0;
+      }
+      default: break;
+    }
+    syntax("invalid escape sequence");
+  }
+
+  bool posix(Ranges& r) {  // at "[:"
+    size_t j = i_ + 2;
+    bool neg = false;
+    if (j < s_.size() && s_[j] == '^') { neg = true; j++; }
+    size_t e = s_.find(":]", j);
+    if (e == std::string::npos) return false;
+    std::string nm = s_.substr(j, e - j);
+    Ranges t;
+    if (nm == "alnum") t = {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}};
+    else if (nm == "alpha") t = {{'A', 'Z'}, {'a', 'z'}};
+    else if (nm == "ascii") t = {{0, 0x7F}};
+    else if (nm == "blank") t = {{'\t', '\t'}, {' ', ' '}};
+    else if (nm == "cntrl") t = {{0, 0x1F}, {0x7F, 0x7F}};
+    else if (nm == "digit") t = {{'0', '9'}};
+    else if (nm == "graph") t = {{'!', '~'}};
+    else if (nm == "lower") t = {{'a', 'z'}};
+    else if (nm == "print") t = {{' ', '~'}};
+    else if (nm == "punct") t = {{'!', '/'}, {':', '@'}, {'[', '`'}, {'{', '~'}};
+    else if (nm == "space") t = {{'\t', '\r'}, {' ', ' '}};
+    else if (nm == "upper") t = {{'A', 'Z'}};
+    else if (nm == "word") t = {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}, {'_', '_'}};
+    else if (nm == "xdigit") t = {{'0', '9'}, {'A', 'F'}, {'a', 'f'}};
+    else syntax("invalid character class range");
+    if (neg) t = negate(t);
+    r.insert(r.end(), t.begin(), t.end());
+    i_ = e + 2;
+    return true;
+  }
+
+  NodeP cls() {  // after '['
+    Ranges r;
+    bool neg = false;
+    if (!eof() && s_[i_] == '^') { neg = true; i_++; }
+    bool first = true;
+    for (;;) {
+      if (eof()) syntax("missing closing ]");
+      if (s_[i_] == ']' && !first) { i_++; break; }
+      first = false;
+      if (i_ + 1 < s_.size() && s_[i_] == '[' && s_[i_ + 1] == ':' && posix(r)) continue;
+      uint32_t lo, hi;
+      char pk = 0;
+      bool pn = false;
+      uint8_t op = 0;
+      if (s_[i_] == '\\') {
+        i_++;
+        int k = escape(lo, pk, pn, op, true);
+        if (k == 1) { perl(r, pk, pn); continue; }
+      } else {
+        int w;
+        lo = rune(w);
+        i_ += w;
+      }
+      hi = lo;
+      if (i_ + 1 < s_.size() && s_[i_] == '-' && s_[i_ + 1] != ']') {
+        i_++;
+        if (s_[i_] == '\\') {
+          i_++;
+          int k = escape(hi, pk, pn, op, true);
+          if (k != 0) syntax("invalid character class range");
+        } else {
+          int w;
+          hi = rune(w);
+          i_ += w;
+        }
+        if (hi < lo) syntax("invalid character class range");
+      }
+      r.push_back({lo, hi});
+    }
+    if (fi_ && !fold_safe(r)) unsupported("unsupported: (?i) with non-ASCII class members");
+    return chars(std::move(r), neg);
+  }
+
+  bool braces(int& mn, int& mx) {  // at '{'
+    size_t j = i_ + 1;
+    auto num = [&](int& v) {
+      size_t st = j;
+      long x = 0;
+      while (j < s_.size() && s_[j] >= '0' && s_[j] <= '9') { if (x < 100000) x = x * 10 + (s_[j] - '0'); j++; }
+      v = (int)x;
+      return j > st;
+    };
+    if (!num(mn)) return false;
+    if (j < s_.size() && s_[j] == ',') {
+      j++;
+      if (j < s_.size() && s_[j] == '}') mx = -1;
+      else if (!num(mx)) return false;
+    } else {
+      mx = mn;
+    }
+    if (j >= s_.size() || s_[j] != '}') return false;
+    i_ = j + 1;
+    return true;
+  }
+
+  NodeP concat() {
+    auto cat = std::make_unique<Node>();
+    cat->kind = Node::Cat;
+    bool last_rep = false;
+    while (!eof() && s_[i_] != '|' && s_[i_] != ')') {
+      char c = s_[i_];
+      if (c == '*' || c == '+' || c == '?' || c == '{') {
+        int mn = 0, mx = 0;
+        bool is_rep = true;
+        if (c == '{') {
+          if (!braces(mn, mx)) is_rep = false;
+          else if (mn > 1000 || mx > 1000 || (mx >= 0 && mn > mx)) syntax("invalid repeat count");
+        } else {
+          i_++;
+          mn = c == '+' ? 1 : 0;
+          mx = c == '?' ? 1 : -1;
+        }
+        if (is_rep) {
+          if (!eof() && s_[i_] == '?') i_++;
+          if (last_rep) syntax("invalid nested repetition operator");
+          if (cat->sub.empty()) syntax("missing argument to repetition operator");
+          auto r = std::make_unique<Node>();
+          r->kind = Node::Rep;
+          r->min = mn;
+          r->max = mx;
+          r->sub.push_back(std::move(cat->sub.back()));
+          cat->sub.back() = std::move(r);
+          last_rep = true;
+          continue;
+        }
+      }
+      last_rep = false;
+      if (c == '(') {
+        i_++;
+        bool si = fi_, sm = fm_, ss = fs_;
+        bool flags_only = false;
+        if (!eof() && s_[i_] == '?') {
+          i_++;
+          if (!eof() && (s_[i_] == 'P' || s_[i_] == '<')) {
+            if (s_[i_] == 'P') i_++;
+            if (eof() || s_[i_] != '<') syntax("invalid named capture");
+            size_t e = s_.find('>', i_ + 1);
+            if (e == std::string::npos || e == i_ + 1) syntax("invalid named capture");
+            i_ = e + 1;
+          } else {
+            bool neg = false, any = false;
+            for (;;) {
+              if (eof()) syntax("missing closing )");
+              char f = s_[i_++];
+              if (f == 'i') { fi_ = !neg; any = true; }
+              else if (f == 'm') { fm_ = !neg; any = true; }
+              else if (f == 's') { fs_ = !neg; any = true; }
+              else if (f == 'U') { any = true; }
+              else if (f == '-') { if (neg) syntax("invalid or unsupported Perl syntax"); neg = true; any = false; }
+              else if (f == ')') { if (neg && !any) syntax("invalid or unsupported Perl syntax"); flags_only = true; break; }
+              else if (f == ':') { if (neg && !any) syntax("invalid or unsupported Perl syntax"); break; }
+              else syntax("invalid or unsupported Perl syntax");
+            }
+          }
+        }
+        if (flags_only) continue;
+        if (++depth_ > 1000) syntax("expression nests too deeply");
+        NodeP sub = alt();
+        depth_--;
+        if (eof() || s_[i_] != ')') syntax("missing closing )");
+        i_++;
+        fi_ = si; fm_ = sm; fs_ = ss;
+        cat->sub.push_back(std::move(sub));
+        continue;
+      }
+      if (c == '[') { i_++; cat->sub.push_back(cls()); continue; }
+      if (c == '.') {
+        i_++;
+        Ranges r = fs_ ? Ranges{{0, kRuneMax}} : Ranges{{0, 9}, {11, kRuneMax}};
+        auto n = std::make_unique<Node>();
+        n->kind = Node::Chars;
+        n->chars = r;
+        cat->sub.push_back(std::move(n));
+        continue;
+      }
+      if (c == '^' || c == '$') {
+        i_++;
+        auto n = std::make_unique<Node>();
+        n->kind = Node::Assert;
+        n->op = c == '^' ? (fm_ ? kBOL : kBOT) : (fm_ ? kEOL : kEOT);
+        cat->sub.push_back(std::move(n));
+        continue;
+      }
+      uint32_t r;
+      if (c == '\\') {
+        i_++;
+        char pk = 0;
+        bool pn = false;
+        uint8_t op = 0;
+        int k = escape(r, pk, pn, op, false);
+        if (k == 1) { Ranges t; perl(t, pk, pn); cat->sub.push_back(chars(t, false)); continue; }
+        if (k == 2) {
+          auto n = std::make_unique<Node>();
+          n->kind = Node::Assert;
+          n->op = op;
+          cat->sub.push_back(std::move(n));
+          continue;
+        }
+      } else {
+        int w;
+        r = rune(w);
+        i_ += w;
+      }
+      if (fi_ && r >= 0x80) unsupported("unsupported: (?i) with non-ASCII literal");
+      cat->sub.push_back(chars(Ranges{{r, r}}, false));
+    }
+    return cat;
+  }
+
+  NodeP alt() {
+    auto a = std::make_unique<Node>();
+    a->kind = Node::Alt;
+    for (;;) {
+      a->sub.push_back(concat());
+      if (!eof() && s_[i_] == '|') { i_++; continue; }
+      break;
+    }
+    return a;
+  }
+};
+
+// ---------------- Thompson NFA ----------------
+struct Inst {
+  enum Op : uint8_t { Rune, Split, Empty, Match, Nop } op;
+  int out = -1, out1 = -1;
+  uint8_t eop = 0;
+  int ranges = -1;   // index into rangesets
+};
+
+struct Nfa {
+  std::vector<Inst> prog;
+  std::vector<Ranges> sets;
+  int start = 0;
+};
+
+struct Frag {
+  int start;
+  std::vector<int*> holes;  // pointers are unstable across reallocation: store (pc, which)
+};
+struct Hole { int pc; bool second; };
+struct FragH { int start; std::vector<Hole> holes; };
+
+class Compiler {
+ public:
+  Nfa nfa;
+  FragH comp(const Node* n) {
+    if (nfa.prog.size() > 100000) throw ParseError{RegexStatus::TooLarge, "expression too large"};
+    switch (n->kind) {
+      case Node::Empty: return nop();
+      case Node::Chars: {
+        int pc = emit(Inst::Rune);
+        nfa.sets.push_back(n->chars);
+        nfa.prog[pc].ranges = (int)nfa.sets.size() - 1;
+        return {pc, {{pc, false}}};
+      }
+      case Node::Assert: {
+        int pc = emit(Inst::Empty);
+        nfa.prog[pc].eop = n->op;
+        return {pc, {{pc, false}}};
+      }
+      case Node::Cat: {
+        if (n->sub.empty()) return nop();
+        FragH f = comp(n->sub[0].get());
+        for (size_t k = 1; k < n->sub.size(); k++) {
+          FragH g = comp(n->sub[k].get());
+          patch(f.holes, g.start);
+          f.holes = std::move(g.holes);
+        }
+        return f;
+      }
+      case Node::Alt: {
+        if (n->sub.size() == 1) return comp(n->sub[0].get());
+        FragH last = comp(n->sub.back().get());
+        for (int k = (int)n->sub.size() - 2; k >= 0; k--) {
+          FragH f = comp(n->sub[k].get());
+          int sp = emit(Inst::Split);
+          nfa.prog[sp].out = f.start;
+          nfa.prog[sp].out1 = last.start;
+          f.holes.insert(f.holes.end(), last.holes.begin(), last.holes.end());
+          last = {sp, std::move(f.holes)};
+        }
+        return last;
+      }
+      case Node::Rep: {
+        const Node* x = n->sub[0].get();
+        FragH acc{-1, {}};
+        bool have = false;
+        auto append = [&](FragH g) {
+          if (!have) { acc = std::move(g); have = true; return; }
+          patch(acc.holes, g.start);
+          acc.holes = std::move(g.holes);
+        };
+        for (int k = 0; k < n->min; k++) append(comp(x));
+        if (n->max < 0) {
+          FragH b = comp(x);
+          int sp = emit(Inst::Split);
+          nfa.prog[sp].out = b.start;
+          patch(b.holes, sp);
+          append(FragH{sp, {{sp, true}}});
+        } else {
+          for (int k = n->min; k < n->max; k++) {
+            FragH b = comp(x);
+            int sp = emit(Inst::Split);
+            nfa.prog[sp].out = b.start;
+            std::vector<Hole> h = b.holes;
+            h.push_back({sp, true});
+            append(FragH{sp, std::move(h)});
+          }
+        }
+        if (!have) return nop();
+        return acc;
+      }
+    }
+    return nop();
+  }
+
+ private:
+  int emit(Inst::Op op) {
+    Inst i;
+    i.op = op;
+    nfa.prog.push_back(i);
+    return (int)nfa.prog.size() - 1;
+  }
+  FragH nop() {
+    int pc = emit(Inst::Nop);
+    return {pc, {{pc, false}}};
+  }
+  void patch(const std::vector<Hole>& hs, int to) {
+    for (auto& h : hs) (h.second ? nfa.prog[h.pc].out1 : nfa.prog[h.pc].out) = to;
+  }
+};
+
+// rune "type" for EmptyOpContext: 0 = none (begin/end of text), 1 = '\n',
+// 2 = word char, 3 = other
+constexpr int kTypeBot = 0, kTypeNL = 1, kTypeWord = 2, kTypeOther = 3;
+
+uint8_t context(int t1, int t2) {  // regexp/syntax.EmptyOpContext
+  uint8_t op = kNWB;
+  int b = 0;
+  if (t1 == kTypeWord) b = 1;
+  else if (t1 == kTypeNL) op |= kBOL;
+  else if (t1 == kTypeBot) op |= kBOT | kBOL;
+  if (t2 == kTypeWord) b ^= 1;
+  else if (t2 == kTypeNL) op |= kEOL;
+  else if (t2 == kTypeBot) op |= kEOT | kEOL;
+  if (b) op ^= (kWB | kNWB);
+  return op;
+}
+
+// epsilon closure of `set` under context ctx; leaves only Rune insts in set.
+void closure(const Nfa& nfa, std::vector<int>& set, uint8_t ctx, std::vector<char>& seen, bool& match) {
+  std::vector<int> stack(set.begin(), set.end());
+  std::vector<int> visited;
+  set.clear();
+  while (!stack.empty()) {
+    int pc = stack.back();
+    stack.pop_back();
+    if (pc < 0 || seen[pc]) continue;
+    seen[pc] = 1;
+    visited.push_back(pc);
+    const Inst& in = nfa.prog[pc];
+    switch (in.op) {
+      case Inst::Match: match = true; break;
+      case Inst::Nop: stack.push_back(in.out); break;
+      case Inst::Split: stack.push_back(in.out1); stack.push_back(in.out); break;
+      case Inst::Empty: if ((in.eop & ~ctx) == 0) stack.push_back(in.out); break;
+      case Inst::Rune: set.push_back(pc); break;
+    }
+  }
+  for (int pc : visited) seen[pc] = 0;
+}
+
+}  // namespace
+
+RegexStatus regex_syntax_check(const std::string& pattern, std::string& err) {
+  try {
+    Parser p(pattern);
+    p.parse();
+    return RegexStatus::Ok;
+  } catch (const ParseError& e) {
+    err = "error parsing regexp: " + e.msg + ": `" + pattern + "`";
+    return e.st == RegexStatus::Unsupported ? RegexStatus::Ok : e.st;   // Go accepts these
+  }
+}
+
+RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) {
+  NodeP root;
+  Compiler cc;
+  try {
+    Parser p(pattern);
+    root = p.parse();
+    FragH f = cc.comp(root.get());
+    Inst m;
+    m.op = Inst::Match;
+    cc.nfa.prog.push_back(m);
+    int mpc = (int)cc.nfa.prog.size() - 1;
+    for (auto& h : f.holes) (h.second ? cc.nfa.prog[h.pc].out1 : cc.nfa.prog[h.pc].out) = mpc;
+    cc.nfa.start = f.start;
+  } catch (const ParseError& e) {
+    err = "error parsing regexp: " + e.msg + ": `" + pattern + "`";
+    return e.st;
+  }
+  const Nfa& nfa = cc.nfa;
+
+  // rune equivalence classes: boundaries of every set, plus '\n' and the word
+  // chars so that each class has one EmptyOpContext type.
+  std::vector<uint32_t> cuts = {0, kRuneMax + 1, '\n', '\n' + 1, '0', '9' + 1, 'A', 'Z' + 1, '_', '_' + 1, 'a', 'z' + 1, 0x80};
+  for (auto& s : nfa.sets)
+    for (auto& r : s) { cuts.push_back(r.first); cuts.push_back(r.second + 1); }
+  std::sort(cuts.begin(), cuts.end());
+  cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+  // elementary intervals [cuts[k], cuts[k+1]) -> signature -> class
+  std::map<std::vector<uint8_t>, uint32_t> sig2cls;
+  std::vector<uint32_t> iv_cls;
+  std::vector<int> cls_type;
+  auto rtype = [](uint32_t r) {
+    if (r == '\n') return kTypeNL;
+    if ((r >= '0' && r <= '9') || (r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z') || r == '_') return kTypeWord;
+    return kTypeOther;
+  };
+  for (size_t k = 0; k + 1 < cuts.size(); k++) {
+    uint32_t lo = cuts[k];
+    std::vector<uint8_t> sig(nfa.sets.size() + 1);
+    for (size_t si = 0; si < nfa.sets.size(); si++) {
+      bool in = false;
+      for (auto& r : nfa.sets[si]) if (lo >= r.first && lo <= r.second) { in = true; break; }
+      sig[si] = in;
+    }
+    sig.back() = (uint8_t)rtype(lo);
+    auto it = sig2cls.find(sig);
+    uint32_t c;
+    if (it == sig2cls.end()) {
+      c = (uint32_t)sig2cls.size();
+      sig2cls.emplace(sig, c);
+      cls_type.push_back(rtype(lo));
+    } else {
+      c = it->second;
+    }
+    iv_cls.push_back(c);
+  }
+  uint32_t ncls = (uint32_t)sig2cls.size();
+  if (ncls > 255) { err = "regexp needs more than 255 rune classes"; return RegexStatus::TooLarge; }
+  out = Dfa{};
+  out.nclasses = ncls;
+  for (size_t k = 0; k + 1 < cuts.size(); k++) {
+    uint32_t lo = cuts[k], hi = cuts[k + 1] - 1;
+    if (lo < 0x80) {
+      for (uint32_t r = lo; r <= std::min<uint32_t>(hi, 0x7F); r++) out.ascii_class[r] = (uint8_t)iv_cls[k];
+    } else {
+      if (!out.hi_lo.empty() && out.hi_cls.back() == iv_cls[k] && out.hi_hi.back() + 1 == lo) out.hi_hi.back() = hi;
+      else { out.hi_lo.push_back(lo); out.hi_hi.push_back(hi); out.hi_cls.push_back((uint8_t)iv_cls[k]); }
+    }
+  }
+  // set membership per class (any interval of the class is representative)
+  std::vector<std::vector<uint8_t>> cls_in(ncls, std::vector<uint8_t>(nfa.sets.size()));
+  for (auto& kv : sig2cls)
+    for (size_t si = 0; si < nfa.sets.size(); si++) cls_in[kv.second][si] = kv.first[si];
+
+  // subset construction.  DFA state = (sorted Rune-inst set before closure,
+  // type of previous rune).  The start inst is re-injected at every position
+  // (unanchored search).  MATCH is absorbing.
+  struct Key {
+    std::vector<int> set;
+    int prev;
+    bool operator<(const Key& o) const { return prev != o.prev ? prev < o.prev : set < o.set; }
+  };
+  std::map<Key, uint32_t> ids;
+  std::vector<Key> states;
+  std::vector<char> seen(nfa.prog.size(), 0);
+  const uint32_t kMatch = 0;
+  // state 0 = MATCH sink
+  states.push_back(Key{{}, -1});
+  auto intern = [&](Key k) -> uint32_t {
+    auto it = ids.find(k);
+    if (it != ids.end()) return it->second;
+    uint32_t id = (uint32_t)states.size();
+    ids.emplace(k, id);
+    states.push_back(std::move(k));
+    return id;
+  };
+  uint32_t start = intern(Key{{}, kTypeBot});
+  std::vector<uint16_t> trans;
+  std::vector<uint8_t> acc_end;
+  trans.resize(ncls);  // row for MATCH
+  for (uint32_t c = 0; c < ncls; c++) trans[c] = kMatch;
+  acc_end.push_back(1);
+  for (uint32_t s = 1; s < states.size(); s++) {
+    if (states.size() > Dfa::kMaxStates) { err = "regexp DFA exceeds " + std::to_string(Dfa::kMaxStates) + " states"; return RegexStatus::TooLarge; }
+    Key cur = states[s];
+    std::vector<uint16_t> row(ncls);
+    for (uint32_t c = 0; c < ncls; c++) {
+      std::vector<int> set = cur.set;
+      set.push_back(nfa.start);
+      bool match = false;
+      closure(nfa, set, context(cur.prev, cls_type[c]), seen, match);
+      if (match) { row[c] = kMatch; continue; }
+      std::vector<int> next;
+      for (int pc : set) {
+        const Inst& in = nfa.prog[pc];
+        if (cls_in[c][in.ranges]) next.push_back(in.out);
+      }
+      std::sort(next.begin(), next.end());
+      next.erase(std::unique(next.begin(), next.end()), next.end());
+      uint32_t t = intern(Key{std::move(next), cls_type[c]});
+      row[c] = (uint16_t)t;
+    }
+    trans.insert(trans.end(), row.begin(), row.end());
+    {
+      std::vector<int> set = cur.set;
+      set.push_back(nfa.start);
+      bool match = false;
+      closure(nfa, set, context(cur.prev, kTypeBot), seen, match);
+      acc_end.push_back(match ? 1 : 0);
+    }
+  }
+  out.nstates = (uint32_t)states.size();
+  out.start = start;
+  out.match = kMatch;
+  out.trans = std::move(trans);
+  out.accept_end = std::move(acc_end);
+  return RegexStatus::Ok;
+}
+
+bool dfa_match(const Dfa& d, const uint8_t* s, size_t n) {
+  uint32_t st = d.start;
+  size_t i = 0;
+  while (i < n) {
+    if (st == d.match) return true;
+    int w;
+    uint32_t r = decode(s + i, n - i, w);
+    i += (size_t)w;
+    uint32_t c;
+    if (r < 0x80) c = d.ascii_class[r];
+    else {
+      size_t lo = 0, hi = d.hi_lo.size();
+      c = 0;
+      while (lo < hi) {
+        size_t m = (lo + hi) / 2;
+        if (r < d.hi_lo[m]) hi = m;
+        else if (r > d.hi_hi[m]) lo = m + 1;
+        else { c = d.hi_cls[m]; break; }
+      }
+    }
+    st = d.trans[(size_t)st * d.nclasses + c];
+  }
+  return st == d.match || d.accept_end[st];
+}
+
+}  // namespace ose

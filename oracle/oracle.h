@@ -1,0 +1,82 @@
+/*
+ * oracle.h — CPU restatement of the reference hot path.  TEST INFRASTRUCTURE.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker / the timed CPU baseline; the
+ * product (odigos_amd) never links or calls it.
+ *
+ * Each function restates a function of damemi/odigos @ 2026-02-13 (paths
+ * relative to collector/processors/) over the columnar batch defined in
+ * include/odigos_amd.h.  Parity is pinned by the reference's own known-answer
+ * tests, transcribed as data under tests/golden/ (Go is not available, so the
+ * reference cannot be run here; see DESIGN.md "Oracle").
+ */
+#ifndef OSE_ORACLE_H
+#define OSE_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+#include "../include/odigos_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- regexp (Go RE2 syntax subset, backtracking; oracle-private) ----- */
+typedef struct orc_re orc_re;
+/* returns NULL and fills err on a syntax error the Go parser would reject */
+orc_re* orc_re_compile(const char* pattern, char* err, size_t errcap);
+/* regexp.MatchString semantics: unanchored search over the UTF-8 string */
+int orc_re_match(const orc_re* re, const uint8_t* s, size_t n);
+void orc_re_free(orc_re* re);
+
+/* ---- odigosurltemplate -------------------------------------------------- */
+typedef struct orc_url orc_url;
+/* rules: templatization_rules strings; custom_*: custom_ids (regexp,
+ * template_name).  Returns NULL + err on the errors
+ * newUrlTemplateProcessor / Config.Validate return (processor.go:27-69,
+ * config.go:133-157). */
+orc_url* orc_url_create(const char* const* rules, int n_rules,
+                        const char* const* custom_regexps,
+                        const char* const* custom_names, int n_custom,
+                        char* err, size_t errcap);
+void orc_url_free(orc_url* u);
+
+/* getSegmentTemplatizationString (templatize.go:242-269): writes the name
+ * (without braces) into out and returns its length, or -1 if the segment is
+ * not an id.  out must hold >= 256 bytes. */
+int orc_url_segment_name(const orc_url* u, const uint8_t* seg, size_t n, char* out);
+
+/* applyTemplatizationOnPath (processor.go:149-186): returns the templated
+ * path length written to out (cap bytes), or -1 if cap is too small. */
+long orc_url_apply_path(const orc_url* u, const uint8_t* path, size_t n,
+                        uint8_t* out, size_t cap);
+
+/* processTraces over a whole batch (processor.go:71-96 + 235-287): fills
+ * outs->url_out, outs->tmpl and outs->tmpl_arena (compact, span order) and
+ * *outs->tmpl_arena_used.  nthreads >= 1 splits the spans over pthreads.
+ * Returns 0, or -1 if the arena capacity is exceeded. */
+int orc_url_process(const orc_url* u, const ose_columns* c, ose_outputs* o,
+                    int nthreads);
+
+/* ---- odigossampling ------------------------------------------------------ */
+typedef struct orc_sampling orc_sampling;
+/* cfg_json: the "odigossampling" config object (global_rules, service_rules,
+ * endpoint_rules); services[] gives the interned id order used for res_svc. */
+orc_sampling* orc_sampling_create(const char* cfg_json, char* err, size_t errcap);
+void orc_sampling_free(orc_sampling* s);
+/* interned id of a rule service name (same contract as ose_engine_service_id) */
+uint32_t orc_sampling_service_id(const orc_sampling* s, const char* name, size_t len);
+int orc_sampling_process(const orc_sampling* s, const ose_columns* c, ose_outputs* o,
+                         uint32_t group_mode, const ose_rand* rnd, int nthreads);
+
+/* ---- odigostrafficmetrics -------------------------------------------------- */
+/* Adds ResourceSpansSize(after mutation) * inverse per attribute set and the
+ * span count (processor.go:71-84).  keep/url_out/tmpl may be NULL. */
+int orc_size_process(const ose_columns* c, const ose_outputs* in_results,
+                     ose_outputs* o, int64_t inverse, double sampling_ratio,
+                     const ose_rand* rnd, int gogo_always_emit);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

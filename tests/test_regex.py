@@ -1,0 +1,130 @@
+"""Regexp semantics: the product's DFA compiler (regex_dfa.cpp, evaluated on
+the host through a test seam) against the oracle's independent backtracker
+(oracle/regex.c), and both against Python's `re` where the two dialects agree
+(ASCII input, `$` rewritten to `\\Z`: Go's `$` is end-of-text without (?m))."""
+import random
+import re
+
+import pytest
+
+from odigos_amd import native
+from tests.oracle_lib import Regex
+
+# patterns from the reference (templatize.go:10-74, README.md custom-id examples,
+# processor_test.go rules) plus syntax coverage
+PATTERNS = [
+    r"^[\d_\-!@#$%^&*()=+{}\[\]:;\"'<>,.?/\\|`~]+$",
+    r"(^[0-9a-fA-F]{8}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{12})|([0-9a-fA-F]{8}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{12}$)",
+    r"^(?:[0-9a-fA-F]{2}){8,}$",
+    r"\d{7,}",
+    r"^\d{4}-\d{2}-\d{2}(?:T\d{2}:\d{2}(?::\d{2})?)?(?:Z|[+-]\d{4})?$",
+    r"^[a-zA-Z0-9._%+-]+@[a-zA-Z0-9.-]+\.[a-zA-Z]{2,}$",
+    r"^in_[0-9]+$", r"^out_[0-9]+$", r"\d+", r"[0-9]+", r"[a-zA-Z]+", r"api-v\d+",
+    r"^SA_\d{4}_\w{2}$", r"^(dev|staging|prod)-[a-z]+-\d{3}$", r"^backup_\d{8}_\d{6}$",
+    r"^v\d+\.\d+\.\d+(-[a-z]+)?$", r"^svc_[a-z]+_[a-zA-Z0-9]+$", r"^svc-[a-z]{2}-[a-z]+-\d-[a-z0-9]+$",
+    r"^ap\d+", r"^v[0-9]+\.[0-9]+$", r"a|b|", r"(ab)*c?", r"x{2,3}y{0,}", r"[^a-c]+", r"\bfoo\b", r"\Bo",
+    r"(?i)abc", r"(?i)[a-f]+$", r"(?s).", r".", r"\Afoo\z", r"(?m)^bar$", r"(?:)", r"", r"a{0}", r"[[:alpha:]]+\d",
+    r"\x41\x{42}", r"[\d\s]+", r"\W+", r"(?i)\W", r"[^\n]*$",
+]
+
+
+def _dfa(pattern, s: bytes):
+    r = native.lib().osehost_regex_match(pattern.encode(), s, len(s))
+    assert r >= 0, (pattern, r)
+    return bool(r)
+
+
+def _py(pattern):
+    """Go -> Python `re` for the shared subset: unescaped `$` outside a class
+    becomes `\\Z` (end of text), `\\z` -> `\\Z`, `\\x{..}` -> `\\x..`."""
+    out, i, in_cls = [], 0, False
+    while i < len(pattern):
+        c = pattern[i]
+        if c == "\\":
+            nxt = pattern[i + 1]
+            if nxt == "z":
+                out.append(r"\Z")
+            elif nxt == "x" and pattern[i + 2] == "{":
+                j = pattern.index("}", i)
+                out.append(r"\x" + pattern[i + 3:j].rjust(2, "0"))
+                i = j + 1
+                continue
+            else:
+                out.append(pattern[i:i + 2])
+            i += 2
+            continue
+        if in_cls:
+            if c == "]":
+                in_cls = False
+        elif c == "[":
+            in_cls = True
+            if pattern.startswith("[[:alpha:]]", i):
+                out.append("[a-zA-Z]")
+                i += len("[[:alpha:]]")
+                in_cls = False
+                continue
+        elif c == "$" and "(?m)" not in pattern:
+            out.append(r"\Z")
+            i += 1
+            continue
+        out.append(c)
+        i += 1
+    return re.compile("".join(out).encode(), re.DOTALL if "(?s)" in pattern else 0)
+
+
+ALPHABET = "aAbcfFkKsSxyz019_-.@:+/ \nT"
+
+
+def _rand_strings(rng, n):
+    out = [b"", b"a", b"\n", b"foo", b"foo bar", b"in_005", b"api-v2", b"2025-12-04T14:55:04+0000",
+           b"123e4567-e89b-12d3-a456-426614174000", b"abc@def.com", b"barx\nbar", b"xxyy", b"ABC"]
+    for _ in range(n):
+        k = rng.randrange(0, 24)
+        out.append("".join(rng.choice(ALPHABET) for _ in range(k)).encode())
+    return out
+
+
+@pytest.mark.parametrize("pattern", PATTERNS)
+def test_dfa_vs_oracle_vs_python(pattern):
+    rng = random.Random(hash(pattern) & 0xFFFF)
+    orc = Regex(pattern)
+    py = _py(pattern)
+    for s in _rand_strings(rng, 300):
+        d = _dfa(pattern, s)
+        o = orc.match(s)
+        assert d == o, (pattern, s)
+        assert o == bool(py.search(s)), (pattern, s)
+
+
+NON_ASCII = [
+    (r"�", "x�y".encode(), True),
+    (r"�", b"bad\xc3x", True),          # invalid byte decodes to U+FFFD
+    (r"�", b"truncated\xe2\x82", True),
+    (r"�", "café".encode(), False),
+    (r".", b"\xff", True),               # '.' matches RuneError
+    (r"^.$", "é".encode(), True),   # one rune, two bytes
+    (r"^..$", "é".encode(), False),
+    (r"(?i)k", "K".encode(), True),  # Kelvin sign folds to k
+    (r"(?i)\W", "K".encode(), False),
+    (r"(?i)[\W]", "K".encode(), False),
+    (r"(?i)[^\w]", "K".encode(), False),
+    (r"[^a]", "é".encode(), True),
+    (r"\w", "é".encode(), False),
+]
+
+
+@pytest.mark.parametrize("pattern,s,expect", NON_ASCII)
+def test_utf8_semantics(pattern, s, expect):
+    assert _dfa(pattern, s) == expect
+    assert Regex(pattern).match(s) == expect
+
+
+@pytest.mark.parametrize("bad", ["(", ")", "[a", "a**", "*a", "x{1001}", "x{3,2}", r"\q", "(?z)", "a{2}{3}"])
+def test_syntax_errors(bad):
+    assert native.lib().osehost_regex_match(bad.encode(), b"", 0) == -1
+    with pytest.raises(ValueError):
+        Regex(bad)
+
+
+def test_unsupported_is_reported_not_guessed():
+    assert native.lib().osehost_regex_match(r"\p{Greek}".encode(), b"", 0) == -2

@@ -1,0 +1,125 @@
+"""odigosurltemplate known-answer tests, transcribed from the reference's
+processor_test.go / factory_test.go (tests/golden/url_kats.json).
+
+Each case is run twice:
+* CPU: host columnariser -> oracle (oracle/url.c) -> host apply, which pins
+  the oracle and the host layer against the reference's expected outputs;
+* GPU (@gpu): the full ConsumeTraces path through the HIP engine.
+"""
+import json
+from pathlib import Path
+
+import pytest
+
+from odigos_amd import host
+from tests.oracle_lib import UrlOracle
+
+GOLD = json.loads((Path(__file__).parent / "golden" / "url_kats.json").read_text())
+
+
+def _case_traces(service, span_name, kind, attrs):
+    res = {}
+    if service:
+        # generateTraceData (processor_test.go:13-26)
+        res = {"service.name": service, "k8s.namespace.name": "default", "k8s.deployment.name": service}
+    return host.traces(host.resource_spans(res, [host.span(name=span_name, kind=kind, attributes=attrs)]))
+
+
+def _all_cases():
+    out = []
+    for g in GOLD["groups"]:
+        for c in g["cases"]:
+            out.append(dict(cfg=g["config"], traces=_case_traces(c["span"], c["span"], c["kind"], c["attrs"]),
+                            name=c["expect_name"], key=c["expect_key"], value=c["expect_value"],
+                            id=f'{g["test"]}:{c["line"]}:{c["name"]}'))
+    for c in GOLD["rule_cases"]["cases"]:
+        cfg = {}
+        if "rules" in c:
+            cfg["templatization_rules"] = c["rules"]
+        if "custom_ids" in c:
+            cfg["custom_ids"] = c["custom_ids"]
+        attrs = {"http.request.method": "GET", "url.path": c["path"]}
+        out.append(dict(cfg=cfg, traces=_case_traces("test-service-name", "GET", 2, attrs)
+                        if False else host.traces(host.resource_spans(
+                            {"service.name": "test-service-name", "k8s.namespace.name": "default",
+                             "k8s.deployment.name": "test-service-name"},
+                            [host.span(name="GET", kind=2, attributes=attrs)])),
+                        name=c["expect_name"], key="http.route", value=c["expect_route"],
+                        id=f'rules:{c["line"]}:{c["name"]}'))
+    ie = GOLD["include_exclude"]
+    for c in ie["cases"]:
+        cfg = {}
+        if "include" in c:
+            cfg["include"] = {"k8s_workloads": c["include"]}
+        if "exclude" in c:
+            cfg["exclude"] = {"k8s_workloads": c["exclude"]}
+        attrs = {"http.request.method": "GET", "url.path": "/user/1234"}
+        tr = host.traces(host.resource_spans(
+            {"service.name": "test-service-name", "k8s.namespace.name": "default",
+             "k8s.deployment.name": "test-service-name"},
+            [host.span(name="GET", kind=2, attributes=attrs)]))
+        if c["templated"]:
+            out.append(dict(cfg=cfg, traces=tr, name="GET /user/{id}", key="http.route", value="/user/{id}",
+                            id=f'include_exclude:{c["line"]}:{c["name"]}'))
+        else:
+            out.append(dict(cfg=cfg, traces=tr, name="GET", key="http.route", value=None,
+                            id=f'include_exclude:{c["line"]}:{c["name"]}'))
+    return out
+
+
+CASES = _all_cases()
+
+
+def _check(out_traces, case):
+    sp = out_traces["resourceSpans"][0]["scopeSpans"][0]["spans"][0]
+    assert sp["name"] == case["name"], case["id"]
+    v = host.find_attr(sp, case["key"]) if case["key"] else None
+    if case["value"] is None:
+        assert v is None, f'{case["id"]}: unexpected {case["key"]}={v}'
+    else:
+        assert v is not None, f'{case["id"]}: missing {case["key"]}'
+        assert host.as_string(v) == case["value"], case["id"]
+
+
+def test_fixture_count():
+    # 24 + 4 + 5 + 3 + 9 + 6 default cases, 20 rule/custom-id cases, 7 include/exclude
+    assert len(CASES) == 78
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["id"] for c in CASES])
+def test_kat_oracle(case):
+    proc = host.Processor("odigosurltemplate", case["cfg"])
+    hb = proc.columnarize(case["traces"])
+    orc = UrlOracle(case["cfg"])
+    assert orc.process(hb.cols, hb.outs) == 0
+    _check(hb.apply(), case)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c["id"] for c in CASES])
+def test_kat_gpu(case):
+    proc = host.Processor("odigosurltemplate", case["cfg"])
+    _check(proc.consume(case["traces"]), case)
+
+
+@pytest.mark.parametrize("rule", [c["rule"] for c in GOLD["invalid_rules"]["cases"]])
+def test_invalid_rules_rejected(rule):
+    # TestInvalidRules (factory_test.go:33-58): CreateTraces returns an error
+    with pytest.raises(ValueError):
+        host.Processor("odigosurltemplate", {"templatization_rules": [rule]})
+    with pytest.raises(ValueError):
+        UrlOracle({"templatization_rules": [rule]})
+
+
+def test_default_config_and_validation():
+    # TestCreateDefaultConfig / config.go:103-157
+    host.Processor("odigosurltemplate", {})
+    bad = [
+        {"exclude": {"k8s_workloads": [{"namespace": "", "kind": "Deployment", "name": "x"}]}},
+        {"include": {"k8s_workloads": [{"namespace": "ns", "kind": "Pod", "name": "x"}]}},
+        {"include": {"k8s_workloads": [{"namespace": "ns", "kind": "Deployment", "name": ""}]}},
+        {"custom_ids": [{"regexp": "(unclosed"}]},
+    ]
+    for cfg in bad:
+        with pytest.raises(ValueError):
+            host.Processor("odigosurltemplate", cfg)
