@@ -30,6 +30,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 WORKLOADS = {
     "url": dict(gen="url", seed=0x0D160002, spans=10_000_000,
                 cfg={"odigosurltemplate": {}}, stages="TEMPLATE",
+                # no include/exclude configured: the shim passes res_url_ok = NULL
+                null_columns=("res_url_ok",),
+                fields=("arena", "kind", "url_flags", "path"),
                 metric_config="C2: URL templatization only, 10M spans/GPU, C2 segment mix, default rules"),
 }
 
@@ -103,8 +106,10 @@ def main():
     n_spans = args.spans or wl["spans"]
     stages = getattr(native, "STAGE_" + wl["stages"])
     gen = Generator(wl["gen"], seed=wl["seed"] + rank, n_spans=n_spans, threads=16)
+    for f in wl.get("null_columns", ()):
+        setattr(gen.cols, f, None)   # columns the configured processors do not read
     eng = Engine(wl["cfg"])
-    db = DeviceBatch(gen.cols)
+    db = DeviceBatch(gen.cols, fields=wl.get("fields"))
     eng.reserve(n_spans)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream

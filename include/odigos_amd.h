@@ -149,7 +149,8 @@ typedef struct ose_columns {
   /* per resource */
   const uint32_t* res_svc;      /* ose_engine_service_id(AsString(service.name)) or OSE_NONE */
   const uint32_t* res_svc_str;  /* same, only if service.name is ValueTypeStr, else OSE_NONE */
-  const uint8_t* res_url_ok;    /* include/exclude PropertiesMatcher verdict (filtermatcher.go) */
+  const uint8_t* res_url_ok;    /* include/exclude PropertiesMatcher verdict (filtermatcher.go);
+                                   NULL = every resource passes (no include/exclude configured) */
   const uint32_t* res_attrset;  /* interned attributeSetFromResource (processor.go:60-69) */
   const uint32_t* res_size;     /* ResourceSpans bytes excluding its scope_spans fields */
 

@@ -104,7 +104,7 @@ class DeviceBatch:
             setattr(self.cols, f, getattr(host_cols, f))
         self.t = {}
         for name, (dim, size) in COLUMN_LAYOUT.items():
-            if fields is not None and name not in fields:
+            if (fields is not None and name not in fields) or not getattr(host_cols, name):
                 continue
             n = _count(host_cols, dim) * size
             if name == "arena":

@@ -82,23 +82,113 @@ __device__ inline uint64_t lookback_prefix(uint64_t* status, uint32_t tile, uint
 struct ByteReader {
   const uint8_t* base;
   uint64_t cached = ~0ull;
-  uint4 chunk;
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;   // named registers: a uint4 member with a runtime
+                                             // word index is lowered to scratch (guide §5.4 rule 20)
   __device__ explicit ByteReader(const uint8_t* b) : base(b) {}
   __device__ __forceinline__ uint32_t at(uint32_t i) {
     uint64_t addr = (uint64_t)(base + i);
     uint64_t al = addr & ~15ull;
     if (al != cached) {
-      chunk = *reinterpret_cast<const uint4*>(al);
+      uint4 v = *reinterpret_cast<const uint4*>(al);
+      c0 = v.x; c1 = v.y; c2 = v.z; c3 = v.w;
       cached = al;
     }
     uint32_t o = (uint32_t)(addr & 15);
-    uint32_t w = (o & 8) ? ((o & 4) ? chunk.w : chunk.z) : ((o & 4) ? chunk.y : chunk.x);
+    uint32_t m4 = 0u - ((o >> 2) & 1u), m8 = 0u - ((o >> 3) & 1u);
+    uint32_t lo = (c0 & ~m4) | (c1 & m4);
+    uint32_t hi = (c2 & ~m4) | (c3 & m4);
+    uint32_t w = (lo & ~m8) | (hi & m8);
     return (w >> ((o & 3) * 8)) & 0xFFu;
+  }
+  // bytes i..i+3, little-endian (reads up to 3 bytes past the string: arena slack)
+  __device__ __forceinline__ uint32_t word(uint32_t i) {
+    return at(i) | (at(i + 1) << 8) | (at(i + 2) << 16) | (at(i + 3) << 24);
+  }
+  struct Stream {
+    ByteReader* rd;
+    uint32_t q;
+    __device__ __forceinline__ uint32_t next() { uint32_t x = rd->word(q); q += 4; return x; }
+  };
+  __device__ __forceinline__ Stream stream(uint32_t i) { return Stream{this, i}; }
+};
+
+// Reader over bytes staged in LDS.  Single bytes are ds_read_u8; words are
+// two aligned ds_read_b32 funnel-shifted with v_alignbyte_b32, and a stream
+// carries the upper dword into the next step (one LDS read per 4 bytes).
+typedef const __attribute__((address_space(3))) uint8_t lds_u8;
+typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+struct LdsReader {
+  lds_u32* base;   // 4-byte aligned slice
+  uint32_t off;    // string start within the slice
+  __device__ LdsReader(lds_u32* b, uint32_t o) : base(b), off(o) {}
+  __device__ __forceinline__ uint32_t at(uint32_t i) const { return ((lds_u8*)base)[off + i]; }
+  __device__ __forceinline__ uint32_t word(uint32_t i) const {
+    const uint32_t p = off + i;
+    return __builtin_amdgcn_alignbyte(base[(p >> 2) + 1], base[p >> 2], p & 3);
+  }
+  // the dword after next is loaded one step ahead so its latency overlaps
+  // the caller's work on the current word (reads up to 11 bytes past i)
+  struct Stream {
+    lds_u32* w;
+    uint32_t sh, lo, mid;
+    __device__ __forceinline__ uint32_t next() {
+      const uint32_t x = __builtin_amdgcn_alignbyte(mid, lo, sh);
+      lo = mid;
+      mid = w[2];
+      w++;
+      return x;
+    }
+  };
+  __device__ __forceinline__ Stream stream(uint32_t i) const {
+    const uint32_t p = off + i;
+    return Stream{base + (p >> 2), p & 3, base[p >> 2], base[(p >> 2) + 1]};
   }
 };
 
+// ---------------------------------------------------------------------------
+// SWAR byte classes over a little-endian word of 4 bytes: each result has bit
+// 7 of byte k set when byte k is in the class.  t = (x & 0x7F7F7F7F) | kH;
+// bytes >= 0x80 are masked out by the caller.
+constexpr uint32_t kH = 0x80808080u, kL = 0x01010101u;
+__device__ __forceinline__ uint32_t swar_t(uint32_t x) { return (x & 0x7F7F7F7Fu) | kH; }
+__device__ __forceinline__ uint32_t swar_ge(uint32_t t, uint32_t k) { return (t - k * kL) & kH; }   // byte >= k (k <= 128)
+__device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint32_t k) {                               // byte == k (any byte)
+  const uint32_t y = x ^ (k * kL);
+  return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & kH;
+}
+// high bits of the bytes at index >= rem (rem < 4), 0 when rem >= 4
+__device__ __forceinline__ uint32_t swar_end(uint32_t rem) { return rem >= 4 ? 0u : kH << (8 * rem); }
+// high bits of the bytes before the first flagged byte of stop
+__device__ __forceinline__ uint32_t swar_before(uint32_t stop) { return ((stop & (0u - stop)) - 1u) & kH; }
+// index of the first flagged byte (4 when none)
+__device__ __forceinline__ uint32_t swar_first(uint32_t m) { return m ? (uint32_t)(__ffs(m) - 1) >> 3 : 4u; }
+
+// first index >= q in [q, n) holding byte ch, or n
+template <class Reader>
+__device__ __forceinline__ uint32_t scan_to(Reader& rd, uint32_t q, uint32_t n, uint32_t ch) {
+  auto st = rd.stream(q);
+  for (;;) {
+    const uint32_t stop = swar_eq(st.next(), ch) | swar_end(n - q);
+    if (stop) return q + swar_first(stop);
+    q += 4;
+  }
+}
+// number of bytes ch in [q, n)
+template <class Reader>
+__device__ __forceinline__ uint32_t count_byte(Reader& rd, uint32_t q, uint32_t n, uint32_t ch) {
+  auto st = rd.stream(q);
+  uint32_t c = 0;
+  for (;;) {
+    const uint32_t end = swar_end(n - q);
+    c += __builtin_popcount(swar_eq(st.next(), ch) & swar_before(end));
+    if (end) return c;
+    q += 4;
+  }
+}
+
 // unicode/utf8.DecodeRune on [i, e): invalid -> (U+FFFD, 1)
-__device__ inline uint32_t decode_rune(ByteReader& rd, uint32_t i, uint32_t e, uint32_t& w) {
+template <class Reader>
+__device__ inline uint32_t decode_rune(Reader& rd, uint32_t i, uint32_t e, uint32_t& w) {
   uint32_t c = rd.at(i);
   if (c < 0x80) { w = 1; return c; }
   uint32_t need, r, lo = 0x80, hi = 0xBF;
@@ -122,7 +212,8 @@ __device__ inline uint32_t decode_rune(ByteReader& rd, uint32_t i, uint32_t e, u
 }
 
 // regexp.MatchString via a compiled DFA (regex_dfa.cpp) over bytes [s, e).
-__device__ inline bool dfa_match(const uint8_t* blob, uint32_t dfa_off, ByteReader& rd, uint32_t s, uint32_t e) {
+template <class Reader>
+__device__ inline bool dfa_match(const uint8_t* blob, uint32_t dfa_off, Reader& rd, uint32_t s, uint32_t e) {
   const DfaDev* d = reinterpret_cast<const DfaDev*>(blob + dfa_off);
   const uint16_t* trans = reinterpret_cast<const uint16_t*>(blob + d->trans_off);
   const uint32_t ncls = d->nclasses, match = d->match;

@@ -274,6 +274,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
     return fail(OSE_EINVAL, "TEMPLATE stage needs url_flags, kind, path, arena, url_out, tmpl, tmpl_arena");
   if (e->url_needs_resource && (!c->resource || !c->res_url_ok))
     return fail(OSE_EINVAL, "include/exclude configured: resource and res_url_ok columns are required");
+  if (c->res_url_ok && !c->resource) return fail(OSE_EINVAL, "res_url_ok needs the resource column");
   if (o->tmpl_arena_cap > 0xFFFFFFFFull) return fail(OSE_ERANGE, "tmpl_arena_cap exceeds the 32-bit offset range");
   uint64_t n = c->n_spans;
   uint32_t tiles = (uint32_t)((n + kUrlTile - 1) / kUrlTile);
@@ -290,7 +291,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.url_flags = c->url_flags;
   a.kind = c->kind;
   a.resource = c->resource;
-  a.res_url_ok = e->url_needs_resource ? c->res_url_ok : nullptr;
+  a.res_url_ok = c->res_url_ok;   // NULL: every resource passes (no include/exclude)
   a.path = c->path;
   a.url_out = o->url_out;
   a.tmpl = o->tmpl;

@@ -27,7 +27,7 @@ struct UrlKernelArgs {
   uint32_t* error;             // bit0 look-back timeout, bit1 output overflow
   uint64_t* used;              // bytes written (optional)
 };
-constexpr uint32_t kUrlTile = 256;
+constexpr uint32_t kUrlTile = 1024;   // spans per workgroup tile (url_kernel.hip kTile)
 void launch_url_template(const UrlKernelArgs& a, hipStream_t st);
 
 }  // namespace ose

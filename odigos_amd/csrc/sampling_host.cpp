@@ -17,7 +17,7 @@ int Engine::build_sampling_tables() {
 }
 
 size_t Engine::workspace_bytes(uint64_t n_spans) const {
-  uint64_t tiles = (n_spans + 255) / 256;
+  uint64_t tiles = (n_spans + 1023) / 1024;
   return 4096 + tiles * 8;
 }
 

@@ -1,22 +1,28 @@
 // url_kernel.hip — odigosurltemplate on CDNA4 (gfx950).
 //
-// One launch templatizes a whole batch in a single pass over HBM:
-//   phase 1  one thread per span decides what the reference would do
-//            (processor.go:235-287 enhanceSpan/processSpan), splits the path,
-//            tries the templatization rules with the same segment count in
-//            config order (processor.go:149-171, templatize.go:192-237) and
-//            otherwise classifies every segment (templatize.go:242-269) with
-//            a streaming byte automaton that evaluates all built-in regexps
-//            (noLetters, \d{7,}, UUID, hex, date, email, U+FFFD) in one read,
-//            plus compiled DFAs for custom_ids / rule regexps.  It records
-//            the output length and per-segment decisions in registers.
-//   scan     block scan of output lengths + decoupled look-back across tiles
-//            gives every span its offset in the compact output arena.
-//   phase 2  each thread writes its template into an LDS image of the tile's
-//            output while wave 0 resolves the look-back; the tile image is
-//            then stored to HBM with coalesced stores.
-// Output is byte-identical to the oracle (oracle/url.c): same template bytes,
-// same compact arena layout (span order).
+// One launch templatizes a whole batch in a single pass over HBM.  A
+// workgroup (4 waves) owns a tile of 1024 consecutive spans; each wave
+// processes 4 groups of 64 consecutive spans (one span per lane) on its own,
+// with no workgroup barrier until the tile scan:
+//   stage    the group's path bytes (the arena range its 64 spans reference)
+//            are copied HBM -> the wave's LDS slice with coalesced 16-byte
+//            loads; all per-byte work below reads LDS.
+//   phase 1  each lane plans its span: what the reference does with it
+//            (processor.go:235-287 enhanceSpan/processSpan), the
+//            templatization rules with the same segment count in config order
+//            (processor.go:149-171, templatize.go:192-237), else a
+//            per-segment classification (templatize.go:242-269).  The cheap
+//            pass reads 4 bytes per step and keeps only AND/OR/run
+//            accumulators (noLetters, hex, \d{7,}, '@' count, non-ASCII);
+//            email, UTF-8 (U+FFFD), date and UUID checks run as second
+//            passes only on the segments the cheap pass flags; compiled DFAs
+//            handle custom_ids / rule regexps.  Plans go to LDS.
+//   scan     workgroup scan of output lengths + decoupled look-back across
+//            tiles gives every span its offset in the compact output arena.
+//   phase 2  groups are re-staged (L2-resident by now) and lanes write their
+//            templates into an LDS image of the tile's output, stored to HBM
+//            with coalesced dword stores.
+// Byte-identical to the oracle (oracle/url.c) including the compact arena.
 #include <hip/hip_runtime.h>
 
 #include "../../include/odigos_amd.h"
@@ -26,18 +32,20 @@
 namespace ose {
 namespace {
 
-constexpr int kTile = 256;
-constexpr uint32_t kOutLds = 24 * 1024;   // LDS image of one tile's output
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kGroups = 4;                       // 64-span groups per wave
+constexpr int kTile = kThreads * kGroups;        // spans per workgroup tile
+constexpr uint32_t kStage = 4 * 1024;            // per-wave LDS copy of one group's bytes
+constexpr uint32_t kOutLds = 20 * 1024;          // LDS image of one tile's output
 
 enum : uint32_t { M_NONE = 0, M_RENAME_SLASH, M_SLASH, M_RULE, M_DEFAULT, M_ORIG };
 
 __device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
 __device__ __forceinline__ bool is_alpha(uint32_t c) { return (c | 0x20u) - 'a' < 26u; }
 __device__ __forceinline__ bool is_hex(uint32_t c) { return is_digit(c) || (c | 0x20u) - 'a' < 6u; }
-
-// noLettersRegex class (templatize.go:14) as a 128-bit set
-__device__ __forceinline__ bool is_noletter(uint32_t c) {
-  // digits and _-!@#$%^&*()=+{}[]:;"'<>,.?/\|`~
+// noLettersRegex class (templatize.go:14): digits and _-!@#$%^&*()=+{}[]:;"'<>,.?/\|`~
+__device__ __forceinline__ bool is_nolet(uint32_t c) {
   constexpr uint64_t lo = (1ull << '!') | (1ull << '"') | (1ull << '#') | (1ull << '$') | (1ull << '%') |
                           (1ull << '&') | (1ull << '\'') | (1ull << '(') | (1ull << ')') | (1ull << '*') |
                           (1ull << '+') | (1ull << ',') | (1ull << '-') | (1ull << '.') | (1ull << '/') |
@@ -47,49 +55,115 @@ __device__ __forceinline__ bool is_noletter(uint32_t c) {
                           (1ull << (']' - 64)) | (1ull << ('^' - 64)) | (1ull << ('_' - 64)) |
                           (1ull << ('`' - 64)) | (1ull << ('{' - 64)) | (1ull << ('|' - 64)) |
                           (1ull << ('}' - 64)) | (1ull << ('~' - 64));
-  return c < 64 ? ((lo >> c) & 1) : (c < 128 ? ((hi >> (c - 64)) & 1) : false);
+  uint64_t m = c < 64 ? lo : hi;
+  return c < 128 && ((m >> (c & 63)) & 1);
 }
+// emailRegex classes (templatize.go:70)
 __device__ __forceinline__ bool is_email_local(uint32_t c) {
   return is_alpha(c) || is_digit(c) || c == '.' || c == '_' || c == '%' || c == '+' || c == '-';
 }
-__device__ __forceinline__ bool is_email_domain(uint32_t c) {
-  return is_alpha(c) || is_digit(c) || c == '.' || c == '-';
-}
+__device__ __forceinline__ bool is_email_domain(uint32_t c) { return is_alpha(c) || is_digit(c) || c == '.' || c == '-'; }
 
-// datesRegex (templatize.go:67) as a position automaton; 255 = dead.
-// accepting: 10 (date), 16 (THH:MM), 19 (THH:MM:SS), 30 (Z), 35 (+hhmm)
-__device__ __forceinline__ uint32_t date_step(uint32_t s, uint32_t c) {
-  if (s < 10) {
-    bool ok = (s == 4 || s == 7) ? c == '-' : is_digit(c);
-    return ok ? s + 1 : 255;
-  }
-  switch (s) {
-    case 10: case 16: case 19:
-      if (c == 'T' && s == 10) return 11;
-      if (c == ':' && s == 16) return 17;
-      if (c == 'Z') return 30;
-      if (c == '+' || c == '-') return 31;
-      return 255;
-    case 11: case 12: case 14: case 15: case 17: case 18:
-      return is_digit(c) ? s + 1 : 255;
-    case 13:
-      return c == ':' ? 14 : 255;
-    case 31: case 32: case 33: case 34:
-      return is_digit(c) ? s + 1 : 255;
-    default:
-      return 255;
-  }
+// datesRegex (templatize.go:67) accepts exactly these lengths
+__device__ __forceinline__ bool date_len(uint32_t n) {
+  return n == 10 || n == 11 || n == 15 || n == 16 || n == 17 || n == 19 || n == 20 || n == 21 || n == 22 || n == 24;
 }
-__device__ __forceinline__ bool date_accept(uint32_t s) {
-  return s == 10 || s == 16 || s == 19 || s == 30 || s == 35;
+// `^\d{4}-\d{2}-\d{2}(?:T\d{2}:\d{2}(?::\d{2})?)?(?:Z|[+-]\d{4})?$`: each
+// optional group starts with a byte nothing later may start with, so the
+// greedy parse is the only possible match.
+template <class R>
+__device__ bool date_match(R& rd, uint32_t s, uint32_t n) {
+  auto d = [&](uint32_t k) { return is_digit(rd.at(s + k)); };
+  if (!(d(0) && d(1) && d(2) && d(3) && rd.at(s + 4) == '-' && d(5) && d(6) && rd.at(s + 7) == '-' && d(8) && d(9)))
+    return false;
+  uint32_t p = 10;
+  if (p < n && rd.at(s + p) == 'T') {
+    if (p + 6 > n || !d(p + 1) || !d(p + 2) || rd.at(s + p + 3) != ':' || !d(p + 4) || !d(p + 5)) return false;
+    p += 6;
+    if (p < n && rd.at(s + p) == ':') {
+      if (p + 3 > n || !d(p + 1) || !d(p + 2)) return false;
+      p += 3;
+    }
+  }
+  if (p < n) {
+    uint32_t c = rd.at(s + p);
+    if (c == 'Z') p += 1;
+    else if (c == '+' || c == '-') {
+      if (p + 5 > n || !d(p + 1) || !d(p + 2) || !d(p + 3) || !d(p + 4)) return false;
+      p += 5;
+    }
+  }
+  return p == n;
 }
-__device__ __forceinline__ bool uuid_char_ok(uint32_t k, uint32_t c) {
-  return (k == 8 || k == 13 || k == 18 || k == 23) ? c == '-' : is_hex(c);
+// one 8-4-4-4-12 hex UUID at s
+template <class R>
+__device__ bool uuid_at(R& rd, uint32_t s) {
+  for (uint32_t k = 0; k < 36; k++) {
+    uint32_t c = rd.at(s + k);
+    bool ok = (k == 8 || k == 13 || k == 18 || k == 23) ? c == '-' : is_hex(c);
+    if (!ok) return false;
+  }
+  return true;
+}
+// `^[a-zA-Z0-9._%+-]+@[a-zA-Z0-9.-]+\.[a-zA-Z]{2,}$` given exactly one '@':
+// local part >= 1 byte, domain all [A-Za-z0-9.-] with its last '.' at index
+// >= 1 followed by >= 2 ASCII letters.
+template <class R>
+__device__ bool email_match(R& rd, uint32_t s, uint32_t e) {
+  uint32_t q = s;
+  while (q < e && rd.at(q) != '@') {
+    if (!is_email_local(rd.at(q))) return false;
+    q++;
+  }
+  if (q == s || q >= e) return false;
+  const uint32_t d0 = q + 1;
+  int32_t lastdot = -1;
+  for (uint32_t k = d0; k < e; k++) {
+    uint32_t c = rd.at(k);
+    if (!is_email_domain(c)) return false;
+    if (c == '.') lastdot = (int32_t)(k - d0);
+  }
+  if (lastdot < 1) return false;
+  const uint32_t t0 = d0 + (uint32_t)lastdot + 1;
+  if (e - t0 < 2) return false;
+  for (uint32_t k = t0; k < e; k++)
+    if (!is_alpha(rd.at(k))) return false;
+  return true;
+}
+// replacementChar (templatize.go:73): Go decodes invalid UTF-8 as U+FFFD
+// (width 1), so the regexp matches EF BF BD or any undecodable byte.
+template <class R>
+__device__ bool has_fffd(R& rd, uint32_t s, uint32_t e) {
+  uint32_t q = s;
+  while (q < e) {
+    uint32_t c = rd.at(q);
+    if (c < 0x80) { q++; continue; }
+    uint32_t need, lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) { need = 2; lo = 0xA0; }
+    else if (c >= 0xE1 && c <= 0xEC) need = 2;
+    else if (c == 0xED) { need = 2; hi = 0x9F; }
+    else if (c >= 0xEE && c <= 0xEF) need = 2;
+    else if (c == 0xF0) { need = 3; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) { need = 3; hi = 0x8F; }
+    else return true;
+    if (q + need >= e) return true;
+    for (uint32_t k = 1; k <= need; k++) {
+      uint32_t b = rd.at(q + k);
+      if (b < (k == 1 ? lo : 0x80u) || b > (k == 1 ? hi : 0xBFu)) return true;
+    }
+    if (need == 2 && c == 0xEF && rd.at(q + 1) == 0xBF && rd.at(q + 2) == 0xBD) return true;
+    q += need + 1;
+  }
+  return false;
 }
 
 struct Cfg {
   const uint8_t* blob;
   const UrlCfgDev* h;
+  lds_u8* names;          // first kNamesLds bytes of the bytes section, staged in LDS
+  uint32_t names_len;
   __device__ const NameDev& name(uint32_t id) const {
     return reinterpret_cast<const NameDev*>(blob + h->names_off)[id];
   }
@@ -98,96 +172,73 @@ struct Cfg {
   }
 };
 
-// getSegmentTemplatizationString (templatize.go:242-269) on bytes [s, e):
-// returns the name id, or -1 when the segment stays as is.
-__device__ int classify_segment(const Cfg& cfg, ByteReader& rd, uint32_t s, uint32_t e) {
-  const uint32_t n = e - s;
-  // custom ids first, in config order
-  for (uint32_t k = 0; k < cfg.h->n_custom; k++) {
+// getSegmentTemplatizationString (templatize.go:242-269) for the segment
+// starting at s (it ends at the next '/' or n; the end is returned in *e_out):
+// the name id, or -1 when the segment stays as is.  One pass over 4-byte
+// words computes every cheap predicate branch-free:
+//   noLetters   every byte in [!-~] and not a letter
+//   hex         every byte [0-9A-Fa-f] (length >= 16 and even checked after)
+//   \d{7,}      longest digit run, carried across words
+//   '@' count and "any byte >= 0x80" gate the email and U+FFFD passes.
+template <class R>
+__device__ __forceinline__ int classify_segment(const Cfg& cfg, R& rd, uint32_t s, uint32_t n, uint32_t* e_out) {
+  uint32_t bad_nl = 0, bad_hex = 0, any_hi = 0, ats = 0, run = 0, longnum = 0;
+  auto st = rd.stream(s);
+  uint32_t q = s;
+  for (;;) {
+    const uint32_t x = st.next();
+    const uint32_t hi = x & kH, asc = hi ^ kH;
+    const uint32_t t = swar_t(x), tl = t | 0x20202020u;
+    const uint32_t digit = swar_ge(t, '0') & ~swar_ge(t, '9' + 1) & asc;
+    const uint32_t ga = swar_ge(tl, 'a');
+    const uint32_t alpha = ga & ~swar_ge(tl, 'z' + 1) & asc;
+    const uint32_t hexl = ga & ~swar_ge(tl, 'f' + 1) & asc;
+    const uint32_t print = swar_ge(t, '!') & ~swar_ge(t, 127) & asc;
+    const uint32_t at = swar_ge(t, '@') & ~swar_ge(t, 'A') & asc;
+    const uint32_t slash = swar_ge(t, '/') & ~swar_ge(t, '0') & asc;
+    const uint32_t stop = slash | swar_end(n - q);
+    const uint32_t v = swar_before(stop);
+    bad_nl |= ~(print & ~alpha) & v;
+    bad_hex |= ~(digit | hexl) & v;
+    any_hi |= hi & v;
+    ats += __builtin_popcount(at & v);
+    const uint32_t nd = ~(digit & v) & kH;   // non-digit (or past the end) bytes
+    const uint32_t lead = swar_first(nd);
+    longnum |= (run + lead >= 7) ? 1u : 0u;
+    if (stop) {
+      q += swar_first(stop);
+      break;
+    }
+    const uint32_t trail = nd ? (uint32_t)__clz(nd) >> 3 : 4u;
+    run = lead == 4 ? run + 4 : trail;
+    q += 4;
+  }
+  *e_out = q;
+  const uint32_t e = q, len = e - s;
+  for (uint32_t k = 0; k < cfg.h->n_custom; k++) {   // custom ids first, in config order
     const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
     if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, e)) return (int)cu.name;
   }
-  bool all_nl = n > 0, all_hex = true, longnum = false, fffd = false, uuid_pre = n >= 36;
-  uint32_t run = 0;
-  uint32_t utf_need = 0, utf_lo = 0x80, utf_hi = 0xBF, utf_seq = 0;   // utf_seq: EF BF BD tracker
-  uint32_t em = 0, local_len = 0, dom_len = 0, tail_n = 0;            // em: 0 local, 1 domain, 2 dead
-  int32_t lastdot = -1;
-  bool tail_ok = true;
-  uint32_t ds = 0;
-  for (uint32_t k = 0; k < n; k++) {
-    uint32_t c = rd.at(s + k);
-    all_nl &= is_noletter(c);
-    all_hex &= is_hex(c);
-    run = is_digit(c) ? run + 1 : 0;
-    longnum |= run >= 7;
-    if (k < 36) uuid_pre &= uuid_char_ok(k, c);
-    ds = date_step(ds, c);
-    // utf8 walk (replacementChar, templatize.go:73): sticky once found
-    if (!fffd) {
-      if (utf_need == 0) {
-        if (c >= 0x80) {
-          utf_lo = 0x80; utf_hi = 0xBF; utf_seq = c == 0xEF ? 1 : 0;
-          if (c >= 0xC2 && c <= 0xDF) utf_need = 1;
-          else if (c == 0xE0) { utf_need = 2; utf_lo = 0xA0; }
-          else if (c >= 0xE1 && c <= 0xEC) utf_need = 2;
-          else if (c == 0xED) { utf_need = 2; utf_hi = 0x9F; }
-          else if (c >= 0xEE && c <= 0xEF) utf_need = 2;
-          else if (c == 0xF0) { utf_need = 3; utf_lo = 0x90; }
-          else if (c >= 0xF1 && c <= 0xF3) utf_need = 3;
-          else if (c == 0xF4) { utf_need = 3; utf_hi = 0x8F; }
-          else fffd = true;
-        }
-      } else {
-        if (c < utf_lo || c > utf_hi) {
-          fffd = true;
-        } else {
-          utf_seq = (utf_seq == 1 && c == 0xBF) ? 2 : (utf_seq == 2 && c == 0xBD ? 3 : 0);
-          if (utf_seq == 3) fffd = true;
-          utf_lo = 0x80; utf_hi = 0xBF;
-          utf_need--;
-        }
-      }
-    }
-    // email (templatize.go:70)
-    if (em == 0) {
-      if (c == '@') em = local_len > 0 ? 1 : 2;
-      else if (is_email_local(c)) local_len++;
-      else em = 2;
-    } else if (em == 1) {
-      if (!is_email_domain(c)) em = 2;
-      else {
-        if (c == '.') { lastdot = (int32_t)dom_len; tail_n = 0; tail_ok = true; }
-        else if (is_alpha(c)) tail_n++;
-        else tail_ok = false;
-        dom_len++;
-      }
-    }
-  }
-  if (utf_need) fffd = true;   // truncated sequence at the end
-  if (date_accept(ds)) return kNameDate;
-  if (em == 1 && lastdot >= 1 && tail_ok && tail_n >= 2) return kNameEmail;
-  bool uuid = uuid_pre;
-  if (!uuid && n >= 36) {
-    uuid = true;
-    for (uint32_t k = 0; k < 36; k++) uuid &= uuid_char_ok(k, rd.at(e - 36 + k));
-  }
-  bool hex = all_hex && n >= 16 && (n & 1) == 0;
-  if (all_nl || longnum || uuid || hex || fffd) return kNameId;
+  if (date_len(len) && date_match(rd, s, len)) return kNameDate;
+  if (ats == 1 && !any_hi && email_match(rd, s, e)) return kNameEmail;
+  if ((bad_nl == 0 && len > 0) || longnum || (bad_hex == 0 && len >= 16 && (len & 1) == 0)) return kNameId;
+  if (len >= 36 && (uuid_at(rd, s) || uuid_at(rd, e - 36))) return kNameId;
+  if (any_hi && has_fffd(rd, s, e)) return kNameId;
   return -1;
 }
 
-// attemptTemplateWithRule (templatize.go:192-237): returns the output body
-// length (without the leading '/') or -1.
-__device__ int64_t attempt_rule(const Cfg& cfg, const UrlRuleDev& r, ByteReader& rd, uint32_t b0, uint32_t n) {
+// attemptTemplateWithRule (templatize.go:192-237): output body length
+// (without the leading '/') or -1.
+template <class R>
+__device__ int64_t attempt_rule(const Cfg& cfg, const UrlRuleDev& r, R& rd, uint32_t b0, uint32_t n) {
   const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h->segs_off) + r.seg_first;
   const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
   uint32_t s = b0;
   int64_t len = 0;
   for (uint32_t k = 0; k < r.nseg; k++) {
-    uint32_t e = s;
-    while (e < n && rd.at(e) != '/') e++;
+    const uint32_t e = scan_to(rd, s, n, '/');
     const UrlRuleSegDev& sg = segs[k];
-    uint32_t sl = e - s;
+    const uint32_t sl = e - s;
     if (sg.kind == kRuleStatic && sg.text_len != 0) {
       if (sg.text_len != sl) return -1;
       for (uint32_t q = 0; q < sl; q++)
@@ -203,253 +254,590 @@ __device__ int64_t attempt_rule(const Cfg& cfg, const UrlRuleDev& r, ByteReader&
   return len;
 }
 
-template <typename Put>
-__device__ void emit_rule(const Cfg& cfg, const UrlRuleDev& r, ByteReader& rd, uint32_t b0, uint32_t n, Put& put) {
+// path end after the http.target '?' cut (strings.SplitN(target, "?", 2)[0])
+template <class R>
+__device__ __forceinline__ uint32_t path_end(R& rd, uint32_t len, uint32_t f) {
+  return (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? scan_to(rd, 0, len, '?') : len;
+}
+
+// Output writers.  word(x, nv) appends the low nv (<= 4) bytes of x; while
+// at least 4 bytes of the span's own output remain it stores all 4 (the
+// extra bytes are overwritten by this lane later), so the common case has no
+// per-byte branches.
+template <class P>
+struct Put {
+  P dst;
+  uint32_t w, cap;
+  __device__ __forceinline__ void byte(uint32_t c) { dst[w++] = (uint8_t)c; }
+  __device__ __forceinline__ void word(uint32_t x, uint32_t nv) {
+    if (w + 4 <= cap) {
+      dst[w] = (uint8_t)x;
+      dst[w + 1] = (uint8_t)(x >> 8);
+      dst[w + 2] = (uint8_t)(x >> 16);
+      dst[w + 3] = (uint8_t)(x >> 24);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        if (k < nv) dst[w + k] = (uint8_t)(x >> (8 * k));
+    }
+    w += nv;
+  }
+};
+typedef __attribute__((address_space(3))) uint8_t lds_out_u8;
+
+// copies [q, n)
+template <class R, class W>
+__device__ __forceinline__ void copy_range(R& rd, uint32_t q, uint32_t n, W& put) {
+  auto st = rd.stream(q);
+  for (; q < n; q += 4) put.word(st.next(), min(4u, n - q));
+}
+// copies the segment starting at q (up to '/' or n); returns its end
+template <class R, class W>
+__device__ __forceinline__ uint32_t copy_segment(R& rd, uint32_t q, uint32_t n, W& put) {
+  auto st = rd.stream(q);
+  for (;;) {
+    const uint32_t x = st.next();
+    const uint32_t stop = swar_eq(x, '/') | swar_end(n - q);
+    const uint32_t nv = swar_first(stop);
+    put.word(x, nv);
+    q += nv;
+    if (stop) return q;
+  }
+}
+template <class W>
+__device__ __forceinline__ void put_name(const Cfg& cfg, uint32_t id, W& put) {
+  const NameDev nm = cfg.name(id);
+  put.byte('{');
+  if (nm.off + nm.len <= cfg.names_len) {
+    for (uint32_t q = 0; q < nm.len; q++) put.byte(cfg.names[nm.off + q]);
+  } else {
+    const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
+    for (uint32_t q = 0; q < nm.len; q++) put.byte(bytes[nm.off + q]);
+  }
+  put.byte('}');
+}
+
+template <class R, class W>
+__device__ void emit_rule(const Cfg& cfg, const UrlRuleDev& r, R& rd, uint32_t b0, uint32_t n, W& put) {
   const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h->segs_off) + r.seg_first;
   const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
   uint32_t s = b0;
   for (uint32_t k = 0; k < r.nseg; k++) {
-    uint32_t e = s;
-    while (e < n && rd.at(e) != '/') e++;
+    const uint32_t e = scan_to(rd, s, n, '/');
     const UrlRuleSegDev& sg = segs[k];
-    if (k) put('/');
+    if (k) put.byte('/');
     if (sg.kind == kRuleTemplate) {
-      put('{');
-      for (uint32_t q = 0; q < sg.text_len; q++) put(bytes[sg.text_off + q]);
-      put('}');
+      put.byte('{');
+      for (uint32_t q = 0; q < sg.text_len; q++) put.byte(bytes[sg.text_off + q]);
+      put.byte('}');
     } else if (sg.kind == kRuleWildcard || sg.kind == kRuleRegex) {
-      for (uint32_t q = s; q < e; q++) put(rd.at(q));
+      copy_range(rd, s, e, put);
     } else {
-      for (uint32_t q = 0; q < sg.text_len; q++) put(bytes[sg.text_off + q]);
+      for (uint32_t q = 0; q < sg.text_len; q++) put.byte(bytes[sg.text_off + q]);
     }
     s = e + 1;
   }
 }
 
-struct SpanPlan {
-  uint32_t mode = M_NONE;
-  uint32_t len = 0;        // output bytes
-  uint32_t b0 = 0, n = 0;  // body start, path end (after '?' cut)
-  uint32_t lead = 0;
-  int32_t rule = -1;
-  uint64_t code_lo = 0, code_hi = 0;   // 4-bit (name id + 1) per segment, first 32 segments
-  bool slow = false;                   // more segments / names than the codes hold
+// The plan of one span (phase 1 -> phase 2).  `n` (path end after the '?'
+// cut) is carried in the meta word when it fits, sparing phase 2 the scan.
+constexpr uint32_t kNField = (1u << 25) - 1;   // "recompute n"
+struct Plan {
+  uint32_t mode = M_NONE, len = 0, lead = 0, field = 0;   // field: rule index (M_RULE) or n
+  uint64_t code = 0;
+  bool slow = false;
 };
 
-__global__ __launch_bounds__(256) void url_template_kernel(UrlKernelArgs a) {
-  __shared__ uint32_t s_tile;
-  __shared__ uint64_t s_prefix;
-  __shared__ uint32_t s_wsum[kTile / kWave];
-  __shared__ uint32_t s_direct;
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[kOutLds];
-
-  const int tid = threadIdx.x;
-  if (tid == 0) s_tile = atomicAdd(a.tile_counter, 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
-  const uint64_t i = (uint64_t)tile * kTile + tid;
-  const bool valid = i < a.n_spans;
-
-  Cfg cfg{a.cfg, reinterpret_cast<const UrlCfgDev*>(a.cfg)};
-  SpanPlan pl;
-  uint8_t oflags = 0;
-  ose_strref path{0, 0};
-  if (valid) {
-    uint32_t f = a.url_flags[i];
-    uint32_t kind = a.kind[i];
-    bool ok = a.res_url_ok == nullptr || a.res_url_ok[a.resource[i]];
-    if (ok && (f & OSE_URL_HAS_METHOD) && (kind == OSE_KIND_SERVER || kind == OSE_KIND_CLIENT)) {
-      uint32_t tgt = f & OSE_URL_TGT_MASK;
-      uint32_t src = f & OSE_URL_PATH_MASK;
-      if (tgt != OSE_URL_TGT_ABSENT) {
-        if (tgt == OSE_URL_TGT_STR_EMPTY && (f & OSE_URL_NAME_EQ_METHOD)) {
-          pl.mode = M_RENAME_SLASH;
-          pl.len = 1;
-          oflags = OSE_OUT_RENAME;
-        }
-      } else if (src != OSE_URL_PATH_NONE) {
-        path = a.path[i];
-        oflags = OSE_OUT_SET_ATTR;
+// phase 1 for one span whose path is available through rd (url_flags f)
+template <class R>
+__device__ __forceinline__ Plan plan_path(const Cfg& cfg, R& rd, uint32_t plen, uint32_t f) {
+  Plan p;
+  const uint32_t n = path_end(rd, plen, f);
+  p.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
+  if (n == p.lead) {   // "" or "/" -> "/" (processor.go:156-160)
+    p.mode = M_SLASH;
+    p.len = 1;
+    return p;
+  }
+  if (cfg.h->n_rules) {
+    const uint32_t nseg = 1 + count_byte(rd, p.lead, n, '/');
+    if (nseg <= cfg.h->max_rule_nseg) {
+      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
+      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
+      for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
+        int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
+        if (l >= 0) { p.mode = M_RULE; p.field = r; p.len = p.lead + (uint32_t)l; return p; }
       }
     }
   }
-  ByteReader rd(a.arena + path.off);
-  if (oflags == OSE_OUT_SET_ATTR) {
-    uint32_t f = a.url_flags[i];
-    uint32_t n = path.len;
-    if ((f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET) {
-      for (uint32_t k = 0; k < n; k++)
-        if (rd.at(k) == '?') { n = k; break; }
-    }
-    pl.n = n;
-    pl.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
-    pl.b0 = pl.lead;
-    if (n == pl.b0) {
-      pl.mode = M_SLASH;
-      pl.len = 1;
+  uint32_t s = p.lead, seg = 0, l = p.lead;
+  bool templated = false;
+  for (;;) {
+    uint32_t e;
+    const int id = classify_segment(cfg, rd, s, n, &e);
+    if (seg) l += 1;
+    if (id >= 0) {
+      templated = true;
+      l += cfg.name((uint32_t)id).len + 2;
+      if (seg < 16 && id < 15) p.code |= (uint64_t)(id + 1) << (seg * 4);
+      else p.slow = true;
     } else {
-      if (cfg.h->n_rules) {
-        uint32_t nseg = 1;
-        for (uint32_t k = pl.b0; k < n; k++) nseg += rd.at(k) == '/';
-        if (nseg <= cfg.h->max_rule_nseg) {
-          const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
-          const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
-          for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
-            int64_t l = attempt_rule(cfg, rules[r], rd, pl.b0, n);
-            if (l >= 0) {
-              pl.mode = M_RULE;
-              pl.rule = (int32_t)r;
-              pl.len = pl.lead + (uint32_t)l;
-              break;
-            }
-          }
-        }
+      l += e - s;
+    }
+    seg++;
+    if (e >= n) break;
+    s = e + 1;
+  }
+  if (templated) { p.mode = M_DEFAULT; p.len = l; }
+  else { p.mode = M_ORIG; p.len = 1 + (n - p.lead); }   // "/" + body (processor.go:182-185)
+  p.field = n < kNField ? n : kNField;
+  return p;
+}
+
+// phase 2 for one span: writes the template through put
+template <class R, class W>
+__device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, uint32_t f, uint32_t mode,
+                                          uint32_t lead, bool slow, uint32_t field, uint64_t code, W& put) {
+  if (mode == M_RENAME_SLASH || mode == M_SLASH) { put.byte('/'); return; }
+  if (mode == M_RULE) {
+    const uint32_t n = path_end(rd, plen, f);
+    if (lead) put.byte('/');
+    const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
+    emit_rule(cfg, rules[field], rd, lead, n, put);
+    return;
+  }
+  const uint32_t n = field != kNField ? field : path_end(rd, plen, f);
+  if (mode == M_ORIG) {
+    put.byte('/');
+    copy_range(rd, lead, n, put);
+    return;
+  }
+  if (lead) put.byte('/');
+  uint32_t s = lead, seg = 0;
+  for (;;) {
+    if (seg) put.byte('/');
+    uint32_t e;
+    int id;
+    if (seg < 16 && !slow) {
+      id = (int)((code >> (seg * 4)) & 15u) - 1;
+      e = id >= 0 ? scan_to(rd, s, n, '/') : copy_segment(rd, s, n, put);
+    } else {
+      id = classify_segment(cfg, rd, s, n, &e);
+      if (id < 0) copy_range(rd, s, e, put);
+    }
+    if (id >= 0) put_name(cfg, (uint32_t)id, put);
+    seg++;
+    if (e >= n) break;
+    s = e + 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Class bitmaps of one wave's staged bytes.  Row r covers stage bytes
+// [32r, 32r+32) and holds one 32-bit mask per class (bit k = byte 32r+k), so
+// the 64-bit windows of all classes at any byte come from 3 rows (6 x
+// ds_read_b128).  Built cooperatively, 32 bytes per lane, branch-free.
+enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, kClasses };
+constexpr uint32_t kBmRows = kStage / 32 + 3;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u4;
+typedef const __attribute__((address_space(3))) u32x4 lds_cu4;
+
+// SWAR high-bit mask (bits 7,15,23,31) -> 4-bit mask
+__device__ __forceinline__ uint32_t movemask4(uint32_t m) { return (((m >> 7) * 0x204081u) >> 21) & 0xFu; }
+
+__device__ __forceinline__ void build_bitmaps(lds_u32* stage32, lds_u4* bm, uint32_t bytes) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t rows = (bytes + 31) / 32;
+  for (uint32_t r = lane; r < rows; r += kWave) {
+    uint32_t acc[kClasses];
+#pragma unroll
+    for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
+    const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
+    const u32x4 v0 = src[0], v1 = src[1];
+    const uint32_t xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+      const uint32_t x = xs[d];
+      const uint32_t hi = x & kH, asc = hi ^ kH;
+      const uint32_t t = swar_t(x), tl = t | 0x20202020u;
+      const uint32_t g0 = swar_ge(t, '0');
+      const uint32_t digit = g0 & ~swar_ge(t, '9' + 1) & asc;
+      const uint32_t ga = swar_ge(tl, 'a');
+      const uint32_t alpha = ga & ~swar_ge(tl, 'z' + 1) & asc;
+      const uint32_t hexl = ga & ~swar_ge(tl, 'f' + 1) & asc;
+      const uint32_t print = swar_ge(t, '!') & ~swar_ge(t, 127) & asc;
+      const uint32_t gat = swar_ge(t, '@');
+      const uint32_t m[kClasses] = {
+          swar_ge(t, '/') & ~g0 & asc,                     // C_SL
+          ~(print & ~alpha) & kH,                          // C_BNL: outside noLetters' class
+          ~(digit | hexl) & kH,                            // C_BHX
+          digit,                                           // C_DG
+          gat & ~swar_ge(t, 'A') & asc,                    // C_AT
+          hi,                                              // C_HI
+          swar_ge(t, '-') & ~swar_ge(t, '.') & asc,        // C_DASH
+          swar_ge(t, '?') & ~gat & asc,                    // C_QM
+      };
+#pragma unroll
+      for (int c = 0; c < (int)kClasses; c++) acc[c] |= movemask4(m[c]) << (4 * d);
+    }
+    bm[2 * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
+    bm[2 * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
+  }
+}
+
+// 64-bit windows of every class starting at stage byte a
+struct Win {
+  uint64_t c[kClasses];
+};
+__device__ __forceinline__ Win load_win(lds_cu4* bm, uint32_t a) {
+  const uint32_t r = a >> 5, sh = a & 31;
+  const u32x4 a0 = bm[2 * r], a1 = bm[2 * r + 1], b0 = bm[2 * r + 2], b1 = bm[2 * r + 3], c0 = bm[2 * r + 4],
+              c1 = bm[2 * r + 5];
+  const uint32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const uint32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  const uint32_t w2[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  Win w;
+#pragma unroll
+  for (int c = 0; c < (int)kClasses; c++)
+    w.c[c] = ((uint64_t)__builtin_amdgcn_alignbit(w2[c], w1[c], sh) << 32) | __builtin_amdgcn_alignbit(w1[c], w0[c], sh);
+  return w;
+}
+__device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
+
+// first byte of class c in [a, e) (stage coordinates), or e
+__device__ __forceinline__ uint32_t first_of(lds_cu4* bm, uint32_t c, uint32_t a, uint32_t e) {
+  const lds_u32* b32 = (const lds_u32*)bm;
+  while (a < e) {
+    const uint32_t r = a >> 5, sh = a & 31;
+    const uint32_t m = __builtin_amdgcn_alignbit(b32[8 * (r + 1) + c], b32[8 * r + c], sh) & (uint32_t)low_mask(e - a);
+    if (m) return a + __builtin_ctz(m);
+    a += 32;
+  }
+  return e;
+}
+
+// getSegmentTemplatizationString (templatize.go:242-269) from the class
+// windows of a segment of length L <= 64 starting at s (reader coordinates).
+constexpr uint64_t kUuidDash = (1ull << 8) | (1ull << 13) | (1ull << 18) | (1ull << 23);
+constexpr uint64_t kUuidHex = ((1ull << 36) - 1) & ~kUuidDash;
+template <class R>
+__device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w, uint32_t s, uint32_t L) {
+  const uint64_t M = low_mask(L);
+  for (uint32_t k = 0; k < cfg.h->n_custom; k++) {   // custom ids first, in config order
+    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
+    if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, s + L)) return (int)cu.name;
+  }
+  if (date_len(L) && (w.c[C_DG] & 0xF) == 0xF && date_match(rd, s, L)) return kNameDate;
+  const bool any_hi = (w.c[C_HI] & M) != 0;
+  if (!any_hi && __popcll(w.c[C_AT] & M) == 1 && email_match(rd, s, s + L)) return kNameEmail;
+  const uint64_t d = w.c[C_DG] & M, d1 = d & (d >> 1), d2 = d1 & (d1 >> 2), d7 = d2 & (d2 >> 3);
+  if ((L > 0 && (w.c[C_BNL] & M) == 0) || d7 || ((w.c[C_BHX] & M) == 0 && L >= 16 && (L & 1) == 0)) return kNameId;
+  if (L >= 36) {
+    const uint64_t hx = ~w.c[C_BHX], ds = w.c[C_DASH], sh = L - 36;
+    if (((hx & kUuidHex) == kUuidHex && (ds & kUuidDash) == kUuidDash) ||
+        (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
+      return kNameId;
+  }
+  if (any_hi && has_fffd(rd, s, s + L)) return kNameId;
+  return -1;
+}
+
+// phase 1 from the class bitmaps: same result as plan_path, with segment
+// ends and the cheap predicates read from the windows.  p0 = stage offset of
+// the path (rd reads relative to it).
+__device__ __forceinline__ Plan plan_bits(const Cfg& cfg, LdsReader& rd, lds_cu4* bm, uint32_t p0, uint32_t plen,
+                                          uint32_t f) {
+  Plan p;
+  const uint32_t n =
+      (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? first_of(bm, C_QM, p0, p0 + plen) - p0 : plen;
+  p.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
+  if (n == p.lead) {   // "" or "/" -> "/" (processor.go:156-160)
+    p.mode = M_SLASH;
+    p.len = 1;
+    return p;
+  }
+  if (cfg.h->n_rules) {
+    const uint32_t nseg = 1 + count_byte(rd, p.lead, n, '/');
+    if (nseg <= cfg.h->max_rule_nseg) {
+      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
+      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
+      for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
+        int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
+        if (l >= 0) { p.mode = M_RULE; p.field = r; p.len = p.lead + (uint32_t)l; return p; }
       }
-      if (pl.mode == M_NONE) {
-        uint32_t s = pl.b0, seg = 0, len = pl.lead;
-        bool templated = false;
-        for (;;) {
-          uint32_t e = s;
-          while (e < n && rd.at(e) != '/') e++;
-          int id = classify_segment(cfg, rd, s, e);
-          if (seg) len += 1;
-          if (id >= 0) {
-            templated = true;
-            len += cfg.name((uint32_t)id).len + 2;
-            if (seg < 32 && id < 15) {
-              uint64_t code = (uint64_t)(id + 1) << ((seg & 15) * 4);
-              if (seg < 16) pl.code_lo |= code; else pl.code_hi |= code;
-            } else {
-              pl.slow = true;
-            }
-          } else {
-            len += e - s;
+    }
+  }
+  uint32_t s = p.lead, seg = 0, l = p.lead;
+  bool templated = false;
+  for (;;) {
+    const uint32_t rem = n - s;
+    const Win w = load_win(bm, p0 + s);
+    const uint64_t slm = w.c[C_SL] & low_mask(rem);
+    uint32_t e;
+    int id;
+    if (slm || rem <= 64) {
+      const uint32_t L = slm ? (uint32_t)__builtin_ctzll(slm) : rem;
+      e = s + L;
+      id = classify_win(cfg, rd, w, s, L);
+    } else {
+      id = classify_segment(cfg, rd, s, n, &e);   // segment longer than 64 bytes
+    }
+    if (seg) l += 1;
+    if (id >= 0) {
+      templated = true;
+      l += cfg.name((uint32_t)id).len + 2;
+      if (seg < 16 && id < 15) p.code |= (uint64_t)(id + 1) << (seg * 4);
+      else p.slow = true;
+    } else {
+      l += e - s;
+    }
+    seg++;
+    if (e >= n) break;
+    s = e + 1;
+  }
+  if (templated) { p.mode = M_DEFAULT; p.len = l; }
+  else { p.mode = M_ORIG; p.len = 1 + (n - p.lead); }
+  p.field = n < kNField ? n : kNField;
+  return p;
+}
+
+// Rare paths kept out of line so the hot LDS->LDS instantiation stays small:
+// a group whose bytes do not fit the stage reads HBM, a tile whose output
+// does not fit the LDS image writes HBM.
+__device__ __noinline__ Plan plan_global(const Cfg& cfg, const uint8_t* p, uint32_t plen, uint32_t f) {
+  ByteReader rd(p);
+  return plan_path(cfg, rd, plen, f);
+}
+template <class R, class P>
+__device__ __noinline__ void emit_out_of_line(const Cfg& cfg, R rd, uint32_t plen, uint32_t f, uint32_t mode,
+                                              uint32_t lead, bool slow, uint32_t field, uint64_t code, P dst,
+                                              uint32_t cap) {
+  Put<P> put{dst, 0, cap};
+  emit_path(cfg, rd, plen, f, mode, lead, slow, field, code, put);
+}
+
+// plan meta word: mode 3 | lead 1 | slow 1 | url_out 2 | field 25
+__device__ __forceinline__ uint32_t pack_meta(uint32_t mode, uint32_t lead, bool slow, uint32_t oflags, uint32_t field) {
+  return mode | (lead << 3) | ((uint32_t)slow << 4) | (oflags << 5) | (field << 7);
+}
+
+constexpr uint32_t kNamesLds = 512;
+struct Smem {
+  uint32_t len[kTile];
+  uint32_t meta[kTile];
+  uint64_t code[kTile];
+  uint32_t wsum[kWaves];
+  uint32_t tile;
+  uint32_t pad;
+  uint64_t prefix;
+  __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
+  union {
+    __attribute__((aligned(16))) uint8_t out[kOutLds];      // phase 2: the tile's output image
+    __attribute__((aligned(16))) u32x4 bm[kWaves][2 * kBmRows];   // phase 1: per-wave class bitmaps
+  };
+  uint8_t names[kNamesLds];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Copies the arena bytes [lo, hi) the wave's 64 lanes reference (16-byte
+// aligned down) into the wave's LDS slice.  Returns the aligned start, or
+// ~0u when the range does not fit (lanes then read HBM directly).
+__device__ uint32_t stage_wave(uint8_t* stage, const uint8_t* arena, uint32_t lo, uint32_t hi, uint32_t* nbytes) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, (uint32_t)__shfl_xor(lo, o, kWave));
+    hi = max(hi, (uint32_t)__shfl_xor(hi, o, kWave));
+  }
+  *nbytes = 0;
+  if (lo >= hi) return 0;   // no lane reads bytes
+  const uint32_t lo16 = lo & ~15u;
+  const uint32_t bytes = (hi - lo16 + 15u) & ~15u;
+  if (bytes > kStage) return ~0u;
+  *nbytes = bytes;
+  const uint4* src = reinterpret_cast<const uint4*>(arena + lo16);
+  uint4* dst = reinterpret_cast<uint4*>(stage);
+  for (uint32_t x = lane; x < bytes / 16; x += kWave) dst[x] = src[x];
+  wave_lds_sync();
+  return lo16;
+}
+
+__global__ __launch_bounds__(kThreads) void url_template_kernel(UrlKernelArgs a) {
+  __shared__ Smem sm;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) sm.tile = atomicAdd(a.tile_counter, 1u);
+  const UrlCfgDev* h = reinterpret_cast<const UrlCfgDev*>(a.cfg);
+  const uint32_t names_len = min(kNamesLds, h->total_bytes - h->bytes_off);
+  for (uint32_t k = tid; k < names_len; k += kThreads) sm.names[k] = a.cfg[h->bytes_off + k];
+  const Cfg cfg{a.cfg, h, (lds_u8*)sm.names, names_len};
+  uint8_t* stage = sm.stage[wv];
+  lds_u32* stage32 = (lds_u32*)stage;
+
+  __syncthreads();
+  const uint32_t tile = sm.tile;
+  const uint64_t base = (uint64_t)tile * kTile;
+
+  // ---------------- phase 1: plan (waves independent) ----------------
+  uint64_t flags_k = 0;   // 16 bits per group: url_flags | 0x100 when the path is read
+#pragma unroll 1
+  for (int g = 0; g < kGroups; g++) {
+    const int j = g * kThreads + wv * kWave + lane;   // 64 consecutive spans per wave and group
+    const uint64_t i = base + j;
+    Plan p;
+    uint32_t oflags = 0, f = 0;
+    ose_strref pr{0, 0};
+    bool needs_path = false;
+    if (i < a.n_spans) {
+      f = a.url_flags[i];
+      const uint32_t kind = a.kind[i];
+      const bool ok = a.res_url_ok == nullptr || a.res_url_ok[a.resource[i]];
+      if (ok && (f & OSE_URL_HAS_METHOD) && (kind == OSE_KIND_SERVER || kind == OSE_KIND_CLIENT)) {
+        const uint32_t tgt = f & OSE_URL_TGT_MASK, src = f & OSE_URL_PATH_MASK;
+        if (tgt != OSE_URL_TGT_ABSENT) {
+          if (tgt == OSE_URL_TGT_STR_EMPTY && (f & OSE_URL_NAME_EQ_METHOD)) {
+            p.mode = M_RENAME_SLASH;   // processor.go:241-243
+            p.len = 1;
+            oflags = OSE_OUT_RENAME;
           }
-          seg++;
-          if (e >= n) break;
-          s = e + 1;
-        }
-        if (templated) {
-          pl.mode = M_DEFAULT;
-          pl.len = len;
-        } else {
-          pl.mode = M_ORIG;        // "/" + body (processor.go:182-185)
-          pl.len = 1 + (n - pl.b0);
+        } else if (src != OSE_URL_PATH_NONE) {
+          pr = a.path[i];
+          needs_path = true;
         }
       }
     }
-    if ((f & OSE_URL_NAME_EQ_METHOD) && pl.len > 0) oflags |= OSE_OUT_RENAME;
+    flags_k |= (uint64_t)(needs_path ? (f | 0x100u) : 0u) << (16 * g);
+    uint32_t bytes;
+    const uint32_t lo16 =
+        stage_wave(stage, a.arena, needs_path ? pr.off : ~0u, needs_path ? pr.off + pr.len : 0u, &bytes);
+    if (lo16 != ~0u && bytes) {
+      build_bitmaps(stage32, (lds_u4*)sm.bm[wv], bytes);
+      wave_lds_sync();
+    }
+    if (needs_path) {
+      if (lo16 != ~0u) {
+        LdsReader rd(stage32, pr.off - lo16);
+        p = plan_bits(cfg, rd, (lds_cu4*)sm.bm[wv], pr.off - lo16, pr.len, f);
+      } else {
+        p = plan_global(cfg, a.arena + pr.off, pr.len, f);
+      }
+      oflags = OSE_OUT_SET_ATTR;                                                   // processor.go:259
+      if ((f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;     // :216-225
+    }
+    sm.len[j] = p.len;
+    sm.meta[j] = pack_meta(p.mode, p.lead, p.slow, oflags, p.field);
+    sm.code[j] = p.code;
+    wave_lds_sync();   // the stage slice is reused by the next group
   }
+  __syncthreads();
 
-  // ---- block exclusive scan of output lengths ----
-  const int lane = tid & 63, wv = tid >> 6;
-  uint32_t incl = pl.len;
+  // ---------------- workgroup exclusive scan (thread t owns spans 4t..4t+3) ----------------
+  const uint32_t l0 = sm.len[4 * tid], l1 = sm.len[4 * tid + 1], l2 = sm.len[4 * tid + 2], l3 = sm.len[4 * tid + 3];
+  const uint32_t mine = l0 + l1 + l2 + l3;
+  uint32_t incl = mine;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
     uint32_t t = __shfl_up(incl, o, kWave);
     if (lane >= o) incl += t;
   }
-  if (lane == kWave - 1) s_wsum[wv] = incl;
+  if (lane == kWave - 1) sm.wsum[wv] = incl;
   __syncthreads();
   uint32_t wbase = 0, total = 0;
 #pragma unroll
-  for (int w = 0; w < kTile / kWave; w++) {
-    uint32_t v = s_wsum[w];
+  for (int w = 0; w < kWaves; w++) {
+    uint32_t v = sm.wsum[w];
     if (w < wv) wbase += v;
     total += v;
   }
-  const uint32_t local = wbase + incl - pl.len;
+  const uint32_t ex = wbase + incl - mine;
+  __syncthreads();
+  // sm.len now holds exclusive offsets within the tile
+  sm.len[4 * tid] = ex;
+  sm.len[4 * tid + 1] = ex + l0;
+  sm.len[4 * tid + 2] = ex + l0 + l1;
+  sm.len[4 * tid + 3] = ex + l0 + l1 + l2;
   const bool direct = total > kOutLds;
 
-  // wave 0 resolves the tile prefix while all waves stage the output in LDS
+  // ---------------- look-back (wave 0) ----------------
   if (wv == 0) {
-    uint64_t p = lookback_prefix(a.tile_status, tile, total, a.error);
+    uint64_t pfx = lookback_prefix(a.tile_status, tile, total, a.error);
     if (lane == 0) {
-      s_prefix = p;
-      s_direct = direct;
-      if (p + total > a.out_cap) atomicOr(a.error, 2u);
-      if (tile == a.n_tiles - 1 && a.used) *a.used = p + total;
+      sm.prefix = pfx;
+      if (pfx + total > a.out_cap) atomicOr(a.error, 2u);
+      if (tile == a.n_tiles - 1 && a.used) *a.used = pfx + total;
     }
   }
-
-  auto emit = [&](uint8_t* dst) {
-    uint32_t w = 0;
-    auto put = [&](uint32_t c) { dst[w++] = (uint8_t)c; };
-    if (pl.mode == M_RENAME_SLASH || pl.mode == M_SLASH) {
-      put('/');
-    } else if (pl.mode == M_ORIG) {
-      put('/');
-      for (uint32_t k = pl.b0; k < pl.n; k++) put(rd.at(k));
-    } else if (pl.mode == M_RULE) {
-      if (pl.lead) put('/');
-      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
-      emit_rule(cfg, rules[pl.rule], rd, pl.b0, pl.n, put);
-    } else if (pl.mode == M_DEFAULT) {
-      if (pl.lead) put('/');
-      const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
-      uint32_t s = pl.b0, seg = 0;
-      for (;;) {
-        uint32_t e = s;
-        while (e < pl.n && rd.at(e) != '/') e++;
-        int id;
-        if (seg < 32 && !pl.slow) {
-          uint64_t word = seg < 16 ? pl.code_lo : pl.code_hi;
-          id = (int)((word >> ((seg & 15) * 4)) & 15) - 1;
-        } else {
-          id = classify_segment(cfg, rd, s, e);
-        }
-        if (seg) put('/');
-        if (id >= 0) {
-          const NameDev& nm = cfg.name((uint32_t)id);
-          put('{');
-          for (uint32_t q = 0; q < nm.len; q++) put(bytes[nm.off + q]);
-          put('}');
-        } else {
-          for (uint32_t q = s; q < e; q++) put(rd.at(q));
-        }
-        seg++;
-        if (e >= pl.n) break;
-        s = e + 1;
-      }
-    }
-  };
-
-  if (!direct && pl.len) emit(s_out + local);
   __syncthreads();
-  const uint64_t prefix = s_prefix;
+  const uint64_t prefix = sm.prefix;
   const bool overflow = prefix + total > a.out_cap;
-  if (!overflow) {
-    if (direct) {
-      if (pl.len) emit(a.out_arena + prefix + local);
-    } else {
-      // coalesced copy of the tile image: 4-byte aligned body + byte edges
-      uint8_t* dst = a.out_arena + prefix;
-      uint32_t head = (uint32_t)((4 - ((uint64_t)dst & 3)) & 3);
-      if (head > total) head = total;
-      if ((uint32_t)tid < head) dst[tid] = s_out[tid];
-      uint32_t body = (total - head) / 4;
-      uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
-      for (uint32_t k = tid; k < body; k += kTile) {
-        uint32_t b = head + 4 * k;
-        d32[k] = (uint32_t)s_out[b] | ((uint32_t)s_out[b + 1] << 8) | ((uint32_t)s_out[b + 2] << 16) |
-                 ((uint32_t)s_out[b + 3] << 24);
-      }
-      uint32_t tail0 = head + 4 * body;
-      if ((uint32_t)tid < total - tail0) dst[tail0 + tid] = s_out[tail0 + tid];
+
+  // ---------------- phase 2: emit (waves independent) ----------------
+#pragma unroll 1
+  for (int g = 0; g < kGroups; g++) {
+    const int j = g * kThreads + wv * kWave + lane;
+    const uint64_t i = base + j;
+    const uint32_t local = sm.len[j];
+    const uint32_t len = (j + 1 < kTile ? sm.len[j + 1] : total) - local;
+    const uint32_t meta = sm.meta[j];
+    const uint32_t f = (uint32_t)(flags_k >> (16 * g)) & 0xFFFFu;
+    const bool needs_path = (f & 0x100u) != 0;
+    if (i < a.n_spans) {
+      a.url_out[i] = (uint8_t)((meta >> 5) & 3u);
+      a.tmpl[i] = ose_strref{(uint32_t)(prefix + local), len};
     }
+    const ose_strref pr = needs_path ? a.path[i] : ose_strref{0, 0};
+    uint32_t bytes;
+    const uint32_t lo16 =
+        stage_wave(stage, a.arena, needs_path ? pr.off : ~0u, needs_path ? pr.off + pr.len : 0u, &bytes);
+    if (len && !overflow) {
+      const uint32_t mode = meta & 7u, lead = (meta >> 3) & 1u, field = meta >> 7;
+      const bool slow = (meta >> 4) & 1u;
+      const uint64_t code = sm.code[j];
+      if (!direct && lo16 != ~0u) {
+        Put<lds_out_u8*> put{(lds_out_u8*)(sm.out + local), 0, len};
+        LdsReader rd(stage32, pr.off - lo16);
+        emit_path(cfg, rd, pr.len, f, mode, lead, slow, field, code, put);
+      } else if (!direct) {
+        emit_out_of_line(cfg, ByteReader(a.arena + pr.off), pr.len, f, mode, lead, slow, field, code,
+                         (lds_out_u8*)(sm.out + local), len);
+      } else if (lo16 != ~0u) {
+        emit_out_of_line(cfg, LdsReader(stage32, pr.off - lo16), pr.len, f, mode, lead, slow, field, code,
+                         a.out_arena + prefix + local, len);
+      } else {
+        emit_out_of_line(cfg, ByteReader(a.arena + pr.off), pr.len, f, mode, lead, slow, field, code,
+                         a.out_arena + prefix + local, len);
+      }
+    }
+    wave_lds_sync();
   }
-  if (valid) {
-    a.url_out[i] = oflags;
-    a.tmpl[i] = ose_strref{(uint32_t)(prefix + local), pl.len};
+  if (direct || overflow) return;
+  __syncthreads();
+  // coalesced copy of the tile image: byte head to 4-byte alignment, dword body, byte tail
+  uint8_t* dst = a.out_arena + prefix;
+  uint32_t head = (uint32_t)((4 - ((uint64_t)dst & 3)) & 3);
+  if (head > total) head = total;
+  if ((uint32_t)tid < head) dst[tid] = sm.out[tid];
+  const uint32_t body = (total - head) / 4;
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+  lds_u32* o32 = (lds_u32*)sm.out;
+  for (uint32_t k = tid; k < body; k += kThreads) {
+    const uint32_t b = head + 4 * k;
+    d32[k] = __builtin_amdgcn_alignbyte(o32[(b >> 2) + 1], o32[b >> 2], b & 3);
   }
+  const uint32_t tail0 = head + 4 * body;
+  if ((uint32_t)tid < total - tail0) dst[tail0 + tid] = sm.out[tail0 + tid];
 }
 
 }  // namespace
 
 void launch_url_template(const UrlKernelArgs& a, hipStream_t st) {
-  uint32_t tiles = a.n_tiles;
-  if (tiles == 0) return;
-  hipLaunchKernelGGL(url_template_kernel, dim3(tiles), dim3(kTile), 0, st, a);
+  if (a.n_tiles == 0) return;
+  hipLaunchKernelGGL(url_template_kernel, dim3(a.n_tiles), dim3(kThreads), 0, st, a);
 }
 
 }  // namespace ose

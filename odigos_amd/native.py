@@ -96,6 +96,14 @@ def lib() -> C.CDLL:
         return _lib
     if not LIB_PATH.exists():
         raise RuntimeError(f"{LIB_PATH} is missing: run `python -m odigos_amd.build` (hipcc, gfx950)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, loaded by file name from torch/lib).  Loading torch
+    # first makes this library bind to that same copy instead of a second
+    # /opt/rocm runtime, which would leave torch without devices.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(LIB_PATH))
     sig = {
         "ose_last_error": (C.c_char_p, []),

@@ -1,0 +1,46 @@
+"""Ablation timings of url_template_kernel on synthetic C2 batches (diagnostic)."""
+import sys, time
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import numpy as np
+import torch
+from odigos_amd import native
+from odigos_amd.batch import DeviceBatch, Engine, Generator
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+g = Generator("url", 0x0D160002, n, threads=16)
+g.cols.res_url_ok = None
+eng = Engine({"odigosurltemplate": {}})
+db = DeviceBatch(g.cols, fields=("arena", "kind", "url_flags", "path"))
+sh = torch.cuda.current_stream().cuda_stream
+
+def timeit(label, reps=5):
+    eng.process_device(db, native.STAGE_TEMPLATE, stream=sh)
+    torch.cuda.synchronize()
+    eng.profile(True)
+    for _ in range(reps):
+        eng.process_device(db, native.STAGE_TEMPLATE, stream=sh)
+    torch.cuda.synchronize()
+    eng.profile(False)
+    p = eng.profile_read()["url_template_kernel"]
+    print(f"{label:40s} {p['ms']/p['launches']:9.3f} ms/launch", flush=True)
+
+orig = db.t["url_flags"].clone()
+timeit("C2 baseline")
+db.t["url_flags"].zero_()
+timeit("no method (skeleton only)")
+db.t["url_flags"].copy_(orig)
+k = db.t["kind"]; korig = k.clone()
+k.fill_(1)
+timeit("all internal kind (skeleton only)")
+k.copy_(korig)
+# only RAW path spans, short path "/"
+p = db.t["path"].view(torch.int32).view(-1, 2)
+porig = p.clone()
+p[:, 1].clamp_(max=1)
+timeit("paths truncated to 1 byte")
+p.copy_(porig)
+p[:, 1].clamp_(max=8)
+timeit("paths truncated to 8 bytes")
+p.copy_(porig)
+timeit("C2 baseline again")
