@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <map>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -277,16 +279,21 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   if (c->res_url_ok && !c->resource) return fail(OSE_EINVAL, "res_url_ok needs the resource column");
   if (o->tmpl_arena_cap > 0xFFFFFFFFull) return fail(OSE_ERANGE, "tmpl_arena_cap exceeds the 32-bit offset range");
   uint64_t n = c->n_spans;
-  uint32_t tiles = (uint32_t)((n + kUrlTile - 1) / kUrlTile);
-  size_t off_status = 64;
-  size_t need = align_up(off_status + (size_t)tiles * 8, 256);
+  const uint32_t groups = (uint32_t)((n + kUrlGroup - 1) / kUrlGroup);
+  // workspace: [0,256) misc | plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | dbg
+  const size_t off_len = 256, off_meta = off_len + 4 * n, off_code = align_up(off_meta + 4 * n, 8);
+  const size_t off_gsum = off_code + 8 * n, off_gbase = off_gsum + 8 * (size_t)groups;
+  const uint32_t scan_tiles = (groups + kUrlScanTile - 1) / kUrlScanTile;
+  const size_t off_sst = off_gbase + 8 * (size_t)groups;
+  const size_t off_dbg = align_up(off_sst + 8 * (size_t)scan_tiles, 256);
+  const size_t need = off_dbg + 256;
+  if (need > url_workspace_bytes(n)) return fail(OSE_EINVAL, "internal: URL workspace layout exceeds its bound");
   int rc = ws->reserve(need);
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(ws->dev);
-  HIP_TRY(hipMemsetAsync(base, 0, off_status + (size_t)tiles * 8, st));
   UrlKernelArgs a{};
   a.n_spans = n;
-  a.n_tiles = tiles;
+  a.n_groups = groups;
   a.arena = c->arena;
   a.url_flags = c->url_flags;
   a.kind = c->kind;
@@ -298,19 +305,48 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.out_arena = o->tmpl_arena;
   a.out_cap = o->tmpl_arena_cap;
   a.cfg = e->url_blob_dev;
-  a.tile_counter = reinterpret_cast<uint32_t*>(base);
+  a.plan_len = reinterpret_cast<uint32_t*>(base + off_len);
+  a.plan_meta = reinterpret_cast<uint32_t*>(base + off_meta);
+  a.plan_code = reinterpret_cast<uint64_t*>(base + off_code);
+  a.group_sum = reinterpret_cast<uint64_t*>(base + off_gsum);
+  a.group_base = reinterpret_cast<uint64_t*>(base + off_gbase);
+  a.n_scan_tiles = scan_tiles;
+  a.scan_counter = reinterpret_cast<uint32_t*>(base);
+  a.scan_status = reinterpret_cast<uint64_t*>(base + off_sst);
   a.error = o->device_status ? o->device_status : reinterpret_cast<uint32_t*>(base + 8);
+  HIP_TRY(hipMemsetAsync(base, 0, 16, st));
+  HIP_TRY(hipMemsetAsync(a.scan_status, 0, 8 * (size_t)scan_tiles, st));
   a.used = o->tmpl_arena_used;
-  a.tile_status = reinterpret_cast<uint64_t*>(base + off_status);
+  if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
   if (n == 0) {
     if (o->tmpl_arena_used) HIP_TRY(hipMemsetAsync(o->tmpl_arena_used, 0, 8, st));
     return 0;
   }
+  if (a.ablate & 512) {   // diagnostics: per-section shader clocks (tools/url_clocks.py)
+    a.dbg = reinterpret_cast<uint64_t*>(base + off_dbg);
+    HIP_TRY(hipMemsetAsync(a.dbg, 0, 256, st));
+  }
   Engine::Timed tm{};
-  e->prof_begin("url_template_kernel", st, tm);
-  launch_url_template(a, st);
+  e->prof_begin("url_plan_kernel", st, tm);
+  launch_url_plan(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
+  e->prof_begin("url_scan_kernel", st, tm);
+  launch_url_scan(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  e->prof_begin("url_emit_kernel", st, tm);
+  launch_url_emit(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  if (a.ablate & 512) {
+    uint64_t h[8];
+    HIP_TRY(hipMemcpyAsync(h, a.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const double wp = h[3] ? (double)h[3] : 1.0, we = h[6] ? (double)h[6] : 1.0;
+    fprintf(stderr, "url clocks/wave: plan[stage %.0f bitmaps %.0f plan %.0f] emit[stage %.0f emit %.0f]\n",
+            h[0] / wp, h[1] / wp, h[2] / wp, h[4] / we, h[5] / we);
+  }
   return 0;
 }
 

@@ -2,6 +2,7 @@
 #include <algorithm>
 
 #include "engine_internal.hpp"
+#include "kernels.hpp"
 #include "host.hpp"
 
 namespace ose {
@@ -17,8 +18,7 @@ int Engine::build_sampling_tables() {
 }
 
 size_t Engine::workspace_bytes(uint64_t n_spans) const {
-  uint64_t tiles = (n_spans + 1023) / 1024;
-  return 4096 + tiles * 8;
+  return url_workspace_bytes(n_spans);
 }
 
 }  // namespace ose

@@ -25,6 +25,8 @@
 // Byte-identical to the oracle (oracle/url.c) including the compact arena.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../../include/odigos_amd.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -34,10 +36,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr int kGroups = 4;                       // 64-span groups per wave
-constexpr int kTile = kThreads * kGroups;        // spans per workgroup tile
 constexpr uint32_t kStage = 4 * 1024;            // per-wave LDS copy of one group's bytes
-constexpr uint32_t kOutLds = 20 * 1024;          // LDS image of one tile's output
 
 enum : uint32_t { M_NONE = 0, M_RENAME_SLASH, M_SLASH, M_RULE, M_DEFAULT, M_ORIG };
 
@@ -159,16 +158,23 @@ __device__ bool has_fffd(R& rd, uint32_t s, uint32_t e) {
   return false;
 }
 
+constexpr uint32_t kNameTab = 64;
+// The header is copied into registers once per workgroup: read through the
+// blob pointer the compiler cannot prove it unclobbered by the kernel's own
+// stores and reloads it (vector load + full wait) in every segment loop.
 struct Cfg {
   const uint8_t* blob;
-  const UrlCfgDev* h;
+  UrlCfgDev h;
   lds_u8* names;          // first kNamesLds bytes of the bytes section, staged in LDS
   uint32_t names_len;
-  __device__ const NameDev& name(uint32_t id) const {
-    return reinterpret_cast<const NameDev*>(blob + h->names_off)[id];
+  uint32_t ablate;        // diagnostics (UrlKernelArgs::ablate)
+  const __attribute__((address_space(3))) NameDev* name_tab;   // first kNameTab entries of the name table, in LDS
+  __device__ NameDev name(uint32_t id) const {
+    if (id < kNameTab) return NameDev{name_tab[id].off, name_tab[id].len};
+    return reinterpret_cast<const NameDev*>(blob + h.names_off)[id];
   }
   __device__ uint32_t dfa_off(int32_t i) const {
-    return reinterpret_cast<const uint32_t*>(blob + h->dfa_off)[i];
+    return reinterpret_cast<const uint32_t*>(blob + h.dfa_off)[i];
   }
 };
 
@@ -215,8 +221,8 @@ __device__ __forceinline__ int classify_segment(const Cfg& cfg, R& rd, uint32_t 
   }
   *e_out = q;
   const uint32_t e = q, len = e - s;
-  for (uint32_t k = 0; k < cfg.h->n_custom; k++) {   // custom ids first, in config order
-    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
+  for (uint32_t k = 0; k < cfg.h.n_custom; k++) {   // custom ids first, in config order
+    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h.custom_off)[k];
     if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, e)) return (int)cu.name;
   }
   if (date_len(len) && date_match(rd, s, len)) return kNameDate;
@@ -231,8 +237,8 @@ __device__ __forceinline__ int classify_segment(const Cfg& cfg, R& rd, uint32_t 
 // (without the leading '/') or -1.
 template <class R>
 __device__ int64_t attempt_rule(const Cfg& cfg, const UrlRuleDev& r, R& rd, uint32_t b0, uint32_t n) {
-  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h->segs_off) + r.seg_first;
-  const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
+  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h.segs_off) + r.seg_first;
+  const uint8_t* bytes = cfg.blob + cfg.h.bytes_off;
   uint32_t s = b0;
   int64_t len = 0;
   for (uint32_t k = 0; k < r.nseg; k++) {
@@ -311,7 +317,7 @@ __device__ __forceinline__ void put_name(const Cfg& cfg, uint32_t id, W& put) {
   if (nm.off + nm.len <= cfg.names_len) {
     for (uint32_t q = 0; q < nm.len; q++) put.byte(cfg.names[nm.off + q]);
   } else {
-    const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
+    const uint8_t* bytes = cfg.blob + cfg.h.bytes_off;
     for (uint32_t q = 0; q < nm.len; q++) put.byte(bytes[nm.off + q]);
   }
   put.byte('}');
@@ -319,8 +325,8 @@ __device__ __forceinline__ void put_name(const Cfg& cfg, uint32_t id, W& put) {
 
 template <class R, class W>
 __device__ void emit_rule(const Cfg& cfg, const UrlRuleDev& r, R& rd, uint32_t b0, uint32_t n, W& put) {
-  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h->segs_off) + r.seg_first;
-  const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
+  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h.segs_off) + r.seg_first;
+  const uint8_t* bytes = cfg.blob + cfg.h.bytes_off;
   uint32_t s = b0;
   for (uint32_t k = 0; k < r.nseg; k++) {
     const uint32_t e = scan_to(rd, s, n, '/');
@@ -359,11 +365,11 @@ __device__ __forceinline__ Plan plan_path(const Cfg& cfg, R& rd, uint32_t plen, 
     p.len = 1;
     return p;
   }
-  if (cfg.h->n_rules) {
+  if (cfg.h.n_rules) {
     const uint32_t nseg = 1 + count_byte(rd, p.lead, n, '/');
-    if (nseg <= cfg.h->max_rule_nseg) {
-      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
-      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
+    if (nseg <= cfg.h.max_rule_nseg) {
+      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h.rules_by_len_off);
+      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
       for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
         int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
         if (l >= 0) { p.mode = M_RULE; p.field = r; p.len = p.lead + (uint32_t)l; return p; }
@@ -402,7 +408,7 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
   if (mode == M_RULE) {
     const uint32_t n = path_end(rd, plen, f);
     if (lead) put.byte('/');
-    const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
+    const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
     emit_rule(cfg, rules[field], rd, lead, n, put);
     return;
   }
@@ -437,7 +443,11 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // [32r, 32r+32) and holds one 32-bit mask per class (bit k = byte 32r+k), so
 // the 64-bit windows of all classes at any byte come from 3 rows (6 x
 // ds_read_b128).  Built cooperatively, 32 bytes per lane, branch-free.
-enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, kClasses };
+// Classes 0-7 are read for every segment; 8-11 (the email classes) only for
+// segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
+enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
+constexpr uint32_t kBase = 8;
+constexpr uint32_t kRowVec = 3;   // u32x4 per row
 constexpr uint32_t kBmRows = kStage / 32 + 3;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
@@ -468,41 +478,56 @@ __device__ __forceinline__ void build_bitmaps(lds_u32* stage32, lds_u4* bm, uint
       const uint32_t hexl = ga & ~swar_ge(tl, 'f' + 1) & asc;
       const uint32_t print = swar_ge(t, '!') & ~swar_ge(t, 127) & asc;
       const uint32_t gat = swar_ge(t, '@');
+      const uint32_t gdot = swar_ge(t, '.'), gsl = swar_ge(t, '/');
+      const uint32_t dash = swar_ge(t, '-') & ~gdot & asc;
+      const uint32_t dot = gdot & ~gsl & asc;
+      const uint32_t extra = ((swar_ge(t, '_') & ~swar_ge(t, '`')) | (swar_ge(t, '%') & ~swar_ge(t, '&')) |
+                              (swar_ge(t, '+') & ~swar_ge(t, ','))) & asc;
+      const uint32_t dom = alpha | digit | dot | dash;
       const uint32_t m[kClasses] = {
-          swar_ge(t, '/') & ~g0 & asc,                     // C_SL
+          gsl & ~g0 & asc,                                 // C_SL
           ~(print & ~alpha) & kH,                          // C_BNL: outside noLetters' class
           ~(digit | hexl) & kH,                            // C_BHX
           digit,                                           // C_DG
           gat & ~swar_ge(t, 'A') & asc,                    // C_AT
           hi,                                              // C_HI
-          swar_ge(t, '-') & ~swar_ge(t, '.') & asc,        // C_DASH
+          dash,                                            // C_DASH
           swar_ge(t, '?') & ~gat & asc,                    // C_QM
+          ~(dom | extra) & kH,                             // C_BLOC: outside [A-Za-z0-9._%+-]
+          ~dom & kH,                                       // C_BDOM: outside [A-Za-z0-9.-]
+          dot,                                             // C_DOT
+          ~alpha & kH,                                     // C_NAL
       };
 #pragma unroll
       for (int c = 0; c < (int)kClasses; c++) acc[c] |= movemask4(m[c]) << (4 * d);
     }
-    bm[2 * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
-    bm[2 * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
+    bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
+    bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
+    bm[kRowVec * r + 2] = u32x4{acc[8], acc[9], acc[10], acc[11]};
   }
 }
 
-// 64-bit windows of every class starting at stage byte a
-struct Win {
-  uint64_t c[kClasses];
+// 64-bit windows of classes [c0, c0+4*nv) starting at stage byte a
+template <int NV>
+struct WinT {
+  uint64_t c[4 * NV];
 };
-__device__ __forceinline__ Win load_win(lds_cu4* bm, uint32_t a) {
+template <int V0, int NV>
+__device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a) {
   const uint32_t r = a >> 5, sh = a & 31;
-  const u32x4 a0 = bm[2 * r], a1 = bm[2 * r + 1], b0 = bm[2 * r + 2], b1 = bm[2 * r + 3], c0 = bm[2 * r + 4],
-              c1 = bm[2 * r + 5];
-  const uint32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-  const uint32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-  const uint32_t w2[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  Win w;
+  WinT<NV> w;
 #pragma unroll
-  for (int c = 0; c < (int)kClasses; c++)
-    w.c[c] = ((uint64_t)__builtin_amdgcn_alignbit(w2[c], w1[c], sh) << 32) | __builtin_amdgcn_alignbit(w1[c], w0[c], sh);
+  for (int v = 0; v < NV; v++) {
+    const u32x4 x0 = bm[kRowVec * r + V0 + v], x1 = bm[kRowVec * (r + 1) + V0 + v], x2 = bm[kRowVec * (r + 2) + V0 + v];
+    const uint32_t w0[4] = {x0.x, x0.y, x0.z, x0.w}, w1[4] = {x1.x, x1.y, x1.z, x1.w}, w2[4] = {x2.x, x2.y, x2.z, x2.w};
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      w.c[4 * v + c] =
+          ((uint64_t)__builtin_amdgcn_alignbit(w2[c], w1[c], sh) << 32) | __builtin_amdgcn_alignbit(w1[c], w0[c], sh);
+  }
   return w;
 }
+typedef WinT<2> Win;   // classes 0-7
 __device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
 // first byte of class c in [a, e) (stage coordinates), or e
@@ -510,27 +535,78 @@ __device__ __forceinline__ uint32_t first_of(lds_cu4* bm, uint32_t c, uint32_t a
   const lds_u32* b32 = (const lds_u32*)bm;
   while (a < e) {
     const uint32_t r = a >> 5, sh = a & 31;
-    const uint32_t m = __builtin_amdgcn_alignbit(b32[8 * (r + 1) + c], b32[8 * r + c], sh) & (uint32_t)low_mask(e - a);
+    const uint32_t m = __builtin_amdgcn_alignbit(b32[4 * kRowVec * (r + 1) + c], b32[4 * kRowVec * r + c], sh) &
+                       (uint32_t)low_mask(e - a);
     if (m) return a + __builtin_ctz(m);
     a += 32;
   }
   return e;
 }
 
+// datesRegex (templatize.go:67) for a segment of length L from the digit and
+// dash windows plus at most four byte reads: every accepted length has one
+// fixed shape (10 + {0, 6 "THH:MM", 9 "THH:MM:SS"} + {0, 1 "Z", 5 "+HHMM"}).
+template <class R>
+__device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint32_t s, uint32_t L) {
+  uint32_t tlen, zlen;
+  switch (L) {
+    case 10: tlen = 0; zlen = 0; break;
+    case 11: tlen = 0; zlen = 1; break;
+    case 15: tlen = 0; zlen = 5; break;
+    case 16: tlen = 6; zlen = 0; break;
+    case 17: tlen = 6; zlen = 1; break;
+    case 21: tlen = 6; zlen = 5; break;
+    case 19: tlen = 9; zlen = 0; break;
+    case 20: tlen = 9; zlen = 1; break;
+    case 24: tlen = 9; zlen = 5; break;
+    default: return false;
+  }
+  uint64_t dm = 0x36Full;                                   // YYYY-MM-DD digits
+  if (tlen) dm |= (3ull << 11) | (3ull << 14);              // THH:MM
+  if (tlen == 9) dm |= 3ull << 17;                          // :SS
+  const uint32_t z = 10 + tlen;
+  if (zlen == 5) dm |= 0xFull << (z + 1);                   // +HHMM
+  if ((dg & dm) != dm || ((dash >> 4) & 1) == 0 || ((dash >> 7) & 1) == 0) return false;
+  const uint32_t c_t = tlen ? rd.at(s + 10) : 'T', c_c1 = tlen ? rd.at(s + 13) : ':';
+  const uint32_t c_c2 = tlen == 9 ? rd.at(s + 16) : ':', c_z = zlen ? rd.at(s + z) : 'Z';
+  return c_t == 'T' && c_c1 == ':' && c_c2 == ':' &&
+         (zlen == 0 || (zlen == 1 ? c_z == 'Z' : (c_z == '+' || c_z == '-')));
+}
+
+// emailRegex (templatize.go:70) from the class windows: exactly one '@' at p,
+// local [0,p) >= 1 byte of [A-Za-z0-9._%+-], domain (p,L) all [A-Za-z0-9.-]
+// whose last '.' is at domain index >= 1 and is followed by >= 2 letters.
+__device__ __forceinline__ bool email_win(uint64_t at, lds_cu4* bm, uint32_t a, uint32_t L) {
+  const uint64_t M = low_mask(L);
+  const uint32_t p = (uint32_t)__builtin_ctzll(at);
+  if (p == 0) return false;
+  const WinT<1> e = load_win<2, 1>(bm, a);   // BLOC, BDOM, DOT, NAL
+  const uint64_t dom = M & ~low_mask(p + 1);
+  if ((e.c[0] & low_mask(p)) || (e.c[1] & dom)) return false;
+  const uint64_t dots = e.c[2] & dom;
+  if (!dots) return false;
+  const uint32_t q = 63 - (uint32_t)__builtin_clzll(dots);
+  if (q < p + 2 || L - q - 1 < 2) return false;
+  return (e.c[3] & M & ~low_mask(q + 1)) == 0;
+}
+
 // getSegmentTemplatizationString (templatize.go:242-269) from the class
-// windows of a segment of length L <= 64 starting at s (reader coordinates).
+// windows of a segment of length L <= 64 starting at s (reader coordinates,
+// stage byte a).
 constexpr uint64_t kUuidDash = (1ull << 8) | (1ull << 13) | (1ull << 18) | (1ull << 23);
 constexpr uint64_t kUuidHex = ((1ull << 36) - 1) & ~kUuidDash;
 template <class R>
-__device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w, uint32_t s, uint32_t L) {
+__device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w, lds_cu4* bm, uint32_t a, uint32_t s,
+                                            uint32_t L) {
   const uint64_t M = low_mask(L);
-  for (uint32_t k = 0; k < cfg.h->n_custom; k++) {   // custom ids first, in config order
-    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
+  for (uint32_t k = 0; k < cfg.h.n_custom; k++) {   // custom ids first, in config order
+    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h.custom_off)[k];
     if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, s + L)) return (int)cu.name;
   }
-  if (date_len(L) && (w.c[C_DG] & 0xF) == 0xF && date_match(rd, s, L)) return kNameDate;
+  if (!(cfg.ablate & 8) && date_len(L) && date_win(rd, w.c[C_DG], w.c[C_DASH], s, L)) return kNameDate;
   const bool any_hi = (w.c[C_HI] & M) != 0;
-  if (!any_hi && __popcll(w.c[C_AT] & M) == 1 && email_match(rd, s, s + L)) return kNameEmail;
+  const uint64_t at = w.c[C_AT] & M;
+  if (!(cfg.ablate & 16) && !any_hi && at && (at & (at - 1)) == 0 && email_win(at, bm, a, L)) return kNameEmail;
   const uint64_t d = w.c[C_DG] & M, d1 = d & (d >> 1), d2 = d1 & (d1 >> 2), d7 = d2 & (d2 >> 3);
   if ((L > 0 && (w.c[C_BNL] & M) == 0) || d7 || ((w.c[C_BHX] & M) == 0 && L >= 16 && (L & 1) == 0)) return kNameId;
   if (L >= 36) {
@@ -539,7 +615,7 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
         (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
       return kNameId;
   }
-  if (any_hi && has_fffd(rd, s, s + L)) return kNameId;
+  if (!(cfg.ablate & 32) && any_hi && has_fffd(rd, s, s + L)) return kNameId;
   return -1;
 }
 
@@ -557,11 +633,11 @@ __device__ __forceinline__ Plan plan_bits(const Cfg& cfg, LdsReader& rd, lds_cu4
     p.len = 1;
     return p;
   }
-  if (cfg.h->n_rules) {
+  if (cfg.h.n_rules) {
     const uint32_t nseg = 1 + count_byte(rd, p.lead, n, '/');
-    if (nseg <= cfg.h->max_rule_nseg) {
-      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
-      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
+    if (nseg <= cfg.h.max_rule_nseg) {
+      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h.rules_by_len_off);
+      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
       for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
         int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
         if (l >= 0) { p.mode = M_RULE; p.field = r; p.len = p.lead + (uint32_t)l; return p; }
@@ -572,14 +648,14 @@ __device__ __forceinline__ Plan plan_bits(const Cfg& cfg, LdsReader& rd, lds_cu4
   bool templated = false;
   for (;;) {
     const uint32_t rem = n - s;
-    const Win w = load_win(bm, p0 + s);
+    const Win w = load_win<0, 2>(bm, p0 + s);
     const uint64_t slm = w.c[C_SL] & low_mask(rem);
     uint32_t e;
     int id;
-    if (slm || rem <= 64) {
-      const uint32_t L = slm ? (uint32_t)__builtin_ctzll(slm) : rem;
+    if (slm || rem <= 64 || (cfg.ablate & 64)) {
+      const uint32_t L = slm ? (uint32_t)__builtin_ctzll(slm) : min(rem, 64u);
       e = s + L;
-      id = classify_win(cfg, rd, w, s, L);
+      id = classify_win(cfg, rd, w, bm, p0 + s, s, L);
     } else {
       id = classify_segment(cfg, rd, s, n, &e);   // segment longer than 64 bytes
     }
@@ -623,21 +699,7 @@ __device__ __forceinline__ uint32_t pack_meta(uint32_t mode, uint32_t lead, bool
 }
 
 constexpr uint32_t kNamesLds = 512;
-struct Smem {
-  uint32_t len[kTile];
-  uint32_t meta[kTile];
-  uint64_t code[kTile];
-  uint32_t wsum[kWaves];
-  uint32_t tile;
-  uint32_t pad;
-  uint64_t prefix;
-  __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
-  union {
-    __attribute__((aligned(16))) uint8_t out[kOutLds];      // phase 2: the tile's output image
-    __attribute__((aligned(16))) u32x4 bm[kWaves][2 * kBmRows];   // phase 1: per-wave class bitmaps
-  };
-  uint8_t names[kNamesLds];
-};
+constexpr uint32_t kWaveOut = 4 * 1024;   // per-wave LDS image of one group's output
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -646,8 +708,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Copies the arena bytes [lo, hi) the wave's 64 lanes reference (16-byte
-// aligned down) into the wave's LDS slice.  Returns the aligned start, or
-// ~0u when the range does not fit (lanes then read HBM directly).
+// aligned down) into the wave's LDS slice.  Returns the aligned start (and
+// the copied size in *nbytes), or ~0u when the range does not fit (lanes then
+// read HBM directly).
 __device__ uint32_t stage_wave(uint8_t* stage, const uint8_t* arena, uint32_t lo, uint32_t hi, uint32_t* nbytes) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -668,176 +731,428 @@ __device__ uint32_t stage_wave(uint8_t* stage, const uint8_t* arena, uint32_t lo
   return lo16;
 }
 
-__global__ __launch_bounds__(kThreads) void url_template_kernel(UrlKernelArgs a) {
-  __shared__ Smem sm;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) sm.tile = atomicAdd(a.tile_counter, 1u);
-  const UrlCfgDev* h = reinterpret_cast<const UrlCfgDev*>(a.cfg);
-  const uint32_t names_len = min(kNamesLds, h->total_bytes - h->bytes_off);
-  for (uint32_t k = tid; k < names_len; k += kThreads) sm.names[k] = a.cfg[h->bytes_off + k];
-  const Cfg cfg{a.cfg, h, (lds_u8*)sm.names, names_len};
+// Names and name table in LDS (whole workgroup, once).
+struct NamesSmem {
+  uint8_t names[kNamesLds];
+  NameDev name_tab[kNameTab];
+};
+__device__ __forceinline__ Cfg load_cfg(const UrlKernelArgs& a, NamesSmem& ns) {
+  const UrlCfgDev h = *reinterpret_cast<const UrlCfgDev*>(a.cfg);
+  const uint32_t names_len = min(kNamesLds, h.total_bytes - h.bytes_off);
+  for (uint32_t k = threadIdx.x; k < names_len; k += blockDim.x) ns.names[k] = a.cfg[h.bytes_off + k];
+  if (threadIdx.x < min(h.n_names, kNameTab))
+    ns.name_tab[threadIdx.x] = reinterpret_cast<const NameDev*>(a.cfg + h.names_off)[threadIdx.x];
+  __syncthreads();
+  return Cfg{a.cfg, h, (lds_u8*)ns.names, names_len, a.ablate,
+             (const __attribute__((address_space(3))) NameDev*)ns.name_tab};
+}
+
+// diagnostics (UrlKernelArgs::dbg): wave-uniform shader clock
+__device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+
+// ---------------------------------------------------------------------------
+// Software pipeline shared by K1 and K3: a wave's next group's arena bytes
+// are loaded into registers (16 B x 4 per lane covers the 4 KB stage) before
+// it works on the current group, and written to its LDS slice afterwards.
+struct StagePf {
+  uint4 v0, v1, v2, v3;
+  uint32_t lo16, bytes;   // bytes == 0: nothing to stage; lo16 == ~0u: range too large (HBM reads)
+};
+__device__ __forceinline__ StagePf stage_issue(const uint8_t* arena, uint32_t lo, uint32_t hi) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, (uint32_t)__shfl_xor(lo, o, kWave));
+    hi = max(hi, (uint32_t)__shfl_xor(hi, o, kWave));
+  }
+  StagePf pf;
+  pf.lo16 = 0;
+  pf.bytes = 0;
+  if (lo >= hi) return pf;
+  pf.lo16 = lo & ~15u;
+  const uint32_t bytes = (hi - pf.lo16 + 15u) & ~15u;
+  if (bytes > kStage) {
+    pf.lo16 = ~0u;
+    return pf;
+  }
+  pf.bytes = bytes;
+  const uint4* src = reinterpret_cast<const uint4*>(arena + pf.lo16);
+  const uint32_t nv = bytes / 16;
+  if (lane < nv) pf.v0 = src[lane];
+  if (lane + 64 < nv) pf.v1 = src[lane + 64];
+  if (lane + 128 < nv) pf.v2 = src[lane + 128];
+  if (lane + 192 < nv) pf.v3 = src[lane + 192];
+  return pf;
+}
+__device__ __forceinline__ void stage_commit(const StagePf& pf, uint8_t* stage) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nv = pf.bytes / 16;
+  uint4* dst = reinterpret_cast<uint4*>(stage);
+  if (lane < nv) dst[lane] = pf.v0;
+  if (lane + 64 < nv) dst[lane + 64] = pf.v1;
+  if (lane + 128 < nv) dst[lane + 128] = pf.v2;
+  if (lane + 192 < nv) dst[lane + 192] = pf.v3;
+  wave_lds_sync();
+}
+
+// Persistent grid: every wave walks groups g = first, first + stride, ...
+__device__ __forceinline__ uint32_t wave_first_group() { return blockIdx.x * kWaves + (threadIdx.x >> 6); }
+__device__ __forceinline__ uint32_t wave_stride() { return gridDim.x * kWaves; }
+
+// ---------------------------------------------------------------------------
+// K1: plan.  Waves are independent (no workgroup barrier after the config
+// load); per group: class bitmaps of the staged bytes, then one plan per span.
+struct PlanSmem {
+  NamesSmem ns;
+  __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
+  __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kBmRows];
+};
+
+// the columns K1 reads per span, and what they decide before the path is read
+struct PlanCols {
+  uint32_t f;
+  ose_strref pr;
+  uint32_t kind;
+  bool ok;
+};
+__device__ __forceinline__ PlanCols plan_cols(const UrlKernelArgs& a, uint64_t i) {
+  PlanCols c{0, {0, 0}, 0, false};
+  if (i < a.n_spans) {
+    c.f = a.url_flags[i];
+    c.kind = a.kind[i];
+    c.pr = a.path[i];
+    c.ok = a.res_url_ok == nullptr || a.res_url_ok[a.resource[i]];
+  }
+  return c;
+}
+// processor.go:235-259 enhanceSpan gate: 0 skip, 1 rename-to-slash, 2 template the path
+__device__ __forceinline__ uint32_t plan_gate(const PlanCols& c) {
+  if (!c.ok || !(c.f & OSE_URL_HAS_METHOD) || (c.kind != OSE_KIND_SERVER && c.kind != OSE_KIND_CLIENT)) return 0;
+  const uint32_t tgt = c.f & OSE_URL_TGT_MASK;
+  if (tgt != OSE_URL_TGT_ABSENT)
+    return (tgt == OSE_URL_TGT_STR_EMPTY && (c.f & OSE_URL_NAME_EQ_METHOD)) ? 1u : 0u;   // :241-243
+  return (c.f & OSE_URL_PATH_MASK) != OSE_URL_PATH_NONE ? 2u : 0u;
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void url_plan_kernel(UrlKernelArgs a) {
+  __shared__ PlanSmem sm;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const Cfg cfg = load_cfg(a, sm.ns);
+  const uint32_t stride = wave_stride();
+  uint32_t g = wave_first_group();
+  if (g >= a.n_groups) return;
+  const bool tm = a.dbg != nullptr;
+  uint64_t t0 = 0, t_stage = 0, t_bm = 0, t_plan = 0;
   uint8_t* stage = sm.stage[wv];
   lds_u32* stage32 = (lds_u32*)stage;
 
-  __syncthreads();
-  const uint32_t tile = sm.tile;
-  const uint64_t base = (uint64_t)tile * kTile;
+  // prologue: columns of groups g and g + stride, bytes of group g
+  PlanCols cur = plan_cols(a, (uint64_t)g * kWave + lane);
+  PlanCols nxt = plan_cols(a, (uint64_t)(g + stride) * kWave + lane);
+  bool np = plan_gate(cur) == 2;
+  StagePf pf = stage_issue(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u);
+  stage_commit(pf, stage);
+  for (;;) {
+    if (tm) t0 = clk();
+    const uint64_t i = (uint64_t)g * kWave + lane;
+    const uint32_t g2 = g + stride;
+    const bool more = g2 < a.n_groups;
+    // in flight while this group is planned: bytes of the next group, columns of the one after
+    const bool np2 = more && plan_gate(nxt) == 2;
+    const StagePf pf2 = stage_issue(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u);
+    const PlanCols nn = plan_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
+    if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
 
-  // ---------------- phase 1: plan (waves independent) ----------------
-  uint64_t flags_k = 0;   // 16 bits per group: url_flags | 0x100 when the path is read
-#pragma unroll 1
-  for (int g = 0; g < kGroups; g++) {
-    const int j = g * kThreads + wv * kWave + lane;   // 64 consecutive spans per wave and group
-    const uint64_t i = base + j;
+    const uint32_t gate = plan_gate(cur);
+    const bool needs_path = gate == 2;
+    const uint32_t lo16 = pf.lo16;
+    if (lo16 != ~0u && pf.bytes && !(a.ablate & 4)) {
+      build_bitmaps(stage32, (lds_u4*)sm.bm[wv], pf.bytes);
+      wave_lds_sync();
+    }
+    if (tm) { const uint64_t t1 = clk(); t_bm += t1 - t0; t0 = t1; }
     Plan p;
-    uint32_t oflags = 0, f = 0;
-    ose_strref pr{0, 0};
-    bool needs_path = false;
+    uint32_t oflags = 0;
+    if (gate == 1) {
+      p.mode = M_RENAME_SLASH;
+      p.len = 1;
+      oflags = OSE_OUT_RENAME;
+    } else if (needs_path && (a.ablate & 2)) {
+      p.mode = M_ORIG;
+      p.len = 1 + cur.pr.len;
+      p.field = cur.pr.len;
+      oflags = OSE_OUT_SET_ATTR;
+    } else if (needs_path) {
+      if (lo16 != ~0u) {
+        LdsReader rd(stage32, cur.pr.off - lo16);
+        p = plan_bits(cfg, rd, (lds_cu4*)sm.bm[wv], cur.pr.off - lo16, cur.pr.len, cur.f);
+      } else {
+        p = plan_global(cfg, a.arena + cur.pr.off, cur.pr.len, cur.f);
+      }
+      oflags = OSE_OUT_SET_ATTR;                                                       // processor.go:259
+      if ((cur.f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;     // :216-225
+    }
     if (i < a.n_spans) {
-      f = a.url_flags[i];
-      const uint32_t kind = a.kind[i];
-      const bool ok = a.res_url_ok == nullptr || a.res_url_ok[a.resource[i]];
-      if (ok && (f & OSE_URL_HAS_METHOD) && (kind == OSE_KIND_SERVER || kind == OSE_KIND_CLIENT)) {
-        const uint32_t tgt = f & OSE_URL_TGT_MASK, src = f & OSE_URL_PATH_MASK;
-        if (tgt != OSE_URL_TGT_ABSENT) {
-          if (tgt == OSE_URL_TGT_STR_EMPTY && (f & OSE_URL_NAME_EQ_METHOD)) {
-            p.mode = M_RENAME_SLASH;   // processor.go:241-243
-            p.len = 1;
-            oflags = OSE_OUT_RENAME;
+      a.plan_len[i] = p.len;
+      a.plan_meta[i] = pack_meta(p.mode, p.lead, p.slow, oflags, p.field);
+      a.plan_code[i] = p.code;
+    }
+    const uint64_t sum = wave_sum_u64(p.len);
+    if (lane == 0) a.group_sum[g] = sum;
+    if (tm) { const uint64_t t1 = clk(); t_plan += t1 - t0; t0 = t1; }
+    if (!more) break;
+    wave_lds_sync();   // every lane is done with this group's stage and bitmaps
+    stage_commit(pf2, stage);
+    if (tm) t_stage += clk() - t0;
+    pf = pf2;
+    cur = nxt;
+    nxt = nn;
+    g = g2;
+  }
+  if (tm && lane == 0) {
+    atomicAdd((unsigned long long*)&a.dbg[0], (unsigned long long)t_stage);
+    atomicAdd((unsigned long long*)&a.dbg[1], (unsigned long long)t_bm);
+    atomicAdd((unsigned long long*)&a.dbg[2], (unsigned long long)t_plan);
+    atomicAdd((unsigned long long*)&a.dbg[3], 1ull);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K2: exclusive scan of the group sums: 1024 groups per workgroup, tiles
+// chained with the decoupled look-back (device_common.hpp).
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a) {
+  __shared__ uint64_t wsum[kScanThreads / kWave];
+  __shared__ uint64_t prefix;
+  __shared__ uint32_t tile_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) tile_s = atomicAdd(a.scan_counter, 1u);
+  __syncthreads();
+  const uint32_t tile = tile_s;
+  const uint64_t k = (uint64_t)tile * kScanThreads + tid;
+  const uint64_t v = k < a.n_groups ? a.group_sum[k] : 0;
+  uint64_t incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint64_t t = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += t;
+  }
+  if (lane == kWave - 1) wsum[wv] = incl;
+  __syncthreads();
+  uint64_t wbase = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / kWave; w++) {
+    const uint64_t x = wsum[w];
+    if (w < wv) wbase += x;
+    total += x;
+  }
+  if (wv == 0) {
+    const uint64_t pfx = lookback_prefix(a.scan_status, tile, total, a.error);
+    if (lane == 0) {
+      prefix = pfx;
+      if (tile == a.n_scan_tiles - 1) {
+        if (a.used) *a.used = pfx + total;
+        if (pfx + total > a.out_cap) atomicOr(a.error, 2u);
+      }
+    }
+  }
+  __syncthreads();
+  if (k < a.n_groups) a.group_base[k] = prefix + wbase + incl - v;
+}
+
+// ---------------------------------------------------------------------------
+// K3: emit.  One wave per 64-span group: the group's output bytes are
+// contiguous, so lanes assemble them in a per-wave LDS image (dword-aligned
+// to the global destination; lanes OR whole dwords in with ds_or_b32, which
+// composes the dwords two spans share) and the wave stores the image with
+// coalesced dword stores.
+typedef __attribute__((address_space(3))) uint32_t lds_w32;
+struct PutOr {
+  lds_w32* img;
+  uint32_t wpos, nb;   // wpos: image offset of acc's first byte (dword aligned); nb: bytes in acc
+  uint64_t acc;
+  __device__ PutOr(lds_w32* im, uint32_t start) : img(im), wpos(start & ~3u), nb(start & 3u), acc(0) {}
+  __device__ __forceinline__ void flush() {
+    __hip_atomic_fetch_or(&img[wpos >> 2], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    acc >>= 32;
+    wpos += 4;
+    nb -= 4;
+  }
+  __device__ __forceinline__ void byte(uint32_t c) {
+    acc |= (uint64_t)(c & 0xFFu) << (8 * nb);
+    if (++nb == 4) flush();
+  }
+  __device__ __forceinline__ void word(uint32_t x, uint32_t nv) {
+    if (nv < 4) x &= (1u << (8 * nv)) - 1u;
+    acc |= (uint64_t)x << (8 * nb);
+    nb += nv;
+    if (nb >= 4) flush();
+  }
+  __device__ __forceinline__ void finish() {
+    if (nb) __hip_atomic_fetch_or(&img[wpos >> 2], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+};
+
+struct EmitSmem {
+  NamesSmem ns;
+  __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
+  __attribute__((aligned(16))) uint32_t img[kWaves][kWaveOut / 4 + 4];
+};
+
+struct EmitCols {
+  uint32_t len, meta;
+  uint64_t code;
+  ose_strref pr;
+};
+__device__ __forceinline__ EmitCols emit_cols(const UrlKernelArgs& a, uint64_t i) {
+  EmitCols c{0, 0, 0, {0, 0}};
+  if (i < a.n_spans) {
+    c.len = a.plan_len[i];
+    c.meta = a.plan_meta[i];
+    c.code = a.plan_code[i];
+    c.pr = a.path[i];
+  }
+  return c;
+}
+__device__ __forceinline__ bool emit_needs_path(uint32_t meta) {
+  const uint32_t mode = meta & 7u;
+  return mode == M_RULE || mode == M_DEFAULT || mode == M_ORIG;
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void url_emit_kernel(UrlKernelArgs a) {
+  __shared__ EmitSmem sm;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const Cfg cfg = load_cfg(a, sm.ns);
+  const uint32_t stride = wave_stride();
+  uint32_t g = wave_first_group();
+  if (g >= a.n_groups) return;
+  const bool tm = a.dbg != nullptr;
+  uint64_t t0 = 0, t_stage = 0, t_emit = 0;
+  uint8_t* stage = sm.stage[wv];
+  lds_u32* stage32 = (lds_u32*)stage;
+  lds_w32* img = (lds_w32*)sm.img[wv];
+
+  EmitCols cur = emit_cols(a, (uint64_t)g * kWave + lane);
+  EmitCols nxt = emit_cols(a, (uint64_t)(g + stride) * kWave + lane);
+  bool np = emit_needs_path(cur.meta);
+  StagePf pf = stage_issue(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u);
+  stage_commit(pf, stage);
+  for (;;) {
+    if (tm) t0 = clk();
+    const uint64_t i = (uint64_t)g * kWave + lane;
+    const bool valid = i < a.n_spans;
+    const uint32_t g2 = g + stride;
+    const bool more = g2 < a.n_groups;
+    const bool np2 = more && emit_needs_path(nxt.meta);
+    const StagePf pf2 = stage_issue(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u);
+    const EmitCols nn = emit_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
+    const uint64_t base = a.group_base[g];
+    const uint64_t gtotal = a.group_sum[g];
+    if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
+
+    const uint32_t len = cur.len, meta = cur.meta, mode = meta & 7u;
+    uint32_t incl = len;   // in-group exclusive offsets
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, kWave);
+      if (lane >= o) incl += t;
+    }
+    const uint32_t local = incl - len;
+    const bool overflow = base + gtotal > a.out_cap;
+    if (valid) {
+      a.url_out[i] = (uint8_t)((meta >> 5) & 3u);
+      a.tmpl[i] = ose_strref{(uint32_t)(base + local), len};
+    }
+    const bool needs_path = emit_needs_path(meta);
+    const ose_strref pr = needs_path ? cur.pr : ose_strref{0, 0};
+    const uint32_t lo16 = pf.lo16;
+    if (!overflow && !(a.ablate & 1)) {
+      const uint32_t shift = (uint32_t)(base & 3);
+      const uint32_t img_bytes = shift + (uint32_t)gtotal;
+      const bool direct = img_bytes > kWaveOut || lo16 == ~0u;   // wave-uniform
+      if (!direct) {
+        for (uint32_t k = lane; k < (img_bytes + 3) / 4; k += kWave) img[k] = 0;
+        wave_lds_sync();
+      }
+      if (len) {
+        const uint32_t lead = (meta >> 3) & 1u, field = meta >> 7;
+        const bool slow = (meta >> 4) & 1u;
+        const uint32_t f = (needs_path && (mode == M_RULE || field == kNField)) ? a.url_flags[i] : 0u;
+        if (!direct) {
+          PutOr put(img, shift + local);
+          LdsReader rd(stage32, pr.off - lo16);
+          emit_path(cfg, rd, pr.len, f, mode, lead, slow, field, cur.code, put);
+          put.finish();
+        } else if (lo16 != ~0u) {
+          emit_out_of_line(cfg, LdsReader(stage32, pr.off - lo16), pr.len, f, mode, lead, slow, field, cur.code,
+                           a.out_arena + base + local, len);
+        } else {
+          emit_out_of_line(cfg, ByteReader(a.arena + pr.off), pr.len, f, mode, lead, slow, field, cur.code,
+                           a.out_arena + base + local, len);
+        }
+      }
+      if (!direct) {
+        wave_lds_sync();
+        // image dword k <-> global bytes [base - shift + 4k, +4); bytes outside [base, base + gtotal)
+        // belong to the neighbouring groups, so partial dwords at the ends are stored bytewise
+        uint8_t* gdst = a.out_arena + (base - shift);
+        const uint32_t nd = (img_bytes + 3) / 4;
+        const uint64_t endb = shift + gtotal;
+        for (uint32_t k = lane; k < nd; k += kWave) {
+          const uint32_t w = img[k];
+          const uint32_t b0 = 4 * k;
+          if (b0 >= shift && b0 + 4 <= endb) {
+            *reinterpret_cast<uint32_t*>(gdst + b0) = w;
+          } else {
+            for (uint32_t q = 0; q < 4; q++)
+              if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(w >> (8 * q));
           }
-        } else if (src != OSE_URL_PATH_NONE) {
-          pr = a.path[i];
-          needs_path = true;
         }
       }
     }
-    flags_k |= (uint64_t)(needs_path ? (f | 0x100u) : 0u) << (16 * g);
-    uint32_t bytes;
-    const uint32_t lo16 =
-        stage_wave(stage, a.arena, needs_path ? pr.off : ~0u, needs_path ? pr.off + pr.len : 0u, &bytes);
-    if (lo16 != ~0u && bytes) {
-      build_bitmaps(stage32, (lds_u4*)sm.bm[wv], bytes);
-      wave_lds_sync();
-    }
-    if (needs_path) {
-      if (lo16 != ~0u) {
-        LdsReader rd(stage32, pr.off - lo16);
-        p = plan_bits(cfg, rd, (lds_cu4*)sm.bm[wv], pr.off - lo16, pr.len, f);
-      } else {
-        p = plan_global(cfg, a.arena + pr.off, pr.len, f);
-      }
-      oflags = OSE_OUT_SET_ATTR;                                                   // processor.go:259
-      if ((f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;     // :216-225
-    }
-    sm.len[j] = p.len;
-    sm.meta[j] = pack_meta(p.mode, p.lead, p.slow, oflags, p.field);
-    sm.code[j] = p.code;
-    wave_lds_sync();   // the stage slice is reused by the next group
+    if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
+    if (!more) break;
+    wave_lds_sync();   // image and stage reads of this group are done
+    stage_commit(pf2, stage);
+    if (tm) t_stage += clk() - t0;
+    pf = pf2;
+    cur = nxt;
+    nxt = nn;
+    g = g2;
   }
-  __syncthreads();
+  if (tm && lane == 0) {
+    atomicAdd((unsigned long long*)&a.dbg[4], (unsigned long long)t_stage);
+    atomicAdd((unsigned long long*)&a.dbg[5], (unsigned long long)t_emit);
+    atomicAdd((unsigned long long*)&a.dbg[6], 1ull);
+  }
+}
 
-  // ---------------- workgroup exclusive scan (thread t owns spans 4t..4t+3) ----------------
-  const uint32_t l0 = sm.len[4 * tid], l1 = sm.len[4 * tid + 1], l2 = sm.len[4 * tid + 2], l3 = sm.len[4 * tid + 3];
-  const uint32_t mine = l0 + l1 + l2 + l3;
-  uint32_t incl = mine;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    uint32_t t = __shfl_up(incl, o, kWave);
-    if (lane >= o) incl += t;
-  }
-  if (lane == kWave - 1) sm.wsum[wv] = incl;
-  __syncthreads();
-  uint32_t wbase = 0, total = 0;
-#pragma unroll
-  for (int w = 0; w < kWaves; w++) {
-    uint32_t v = sm.wsum[w];
-    if (w < wv) wbase += v;
-    total += v;
-  }
-  const uint32_t ex = wbase + incl - mine;
-  __syncthreads();
-  // sm.len now holds exclusive offsets within the tile
-  sm.len[4 * tid] = ex;
-  sm.len[4 * tid + 1] = ex + l0;
-  sm.len[4 * tid + 2] = ex + l0 + l1;
-  sm.len[4 * tid + 3] = ex + l0 + l1 + l2;
-  const bool direct = total > kOutLds;
-
-  // ---------------- look-back (wave 0) ----------------
-  if (wv == 0) {
-    uint64_t pfx = lookback_prefix(a.tile_status, tile, total, a.error);
-    if (lane == 0) {
-      sm.prefix = pfx;
-      if (pfx + total > a.out_cap) atomicOr(a.error, 2u);
-      if (tile == a.n_tiles - 1 && a.used) *a.used = pfx + total;
-    }
-  }
-  __syncthreads();
-  const uint64_t prefix = sm.prefix;
-  const bool overflow = prefix + total > a.out_cap;
-
-  // ---------------- phase 2: emit (waves independent) ----------------
-#pragma unroll 1
-  for (int g = 0; g < kGroups; g++) {
-    const int j = g * kThreads + wv * kWave + lane;
-    const uint64_t i = base + j;
-    const uint32_t local = sm.len[j];
-    const uint32_t len = (j + 1 < kTile ? sm.len[j + 1] : total) - local;
-    const uint32_t meta = sm.meta[j];
-    const uint32_t f = (uint32_t)(flags_k >> (16 * g)) & 0xFFFFu;
-    const bool needs_path = (f & 0x100u) != 0;
-    if (i < a.n_spans) {
-      a.url_out[i] = (uint8_t)((meta >> 5) & 3u);
-      a.tmpl[i] = ose_strref{(uint32_t)(prefix + local), len};
-    }
-    const ose_strref pr = needs_path ? a.path[i] : ose_strref{0, 0};
-    uint32_t bytes;
-    const uint32_t lo16 =
-        stage_wave(stage, a.arena, needs_path ? pr.off : ~0u, needs_path ? pr.off + pr.len : 0u, &bytes);
-    if (len && !overflow) {
-      const uint32_t mode = meta & 7u, lead = (meta >> 3) & 1u, field = meta >> 7;
-      const bool slow = (meta >> 4) & 1u;
-      const uint64_t code = sm.code[j];
-      if (!direct && lo16 != ~0u) {
-        Put<lds_out_u8*> put{(lds_out_u8*)(sm.out + local), 0, len};
-        LdsReader rd(stage32, pr.off - lo16);
-        emit_path(cfg, rd, pr.len, f, mode, lead, slow, field, code, put);
-      } else if (!direct) {
-        emit_out_of_line(cfg, ByteReader(a.arena + pr.off), pr.len, f, mode, lead, slow, field, code,
-                         (lds_out_u8*)(sm.out + local), len);
-      } else if (lo16 != ~0u) {
-        emit_out_of_line(cfg, LdsReader(stage32, pr.off - lo16), pr.len, f, mode, lead, slow, field, code,
-                         a.out_arena + prefix + local, len);
-      } else {
-        emit_out_of_line(cfg, ByteReader(a.arena + pr.off), pr.len, f, mode, lead, slow, field, code,
-                         a.out_arena + prefix + local, len);
-      }
-    }
-    wave_lds_sync();
-  }
-  if (direct || overflow) return;
-  __syncthreads();
-  // coalesced copy of the tile image: byte head to 4-byte alignment, dword body, byte tail
-  uint8_t* dst = a.out_arena + prefix;
-  uint32_t head = (uint32_t)((4 - ((uint64_t)dst & 3)) & 3);
-  if (head > total) head = total;
-  if ((uint32_t)tid < head) dst[tid] = sm.out[tid];
-  const uint32_t body = (total - head) / 4;
-  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
-  lds_u32* o32 = (lds_u32*)sm.out;
-  for (uint32_t k = tid; k < body; k += kThreads) {
-    const uint32_t b = head + 4 * k;
-    d32[k] = __builtin_amdgcn_alignbyte(o32[(b >> 2) + 1], o32[b >> 2], b & 3);
-  }
-  const uint32_t tail0 = head + 4 * body;
-  if ((uint32_t)tid < total - tail0) dst[tail0 + tid] = sm.out[tail0 + tid];
+// Persistent grid: as many workgroups as fit on the device at once (capped
+// by the number of groups).
+template <class K>
+static uint32_t resident_blocks(K kernel, size_t dyn_lds) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, dyn_lds) != hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  return (uint32_t)(cus * per_cu);
 }
 
 }  // namespace
 
-void launch_url_template(const UrlKernelArgs& a, hipStream_t st) {
-  if (a.n_tiles == 0) return;
-  hipLaunchKernelGGL(url_template_kernel, dim3(a.n_tiles), dim3(kThreads), 0, st, a);
+void launch_url_plan(const UrlKernelArgs& a, hipStream_t st) {
+  static const uint32_t cap = resident_blocks(url_plan_kernel, 0);
+  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL(url_plan_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+}
+void launch_url_scan(const UrlKernelArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(url_scan_kernel, dim3(a.n_scan_tiles), dim3(kScanThreads), 0, st, a);
+}
+void launch_url_emit(const UrlKernelArgs& a, hipStream_t st) {
+  static const uint32_t cap = resident_blocks(url_emit_kernel, 0);
+  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL(url_emit_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
 }
 
 }  // namespace ose

@@ -1,4 +1,4 @@
-"""Ablation timings of url_template_kernel on synthetic C2 batches (diagnostic)."""
+"""Ablation timings of the URL kernels on synthetic C2 batches (diagnostic)."""
 import sys, time
 from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
@@ -22,8 +22,9 @@ def timeit(label, reps=5):
         eng.process_device(db, native.STAGE_TEMPLATE, stream=sh)
     torch.cuda.synchronize()
     eng.profile(False)
-    p = eng.profile_read()["url_template_kernel"]
-    print(f"{label:40s} {p['ms']/p['launches']:9.3f} ms/launch", flush=True)
+    pr = eng.profile_read()
+    ms = {k: pr[k]["ms"] / pr[k]["launches"] for k in ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel")}
+    print(f"{label:40s} {sum(ms.values()):9.3f} ms  (plan {ms['url_plan_kernel']:.3f} scan {ms['url_scan_kernel']:.3f} emit {ms['url_emit_kernel']:.3f})", flush=True)
 
 orig = db.t["url_flags"].clone()
 timeit("C2 baseline")
@@ -44,3 +45,10 @@ p[:, 1].clamp_(max=8)
 timeit("paths truncated to 8 bytes")
 p.copy_(porig)
 timeit("C2 baseline again")
+import os
+for v, label in ((1, "skip emission"), (2, "skip planning"), (3, "skip planning+emission"), (7, "stage only (no bitmaps/plan/emit)"),
+                 (1 | 8, "no emit, skip date"), (1 | 16, "no emit, skip email"), (1 | 32, "no emit, skip fffd"),
+                 (1 | 64, "no emit, long segs cut to 64"), (1 | 8 | 16 | 32 | 64, "no emit, skip all rare")):
+    os.environ["OSE_URL_ABLATE"] = str(v)
+    timeit(label)
+os.environ.pop("OSE_URL_ABLATE")

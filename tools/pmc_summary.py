@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc CSVs: per-counter mean per dispatch of a kernel."""
 import csv, glob, sys, collections
-kern = sys.argv[2] if len(sys.argv) > 2 else "url_template_kernel"
+kern = sys.argv[2] if len(sys.argv) > 2 else "url_plan_kernel"
 acc = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):

@@ -1,0 +1,21 @@
+"""Per-section shader-clock breakdown of the URL kernels (diagnostic;
+OSE_URL_ABLATE bit 512 makes the engine print the per-wave sums)."""
+import os, sys
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import torch
+from odigos_amd import native
+from odigos_amd.batch import DeviceBatch, Engine, Generator
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+g = Generator("url", 0x0D160002, n, threads=16)
+g.cols.res_url_ok = None
+eng = Engine({"odigosurltemplate": {}})
+db = DeviceBatch(g.cols, fields=("arena", "kind", "url_flags", "path"))
+sh = torch.cuda.current_stream().cuda_stream
+names = ["total", "stage1", "bitmaps", "plan", "scan+lb", "stage2", "emit", "copyout", "waves"]
+for ab in (512, 512 | 8 | 16 | 32 | 64):
+    os.environ["OSE_URL_ABLATE"] = str(ab)
+    eng.process_device(db, native.STAGE_TEMPLATE, stream=sh)
+    torch.cuda.synchronize()
+    print("ablate", ab, flush=True)
