@@ -802,11 +802,117 @@ __device__ __forceinline__ uint32_t wave_stride() { return gridDim.x * kWaves; }
 // ---------------------------------------------------------------------------
 // K1: plan.  Waves are independent (no workgroup barrier after the config
 // load); per group: class bitmaps of the staged bytes, then one plan per span.
+constexpr uint32_t kSegCap = 192;   // per-wave segment list (C2 groups hold ~118 segments, max seen 182)
 struct PlanSmem {
   NamesSmem ns;
   __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
   __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kBmRows];
+  uint32_t segs[kWaves][kSegCap];
 };
+
+// number of bytes of class c in [a, e) (stage coordinates)
+__device__ __forceinline__ uint32_t count_of(lds_cu4* bm, uint32_t c, uint32_t a, uint32_t e) {
+  const lds_u32* b32 = (const lds_u32*)bm;
+  uint32_t k = 0;
+  while (a < e) {
+    const uint32_t r = a >> 5, sh = a & 31;
+    k += __builtin_popcount(__builtin_amdgcn_alignbit(b32[4 * kRowVec * (r + 1) + c], b32[4 * kRowVec * r + c], sh) &
+                            (uint32_t)low_mask(e - a));
+    a += 32;
+  }
+  return k;
+}
+
+// Phase 1 for a whole group through a segment list: each lane enumerates its
+// span's segments into the wave's list; the wave classifies the list 64
+// segments per step (about 2 steps for a C2 group, instead of one step per
+// segment index of the longest path); each lane then folds its own entries.
+// Entries: start 12 | len 13 before classification, len << 8 | (id + 1) after.
+// Returns false (nothing written) when the list would overflow.
+__device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32, lds_cu4* bm, uint32_t* segs,
+                                                bool needs_path, uint32_t p0, uint32_t plen, uint32_t f, Plan& p) {
+  const int lane = threadIdx.x & 63;
+  LdsReader rd(stage32, p0);
+  uint32_t n = 0, nseg = 0;
+  if (needs_path) {
+    n = (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? first_of(bm, C_QM, p0, p0 + plen) - p0 : plen;
+    p.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
+    if (n == p.lead) {   // "" or "/" -> "/" (processor.go:156-160)
+      p.mode = M_SLASH;
+      p.len = 1;
+    } else {
+      nseg = 1 + count_of(bm, C_SL, p0 + p.lead, p0 + n);
+      if (cfg.h.n_rules && nseg <= cfg.h.max_rule_nseg) {   // processor.go:162-171: rules first
+        const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h.rules_by_len_off);
+        const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
+        for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
+          const int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
+          if (l >= 0) {
+            p.mode = M_RULE;
+            p.field = r;
+            p.len = p.lead + (uint32_t)l;
+            nseg = 0;
+            break;
+          }
+        }
+      }
+    }
+  }
+  uint32_t incl = nseg;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += t;
+  }
+  const uint32_t total = __shfl(incl, kWave - 1, kWave);
+  if (total > kSegCap) return false;
+  const uint32_t off = incl - nseg;
+  if (nseg) {   // enumerate
+    const uint32_t bend = p0 + n;
+    uint32_t s = p0 + p.lead;
+    for (uint32_t k = 0; k < nseg; k++) {
+      const uint32_t e = k + 1 < nseg ? first_of(bm, C_SL, s, bend) : bend;
+      segs[off + k] = s | ((e - s) << 12);
+      s = e + 1;
+    }
+  }
+  wave_lds_sync();
+  LdsReader rd0(stage32, 0);
+  for (uint32_t x = lane; x < total; x += kWave) {   // classify
+    const uint32_t ent = segs[x];
+    const uint32_t s = ent & 0xFFFu, L = ent >> 12;
+    int id;
+    if (L <= 64) {
+      const Win w = load_win<0, 2>(bm, s);
+      id = classify_win(cfg, rd0, w, bm, s, s, L);
+    } else {
+      uint32_t e;
+      id = classify_segment(cfg, rd0, s, s + L, &e);   // segment longer than 64 bytes
+    }
+    segs[x] = (L << 8) | (uint32_t)(id + 1);
+  }
+  wave_lds_sync();
+  if (nseg) {   // fold
+    uint32_t l = p.lead + nseg - 1;
+    bool templated = false;
+    for (uint32_t k = 0; k < nseg; k++) {
+      const uint32_t r = segs[off + k];
+      const int id = (int)(r & 0xFFu) - 1;
+      if (id >= 0) {
+        templated = true;
+        l += cfg.name((uint32_t)id).len + 2;
+        if (k < 16 && id < 15) p.code |= (uint64_t)(id + 1) << (k * 4);
+        else p.slow = true;
+      } else {
+        l += r >> 8;
+      }
+    }
+    if (templated) { p.mode = M_DEFAULT; p.len = l; }
+    else { p.mode = M_ORIG; p.len = 1 + (n - p.lead); }   // "/" + body (processor.go:182-185)
+    p.field = n < kNField ? n : kNField;
+  }
+  return true;
+}
 
 // the columns K1 reads per span, and what they decide before the path is read
 struct PlanCols {
@@ -873,6 +979,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     if (tm) { const uint64_t t1 = clk(); t_bm += t1 - t0; t0 = t1; }
     Plan p;
     uint32_t oflags = 0;
+    // the list planner uses wave shuffles: called by the whole wave (lanes without a path add no segments)
+    bool listed = false;
+    if (lo16 != ~0u && !(a.ablate & (1024 | 2)))
+      listed = plan_group_list(cfg, stage32, (lds_cu4*)sm.bm[wv], sm.segs[wv], needs_path, cur.pr.off - lo16,
+                               cur.pr.len, cur.f, p);
     if (gate == 1) {
       p.mode = M_RENAME_SLASH;
       p.len = 1;
@@ -882,13 +993,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
       p.len = 1 + cur.pr.len;
       p.field = cur.pr.len;
       oflags = OSE_OUT_SET_ATTR;
-    } else if (needs_path) {
+    } else if (needs_path && !listed) {
       if (lo16 != ~0u) {
         LdsReader rd(stage32, cur.pr.off - lo16);
         p = plan_bits(cfg, rd, (lds_cu4*)sm.bm[wv], cur.pr.off - lo16, cur.pr.len, cur.f);
       } else {
         p = plan_global(cfg, a.arena + cur.pr.off, cur.pr.len, cur.f);
       }
+    }
+    if (needs_path && !(a.ablate & 2)) {
       oflags = OSE_OUT_SET_ATTR;                                                       // processor.go:259
       if ((cur.f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;     // :216-225
     }

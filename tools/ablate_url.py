@@ -48,7 +48,7 @@ timeit("C2 baseline again")
 import os
 for v, label in ((1, "skip emission"), (2, "skip planning"), (3, "skip planning+emission"), (7, "stage only (no bitmaps/plan/emit)"),
                  (1 | 8, "no emit, skip date"), (1 | 16, "no emit, skip email"), (1 | 32, "no emit, skip fffd"),
-                 (1 | 64, "no emit, long segs cut to 64"), (1 | 8 | 16 | 32 | 64, "no emit, skip all rare")):
+                 (1 | 64, "no emit, long segs cut to 64"), (1 | 8 | 16 | 32 | 64, "no emit, skip all rare"), (1 | 1024, "no emit, per-lane planner (no list)")):
     os.environ["OSE_URL_ABLATE"] = str(v)
     timeit(label)
 os.environ.pop("OSE_URL_ABLATE")

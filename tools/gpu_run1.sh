@@ -10,3 +10,4 @@ cat gpurun_out/bench.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_r1 -o url --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log 2>&1 || { echo "rocprof failed"; tail -30 $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log; exit 1; }
 find $GRAFT_REPO_ROOT/gpurun_out/prof_r1 -name "*stats*" | head
+bash $GRAFT_REPO_ROOT/tools/pmc_traffic.sh url || exit 1

@@ -1,0 +1,36 @@
+"""Turn FETCH_SIZE / WRITE_SIZE rocprofv3 CSVs into HBM bytes per launch of the
+bench workload's kernels (written to a JSON merged into profiles/pmc_traffic.json).
+
+traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB counters -> bytes); FETCH_SIZE is
+doubled per MI355X_MICROARCH.md (wide reads tallied at half).  The bench line's
+kernel key is the '+'-joined kernel list of the stage."""
+import csv, glob, json, re, sys
+from collections import defaultdict
+
+wl, root, out = sys.argv[1], sys.argv[2], sys.argv[3]
+STAGES = {"url": ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel")}
+kernels = STAGES[wl]
+vals = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+for c in vals:
+    for f in glob.glob(f"{root}/{c}/**/*counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            for k in kernels:
+                if k in row.get("Kernel_Name", ""):
+                    vals[c][k].append(float(row["Counter_Value"]))
+spans = None
+for f in glob.glob(f"{root}/FETCH_SIZE.log"):
+    for line in open(f):
+        if line.startswith("{"):
+            spans = json.loads(line)["config"]["spans_per_gpu"]
+per_k = {}
+for k in kernels:
+    fe = vals["FETCH_SIZE"][k]
+    wr = vals["WRITE_SIZE"][k]
+    if not fe or not wr:
+        sys.exit(f"missing counters for {k}")
+    fkb, wkb = sum(fe) / len(fe), sum(wr) / len(wr)
+    per_k[k] = {"fetch_kib": fkb, "write_kib": wkb, "hbm_bytes": (2 * fkb + wkb) * 1024}
+ent = {"spans": spans, "hbm_bytes_per_launch": sum(v["hbm_bytes"] for v in per_k.values()),
+       "per_kernel": per_k, "method": "2*FETCH_SIZE + WRITE_SIZE, KiB, mean per dispatch"}
+json.dump({wl: {"+".join(kernels): ent}}, open(out, "w"), indent=1)
+print(json.dumps(ent))
