@@ -93,10 +93,10 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
   IN(scope_size, 4 * S);
   OUT(keep, n);
   OUT(trace_count, 4);
-  OUT(trace_first_span, 4 * n);
-  OUT(trace_keep, n);
-  OUT(trace_level, n);
-  OUT(trace_ratio, 8 * n);
+  OUT(trace_first_span, 4 * std::max<uint64_t>(n, 1));   // BATCH mode: one trace even with no spans
+  OUT(trace_keep, 1 * std::max<uint64_t>(n, 1));
+  OUT(trace_level, 1 * std::max<uint64_t>(n, 1));
+  OUT(trace_ratio, 8 * std::max<uint64_t>(n, 1));
   OUT(url_out, n);
   OUT(tmpl, 8 * n);
   OUT(tmpl_arena, 2 * dims->arena_bytes + 8 * n + 4096);

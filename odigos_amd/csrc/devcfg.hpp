@@ -54,3 +54,41 @@ struct UrlCfgDev {
 };
 
 }  // namespace ose
+
+namespace ose {
+
+// odigossampling tables (sampling_host.cpp builds them from the decoded
+// Config; trace_kernel.hip reads them).  Rules are stored in level order
+// global, service, endpoint (rule_engine.go:56-60), config order inside a
+// level (evaluateLevel is an order-sensitive fold, rule_engine.go:89-115).
+enum : uint32_t { kSampError = 0, kSampLatency = 1, kSampService = 2 };
+constexpr uint32_t kMaxLatencyRules = 64;   // bits of the per-trace latency masks
+constexpr uint32_t kMaxServiceRules = 64;   // bits of the per-trace service mask
+struct SampRuleDev {
+  uint32_t type;
+  uint32_t bit;          // latency: latency-rule index; service: service-rule index
+  double ratio;          // service_name sampling_ratio
+  double fallback;       // fallback_sampling_ratio
+};
+struct SampLatDev {      // one http_latency rule (latency.go:12-17)
+  uint32_t slot;         // latency-service slot of its service_name
+  uint32_t route_off, route_len;   // http_route prefix bytes (bytes section)
+  uint32_t _pad;
+  int64_t threshold;     // ms
+};
+struct SampCfgDev {
+  uint32_t n_rules;
+  uint32_t level_first[4];   // rules of level L: [level_first[L], level_first[L+1])
+  uint32_t n_lat;            // http_latency rules
+  uint32_t n_lat_slots;      // distinct service names among them
+  uint32_t n_services;       // interned service ids (res_svc values >= this are "no rule service")
+  uint32_t rules_off;        // SampRuleDev[n_rules]
+  uint32_t lat_off;          // SampLatDev[n_lat]
+  uint32_t svc_slot_off;     // uint32 [n_services]: latency slot of each service, or ~0
+  uint32_t slot_rules_off;   // uint64 [n_lat_slots]: latency rules of each slot
+  uint32_t svc_bits_off;     // uint64 [n_services]: service rules naming each service
+  uint32_t bytes_off;
+  uint32_t total_bytes;
+};
+
+}  // namespace ose

@@ -191,6 +191,7 @@ Engine::~Engine() {
   if (sampling_blob_dev) (void)hipFree(sampling_blob_dev);
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
+    if (w->table) (void)hipFree(w->table);
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
   }
@@ -354,13 +355,12 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
                const ose_rand* rnd, hipStream_t st) {
   if (!c || !o) return fail(OSE_EINVAL, "columns and outputs are required");
   if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE)) return fail(OSE_EINVAL, "unknown stage bit");
-  (void)group_mode;
-  (void)rnd;
-  if (mask & OSE_STAGE_SAMPLE) return fail(OSE_ENOTSUP, "SAMPLE stage not built yet");
   if (mask & OSE_STAGE_SIZE) return fail(OSE_ENOTSUP, "SIZE stage not built yet");
   Workspace* ws = e->acquire_ws();
   int rc = 0;
-  if (mask & OSE_STAGE_TEMPLATE) rc = run_url(e, c, o, st, ws);
+  // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
+  if (mask & OSE_STAGE_SAMPLE) rc = run_sampling(e, c, o, group_mode, rnd, st, ws);
+  if (!rc && (mask & OSE_STAGE_TEMPLATE)) rc = run_url(e, c, o, st, ws);
   e->release_ws(ws);
   return rc;
 }
@@ -415,6 +415,10 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
     rc = upload(e->url_blob_host, &e->url_blob_dev);
     if (rc) { delete e; return rc; }
   }
+  if (e->has_sampling) {
+    rc = upload(e->sampling_blob_host, &e->sampling_blob_dev);
+    if (rc) { delete e; return rc; }
+  }
   *out = reinterpret_cast<ose_engine*>(e);
   return 0;
 }
@@ -445,6 +449,7 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   Engine* e = reinterpret_cast<Engine*>(eng);
   Workspace* ws = e->acquire_ws();
   int rc = ws->reserve(e->workspace_bytes(n_spans));
+  if (!rc && e->has_sampling) rc = ws->reserve_table(n_spans);
   e->release_ws(ws);
   return rc;
 }

@@ -24,6 +24,12 @@ struct Workspace {
   size_t cap = 0;
   hipStream_t stream = nullptr;   // used by ose_process (host batches)
   int reserve(size_t bytes);
+  // exact trace_id hash table of the SAMPLE stage (trace_kernel.hip), kept
+  // across calls: entries carry a generation tag, so nothing is cleared
+  void* table = nullptr;
+  uint64_t table_slots_cap = 0;
+  uint32_t epoch = 0;
+  int reserve_table(uint64_t n_spans);
 };
 
 struct Engine {
@@ -40,6 +46,7 @@ struct Engine {
   std::vector<uint8_t> sampling_blob_host;
   uint8_t* sampling_blob_dev = nullptr;
   std::unordered_map<std::string, uint32_t> service_ids;
+  uint32_t sampling_n_lat = 0;
 
   std::mutex mu;
   std::vector<Workspace*> pool, free_ws;
@@ -60,6 +67,8 @@ struct Engine {
   size_t workspace_bytes(uint64_t n_spans) const;
 };
 
+int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
+                 hipStream_t st, Workspace* ws);
 int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
                const ose_rand* rnd, hipStream_t st);
 

@@ -314,7 +314,8 @@ void TracesProcessor::Apply(HostBatch& hb, Traces& td) {
   }
   if (!keep.empty()) {
     if (group_mode == OSE_GROUP_BATCH) {
-      if (hb.cols.n_spans > 0 && !keep[0]) td.resource_spans.clear();
+      // one decision for the whole call, spanless resources included
+      if (!o.trace_keep[0]) td.resource_spans.clear();
     } else {
       size_t k = 0;
       std::vector<ResourceSpans> rout;
@@ -384,6 +385,10 @@ int TracesProcessor::ProcessTraces(Traces& td) {
   if (rc) { ose_batch_release(b); return rc; }
   // read back into the host batch and apply
   cp(hb->outs.keep, o->keep, n);
+  if (stages() & OSE_STAGE_SAMPLE) {
+    cp(hb->outs.trace_count, o->trace_count, 4);
+    cp(hb->outs.trace_keep, o->trace_keep, 1);
+  }
   cp(hb->outs.url_out, o->url_out, n);
   cp(hb->outs.tmpl, o->tmpl, 8 * n);
   uint64_t used = *o->tmpl_arena_used;

@@ -53,3 +53,106 @@ void launch_url_scan(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_emit(const UrlKernelArgs& a, hipStream_t st);
 
 }  // namespace ose
+
+namespace ose {
+
+// odigossampling: trace grouping, per-trace reduction and the rule fold
+// (trace_kernel.hip).  A "position" is an index into the evaluation order:
+// the batch order itself (fast path) or the stable sort of spans by trace
+// (slow path, perm != null).
+struct TraceSlot {            // exact trace_id hash table entry (32 B)
+  uint32_t state;             // epoch << 2 | {0 empty, 1 busy, 2 ready}
+  uint32_t first;             // smallest run-head position of this trace_id
+  uint64_t hi, lo;
+  uint64_t _pad;
+};
+struct TraceRec {             // per-trace record, stored at the trace's head position
+  uint32_t first_span;
+  uint8_t keep, level, _p0, _p1;
+  double ratio;
+};
+enum : uint32_t { kTraceRuns = 0, kTracePerm = 1, kTraceBatch = 2 };
+struct TraceKernelArgs {
+  uint64_t n_spans;
+  uint32_t n_windows;         // ceil(n_spans / 64), >= 1
+  uint32_t mode;              // kTrace*
+  uint32_t n_resources;
+  uint32_t epoch;             // hash table generation (>= 1)
+  const uint64_t* tid;
+  const uint64_t* start;
+  const uint64_t* end;
+  const uint8_t* status;
+  const uint32_t* resource;
+  const ose_strref* route;
+  const uint8_t* arena;
+  const uint32_t* res_svc;
+  const uint32_t* res_svc_str;
+  const uint8_t* cfg;         // SampCfgDev blob
+  uint64_t seed;
+  uint8_t* keep;              // [n_spans]
+  TraceRec* rec;              // [max(n,1)] or null (no per-trace outputs)
+  uint64_t* win_heads;        // [n_windows] head bitmap of each window
+  // slow path
+  TraceSlot* table;
+  uint64_t table_mask;
+  uint32_t* dup;              // set by the fast path when a trace_id spans several runs
+  const uint32_t* perm;       // kTracePerm: position -> span
+  const uint32_t* key;        // kTracePerm: span -> canonical trace (first run-head position)
+  uint32_t* error;            // bit0 spin timeout, bit2 trace table full
+};
+void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
+
+// Slow path (runs only when *dup != 0; every launch checks the flag first).
+struct TraceSortArgs {
+  uint64_t n_spans;
+  uint32_t n_tiles;           // ceil(n / kSortTile)
+  uint32_t shift;             // digit shift of this pass
+  const uint32_t* gate;       // == TraceKernelArgs::dup
+  const uint64_t* tid;
+  const TraceSlot* table;
+  uint64_t table_mask;
+  uint32_t epoch;
+  const uint32_t* keys_in;    // null on the first pass: keys_in = key, vals = identity
+  const uint32_t* vals_in;
+  uint32_t* keys_out;
+  uint32_t* vals_out;
+  uint32_t* hist;             // [256 * n_tiles] digit-major
+  uint32_t* key;              // canonical key per span (trace_key kernel output)
+  uint32_t* error;
+};
+constexpr uint32_t kSortTile = 4096;
+void launch_trace_key(const TraceSortArgs& a, hipStream_t st);
+void launch_sort_hist(const TraceSortArgs& a, hipStream_t st);
+void launch_sort_scatter(const TraceSortArgs& a, hipStream_t st);
+
+// Exclusive scan of u32 counts (or popcounts of u64 bitmaps) with the
+// decoupled look-back; *total receives the sum.  gate may be null.
+struct ScanArgs {
+  uint64_t n;
+  uint32_t n_tiles;           // ceil(n / kScanTileItems)
+  uint32_t popcount;          // 1: input is u64 bitmaps
+  const uint32_t* gate;
+  const void* in;
+  uint32_t* out;
+  uint32_t* total;            // may be null
+  uint32_t* counter;          // zeroed before launch
+  uint64_t* status;           // [n_tiles], zeroed before launch
+  uint32_t* error;
+};
+constexpr uint32_t kScanTileItems = 1024;
+void launch_scan_u32(const ScanArgs& a, hipStream_t st);
+
+// Dense per-trace outputs from the records (first-appearance order).
+struct TraceCompactArgs {
+  uint32_t n_windows;
+  const uint64_t* win_heads;
+  const uint32_t* win_base;
+  const TraceRec* rec;
+  uint32_t* trace_first_span;
+  uint8_t* trace_keep;
+  uint8_t* trace_level;
+  double* trace_ratio;
+};
+void launch_trace_compact(const TraceCompactArgs& a, hipStream_t st);
+
+}  // namespace ose

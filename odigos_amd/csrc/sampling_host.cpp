@@ -1,24 +1,347 @@
-// sampling_host.cpp — odigossampling rule tables (built once per engine).
+// sampling_host.cpp — odigossampling: rule tables (built once per engine)
+// and the launch sequence of the trace stage (trace_kernel.hip).
 #include <algorithm>
+#include <cstring>
 
+#include "devcfg.hpp"
 #include "engine_internal.hpp"
-#include "kernels.hpp"
 #include "host.hpp"
+#include "kernels.hpp"
 
 namespace ose {
 
+#define HIP_TRY(expr)                                                                                  \
+  do {                                                                                                 \
+    hipError_t _e = (expr);                                                                            \
+    if (_e != hipSuccess) return fail(OSE_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+uint64_t windows_of(uint64_t n) { return std::max<uint64_t>(1, (n + 63) / 64); }
+uint64_t table_slots(uint64_t n) {
+  uint64_t cap = 1024;
+  while (cap < 2 * n) cap <<= 1;
+  return cap;
+}
+}  // namespace
+
 // Interns every service name a rule compares against (latency.go:55,
 // servicename.go:40, spanattribute.go:130); the shim maps resources onto
-// these ids with ose_engine_service_id.
+// these ids with ose_engine_service_id.  Then lays out the device tables
+// (devcfg.hpp SampCfgDev): rules in level order global, service, endpoint
+// (rule_engine.go:56-60), config order within a level.
 int Engine::build_sampling_tables() {
   service_ids.clear();
   if (!has_sampling) return 0;
   for (auto& kv : intern_services(sampling)) service_ids.emplace(kv.first, kv.second);
+  const uint32_t nsvc = (uint32_t)service_ids.size();
+  std::vector<SampRuleDev> rules;
+  std::vector<SampLatDev> lat;
+  std::vector<uint32_t> svc_slot(std::max<uint32_t>(nsvc, 1), 0xFFFFFFFFu);
+  std::vector<uint64_t> slot_rules;
+  std::vector<uint64_t> svc_bits(std::max<uint32_t>(nsvc, 1), 0);
+  std::string bytes;
+  SampCfgDev h{};
+  uint32_t n_svc_rules = 0;
+  const std::vector<SamplingRule>* levels[3] = {&sampling.global_rules, &sampling.service_rules,
+                                                &sampling.endpoint_rules};
+  for (int L = 0; L < 3; L++) {
+    h.level_first[L] = (uint32_t)rules.size();
+    for (const SamplingRule& r : *levels[L]) {
+      SampRuleDev d{};
+      switch (r.rtype) {
+        case RuleType::Error:
+          d.type = kSampError;
+          d.fallback = r.error.fallback_sampling_ratio;
+          break;
+        case RuleType::HttpLatency: {
+          if (lat.size() >= kMaxLatencyRules)
+            return fail(OSE_ENOTSUP, "more than 64 http_latency rules are not supported by the GPU trace stage");
+          d.type = kSampLatency;
+          d.bit = (uint32_t)lat.size();
+          d.fallback = r.latency.fallback_sampling_ratio;
+          const uint32_t s = service_ids.at(r.latency.service_name);
+          if (svc_slot[s] == 0xFFFFFFFFu) {
+            svc_slot[s] = (uint32_t)slot_rules.size();
+            slot_rules.push_back(0);
+          }
+          SampLatDev ld{};
+          ld.slot = svc_slot[s];
+          ld.route_off = (uint32_t)bytes.size();
+          ld.route_len = (uint32_t)r.latency.http_route.size();
+          ld.threshold = r.latency.threshold;
+          bytes += r.latency.http_route;
+          slot_rules[ld.slot] |= 1ull << d.bit;
+          lat.push_back(ld);
+          break;
+        }
+        case RuleType::ServiceName: {
+          if (n_svc_rules >= kMaxServiceRules)
+            return fail(OSE_ENOTSUP, "more than 64 service_name rules are not supported by the GPU trace stage");
+          d.type = kSampService;
+          d.bit = n_svc_rules++;
+          d.ratio = r.service.sampling_ratio;
+          d.fallback = r.service.fallback_sampling_ratio;
+          svc_bits[service_ids.at(r.service.service_name)] |= 1ull << d.bit;
+          break;
+        }
+        case RuleType::SpanAttribute:
+          return fail(OSE_ENOTSUP,
+                      "span_attribute sampling rules are not supported by the GPU trace stage yet "
+                      "(internal/sampling/spanattribute.go; SURVEY.md §8f)");
+      }
+      rules.push_back(d);
+    }
+  }
+  h.level_first[3] = (uint32_t)rules.size();
+  h.n_rules = (uint32_t)rules.size();
+  h.n_lat = (uint32_t)lat.size();
+  h.n_lat_slots = (uint32_t)slot_rules.size();
+  h.n_services = nsvc;
+  if (slot_rules.empty()) slot_rules.push_back(0);
+  std::vector<uint8_t> b(sizeof(SampCfgDev), 0);
+  auto put = [&](const void* p, size_t nb) {
+    while (b.size() % 16) b.push_back(0);
+    uint32_t off = (uint32_t)b.size();
+    const uint8_t* s = static_cast<const uint8_t*>(p);
+    b.insert(b.end(), s, s + nb);
+    return off;
+  };
+  h.rules_off = put(rules.data(), rules.size() * sizeof(SampRuleDev));
+  h.lat_off = put(lat.data(), lat.size() * sizeof(SampLatDev));
+  h.svc_slot_off = put(svc_slot.data(), svc_slot.size() * 4);
+  h.slot_rules_off = put(slot_rules.data(), slot_rules.size() * 8);
+  h.svc_bits_off = put(svc_bits.data(), svc_bits.size() * 8);
+  h.bytes_off = put(bytes.data(), bytes.size());
+  while (b.size() % 16) b.push_back(0);
+  b.resize(b.size() + 16, 0);
+  h.total_bytes = (uint32_t)b.size();
+  std::memcpy(b.data(), &h, sizeof h);
+  sampling_blob_host = std::move(b);
+  sampling_n_lat = h.n_lat;
   return 0;
 }
 
+// Scratch of the trace stage for n spans (run_sampling layout).
+static size_t sampling_scratch_bytes(uint64_t n) {
+  const uint64_t W = windows_of(n);
+  const uint64_t N = std::max<uint64_t>(n, 1);
+  const uint64_t T = (N + kSortTile - 1) / kSortTile;
+  const uint64_t wtiles = (W + kScanTileItems - 1) / kScanTileItems;
+  const uint64_t htiles = (256 * T + kScanTileItems - 1) / kScanTileItems;
+  size_t s = 256;
+  s = align_up(s + 8 * W, 256);        // win_heads
+  s = align_up(s + 4 * W, 256);        // win_base
+  s = align_up(s + 8 * wtiles, 256);   // scan status (windows)
+  s = align_up(s + 16 * N, 256);       // rec
+  s = align_up(s + 4 * N, 256) * 1;    // key
+  s = align_up(s + 4 * N, 256);        // keys2
+  s = align_up(s + 4 * N, 256);        // vals
+  s = align_up(s + 4 * N, 256);        // keys3
+  s = align_up(s + 4 * N, 256);        // vals2
+  s = align_up(s + 4 * 256 * T, 256);  // hist
+  s = align_up(s + 4 * 256 * T, 256);  // hist offsets
+  s = align_up(s + 8 * htiles, 256);   // scan status (hist)
+  return s + 256;
+}
+
 size_t Engine::workspace_bytes(uint64_t n_spans) const {
-  return url_workspace_bytes(n_spans);
+  size_t s = url_workspace_bytes(n_spans);
+  if (has_sampling) s = std::max(s, sampling_scratch_bytes(n_spans));
+  return s;
+}
+
+int Workspace::reserve_table(uint64_t n_spans) {
+  const uint64_t slots = table_slots(n_spans);
+  if (slots <= table_slots_cap) return 0;
+  if (table) HIP_TRY(hipFree(table));
+  table = nullptr;
+  table_slots_cap = 0;
+  HIP_TRY(hipMalloc(&table, slots * sizeof(TraceSlot)));
+  HIP_TRY(hipMemset(table, 0, slots * sizeof(TraceSlot)));
+  table_slots_cap = slots;
+  epoch = 0;
+  return 0;
+}
+
+int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
+                 hipStream_t st, Workspace* ws) {
+  if (!e->has_sampling) return fail(OSE_EINVAL, "odigossampling is not configured on this engine");
+  if (group_mode != OSE_GROUP_TRACE_ID && group_mode != OSE_GROUP_BATCH) return fail(OSE_EINVAL, "unknown group_mode");
+  const uint64_t n = c->n_spans;
+  if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "SAMPLE stage: more than 2^32-16 spans in one batch");
+  const bool lat = e->sampling_n_lat > 0;
+  if (n > 0) {
+    if (!c->status || !c->resource || !c->res_svc || !c->res_svc_str || !o->keep)
+      return fail(OSE_EINVAL, "SAMPLE stage needs status, resource, res_svc, res_svc_str and keep");
+    if (!c->trace_id && (group_mode == OSE_GROUP_TRACE_ID || o->trace_keep || o->trace_level || o->trace_ratio))
+      return fail(OSE_EINVAL, "SAMPLE stage needs the trace_id column");
+    if (lat && (!c->start_ns || !c->end_ns || !c->route || !c->arena))
+      return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns, route and arena");
+  } else if (!c->res_svc_str && c->n_resources) {
+    return fail(OSE_EINVAL, "SAMPLE stage needs res_svc_str");
+  }
+  const bool per_trace = o->trace_count || o->trace_first_span || o->trace_keep || o->trace_level || o->trace_ratio;
+  if (group_mode == OSE_GROUP_TRACE_ID && n == 0) {
+    if (o->trace_count) HIP_TRY(hipMemsetAsync(o->trace_count, 0, 4, st));
+    return 0;
+  }
+  const uint64_t W = windows_of(n), N = std::max<uint64_t>(n, 1);
+  const uint64_t T = (N + kSortTile - 1) / kSortTile;
+  const uint32_t wtiles = (uint32_t)((W + kScanTileItems - 1) / kScanTileItems);
+  const uint32_t htiles = (uint32_t)((256 * T + kScanTileItems - 1) / kScanTileItems);
+  const size_t need = sampling_scratch_bytes(n);
+  int rc = ws->reserve(need);
+  if (rc) return rc;
+  if (group_mode == OSE_GROUP_TRACE_ID) {
+    rc = ws->reserve_table(n);
+    if (rc) return rc;
+    if (++ws->epoch >= (1u << 30)) {   // generation tags wrap: clear the table once
+      HIP_TRY(hipMemsetAsync(ws->table, 0, ws->table_slots_cap * sizeof(TraceSlot), st));
+      ws->epoch = 1;
+    }
+  }
+  uint8_t* base = static_cast<uint8_t*>(ws->dev);
+  size_t off = 256;
+  auto take = [&](size_t bytes) {
+    uint8_t* p = base + off;
+    off = align_up(off + bytes, 256);
+    return p;
+  };
+  uint32_t* misc = reinterpret_cast<uint32_t*>(base);   // [0] dup, [2] scan counter (windows), [4] scan counter (hist)
+  uint64_t* win_heads = reinterpret_cast<uint64_t*>(take(8 * W));
+  uint32_t* win_base = reinterpret_cast<uint32_t*>(take(4 * W));
+  uint64_t* wstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)wtiles));
+  TraceRec* rec = reinterpret_cast<TraceRec*>(take(16 * N));
+  uint32_t* key = reinterpret_cast<uint32_t*>(take(4 * N));
+  uint32_t* k2 = reinterpret_cast<uint32_t*>(take(4 * N));
+  uint32_t* v2 = reinterpret_cast<uint32_t*>(take(4 * N));
+  uint32_t* k3 = reinterpret_cast<uint32_t*>(take(4 * N));
+  uint32_t* v3 = reinterpret_cast<uint32_t*>(take(4 * N));
+  uint32_t* hist = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
+  uint32_t* hoff = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
+  uint64_t* hstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)htiles));
+  if (off > need) return fail(OSE_EINVAL, "internal: trace workspace layout exceeds its bound");
+  uint32_t* err = o->device_status ? o->device_status : misc + 8;
+  HIP_TRY(hipMemsetAsync(base, 0, 64, st));
+
+  TraceKernelArgs a{};
+  a.n_spans = n;
+  a.n_windows = (uint32_t)W;
+  a.mode = group_mode == OSE_GROUP_BATCH ? kTraceBatch : kTraceRuns;
+  a.n_resources = c->n_resources;
+  a.epoch = ws->epoch;
+  a.tid = c->trace_id;
+  a.start = c->start_ns;
+  a.end = c->end_ns;
+  a.status = c->status;
+  a.resource = c->resource;
+  a.route = c->route;
+  a.arena = c->arena;
+  a.res_svc = c->res_svc;
+  a.res_svc_str = c->res_svc_str;
+  a.cfg = e->sampling_blob_dev;
+  a.seed = rnd ? rnd->seed : 0;
+  a.keep = o->keep;
+  a.rec = per_trace ? rec : nullptr;
+  a.win_heads = win_heads;
+  a.table = static_cast<TraceSlot*>(ws->table);
+  a.table_mask = ws->table_slots_cap ? ws->table_slots_cap - 1 : 0;
+  a.dup = misc;
+  a.error = err;
+  Engine::Timed tm{};
+  e->prof_begin("trace_eval_kernel", st, tm);
+  launch_trace_eval(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+
+  if (group_mode == OSE_GROUP_TRACE_ID) {
+    // slow path: every launch returns at once unless the fast path set *dup
+    TraceSortArgs s{};
+    s.n_spans = n;
+    s.n_tiles = (uint32_t)T;
+    s.gate = misc;
+    s.tid = c->trace_id;
+    s.table = a.table;
+    s.table_mask = a.table_mask;
+    s.epoch = a.epoch;
+    s.key = key;
+    s.error = err;
+    launch_trace_key(s, st);
+    HIP_TRY(hipGetLastError());
+    int bits = 1;
+    while (bits < 32 && (n - 1) >> bits) bits++;
+    const uint32_t* kin = nullptr;
+    const uint32_t* vin = nullptr;
+    uint32_t* kbuf[2] = {k2, k3};
+    uint32_t* vbuf[2] = {v2, v3};
+    int pass = 0;
+    for (int shift = 0; shift < bits; shift += 8, pass++) {
+      s.shift = (uint32_t)shift;
+      s.keys_in = kin;
+      s.vals_in = vin;
+      s.keys_out = kbuf[pass & 1];
+      s.vals_out = vbuf[pass & 1];
+      s.hist = hist;
+      launch_sort_hist(s, st);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemsetAsync(misc + 4, 0, 4, st));
+      HIP_TRY(hipMemsetAsync(hstatus, 0, 8 * (size_t)htiles, st));
+      ScanArgs sa{};
+      sa.n = 256 * T;
+      sa.n_tiles = htiles;
+      sa.popcount = 0;
+      sa.gate = misc;
+      sa.in = hist;
+      sa.out = hoff;
+      sa.counter = misc + 4;
+      sa.status = hstatus;
+      sa.error = err;
+      launch_scan_u32(sa, st);
+      HIP_TRY(hipGetLastError());
+      TraceSortArgs s2 = s;
+      s2.hist = hoff;
+      launch_sort_scatter(s2, st);
+      HIP_TRY(hipGetLastError());
+      kin = kbuf[pass & 1];
+      vin = vbuf[pass & 1];
+    }
+    TraceKernelArgs b = a;
+    b.mode = kTracePerm;
+    b.perm = vin;
+    b.key = key;
+    launch_trace_eval(b, st);
+    HIP_TRY(hipGetLastError());
+  }
+
+  if (per_trace) {
+    HIP_TRY(hipMemsetAsync(wstatus, 0, 8 * (size_t)wtiles, st));
+    ScanArgs sa{};
+    sa.n = W;
+    sa.n_tiles = wtiles;
+    sa.popcount = 1;
+    sa.in = win_heads;
+    sa.out = win_base;
+    sa.total = o->trace_count;
+    sa.counter = misc + 2;
+    sa.status = wstatus;
+    sa.error = err;
+    launch_scan_u32(sa, st);
+    HIP_TRY(hipGetLastError());
+    TraceCompactArgs ca{};
+    ca.n_windows = (uint32_t)W;
+    ca.win_heads = win_heads;
+    ca.win_base = win_base;
+    ca.rec = rec;
+    ca.trace_first_span = o->trace_first_span;
+    ca.trace_keep = o->trace_keep;
+    ca.trace_level = o->trace_level;
+    ca.trace_ratio = o->trace_ratio;
+    launch_trace_compact(ca, st);
+    HIP_TRY(hipGetLastError());
+  }
+  return 0;
 }
 
 }  // namespace ose

@@ -1,0 +1,696 @@
+// trace_kernel.hip — odigossampling on CDNA4 (gfx950).
+//
+// Replaces RuleEngine.ShouldSample over every trace of a batch
+// (odigossamplingprocessor/rule_engine.go:55-115 with the Evaluate functions
+// of internal/sampling/{error,latency,servicename}.go), grouped by trace_id
+// as groupbytrace would release them (sampling_controller.go:193-220).
+//
+// Fast path (one launch): positions are batch order.  A run is a maximal
+// stretch of consecutive spans with one trace_id; when every trace_id forms
+// exactly one run (groupbytrace release order) each run is a trace.  One
+// wave owns the runs whose head lies in its 64-span window and walks them in
+// 64-span steps: per-span contributions (error bit, endpoint-match bits of
+// the latency rules of the span's service, service-rule bits) are combined
+// by wave-segmented scans (shuffles, no LDS), the latency state (min start
+// with the Go sentinel quirk, max end) by a segmented scan of the monoid
+// below, once per distinct latency service present in the step.  A run that
+// continues past the step is carried in wave-uniform registers plus one lane
+// per latency service.  Every run head also inserts its trace_id into an
+// exact hash table; a trace_id found twice sets *dup.
+//
+// Slow path (only when *dup; every launch checks the flag first): key every
+// span by its trace's first run-head position (table lookup), stable LSD
+// radix sort of the spans by that key, then the same evaluation kernel over
+// the sorted positions, which makes every trace one run in batch order.
+//
+// Latency monoid (latency.go:69-80): minStart is replaced when it is 0 or the
+// new start is smaller, so a span with start 0 resets it.  Element
+// (f, m, e): f bit0 = contains a zero start, bit1 = contains a span of the
+// service; m = min start after the last zero start (+inf if none); e = max
+// end.  later∘earlier = {f_a|f_b, b.reset ? b.m : min(a.m, b.m), max}.  The
+// final minStart is m, or 0 when m = +inf.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "devcfg.hpp"
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+namespace ose {
+namespace {
+
+constexpr int kTWaves = 4;
+constexpr int kTThreads = kTWaves * kWave;
+constexpr uint64_t kInf = ~0ull;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t tid_hash(uint64_t hi, uint64_t lo) { return splitmix64(hi ^ splitmix64(lo)); }
+
+// include/odigos_amd.h "injected randomness"
+__device__ __forceinline__ double trace_uniform(uint64_t hi, uint64_t lo, uint64_t seed) {
+  const uint64_t x = hi ^ ((lo << 29) | (lo >> 35)) ^ seed;
+  return (double)(splitmix64(x) >> 11) * 0x1.0p-53;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1; }
+__device__ __forceinline__ uint64_t lanemask_le(int lane) { return lane == 63 ? ~0ull : ((2ull << lane) - 1); }
+__device__ __forceinline__ int ffs64(uint64_t x) { return __ffsll((unsigned long long)x) - 1; }
+__device__ __forceinline__ int fls64(uint64_t x) { return 63 - __clzll((long long)x); }
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
+  return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
+}
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, kWave);
+  return v;
+}
+
+struct Cfg {
+  const SampCfgDev* h;
+  const SampRuleDev* rules;
+  const SampLatDev* lat;
+  const uint32_t* svc_slot;
+  const uint64_t* slot_rules;
+  const uint64_t* svc_bits;
+  const uint8_t* bytes;
+};
+__device__ __forceinline__ Cfg load_cfg(const uint8_t* b) {
+  Cfg c;
+  c.h = reinterpret_cast<const SampCfgDev*>(b);
+  c.rules = reinterpret_cast<const SampRuleDev*>(b + c.h->rules_off);
+  c.lat = reinterpret_cast<const SampLatDev*>(b + c.h->lat_off);
+  c.svc_slot = reinterpret_cast<const uint32_t*>(b + c.h->svc_slot_off);
+  c.slot_rules = reinterpret_cast<const uint64_t*>(b + c.h->slot_rules_off);
+  c.svc_bits = reinterpret_cast<const uint64_t*>(b + c.h->svc_bits_off);
+  c.bytes = b + c.h->bytes_off;
+  return c;
+}
+
+struct Lat {
+  uint32_t f;
+  uint64_t m, e;
+};
+__device__ __forceinline__ Lat lat_comb(const Lat& a, const Lat& b) {   // a earlier, b later
+  Lat r;
+  r.f = a.f | b.f;
+  r.m = (b.f & 1u) ? b.m : (a.m < b.m ? a.m : b.m);
+  r.e = a.e > b.e ? a.e : b.e;
+  return r;
+}
+
+// strings.HasPrefix(route, rule.HttpRoute) (latency.go:97-100)
+__device__ __forceinline__ bool route_has_prefix(const uint8_t* arena, ose_strref r, const uint8_t* pre, uint32_t n) {
+  if (r.len < n) return false;
+  const uint8_t* s = arena + r.off;
+  for (uint32_t k = 0; k < n; k++)
+    if (s[k] != pre[k]) return false;
+  return true;
+}
+
+// Latency rules of `slot` that matched (endpoint found) and whose duration
+// reaches the threshold.  Duration: maxEnd.AsTime().Sub(minStart.AsTime())
+// .Milliseconds() — int64 ns difference saturated like time.Sub, truncated.
+__device__ __forceinline__ uint64_t latency_satisfied(const Cfg& c, uint32_t slot, uint64_t ep, uint64_t m, uint64_t e) {
+  uint64_t rules = c.slot_rules[slot] & ep;
+  if (!rules) return 0;
+  const int64_t t = (int64_t)e, u = (int64_t)(m == kInf ? 0 : m);
+  int64_t d;
+  if (__builtin_sub_overflow(t, u, &d)) d = t < u ? INT64_MIN : INT64_MAX;
+  const int64_t ms = d / 1000000;
+  uint64_t sat = 0;
+  while (rules) {
+    const int r = ffs64(rules);
+    rules &= rules - 1;
+    if (ms >= c.lat[r].threshold) sat |= 1ull << r;
+  }
+  return sat;
+}
+
+// ShouldSample's level walk (rule_engine.go:55-83) over evaluateLevel's fold
+// (rule_engine.go:89-115).  level: 0..2 satisfied level, 3 min fallback, 4 none.
+__device__ inline void decide(const Cfg& c, uint32_t err, uint64_t ep, uint64_t lsat, uint64_t svc, double u,
+                              uint8_t& keep, uint8_t& level, double& ratio_out) {
+  bool have_min = false;
+  double min_fb = 0;
+  for (int L = 0; L < 3; L++) {
+    double ratio = 0;
+    bool sat = false, matched = false, found_fb = false;
+    for (uint32_t k = c.h->level_first[L]; k < c.h->level_first[L + 1]; k++) {
+      const SampRuleDev& r = c.rules[k];
+      bool mt, st;
+      double p;
+      if (r.type == kSampError) {            // error.go:29-44
+        mt = true;
+        st = err != 0;
+        p = st ? 100.0 : r.fallback;
+      } else if (r.type == kSampLatency) {   // latency.go:84-95
+        mt = (ep >> r.bit) & 1;
+        st = mt && ((lsat >> r.bit) & 1);
+        p = st ? 100.0 : (mt ? r.fallback : 0.0);
+      } else {                               // servicename.go:35-51
+        mt = st = (svc >> r.bit) & 1;
+        p = st ? r.ratio : r.fallback;
+      }
+      if (st) {
+        sat = true;
+        ratio = ratio > p ? ratio : p;
+        matched = true;
+      } else if (mt) {
+        matched = true;
+        if (!found_fb) {
+          ratio = p;
+          found_fb = true;
+        } else {
+          ratio = ratio < p ? ratio : p;
+        }
+      }
+    }
+    if (sat) {
+      level = (uint8_t)L;
+      ratio_out = ratio;
+      keep = u * 100 < ratio;
+      return;
+    }
+    if (matched && (!have_min || ratio < min_fb)) {
+      min_fb = ratio;
+      have_min = true;
+    }
+  }
+  if (have_min) {
+    level = 3;
+    ratio_out = min_fb;
+    keep = u * 100 < min_fb;
+  } else {
+    level = 4;
+    ratio_out = 100.0;
+    keep = 1;
+  }
+}
+
+// ---- exact trace_id table -------------------------------------------------
+// Insert protocol: CAS the state from a stale epoch to BUSY, store the key
+// with sc1 (agent-scope relaxed) stores, drain them (s_waitcnt vmcnt(0)), then
+// store READY; readers poll the state and read the key with sc1 loads
+// (MI355X_MICROARCH.md "Valid forms": sc1 payload + drained flag).  A lane
+// that finds the key ready and equal is a second run of that trace_id.
+__device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint64_t lo, uint32_t pos) {
+  const uint32_t busy = (a.epoch << 2) | 1u, ready = (a.epoch << 2) | 2u;
+  uint64_t h = tid_hash(hi, lo) & a.table_mask;
+  uint32_t probes = 0, spins = 0;
+  for (;;) {
+    TraceSlot* s = &a.table[h];
+    const uint32_t st = __hip_atomic_load(&s->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((st >> 2) != a.epoch) {
+      uint32_t expect = st;
+      if (__hip_atomic_compare_exchange_strong(&s->state, &expect, busy, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(&s->hi, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->lo, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->first, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&s->state, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      continue;   // lost the race for this slot: look at it again
+    }
+    if ((st & 3u) != 2u) {   // another lane is publishing this slot
+      if (++spins > (1u << 20)) {
+        atomicOr(a.error, 1u);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const uint64_t h2 = __hip_atomic_load(&s->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t l2 = __hip_atomic_load(&s->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (h2 == hi && l2 == lo) {
+      atomicMin(&s->first, pos);
+      atomicOr(a.dup, 1u);
+      return;
+    }
+    h = (h + 1) & a.table_mask;
+    if (++probes > a.table_mask) {
+      atomicOr(a.error, 4u);
+      return;
+    }
+  }
+}
+
+// Head of a run: position p starts a new trace in the evaluation order.
+struct StepCols {
+  bool valid;
+  uint64_t i;          // span index
+  uint64_t hi, lo;     // trace id (kTraceRuns / kTraceBatch)
+  bool head;
+};
+__device__ __forceinline__ StepCols load_step(const TraceKernelArgs& a, uint64_t base, int lane) {
+  StepCols s;
+  const uint64_t p = base + lane;
+  s.valid = p < a.n_spans;
+  s.i = 0;
+  s.hi = s.lo = 0;
+  s.head = false;
+  uint64_t ph = 0, pl = 0;
+  if (a.mode == kTracePerm) {
+    uint32_t k = 0;
+    if (s.valid) {
+      s.i = a.perm[p];
+      k = a.key[s.i];
+      s.hi = a.tid[2 * s.i];
+      s.lo = a.tid[2 * s.i + 1];
+    }
+    uint32_t pk = __shfl_up(k, 1, kWave);
+    if (lane == 0 && s.valid && p > 0) pk = a.key[a.perm[p - 1]];
+    s.head = s.valid && (p == 0 || pk != k);
+    return s;
+  }
+  s.i = p;
+  if (s.valid) {
+    const uint4 v = reinterpret_cast<const uint4*>(a.tid)[p];
+    s.hi = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    s.lo = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
+  if (a.mode == kTraceBatch) {
+    s.head = s.valid && p == 0;
+    return s;
+  }
+  ph = __shfl_up(s.hi, 1, kWave);
+  pl = __shfl_up(s.lo, 1, kWave);
+  if (lane == 0 && s.valid && p > 0) {
+    ph = a.tid[2 * p - 2];
+    pl = a.tid[2 * p - 1];
+  }
+  s.head = s.valid && (p == 0 || ph != s.hi || pl != s.lo);
+  return s;
+}
+__device__ __forceinline__ bool head_at(const TraceKernelArgs& a, uint64_t p) {   // p < n, p > 0
+  if (a.mode == kTraceBatch) return false;
+  if (a.mode == kTracePerm) return a.key[a.perm[p]] != a.key[a.perm[p - 1]];
+  return a.tid[2 * p] != a.tid[2 * p - 2] || a.tid[2 * p + 1] != a.tid[2 * p - 1];
+}
+
+__device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos, uint8_t keep, uint8_t level,
+                                          double ratio) {
+  if (!a.rec) return;
+  TraceRec r;
+  r.first_span = a.mode == kTracePerm ? a.perm[pos] : (uint32_t)pos;
+  r.keep = keep;
+  r.level = level;
+  r._p0 = r._p1 = 0;
+  r.ratio = ratio;
+  a.rec[pos] = r;
+}
+
+__global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a) {
+  if (a.mode == kTracePerm && __hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t w = blockIdx.x * kTWaves + (threadIdx.x >> 6);
+  if (w >= a.n_windows) return;
+  const Cfg c = load_cfg(a.cfg);
+  const uint64_t n = a.n_spans;
+  const uint32_t nsvc = c.h->n_services;
+
+  // OSE_GROUP_BATCH: ServiceNameRule looks at every resource of the call,
+  // spanless ones included (servicename.go:38-47).
+  uint64_t batch_svc = 0;
+  if (a.mode == kTraceBatch && w == 0) {
+    for (uint32_t r = lane; r < a.n_resources; r += kWave) {
+      const uint32_t s = a.res_svc_str[r];
+      if (s < nsvc) batch_svc |= c.svc_bits[s];
+    }
+    batch_svc = wave_or64(batch_svc);
+  }
+  if (n == 0) {   // kTraceBatch only: one trace with no spans
+    if (w == 0) {
+      uint8_t k, l;
+      double r;
+      decide(c, 0, 0, 0, batch_svc, trace_uniform(0, 0, a.seed), k, l, r);
+      if (lane == 0) {
+        if (a.win_heads) a.win_heads[0] = 1;
+        if (a.rec) {
+          TraceRec rr{0, k, l, 0, 0, r};
+          a.rec[0] = rr;
+        }
+      }
+    }
+    return;
+  }
+
+  const uint64_t p0 = (uint64_t)w * kWave;
+  StepCols sc = load_step(a, p0, lane);
+  const uint64_t heads0 = __ballot(sc.head);
+  if (lane == 0 && a.win_heads) a.win_heads[w] = heads0;
+  if (!heads0) return;
+  if (a.mode == kTraceRuns && sc.head) table_insert(a, sc.hi, sc.lo, (uint32_t)(p0 + lane));
+
+  // carried (open) trace: wave-uniform masks + one lane per latency slot
+  bool open = false;
+  uint32_t c_err = 0;
+  uint64_t c_ep = 0, c_svc = 0, c_kmask = 0, c_pos = 0, c_hi = 0, c_lo = 0;
+  Lat cur{0, kInf, 0};
+  uint64_t base = p0;
+  const int own_from = ffs64(heads0);
+  for (;;) {
+    if (base != p0) sc = load_step(a, base, lane);
+    const uint64_t vmask = __ballot(sc.valid);
+    const uint64_t hmask = __ballot(sc.head);
+    uint64_t own;
+    if (base == p0) own = vmask & ~lanemask_lt(own_from);
+    else own = vmask & (hmask ? lanemask_lt(ffs64(hmask)) : ~0ull);
+    if (!own) break;
+    const uint64_t segmask = (hmask & own) | (open ? 1ull : 0ull);
+    const int last_own = fls64(own);
+    bool cont_next = false;
+    if (last_own == 63 && base + kWave < n) {
+      bool h = false;
+      if (lane == 63) h = head_at(a, base + kWave);
+      cont_next = !rdl((uint32_t)h, 63);
+    }
+    const bool mine = (own >> lane) & 1;
+    const int sst = mine ? fls64(segmask & lanemask_le(lane)) : lane;
+    const bool tail = mine && (lane == last_own || ((segmask >> (lane + 1)) & 1));
+    const uint64_t tails = __ballot(tail);
+    const int t0 = ffs64(tails);
+    const bool seg0_cont = open;
+    const bool single = t0 == last_own;
+    const bool last_open = cont_next && !(single && seg0_cont);   // a new trace opens in this step and continues
+    const int sst_last = rdl((uint32_t)sst, last_own);
+
+    // ---- per-span contributions ----
+    uint32_t err = 0, slot = kNoSlot;
+    uint64_t ep = 0, svcb = 0, st = 0, en = 0;
+    if (mine) {
+      const uint64_t i = sc.i;
+      const uint32_t r = a.resource[i];
+      const uint32_t s = a.res_svc[r], ss = a.res_svc_str[r];
+      err = a.status[i] == OSE_STATUS_ERROR;
+      if (a.mode != kTraceBatch && ss < nsvc) svcb = c.svc_bits[ss];
+      if (s < nsvc) {
+        slot = c.svc_slot[s];
+        if (slot != kNoSlot) {
+          uint64_t rules = c.slot_rules[slot];
+          const ose_strref rt = a.route[i];
+          while (rules) {
+            const int k = ffs64(rules);
+            rules &= rules - 1;
+            const SampLatDev& L = c.lat[k];
+            if (route_has_prefix(a.arena, rt, c.bytes + L.route_off, L.route_len)) ep |= 1ull << k;
+          }
+          st = a.start[i];
+          en = a.end[i];
+        }
+      }
+    }
+    // ---- segmented OR of the flag masks ----
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t oe = __shfl_up(err, d, kWave);
+      const uint64_t oep = __shfl_up(ep, d, kWave), osv = __shfl_up(svcb, d, kWave);
+      if (lane >= d && lane - d >= sst) {
+        err |= oe;
+        ep |= oep;
+        svcb |= osv;
+      }
+    }
+    // ---- latency state, one segmented scan per latency slot present ----
+    uint64_t lsat = 0, n_kmask = 0;
+    Lat nxt{0, kInf, 0};
+    const bool carried_tail = (lane == t0 && seg0_cont) || (lane == last_own && last_open);
+    const uint64_t ep0 = rdl64(ep, t0), epl = rdl64(ep, last_own);
+    uint64_t pend = __ballot(slot != kNoSlot);
+    while (pend) {
+      const uint32_t ks = rdl(slot, ffs64(pend));
+      const bool ink = slot == ks;
+      pend &= ~__ballot(ink);
+      Lat v = ink ? Lat{st == 0 ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        Lat o;
+        o.f = __shfl_up(v.f, d, kWave);
+        o.m = __shfl_up(v.m, d, kWave);
+        o.e = __shfl_up(v.e, d, kWave);
+        if (lane >= d && lane - d >= sst) v = lat_comb(o, v);
+      }
+      if (tail && !carried_tail && (v.f & 2u)) lsat |= latency_satisfied(c, ks, ep, v.m, v.e);
+      if (seg0_cont) {
+        const uint32_t f0 = rdl(v.f, t0);
+        if (f0 & 2u) {
+          const Lat v0{f0, rdl64(v.m, t0), rdl64(v.e, t0)};
+          if ((uint32_t)lane == ks) cur = lat_comb(cur, v0);
+          c_kmask |= 1ull << ks;
+        }
+      }
+      if (last_open) {
+        const uint32_t fl = rdl(v.f, last_own);
+        if (fl & 2u) {
+          if ((uint32_t)lane == ks) nxt = Lat{fl, rdl64(v.m, last_own), rdl64(v.e, last_own)};
+          n_kmask |= 1ull << ks;
+        }
+      }
+    }
+    (void)ep0;
+    (void)epl;
+    // ---- decisions of the traces that start and end in this step ----
+    uint8_t dk = 0, dl = 0;
+    double dr = 0;
+    const uint64_t hh = __shfl(sc.hi, sst, kWave), hl = __shfl(sc.lo, sst, kWave);
+    if (tail && !carried_tail) {
+      decide(c, err, ep, lsat, a.mode == kTraceBatch ? batch_svc : svcb, trace_uniform(hh, hl, a.seed), dk, dl, dr);
+      write_rec(a, base + sst, dk, dl, dr);
+    }
+    // ---- the carried trace closes in this step ----
+    const bool cont_close = seg0_cont && !(single && cont_next);
+    uint8_t cdk = 0;
+    if (cont_close) {
+      const uint32_t E = c_err | rdl(err, t0);
+      const uint64_t EP = c_ep | rdl64(ep, t0);
+      const uint64_t SV = a.mode == kTraceBatch ? batch_svc : (c_svc | rdl64(svcb, t0));
+      uint64_t s_l = 0;
+      if ((c_kmask >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, cur.m, cur.e);
+      s_l = wave_or64(s_l);
+      uint8_t cdl;
+      double cdr;
+      decide(c, E, EP, s_l, SV, trace_uniform(c_hi, c_lo, a.seed), cdk, cdl, cdr);
+      for (uint64_t q = c_pos + lane; q < base; q += kWave) a.keep[a.mode == kTracePerm ? a.perm[q] : q] = cdk;
+      if (lane == 0) write_rec(a, c_pos, cdk, cdl, cdr);
+      open = false;
+      cur = Lat{0, kInf, 0};
+      c_kmask = 0;
+    }
+    // ---- keep bytes of this step's spans ----
+    const int my_tail = mine ? ffs64(tails & ~lanemask_lt(lane)) : lane;
+    const uint8_t kd = (uint8_t)__shfl((uint32_t)dk, my_tail, kWave);
+    if (mine) {
+      const bool in_seg0c = seg0_cont && lane <= t0;
+      const bool in_lastopen = last_open && lane >= sst_last;
+      if (in_seg0c) {
+        if (cont_close) a.keep[sc.i] = cdk;
+      } else if (!in_lastopen) {
+        a.keep[sc.i] = kd;
+      }
+    }
+    // ---- carry into the next step ----
+    if (last_open) {
+      open = true;
+      c_pos = base + sst_last;
+      c_hi = rdl64(sc.hi, sst_last);
+      c_lo = rdl64(sc.lo, sst_last);
+      c_err = rdl(err, last_own);
+      c_ep = rdl64(ep, last_own);
+      c_svc = rdl64(svcb, last_own);
+      cur = nxt;
+      c_kmask = n_kmask;
+    } else if (seg0_cont && single && cont_next) {
+      c_err |= rdl(err, t0);
+      c_ep |= rdl64(ep, t0);
+      c_svc |= rdl64(svcb, t0);
+    }
+    if (!open) break;
+    base += kWave;
+  }
+}
+
+// ---- slow path ---------------------------------------------------------------
+__device__ __forceinline__ bool gated(const uint32_t* g) {
+  return g && __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+}
+
+// key[i] = first run-head position of span i's trace_id (read-only probe of
+// the table the fast path filled).
+__global__ __launch_bounds__(256) void trace_key_kernel(TraceSortArgs a) {
+  if (gated(a.gate)) return;
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n_spans) return;
+  const uint64_t hi = a.tid[2 * i], lo = a.tid[2 * i + 1];
+  const uint32_t ready = (a.epoch << 2) | 2u;
+  uint64_t h = tid_hash(hi, lo) & a.table_mask;
+  for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
+    const TraceSlot& s = a.table[h];
+    if (s.state == ready && s.hi == hi && s.lo == lo) {
+      a.key[i] = s.first;
+      return;
+    }
+    if ((s.state >> 2) != a.epoch) break;
+    h = (h + 1) & a.table_mask;
+  }
+  atomicOr(a.error, 4u);
+  a.key[i] = 0;
+}
+
+constexpr int kSortThreads = 256;
+constexpr int kSortRounds = kSortTile / kSortThreads;
+
+__global__ __launch_bounds__(kSortThreads) void sort_hist_kernel(TraceSortArgs a) {
+  if (gated(a.gate)) return;
+  __shared__ uint32_t hist[256];
+  const int t = threadIdx.x;
+  hist[t] = 0;
+  __syncthreads();
+  const uint32_t* keys = a.keys_in ? a.keys_in : a.key;
+  const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
+  for (int r = 0; r < kSortRounds; r++) {
+    const uint64_t j = b + (uint64_t)r * kSortThreads + t;
+    if (j < a.n_spans) atomicAdd(&hist[(keys[j] >> a.shift) & 255u], 1u);
+  }
+  __syncthreads();
+  a.hist[(uint64_t)t * a.n_tiles + blockIdx.x] = hist[t];
+}
+
+// Stable scatter: items keep tile order (round-major, lane order inside a
+// wave); ranks among equal digits come from per-wave match masks (8 ballots)
+// and per-round wave offsets in LDS.
+__global__ __launch_bounds__(kSortThreads) void sort_scatter_kernel(TraceSortArgs a) {
+  if (gated(a.gate)) return;
+  __shared__ uint32_t goff[256], run[256];
+  __shared__ uint32_t wcnt[kSortThreads / kWave][256], woff[kSortThreads / kWave][256];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  goff[t] = a.hist[(uint64_t)t * a.n_tiles + blockIdx.x];
+  run[t] = 0;
+  for (int k = 0; k < kSortThreads / kWave; k++) wcnt[k][t] = 0;
+  __syncthreads();
+  const uint32_t* keys = a.keys_in ? a.keys_in : a.key;
+  const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
+  for (int r = 0; r < kSortRounds; r++) {
+    const uint64_t j = b + (uint64_t)r * kSortThreads + t;
+    const bool valid = j < a.n_spans;
+    const uint32_t k = valid ? keys[j] : 0;
+    const uint32_t v = valid ? (a.vals_in ? a.vals_in[j] : (uint32_t)j) : 0;
+    const uint32_t d = (k >> a.shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; bit++) {
+      const uint64_t bal = __ballot((d >> bit) & 1u);
+      peers &= ((d >> bit) & 1u) ? bal : ~bal;
+    }
+    const uint32_t rank = __popcll(peers & lanemask_lt(lane));
+    const uint32_t cnt = __popcll(peers);
+    if (valid && rank == cnt - 1) wcnt[wv][d] = cnt;
+    __syncthreads();
+    {
+      uint32_t acc = run[t];
+      for (int k2 = 0; k2 < kSortThreads / kWave; k2++) {
+        woff[k2][t] = acc;
+        acc += wcnt[k2][t];
+        wcnt[k2][t] = 0;
+      }
+      run[t] = acc;
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t pos = goff[d] + woff[wv][d] + rank;
+      a.keys_out[pos] = k;
+      a.vals_out[pos] = v;
+    }
+  }
+}
+
+// ---- exclusive scan of u32 counts --------------------------------------------
+__global__ __launch_bounds__(kScanTileItems) void scan_u32_kernel(ScanArgs a) {
+  if (gated(a.gate)) return;
+  __shared__ uint64_t wsum[kScanTileItems / kWave];
+  __shared__ uint64_t prefix;
+  __shared__ uint32_t tile_s;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) tile_s = atomicAdd(a.counter, 1u);
+  __syncthreads();
+  const uint32_t tile = tile_s;
+  const uint64_t k = (uint64_t)tile * kScanTileItems + t;
+  uint64_t v = 0;
+  if (k < a.n)
+    v = a.popcount ? (uint64_t)__popcll(static_cast<const uint64_t*>(a.in)[k]) : static_cast<const uint32_t*>(a.in)[k];
+  uint64_t incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint64_t x = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += x;
+  }
+  if (lane == kWave - 1) wsum[wv] = incl;
+  __syncthreads();
+  uint64_t wbase = 0, total = 0;
+#pragma unroll
+  for (int q = 0; q < kScanTileItems / kWave; q++) {
+    const uint64_t x = wsum[q];
+    if (q < wv) wbase += x;
+    total += x;
+  }
+  if (wv == 0) {
+    const uint64_t pfx = lookback_prefix(a.status, tile, total, a.error);
+    if (lane == 0) {
+      prefix = pfx;
+      if (tile == a.n_tiles - 1 && a.total) *a.total = (uint32_t)(pfx + total);
+    }
+  }
+  __syncthreads();
+  if (k < a.n) a.out[k] = (uint32_t)(prefix + wbase + incl - v);
+}
+
+// ---- dense per-trace outputs ---------------------------------------------------
+__global__ __launch_bounds__(kTThreads) void trace_compact_kernel(TraceCompactArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t w = blockIdx.x * kTWaves + (threadIdx.x >> 6);
+  if (w >= a.n_windows) return;
+  const uint64_t heads = a.win_heads[w];
+  if (!((heads >> lane) & 1)) return;
+  const uint32_t t = a.win_base[w] + __popcll(heads & lanemask_lt(lane));
+  const TraceRec r = a.rec[(uint64_t)w * kWave + lane];
+  if (a.trace_first_span) a.trace_first_span[t] = r.first_span;
+  if (a.trace_keep) a.trace_keep[t] = r.keep;
+  if (a.trace_level) a.trace_level[t] = r.level;
+  if (a.trace_ratio) a.trace_ratio[t] = r.ratio;
+}
+
+}  // namespace
+
+void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
+  const uint32_t blocks = (a.n_windows + kTWaves - 1) / kTWaves;
+  hipLaunchKernelGGL(trace_eval_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
+}
+void launch_trace_key(const TraceSortArgs& a, hipStream_t st) {
+  const uint64_t blocks = (a.n_spans + 255) / 256;
+  hipLaunchKernelGGL(trace_key_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+}
+void launch_sort_hist(const TraceSortArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(sort_hist_kernel, dim3(a.n_tiles), dim3(kSortThreads), 0, st, a);
+}
+void launch_sort_scatter(const TraceSortArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(a.n_tiles), dim3(kSortThreads), 0, st, a);
+}
+void launch_scan_u32(const ScanArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(scan_u32_kernel, dim3(a.n_tiles), dim3(kScanTileItems), 0, st, a);
+}
+void launch_trace_compact(const TraceCompactArgs& a, hipStream_t st) {
+  const uint32_t blocks = (a.n_windows + kTWaves - 1) / kTWaves;
+  hipLaunchKernelGGL(trace_compact_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
+}
+
+}  // namespace ose

@@ -59,15 +59,35 @@ int orc_url_process(const orc_url* u, const ose_columns* c, ose_outputs* o,
                     int nthreads);
 
 /* ---- odigossampling ------------------------------------------------------ */
+/* One rule of the decoded config (odigossamplingprocessor/config.go:28-32
+ * after decodeAndValidate).  svc is the interned id of the rule's service
+ * name in first-appearance order over global, service, endpoint rules (the
+ * id the shim writes into res_svc / res_svc_str). */
+#define ORC_RULE_ERROR    0
+#define ORC_RULE_LATENCY  1
+#define ORC_RULE_SERVICE  2
+typedef struct orc_rule {
+  int32_t level;        /* 0 global, 1 service, 2 endpoint (rule_engine.go:56-60) */
+  int32_t type;         /* ORC_RULE_* */
+  uint32_t svc;         /* http_latency / service_name */
+  uint32_t route_len;   /* http_latency http_route */
+  const char* route;
+  int64_t threshold;    /* http_latency threshold (ms) */
+  double ratio;         /* service_name sampling_ratio */
+  double fallback;      /* fallback_sampling_ratio */
+} orc_rule;
 typedef struct orc_sampling orc_sampling;
-/* cfg_json: the "odigossampling" config object (global_rules, service_rules,
- * endpoint_rules); services[] gives the interned id order used for res_svc. */
-orc_sampling* orc_sampling_create(const char* cfg_json, char* err, size_t errcap);
+orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules);
 void orc_sampling_free(orc_sampling* s);
-/* interned id of a rule service name (same contract as ose_engine_service_id) */
-uint32_t orc_sampling_service_id(const orc_sampling* s, const char* name, size_t len);
+/* RuleEngine.ShouldSample per trace (rule_engine.go:55-115 and the four
+ * Evaluate functions), grouping spans by trace_id in first-appearance order
+ * (OSE_GROUP_TRACE_ID) or treating the batch as one trace (OSE_GROUP_BATCH);
+ * fills keep, trace_* and trace_count.  rand.Float64() is the injected
+ * uniform of include/odigos_amd.h. */
 int orc_sampling_process(const orc_sampling* s, const ose_columns* c, ose_outputs* o,
                          uint32_t group_mode, const ose_rand* rnd, int nthreads);
+/* the injected uniform for a trace whose first span has trace id {hi, lo} */
+double orc_trace_uniform(uint64_t hi, uint64_t lo, uint64_t seed);
 
 /* ---- odigostrafficmetrics -------------------------------------------------- */
 /* Adds ResourceSpansSize(after mutation) * inverse per attribute set and the

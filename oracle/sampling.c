@@ -1,0 +1,302 @@
+/*
+ * sampling.c — CPU restatement of odigossamplingprocessor.  TEST
+ * INFRASTRUCTURE (see oracle.h): the checker for the HIP trace stage and the
+ * timed CPU baseline, never part of the product.
+ *
+ * Restates (paths under collector/processors/odigossamplingprocessor/):
+ *   processor.go:16-25            processTraces / removeAllSpans (keep column)
+ *   rule_engine.go:55-83          RuleEngine.ShouldSample
+ *   rule_engine.go:89-115         evaluateLevel (order-sensitive fold)
+ *   internal/sampling/error.go:29-44        ErrorRule.Evaluate
+ *   internal/sampling/latency.go:44-100     HttpRouteLatencyRule.Evaluate
+ *   internal/sampling/servicename.go:35-51  ServiceNameRule.Evaluate
+ *
+ * The rules are evaluated literally: one pass over the trace's spans per
+ * rule, in batch order, with the same sentinel logic as the Go code.  The
+ * only departure is rand.Float64(), replaced by the injected uniform of
+ * include/odigos_amd.h so that decisions are reproducible.
+ */
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+struct orc_sampling {
+  int n;
+  orc_rule* rules;   /* copies; route strings owned */
+};
+
+orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules) {
+  orc_sampling* s = (orc_sampling*)calloc(1, sizeof *s);
+  s->n = n_rules;
+  s->rules = (orc_rule*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(orc_rule));
+  for (int i = 0; i < n_rules; i++) {
+    s->rules[i] = rules[i];
+    char* r = (char*)malloc(rules[i].route_len + 1);
+    if (rules[i].route_len) memcpy(r, rules[i].route, rules[i].route_len);
+    r[rules[i].route_len] = 0;
+    s->rules[i].route = r;
+  }
+  return s;
+}
+
+void orc_sampling_free(orc_sampling* s) {
+  if (!s) return;
+  for (int i = 0; i < s->n; i++) free((void*)s->rules[i].route);
+  free(s->rules);
+  free(s);
+}
+
+static uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+double orc_trace_uniform(uint64_t hi, uint64_t lo, uint64_t seed) {
+  uint64_t x = hi ^ ((lo << 29) | (lo >> 35)) ^ seed;
+  return (double)(splitmix64(x) >> 11) * 0x1.0p-53;
+}
+
+/* One trace = a list of span indices in batch order. */
+typedef struct {
+  const ose_columns* c;
+  const uint32_t* spans;
+  uint64_t n;
+  int batch_mode;   /* ServiceNameRule scans every resource of the batch */
+} trace_view;
+
+typedef struct { int matched, satisfied; double ratio; } eval_t;
+
+static eval_t eval_error(const orc_rule* r, const trace_view* t) {
+  /* error.go:29-44: matched is always true */
+  for (uint64_t k = 0; k < t->n; k++)
+    if (t->c->status[t->spans[k]] == OSE_STATUS_ERROR) return (eval_t){1, 1, 100.0};
+  return (eval_t){1, 0, r->fallback};
+}
+
+/* time.Time.Sub on two time.Unix(0, ns) values: exact int64 difference,
+ * saturated at the Duration range (time.go Sub's overflow checks). */
+static int64_t go_sub_ns(int64_t t, int64_t u) {
+  int64_t d;
+  if (__builtin_sub_overflow(t, u, &d)) return t < u ? INT64_MIN : INT64_MAX;
+  return d;
+}
+
+static eval_t eval_latency(const orc_rule* r, const trace_view* t) {
+  const ose_columns* c = t->c;
+  int service_found = 0, endpoint_found = 0;
+  uint64_t min_start = 0, max_end = 0;   /* pcommon.Timestamp sentinels */
+  for (uint64_t k = 0; k < t->n; k++) {
+    uint32_t i = t->spans[k];
+    /* AsString(service.name) != ServiceName -> skip the resource (latency.go:51-56) */
+    if (c->res_svc[c->resource[i]] != r->svc || r->svc == OSE_NONE) continue;
+    service_found = 1;
+    ose_strref rt = c->route[i];   /* AsString(http.route); absent == "" here */
+    if (rt.len >= r->route_len && memcmp(c->arena + rt.off, r->route, r->route_len) == 0)
+      endpoint_found = 1;   /* strings.HasPrefix (latency.go:97-100) */
+    uint64_t s = c->start_ns[i], e = c->end_ns[i];
+    if (min_start == 0 || s < min_start) min_start = s;
+    if (max_end == 0 || e > max_end) max_end = e;
+  }
+  if (!service_found || !endpoint_found) return (eval_t){0, 0, 0.0};
+  /* maxEnd.AsTime().Sub(minStart.AsTime()).Milliseconds() */
+  int64_t ms = go_sub_ns((int64_t)max_end, (int64_t)min_start) / 1000000;
+  if (ms >= r->threshold) return (eval_t){1, 1, 100.0};
+  return (eval_t){1, 0, r->fallback};
+}
+
+static eval_t eval_service(const orc_rule* r, const trace_view* t) {
+  const ose_columns* c = t->c;
+  /* resourceAttrs service.name Str() == ServiceName (servicename.go:38-47) */
+  if (r->svc != OSE_NONE) {
+    if (t->batch_mode) {
+      for (uint32_t q = 0; q < c->n_resources; q++)
+        if (c->res_svc_str[q] == r->svc) return (eval_t){1, 1, r->ratio};
+    } else {
+      for (uint64_t k = 0; k < t->n; k++)
+        if (c->res_svc_str[c->resource[t->spans[k]]] == r->svc) return (eval_t){1, 1, r->ratio};
+    }
+  }
+  return (eval_t){0, 0, r->fallback};
+}
+
+/* evaluateLevel (rule_engine.go:89-115) */
+static void evaluate_level(const orc_sampling* s, int level, const trace_view* t, double* ratio, int* sat,
+                           int* matched) {
+  int found_fallback = 0;
+  *ratio = 0;
+  *sat = 0;
+  *matched = 0;
+  for (int k = 0; k < s->n; k++) {
+    const orc_rule* r = &s->rules[k];
+    if (r->level != level) continue;
+    eval_t e;
+    switch (r->type) {
+      case ORC_RULE_ERROR: e = eval_error(r, t); break;
+      case ORC_RULE_LATENCY: e = eval_latency(r, t); break;
+      default: e = eval_service(r, t); break;
+    }
+    if (e.satisfied) {
+      *sat = 1;
+      *ratio = *ratio > e.ratio ? *ratio : e.ratio;   /* Go max(): ratios are never NaN (Validate) */
+      *matched = 1;
+    } else if (e.matched) {
+      *matched = 1;
+      if (!found_fallback) {
+        *ratio = e.ratio;
+        found_fallback = 1;
+      } else {
+        *ratio = *ratio < e.ratio ? *ratio : e.ratio;
+      }
+    }
+  }
+}
+
+/* ShouldSample (rule_engine.go:55-83).  level out: 0..2 = the satisfied
+ * level, 3 = min fallback over matched levels, 4 = nothing matched. */
+static int should_sample(const orc_sampling* s, const trace_view* t, double u, uint8_t* level, double* ratio_out) {
+  int have_min = 0;
+  double min_fb = 0;
+  for (int L = 0; L < 3; L++) {
+    double ratio;
+    int sat, matched;
+    evaluate_level(s, L, t, &ratio, &sat, &matched);
+    if (sat) {
+      *level = (uint8_t)L;
+      *ratio_out = ratio;
+      return u * 100 < ratio;
+    }
+    if (matched && (!have_min || ratio < min_fb)) {
+      min_fb = ratio;
+      have_min = 1;
+    }
+  }
+  if (have_min) {
+    *level = 3;
+    *ratio_out = min_fb;
+    return u * 100 < min_fb;
+  }
+  *level = 4;
+  *ratio_out = 100.0;
+  return 1;
+}
+
+/* ---- grouping by trace_id (first-appearance order) ---- */
+typedef struct { uint64_t hi, lo; uint32_t trace; uint32_t used; } slot_t;
+
+static uint64_t mix(uint64_t hi, uint64_t lo) { return splitmix64(hi ^ splitmix64(lo)); }
+
+typedef struct {
+  const orc_sampling* s;
+  const ose_columns* c;
+  ose_outputs* o;
+  const uint32_t* first;   /* trace -> offset into members */
+  const uint32_t* members; /* span indices grouped by trace, batch order */
+  uint32_t lo, hi;         /* trace range */
+  int batch_mode;
+  uint64_t seed;
+  uint8_t* tkeep;
+} job_t;
+
+static void* run_traces(void* arg) {
+  job_t* j = (job_t*)arg;
+  const ose_columns* c = j->c;
+  for (uint32_t t = j->lo; t < j->hi; t++) {
+    trace_view v = {c, j->members + j->first[t], (uint64_t)(j->first[t + 1] - j->first[t]), j->batch_mode};
+    uint64_t hi = 0, lo = 0;
+    if (v.n) {
+      hi = c->trace_id[2 * (uint64_t)v.spans[0]];
+      lo = c->trace_id[2 * (uint64_t)v.spans[0] + 1];
+    }
+    uint8_t level;
+    double ratio;
+    int keep = should_sample(j->s, &v, orc_trace_uniform(hi, lo, j->seed), &level, &ratio);
+    j->tkeep[t] = (uint8_t)keep;
+    ose_outputs* o = j->o;
+    if (o->trace_keep) o->trace_keep[t] = (uint8_t)keep;
+    if (o->trace_level) o->trace_level[t] = level;
+    if (o->trace_ratio) o->trace_ratio[t] = ratio;
+    if (o->trace_first_span) o->trace_first_span[t] = v.n ? v.spans[0] : 0;
+    if (o->keep)
+      for (uint64_t k = 0; k < v.n; k++) o->keep[v.spans[k]] = (uint8_t)keep;
+  }
+  return NULL;
+}
+
+int orc_sampling_process(const orc_sampling* s, const ose_columns* c, ose_outputs* o, uint32_t group_mode,
+                         const ose_rand* rnd, int nthreads) {
+  const uint64_t n = c->n_spans;
+  if (n > 0xFFFFFFFEull) return -1;
+  uint32_t* trace_of = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+  uint32_t ntr = 0;
+  if (group_mode == OSE_GROUP_BATCH) {
+    for (uint64_t i = 0; i < n; i++) trace_of[i] = 0;
+    ntr = 1;
+  } else {
+    uint64_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    slot_t* tab = (slot_t*)calloc(cap, sizeof(slot_t));
+    for (uint64_t i = 0; i < n; i++) {
+      uint64_t hi = c->trace_id[2 * i], lo = c->trace_id[2 * i + 1];
+      uint64_t h = mix(hi, lo) & (cap - 1);
+      for (;;) {
+        slot_t* e = &tab[h];
+        if (!e->used) {
+          e->used = 1;
+          e->hi = hi;
+          e->lo = lo;
+          e->trace = ntr++;
+          trace_of[i] = e->trace;
+          break;
+        }
+        if (e->hi == hi && e->lo == lo) {
+          trace_of[i] = e->trace;
+          break;
+        }
+        h = (h + 1) & (cap - 1);
+      }
+    }
+    free(tab);
+  }
+  uint32_t* first = (uint32_t*)calloc((size_t)ntr + 1, sizeof(uint32_t));
+  for (uint64_t i = 0; i < n; i++) first[trace_of[i] + 1]++;
+  for (uint32_t t = 0; t < ntr; t++) first[t + 1] += first[t];
+  uint32_t* fill = (uint32_t*)malloc(((size_t)ntr + 1) * sizeof(uint32_t));
+  memcpy(fill, first, ((size_t)ntr + 1) * sizeof(uint32_t));
+  uint32_t* members = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+  for (uint64_t i = 0; i < n; i++) members[fill[trace_of[i]]++] = (uint32_t)i;
+  uint8_t* tkeep = (uint8_t*)malloc(ntr ? ntr : 1);
+
+  if (nthreads < 1) nthreads = 1;
+  if ((uint32_t)nthreads > ntr) nthreads = ntr ? (int)ntr : 1;
+  job_t* jobs = (job_t*)calloc((size_t)nthreads, sizeof(job_t));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    job_t* j = &jobs[t];
+    j->s = s;
+    j->c = c;
+    j->o = o;
+    j->first = first;
+    j->members = members;
+    j->lo = (uint32_t)((uint64_t)ntr * (uint64_t)t / (uint64_t)nthreads);
+    j->hi = (uint32_t)((uint64_t)ntr * (uint64_t)(t + 1) / (uint64_t)nthreads);
+    j->batch_mode = group_mode == OSE_GROUP_BATCH;
+    j->seed = rnd ? rnd->seed : 0;
+    j->tkeep = tkeep;
+  }
+  for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, run_traces, &jobs[t]);
+  run_traces(&jobs[0]);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  if (o->trace_count) *o->trace_count = ntr;
+  free(jobs);
+  free(th);
+  free(tkeep);
+  free(members);
+  free(fill);
+  free(first);
+  free(trace_of);
+  return 0;
+}

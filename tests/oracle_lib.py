@@ -12,6 +12,11 @@ _p = C.c_void_p
 _L = None
 
 
+class OrcRule(C.Structure):
+    _fields_ = [("level", C.c_int32), ("type", C.c_int32), ("svc", C.c_uint32), ("route_len", C.c_uint32),
+                ("route", C.c_char_p), ("threshold", C.c_int64), ("ratio", C.c_double), ("fallback", C.c_double)]
+
+
 def lib():
     global _L
     if _L is None:
@@ -26,6 +31,11 @@ def lib():
             "orc_url_segment_name": (C.c_int, [_p, C.c_char_p, C.c_size_t, C.c_char_p]),
             "orc_url_apply_path": (C.c_long, [_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
             "orc_url_process": (C.c_int, [_p, C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_int]),
+            "orc_sampling_create": (_p, [C.POINTER(OrcRule), C.c_int]),
+            "orc_sampling_free": (None, [_p]),
+            "orc_sampling_process": (C.c_int, [_p, C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32,
+                                               C.POINTER(native.Rand), C.c_int]),
+            "orc_trace_uniform": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64]),
         }
         for name, (res, args) in sig.items():
             try:
@@ -95,3 +105,45 @@ class UrlOracle:
     def __del__(self):
         if getattr(self, "h", None):
             lib().orc_url_free(self.h)
+
+
+def intern_services(cfg: dict) -> dict:
+    """Service-name ids in first-appearance order over global, service and
+    endpoint rules (the ids the shim writes into res_svc / res_svc_str)."""
+    ids = {}
+    for lvl in ("global_rules", "service_rules", "endpoint_rules"):
+        for r in cfg.get(lvl) or []:
+            name = (r.get("rule_details") or {}).get("service_name")
+            if r.get("type") in ("http_latency", "service_name", "span_attribute") and name is not None:
+                ids.setdefault(name, len(ids))
+    return ids
+
+
+class SamplingOracle:
+    """RuleEngine.ShouldSample per trace, restated (oracle/sampling.c)."""
+    TYPES = {"error": 0, "http_latency": 1, "service_name": 2}
+
+    def __init__(self, cfg: dict | None = None):
+        cfg = cfg or {}
+        self.services = intern_services(cfg)
+        rules = []
+        for level, key in enumerate(("global_rules", "service_rules", "endpoint_rules")):
+            for r in cfg.get(key) or []:
+                d = r.get("rule_details") or {}
+                if r["type"] not in self.TYPES:
+                    raise ValueError(f"oracle: rule type {r['type']} not restated")
+                route = (d.get("http_route") or "").encode()
+                rules.append(OrcRule(level, self.TYPES[r["type"]], self.services.get(d.get("service_name"), native.OSE_NONE),
+                                     len(route), route, int(d.get("threshold", 0)), float(d.get("sampling_ratio", 0.0)),
+                                     float(d.get("fallback_sampling_ratio", 0.0))))
+        arr = (OrcRule * max(len(rules), 1))(*rules)
+        self._keep = arr
+        self.h = lib().orc_sampling_create(arr, len(rules))
+
+    def process(self, cols, outs, group_mode: int, seed: int = 0, nthreads: int = 1) -> int:
+        rnd = native.Rand(seed, 0.0)
+        return lib().orc_sampling_process(self.h, C.byref(cols), C.byref(outs), group_mode, C.byref(rnd), nthreads)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_sampling_free(self.h)
