@@ -9,7 +9,8 @@ SURVEY.md §8e), the timed region is bracketed by barrier + synchronize, and
 the max over ranks is reported.  Rank 0 prints ONE JSON line.
 
 Workloads (per GPU):
-  url   C2  odigosurltemplate, 10M spans, default rules          (configs[1])
+  url       C2  odigosurltemplate, 10M spans, default rules          (configs[1])
+  sampling  C3  odigossampling, 50M spans / ~5M traces, C3 rules     (configs[2])
 """
 from __future__ import annotations
 
@@ -29,31 +30,61 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 WORKLOADS = {
     "url": dict(gen="url", seed=0x0D160002, spans=10_000_000,
-                cfg={"odigosurltemplate": {}}, stages="TEMPLATE",
+                cfg={"odigosurltemplate": {}}, stages="TEMPLATE", group="TRACE_ID",
                 # no include/exclude configured: the shim passes res_url_ok = NULL
-                null_columns=("res_url_ok",),
+                null_columns=("res_url_ok",), null_outputs=(),
                 fields=("arena", "kind", "url_flags", "path"),
+                kernels=("url_plan_kernel", "url_scan_kernel", "url_emit_kernel"),
                 metric_config="C2: URL templatization only, 10M spans/GPU, C2 segment mix, default rules"),
+    "sampling": dict(gen="sampling", seed=0x0D160003, spans=50_000_000,
+                     cfg=None, stages="SAMPLE", group="TRACE_ID",
+                     null_columns=(), null_outputs=("trace_count", "trace_first_span", "trace_keep", "trace_level",
+                                                    "trace_ratio"),
+                     fields=("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc",
+                             "res_svc_str"),
+                     kernels=("trace_eval_kernel",),
+                     metric_config="C3: trace-level sampling (1 error + 4 service + 16 latency rules), "
+                                   "50M spans / ~5M traces per GPU, grouped by trace_id"),
 }
 
 
-def algorithmic_bytes_url(cols, url_out: np.ndarray, tmpl_used: int, gen) -> int:
+def _cfg(wl):
+    if wl["cfg"] is not None:
+        return wl["cfg"]
+    from tests.workloads import c3_sampling_config
+    return {"odigossampling": c3_sampling_config()}
+
+
+def algorithmic_bytes_url(gen, db, n) -> int:
     """SURVEY.md §8(d) URL row: per span 8 B path ref + 1 B kind + 1 B url_flags
     read, 8 B template ref + 1 B url_out written; plus the path bytes of every
     span whose path is templatized (read) and the template bytes written."""
-    n = cols.n_spans
+    url_out = db.out_numpy("url_out")[:n]
     path = gen.array("path").view(np.uint32).reshape(-1, 2)[:n]
     templ_read = int(path[(url_out & 1) != 0, 1].sum())
-    return n * (8 + 1 + 1) + n * (8 + 1) + templ_read + tmpl_used
+    return n * (8 + 1 + 1) + n * (8 + 1) + templ_read + db.used()
 
 
-def cpu_baseline(gen, cfg_url, threads: int, budget_s: float = 12.0):
+def algorithmic_bytes_sampling(gen, db, n, cfg) -> int:
+    """SURVEY.md §8(d) sampling row: per span 16 B trace_id + 8 B start + 8 B
+    end + 1 B status + 4 B resource + 8 B route ref read and 1 B keep written;
+    per resource 8 B (res_svc, res_svc_str); plus min(len(route), longest
+    rule route) route bytes per span that carries one."""
+    rules = cfg["odigossampling"].get("endpoint_rules", []) + cfg["odigossampling"].get("service_rules", []) + \
+        cfg["odigossampling"].get("global_rules", [])
+    pmax = max([len(r["rule_details"].get("http_route", "")) for r in rules] + [0])
+    route = gen.array("route").view(np.uint32).reshape(-1, 2)[:n]
+    rb = int(np.minimum(route[:, 1], pmax).sum())
+    return n * (16 + 8 + 8 + 1 + 4 + 8 + 1) + gen.cols.n_resources * 8 + rb
+
+
+def cpu_baseline_url(gen, cfg, threads: int, budget_s: float = 12.0):
     """Oracle (oracle/url.c, -O3) on the same batch: `threads` pthreads over
     the whole batch, repeated until ~budget_s of wall time; plus one
     single-thread pass over a 1M-span prefix."""
     from odigos_amd.batch import HostOutputs
     from tests.oracle_lib import UrlOracle
-    orc = UrlOracle(cfg_url)
+    orc = UrlOracle(cfg["odigosurltemplate"])
     ho = HostOutputs(gen.cols)
     n = gen.cols.n_spans
     reps, t0 = 0, time.perf_counter()
@@ -64,17 +95,59 @@ def cpu_baseline(gen, cfg_url, threads: int, budget_s: float = 12.0):
             break
     dt = time.perf_counter() - t0
     mt = n * reps / dt
-    # single core on a bounded prefix
-    import ctypes as C
-    from odigos_amd import native
-    c1 = native.Columns()
-    C.memmove(C.addressof(c1), C.addressof(gen.cols), C.sizeof(native.Columns))
-    c1.n_spans = min(n, 1_000_000)
+    c1 = _prefix(gen.cols, 1_000_000)
     ho1 = HostOutputs(c1)
     t1 = time.perf_counter()
     assert orc.process(c1, ho1.outs, 1) == 0
     st = c1.n_spans / (time.perf_counter() - t1)
-    return mt, st, reps, ho
+    sample = f"{n} spans (the same C2 batch) x {reps} passes, oracle/url.c -O3 pthreads"
+
+    def parity(db):
+        return (int(ho.used[0]) == db.used() and
+                np.array_equal(ho.view("url_out", np.uint8)[:n], db.out_numpy("url_out")[:n]))
+    return mt, st, sample, parity
+
+
+def cpu_baseline_sampling(gen, cfg, threads: int, budget_s: float = 12.0):
+    """Oracle (oracle/sampling.c, -O3: trace_id grouping + per-trace rule
+    fold) on a 5M-span prefix of the same batch, `threads` pthreads for the
+    fold, repeated to ~budget_s/2; plus a single-thread pass over 1M spans.
+    Parity: the full batch's keep column against the GPU's."""
+    from odigos_amd import native
+    from odigos_amd.batch import HostOutputs
+    from tests.oracle_lib import SamplingOracle
+    orc = SamplingOracle(cfg["odigossampling"])
+    n = gen.cols.n_spans
+    c5 = _prefix(gen.cols, min(n, 5_000_000))
+    ho5 = HostOutputs(c5)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        assert orc.process(c5, ho5.outs, native.GROUP_TRACE_ID, 0x5EED, threads) == 0
+        reps += 1
+        if time.perf_counter() - t0 > budget_s / 2 or reps >= 20:
+            break
+    mt = c5.n_spans * reps / (time.perf_counter() - t0)
+    c1 = _prefix(gen.cols, min(n, 1_000_000))
+    ho1 = HostOutputs(c1)
+    t1 = time.perf_counter()
+    assert orc.process(c1, ho1.outs, native.GROUP_TRACE_ID, 0x5EED, 1) == 0
+    st = c1.n_spans / (time.perf_counter() - t1)
+    sample = f"{c5.n_spans}-span prefix of the C3 batch x {reps} passes, oracle/sampling.c -O3 pthreads"
+
+    def parity(db):
+        ho = HostOutputs(gen.cols)
+        assert orc.process(gen.cols, ho.outs, native.GROUP_TRACE_ID, 0x5EED, threads) == 0
+        return bool(np.array_equal(ho.view("keep", np.uint8)[:n], db.out_numpy("keep")[:n]))
+    return mt, st, sample, parity
+
+
+def _prefix(cols, k):
+    import ctypes as C
+    from odigos_amd import native
+    c1 = native.Columns()
+    C.memmove(C.addressof(c1), C.addressof(cols), C.sizeof(native.Columns))
+    c1.n_spans = min(cols.n_spans, k)
+    return c1
 
 
 def main():
@@ -105,17 +178,21 @@ def main():
     wl = WORKLOADS[args.workload]
     n_spans = args.spans or wl["spans"]
     stages = getattr(native, "STAGE_" + wl["stages"])
+    cfg = _cfg(wl)
     gen = Generator(wl["gen"], seed=wl["seed"] + rank, n_spans=n_spans, threads=16)
     for f in wl.get("null_columns", ()):
         setattr(gen.cols, f, None)   # columns the configured processors do not read
-    eng = Engine(wl["cfg"])
+    eng = Engine(cfg)
     db = DeviceBatch(gen.cols, fields=wl.get("fields"))
+    for f in wl.get("null_outputs", ()):
+        setattr(db.outs, f, None)    # outputs the shim does not read (per-trace diagnostics)
     eng.reserve(n_spans)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
+    group = getattr(native, "GROUP_" + wl["group"])
 
     def step():
-        eng.process_device(db, stages, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
+        eng.process_device(db, stages, group, seed=0x5EED, stream=sh)
 
     for _ in range(args.warmup):
         step()
@@ -141,11 +218,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    url_out = db.out_numpy("url_out")[:n_spans]
-    used = db.used()
-    b_alg = algorithmic_bytes_url(gen.cols, url_out, used, gen)
-    # the URL stage is three launches (plan, scan, emit); the roofline is taken over their sum
-    knames = ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel")
+    if args.workload == "url":
+        b_alg = algorithmic_bytes_url(gen, db, n_spans)
+    else:
+        b_alg = algorithmic_bytes_sampling(gen, db, n_spans, cfg)
+    knames = wl["kernels"]
     per_k = {}
     for kn in knames:
         k = prof.get(kn, {"launches": 0, "ms": 0.0})
@@ -181,7 +258,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded generator, SURVEY.md §8d mix)",
         "config": {"workload": wl["metric_config"], "spans_per_gpu": n_spans, "seed": wl["seed"],
-                   "processors": list(wl["cfg"].keys()), "parallelism": f"trace-sharded x{world}, no data-path collective"},
+                   "processors": list(cfg.keys()), "parallelism": f"trace-sharded x{world}, no data-path collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kname, "kernel_ms": k_ms, "kernel_ms_each": per_k,
@@ -189,14 +266,12 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        mt, st, reps, ho = cpu_baseline(gen, wl["cfg"]["odigosurltemplate"], threads)
-        # the CPU pass doubles as a parity spot-check of the timed GPU output
-        parity = (int(ho.used[0]) == used and
-                  np.array_equal(ho.view("url_out", np.uint8)[:n_spans], url_out))
+        fn = cpu_baseline_url if args.workload == "url" else cpu_baseline_sampling
+        mt, st, sample, parity = fn(gen, cfg, threads)
         out["cpu_baseline"] = {"value": mt, "unit": "spans/s", "cores": threads, "kind": "port",
-                               "sample": f"{n_spans} spans (the same C2 batch) x {reps} passes, oracle/url.c -O3 pthreads",
-                               "value_1core": st}
-        out["parity_vs_oracle"] = bool(parity)
+                               "sample": sample, "value_1core": st}
+        # the CPU pass doubles as a parity spot-check of the timed GPU output
+        out["parity_vs_oracle"] = bool(parity(db))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -8,7 +8,7 @@ import csv, glob, json, re, sys
 from collections import defaultdict
 
 wl, root, out = sys.argv[1], sys.argv[2], sys.argv[3]
-STAGES = {"url": ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel")}
+STAGES = {"url": ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel"), "sampling": ("trace_eval_kernel",)}
 kernels = STAGES[wl]
 vals = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
 for c in vals:
