@@ -156,6 +156,7 @@ typedef struct ose_columns {
 
   /* per scope */
   const uint32_t* scope_size;   /* ScopeSpans bytes excluding its spans fields */
+  const uint32_t* scope_resource; /* index of the scope's ResourceSpans (non-decreasing) */
 } ose_columns;
 
 /* ---- results -----------------------------------------------------------

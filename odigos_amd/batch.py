@@ -20,7 +20,7 @@ COLUMN_LAYOUT = {
     "kind": ("span", 1), "resource": ("span", 4), "scope": ("span", 4), "url_flags": ("span", 1),
     "path": ("span", 8), "route": ("span", 8), "span_size": ("span", 4), "name_len": ("span", 4),
     "res_svc": ("res", 4), "res_svc_str": ("res", 4), "res_url_ok": ("res", 1), "res_attrset": ("res", 4),
-    "res_size": ("res", 4), "scope_size": ("scope", 4),
+    "res_size": ("res", 4), "scope_size": ("scope", 4), "scope_resource": ("scope", 4),
 }
 OUTPUT_LAYOUT = {
     "keep": ("span", 1), "trace_count": ("one", 4), "trace_first_span": ("span", 4), "trace_keep": ("span", 1),

@@ -91,6 +91,7 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
   IN(res_attrset, 4 * R);
   IN(res_size, 4 * R);
   IN(scope_size, 4 * S);
+  IN(scope_resource, 4 * S);
   OUT(keep, n);
   OUT(trace_count, 4);
   OUT(trace_first_span, 4 * std::max<uint64_t>(n, 1));   // BATCH mode: one trace even with no spans

@@ -355,12 +355,19 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
                const ose_rand* rnd, hipStream_t st) {
   if (!c || !o) return fail(OSE_EINVAL, "columns and outputs are required");
   if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE)) return fail(OSE_EINVAL, "unknown stage bit");
-  if (mask & OSE_STAGE_SIZE) return fail(OSE_ENOTSUP, "SIZE stage not built yet");
   Workspace* ws = e->acquire_ws();
-  int rc = 0;
+  // one reservation for every stage of the call: a stage must not reallocate
+  // scratch an earlier stage of the same call is still using on the stream
+  size_t need = 0;
+  if (mask & OSE_STAGE_TEMPLATE) need = std::max(need, url_workspace_bytes(c->n_spans));
+  if (mask & OSE_STAGE_SAMPLE) need = std::max(need, e->workspace_bytes(c->n_spans));
+  if (mask & OSE_STAGE_SIZE) need = std::max(need, size_scratch_bytes(c->n_scopes, c->n_resources));
+  int rc = ws->reserve(need);
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
-  if (mask & OSE_STAGE_SAMPLE) rc = run_sampling(e, c, o, group_mode, rnd, st, ws);
+  if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws);
   if (!rc && (mask & OSE_STAGE_TEMPLATE)) rc = run_url(e, c, o, st, ws);
+  // odigostrafficmetrics runs last, on what the earlier stages left
+  if (!rc && (mask & OSE_STAGE_SIZE)) rc = run_size(e, c, o, mask, group_mode, rnd, st, ws);
   e->release_ws(ws);
   return rc;
 }

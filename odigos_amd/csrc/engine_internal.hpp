@@ -69,6 +69,9 @@ struct Engine {
 
 int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
                  hipStream_t st, Workspace* ws);
+int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
+             const ose_rand* rnd, hipStream_t st, Workspace* ws);
+size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources);
 int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
                const ose_rand* rnd, hipStream_t st);
 

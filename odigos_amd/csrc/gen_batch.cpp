@@ -264,7 +264,8 @@ struct Gen {
   std::vector<uint8_t> arena;
   std::vector<uint64_t> trace_id, start, end;
   std::vector<uint8_t> status, kind, url_flags, res_url_ok;
-  std::vector<uint32_t> resource, scope, span_size, name_len, res_svc, res_svc_str, res_attrset, res_size, scope_size;
+  std::vector<uint32_t> resource, scope, span_size, name_len, res_svc, res_svc_str, res_attrset, res_size, scope_size,
+      scope_resource;
   std::vector<ose_strref> path, route;
 };
 
@@ -321,6 +322,7 @@ void* osegen_create(const char* workload, uint64_t seed, uint64_t n_spans, int t
     g->res_attrset.push_back(c.res_attrset[r]);
     g->res_size.push_back(c.res_size[r]);
     g->scope_size.push_back(c.scope_size[r]);
+    g->scope_resource.push_back(res);   // one ScopeSpans per ResourceSpans
     for (uint32_t i = s0; i < s1; i++) {
       g->trace_id.push_back(c.trace_id[2 * i]);
       g->trace_id.push_back(c.trace_id[2 * i + 1]);
@@ -372,6 +374,7 @@ void* osegen_create(const char* workload, uint64_t seed, uint64_t n_spans, int t
   c.res_attrset = g->res_attrset.data();
   c.res_size = g->res_size.data();
   c.scope_size = g->scope_size.data();
+  c.scope_resource = g->scope_resource.data();
   return g;
 }
 

@@ -42,6 +42,7 @@ void HostBatch::bind() {
   cols.res_attrset = res_attrset.data();
   cols.res_size = res_size.data();
   cols.scope_size = scope_size.data();
+  cols.scope_resource = scope_resource.data();
   outs.keep = keep.data();
   outs.trace_count = trace_count.data();
   outs.trace_first_span = trace_first_span.data();
@@ -189,6 +190,7 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
     hb->res_size.push_back((uint32_t)sizer.resource_fixed(rs));
     for (auto& ss : rs.scope_spans) {
       hb->scope_size.push_back((uint32_t)sizer.scope_fixed(ss));
+      hb->scope_resource.push_back((uint32_t)ri);
       for (auto& sp : ss.spans) {
         uint64_t hi = 0, lo = 0;
         for (int k = 0; k < 8; k++) { hi = hi << 8 | sp.trace_id[k]; lo = lo << 8 | sp.trace_id[8 + k]; }
@@ -272,7 +274,7 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
   hb->res_bytes.assign(std::max<size_t>(hb->res_svc.size(), 1), 0);
   hb->tmpl_used.assign(1, 0);
   hb->device_status.assign(4, 0);
-  for (auto* v : {&hb->res_svc, &hb->res_svc_str, &hb->res_attrset, &hb->res_size, &hb->scope_size,
+  for (auto* v : {&hb->res_svc, &hb->res_svc_str, &hb->res_attrset, &hb->res_size, &hb->scope_size, &hb->scope_resource,
                   &hb->resource, &hb->scope, &hb->span_size, &hb->name_len})
     if (v->empty()) v->push_back(0);
   for (auto* v : {&hb->status, &hb->kind, &hb->url_flags, &hb->res_url_ok})
@@ -292,12 +294,13 @@ void TracesProcessor::Apply(HostBatch& hb, Traces& td) {
   // call (OSE_GROUP_BATCH) this is exactly ResourceSpans().RemoveIf(true)
   // (processor.go:23-25); per trace_id, emptied scopes/resources go too.
   std::vector<uint8_t> keep;
-  if (st & OSE_STAGE_SAMPLE) keep.assign(o.keep, o.keep + hb.cols.n_spans);
+  const bool sampled = st & OSE_STAGE_SAMPLE;
+  if (sampled) keep.assign(o.keep, o.keep + hb.cols.n_spans);
   size_t i = 0;
   for (auto& rs : td.resource_spans) {
     for (auto& ss : rs.scope_spans) {
       for (auto& sp : ss.spans) {
-        bool kept = keep.empty() || keep[i];
+        bool kept = !sampled || keep[i];
         if (kept && (st & OSE_STAGE_TEMPLATE) && o.url_out[i]) {
           std::string tmpl(reinterpret_cast<const char*>(o.tmpl_arena) + o.tmpl[i].off, o.tmpl[i].len);
           if (o.url_out[i] & OSE_OUT_SET_ATTR)
@@ -312,7 +315,7 @@ void TracesProcessor::Apply(HostBatch& hb, Traces& td) {
       }
     }
   }
-  if (!keep.empty()) {
+  if (sampled) {
     if (group_mode == OSE_GROUP_BATCH) {
       // one decision for the whole call, spanless resources included
       if (!o.trace_keep[0]) td.resource_spans.clear();
@@ -379,6 +382,7 @@ int TracesProcessor::ProcessTraces(Traces& td) {
   cp(c->res_attrset, hb->cols.res_attrset, 4 * R);
   cp(c->res_size, hb->cols.res_size, 4 * R);
   cp(c->scope_size, hb->cols.scope_size, 4 * S);
+  cp(c->scope_resource, hb->cols.scope_resource, 4 * S);
   std::memset(o->attrset_bytes, 0, 8 * (size_t)A);
   std::memset(o->accepted_spans, 0, 8);
   rc = ose_process(eng_, b, stages(), group_mode, &rnd);

@@ -32,7 +32,7 @@ struct HostBatch {
   std::vector<uint8_t> status, kind, url_flags;
   std::vector<uint32_t> resource, scope, span_size, name_len;
   std::vector<ose_strref> path, route;
-  std::vector<uint32_t> res_svc, res_svc_str, res_attrset, res_size, scope_size;
+  std::vector<uint32_t> res_svc, res_svc_str, res_attrset, res_size, scope_size, scope_resource;
   std::vector<uint8_t> res_url_ok;
   // outputs
   std::vector<uint8_t> keep, trace_keep, trace_level, url_out, tmpl_arena;

@@ -99,6 +99,7 @@ struct TraceKernelArgs {
   const uint32_t* perm;       // kTracePerm: position -> span
   const uint32_t* key;        // kTracePerm: span -> canonical trace (first run-head position)
   uint32_t* error;            // bit0 spin timeout, bit2 trace table full
+  uint32_t* batch_keep;       // kTraceBatch: the call's decision (read by the SIZE stage)
 };
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
 
@@ -154,5 +155,45 @@ struct TraceCompactArgs {
   double* trace_ratio;
 };
 void launch_trace_compact(const TraceCompactArgs& a, hipStream_t st);
+
+// Workspace words shared between stages of one call (uint32 index into the
+// first 256 bytes of the workspace; URL uses words 0-3, SAMPLE 0-15).
+constexpr uint32_t kBatchKeepWord = 16;   // OSE_GROUP_BATCH decision of the SAMPLE stage
+
+// odigostrafficmetrics (size_kernel.hip): three passes, spans -> scopes ->
+// resources, each a wave-segmented reduction (the columns are in pdata
+// order, so scope and resource indices are non-decreasing).
+struct SizeKernelArgs {
+  uint64_t n_spans;
+  uint32_t n_scopes, n_resources, n_attrsets;
+  uint32_t sampled;           // SAMPLE ran in this call: keep decides which spans survive
+  uint32_t templated;         // TEMPLATE ran: url_out / tmpl grow the spans
+  uint32_t remove_empty;      // OSE_GROUP_TRACE_ID sampling: emptied scopes/resources are removed
+  const uint32_t* batch_keep; // OSE_GROUP_BATCH sampling: 0 empties the whole call (null otherwise)
+  const uint32_t* span_size;
+  const uint32_t* name_len;
+  const uint32_t* scope;
+  const uint32_t* scope_size;
+  const uint32_t* scope_resource;
+  const uint32_t* res_size;
+  const uint32_t* res_attrset;
+  const uint8_t* keep;
+  const uint8_t* url_out;
+  const uint8_t* kind;
+  const ose_strref* tmpl;
+  int64_t inverse;
+  uint64_t* scope_body;       // [S] zeroed
+  uint32_t* scope_kept;       // [S] zeroed
+  uint32_t* scope_had;        // [S] zeroed
+  uint64_t* res_body;         // [R] zeroed
+  uint32_t* res_alive;        // [R] zeroed
+  uint32_t* res_had;          // [R] zeroed
+  int64_t* attrset_bytes;     // [n_attrsets] added to
+  int64_t* accepted;          // [1] added to
+  uint64_t* res_bytes;        // [R] or null
+};
+void launch_size_spans(const SizeKernelArgs& a, hipStream_t st);
+void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st);
+void launch_size_resources(const SizeKernelArgs& a, hipStream_t st);
 
 }  // namespace ose

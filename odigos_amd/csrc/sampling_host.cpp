@@ -149,6 +149,7 @@ static size_t sampling_scratch_bytes(uint64_t n) {
 size_t Engine::workspace_bytes(uint64_t n_spans) const {
   size_t s = url_workspace_bytes(n_spans);
   if (has_sampling) s = std::max(s, sampling_scratch_bytes(n_spans));
+  if (has_traffic) s = std::max(s, size_scratch_bytes(n_spans, n_spans));
   return s;
 }
 
@@ -250,6 +251,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.table_mask = ws->table_slots_cap ? ws->table_slots_cap - 1 : 0;
   a.dup = misc;
   a.error = err;
+  a.batch_keep = misc + kBatchKeepWord;
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);
   launch_trace_eval(a, st);

@@ -1,0 +1,97 @@
+// size_host.cpp — odigostrafficmetrics: the launch sequence of the size
+// stage (size_kernel.hip).
+#include <algorithm>
+
+#include "engine_internal.hpp"
+#include "kernels.hpp"
+
+namespace ose {
+
+#define HIP_TRY(expr)                                                                                  \
+  do {                                                                                                 \
+    hipError_t _e = (expr);                                                                            \
+    if (_e != hipSuccess) return fail(OSE_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+}  // namespace
+
+size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources) {
+  return align_up(256 + 16 * std::max<uint64_t>(n_scopes, 1), 256) + align_up(16 * std::max<uint64_t>(n_resources, 1), 256) + 256;
+}
+
+// dataSizesMetricsProcessor.processTraces (odigostrafficmetrics/
+// processor.go:71-84) after the stages of `mask` that ran before it in this
+// call (gateway order: sampling, then templating, then size).
+int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
+             const ose_rand* rnd, hipStream_t st, Workspace* ws) {
+  if (!e->has_traffic) return fail(OSE_EINVAL, "odigostrafficmetrics is not configured on this engine");
+  if (!o->attrset_bytes || !o->accepted_spans) return fail(OSE_EINVAL, "SIZE stage needs attrset_bytes and accepted_spans");
+  const uint64_t n = c->n_spans;
+  if (n && (!c->span_size || !c->scope)) return fail(OSE_EINVAL, "SIZE stage needs span_size and scope");
+  if (c->n_scopes && (!c->scope_size || !c->scope_resource)) return fail(OSE_EINVAL, "SIZE stage needs scope_size and scope_resource");
+  if (c->n_resources && (!c->res_size || !c->res_attrset)) return fail(OSE_EINVAL, "SIZE stage needs res_size and res_attrset");
+  const bool sampled = mask & OSE_STAGE_SAMPLE, templated = mask & OSE_STAGE_TEMPLATE;
+  if (templated && n && (!c->kind || !c->name_len || !o->url_out || !o->tmpl))
+    return fail(OSE_EINVAL, "SIZE after TEMPLATE needs kind, name_len, url_out and tmpl");
+  // if p.samplingFraction != 0 && rand.Float64() < p.samplingFraction (processor.go:72)
+  const double ratio = e->traffic.sampling_ratio;
+  const double u = rnd ? rnd->traffic_u : 0.0;
+  if (!(ratio != 0 && u < ratio)) return 0;
+  if (o->res_bytes && c->n_resources) HIP_TRY(hipMemsetAsync(o->res_bytes, 0, 8 * (size_t)c->n_resources, st));
+  const uint64_t S = c->n_scopes, R = c->n_resources;
+  int rc = ws->reserve(size_scratch_bytes(S, R));
+  if (rc) return rc;
+  uint8_t* base = static_cast<uint8_t*>(ws->dev);
+  uint8_t* sc = base + 256;
+  uint8_t* rs = base + align_up(256 + 16 * std::max<uint64_t>(S, 1), 256);
+  HIP_TRY(hipMemsetAsync(sc, 0, 16 * std::max<uint64_t>(S, 1), st));
+  HIP_TRY(hipMemsetAsync(rs, 0, 16 * std::max<uint64_t>(R, 1), st));
+  SizeKernelArgs a{};
+  a.n_spans = n;
+  a.n_scopes = (uint32_t)S;
+  a.n_resources = (uint32_t)R;
+  a.n_attrsets = c->n_attrsets;
+  a.sampled = sampled;
+  a.templated = templated;
+  a.remove_empty = sampled && group_mode == OSE_GROUP_TRACE_ID;
+  a.batch_keep = sampled && group_mode == OSE_GROUP_BATCH ? reinterpret_cast<const uint32_t*>(base) + kBatchKeepWord : nullptr;
+  a.span_size = c->span_size;
+  a.name_len = c->name_len;
+  a.scope = c->scope;
+  a.scope_size = c->scope_size;
+  a.scope_resource = c->scope_resource;
+  a.res_size = c->res_size;
+  a.res_attrset = c->res_attrset;
+  a.keep = o->keep;
+  a.url_out = o->url_out;
+  a.kind = c->kind;
+  a.tmpl = o->tmpl;
+  a.inverse = e->inverse;
+  a.scope_body = reinterpret_cast<uint64_t*>(sc);
+  a.scope_kept = reinterpret_cast<uint32_t*>(sc + 8 * S);
+  a.scope_had = reinterpret_cast<uint32_t*>(sc + 12 * S);
+  a.res_body = reinterpret_cast<uint64_t*>(rs);
+  a.res_alive = reinterpret_cast<uint32_t*>(rs + 8 * R);
+  a.res_had = reinterpret_cast<uint32_t*>(rs + 12 * R);
+  a.attrset_bytes = o->attrset_bytes;
+  a.accepted = o->accepted_spans;
+  a.res_bytes = o->res_bytes;
+  Engine::Timed tm{};
+  e->prof_begin("size_span_kernel", st, tm);
+  launch_size_spans(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  e->prof_begin("size_scope_kernel", st, tm);
+  launch_size_scopes(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  e->prof_begin("size_res_kernel", st, tm);
+  launch_size_resources(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  return 0;
+}
+
+}  // namespace ose

@@ -1,0 +1,173 @@
+// size_kernel.hip — odigostrafficmetrics on CDNA4 (gfx950).
+//
+// Replaces dataSizesMetricsProcessor.processTraces (odigostrafficmetrics/
+// processor.go:71-84): per surviving ResourceSpans, its protobuf wire size
+// (ptrace.ProtoMarshaler.ResourceSpansSize, pdata v1.47.0) times
+// inverseSamplingFraction, added to the counter of its resource attribute
+// set, and the surviving span count.  The host sizes the immutable parts of
+// each message once when it columnarises (span_size, scope_size, res_size);
+// the GPU adds what the earlier gateway stages changed — spans dropped by
+// odigossampling, the attribute and name odigosurltemplate wrote — and the
+// length framing of every level, which depends on the final sizes:
+//   K1 spans     framed span sizes, wave-segmented by scope  -> scope sums
+//   K2 scopes    framed scope sizes, segmented by resource   -> resource sums
+//   K3 resources ResourceSpans sizes x inverse -> LDS-privatised attribute-set
+//                histogram -> one global atomic per non-empty bin per block
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+namespace ose {
+namespace {
+
+constexpr int kSThreads = 256;
+constexpr uint32_t kLdsAttrsets = 2048;   // attribute sets privatised in LDS (16 KiB of int64)
+
+__device__ __forceinline__ uint32_t sov(uint64_t x) {
+  // varint length: 1 + floor(log2(x|1) / 7)
+  return 1u + (uint32_t)((63 - __clzll((long long)(x | 1))) / 7);
+}
+__device__ __forceinline__ uint64_t field_len(uint64_t l) { return 1 + sov(l) + l; }
+
+__device__ __forceinline__ bool batch_dropped(const SizeKernelArgs& a) {
+  return a.batch_keep && __hip_atomic_load(a.batch_keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+}
+
+// Segmented (by non-decreasing key) inclusive sums over one wave; returns
+// true on the lane that ends its key's run inside the wave.
+template <typename T>
+__device__ __forceinline__ bool wave_seg_sum(uint32_t key, bool valid, T& v, uint32_t& c) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t vmask = __ballot(valid);
+  const uint32_t nk = __shfl_down(key, 1, kWave);
+  const bool last = valid && (lane == 63 || !((vmask >> (lane + 1)) & 1) || nk != key);
+  const uint64_t starts = __ballot(valid && (lane == 0 || __shfl_up(key, 1, kWave) != key));
+  // lanes whose key differs from lane-1's start a run; pull only from the same run
+  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  const int sst = valid ? 63 - __clzll((long long)(starts & le)) : lane;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const T ov = __shfl_up(v, d, kWave);
+    const uint32_t oc = __shfl_up(c, d, kWave);
+    if (lane >= d && lane - d >= sst) {
+      v += ov;
+      c += oc;
+    }
+  }
+  return last;
+}
+
+__global__ __launch_bounds__(kSThreads) void size_span_kernel(SizeKernelArgs a) {
+  if (batch_dropped(a)) return;
+  const uint64_t i = (uint64_t)blockIdx.x * kSThreads + threadIdx.x;
+  const bool valid = i < a.n_spans;
+  uint32_t s = 0, kept = 0;
+  uint64_t contrib = 0;
+  if (valid) {
+    s = a.scope[i];
+    kept = a.sampled ? a.keep[i] : 1u;
+    if (kept) {
+      uint64_t sz = a.span_size[i];
+      const uint8_t u = a.templated ? a.url_out[i] : 0;
+      if (u) {
+        const uint64_t tl = a.tmpl[i].len;
+        if (u & OSE_OUT_SET_ATTR) {   // PutStr(http.route | url.template, tmpl): one more KeyValue
+          const uint64_t keylen = a.kind[i] == OSE_KIND_CLIENT ? 12 : 10;
+          sz += field_len(field_len(keylen) + field_len(field_len(tl)));
+        }
+        if (u & OSE_OUT_RENAME) {     // SetName(method + " " + tmpl), old name == method
+          const uint64_t old = a.name_len[i];
+          sz += field_len(old + 1 + tl) - (old ? field_len(old) : 0);
+        }
+      }
+      contrib = field_len(sz);
+    }
+  }
+  uint64_t v = contrib;
+  uint32_t c = kept;
+  const bool tail = wave_seg_sum(s, valid, v, c);
+  if (tail) {
+    if (v) atomicAdd((unsigned long long*)&a.scope_body[s], (unsigned long long)v);
+    if (c) atomicAdd(&a.scope_kept[s], c);
+    a.scope_had[s] = 1;
+  }
+  // SpanCount of the surviving batch
+  uint32_t k = kept;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, kWave);
+  if ((threadIdx.x & 63) == 0 && k) atomicAdd((unsigned long long*)a.accepted, (unsigned long long)k);
+}
+
+__global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a) {
+  if (batch_dropped(a)) return;
+  const uint32_t s = blockIdx.x * kSThreads + threadIdx.x;
+  const bool valid = s < a.n_scopes;
+  uint32_t r = 0, alive = 0, had = 0;
+  uint64_t contrib = 0;
+  if (valid) {
+    r = a.scope_resource[s];
+    had = a.scope_had[s];
+    alive = !a.remove_empty || !had || a.scope_kept[s];   // an emptied ScopeSpans is removed
+    if (alive) contrib = field_len((uint64_t)a.scope_size[s] + a.scope_body[s]);
+  }
+  uint64_t v = contrib;
+  uint32_t c = alive;
+  const bool tail = wave_seg_sum(r, valid, v, c);
+  // any scope of the run had spans: OR over the run == (run's had bits != 0)
+  uint32_t h = had;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t oh = __shfl_up(h, d, kWave);
+    const uint32_t orr = __shfl_up(r, d, kWave);
+    if ((int)(threadIdx.x & 63) >= d && orr == r) h |= oh;
+  }
+  if (tail) {
+    if (v) atomicAdd((unsigned long long*)&a.res_body[r], (unsigned long long)v);
+    if (c) atomicAdd(&a.res_alive[r], c);
+    if (h) a.res_had[r] = 1;
+  }
+}
+
+__global__ __launch_bounds__(kSThreads) void size_res_kernel(SizeKernelArgs a) {
+  if (batch_dropped(a)) return;
+  __shared__ unsigned long long hist[kLdsAttrsets];   // two's-complement sums
+  const bool lds = a.n_attrsets <= kLdsAttrsets;
+  if (lds)
+    for (uint32_t k = threadIdx.x; k < a.n_attrsets; k += kSThreads) hist[k] = 0;
+  __syncthreads();
+  for (uint32_t r = blockIdx.x * kSThreads + threadIdx.x; r < a.n_resources; r += gridDim.x * kSThreads) {
+    const bool removed = a.remove_empty && a.res_had[r] && !a.res_alive[r];
+    const uint64_t size = removed ? 0 : (uint64_t)a.res_size[r] + a.res_body[r];
+    if (a.res_bytes) a.res_bytes[r] = size;
+    if (removed) continue;
+    const long long add = (long long)size * a.inverse;
+    const uint32_t set = a.res_attrset[r];
+    if (lds) atomicAdd(&hist[set], (unsigned long long)add);
+    else atomicAdd((unsigned long long*)&a.attrset_bytes[set], (unsigned long long)add);
+  }
+  if (!lds) return;
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < a.n_attrsets; k += kSThreads)
+    if (hist[k]) atomicAdd((unsigned long long*)&a.attrset_bytes[k], hist[k]);
+}
+
+}  // namespace
+
+void launch_size_spans(const SizeKernelArgs& a, hipStream_t st) {
+  const uint64_t blocks = (a.n_spans + kSThreads - 1) / kSThreads;
+  if (blocks) hipLaunchKernelGGL(size_span_kernel, dim3((uint32_t)blocks), dim3(kSThreads), 0, st, a);
+}
+void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st) {
+  const uint32_t blocks = (a.n_scopes + kSThreads - 1) / kSThreads;
+  if (blocks) hipLaunchKernelGGL(size_scope_kernel, dim3(blocks), dim3(kSThreads), 0, st, a);
+}
+void launch_size_resources(const SizeKernelArgs& a, hipStream_t st) {
+  uint32_t blocks = (a.n_resources + kSThreads * 16 - 1) / (kSThreads * 16);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks) hipLaunchKernelGGL(size_res_kernel, dim3(blocks), dim3(kSThreads), 0, st, a);
+}
+
+}  // namespace ose

@@ -301,6 +301,7 @@ __device__ __forceinline__ bool head_at(const TraceKernelArgs& a, uint64_t p) { 
 
 __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos, uint8_t keep, uint8_t level,
                                           double ratio) {
+  if (a.mode == kTraceBatch && a.batch_keep) *a.batch_keep = keep;
   if (!a.rec) return;
   TraceRec r;
   r.first_span = a.mode == kTracePerm ? a.perm[pos] : (uint32_t)pos;
@@ -336,6 +337,7 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
       double r;
       decide(c, 0, 0, 0, batch_svc, trace_uniform(0, 0, a.seed), k, l, r);
       if (lane == 0) {
+        if (a.batch_keep) *a.batch_keep = k;
         if (a.win_heads) a.win_heads[0] = 1;
         if (a.rec) {
           TraceRec rr{0, k, l, 0, 0, r};

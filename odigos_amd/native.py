@@ -59,7 +59,7 @@ class Rand(C.Structure):
 COLUMN_FIELDS = [
     "arena", "trace_id", "start_ns", "end_ns", "status", "kind", "resource", "scope", "url_flags",
     "path", "route", "span_size", "name_len", "res_svc", "res_svc_str", "res_url_ok", "res_attrset",
-    "res_size", "scope_size",
+    "res_size", "scope_size", "scope_resource",
 ]
 
 

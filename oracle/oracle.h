@@ -90,11 +90,18 @@ int orc_sampling_process(const orc_sampling* s, const ose_columns* c, ose_output
 double orc_trace_uniform(uint64_t hi, uint64_t lo, uint64_t seed);
 
 /* ---- odigostrafficmetrics -------------------------------------------------- */
-/* Adds ResourceSpansSize(after mutation) * inverse per attribute set and the
- * span count (processor.go:71-84).  keep/url_out/tmpl may be NULL. */
-int orc_size_process(const ose_columns* c, const ose_outputs* in_results,
-                     ose_outputs* o, int64_t inverse, double sampling_ratio,
-                     const ose_rand* rnd, int gogo_always_emit);
+/* dataSizesMetricsProcessor.processTraces (odigostrafficmetrics/
+ * processor.go:71-84) on the batch as the earlier gateway stages left it:
+ * `stages` says which ran (OSE_STAGE_SAMPLE: res->keep / res->trace_keep,
+ * OSE_STAGE_TEMPLATE: res->url_out / res->tmpl).  When traffic_u <
+ * sampling_ratio (and sampling_ratio != 0) it ADDS ResourceSpansSize(rs) *
+ * inverse to o->attrset_bytes[res_attrset[rs]] for every surviving
+ * ResourceSpans, writes the sizes to o->res_bytes (0 = removed) and adds
+ * the surviving span count to *o->accepted_spans. */
+int orc_size_process(const ose_columns* c, const ose_outputs* res, uint32_t stages, uint32_t group_mode,
+                     ose_outputs* o, int64_t inverse, double sampling_ratio, double traffic_u);
+/* wire size of a Span body after the odigosurltemplate mutation of span i */
+uint64_t orc_span_size_after(const ose_columns* c, const ose_outputs* res, uint32_t stages, uint64_t i);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,97 @@
+/*
+ * size.c — CPU restatement of odigostrafficmetrics (traces).  TEST
+ * INFRASTRUCTURE (see oracle.h): the checker for the HIP size stage and the
+ * timed CPU baseline, never part of the product.
+ *
+ * Restates (paths under collector/processors/odigostrafficmetrics/):
+ *   processor.go:31-58   newThroughputMeasurementProcessor (inverse = int64(1/ratio))
+ *   processor.go:60-69   attributeSetFromResource (host-interned: res_attrset column)
+ *   processor.go:71-84   processTraces
+ * and the third-party size it calls, ptrace.ProtoMarshaler.ResourceSpansSize
+ * (pdata v1.47.0), as the OTLP trace.proto wire size over the columns:
+ *   ResourceSpans = res_size (resource + schema_url, host-sized)
+ *                 + sum over surviving scopes of framed ScopeSpans
+ *   ScopeSpans    = scope_size (scope + schema_url) + sum of framed Spans
+ *   Span          = span_size (host-sized before mutation) + the growth the
+ *                   odigosurltemplate stage causes: one appended KeyValue
+ *                   (http.route / url.template, processor.go:259-261) and the
+ *                   renamed span (processor.go:214-233).
+ * The batch is the one the earlier gateway stages produced: spans of
+ * dropped traces are gone, and a ScopeSpans / ResourceSpans emptied by the
+ * drop is gone (host apply, odigos_amd/csrc/host.cpp TracesProcessor::Apply);
+ * with OSE_GROUP_BATCH a dropped trace empties the whole call
+ * (removeAllSpans, odigossamplingprocessor/processor.go:23-25).
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+static uint64_t sov(uint64_t x) {
+  uint64_t n = 1;
+  while (x >= 0x80) { x >>= 7; n++; }
+  return n;
+}
+static uint64_t field_len(uint64_t l) { return 1 + sov(l) + l; }   /* tag (field < 16) + varint + payload */
+
+uint64_t orc_span_size_after(const ose_columns* c, const ose_outputs* res, uint32_t stages, uint64_t i) {
+  uint64_t sz = c->span_size[i];
+  if (!(stages & OSE_STAGE_TEMPLATE) || !res->url_out[i]) return sz;
+  const uint64_t tl = res->tmpl[i].len;
+  if (res->url_out[i] & OSE_OUT_SET_ATTR) {
+    /* attr.PutStr(target, tmpl) on an absent key: one more KeyValue (field 9)
+     * {key (1): target, value (2): AnyValue{string_value (1): tmpl}} */
+    const uint64_t keylen = c->kind[i] == OSE_KIND_CLIENT ? 12 /* url.template */ : 10 /* http.route */;
+    const uint64_t kv = field_len(keylen) + field_len(field_len(tl));
+    sz += field_len(kv);
+  }
+  if (res->url_out[i] & OSE_OUT_RENAME) {
+    /* span.SetName(method + " " + tmpl) where the old name == method (field 5) */
+    const uint64_t old = c->name_len[i];
+    sz += field_len(old + 1 + tl) - (old ? field_len(old) : 0);
+  }
+  return sz;
+}
+
+int orc_size_process(const ose_columns* c, const ose_outputs* res, uint32_t stages, uint32_t group_mode,
+                     ose_outputs* o, int64_t inverse, double sampling_ratio, double traffic_u) {
+  const uint64_t n = c->n_spans;
+  const uint32_t R = c->n_resources, S = c->n_scopes;
+  /* if p.samplingFraction != 0 && rand.Float64() < p.samplingFraction (processor.go:72) */
+  if (!(sampling_ratio != 0 && traffic_u < sampling_ratio)) return 0;
+  const int sampled = (stages & OSE_STAGE_SAMPLE) != 0;
+  if (o->res_bytes) memset(o->res_bytes, 0, (size_t)R * sizeof(uint64_t));
+  if (sampled && group_mode == OSE_GROUP_BATCH && !res->trace_keep[0]) return 0;   /* td emptied */
+  uint64_t* sbody = (uint64_t*)calloc(S ? S : 1, sizeof(uint64_t));
+  uint8_t* shad = (uint8_t*)calloc(S ? S : 1, 1);
+  uint64_t* skept = (uint64_t*)calloc(S ? S : 1, sizeof(uint64_t));
+  int64_t accepted = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t s = c->scope[i];
+    shad[s] = 1;
+    if (sampled && !res->keep[i]) continue;
+    skept[s]++;
+    accepted++;
+    sbody[s] += field_len(orc_span_size_after(c, res, stages, i));   /* ScopeSpans.spans (2) */
+  }
+  uint64_t* rbody = (uint64_t*)calloc(R ? R : 1, sizeof(uint64_t));
+  uint8_t* rhad = (uint8_t*)calloc(R ? R : 1, 1);
+  uint32_t* ralive = (uint32_t*)calloc(R ? R : 1, sizeof(uint32_t));
+  for (uint32_t s = 0; s < S; s++) {
+    const uint32_t r = c->scope_resource[s];
+    rhad[r] |= shad[s];
+    if (!shad[s] || skept[s]) {   /* emptied scopes are removed, spanless ones stay */
+      ralive[r]++;
+      rbody[r] += field_len(c->scope_size[s] + sbody[s]);   /* ResourceSpans.scope_spans (2) */
+    }
+  }
+  for (uint32_t r = 0; r < R; r++) {
+    if (sampled && rhad[r] && !ralive[r]) continue;   /* emptied resource removed */
+    const uint64_t size = c->res_size[r] + rbody[r];
+    if (o->res_bytes) o->res_bytes[r] = size;
+    o->attrset_bytes[c->res_attrset[r]] += (int64_t)size * inverse;
+  }
+  *o->accepted_spans += accepted;
+  free(sbody); free(shad); free(skept); free(rbody); free(rhad); free(ralive);
+  return 0;
+}

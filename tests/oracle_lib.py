@@ -36,6 +36,8 @@ def lib():
             "orc_sampling_process": (C.c_int, [_p, C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32,
                                                C.POINTER(native.Rand), C.c_int]),
             "orc_trace_uniform": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64]),
+            "orc_size_process": (C.c_int, [C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32, C.c_uint32,
+                                           C.POINTER(native.Outputs), C.c_int64, C.c_double, C.c_double]),
         }
         for name, (res, args) in sig.items():
             try:
@@ -147,3 +149,11 @@ class SamplingOracle:
     def __del__(self):
         if getattr(self, "h", None):
             lib().orc_sampling_free(self.h)
+
+
+def size_process(cols, res_outs, stages: int, group_mode: int, outs, inverse: int = 1, ratio: float = 1.0,
+                 traffic_u: float = 0.0) -> int:
+    """dataSizesMetricsProcessor.processTraces restated (oracle/size.c); res_outs
+    holds the earlier stages' results (keep / trace_keep / url_out / tmpl)."""
+    return lib().orc_size_process(C.byref(cols), C.byref(res_outs), stages, group_mode, C.byref(outs), inverse,
+                                  ratio, traffic_u)
