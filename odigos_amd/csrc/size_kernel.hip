@@ -42,9 +42,12 @@ template <typename T>
 __device__ __forceinline__ bool wave_seg_sum(uint32_t key, bool valid, T& v, uint32_t& c) {
   const int lane = threadIdx.x & 63;
   const uint64_t vmask = __ballot(valid);
+  // cross-lane reads are taken by every lane (a shuffle from a lane that is
+  // not executing it is undefined), then used under conditions
   const uint32_t nk = __shfl_down(key, 1, kWave);
+  const uint32_t pk = __shfl_up(key, 1, kWave);
   const bool last = valid && (lane == 63 || !((vmask >> (lane + 1)) & 1) || nk != key);
-  const uint64_t starts = __ballot(valid && (lane == 0 || __shfl_up(key, 1, kWave) != key));
+  const uint64_t starts = __ballot(valid && (lane == 0 || pk != key));
   // lanes whose key differs from lane-1's start a run; pull only from the same run
   const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   const int sst = valid ? 63 - __clzll((long long)(starts & le)) : lane;
