@@ -11,6 +11,9 @@ the max over ranks is reported.  Rank 0 prints ONE JSON line.
 Workloads (per GPU):
   url       C2  odigosurltemplate, 10M spans, default rules          (configs[1])
   sampling  C3  odigossampling, 50M spans / ~5M traces, C3 rules     (configs[2])
+  fused     C4  all three processors, 12.5M spans/GPU (100M on 8)    (configs[3]);
+                with N > 1 the sampling records go to each trace's owner
+                GPU through an RCCL all-to-all (odigos_amd/exchange.py)
 """
 from __future__ import annotations
 
@@ -45,14 +48,44 @@ WORKLOADS = {
                      kernels=("trace_eval_kernel",),
                      metric_config="C3: trace-level sampling (1 error + 4 service + 16 latency rules), "
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
+    "fused": dict(gen="fused", seed=0x0D160004, spans=12_500_000,
+                  cfg=None, stages="SAMPLE|TEMPLATE|SIZE", group="TRACE_ID",
+                  null_columns=("res_url_ok",), null_outputs=("trace_count", "trace_first_span", "trace_keep",
+                                                             "trace_level", "trace_ratio", "res_bytes"),
+                  fields=("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "resource", "scope",
+                          "url_flags", "path", "route", "span_size", "name_len", "res_svc", "res_svc_str",
+                          "res_attrset", "res_size", "scope_size", "scope_resource"),
+                  kernels=("trace_eval_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel",
+                           "size_span_kernel", "size_scope_kernel", "size_res_kernel"),
+                  metric_config="C4: fused odigossampling -> odigosurltemplate -> odigostrafficmetrics, "
+                                "12.5M spans/GPU (100M on 8), trace-id all-to-all over RCCL when N > 1"),
 }
+
+# node-collector res_attributes_keys (autoscaler/controllers/nodecollector/collectorconfig/ownmetrics-ui.go:33-47)
+NODE_KEYS = ["k8s.namespace.name", "k8s.deployment.name", "k8s.statefulset.name", "k8s.daemonset.name",
+             "k8s.cronjob.name", "k8s.job.name", "k8s.pod.name", "k8s.node.name", "service.name"]
 
 
 def _cfg(wl):
     if wl["cfg"] is not None:
         return wl["cfg"]
     from tests.workloads import c3_sampling_config
+    if wl["gen"] == "fused":
+        return {"odigossampling": c3_sampling_config(), "odigosurltemplate": {},
+                "odigostrafficmetrics": {"res_attributes_keys": NODE_KEYS}}
     return {"odigossampling": c3_sampling_config()}
+
+
+def algorithmic_bytes_fused(gen, db, n, cfg) -> int:
+    """SURVEY.md §8(d) fused row: the union of the three stages' columns, each
+    read once (trace_id, start, end, status, resource, route ref + compared
+    route bytes, kind, url_flags, path ref + templated path bytes, span_size,
+    scope, name_len; per scope 8 B, per resource 20 B) and each output written
+    once (keep, url_out, tmpl ref + bytes, attribute-set counters)."""
+    samp = algorithmic_bytes_sampling(gen, db, n, cfg)          # includes the 1 B keep
+    url = algorithmic_bytes_url(gen, db, n)
+    size = n * (4 + 4 + 4) + gen.cols.n_scopes * 8 + gen.cols.n_resources * 12 + gen.cols.n_attrsets * 8
+    return samp + url + size
 
 
 def algorithmic_bytes_url(gen, db, n) -> int:
@@ -106,6 +139,47 @@ def cpu_baseline_url(gen, cfg, threads: int, budget_s: float = 12.0):
         return (int(ho.used[0]) == db.used() and
                 np.array_equal(ho.view("url_out", np.uint8)[:n], db.out_numpy("url_out")[:n]))
     return mt, st, sample, parity
+
+
+def cpu_baseline_fused(gen, cfg, threads: int, budget_s: float = 12.0):
+    """The three oracles chained in gateway order (sampling -> templating ->
+    size; oracle/{sampling,url,size}.c -O3, pthreads for the first two) on a
+    2M-span prefix of the same batch, repeated to ~budget_s/2.  Parity: keep,
+    url_out and the attribute-set counters of the full batch."""
+    from odigos_amd import native
+    from odigos_amd.batch import HostOutputs
+    from tests.oracle_lib import SamplingOracle, UrlOracle, size_process
+    so, uo = SamplingOracle(cfg["odigossampling"]), UrlOracle(cfg["odigosurltemplate"])
+    st = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE
+
+    def chain(cols, nt):
+        ho = HostOutputs(cols)
+        assert so.process(cols, ho.outs, native.GROUP_TRACE_ID, 0x5EED, nt) == 0
+        assert uo.process(cols, ho.outs, nt) == 0
+        assert size_process(cols, ho.outs, st, native.GROUP_TRACE_ID, ho.outs, 1, 1.0, 0.0) == 0
+        return ho
+    n = gen.cols.n_spans
+    c2 = _prefix(gen.cols, min(n, 2_000_000))
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        chain(c2, threads)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s / 2 or reps >= 20:
+            break
+    mt = c2.n_spans * reps / (time.perf_counter() - t0)
+    c1 = _prefix(gen.cols, min(n, 500_000))
+    t1 = time.perf_counter()
+    chain(c1, 1)
+    st1 = c1.n_spans / (time.perf_counter() - t1)
+    sample = f"{c2.n_spans}-span prefix of the C4 shard x {reps} passes, oracle/{{sampling,url,size}}.c -O3"
+
+    def parity(db):
+        ho = chain(gen.cols, threads)
+        A = gen.cols.n_attrsets
+        return bool(np.array_equal(ho.view("keep", np.uint8)[:n], db.out_numpy("keep")[:n]) and
+                    np.array_equal(ho.view("url_out", np.uint8)[:n], db.out_numpy("url_out")[:n]) and
+                    np.array_equal(ho.view("attrset_bytes", np.int64)[:A], db.out_numpy("attrset_bytes", np.int64)[:A]))
+    return mt, st1, sample, parity
 
 
 def cpu_baseline_sampling(gen, cfg, threads: int, budget_s: float = 12.0):
@@ -177,7 +251,9 @@ def main():
 
     wl = WORKLOADS[args.workload]
     n_spans = args.spans or wl["spans"]
-    stages = getattr(native, "STAGE_" + wl["stages"])
+    stages = 0
+    for s in wl["stages"].split("|"):
+        stages |= getattr(native, "STAGE_" + s)
     cfg = _cfg(wl)
     gen = Generator(wl["gen"], seed=wl["seed"] + rank, n_spans=n_spans, threads=16)
     for f in wl.get("null_columns", ()):
@@ -191,8 +267,21 @@ def main():
     sh = stream.cuda_stream
     group = getattr(native, "GROUP_" + wl["group"])
 
-    def step():
-        eng.process_device(db, stages, group, seed=0x5EED, stream=sh)
+    if world > 1 and stages & native.STAGE_SAMPLE:
+        # route every span's sampling record to its trace's owner
+        # GPU (RCCL all-to-all), decide there, bring keep back, then template
+        # and size locally on the decisions
+        from odigos_amd.exchange import DeviceExchange, route_and_sample
+        ex = DeviceExchange(eng, db, stream=sh)
+        local = (stages & ~native.STAGE_SAMPLE) | native.STAGE_APPLY_KEEP
+
+        def step():
+            route_and_sample(ex, world)
+            if local & (native.STAGE_TEMPLATE | native.STAGE_SIZE):
+                eng.process_device(db, local, group, seed=0x5EED, stream=sh)
+    else:
+        def step():
+            eng.process_device(db, stages, group, seed=0x5EED, stream=sh)
 
     for _ in range(args.warmup):
         step()
@@ -220,6 +309,8 @@ def main():
 
     if args.workload == "url":
         b_alg = algorithmic_bytes_url(gen, db, n_spans)
+    elif args.workload == "fused":
+        b_alg = algorithmic_bytes_fused(gen, db, n_spans, cfg)
     else:
         b_alg = algorithmic_bytes_sampling(gen, db, n_spans, cfg)
     knames = wl["kernels"]
@@ -258,7 +349,10 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded generator, SURVEY.md §8d mix)",
         "config": {"workload": wl["metric_config"], "spans_per_gpu": n_spans, "seed": wl["seed"],
-                   "processors": list(cfg.keys()), "parallelism": f"trace-sharded x{world}, no data-path collective"},
+                   "processors": list(cfg.keys()),
+                   "parallelism": (f"dp{world}: trace-id all-to-all (RCCL) of sampling records, local templating/size"
+                                   if world > 1 and stages & native.STAGE_SAMPLE else
+                                   f"dp{world}: independent span shards, no data-path collective")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kname, "kernel_ms": k_ms, "kernel_ms_each": per_k,
@@ -266,7 +360,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        fn = cpu_baseline_url if args.workload == "url" else cpu_baseline_sampling
+        fn = {"url": cpu_baseline_url, "sampling": cpu_baseline_sampling, "fused": cpu_baseline_fused}[args.workload]
         mt, st, sample, parity = fn(gen, cfg, threads)
         out["cpu_baseline"] = {"value": mt, "unit": "spans/s", "cores": threads, "kind": "port",
                                "sample": sample, "value_1core": st}

@@ -92,6 +92,10 @@ extern "C" {
 #define OSE_STAGE_SAMPLE   0x1u  /* odigossampling       */
 #define OSE_STAGE_TEMPLATE 0x2u  /* odigosurltemplate    */
 #define OSE_STAGE_SIZE     0x4u  /* odigostrafficmetrics */
+/* keep already holds the sampling decisions (made by an earlier call, e.g.
+ * on the trace's owner GPU after the trace-id exchange): SIZE honours them
+ * as if SAMPLE had run in this call with group_mode OSE_GROUP_TRACE_ID.    */
+#define OSE_STAGE_APPLY_KEEP 0x8u
 
 /* ---- grouping of spans into "traces" for odigossampling --------------
  * TRACE_ID: spans sharing a 128-bit trace_id form one trace (the contract
@@ -145,6 +149,10 @@ typedef struct ose_columns {
   const ose_strref* route;    /* AsString(http.route) before templating; len 0 if absent */
   const uint32_t* span_size;  /* wire size of the Span message before mutation */
   const uint32_t* name_len;   /* len(span.Name()) before mutation */
+  const uint64_t* route_match; /* optional: bit r = strings.HasPrefix(AsString(http.route), http_route
+                                  of the r-th http_latency rule) for the rules of the span's service
+                                  (latency.go:64-68, 97-100); when non-NULL the engine reads it
+                                  instead of route/arena (set by ose_shard_unpack)               */
 
   /* per resource */
   const uint32_t* res_svc;      /* ose_engine_service_id(AsString(service.name)) or OSE_NONE */
@@ -252,6 +260,29 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes);
  * and resets the counters; it synchronises the recorded events.           */
 int ose_profile_enable(ose_engine* eng, int on);
 int ose_profile_read(ose_engine* eng, char* json, size_t cap);
+
+/* ---- trace-id exchange across the GPUs of a node ----------------------
+ * odigossampling needs every span of a trace on one GPU.  In the reference
+ * that co-location is the node collector's loadbalancing exporter keyed by
+ * trace id (autoscaler/controllers/nodecollector/collectorconfig/
+ * traces.go:26-84).  Here: ose_shard_pack writes, per span, the record the
+ * trace stage reads into per-owner buckets of `send` (owner = trace-id hash
+ * mod n_ranks; batch order kept inside a bucket), with counts[n_ranks] and
+ * pack_pos[n_spans] (the span's slot in `send`); the caller moves the
+ * buckets with an all-to-all (RCCL), ose_shard_unpack turns the received
+ * records into columns for ose_process_device(SAMPLE, OSE_GROUP_TRACE_ID),
+ * the keep bytes go back with the reverse all-to-all, and
+ * ose_shard_scatter_keep puts them at the original spans.  All pointers are
+ * device pointers; calls are asynchronous on hip_stream.                    */
+#define OSE_XREC_BYTES 56u
+uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks);
+int ose_shard_pack(ose_engine* eng, const ose_columns* cols, uint32_t n_ranks, void* send,
+                   uint64_t* counts, uint32_t* pack_pos, void* hip_stream);
+int ose_shard_unpack(const void* recv, uint64_t n, uint64_t* trace_id, uint64_t* start_ns,
+                     uint64_t* end_ns, uint8_t* status, uint32_t* resource, uint32_t* res_svc,
+                     uint32_t* res_svc_str, uint64_t* route_match, void* hip_stream);
+int ose_shard_scatter_keep(const uint8_t* keep_back, const uint32_t* pack_pos, uint64_t n,
+                           uint8_t* keep, void* hip_stream);
 
 /* Message of the last failure on this thread ("" if none). */
 const char* ose_last_error(void);

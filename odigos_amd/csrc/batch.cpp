@@ -84,7 +84,7 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
   IN(path, 8 * n);
   IN(route, 8 * n);
   IN(span_size, 4 * n);
-  IN(name_len, 4 * n);
+  IN(name_len, 4 * n);   // route_match stays NULL: host batches carry route bytes
   IN(res_svc, 4 * R);
   IN(res_svc_str, 4 * R);
   IN(res_url_ok, R);
@@ -125,13 +125,13 @@ int ose_process(ose_engine* eng, ose_batch* bb, uint32_t stage_mask, uint32_t gr
   if (!eng || !bb) return fail(OSE_EINVAL, "NULL argument");
   Engine* e = reinterpret_cast<Engine*>(eng);
   Batch* b = reinterpret_cast<Batch*>(bb);
-  Workspace* ws = e->acquire_ws();
-  if (!ws->stream) {
-    hipError_t he = hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking);
-    if (he != hipSuccess) { e->release_ws(ws); return fail(OSE_EDEVICE, "hipStreamCreate failed"); }
-  }
-  hipStream_t st = ws->stream;
-  e->release_ws(ws);
+  hipStream_t st = e->take_stream();
+  if (!st) return fail(OSE_EDEVICE, "hipStreamCreate failed");
+  struct GiveBack {
+    Engine* e;
+    hipStream_t s;
+    ~GiveBack() { e->give_stream(s); }
+  } give_back{e, st};
   // sizes the shim may have shrunk after acquire (n_spans etc. <= capacity)
   b->cols_d.n_spans = b->cols_h.n_spans;
   b->cols_d.n_resources = b->cols_h.n_resources;

@@ -186,13 +186,14 @@ int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32
 // ---------------- engine ----------------
 Engine::~Engine() {
   for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+  for (auto s : streams) (void)hipStreamDestroy(s);
   for (auto ev : event_pool) (void)hipEventDestroy(ev);
   if (url_blob_dev) (void)hipFree(url_blob_dev);
   if (sampling_blob_dev) (void)hipFree(sampling_blob_dev);
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
     if (w->table) (void)hipFree(w->table);
-    if (w->stream) (void)hipStreamDestroy(w->stream);
+    if (w->pending) (void)hipEventDestroy(w->pending);
     delete w;
   }
 }
@@ -222,20 +223,46 @@ void Engine::prof_end(Timed& t, hipStream_t st) {
   timed.push_back(t);
 }
 
-Workspace* Engine::acquire_ws() {
-  std::lock_guard<std::mutex> g(mu);
-  if (!free_ws.empty()) {
-    Workspace* w = free_ws.back();
-    free_ws.pop_back();
-    return w;
+// Stream-ordered pool: work enqueued on a workspace may still be running
+// when the call returns (ose_process_device is asynchronous), so release
+// records an event on the caller's stream and the next user of that
+// workspace makes its own stream wait for it.
+Workspace* Engine::acquire_ws(hipStream_t st) {
+  Workspace* w = nullptr;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if (!free_ws.empty()) {
+      w = free_ws.back();
+      free_ws.pop_back();
+    } else {
+      w = new Workspace();
+      pool.push_back(w);
+    }
   }
-  Workspace* w = new Workspace();
-  pool.push_back(w);
+  if (w->pending_set) (void)hipStreamWaitEvent(st, w->pending, 0);
   return w;
 }
-void Engine::release_ws(Workspace* w) {
+void Engine::release_ws(Workspace* w, hipStream_t st) {
+  if (!w->pending) (void)hipEventCreateWithFlags(&w->pending, hipEventDisableTiming);
+  w->pending_set = w->pending && hipEventRecord(w->pending, st) == hipSuccess;
   std::lock_guard<std::mutex> g(mu);
   free_ws.push_back(w);
+}
+hipStream_t Engine::take_stream() {
+  std::lock_guard<std::mutex> g(mu);
+  if (!free_streams.empty()) {
+    hipStream_t s = free_streams.back();
+    free_streams.pop_back();
+    return s;
+  }
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  streams.push_back(s);
+  return s;
+}
+void Engine::give_stream(hipStream_t s) {
+  std::lock_guard<std::mutex> g(mu);
+  free_streams.push_back(s);
 }
 
 int Workspace::reserve(size_t bytes) {
@@ -354,8 +381,11 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
 int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
                const ose_rand* rnd, hipStream_t st) {
   if (!c || !o) return fail(OSE_EINVAL, "columns and outputs are required");
-  if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE)) return fail(OSE_EINVAL, "unknown stage bit");
-  Workspace* ws = e->acquire_ws();
+  if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE | OSE_STAGE_APPLY_KEEP))
+    return fail(OSE_EINVAL, "unknown stage bit");
+  if ((mask & OSE_STAGE_APPLY_KEEP) && (mask & OSE_STAGE_SAMPLE))
+    return fail(OSE_EINVAL, "OSE_STAGE_APPLY_KEEP and OSE_STAGE_SAMPLE exclude each other");
+  Workspace* ws = e->acquire_ws(st);
   // one reservation for every stage of the call: a stage must not reallocate
   // scratch an earlier stage of the same call is still using on the stream
   size_t need = 0;
@@ -368,7 +398,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   if (!rc && (mask & OSE_STAGE_TEMPLATE)) rc = run_url(e, c, o, st, ws);
   // odigostrafficmetrics runs last, on what the earlier stages left
   if (!rc && (mask & OSE_STAGE_SIZE)) rc = run_size(e, c, o, mask, group_mode, rnd, st, ws);
-  e->release_ws(ws);
+  e->release_ws(ws, st);
   return rc;
 }
 
@@ -454,10 +484,10 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   if (!eng) return fail(OSE_EINVAL, "NULL engine");
   (void)arena_bytes;
   Engine* e = reinterpret_cast<Engine*>(eng);
-  Workspace* ws = e->acquire_ws();
+  Workspace* ws = e->acquire_ws(nullptr);
   int rc = ws->reserve(e->workspace_bytes(n_spans));
   if (!rc && e->has_sampling) rc = ws->reserve_table(n_spans);
-  e->release_ws(ws);
+  e->release_ws(ws, nullptr);
   return rc;
 }
 

@@ -22,7 +22,8 @@ int ensure_device();
 struct Workspace {
   void* dev = nullptr;
   size_t cap = 0;
-  hipStream_t stream = nullptr;   // used by ose_process (host batches)
+  hipEvent_t pending = nullptr;   // recorded at release on the last user's stream
+  bool pending_set = false;
   int reserve(size_t bytes);
   // exact trace_id hash table of the SAMPLE stage (trace_kernel.hip), kept
   // across calls: entries carry a generation tag, so nothing is cleared
@@ -61,8 +62,11 @@ struct Engine {
   void prof_end(Timed& t, hipStream_t st);
 
   ~Engine();
-  Workspace* acquire_ws();
-  void release_ws(Workspace* w);
+  Workspace* acquire_ws(hipStream_t st);
+  void release_ws(Workspace* w, hipStream_t st);
+  std::vector<hipStream_t> streams, free_streams;   // ose_process (host batches)
+  hipStream_t take_stream();
+  void give_stream(hipStream_t s);
   int build_sampling_tables();
   size_t workspace_bytes(uint64_t n_spans) const;
 };

@@ -100,6 +100,7 @@ struct TraceKernelArgs {
   const uint32_t* key;        // kTracePerm: span -> canonical trace (first run-head position)
   uint32_t* error;            // bit0 spin timeout, bit2 trace table full
   uint32_t* batch_keep;       // kTraceBatch: the call's decision (read by the SIZE stage)
+  const uint64_t* route_match;// optional precomputed endpoint bits (ose_columns.route_match)
 };
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
 
@@ -155,6 +156,47 @@ struct TraceCompactArgs {
   double* trace_ratio;
 };
 void launch_trace_compact(const TraceCompactArgs& a, hipStream_t st);
+
+// Trace-id exchange (ose_shard_*; trace_kernel.hip).
+struct ShardArgs {
+  uint64_t n_spans;
+  uint32_t n_tiles;           // ceil(n / kSortTile)
+  uint32_t n_ranks;           // <= 64
+  const uint64_t* tid;
+  const uint64_t* start;
+  const uint64_t* end;
+  const uint8_t* status;
+  const uint32_t* resource;
+  const ose_strref* route;
+  const uint8_t* arena;
+  const uint64_t* route_match;
+  const uint32_t* res_svc;
+  const uint32_t* res_svc_str;
+  const uint8_t* cfg;         // SampCfgDev blob
+  uint32_t* hist;             // [n_ranks * n_tiles] counts, then offsets (second buffer)
+  uint32_t* hoff;
+  uint64_t* counts;           // [n_ranks] zeroed before launch
+  uint8_t* send;              // [n * kXRec]
+  uint32_t* pack_pos;         // [n]
+};
+constexpr uint32_t kXRec = 56;
+void launch_shard_hist(const ShardArgs& a, hipStream_t st);
+void launch_shard_scatter(const ShardArgs& a, hipStream_t st);
+struct UnpackArgs {
+  const uint8_t* recv;
+  uint64_t n;
+  uint64_t* tid;
+  uint64_t* start;
+  uint64_t* end;
+  uint8_t* status;
+  uint32_t* resource;
+  uint32_t* res_svc;
+  uint32_t* res_svc_str;
+  uint64_t* route_match;
+};
+void launch_shard_unpack(const UnpackArgs& a, hipStream_t st);
+void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);
+uint32_t shard_owner_host(uint64_t hi, uint64_t lo, uint32_t n_ranks);
 
 // Workspace words shared between stages of one call (uint32 index into the
 // first 256 bytes of the workspace; URL uses words 0-3, SAMPLE 0-15).

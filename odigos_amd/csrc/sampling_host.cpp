@@ -178,8 +178,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
       return fail(OSE_EINVAL, "SAMPLE stage needs status, resource, res_svc, res_svc_str and keep");
     if (!c->trace_id && (group_mode == OSE_GROUP_TRACE_ID || o->trace_keep || o->trace_level || o->trace_ratio))
       return fail(OSE_EINVAL, "SAMPLE stage needs the trace_id column");
-    if (lat && (!c->start_ns || !c->end_ns || !c->route || !c->arena))
-      return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns, route and arena");
+    if (lat && (!c->start_ns || !c->end_ns || (!c->route_match && (!c->route || !c->arena))))
+      return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns and route + arena (or route_match)");
   } else if (!c->res_svc_str && c->n_resources) {
     return fail(OSE_EINVAL, "SAMPLE stage needs res_svc_str");
   }
@@ -252,6 +252,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.dup = misc;
   a.error = err;
   a.batch_keep = misc + kBatchKeepWord;
+  a.route_match = c->route_match;
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);
   launch_trace_eval(a, st);

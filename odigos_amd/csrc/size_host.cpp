@@ -32,7 +32,9 @@ int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mas
   if (n && (!c->span_size || !c->scope)) return fail(OSE_EINVAL, "SIZE stage needs span_size and scope");
   if (c->n_scopes && (!c->scope_size || !c->scope_resource)) return fail(OSE_EINVAL, "SIZE stage needs scope_size and scope_resource");
   if (c->n_resources && (!c->res_size || !c->res_attrset)) return fail(OSE_EINVAL, "SIZE stage needs res_size and res_attrset");
-  const bool sampled = mask & OSE_STAGE_SAMPLE, templated = mask & OSE_STAGE_TEMPLATE;
+  const bool applied = mask & OSE_STAGE_APPLY_KEEP;   // decisions made by an earlier call
+  const bool sampled = (mask & OSE_STAGE_SAMPLE) || applied, templated = mask & OSE_STAGE_TEMPLATE;
+  if (applied && n && !o->keep) return fail(OSE_EINVAL, "OSE_STAGE_APPLY_KEEP needs keep");
   if (templated && n && (!c->kind || !c->name_len || !o->url_out || !o->tmpl))
     return fail(OSE_EINVAL, "SIZE after TEMPLATE needs kind, name_len, url_out and tmpl");
   // if p.samplingFraction != 0 && rand.Float64() < p.samplingFraction (processor.go:72)
@@ -55,8 +57,8 @@ int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mas
   a.n_attrsets = c->n_attrsets;
   a.sampled = sampled;
   a.templated = templated;
-  a.remove_empty = sampled && group_mode == OSE_GROUP_TRACE_ID;
-  a.batch_keep = sampled && group_mode == OSE_GROUP_BATCH ? reinterpret_cast<const uint32_t*>(base) + kBatchKeepWord : nullptr;
+  a.remove_empty = applied || (sampled && group_mode == OSE_GROUP_TRACE_ID);
+  a.batch_keep = !applied && sampled && group_mode == OSE_GROUP_BATCH ? reinterpret_cast<const uint32_t*>(base) + kBatchKeepWord : nullptr;
   a.span_size = c->span_size;
   a.name_len = c->name_len;
   a.scope = c->scope;

@@ -117,6 +117,19 @@ __device__ __forceinline__ bool route_has_prefix(const uint8_t* arena, ose_strre
   return true;
 }
 
+// Endpoint bits of one span: the latency rules of its service whose
+// http_route prefixes the span's AsString(http.route).
+__device__ __forceinline__ uint64_t endpoint_bits(const Cfg& c, uint32_t slot, const uint8_t* arena, ose_strref rt) {
+  uint64_t rules = c.slot_rules[slot], ep = 0;
+  while (rules) {
+    const int k = ffs64(rules);
+    rules &= rules - 1;
+    const SampLatDev& L = c.lat[k];
+    if (route_has_prefix(arena, rt, c.bytes + L.route_off, L.route_len)) ep |= 1ull << k;
+  }
+  return ep;
+}
+
 // Latency rules of `slot` that matched (endpoint found) and whose duration
 // reaches the threshold.  Duration: maxEnd.AsTime().Sub(minStart.AsTime())
 // .Milliseconds() — int64 ns difference saturated like time.Sub, truncated.
@@ -400,14 +413,7 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
       if (s < nsvc) {
         slot = c.svc_slot[s];
         if (slot != kNoSlot) {
-          uint64_t rules = c.slot_rules[slot];
-          const ose_strref rt = a.route[i];
-          while (rules) {
-            const int k = ffs64(rules);
-            rules &= rules - 1;
-            const SampLatDev& L = c.lat[k];
-            if (route_has_prefix(a.arena, rt, c.bytes + L.route_off, L.route_len)) ep |= 1ull << k;
-          }
+          ep = a.route_match ? a.route_match[i] & c.slot_rules[slot] : endpoint_bits(c, slot, a.arena, a.route[i]);
           st = a.start[i];
           en = a.end[i];
         }
@@ -671,7 +677,141 @@ __global__ __launch_bounds__(kTThreads) void trace_compact_kernel(TraceCompactAr
   if (a.trace_ratio) a.trace_ratio[t] = r.ratio;
 }
 
+// ---- trace-id exchange ---------------------------------------------------------
+__device__ __forceinline__ uint32_t shard_owner(uint64_t hi, uint64_t lo, uint32_t n) {
+  return (uint32_t)((tid_hash(hi, lo) >> 32) % n);
+}
+
+__global__ __launch_bounds__(kSortThreads) void shard_hist_kernel(ShardArgs a) {
+  __shared__ uint32_t hist[64];
+  const int t = threadIdx.x;
+  if (t < 64) hist[t] = 0;
+  __syncthreads();
+  const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
+  for (int r = 0; r < kSortRounds; r++) {
+    const uint64_t j = b + (uint64_t)r * kSortThreads + t;
+    if (j < a.n_spans) atomicAdd(&hist[shard_owner(a.tid[2 * j], a.tid[2 * j + 1], a.n_ranks)], 1u);
+  }
+  __syncthreads();
+  if ((uint32_t)t < a.n_ranks) {
+    a.hist[(uint64_t)t * a.n_tiles + blockIdx.x] = hist[t];
+    if (hist[t]) atomicAdd((unsigned long long*)&a.counts[t], (unsigned long long)hist[t]);
+  }
+}
+
+// Stable bucketing by owner (the radix-sort scatter with the owner as the
+// digit) plus the record the trace stage reads on the owner GPU.
+__global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a) {
+  __shared__ uint32_t goff[64], run[64];
+  __shared__ uint32_t wcnt[kSortThreads / kWave][64], woff[kSortThreads / kWave][64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t < 64) {
+    goff[t] = (uint32_t)t < a.n_ranks ? a.hoff[(uint64_t)t * a.n_tiles + blockIdx.x] : 0;
+    run[t] = 0;
+    for (int k = 0; k < kSortThreads / kWave; k++) wcnt[k][t] = 0;
+  }
+  __syncthreads();
+  const Cfg c = load_cfg(a.cfg);
+  const uint32_t nsvc = c.h->n_services;
+  const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
+  for (int r = 0; r < kSortRounds; r++) {
+    const uint64_t j = b + (uint64_t)r * kSortThreads + t;
+    const bool valid = j < a.n_spans;
+    uint64_t hi = 0, lo = 0;
+    uint32_t d = 0;
+    if (valid) {
+      hi = a.tid[2 * j];
+      lo = a.tid[2 * j + 1];
+      d = shard_owner(hi, lo, a.n_ranks);
+    }
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 6; bit++) {
+      const uint64_t bal = __ballot((d >> bit) & 1u);
+      peers &= ((d >> bit) & 1u) ? bal : ~bal;
+    }
+    const uint32_t rank = __popcll(peers & lanemask_lt(lane));
+    const uint32_t cnt = __popcll(peers);
+    if (valid && rank == cnt - 1) wcnt[wv][d] = cnt;
+    __syncthreads();
+    if (t < 64) {
+      uint32_t acc = run[t];
+      for (int k2 = 0; k2 < kSortThreads / kWave; k2++) {
+        woff[k2][t] = acc;
+        acc += wcnt[k2][t];
+        wcnt[k2][t] = 0;
+      }
+      run[t] = acc;
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t pos = goff[d] + woff[wv][d] + rank;
+      const uint32_t res = a.resource[j];
+      const uint32_t s = a.res_svc[res], ss = a.res_svc_str[res];
+      uint64_t ep = 0;
+      if (s < nsvc) {
+        const uint32_t slot = c.svc_slot[s];
+        if (slot != kNoSlot)
+          ep = a.route_match ? a.route_match[j] & c.slot_rules[slot] : endpoint_bits(c, slot, a.arena, a.route[j]);
+      }
+      uint64_t* rec = reinterpret_cast<uint64_t*>(a.send + (uint64_t)pos * kXRec);
+      rec[0] = hi;
+      rec[1] = lo;
+      rec[2] = a.start ? a.start[j] : 0;
+      rec[3] = a.end ? a.end[j] : 0;
+      rec[4] = ep;
+      rec[5] = (uint64_t)s | ((uint64_t)ss << 32);
+      rec[6] = a.status[j];
+      a.pack_pos[j] = pos;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t* rec = reinterpret_cast<const uint64_t*>(a.recv + i * kXRec);
+  a.tid[2 * i] = rec[0];
+  a.tid[2 * i + 1] = rec[1];
+  a.start[i] = rec[2];
+  a.end[i] = rec[3];
+  a.route_match[i] = rec[4];
+  const uint64_t sv = rec[5];
+  a.res_svc[i] = (uint32_t)sv;
+  a.res_svc_str[i] = (uint32_t)(sv >> 32);
+  a.status[i] = (uint8_t)rec[6];
+  a.resource[i] = (uint32_t)i;   // one "resource" per received span carries its service ids
+}
+
+__global__ __launch_bounds__(256) void scatter_keep_kernel(const uint8_t* back, const uint32_t* pos, uint64_t n,
+                                                           uint8_t* keep) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) keep[i] = back[pos[i]];
+}
+
 }  // namespace
+
+uint32_t shard_owner_host(uint64_t hi, uint64_t lo, uint32_t n) {
+  auto sm = [](uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  return (uint32_t)((sm(hi ^ sm(lo)) >> 32) % n);
+}
+void launch_shard_hist(const ShardArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(shard_hist_kernel, dim3(a.n_tiles), dim3(kSortThreads), 0, st, a);
+}
+void launch_shard_scatter(const ShardArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(shard_scatter_kernel, dim3(a.n_tiles), dim3(kSortThreads), 0, st, a);
+}
+void launch_shard_unpack(const UnpackArgs& a, hipStream_t st) {
+  if (a.n) hipLaunchKernelGGL(shard_unpack_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, st, a);
+}
+void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(scatter_keep_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, back, pos, n, keep);
+}
 
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t blocks = (a.n_windows + kTWaves - 1) / kTWaves;

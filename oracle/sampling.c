@@ -25,12 +25,16 @@
 struct orc_sampling {
   int n;
   orc_rule* rules;   /* copies; route strings owned */
+  int* lat_index;    /* index of each http_latency rule among them (route_match bit) */
 };
 
 orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules) {
   orc_sampling* s = (orc_sampling*)calloc(1, sizeof *s);
   s->n = n_rules;
   s->rules = (orc_rule*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(orc_rule));
+  s->lat_index = (int*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(int));
+  int nl = 0;
+  for (int i = 0; i < n_rules; i++) s->lat_index[i] = rules[i].type == ORC_RULE_LATENCY ? nl++ : -1;
   for (int i = 0; i < n_rules; i++) {
     s->rules[i] = rules[i];
     char* r = (char*)malloc(rules[i].route_len + 1);
@@ -45,6 +49,7 @@ void orc_sampling_free(orc_sampling* s) {
   if (!s) return;
   for (int i = 0; i < s->n; i++) free((void*)s->rules[i].route);
   free(s->rules);
+  free(s->lat_index);
   free(s);
 }
 
@@ -85,7 +90,7 @@ static int64_t go_sub_ns(int64_t t, int64_t u) {
   return d;
 }
 
-static eval_t eval_latency(const orc_rule* r, const trace_view* t) {
+static eval_t eval_latency(const orc_rule* r, int lat_index, const trace_view* t) {
   const ose_columns* c = t->c;
   int service_found = 0, endpoint_found = 0;
   uint64_t min_start = 0, max_end = 0;   /* pcommon.Timestamp sentinels */
@@ -94,9 +99,13 @@ static eval_t eval_latency(const orc_rule* r, const trace_view* t) {
     /* AsString(service.name) != ServiceName -> skip the resource (latency.go:51-56) */
     if (c->res_svc[c->resource[i]] != r->svc || r->svc == OSE_NONE) continue;
     service_found = 1;
-    ose_strref rt = c->route[i];   /* AsString(http.route); absent == "" here */
-    if (rt.len >= r->route_len && memcmp(c->arena + rt.off, r->route, r->route_len) == 0)
-      endpoint_found = 1;   /* strings.HasPrefix (latency.go:97-100) */
+    if (c->route_match) {   /* precomputed HasPrefix bits (ose_columns.route_match) */
+      if ((c->route_match[i] >> lat_index) & 1) endpoint_found = 1;
+    } else {
+      ose_strref rt = c->route[i];   /* AsString(http.route); absent == "" here */
+      if (rt.len >= r->route_len && memcmp(c->arena + rt.off, r->route, r->route_len) == 0)
+        endpoint_found = 1;   /* strings.HasPrefix (latency.go:97-100) */
+    }
     uint64_t s = c->start_ns[i], e = c->end_ns[i];
     if (min_start == 0 || s < min_start) min_start = s;
     if (max_end == 0 || e > max_end) max_end = e;
@@ -136,7 +145,7 @@ static void evaluate_level(const orc_sampling* s, int level, const trace_view* t
     eval_t e;
     switch (r->type) {
       case ORC_RULE_ERROR: e = eval_error(r, t); break;
-      case ORC_RULE_LATENCY: e = eval_latency(r, t); break;
+      case ORC_RULE_LATENCY: e = eval_latency(r, s->lat_index[k], t); break;
       default: e = eval_service(r, t); break;
     }
     if (e.satisfied) {

@@ -59,9 +59,9 @@ int orc_size_process(const ose_columns* c, const ose_outputs* res, uint32_t stag
   const uint32_t R = c->n_resources, S = c->n_scopes;
   /* if p.samplingFraction != 0 && rand.Float64() < p.samplingFraction (processor.go:72) */
   if (!(sampling_ratio != 0 && traffic_u < sampling_ratio)) return 0;
-  const int sampled = (stages & OSE_STAGE_SAMPLE) != 0;
+  const int sampled = (stages & (OSE_STAGE_SAMPLE | OSE_STAGE_APPLY_KEEP)) != 0;
   if (o->res_bytes) memset(o->res_bytes, 0, (size_t)R * sizeof(uint64_t));
-  if (sampled && group_mode == OSE_GROUP_BATCH && !res->trace_keep[0]) return 0;   /* td emptied */
+  if ((stages & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_BATCH && !res->trace_keep[0]) return 0;   /* td emptied */
   uint64_t* sbody = (uint64_t*)calloc(S ? S : 1, sizeof(uint64_t));
   uint8_t* shad = (uint8_t*)calloc(S ? S : 1, 1);
   uint64_t* skept = (uint64_t*)calloc(S ? S : 1, sizeof(uint64_t));
