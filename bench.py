@@ -111,7 +111,7 @@ def algorithmic_bytes_sampling(gen, db, n, cfg) -> int:
     return n * (16 + 8 + 8 + 1 + 4 + 8 + 1) + gen.cols.n_resources * 8 + rb
 
 
-def cpu_baseline_url(gen, cfg, threads: int, budget_s: float = 12.0):
+def cpu_baseline_url(gen, cfg, threads: int, budget_s: float = 12.0, calls: int = 1):
     """Oracle (oracle/url.c, -O3) on the same batch: `threads` pthreads over
     the whole batch, repeated until ~budget_s of wall time; plus one
     single-thread pass over a 1M-span prefix."""
@@ -141,7 +141,7 @@ def cpu_baseline_url(gen, cfg, threads: int, budget_s: float = 12.0):
     return mt, st, sample, parity
 
 
-def cpu_baseline_fused(gen, cfg, threads: int, budget_s: float = 12.0):
+def cpu_baseline_fused(gen, cfg, threads: int, budget_s: float = 12.0, calls: int = 1):
     """The three oracles chained in gateway order (sampling -> templating ->
     size; oracle/{sampling,url,size}.c -O3, pthreads for the first two) on a
     2M-span prefix of the same batch, repeated to ~budget_s/2.  Parity: keep,
@@ -178,11 +178,13 @@ def cpu_baseline_fused(gen, cfg, threads: int, budget_s: float = 12.0):
         A = gen.cols.n_attrsets
         return bool(np.array_equal(ho.view("keep", np.uint8)[:n], db.out_numpy("keep")[:n]) and
                     np.array_equal(ho.view("url_out", np.uint8)[:n], db.out_numpy("url_out")[:n]) and
-                    np.array_equal(ho.view("attrset_bytes", np.int64)[:A], db.out_numpy("attrset_bytes", np.int64)[:A]))
+                    # the device counters were ADDED to by every timed and warm-up call
+                    np.array_equal(calls * ho.view("attrset_bytes", np.int64)[:A],
+                                   db.out_numpy("attrset_bytes", np.int64)[:A]))
     return mt, st1, sample, parity
 
 
-def cpu_baseline_sampling(gen, cfg, threads: int, budget_s: float = 12.0):
+def cpu_baseline_sampling(gen, cfg, threads: int, budget_s: float = 12.0, calls: int = 1):
     """Oracle (oracle/sampling.c, -O3: trace_id grouping + per-trace rule
     fold) on a 5M-span prefix of the same batch, `threads` pthreads for the
     fold, repeated to ~budget_s/2; plus a single-thread pass over 1M spans.
@@ -361,7 +363,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         fn = {"url": cpu_baseline_url, "sampling": cpu_baseline_sampling, "fused": cpu_baseline_fused}[args.workload]
-        mt, st, sample, parity = fn(gen, cfg, threads)
+        mt, st, sample, parity = fn(gen, cfg, threads, calls=args.steps + args.warmup)
         out["cpu_baseline"] = {"value": mt, "unit": "spans/s", "cores": threads, "kind": "port",
                                "sample": sample, "value_1core": st}
         # the CPU pass doubles as a parity spot-check of the timed GPU output

@@ -101,6 +101,7 @@ struct TraceKernelArgs {
   uint32_t* error;            // bit0 spin timeout, bit2 trace table full
   uint32_t* batch_keep;       // kTraceBatch: the call's decision (read by the SIZE stage)
   const uint64_t* route_match;// optional precomputed endpoint bits (ose_columns.route_match)
+  uint32_t ablate;            // diagnostics only (OSE_TRACE_ABLATE, tools/ablate_trace.py): skip parts
 };
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
 

@@ -1,6 +1,7 @@
 // sampling_host.cpp — odigossampling: rule tables (built once per engine)
 // and the launch sequence of the trace stage (trace_kernel.hip).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "devcfg.hpp"
@@ -253,6 +254,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.error = err;
   a.batch_keep = misc + kBatchKeepWord;
   a.route_match = c->route_match;
+  if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);
   launch_trace_eval(a, st);

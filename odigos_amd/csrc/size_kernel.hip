@@ -15,6 +15,7 @@
 //                histogram -> one global atomic per non-empty bin per block
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "device_common.hpp"
@@ -63,9 +64,30 @@ __device__ __forceinline__ bool wave_seg_sum(uint32_t key, bool valid, T& v, uin
   return last;
 }
 
+__device__ __forceinline__ uint32_t size_span_tile(const SizeKernelArgs& a, uint64_t i);
+
+// Grid-stride over 256-span tiles (a capped grid: the surviving-span count
+// is reduced per block and added with ONE atomic per block — a per-wave
+// atomic on that single word serialises at the memory side).
 __global__ __launch_bounds__(kSThreads) void size_span_kernel(SizeKernelArgs a) {
   if (batch_dropped(a)) return;
-  const uint64_t i = (uint64_t)blockIdx.x * kSThreads + threadIdx.x;
+  __shared__ uint32_t wk[kSThreads / kWave];
+  uint32_t kept_total = 0;
+  for (uint64_t base = (uint64_t)blockIdx.x * kSThreads; base < a.n_spans; base += (uint64_t)gridDim.x * kSThreads) {
+    kept_total += size_span_tile(a, base + threadIdx.x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kept_total += __shfl_xor(kept_total, o, kWave);
+  if ((threadIdx.x & 63) == 0) wk[threadIdx.x >> 6] = kept_total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t k = 0;
+    for (int w = 0; w < kSThreads / kWave; w++) k += wk[w];
+    if (k) atomicAdd((unsigned long long*)a.accepted, (unsigned long long)k);
+  }
+}
+
+__device__ __forceinline__ uint32_t size_span_tile(const SizeKernelArgs& a, uint64_t i) {
   const bool valid = i < a.n_spans;
   uint32_t s = 0, kept = 0;
   uint64_t contrib = 0;
@@ -97,11 +119,7 @@ __global__ __launch_bounds__(kSThreads) void size_span_kernel(SizeKernelArgs a) 
     if (c) atomicAdd(&a.scope_kept[s], c);
     a.scope_had[s] = 1;
   }
-  // SpanCount of the surviving batch
-  uint32_t k = kept;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, kWave);
-  if ((threadIdx.x & 63) == 0 && k) atomicAdd((unsigned long long*)a.accepted, (unsigned long long)k);
+  return kept;
 }
 
 __global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a) {
@@ -160,7 +178,7 @@ __global__ __launch_bounds__(kSThreads) void size_res_kernel(SizeKernelArgs a) {
 }  // namespace
 
 void launch_size_spans(const SizeKernelArgs& a, hipStream_t st) {
-  const uint64_t blocks = (a.n_spans + kSThreads - 1) / kSThreads;
+  const uint64_t blocks = std::min<uint64_t>((a.n_spans + kSThreads - 1) / kSThreads, 2048);
   if (blocks) hipLaunchKernelGGL(size_span_kernel, dim3((uint32_t)blocks), dim3(kSThreads), 0, st, a);
 }
 void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st) {

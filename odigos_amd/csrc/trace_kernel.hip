@@ -366,7 +366,7 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
   const uint64_t heads0 = __ballot(sc.head);
   if (lane == 0 && a.win_heads) a.win_heads[w] = heads0;
   if (!heads0) return;
-  if (a.mode == kTraceRuns && sc.head) table_insert(a, sc.hi, sc.lo, (uint32_t)(p0 + lane));
+  if (a.mode == kTraceRuns && sc.head && !(a.ablate & 1)) table_insert(a, sc.hi, sc.lo, (uint32_t)(p0 + lane));
 
   // carried (open) trace: wave-uniform masks + one lane per latency slot
   bool open = false;
@@ -413,7 +413,8 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
       if (s < nsvc) {
         slot = c.svc_slot[s];
         if (slot != kNoSlot) {
-          ep = a.route_match ? a.route_match[i] & c.slot_rules[slot] : endpoint_bits(c, slot, a.arena, a.route[i]);
+          if (!(a.ablate & 8))
+            ep = a.route_match ? a.route_match[i] & c.slot_rules[slot] : endpoint_bits(c, slot, a.arena, a.route[i]);
           st = a.start[i];
           en = a.end[i];
         }
@@ -422,6 +423,7 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
     // ---- segmented OR of the flag masks ----
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
+      if (a.ablate & 16) break;
       const uint32_t oe = __shfl_up(err, d, kWave);
       const uint64_t oep = __shfl_up(ep, d, kWave), osv = __shfl_up(svcb, d, kWave);
       if (lane >= d && lane - d >= sst) {
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
     Lat nxt{0, kInf, 0};
     const bool carried_tail = (lane == t0 && seg0_cont) || (lane == last_own && last_open);
     const uint64_t ep0 = rdl64(ep, t0), epl = rdl64(ep, last_own);
-    uint64_t pend = __ballot(slot != kNoSlot);
+    uint64_t pend = (a.ablate & 2) ? 0 : __ballot(slot != kNoSlot);
     while (pend) {
       const uint32_t ks = rdl(slot, ffs64(pend));
       const bool ink = slot == ks;
@@ -472,7 +474,7 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
     uint8_t dk = 0, dl = 0;
     double dr = 0;
     const uint64_t hh = __shfl(sc.hi, sst, kWave), hl = __shfl(sc.lo, sst, kWave);
-    if (tail && !carried_tail) {
+    if (tail && !carried_tail && !(a.ablate & 4)) {
       decide(c, err, ep, lsat, a.mode == kTraceBatch ? batch_svc : svcb, trace_uniform(hh, hl, a.seed), dk, dl, dr);
       write_rec(a, base + sst, dk, dl, dr);
     }

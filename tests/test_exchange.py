@@ -145,7 +145,7 @@ def test_gpu_shard_kernels_vs_emulation():
     torch.cuda.synchronize()
     hc = unpack(rec.view(np.uint8))
     for k in cols:
-        np.testing.assert_array_equal(cols[k].cpu().numpy(), hc.a[k][: n * 1].view(np.uint8)[: cols[k].numel()])
+        np.testing.assert_array_equal(cols[k].cpu().numpy(), hc.a[k].view(np.uint8)[: cols[k].numel()])
 
 
 @pytest.mark.gpu
