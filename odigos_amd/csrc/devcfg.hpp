@@ -64,6 +64,7 @@ namespace ose {
 enum : uint32_t { kSampError = 0, kSampLatency = 1, kSampService = 2 };
 constexpr uint32_t kMaxLatencyRules = 64;   // bits of the per-trace latency masks
 constexpr uint32_t kMaxServiceRules = 64;   // bits of the per-trace service mask
+constexpr uint32_t kSampCfgLds = 12288;     // the trace kernel keeps the whole table blob in LDS
 struct SampRuleDev {
   uint32_t type;
   uint32_t bit;          // latency: latency-rule index; service: service-rule index
@@ -75,6 +76,9 @@ struct SampLatDev {      // one http_latency rule (latency.go:12-17)
   uint32_t route_off, route_len;   // http_route prefix bytes (bytes section)
   uint32_t _pad;
   int64_t threshold;     // ms
+  int64_t threshold_ns;  // threshold * 1e6, or INT64_MAX when that overflows (never satisfied)
+  uint32_t pre[4];       // first 16 prefix bytes, little-endian dwords, zero-padded
+  uint32_t msk[4];       // byte mask of the prefix within those 16 bytes
 };
 struct SampCfgDev {
   uint32_t n_rules;

@@ -193,6 +193,7 @@ Engine::~Engine() {
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
     if (w->table) (void)hipFree(w->table);
+    if (w->fp_table) (void)hipFree(w->fp_table);
     if (w->pending) (void)hipEventDestroy(w->pending);
     delete w;
   }

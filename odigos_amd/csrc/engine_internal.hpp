@@ -29,6 +29,8 @@ struct Workspace {
   // across calls: entries carry a generation tag, so nothing is cleared
   void* table = nullptr;
   uint64_t table_slots_cap = 0;
+  uint64_t* fp_table = nullptr;   // fast-path fingerprint cells
+  uint64_t fp_slots_cap = 0;
   uint32_t epoch = 0;
   int reserve_table(uint64_t n_spans);
 };

@@ -93,8 +93,10 @@ struct TraceKernelArgs {
   TraceRec* rec;              // [max(n,1)] or null (no per-trace outputs)
   uint64_t* win_heads;        // [n_windows] head bitmap of each window
   // slow path
-  TraceSlot* table;
+  TraceSlot* table;            // exact table (slow path)
   uint64_t table_mask;
+  uint64_t* fp_table;          // fingerprint cells (fast-path duplicate detection)
+  uint64_t fp_mask;
   uint32_t* dup;              // set by the fast path when a trace_id spans several runs
   const uint32_t* perm;       // kTracePerm: position -> span
   const uint32_t* key;        // kTracePerm: span -> canonical trace (first run-head position)
@@ -104,6 +106,7 @@ struct TraceKernelArgs {
   uint32_t ablate;            // diagnostics only (OSE_TRACE_ABLATE, tools/ablate_trace.py): skip parts
 };
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
+void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st);   // slow path, gated on *dup
 
 // Slow path (runs only when *dup != 0; every launch checks the flag first).
 struct TraceSortArgs {

@@ -25,6 +25,14 @@ uint64_t table_slots(uint64_t n) {
   while (cap < 2 * n) cap <<= 1;
   return cap;
 }
+// Fingerprint cells: sized for the run heads of groupbytrace-ordered input
+// (~1 per 4 spans or fewer) so the table stays in the 256 MiB Infinity
+// Cache; an overfull probe sequence only sends the call down the exact path.
+uint64_t fp_slots(uint64_t n) {
+  uint64_t cap = 1024;
+  while (cap < n / 4) cap <<= 1;
+  return cap;
+}
 }  // namespace
 
 // Interns every service name a rule compares against (latency.go:55,
@@ -72,6 +80,13 @@ int Engine::build_sampling_tables() {
           ld.route_off = (uint32_t)bytes.size();
           ld.route_len = (uint32_t)r.latency.http_route.size();
           ld.threshold = r.latency.threshold;
+          // Milliseconds() >= threshold  <=>  ns >= threshold * 1e6 for threshold >= 1
+          // (truncation toward zero; Validate rejects threshold <= 0)
+          ld.threshold_ns = r.latency.threshold <= INT64_MAX / 1000000 ? r.latency.threshold * 1000000 : INT64_MAX;
+          for (uint32_t b = 0; b < 16 && b < ld.route_len; b++) {
+            ld.pre[b / 4] |= (uint32_t)(uint8_t)r.latency.http_route[b] << (8 * (b % 4));
+            ld.msk[b / 4] |= 0xFFu << (8 * (b % 4));
+          }
           bytes += r.latency.http_route;
           slot_rules[ld.slot] |= 1ull << d.bit;
           lat.push_back(ld);
@@ -118,6 +133,9 @@ int Engine::build_sampling_tables() {
   while (b.size() % 16) b.push_back(0);
   b.resize(b.size() + 16, 0);
   h.total_bytes = (uint32_t)b.size();
+  if (h.total_bytes > kSampCfgLds)
+    return fail(OSE_ENOTSUP, "odigossampling rule tables exceed " + std::to_string(kSampCfgLds) +
+                                 " bytes (the GPU trace stage keeps them in LDS): shorten http_route values or rules");
   std::memcpy(b.data(), &h, sizeof h);
   sampling_blob_host = std::move(b);
   sampling_n_lat = h.n_lat;
@@ -158,10 +176,15 @@ int Workspace::reserve_table(uint64_t n_spans) {
   const uint64_t slots = table_slots(n_spans);
   if (slots <= table_slots_cap) return 0;
   if (table) HIP_TRY(hipFree(table));
+  if (fp_table) HIP_TRY(hipFree(fp_table));
   table = nullptr;
+  fp_table = nullptr;
   table_slots_cap = 0;
   HIP_TRY(hipMalloc(&table, slots * sizeof(TraceSlot)));
   HIP_TRY(hipMemset(table, 0, slots * sizeof(TraceSlot)));
+  fp_slots_cap = fp_slots(n_spans);
+  HIP_TRY(hipMalloc(&fp_table, fp_slots_cap * sizeof(uint64_t)));
+  HIP_TRY(hipMemset(fp_table, 0, fp_slots_cap * sizeof(uint64_t)));
   table_slots_cap = slots;
   epoch = 0;
   return 0;
@@ -199,9 +222,15 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   if (group_mode == OSE_GROUP_TRACE_ID) {
     rc = ws->reserve_table(n);
     if (rc) return rc;
-    if (++ws->epoch >= (1u << 30)) {   // generation tags wrap: clear the table once
+    // generation tags: 30 bits in the exact table, 16 in the fingerprint
+    // cells; a table is cleared once when its tag wraps (0 is "never used")
+    if (++ws->epoch >= (1u << 30)) {
       HIP_TRY(hipMemsetAsync(ws->table, 0, ws->table_slots_cap * sizeof(TraceSlot), st));
       ws->epoch = 1;
+    }
+    if ((ws->epoch & 0xFFFFu) == 0) {
+      HIP_TRY(hipMemsetAsync(ws->fp_table, 0, ws->fp_slots_cap * sizeof(uint64_t), st));
+      ++ws->epoch;
     }
   }
   uint8_t* base = static_cast<uint8_t*>(ws->dev);
@@ -250,6 +279,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.win_heads = win_heads;
   a.table = static_cast<TraceSlot*>(ws->table);
   a.table_mask = ws->table_slots_cap ? ws->table_slots_cap - 1 : 0;
+  a.fp_table = ws->fp_table;
+  a.fp_mask = ws->fp_slots_cap - 1;
   a.dup = misc;
   a.error = err;
   a.batch_keep = misc + kBatchKeepWord;
@@ -273,6 +304,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     s.epoch = a.epoch;
     s.key = key;
     s.error = err;
+    launch_trace_insert_exact(a, st);
+    HIP_TRY(hipGetLastError());
     launch_trace_key(s, st);
     HIP_TRY(hipGetLastError());
     int bits = 1;

@@ -117,17 +117,54 @@ __device__ __forceinline__ bool route_has_prefix(const uint8_t* arena, ose_strre
   return true;
 }
 
+// The first 16 bytes of a string at arena offset `off` with `len` bytes:
+// one aligned dwordx4 load, a second only when the bytes cross into the next
+// 16-byte chunk (never past the string's own last chunk: the arena contract
+// pads allocations to 16 bytes), funnel-shifted with v_alignbyte.
+__device__ __forceinline__ uint4 head16(const uint8_t* arena, uint32_t off, uint32_t len) {
+  const uint8_t* b = arena + (off & ~15u);
+  const uint4 c0 = *reinterpret_cast<const uint4*>(b);
+  uint4 c1 = make_uint4(0, 0, 0, 0);
+  const uint32_t o = off & 15u;
+  if (o + (len < 16u ? len : 16u) > 16u) c1 = *reinterpret_cast<const uint4*>(b + 16);
+  const uint32_t q = o >> 2, sh = o & 3u;
+  const uint32_t d0 = c0.x, d1 = c0.y, d2 = c0.z, d3 = c0.w, d4 = c1.x, d5 = c1.y, d6 = c1.z, d7 = c1.w;
+  auto pick = [&](uint32_t j0, uint32_t j1, uint32_t j2, uint32_t j3) {   // d[k + q] for q = 0..3
+    return q == 0 ? j0 : q == 1 ? j1 : q == 2 ? j2 : j3;
+  };
+  const uint32_t e0 = pick(d0, d1, d2, d3), e1 = pick(d1, d2, d3, d4), e2 = pick(d2, d3, d4, d5),
+                 e3 = pick(d3, d4, d5, d6), e4 = pick(d4, d5, d6, d7);
+  return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
+                    __builtin_amdgcn_alignbyte(e3, e2, sh), __builtin_amdgcn_alignbyte(e4, e3, sh));
+}
+
 // Endpoint bits of one span: the latency rules of its service whose
-// http_route prefixes the span's AsString(http.route).
-__device__ __forceinline__ uint64_t endpoint_bits(const Cfg& c, uint32_t slot, const uint8_t* arena, ose_strref rt) {
+// http_route prefixes the span's AsString(http.route) (strings.HasPrefix,
+// latency.go:97-100): one 16-byte window of the route, compared under each
+// rule's byte mask; prefixes longer than 16 bytes finish bytewise.
+__device__ __forceinline__ uint64_t endpoint_bits_w(const Cfg& c, uint32_t slot, const uint8_t* arena, ose_strref rt,
+                                                    const uint4 w) {
   uint64_t rules = c.slot_rules[slot], ep = 0;
+  if (!rules || rt.len == 0) return 0;
   while (rules) {
     const int k = ffs64(rules);
     rules &= rules - 1;
     const SampLatDev& L = c.lat[k];
-    if (route_has_prefix(arena, rt, c.bytes + L.route_off, L.route_len)) ep |= 1ull << k;
+    if (rt.len < L.route_len) continue;
+    const bool head_ok = ((w.x & L.msk[0]) == L.pre[0]) && ((w.y & L.msk[1]) == L.pre[1]) &&
+                         ((w.z & L.msk[2]) == L.pre[2]) && ((w.w & L.msk[3]) == L.pre[3]);
+    if (!head_ok) continue;
+    if (L.route_len > 16) {
+      ose_strref tail{rt.off + 16, rt.len - 16};
+      if (!route_has_prefix(arena, tail, c.bytes + L.route_off + 16, L.route_len - 16)) continue;
+    }
+    ep |= 1ull << k;
   }
   return ep;
+}
+__device__ __forceinline__ uint64_t endpoint_bits(const Cfg& c, uint32_t slot, const uint8_t* arena, ose_strref rt) {
+  if (rt.len == 0 || !c.slot_rules[slot]) return 0;
+  return endpoint_bits_w(c, slot, arena, rt, head16(arena, rt.off, rt.len));
 }
 
 // Latency rules of `slot` that matched (endpoint found) and whose duration
@@ -139,19 +176,20 @@ __device__ __forceinline__ uint64_t latency_satisfied(const Cfg& c, uint32_t slo
   const int64_t t = (int64_t)e, u = (int64_t)(m == kInf ? 0 : m);
   int64_t d;
   if (__builtin_sub_overflow(t, u, &d)) d = t < u ? INT64_MIN : INT64_MAX;
-  const int64_t ms = d / 1000000;
+  // d / 1e6 >= threshold  <=>  d >= threshold_ns (no 64-bit division)
   uint64_t sat = 0;
   while (rules) {
     const int r = ffs64(rules);
     rules &= rules - 1;
-    if (ms >= c.lat[r].threshold) sat |= 1ull << r;
+    const int64_t tn = c.lat[r].threshold_ns;
+    if (tn != INT64_MAX && d >= tn) sat |= 1ull << r;
   }
   return sat;
 }
 
 // ShouldSample's level walk (rule_engine.go:55-83) over evaluateLevel's fold
 // (rule_engine.go:89-115).  level: 0..2 satisfied level, 3 min fallback, 4 none.
-__device__ inline void decide(const Cfg& c, uint32_t err, uint64_t ep, uint64_t lsat, uint64_t svc, double u,
+__device__ __forceinline__ void decide(const Cfg& c, uint32_t err, uint64_t ep, uint64_t lsat, uint64_t svc, double u,
                               uint8_t& keep, uint8_t& level, double& ratio_out) {
   bool have_min = false;
   double min_fb = 0;
@@ -259,57 +297,102 @@ __device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint6
   }
 }
 
-// Head of a run: position p starts a new trace in the evaluation order.
-struct StepCols {
-  bool valid;
-  uint64_t i;          // span index
-  uint64_t hi, lo;     // trace id (kTraceRuns / kTraceBatch)
-  bool head;
+// ---- per-step columns ---------------------------------------------------------
+// Raw loads of one 64-span step, issued one step ahead of their use (the
+// compiler places the waits at the first use, in the next iteration), so a
+// wave keeps two steps of HBM reads in flight.
+struct StepRaw {
+  uint64_t i;          // span index (perm[p] in kTracePerm)
+  uint64_t hi, lo;     // trace id
+  uint64_t ph, pl;     // lane 0: trace id of position p-1 (head test)
+  uint32_t k, pk;      // kTracePerm: canonical key of p and (lane 0) of p-1
+  uint32_t res;
+  uint32_t status;
+  ose_strref route;
+  uint64_t start, end;
 };
-__device__ __forceinline__ StepCols load_step(const TraceKernelArgs& a, uint64_t base, int lane) {
-  StepCols s;
+__device__ __forceinline__ StepRaw load_raw(const TraceKernelArgs& a, uint64_t base, int lane) {
+  StepRaw r{};
   const uint64_t p = base + lane;
-  s.valid = p < a.n_spans;
-  s.i = 0;
-  s.hi = s.lo = 0;
-  s.head = false;
-  uint64_t ph = 0, pl = 0;
+  const bool valid = p < a.n_spans;
+  if (!valid) return r;
   if (a.mode == kTracePerm) {
-    uint32_t k = 0;
-    if (s.valid) {
-      s.i = a.perm[p];
-      k = a.key[s.i];
-      s.hi = a.tid[2 * s.i];
-      s.lo = a.tid[2 * s.i + 1];
+    r.i = a.perm[p];
+    r.k = a.key[r.i];
+    if (lane == 0 && p > 0) r.pk = a.key[a.perm[p - 1]];
+  } else {
+    r.i = p;
+    if (lane == 0 && p > 0 && a.mode == kTraceRuns) {
+      r.ph = a.tid[2 * p - 2];
+      r.pl = a.tid[2 * p - 1];
     }
-    uint32_t pk = __shfl_up(k, 1, kWave);
-    if (lane == 0 && s.valid && p > 0) pk = a.key[a.perm[p - 1]];
-    s.head = s.valid && (p == 0 || pk != k);
-    return s;
   }
-  s.i = p;
-  if (s.valid) {
-    const uint4 v = reinterpret_cast<const uint4*>(a.tid)[p];
-    s.hi = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    s.lo = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  const uint4 v = reinterpret_cast<const uint4*>(a.tid)[r.i];
+  r.hi = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  r.lo = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  r.res = a.resource[r.i];
+  r.status = a.status[r.i];
+  if (a.start) {
+    r.start = a.start[r.i];
+    r.end = a.end[r.i];
   }
-  if (a.mode == kTraceBatch) {
-    s.head = s.valid && p == 0;
-    return s;
+  if (a.route) r.route = a.route[r.i];
+  return r;
+}
+// head flag of every lane of a step (all lanes take the shuffles)
+__device__ __forceinline__ bool step_head(const TraceKernelArgs& a, const StepRaw& r, uint64_t base, int lane) {
+  const uint64_t p = base + lane;
+  const bool valid = p < a.n_spans;
+  if (a.mode == kTracePerm) {
+    uint32_t pk = __shfl_up(r.k, 1, kWave);
+    if (lane == 0) pk = r.pk;
+    return valid && (p == 0 || pk != r.k);
   }
-  ph = __shfl_up(s.hi, 1, kWave);
-  pl = __shfl_up(s.lo, 1, kWave);
-  if (lane == 0 && s.valid && p > 0) {
-    ph = a.tid[2 * p - 2];
-    pl = a.tid[2 * p - 1];
+  uint64_t ph = __shfl_up(r.hi, 1, kWave), pl = __shfl_up(r.lo, 1, kWave);
+  if (lane == 0) {
+    ph = r.ph;
+    pl = r.pl;
   }
-  s.head = s.valid && (p == 0 || ph != s.hi || pl != s.lo);
-  return s;
+  if (a.mode == kTraceBatch) return valid && p == 0;
+  return valid && (p == 0 || ph != r.hi || pl != r.lo);
 }
 __device__ __forceinline__ bool head_at(const TraceKernelArgs& a, uint64_t p) {   // p < n, p > 0
   if (a.mode == kTraceBatch) return false;
   if (a.mode == kTracePerm) return a.key[a.perm[p]] != a.key[a.perm[p - 1]];
   return a.tid[2 * p] != a.tid[2 * p - 2] || a.tid[2 * p + 1] != a.tid[2 * p - 1];
+}
+
+// ---- fingerprint table (fast path duplicate detection) -----------------------
+// One 8-byte cell per slot: epoch (16 bits) | fingerprint (48 bits, never 0).
+// A run head claims an empty (stale-epoch) cell with one CAS; finding its own
+// fingerprint means the trace id (probably) formed an earlier run: *dup is
+// set and the exact, sort-based path recomputes every decision.  A 48-bit
+// collision between different trace ids only costs that slow path.
+__device__ __forceinline__ uint64_t fp_cell(const TraceKernelArgs& a, uint64_t hi, uint64_t lo) {
+  const uint64_t fp = ((splitmix64(lo ^ (hi << 1)) >> 16) | 1ull) & 0xFFFFFFFFFFFFull;
+  return ((uint64_t)(a.epoch & 0xFFFFu) << 48) | fp;
+}
+__device__ inline void fp_insert_cell(const TraceKernelArgs& a, uint64_t cell, uint64_t idx) {
+  const uint64_t ep = cell & ~0xFFFFFFFFFFFFull, fp = cell & 0xFFFFFFFFFFFFull;
+  for (uint32_t probes = 0; probes < 64; probes++) {
+    uint64_t* q = &a.fp_table[idx];
+    uint64_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if ((v & ~0xFFFFFFFFFFFFull) != ep) {
+        if (__hip_atomic_compare_exchange_strong(q, &v, cell, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          return;
+        continue;   // v now holds the current cell
+      }
+      break;
+    }
+    if ((v & 0xFFFFFFFFFFFFull) == fp) {
+      atomicOr(a.dup, 1u);
+      return;
+    }
+    idx = (idx + 1) & a.fp_mask;
+  }
+  atomicOr(a.dup, 1u);   // probe sequence too long: let the exact path decide
 }
 
 __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos, uint8_t keep, uint8_t level,
@@ -325,19 +408,85 @@ __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos
   a.rec[pos] = r;
 }
 
-__global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a) {
+// Run heads are collected per wave in LDS and inserted 64 at a time: each
+// insert is a load and a dependent CAS, so batching turns a per-step pair of
+// round trips into one pair per 64 heads.
+constexpr int kHeadQ = 128;
+struct HeadQ {
+  uint64_t cell[kHeadQ];
+  uint32_t idx[kHeadQ];
+};
+__device__ void flush_heads(const TraceKernelArgs& a, HeadQ& H, uint32_t& hn, int lane) {
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t b = 0; b < hn; b += kWave)
+    if (b + lane < hn) fp_insert_cell(a, H.cell[b + lane], H.idx[b + lane]);
+  __builtin_amdgcn_wave_barrier();
+  hn = 0;
+}
+
+// ---- decide queue ---------------------------------------------------------------
+// Closed traces are queued per wave in LDS and decided 64 at a time, so the
+// rule fold runs with every lane busy instead of once per trace tail.
+constexpr int kQ = 64;
+struct DecideQ {
+  uint64_t ep[kQ], lsat[kQ], svc[kQ], hi[kQ], lo[kQ];
+  uint32_t pos[kQ], len[kQ], err[kQ];
+};
+
+__device__ __forceinline__ void write_keep_range(const TraceKernelArgs& a, uint64_t pos, uint32_t len, uint8_t k,
+                                                 int lane) {
+  for (uint32_t q = lane; q < len; q += kWave) a.keep[a.mode == kTracePerm ? a.perm[pos + q] : pos + q] = k;
+}
+
+__device__ void flush_queue(const TraceKernelArgs& a, const Cfg& c, DecideQ& Q, uint32_t& qn, int lane) {
+  if (!qn) return;
+  __builtin_amdgcn_wave_barrier();
+  uint8_t dk = 0, dl = 0;
+  double dr = 0;
+  uint32_t pos = 0, len = 0;
+  if ((uint32_t)lane < qn) {
+    pos = Q.pos[lane];
+    len = Q.len[lane];
+    if (!(a.ablate & 4))
+      decide(c, Q.err[lane], Q.ep[lane], Q.lsat[lane], Q.svc[lane], trace_uniform(Q.hi[lane], Q.lo[lane], a.seed), dk,
+             dl, dr);
+    write_rec(a, pos, dk, dl, dr);
+  }
+  for (uint32_t e = 0; e < qn; e++)
+    write_keep_range(a, rdl(pos, e), rdl(len, e), (uint8_t)rdl(dk, e), lane);
+  __builtin_amdgcn_wave_barrier();
+  qn = 0;
+}
+
+constexpr int kWinPerWave = 8;   // 64-span windows whose run heads one wave owns
+
+__global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void trace_eval_kernel(TraceKernelArgs a) {
   if (a.mode == kTracePerm && __hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  __shared__ DecideQ queues[kTWaves];
+  __shared__ HeadQ headqs[kTWaves];
+  __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
   const int lane = threadIdx.x & 63;
-  const uint32_t w = blockIdx.x * kTWaves + (threadIdx.x >> 6);
-  if (w >= a.n_windows) return;
-  const Cfg c = load_cfg(a.cfg);
+  const uint32_t wv = threadIdx.x >> 6;
+  DecideQ& Q = queues[wv];
+  HeadQ& HQ = headqs[wv];
+  {
+    // the rule tables (<= kSampCfgLds bytes, checked by the host) live in LDS:
+    // every lookup below is a ds_read instead of a dependent L2 round trip
+    const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
+    for (uint32_t k = threadIdx.x * 16; k < nb; k += kTThreads * 16)
+      *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
+    __syncthreads();
+  }
+  const uint64_t w0 = ((uint64_t)blockIdx.x * kTWaves + wv) * kWinPerWave;   // first owned window
+  if (w0 >= a.n_windows) return;
+  const Cfg c = load_cfg(cfg_lds);
   const uint64_t n = a.n_spans;
   const uint32_t nsvc = c.h->n_services;
 
   // OSE_GROUP_BATCH: ServiceNameRule looks at every resource of the call,
   // spanless ones included (servicename.go:38-47).
   uint64_t batch_svc = 0;
-  if (a.mode == kTraceBatch && w == 0) {
+  if (a.mode == kTraceBatch && w0 == 0) {
     for (uint32_t r = lane; r < a.n_resources; r += kWave) {
       const uint32_t s = a.res_svc_str[r];
       if (s < nsvc) batch_svc |= c.svc_bits[s];
@@ -345,44 +494,79 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
     batch_svc = wave_or64(batch_svc);
   }
   if (n == 0) {   // kTraceBatch only: one trace with no spans
-    if (w == 0) {
-      uint8_t k, l;
-      double r;
-      decide(c, 0, 0, 0, batch_svc, trace_uniform(0, 0, a.seed), k, l, r);
-      if (lane == 0) {
-        if (a.batch_keep) *a.batch_keep = k;
-        if (a.win_heads) a.win_heads[0] = 1;
-        if (a.rec) {
-          TraceRec rr{0, k, l, 0, 0, r};
-          a.rec[0] = rr;
-        }
+    uint8_t k, l;
+    double r;
+    decide(c, 0, 0, 0, batch_svc, trace_uniform(0, 0, a.seed), k, l, r);
+    if (lane == 0) {
+      if (a.batch_keep) *a.batch_keep = k;
+      if (a.win_heads) a.win_heads[0] = 1;
+      if (a.rec) {
+        TraceRec rr{0, k, l, 0, 0, r};
+        a.rec[0] = rr;
       }
     }
     return;
   }
 
-  const uint64_t p0 = (uint64_t)w * kWave;
-  StepCols sc = load_step(a, p0, lane);
-  const uint64_t heads0 = __ballot(sc.head);
-  if (lane == 0 && a.win_heads) a.win_heads[w] = heads0;
-  if (!heads0) return;
-  if (a.mode == kTraceRuns && sc.head && !(a.ablate & 1)) table_insert(a, sc.hi, sc.lo, (uint32_t)(p0 + lane));
-
-  // carried (open) trace: wave-uniform masks + one lane per latency slot
-  bool open = false;
+  const uint64_t range_end = min((w0 + kWinPerWave) * kWave, n);
+  uint32_t qn = 0, hn = 0;
+  bool started = false, open = false;
   uint32_t c_err = 0;
   uint64_t c_ep = 0, c_svc = 0, c_kmask = 0, c_pos = 0, c_hi = 0, c_lo = 0;
   Lat cur{0, kInf, 0};
-  uint64_t base = p0;
-  const int own_from = ffs64(heads0);
+  uint64_t base = w0 * kWave;
+  const bool want_route = c.h->n_lat && !a.route_match && a.route;
+  StepRaw nx = load_raw(a, base, lane);
   for (;;) {
-    if (base != p0) sc = load_step(a, base, lane);
-    const uint64_t vmask = __ballot(sc.valid);
-    const uint64_t hmask = __ballot(sc.head);
+    // Order of the memory operations per step: this step's dependent loads
+    // (resource service ids, the route window, the fingerprint cell), then
+    // the next step's column loads, then the arithmetic — a wait for a load
+    // also waits for every load issued before it (vmcnt counts in order),
+    // so nothing this step consumes may be issued after the prefetch.
+    const StepRaw r = nx;
+    const bool valid = base + lane < n;
+    const bool hd = step_head(a, r, base, lane);
+    uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu;
+    uint4 rw = make_uint4(0, 0, 0, 0);
+    if (valid) {
+      sv = a.res_svc[r.res];
+      ss = a.res_svc_str[r.res];
+      if (want_route && r.route.len) rw = head16(a.arena, r.route.off, r.route.len);
+    }
+    const uint64_t vmask = __ballot(valid);
+    const uint64_t hmask = __ballot(hd);
+    const bool in_range = base < range_end;
+    if (in_range) {
+      if (lane == 0 && a.win_heads) a.win_heads[base / kWave] = hmask;
+      if (a.mode == kTraceRuns && !(a.ablate & 1) && hmask) {
+        const uint32_t nh = __popcll(hmask);
+        if (hn + nh > kHeadQ) flush_heads(a, HQ, hn, lane);
+        if (hd) {
+          const uint32_t e = hn + __popcll(hmask & lanemask_lt(lane));
+          HQ.cell[e] = fp_cell(a, r.hi, r.lo);
+          HQ.idx[e] = (uint32_t)(tid_hash(r.hi, r.lo) & a.fp_mask);
+        }
+        hn += nh;
+      }
+    }
+    if (base + kWave < n) nx = load_raw(a, base + kWave, lane);   // prefetch the next step
     uint64_t own;
-    if (base == p0) own = vmask & ~lanemask_lt(own_from);
-    else own = vmask & (hmask ? lanemask_lt(ffs64(hmask)) : ~0ull);
-    if (!own) break;
+    if (in_range) {
+      if (!started) {
+        if (!hmask) {   // still inside a trace an earlier wave owns
+          base += kWave;
+          if (base >= range_end) break;
+          continue;
+        }
+        started = true;
+        own = vmask & ~lanemask_lt(ffs64(hmask));
+      } else {
+        own = vmask;
+      }
+    } else {
+      if (!open) break;
+      own = vmask & (hmask ? lanemask_lt(ffs64(hmask)) : ~0ull);
+    }
     const uint64_t segmask = (hmask & own) | (open ? 1ull : 0ull);
     const int last_own = fls64(own);
     bool cont_next = false;
@@ -405,25 +589,23 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
     uint32_t err = 0, slot = kNoSlot;
     uint64_t ep = 0, svcb = 0, st = 0, en = 0;
     if (mine) {
-      const uint64_t i = sc.i;
-      const uint32_t r = a.resource[i];
-      const uint32_t s = a.res_svc[r], ss = a.res_svc_str[r];
-      err = a.status[i] == OSE_STATUS_ERROR;
+      const uint32_t s = sv;
+      err = r.status == OSE_STATUS_ERROR;
       if (a.mode != kTraceBatch && ss < nsvc) svcb = c.svc_bits[ss];
       if (s < nsvc) {
         slot = c.svc_slot[s];
         if (slot != kNoSlot) {
           if (!(a.ablate & 8))
-            ep = a.route_match ? a.route_match[i] & c.slot_rules[slot] : endpoint_bits(c, slot, a.arena, a.route[i]);
-          st = a.start[i];
-          en = a.end[i];
+            ep = a.route_match ? a.route_match[r.i] & c.slot_rules[slot]
+                               : endpoint_bits_w(c, slot, a.arena, r.route, rw);
+          st = r.start;
+          en = r.end;
         }
       }
     }
     // ---- segmented OR of the flag masks ----
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
-      if (a.ablate & 16) break;
       const uint32_t oe = __shfl_up(err, d, kWave);
       const uint64_t oep = __shfl_up(ep, d, kWave), osv = __shfl_up(svcb, d, kWave);
       if (lane >= d && lane - d >= sst) {
@@ -436,7 +618,6 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
     uint64_t lsat = 0, n_kmask = 0;
     Lat nxt{0, kInf, 0};
     const bool carried_tail = (lane == t0 && seg0_cont) || (lane == last_own && last_open);
-    const uint64_t ep0 = rdl64(ep, t0), epl = rdl64(ep, last_own);
     uint64_t pend = (a.ablate & 2) ? 0 : __ballot(slot != kNoSlot);
     while (pend) {
       const uint32_t ks = rdl(slot, ffs64(pend));
@@ -468,19 +649,8 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
         }
       }
     }
-    (void)ep0;
-    (void)epl;
-    // ---- decisions of the traces that start and end in this step ----
-    uint8_t dk = 0, dl = 0;
-    double dr = 0;
-    const uint64_t hh = __shfl(sc.hi, sst, kWave), hl = __shfl(sc.lo, sst, kWave);
-    if (tail && !carried_tail && !(a.ablate & 4)) {
-      decide(c, err, ep, lsat, a.mode == kTraceBatch ? batch_svc : svcb, trace_uniform(hh, hl, a.seed), dk, dl, dr);
-      write_rec(a, base + sst, dk, dl, dr);
-    }
-    // ---- the carried trace closes in this step ----
+    // ---- the carried trace closes in this step: queue it ----
     const bool cont_close = seg0_cont && !(single && cont_next);
-    uint8_t cdk = 0;
     if (cont_close) {
       const uint32_t E = c_err | rdl(err, t0);
       const uint64_t EP = c_ep | rdl64(ep, t0);
@@ -488,33 +658,47 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
       uint64_t s_l = 0;
       if ((c_kmask >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, cur.m, cur.e);
       s_l = wave_or64(s_l);
-      uint8_t cdl;
-      double cdr;
-      decide(c, E, EP, s_l, SV, trace_uniform(c_hi, c_lo, a.seed), cdk, cdl, cdr);
-      for (uint64_t q = c_pos + lane; q < base; q += kWave) a.keep[a.mode == kTracePerm ? a.perm[q] : q] = cdk;
-      if (lane == 0) write_rec(a, c_pos, cdk, cdl, cdr);
+      if (qn == kQ) flush_queue(a, c, Q, qn, lane);
+      if (lane == 0) {
+        Q.err[qn] = E;
+        Q.ep[qn] = EP;
+        Q.lsat[qn] = s_l;
+        Q.svc[qn] = SV;
+        Q.hi[qn] = c_hi;
+        Q.lo[qn] = c_lo;
+        Q.pos[qn] = (uint32_t)c_pos;
+        Q.len[qn] = (uint32_t)(base + t0 + 1 - c_pos);
+      }
+      qn++;
       open = false;
       cur = Lat{0, kInf, 0};
       c_kmask = 0;
     }
-    // ---- keep bytes of this step's spans ----
-    const int my_tail = mine ? ffs64(tails & ~lanemask_lt(lane)) : lane;
-    const uint8_t kd = (uint8_t)__shfl((uint32_t)dk, my_tail, kWave);
-    if (mine) {
-      const bool in_seg0c = seg0_cont && lane <= t0;
-      const bool in_lastopen = last_open && lane >= sst_last;
-      if (in_seg0c) {
-        if (cont_close) a.keep[sc.i] = cdk;
-      } else if (!in_lastopen) {
-        a.keep[sc.i] = kd;
+    // ---- traces that start and end in this step: queue them ----
+    const uint64_t qmask = __ballot(tail && !carried_tail);
+    const uint32_t nq = __popcll(qmask);
+    if (nq) {
+      if (qn + nq > kQ) flush_queue(a, c, Q, qn, lane);
+      const uint64_t hh = __shfl(r.hi, sst, kWave), hl = __shfl(r.lo, sst, kWave);
+      if ((qmask >> lane) & 1) {
+        const uint32_t e = qn + __popcll(qmask & lanemask_lt(lane));
+        Q.err[e] = err;
+        Q.ep[e] = ep;
+        Q.lsat[e] = lsat;
+        Q.svc[e] = a.mode == kTraceBatch ? batch_svc : svcb;
+        Q.hi[e] = hh;
+        Q.lo[e] = hl;
+        Q.pos[e] = (uint32_t)(base + sst);
+        Q.len[e] = (uint32_t)(lane - sst + 1);
       }
+      qn += nq;
     }
     // ---- carry into the next step ----
     if (last_open) {
       open = true;
       c_pos = base + sst_last;
-      c_hi = rdl64(sc.hi, sst_last);
-      c_lo = rdl64(sc.lo, sst_last);
+      c_hi = rdl64(r.hi, sst_last);
+      c_lo = rdl64(r.lo, sst_last);
       c_err = rdl(err, last_own);
       c_ep = rdl64(ep, last_own);
       c_svc = rdl64(svcb, last_own);
@@ -525,14 +709,28 @@ __global__ __launch_bounds__(kTThreads) void trace_eval_kernel(TraceKernelArgs a
       c_ep |= rdl64(ep, t0);
       c_svc |= rdl64(svcb, t0);
     }
-    if (!open) break;
     base += kWave;
+    if (!open && base >= range_end) break;
   }
+  flush_queue(a, c, Q, qn, lane);
+  flush_heads(a, HQ, hn, lane);
 }
 
 // ---- slow path ---------------------------------------------------------------
 __device__ __forceinline__ bool gated(const uint32_t* g) {
   return g && __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+}
+
+// Exact table of the slow path: every run head inserts its full trace id
+// (table_insert's publish protocol); a trace's entry keeps its smallest
+// run-head position.
+__global__ __launch_bounds__(256) void trace_insert_exact_kernel(TraceKernelArgs a) {
+  if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= a.n_spans) return;
+  const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
+  if (p > 0 && a.tid[2 * p - 2] == hi && a.tid[2 * p - 1] == lo) return;
+  table_insert(a, hi, lo, (uint32_t)p);
 }
 
 // key[i] = first run-head position of span i's trace_id (read-only probe of
@@ -816,8 +1014,13 @@ void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, u
 }
 
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
-  const uint32_t blocks = (a.n_windows + kTWaves - 1) / kTWaves;
+  const uint32_t per_block = kTWaves * kWinPerWave;
+  const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
   hipLaunchKernelGGL(trace_eval_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
+}
+void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st) {
+  if (a.n_spans)
+    hipLaunchKernelGGL(trace_insert_exact_kernel, dim3((uint32_t)((a.n_spans + 255) / 256)), dim3(256), 0, st, a);
 }
 void launch_trace_key(const TraceSortArgs& a, hipStream_t st) {
   const uint64_t blocks = (a.n_spans + 255) / 256;

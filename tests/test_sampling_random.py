@@ -258,3 +258,43 @@ def test_gpu_sampling_parity_full_c3():
     g = Generator("sampling", seed=0x0D160003, n_spans=50_000_000, threads=16)
     ho = gpu_vs_oracle(g, per_trace=True)
     assert int(ho.view("trace_count", np.uint32)[0]) > 4_000_000
+
+
+def long_prefix_config():
+    """http_route prefixes of every length 1..24 (crossing the 16-byte window
+    of the vectorised HasPrefix) over the generator's routes
+    /api/v{1,2}/<word>[/{id}][/<word>]."""
+    cfg = c3_sampling_config()
+    routes = ["/api/v1/users/{id}", "/api/v2/orders", "/api/v1/checkout/{id}/", "/api/v2/products/{id}",
+              "/api/v1/users", "/api/v2/", "/", "/api/v1/items/{id}", "/api/v2/cart/{id}/users",
+              "/api/v1/search/{id}", "/api/v1/settings/{id}", "/api/v2/billing/{id}", "/api/v1/invoices/{id}/",
+              "/api/v2/payments", "/api/v1/authx", "/api/v1/login/{id}/"]
+    for r, route in zip(cfg["endpoint_rules"], routes):
+        r["rule_details"]["http_route"] = route
+        r["rule_details"]["threshold"] = 1
+    return cfg
+
+
+def test_long_prefix_config_oracle_vs_python():
+    import ctypes as C
+    cfg = long_prefix_config()
+    g = Generator("sampling", seed=0x0D160203, n_spans=4000)
+    cols = g.cols
+    ho = oracle_run(cols, native.GROUP_TRACE_ID, cfg=cfg)
+    traces = _group(cols, False)
+    svc_ids = intern_services(cfg)
+    res = _arr(cols.resource, C.c_uint32, cols.n_spans)
+    tid = _arr(cols.trace_id, C.c_uint64, 2 * cols.n_spans).reshape(-1, 2)
+    matched = 0
+    for t, spans in enumerate(traces):
+        u = orc_lib().orc_trace_uniform(int(tid[spans[0], 0]), int(tid[spans[0], 1]), SEED)
+        k, lvl, ratio = _py_eval(cfg, svc_ids, cols, res, spans, False, u)
+        assert ho.view("trace_level", np.uint8)[t] == lvl and ho.view("trace_ratio", np.float64)[t] == ratio
+        matched += lvl == 2
+    assert matched > 0
+
+
+@pytest.mark.gpu
+def test_gpu_sampling_long_prefixes():
+    gpu_vs_oracle(Generator("sampling", seed=0x0D160063, n_spans=300_000), cfg=long_prefix_config())
+    gpu_vs_oracle(Generator("sampling", seed=0x0D160073, n_spans=100_000, shuffle=True), cfg=long_prefix_config())
