@@ -231,7 +231,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="url", choices=sorted(WORKLOADS))
+    # default: the whole hot path (C4 shard), which is also the configuration the
+    # multi-GPU runs exercise (trace-id exchange when N > 1); DESIGN.md §6
+    ap.add_argument("--workload", default="fused", choices=sorted(WORKLOADS))
     ap.add_argument("--spans", type=int, default=0, help="override spans per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
