@@ -153,6 +153,10 @@ typedef struct ose_columns {
                                   of the r-th http_latency rule) for the rules of the span's service
                                   (latency.go:64-68, 97-100); when non-NULL the engine reads it
                                   instead of route/arena (set by ose_shard_unpack)               */
+  const uint64_t* attr_match;  /* bit k = the span meets the k-th span_attribute rule (in level order):
+                                  its resource's AsString(service.name) is the rule's service_name and
+                                  its attribute satisfies the condition (spanattribute.go:126-320,
+                                  evaluated by the shim); required when such rules are configured */
 
   /* per resource */
   const uint32_t* res_svc;      /* ose_engine_service_id(AsString(service.name)) or OSE_NONE */
@@ -274,13 +278,14 @@ int ose_profile_read(ose_engine* eng, char* json, size_t cap);
  * the keep bytes go back with the reverse all-to-all, and
  * ose_shard_scatter_keep puts them at the original spans.  All pointers are
  * device pointers; calls are asynchronous on hip_stream.                    */
-#define OSE_XREC_BYTES 56u
+#define OSE_XREC_BYTES 64u
 uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks);
 int ose_shard_pack(ose_engine* eng, const ose_columns* cols, uint32_t n_ranks, void* send,
                    uint64_t* counts, uint32_t* pack_pos, void* hip_stream);
 int ose_shard_unpack(const void* recv, uint64_t n, uint64_t* trace_id, uint64_t* start_ns,
                      uint64_t* end_ns, uint8_t* status, uint32_t* resource, uint32_t* res_svc,
-                     uint32_t* res_svc_str, uint64_t* route_match, void* hip_stream);
+                     uint32_t* res_svc_str, uint64_t* route_match, uint64_t* attr_match,
+                     void* hip_stream);
 int ose_shard_scatter_keep(const uint8_t* keep_back, const uint32_t* pack_pos, uint64_t n,
                            uint8_t* keep, void* hip_stream);
 

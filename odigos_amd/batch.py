@@ -19,7 +19,7 @@ COLUMN_LAYOUT = {
     "trace_id": ("span", 16), "start_ns": ("span", 8), "end_ns": ("span", 8), "status": ("span", 1),
     "kind": ("span", 1), "resource": ("span", 4), "scope": ("span", 4), "url_flags": ("span", 1),
     "path": ("span", 8), "route": ("span", 8), "span_size": ("span", 4), "name_len": ("span", 4),
-    "route_match": ("span", 8),
+    "route_match": ("span", 8), "attr_match": ("span", 8),
     "res_svc": ("res", 4), "res_svc_str": ("res", 4), "res_url_ok": ("res", 1), "res_attrset": ("res", 4),
     "res_size": ("res", 4), "scope_size": ("scope", 4), "scope_resource": ("scope", 4),
 }

@@ -85,6 +85,7 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
   IN(route, 8 * n);
   IN(span_size, 4 * n);
   IN(name_len, 4 * n);   // route_match stays NULL: host batches carry route bytes
+  IN(attr_match, 8 * n);
   IN(res_svc, 4 * R);
   IN(res_svc_str, 4 * R);
   IN(res_url_ok, R);

@@ -49,7 +49,7 @@ struct Engine {
   std::vector<uint8_t> sampling_blob_host;
   uint8_t* sampling_blob_dev = nullptr;
   std::unordered_map<std::string, uint32_t> service_ids;
-  uint32_t sampling_n_lat = 0;
+  uint32_t sampling_n_lat = 0, sampling_n_attr = 0;
 
   std::mutex mu;
   std::vector<Workspace*> pool, free_ws;

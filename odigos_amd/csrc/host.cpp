@@ -6,6 +6,7 @@
 #include <cstring>
 #include <set>
 
+#include "span_attr.hpp"
 #include "urlparse.hpp"
 
 namespace ose {
@@ -43,6 +44,7 @@ void HostBatch::bind() {
   cols.res_size = res_size.data();
   cols.scope_size = scope_size.data();
   cols.scope_resource = scope_resource.data();
+  cols.attr_match = attr_match.data();
   outs.keep = keep.data();
   outs.trace_count = trace_count.data();
   outs.trace_first_span = trace_first_span.data();
@@ -105,6 +107,17 @@ TracesProcessor::TracesProcessor(ProcKind k, const Json& cfg) : kind_(k), cfg_js
       break;
   }
   if (has_sampling_) services_ = intern_services(sampling_);
+  if (err_.empty() && has_sampling_) {
+    // span_attribute conditions run here, per span, into attr_match (level order)
+    for (auto* lvl : {&sampling_.global_rules, &sampling_.service_rules, &sampling_.endpoint_rules})
+      for (auto& r : *lvl)
+        if (r.rtype == RuleType::SpanAttribute) {
+          attr_preds_.emplace_back();
+          std::string e = attr_preds_.back().compile(r.attr);
+          if (!e.empty() && err_.empty()) err_ = e;
+        }
+    if (attr_preds_.size() > 64 && err_.empty()) err_ = "more than 64 span_attribute rules are not supported";
+  }
   if (err_.empty() && has_url_) {
     // newUrlTemplateProcessor errors (rule parsing, custom id regexps) are
     // create-time errors too (factory.go:37-40); decode_url_config covers them.
@@ -160,6 +173,11 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
     const AttrMap& ra = rs.resource_attrs;
     // service ids (latency.go:51-56 AsString; servicename.go:38-42 Str)
     uint32_t svc = OSE_NONE, svc_str = OSE_NONE;
+    const Value* svc_val = ra.Get("service.name");
+    const std::string svc_as = svc_val ? svc_val->AsString() : std::string();
+    uint64_t attr_res = 0;   // span_attribute rules whose service this resource is (spanattribute.go:130-132)
+    for (size_t k = 0; k < attr_preds_.size(); k++)
+      if (svc_val && attr_preds_[k].service() == svc_as) attr_res |= 1ull << k;
     if (const Value* v = ra.Get("service.name")) {
       auto it = services_.find(v->AsString());
       if (it != services_.end()) svc = it->second;
@@ -204,6 +222,13 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
         hb->scope.push_back(scope_idx);
         hb->span_size.push_back((uint32_t)sizer.span(sp));
         hb->name_len.push_back((uint32_t)sp.name.size());
+        uint64_t am = 0;
+        for (uint64_t m = attr_res; m; m &= m - 1) {
+          const int k = __builtin_ctzll(m);
+          if (const Value* av = sp.attrs.Get(attr_preds_[k].key()))
+            if (attr_preds_[k].eval(*av)) am |= 1ull << k;
+        }
+        hb->attr_match.push_back(am);
         const AttrMap& a = sp.attrs;
         // sampling: AsString(http.route) (latency.go:64-68)
         const Value* route = a.Get("http.route");
@@ -279,7 +304,7 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
     if (v->empty()) v->push_back(0);
   for (auto* v : {&hb->status, &hb->kind, &hb->url_flags, &hb->res_url_ok})
     if (v->empty()) v->push_back(0);
-  for (auto* v : {&hb->trace_id, &hb->start, &hb->end})
+  for (auto* v : {&hb->trace_id, &hb->start, &hb->end, &hb->attr_match})
     if (v->empty()) v->push_back(0);
   if (hb->path.empty()) hb->path.push_back(ose_strref{0, 0});
   if (hb->route.empty()) hb->route.push_back(ose_strref{0, 0});
@@ -383,6 +408,7 @@ int TracesProcessor::ProcessTraces(Traces& td) {
   cp(c->res_size, hb->cols.res_size, 4 * R);
   cp(c->scope_size, hb->cols.scope_size, 4 * S);
   cp(c->scope_resource, hb->cols.scope_resource, 4 * S);
+  cp(c->attr_match, hb->cols.attr_match, 8 * n);
   std::memset(o->attrset_bytes, 0, 8 * (size_t)A);
   std::memset(o->accepted_spans, 0, 8);
   rc = ose_process(eng_, b, stages(), group_mode, &rnd);
@@ -569,6 +595,47 @@ void osehost_free(char* s) { std::free(s); }
 
 // ---- test seam: the product regex->DFA compiler evaluated on the host ----
 #include "regex_dfa.hpp"
+// One span_attribute condition on one attribute value (tests): rule_json is
+// the rule_details object, value_json an OTLP/JSON AnyValue.  1 / 0, or -1
+// with osehost_last_error() when the rule cannot be compiled.
+extern "C" int osehost_span_attr_eval(const char* rule_json, const char* value_json) {
+  try {
+    ose::Json d = ose::parse_json(rule_json);
+    ose::SpanAttributeRule r;
+    auto gs = [&](const char* k, std::string& out) {
+      if (const ose::Json* v = d.get(k)) out = v->s;
+    };
+    gs("service_name", r.service_name);
+    gs("attribute_key", r.attribute_key);
+    gs("condition_type", r.condition_type);
+    gs("operation", r.operation);
+    gs("expected_value", r.expected_value);
+    gs("json_path", r.json_path);
+    ose::SpanAttrPredicate p;
+    std::string e = p.compile(r);
+    if (!e.empty()) { g_host_err = e; return -1; }
+    ose::Json vj = ose::parse_json(value_json);
+    ose::Json wrapper = ose::Json::object();
+    ose::Json attrs = ose::Json::array();
+    ose::Json kv = ose::Json::object();
+    kv.set("key", ose::Json::str("k"));
+    kv.set("value", vj);
+    attrs.push(kv);
+    ose::Json res = ose::Json::object();
+    res.set("attributes", attrs);
+    ose::Json rs = ose::Json::object();
+    rs.set("resource", res);
+    ose::Json rss = ose::Json::array();
+    rss.push(rs);
+    wrapper.set("resourceSpans", rss);
+    ose::Traces t = ose::traces_from_json(wrapper);
+    return p.eval(t.resource_spans[0].resource_attrs.kv[0].second) ? 1 : 0;
+  } catch (const std::exception& ex) {
+    g_host_err = ex.what();
+    return -1;
+  }
+}
+
 extern "C" int osehost_regex_match(const char* pattern, const char* s, size_t n) {
   ose::Dfa d;
   std::string err;

@@ -19,6 +19,7 @@
 #include "../../include/odigos_amd.h"
 #include "config.hpp"
 #include "pdata.hpp"
+#include "span_attr.hpp"
 
 namespace ose {
 
@@ -28,7 +29,7 @@ struct HostBatch {
   ose_columns cols{};
   ose_outputs outs{};
   std::vector<uint8_t> arena;               // 16-byte aligned via arena_storage
-  std::vector<uint64_t> trace_id, start, end;
+  std::vector<uint64_t> trace_id, start, end, attr_match;
   std::vector<uint8_t> status, kind, url_flags;
   std::vector<uint32_t> resource, scope, span_size, name_len;
   std::vector<ose_strref> path, route;
@@ -78,6 +79,7 @@ class TracesProcessor {
   TrafficMetricsConfig traffic_;
   bool has_url_ = false, has_sampling_ = false, has_traffic_ = false;
   std::map<std::string, uint32_t> services_;
+  std::vector<SpanAttrPredicate> attr_preds_;   // span_attribute rules, level order
   ose_engine* eng_ = nullptr;
   uint64_t seed_ = 0x0D16A5EEDull;
   uint64_t draws_ = 0;

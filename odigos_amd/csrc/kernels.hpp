@@ -103,6 +103,7 @@ struct TraceKernelArgs {
   uint32_t* error;            // bit0 spin timeout, bit2 trace table full
   uint32_t* batch_keep;       // kTraceBatch: the call's decision (read by the SIZE stage)
   const uint64_t* route_match;// optional precomputed endpoint bits (ose_columns.route_match)
+  const uint64_t* attr_match; // span_attribute bits (null when no such rule)
   uint32_t ablate;            // diagnostics only (OSE_TRACE_ABLATE, tools/ablate_trace.py): skip parts
 };
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
@@ -174,6 +175,7 @@ struct ShardArgs {
   const ose_strref* route;
   const uint8_t* arena;
   const uint64_t* route_match;
+  const uint64_t* attr_match;
   const uint32_t* res_svc;
   const uint32_t* res_svc_str;
   const uint8_t* cfg;         // SampCfgDev blob
@@ -183,7 +185,7 @@ struct ShardArgs {
   uint8_t* send;              // [n * kXRec]
   uint32_t* pack_pos;         // [n]
 };
-constexpr uint32_t kXRec = 56;
+constexpr uint32_t kXRec = 64;
 void launch_shard_hist(const ShardArgs& a, hipStream_t st);
 void launch_shard_scatter(const ShardArgs& a, hipStream_t st);
 struct UnpackArgs {
@@ -197,6 +199,7 @@ struct UnpackArgs {
   uint32_t* res_svc;
   uint32_t* res_svc_str;
   uint64_t* route_match;
+  uint64_t* attr_match;
 };
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st);
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);

@@ -52,9 +52,16 @@ int Engine::build_sampling_tables() {
   std::vector<uint64_t> svc_bits(std::max<uint32_t>(nsvc, 1), 0);
   std::string bytes;
   SampCfgDev h{};
-  uint32_t n_svc_rules = 0;
+  uint32_t n_svc_rules = 0, n_attr = 0, total_svc = 0, total_attr = 0;
   const std::vector<SamplingRule>* levels[3] = {&sampling.global_rules, &sampling.service_rules,
                                                 &sampling.endpoint_rules};
+  for (auto* lvl : levels)
+    for (const SamplingRule& r : *lvl) {
+      total_svc += r.rtype == RuleType::ServiceName;
+      total_attr += r.rtype == RuleType::SpanAttribute;
+    }
+  if (total_svc + total_attr > kMaxServiceRules)
+    return fail(OSE_ENOTSUP, "more than 64 service_name + span_attribute rules are not supported by the GPU trace stage");
   for (int L = 0; L < 3; L++) {
     h.level_first[L] = (uint32_t)rules.size();
     for (const SamplingRule& r : *levels[L]) {
@@ -103,9 +110,15 @@ int Engine::build_sampling_tables() {
           break;
         }
         case RuleType::SpanAttribute:
-          return fail(OSE_ENOTSUP,
-                      "span_attribute sampling rules are not supported by the GPU trace stage yet "
-                      "(internal/sampling/spanattribute.go; SURVEY.md §8f)");
+          // the shim evaluates the per-span condition (attr_match column,
+          // odigos_amd/csrc/span_attr.cpp); the trace stage ORs the bits per
+          // trace: satisfied iff any span met it, never matched-but-unsatisfied
+          // (spanattribute.go:126-320), i.e. a service_name-shaped rule
+          d.type = kSampService;
+          d.bit = total_svc + n_attr++;
+          d.ratio = r.attr.sampling_ratio;
+          d.fallback = r.attr.fallback_sampling_ratio;
+          break;
       }
       rules.push_back(d);
     }
@@ -115,6 +128,8 @@ int Engine::build_sampling_tables() {
   h.n_lat = (uint32_t)lat.size();
   h.n_lat_slots = (uint32_t)slot_rules.size();
   h.n_services = nsvc;
+  h.n_attr = n_attr;
+  h.attr_shift = total_svc;
   if (slot_rules.empty()) slot_rules.push_back(0);
   std::vector<uint8_t> b(sizeof(SampCfgDev), 0);
   auto put = [&](const void* p, size_t nb) {
@@ -139,6 +154,7 @@ int Engine::build_sampling_tables() {
   std::memcpy(b.data(), &h, sizeof h);
   sampling_blob_host = std::move(b);
   sampling_n_lat = h.n_lat;
+  sampling_n_attr = h.n_attr;
   return 0;
 }
 
@@ -202,6 +218,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
       return fail(OSE_EINVAL, "SAMPLE stage needs status, resource, res_svc, res_svc_str and keep");
     if (!c->trace_id && (group_mode == OSE_GROUP_TRACE_ID || o->trace_keep || o->trace_level || o->trace_ratio))
       return fail(OSE_EINVAL, "SAMPLE stage needs the trace_id column");
+    if (e->sampling_n_attr && !c->attr_match)
+      return fail(OSE_EINVAL, "span_attribute rules need the attr_match column");
     if (lat && (!c->start_ns || !c->end_ns || (!c->route_match && (!c->route || !c->arena))))
       return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns and route + arena (or route_match)");
   } else if (!c->res_svc_str && c->n_resources) {
@@ -285,6 +303,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.error = err;
   a.batch_keep = misc + kBatchKeepWord;
   a.route_match = c->route_match;
+  a.attr_match = e->sampling_n_attr ? c->attr_match : nullptr;
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);

@@ -66,6 +66,11 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.route = c->route;
   a.arena = c->arena;
   a.route_match = c->route_match;
+  a.attr_match = e->sampling_n_attr ? c->attr_match : nullptr;
+  if (n && e->sampling_n_attr && !c->attr_match) {
+    e->release_ws(ws, st);
+    return fail(OSE_EINVAL, "span_attribute rules need the attr_match column");
+  }
   a.res_svc = c->res_svc;
   a.res_svc_str = c->res_svc_str;
   a.cfg = e->sampling_blob_dev;
@@ -103,12 +108,12 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
 
 int ose_shard_unpack(const void* recv, uint64_t n, uint64_t* trace_id, uint64_t* start_ns, uint64_t* end_ns,
                      uint8_t* status, uint32_t* resource, uint32_t* res_svc, uint32_t* res_svc_str,
-                     uint64_t* route_match, void* hip_stream) {
+                     uint64_t* route_match, uint64_t* attr_match, void* hip_stream) {
   if (n && (!recv || !trace_id || !start_ns || !end_ns || !status || !resource || !res_svc || !res_svc_str ||
-            !route_match))
+            !route_match || !attr_match))
     return fail(OSE_EINVAL, "NULL argument");
   UnpackArgs a{static_cast<const uint8_t*>(recv), n, trace_id, start_ns, end_ns, status, resource, res_svc, res_svc_str,
-               route_match};
+               route_match, attr_match};
   launch_shard_unpack(a, static_cast<hipStream_t>(hip_stream));
   HIP_TRY(hipGetLastError());
   return 0;

@@ -1,0 +1,497 @@
+// span_attr.cpp — see span_attr.hpp.
+#include "span_attr.hpp"
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+
+namespace ose {
+
+// ---------------- strconv ----------------
+
+// strconv.ParseFloat(s, 64): the whole string must parse; out-of-range
+// magnitudes are an error (ErrRange), underflow rounds to zero silently.
+bool go_parse_float(const std::string& s, double& out) {
+  if (s.empty() || std::isspace((unsigned char)s[0])) return false;
+  // strtod extensions Go rejects: "nan(...)" payloads and "infinity" tails
+  std::string low;
+  for (char ch : s) low += (char)std::tolower((unsigned char)ch);
+  size_t k = (low[0] == '+' || low[0] == '-') ? 1 : 0;
+  const std::string body = low.substr(k);
+  if (body.find('(') != std::string::npos) return false;
+  if (body.compare(0, 3, "inf") == 0 && body != "inf" && body != "infinity") return false;
+  if (body.compare(0, 3, "nan") == 0 && (body != "nan" || k)) return false;
+  errno = 0;
+  char* end = nullptr;
+  const double v = std::strtod(s.c_str(), &end);
+  if (end != s.c_str() + s.size()) return false;
+  if (errno == ERANGE && std::isinf(v)) return false;
+  out = v;
+  return true;
+}
+
+// strconv.ParseBool
+bool go_parse_bool(const std::string& s, bool& out) {
+  static const char* t[] = {"1", "t", "T", "TRUE", "true", "True"};
+  static const char* f[] = {"0", "f", "F", "FALSE", "false", "False"};
+  for (auto* x : t)
+    if (s == x) { out = true; return true; }
+  for (auto* x : f)
+    if (s == x) { out = false; return true; }
+  return false;
+}
+
+namespace {
+// shortest round-trip decimal digits of v (v finite, != 0): digits and the
+// decimal exponent e such that v = 0.d1d2... * 10^e
+void shortest_digits(double v, std::string& digits, int& e) {
+  char buf[64];
+  for (int p = 1; p <= 17; p++) {
+    std::snprintf(buf, sizeof buf, "%.*e", p - 1, v);
+    if (std::strtod(buf, nullptr) == v) break;
+  }
+  // buf = d.ddddde[+-]XX
+  std::string m = buf;
+  const size_t epos = m.find('e');
+  const int ex = std::atoi(m.c_str() + epos + 1);
+  digits.clear();
+  for (size_t i = 0; i < epos; i++)
+    if (std::isdigit((unsigned char)m[i])) digits += m[i];
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  e = ex + 1;
+}
+}  // namespace
+
+// strconv.FormatFloat(v, 'f', -1, 64)
+std::string go_format_float_f(double v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "+Inf" : "-Inf";
+  std::string out = std::signbit(v) ? "-" : "";
+  if (v == 0) return out + "0";
+  std::string d;
+  int e;
+  shortest_digits(std::fabs(v), d, e);
+  if (e <= 0) {
+    out += "0.";
+    out.append((size_t)(-e), '0');
+    out += d;
+  } else if ((size_t)e >= d.size()) {
+    out += d;
+    out.append((size_t)e - d.size(), '0');
+  } else {
+    out += d.substr(0, (size_t)e);
+    out += '.';
+    out += d.substr((size_t)e);
+  }
+  return out;
+}
+
+namespace {
+
+// ---------------- encoding/json ----------------
+struct JVal {
+  enum T { Null, Bool, Num, Str, Arr, Obj } t = Null;
+  bool b = false;
+  double n = 0;
+  std::string s;
+  std::vector<JVal> a;
+  std::map<std::string, JVal> o;   // Go unmarshals into map: last duplicate wins, Marshal sorts keys
+};
+
+struct JParser {
+  const std::string& s;
+  size_t p = 0;
+  explicit JParser(const std::string& src) : s(src) {}
+  void ws() {
+    while (p < s.size() && (s[p] == ' ' || s[p] == '\t' || s[p] == '\n' || s[p] == '\r')) p++;
+  }
+  bool lit(const char* w) {
+    size_t n = std::strlen(w);
+    if (s.compare(p, n, w) != 0) return false;
+    p += n;
+    return true;
+  }
+  static void put_utf8(std::string& o, uint32_t c) {
+    if (c < 0x80) o += (char)c;
+    else if (c < 0x800) { o += (char)(0xC0 | (c >> 6)); o += (char)(0x80 | (c & 63)); }
+    else if (c < 0x10000) { o += (char)(0xE0 | (c >> 12)); o += (char)(0x80 | ((c >> 6) & 63)); o += (char)(0x80 | (c & 63)); }
+    else { o += (char)(0xF0 | (c >> 18)); o += (char)(0x80 | ((c >> 12) & 63)); o += (char)(0x80 | ((c >> 6) & 63)); o += (char)(0x80 | (c & 63)); }
+  }
+  bool hex4(uint32_t& v) {
+    if (p + 4 > s.size()) return false;
+    v = 0;
+    for (int k = 0; k < 4; k++) {
+      char c = s[p + k];
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= (uint32_t)(c - '0');
+      else if (c >= 'a' && c <= 'f') v |= (uint32_t)(c - 'a' + 10);
+      else if (c >= 'A' && c <= 'F') v |= (uint32_t)(c - 'A' + 10);
+      else return false;
+    }
+    p += 4;
+    return true;
+  }
+  bool str(std::string& o) {
+    if (p >= s.size() || s[p] != '"') return false;
+    p++;
+    while (p < s.size()) {
+      unsigned char c = (unsigned char)s[p];
+      if (c == '"') { p++; return true; }
+      if (c < 0x20) return false;
+      if (c == '\\') {
+        p++;
+        if (p >= s.size()) return false;
+        char e = s[p++];
+        switch (e) {
+          case '"': o += '"'; break;
+          case '\\': o += '\\'; break;
+          case '/': o += '/'; break;
+          case 'b': o += '\b'; break;
+          case 'f': o += '\f'; break;
+          case 'n': o += '\n'; break;
+          case 'r': o += '\r'; break;
+          case 't': o += '\t'; break;
+          case 'u': {
+            uint32_t u;
+            if (!hex4(u)) return false;
+            if (u >= 0xD800 && u < 0xDC00) {   // surrogate pair, else U+FFFD (encoding/json)
+              size_t save = p;
+              uint32_t l;
+              if (p + 1 < s.size() && s[p] == '\\' && s[p + 1] == 'u' && (p += 2, hex4(l)) && l >= 0xDC00 && l < 0xE000) {
+                u = 0x10000 + ((u - 0xD800) << 10) + (l - 0xDC00);
+              } else {
+                p = save;
+                u = 0xFFFD;
+              }
+            } else if (u >= 0xDC00 && u < 0xE000) {
+              u = 0xFFFD;
+            }
+            put_utf8(o, u);
+            break;
+          }
+          default: return false;
+        }
+        continue;
+      }
+      o += (char)c;   // invalid UTF-8 is kept here; Marshal replaces it
+      p++;
+    }
+    return false;
+  }
+  bool num(double& v) {
+    const size_t b = p;
+    if (p < s.size() && s[p] == '-') p++;
+    if (p >= s.size()) return false;
+    if (s[p] == '0') p++;
+    else if (s[p] >= '1' && s[p] <= '9') { while (p < s.size() && std::isdigit((unsigned char)s[p])) p++; }
+    else return false;
+    if (p < s.size() && s[p] == '.') {
+      p++;
+      if (p >= s.size() || !std::isdigit((unsigned char)s[p])) return false;
+      while (p < s.size() && std::isdigit((unsigned char)s[p])) p++;
+    }
+    if (p < s.size() && (s[p] == 'e' || s[p] == 'E')) {
+      p++;
+      if (p < s.size() && (s[p] == '+' || s[p] == '-')) p++;
+      if (p >= s.size() || !std::isdigit((unsigned char)s[p])) return false;
+      while (p < s.size() && std::isdigit((unsigned char)s[p])) p++;
+    }
+    // float64 conversion: out of range is an UnmarshalTypeError
+    return go_parse_float(s.substr(b, p - b), v);
+  }
+  bool value(JVal& v, int depth) {
+    if (depth > 10000) return false;
+    ws();
+    if (p >= s.size()) return false;
+    char c = s[p];
+    if (c == '{') {
+      p++;
+      v.t = JVal::Obj;
+      ws();
+      if (p < s.size() && s[p] == '}') { p++; return true; }
+      for (;;) {
+        ws();
+        std::string k;
+        if (!str(k)) return false;
+        ws();
+        if (p >= s.size() || s[p] != ':') return false;
+        p++;
+        JVal x;
+        if (!value(x, depth + 1)) return false;
+        v.o[k] = std::move(x);
+        ws();
+        if (p < s.size() && s[p] == ',') { p++; continue; }
+        if (p < s.size() && s[p] == '}') { p++; return true; }
+        return false;
+      }
+    }
+    if (c == '[') {
+      p++;
+      v.t = JVal::Arr;
+      ws();
+      if (p < s.size() && s[p] == ']') { p++; return true; }
+      for (;;) {
+        JVal x;
+        if (!value(x, depth + 1)) return false;
+        v.a.push_back(std::move(x));
+        ws();
+        if (p < s.size() && s[p] == ',') { p++; continue; }
+        if (p < s.size() && s[p] == ']') { p++; return true; }
+        return false;
+      }
+    }
+    if (c == '"') { v.t = JVal::Str; return str(v.s); }
+    if (lit("true")) { v.t = JVal::Bool; v.b = true; return true; }
+    if (lit("false")) { v.t = JVal::Bool; v.b = false; return true; }
+    if (lit("null")) { v.t = JVal::Null; return true; }
+    v.t = JVal::Num;
+    return num(v.n);
+  }
+};
+
+// json.Unmarshal([]byte(s), &interface{}) == nil
+bool json_unmarshal(const std::string& s, JVal& out) {
+  JParser ps(s);
+  if (!ps.value(out, 0)) return false;
+  ps.ws();
+  return ps.p == s.size();
+}
+
+// json.Marshal float64 (encoding/json floatEncoder)
+std::string marshal_float(double f) {
+  const double a = std::fabs(f);
+  if (a != 0 && (a < 1e-6 || a >= 1e21)) {
+    char buf[64];
+    std::string d;
+    int e;
+    shortest_digits(a, d, e);
+    // strconv 'e' with -1 precision: d[0].d[1:]e±XX, then Go trims "e-07" to "e-7"
+    std::string m = d.substr(0, 1);
+    if (d.size() > 1) m += "." + d.substr(1);
+    int ex = e - 1;
+    std::snprintf(buf, sizeof buf, "e%c%02d", ex < 0 ? '-' : '+', ex < 0 ? -ex : ex);
+    std::string es = buf;
+    if (es.size() == 4 && es[2] == '0') es.erase(2, 1);   // e-07 -> e-7
+    return (f < 0 ? "-" : "") + m + es;
+  }
+  return go_format_float_f(f);
+}
+
+void marshal_string(const std::string& s, std::string& o) {
+  static const char* hex = "0123456789abcdef";
+  o += '"';
+  size_t i = 0;
+  while (i < s.size()) {
+    unsigned char c = (unsigned char)s[i];
+    if (c < 0x80) {
+      if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+      else if (c == '\n') o += "\\n";
+      else if (c == '\r') o += "\\r";
+      else if (c == '\t') o += "\\t";
+      else if (c < 0x20 || c == '<' || c == '>' || c == '&') { o += "\\u00"; o += hex[c >> 4]; o += hex[c & 15]; }
+      else o += (char)c;
+      i++;
+      continue;
+    }
+    // UTF-8 decode; invalid -> �; U+2028/2029 escaped
+    uint32_t cp = 0;
+    size_t n = 0;
+    if ((c & 0xE0) == 0xC0) { cp = c & 0x1F; n = 2; }
+    else if ((c & 0xF0) == 0xE0) { cp = c & 0x0F; n = 3; }
+    else if ((c & 0xF8) == 0xF0) { cp = c & 0x07; n = 4; }
+    bool ok = n && i + n <= s.size();
+    for (size_t k = 1; ok && k < n; k++) {
+      unsigned char cc = (unsigned char)s[i + k];
+      if ((cc & 0xC0) != 0x80) ok = false;
+      cp = (cp << 6) | (cc & 63);
+    }
+    if (ok && ((n == 2 && cp < 0x80) || (n == 3 && (cp < 0x800 || (cp >= 0xD800 && cp < 0xE000))) ||
+               (n == 4 && (cp < 0x10000 || cp > 0x10FFFF))))
+      ok = false;
+    if (!ok) { o += "\\ufffd"; i++; continue; }
+    if (cp == 0x2028 || cp == 0x2029) { o += cp == 0x2028 ? "\\u2028" : "\\u2029"; i += n; continue; }
+    o.append(s, i, n);
+    i += n;
+  }
+  o += '"';
+}
+
+void marshal(const JVal& v, std::string& o) {
+  switch (v.t) {
+    case JVal::Null: o += "null"; break;
+    case JVal::Bool: o += v.b ? "true" : "false"; break;
+    case JVal::Num: o += marshal_float(v.n); break;
+    case JVal::Str: marshal_string(v.s, o); break;
+    case JVal::Arr:
+      o += '[';
+      for (size_t k = 0; k < v.a.size(); k++) {
+        if (k) o += ',';
+        marshal(v.a[k], o);
+      }
+      o += ']';
+      break;
+    case JVal::Obj: {
+      o += '{';
+      bool first = true;
+      for (auto& kv : v.o) {   // std::map: sorted by key bytes, as Go sorts map keys
+        if (!first) o += ',';
+        first = false;
+        marshal_string(kv.first, o);
+        o += ':';
+        marshal(kv.second, o);
+      }
+      o += '}';
+      break;
+    }
+  }
+}
+
+// jsonpath.Get on a parsed simple path; false = an error (unknown key,
+// index out of range, step on a non-container).
+bool jsonpath_get(const std::vector<JsonPathStep>& path, const JVal& root, const JVal*& out) {
+  const JVal* cur = &root;
+  for (auto& st : path) {
+    if (st.is_index) {
+      if (cur->t != JVal::Arr) return false;
+      long long i = st.index;
+      if (i < 0) i += (long long)cur->a.size();
+      if (i < 0 || i >= (long long)cur->a.size()) return false;
+      cur = &cur->a[(size_t)i];
+    } else {
+      if (cur->t != JVal::Obj) return false;
+      auto it = cur->o.find(st.key);
+      if (it == cur->o.end()) return false;
+      cur = &it->second;
+    }
+  }
+  out = cur;
+  return true;
+}
+
+bool parse_jsonpath(const std::string& p, std::vector<JsonPathStep>& out) {
+  if (p.empty() || p[0] != '$') return false;
+  size_t i = 1;
+  while (i < p.size()) {
+    if (p[i] == '.') {
+      i++;
+      size_t b = i;
+      while (i < p.size() && (std::isalnum((unsigned char)p[i]) || p[i] == '_' || p[i] == '-')) i++;
+      if (i == b) return false;   // "..", ".*" and friends: not a simple path
+      out.push_back(JsonPathStep{false, p.substr(b, i - b), 0});
+    } else if (p[i] == '[') {
+      i++;
+      if (i < p.size() && (p[i] == '\'' || p[i] == '"')) {
+        char q = p[i++];
+        size_t b = i;
+        while (i < p.size() && p[i] != q) i++;
+        if (i >= p.size()) return false;
+        out.push_back(JsonPathStep{false, p.substr(b, i - b), 0});
+        i++;
+      } else {
+        size_t b = i;
+        if (i < p.size() && p[i] == '-') i++;
+        while (i < p.size() && std::isdigit((unsigned char)p[i])) i++;
+        if (i == b || (p[b] == '-' && i == b + 1)) return false;
+        out.push_back(JsonPathStep{true, "", std::atoll(p.substr(b, i - b).c_str())});
+      }
+      if (i >= p.size() || p[i] != ']') return false;
+      i++;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+std::string SpanAttrPredicate::compile(const SpanAttributeRule& r) {
+  service_ = r.service_name;
+  key_ = r.attribute_key;
+  cond_ = r.condition_type;
+  op_ = r.operation;
+  expected_ = r.expected_value;
+  if (cond_ == "string" && op_ == "regex") {
+    std::string err;
+    RegexStatus st = compile_dfa(expected_, re_, err);
+    if (st == RegexStatus::Ok) re_ok_ = true;
+    else if (st == RegexStatus::Syntax) re_ok_ = false;   // regexp.Compile error: the span is skipped (:171-174)
+    else return "span_attribute regex not supported by the DFA compiler: " + err;
+  }
+  if (cond_ == "number") num_ok_ = go_parse_float(expected_, num_);
+  if (cond_ == "boolean") bool_ok_ = go_parse_bool(expected_, bool_);
+  if (cond_ == "json" && (op_ == "contains_key" || op_ == "not_contains_key" || op_ == "key_equals" ||
+                          op_ == "key_not_equals")) {
+    if (!parse_jsonpath(r.json_path, path_))
+      return "span_attribute json_path \"" + r.json_path +
+             "\" is not a simple path ($, .key, ['key'], [index]): not supported by the engine";
+  }
+  return "";
+}
+
+// One span of spanattribute.go:136-316, given that the attribute exists.
+bool SpanAttrPredicate::eval(const Value& attr) const {
+  if (cond_ == "string") {
+    if (op_ == "exists" && attr.type == Value::TStr && !attr.s.empty()) return true;
+    if (attr.type != Value::TStr) return false;
+    const std::string& v = attr.s;
+    if (op_ == "equals") return v == expected_;
+    if (op_ == "not_equals") return v != expected_;
+    if (op_ == "contains") return v.find(expected_) != std::string::npos;
+    if (op_ == "not_contains") return v.find(expected_) == std::string::npos;
+    if (op_ == "regex") return re_ok_ && dfa_match(re_, reinterpret_cast<const uint8_t*>(v.data()), v.size());
+    return false;
+  }
+  if (cond_ == "number") {
+    if (op_ == "exists" && (attr.type == Value::TInt || attr.type == Value::TDouble)) return true;
+    if (!num_ok_) return false;
+    double x;
+    if (attr.type == Value::TInt) x = (double)attr.i;
+    else if (attr.type == Value::TDouble) x = attr.d;
+    else return false;
+    if (op_ == "equals") return x == num_;
+    if (op_ == "not_equals") return x != num_;
+    if (op_ == "greater_than") return x > num_;
+    if (op_ == "less_than") return x < num_;
+    if (op_ == "greater_than_or_equal") return x >= num_;
+    if (op_ == "less_than_or_equal") return x <= num_;
+    return false;
+  }
+  if (cond_ == "boolean") {
+    if (op_ == "exists" && attr.type == Value::TBool) return true;
+    if (!bool_ok_ || attr.type != Value::TBool) return false;
+    return op_ == "equals" && attr.b == bool_;
+  }
+  if (cond_ == "json") {
+    if (attr.type != Value::TStr) return false;
+    JVal root;
+    const bool ok = json_unmarshal(attr.s, root);
+    if (op_ == "is_valid_json") return ok;
+    if (op_ == "is_invalid_json") return !ok;
+    if (!ok) return false;
+    const JVal* res = nullptr;
+    const bool found = jsonpath_get(path_, root, res);
+    if (op_ == "contains_key") return found && res->t != JVal::Null;
+    if (op_ == "not_contains_key") return !found;
+    if (op_ == "key_equals" || op_ == "key_not_equals") {
+      if (!found) return false;
+      std::string vs;
+      switch (res->t) {
+        case JVal::Str: vs = res->s; break;
+        case JVal::Num: vs = go_format_float_f(res->n); break;
+        case JVal::Bool: vs = res->b ? "true" : "false"; break;
+        case JVal::Null: vs = "null"; break;
+        default: marshal(*res, vs); break;
+      }
+      return op_ == "key_equals" ? vs == expected_ : vs != expected_;
+    }
+    return false;   // "exists" / "jsonpath_exists": accepted by Validate, never satisfied (:241-315)
+  }
+  return false;
+}
+
+}  // namespace ose

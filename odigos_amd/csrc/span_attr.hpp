@@ -1,0 +1,58 @@
+// span_attr.hpp — the per-span predicate of odigossampling's span_attribute
+// rule (internal/sampling/spanattribute.go:126-320), evaluated by the host
+// columniser into the attr_match column; the GPU trace stage ORs the bits
+// per trace (a rule is satisfied iff one span of a resource with the rule's
+// AsString(service.name) meets the condition; it is never matched-but-
+// unsatisfied, spanattribute.go:319).
+//
+// Third-party semantics restated here (parity pinned by the reference's
+// spanattribute_test.go cases, tests/golden/span_attribute_kats.json):
+//   encoding/json  Unmarshal validity (RFC 8259; numbers must fit float64),
+//                  Marshal of nested values (sorted keys, HTML escaping)
+//   strconv        ParseFloat, ParseBool, FormatFloat(v, 'f', -1, 64)
+//   regexp         the DFA compiler of regex_dfa.hpp
+//   PaesslerAG/jsonpath v0.1.1  Get on simple paths: $, .key, ['key'],
+//                  ["key"], [index]; other syntax is OSE_ENOTSUP at
+//                  engine creation (documented, parity unpinned)
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "config.hpp"
+#include "pdata.hpp"
+#include "regex_dfa.hpp"
+
+namespace ose {
+
+struct JsonPathStep {
+  bool is_index = false;
+  std::string key;
+  long long index = 0;
+};
+
+class SpanAttrPredicate {
+ public:
+  // "" on success, else the reason the engine cannot run this rule
+  std::string compile(const SpanAttributeRule& r);
+  const std::string& service() const { return service_; }
+  const std::string& key() const { return key_; }
+  // the condition on the span's attribute value (found = the key exists)
+  bool eval(const Value& attr) const;
+
+ private:
+  std::string service_, key_, cond_, op_, expected_;
+  bool re_ok_ = false;
+  Dfa re_;
+  bool num_ok_ = false;
+  double num_ = 0;
+  bool bool_ok_ = false, bool_ = false;
+  std::vector<JsonPathStep> path_;
+};
+
+// helpers exposed for tests
+bool go_parse_float(const std::string& s, double& out);
+bool go_parse_bool(const std::string& s, bool& out);
+std::string go_format_float_f(double v);
+
+}  // namespace ose

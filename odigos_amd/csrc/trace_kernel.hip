@@ -592,6 +592,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
       const uint32_t s = sv;
       err = r.status == OSE_STATUS_ERROR;
       if (a.mode != kTraceBatch && ss < nsvc) svcb = c.svc_bits[ss];
+      if (a.attr_match) svcb |= a.attr_match[r.i] << c.h->attr_shift;
       if (s < nsvc) {
         slot = c.svc_slot[s];
         if (slot != kNoSlot) {
@@ -654,7 +655,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     if (cont_close) {
       const uint32_t E = c_err | rdl(err, t0);
       const uint64_t EP = c_ep | rdl64(ep, t0);
-      const uint64_t SV = a.mode == kTraceBatch ? batch_svc : (c_svc | rdl64(svcb, t0));
+      const uint64_t SV = batch_svc | c_svc | rdl64(svcb, t0);
       uint64_t s_l = 0;
       if ((c_kmask >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, cur.m, cur.e);
       s_l = wave_or64(s_l);
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         Q.err[e] = err;
         Q.ep[e] = ep;
         Q.lsat[e] = lsat;
-        Q.svc[e] = a.mode == kTraceBatch ? batch_svc : svcb;
+        Q.svc[e] = batch_svc | svcb;   // batch mode: resource bits of the call + span_attribute bits
         Q.hi[e] = hh;
         Q.lo[e] = hl;
         Q.pos[e] = (uint32_t)(base + sst);
@@ -962,6 +963,7 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
       rec[4] = ep;
       rec[5] = (uint64_t)s | ((uint64_t)ss << 32);
       rec[6] = a.status[j];
+      rec[7] = a.attr_match ? a.attr_match[j] : 0;
       a.pack_pos[j] = pos;
     }
   }
@@ -980,6 +982,7 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
   a.res_svc[i] = (uint32_t)sv;
   a.res_svc_str[i] = (uint32_t)(sv >> 32);
   a.status[i] = (uint8_t)rec[6];
+  a.attr_match[i] = rec[7];
   a.resource[i] = (uint32_t)i;   // one "resource" per received span carries its service ids
 }
 

@@ -5,8 +5,9 @@ that co-location is the node collector's loadbalancing exporter keyed by
 trace id (autoscaler/controllers/nodecollector/collectorconfig/
 traces.go:26-84).  Here, per step:
 
-1. ``ose_shard_pack`` buckets, per span, the 56-byte record the trace stage
-   reads (trace id, start, end, endpoint-match bits, service ids, status) by
+1. ``ose_shard_pack`` buckets, per span, the 64-byte record the trace stage
+   reads (trace id, start, end, endpoint-match bits, service ids, status,
+   span_attribute bits) by
    owner = hash(trace id) mod world, keeping batch order inside a bucket;
 2. an all-to-all of the bucket sizes, then of the records (RCCL over xGMI:
    torch.distributed's "nccl" backend is RCCL on ROCm);
@@ -91,6 +92,7 @@ class DeviceExchange:
              "res_svc": torch.empty(cap, dtype=torch.int32, device=d),
              "res_svc_str": torch.empty(cap, dtype=torch.int32, device=d),
              "route_match": torch.empty(cap, dtype=torch.int64, device=d),
+             "attr_match": torch.empty(cap, dtype=torch.int64, device=d),
              "keep": torch.empty(cap, dtype=torch.uint8, device=d),
              "status_word": torch.zeros(4, dtype=torch.int32, device=d)}
         self._x, self._recv_cap = x, cap
@@ -101,11 +103,12 @@ class DeviceExchange:
         p = {k: v.data_ptr() for k, v in x.items()}
         native.check(self.L.ose_shard_unpack(recv.data_ptr(), n, p["trace_id"], p["start_ns"], p["end_ns"],
                                              p["status"], p["resource"], p["res_svc"], p["res_svc_str"],
-                                             p["route_match"], self._s()))
+                                             p["route_match"], p["attr_match"], self._s()))
         cols = native.Columns()
         cols.n_spans = n
         cols.n_resources = n
-        for f in ("trace_id", "start_ns", "end_ns", "status", "resource", "res_svc", "res_svc_str", "route_match"):
+        for f in ("trace_id", "start_ns", "end_ns", "status", "resource", "res_svc", "res_svc_str", "route_match",
+                  "attr_match"):
             setattr(cols, f, p[f])
         outs = native.Outputs()
         outs.keep = p["keep"]

@@ -42,7 +42,7 @@ STAGE_SAMPLE = 0x1
 STAGE_TEMPLATE = 0x2
 STAGE_SIZE = 0x4
 STAGE_APPLY_KEEP = 0x8
-XREC_BYTES = 56
+XREC_BYTES = 64
 
 GROUP_TRACE_ID = 0
 GROUP_BATCH = 1
@@ -60,7 +60,7 @@ class Rand(C.Structure):
 
 COLUMN_FIELDS = [
     "arena", "trace_id", "start_ns", "end_ns", "status", "kind", "resource", "scope", "url_flags",
-    "path", "route", "span_size", "name_len", "route_match", "res_svc", "res_svc_str", "res_url_ok", "res_attrset",
+    "path", "route", "span_size", "name_len", "route_match", "attr_match", "res_svc", "res_svc_str", "res_url_ok", "res_attrset",
     "res_size", "scope_size", "scope_resource",
 ]
 
@@ -124,7 +124,7 @@ def lib() -> C.CDLL:
         "ose_device_info": (C.c_int, [C.c_char_p, C.c_size_t]),
         "ose_shard_owner": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint32]),
         "ose_shard_pack": (C.c_int, [_p, C.POINTER(Columns), C.c_uint32, _p, _p, _p, _p]),
-        "ose_shard_unpack": (C.c_int, [_p, C.c_uint64, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+        "ose_shard_unpack": (C.c_int, [_p, C.c_uint64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
         "ose_shard_scatter_keep": (C.c_int, [_p, _p, C.c_uint64, _p, _p]),
         "ose_profile_enable": (C.c_int, [_p, C.c_int]),
         "ose_profile_read": (C.c_int, [_p, C.c_char_p, C.c_size_t]),
@@ -145,6 +145,7 @@ def lib() -> C.CDLL:
         "osehost_as_string": (_p, [C.c_char_p]),
         "osehost_free": (None, [_p]),
         "osehost_regex_match": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+        "osehost_span_attr_eval": (C.c_int, [C.c_char_p, C.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

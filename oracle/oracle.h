@@ -66,6 +66,9 @@ int orc_url_process(const orc_url* u, const ose_columns* c, ose_outputs* o,
 #define ORC_RULE_ERROR    0
 #define ORC_RULE_LATENCY  1
 #define ORC_RULE_SERVICE  2
+#define ORC_RULE_ATTR     3   /* span_attribute: the per-span condition comes from
+                                 the attr_match column (bit = index among the
+                                 span_attribute rules, level order) */
 typedef struct orc_rule {
   int32_t level;        /* 0 global, 1 service, 2 endpoint (rule_engine.go:56-60) */
   int32_t type;         /* ORC_RULE_* */

@@ -26,6 +26,7 @@ struct orc_sampling {
   int n;
   orc_rule* rules;   /* copies; route strings owned */
   int* lat_index;    /* index of each http_latency rule among them (route_match bit) */
+  int* attr_index;   /* index of each span_attribute rule among them (attr_match bit) */
 };
 
 orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules) {
@@ -33,8 +34,12 @@ orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules) {
   s->n = n_rules;
   s->rules = (orc_rule*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(orc_rule));
   s->lat_index = (int*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(int));
-  int nl = 0;
-  for (int i = 0; i < n_rules; i++) s->lat_index[i] = rules[i].type == ORC_RULE_LATENCY ? nl++ : -1;
+  s->attr_index = (int*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(int));
+  int nl = 0, na = 0;
+  for (int i = 0; i < n_rules; i++) {
+    s->lat_index[i] = rules[i].type == ORC_RULE_LATENCY ? nl++ : -1;
+    s->attr_index[i] = rules[i].type == ORC_RULE_ATTR ? na++ : -1;
+  }
   for (int i = 0; i < n_rules; i++) {
     s->rules[i] = rules[i];
     char* r = (char*)malloc(rules[i].route_len + 1);
@@ -50,6 +55,7 @@ void orc_sampling_free(orc_sampling* s) {
   for (int i = 0; i < s->n; i++) free((void*)s->rules[i].route);
   free(s->rules);
   free(s->lat_index);
+  free(s->attr_index);
   free(s);
 }
 
@@ -132,6 +138,16 @@ static eval_t eval_service(const orc_rule* r, const trace_view* t) {
   return (eval_t){0, 0, r->fallback};
 }
 
+/* SpanAttributeRule.Evaluate (spanattribute.go:126-320) over the per-span
+ * condition bits: (true, true, ratio) as soon as one span of the trace meets
+ * it, else (false, false, fallback) — never matched-but-unsatisfied. */
+static eval_t eval_attr(const orc_rule* r, int attr_index, const trace_view* t) {
+  const ose_columns* c = t->c;
+  for (uint64_t k = 0; k < t->n; k++)
+    if ((c->attr_match[t->spans[k]] >> attr_index) & 1) return (eval_t){1, 1, r->ratio};
+  return (eval_t){0, 0, r->fallback};
+}
+
 /* evaluateLevel (rule_engine.go:89-115) */
 static void evaluate_level(const orc_sampling* s, int level, const trace_view* t, double* ratio, int* sat,
                            int* matched) {
@@ -146,6 +162,7 @@ static void evaluate_level(const orc_sampling* s, int level, const trace_view* t
     switch (r->type) {
       case ORC_RULE_ERROR: e = eval_error(r, t); break;
       case ORC_RULE_LATENCY: e = eval_latency(r, s->lat_index[k], t); break;
+      case ORC_RULE_ATTR: e = eval_attr(r, s->attr_index[k], t); break;
       default: e = eval_service(r, t); break;
     }
     if (e.satisfied) {

@@ -11,7 +11,7 @@ import numpy as np
 from odigos_amd import native
 
 XDT = np.dtype([("hi", "<u8"), ("lo", "<u8"), ("start", "<u8"), ("end", "<u8"), ("ep", "<u8"),
-                ("svc", "<u4"), ("svc_str", "<u4"), ("status", "<u8")])
+                ("svc", "<u4"), ("svc_str", "<u4"), ("status", "<u8"), ("attr", "<u8")])
 assert XDT.itemsize == native.XREC_BYTES
 
 M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
@@ -49,7 +49,7 @@ def endpoint_bits(cfg: dict, res_svc_of_span, route_bytes) -> np.ndarray:
     return out
 
 
-def pack(tid: np.ndarray, start, end, status, svc, svc_str, ep, world: int):
+def pack(tid: np.ndarray, start, end, status, svc, svc_str, ep, world: int, attr=None):
     """-> (records in bucket order, counts[world], pack_pos[n])"""
     hi, lo = tid[:, 0], tid[:, 1]
     own = owners(hi, lo, world)
@@ -57,6 +57,7 @@ def pack(tid: np.ndarray, start, end, status, svc, svc_str, ep, world: int):
     rec = np.zeros(len(hi), dtype=XDT)
     rec["hi"], rec["lo"], rec["start"], rec["end"], rec["ep"] = hi, lo, start, end, ep
     rec["svc"], rec["svc_str"], rec["status"] = svc, svc_str, status
+    rec["attr"] = 0 if attr is None else attr
     pos = np.empty(len(hi), dtype=np.int64)
     pos[order] = np.arange(len(hi))
     return rec[order], np.bincount(own, minlength=world).astype(np.int64), pos
@@ -66,14 +67,15 @@ class HostCols:
     """Owns numpy arrays and an ose_columns view of a sampling batch whose
     resources are one per span (the shape ose_shard_unpack produces)."""
 
-    def __init__(self, tid, start, end, status, svc, svc_str, ep):
+    def __init__(self, tid, start, end, status, svc, svc_str, ep, attr=None):
         n = len(start)
         c = np.ascontiguousarray   # structured-record fields are strided views
         self.a = dict(trace_id=c(np.asarray(tid, np.uint64).reshape(-1)),
                       start_ns=c(start, np.uint64), end_ns=c(end, np.uint64),
                       status=c(status, np.uint8), resource=np.arange(n, dtype=np.uint32),
                       res_svc=c(svc, np.uint32), res_svc_str=c(svc_str, np.uint32),
-                      route_match=c(ep, np.uint64))
+                      route_match=c(ep, np.uint64),
+                      attr_match=c(np.zeros(n, np.uint64) if attr is None else attr, np.uint64))
         for k in list(self.a):
             if self.a[k].size == 0:
                 self.a[k] = np.zeros(2, dtype=self.a[k].dtype)
@@ -87,7 +89,8 @@ class HostCols:
 def unpack(recv: np.ndarray) -> HostCols:
     r = recv.view(XDT)
     tid = np.stack([r["hi"], r["lo"]], axis=1)
-    return HostCols(tid, r["start"], r["end"], r["status"].astype(np.uint8), r["svc"], r["svc_str"], r["ep"])
+    return HostCols(tid, r["start"], r["end"], r["status"].astype(np.uint8), r["svc"], r["svc_str"], r["ep"],
+                    r["attr"])
 
 
 class CpuOps:
@@ -104,7 +107,8 @@ class CpuOps:
         a = self.b.a
         n = self.b.cols.n_spans
         rec, counts, pos = pack(a["trace_id"][: 2 * n].reshape(-1, 2), a["start_ns"][:n], a["end_ns"][:n],
-                                a["status"][:n], a["res_svc"][:n], a["res_svc_str"][:n], a["route_match"][:n], world)
+                                a["status"][:n], a["res_svc"][:n], a["res_svc_str"][:n], a["route_match"][:n], world,
+                                a["attr_match"][:n])
         self.pos = pos
         return (self.torch.from_numpy(rec.view(np.uint8).copy()), self.torch.from_numpy(counts), pos)
 

@@ -123,7 +123,7 @@ def intern_services(cfg: dict) -> dict:
 
 class SamplingOracle:
     """RuleEngine.ShouldSample per trace, restated (oracle/sampling.c)."""
-    TYPES = {"error": 0, "http_latency": 1, "service_name": 2}
+    TYPES = {"error": 0, "http_latency": 1, "service_name": 2, "span_attribute": 3}
 
     def __init__(self, cfg: dict | None = None):
         cfg = cfg or {}

@@ -138,10 +138,10 @@ def test_gpu_shard_kernels_vs_emulation():
     # unpack
     cols = {k: torch.empty(n * w, dtype=torch.uint8, device="cuda") for k, w in
             (("trace_id", 16), ("start_ns", 8), ("end_ns", 8), ("status", 1), ("resource", 4), ("res_svc", 4),
-             ("res_svc_str", 4), ("route_match", 8))}
+             ("res_svc_str", 4), ("route_match", 8), ("attr_match", 8))}
     native.check(L.ose_shard_unpack(send.data_ptr(), n, *[cols[k].data_ptr() for k in
                                     ("trace_id", "start_ns", "end_ns", "status", "resource", "res_svc", "res_svc_str",
-                                     "route_match")], None))
+                                     "route_match", "attr_match")], None))
     torch.cuda.synchronize()
     hc = unpack(rec.view(np.uint8))
     for k in cols:
