@@ -37,7 +37,7 @@ WORKLOADS = {
                 # no include/exclude configured: the shim passes res_url_ok = NULL
                 null_columns=("res_url_ok",), null_outputs=(),
                 fields=("arena", "kind", "url_flags", "path"),
-                kernels=("url_plan_kernel", "url_scan_kernel", "url_emit_kernel"),
+                kernels=("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel"),
                 metric_config="C2: URL templatization only, 10M spans/GPU, C2 segment mix, default rules"),
     "sampling": dict(gen="sampling", seed=0x0D160003, spans=50_000_000,
                      cfg=None, stages="SAMPLE", group="TRACE_ID",
@@ -55,7 +55,7 @@ WORKLOADS = {
                   fields=("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "resource", "scope",
                           "url_flags", "path", "route", "span_size", "name_len", "res_svc", "res_svc_str",
                           "res_attrset", "res_size", "scope_size", "scope_resource"),
-                  kernels=("trace_eval_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel",
+                  kernels=("trace_eval_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel",
                            "size_span_kernel", "size_scope_kernel", "size_res_kernel"),
                   metric_config="C4: fused odigossampling -> odigosurltemplate -> odigostrafficmetrics, "
                                 "12.5M spans/GPU (100M on 8), trace-id all-to-all over RCCL when N > 1"),

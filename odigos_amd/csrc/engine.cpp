@@ -309,12 +309,15 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   if (o->tmpl_arena_cap > 0xFFFFFFFFull) return fail(OSE_ERANGE, "tmpl_arena_cap exceeds the 32-bit offset range");
   uint64_t n = c->n_spans;
   const uint32_t groups = (uint32_t)((n + kUrlGroup - 1) / kUrlGroup);
-  // workspace: [0,256) misc | plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | dbg
-  const size_t off_len = 256, off_meta = off_len + 4 * n, off_code = align_up(off_meta + 4 * n, 8);
-  const size_t off_gsum = off_code + 8 * n, off_gbase = off_gsum + 8 * (size_t)groups;
+  // workspace: [0,16) scan counter, slow count, error | scan status 8t (both zeroed by one memset) |
+  // plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | slow groups 4g | dbg
   const uint32_t scan_tiles = (groups + kUrlScanTile - 1) / kUrlScanTile;
-  const size_t off_sst = off_gbase + 8 * (size_t)groups;
-  const size_t off_dbg = align_up(off_sst + 8 * (size_t)scan_tiles, 256);
+  const size_t off_sst = 16, zero_bytes = off_sst + 8 * (size_t)scan_tiles;
+  const size_t off_len = align_up(zero_bytes, 256), off_meta = off_len + 4 * n;
+  const size_t off_code = align_up(off_meta + 4 * n, 8);
+  const size_t off_gsum = off_code + 8 * n, off_gbase = off_gsum + 8 * (size_t)groups;
+  const size_t off_slow = off_gbase + 8 * (size_t)groups;
+  const size_t off_dbg = align_up(off_slow + 4 * (size_t)groups, 256);
   const size_t need = off_dbg + 256;
   if (need > url_workspace_bytes(n)) return fail(OSE_EINVAL, "internal: URL workspace layout exceeds its bound");
   int rc = ws->reserve(need);
@@ -343,8 +346,9 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.scan_counter = reinterpret_cast<uint32_t*>(base);
   a.scan_status = reinterpret_cast<uint64_t*>(base + off_sst);
   a.error = o->device_status ? o->device_status : reinterpret_cast<uint32_t*>(base + 8);
-  HIP_TRY(hipMemsetAsync(base, 0, 16, st));
-  HIP_TRY(hipMemsetAsync(a.scan_status, 0, 8 * (size_t)scan_tiles, st));
+  a.slow_count = reinterpret_cast<uint32_t*>(base + 4);
+  a.slow_groups = reinterpret_cast<uint32_t*>(base + off_slow);
+  HIP_TRY(hipMemsetAsync(base, 0, zero_bytes, st));
   a.used = o->tmpl_arena_used;
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
   if (n == 0) {
@@ -368,13 +372,19 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   launch_url_emit(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
+  e->prof_begin("url_emit_slow_kernel", st, tm);
+  launch_url_emit_slow(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
   if (a.ablate & 512) {
-    uint64_t h[8];
+    uint64_t h[16];
     HIP_TRY(hipMemcpyAsync(h, a.dbg, sizeof h, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const double wp = h[3] ? (double)h[3] : 1.0, we = h[6] ? (double)h[6] : 1.0;
     fprintf(stderr, "url clocks/wave: plan[stage %.0f bitmaps %.0f plan %.0f] emit[stage %.0f emit %.0f]\n",
             h[0] / wp, h[1] / wp, h[2] / wp, h[4] / we, h[5] / we);
+    fprintf(stderr, "url emit cumulative clocks/wave: counts %.0f bitmap %.0f pieces %.0f gather %.0f stores(after stage) %.0f\n",
+            h[8] / we, h[9] / we, h[10] / we, h[11] / we, h[12] / we);
   }
   return 0;
 }

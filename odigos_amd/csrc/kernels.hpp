@@ -37,6 +37,8 @@ struct UrlKernelArgs {
   uint64_t* scan_status;       // [n_scan_tiles], zeroed before launch
   uint32_t* error;             // bit0 look-back timeout, bit1 output overflow
   uint64_t* used;              // bytes written (optional)
+  uint32_t* slow_count;        // groups K3 left to K3s (zeroed before launch)
+  uint32_t* slow_groups;       // [n_groups]
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
   uint64_t* dbg;               // diagnostics only (ablate & 512): per-section clock sums
 };
@@ -46,11 +48,12 @@ constexpr uint32_t kUrlScanTile = 1024;  // groups per scan workgroup (url_kerne
 inline size_t url_workspace_bytes(uint64_t n) {
   const uint64_t g = (n + kUrlGroup - 1) / kUrlGroup;
   const uint64_t t = (g + kUrlScanTile - 1) / kUrlScanTile;
-  return 256 + n * 16 + g * 16 + t * 8 + 1024;
+  return 16 + t * 8 + 256 + n * 16 + 8 + g * 20 + 512;
 }
 void launch_url_plan(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_emit(const UrlKernelArgs& a, hipStream_t st);
+void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st);
 
 }  // namespace ose
 

@@ -1106,19 +1106,118 @@ struct PutOr {
   }
 };
 
+// Piece gather (the K3 fast path).  A group's output is a concatenation of
+// pieces, each a copy of LDS bytes: for M_DEFAULT the source stretch before a
+// templated segment (kept segments and the '/' separators are source bytes
+// already), then "{name}" from a braced name table; M_ORIG is "/" + body and
+// M_SLASH a lone "/".  Lanes list their span's pieces, then every lane
+// assembles an equal contiguous run of output dwords from the piece list, so
+// the per-byte work no longer follows the longest path of the group.
+// Groups with user rules, out-of-table names or >16 segments (plan `slow`)
+// take the per-span writer (emit_path).
+constexpr uint32_t kPieceCap = 448;   // per wave; a C2 group lists ~260
+constexpr uint32_t kBNames = 1024;    // braced names for template ids 0..14, '/' at byte 0
+constexpr uint32_t kSlashWords = kStage / 32 + 2;
+struct BracedNames {
+  __attribute__((aligned(16))) uint8_t b[kBNames + 16];
+  uint16_t off[16];
+  uint8_t len[16];
+  uint32_t ok;
+};
 struct EmitSmem {
   NamesSmem ns;
+  BracedNames bn;
   __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
   __attribute__((aligned(16))) uint32_t img[kWaves][kWaveOut / 4 + 4];
+  uint32_t slash[kWaves][kSlashWords];
+  uint32_t pdl[kWaves][kPieceCap];   // dst | len << 16 (output bytes of the group)
+  uint16_t psrc[kWaves][kPieceCap];  // source byte offset within EmitSmem
 };
 
+// "{name}" for ids 0..14 (the ids a plan code can carry), once per workgroup.
+__device__ void load_braced_names(const Cfg& cfg, BracedNames& bn) {
+  if (threadIdx.x == 0) {
+    const uint32_t nn = min(cfg.h.n_names, 15u);
+    uint32_t o = 4;
+    bool ok = true;
+    bn.b[0] = '/';
+    for (uint32_t id = 0; id < nn; id++) {
+      const uint32_t l = cfg.name(id).len + 2;
+      if (o + l > kBNames || l > 255) { ok = false; break; }
+      bn.off[id] = (uint16_t)o;
+      bn.len[id] = (uint8_t)l;
+      o += l;
+    }
+    bn.ok = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  if (bn.ok && threadIdx.x < min(cfg.h.n_names, 15u)) {
+    const NameDev nm = cfg.name(threadIdx.x);
+    const uint8_t* src = cfg.blob + cfg.h.bytes_off + nm.off;
+    uint8_t* d = bn.b + bn.off[threadIdx.x];
+    d[0] = '{';
+    for (uint32_t q = 0; q < nm.len; q++) d[1 + q] = src[q];
+    d[1 + nm.len] = '}';
+  }
+  __syncthreads();
+}
+
+// first '/' in [a, e) (stage coordinates) from the slash bitmap, or e
+__device__ __forceinline__ uint32_t next_slash(const lds_u32* sl, uint32_t a, uint32_t e) {
+  while (a < e) {
+    const uint32_t r = a >> 5, sh = a & 31;
+    const uint32_t m = __builtin_amdgcn_alignbit(sl[r + 1], sl[r], sh) & (uint32_t)low_mask(e - a);
+    if (m) return a + __builtin_ctz(m);
+    a += 32;
+  }
+  return e;
+}
+
+// Appends the pieces of one lane (dst = output offset within the group).
+struct PieceWriter {
+  uint32_t* pdl;
+  uint16_t* psrc;
+  uint32_t idx, dst;
+  __device__ __forceinline__ void put(uint32_t src, uint32_t len) {
+    pdl[idx] = dst | (len << 16);
+    psrc[idx] = (uint16_t)src;
+    dst += len;
+    idx++;
+  }
+};
+
+// the last piece whose output offset is <= ob (pieces are in output order)
+__device__ __forceinline__ uint32_t find_piece(const uint32_t* pdl, uint32_t np, uint32_t ob) {
+  uint32_t lo = 0, n = np;
+  while (n > 1) {
+    const uint32_t h = n >> 1;
+    if ((pdl[lo + h] & 0xFFFFu) <= ob) lo += h;
+    n -= h;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t lds_word(const lds_u8* L, uint32_t p) {
+  const lds_u32* w = (const lds_u32*)(L + (p & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], p & 3);
+}
+
+// The columns K3 reads for one group, loaded two groups ahead (with the
+// group's output base and size, so nothing is loaded after a stage prefetch
+// and waited for before the group is done).
 struct EmitCols {
   uint32_t len, meta;
   uint64_t code;
   ose_strref pr;
+  uint64_t base, gsum;
 };
-__device__ __forceinline__ EmitCols emit_cols(const UrlKernelArgs& a, uint64_t i) {
-  EmitCols c{0, 0, 0, {0, 0}};
+__device__ __forceinline__ EmitCols emit_cols(const UrlKernelArgs& a, uint32_t g, int lane) {
+  EmitCols c{0, 0, 0, {0, 0}, 0, 0};
+  const uint64_t i = (uint64_t)g * kWave + lane;
+  if (g < a.n_groups) {
+    c.base = a.group_base[g];
+    c.gsum = a.group_sum[g];
+  }
   if (i < a.n_spans) {
     c.len = a.plan_len[i];
     c.meta = a.plan_meta[i];
@@ -1132,21 +1231,62 @@ __device__ __forceinline__ bool emit_needs_path(uint32_t meta) {
   return mode == M_RULE || mode == M_DEFAULT || mode == M_ORIG;
 }
 
+// image dword k <-> global bytes [base - shift + 4k, +4); bytes outside
+// [base, base + gtotal) belong to the neighbouring groups, so partial dwords
+// at the ends are stored bytewise
+__device__ __forceinline__ void store_image(const UrlKernelArgs& a, const lds_w32* img, uint64_t base, uint32_t shift,
+                                            uint64_t gtotal) {
+  const int lane = threadIdx.x & 63;
+  uint8_t* gdst = a.out_arena + (base - shift);
+  const uint32_t nd = (uint32_t)((shift + gtotal + 3) / 4);
+  const uint64_t endb = shift + gtotal;
+  for (uint32_t k = lane; k < nd; k += kWave) {
+    const uint32_t w = img[k];
+    const uint32_t b0 = 4 * k;
+    if (b0 >= shift && b0 + 4 <= endb) {
+      *reinterpret_cast<uint32_t*>(gdst + b0) = w;
+    } else {
+      for (uint32_t q = 0; q < 4; q++)
+        if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(w >> (8 * q));
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += t;
+  }
+  *total = __shfl(incl, kWave - 1, kWave);
+  return incl - v;
+}
+
+// K3: emit, piece-gather groups only (the others are listed for K3s).  One
+// wave per 64-span group, persistent, with the next group's bytes and the
+// group after's columns in flight while a group is assembled.
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void url_emit_kernel(UrlKernelArgs a) {
   __shared__ EmitSmem sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const Cfg cfg = load_cfg(a, sm.ns);
+  load_braced_names(cfg, sm.bn);
+  const bool fast_cfg = sm.bn.ok && !(a.ablate & 2048);
+  const lds_u8* L = (const lds_u8*)(void*)&sm;
+  const uint32_t stage_src = (uint32_t)((uint8_t*)sm.stage[wv] - (uint8_t*)&sm);
+  const uint32_t bn_src = (uint32_t)((uint8_t*)sm.bn.b - (uint8_t*)&sm);
   const uint32_t stride = wave_stride();
   uint32_t g = wave_first_group();
   if (g >= a.n_groups) return;
   const bool tm = a.dbg != nullptr;
-  uint64_t t0 = 0, t_stage = 0, t_emit = 0;
+  uint64_t t0 = 0, t_stage = 0, t_emit = 0, ts[5] = {0, 0, 0, 0, 0};
   uint8_t* stage = sm.stage[wv];
   lds_u32* stage32 = (lds_u32*)stage;
   lds_w32* img = (lds_w32*)sm.img[wv];
 
-  EmitCols cur = emit_cols(a, (uint64_t)g * kWave + lane);
-  EmitCols nxt = emit_cols(a, (uint64_t)(g + stride) * kWave + lane);
+  EmitCols cur = emit_cols(a, g, lane);
+  EmitCols nxt = emit_cols(a, g + stride, lane);
   bool np = emit_needs_path(cur.meta);
   StagePf pf = stage_issue(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u);
   stage_commit(pf, stage);
@@ -1158,76 +1298,133 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     const bool more = g2 < a.n_groups;
     const bool np2 = more && emit_needs_path(nxt.meta);
     const StagePf pf2 = stage_issue(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u);
-    const EmitCols nn = emit_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
-    const uint64_t base = a.group_base[g];
-    const uint64_t gtotal = a.group_sum[g];
+    const EmitCols nn = emit_cols(a, g2 + stride, lane);
     if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
 
+    const uint64_t base = cur.base, gtotal = cur.gsum;
     const uint32_t len = cur.len, meta = cur.meta, mode = meta & 7u;
-    uint32_t incl = len;   // in-group exclusive offsets
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, kWave);
-      if (lane >= o) incl += t;
+    uint32_t unused;
+    const uint32_t local = wave_excl_scan(len, &unused);
+    const bool work = base + gtotal <= a.out_cap && !(a.ablate & 1);   // overflow: the scan flagged it
+    const uint32_t lo16 = pf.lo16;
+    const uint32_t shift = (uint32_t)(base & 3);
+    const uint32_t img_bytes = shift + (uint32_t)gtotal;
+    const uint32_t lead = (meta >> 3) & 1u, field = meta >> 7;
+    const bool slow = (meta >> 4) & 1u;
+    // piece counts: M_DEFAULT 2T+1 (T templated segments), M_ORIG 2, M_SLASH / M_RENAME_SLASH 1
+    uint32_t npc = 0;
+    bool lane_bad = false;
+    if (len) {
+      if (mode == M_DEFAULT) {
+        uint64_t x = cur.code;
+        x |= x >> 1;
+        x = (x | (x >> 2)) & 0x1111111111111111ull;
+        npc = 2 * (uint32_t)__builtin_popcountll(x) + 1;
+        lane_bad = slow || field == kNField;
+      } else if (mode == M_ORIG) {
+        npc = 2;
+        lane_bad = field == kNField;
+      } else if (mode == M_SLASH || mode == M_RENAME_SLASH) {
+        npc = 1;
+      } else {
+        lane_bad = true;   // M_RULE
+      }
     }
-    const uint32_t local = incl - len;
-    const bool overflow = base + gtotal > a.out_cap;
+    uint32_t npieces;
+    const uint32_t poff = wave_excl_scan(npc, &npieces);
+    const bool fast = work && fast_cfg && img_bytes <= kWaveOut && lo16 != ~0u && __ballot(lane_bad) == 0 &&
+                      npieces <= kPieceCap;   // wave-uniform
+    if (tm) { const uint64_t t1 = clk(); ts[0] += t1 - t0; }
+    if (fast) {
+      const ose_strref pr = emit_needs_path(meta) ? cur.pr : ose_strref{0, 0};
+      lds_u32* sl = (lds_u32*)sm.slash[wv];
+      if (__ballot(mode == M_DEFAULT && len != 0)) {   // '/' bitmap of the staged bytes
+        const uint32_t rows = (pf.bytes + 31) / 32;
+        for (uint32_t r = lane; r < rows; r += kWave) {
+          const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
+          const u32x4 v0 = src[0], v1 = src[1];
+          const uint32_t xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          uint32_t acc = 0;
+#pragma unroll
+          for (int d = 0; d < 8; d++) acc |= movemask4(swar_eq(xs[d], '/')) << (4 * d);
+          sm.slash[wv][r] = acc;
+        }
+        wave_lds_sync();
+      }
+      if (tm) { const uint64_t t1 = clk(); ts[1] += t1 - t0; }
+      const uint32_t nd = (img_bytes + 3) / 4;
+      const uint32_t cb = 4 * ((nd + kWave - 1) / kWave);
+      PieceWriter pw{sm.pdl[wv], sm.psrc[wv], poff, local};
+      if (len) {
+        if (mode == M_DEFAULT) {
+          const uint32_t p0 = pr.off - lo16, n = field;
+          uint32_t cs = 0, s = lead;
+          for (uint64_t c = (a.ablate & 8192) ? 0 : cur.code; c; c >>= 4) {
+            const uint32_t e = next_slash(sl, p0 + s, p0 + n) - p0;
+            const uint32_t nib = (uint32_t)(c & 15u);
+            if (nib) {
+              pw.put(stage_src + p0 + cs, s - cs);
+              pw.put(bn_src + sm.bn.off[nib - 1], sm.bn.len[nib - 1]);
+              cs = e;
+            }
+            s = e + 1;
+          }
+          pw.put(stage_src + p0 + cs, n - cs);
+        } else if (mode == M_ORIG) {
+          pw.put(bn_src, 1);
+          pw.put(stage_src + (pr.off - lo16) + lead, field - lead);
+        } else {
+          pw.put(bn_src, 1);
+        }
+      }
+      wave_lds_sync();
+      if (tm) { const uint64_t t1 = clk(); ts[2] += t1 - t0; }
+      // each lane assembles image dwords [lane*q, lane*q + q)
+      const uint32_t q = cb / 4, d0 = lane * q, d1 = min(nd, d0 + q);
+      if (d0 < d1 && gtotal != 0) {
+        const uint32_t* pdl = sm.pdl[wv];
+        const uint16_t* psrc = sm.psrc[wv];
+        const uint32_t ob = lane ? 4 * d0 - shift : 0u;
+        uint32_t idx = find_piece(pdl, npieces, ob);
+        uint32_t pd = pdl[idx];
+        uint32_t src = psrc[idx] + (ob - (pd & 0xFFFFu));
+        uint32_t rem = (pd >> 16) - (ob - (pd & 0xFFFFu));
+        for (uint32_t d = d0; d < d1; d++) {
+          uint32_t w = 0, have = (d == 0) ? shift : 0u;
+          while (have < 4) {
+            while (rem == 0 && idx + 1 < npieces) {
+              pd = pdl[++idx];
+              src = psrc[idx];
+              rem = pd >> 16;
+            }
+            if (rem == 0) break;   // end of the group's output
+            const uint32_t x = lds_word(L, src);
+            const uint32_t take = min(rem, 4u - have);
+            w |= (take == 4 ? x : (x & ((1u << (8 * take)) - 1u))) << (8 * have);
+            have += take;
+            src += take;
+            rem -= take;
+          }
+          img[d] = w;
+        }
+      }
+    } else if (work && lane == 0) {
+      a.slow_groups[atomicAdd(a.slow_count, 1u)] = g;
+    }
+    wave_lds_sync();   // image writes and stage reads of this group are done
+    if (tm) { const uint64_t t1 = clk(); ts[3] += t1 - t0; }
+    if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
+    // The next group's stage is committed before this group's stores are
+    // issued: waiting for the prefetch (older) then never waits for them.
+    if (more) stage_commit(pf2, stage);
+    if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
     if (valid) {
       a.url_out[i] = (uint8_t)((meta >> 5) & 3u);
       a.tmpl[i] = ose_strref{(uint32_t)(base + local), len};
     }
-    const bool needs_path = emit_needs_path(meta);
-    const ose_strref pr = needs_path ? cur.pr : ose_strref{0, 0};
-    const uint32_t lo16 = pf.lo16;
-    if (!overflow && !(a.ablate & 1)) {
-      const uint32_t shift = (uint32_t)(base & 3);
-      const uint32_t img_bytes = shift + (uint32_t)gtotal;
-      const bool direct = img_bytes > kWaveOut || lo16 == ~0u;   // wave-uniform
-      if (!direct) {
-        for (uint32_t k = lane; k < (img_bytes + 3) / 4; k += kWave) img[k] = 0;
-        wave_lds_sync();
-      }
-      if (len) {
-        const uint32_t lead = (meta >> 3) & 1u, field = meta >> 7;
-        const bool slow = (meta >> 4) & 1u;
-        const uint32_t f = (needs_path && (mode == M_RULE || field == kNField)) ? a.url_flags[i] : 0u;
-        if (!direct) {
-          PutOr put(img, shift + local);
-          LdsReader rd(stage32, pr.off - lo16);
-          emit_path(cfg, rd, pr.len, f, mode, lead, slow, field, cur.code, put);
-          put.finish();
-        } else if (lo16 != ~0u) {
-          emit_out_of_line(cfg, LdsReader(stage32, pr.off - lo16), pr.len, f, mode, lead, slow, field, cur.code,
-                           a.out_arena + base + local, len);
-        } else {
-          emit_out_of_line(cfg, ByteReader(a.arena + pr.off), pr.len, f, mode, lead, slow, field, cur.code,
-                           a.out_arena + base + local, len);
-        }
-      }
-      if (!direct) {
-        wave_lds_sync();
-        // image dword k <-> global bytes [base - shift + 4k, +4); bytes outside [base, base + gtotal)
-        // belong to the neighbouring groups, so partial dwords at the ends are stored bytewise
-        uint8_t* gdst = a.out_arena + (base - shift);
-        const uint32_t nd = (img_bytes + 3) / 4;
-        const uint64_t endb = shift + gtotal;
-        for (uint32_t k = lane; k < nd; k += kWave) {
-          const uint32_t w = img[k];
-          const uint32_t b0 = 4 * k;
-          if (b0 >= shift && b0 + 4 <= endb) {
-            *reinterpret_cast<uint32_t*>(gdst + b0) = w;
-          } else {
-            for (uint32_t q = 0; q < 4; q++)
-              if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(w >> (8 * q));
-          }
-        }
-      }
-    }
-    if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
+    if (fast) store_image(a, img, base, shift, gtotal);
+    if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; ts[4] += t1 - t0; }
     if (!more) break;
-    wave_lds_sync();   // image and stage reads of this group are done
-    stage_commit(pf2, stage);
-    if (tm) t_stage += clk() - t0;
     pf = pf2;
     cur = nxt;
     nxt = nn;
@@ -1237,6 +1434,68 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     atomicAdd((unsigned long long*)&a.dbg[4], (unsigned long long)t_stage);
     atomicAdd((unsigned long long*)&a.dbg[5], (unsigned long long)t_emit);
     atomicAdd((unsigned long long*)&a.dbg[6], 1ull);
+    for (int q = 0; q < 5; q++) atomicAdd((unsigned long long*)&a.dbg[8 + q], (unsigned long long)ts[q]);
+  }
+}
+
+// K3s: the groups K3 listed (user rules, plan `slow`, names outside the
+// braced table, an output image or a stage larger than LDS), with the
+// per-span writer (emit_path).  One wave per listed group; exits at once when
+// the list is empty.
+struct EmitSlowSmem {
+  NamesSmem ns;
+  __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
+  __attribute__((aligned(16))) uint32_t img[kWaves][kWaveOut / 4 + 4];
+};
+__global__ __launch_bounds__(kThreads) void url_emit_slow_kernel(UrlKernelArgs a) {
+  __shared__ EmitSlowSmem sm;
+  const uint32_t count = *a.slow_count;
+  if (blockIdx.x * kWaves >= count) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const Cfg cfg = load_cfg(a, sm.ns);
+  uint8_t* stage = sm.stage[wv];
+  lds_u32* stage32 = (lds_u32*)stage;
+  lds_w32* img = (lds_w32*)sm.img[wv];
+  for (uint32_t k = wave_first_group(); k < count; k += wave_stride()) {
+    const uint32_t g = a.slow_groups[k];
+    const uint64_t i = (uint64_t)g * kWave + lane;
+    const EmitCols c = emit_cols(a, g, lane);
+    const uint64_t base = c.base, gtotal = c.gsum;
+    const uint32_t len = c.len, meta = c.meta, mode = meta & 7u;
+    uint32_t unused;
+    const uint32_t local = wave_excl_scan(len, &unused);
+    const bool needs_path = emit_needs_path(meta);
+    const ose_strref pr = needs_path ? c.pr : ose_strref{0, 0};
+    uint32_t nbytes;
+    const uint32_t lo16 = stage_wave(stage, a.arena, needs_path ? pr.off : ~0u, needs_path ? pr.off + pr.len : 0u,
+                                     &nbytes);
+    const uint32_t shift = (uint32_t)(base & 3);
+    const uint32_t img_bytes = shift + (uint32_t)gtotal;
+    const bool direct = img_bytes > kWaveOut || lo16 == ~0u;   // wave-uniform
+    if (!direct) {
+      for (uint32_t k2 = lane; k2 < (img_bytes + 3) / 4; k2 += kWave) img[k2] = 0;
+      wave_lds_sync();
+    }
+    if (len) {
+      const uint32_t lead = (meta >> 3) & 1u, field = meta >> 7;
+      const bool slow = (meta >> 4) & 1u;
+      const uint32_t f = (needs_path && (mode == M_RULE || field == kNField)) ? a.url_flags[i] : 0u;
+      if (!direct) {
+        PutOr put(img, shift + local);
+        LdsReader rd(stage32, pr.off - lo16);
+        emit_path(cfg, rd, pr.len, f, mode, lead, slow, field, c.code, put);
+        put.finish();
+      } else if (lo16 != ~0u) {
+        emit_out_of_line(cfg, LdsReader(stage32, pr.off - lo16), pr.len, f, mode, lead, slow, field, c.code,
+                         a.out_arena + base + local, len);
+      } else {
+        emit_out_of_line(cfg, ByteReader(a.arena + pr.off), pr.len, f, mode, lead, slow, field, c.code,
+                         a.out_arena + base + local, len);
+      }
+    }
+    wave_lds_sync();
+    if (!direct) store_image(a, img, base, shift, gtotal);
+    wave_lds_sync();   // image and stage are reused by the next group
   }
 }
 
@@ -1266,6 +1525,12 @@ void launch_url_emit(const UrlKernelArgs& a, hipStream_t st) {
   static const uint32_t cap = resident_blocks(url_emit_kernel, 0);
   const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
   hipLaunchKernelGGL(url_emit_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+}
+void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st) {
+  // the list length is on the device: a grid for every group, blocks past it exit at once
+  static const uint32_t cap = resident_blocks(url_emit_slow_kernel, 0);
+  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL(url_emit_slow_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
 }
 
 }  // namespace ose

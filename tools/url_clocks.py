@@ -13,8 +13,8 @@ g.cols.res_url_ok = None
 eng = Engine({"odigosurltemplate": {}})
 db = DeviceBatch(g.cols, fields=("arena", "kind", "url_flags", "path"))
 sh = torch.cuda.current_stream().cuda_stream
-names = ["total", "stage1", "bitmaps", "plan", "scan+lb", "stage2", "emit", "copyout", "waves"]
-for ab in (512, 512 | 8 | 16 | 32 | 64):
+extra = [int(x, 0) for x in sys.argv[2:]] or [8 | 16 | 32 | 64]
+for ab in [512] + [512 | x for x in extra]:
     os.environ["OSE_URL_ABLATE"] = str(ab)
     eng.process_device(db, native.STAGE_TEMPLATE, stream=sh)
     torch.cuda.synchronize()
