@@ -18,6 +18,39 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
+// DPP wave64 scans and reductions (gfx9 row_shr / row_bcast): register-only,
+// no ds_bpermute round trip through the LDS pipeline per step.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t old, uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROWS, 0xF, false);
+}
+// inclusive prefix sum over the wave's lanes
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
+  x += dpp_mov<0x111>(0, x);   // row_shr:1
+  x += dpp_mov<0x112>(0, x);   // row_shr:2
+  x += dpp_mov<0x114>(0, x);   // row_shr:4
+  x += dpp_mov<0x118>(0, x);   // row_shr:8
+  x += dpp_mov<0x142, 0xA>(0, x);   // row_bcast:15 into rows 1, 3
+  x += dpp_mov<0x143, 0xC>(0, x);   // row_bcast:31 into rows 2, 3
+  return x;
+}
+__device__ __forceinline__ uint32_t lane_value(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+// wave-uniform min / max (lanes 15, 31, 47, 63 hold their row's after the row_shr steps)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+  x = min(x, dpp_mov<0x111>(x, x));
+  x = min(x, dpp_mov<0x112>(x, x));
+  x = min(x, dpp_mov<0x114>(x, x));
+  x = min(x, dpp_mov<0x118>(x, x));
+  return min(min(lane_value(x, 15), lane_value(x, 31)), min(lane_value(x, 47), lane_value(x, 63)));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+  x = max(x, dpp_mov<0x111>(x, x));
+  x = max(x, dpp_mov<0x112>(x, x));
+  x = max(x, dpp_mov<0x114>(x, x));
+  x = max(x, dpp_mov<0x118>(x, x));
+  return max(max(lane_value(x, 15), lane_value(x, 31)), max(lane_value(x, 47), lane_value(x, 63)));
+}
+
 // ---------------------------------------------------------------------------
 // Decoupled look-back (single-pass tile prefix).  Tile ids come from an
 // atomic counter taken at block start, so every tile a block waits on was

@@ -385,6 +385,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
             h[0] / wp, h[1] / wp, h[2] / wp, h[4] / we, h[5] / we);
     fprintf(stderr, "url emit cumulative clocks/wave: counts %.0f bitmap %.0f pieces %.0f gather %.0f stores(after stage) %.0f\n",
             h[8] / we, h[9] / we, h[10] / we, h[11] / we, h[12] / we);
+    fprintf(stderr, "url plan list clocks/wave: enumerate %.0f classify %.0f fold %.0f\n", h[13] / wp, h[14] / wp,
+            h[15] / wp);
   }
   return 0;
 }

@@ -162,19 +162,21 @@ constexpr uint32_t kNameTab = 64;
 // The header is copied into registers once per workgroup: read through the
 // blob pointer the compiler cannot prove it unclobbered by the kernel's own
 // stores and reloads it (vector load + full wait) in every segment loop.
+typedef const __attribute__((address_space(3))) UrlCfgDev lds_cfg;
 struct Cfg {
   const uint8_t* blob;
-  UrlCfgDev h;
+  lds_cfg* h;             // header copy in LDS: fields are read where used, no registers held
+  uint32_t n_custom, n_rules, max_rule_nseg;   // the fields every span's plan tests
   lds_u8* names;          // first kNamesLds bytes of the bytes section, staged in LDS
   uint32_t names_len;
   uint32_t ablate;        // diagnostics (UrlKernelArgs::ablate)
   const __attribute__((address_space(3))) NameDev* name_tab;   // first kNameTab entries of the name table, in LDS
   __device__ NameDev name(uint32_t id) const {
     if (id < kNameTab) return NameDev{name_tab[id].off, name_tab[id].len};
-    return reinterpret_cast<const NameDev*>(blob + h.names_off)[id];
+    return reinterpret_cast<const NameDev*>(blob + h->names_off)[id];
   }
   __device__ uint32_t dfa_off(int32_t i) const {
-    return reinterpret_cast<const uint32_t*>(blob + h.dfa_off)[i];
+    return reinterpret_cast<const uint32_t*>(blob + h->dfa_off)[i];
   }
 };
 
@@ -221,8 +223,8 @@ __device__ __forceinline__ int classify_segment(const Cfg& cfg, R& rd, uint32_t 
   }
   *e_out = q;
   const uint32_t e = q, len = e - s;
-  for (uint32_t k = 0; k < cfg.h.n_custom; k++) {   // custom ids first, in config order
-    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h.custom_off)[k];
+  for (uint32_t k = 0; k < cfg.n_custom; k++) {   // custom ids first, in config order
+    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
     if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, e)) return (int)cu.name;
   }
   if (date_len(len) && date_match(rd, s, len)) return kNameDate;
@@ -237,8 +239,8 @@ __device__ __forceinline__ int classify_segment(const Cfg& cfg, R& rd, uint32_t 
 // (without the leading '/') or -1.
 template <class R>
 __device__ int64_t attempt_rule(const Cfg& cfg, const UrlRuleDev& r, R& rd, uint32_t b0, uint32_t n) {
-  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h.segs_off) + r.seg_first;
-  const uint8_t* bytes = cfg.blob + cfg.h.bytes_off;
+  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h->segs_off) + r.seg_first;
+  const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
   uint32_t s = b0;
   int64_t len = 0;
   for (uint32_t k = 0; k < r.nseg; k++) {
@@ -317,7 +319,7 @@ __device__ __forceinline__ void put_name(const Cfg& cfg, uint32_t id, W& put) {
   if (nm.off + nm.len <= cfg.names_len) {
     for (uint32_t q = 0; q < nm.len; q++) put.byte(cfg.names[nm.off + q]);
   } else {
-    const uint8_t* bytes = cfg.blob + cfg.h.bytes_off;
+    const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
     for (uint32_t q = 0; q < nm.len; q++) put.byte(bytes[nm.off + q]);
   }
   put.byte('}');
@@ -325,8 +327,8 @@ __device__ __forceinline__ void put_name(const Cfg& cfg, uint32_t id, W& put) {
 
 template <class R, class W>
 __device__ void emit_rule(const Cfg& cfg, const UrlRuleDev& r, R& rd, uint32_t b0, uint32_t n, W& put) {
-  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h.segs_off) + r.seg_first;
-  const uint8_t* bytes = cfg.blob + cfg.h.bytes_off;
+  const UrlRuleSegDev* segs = reinterpret_cast<const UrlRuleSegDev*>(cfg.blob + cfg.h->segs_off) + r.seg_first;
+  const uint8_t* bytes = cfg.blob + cfg.h->bytes_off;
   uint32_t s = b0;
   for (uint32_t k = 0; k < r.nseg; k++) {
     const uint32_t e = scan_to(rd, s, n, '/');
@@ -365,11 +367,11 @@ __device__ __forceinline__ Plan plan_path(const Cfg& cfg, R& rd, uint32_t plen, 
     p.len = 1;
     return p;
   }
-  if (cfg.h.n_rules) {
+  if (cfg.n_rules) {
     const uint32_t nseg = 1 + count_byte(rd, p.lead, n, '/');
-    if (nseg <= cfg.h.max_rule_nseg) {
-      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h.rules_by_len_off);
-      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
+    if (nseg <= cfg.max_rule_nseg) {
+      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
+      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
       for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
         int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
         if (l >= 0) { p.mode = M_RULE; p.field = r; p.len = p.lead + (uint32_t)l; return p; }
@@ -408,7 +410,7 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
   if (mode == M_RULE) {
     const uint32_t n = path_end(rd, plen, f);
     if (lead) put.byte('/');
-    const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
+    const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
     emit_rule(cfg, rules[field], rd, lead, n, put);
     return;
   }
@@ -590,6 +592,35 @@ __device__ __forceinline__ bool email_win(uint64_t at, lds_cu4* bm, uint32_t a, 
   return (e.c[3] & M & ~low_mask(q + 1)) == 0;
 }
 
+// has_fffd for a segment of length L <= 64 at s whose high-bit bytes are the
+// set bits of hm: only the sequences are visited, each from one word read
+// (UTF-8 rules as in has_fffd above).
+template <class R>
+__device__ __forceinline__ bool has_fffd_win(R& rd, uint64_t hm, uint32_t s, uint32_t L) {
+  while (hm) {
+    const uint32_t q = (uint32_t)__builtin_ctzll(hm);
+    const uint32_t x = rd.word(s + q), c = x & 0xFFu;
+    uint32_t need, lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) { need = 2; lo = 0xA0; }
+    else if (c >= 0xE1 && c <= 0xEC) need = 2;
+    else if (c == 0xED) { need = 2; hi = 0x9F; }
+    else if (c >= 0xEE && c <= 0xEF) need = 2;
+    else if (c == 0xF0) { need = 3; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) { need = 3; hi = 0x8F; }
+    else return true;
+    if (q + need >= L) return true;
+    const uint32_t b1 = (x >> 8) & 0xFFu, b2 = (x >> 16) & 0xFFu, b3 = x >> 24;
+    if (b1 < lo || b1 > hi) return true;
+    if (need >= 2 && (b2 < 0x80u || b2 > 0xBFu)) return true;
+    if (need == 3 && (b3 < 0x80u || b3 > 0xBFu)) return true;
+    if (need == 2 && (x & 0xFFFFFFu) == 0xBDBFEFu) return true;
+    hm &= ~low_mask(q + need + 1);
+  }
+  return false;
+}
+
 // getSegmentTemplatizationString (templatize.go:242-269) from the class
 // windows of a segment of length L <= 64 starting at s (reader coordinates,
 // stage byte a).
@@ -599,8 +630,8 @@ template <class R>
 __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w, lds_cu4* bm, uint32_t a, uint32_t s,
                                             uint32_t L) {
   const uint64_t M = low_mask(L);
-  for (uint32_t k = 0; k < cfg.h.n_custom; k++) {   // custom ids first, in config order
-    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h.custom_off)[k];
+  for (uint32_t k = 0; k < cfg.n_custom; k++) {   // custom ids first, in config order
+    const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
     if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, s + L)) return (int)cu.name;
   }
   if (!(cfg.ablate & 8) && date_len(L) && date_win(rd, w.c[C_DG], w.c[C_DASH], s, L)) return kNameDate;
@@ -615,7 +646,7 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
         (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
       return kNameId;
   }
-  if (!(cfg.ablate & 32) && any_hi && has_fffd(rd, s, s + L)) return kNameId;
+  if (!(cfg.ablate & 32) && any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
   return -1;
 }
 
@@ -633,11 +664,11 @@ __device__ __forceinline__ Plan plan_bits(const Cfg& cfg, LdsReader& rd, lds_cu4
     p.len = 1;
     return p;
   }
-  if (cfg.h.n_rules) {
+  if (cfg.n_rules) {
     const uint32_t nseg = 1 + count_byte(rd, p.lead, n, '/');
-    if (nseg <= cfg.h.max_rule_nseg) {
-      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h.rules_by_len_off);
-      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
+    if (nseg <= cfg.max_rule_nseg) {
+      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
+      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
       for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
         int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
         if (l >= 0) { p.mode = M_RULE; p.field = r; p.len = p.lead + (uint32_t)l; return p; }
@@ -713,11 +744,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 // read HBM directly).
 __device__ uint32_t stage_wave(uint8_t* stage, const uint8_t* arena, uint32_t lo, uint32_t hi, uint32_t* nbytes) {
   const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = min(lo, (uint32_t)__shfl_xor(lo, o, kWave));
-    hi = max(hi, (uint32_t)__shfl_xor(hi, o, kWave));
-  }
+  lo = wave_min_u32(lo);
+  hi = wave_max_u32(hi);
   *nbytes = 0;
   if (lo >= hi) return 0;   // no lane reads bytes
   const uint32_t lo16 = lo & ~15u;
@@ -733,6 +761,7 @@ __device__ uint32_t stage_wave(uint8_t* stage, const uint8_t* arena, uint32_t lo
 
 // Names and name table in LDS (whole workgroup, once).
 struct NamesSmem {
+  UrlCfgDev hdr;
   uint8_t names[kNamesLds];
   NameDev name_tab[kNameTab];
 };
@@ -742,8 +771,9 @@ __device__ __forceinline__ Cfg load_cfg(const UrlKernelArgs& a, NamesSmem& ns) {
   for (uint32_t k = threadIdx.x; k < names_len; k += blockDim.x) ns.names[k] = a.cfg[h.bytes_off + k];
   if (threadIdx.x < min(h.n_names, kNameTab))
     ns.name_tab[threadIdx.x] = reinterpret_cast<const NameDev*>(a.cfg + h.names_off)[threadIdx.x];
+  if (threadIdx.x == 0) ns.hdr = h;
   __syncthreads();
-  return Cfg{a.cfg, h, (lds_u8*)ns.names, names_len, a.ablate,
+  return Cfg{a.cfg, (lds_cfg*)&ns.hdr, h.n_custom, h.n_rules, h.max_rule_nseg, (lds_u8*)ns.names, names_len, a.ablate,
              (const __attribute__((address_space(3))) NameDev*)ns.name_tab};
 }
 
@@ -760,11 +790,8 @@ struct StagePf {
 };
 __device__ __forceinline__ StagePf stage_issue(const uint8_t* arena, uint32_t lo, uint32_t hi) {
   const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = min(lo, (uint32_t)__shfl_xor(lo, o, kWave));
-    hi = max(hi, (uint32_t)__shfl_xor(hi, o, kWave));
-  }
+  lo = wave_min_u32(lo);
+  hi = wave_max_u32(hi);
   StagePf pf;
   pf.lo16 = 0;
   pf.bytes = 0;
@@ -803,12 +830,56 @@ __device__ __forceinline__ uint32_t wave_stride() { return gridDim.x * kWaves; }
 // K1: plan.  Waves are independent (no workgroup barrier after the config
 // load); per group: class bitmaps of the staged bytes, then one plan per span.
 constexpr uint32_t kSegCap = 192;   // per-wave segment list (C2 groups hold ~118 segments, max seen 182)
+// K1 stages each group through LDS-DMA into one of two per-wave buffers, so
+// the next group's bytes land while this one is planned without holding them
+// in VGPRs (a register prefetch spilled to scratch at this kernel's VGPR
+// budget, which forced a full vmcnt wait per group).  3 KB per buffer covers
+// 99.9% of C2/C4 groups (p99 of a group's byte range is 2.9 KB); larger
+// groups plan from HBM.  2 x 3 KB stage + 12-class bitmaps + segment list per
+// wave keep three 4-wave workgroups per CU.
+constexpr uint32_t kPlanStage = 3 * 1024;
+constexpr uint32_t kPlanBmRows = kPlanStage / 32 + 3;
 struct PlanSmem {
   NamesSmem ns;
-  __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
-  __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kBmRows];
+  __attribute__((aligned(16))) uint8_t stage[2][kWaves][kPlanStage + 16];
+  __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kPlanBmRows];
   uint32_t segs[kWaves][kSegCap];
 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+struct StageDma {
+  uint32_t lo16, bytes;   // bytes == 0: nothing staged; lo16 == ~0u: range too large (HBM reads)
+};
+// Issues the copy of the arena bytes [lo, hi) the wave's lanes reference
+// (16-byte aligned down) into `stage` by LDS-DMA (global_load_lds_dwordx4:
+// lane k's 16 bytes land at stage + 16k of each 1 KB piece).  The caller
+// waits vmcnt before reading the buffer.
+__device__ __forceinline__ StageDma stage_dma(const uint8_t* arena, uint32_t lo, uint32_t hi, uint8_t* stage) {
+  const int lane = threadIdx.x & 63;
+  lo = wave_min_u32(lo);
+  hi = wave_max_u32(hi);
+  StageDma sd{0, 0};
+  if (lo >= hi) return sd;
+  sd.lo16 = lo & ~15u;
+  const uint32_t bytes = (hi - sd.lo16 + 15u) & ~15u;
+  if (bytes > kPlanStage) {
+    sd.lo16 = ~0u;
+    return sd;
+  }
+  sd.bytes = bytes;
+  const uint4* src = reinterpret_cast<const uint4*>(arena + sd.lo16) + lane;
+  const uint32_t nv = bytes / 16;
+#pragma unroll
+  for (uint32_t k = 0; k < kPlanStage / 1024; k++)
+    if (lane + 64 * k < nv)
+      __builtin_amdgcn_global_load_lds((glb_void*)(src + 64 * k), (lds_void*)(stage + 1024 * k), 16, 0, 0);
+  return sd;
+}
+__device__ __forceinline__ void wait_dma() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+  wave_lds_sync();
+}
 
 // number of bytes of class c in [a, e) (stage coordinates)
 __device__ __forceinline__ uint32_t count_of(lds_cu4* bm, uint32_t c, uint32_t a, uint32_t e) {
@@ -823,28 +894,71 @@ __device__ __forceinline__ uint32_t count_of(lds_cu4* bm, uint32_t c, uint32_t a
   return k;
 }
 
+// 64-bit mask of bits [lo, hi) of the 64-bit half starting at bit `base` of a
+// 128-bit window (lo, hi are window coordinates)
+__device__ __forceinline__ uint64_t half_mask(uint32_t lo, uint32_t hi, uint32_t base) {
+  const uint32_t l = lo > base ? min(lo - base, 64u) : 0u, h = hi > base ? min(hi - base, 64u) : 0u;
+  return low_mask(h) & ~low_mask(l);
+}
+
 // Phase 1 for a whole group through a segment list: each lane enumerates its
 // span's segments into the wave's list; the wave classifies the list 64
 // segments per step (about 2 steps for a C2 group, instead of one step per
 // segment index of the longest path); each lane then folds its own entries.
-// Entries: start 12 | len 13 before classification, len << 8 | (id + 1) after.
+// Entries: start 12 | len 13 before classification, then out_len << 8 | (id + 1)
+// where out_len is what the segment adds to the template ({name} or itself).
+// A path whose bytes lie in 4 bitmap rows (the common case) finds its '?' cut,
+// leading '/' and segment ends in one read of those rows' slash and '?' words
+// and folds its entries (<= 8) in one read; longer paths walk the rows.
 // Returns false (nothing written) when the list would overflow.
 __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32, lds_cu4* bm, uint32_t* segs,
-                                                bool needs_path, uint32_t p0, uint32_t plen, uint32_t f, Plan& p) {
+                                                bool needs_path, uint32_t p0, uint32_t plen, uint32_t f, Plan& p,
+                                                bool tm, uint64_t* tt) {
   const int lane = threadIdx.x & 63;
+  uint64_t c0 = tm ? clk() : 0;
   LdsReader rd(stage32, p0);
+  const lds_u32* b32 = (const lds_u32*)bm;
   uint32_t n = 0, nseg = 0;
+  // window: stage bytes [32 r0, 32 r0 + 128), the path at window bit b0
+  const uint32_t r0 = p0 >> 5, b0 = p0 & 31;
+  const bool win = needs_path && b0 + plen <= 128;
+  uint64_t sl0 = 0, sl1 = 0;
   if (needs_path) {
-    n = (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? first_of(bm, C_QM, p0, p0 + plen) - p0 : plen;
-    p.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
+    if (win) {
+      uint32_t w[8];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        w[j] = b32[4 * kRowVec * (r0 + j) + C_SL];
+        w[4 + j] = b32[4 * kRowVec * (r0 + j) + C_QM];
+      }
+      sl0 = w[0] | ((uint64_t)w[1] << 32);
+      sl1 = w[2] | ((uint64_t)w[3] << 32);
+      n = plen;
+      if ((f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET) {   // strings.SplitN(target, "?", 2)[0]
+        const uint64_t q0 = (w[4] | ((uint64_t)w[5] << 32)) & half_mask(b0, b0 + plen, 0);
+        const uint64_t q1 = (w[6] | ((uint64_t)w[7] << 32)) & half_mask(b0, b0 + plen, 64);
+        if (q0) n = (uint32_t)__builtin_ctzll(q0) - b0;
+        else if (q1) n = 64 + (uint32_t)__builtin_ctzll(q1) - b0;
+      }
+      p.lead = (n > 0 && ((b0 < 64 ? sl0 >> b0 : sl1 >> (b0 - 64)) & 1)) ? 1 : 0;
+    } else {
+      n = (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? first_of(bm, C_QM, p0, p0 + plen) - p0 : plen;
+      p.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
+    }
     if (n == p.lead) {   // "" or "/" -> "/" (processor.go:156-160)
       p.mode = M_SLASH;
       p.len = 1;
     } else {
-      nseg = 1 + count_of(bm, C_SL, p0 + p.lead, p0 + n);
-      if (cfg.h.n_rules && nseg <= cfg.h.max_rule_nseg) {   // processor.go:162-171: rules first
-        const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h.rules_by_len_off);
-        const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h.rules_off);
+      if (win) {
+        sl0 &= half_mask(b0 + p.lead, b0 + n, 0);
+        sl1 &= half_mask(b0 + p.lead, b0 + n, 64);
+        nseg = 1 + __builtin_popcountll(sl0) + __builtin_popcountll(sl1);
+      } else {
+        nseg = 1 + count_of(bm, C_SL, p0 + p.lead, p0 + n);
+      }
+      if (cfg.n_rules && nseg <= cfg.max_rule_nseg) {   // processor.go:162-171: rules first
+        const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
+        const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
         for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
           const int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
           if (l >= 0) {
@@ -858,25 +972,36 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       }
     }
   }
-  uint32_t incl = nseg;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t t = __shfl_up(incl, o, kWave);
-    if (lane >= o) incl += t;
-  }
-  const uint32_t total = __shfl(incl, kWave - 1, kWave);
+  const uint32_t incl = wave_incl_sum_u32(nseg);
+  const uint32_t total = lane_value(incl, kWave - 1);
   if (total > kSegCap) return false;
   const uint32_t off = incl - nseg;
   if (nseg) {   // enumerate
     const uint32_t bend = p0 + n;
-    uint32_t s = p0 + p.lead;
-    for (uint32_t k = 0; k < nseg; k++) {
-      const uint32_t e = k + 1 < nseg ? first_of(bm, C_SL, s, bend) : bend;
-      segs[off + k] = s | ((e - s) << 12);
-      s = e + 1;
+    uint32_t s = p0 + p.lead, k = 0;
+    if (win) {
+      const uint32_t wb = p0 - b0;   // stage coordinate of window bit 0
+      for (uint64_t m = sl0; m; m &= m - 1) {
+        const uint32_t e = wb + (uint32_t)__builtin_ctzll(m);
+        segs[off + k++] = s | ((e - s) << 12);
+        s = e + 1;
+      }
+      for (uint64_t m = sl1; m; m &= m - 1) {
+        const uint32_t e = wb + 64 + (uint32_t)__builtin_ctzll(m);
+        segs[off + k++] = s | ((e - s) << 12);
+        s = e + 1;
+      }
+      segs[off + k] = s | ((bend - s) << 12);
+    } else {
+      for (; k < nseg; k++) {
+        const uint32_t e = k + 1 < nseg ? first_of(bm, C_SL, s, bend) : bend;
+        segs[off + k] = s | ((e - s) << 12);
+        s = e + 1;
+      }
     }
   }
   wave_lds_sync();
+  if (tm) { const uint64_t c1 = clk(); tt[0] += c1 - c0; c0 = c1; }
   LdsReader rd0(stage32, 0);
   for (uint32_t x = lane; x < total; x += kWave) {   // classify
     const uint32_t ent = segs[x];
@@ -889,28 +1014,47 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       uint32_t e;
       id = classify_segment(cfg, rd0, s, s + L, &e);   // segment longer than 64 bytes
     }
-    segs[x] = (L << 8) | (uint32_t)(id + 1);
+    const uint32_t out = id >= 0 ? cfg.name((uint32_t)id).len + 2 : L;
+    segs[x] = (out << 8) | (uint32_t)(id + 1);
   }
   wave_lds_sync();
+  if (tm) { const uint64_t c1 = clk(); tt[1] += c1 - c0; c0 = c1; }
   if (nseg) {   // fold
     uint32_t l = p.lead + nseg - 1;
     bool templated = false;
-    for (uint32_t k = 0; k < nseg; k++) {
-      const uint32_t r = segs[off + k];
-      const int id = (int)(r & 0xFFu) - 1;
-      if (id >= 0) {
-        templated = true;
-        l += cfg.name((uint32_t)id).len + 2;
-        if (k < 16 && id < 15) p.code |= (uint64_t)(id + 1) << (k * 4);
-        else p.slow = true;
-      } else {
+    if (nseg <= 8) {   // one read of the (at most 8) entries
+      uint32_t r[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) r[k] = segs[min(off + k, kSegCap - 1)];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        if (k < nseg) {
+          const int id = (int)(r[k] & 0xFFu) - 1;
+          l += r[k] >> 8;
+          if (id >= 0) {
+            templated = true;
+            if (id < 15) p.code |= (uint64_t)(id + 1) << (k * 4);
+            else p.slow = true;
+          }
+        }
+      }
+    } else {
+      for (uint32_t k = 0; k < nseg; k++) {
+        const uint32_t r = segs[off + k];
+        const int id = (int)(r & 0xFFu) - 1;
         l += r >> 8;
+        if (id >= 0) {
+          templated = true;
+          if (k < 16 && id < 15) p.code |= (uint64_t)(id + 1) << (k * 4);
+          else p.slow = true;
+        }
       }
     }
     if (templated) { p.mode = M_DEFAULT; p.len = l; }
     else { p.mode = M_ORIG; p.len = 1 + (n - p.lead); }   // "/" + body (processor.go:182-185)
     p.field = n < kNField ? n : kNField;
   }
+  if (tm) tt[2] += clk() - c0;
   return true;
 }
 
@@ -948,24 +1092,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
   uint32_t g = wave_first_group();
   if (g >= a.n_groups) return;
   const bool tm = a.dbg != nullptr;
-  uint64_t t0 = 0, t_stage = 0, t_bm = 0, t_plan = 0;
-  uint8_t* stage = sm.stage[wv];
-  lds_u32* stage32 = (lds_u32*)stage;
+  uint64_t t0 = 0, t_stage = 0, t_bm = 0, t_plan = 0, tt[3] = {0, 0, 0};
+  uint32_t buf = 0;
 
   // prologue: columns of groups g and g + stride, bytes of group g
   PlanCols cur = plan_cols(a, (uint64_t)g * kWave + lane);
   PlanCols nxt = plan_cols(a, (uint64_t)(g + stride) * kWave + lane);
   bool np = plan_gate(cur) == 2;
-  StagePf pf = stage_issue(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u);
-  stage_commit(pf, stage);
+  StageDma pf = stage_dma(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u, sm.stage[0][wv]);
   for (;;) {
     if (tm) t0 = clk();
+    wait_dma();   // this group's bytes and the next group's columns have landed
+    uint8_t* stage = sm.stage[buf][wv];
+    lds_u32* stage32 = (lds_u32*)stage;
     const uint64_t i = (uint64_t)g * kWave + lane;
     const uint32_t g2 = g + stride;
     const bool more = g2 < a.n_groups;
     // in flight while this group is planned: bytes of the next group, columns of the one after
     const bool np2 = more && plan_gate(nxt) == 2;
-    const StagePf pf2 = stage_issue(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u);
+    const StageDma pf2 =
+        stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[buf ^ 1][wv]);
     const PlanCols nn = plan_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
     if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
 
@@ -983,7 +1129,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     bool listed = false;
     if (lo16 != ~0u && !(a.ablate & (1024 | 2)))
       listed = plan_group_list(cfg, stage32, (lds_cu4*)sm.bm[wv], sm.segs[wv], needs_path, cur.pr.off - lo16,
-                               cur.pr.len, cur.f, p);
+                               cur.pr.len, cur.f, p, tm, tt);
     if (gate == 1) {
       p.mode = M_RENAME_SLASH;
       p.len = 1;
@@ -1015,9 +1161,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     if (tm) { const uint64_t t1 = clk(); t_plan += t1 - t0; t0 = t1; }
     if (!more) break;
     wave_lds_sync();   // every lane is done with this group's stage and bitmaps
-    stage_commit(pf2, stage);
-    if (tm) t_stage += clk() - t0;
     pf = pf2;
+    buf ^= 1;
     cur = nxt;
     nxt = nn;
     g = g2;
@@ -1027,6 +1172,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     atomicAdd((unsigned long long*)&a.dbg[1], (unsigned long long)t_bm);
     atomicAdd((unsigned long long*)&a.dbg[2], (unsigned long long)t_plan);
     atomicAdd((unsigned long long*)&a.dbg[3], 1ull);
+    atomicAdd((unsigned long long*)&a.dbg[13], (unsigned long long)tt[0]);
+    atomicAdd((unsigned long long*)&a.dbg[14], (unsigned long long)tt[1]);
+    atomicAdd((unsigned long long*)&a.dbg[15], (unsigned long long)tt[2]);
   }
 }
 
@@ -1137,7 +1285,7 @@ struct EmitSmem {
 // "{name}" for ids 0..14 (the ids a plan code can carry), once per workgroup.
 __device__ void load_braced_names(const Cfg& cfg, BracedNames& bn) {
   if (threadIdx.x == 0) {
-    const uint32_t nn = min(cfg.h.n_names, 15u);
+    const uint32_t nn = min(cfg.h->n_names, 15u);
     uint32_t o = 4;
     bool ok = true;
     bn.b[0] = '/';
@@ -1151,9 +1299,9 @@ __device__ void load_braced_names(const Cfg& cfg, BracedNames& bn) {
     bn.ok = ok ? 1u : 0u;
   }
   __syncthreads();
-  if (bn.ok && threadIdx.x < min(cfg.h.n_names, 15u)) {
+  if (bn.ok && threadIdx.x < min(cfg.h->n_names, 15u)) {
     const NameDev nm = cfg.name(threadIdx.x);
-    const uint8_t* src = cfg.blob + cfg.h.bytes_off + nm.off;
+    const uint8_t* src = cfg.blob + cfg.h->bytes_off + nm.off;
     uint8_t* d = bn.b + bn.off[threadIdx.x];
     d[0] = '{';
     for (uint32_t q = 0; q < nm.len; q++) d[1 + q] = src[q];
@@ -1253,14 +1401,8 @@ __device__ __forceinline__ void store_image(const UrlKernelArgs& a, const lds_w3
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
-  const int lane = threadIdx.x & 63;
-  uint32_t incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t t = __shfl_up(incl, o, kWave);
-    if (lane >= o) incl += t;
-  }
-  *total = __shfl(incl, kWave - 1, kWave);
+  const uint32_t incl = wave_incl_sum_u32(v);
+  *total = lane_value(incl, kWave - 1);
   return incl - v;
 }
 
