@@ -548,31 +548,37 @@ __device__ __forceinline__ uint32_t first_of(lds_cu4* bm, uint32_t c, uint32_t a
 // datesRegex (templatize.go:67) for a segment of length L from the digit and
 // dash windows plus at most four byte reads: every accepted length has one
 // fixed shape (10 + {0, 6 "THH:MM", 9 "THH:MM:SS"} + {0, 1 "Z", 5 "+HHMM"}).
+// Shape per length: 2 bits T-part (1: none, 2: "THH:MM", 3: "THH:MM:SS";
+// 0: no date has this length) | 2 bits zone (0: none, 1: "Z", 2: "+HHMM"),
+// 4 bits per L in [0, 32).
+constexpr uint64_t date_shape_bits(uint32_t L) {
+  return L == 10 ? 0x1 : L == 11 ? 0x5 : L == 15 ? 0x9 : L == 16 ? 0x2 : L == 17 ? 0x6 : L == 21 ? 0xA
+       : L == 19 ? 0x3 : L == 20 ? 0x7 : L == 24 ? 0xB : 0x0;
+}
+constexpr uint64_t date_shape_tab(uint32_t base) {
+  uint64_t t = 0;
+  for (uint32_t k = 0; k < 16; k++) t |= date_shape_bits(base + k) << (4 * k);
+  return t;
+}
 template <class R>
 __device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint32_t s, uint32_t L) {
-  uint32_t tlen, zlen;
-  switch (L) {
-    case 10: tlen = 0; zlen = 0; break;
-    case 11: tlen = 0; zlen = 1; break;
-    case 15: tlen = 0; zlen = 5; break;
-    case 16: tlen = 6; zlen = 0; break;
-    case 17: tlen = 6; zlen = 1; break;
-    case 21: tlen = 6; zlen = 5; break;
-    case 19: tlen = 9; zlen = 0; break;
-    case 20: tlen = 9; zlen = 1; break;
-    case 24: tlen = 9; zlen = 5; break;
-    default: return false;
-  }
-  uint64_t dm = 0x36Full;                                   // YYYY-MM-DD digits
-  if (tlen) dm |= (3ull << 11) | (3ull << 14);              // THH:MM
-  if (tlen == 9) dm |= 3ull << 17;                          // :SS
+  constexpr uint64_t kLo = date_shape_tab(0), kHi = date_shape_tab(16);
+  const uint32_t sh = (uint32_t)(((L < 16 ? kLo : kHi) >> (4 * (L & 15))) & 15u);
+  const uint32_t tsel = sh & 3u, zsel = sh >> 2;
+  if (L >= 32 || tsel == 0) return false;
+  const uint32_t tlen = tsel == 1 ? 0u : tsel == 2 ? 6u : 9u;
+  uint64_t dm = 0x36Full;                                     // YYYY-MM-DD digits
+  dm |= tsel >= 2 ? (3ull << 11) | (3ull << 14) : 0ull;       // THH:MM
+  dm |= tsel == 3 ? 3ull << 17 : 0ull;                        // :SS
   const uint32_t z = 10 + tlen;
-  if (zlen == 5) dm |= 0xFull << (z + 1);                   // +HHMM
+  dm |= zsel == 2 ? 0xFull << (z + 1) : 0ull;                 // +HHMM
   if ((dg & dm) != dm || ((dash >> 4) & 1) == 0 || ((dash >> 7) & 1) == 0) return false;
-  const uint32_t c_t = tlen ? rd.at(s + 10) : 'T', c_c1 = tlen ? rd.at(s + 13) : ':';
-  const uint32_t c_c2 = tlen == 9 ? rd.at(s + 16) : ':', c_z = zlen ? rd.at(s + z) : 'Z';
-  return c_t == 'T' && c_c1 == ':' && c_c2 == ':' &&
-         (zlen == 0 || (zlen == 1 ? c_z == 'Z' : (c_z == '+' || c_z == '-')));
+  // bytes 10-13 and 16-19 hold every fixed punctuation position and the zone
+  const uint32_t wa = rd.word(s + 10), wb = rd.word(s + 16);
+  const uint32_t c_t = wa & 0xFFu, c_c1 = (wa >> 24) & 0xFFu, c_c2 = wb & 0xFFu;
+  const uint32_t c_z = tlen == 0 ? c_t : tlen == 6 ? c_c2 : wb >> 24;
+  return (tlen == 0 || (c_t == 'T' && c_c1 == ':')) && (tlen != 9 || c_c2 == ':') &&
+         (zsel == 0 || (zsel == 1 ? c_z == 'Z' : (c_z == '+' || c_z == '-')));
 }
 
 // emailRegex (templatize.go:70) from the class windows: exactly one '@' at p,
@@ -634,7 +640,7 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
     const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
     if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, s + L)) return (int)cu.name;
   }
-  if (!(cfg.ablate & 8) && date_len(L) && date_win(rd, w.c[C_DG], w.c[C_DASH], s, L)) return kNameDate;
+  if (!(cfg.ablate & 8) && date_win(rd, w.c[C_DG], w.c[C_DASH], s, L)) return kNameDate;
   const bool any_hi = (w.c[C_HI] & M) != 0;
   const uint64_t at = w.c[C_AT] & M;
   if (!(cfg.ablate & 16) && !any_hi && at && (at & (at - 1)) == 0 && email_win(at, bm, a, L)) return kNameEmail;
