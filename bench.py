@@ -11,6 +11,7 @@ the max over ranks is reported.  Rank 0 prints ONE JSON line.
 Workloads (per GPU):
   url       C2  odigosurltemplate, 10M spans, default rules          (configs[1])
   sampling  C3  odigossampling, 50M spans / ~5M traces, C3 rules     (configs[2])
+  zipf      C5  odigossampling on Zipf trace sizes (1-50k spans), 50M spans  (configs[4])
   fused     C4  all three processors, 12.5M spans/GPU (100M on 8)    (configs[3]);
                 with N > 1 the sampling records go to each trace's owner
                 GPU through an RCCL all-to-all (odigos_amd/exchange.py)
@@ -45,9 +46,18 @@ WORKLOADS = {
                                                     "trace_ratio"),
                      fields=("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc",
                              "res_svc_str"),
-                     kernels=("trace_eval_kernel",),
+                     kernels=("trace_eval_kernel", "trace_long_kernel"),
                      metric_config="C3: trace-level sampling (1 error + 4 service + 16 latency rules), "
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
+    "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000,
+                 cfg=None, stages="SAMPLE", group="TRACE_ID",
+                 null_columns=(), null_outputs=("trace_count", "trace_first_span", "trace_keep", "trace_level",
+                                                "trace_ratio"),
+                 fields=("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc",
+                         "res_svc_str"),
+                 kernels=("trace_eval_kernel", "trace_long_kernel"),
+                 metric_config="C5: trace-level sampling on Zipf(1.1) trace sizes (1 to 50k spans/trace), "
+                               "50M spans per GPU, C3 rules, grouped by trace_id"),
     "fused": dict(gen="fused", seed=0x0D160004, spans=12_500_000,
                   cfg=None, stages="SAMPLE|TEMPLATE|SIZE", group="TRACE_ID",
                   null_columns=("res_url_ok",), null_outputs=("trace_count", "trace_first_span", "trace_keep",
@@ -55,7 +65,7 @@ WORKLOADS = {
                   fields=("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "resource", "scope",
                           "url_flags", "path", "route", "span_size", "name_len", "res_svc", "res_svc_str",
                           "res_attrset", "res_size", "scope_size", "scope_resource"),
-                  kernels=("trace_eval_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel",
+                  kernels=("trace_eval_kernel", "trace_long_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel",
                            "size_span_kernel", "size_scope_kernel", "size_res_kernel"),
                   metric_config="C4: fused odigossampling -> odigosurltemplate -> odigostrafficmetrics, "
                                 "12.5M spans/GPU (100M on 8), trace-id all-to-all over RCCL when N > 1"),
@@ -208,7 +218,7 @@ def cpu_baseline_sampling(gen, cfg, threads: int, budget_s: float = 12.0, calls:
     t1 = time.perf_counter()
     assert orc.process(c1, ho1.outs, native.GROUP_TRACE_ID, 0x5EED, 1) == 0
     st = c1.n_spans / (time.perf_counter() - t1)
-    sample = f"{c5.n_spans}-span prefix of the C3 batch x {reps} passes, oracle/sampling.c -O3 pthreads"
+    sample = f"{c5.n_spans}-span prefix of the same batch x {reps} passes, oracle/sampling.c -O3 pthreads"
 
     def parity(db):
         ho = HostOutputs(gen.cols)
@@ -364,7 +374,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        fn = {"url": cpu_baseline_url, "sampling": cpu_baseline_sampling, "fused": cpu_baseline_fused}[args.workload]
+        fn = {"url": cpu_baseline_url, "sampling": cpu_baseline_sampling, "zipf": cpu_baseline_sampling,
+              "fused": cpu_baseline_fused}[args.workload]
         mt, st, sample, parity = fn(gen, cfg, threads, calls=args.steps + args.warmup)
         out["cpu_baseline"] = {"value": mt, "unit": "spans/s", "cores": threads, "kind": "port",
                                "sample": sample, "value_1core": st}

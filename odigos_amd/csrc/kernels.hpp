@@ -108,8 +108,14 @@ struct TraceKernelArgs {
   const uint64_t* route_match;// optional precomputed endpoint bits (ose_columns.route_match)
   const uint64_t* attr_match; // span_attribute bits (null when no such rule)
   uint32_t ablate;            // diagnostics only (OSE_TRACE_ABLATE, tools/ablate_trace.py): skip parts
+  // kTraceRuns: runs still open kLongSteps steps past their owner's windows
+  // are listed here (head positions) and decided by trace_long_kernel
+  uint32_t* n_long;
+  uint32_t* long_runs;        // [n_spans / (kLongSteps * 64) + 1]
 };
+constexpr uint32_t kLongSteps = 16;
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
+void launch_trace_long(const TraceKernelArgs& a, hipStream_t st);
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st);   // slow path, gated on *dup
 
 // Slow path (runs only when *dup != 0; every launch checks the flag first).

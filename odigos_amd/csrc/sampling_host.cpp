@@ -178,6 +178,7 @@ static size_t sampling_scratch_bytes(uint64_t n) {
   s = align_up(s + 4 * 256 * T, 256);  // hist
   s = align_up(s + 4 * 256 * T, 256);  // hist offsets
   s = align_up(s + 8 * htiles, 256);   // scan status (hist)
+  s = align_up(s + 4 * (N / (kLongSteps * 64) + 1), 256);   // long runs
   return s + 256;
 }
 
@@ -258,7 +259,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     off = align_up(off + bytes, 256);
     return p;
   };
-  uint32_t* misc = reinterpret_cast<uint32_t*>(base);   // [0] dup, [2] scan counter (windows), [4] scan counter (hist)
+  uint32_t* misc = reinterpret_cast<uint32_t*>(base);   // [0] dup, [2] scan counter (windows), [4] scan counter (hist), [12] long runs
   uint64_t* win_heads = reinterpret_cast<uint64_t*>(take(8 * W));
   uint32_t* win_base = reinterpret_cast<uint32_t*>(take(4 * W));
   uint64_t* wstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)wtiles));
@@ -271,6 +272,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   uint32_t* hist = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
   uint32_t* hoff = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
   uint64_t* hstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)htiles));
+  uint32_t* long_runs = reinterpret_cast<uint32_t*>(take(4 * (N / (kLongSteps * 64) + 1)));
   if (off > need) return fail(OSE_EINVAL, "internal: trace workspace layout exceeds its bound");
   uint32_t* err = o->device_status ? o->device_status : misc + 8;
   HIP_TRY(hipMemsetAsync(base, 0, 64, st));
@@ -305,11 +307,19 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.route_match = c->route_match;
   a.attr_match = e->sampling_n_attr ? c->attr_match : nullptr;
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
+  a.n_long = misc + 12;
+  a.long_runs = a.mode == kTraceRuns ? long_runs : nullptr;
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);
   launch_trace_eval(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
+  if (a.long_runs) {
+    e->prof_begin("trace_long_kernel", st, tm);
+    launch_trace_long(a, st);
+    HIP_TRY(hipGetLastError());
+    e->prof_end(tm, st);
+  }
 
   if (group_mode == OSE_GROUP_TRACE_ID) {
     // slow path: every launch returns at once unless the fast path set *dup
@@ -366,6 +376,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     }
     TraceKernelArgs b = a;
     b.mode = kTracePerm;
+    b.long_runs = nullptr;   // the sorted pass walks every run itself
     b.perm = vin;
     b.key = key;
     launch_trace_eval(b, st);

@@ -712,9 +712,166 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     }
     base += kWave;
     if (!open && base >= range_end) break;
+    if (open && a.long_runs && base >= range_end + kLongSteps * kWave) {
+      // a long run: trace_long_kernel splits it over a workgroup's waves
+      if (lane == 0) a.long_runs[atomicAdd(a.n_long, 1u)] = (uint32_t)c_pos;
+      break;
+    }
   }
   flush_queue(a, c, Q, qn, lane);
   flush_heads(a, HQ, hn, lane);
+}
+
+// ---- long runs ------------------------------------------------------------------
+// A run the fast path listed (kTraceRuns; still open kLongSteps steps past
+// its owner's windows) is one trace: a workgroup finds its end from the
+// window head masks, its 8 waves fold contiguous 64-span-step pieces of it
+// (per-span contributions exactly as trace_eval_kernel computes them; the
+// latency monoid reduced in lane order, then piece order), wave 0 combines
+// the pieces and decides, and the workgroup writes the run's keep bytes.
+// Workgroups take the listed runs in turn (persistent grid).
+constexpr int kLWaves = 8;
+constexpr int kLThreads = kLWaves * kWave;
+struct LongSmem {
+  uint64_t ep[kLWaves], svc[kLWaves], kmask[kLWaves];
+  uint32_t err[kLWaves];
+  uint64_t lm[kLWaves][kWave], le[kLWaves][kWave];
+  uint32_t lf[kLWaves][kWave];
+  uint32_t end_win;
+  uint32_t keep;
+};
+__global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a) {
+  const uint32_t nl = __hip_atomic_load(a.n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x >= nl) return;
+  __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
+  __shared__ LongSmem sm;
+  {
+    const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
+    for (uint32_t k = threadIdx.x * 16; k < nb; k += kLThreads * 16)
+      *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
+  }
+  const Cfg c = load_cfg(cfg_lds);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint64_t n = a.n_spans;
+  const uint32_t nsvc = c.h->n_services;
+  const bool want_route = c.h->n_lat && !a.route_match && a.route;
+  for (uint32_t r = blockIdx.x; r < nl; r += gridDim.x) {
+    const uint64_t pos = a.long_runs[r];
+    // ---- run end: the first head after pos (window head masks of the fast path)
+    if (threadIdx.x == 0) sm.end_win = 0xFFFFFFFFu;
+    __syncthreads();
+    const uint32_t w0 = (uint32_t)(pos / kWave);
+    const uint64_t m0 = a.win_heads[w0] & ~lanemask_le((int)(pos % kWave));
+    uint64_t end;
+    if (m0) {
+      end = (uint64_t)w0 * kWave + ffs64(m0);
+    } else {
+      for (uint32_t wb = w0 + 1; wb < a.n_windows; wb += kLThreads) {
+        const uint32_t w = wb + threadIdx.x;
+        if (w < a.n_windows && a.win_heads[w]) atomicMin(&sm.end_win, w);
+        __syncthreads();
+        const uint32_t found = sm.end_win;
+        __syncthreads();   // every thread has read it before the next round's atomics
+        if (found != 0xFFFFFFFFu) break;
+      }
+      const uint32_t we = sm.end_win;
+      end = we == 0xFFFFFFFFu ? n : (uint64_t)we * kWave + ffs64(a.win_heads[we]);
+    }
+    // ---- this wave's piece [lo, hi) of [pos, end), whole 64-span steps
+    const uint64_t steps = (end - pos + kWave - 1) / kWave;
+    const uint64_t per = (steps + kLWaves - 1) / kLWaves;
+    const uint64_t lo = pos + (uint64_t)wv * per * kWave, hi = min(end, lo + per * kWave);
+    uint32_t err = 0;
+    uint64_t ep_acc = 0, svc_acc = 0, kmask = 0;
+    Lat cur{0, kInf, 0};   // lane k: latency slot k
+    for (uint64_t base = lo; base < hi; base += kWave) {
+      const uint64_t p = base + lane;
+      const bool valid = p < hi;
+      uint32_t slot = kNoSlot;
+      uint64_t st = 0, en = 0;
+      if (valid) {
+        const uint32_t res = a.resource[p];
+        err |= a.status[p] == OSE_STATUS_ERROR;
+        const uint32_t sv = a.res_svc[res], ss = a.res_svc_str[res];
+        if (ss < nsvc) svc_acc |= c.svc_bits[ss];
+        if (a.attr_match) svc_acc |= a.attr_match[p] << c.h->attr_shift;
+        if (sv < nsvc) {
+          slot = c.svc_slot[sv];
+          if (slot != kNoSlot) {
+            if (a.route_match) {
+              ep_acc |= a.route_match[p] & c.slot_rules[slot];
+            } else {
+              const ose_strref rt = a.route ? a.route[p] : ose_strref{0, 0};
+              const uint4 rw = want_route && rt.len ? head16(a.arena, rt.off, rt.len) : make_uint4(0, 0, 0, 0);
+              ep_acc |= endpoint_bits_w(c, slot, a.arena, rt, rw);
+            }
+            st = a.start[p];
+            en = a.end[p];
+          }
+        }
+      }
+      uint64_t pend = __ballot(slot != kNoSlot);
+      while (pend) {
+        const uint32_t ks = rdl(slot, ffs64(pend));
+        const bool ink = slot == ks;
+        pend &= ~__ballot(ink);
+        Lat v = ink ? Lat{st == 0 ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {   // lane-order reduction into lane 0
+          Lat o;
+          o.f = __shfl_down(v.f, d, kWave);
+          o.m = __shfl_down(v.m, d, kWave);
+          o.e = __shfl_down(v.e, d, kWave);
+          if ((lane & (2 * d - 1)) == 0) v = lat_comb(v, o);
+        }
+        const Lat v0{rdl(v.f, 0), rdl64(v.m, 0), rdl64(v.e, 0)};
+        if ((uint32_t)lane == ks) cur = lat_comb(cur, v0);
+        kmask |= 1ull << ks;
+      }
+    }
+    err = __ballot(err != 0) ? 1u : 0u;
+    ep_acc = wave_or64(ep_acc);
+    svc_acc = wave_or64(svc_acc);
+    sm.lf[wv][lane] = cur.f;
+    sm.lm[wv][lane] = cur.m;
+    sm.le[wv][lane] = cur.e;
+    if (lane == 0) {
+      sm.err[wv] = err;
+      sm.ep[wv] = ep_acc;
+      sm.svc[wv] = svc_acc;
+      sm.kmask[wv] = kmask;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      uint32_t E = 0;
+      uint64_t EP = 0, SV = 0, K = 0;
+      Lat tot{0, kInf, 0};
+      for (int w = 0; w < kLWaves; w++) {
+        E |= sm.err[w];
+        EP |= sm.ep[w];
+        SV |= sm.svc[w];
+        K |= sm.kmask[w];
+        if ((sm.kmask[w] >> lane) & 1) tot = lat_comb(tot, Lat{sm.lf[w][lane], sm.lm[w][lane], sm.le[w][lane]});
+      }
+      uint64_t s_l = 0;
+      if ((K >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, tot.m, tot.e);
+      s_l = wave_or64(s_l);
+      if (lane == 0) {
+        const uint4 t = reinterpret_cast<const uint4*>(a.tid)[pos];
+        uint8_t dk = 0, dl = 0;
+        double dr = 0;
+        decide(c, E, EP, s_l, SV, trace_uniform((uint64_t)t.x | ((uint64_t)t.y << 32), (uint64_t)t.z | ((uint64_t)t.w << 32), a.seed),
+               dk, dl, dr);
+        write_rec(a, pos, dk, dl, dr);
+        sm.keep = dk;
+      }
+    }
+    __syncthreads();
+    const uint8_t k = (uint8_t)sm.keep;
+    for (uint64_t q = pos + threadIdx.x; q < end; q += kLThreads) a.keep[q] = k;
+    __syncthreads();
+  }
 }
 
 // ---- slow path ---------------------------------------------------------------
@@ -1020,6 +1177,10 @@ void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t per_block = kTWaves * kWinPerWave;
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
   hipLaunchKernelGGL(trace_eval_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
+}
+void launch_trace_long(const TraceKernelArgs& a, hipStream_t st) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(a.n_spans / (kLongSteps * kWave) + 1, 1024);
+  hipLaunchKernelGGL(trace_long_kernel, dim3(blocks), dim3(kLThreads), 0, st, a);
 }
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st) {
   if (a.n_spans)

@@ -298,3 +298,30 @@ def test_long_prefix_config_oracle_vs_python():
 def test_gpu_sampling_long_prefixes():
     gpu_vs_oracle(Generator("sampling", seed=0x0D160063, n_spans=300_000), cfg=long_prefix_config())
     gpu_vs_oracle(Generator("sampling", seed=0x0D160073, n_spans=100_000, shuffle=True), cfg=long_prefix_config())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0x0D160105, 0x0D160205])
+def test_gpu_sampling_long_runs_split(seed):
+    # runs still open kLongSteps steps past their owner's windows are decided
+    # by trace_long_kernel (a workgroup folds contiguous pieces in order):
+    # zero starts reset minStart inside and across the pieces, fractional
+    # ratios make the decision depend on the injected uniform
+    g = Generator("zipf", seed=seed, n_spans=600_000)
+    inject_zero_starts(g, 0.01, seed & 0xFF)
+    gpu_vs_oracle(g, cfg=fractional_config(), seed=seed)
+    gpu_vs_oracle(g, cfg=long_prefix_config())
+
+
+@pytest.mark.gpu
+def test_gpu_sampling_long_runs_slow_path():
+    # shuffled Zipf traces: split runs send the batch down the sort-based
+    # path, which must overwrite the long-run decisions of the fast pass
+    gpu_vs_oracle(Generator("zipf", seed=0x0D160305, n_spans=300_000, shuffle=True))
+
+
+@pytest.mark.gpu
+def test_gpu_sampling_parity_full_c5():
+    # BASELINE.json configs[4]: 50M spans, Zipf(1.1) trace sizes up to 50k
+    g = Generator("zipf", seed=0x0D160005, n_spans=50_000_000, threads=16)
+    gpu_vs_oracle(g, per_trace=True)

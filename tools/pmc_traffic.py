@@ -8,8 +8,9 @@ import csv, glob, json, re, sys
 from collections import defaultdict
 
 wl, root, out = sys.argv[1], sys.argv[2], sys.argv[3]
-STAGES = {"url": ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel"), "sampling": ("trace_eval_kernel",),
-          "fused": ("trace_eval_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel",
+STAGES = {"url": ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel"), "sampling": ("trace_eval_kernel", "trace_long_kernel"),
+          "zipf": ("trace_eval_kernel", "trace_long_kernel"),
+          "fused": ("trace_eval_kernel", "trace_long_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel",
                     "size_span_kernel", "size_scope_kernel", "size_res_kernel")}
 kernels = STAGES[wl]
 vals = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
