@@ -111,9 +111,10 @@ struct TraceKernelArgs {
   // kTraceRuns: runs still open kLongSteps steps past their owner's windows
   // are listed here (head positions) and decided by trace_long_kernel
   uint32_t* n_long;
-  uint32_t* long_runs;        // [n_spans / (kLongSteps * 64) + 1]
+  uint32_t* long_runs;        // [n_spans / 64 + 1]
+  uint32_t long_steps;        // hand-off distance in 64-span steps (kLongSteps)
 };
-constexpr uint32_t kLongSteps = 16;
+constexpr uint32_t kLongSteps = 4;   // tools/gpu_long_iter.sh: C5 16 -> 4 steps 2.75 -> 2.13 ms, C3 unchanged
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st);
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st);   // slow path, gated on *dup

@@ -178,7 +178,7 @@ static size_t sampling_scratch_bytes(uint64_t n) {
   s = align_up(s + 4 * 256 * T, 256);  // hist
   s = align_up(s + 4 * 256 * T, 256);  // hist offsets
   s = align_up(s + 8 * htiles, 256);   // scan status (hist)
-  s = align_up(s + 4 * (N / (kLongSteps * 64) + 1), 256);   // long runs
+  s = align_up(s + 4 * (N / 64 + 1), 256);   // long runs
   return s + 256;
 }
 
@@ -272,7 +272,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   uint32_t* hist = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
   uint32_t* hoff = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
   uint64_t* hstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)htiles));
-  uint32_t* long_runs = reinterpret_cast<uint32_t*>(take(4 * (N / (kLongSteps * 64) + 1)));
+  uint32_t* long_runs = reinterpret_cast<uint32_t*>(take(4 * (N / 64 + 1)));
   if (off > need) return fail(OSE_EINVAL, "internal: trace workspace layout exceeds its bound");
   uint32_t* err = o->device_status ? o->device_status : misc + 8;
   HIP_TRY(hipMemsetAsync(base, 0, 64, st));
@@ -309,6 +309,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
   a.n_long = misc + 12;
   a.long_runs = a.mode == kTraceRuns ? long_runs : nullptr;
+  a.long_steps = kLongSteps;
+  if (const char* ls = getenv("OSE_LONG_STEPS")) a.long_steps = std::max<uint32_t>(1, (uint32_t)strtoul(ls, nullptr, 0));   // tuning
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);
   launch_trace_eval(a, st);

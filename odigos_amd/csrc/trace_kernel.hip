@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     }
     base += kWave;
     if (!open && base >= range_end) break;
-    if (open && a.long_runs && base >= range_end + kLongSteps * kWave) {
+    if (open && a.long_runs && base >= range_end + (uint64_t)a.long_steps * kWave) {
       // a long run: trace_long_kernel splits it over a workgroup's waves
       if (lane == 0) a.long_runs[atomicAdd(a.n_long, 1u)] = (uint32_t)c_pos;
       break;
@@ -723,13 +723,33 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
 }
 
 // ---- long runs ------------------------------------------------------------------
-// A run the fast path listed (kTraceRuns; still open kLongSteps steps past
+// A run the fast path listed (kTraceRuns; still open long_steps steps past
 // its owner's windows) is one trace: a workgroup finds its end from the
 // window head masks, its 8 waves fold contiguous 64-span-step pieces of it
 // (per-span contributions exactly as trace_eval_kernel computes them; the
 // latency monoid reduced in lane order, then piece order), wave 0 combines
 // the pieces and decides, and the workgroup writes the run's keep bytes.
 // Workgroups take the listed runs in turn (persistent grid).
+// the columns of one span of a long run (loaded one step ahead)
+struct LongRaw {
+  uint32_t res, status;
+  uint64_t st, en, am, rm;
+  ose_strref rt;
+};
+__device__ __forceinline__ LongRaw long_raw(const TraceKernelArgs& a, uint64_t p, uint64_t hi) {
+  LongRaw r{};
+  if (p >= hi) return r;
+  r.res = a.resource[p];
+  r.status = a.status[p];
+  if (a.start) {
+    r.st = a.start[p];
+    r.en = a.end[p];
+  }
+  if (a.attr_match) r.am = a.attr_match[p];
+  if (a.route_match) r.rm = a.route_match[p];
+  else if (a.route) r.rt = a.route[p];
+  return r;
+}
 constexpr int kLWaves = 8;
 constexpr int kLThreads = kLWaves * kWave;
 struct LongSmem {
@@ -785,29 +805,31 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
     uint32_t err = 0;
     uint64_t ep_acc = 0, svc_acc = 0, kmask = 0;
     Lat cur{0, kInf, 0};   // lane k: latency slot k
+    LongRaw nx = long_raw(a, lo + lane, hi);
     for (uint64_t base = lo; base < hi; base += kWave) {
       const uint64_t p = base + lane;
       const bool valid = p < hi;
+      const LongRaw r = nx;
+      uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu;
+      uint4 rw = make_uint4(0, 0, 0, 0);
+      if (valid) {   // this step's dependent loads, then the next step's columns
+        sv = a.res_svc[r.res];
+        ss = a.res_svc_str[r.res];
+        if (want_route && r.rt.len) rw = head16(a.arena, r.rt.off, r.rt.len);
+      }
+      if (base + kWave < hi) nx = long_raw(a, p + kWave, hi);
       uint32_t slot = kNoSlot;
       uint64_t st = 0, en = 0;
       if (valid) {
-        const uint32_t res = a.resource[p];
-        err |= a.status[p] == OSE_STATUS_ERROR;
-        const uint32_t sv = a.res_svc[res], ss = a.res_svc_str[res];
+        err |= r.status == OSE_STATUS_ERROR;
         if (ss < nsvc) svc_acc |= c.svc_bits[ss];
-        if (a.attr_match) svc_acc |= a.attr_match[p] << c.h->attr_shift;
+        svc_acc |= r.am << c.h->attr_shift;
         if (sv < nsvc) {
           slot = c.svc_slot[sv];
           if (slot != kNoSlot) {
-            if (a.route_match) {
-              ep_acc |= a.route_match[p] & c.slot_rules[slot];
-            } else {
-              const ose_strref rt = a.route ? a.route[p] : ose_strref{0, 0};
-              const uint4 rw = want_route && rt.len ? head16(a.arena, rt.off, rt.len) : make_uint4(0, 0, 0, 0);
-              ep_acc |= endpoint_bits_w(c, slot, a.arena, rt, rw);
-            }
-            st = a.start[p];
-            en = a.end[p];
+            ep_acc |= a.route_match ? r.rm & c.slot_rules[slot] : endpoint_bits_w(c, slot, a.arena, r.rt, rw);
+            st = r.st;
+            en = r.en;
           }
         }
       }
@@ -1179,7 +1201,7 @@ void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(trace_eval_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
 }
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(a.n_spans / (kLongSteps * kWave) + 1, 1024);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(a.n_spans / ((uint64_t)a.long_steps * kWave) + 1, 1024);
   hipLaunchKernelGGL(trace_long_kernel, dim3(blocks), dim3(kLThreads), 0, st, a);
 }
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st) {
