@@ -310,9 +310,13 @@ struct StepRaw {
   uint32_t status;
   ose_strref route;
   uint64_t start, end;
+  bool full;           // the per-span columns below the trace id were loaded
 };
-__device__ __forceinline__ StepRaw load_raw(const TraceKernelArgs& a, uint64_t base, int lane) {
+// full = false loads only what the head test needs: a wave skipping windows
+// inside a run an earlier wave owns reads 16 B per span, not every column.
+__device__ __forceinline__ StepRaw load_raw(const TraceKernelArgs& a, uint64_t base, int lane, bool full = true) {
   StepRaw r{};
+  r.full = full;
   const uint64_t p = base + lane;
   const bool valid = p < a.n_spans;
   if (!valid) return r;
@@ -330,6 +334,7 @@ __device__ __forceinline__ StepRaw load_raw(const TraceKernelArgs& a, uint64_t b
   const uint4 v = reinterpret_cast<const uint4*>(a.tid)[r.i];
   r.hi = (uint64_t)v.x | ((uint64_t)v.y << 32);
   r.lo = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  if (!full) return r;
   r.res = a.resource[r.i];
   r.status = a.status[r.i];
   if (a.start) {
@@ -523,12 +528,14 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     // the next step's column loads, then the arithmetic — a wait for a load
     // also waits for every load issued before it (vmcnt counts in order),
     // so nothing this step consumes may be issued after the prefetch.
-    const StepRaw r = nx;
+    StepRaw r = nx;
     const bool valid = base + lane < n;
     const bool hd = step_head(a, r, base, lane);
+    const bool work = started || __ballot(hd) != 0;   // wave-uniform: this step is evaluated
+    if (work && !r.full) r = load_raw(a, base, lane);   // first owned step after skipped ones
     uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu;
     uint4 rw = make_uint4(0, 0, 0, 0);
-    if (valid) {
+    if (valid && work) {
       sv = a.res_svc[r.res];
       ss = a.res_svc_str[r.res];
       if (want_route && r.route.len) rw = head16(a.arena, r.route.off, r.route.len);
@@ -549,7 +556,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         hn += nh;
       }
     }
-    if (base + kWave < n) nx = load_raw(a, base + kWave, lane);   // prefetch the next step
+    if (base + kWave < n) nx = load_raw(a, base + kWave, lane, work);   // prefetch the next step
     uint64_t own;
     if (in_range) {
       if (!started) {
