@@ -538,7 +538,11 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     if (valid && work) {
       sv = a.res_svc[r.res];
       ss = a.res_svc_str[r.res];
-      if (want_route && r.route.len) rw = head16(a.arena, r.route.off, r.route.len);
+      // route bytes only for spans of a latency-rule service (strings.HasPrefix
+      // is evaluated for nothing else): one dependent LDS lookup, and the
+      // random 16-byte arena reads of every other routed span are skipped
+      if (want_route && r.route.len && sv < nsvc && c.svc_slot[sv] != kNoSlot)
+        rw = head16(a.arena, r.route.off, r.route.len);
     }
     const uint64_t vmask = __ballot(valid);
     const uint64_t hmask = __ballot(hd);
@@ -822,7 +826,8 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
       if (valid) {   // this step's dependent loads, then the next step's columns
         sv = a.res_svc[r.res];
         ss = a.res_svc_str[r.res];
-        if (want_route && r.rt.len) rw = head16(a.arena, r.rt.off, r.rt.len);
+        if (want_route && r.rt.len && sv < nsvc && c.svc_slot[sv] != kNoSlot)
+          rw = head16(a.arena, r.rt.off, r.rt.len);
       }
       if (base + kWave < hi) nx = long_raw(a, p + kWave, hi);
       uint32_t slot = kNoSlot;
