@@ -916,35 +916,43 @@ __device__ __forceinline__ bool gated(const uint32_t* g) {
 // Exact table of the slow path: every run head inserts its full trace id
 // (table_insert's publish protocol); a trace's entry keeps its smallest
 // run-head position.
+// Gated kernels use a grid-stride loop over a capped grid: when the gate is
+// closed (the common case) the launch costs a few microseconds, not one
+// block per 256 spans.
+constexpr uint32_t kGatedBlocks = 2048;
 __global__ __launch_bounds__(256) void trace_insert_exact_kernel(TraceKernelArgs a) {
   if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= a.n_spans) return;
-  const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
-  if (p > 0 && a.tid[2 * p - 2] == hi && a.tid[2 * p - 1] == lo) return;
-  table_insert(a, hi, lo, (uint32_t)p);
+  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < a.n_spans; p += (uint64_t)gridDim.x * 256) {
+    const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
+    if (p > 0 && a.tid[2 * p - 2] == hi && a.tid[2 * p - 1] == lo) continue;
+    table_insert(a, hi, lo, (uint32_t)p);
+  }
 }
 
 // key[i] = first run-head position of span i's trace_id (read-only probe of
 // the table the fast path filled).
 __global__ __launch_bounds__(256) void trace_key_kernel(TraceSortArgs a) {
   if (gated(a.gate)) return;
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n_spans) return;
-  const uint64_t hi = a.tid[2 * i], lo = a.tid[2 * i + 1];
   const uint32_t ready = (a.epoch << 2) | 2u;
-  uint64_t h = tid_hash(hi, lo) & a.table_mask;
-  for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
-    const TraceSlot& s = a.table[h];
-    if (s.state == ready && s.hi == hi && s.lo == lo) {
-      a.key[i] = s.first;
-      return;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n_spans; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t hi = a.tid[2 * i], lo = a.tid[2 * i + 1];
+    uint64_t h = tid_hash(hi, lo) & a.table_mask;
+    bool found = false;
+    for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
+      const TraceSlot& s = a.table[h];
+      if (s.state == ready && s.hi == hi && s.lo == lo) {
+        a.key[i] = s.first;
+        found = true;
+        break;
+      }
+      if ((s.state >> 2) != a.epoch) break;
+      h = (h + 1) & a.table_mask;
     }
-    if ((s.state >> 2) != a.epoch) break;
-    h = (h + 1) & a.table_mask;
+    if (!found) {
+      atomicOr(a.error, 4u);
+      a.key[i] = 0;
+    }
   }
-  atomicOr(a.error, 4u);
-  a.key[i] = 0;
 }
 
 constexpr int kSortThreads = 256;
@@ -1218,10 +1226,11 @@ void launch_trace_long(const TraceKernelArgs& a, hipStream_t st) {
 }
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st) {
   if (a.n_spans)
-    hipLaunchKernelGGL(trace_insert_exact_kernel, dim3((uint32_t)((a.n_spans + 255) / 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(trace_insert_exact_kernel, dim3((uint32_t)std::min<uint64_t>((a.n_spans + 255) / 256, kGatedBlocks)),
+                       dim3(256), 0, st, a);
 }
 void launch_trace_key(const TraceSortArgs& a, hipStream_t st) {
-  const uint64_t blocks = (a.n_spans + 255) / 256;
+  const uint64_t blocks = std::min<uint64_t>((a.n_spans + 255) / 256, kGatedBlocks);
   hipLaunchKernelGGL(trace_key_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, a);
 }
 void launch_sort_hist(const TraceSortArgs& a, hipStream_t st) {
