@@ -136,6 +136,11 @@ struct TraceSortArgs {
   uint32_t* hist;             // [256 * n_tiles] digit-major
   uint32_t* key;              // canonical key per span (trace_key kernel output)
   uint32_t* error;
+  // sort_hist_kernel zeroes the following scan's tile counter and look-back
+  // status (only when the gate is open: no memset launches per closed call)
+  uint32_t* scan_counter;
+  uint64_t* scan_status;
+  uint32_t scan_status_n;
 };
 constexpr uint32_t kSortTile = 4096;
 void launch_trace_key(const TraceSortArgs& a, hipStream_t st);

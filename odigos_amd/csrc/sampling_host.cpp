@@ -353,10 +353,11 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
       s.keys_out = kbuf[pass & 1];
       s.vals_out = vbuf[pass & 1];
       s.hist = hist;
+      s.scan_counter = misc + 4;
+      s.scan_status = hstatus;
+      s.scan_status_n = htiles;
       launch_sort_hist(s, st);
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemsetAsync(misc + 4, 0, 4, st));
-      HIP_TRY(hipMemsetAsync(hstatus, 0, 8 * (size_t)htiles, st));
       ScanArgs sa{};
       sa.n = 256 * T;
       sa.n_tiles = htiles;

@@ -962,6 +962,11 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist_kernel(TraceSortArgs a
   if (gated(a.gate)) return;
   __shared__ uint32_t hist[256];
   const int t = threadIdx.x;
+  if (a.scan_status) {
+    for (uint32_t k = blockIdx.x * kSortThreads + t; k < a.scan_status_n; k += gridDim.x * kSortThreads)
+      a.scan_status[k] = 0;
+    if (blockIdx.x == 0 && t == 0) *a.scan_counter = 0;
+  }
   hist[t] = 0;
   __syncthreads();
   const uint32_t* keys = a.keys_in ? a.keys_in : a.key;
