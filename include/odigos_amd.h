@@ -278,14 +278,21 @@ int ose_profile_read(ose_engine* eng, char* json, size_t cap);
  * the keep bytes go back with the reverse all-to-all, and
  * ose_shard_scatter_keep puts them at the original spans.  All pointers are
  * device pointers; calls are asynchronous on hip_stream.                    */
+/* Record: u64 trace_id hi, lo, start_ns, end_ns, endpoint bits (the
+ * latency rules whose HasPrefix matched), then u64 {res_svc : 24 |
+ * res_svc_str : 24 | status : 8} (ids no rule names travel as 0xFFFFFF and
+ * unpack as 0xFFFFFFFF), then u64 attr_match only when the engine has
+ * span_attribute rules: ose_shard_record_bytes() = 48 or 56 bytes
+ * (OSE_XREC_BYTES is the largest). */
 #define OSE_XREC_BYTES 64u
+uint32_t ose_shard_record_bytes(const ose_engine* eng);
 uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks);
 int ose_shard_pack(ose_engine* eng, const ose_columns* cols, uint32_t n_ranks, void* send,
                    uint64_t* counts, uint32_t* pack_pos, void* hip_stream);
-int ose_shard_unpack(const void* recv, uint64_t n, uint64_t* trace_id, uint64_t* start_ns,
-                     uint64_t* end_ns, uint8_t* status, uint32_t* resource, uint32_t* res_svc,
-                     uint32_t* res_svc_str, uint64_t* route_match, uint64_t* attr_match,
-                     void* hip_stream);
+int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t* trace_id,
+                     uint64_t* start_ns, uint64_t* end_ns, uint8_t* status, uint32_t* resource,
+                     uint32_t* res_svc, uint32_t* res_svc_str, uint64_t* route_match,
+                     uint64_t* attr_match, void* hip_stream);
 int ose_shard_scatter_keep(const uint8_t* keep_back, const uint32_t* pack_pos, uint64_t n,
                            uint8_t* keep, void* hip_stream);
 

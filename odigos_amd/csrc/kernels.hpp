@@ -197,7 +197,8 @@ struct ShardArgs {
   uint32_t* hist;             // [n_ranks * n_tiles] counts, then offsets (second buffer)
   uint32_t* hoff;
   uint64_t* counts;           // [n_ranks] zeroed before launch
-  uint8_t* send;              // [n * kXRec]
+  uint8_t* send;              // [n * rec_words * 8]
+  uint32_t rec_words;         // 6 (48-byte records) or 7 (with span_attribute bits)
   uint32_t* pack_pos;         // [n]
 };
 constexpr uint32_t kXRec = 64;
@@ -215,6 +216,7 @@ struct UnpackArgs {
   uint32_t* res_svc_str;
   uint64_t* route_match;
   uint64_t* attr_match;
+  uint32_t rec_words;
 };
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st);
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);

@@ -28,6 +28,12 @@ uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks) {
   return n_ranks ? shard_owner_host(tid_hi, tid_lo, n_ranks) : 0;
 }
 
+uint32_t ose_shard_record_bytes(const ose_engine* eng) {
+  const Engine* e = reinterpret_cast<const Engine*>(eng);
+  if (!e || !e->has_sampling) return 0;
+  return e->sampling_n_attr ? 56u : 48u;
+}
+
 int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void* send, uint64_t* counts,
                    uint32_t* pack_pos, void* hip_stream) {
   if (!eng || !c || !send || !counts || !pack_pos) return fail(OSE_EINVAL, "NULL argument");
@@ -79,6 +85,7 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.counts = counts;
   a.send = static_cast<uint8_t*>(send);
   a.pack_pos = pack_pos;
+  a.rec_words = ose_shard_record_bytes(eng) / 8;
   uint32_t* err = reinterpret_cast<uint32_t*>(base) + 8;
   rc = 0;
   do {
@@ -106,14 +113,15 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   return rc;
 }
 
-int ose_shard_unpack(const void* recv, uint64_t n, uint64_t* trace_id, uint64_t* start_ns, uint64_t* end_ns,
-                     uint8_t* status, uint32_t* resource, uint32_t* res_svc, uint32_t* res_svc_str,
+int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t* trace_id, uint64_t* start_ns,
+                     uint64_t* end_ns, uint8_t* status, uint32_t* resource, uint32_t* res_svc, uint32_t* res_svc_str,
                      uint64_t* route_match, uint64_t* attr_match, void* hip_stream) {
+  if (rec_bytes != 48 && rec_bytes != 56) return fail(OSE_EINVAL, "rec_bytes must be ose_shard_record_bytes()");
   if (n && (!recv || !trace_id || !start_ns || !end_ns || !status || !resource || !res_svc || !res_svc_str ||
             !route_match || !attr_match))
     return fail(OSE_EINVAL, "NULL argument");
   UnpackArgs a{static_cast<const uint8_t*>(recv), n, trace_id, start_ns, end_ns, status, resource, res_svc, res_svc_str,
-               route_match, attr_match};
+               route_match, attr_match, rec_bytes / 8};
   launch_shard_unpack(a, static_cast<hipStream_t>(hip_stream));
   HIP_TRY(hipGetLastError());
   return 0;

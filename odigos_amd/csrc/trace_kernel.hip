@@ -1083,6 +1083,7 @@ __global__ __launch_bounds__(kTThreads) void trace_compact_kernel(TraceCompactAr
 }
 
 // ---- trace-id exchange ---------------------------------------------------------
+constexpr uint32_t kXNone = 0xFFFFFFu;   // 24-bit "no rule names this service"
 __device__ __forceinline__ uint32_t shard_owner(uint64_t hi, uint64_t lo, uint32_t n) {
   return (uint32_t)((tid_hash(hi, lo) >> 32) % n);
 }
@@ -1159,15 +1160,17 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
         if (slot != kNoSlot)
           ep = a.route_match ? a.route_match[j] & c.slot_rules[slot] : endpoint_bits(c, slot, a.arena, a.route[j]);
       }
-      uint64_t* rec = reinterpret_cast<uint64_t*>(a.send + (uint64_t)pos * kXRec);
+      // record (include/odigos_amd.h "trace-id exchange"): service ids the
+      // rules do not name all behave as NONE, so they travel as 24 bits
+      uint64_t* rec = reinterpret_cast<uint64_t*>(a.send + (uint64_t)pos * a.rec_words * 8);
       rec[0] = hi;
       rec[1] = lo;
       rec[2] = a.start ? a.start[j] : 0;
       rec[3] = a.end ? a.end[j] : 0;
       rec[4] = ep;
-      rec[5] = (uint64_t)s | ((uint64_t)ss << 32);
-      rec[6] = a.status[j];
-      rec[7] = a.attr_match ? a.attr_match[j] : 0;
+      rec[5] = (uint64_t)(s < nsvc ? s : kXNone) | ((uint64_t)(ss < nsvc ? ss : kXNone) << 24) |
+               ((uint64_t)a.status[j] << 48);
+      if (a.rec_words > 6) rec[6] = a.attr_match ? a.attr_match[j] : 0;
       a.pack_pos[j] = pos;
     }
   }
@@ -1176,17 +1179,18 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
 __global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
-  const uint64_t* rec = reinterpret_cast<const uint64_t*>(a.recv + i * kXRec);
+  const uint64_t* rec = reinterpret_cast<const uint64_t*>(a.recv + i * a.rec_words * 8);
   a.tid[2 * i] = rec[0];
   a.tid[2 * i + 1] = rec[1];
   a.start[i] = rec[2];
   a.end[i] = rec[3];
   a.route_match[i] = rec[4];
   const uint64_t sv = rec[5];
-  a.res_svc[i] = (uint32_t)sv;
-  a.res_svc_str[i] = (uint32_t)(sv >> 32);
-  a.status[i] = (uint8_t)rec[6];
-  a.attr_match[i] = rec[7];
+  const uint32_t s = (uint32_t)(sv & kXNone), ss = (uint32_t)((sv >> 24) & kXNone);
+  a.res_svc[i] = s == kXNone ? 0xFFFFFFFFu : s;
+  a.res_svc_str[i] = ss == kXNone ? 0xFFFFFFFFu : ss;
+  a.status[i] = (uint8_t)(sv >> 48);
+  a.attr_match[i] = a.rec_words > 6 ? rec[6] : 0;
   a.resource[i] = (uint32_t)i;   // one "resource" per received span carries its service ids
 }
 

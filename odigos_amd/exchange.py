@@ -5,7 +5,8 @@ that co-location is the node collector's loadbalancing exporter keyed by
 trace id (autoscaler/controllers/nodecollector/collectorconfig/
 traces.go:26-84).  Here, per step:
 
-1. ``ose_shard_pack`` buckets, per span, the 64-byte record the trace stage
+1. ``ose_shard_pack`` buckets, per span, the 48-byte record (56 with
+   span_attribute bits) the trace stage
    reads (trace id, start, end, endpoint-match bits, service ids, status,
    span_attribute bits) by
    owner = hash(trace id) mod world, keeping batch order inside a bucket;
@@ -26,13 +27,13 @@ import ctypes as C
 
 from . import native
 
-XREC = native.XREC_BYTES
 
 
 def route_and_sample(ops, world: int, group=None) -> None:
     """One exchange round; ops provides pack/alloc/unpack_sample/scatter."""
     import torch
     import torch.distributed as dist
+    XREC = ops.rec_bytes                                # bytes per exchanged span record
     send, counts, pos = ops.pack(world)                 # counts: int64 tensor [world] on ops.device
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=group)
@@ -59,7 +60,10 @@ class DeviceExchange:
         self.device = torch.device("cuda", torch.cuda.current_device())
         n = db.cols.n_spans
         self.n = n
-        self.send = torch.empty(max(n, 1) * XREC, dtype=torch.uint8, device=self.device)
+        self.rec_bytes = int(self.L.ose_shard_record_bytes(engine.h))
+        if not self.rec_bytes:
+            raise RuntimeError("the trace-id exchange needs odigossampling on the engine")
+        self.send = torch.empty(max(n, 1) * self.rec_bytes, dtype=torch.uint8, device=self.device)
         self.pos = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         self.counts = None
         self._recv_cap = 0
@@ -101,7 +105,7 @@ class DeviceExchange:
     def unpack_sample(self, recv, n):
         x = self._ensure(n)
         p = {k: v.data_ptr() for k, v in x.items()}
-        native.check(self.L.ose_shard_unpack(recv.data_ptr(), n, p["trace_id"], p["start_ns"], p["end_ns"],
+        native.check(self.L.ose_shard_unpack(recv.data_ptr(), n, self.rec_bytes, p["trace_id"], p["start_ns"], p["end_ns"],
                                              p["status"], p["resource"], p["res_svc"], p["res_svc_str"],
                                              p["route_match"], p["attr_match"], self._s()))
         cols = native.Columns()

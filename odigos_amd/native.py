@@ -124,7 +124,8 @@ def lib() -> C.CDLL:
         "ose_device_info": (C.c_int, [C.c_char_p, C.c_size_t]),
         "ose_shard_owner": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint32]),
         "ose_shard_pack": (C.c_int, [_p, C.POINTER(Columns), C.c_uint32, _p, _p, _p, _p]),
-        "ose_shard_unpack": (C.c_int, [_p, C.c_uint64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+        "ose_shard_unpack": (C.c_int, [_p, C.c_uint64, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+        "ose_shard_record_bytes": (C.c_uint32, [_p]),
         "ose_shard_scatter_keep": (C.c_int, [_p, _p, C.c_uint64, _p, _p]),
         "ose_profile_enable": (C.c_int, [_p, C.c_int]),
         "ose_profile_read": (C.c_int, [_p, C.c_char_p, C.c_size_t]),

@@ -1,5 +1,5 @@
 """numpy restatement of the trace-id exchange records (test infrastructure):
-owner hash, stable per-owner bucketing, the 56-byte record and its unpacking
+owner hash, stable per-owner bucketing, the 48/56-byte record and its unpacking
 (odigos_amd/csrc/trace_kernel.hip shard_* kernels, include/odigos_amd.h
 ose_shard_*), plus CPU ops for odigos_amd.exchange.route_and_sample."""
 from __future__ import annotations
@@ -10,9 +10,24 @@ import numpy as np
 
 from odigos_amd import native
 
-XDT = np.dtype([("hi", "<u8"), ("lo", "<u8"), ("start", "<u8"), ("end", "<u8"), ("ep", "<u8"),
-                ("svc", "<u4"), ("svc_str", "<u4"), ("status", "<u8"), ("attr", "<u8")])
-assert XDT.itemsize == native.XREC_BYTES
+NONE24 = 0xFFFFFF   # service ids no rule names travel as 24-bit NONE
+
+
+def rec_layout(cfg: dict):
+    """(interned service count, records carry attr_match) for a sampling config."""
+    from tests.oracle_lib import intern_services
+    with_attr = any(r.get("type") == "span_attribute"
+                    for lvl in ("global_rules", "service_rules", "endpoint_rules") for r in cfg.get(lvl) or [])
+    return len(intern_services(cfg)), with_attr
+
+
+def xdt(with_attr: bool) -> np.dtype:
+    f = [("hi", "<u8"), ("lo", "<u8"), ("start", "<u8"), ("end", "<u8"), ("ep", "<u8"), ("sv", "<u8")]
+    return np.dtype(f + ([("attr", "<u8")] if with_attr else []))
+
+
+def rec_bytes(cfg: dict) -> int:
+    return xdt(rec_layout(cfg)[1]).itemsize
 
 M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
@@ -49,15 +64,19 @@ def endpoint_bits(cfg: dict, res_svc_of_span, route_bytes) -> np.ndarray:
     return out
 
 
-def pack(tid: np.ndarray, start, end, status, svc, svc_str, ep, world: int, attr=None):
+def pack(tid: np.ndarray, start, end, status, svc, svc_str, ep, world: int, attr=None, *, cfg: dict):
     """-> (records in bucket order, counts[world], pack_pos[n])"""
+    nsvc, with_attr = rec_layout(cfg)
     hi, lo = tid[:, 0], tid[:, 1]
     own = owners(hi, lo, world)
     order = np.argsort(own, kind="stable")
-    rec = np.zeros(len(hi), dtype=XDT)
+    rec = np.zeros(len(hi), dtype=xdt(with_attr))
     rec["hi"], rec["lo"], rec["start"], rec["end"], rec["ep"] = hi, lo, start, end, ep
-    rec["svc"], rec["svc_str"], rec["status"] = svc, svc_str, status
-    rec["attr"] = 0 if attr is None else attr
+    s = np.where(np.asarray(svc, np.uint64) < nsvc, np.asarray(svc, np.uint64), NONE24)
+    ss = np.where(np.asarray(svc_str, np.uint64) < nsvc, np.asarray(svc_str, np.uint64), NONE24)
+    rec["sv"] = (s | (ss << np.uint64(24)) | (np.asarray(status, np.uint64) << np.uint64(48))).astype(np.uint64)
+    if with_attr:
+        rec["attr"] = 0 if attr is None else attr
     pos = np.empty(len(hi), dtype=np.int64)
     pos[order] = np.arange(len(hi))
     return rec[order], np.bincount(own, minlength=world).astype(np.int64), pos
@@ -86,11 +105,17 @@ class HostCols:
             setattr(self.cols, k, v.ctypes.data)
 
 
-def unpack(recv: np.ndarray) -> HostCols:
-    r = recv.view(XDT)
+def unpack(recv: np.ndarray, cfg: dict) -> HostCols:
+    nsvc, with_attr = rec_layout(cfg)
+    r = recv.view(xdt(with_attr))
     tid = np.stack([r["hi"], r["lo"]], axis=1)
-    return HostCols(tid, r["start"], r["end"], r["status"].astype(np.uint8), r["svc"], r["svc_str"], r["ep"],
-                    r["attr"])
+    sv = r["sv"]
+    s = (sv & np.uint64(NONE24)).astype(np.uint32)
+    ss = ((sv >> np.uint64(24)) & np.uint64(NONE24)).astype(np.uint32)
+    s[s == NONE24] = 0xFFFFFFFF
+    ss[ss == NONE24] = 0xFFFFFFFF
+    status = (sv >> np.uint64(48)).astype(np.uint8)
+    return HostCols(tid, r["start"], r["end"], status, s, ss, r["ep"], r["attr"] if with_attr else None)
 
 
 class CpuOps:
@@ -100,6 +125,7 @@ class CpuOps:
     def __init__(self, batch: HostCols, cfg: dict, seed: int):
         import torch
         self.torch, self.b, self.cfg, self.seed = torch, batch, cfg, seed
+        self.rec_bytes = rec_bytes(cfg)
         self.device = torch.device("cpu")
         self.keep = np.zeros(batch.cols.n_spans, dtype=np.uint8)
 
@@ -108,7 +134,7 @@ class CpuOps:
         n = self.b.cols.n_spans
         rec, counts, pos = pack(a["trace_id"][: 2 * n].reshape(-1, 2), a["start_ns"][:n], a["end_ns"][:n],
                                 a["status"][:n], a["res_svc"][:n], a["res_svc_str"][:n], a["route_match"][:n], world,
-                                a["attr_match"][:n])
+                                a["attr_match"][:n], cfg=self.cfg)
         self.pos = pos
         return (self.torch.from_numpy(rec.view(np.uint8).copy()), self.torch.from_numpy(counts), pos)
 
@@ -118,7 +144,7 @@ class CpuOps:
     def unpack_sample(self, recv, n):
         from odigos_amd.batch import HostOutputs
         from tests.oracle_lib import SamplingOracle
-        hc = unpack(recv.numpy()[: n * native.XREC_BYTES].copy())
+        hc = unpack(recv.numpy()[: n * self.rec_bytes].copy(), self.cfg)
         ho = HostOutputs(hc.cols)
         assert SamplingOracle(self.cfg).process(hc.cols, ho.outs, native.GROUP_TRACE_ID, self.seed, 1) == 0
         return self.torch.from_numpy(ho.view("keep", np.uint8)[:max(n, 1)].copy())

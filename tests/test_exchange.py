@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from odigos_amd import native
-from tests.exchange_emul import CpuOps, HostCols, owners, pack, synthetic_global_batch, unpack, endpoint_bits
+from tests.exchange_emul import CpuOps, HostCols, endpoint_bits, owners, pack, rec_bytes, synthetic_global_batch, unpack
 from tests.workloads import c3_sampling_config
 
 CFG = c3_sampling_config()
@@ -41,9 +41,10 @@ def test_owner_hash_matches_abi():
 
 def test_pack_unpack_roundtrip():
     tid, start, end, status, svc, svc_str, ep = synthetic_global_batch(1, 2000, 5)
-    rec, counts, pos = pack(tid, start, end, status, svc, svc_str, ep, 4)
+    rec, counts, pos = pack(tid, start, end, status, svc, svc_str, ep, 4, cfg=CFG)
     assert counts.sum() == 2000
-    hc = unpack(rec.view(np.uint8))
+    assert rec.itemsize == rec_bytes(CFG) == 48
+    hc = unpack(rec.view(np.uint8), CFG)
     a = hc.a
     np.testing.assert_array_equal(a["start_ns"][pos], start)
     np.testing.assert_array_equal(a["trace_id"].reshape(-1, 2)[pos], tid)
@@ -106,17 +107,22 @@ def test_straddling_traces_exist():
 
 # ---------------- GPU ----------------
 
-@pytest.mark.gpu
-def test_gpu_shard_kernels_vs_emulation():
+def _shard_vs_emulation(cfg, with_attr):
     import ctypes as C
     import torch
     from odigos_amd.batch import DeviceBatch, Engine, Generator
     g = Generator("sampling", seed=0x0D160053, n_spans=120_000)
-    eng = Engine({"odigossampling": CFG})
-    db = DeviceBatch(g.cols)
     n = g.cols.n_spans
+    attr = None
+    if with_attr:
+        attr = np.random.default_rng(7).integers(0, 2**62, size=n, dtype=np.int64).astype(np.uint64)
+        g.cols.attr_match = attr.ctypes.data
+    eng = Engine({"odigossampling": cfg})
+    db = DeviceBatch(g.cols)
     world = 3
-    send = torch.empty(n * native.XREC_BYTES, dtype=torch.uint8, device="cuda")
+    rb = native.lib().ose_shard_record_bytes(eng.h)
+    assert rb == rec_bytes(cfg) == (56 if with_attr else 48)
+    send = torch.empty(n * rb, dtype=torch.uint8, device="cuda")
     counts = torch.zeros(world, dtype=torch.int64, device="cuda")
     pos = torch.empty(n, dtype=torch.int32, device="cuda")
     L = native.lib()
@@ -128,10 +134,10 @@ def test_gpu_shard_kernels_vs_emulation():
     rstr = g.array("res_svc_str").view(np.uint32)
     route = g.array("route").view(np.uint32).reshape(-1, 2)[:n]
     arena = g.array("arena")
-    rb = [bytes(arena[o:o + ln]) for o, ln in route]
-    ep = endpoint_bits(CFG, rsvc[res], rb)
+    rb_ = [bytes(arena[o:o + ln]) for o, ln in route]
+    ep = endpoint_bits(cfg, rsvc[res], rb_)
     rec, cnt, p = pack(tid, g.array("start_ns").view(np.uint64)[:n], g.array("end_ns").view(np.uint64)[:n],
-                       g.array("status")[:n], rsvc[res], rstr[res], ep, world)
+                       g.array("status")[:n], rsvc[res], rstr[res], ep, world, attr, cfg=cfg)
     np.testing.assert_array_equal(counts.cpu().numpy(), cnt)
     np.testing.assert_array_equal(pos.cpu().numpy(), p)
     np.testing.assert_array_equal(send.cpu().numpy(), rec.view(np.uint8))
@@ -139,13 +145,29 @@ def test_gpu_shard_kernels_vs_emulation():
     cols = {k: torch.empty(n * w, dtype=torch.uint8, device="cuda") for k, w in
             (("trace_id", 16), ("start_ns", 8), ("end_ns", 8), ("status", 1), ("resource", 4), ("res_svc", 4),
              ("res_svc_str", 4), ("route_match", 8), ("attr_match", 8))}
-    native.check(L.ose_shard_unpack(send.data_ptr(), n, *[cols[k].data_ptr() for k in
+    native.check(L.ose_shard_unpack(send.data_ptr(), n, rb, *[cols[k].data_ptr() for k in
                                     ("trace_id", "start_ns", "end_ns", "status", "resource", "res_svc", "res_svc_str",
                                      "route_match", "attr_match")], None))
     torch.cuda.synchronize()
-    hc = unpack(rec.view(np.uint8))
+    hc = unpack(rec.view(np.uint8), cfg)
     for k in cols:
         np.testing.assert_array_equal(cols[k].cpu().numpy(), hc.a[k].view(np.uint8)[: cols[k].numel()])
+
+
+@pytest.mark.gpu
+def test_gpu_shard_kernels_vs_emulation():
+    _shard_vs_emulation(CFG, False)
+
+
+@pytest.mark.gpu
+def test_gpu_shard_kernels_with_attr_bits():
+    # span_attribute rules: 56-byte records carry the attr_match bits
+    cfg = dict(CFG)
+    cfg["global_rules"] = list(CFG.get("global_rules") or []) + [
+        {"name": "attr", "type": "span_attribute",
+         "rule_details": {"service_name": "svc-attr", "attribute_key": "env", "condition_type": "string",
+                          "operation": "equals", "expected_value": "prod", "sampling_ratio": 50.0}}]
+    _shard_vs_emulation(cfg, True)
 
 
 @pytest.mark.gpu
