@@ -69,6 +69,37 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return __builtin_am
 __device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
   return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
 }
+// ---- DPP segmented scans ------------------------------------------------------
+// Inclusive scans over the wave in lane order with (head, value) elements:
+// earlier ⊕ later = (h_e | h_l, h_l ? v_l : v_e ∘ v_l).  row_shr 1/2/4/8 scan
+// each 16-lane row, row_bcast:15 and :31 carry the row totals (the pattern of
+// wave_incl_sum_u32); a source lane outside the row yields the identity.
+// Register-only: no ds_bpermute round trip per step.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t x) {
+  return (uint64_t)dpp_mov<CTRL, ROWS>((uint32_t)old, (uint32_t)x) |
+         ((uint64_t)dpp_mov<CTRL, ROWS>((uint32_t)(old >> 32), (uint32_t)(x >> 32)) << 32);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_or_step(uint32_t& h, uint32_t& err, uint64_t& ep, uint64_t& sv) {
+  const uint32_t oh = dpp_mov<CTRL, ROWS>(0u, h), oe = dpp_mov<CTRL, ROWS>(0u, err);
+  const uint64_t oep = dpp64<CTRL, ROWS>(0ull, ep), osv = dpp64<CTRL, ROWS>(0ull, sv);
+  if (!h) {
+    err |= oe;
+    ep |= oep;
+    sv |= osv;
+  }
+  h |= oh;
+}
+__device__ __forceinline__ void seg_or_scan(uint32_t h, uint32_t& err, uint64_t& ep, uint64_t& sv) {
+  seg_or_step<0x111, 0xF>(h, err, ep, sv);
+  seg_or_step<0x112, 0xF>(h, err, ep, sv);
+  seg_or_step<0x114, 0xF>(h, err, ep, sv);
+  seg_or_step<0x118, 0xF>(h, err, ep, sv);
+  seg_or_step<0x142, 0xA>(h, err, ep, sv);
+  seg_or_step<0x143, 0xC>(h, err, ep, sv);
+}
+
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, kWave);
@@ -106,6 +137,25 @@ __device__ __forceinline__ Lat lat_comb(const Lat& a, const Lat& b) {   // a ear
   r.m = (b.f & 1u) ? b.m : (a.m < b.m ? a.m : b.m);
   r.e = a.e > b.e ? a.e : b.e;
   return r;
+}
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_lat_step(uint32_t& h, Lat& v) {
+  const uint32_t oh = dpp_mov<CTRL, ROWS>(0u, h);
+  Lat o;
+  o.f = dpp_mov<CTRL, ROWS>(0u, v.f);
+  o.m = dpp64<CTRL, ROWS>(kInf, v.m);
+  o.e = dpp64<CTRL, ROWS>(0ull, v.e);
+  if (!h) v = lat_comb(o, v);
+  h |= oh;
+}
+__device__ __forceinline__ void seg_lat_scan(uint32_t h, Lat& v) {
+  seg_lat_step<0x111, 0xF>(h, v);
+  seg_lat_step<0x112, 0xF>(h, v);
+  seg_lat_step<0x114, 0xF>(h, v);
+  seg_lat_step<0x118, 0xF>(h, v);
+  seg_lat_step<0x142, 0xA>(h, v);
+  seg_lat_step<0x143, 0xC>(h, v);
 }
 
 // strings.HasPrefix(route, rule.HttpRoute) (latency.go:97-100)
@@ -353,11 +403,8 @@ __device__ __forceinline__ bool step_head(const TraceKernelArgs& a, const StepRa
     if (lane == 0) pk = r.pk;
     return valid && (p == 0 || pk != r.k);
   }
-  uint64_t ph = __shfl_up(r.hi, 1, kWave), pl = __shfl_up(r.lo, 1, kWave);
-  if (lane == 0) {
-    ph = r.ph;
-    pl = r.pl;
-  }
+  // wave_shr:1 (DPP): lane l gets lane l-1's trace id, lane 0 its own prefetched p-1 id
+  const uint64_t ph = dpp64<0x138, 0xF>(r.ph, r.hi), pl = dpp64<0x138, 0xF>(r.pl, r.lo);
   if (a.mode == kTraceBatch) return valid && p == 0;
   return valid && (p == 0 || ph != r.hi || pl != r.lo);
 }
@@ -615,17 +662,9 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         }
       }
     }
-    // ---- segmented OR of the flag masks ----
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t oe = __shfl_up(err, d, kWave);
-      const uint64_t oep = __shfl_up(ep, d, kWave), osv = __shfl_up(svcb, d, kWave);
-      if (lane >= d && lane - d >= sst) {
-        err |= oe;
-        ep |= oep;
-        svcb |= osv;
-      }
-    }
+    // ---- segmented OR of the flag masks (DPP scan; h = segment head) ----
+    const uint32_t hseg = mine ? (uint32_t)((segmask >> lane) & 1) : 1u;
+    seg_or_scan(hseg, err, ep, svcb);
     // ---- latency state, one segmented scan per latency slot present ----
     uint64_t lsat = 0, n_kmask = 0;
     Lat nxt{0, kInf, 0};
@@ -636,14 +675,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
       const bool ink = slot == ks;
       pend &= ~__ballot(ink);
       Lat v = ink ? Lat{st == 0 ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
-#pragma unroll
-      for (int d = 1; d < kWave; d <<= 1) {
-        Lat o;
-        o.f = __shfl_up(v.f, d, kWave);
-        o.m = __shfl_up(v.m, d, kWave);
-        o.e = __shfl_up(v.e, d, kWave);
-        if (lane >= d && lane - d >= sst) v = lat_comb(o, v);
-      }
+      seg_lat_scan(hseg, v);
       if (tail && !carried_tail && (v.f & 2u)) lsat |= latency_satisfied(c, ks, ep, v.m, v.e);
       if (seg0_cont) {
         const uint32_t f0 = rdl(v.f, t0);
