@@ -113,7 +113,9 @@ struct TraceKernelArgs {
   uint32_t* n_long;
   uint32_t* long_runs;        // [n_spans / 64 + 1]
   uint32_t long_steps;        // hand-off distance in 64-span steps (kLongSteps)
+  uint32_t win_per_wave;      // 64-span windows whose run heads one wave owns (kWinPerWave)
 };
+constexpr uint32_t kWinPerWave = 16;   // tools/gpu_wpw.sh: C5 0.97 -> 0.83 ms, C3 2.03 -> 1.99 ms, C4 unchanged
 constexpr uint32_t kLongSteps = 4;   // tools/gpu_long_iter.sh: C5 16 -> 4 steps 2.75 -> 2.13 ms, C3 unchanged
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st);

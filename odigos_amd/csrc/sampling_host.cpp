@@ -310,6 +310,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.n_long = misc + 12;
   a.long_runs = a.mode == kTraceRuns ? long_runs : nullptr;
   a.long_steps = kLongSteps;
+  a.win_per_wave = kWinPerWave;
+  if (const char* ww = getenv("OSE_WIN_PER_WAVE")) a.win_per_wave = std::max<uint32_t>(1, (uint32_t)strtoul(ww, nullptr, 0));   // tuning
   if (const char* ls = getenv("OSE_LONG_STEPS")) a.long_steps = std::max<uint32_t>(1, (uint32_t)strtoul(ls, nullptr, 0));   // tuning
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);

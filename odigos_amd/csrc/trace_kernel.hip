@@ -510,7 +510,7 @@ __device__ void flush_queue(const TraceKernelArgs& a, const Cfg& c, DecideQ& Q, 
   qn = 0;
 }
 
-constexpr int kWinPerWave = 8;   // 64-span windows whose run heads one wave owns
+
 
 __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void trace_eval_kernel(TraceKernelArgs a) {
   if (a.mode == kTracePerm && __hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
@@ -529,7 +529,8 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
       *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
     __syncthreads();
   }
-  const uint64_t w0 = ((uint64_t)blockIdx.x * kTWaves + wv) * kWinPerWave;   // first owned window
+  const uint64_t wpw = a.win_per_wave;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * kTWaves + wv) * wpw;   // first owned window
   if (w0 >= a.n_windows) return;
   const Cfg c = load_cfg(cfg_lds);
   const uint64_t n = a.n_spans;
@@ -560,7 +561,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     return;
   }
 
-  const uint64_t range_end = min((w0 + kWinPerWave) * kWave, n);
+  const uint64_t range_end = min((w0 + wpw) * kWave, n);
   uint32_t qn = 0, hn = 0;
   bool started = false, open = false;
   uint32_t c_err = 0;
@@ -1257,7 +1258,7 @@ void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, u
 }
 
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
-  const uint32_t per_block = kTWaves * kWinPerWave;
+  const uint32_t per_block = kTWaves * a.win_per_wave;
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
   hipLaunchKernelGGL(trace_eval_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
 }
