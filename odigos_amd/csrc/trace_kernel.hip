@@ -504,8 +504,16 @@ __device__ void flush_queue(const TraceKernelArgs& a, const Cfg& c, DecideQ& Q, 
              dl, dr);
     write_rec(a, pos, dk, dl, dr);
   }
-  for (uint32_t e = 0; e < qn; e++)
-    write_keep_range(a, rdl(pos, e), rdl(len, e), (uint8_t)rdl(dk, e), lane);
+  const uint32_t mlen = wave_max_u32((uint32_t)lane < qn ? len : 0u);
+  if (a.mode != kTracePerm && mlen <= 32) {
+    // short traces: each lane writes its own trace's keep bytes (at most 32
+    // store instructions per 64 traces instead of one per trace)
+    if ((uint32_t)lane < qn)
+      for (uint32_t q = 0; q < len; q++) a.keep[pos + q] = dk;
+  } else {
+    for (uint32_t e = 0; e < qn; e++)
+      write_keep_range(a, rdl(pos, e), rdl(len, e), (uint8_t)rdl(dk, e), lane);
+  }
   __builtin_amdgcn_wave_barrier();
   qn = 0;
 }
