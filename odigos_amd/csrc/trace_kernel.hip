@@ -354,7 +354,7 @@ __device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint6
 struct StepRaw {
   uint64_t i;          // span index (perm[p] in kTracePerm)
   uint64_t hi, lo;     // trace id
-  uint64_t ph, pl;     // lane 0: trace id of position p-1 (head test)
+  uint64_t ph, pl;     // lane 0: trace id of position p-1 (head test); lane 63: of p+1 (kTraceRuns)
   uint32_t k, pk;      // kTracePerm: canonical key of p and (lane 0) of p-1
   uint32_t res;
   uint32_t status;
@@ -379,6 +379,10 @@ __device__ __forceinline__ StepRaw load_raw(const TraceKernelArgs& a, uint64_t b
     if (lane == 0 && p > 0 && a.mode == kTraceRuns) {
       r.ph = a.tid[2 * p - 2];
       r.pl = a.tid[2 * p - 1];
+    }
+    if (lane == kWave - 1 && p + 1 < a.n_spans && a.mode == kTraceRuns) {   // the span after the step
+      r.ph = a.tid[2 * p + 2];
+      r.pl = a.tid[2 * p + 3];
     }
   }
   const uint4 v = reinterpret_cast<const uint4*>(a.tid)[r.i];
@@ -639,7 +643,8 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     bool cont_next = false;
     if (last_own == 63 && base + kWave < n) {
       bool h = false;
-      if (lane == 63) h = head_at(a, base + kWave);
+      // kTraceRuns: lane 63 loaded the next step's first trace id with this step
+      if (lane == 63) h = a.mode == kTraceRuns ? (r.ph != r.hi || r.pl != r.lo) : head_at(a, base + kWave);
       cont_next = !rdl((uint32_t)h, 63);
     }
     const bool mine = (own >> lane) & 1;
