@@ -43,6 +43,13 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
   x = min(x, dpp_mov<0x118>(x, x));
   return min(min(lane_value(x, 15), lane_value(x, 31)), min(lane_value(x, 47), lane_value(x, 63)));
 }
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t x) {
+  x |= dpp_mov<0x111>(0u, x);
+  x |= dpp_mov<0x112>(0u, x);
+  x |= dpp_mov<0x114>(0u, x);
+  x |= dpp_mov<0x118>(0u, x);
+  return lane_value(x, 15) | lane_value(x, 31) | lane_value(x, 47) | lane_value(x, 63);
+}
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
   x = max(x, dpp_mov<0x111>(x, x));
   x = max(x, dpp_mov<0x112>(x, x));

@@ -458,10 +458,8 @@ typedef const __attribute__((address_space(3))) u32x4 lds_cu4;
 // SWAR high-bit mask (bits 7,15,23,31) -> 4-bit mask
 __device__ __forceinline__ uint32_t movemask4(uint32_t m) { return (((m >> 7) * 0x204081u) >> 21) & 0xFu; }
 
-__device__ __forceinline__ void build_bitmaps(lds_u32* stage32, lds_u4* bm, uint32_t bytes) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t rows = (bytes + 31) / 32;
-  for (uint32_t r = lane; r < rows; r += kWave) {
+__device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t r) {
+  {
     uint32_t acc[kClasses];
 #pragma unroll
     for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
@@ -507,6 +505,43 @@ __device__ __forceinline__ void build_bitmaps(lds_u32* stage32, lds_u4* bm, uint
     bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
     bm[kRowVec * r + 2] = u32x4{acc[8], acc[9], acc[10], acc[11]};
   }
+}
+__device__ __forceinline__ void build_bitmaps(lds_u32* stage32, lds_u4* bm, uint32_t bytes) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t rows = (bytes + 31) / 32;
+  for (uint32_t r = lane; r < rows; r += kWave) build_row(stage32, bm, r);
+}
+// position of the k-th set bit of m (k < popcount(m))
+__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t k) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 16; w; w >>= 1) {
+    const uint32_t c = __builtin_popcount(m & ((1u << w) - 1u));
+    if (k >= c) {
+      k -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
+// Only the rows (bit r of the 96-bit mask {m0, m1, m2}) that hold path bytes:
+// every reader of the bitmaps masks its windows to a path's own bytes, so the
+// rows between paths (other strings of the arena) are never looked at.
+__device__ __forceinline__ void build_bitmaps_rows(lds_u32* stage32, lds_u4* bm, uint32_t m0, uint32_t m1,
+                                                   uint32_t m2) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t c0 = __builtin_popcount(m0), c1 = __builtin_popcount(m1), total = c0 + c1 + __builtin_popcount(m2);
+  for (uint32_t k = lane; k < total; k += kWave) {
+    const uint32_t r = k < c0 ? select_bit(m0, k) : k < c0 + c1 ? 32 + select_bit(m1, k - c0) : 64 + select_bit(m2, k - c0 - c1);
+    build_row(stage32, bm, r);
+  }
+}
+// bits [lo, hi] (rows) of the 32-row word starting at row w0
+__device__ __forceinline__ uint32_t row_bits(uint32_t lo, uint32_t hi, uint32_t w0) {
+  if (hi < w0 || lo > w0 + 31) return 0u;
+  const uint32_t l = lo > w0 ? lo - w0 : 0u, h = min(hi - w0, 31u);
+  return (h == 31 ? ~0u : ((2u << h) - 1u)) & ~((1u << l) - 1u);
 }
 
 // 64-bit windows of classes [c0, c0+4*nv) starting at stage byte a
@@ -1125,7 +1160,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     const bool needs_path = gate == 2;
     const uint32_t lo16 = pf.lo16;
     if (lo16 != ~0u && pf.bytes && !(a.ablate & 4)) {
-      build_bitmaps(stage32, (lds_u4*)sm.bm[wv], pf.bytes);
+      // rows holding path bytes; when other strings of the arena fill a good
+      // part of the staged range (C4), only those rows get bitmaps
+      uint32_t m0 = 0, m1 = 0, m2 = 0;
+      if (needs_path && cur.pr.len) {
+        const uint32_t rl = (cur.pr.off - lo16) >> 5, rh = (cur.pr.off - lo16 + cur.pr.len - 1) >> 5;
+        m0 = row_bits(rl, rh, 0);
+        m1 = row_bits(rl, rh, 32);
+        m2 = row_bits(rl, rh, 64);
+      }
+      m0 = wave_or_u32(m0);
+      m1 = wave_or_u32(m1);
+      m2 = wave_or_u32(m2);
+      const uint32_t need = __builtin_popcount(m0) + __builtin_popcount(m1) + __builtin_popcount(m2);
+      const uint32_t rows = (pf.bytes + 31) / 32;
+      if ((need + kWave - 1) / kWave < (rows + kWave - 1) / kWave)
+        build_bitmaps_rows(stage32, (lds_u4*)sm.bm[wv], m0, m1, m2);
+      else
+        build_bitmaps(stage32, (lds_u4*)sm.bm[wv], pf.bytes);
       wave_lds_sync();
     }
     if (tm) { const uint64_t t1 = clk(); t_bm += t1 - t0; t0 = t1; }
