@@ -24,6 +24,11 @@ template <int CTRL, int ROWS = 0xF>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t old, uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROWS, 0xF, false);
 }
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint64_t dpp_mov64(uint64_t old, uint64_t x) {
+  return (uint64_t)dpp_mov<CTRL, ROWS>((uint32_t)old, (uint32_t)x) |
+         ((uint64_t)dpp_mov<CTRL, ROWS>((uint32_t)(old >> 32), (uint32_t)(x >> 32)) << 32);
+}
 // inclusive prefix sum over the wave's lanes
 __device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
   x += dpp_mov<0x111>(0, x);   // row_shr:1

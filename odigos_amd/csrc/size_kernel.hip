@@ -39,28 +39,38 @@ __device__ __forceinline__ bool batch_dropped(const SizeKernelArgs& a) {
 
 // Segmented (by non-decreasing key) inclusive sums over one wave; returns
 // true on the lane that ends its key's run inside the wave.
+// One DPP step of the segmented sum: (h, v, c) elements, earlier ⊕ later =
+// (h_e | h_l, h_l ? (v_l, c_l) : (v_e + v_l, c_e + c_l)); a source lane
+// outside the row yields the identity (0, 0, 0).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_sum_step(uint32_t& h, uint64_t& v, uint32_t& c) {
+  const uint32_t oh = dpp_mov<CTRL, ROWS>(0u, h), oc = dpp_mov<CTRL, ROWS>(0u, c);
+  const uint64_t ov = dpp_mov64<CTRL, ROWS>(0ull, v);
+  if (!h) {
+    v += ov;
+    c += oc;
+  }
+  h |= oh;
+}
 template <typename T>
 __device__ __forceinline__ bool wave_seg_sum(uint32_t key, bool valid, T& v, uint32_t& c) {
   const int lane = threadIdx.x & 63;
   const uint64_t vmask = __ballot(valid);
-  // cross-lane reads are taken by every lane (a shuffle from a lane that is
-  // not executing it is undefined), then used under conditions
-  const uint32_t nk = __shfl_down(key, 1, kWave);
-  const uint32_t pk = __shfl_up(key, 1, kWave);
+  // neighbours' keys by DPP wave_shl:1 / wave_shr:1 (every lane takes them)
+  const uint32_t nk = dpp_mov<0x130>(key, key);
+  const uint32_t pk = dpp_mov<0x138>(key, key);
   const bool last = valid && (lane == 63 || !((vmask >> (lane + 1)) & 1) || nk != key);
-  const uint64_t starts = __ballot(valid && (lane == 0 || pk != key));
-  // lanes whose key differs from lane-1's start a run; pull only from the same run
-  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-  const int sst = valid ? 63 - __clzll((long long)(starts & le)) : lane;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const T ov = __shfl_up(v, d, kWave);
-    const uint32_t oc = __shfl_up(c, d, kWave);
-    if (lane >= d && lane - d >= sst) {
-      v += ov;
-      c += oc;
-    }
-  }
+  // lanes whose key differs from lane-1's start a run; invalid lanes are runs of their own
+  const uint32_t h = valid ? ((lane == 0 || pk != key) ? 1u : 0u) : 1u;
+  uint64_t w = v;
+  uint32_t hh = h;
+  seg_sum_step<0x111, 0xF>(hh, w, c);
+  seg_sum_step<0x112, 0xF>(hh, w, c);
+  seg_sum_step<0x114, 0xF>(hh, w, c);
+  seg_sum_step<0x118, 0xF>(hh, w, c);
+  seg_sum_step<0x142, 0xA>(hh, w, c);
+  seg_sum_step<0x143, 0xC>(hh, w, c);
+  v = (T)w;
   return last;
 }
 
