@@ -948,7 +948,7 @@ __device__ __forceinline__ uint64_t half_mask(uint32_t lo, uint32_t hi, uint32_t
 // segment index of the longest path); each lane then folds its own entries.
 // Entries: start 12 | len 13 before classification, then out_len << 8 | (id + 1)
 // where out_len is what the segment adds to the template ({name} or itself).
-// A path whose bytes lie in 4 bitmap rows (the common case) finds its '?' cut,
+// A path whose bytes lie in 6 bitmap rows (the common case) finds its '?' cut,
 // leading '/' and segment ends in one read of those rows' slash and '?' words
 // and folds its entries (<= 8) in one read; longer paths walk the rows.
 // Returns false (nothing written) when the list would overflow.
@@ -960,28 +960,33 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   LdsReader rd(stage32, p0);
   const lds_u32* b32 = (const lds_u32*)bm;
   uint32_t n = 0, nseg = 0;
-  // window: stage bytes [32 r0, 32 r0 + 128), the path at window bit b0
+  // window: stage bytes [32 r0, 32 r0 + 192) (6 bitmap rows, p99 of a C2
+  // path is 129 bytes), the path at window bit b0 < 32
   const uint32_t r0 = p0 >> 5, b0 = p0 & 31;
-  const bool win = needs_path && b0 + plen <= 128;
-  uint64_t sl0 = 0, sl1 = 0;
+  const bool win = needs_path && b0 + plen <= 192;
+  uint64_t sl0 = 0, sl1 = 0, sl2 = 0;
   if (needs_path) {
     if (win) {
-      uint32_t w[8];
+      uint32_t w[12];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        w[j] = b32[4 * kRowVec * (r0 + j) + C_SL];
-        w[4 + j] = b32[4 * kRowVec * (r0 + j) + C_QM];
+      for (int j = 0; j < 6; j++) {
+        const uint32_t r = min(r0 + j, kPlanBmRows - 1);   // rows past the path are masked off below
+        w[j] = b32[4 * kRowVec * r + C_SL];
+        w[6 + j] = b32[4 * kRowVec * r + C_QM];
       }
       sl0 = w[0] | ((uint64_t)w[1] << 32);
       sl1 = w[2] | ((uint64_t)w[3] << 32);
+      sl2 = w[4] | ((uint64_t)w[5] << 32);
       n = plen;
       if ((f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET) {   // strings.SplitN(target, "?", 2)[0]
-        const uint64_t q0 = (w[4] | ((uint64_t)w[5] << 32)) & half_mask(b0, b0 + plen, 0);
-        const uint64_t q1 = (w[6] | ((uint64_t)w[7] << 32)) & half_mask(b0, b0 + plen, 64);
+        const uint64_t q0 = (w[6] | ((uint64_t)w[7] << 32)) & half_mask(b0, b0 + plen, 0);
+        const uint64_t q1 = (w[8] | ((uint64_t)w[9] << 32)) & half_mask(b0, b0 + plen, 64);
+        const uint64_t q2 = (w[10] | ((uint64_t)w[11] << 32)) & half_mask(b0, b0 + plen, 128);
         if (q0) n = (uint32_t)__builtin_ctzll(q0) - b0;
         else if (q1) n = 64 + (uint32_t)__builtin_ctzll(q1) - b0;
+        else if (q2) n = 128 + (uint32_t)__builtin_ctzll(q2) - b0;
       }
-      p.lead = (n > 0 && ((b0 < 64 ? sl0 >> b0 : sl1 >> (b0 - 64)) & 1)) ? 1 : 0;
+      p.lead = (n > 0 && ((sl0 >> b0) & 1)) ? 1 : 0;
     } else {
       n = (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? first_of(bm, C_QM, p0, p0 + plen) - p0 : plen;
       p.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
@@ -993,7 +998,8 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       if (win) {
         sl0 &= half_mask(b0 + p.lead, b0 + n, 0);
         sl1 &= half_mask(b0 + p.lead, b0 + n, 64);
-        nseg = 1 + __builtin_popcountll(sl0) + __builtin_popcountll(sl1);
+        sl2 &= half_mask(b0 + p.lead, b0 + n, 128);
+        nseg = 1 + __builtin_popcountll(sl0) + __builtin_popcountll(sl1) + __builtin_popcountll(sl2);
       } else {
         nseg = 1 + count_of(bm, C_SL, p0 + p.lead, p0 + n);
       }
@@ -1029,6 +1035,11 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       }
       for (uint64_t m = sl1; m; m &= m - 1) {
         const uint32_t e = wb + 64 + (uint32_t)__builtin_ctzll(m);
+        segs[off + k++] = s | ((e - s) << 12);
+        s = e + 1;
+      }
+      for (uint64_t m = sl2; m; m &= m - 1) {
+        const uint32_t e = wb + 128 + (uint32_t)__builtin_ctzll(m);
         segs[off + k++] = s | ((e - s) << 12);
         s = e + 1;
       }
