@@ -1570,15 +1570,45 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
         if (mode == M_DEFAULT) {
           const uint32_t p0 = pr.off - lo16, n = field;
           uint32_t cs = 0, s = lead;
-          for (uint64_t c = (a.ablate & 8192) ? 0 : cur.code; c; c >>= 4) {
-            const uint32_t e = next_slash(sl, p0 + s, p0 + n) - p0;
-            const uint32_t nib = (uint32_t)(c & 15u);
-            if (nib) {
-              pw.put(stage_src + p0 + cs, s - cs);
-              pw.put(bn_src + sm.bn.off[nib - 1], sm.bn.len[nib - 1]);
-              cs = e;
+          const uint32_t b0 = p0 & 31, r0 = p0 >> 5;
+          if (b0 + n <= 192) {
+            // the path's '/' bits from one read of 6 slash-bitmap rows (window
+            // bit 0 = stage byte 32 r0), kept to [lead, n) of the path
+            uint32_t w[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) w[j] = sl[min(r0 + j, kSlashWords - 1)];
+            uint64_t h[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+              h[j] = (w[2 * j] | ((uint64_t)w[2 * j + 1] << 32)) & half_mask(b0 + lead, b0 + n, 64 * j);
+            for (uint64_t c = (a.ablate & 8192) ? 0 : cur.code; c; c >>= 4) {
+              // first '/' at path offset >= s, else n
+              const uint32_t q = b0 + s;
+              uint32_t e = n;
+#pragma unroll
+              for (int j = 2; j >= 0; j--) {
+                const uint64_t m = h[j] & ~(q > 64u * j ? low_mask(q - 64u * j) : 0ull);
+                if (m) e = 64u * j + (uint32_t)__builtin_ctzll(m) - b0;
+              }
+              const uint32_t nib = (uint32_t)(c & 15u);
+              if (nib) {
+                pw.put(stage_src + p0 + cs, s - cs);
+                pw.put(bn_src + sm.bn.off[nib - 1], sm.bn.len[nib - 1]);
+                cs = e;
+              }
+              s = e + 1;
             }
-            s = e + 1;
+          } else {
+            for (uint64_t c = (a.ablate & 8192) ? 0 : cur.code; c; c >>= 4) {
+              const uint32_t e = next_slash(sl, p0 + s, p0 + n) - p0;
+              const uint32_t nib = (uint32_t)(c & 15u);
+              if (nib) {
+                pw.put(stage_src + p0 + cs, s - cs);
+                pw.put(bn_src + sm.bn.off[nib - 1], sm.bn.len[nib - 1]);
+                cs = e;
+              }
+              s = e + 1;
+            }
           }
           pw.put(stage_src + p0 + cs, n - cs);
         } else if (mode == M_ORIG) {
