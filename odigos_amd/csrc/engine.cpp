@@ -195,6 +195,8 @@ Engine::~Engine() {
     if (w->table) (void)hipFree(w->table);
     if (w->fp_table) (void)hipFree(w->fp_table);
     if (w->pending) (void)hipEventDestroy(w->pending);
+    if (w->dup_host) (void)hipHostFree(w->dup_host);
+    if (w->dup_ready) (void)hipEventDestroy(w->dup_ready);
     delete w;
   }
 }
@@ -299,7 +301,9 @@ int upload(const std::vector<uint8_t>& host, uint8_t** dev) {
 // Workspace layout for one call (byte offsets), see run_stages.
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws) {
+// ws_off: the URL scratch starts this many bytes into the workspace (past a
+// SAMPLE stage's scratch whose slow path is still to be queued)
+int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws, size_t ws_off = 0) {
   if (!e->has_url) return fail(OSE_EINVAL, "odigosurltemplate is not configured on this engine");
   if (!c->url_flags || !c->kind || !c->path || !c->arena || !o->url_out || !o->tmpl || !o->tmpl_arena)
     return fail(OSE_EINVAL, "TEMPLATE stage needs url_flags, kind, path, arena, url_out, tmpl, tmpl_arena");
@@ -320,9 +324,9 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   const size_t off_dbg = align_up(off_slow + 4 * (size_t)groups, 256);
   const size_t need = off_dbg + 256;
   if (need > url_workspace_bytes(n)) return fail(OSE_EINVAL, "internal: URL workspace layout exceeds its bound");
-  int rc = ws->reserve(need);
+  int rc = ws->reserve(ws_off + need);
   if (rc) return rc;
-  uint8_t* base = static_cast<uint8_t*>(ws->dev);
+  uint8_t* base = static_cast<uint8_t*>(ws->dev) + ws_off;
   UrlKernelArgs a{};
   a.n_spans = n;
   a.n_groups = groups;
@@ -405,10 +409,24 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   if (mask & OSE_STAGE_TEMPLATE) need = std::max(need, url_workspace_bytes(c->n_spans));
   if (mask & OSE_STAGE_SAMPLE) need = std::max(need, e->workspace_bytes(c->n_spans));
   if (mask & OSE_STAGE_SIZE) need = std::max(need, size_scratch_bytes(c->n_scopes, c->n_resources));
+  // SAMPLE + TEMPLATE by trace id: the URL stage reads nothing SAMPLE writes,
+  // so its launches are queued between SAMPLE's fast path and the rest of
+  // SAMPLE, which is queued once the host has read the fast path's dup flag
+  // (by then the GPU is busy with the URL kernels, and the ~12 gated
+  // slow-path launches are skipped when no trace id repeats)
+  const bool defer = (mask & OSE_STAGE_SAMPLE) && (mask & OSE_STAGE_TEMPLATE) &&
+                     group_mode == OSE_GROUP_TRACE_ID && c->n_spans > 0 && !getenv("OSE_NO_DEFER_SLOW");
+  const size_t url_off = defer ? (sampling_scratch_bytes(c->n_spans) + 255) / 256 * 256 : 0;
+  if (defer) need = std::max(need, url_off + url_workspace_bytes(c->n_spans));
   int rc = ws->reserve(need);
+  std::function<int()> sample_tail;
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
-  if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws);
-  if (!rc && (mask & OSE_STAGE_TEMPLATE)) rc = run_url(e, c, o, st, ws);
+  if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws, defer ? &sample_tail : nullptr);
+  if (!rc && (mask & OSE_STAGE_TEMPLATE)) rc = run_url(e, c, o, st, ws, url_off);
+  if (sample_tail) {
+    const int trc = sample_tail();   // always drained: the host event wait must not be skipped
+    if (!rc) rc = trc;
+  }
   // odigostrafficmetrics runs last, on what the earlier stages left
   if (!rc && (mask & OSE_STAGE_SIZE)) rc = run_size(e, c, o, mask, group_mode, rnd, st, ws);
   e->release_ws(ws, st);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -33,6 +34,11 @@ struct Workspace {
   uint64_t fp_slots_cap = 0;
   uint32_t epoch = 0;
   int reserve_table(uint64_t n_spans);
+  // SAMPLE + TEMPLATE in one call: the fast path's dup flag is copied here and
+  // read by the host after the URL launches are queued (run_stages), so the
+  // slow-path launches are only queued when a trace id repeats
+  uint32_t* dup_host = nullptr;   // pinned
+  hipEvent_t dup_ready = nullptr;
 };
 
 struct Engine {
@@ -73,8 +79,13 @@ struct Engine {
   size_t workspace_bytes(uint64_t n_spans) const;
 };
 
+// tail != nullptr (OSE_GROUP_TRACE_ID only): queue the fast path, then hand
+// back in *tail the rest of the stage (slow path if the fast path saw a
+// repeated trace id, per-trace compaction); the caller queues other work on
+// the stream first and calls *tail before anything that reads keep
 int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
-                 hipStream_t st, Workspace* ws);
+                 hipStream_t st, Workspace* ws, std::function<int()>* tail = nullptr);
+size_t sampling_scratch_bytes(uint64_t n_spans);
 int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
              const ose_rand* rnd, hipStream_t st, Workspace* ws);
 size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources);

@@ -159,7 +159,7 @@ int Engine::build_sampling_tables() {
 }
 
 // Scratch of the trace stage for n spans (run_sampling layout).
-static size_t sampling_scratch_bytes(uint64_t n) {
+size_t sampling_scratch_bytes(uint64_t n) {
   const uint64_t W = windows_of(n);
   const uint64_t N = std::max<uint64_t>(n, 1);
   const uint64_t T = (N + kSortTile - 1) / kSortTile;
@@ -208,7 +208,7 @@ int Workspace::reserve_table(uint64_t n_spans) {
 }
 
 int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
-                 hipStream_t st, Workspace* ws) {
+                 hipStream_t st, Workspace* ws, std::function<int()>* tail) {
   if (!e->has_sampling) return fail(OSE_EINVAL, "odigossampling is not configured on this engine");
   if (group_mode != OSE_GROUP_TRACE_ID && group_mode != OSE_GROUP_BATCH) return fail(OSE_EINVAL, "unknown group_mode");
   const uint64_t n = c->n_spans;
@@ -325,7 +325,10 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     e->prof_end(tm, st);
   }
 
-  if (group_mode == OSE_GROUP_TRACE_ID) {
+  // the rest of the stage; run_slow = false skips the slow-path launches
+  // (they would all return at once: the fast path left *dup clear)
+  auto rest = [=](bool run_slow) -> int {
+  if (run_slow) {
     // slow path: every launch returns at once unless the fast path set *dup
     TraceSortArgs s{};
     s.n_spans = n;
@@ -414,6 +417,18 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     launch_trace_compact(ca, st);
     HIP_TRY(hipGetLastError());
   }
+  return 0;
+  };
+  if (group_mode != OSE_GROUP_TRACE_ID) return rest(false);
+  if (!tail) return rest(true);
+  if (!ws->dup_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ws->dup_host), 64, hipHostMallocDefault));
+  if (!ws->dup_ready) HIP_TRY(hipEventCreateWithFlags(&ws->dup_ready, hipEventDisableTiming));
+  HIP_TRY(hipMemcpyAsync(ws->dup_host, misc, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(ws->dup_ready, st));
+  *tail = [rest, ws]() -> int {
+    HIP_TRY(hipEventSynchronize(ws->dup_ready));
+    return rest(*ws->dup_host != 0);
+  };
   return 0;
 }
 

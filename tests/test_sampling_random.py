@@ -325,3 +325,34 @@ def test_gpu_sampling_parity_full_c5():
     # BASELINE.json configs[4]: 50M spans, Zipf(1.1) trace sizes up to 50k
     g = Generator("zipf", seed=0x0D160005, n_spans=50_000_000, threads=16)
     gpu_vs_oracle(g, per_trace=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_gpu_sample_and_template_one_call(shuffle):
+    # SAMPLE | TEMPLATE in one call queues the URL launches between SAMPLE's
+    # fast path and its (host-gated) slow path and per-trace compaction
+    # (engine.cpp run_stages): keep, per-trace records and URL outputs must
+    # all match the oracle, with and without repeated trace ids
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine
+    from tests.oracle_lib import UrlOracle
+    g = Generator("fused", seed=0x0D160044, n_spans=200_000, shuffle=shuffle)
+    eng = Engine({"odigossampling": CFG, "odigosurltemplate": {}})
+    db = DeviceBatch(g.cols)
+    eng.process_device(db, native.STAGE_SAMPLE | native.STAGE_TEMPLATE, native.GROUP_TRACE_ID, seed=SEED)
+    torch.cuda.synchronize()
+    assert int(db.out_numpy("device_status", np.uint32)[0]) == 0
+    ho = oracle_run(g.cols, native.GROUP_TRACE_ID, seed=SEED, cfg=CFG)
+    n = g.cols.n_spans
+    np.testing.assert_array_equal(db.out_numpy("keep")[:n], ho.view("keep", np.uint8)[:n])
+    t = int(ho.view("trace_count", np.uint32)[0])
+    assert int(db.out_numpy("trace_count", np.uint32)[0]) == t
+    np.testing.assert_array_equal(db.out_numpy("trace_first_span", np.uint32)[:t], ho.view("trace_first_span", np.uint32)[:t])
+    np.testing.assert_array_equal(db.out_numpy("trace_keep")[:t], ho.view("trace_keep", np.uint8)[:t])
+    uo = HostOutputs(g.cols)
+    assert UrlOracle({}).process(g.cols, uo.outs, nthreads=8) == 0
+    np.testing.assert_array_equal(db.out_numpy("url_out")[:n], uo.view("url_out", np.uint8)[:n])
+    used = db.used()
+    assert used == int(uo.used[0])
+    np.testing.assert_array_equal(db.out_numpy("tmpl_arena")[:used], uo.bufs["tmpl_arena"][:used])
