@@ -74,7 +74,13 @@ __device__ __forceinline__ bool wave_seg_sum(uint32_t key, bool valid, T& v, uin
   return last;
 }
 
-__device__ __forceinline__ uint32_t size_span_tile(const SizeKernelArgs& a, uint64_t i);
+struct SpanCols {
+  uint32_t s, kept, span_size, tl, old;
+  uint8_t u, kd;
+  bool valid;
+};
+__device__ __forceinline__ SpanCols size_span_load(const SizeKernelArgs& a, uint64_t i);
+__device__ __forceinline__ uint32_t size_span_finish(const SizeKernelArgs& a, const SpanCols& x);
 
 // Grid-stride over 256-span tiles (a capped grid: the surviving-span count
 // is reduced per block and added with ONE atomic per block — a per-wave
@@ -83,8 +89,13 @@ __global__ __launch_bounds__(kSThreads) void size_span_kernel(SizeKernelArgs a) 
   if (batch_dropped(a)) return;
   __shared__ uint32_t wk[kSThreads / kWave];
   uint32_t kept_total = 0;
-  for (uint64_t base = (uint64_t)blockIdx.x * kSThreads; base < a.n_spans; base += (uint64_t)gridDim.x * kSThreads) {
-    kept_total += size_span_tile(a, base + threadIdx.x);
+  // two tiles per iteration: both tiles' loads are in flight together
+  const uint64_t stride = (uint64_t)gridDim.x * kSThreads;
+  for (uint64_t base = (uint64_t)blockIdx.x * kSThreads; base < a.n_spans; base += 2 * stride) {
+    const SpanCols x0 = size_span_load(a, base + threadIdx.x);
+    const SpanCols x1 = size_span_load(a, base + stride + threadIdx.x);
+    kept_total += size_span_finish(a, x0);
+    if (base + stride < a.n_spans) kept_total += size_span_finish(a, x1);   // wave-uniform
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) kept_total += __shfl_xor(kept_total, o, kWave);
@@ -97,39 +108,51 @@ __global__ __launch_bounds__(kSThreads) void size_span_kernel(SizeKernelArgs a) 
   }
 }
 
-__device__ __forceinline__ uint32_t size_span_tile(const SizeKernelArgs& a, uint64_t i) {
-  const bool valid = i < a.n_spans;
-  uint32_t s = 0, kept = 0;
-  uint64_t contrib = 0;
-  if (valid) {
-    s = a.scope[i];
-    kept = a.sampled ? a.keep[i] : 1u;
-    if (kept) {
-      uint64_t sz = a.span_size[i];
-      const uint8_t u = a.templated ? a.url_out[i] : 0;
-      if (u) {
-        const uint64_t tl = a.tmpl[i].len;
-        if (u & OSE_OUT_SET_ATTR) {   // PutStr(http.route | url.template, tmpl): one more KeyValue
-          const uint64_t keylen = a.kind[i] == OSE_KIND_CLIENT ? 12 : 10;
-          sz += field_len(field_len(keylen) + field_len(field_len(tl)));
-        }
-        if (u & OSE_OUT_RENAME) {     // SetName(method + " " + tmpl), old name == method
-          const uint64_t old = a.name_len[i];
-          sz += field_len(old + 1 + tl) - (old ? field_len(old) : 0);
-        }
-      }
-      contrib = field_len(sz);
+__device__ __forceinline__ SpanCols size_span_load(const SizeKernelArgs& a, uint64_t i) {
+  // every column is loaded up front, whatever keep and url_out say: one
+  // memory round trip per tile instead of three dependent ones (the kernel
+  // is latency-bound; the extra bytes of dropped/untemplated spans are cheap)
+  SpanCols x{};
+  x.valid = i < a.n_spans;
+  if (x.valid) {
+    x.s = a.scope[i];
+    x.kept = a.sampled ? a.keep[i] : 1u;
+    x.span_size = a.span_size[i];
+    if (a.templated) {
+      x.u = a.url_out[i];
+      x.tl = a.tmpl[i].len;
+      x.kd = a.kind[i];
+      x.old = a.name_len[i];
     }
   }
+  return x;
+}
+
+__device__ __forceinline__ uint32_t size_span_finish(const SizeKernelArgs& a, const SpanCols& x) {
+  uint64_t contrib = 0;
+  if (x.valid && x.kept) {
+    uint64_t sz = x.span_size;
+    const uint64_t tl = x.tl;
+    if (x.u & OSE_OUT_SET_ATTR) {   // PutStr(http.route | url.template, tmpl): one more KeyValue
+      const uint64_t keylen = x.kd == OSE_KIND_CLIENT ? 12 : 10;
+      sz += field_len(field_len(keylen) + field_len(field_len(tl)));
+    }
+    if (x.u & OSE_OUT_RENAME) {     // SetName(method + " " + tmpl), old name == method
+      const uint64_t old = x.old;
+      sz += field_len(old + 1 + tl) - (old ? field_len(old) : 0);
+    }
+    contrib = field_len(sz);
+  }
   uint64_t v = contrib;
-  uint32_t c = kept;
-  const bool tail = wave_seg_sum(s, valid, v, c);
+  uint32_t c = x.valid ? x.kept : 0u;
+  const uint32_t s = x.s;
+  const bool tail = wave_seg_sum(s, x.valid, v, c);
   if (tail) {
     if (v) atomicAdd((unsigned long long*)&a.scope_body[s], (unsigned long long)v);
     if (c) atomicAdd(&a.scope_kept[s], c);
     a.scope_had[s] = 1;
   }
-  return kept;
+  return x.valid ? x.kept : 0u;
 }
 
 __global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a) {
