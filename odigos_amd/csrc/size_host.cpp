@@ -41,15 +41,15 @@ int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mas
   const double ratio = e->traffic.sampling_ratio;
   const double u = rnd ? rnd->traffic_u : 0.0;
   if (!(ratio != 0 && u < ratio)) return 0;
-  if (o->res_bytes && c->n_resources) HIP_TRY(hipMemsetAsync(o->res_bytes, 0, 8 * (size_t)c->n_resources, st));
+  // res_bytes needs no clearing: size_res_kernel writes every entry, zeros
+  // when the batch was dropped
   const uint64_t S = c->n_scopes, R = c->n_resources;
   int rc = ws->reserve(size_scratch_bytes(S, R));
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(ws->dev);
   uint8_t* sc = base + 256;
   uint8_t* rs = base + align_up(256 + 16 * std::max<uint64_t>(S, 1), 256);
-  HIP_TRY(hipMemsetAsync(sc, 0, 16 * std::max<uint64_t>(S, 1), st));
-  HIP_TRY(hipMemsetAsync(rs, 0, 16 * std::max<uint64_t>(R, 1), st));
+  HIP_TRY(hipMemsetAsync(sc, 0, (size_t)(rs - sc) + 16 * std::max<uint64_t>(R, 1), st));   // scope and resource sums
   SizeKernelArgs a{};
   a.n_spans = n;
   a.n_scopes = (uint32_t)S;

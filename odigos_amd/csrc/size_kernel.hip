@@ -186,7 +186,11 @@ __global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a)
 }
 
 __global__ __launch_bounds__(kSThreads) void size_res_kernel(SizeKernelArgs a) {
-  if (batch_dropped(a)) return;
+  if (batch_dropped(a)) {   // nothing survived: every ResourceSpans is 0 bytes
+    if (a.res_bytes)
+      for (uint32_t r = blockIdx.x * kSThreads + threadIdx.x; r < a.n_resources; r += gridDim.x * kSThreads) a.res_bytes[r] = 0;
+    return;
+  }
   __shared__ unsigned long long hist[kLdsAttrsets];   // two's-complement sums
   const bool lds = a.n_attrsets <= kLdsAttrsets;
   if (lds)
