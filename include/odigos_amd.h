@@ -249,7 +249,11 @@ int ose_process(ose_engine* eng, ose_batch* b, uint32_t stage_mask,
 
 /* Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream):
  * columns/outputs are device pointers already resident in HBM.  This is the
- * entry point the benchmark times.                                          */
+ * entry point the benchmark times.  One exception to "asynchronous": with
+ * SAMPLE | TEMPLATE and OSE_GROUP_TRACE_ID, the host waits (after queueing
+ * the URL kernels) for SAMPLE's fast pass to finish, to queue the repeated-
+ * trace-id slow path only when it is needed; the call still returns before
+ * the URL and SIZE kernels finish.                                          */
 int ose_process_device(ose_engine* eng, const ose_columns* cols,
                        const ose_outputs* outs, uint32_t stage_mask,
                        uint32_t group_mode, const ose_rand* rnd, void* hip_stream);

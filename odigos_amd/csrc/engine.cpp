@@ -414,14 +414,21 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   // SAMPLE, which is queued once the host has read the fast path's dup flag
   // (by then the GPU is busy with the URL kernels, and the ~12 gated
   // slow-path launches are skipped when no trace id repeats)
-  const bool defer = (mask & OSE_STAGE_SAMPLE) && (mask & OSE_STAGE_TEMPLATE) &&
-                     group_mode == OSE_GROUP_TRACE_ID && c->n_spans > 0 && !getenv("OSE_NO_DEFER_SLOW");
+  // SAMPLE without TEMPLATE: the host waits for the fast path right away (an
+  // idle gap of one launch latency instead of ~12 gated launches)
+  const bool gate_on_host = (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID && c->n_spans > 0 &&
+                            !getenv("OSE_NO_DEFER_SLOW");
+  const bool defer = gate_on_host && (mask & OSE_STAGE_TEMPLATE);
   const size_t url_off = defer ? (sampling_scratch_bytes(c->n_spans) + 255) / 256 * 256 : 0;
   if (defer) need = std::max(need, url_off + url_workspace_bytes(c->n_spans));
   int rc = ws->reserve(need);
   std::function<int()> sample_tail;
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
-  if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws, defer ? &sample_tail : nullptr);
+  if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws, gate_on_host ? &sample_tail : nullptr);
+  if (sample_tail && !defer) {
+    rc = sample_tail();
+    sample_tail = nullptr;
+  }
   if (!rc && (mask & OSE_STAGE_TEMPLATE)) rc = run_url(e, c, o, st, ws, url_off);
   if (sample_tail) {
     const int trc = sample_tail();   // always drained: the host event wait must not be skipped
