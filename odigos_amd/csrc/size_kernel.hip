@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -215,7 +216,11 @@ __global__ __launch_bounds__(kSThreads) void size_res_kernel(SizeKernelArgs a) {
 }  // namespace
 
 void launch_size_spans(const SizeKernelArgs& a, hipStream_t st) {
-  const uint64_t blocks = std::min<uint64_t>((a.n_spans + kSThreads - 1) / kSThreads, 2048);
+  static const uint64_t cap = [] {
+    const char* g = getenv("OSE_SIZE_GRID");   // tuning
+    return g ? std::max<uint64_t>(1, strtoull(g, nullptr, 0)) : 1024ull;   // swept on C4: 512 0.127 ms, 1024 0.088, 2048 0.094, 8192 0.126
+  }();
+  const uint64_t blocks = std::min<uint64_t>((a.n_spans + kSThreads - 1) / kSThreads, cap);
   if (blocks) hipLaunchKernelGGL(size_span_kernel, dim3((uint32_t)blocks), dim3(kSThreads), 0, st, a);
 }
 void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st) {
