@@ -172,13 +172,15 @@ __global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a)
   uint32_t c = alive;
   const bool tail = wave_seg_sum(r, valid, v, c);
   // any scope of the run had spans: OR over the run == (run's had bits != 0)
-  uint32_t h = had;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t oh = __shfl_up(h, d, kWave);
-    const uint32_t orr = __shfl_up(r, d, kWave);
-    if ((int)(threadIdx.x & 63) >= d && orr == r) h |= oh;
-  }
+  // (keys are non-decreasing: the run is lanes [its head, this lane]; two
+  // ballots and a bit search instead of a 6-step shuffle scan)
+  const int lane = threadIdx.x & 63;
+  const uint32_t pr = dpp_mov<0x138>(r, r);   // lane - 1's key (wave_shr:1)
+  const uint64_t heads = __ballot(lane == 0 || pr != r);
+  const uint64_t hadm = __ballot(had != 0);
+  const uint64_t upto = ~0ull >> (63 - lane);
+  const int start = 63 - __clzll((long long)(heads & upto));   // lane 0 is always a head
+  const uint32_t h = (hadm & upto & (~0ull << start)) ? 1u : 0u;
   if (tail) {
     if (v) atomicAdd((unsigned long long*)&a.res_body[r], (unsigned long long)v);
     if (c) atomicAdd(&a.res_alive[r], c);
