@@ -318,11 +318,19 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   launch_trace_eval(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
-  if (a.long_runs) {
-    e->prof_begin("trace_long_kernel", st, tm);
+  auto long_pass = [=]() -> int {
+    Engine::Timed tl{};
+    e->prof_begin("trace_long_kernel", st, tl);
     launch_trace_long(a, st);
     HIP_TRY(hipGetLastError());
-    e->prof_end(tm, st);
+    e->prof_end(tl, st);
+    return 0;
+  };
+  // host-gated (tail): queued only when the fast path listed long runs
+  const bool gate_long = tail && group_mode == OSE_GROUP_TRACE_ID;
+  if (a.long_runs && !gate_long) {
+    const int lr = long_pass();
+    if (lr) return lr;
   }
 
   // the rest of the stage; run_slow = false skips the slow-path launches
@@ -423,11 +431,17 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   if (!tail) return rest(true);
   if (!ws->dup_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ws->dup_host), 64, hipHostMallocDefault));
   if (!ws->dup_ready) HIP_TRY(hipEventCreateWithFlags(&ws->dup_ready, hipEventDisableTiming));
-  HIP_TRY(hipMemcpyAsync(ws->dup_host, misc, 4, hipMemcpyDeviceToHost, st));
+  // misc[0] = dup, misc[12] = long runs listed by the fast path
+  HIP_TRY(hipMemcpyAsync(ws->dup_host, misc, 64, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipEventRecord(ws->dup_ready, st));
-  *tail = [rest, ws]() -> int {
+  const bool has_long = a.long_runs != nullptr;
+  *tail = [rest, long_pass, has_long, ws]() -> int {
     HIP_TRY(hipEventSynchronize(ws->dup_ready));
-    return rest(*ws->dup_host != 0);
+    if (has_long && ws->dup_host[12]) {   // before the slow path, which rewrites every trace's keep
+      const int lr = long_pass();
+      if (lr) return lr;
+    }
+    return rest(ws->dup_host[0] != 0);
   };
   return 0;
 }
