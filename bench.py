@@ -3,25 +3,41 @@
 
 One "step" = one pass of the configured processors over one device-resident
 synthetic batch (BASELINE.json configs; seeds from SURVEY.md §8d).  With
---gpus N the driver launches one rank per GPU (torch.distributed.run); every
-rank processes its own shard (weak scaling: the path partitions by trace,
-SURVEY.md §8e), the timed region is bracketed by barrier + synchronize, and
-the max over ranks is reported.  Rank 0 prints ONE JSON line.
+--gpus N the driver launches one rank per GPU (torch.distributed.run); the
+timed region is bracketed by barrier + synchronize, the max over ranks is
+reported and rank 0 prints ONE JSON line.
 
-Workloads (per GPU):
-  url       C2  odigosurltemplate, 10M spans, default rules          (configs[1])
-  sampling  C3  odigossampling, 50M spans / ~5M traces, C3 rules     (configs[2])
-  zipf      C5  odigossampling on Zipf trace sizes (1-50k spans), 50M spans  (configs[4])
-  fused     C4  all three processors, 12.5M spans/GPU (100M on 8)    (configs[3]);
-                with N > 1 the sampling records go to each trace's owner
-                GPU through an RCCL all-to-all (odigos_amd/exchange.py)
+Workloads:
+  fused     C4 (configs[3], the default): odigossampling -> odigosurltemplate
+            -> odigostrafficmetrics over 100M spans in total.  N = 1: all
+            100M spans on one GPU.  N > 1: rank r holds the batch node
+            collector r of N delivers (gen_batch.cpp split mode: the
+            ResourceSpans of one trace land on different ranks), ~100M/N
+            spans each (strong scaling); sampling partials go to each trace's
+            owner GPU through an RCCL all-to-all (odigos_amd/exchange.py).
+  url       C2 (configs[1]): odigosurltemplate, 10M spans/GPU, default rules
+  sampling  C3 (configs[2]): odigossampling, 50M spans / ~5M traces per GPU
+  zipf      C5 (configs[4]): odigossampling + odigosurltemplate on Zipf(1.1)
+            trace sizes (1-50k spans) with 1M distinct routes and 64-bit ids
+            in paths, 50M spans per GPU
+  owner     diagnostic: on ONE GPU, the batch trace owner 0 receives in an
+            8-GPU C4 step (the partial records of 8 source shards in rank
+            order, so a trace arrives as several runs): unpack + the SAMPLE
+            stage, which takes the sort-based path.
+
+The CPU baseline (rank 0, N = 1) is the oracle (oracle/*.c, built with
+-march=native on this host) on C1 = 1M spans of the fused mix, seed
+0x0D160001, on this process's CPU share; the same oracle
+then checks the timed GPU output at full size (parity_vs_oracle).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -31,88 +47,92 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "spans/sec processed (whole node) at 1/2/4/8 MI355X; % of HBM roofline"
+
+FUSED_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "resource", "scope", "url_flags", "path",
+                "route", "span_size", "name_len", "res_svc", "res_svc_str", "res_attrset", "res_size", "scope_size",
+                "scope_resource")
+SAMPLE_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc", "res_svc_str")
+URL_KERNELS = ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel")
+TRACE_KERNELS = ("trace_eval_kernel", "trace_long_kernel")
+SLOW_KERNELS = ("trace_insert_exact_kernel", "trace_key_kernel", "sort_hist_kernel", "scan_u32_kernel",
+                "sort_scatter_kernel")
+SIZE_KERNELS = ("size_span_kernel", "size_scope_kernel", "size_res_kernel")
+PER_TRACE_OUTS = ("trace_count", "trace_first_span", "trace_keep", "trace_level", "trace_ratio")
 
 WORKLOADS = {
-    "url": dict(gen="url", seed=0x0D160002, spans=10_000_000,
-                cfg={"odigosurltemplate": {}}, stages="TEMPLATE", group="TRACE_ID",
+    "url": dict(gen="url", seed=0x0D160002, spans=10_000_000, per_gpu=True,
+                cfg={"odigosurltemplate": {}}, stages="TEMPLATE",
                 # no include/exclude configured: the shim passes res_url_ok = NULL
                 null_columns=("res_url_ok",), null_outputs=(),
-                fields=("arena", "kind", "url_flags", "path"),
-                kernels=("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel"),
+                fields=("arena", "kind", "url_flags", "path"), kernels=URL_KERNELS,
                 metric_config="C2: URL templatization only, 10M spans/GPU, C2 segment mix, default rules"),
-    "sampling": dict(gen="sampling", seed=0x0D160003, spans=50_000_000,
-                     cfg=None, stages="SAMPLE", group="TRACE_ID",
-                     null_columns=(), null_outputs=("trace_count", "trace_first_span", "trace_keep", "trace_level",
-                                                    "trace_ratio"),
-                     fields=("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc",
-                             "res_svc_str"),
-                     kernels=("trace_eval_kernel", "trace_long_kernel"),
+    "sampling": dict(gen="sampling", seed=0x0D160003, spans=50_000_000, per_gpu=True,
+                     cfg=None, stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
+                     fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS,
                      metric_config="C3: trace-level sampling (1 error + 4 service + 16 latency rules), "
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
-    "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000,
-                 cfg=None, stages="SAMPLE", group="TRACE_ID",
-                 null_columns=(), null_outputs=("trace_count", "trace_first_span", "trace_keep", "trace_level",
-                                                "trace_ratio"),
-                 fields=("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc",
-                         "res_svc_str"),
-                 kernels=("trace_eval_kernel", "trace_long_kernel"),
-                 metric_config="C5: trace-level sampling on Zipf(1.1) trace sizes (1 to 50k spans/trace), "
-                               "50M spans per GPU, C3 rules, grouped by trace_id"),
-    "fused": dict(gen="fused", seed=0x0D160004, spans=12_500_000,
-                  cfg=None, stages="SAMPLE|TEMPLATE|SIZE", group="TRACE_ID",
-                  null_columns=("res_url_ok",), null_outputs=("trace_count", "trace_first_span", "trace_keep",
-                                                             "trace_level", "trace_ratio", "res_bytes"),
-                  fields=("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "resource", "scope",
-                          "url_flags", "path", "route", "span_size", "name_len", "res_svc", "res_svc_str",
-                          "res_attrset", "res_size", "scope_size", "scope_resource"),
-                  kernels=("trace_eval_kernel", "trace_long_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel",
-                           "size_span_kernel", "size_scope_kernel", "size_res_kernel"),
-                  metric_config="C4: fused odigossampling -> odigosurltemplate -> odigostrafficmetrics, "
-                                "12.5M spans/GPU (100M on 8), trace-id all-to-all over RCCL when N > 1"),
+    "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000, per_gpu=True,
+                 cfg=None, stages="SAMPLE|TEMPLATE", null_columns=("res_url_ok",), null_outputs=PER_TRACE_OUTS,
+                 fields=SAMPLE_FIELDS + ("kind", "url_flags", "path"), kernels=TRACE_KERNELS + URL_KERNELS,
+                 metric_config="C5: odigossampling + odigosurltemplate on Zipf(1.1) trace sizes (1 to 50k "
+                               "spans/trace), 1M distinct routes, 64-bit user ids in paths, 50M spans per GPU"),
+    "fused": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False,
+                  cfg=None, stages="SAMPLE|TEMPLATE|SIZE", null_columns=("res_url_ok",),
+                  null_outputs=PER_TRACE_OUTS + ("res_bytes",), fields=FUSED_FIELDS,
+                  kernels=TRACE_KERNELS + URL_KERNELS + SIZE_KERNELS,
+                  metric_config="C4: fused odigossampling -> odigosurltemplate -> odigostrafficmetrics, 100M spans "
+                                "in total (all on one GPU at N=1; ~100M/N per GPU, trace-id all-to-all over RCCL "
+                                "at N>1)"),
+    "owner": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False, sources=8,
+                  cfg=None, stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
+                  fields=SAMPLE_FIELDS, kernels=("shard_unpack",) + TRACE_KERNELS + SLOW_KERNELS,
+                  metric_config="C4 owner side on one GPU: the records trace owner 0 of 8 receives "
+                                "(8 source shards of the 100M-span C4 batch, rank order), unpack + SAMPLE"),
 }
 
 # node-collector res_attributes_keys (autoscaler/controllers/nodecollector/collectorconfig/ownmetrics-ui.go:33-47)
 NODE_KEYS = ["k8s.namespace.name", "k8s.deployment.name", "k8s.statefulset.name", "k8s.daemonset.name",
              "k8s.cronjob.name", "k8s.job.name", "k8s.pod.name", "k8s.node.name", "service.name"]
+C1 = dict(gen="fused", seed=0x0D160001, spans=1_000_000)   # SURVEY.md §8d CPU reference config
 
 
 def _cfg(wl):
     if wl["cfg"] is not None:
         return wl["cfg"]
     from tests.workloads import c3_sampling_config
-    if wl["gen"] == "fused":
-        return {"odigossampling": c3_sampling_config(), "odigosurltemplate": {},
-                "odigostrafficmetrics": {"res_attributes_keys": NODE_KEYS}}
-    return {"odigossampling": c3_sampling_config()}
+    st = wl["stages"]
+    cfg = {"odigossampling": c3_sampling_config()}
+    if "TEMPLATE" in st:
+        cfg["odigosurltemplate"] = {}
+    if "SIZE" in st:
+        cfg["odigostrafficmetrics"] = {"res_attributes_keys": NODE_KEYS}
+    return cfg
 
 
-def algorithmic_bytes_fused(gen, db, n, cfg) -> int:
-    """SURVEY.md §8(d) fused row: the union of the three stages' columns, each
-    read once (trace_id, start, end, status, resource, route ref + compared
-    route bytes, kind, url_flags, path ref + templated path bytes, span_size,
-    scope, name_len; per scope 8 B, per resource 20 B) and each output written
-    once (keep, url_out, tmpl ref + bytes, attribute-set counters)."""
-    samp = algorithmic_bytes_sampling(gen, db, n, cfg)          # includes the 1 B keep
-    url = algorithmic_bytes_url(gen, db, n)
-    size = n * (4 + 4 + 4) + gen.cols.n_scopes * 8 + gen.cols.n_resources * 12 + gen.cols.n_attrsets * 8
-    return samp + url + size
+def _stages(wl):
+    from odigos_amd import native
+    m = 0
+    for s in wl["stages"].split("|"):
+        m |= getattr(native, "STAGE_" + s)
+    return m
 
 
-def algorithmic_bytes_url(gen, db, n) -> int:
-    """SURVEY.md §8(d) URL row: per span 8 B path ref + 1 B kind + 1 B url_flags
-    read, 8 B template ref + 1 B url_out written; plus the path bytes of every
-    span whose path is templatized (read) and the template bytes written."""
-    url_out = db.out_numpy("url_out")[:n]
+# ---- algorithmic bytes -------------------------------
+def algorithmic_bytes_url(gen, url_out, used, n) -> int:
+    """URL row: per span 8 B path ref + 1 B kind + 1 B url_flags read, 8 B
+    template ref + 1 B url_out written; plus the path bytes of every span
+    whose path is templatized (read) and the template bytes written."""
     path = gen.array("path").view(np.uint32).reshape(-1, 2)[:n]
-    templ_read = int(path[(url_out & 1) != 0, 1].sum())
-    return n * (8 + 1 + 1) + n * (8 + 1) + templ_read + db.used()
+    templ_read = int(path[(url_out[:n] & 1) != 0, 1].sum())
+    return n * (8 + 1 + 1) + n * (8 + 1) + templ_read + used
 
 
-def algorithmic_bytes_sampling(gen, db, n, cfg) -> int:
-    """SURVEY.md §8(d) sampling row: per span 16 B trace_id + 8 B start + 8 B
-    end + 1 B status + 4 B resource + 8 B route ref read and 1 B keep written;
-    per resource 8 B (res_svc, res_svc_str); plus min(len(route), longest
-    rule route) route bytes per span that carries one."""
+def algorithmic_bytes_sampling(gen, n, cfg) -> int:
+    """Sampling row: per span 16 B trace_id + 8 B start + 8 B end + 1 B
+    status + 4 B resource + 8 B route ref read and 1 B keep written; per
+    resource 8 B (res_svc, res_svc_str); plus min(len(route), longest rule
+    route) route bytes per span that carries one."""
     rules = cfg["odigossampling"].get("endpoint_rules", []) + cfg["odigossampling"].get("service_rules", []) + \
         cfg["odigossampling"].get("global_rules", [])
     pmax = max([len(r["rule_details"].get("http_route", "")) for r in rules] + [0])
@@ -121,119 +141,165 @@ def algorithmic_bytes_sampling(gen, db, n, cfg) -> int:
     return n * (16 + 8 + 8 + 1 + 4 + 8 + 1) + gen.cols.n_resources * 8 + rb
 
 
-def cpu_baseline_url(gen, cfg, threads: int, budget_s: float = 12.0, calls: int = 1):
-    """Oracle (oracle/url.c, -O3) on the same batch: `threads` pthreads over
-    the whole batch, repeated until ~budget_s of wall time; plus one
-    single-thread pass over a 1M-span prefix."""
-    from odigos_amd.batch import HostOutputs
-    from tests.oracle_lib import UrlOracle
-    orc = UrlOracle(cfg["odigosurltemplate"])
-    ho = HostOutputs(gen.cols)
-    n = gen.cols.n_spans
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        assert orc.process(gen.cols, ho.outs, threads) == 0
-        reps += 1
-        if time.perf_counter() - t0 > budget_s / 2 or reps >= 50:
-            break
-    dt = time.perf_counter() - t0
-    mt = n * reps / dt
-    c1 = _prefix(gen.cols, 1_000_000)
-    ho1 = HostOutputs(c1)
-    t1 = time.perf_counter()
-    assert orc.process(c1, ho1.outs, 1) == 0
-    st = c1.n_spans / (time.perf_counter() - t1)
-    sample = f"{n} spans (the same C2 batch) x {reps} passes, oracle/url.c -O3 pthreads"
-
-    def parity(db):
-        return (int(ho.used[0]) == db.used() and
-                np.array_equal(ho.view("url_out", np.uint8)[:n], db.out_numpy("url_out")[:n]))
-    return mt, st, sample, parity
+def algorithmic_bytes(wl, gen, db, n, cfg) -> int:
+    st = wl["stages"]
+    b = 0
+    if "SAMPLE" in st:
+        b += algorithmic_bytes_sampling(gen, n, cfg)
+    if "TEMPLATE" in st:
+        b += algorithmic_bytes_url(gen, db.out_numpy("url_out", n=n), db.used(), n)
+    if "SIZE" in st:
+        # span_size, scope, name_len per span; 8 B per scope, 12 B per resource, 8 B per attribute set
+        b += n * 12 + gen.cols.n_scopes * 8 + gen.cols.n_resources * 12 + gen.cols.n_attrsets * 8
+    return b
 
 
-def cpu_baseline_fused(gen, cfg, threads: int, budget_s: float = 12.0, calls: int = 1):
-    """The three oracles chained in gateway order (sampling -> templating ->
-    size; oracle/{sampling,url,size}.c -O3, pthreads for the first two) on a
-    2M-span prefix of the same batch, repeated to ~budget_s/2.  Parity: keep,
-    url_out and the attribute-set counters of the full batch."""
+# ---- CPU baseline (oracle) ----------------------------------------------------------
+def cpu_share():
+    """(threads this process may use, nproc, CPU model).  The GPU box gives a
+    one-GPU job a share of the host (16 CPUs); nproc shows every CPU of the
+    machine, so the share is read from the affinity mask, the cgroup quota
+    and OMP_NUM_THREADS (set to the share on the box)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    share = aff
+    try:
+        q, p = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            share = min(share, max(1, int(int(q) / int(p))))
+    except Exception:
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        share = min(share, max(1, int(os.environ["OMP_NUM_THREADS"])))
+    model = ""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return share, os.cpu_count() or 1, model
+
+
+def native_oracle() -> str:
+    """Builds oracle/*.c with -march=native for this host (the checker and the
+    CPU baseline; the in-tree liboracle.so is built for a generic x86-64)."""
+    out = Path(tempfile.gettempdir()) / f"liboracle_native_{os.getpid()}.so"
+    src = sorted(str(p) for p in (ROOT / "oracle").glob("*.c"))
+    r = subprocess.run(["gcc", "-std=c11", "-O3", "-march=native", "-fPIC", "-pthread", "-shared", "-o", str(out),
+                        *src, "-lm"], capture_output=True, text=True)
+    if r.returncode != 0:
+        return ""
+    os.environ["OSE_ORACLE_LIB"] = str(out)
+    return "-O3 -march=native"
+
+
+def oracle_chain(cfg, stages):
+    """The oracles chained in gateway order (sampling -> templating -> size)."""
     from odigos_amd import native
     from odigos_amd.batch import HostOutputs
     from tests.oracle_lib import SamplingOracle, UrlOracle, size_process
-    so, uo = SamplingOracle(cfg["odigossampling"]), UrlOracle(cfg["odigosurltemplate"])
-    st = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE
+    so = SamplingOracle(cfg["odigossampling"]) if stages & native.STAGE_SAMPLE else None
+    uo = UrlOracle(cfg["odigosurltemplate"]) if stages & native.STAGE_TEMPLATE else None
 
     def chain(cols, nt):
         ho = HostOutputs(cols)
-        assert so.process(cols, ho.outs, native.GROUP_TRACE_ID, 0x5EED, nt) == 0
-        assert uo.process(cols, ho.outs, nt) == 0
-        assert size_process(cols, ho.outs, st, native.GROUP_TRACE_ID, ho.outs, 1, 1.0, 0.0) == 0
+        if so:
+            assert so.process(cols, ho.outs, native.GROUP_TRACE_ID, 0x5EED, nt) == 0
+        if uo:
+            assert uo.process(cols, ho.outs, nt) == 0
+        if stages & native.STAGE_SIZE:
+            assert size_process(cols, ho.outs, stages, native.GROUP_TRACE_ID, ho.outs, 1, 1.0, 0.0, nt) == 0
         return ho
-    n = gen.cols.n_spans
-    c2 = _prefix(gen.cols, min(n, 2_000_000))
+    return chain
+
+
+def cpu_baseline(wl, cfg, stages, threads, budget_s=12.0):
+    """C1 (1M spans of the fused mix, seed 0x0D160001) through the oracle
+    chain of this workload's stages: `threads` pthreads repeated to about
+    budget_s/2, then one single-thread pass."""
+    from odigos_amd.batch import Generator
+    chain = oracle_chain(cfg, stages)
+    g = Generator(C1["gen"], seed=C1["seed"], n_spans=C1["spans"], threads=threads)
+    n = g.cols.n_spans
     reps, t0 = 0, time.perf_counter()
     while True:
-        chain(c2, threads)
+        chain(g.cols, threads)
         reps += 1
-        if time.perf_counter() - t0 > budget_s / 2 or reps >= 20:
+        if time.perf_counter() - t0 > budget_s / 2 or reps >= 200:
             break
-    mt = c2.n_spans * reps / (time.perf_counter() - t0)
-    c1 = _prefix(gen.cols, min(n, 500_000))
+    mt = n * reps / (time.perf_counter() - t0)
     t1 = time.perf_counter()
-    chain(c1, 1)
-    st1 = c1.n_spans / (time.perf_counter() - t1)
-    sample = f"{c2.n_spans}-span prefix of the C4 shard x {reps} passes, oracle/{{sampling,url,size}}.c -O3"
+    chain(g.cols, 1)
+    st = n / (time.perf_counter() - t1)
+    return mt, st, f"C1: {n} spans of the fused mix (seed 0x0D160001) x {reps} passes, oracle chain " \
+                   f"[{wl['stages']}] with {threads} pthreads"
 
-    def parity(db):
-        ho = chain(gen.cols, threads)
+
+def parity_full(wl, gen, db, cfg, stages, threads, calls):
+    """The oracle chain on the whole timed batch against the GPU outputs:
+    keep, url_out, template refs and bytes, attribute-set counters."""
+    from odigos_amd import native
+    chain = oracle_chain(cfg, stages)
+    ho = chain(gen.cols, threads)
+    n = gen.cols.n_spans
+    res = {}
+    if stages & native.STAGE_SAMPLE:
+        res["keep"] = bool(np.array_equal(ho.view("keep", np.uint8)[:n], db.out_numpy("keep", n=n)))
+    if stages & native.STAGE_TEMPLATE:
+        uo = db.out_numpy("url_out", n=n)
+        res["url_out"] = bool(np.array_equal(ho.view("url_out", np.uint8)[:n], uo))
+        m = uo != 0
+        res["tmpl_refs"] = bool(np.array_equal(ho.view("tmpl", np.uint64)[:n][m], db.out_numpy("tmpl", np.uint64, n=n)[m]))
+        used = db.used()
+        res["tmpl_arena"] = bool(used == int(ho.used[0]) and
+                                 np.array_equal(ho.bufs["tmpl_arena"][:used], db.out_numpy("tmpl_arena", n=used)))
+    if stages & native.STAGE_SIZE:
         A = gen.cols.n_attrsets
-        return bool(np.array_equal(ho.view("keep", np.uint8)[:n], db.out_numpy("keep")[:n]) and
-                    np.array_equal(ho.view("url_out", np.uint8)[:n], db.out_numpy("url_out")[:n]) and
-                    # the device counters were ADDED to by every timed and warm-up call
-                    np.array_equal(calls * ho.view("attrset_bytes", np.int64)[:A],
-                                   db.out_numpy("attrset_bytes", np.int64)[:A]))
-    return mt, st1, sample, parity
+        # the device counters were ADDED to by every timed and warm-up call
+        res["attrset_bytes"] = bool(np.array_equal(calls * ho.view("attrset_bytes", np.int64)[:A],
+                                                   db.out_numpy("attrset_bytes", np.int64, n=A)))
+        res["accepted_spans"] = bool(calls * int(ho.view("accepted_spans", np.int64)[0]) ==
+                                     int(db.out_numpy("accepted_spans", np.int64, n=1)[0]))
+    return res
 
 
-def cpu_baseline_sampling(gen, cfg, threads: int, budget_s: float = 12.0, calls: int = 1):
-    """Oracle (oracle/sampling.c, -O3: trace_id grouping + per-trace rule
-    fold) on a 5M-span prefix of the same batch, `threads` pthreads for the
-    fold, repeated to ~budget_s/2; plus a single-thread pass over 1M spans.
-    Parity: the full batch's keep column against the GPU's."""
-    from odigos_amd import native
-    from odigos_amd.batch import HostOutputs
-    from tests.oracle_lib import SamplingOracle
-    orc = SamplingOracle(cfg["odigossampling"])
-    n = gen.cols.n_spans
-    c5 = _prefix(gen.cols, min(n, 5_000_000))
-    ho5 = HostOutputs(c5)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        assert orc.process(c5, ho5.outs, native.GROUP_TRACE_ID, 0x5EED, threads) == 0
-        reps += 1
-        if time.perf_counter() - t0 > budget_s / 2 or reps >= 20:
-            break
-    mt = c5.n_spans * reps / (time.perf_counter() - t0)
-    c1 = _prefix(gen.cols, min(n, 1_000_000))
-    ho1 = HostOutputs(c1)
-    t1 = time.perf_counter()
-    assert orc.process(c1, ho1.outs, native.GROUP_TRACE_ID, 0x5EED, 1) == 0
-    st = c1.n_spans / (time.perf_counter() - t1)
-    sample = f"{c5.n_spans}-span prefix of the same batch x {reps} passes, oracle/sampling.c -O3 pthreads"
-
-    def parity(db):
-        ho = HostOutputs(gen.cols)
-        assert orc.process(gen.cols, ho.outs, native.GROUP_TRACE_ID, 0x5EED, threads) == 0
-        return bool(np.array_equal(ho.view("keep", np.uint8)[:n], db.out_numpy("keep")[:n]))
-    return mt, st, sample, parity
-
-
-def _prefix(cols, k):
+# ---- owner-side workload --------------------------------------------------------------
+def build_owner_batch(eng, wl, threads):
+    """Packs the 8 source shards of the C4 batch on this GPU and keeps what
+    trace owner 0 receives, in source-rank order (what the all-to-all
+    delivers).  Returns the device record buffer, its record count and the
+    number of source spans those records stand for."""
     import ctypes as C
+
+    import torch
+
     from odigos_amd import native
-    c1 = native.Columns()
-    C.memmove(C.addressof(c1), C.addressof(cols), C.sizeof(native.Columns))
-    c1.n_spans = min(cols.n_spans, k)
-    return c1
+    from odigos_amd.batch import DeviceBatch, Generator
+    L = native.lib()
+    W = wl["sources"]
+    rb = int(L.ose_shard_record_bytes(eng.h))
+    parts, spans_repr = [], 0
+    for s in range(W):
+        g = Generator(wl["gen"], seed=wl["seed"], n_spans=wl["spans"], threads=threads, rank=s, world=W)
+        db = DeviceBatch(g.cols, fields=SAMPLE_FIELDS)
+        n = g.cols.n_spans
+        send = torch.empty(max(n, 1) * rb, dtype=torch.uint8, device="cuda")
+        counts = torch.zeros(W, dtype=torch.int64, device="cuda")
+        pos = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+        native.check(L.ose_shard_pack(eng.h, C.byref(db.cols), W, send.data_ptr(), counts.data_ptr(),
+                                      pos.data_ptr(), None))
+        c0 = int(counts[0].item())
+        parts.append(send[: c0 * rb].clone())
+        # spans whose trace owner is rank 0
+        pos_np = pos[:n].cpu().numpy()
+        spans_repr += int((pos_np.astype(np.int64) < c0).sum())
+        del db, send, pos, g
+    recv = torch.cat(parts)
+    return recv, recv.numel() // rb, spans_repr, rb
 
 
 def main():
@@ -241,11 +307,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    # default: the whole hot path (C4 shard), which is also the configuration the
+    # default: the whole hot path (C4), which is also the configuration the
     # multi-GPU runs exercise (trace-id exchange when N > 1); DESIGN.md §6
     ap.add_argument("--workload", default="fused", choices=sorted(WORKLOADS))
-    ap.add_argument("--spans", type=int, default=0, help="override spans per GPU")
+    ap.add_argument("--spans", type=int, default=0, help="override the workload's span count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -264,38 +331,55 @@ def main():
     from odigos_amd.batch import DeviceBatch, Engine, Generator
 
     wl = WORKLOADS[args.workload]
-    n_spans = args.spans or wl["spans"]
-    stages = 0
-    for s in wl["stages"].split("|"):
-        stages |= getattr(native, "STAGE_" + s)
+    stages = _stages(wl)
     cfg = _cfg(wl)
-    gen = Generator(wl["gen"], seed=wl["seed"] + rank, n_spans=n_spans, threads=16)
-    for f in wl.get("null_columns", ()):
-        setattr(gen.cols, f, None)   # columns the configured processors do not read
+    share, nproc, model = cpu_share()
+    gen_threads = max(1, min(16, share))
     eng = Engine(cfg)
-    db = DeviceBatch(gen.cols, fields=wl.get("fields"))
-    for f in wl.get("null_outputs", ()):
-        setattr(db.outs, f, None)    # outputs the shim does not read (per-trace diagnostics)
-    eng.reserve(n_spans)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
-    group = getattr(native, "GROUP_" + wl["group"])
+    total = args.spans or wl["spans"]
+    gen = db = None
+    extra = {}
 
-    if world > 1 and stages & native.STAGE_SAMPLE:
-        # route every span's sampling record to its trace's owner
-        # GPU (RCCL all-to-all), decide there, bring keep back, then template
-        # and size locally on the decisions
-        from odigos_amd.exchange import DeviceExchange, route_and_sample
-        ex = DeviceExchange(eng, db, stream=sh)
-        local = (stages & ~native.STAGE_SAMPLE) | native.STAGE_APPLY_KEEP
+    if args.workload == "owner":
+        assert world == 1, "the owner workload emulates an 8-GPU step on one GPU"
+        recv, n_rec, spans_repr, rb = build_owner_batch(eng, wl, gen_threads)
+        from odigos_amd.exchange import DeviceExchange
+        ex = DeviceExchange.receiver(eng, rb, stream=sh)
+        n_units = spans_repr
+        extra = {"records": n_rec, "record_bytes": rb, "spans_represented": spans_repr}
+        eng.reserve(max(n_rec, 1))
 
         def step():
-            route_and_sample(ex, world)
-            if local & (native.STAGE_TEMPLATE | native.STAGE_SIZE):
-                eng.process_device(db, local, group, seed=0x5EED, stream=sh)
+            ex.unpack_sample(recv, n_rec)
     else:
-        def step():
-            eng.process_device(db, stages, group, seed=0x5EED, stream=sh)
+        if wl["per_gpu"]:
+            gen = Generator(wl["gen"], seed=wl["seed"] + rank, n_spans=total, threads=gen_threads)
+        else:
+            gen = Generator(wl["gen"], seed=wl["seed"], n_spans=total, threads=gen_threads, rank=rank, world=world)
+        for f in wl.get("null_columns", ()):
+            setattr(gen.cols, f, None)   # columns the configured processors do not read
+        db = DeviceBatch(gen.cols, fields=wl.get("fields"))
+        for f in wl.get("null_outputs", ()):
+            setattr(db.outs, f, None)    # outputs the shim does not read (per-trace diagnostics)
+        n_units = gen.cols.n_spans
+        eng.reserve(n_units)
+        if world > 1 and stages & native.STAGE_SAMPLE:
+            # route every span's sampling record to its trace's owner
+            # GPU (RCCL all-to-all), decide there, bring keep back, then template
+            # and size locally on the decisions
+            from odigos_amd.exchange import DeviceExchange, route_and_sample
+            ex = DeviceExchange(eng, db, stream=sh)
+            local_st = (stages & ~native.STAGE_SAMPLE) | native.STAGE_APPLY_KEEP
+
+            def step():
+                route_and_sample(ex, world)
+                if local_st & (native.STAGE_TEMPLATE | native.STAGE_SIZE):
+                    eng.process_device(db, local_st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
+        else:
+            def step():
+                eng.process_device(db, stages, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
 
     for _ in range(args.warmup):
         step()
@@ -313,28 +397,30 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.profile(False)
     prof = eng.profile_read()
-    status = int(db.out_numpy("device_status", np.uint32)[0])
-    if status:
-        raise SystemExit(f"device status {status}: kernel reported a failure")
+    if db is not None:
+        status = int(db.out_numpy("device_status", np.uint32)[0])
+        if status:
+            raise SystemExit(f"device status {status}: kernel reported a failure")
+    units = torch.tensor([float(n_units)], dtype=torch.float64, device="cuda")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        dist.all_reduce(units, op=dist.ReduceOp.SUM)
+    total_units = float(units.item())
 
-    if args.workload == "url":
-        b_alg = algorithmic_bytes_url(gen, db, n_spans)
-    elif args.workload == "fused":
-        b_alg = algorithmic_bytes_fused(gen, db, n_spans, cfg)
-    else:
-        b_alg = algorithmic_bytes_sampling(gen, db, n_spans, cfg)
-    knames = wl["kernels"]
     per_k = {}
-    for kn in knames:
+    for kn in wl["kernels"]:
         k = prof.get(kn, {"launches": 0, "ms": 0.0})
-        per_k[kn] = k["ms"] / max(k["launches"], 1)
+        per_k[kn] = k["ms"] / max(args.steps, 1)   # device ms per step (gated kernels: 0 when not launched)
     k_ms = sum(per_k.values())
-    kname = "+".join(knames)
-    achieved = b_alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
+    kname = "+".join(wl["kernels"])
+    if args.workload == "owner":
+        b_alg = None
+        achieved = 0.0
+    else:
+        b_alg = algorithmic_bytes(wl, gen, db, n_units, cfg)
+        achieved = b_alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
 
     traffic = None
     tj = Path(args.traffic_json)
@@ -342,15 +428,14 @@ def main():
         try:
             d = json.loads(tj.read_text())
             ent = d.get(args.workload, {}).get(kname)
-            if ent and ent.get("spans") == n_spans:
+            if ent and ent.get("spans") == n_units:
                 traffic = ent["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
 
-    total_spans = n_spans * world * args.steps
-    value = total_spans / elapsed
+    value = total_units * args.steps / elapsed
     out = {
-        "metric": "spans/sec processed (whole node) at 1/2/4/8 MI355X; % of HBM roofline",
+        "metric": METRIC,
         "value": value,
         "unit": "spans/s",
         "n_gpus": world,
@@ -358,29 +443,32 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if wl["per_gpu"] else "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded generator, SURVEY.md §8d mix)",
-        "config": {"workload": wl["metric_config"], "spans_per_gpu": n_spans, "seed": wl["seed"],
-                   "processors": list(cfg.keys()),
-                   "parallelism": (f"dp{world}: trace-id all-to-all (RCCL) of sampling records, local templating/size"
+        "config": {"workload": wl["metric_config"], "spans_per_gpu": n_units, "spans_total": int(total_units),
+                   "seed": wl["seed"], "processors": list(cfg.keys()),
+                   "parallelism": (f"dp{world}: trace-id all-to-all (RCCL) of sampling partials, local templating/size"
                                    if world > 1 and stages & native.STAGE_SAMPLE else
-                                   f"dp{world}: independent span shards, no data-path collective")},
+                                   f"dp{world}: independent span shards, no data-path collective"), **extra},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kname, "kernel_ms": k_ms, "kernel_ms_each": per_k,
                      "algorithmic_bytes_per_launch": b_alg},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        fn = {"url": cpu_baseline_url, "sampling": cpu_baseline_sampling, "zipf": cpu_baseline_sampling,
-              "fused": cpu_baseline_fused}[args.workload]
-        mt, st, sample, parity = fn(gen, cfg, threads, calls=args.steps + args.warmup)
-        out["cpu_baseline"] = {"value": mt, "unit": "spans/s", "cores": threads, "kind": "port",
-                               "sample": sample, "value_1core": st}
-        # the CPU pass doubles as a parity spot-check of the timed GPU output
-        out["parity_vs_oracle"] = bool(parity(db))
+    if rank == 0 and world == 1 and args.workload != "owner":
+        orc = native_oracle()
+        if not args.no_cpu_baseline:
+            mt, st1, sample = cpu_baseline(wl, cfg, stages, share)
+            out["cpu_baseline"] = {"value": mt, "unit": "spans/s", "cores": share, "kind": "port", "sample": sample,
+                                   "value_1core": st1, "nproc": nproc, "cpu_model": model,
+                                   "build": orc or "in-tree liboracle.so (-O3 -march=x86-64-v2)"}
+        if not args.no_parity:
+            # the oracle on the whole timed batch checks the GPU output
+            par = parity_full(wl, gen, db, cfg, stages, share, args.steps + args.warmup)
+            out["parity_vs_oracle"] = all(par.values())
+            out["parity"] = par
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

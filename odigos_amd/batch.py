@@ -36,6 +36,12 @@ def _count(cols, dim: str) -> int:
             "attrset": cols.n_attrsets, "one": 1}[dim]
 
 
+def default_tmpl_cap(cols) -> int:
+    """Output arena capacity: every template fits in 2x the input bytes plus
+    16 per span, capped at the 32-bit offset range of ose_strref."""
+    return min(int(2 * cols.arena_bytes + 16 * cols.n_spans + 4096), 0xFFFFFFF0)
+
+
 def host_array(ptr: int, nbytes: int) -> np.ndarray:
     if nbytes == 0 or not ptr:
         return np.zeros(0, dtype=np.uint8)
@@ -47,16 +53,27 @@ class Generator:
     LIB = Path(__file__).resolve().parent / "_lib" / "libosegen.so"
     _L = None
 
-    def __init__(self, workload: str, seed: int, n_spans: int, threads: int = 8, shuffle: bool = False):
+    def __init__(self, workload: str, seed: int, n_spans: int, threads: int = 8, shuffle: bool = False,
+                 rank: int | None = None, world: int | None = None):
+        """world given: split mode, the batch node-collector source `rank` of
+        `world` holds of a global batch of n_spans spans (gen_batch.cpp)."""
         if Generator._L is None:
             L = C.CDLL(str(self.LIB))
             L.osegen_create.restype = C.c_void_p
             L.osegen_create.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int]
+            L.osegen_create_split.restype = C.c_void_p
+            L.osegen_create_split.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32]
             L.osegen_columns.restype = C.POINTER(native.Columns)
             L.osegen_columns.argtypes = [C.c_void_p]
             L.osegen_free.argtypes = [C.c_void_p]
             Generator._L = L
-        self.h = Generator._L.osegen_create(workload.encode(), seed, n_spans, threads, int(shuffle))
+        if world is None:
+            self.h = Generator._L.osegen_create(workload.encode(), seed, n_spans, threads, int(shuffle))
+        else:
+            assert not shuffle and 0 <= (rank or 0) < world
+            self.h = Generator._L.osegen_create_split(workload.encode(), seed, n_spans, threads, rank or 0, world)
+        if not self.h:
+            raise ValueError("osegen: bad arguments")
         self.cols = Generator._L.osegen_columns(self.h).contents
         self.workload = workload
 
@@ -83,7 +100,7 @@ class HostOutputs:
             a = np.zeros(max(_count(cols, dim) * size, 16), dtype=np.uint8)
             self.bufs[name] = a
             setattr(self.outs, name, a.ctypes.data)
-        cap = tmpl_cap if tmpl_cap is not None else int(2 * cols.arena_bytes + 16 * cols.n_spans + 4096)
+        cap = tmpl_cap if tmpl_cap is not None else default_tmpl_cap(cols)
         self.bufs["tmpl_arena"] = np.zeros(cap + 16, dtype=np.uint8)
         self.outs.tmpl_arena = self.bufs["tmpl_arena"].ctypes.data
         self.outs.tmpl_arena_cap = cap
@@ -123,15 +140,19 @@ class DeviceBatch:
             t = torch.zeros(n + 16, dtype=torch.uint8, device=device)
             self.o[name] = t
             setattr(self.outs, name, t.data_ptr())
-        cap = tmpl_cap if tmpl_cap is not None else int(2 * host_cols.arena_bytes + 16 * host_cols.n_spans + 4096)
+        cap = tmpl_cap if tmpl_cap is not None else default_tmpl_cap(host_cols)
         self.o["tmpl_arena"] = torch.zeros(cap + 16, dtype=torch.uint8, device=device)
         self.outs.tmpl_arena = self.o["tmpl_arena"].data_ptr()
         self.outs.tmpl_arena_cap = cap
         self.o["used"] = torch.zeros(2, dtype=torch.int64, device=device)
         self.outs.tmpl_arena_used = self.o["used"].data_ptr()
 
-    def out_numpy(self, name: str, dtype=np.uint8) -> np.ndarray:
-        return self.o[name].cpu().numpy().view(dtype)
+    def out_numpy(self, name: str, dtype=np.uint8, n: int | None = None) -> np.ndarray:
+        """Host copy of an output (the first n elements of dtype, or all)."""
+        t = self.o[name]
+        if n is not None:
+            t = t[: n * np.dtype(dtype).itemsize]
+        return t.cpu().numpy().view(dtype)
 
     def used(self) -> int:
         return int(self.o["used"][0].item())

@@ -11,9 +11,20 @@
 //            clipped to [1 us, 60 s]), http.route on 50 % of server spans
 //            from 200 routes.
 //   fused    C4: both mixes on every span.
-//   zipf     C5: trace sizes Zipf(1.1) truncated to [1, 50000].
+//   zipf     C5: trace sizes Zipf(1.1) truncated to [1, 50000], plus the
+//            high-cardinality half: http.route from 1M distinct routes and
+//            paths carrying 64-bit user ids.
 // Spans are grouped by trace (groupbytrace release order) unless shuffle=1,
 // which permutes whole resources across the batch.
+//
+// Split mode (osegen_create_split): the batch one of `world` node collectors
+// holds.  Trace structure (id, size, timing, services) is shared by every
+// source; each ResourceSpans (one (trace, service) group) lands on the
+// source hash(trace, resource) mod world, as spans of one trace reach the
+// gateway through the node collectors of the services that emitted them
+// (autoscaler/controllers/nodecollector/collectorconfig/traces.go:26-84).
+// Concatenating the sources in rank order gives the same resources as the
+// world = 1 batch of the same seed.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -62,7 +73,7 @@ constexpr int kNWords = sizeof(kWords) / sizeof(kWords[0]);
 const char* kMethods[] = {"GET", "POST", "PUT", "DELETE", "PATCH", "HEAD", "OPTIONS"};
 
 struct Mix {
-  bool url = true, sampling = false, zipf = false;
+  bool url = true, sampling = false, zipf = false, hicard = false;
   double p_route = 0.10;     // server spans carrying http.route already
 };
 
@@ -155,8 +166,12 @@ ose_strref add(std::string& arena, const std::string& s) {
 }
 
 // One trace (sampling/fused/zipf) or a run of independent spans (url).
-void gen_chunk(uint64_t seed, uint64_t n_spans, const Mix& mx, Chunk& c) {
+// world == 0: classic batch; world >= 1: split mode, only the resources of
+// source `rank` are emitted (their span contents come from a per-resource
+// generator, so a skipped resource costs no draws)
+void gen_chunk(uint64_t seed, uint64_t n_spans, const Mix& mx, Chunk& c, uint32_t rank = 0, uint32_t world = 0) {
   Rng r(seed);
+  uint64_t trace_no = 0;
   std::string tmp;
   uint64_t made = 0;
   while (made < n_spans) {
@@ -182,69 +197,83 @@ void gen_chunk(uint64_t seed, uint64_t n_spans, const Mix& mx, Chunk& c) {
     uint64_t trace_dur = (uint64_t)(dur_ms * 1e6);
     // split the spans over the trace's services (one resource each)
     uint64_t left = tsz;
+    trace_no++;
     for (uint32_t sv = 0; sv < nsvc; sv++) {
       uint64_t k = sv == nsvc - 1 ? left : 1 + r.below((uint32_t)std::min<uint64_t>(left - (nsvc - 1 - sv), 1u << 30)) ;
       if (k > left - (nsvc - 1 - sv)) k = left - (nsvc - 1 - sv);
       left -= k;
-      uint32_t svc = r.below(64);
+      Rng rres(seed ^ (trace_no * 0xD1B54A32D192ED03ull) ^ ((uint64_t)(sv + 1) * 0x8CB92BA72F3D8DD7ull));
+      if (world) {
+        uint64_t h = hi ^ (0x9E3779B97F4A7C15ull * (sv + 1));
+        if ((uint32_t)(Rng::sm(h) % world) != rank) continue;
+      }
+      Rng& q_r = world ? rres : r;   // the resource's span contents
+      uint32_t svc = q_r.below(64);
       uint32_t res = (uint32_t)c.res_svc.size();
       c.res_svc.push_back(svc);
-      c.res_svc_str.push_back(r.chance(0.02) ? OSE_NONE : svc);   // 2 % service.name not a Str
-      c.res_url_ok.push_back(r.chance(0.97) ? 1 : 0);
-      c.res_attrset.push_back(svc * 4 + r.below(4));
-      c.res_size.push_back(180 + r.below(240));
-      c.scope_size.push_back(20 + r.below(40));
+      c.res_svc_str.push_back(q_r.chance(0.02) ? OSE_NONE : svc);   // 2 % service.name not a Str
+      c.res_url_ok.push_back(q_r.chance(0.97) ? 1 : 0);
+      c.res_attrset.push_back(svc * 4 + q_r.below(4));
+      c.res_size.push_back(180 + q_r.below(240));
+      c.scope_size.push_back(20 + q_r.below(40));
       c.res_first_span.push_back((uint32_t)c.kind.size());
       for (uint64_t q = 0; q < k; q++) {
         c.trace_id.push_back(hi);
         c.trace_id.push_back(lo);
-        uint64_t off = trace_dur ? r.next() % (trace_dur + 1) : 0;
+        uint64_t off = trace_dur ? q_r.next() % (trace_dur + 1) : 0;
         uint64_t st = base + off;
-        uint64_t en = st + (trace_dur - off) * (uint64_t)r.below(1000) / 1000;
+        uint64_t en = st + (trace_dur - off) * (uint64_t)q_r.below(1000) / 1000;
         c.start.push_back(st);
         c.end.push_back(en);
-        c.status.push_back(r.chance(0.02) ? OSE_STATUS_ERROR : (r.chance(0.5) ? OSE_STATUS_OK : OSE_STATUS_UNSET));
-        uint32_t kp = r.below(100);
+        c.status.push_back(q_r.chance(0.02) ? OSE_STATUS_ERROR : (q_r.chance(0.5) ? OSE_STATUS_OK : OSE_STATUS_UNSET));
+        uint32_t kp = q_r.below(100);
         uint8_t kind = kp < 45 ? OSE_KIND_SERVER : (kp < 80 ? OSE_KIND_CLIENT : OSE_KIND_INTERNAL);
         c.kind.push_back(kind);
         c.res_local.push_back(res);
         uint8_t f = 0;
         ose_strref pref{0, 0}, rref{0, 0};
-        const char* method = kMethods[r.below(3) ? r.below(2) : r.below(7)];
-        bool http = (kind == OSE_KIND_SERVER || kind == OSE_KIND_CLIENT) && r.chance(0.8);
-        bool has_route = kind == OSE_KIND_SERVER && r.chance(mx.p_route);
+        const char* method = kMethods[q_r.below(3) ? q_r.below(2) : q_r.below(7)];
+        bool http = (kind == OSE_KIND_SERVER || kind == OSE_KIND_CLIENT) && q_r.chance(0.8);
+        bool has_route = kind == OSE_KIND_SERVER && q_r.chance(mx.p_route);
         uint32_t nl;
         if (http) {
           f |= OSE_URL_HAS_METHOD;
-          bool eq = r.chance(0.7);
+          bool eq = q_r.chance(0.7);
           if (eq) f |= OSE_URL_NAME_EQ_METHOD;
-          nl = eq ? (uint32_t)std::strlen(method) : 8 + r.below(32);
+          nl = eq ? (uint32_t)std::strlen(method) : 8 + q_r.below(32);
           if (has_route) {
-            f |= r.chance(0.01) ? OSE_URL_TGT_STR_EMPTY : OSE_URL_TGT_STR;
-          } else if (kind == OSE_KIND_CLIENT && r.chance(0.05)) {
+            f |= q_r.chance(0.01) ? OSE_URL_TGT_STR_EMPTY : OSE_URL_TGT_STR;
+          } else if (kind == OSE_KIND_CLIENT && q_r.chance(0.05)) {
             f |= OSE_URL_TGT_STR;
           }
-          uint32_t src = r.below(100);
+          uint32_t src = q_r.below(100);
           tmp.clear();
-          gen_path(r, tmp);
+          if (mx.hicard && q_r.chance(0.5)) {
+            // C5 high-cardinality paths: 64-bit user ids (\\d{7,} -> {id})
+            tmp += "/users/"; tmp += std::to_string(q_r.next()); tmp += '/'; gen_word(q_r, tmp);
+            if (q_r.chance(0.5)) { tmp += "/"; tmp += std::to_string(q_r.next() >> q_r.below(40)); }
+          } else {
+            gen_path(q_r, tmp);
+          }
           if (src < 75) {
             f |= OSE_URL_PATH_RAW;
             pref = add(c.arena, tmp);
           } else if (src < 97) {
             f |= OSE_URL_PATH_TARGET;
-            if (r.chance(0.5)) { tmp += "?id="; gen_digits(r, tmp, 6); tmp += "&q=a/b"; }
+            if (q_r.chance(0.5)) { tmp += "?id="; gen_digits(q_r, tmp, 6); tmp += "&q=a/b"; }
             pref = add(c.arena, tmp);
           }   // else: no path source
         } else {
-          nl = 8 + r.below(32);
+          nl = 8 + q_r.below(32);
         }
         if (has_route) {
-          // 200 routes: /api/v{1,2}/<word>[/{id}]...
-          uint32_t rid = r.below(200);
+          // 200 routes: /api/v{1,2}/<word>[/{id}]...; C5: 1M distinct routes
+          uint32_t rid = q_r.below(mx.hicard ? 1000000 : 200);
           tmp.clear();
           tmp += "/api/v"; tmp += (char)('1' + rid % 2); tmp += '/'; tmp += kWords[rid % kNWords];
           if (rid % 3 == 0) tmp += "/{id}";
           if (rid % 5 == 0) { tmp += '/'; tmp += kWords[(rid / 7) % kNWords]; }
+          if (mx.hicard) { tmp += "/r"; tmp += std::to_string(rid); }
           // http.route "" (TGT_STR_EMPTY) is an empty route string for sampling
           if ((f & OSE_URL_TGT_MASK) != OSE_URL_TGT_STR_EMPTY) rref = add(c.arena, tmp);
         }
@@ -252,7 +281,7 @@ void gen_chunk(uint64_t seed, uint64_t n_spans, const Mix& mx, Chunk& c) {
         c.path.push_back(pref);
         c.route.push_back(rref);
         c.name_len.push_back(nl);
-        c.span_size.push_back(120 + pref.len + rref.len + nl + r.below(200));
+        c.span_size.push_back(120 + pref.len + rref.len + nl + q_r.below(200));
       }
     }
     made += tsz;
@@ -267,22 +296,86 @@ struct Gen {
   std::vector<uint32_t> resource, scope, span_size, name_len, res_svc, res_svc_str, res_attrset, res_size, scope_size,
       scope_resource;
   std::vector<ose_strref> path, route;
+  uint64_t arena_used = 0;
 };
 
 template <typename T>
 void append(std::vector<T>& dst, const std::vector<T>& src) { dst.insert(dst.end(), src.begin(), src.end()); }
 
-}  // namespace
 
-extern "C" {
-
-// workload: "url" | "sampling" | "fused" | "zipf"
-void* osegen_create(const char* workload, uint64_t seed, uint64_t n_spans, int threads, int shuffle) {
+Mix mix_of(const char* workload) {
   Mix mx;
   std::string w = workload ? workload : "url";
   if (w == "sampling") { mx.url = false; mx.sampling = true; mx.p_route = 0.5; }
   else if (w == "fused") { mx.sampling = true; mx.p_route = 0.5; }
-  else if (w == "zipf") { mx.sampling = true; mx.zipf = true; mx.p_route = 0.5; }
+  else if (w == "zipf") { mx.sampling = true; mx.zipf = true; mx.hicard = true; mx.p_route = 0.5; }
+  return mx;
+}
+
+// Concatenates the chunks in order (threads copy whole chunks: each chunk's
+// arena is already in span order, path then route per span).
+void assemble_ordered(Gen* g, std::vector<Chunk>& chunks, int threads) {
+  const size_t K = chunks.size();
+  std::vector<uint64_t> s0(K + 1, 0), r0(K + 1, 0), a0(K + 1, 0);
+  for (size_t k = 0; k < K; k++) {
+    s0[k + 1] = s0[k] + chunks[k].kind.size();
+    r0[k + 1] = r0[k] + chunks[k].res_svc.size();
+    a0[k + 1] = a0[k] + chunks[k].arena.size();
+  }
+  const uint64_t n = s0[K], R = r0[K];
+  g->arena.assign(((a0[K] + 15) / 16) * 16 + 64, 0);
+  g->trace_id.resize(2 * n);
+  for (auto* v : {&g->start, &g->end}) v->resize(n);
+  for (auto* v : {&g->status, &g->kind, &g->url_flags}) v->resize(n);
+  for (auto* v : {&g->resource, &g->scope, &g->span_size, &g->name_len}) v->resize(n);
+  g->path.resize(n);
+  g->route.resize(n);
+  for (auto* v : {&g->res_svc, &g->res_svc_str, &g->res_attrset, &g->res_size, &g->scope_size, &g->scope_resource})
+    v->resize(R);
+  g->res_url_ok.resize(R);
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&, t] {
+      for (size_t k = (size_t)t; k < K; k += (size_t)threads) {
+        Chunk& c = chunks[k];
+        const uint64_t sb = s0[k], rb = r0[k], ab = a0[k];
+        std::memcpy(g->arena.data() + ab, c.arena.data(), c.arena.size());
+        const size_t m = c.kind.size(), rr = c.res_svc.size();
+        std::memcpy(&g->trace_id[2 * sb], c.trace_id.data(), 16 * m);
+        std::memcpy(&g->start[sb], c.start.data(), 8 * m);
+        std::memcpy(&g->end[sb], c.end.data(), 8 * m);
+        std::memcpy(&g->status[sb], c.status.data(), m);
+        std::memcpy(&g->kind[sb], c.kind.data(), m);
+        std::memcpy(&g->url_flags[sb], c.url_flags.data(), m);
+        std::memcpy(&g->span_size[sb], c.span_size.data(), 4 * m);
+        std::memcpy(&g->name_len[sb], c.name_len.data(), 4 * m);
+        for (size_t i = 0; i < m; i++) {
+          const uint32_t res = (uint32_t)(rb + c.res_local[i]);
+          g->resource[sb + i] = res;
+          g->scope[sb + i] = res;   // one ScopeSpans per ResourceSpans
+          ose_strref p = c.path[i], q = c.route[i];
+          g->path[sb + i] = p.len ? ose_strref{(uint32_t)(ab + p.off), p.len} : ose_strref{0, 0};
+          g->route[sb + i] = q.len ? ose_strref{(uint32_t)(ab + q.off), q.len} : ose_strref{0, 0};
+        }
+        for (size_t r = 0; r < rr; r++) {
+          g->res_svc[rb + r] = c.res_svc[r];
+          g->res_svc_str[rb + r] = c.res_svc_str[r];
+          g->res_url_ok[rb + r] = c.res_url_ok[r];
+          g->res_attrset[rb + r] = c.res_attrset[r];
+          g->res_size[rb + r] = c.res_size[r];
+          g->scope_size[rb + r] = c.scope_size[r];
+          g->scope_resource[rb + r] = (uint32_t)(rb + r);
+        }
+        Chunk().arena.swap(c.arena);   // free as we go
+      }
+    });
+  for (auto& x : th) x.join();
+  g->arena_used = a0[K];
+}
+
+void* create(const char* workload, uint64_t seed, uint64_t n_spans, int threads, int shuffle, uint32_t rank,
+             uint32_t world) {
+  Mix mx = mix_of(workload);
   if (threads < 1) threads = 1;
   const uint64_t kChunk = 1 << 16;
   uint64_t nchunks = (n_spans + kChunk - 1) / kChunk;
@@ -292,16 +385,20 @@ void* osegen_create(const char* workload, uint64_t seed, uint64_t n_spans, int t
     th.emplace_back([&, t] {
       for (uint64_t k = (uint64_t)t; k < nchunks; k += (uint64_t)threads) {
         uint64_t s = seed ^ (0x9E3779B97F4A7C15ull * (k + 1));
-        gen_chunk(s, std::min(kChunk, n_spans - k * kChunk), mx, chunks[k]);
+        gen_chunk(s, std::min(kChunk, n_spans - k * kChunk), mx, chunks[k], rank, world);
       }
     });
   for (auto& x : th) x.join();
   auto* g = new Gen();
+  if (!shuffle) {
+    assemble_ordered(g, chunks, threads);
+    return g;
+  }
   // resource permutation (shuffle) keeps each resource's spans contiguous
   std::vector<std::pair<uint64_t, uint32_t>> order;   // (chunk, local resource)
   for (uint64_t k = 0; k < nchunks; k++)
     for (uint32_t r = 0; r < chunks[k].res_svc.size(); r++) order.emplace_back(k, r);
-  if (shuffle) {
+  {
     Rng rr(seed ^ 0x5A5A5A5A5A5A5A5Aull);
     for (size_t i = order.size(); i > 1; i--) std::swap(order[i - 1], order[rr.below((uint32_t)i)]);
   }
@@ -347,7 +444,12 @@ void* osegen_create(const char* workload, uint64_t seed, uint64_t n_spans, int t
       g->route.push_back(nq);
     }
   }
-  uint64_t abytes = g->arena.size();
+  g->arena_used = g->arena.size();
+  return g;
+}
+
+void* finish(Gen* g) {
+  const uint64_t abytes = g->arena_used;
   g->arena.resize(((abytes + 15) / 16) * 16 + 64, 0);
   ose_columns& c = g->cols;
   c.n_spans = g->kind.size();
@@ -376,6 +478,24 @@ void* osegen_create(const char* workload, uint64_t seed, uint64_t n_spans, int t
   c.scope_size = g->scope_size.data();
   c.scope_resource = g->scope_resource.data();
   return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+// workload: "url" | "sampling" | "fused" | "zipf"
+void* osegen_create(const char* workload, uint64_t seed, uint64_t n_spans, int threads, int shuffle) {
+  return finish(static_cast<Gen*>(create(workload, seed, n_spans, threads, shuffle, 0, 0)));
+}
+
+// The batch source `rank` of `world` holds when a global batch of n_spans
+// spans (same seed) reaches the gateway through `world` node collectors
+// (split mode above); world = 1 is the whole global batch.
+void* osegen_create_split(const char* workload, uint64_t seed, uint64_t n_spans, int threads, uint32_t rank,
+                          uint32_t world) {
+  if (world < 1 || rank >= world) return nullptr;
+  return finish(static_cast<Gen*>(create(workload, seed, n_spans, threads, 0, rank, world)));
 }
 
 const ose_columns* osegen_columns(void* g) { return &static_cast<Gen*>(g)->cols; }

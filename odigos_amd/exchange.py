@@ -69,6 +69,24 @@ class DeviceExchange:
         self._recv_cap = 0
         self._x = None
 
+    @classmethod
+    def receiver(cls, engine, rec_bytes, stream=None):
+        """Owner-side ops only (unpack_sample), for a batch of records that
+        arrived without a local source batch (bench.py's owner workload)."""
+        import torch
+        self = cls.__new__(cls)
+        self.torch = torch
+        self.eng, self.db = engine, None
+        self.L = native.lib()
+        self.stream = stream
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        self.n = 0
+        self.rec_bytes = rec_bytes
+        self.counts = None
+        self._recv_cap = 0
+        self._x = None
+        return self
+
     def _s(self):
         return None if self.stream is None else C.c_void_p(self.stream)
 

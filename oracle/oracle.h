@@ -103,6 +103,11 @@ double orc_trace_uniform(uint64_t hi, uint64_t lo, uint64_t seed);
  * the surviving span count to *o->accepted_spans. */
 int orc_size_process(const ose_columns* c, const ose_outputs* res, uint32_t stages, uint32_t group_mode,
                      ose_outputs* o, int64_t inverse, double sampling_ratio, double traffic_u);
+/* the same with up to ORC_MAX_THREADS pthreads (spans, scopes and resources
+ * cut at scope / resource boundaries; per-thread attribute-set sums) */
+#define ORC_MAX_THREADS 256
+int orc_size_process_mt(const ose_columns* c, const ose_outputs* res, uint32_t stages, uint32_t group_mode,
+                        ose_outputs* o, int64_t inverse, double sampling_ratio, double traffic_u, int nthreads);
 /* wire size of a Span body after the odigosurltemplate mutation of span i */
 uint64_t orc_span_size_after(const ose_columns* c, const ose_outputs* res, uint32_t stages, uint64_t i);
 

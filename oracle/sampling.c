@@ -252,48 +252,207 @@ static void* run_traces(void* arg) {
   return NULL;
 }
 
+/* Grouping by trace_id in first-appearance order, threaded: spans are
+ * partitioned by trace hash (stable, batch order inside a partition), each
+ * partition groups its spans with a private table, and a trace's global
+ * index is the rank of its first span among all first spans. */
+typedef struct {
+  const ose_columns* c;
+  uint64_t lo, hi;            /* span range (passes 1, 2, 4) */
+  uint32_t part, nparts;      /* partition (pass 3, 5) */
+  uint64_t* counts;           /* [nparts] spans per partition in this range */
+  uint64_t* offs;             /* [nparts] scatter cursors */
+  uint32_t* part_spans;
+  const uint64_t* part_first; /* [nparts + 1] */
+  uint8_t* is_first;
+  uint32_t* trace_local;      /* local trace id per span (pass 3) -> global (pass 5) */
+  uint64_t nfirst;            /* pass 4: first spans in the range; then the range's base */
+  uint32_t* rank_first;       /* global trace index at each first span */
+  uint32_t* first;            /* [ntr + 1] offsets (pass 5 counts, pass 6 fill) */
+  uint32_t* members;
+  uint32_t* local_first;      /* pass 3: local trace -> first span (per partition, in part_spans space) */
+} group_job;
+
+static uint32_t part_of(uint64_t hi, uint64_t lo, uint32_t nparts) {
+  return (uint32_t)((mix(hi, lo) >> 40) % nparts);
+}
+static void* g_count(void* p) {
+  group_job* j = (group_job*)p;
+  for (uint64_t i = j->lo; i < j->hi; i++)
+    j->counts[part_of(j->c->trace_id[2 * i], j->c->trace_id[2 * i + 1], j->nparts)]++;
+  return NULL;
+}
+static void* g_scatter(void* p) {
+  group_job* j = (group_job*)p;
+  for (uint64_t i = j->lo; i < j->hi; i++)
+    j->part_spans[j->offs[part_of(j->c->trace_id[2 * i], j->c->trace_id[2 * i + 1], j->nparts)]++] = (uint32_t)i;
+  return NULL;
+}
+static void* g_local(void* p) {   /* private table over one partition, batch order */
+  group_job* j = (group_job*)p;
+  const uint64_t a = j->part_first[j->part], b = j->part_first[j->part + 1], m = b - a;
+  uint64_t cap = 16;
+  while (cap < 2 * m) cap <<= 1;
+  slot_t* tab = (slot_t*)calloc(cap, sizeof(slot_t));
+  uint32_t nt = 0;
+  for (uint64_t k = a; k < b; k++) {
+    const uint32_t i = j->part_spans[k];
+    const uint64_t hi = j->c->trace_id[2 * (uint64_t)i], lo = j->c->trace_id[2 * (uint64_t)i + 1];
+    uint64_t h = mix(hi, lo) & (cap - 1);
+    for (;;) {
+      slot_t* e = &tab[h];
+      if (!e->used) {
+        e->used = 1;
+        e->hi = hi;
+        e->lo = lo;
+        e->trace = nt++;
+        j->is_first[i] = 1;
+        j->trace_local[i] = e->trace;
+        break;
+      }
+      if (e->hi == hi && e->lo == lo) {
+        j->trace_local[i] = e->trace;
+        break;
+      }
+      h = (h + 1) & (cap - 1);
+    }
+  }
+  free(tab);
+  /* local trace -> its first span (first occurrences are in batch order) */
+  j->local_first = (uint32_t*)malloc((nt ? nt : 1) * sizeof(uint32_t));
+  for (uint64_t k = a; k < b; k++) {
+    const uint32_t i = j->part_spans[k];
+    if (j->is_first[i]) j->local_first[j->trace_local[i]] = i;
+  }
+  j->nfirst = nt;
+  return NULL;
+}
+static void* g_rank_count(void* p) {
+  group_job* j = (group_job*)p;
+  uint64_t c = 0;
+  for (uint64_t i = j->lo; i < j->hi; i++) c += j->is_first[i];
+  j->nfirst = c;
+  return NULL;
+}
+static void* g_rank_fill(void* p) {
+  group_job* j = (group_job*)p;
+  uint64_t r = j->nfirst;
+  for (uint64_t i = j->lo; i < j->hi; i++)
+    if (j->is_first[i]) j->rank_first[i] = (uint32_t)r++;
+  return NULL;
+}
+static void* g_globalize(void* p) {   /* per partition: global trace ids, span counts per trace */
+  group_job* j = (group_job*)p;
+  const uint64_t a = j->part_first[j->part], b = j->part_first[j->part + 1];
+  for (uint64_t k = a; k < b; k++) {
+    const uint32_t i = j->part_spans[k];
+    const uint32_t g = j->rank_first[j->local_first[j->trace_local[i]]];
+    j->trace_local[i] = g;
+    j->first[g + 1]++;
+  }
+  free(j->local_first);
+  return NULL;
+}
+static void* g_members(void* p) {   /* per partition: members in batch order (traces are disjoint) */
+  group_job* j = (group_job*)p;
+  const uint64_t a = j->part_first[j->part], b = j->part_first[j->part + 1];
+  for (uint64_t k = a; k < b; k++) {
+    const uint32_t i = j->part_spans[k];
+    j->members[j->first[j->trace_local[i]]++] = i;   /* `first` holds fill cursors here */
+  }
+  return NULL;
+}
+static void run_group(void* (*fn)(void*), group_job* jobs, int T) {
+  pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+  for (int t = 1; t < T; t++) pthread_create(&th[t], NULL, fn, &jobs[t]);
+  fn(&jobs[0]);
+  for (int t = 1; t < T; t++) pthread_join(th[t], NULL);
+  free(th);
+}
+
+/* trace_of[i] = trace index (first-appearance order); first[] = offsets of
+ * each trace in members[] (spans in batch order); returns the trace count */
+static uint32_t group_traces(const ose_columns* c, int T, uint32_t* trace_of, uint32_t** first_out,
+                             uint32_t** members_out) {
+  const uint64_t n = c->n_spans;
+  if (T < 1) T = 1;
+  if (T > ORC_MAX_THREADS) T = ORC_MAX_THREADS;
+  if (n < (uint64_t)T * 4096) T = 1;
+  group_job* jobs = (group_job*)calloc((size_t)T, sizeof(group_job));
+  uint64_t* counts = (uint64_t*)calloc((size_t)T * T, sizeof(uint64_t));
+  uint32_t* part_spans = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+  uint64_t* part_first = (uint64_t*)calloc((size_t)T + 1, sizeof(uint64_t));
+  uint8_t* is_first = (uint8_t*)calloc(n ? n : 1, 1);
+  uint32_t* rank_first = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+  for (int t = 0; t < T; t++) {
+    group_job* j = &jobs[t];
+    j->c = c;
+    j->lo = n * (uint64_t)t / (uint64_t)T;
+    j->hi = n * (uint64_t)(t + 1) / (uint64_t)T;
+    j->part = (uint32_t)t;
+    j->nparts = (uint32_t)T;
+    j->counts = counts + (size_t)t * T;
+    j->offs = j->counts;
+    j->part_spans = part_spans;
+    j->part_first = part_first;
+    j->is_first = is_first;
+    j->trace_local = trace_of;
+    j->rank_first = rank_first;
+  }
+  run_group(g_count, jobs, T);
+  /* cursor of range t in partition p = partition start + counts of earlier ranges */
+  uint64_t acc = 0;
+  for (int p = 0; p < T; p++) {
+    part_first[p] = acc;
+    for (int t = 0; t < T; t++) {
+      const uint64_t k = counts[(size_t)t * T + p];
+      counts[(size_t)t * T + p] = acc;
+      acc += k;
+    }
+  }
+  part_first[T] = acc;
+  run_group(g_scatter, jobs, T);
+  run_group(g_local, jobs, T);
+  uint64_t local_tr[ORC_MAX_THREADS];
+  uint64_t ntr = 0;
+  for (int t = 0; t < T; t++) { local_tr[t] = jobs[t].nfirst; ntr += jobs[t].nfirst; }
+  run_group(g_rank_count, jobs, T);
+  uint64_t base = 0;
+  for (int t = 0; t < T; t++) { const uint64_t k = jobs[t].nfirst; jobs[t].nfirst = base; base += k; }
+  run_group(g_rank_fill, jobs, T);
+  uint32_t* first = (uint32_t*)calloc((size_t)ntr + 1, sizeof(uint32_t));
+  uint32_t* members = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+  for (int t = 0; t < T; t++) { jobs[t].first = first; jobs[t].members = members; jobs[t].nfirst = local_tr[t]; }
+  run_group(g_globalize, jobs, T);
+  for (uint64_t t = 0; t < ntr; t++) first[t + 1] += first[t];
+  uint32_t* fill = (uint32_t*)malloc(((size_t)ntr + 1) * sizeof(uint32_t));
+  memcpy(fill, first, ((size_t)ntr + 1) * sizeof(uint32_t));
+  for (int t = 0; t < T; t++) jobs[t].first = fill;
+  run_group(g_members, jobs, T);
+  free(fill);
+  free(jobs); free(counts); free(part_spans); free(part_first); free(is_first); free(rank_first);
+  *first_out = first;
+  *members_out = members;
+  return (uint32_t)ntr;
+}
+
 int orc_sampling_process(const orc_sampling* s, const ose_columns* c, ose_outputs* o, uint32_t group_mode,
                          const ose_rand* rnd, int nthreads) {
   const uint64_t n = c->n_spans;
   if (n > 0xFFFFFFFEull) return -1;
   uint32_t* trace_of = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
   uint32_t ntr = 0;
+  uint32_t* first;
+  uint32_t* members;
   if (group_mode == OSE_GROUP_BATCH) {
-    for (uint64_t i = 0; i < n; i++) trace_of[i] = 0;
     ntr = 1;
+    first = (uint32_t*)calloc(2, sizeof(uint32_t));
+    first[1] = (uint32_t)n;
+    members = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+    for (uint64_t i = 0; i < n; i++) { trace_of[i] = 0; members[i] = (uint32_t)i; }
   } else {
-    uint64_t cap = 16;
-    while (cap < 2 * n) cap <<= 1;
-    slot_t* tab = (slot_t*)calloc(cap, sizeof(slot_t));
-    for (uint64_t i = 0; i < n; i++) {
-      uint64_t hi = c->trace_id[2 * i], lo = c->trace_id[2 * i + 1];
-      uint64_t h = mix(hi, lo) & (cap - 1);
-      for (;;) {
-        slot_t* e = &tab[h];
-        if (!e->used) {
-          e->used = 1;
-          e->hi = hi;
-          e->lo = lo;
-          e->trace = ntr++;
-          trace_of[i] = e->trace;
-          break;
-        }
-        if (e->hi == hi && e->lo == lo) {
-          trace_of[i] = e->trace;
-          break;
-        }
-        h = (h + 1) & (cap - 1);
-      }
-    }
-    free(tab);
+    ntr = group_traces(c, nthreads, trace_of, &first, &members);
   }
-  uint32_t* first = (uint32_t*)calloc((size_t)ntr + 1, sizeof(uint32_t));
-  for (uint64_t i = 0; i < n; i++) first[trace_of[i] + 1]++;
-  for (uint32_t t = 0; t < ntr; t++) first[t + 1] += first[t];
-  uint32_t* fill = (uint32_t*)malloc(((size_t)ntr + 1) * sizeof(uint32_t));
-  memcpy(fill, first, ((size_t)ntr + 1) * sizeof(uint32_t));
-  uint32_t* members = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
-  for (uint64_t i = 0; i < n; i++) members[fill[trace_of[i]]++] = (uint32_t)i;
   uint8_t* tkeep = (uint8_t*)malloc(ntr ? ntr : 1);
 
   if (nthreads < 1) nthreads = 1;
@@ -321,7 +480,6 @@ int orc_sampling_process(const orc_sampling* s, const ose_columns* c, ose_output
   free(th);
   free(tkeep);
   free(members);
-  free(fill);
   free(first);
   free(trace_of);
   return 0;

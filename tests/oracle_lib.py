@@ -7,7 +7,12 @@ from pathlib import Path
 
 from odigos_amd import native
 
-ORACLE_PATH = Path(__file__).resolve().parent.parent / "oracle" / "liboracle.so"
+import os
+
+# OSE_ORACLE_LIB: a host-tuned build of the same sources (bench.py builds one
+# with -march=native on the GPU box for the CPU baseline)
+ORACLE_PATH = Path(os.environ.get("OSE_ORACLE_LIB") or
+                   Path(__file__).resolve().parent.parent / "oracle" / "liboracle.so")
 _p = C.c_void_p
 _L = None
 
@@ -38,6 +43,9 @@ def lib():
             "orc_trace_uniform": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64]),
             "orc_size_process": (C.c_int, [C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32, C.c_uint32,
                                            C.POINTER(native.Outputs), C.c_int64, C.c_double, C.c_double]),
+            "orc_size_process_mt": (C.c_int, [C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32,
+                                              C.c_uint32, C.POINTER(native.Outputs), C.c_int64, C.c_double, C.c_double,
+                                              C.c_int]),
         }
         for name, (res, args) in sig.items():
             try:
@@ -152,8 +160,8 @@ class SamplingOracle:
 
 
 def size_process(cols, res_outs, stages: int, group_mode: int, outs, inverse: int = 1, ratio: float = 1.0,
-                 traffic_u: float = 0.0) -> int:
+                 traffic_u: float = 0.0, nthreads: int = 1) -> int:
     """dataSizesMetricsProcessor.processTraces restated (oracle/size.c); res_outs
     holds the earlier stages' results (keep / trace_keep / url_out / tmpl)."""
-    return lib().orc_size_process(C.byref(cols), C.byref(res_outs), stages, group_mode, C.byref(outs), inverse,
-                                  ratio, traffic_u)
+    return lib().orc_size_process_mt(C.byref(cols), C.byref(res_outs), stages, group_mode, C.byref(outs), inverse,
+                                     ratio, traffic_u, nthreads)
