@@ -55,8 +55,7 @@ FUSED_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "re
 SAMPLE_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc", "res_svc_str")
 URL_KERNELS = ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel")
 TRACE_KERNELS = ("trace_eval_kernel", "trace_long_kernel")
-SLOW_KERNELS = ("trace_insert_exact_kernel", "trace_key_kernel", "sort_hist_kernel", "scan_u32_kernel",
-                "sort_scatter_kernel")
+SLOW_KERNELS = ("trace_sort_path",)   # the repeated-trace-id path, timed as one span of launches
 SIZE_KERNELS = ("size_span_kernel", "size_scope_kernel", "size_res_kernel")
 PER_TRACE_OUTS = ("trace_count", "trace_first_span", "trace_keep", "trace_level", "trace_ratio")
 
@@ -69,7 +68,7 @@ WORKLOADS = {
                 metric_config="C2: URL templatization only, 10M spans/GPU, C2 segment mix, default rules"),
     "sampling": dict(gen="sampling", seed=0x0D160003, spans=50_000_000, per_gpu=True,
                      cfg=None, stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
-                     fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS,
+                     fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
                      metric_config="C3: trace-level sampling (1 error + 4 service + 16 latency rules), "
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
     "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000, per_gpu=True,
@@ -86,7 +85,7 @@ WORKLOADS = {
                                 "at N>1)"),
     "owner": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False, sources=8,
                   cfg=None, stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
-                  fields=SAMPLE_FIELDS, kernels=("shard_unpack",) + TRACE_KERNELS + SLOW_KERNELS,
+                  fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
                   metric_config="C4 owner side on one GPU: the records trace owner 0 of 8 receives "
                                 "(8 source shards of the 100M-span C4 batch, rank order), unpack + SAMPLE"),
 }
@@ -366,17 +365,24 @@ def main():
         n_units = gen.cols.n_spans
         eng.reserve(n_units)
         if world > 1 and stages & native.STAGE_SAMPLE:
-            # route every span's sampling record to its trace's owner
-            # GPU (RCCL all-to-all), decide there, bring keep back, then template
-            # and size locally on the decisions
-            from odigos_amd.exchange import DeviceExchange, route_and_sample
-            ex = DeviceExchange(eng, db, stream=sh)
+            # fold each rank's spans into partial records, route them
+            # to each trace's owner GPU (RCCL over xGMI), decide there, bring keep
+            # back (one C-ABI call: ose_exchange_sample), then template and size
+            # locally on the decisions and sum the traffic counters over the node
+            from odigos_amd.exchange import NcclComm, NcclExchange
+            comm = NcclComm(rank, world)
+            nx = NcclExchange(eng, db, comm, stream=sh)
             local_st = (stages & ~native.STAGE_SAMPLE) | native.STAGE_APPLY_KEEP
+            A = gen.cols.n_attrsets
+            node_ctr = torch.zeros(A + 1, dtype=torch.int64, device="cuda")
 
             def step():
-                route_and_sample(ex, world)
+                nx.round()
                 if local_st & (native.STAGE_TEMPLATE | native.STAGE_SIZE):
                     eng.process_device(db, local_st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
+                if local_st & native.STAGE_SIZE:
+                    nx.allreduce_counters(db.outs.attrset_bytes, node_ctr.data_ptr(), A)
+                    nx.allreduce_counters(db.outs.accepted_spans, node_ctr.data_ptr() + 8 * A, 1)
         else:
             def step():
                 eng.process_device(db, stages, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
@@ -415,6 +421,13 @@ def main():
         per_k[kn] = k["ms"] / max(args.steps, 1)   # device ms per step (gated kernels: 0 when not launched)
     k_ms = sum(per_k.values())
     kname = "+".join(wl["kernels"])
+    if world > 1 and stages & native.STAGE_SAMPLE:
+        st_ = [int(x) for x in nx.stats]
+        extra.update({"exchange_records_sent": st_[0], "exchange_records_received": st_[1],
+                      "exchange_record_bytes_per_span": native.XREC_BYTES * st_[0] / max(st_[2], 1)})
+        out_kernels = dict(prof)
+        extra["exchange_kernels_ms"] = {k: v["ms"] / max(args.steps, 1) for k, v in out_kernels.items()
+                                        if k in ("shard_pack", "shard_unpack")}
     if args.workload == "owner":
         b_alg = None
         achieved = 0.0

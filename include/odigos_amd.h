@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define OSE_ABI_VERSION 1
+#define OSE_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------- */
 #define OSE_OK        0
@@ -169,6 +169,13 @@ typedef struct ose_columns {
   /* per scope */
   const uint32_t* scope_size;   /* ScopeSpans bytes excluding its spans fields */
   const uint32_t* scope_resource; /* index of the scope's ResourceSpans (non-decreasing) */
+
+  /* per span, optional (set by ose_shard_unpack on the trace's owner GPU):
+   * the OR of the service_name rule bits (servicename.go:35-51, by
+   * res_svc_str) and span_attribute rule bits (attr_match, shifted past the
+   * service rules) of the spans a partial record folds; when non-NULL the
+   * engine reads it instead of res_svc_str / attr_match                   */
+  const uint64_t* svc_match;
 } ose_columns;
 
 /* ---- results -----------------------------------------------------------
@@ -250,16 +257,21 @@ int ose_process(ose_engine* eng, ose_batch* b, uint32_t stage_mask,
 /* Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream):
  * columns/outputs are device pointers already resident in HBM.  This is the
  * entry point the benchmark times.  One exception to "asynchronous": with
- * SAMPLE | TEMPLATE and OSE_GROUP_TRACE_ID, the host waits (after queueing
- * the URL kernels) for SAMPLE's fast pass to finish, to queue the repeated-
- * trace-id slow path only when it is needed; the call still returns before
- * the URL and SIZE kernels finish.                                          */
+ * SAMPLE and OSE_GROUP_TRACE_ID the calling thread waits for SAMPLE's fast
+ * pass (after queueing the URL kernels when TEMPLATE is in the mask) and
+ * then queues trace_long_kernel only when the fast pass listed long runs and
+ * the repeated-trace-id slow path only when a trace id repeats; the call
+ * still returns before the URL and SIZE kernels finish.
+ * hipGraph capture: every stage except SAMPLE with OSE_GROUP_TRACE_ID can be
+ * captured (that one returns OSE_ENOTSUP while the stream is capturing); a
+ * captured call keeps its workspace for the graph, so call ose_reserve
+ * first.                                                                    */
 int ose_process_device(ose_engine* eng, const ose_columns* cols,
                        const ose_outputs* outs, uint32_t stage_mask,
                        uint32_t group_mode, const ose_rand* rnd, void* hip_stream);
 
 /* Workspace pre-sizing for ose_process_device (so the timed call performs no
- * allocation and can be captured into a hipGraph).                          */
+ * allocation; required before a hipGraph capture).                          */
 int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes);
 
 /* Per-kernel device time, measured with hipEvents recorded on the stream
@@ -273,32 +285,71 @@ int ose_profile_read(ose_engine* eng, char* json, size_t cap);
  * odigossampling needs every span of a trace on one GPU.  In the reference
  * that co-location is the node collector's loadbalancing exporter keyed by
  * trace id (autoscaler/controllers/nodecollector/collectorconfig/
- * traces.go:26-84).  Here: ose_shard_pack writes, per span, the record the
- * trace stage reads into per-owner buckets of `send` (owner = trace-id hash
- * mod n_ranks; batch order kept inside a bucket), with counts[n_ranks] and
- * pack_pos[n_spans] (the span's slot in `send`); the caller moves the
- * buckets with an all-to-all (RCCL), ose_shard_unpack turns the received
- * records into columns for ose_process_device(SAMPLE, OSE_GROUP_TRACE_ID),
- * the keep bytes go back with the reverse all-to-all, and
- * ose_shard_scatter_keep puts them at the original spans.  All pointers are
- * device pointers; calls are asynchronous on hip_stream.                    */
-/* Record: u64 trace_id hi, lo, start_ns, end_ns, endpoint bits (the
- * latency rules whose HasPrefix matched), then u64 {res_svc : 24 |
- * res_svc_str : 24 | status : 8} (ids no rule names travel as 0xFFFFFF and
- * unpack as 0xFFFFFFFF), then u64 attr_match only when the engine has
- * span_attribute rules: ose_shard_record_bytes() = 48 or 56 bytes
- * (OSE_XREC_BYTES is the largest). */
-#define OSE_XREC_BYTES 64u
-uint32_t ose_shard_record_bytes(const ose_engine* eng);
+ * traces.go:26-84).  Here each GPU folds its spans into partial records
+ * before the exchange: one record per stretch of consecutive spans with the
+ * same trace id and the same latency service (and inside one 64-span
+ * step), holding that stretch's share of the rule state — the error bit,
+ * the endpoint bits (strings.HasPrefix of http.route against the service's
+ * http_latency rules, latency.go:64-68 — route bytes never leave the
+ * source), the service_name / span_attribute bits, and the latency element
+ * (a zero start seen, min start after the last zero start, max end;
+ * latency.go:69-80).  The trace's owner (trace-id hash mod n_ranks) folds
+ * the records in (source rank, source order), i.e. in global batch order,
+ * so decisions equal the single-GPU ones.
+ *
+ * Record (OSE_XREC_BYTES = 56): u64 trace_id hi, lo, min start (~0 = none),
+ * max end, endpoint bits, rule bits, then u64 {latency service id : 24
+ * (0xFFFFFF = none) | flags : 8 (1 error, 2 latency element present, 4 a
+ * zero start came first)}.
+ *
+ * ose_shard_pack writes the records into per-owner buckets of `send`
+ * (stable: source order inside a bucket), counts[n_ranks] (records per
+ * owner) and pack_pos[n_spans] (the slot of each span's record);
+ * ose_shard_unpack turns received records into owner-side columns for
+ * ose_process_device(SAMPLE, OSE_GROUP_TRACE_ID): one span and one
+ * resource per record, svc_match set, status bit 7 marking a record whose
+ * zero start came first; the keep bytes go back with the reverse split and
+ * ose_shard_scatter_keep puts them on the original spans.  All pointers
+ * are device pointers; calls are asynchronous on hip_stream.
+ * ose_exchange_sample runs the whole round over an RCCL communicator.      */
+#define OSE_XREC_BYTES 56u
+uint32_t ose_shard_record_bytes(const ose_engine* eng);   /* OSE_XREC_BYTES, 0 without odigossampling */
 uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks);
 int ose_shard_pack(ose_engine* eng, const ose_columns* cols, uint32_t n_ranks, void* send,
                    uint64_t* counts, uint32_t* pack_pos, void* hip_stream);
 int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t* trace_id,
                      uint64_t* start_ns, uint64_t* end_ns, uint8_t* status, uint32_t* resource,
                      uint32_t* res_svc, uint32_t* res_svc_str, uint64_t* route_match,
-                     uint64_t* attr_match, void* hip_stream);
+                     uint64_t* svc_match, void* hip_stream);
 int ose_shard_scatter_keep(const uint8_t* keep_back, const uint32_t* pack_pos, uint64_t n,
                            uint8_t* keep, void* hip_stream);
+
+/* RCCL (resolved at run time; OSE_ENOTSUP when librccl is absent).  The
+ * communicator is the caller's ncclComm_t as void*; these helpers create one
+ * for a shim that does not link RCCL itself: rank 0 calls
+ * ose_nccl_unique_id, the 128 bytes reach every rank out of band, and every
+ * rank calls ose_nccl_comm_init.                                           */
+int ose_nccl_unique_id(void* id_out, size_t cap);
+int ose_nccl_comm_init(void** comm_out, int n_ranks, const void* id, int rank);
+void ose_nccl_comm_destroy(void* comm);
+
+/* One exchange round for this rank's batch (device columns, as
+ * ose_process_device): pack, all-to-all of the record counts, grouped
+ * send/recv of the records over xGMI, unpack + the SAMPLE stage by trace id
+ * for the traces this rank owns, the reverse split of the keep bytes and
+ * the scatter into outs->keep.  Every rank of the communicator calls it for
+ * the same round.  The calling thread waits once (the record counts size
+ * the split).  stats (optional, [3]): records sent, records received, spans.
+ * Rounds on one engine are serialised.                                      */
+int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs,
+                        void* nccl_comm, int rank, int n_ranks, const ose_rand* rnd,
+                        void* hip_stream, uint64_t* stats);
+
+/* Node-wide odigostrafficmetrics counters: node[k] = sum over the ranks of
+ * local[k] (int64 ncclAllReduce; the counters of processor.go:76-81 summed
+ * over the node's GPUs, as a scrape would sum the gateway replicas).       */
+int ose_allreduce_counters(const int64_t* local, int64_t* node, uint64_t n, void* nccl_comm,
+                           void* hip_stream);
 
 /* Message of the last failure on this thread ("" if none). */
 const char* ose_last_error(void);

@@ -2,6 +2,7 @@
 // synchronous ose_process path used by the host processors / a cgo shim.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -101,14 +102,17 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
   OUT(trace_ratio, 8 * std::max<uint64_t>(n, 1));
   OUT(url_out, n);
   OUT(tmpl, 8 * n);
-  OUT(tmpl_arena, 2 * dims->arena_bytes + 8 * n + 4096);
+  // every template fits in 2x the input bytes + 8 per span; capped at the
+  // 32-bit offset range of ose_strref (an overflow regrows it below)
+  const uint64_t tcap = std::min<uint64_t>(2 * dims->arena_bytes + 8 * n + 4096, 0xFFFFFFF0ull);
+  OUT(tmpl_arena, tcap);
   OUT(attrset_bytes, 8 * A);
   OUT(accepted_spans, 8);
   OUT(res_bytes, 8 * R);
   OUT(device_status, 4);
 #undef IN
 #undef OUT
-  b->outs_h.tmpl_arena_cap = b->outs_d.tmpl_arena_cap = 2 * dims->arena_bytes + 8 * n + 4096;
+  b->outs_h.tmpl_arena_cap = b->outs_d.tmpl_arena_cap = tcap;
   for (auto& x : b->bufs) {
     rc = b->alloc(x);
     if (rc) { delete b; return rc; }

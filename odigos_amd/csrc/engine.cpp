@@ -185,6 +185,7 @@ int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32
 
 // ---------------- engine ----------------
 Engine::~Engine() {
+  release_exchange_scratch(this);
   for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto s : streams) (void)hipStreamDestroy(s);
   for (auto ev : event_pool) (void)hipEventDestroy(ev);
@@ -226,11 +227,35 @@ void Engine::prof_end(Timed& t, hipStream_t st) {
   timed.push_back(t);
 }
 
+// True while `st` is being captured into a hipGraph.
+bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
 // Stream-ordered pool: work enqueued on a workspace may still be running
 // when the call returns (ose_process_device is asynchronous), so release
 // records an event on the caller's stream and the next user of that
-// workspace makes its own stream wait for it.
+// workspace makes its own stream wait for it.  A call captured into a
+// hipGraph takes a workspace out of the pool for good: the graph replays
+// into it whenever it is launched, so no later call may share it (and no
+// event recorded outside the capture may be waited on inside it).
 Workspace* Engine::acquire_ws(hipStream_t st) {
+  if (stream_capturing(st)) {
+    std::lock_guard<std::mutex> g(mu);
+    Workspace* w = nullptr;
+    if (!free_ws.empty()) {   // the largest free one (ose_reserve sized it)
+      auto it = std::max_element(free_ws.begin(), free_ws.end(),
+                                 [](const Workspace* a, const Workspace* b) { return a->cap < b->cap; });
+      w = *it;
+      free_ws.erase(it);
+    } else {
+      w = new Workspace();
+      pool.push_back(w);
+    }
+    w->captured = true;
+    return w;
+  }
   Workspace* w = nullptr;
   {
     std::lock_guard<std::mutex> g(mu);
@@ -245,7 +270,14 @@ Workspace* Engine::acquire_ws(hipStream_t st) {
   if (w->pending_set) (void)hipStreamWaitEvent(st, w->pending, 0);
   return w;
 }
+// A workspace taken for a capture that queued nothing goes back to the pool.
+void Engine::return_unused_ws(Workspace* w) {
+  std::lock_guard<std::mutex> g(mu);
+  w->captured = false;
+  free_ws.push_back(w);
+}
 void Engine::release_ws(Workspace* w, hipStream_t st) {
+  if (w->captured) return;   // owned by the graph it was captured into
   if (!w->pending) (void)hipEventCreateWithFlags(&w->pending, hipEventDisableTiming);
   w->pending_set = w->pending && hipEventRecord(w->pending, st) == hipSuccess;
   std::lock_guard<std::mutex> g(mu);
@@ -270,6 +302,7 @@ void Engine::give_stream(hipStream_t s) {
 
 int Workspace::reserve(size_t bytes) {
   if (bytes <= cap) return 0;
+  if (captured) return fail(OSE_ENOMEM, "workspace too small inside a hipGraph capture: call ose_reserve first");
   if (dev) HIP_TRY(hipFree(dev));
   dev = nullptr;
   cap = 0;
@@ -341,6 +374,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.out_arena = o->tmpl_arena;
   a.out_cap = o->tmpl_arena_cap;
   a.cfg = e->url_blob_dev;
+  a.general = (!e->url.custom_ids.empty() || !e->url.templatization_rules.empty()) ? 1u : 0u;
   a.plan_len = reinterpret_cast<uint32_t*>(base + off_len);
   a.plan_meta = reinterpret_cast<uint32_t*>(base + off_meta);
   a.plan_code = reinterpret_cast<uint64_t*>(base + off_code);
@@ -416,8 +450,17 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   // slow-path launches are skipped when no trace id repeats)
   // SAMPLE without TEMPLATE: the host waits for the fast path right away (an
   // idle gap of one launch latency instead of ~12 gated launches)
+  // Inside a hipGraph capture the host can neither wait nor decide: the
+  // trace-id stage keeps host state per call (table generations), so it is
+  // refused there; every other stage is captured as plain launches.
+  const bool capturing = stream_capturing(st);
+  if (capturing && (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID) {
+    e->return_unused_ws(ws);   // nothing was captured into it
+    return fail(OSE_ENOTSUP, "SAMPLE with OSE_GROUP_TRACE_ID cannot be captured into a hipGraph "
+                             "(its trace-id tables advance a host-side generation per call)");
+  }
   const bool gate_on_host = (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID && c->n_spans > 0 &&
-                            !getenv("OSE_NO_DEFER_SLOW");
+                            !capturing && !getenv("OSE_NO_DEFER_SLOW");
   const bool defer = gate_on_host && (mask & OSE_STAGE_TEMPLATE);
   const size_t url_off = defer ? (sampling_scratch_bytes(c->n_spans) + 255) / 256 * 256 : 0;
   if (defer) need = std::max(need, url_off + url_workspace_bytes(c->n_spans));

@@ -16,6 +16,9 @@ namespace ose {
 
 int fail(int code, const std::string& msg);
 int ensure_device();
+bool stream_capturing(hipStream_t st);
+struct Engine;
+void release_exchange_scratch(const Engine* e);   // shard_host.cpp
 
 // Device scratch for one in-flight call (look-back status words, sort
 // buffers, partial records).  Engines keep a pool so concurrent callers never
@@ -25,6 +28,7 @@ struct Workspace {
   size_t cap = 0;
   hipEvent_t pending = nullptr;   // recorded at release on the last user's stream
   bool pending_set = false;
+  bool captured = false;          // taken by a hipGraph capture: never returned to the pool
   int reserve(size_t bytes);
   // exact trace_id hash table of the SAMPLE stage (trace_kernel.hip), kept
   // across calls: entries carry a generation tag, so nothing is cleared
@@ -72,6 +76,7 @@ struct Engine {
   ~Engine();
   Workspace* acquire_ws(hipStream_t st);
   void release_ws(Workspace* w, hipStream_t st);
+  void return_unused_ws(Workspace* w);
   std::vector<hipStream_t> streams, free_streams;   // ose_process (host batches)
   hipStream_t take_stream();
   void give_stream(hipStream_t s);

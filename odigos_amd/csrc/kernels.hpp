@@ -39,6 +39,7 @@ struct UrlKernelArgs {
   uint64_t* used;              // bytes written (optional)
   uint32_t* slow_count;        // groups K3 left to K3s (zeroed before launch)
   uint32_t* slow_groups;       // [n_groups]
+  uint32_t general;            // user rules or custom ids configured (selects the general kernel instances)
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
   uint64_t* dbg;               // diagnostics only (ablate & 512): per-section clock sums
 };
@@ -107,6 +108,7 @@ struct TraceKernelArgs {
   uint32_t* batch_keep;       // kTraceBatch: the call's decision (read by the SIZE stage)
   const uint64_t* route_match;// optional precomputed endpoint bits (ose_columns.route_match)
   const uint64_t* attr_match; // span_attribute bits (null when no such rule)
+  const uint64_t* svc_match;  // owner-side records: OR of service_name + span_attribute rule bits (replaces both)
   uint32_t ablate;            // diagnostics only (OSE_TRACE_ABLATE, tools/ablate_trace.py): skip parts
   // kTraceRuns: runs still open kLongSteps steps past their owner's windows
   // are listed here (head positions) and decided by trace_long_kernel
@@ -118,7 +120,7 @@ struct TraceKernelArgs {
 constexpr uint32_t kWinPerWave = 16;   // tools/gpu_wpw.sh: C5 0.97 -> 0.83 ms, C3 2.03 -> 1.99 ms, C4 unchanged
 constexpr uint32_t kLongSteps = 4;   // tools/gpu_long_iter.sh: C5 16 -> 4 steps 2.75 -> 2.13 ms, C3 unchanged
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
-void launch_trace_long(const TraceKernelArgs& a, hipStream_t st);
+void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs = 0);
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st);   // slow path, gated on *dup
 
 // Slow path (runs only when *dup != 0; every launch checks the flag first).
@@ -199,11 +201,10 @@ struct ShardArgs {
   uint32_t* hist;             // [n_ranks * n_tiles] counts, then offsets (second buffer)
   uint32_t* hoff;
   uint64_t* counts;           // [n_ranks] zeroed before launch
-  uint8_t* send;              // [n * rec_words * 8]
-  uint32_t rec_words;         // 6 (48-byte records) or 7 (with span_attribute bits)
-  uint32_t* pack_pos;         // [n]
+  uint8_t* send;              // [records * kXRecBytes], records <= n
+  uint32_t* pack_pos;         // [n] slot of each span's record
 };
-constexpr uint32_t kXRec = 64;
+constexpr uint32_t kXRecBytes = 56;   // partial record (trace_kernel.hip "trace-id exchange")
 void launch_shard_hist(const ShardArgs& a, hipStream_t st);
 void launch_shard_scatter(const ShardArgs& a, hipStream_t st);
 struct UnpackArgs {
@@ -217,8 +218,7 @@ struct UnpackArgs {
   uint32_t* res_svc;
   uint32_t* res_svc_str;
   uint64_t* route_match;
-  uint64_t* attr_match;
-  uint32_t rec_words;
+  uint64_t* svc_match;
 };
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st);
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);

@@ -219,7 +219,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
       return fail(OSE_EINVAL, "SAMPLE stage needs status, resource, res_svc, res_svc_str and keep");
     if (!c->trace_id && (group_mode == OSE_GROUP_TRACE_ID || o->trace_keep || o->trace_level || o->trace_ratio))
       return fail(OSE_EINVAL, "SAMPLE stage needs the trace_id column");
-    if (e->sampling_n_attr && !c->attr_match)
+    if (e->sampling_n_attr && !c->attr_match && !c->svc_match)
       return fail(OSE_EINVAL, "span_attribute rules need the attr_match column");
     if (lat && (!c->start_ns || !c->end_ns || (!c->route_match && (!c->route || !c->arena))))
       return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns and route + arena (or route_match)");
@@ -306,6 +306,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.batch_keep = misc + kBatchKeepWord;
   a.route_match = c->route_match;
   a.attr_match = e->sampling_n_attr ? c->attr_match : nullptr;
+  a.svc_match = c->svc_match;
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
   a.n_long = misc + 12;
   a.long_runs = a.mode == kTraceRuns ? long_runs : nullptr;
@@ -318,10 +319,10 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   launch_trace_eval(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
-  auto long_pass = [=]() -> int {
+  auto long_pass = [=](uint32_t known_runs) -> int {
     Engine::Timed tl{};
     e->prof_begin("trace_long_kernel", st, tl);
-    launch_trace_long(a, st);
+    launch_trace_long(a, st, known_runs);
     HIP_TRY(hipGetLastError());
     e->prof_end(tl, st);
     return 0;
@@ -329,7 +330,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // host-gated (tail): queued only when the fast path listed long runs
   const bool gate_long = tail && group_mode == OSE_GROUP_TRACE_ID;
   if (a.long_runs && !gate_long) {
-    const int lr = long_pass();
+    const int lr = long_pass(0);
     if (lr) return lr;
   }
 
@@ -338,6 +339,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   auto rest = [=](bool run_slow) -> int {
   if (run_slow) {
     // slow path: every launch returns at once unless the fast path set *dup
+    Engine::Timed ts{};
+    e->prof_begin("trace_sort_path", st, ts);
     TraceSortArgs s{};
     s.n_spans = n;
     s.n_tiles = (uint32_t)T;
@@ -397,6 +400,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     b.key = key;
     launch_trace_eval(b, st);
     HIP_TRY(hipGetLastError());
+    e->prof_end(ts, st);
   }
 
   if (per_trace) {
@@ -438,7 +442,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   *tail = [rest, long_pass, has_long, ws]() -> int {
     HIP_TRY(hipEventSynchronize(ws->dup_ready));
     if (has_long && ws->dup_host[12]) {   // before the slow path, which rewrites every trace's keep
-      const int lr = long_pass();
+      const int lr = long_pass(ws->dup_host[12]);
       if (lr) return lr;
     }
     return rest(ws->dup_host[0] != 0);

@@ -1,9 +1,18 @@
 // shard_host.cpp — C ABI of the trace-id exchange (include/odigos_amd.h,
-// ose_shard_*): bucketing spans by owner GPU, unpacking received records,
-// scattering the returned decisions.  The collective itself (an all-to-all
-// over RCCL/xGMI) is the caller's: these calls only touch device memory on
-// the caller's stream.
+// ose_shard_*, ose_exchange_*): folding spans into per-owner partial
+// records, unpacking received records, scattering the returned decisions,
+// and the whole round over an RCCL communicator (ose_exchange_sample), the
+// in-node replacement of the node collector's loadbalancing exporter keyed
+// by trace id (autoscaler/controllers/nodecollector/collectorconfig/
+// traces.go:26-84).
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <type_traits>
+#include <vector>
 
 #include "engine_internal.hpp"
 #include "kernels.hpp"
@@ -11,7 +20,105 @@
 namespace ose {
 namespace {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// RCCL, resolved at run time: the process's already loaded copy when there
+// is one (PyTorch loads its own), else the system librccl.  Nothing links
+// against it, so the library still loads where RCCL is absent.
+struct Rccl {
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_NOLOAD))) break;
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    auto sym = [&](auto& fn, const char* n) { fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, n)); };
+    sym(r.get_unique_id, "ncclGetUniqueId");
+    sym(r.comm_init_rank, "ncclCommInitRank");
+    sym(r.comm_destroy, "ncclCommDestroy");
+    sym(r.send, "ncclSend");
+    sym(r.recv, "ncclRecv");
+    sym(r.group_start, "ncclGroupStart");
+    sym(r.group_end, "ncclGroupEnd");
+    sym(r.all_reduce, "ncclAllReduce");
+    sym(r.error_string, "ncclGetErrorString");
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.send && r.recv && r.group_start &&
+           r.group_end && r.all_reduce;
+  });
+  return r;
+}
+int nccl_fail(const char* what, ncclResult_t rc) {
+  const Rccl& r = rccl();
+  return fail(OSE_EDEVICE, std::string(what) + ": " + (r.error_string ? r.error_string(rc) : "RCCL error"));
+}
+#define NCCL_TRY(expr)                                  \
+  do {                                                  \
+    ncclResult_t _r = (expr);                           \
+    if (_r != ncclSuccess) return nccl_fail(#expr, _r); \
+  } while (0)
+
+// device scratch of one exchange round (per engine; rounds on one engine are
+// serialised by its mutex)
+struct XBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int need(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) return fail(OSE_ENOMEM, "exchange scratch");
+    cap = std::max<size_t>(bytes, 256);
+    return 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+struct XScratch {
+  std::mutex mu;
+  XBuf send, recv, pos, counts, keep_back, keep_x, cols;
+  uint64_t* host_counts = nullptr;   // pinned [2 * 64]
+  ~XScratch() {
+    for (XBuf* b : {&send, &recv, &pos, &counts, &keep_back, &keep_x, &cols})
+      if (b->p) (void)hipFree(b->p);
+    if (host_counts) (void)hipHostFree(host_counts);
+  }
+};
+std::mutex g_xs_mu;
+std::vector<std::pair<const Engine*, XScratch*>> g_xs;   // engine -> scratch (few engines)
+XScratch* scratch_of(const Engine* e) {
+  std::lock_guard<std::mutex> g(g_xs_mu);
+  for (auto& kv : g_xs)
+    if (kv.first == e) return kv.second;
+  auto* x = new XScratch();
+  g_xs.emplace_back(e, x);
+  return x;
+}
 }  // namespace
+
+void release_exchange_scratch(const Engine* e) {
+  std::lock_guard<std::mutex> g(g_xs_mu);
+  for (size_t k = 0; k < g_xs.size(); k++)
+    if (g_xs[k].first == e) {
+      delete g_xs[k].second;
+      g_xs.erase(g_xs.begin() + (long)k);
+      return;
+    }
+}
 }  // namespace ose
 
 using namespace ose;
@@ -31,7 +138,7 @@ uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks) {
 uint32_t ose_shard_record_bytes(const ose_engine* eng) {
   const Engine* e = reinterpret_cast<const Engine*>(eng);
   if (!e || !e->has_sampling) return 0;
-  return e->sampling_n_attr ? 56u : 48u;
+  return kXRecBytes;
 }
 
 int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void* send, uint64_t* counts,
@@ -46,6 +153,7 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
     return fail(OSE_EINVAL, "ose_shard_pack needs trace_id, status, resource, res_svc, res_svc_str");
   if (n && e->sampling_n_lat && (!c->start_ns || !c->end_ns || (!c->route_match && (!c->route || !c->arena))))
     return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns and route + arena (or route_match)");
+  if (n && e->sampling_n_attr && !c->attr_match) return fail(OSE_EINVAL, "span_attribute rules need the attr_match column");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipMemsetAsync(counts, 0, 8 * (size_t)n_ranks, st));
   if (n == 0) return 0;
@@ -73,10 +181,6 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.arena = c->arena;
   a.route_match = c->route_match;
   a.attr_match = e->sampling_n_attr ? c->attr_match : nullptr;
-  if (n && e->sampling_n_attr && !c->attr_match) {
-    e->release_ws(ws, st);
-    return fail(OSE_EINVAL, "span_attribute rules need the attr_match column");
-  }
   a.res_svc = c->res_svc;
   a.res_svc_str = c->res_svc_str;
   a.cfg = e->sampling_blob_dev;
@@ -85,7 +189,6 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.counts = counts;
   a.send = static_cast<uint8_t*>(send);
   a.pack_pos = pack_pos;
-  a.rec_words = ose_shard_record_bytes(eng) / 8;
   uint32_t* err = reinterpret_cast<uint32_t*>(base) + 8;
   rc = 0;
   do {
@@ -115,13 +218,13 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
 
 int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t* trace_id, uint64_t* start_ns,
                      uint64_t* end_ns, uint8_t* status, uint32_t* resource, uint32_t* res_svc, uint32_t* res_svc_str,
-                     uint64_t* route_match, uint64_t* attr_match, void* hip_stream) {
-  if (rec_bytes != 48 && rec_bytes != 56) return fail(OSE_EINVAL, "rec_bytes must be ose_shard_record_bytes()");
+                     uint64_t* route_match, uint64_t* svc_match, void* hip_stream) {
+  if (rec_bytes != kXRecBytes) return fail(OSE_EINVAL, "rec_bytes must be ose_shard_record_bytes()");
   if (n && (!recv || !trace_id || !start_ns || !end_ns || !status || !resource || !res_svc || !res_svc_str ||
-            !route_match || !attr_match))
+            !route_match || !svc_match))
     return fail(OSE_EINVAL, "NULL argument");
   UnpackArgs a{static_cast<const uint8_t*>(recv), n, trace_id, start_ns, end_ns, status, resource, res_svc, res_svc_str,
-               route_match, attr_match, rec_bytes / 8};
+               route_match, svc_match};
   launch_shard_unpack(a, static_cast<hipStream_t>(hip_stream));
   HIP_TRY(hipGetLastError());
   return 0;
@@ -132,6 +235,152 @@ int ose_shard_scatter_keep(const uint8_t* keep_back, const uint32_t* pack_pos, u
   if (n && (!keep_back || !pack_pos || !keep)) return fail(OSE_EINVAL, "NULL argument");
   launch_scatter_keep(keep_back, pack_pos, n, keep, static_cast<hipStream_t>(hip_stream));
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// ---- RCCL -----------------------------------------------------------------------
+int ose_nccl_unique_id(void* id_out, size_t cap) {
+  if (!id_out || cap < NCCL_UNIQUE_ID_BYTES) return fail(OSE_EINVAL, "id buffer must hold 128 bytes");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(OSE_ENOTSUP, "RCCL (librccl.so.1) is not available");
+  ncclUniqueId id;
+  NCCL_TRY(r.get_unique_id(&id));
+  std::memcpy(id_out, &id, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+int ose_nccl_comm_init(void** comm_out, int n_ranks, const void* id, int rank) {
+  if (!comm_out || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(OSE_EINVAL, "bad argument");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(OSE_ENOTSUP, "RCCL (librccl.so.1) is not available");
+  int rc = ensure_device();
+  if (rc) return rc;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t comm = nullptr;
+  NCCL_TRY(r.comm_init_rank(&comm, n_ranks, uid, rank));
+  *comm_out = comm;
+  return 0;
+}
+
+void ose_nccl_comm_destroy(void* comm) {
+  if (comm && rccl().ok) (void)rccl().comm_destroy(static_cast<ncclComm_t>(comm));
+}
+
+int ose_allreduce_counters(const int64_t* local, int64_t* node, uint64_t n, void* nccl_comm, void* hip_stream) {
+  if (!nccl_comm || (n && (!local || !node))) return fail(OSE_EINVAL, "NULL argument");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(OSE_ENOTSUP, "RCCL (librccl.so.1) is not available");
+  if (!n) return 0;
+  NCCL_TRY(r.all_reduce(local, node, n, ncclInt64, ncclSum, static_cast<ncclComm_t>(nccl_comm),
+                        static_cast<hipStream_t>(hip_stream)));
+  return 0;
+}
+
+int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, void* nccl_comm,
+                        int rank, int n_ranks, const ose_rand* rnd, void* hip_stream, uint64_t* stats) {
+  if (!eng || !cols || !outs || !nccl_comm) return fail(OSE_EINVAL, "NULL argument");
+  if (n_ranks < 1 || n_ranks > 64 || rank < 0 || rank >= n_ranks) return fail(OSE_EINVAL, "rank / n_ranks out of range");
+  if (cols->n_spans && !outs->keep) return fail(OSE_EINVAL, "outs->keep is required");
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  if (!e->has_sampling) return fail(OSE_EINVAL, "the exchange needs odigossampling on the engine");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(OSE_ENOTSUP, "RCCL (librccl.so.1) is not available");
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  ncclComm_t comm = static_cast<ncclComm_t>(nccl_comm);
+  XScratch* xs = scratch_of(e);
+  std::lock_guard<std::mutex> g(xs->mu);
+  const uint64_t n = cols->n_spans, W = (uint64_t)n_ranks;
+  int rc;
+  if ((rc = xs->send.need(std::max<uint64_t>(n, 1) * kXRecBytes)) || (rc = xs->pos.need(4 * std::max<uint64_t>(n, 1))) ||
+      (rc = xs->counts.need(16 * W)) || (rc = xs->keep_back.need(std::max<uint64_t>(n, 1))))
+    return rc;
+  if (!xs->host_counts) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&xs->host_counts), 16 * 64, hipHostMallocDefault));
+  uint64_t* scnt_d = xs->counts.as<uint64_t>();
+  uint64_t* rcnt_d = scnt_d + W;
+  // 1. partial records per owner
+  rc = ose_shard_pack(eng, cols, (uint32_t)W, xs->send.p, scnt_d, xs->pos.as<uint32_t>(), st);
+  if (rc) return rc;
+  // 2. record counts, all-to-all (one u64 per peer)
+  NCCL_TRY(r.group_start());
+  for (int p = 0; p < n_ranks; p++) {
+    NCCL_TRY(r.send(scnt_d + p, 1, ncclUint64, p, comm, st));
+    NCCL_TRY(r.recv(rcnt_d + p, 1, ncclUint64, p, comm, st));
+  }
+  NCCL_TRY(r.group_end());
+  HIP_TRY(hipMemcpyAsync(xs->host_counts, scnt_d, 16 * W, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));   // the host needs the split sizes
+  std::vector<uint64_t> sc(xs->host_counts, xs->host_counts + W), rcv(xs->host_counts + W, xs->host_counts + 2 * W);
+  std::vector<uint64_t> sd(W + 1, 0), rd(W + 1, 0);
+  for (uint64_t p = 0; p < W; p++) {
+    sd[p + 1] = sd[p] + sc[p];
+    rd[p + 1] = rd[p] + rcv[p];
+  }
+  const uint64_t n_recv = rd[W];
+  if (n_recv > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "more than 2^32-16 records received");
+  // owner-side columns: trace_id 16, start 8, end 8, route_match 8, svc_match 8, resource 4, res_svc 4,
+  // res_svc_str 4, status 1 per record
+  const uint64_t R = std::max<uint64_t>(n_recv, 1);
+  const size_t o_tid = 0, o_st = align_up(o_tid + 16 * R, 256), o_en = align_up(o_st + 8 * R, 256),
+               o_rm = align_up(o_en + 8 * R, 256), o_sm = align_up(o_rm + 8 * R, 256),
+               o_res = align_up(o_sm + 8 * R, 256), o_sv = align_up(o_res + 4 * R, 256),
+               o_ss = align_up(o_sv + 4 * R, 256), o_stat = align_up(o_ss + 4 * R, 256), o_end = o_stat + R + 256;
+  if ((rc = xs->recv.need(R * kXRecBytes)) || (rc = xs->keep_x.need(R)) || (rc = xs->cols.need(o_end))) return rc;
+  // 3. the records, grouped point-to-point (variable sizes per peer)
+  uint8_t* sendb = xs->send.as<uint8_t>();
+  uint8_t* recvb = xs->recv.as<uint8_t>();
+  NCCL_TRY(r.group_start());
+  for (int p = 0; p < n_ranks; p++) {
+    if (sc[p]) NCCL_TRY(r.send(sendb + sd[p] * kXRecBytes, sc[p] * kXRecBytes, ncclUint8, p, comm, st));
+    if (rcv[p]) NCCL_TRY(r.recv(recvb + rd[p] * kXRecBytes, rcv[p] * kXRecBytes, ncclUint8, p, comm, st));
+  }
+  NCCL_TRY(r.group_end());
+  // 4. owner: unpack (source-rank order) + the SAMPLE stage by trace id
+  uint8_t* cb = xs->cols.as<uint8_t>();
+  ose_columns oc{};
+  oc.n_spans = n_recv;
+  oc.n_resources = (uint32_t)n_recv;
+  oc.trace_id = reinterpret_cast<uint64_t*>(cb + o_tid);
+  oc.start_ns = reinterpret_cast<uint64_t*>(cb + o_st);
+  oc.end_ns = reinterpret_cast<uint64_t*>(cb + o_en);
+  oc.route_match = reinterpret_cast<uint64_t*>(cb + o_rm);
+  oc.svc_match = reinterpret_cast<uint64_t*>(cb + o_sm);
+  oc.resource = reinterpret_cast<uint32_t*>(cb + o_res);
+  oc.res_svc = reinterpret_cast<uint32_t*>(cb + o_sv);
+  oc.res_svc_str = reinterpret_cast<uint32_t*>(cb + o_ss);
+  oc.status = cb + o_stat;
+  if (n_recv) {
+    Engine::Timed tm{};
+    e->prof_begin("shard_unpack", st, tm);
+    rc = ose_shard_unpack(recvb, n_recv, kXRecBytes, const_cast<uint64_t*>(oc.trace_id), const_cast<uint64_t*>(oc.start_ns),
+                          const_cast<uint64_t*>(oc.end_ns), const_cast<uint8_t*>(oc.status),
+                          const_cast<uint32_t*>(oc.resource), const_cast<uint32_t*>(oc.res_svc),
+                          const_cast<uint32_t*>(oc.res_svc_str), const_cast<uint64_t*>(oc.route_match),
+                          const_cast<uint64_t*>(oc.svc_match), st);
+    e->prof_end(tm, st);
+    if (rc) return rc;
+    ose_outputs ox{};
+    ox.keep = xs->keep_x.as<uint8_t>();
+    ox.device_status = outs->device_status;
+    rc = run_stages(e, &oc, &ox, OSE_STAGE_SAMPLE, OSE_GROUP_TRACE_ID, rnd, st);
+    if (rc) return rc;
+  }
+  // 5. decisions back to the sources (reverse split), 6. onto the spans
+  uint8_t* kx = xs->keep_x.as<uint8_t>();
+  uint8_t* kb = xs->keep_back.as<uint8_t>();
+  NCCL_TRY(r.group_start());
+  for (int p = 0; p < n_ranks; p++) {
+    if (rcv[p]) NCCL_TRY(r.send(kx + rd[p], rcv[p], ncclUint8, p, comm, st));
+    if (sc[p]) NCCL_TRY(r.recv(kb + sd[p], sc[p], ncclUint8, p, comm, st));
+  }
+  NCCL_TRY(r.group_end());
+  rc = ose_shard_scatter_keep(kb, xs->pos.as<uint32_t>(), n, outs->keep, hip_stream);
+  if (rc) return rc;
+  if (stats) {   // records sent, records received, spans
+    stats[0] = sd[W];
+    stats[1] = n_recv;
+    stats[2] = n;
+  }
   return 0;
 }
 

@@ -41,6 +41,10 @@
 namespace ose {
 namespace {
 
+// Owner-side record columns (ose_shard_unpack): status bit 7 says the
+// record's latency element begins with a zero start (a reset of minStart
+// before its min start), include/odigos_amd.h "trace-id exchange".
+constexpr uint32_t kStatusReset = 0x80u;
 constexpr int kTWaves = 4;
 constexpr int kTThreads = kTWaves * kWave;
 constexpr uint64_t kInf = ~0ull;
@@ -360,6 +364,7 @@ struct StepRaw {
   uint32_t status;
   ose_strref route;
   uint64_t start, end;
+  uint64_t svm;        // svc_match (owner-side record columns)
   bool full;           // the per-span columns below the trace id were loaded
 };
 // full = false loads only what the head test needs: a wave skipping windows
@@ -396,6 +401,7 @@ __device__ __forceinline__ StepRaw load_raw(const TraceKernelArgs& a, uint64_t b
     r.end = a.end[r.i];
   }
   if (a.route) r.route = a.route[r.i];
+  if (a.svc_match) r.svm = a.svc_match[r.i];
   return r;
 }
 // head flag of every lane of a step (all lanes take the shuffles)
@@ -660,11 +666,16 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     // ---- per-span contributions ----
     uint32_t err = 0, slot = kNoSlot;
     uint64_t ep = 0, svcb = 0, st = 0, en = 0;
+    const uint32_t rst = (r.status & kStatusReset) ? 1u : 0u;   // owner-side record: a zero start came first
     if (mine) {
       const uint32_t s = sv;
-      err = r.status == OSE_STATUS_ERROR;
-      if (a.mode != kTraceBatch && ss < nsvc) svcb = c.svc_bits[ss];
-      if (a.attr_match) svcb |= a.attr_match[r.i] << c.h->attr_shift;
+      err = (r.status & ~kStatusReset) == OSE_STATUS_ERROR;
+      if (a.svc_match) {
+        svcb = r.svm;
+      } else {
+        if (a.mode != kTraceBatch && ss < nsvc) svcb = c.svc_bits[ss];
+        if (a.attr_match) svcb |= a.attr_match[r.i] << c.h->attr_shift;
+      }
       if (s < nsvc) {
         slot = c.svc_slot[s];
         if (slot != kNoSlot) {
@@ -688,7 +699,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
       const uint32_t ks = rdl(slot, ffs64(pend));
       const bool ink = slot == ks;
       pend &= ~__ballot(ink);
-      Lat v = ink ? Lat{st == 0 ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+      Lat v = ink ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
       seg_lat_scan(hseg, v);
       if (tail && !carried_tail && (v.f & 2u)) lsat |= latency_satisfied(c, ks, ep, v.m, v.e);
       if (seg0_cont) {
@@ -790,7 +801,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
 // the columns of one span of a long run (loaded one step ahead)
 struct LongRaw {
   uint32_t res, status;
-  uint64_t st, en, am, rm;
+  uint64_t st, en, am, rm, svm;
   ose_strref rt;
 };
 __device__ __forceinline__ LongRaw long_raw(const TraceKernelArgs& a, uint64_t p, uint64_t hi) {
@@ -803,6 +814,7 @@ __device__ __forceinline__ LongRaw long_raw(const TraceKernelArgs& a, uint64_t p
     r.en = a.end[p];
   }
   if (a.attr_match) r.am = a.attr_match[p];
+  if (a.svc_match) r.svm = a.svc_match[p];
   if (a.route_match) r.rm = a.route_match[p];
   else if (a.route) r.rt = a.route[p];
   return r;
@@ -878,10 +890,15 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
       if (base + kWave < hi) nx = long_raw(a, p + kWave, hi);
       uint32_t slot = kNoSlot;
       uint64_t st = 0, en = 0;
+      const uint32_t rst = (r.status & kStatusReset) ? 1u : 0u;
       if (valid) {
-        err |= r.status == OSE_STATUS_ERROR;
-        if (ss < nsvc) svc_acc |= c.svc_bits[ss];
-        svc_acc |= r.am << c.h->attr_shift;
+        err |= (r.status & ~kStatusReset) == OSE_STATUS_ERROR;
+        if (a.svc_match) {
+          svc_acc |= r.svm;
+        } else {
+          if (ss < nsvc) svc_acc |= c.svc_bits[ss];
+          svc_acc |= r.am << c.h->attr_shift;
+        }
         if (sv < nsvc) {
           slot = c.svc_slot[sv];
           if (slot != kNoSlot) {
@@ -896,7 +913,7 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
         const uint32_t ks = rdl(slot, ffs64(pend));
         const bool ink = slot == ks;
         pend &= ~__ballot(ink);
-        Lat v = ink ? Lat{st == 0 ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+        Lat v = ink ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {   // lane-order reduction into lane 0
           Lat o;
@@ -1129,20 +1146,88 @@ __global__ __launch_bounds__(kTThreads) void trace_compact_kernel(TraceCompactAr
 }
 
 // ---- trace-id exchange ---------------------------------------------------------
-constexpr uint32_t kXNone = 0xFFFFFFu;   // 24-bit "no rule names this service"
+// Partial records (include/odigos_amd.h "trace-id exchange"): the source
+// folds each stretch of its batch that shares a trace id and a latency slot
+// (and lies in one 64-span step) into one 56-byte record, so the owner GPU
+// receives one record per stretch instead of one per span.  The record is
+// the stretch's share of what trace_eval_kernel combines per trace: the
+// error bit, the endpoint (HasPrefix) bits, the service_name /
+// span_attribute bits and the latency monoid element (reset, min start after
+// the last reset, max end) of its slot.  The owner folds records in
+// (source rank, source order), which is the global batch order restricted
+// to the trace, so the fold equals the single-GPU one (the monoid is
+// associative, the rest are ORs).
+constexpr uint32_t kXNone = 0xFFFFFFu;   // 24-bit "no latency service"
+constexpr uint32_t kXWords = 7;
+constexpr uint32_t kXErr = 1u, kXLat = 2u, kXReset = 4u;
 __device__ __forceinline__ uint32_t shard_owner(uint64_t hi, uint64_t lo, uint32_t n) {
   return (uint32_t)((tid_hash(hi, lo) >> 32) % n);
 }
 
+// one span of a 64-span step: its trace id and latency slot (the record
+// boundary test) and, with `full`, its contributions
+struct XSpan {
+  bool valid;
+  uint64_t hi, lo;
+  uint32_t slot, sv, err;
+  uint64_t ep, svcb, st, en;
+};
+__device__ __forceinline__ XSpan x_span(const ShardArgs& a, const Cfg& c, uint64_t j, bool full) {
+  XSpan x{};
+  x.valid = j < a.n_spans;
+  x.slot = kNoSlot;
+  x.sv = kXNone;
+  if (!x.valid) return x;
+  const uint4 t = reinterpret_cast<const uint4*>(a.tid)[j];
+  x.hi = (uint64_t)t.x | ((uint64_t)t.y << 32);
+  x.lo = (uint64_t)t.z | ((uint64_t)t.w << 32);
+  const uint32_t nsvc = c.h->n_services;
+  const uint32_t res = a.resource[j];
+  const uint32_t s = a.res_svc[res];
+  if (s < nsvc && c.svc_slot[s] != kNoSlot) {
+    x.slot = c.svc_slot[s];
+    x.sv = s;
+  }
+  if (!full) return x;
+  x.err = a.status[j] == OSE_STATUS_ERROR;
+  const uint32_t ss = a.res_svc_str[res];
+  x.svcb = ss < nsvc ? c.svc_bits[ss] : 0;
+  if (a.attr_match) x.svcb |= a.attr_match[j] << c.h->attr_shift;
+  if (x.slot != kNoSlot) {
+    x.ep = a.route_match ? a.route_match[j] & c.slot_rules[x.slot] : endpoint_bits(c, x.slot, a.arena, a.route[j]);
+    x.st = a.start ? a.start[j] : 0;
+    x.en = a.end ? a.end[j] : 0;
+  }
+  return x;
+}
+// record heads of the step (lane 0 always starts one) and tails (where a
+// record's folded value sits after the inclusive segmented scans)
+__device__ __forceinline__ void x_bounds(const XSpan& x, int lane, uint64_t& heads, uint64_t& tails) {
+  const uint64_t ph = __shfl_up(x.hi, 1, kWave), pl = __shfl_up(x.lo, 1, kWave);
+  const uint32_t ps = __shfl_up(x.slot, 1, kWave);
+  const bool head = x.valid && (lane == 0 || ph != x.hi || pl != x.lo || ps != x.slot);
+  const uint64_t vm = __ballot(x.valid);
+  heads = __ballot(head);
+  const uint64_t nxt = (heads | ~vm) >> 1 | (1ull << 63);   // bit l: span l+1 starts a record or is past the end
+  tails = vm & nxt;
+}
+
+constexpr int kXRounds = kSortTile / kSortThreads;   // 64-span steps per wave per tile
+
 __global__ __launch_bounds__(kSortThreads) void shard_hist_kernel(ShardArgs a) {
   __shared__ uint32_t hist[64];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t < 64) hist[t] = 0;
   __syncthreads();
+  const Cfg c = load_cfg(a.cfg);
   const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
-  for (int r = 0; r < kSortRounds; r++) {
-    const uint64_t j = b + (uint64_t)r * kSortThreads + t;
-    if (j < a.n_spans) atomicAdd(&hist[shard_owner(a.tid[2 * j], a.tid[2 * j + 1], a.n_ranks)], 1u);
+  for (int r = 0; r < kXRounds; r++) {
+    const uint64_t base = b + ((uint64_t)r * (kSortThreads / kWave) + wv) * kWave;
+    if (base >= a.n_spans) break;   // wave-uniform
+    const XSpan x = x_span(a, c, base + lane, false);
+    uint64_t heads, tails;
+    x_bounds(x, lane, heads, tails);
+    if ((tails >> lane) & 1) atomicAdd(&hist[shard_owner(x.hi, x.lo, a.n_ranks)], 1u);
   }
   __syncthreads();
   if ((uint32_t)t < a.n_ranks) {
@@ -1151,32 +1236,44 @@ __global__ __launch_bounds__(kSortThreads) void shard_hist_kernel(ShardArgs a) {
   }
 }
 
-// Stable bucketing by owner (the radix-sort scatter with the owner as the
-// digit) plus the record the trace stage reads on the owner GPU.
+// Stable bucketing of the records by owner (records keep source order inside
+// a bucket: tiles in order, rounds in order, waves in order, lanes in order)
+// and the records themselves; pack_pos[span] = its record's slot in `send`.
 __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a) {
+  constexpr int kW = kSortThreads / kWave;
   __shared__ uint32_t goff[64], run[64];
-  __shared__ uint32_t wcnt[kSortThreads / kWave][64], woff[kSortThreads / kWave][64];
+  __shared__ uint32_t wcnt[kW][64], woff[kW][64];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t < 64) {
     goff[t] = (uint32_t)t < a.n_ranks ? a.hoff[(uint64_t)t * a.n_tiles + blockIdx.x] : 0;
     run[t] = 0;
-    for (int k = 0; k < kSortThreads / kWave; k++) wcnt[k][t] = 0;
+    for (int k = 0; k < kW; k++) wcnt[k][t] = 0;
   }
   __syncthreads();
   const Cfg c = load_cfg(a.cfg);
-  const uint32_t nsvc = c.h->n_services;
   const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
-  for (int r = 0; r < kSortRounds; r++) {
-    const uint64_t j = b + (uint64_t)r * kSortThreads + t;
-    const bool valid = j < a.n_spans;
-    uint64_t hi = 0, lo = 0;
-    uint32_t d = 0;
-    if (valid) {
-      hi = a.tid[2 * j];
-      lo = a.tid[2 * j + 1];
-      d = shard_owner(hi, lo, a.n_ranks);
+  for (int r = 0; r < kXRounds; r++) {
+    const uint64_t base = b + ((uint64_t)r * kW + wv) * kWave;
+    const bool live = base < a.n_spans;   // wave-uniform; dead waves still take the barriers
+    XSpan x{};
+    uint64_t heads = 0, tails = 0;
+    if (live) {
+      x = x_span(a, c, base + lane, true);
+      x_bounds(x, lane, heads, tails);
     }
-    uint64_t peers = __ballot(valid);
+    const bool tail = (tails >> lane) & 1;
+    // fold each record (inclusive segmented scans; invalid lanes are lone segments)
+    const uint32_t h = x.valid ? (uint32_t)((heads >> lane) & 1) : 1u;
+    uint32_t err = x.err;
+    uint64_t ep = x.ep, svcb = x.svcb;
+    Lat v = x.slot != kNoSlot ? Lat{x.st == 0 ? 3u : 2u, x.st == 0 ? kInf : x.st, x.en} : Lat{0u, kInf, 0ull};
+    if (live) {
+      seg_or_scan(h, err, ep, svcb);
+      seg_lat_scan(h, v);
+    }
+    // rank among this wave's records with the same owner
+    const uint32_t d = tail ? shard_owner(x.hi, x.lo, a.n_ranks) : 0u;
+    uint64_t peers = __ballot(tail);
 #pragma unroll
     for (int bit = 0; bit < 6; bit++) {
       const uint64_t bal = __ballot((d >> bit) & 1u);
@@ -1184,11 +1281,11 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     }
     const uint32_t rank = __popcll(peers & lanemask_lt(lane));
     const uint32_t cnt = __popcll(peers);
-    if (valid && rank == cnt - 1) wcnt[wv][d] = cnt;
+    if (tail && rank == cnt - 1) wcnt[wv][d] = cnt;
     __syncthreads();
     if (t < 64) {
       uint32_t acc = run[t];
-      for (int k2 = 0; k2 < kSortThreads / kWave; k2++) {
+      for (int k2 = 0; k2 < kW; k2++) {
         woff[k2][t] = acc;
         acc += wcnt[k2][t];
         wcnt[k2][t] = 0;
@@ -1196,48 +1293,48 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
       run[t] = acc;
     }
     __syncthreads();
-    if (valid) {
-      const uint32_t pos = goff[d] + woff[wv][d] + rank;
-      const uint32_t res = a.resource[j];
-      const uint32_t s = a.res_svc[res], ss = a.res_svc_str[res];
-      uint64_t ep = 0;
-      if (s < nsvc) {
-        const uint32_t slot = c.svc_slot[s];
-        if (slot != kNoSlot)
-          ep = a.route_match ? a.route_match[j] & c.slot_rules[slot] : endpoint_bits(c, slot, a.arena, a.route[j]);
-      }
-      // record (include/odigos_amd.h "trace-id exchange"): service ids the
-      // rules do not name all behave as NONE, so they travel as 24 bits
-      uint64_t* rec = reinterpret_cast<uint64_t*>(a.send + (uint64_t)pos * a.rec_words * 8);
-      rec[0] = hi;
-      rec[1] = lo;
-      rec[2] = a.start ? a.start[j] : 0;
-      rec[3] = a.end ? a.end[j] : 0;
+    uint32_t pos = 0;
+    if (tail) {
+      pos = goff[d] + woff[wv][d] + rank;
+      uint64_t* rec = reinterpret_cast<uint64_t*>(a.send) + (uint64_t)pos * kXWords;
+      const uint32_t flags = (err ? kXErr : 0u) | ((v.f & 2u) ? kXLat : 0u) | ((v.f & 1u) ? kXReset : 0u);
+      rec[0] = x.hi;
+      rec[1] = x.lo;
+      rec[2] = v.m;
+      rec[3] = v.e;
       rec[4] = ep;
-      rec[5] = (uint64_t)(s < nsvc ? s : kXNone) | ((uint64_t)(ss < nsvc ? ss : kXNone) << 24) |
-               ((uint64_t)a.status[j] << 48);
-      if (a.rec_words > 6) rec[6] = a.attr_match ? a.attr_match[j] : 0;
-      a.pack_pos[j] = pos;
+      rec[5] = svcb;
+      rec[6] = (uint64_t)((x.slot != kNoSlot ? x.sv : kXNone) | (flags << 24));
     }
+    // every span learns its record's slot from the record's tail lane
+    const int tl = ffs64(tails & ~lanemask_lt(lane));
+    const uint32_t my = __shfl(pos, tl < 0 ? lane : tl, kWave);
+    if (x.valid) a.pack_pos[base + lane] = my;
   }
 }
 
+// Records -> the owner's SAMPLE columns: one "span" per record with its own
+// resource.  The record's latency element becomes start / end plus status
+// bit 7 (kStatusReset) when a zero start came before its min start; the
+// endpoint bits go to route_match, the rule bits to svc_match.
 __global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
-  const uint64_t* rec = reinterpret_cast<const uint64_t*>(a.recv + i * a.rec_words * 8);
+  const uint64_t* rec = reinterpret_cast<const uint64_t*>(a.recv) + i * kXWords;
+  const uint64_t m = rec[2], e = rec[3], w6 = rec[6];
+  const uint32_t sv = (uint32_t)(w6 & kXNone), flags = (uint32_t)(w6 >> 24) & 0xFFu;
+  const bool lat = flags & kXLat;
   a.tid[2 * i] = rec[0];
   a.tid[2 * i + 1] = rec[1];
-  a.start[i] = rec[2];
-  a.end[i] = rec[3];
+  a.start[i] = lat && m != kInf ? m : 0;
+  a.end[i] = lat ? e : 0;
+  a.status[i] = (uint8_t)(((flags & kXErr) ? OSE_STATUS_ERROR : 0u) |
+                          ((lat && (flags & kXReset) && m != kInf) ? kStatusReset : 0u));
   a.route_match[i] = rec[4];
-  const uint64_t sv = rec[5];
-  const uint32_t s = (uint32_t)(sv & kXNone), ss = (uint32_t)((sv >> 24) & kXNone);
-  a.res_svc[i] = s == kXNone ? 0xFFFFFFFFu : s;
-  a.res_svc_str[i] = ss == kXNone ? 0xFFFFFFFFu : ss;
-  a.status[i] = (uint8_t)(sv >> 48);
-  a.attr_match[i] = a.rec_words > 6 ? rec[6] : 0;
-  a.resource[i] = (uint32_t)i;   // one "resource" per received span carries its service ids
+  a.svc_match[i] = rec[5];
+  a.res_svc[i] = lat && sv != kXNone ? sv : 0xFFFFFFFFu;
+  a.res_svc_str[i] = 0xFFFFFFFFu;
+  a.resource[i] = (uint32_t)i;   // one "resource" per record carries its latency service
 }
 
 __global__ __launch_bounds__(256) void scatter_keep_kernel(const uint8_t* back, const uint32_t* pos, uint64_t n,
@@ -1275,8 +1372,11 @@ void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
   hipLaunchKernelGGL(trace_eval_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
 }
-void launch_trace_long(const TraceKernelArgs& a, hipStream_t st) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(a.n_spans / ((uint64_t)a.long_steps * kWave) + 1, 1024);
+void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs) {
+  // known_runs: the listed-run count the host read (host-gated form); else a
+  // grid for the most runs the fast path can list, blocks past *n_long exit
+  const uint64_t most = known_runs ? known_runs : a.n_spans / ((uint64_t)a.long_steps * kWave) + 1;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(most, 1024);
   hipLaunchKernelGGL(trace_long_kernel, dim3(blocks), dim3(kLThreads), 0, st, a);
 }
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st) {

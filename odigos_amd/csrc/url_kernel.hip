@@ -694,8 +694,8 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
 // phase 1 from the class bitmaps: same result as plan_path, with segment
 // ends and the cheap predicates read from the windows.  p0 = stage offset of
 // the path (rd reads relative to it).
-__device__ __forceinline__ Plan plan_bits(const Cfg& cfg, LdsReader& rd, lds_cu4* bm, uint32_t p0, uint32_t plen,
-                                          uint32_t f) {
+__device__ __noinline__ Plan plan_bits(const Cfg& cfg, LdsReader& rd, lds_cu4* bm, uint32_t p0, uint32_t plen,
+                                       uint32_t f) {
   Plan p;
   const uint32_t n =
       (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? first_of(bm, C_QM, p0, p0 + plen) - p0 : plen;
@@ -942,6 +942,14 @@ __device__ __forceinline__ uint64_t half_mask(uint32_t lo, uint32_t hi, uint32_t
   return low_mask(h) & ~low_mask(l);
 }
 
+// getSegmentTemplatizationString for a segment longer than a 64-bit window
+// (rare: kept out of line so the list planner's registers stay small)
+__device__ __noinline__ int classify_long(const Cfg& cfg, const LdsReader& rd, uint32_t s, uint32_t L) {
+  LdsReader r = rd;
+  uint32_t e;
+  return classify_segment(cfg, r, s, s + L, &e);
+}
+
 // Phase 1 for a whole group through a segment list: each lane enumerates its
 // span's segments into the wave's list; the wave classifies the list 64
 // segments per step (about 2 steps for a C2 group, instead of one step per
@@ -952,9 +960,13 @@ __device__ __forceinline__ uint64_t half_mask(uint32_t lo, uint32_t hi, uint32_t
 // leading '/' and segment ends in one read of those rows' slash and '?' words
 // and folds its entries (<= 8) in one read; longer paths walk the rows.
 // Returns false (nothing written) when the list would overflow.
+// cls: where the classified entries go (== segs: in place; else segs keeps
+// start | len << 12 for a fused emit)
 __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32, lds_cu4* bm, uint32_t* segs,
                                                 bool needs_path, uint32_t p0, uint32_t plen, uint32_t f, Plan& p,
-                                                bool tm, uint64_t* tt) {
+                                                bool tm, uint64_t* tt, uint32_t* cls = nullptr,
+                                                uint32_t* seg_off = nullptr) {
+  if (!cls) cls = segs;
   const int lane = threadIdx.x & 63;
   uint64_t c0 = tm ? clk() : 0;
   LdsReader rd(stage32, p0);
@@ -1063,11 +1075,10 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       const Win w = load_win<0, 2>(bm, s);
       id = classify_win(cfg, rd0, w, bm, s, s, L);
     } else {
-      uint32_t e;
-      id = classify_segment(cfg, rd0, s, s + L, &e);   // segment longer than 64 bytes
+      id = classify_long(cfg, rd0, s, L);   // segment longer than 64 bytes
     }
     const uint32_t out = id >= 0 ? cfg.name((uint32_t)id).len + 2 : L;
-    segs[x] = (out << 8) | (uint32_t)(id + 1);
+    cls[x] = (out << 8) | (uint32_t)(id + 1);
   }
   wave_lds_sync();
   if (tm) { const uint64_t c1 = clk(); tt[1] += c1 - c0; c0 = c1; }
@@ -1077,7 +1088,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
     if (nseg <= 8) {   // one read of the (at most 8) entries
       uint32_t r[8];
 #pragma unroll
-      for (uint32_t k = 0; k < 8; k++) r[k] = segs[min(off + k, kSegCap - 1)];
+      for (uint32_t k = 0; k < 8; k++) r[k] = cls[min(off + k, kSegCap - 1)];
 #pragma unroll
       for (uint32_t k = 0; k < 8; k++) {
         if (k < nseg) {
@@ -1092,7 +1103,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       }
     } else {
       for (uint32_t k = 0; k < nseg; k++) {
-        const uint32_t r = segs[off + k];
+        const uint32_t r = cls[off + k];
         const int id = (int)(r & 0xFFu) - 1;
         l += r >> 8;
         if (id >= 0) {
@@ -1107,6 +1118,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
     p.field = n < kNField ? n : kNField;
   }
   if (tm) tt[2] += clk() - c0;
+  if (seg_off) *seg_off = off | (nseg << 16);
   return true;
 }
 
@@ -1136,14 +1148,30 @@ __device__ __forceinline__ uint32_t plan_gate(const PlanCols& c) {
   return (c.f & OSE_URL_PATH_MASK) != OSE_URL_PATH_NONE ? 2u : 0u;
 }
 
+// kMode bit 0 (kModeGeneral): user templatization rules or custom ids are
+// configured; without it the instance is compiled with neither (their loops
+// fold away, which is what keeps the default-config kernel off scratch).
+// bit 1 (kModeDiag): OSE_URL_ABLATE / per-section clocks.
+constexpr int kModeGeneral = 1, kModeDiag = 2;
+template <int kMode>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void url_plan_kernel(UrlKernelArgs a) {
   __shared__ PlanSmem sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const Cfg cfg = load_cfg(a, sm.ns);
+  Cfg cfg = load_cfg(a, sm.ns);
+  if (!(kMode & kModeGeneral)) {
+    cfg.n_custom = 0;
+    cfg.n_rules = 0;
+    cfg.max_rule_nseg = 0;
+  }
+  if (!(kMode & kModeDiag)) {
+    cfg.ablate = 0;
+    a.ablate = 0;
+    a.dbg = nullptr;
+  }
   const uint32_t stride = wave_stride();
   uint32_t g = wave_first_group();
   if (g >= a.n_groups) return;
-  const bool tm = a.dbg != nullptr;
+  const bool tm = (kMode & kModeDiag) && a.dbg != nullptr;
   uint64_t t0 = 0, t_stage = 0, t_bm = 0, t_plan = 0, tt[3] = {0, 0, 0};
   uint32_t buf = 0;
 
@@ -1183,12 +1211,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
       m0 = wave_or_u32(m0);
       m1 = wave_or_u32(m1);
       m2 = wave_or_u32(m2);
-      const uint32_t need = __builtin_popcount(m0) + __builtin_popcount(m1) + __builtin_popcount(m2);
-      const uint32_t rows = (pf.bytes + 31) / 32;
-      if ((need + kWave - 1) / kWave < (rows + kWave - 1) / kWave)
-        build_bitmaps_rows(stage32, (lds_u4*)sm.bm[wv], m0, m1, m2);
-      else
-        build_bitmaps(stage32, (lds_u4*)sm.bm[wv], pf.bytes);
+      build_bitmaps_rows(stage32, (lds_u4*)sm.bm[wv], m0, m1, m2);
       wave_lds_sync();
     }
     if (tm) { const uint64_t t1 = clk(); t_bm += t1 - t0; t0 = t1; }
@@ -1390,15 +1413,40 @@ __device__ __forceinline__ uint32_t next_slash(const lds_u32* sl, uint32_t a, ui
   return e;
 }
 
-// Appends the pieces of one lane (dst = output offset within the group).
+// Appends the pieces of one lane (dst = output offset within the group) and
+// records, for every gathering lane L >= 1 whose first output byte
+// L * cb - shift this lane's output holds, the piece index (so no gathering
+// lane searches the list).  The lane tracks the next such L: one compare per
+// piece, one division per lane.
 struct PieceWriter {
   uint32_t* pdl;
   uint16_t* psrc;
+  uint16_t* start;
   uint32_t idx, dst;
+  uint32_t nl, nl_byte, cb;   // next gathering lane whose first byte lies at or after dst, and that byte
+  __device__ PieceWriter(uint32_t* p, uint16_t* ps, uint16_t* st, uint32_t i, uint32_t d, uint32_t cb_, uint32_t shift)
+      : pdl(p), psrc(ps), start(st), idx(i), dst(d), cb(cb_) {
+    if (!start) {   // no start table: the gathering lanes search the list
+      nl = kWave;
+      nl_byte = ~0u;
+      return;
+    }
+    const uint32_t a = d + shift;                      // image byte of this lane's first output byte
+    uint32_t l = (uint32_t)((float)(a + cb - 1) * (1.0f / (float)cb));   // ceil(a / cb)
+    if (l * cb < a) l++;
+    if (l && (l - 1) * cb >= a) l--;
+    nl = l ? l : 1u;
+    nl_byte = nl * cb - shift;
+  }
   __device__ __forceinline__ void put(uint32_t src, uint32_t len) {
     pdl[idx] = dst | (len << 16);
     psrc[idx] = (uint16_t)src;
     dst += len;
+    while (nl_byte < dst && nl < (uint32_t)kWave) {   // the piece [dst - len, dst) holds lane nl's first byte
+      start[nl] = (uint16_t)idx;
+      nl++;
+      nl_byte += cb;
+    }
     idx++;
   }
 };
@@ -1478,10 +1526,21 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
 // K3: emit, piece-gather groups only (the others are listed for K3s).  One
 // wave per 64-span group, persistent, with the next group's bytes and the
 // group after's columns in flight while a group is assembled.
+template <int kMode>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void url_emit_kernel(UrlKernelArgs a) {
   __shared__ EmitSmem sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const Cfg cfg = load_cfg(a, sm.ns);
+  Cfg cfg = load_cfg(a, sm.ns);
+  if (!(kMode & kModeGeneral)) {
+    cfg.n_custom = 0;
+    cfg.n_rules = 0;
+    cfg.max_rule_nseg = 0;
+  }
+  if (!(kMode & kModeDiag)) {
+    cfg.ablate = 0;
+    a.ablate = 0;
+    a.dbg = nullptr;
+  }
   load_braced_names(cfg, sm.bn);
   const bool fast_cfg = sm.bn.ok && !(a.ablate & 2048);
   const lds_u8* L = (const lds_u8*)(void*)&sm;
@@ -1490,7 +1549,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
   const uint32_t stride = wave_stride();
   uint32_t g = wave_first_group();
   if (g >= a.n_groups) return;
-  const bool tm = a.dbg != nullptr;
+  const bool tm = (kMode & kModeDiag) && a.dbg != nullptr;
   uint64_t t0 = 0, t_stage = 0, t_emit = 0, ts[5] = {0, 0, 0, 0, 0};
   uint8_t* stage = sm.stage[wv];
   lds_u32* stage32 = (lds_u32*)stage;
@@ -1565,7 +1624,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
       if (tm) { const uint64_t t1 = clk(); ts[1] += t1 - t0; }
       const uint32_t nd = (img_bytes + 3) / 4;
       const uint32_t cb = 4 * ((nd + kWave - 1) / kWave);
-      PieceWriter pw{sm.pdl[wv], sm.psrc[wv], poff, local};
+      PieceWriter pw(sm.pdl[wv], sm.psrc[wv], nullptr, poff, local, cb, shift);
       if (len) {
         if (mode == M_DEFAULT) {
           const uint32_t p0 = pr.off - lo16, n = field;
@@ -1754,18 +1813,39 @@ static uint32_t resident_blocks(K kernel, size_t dyn_lds) {
 
 }  // namespace
 
-void launch_url_plan(const UrlKernelArgs& a, hipStream_t st) {
-  static const uint32_t cap = resident_blocks(url_plan_kernel, 0);
+static int url_mode(const UrlKernelArgs& a) {
+  return (a.general ? kModeGeneral : 0) | ((a.ablate || a.dbg) ? kModeDiag : 0);
+}
+template <int M>
+static void launch_plan_mode(const UrlKernelArgs& a, hipStream_t st) {
+  static const uint32_t cap = resident_blocks(url_plan_kernel<M>, 0);
   const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
-  hipLaunchKernelGGL(url_plan_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(url_plan_kernel<M>, dim3(blocks), dim3(kThreads), 0, st, a);
+}
+template <int M>
+static void launch_emit_mode(const UrlKernelArgs& a, hipStream_t st) {
+  static const uint32_t cap = resident_blocks(url_emit_kernel<M>, 0);
+  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL(url_emit_kernel<M>, dim3(blocks), dim3(kThreads), 0, st, a);
+}
+void launch_url_plan(const UrlKernelArgs& a, hipStream_t st) {
+  switch (url_mode(a)) {
+    case 0: launch_plan_mode<0>(a, st); break;
+    case 1: launch_plan_mode<1>(a, st); break;
+    case 2: launch_plan_mode<2>(a, st); break;
+    default: launch_plan_mode<3>(a, st); break;
+  }
 }
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(url_scan_kernel, dim3(a.n_scan_tiles), dim3(kScanThreads), 0, st, a);
 }
 void launch_url_emit(const UrlKernelArgs& a, hipStream_t st) {
-  static const uint32_t cap = resident_blocks(url_emit_kernel, 0);
-  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
-  hipLaunchKernelGGL(url_emit_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+  switch (url_mode(a)) {
+    case 0: launch_emit_mode<0>(a, st); break;
+    case 1: launch_emit_mode<1>(a, st); break;
+    case 2: launch_emit_mode<2>(a, st); break;
+    default: launch_emit_mode<3>(a, st); break;
+  }
 }
 void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st) {
   // the list length is on the device: a grid for every group, blocks past it exit at once

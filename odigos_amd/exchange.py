@@ -5,21 +5,23 @@ that co-location is the node collector's loadbalancing exporter keyed by
 trace id (autoscaler/controllers/nodecollector/collectorconfig/
 traces.go:26-84).  Here, per step:
 
-1. ``ose_shard_pack`` buckets, per span, the 48-byte record (56 with
-   span_attribute bits) the trace stage
-   reads (trace id, start, end, endpoint-match bits, service ids, status,
-   span_attribute bits) by
-   owner = hash(trace id) mod world, keeping batch order inside a bucket;
-2. an all-to-all of the bucket sizes, then of the records (RCCL over xGMI:
-   torch.distributed's "nccl" backend is RCCL on ROCm);
-3. ``ose_shard_unpack`` + the SAMPLE stage on the received spans (source
-   rank order, then batch order: a trace split over sources is found by the
-   trace-id table and handled by the sort-based path);
+1. ``ose_shard_pack`` folds the batch into partial records (one per stretch
+   of spans with one trace id and one latency service, 56 bytes: the error,
+   endpoint and rule bits and the latency monoid element of the stretch) and
+   buckets them by owner = hash(trace id) mod world, keeping source order;
+2. an all-to-all of the record counts, then of the records (RCCL over xGMI);
+3. ``ose_shard_unpack`` + the SAMPLE stage on the received records, folded in
+   (source rank, source order) = global batch order;
 4. the reverse all-to-all of the keep bytes and ``ose_shard_scatter_keep``.
 
-The protocol (``route_and_sample``) is written against a small ops object
-so the same code runs on the device ops below and, in tests, on CPU ops
-over gloo.
+Two drivers of the same round:
+* ``NcclExchange`` — the product path: one C-ABI call per round
+  (``ose_exchange_sample``) on an RCCL communicator the engine library
+  creates (``ose_nccl_comm_init``; the 128-byte unique id travels over
+  torch.distributed once), exactly what a cgo shim would call;
+* ``route_and_sample`` — the protocol written against a small ops object
+  over torch.distributed collectives, so the same code runs on the device ops
+  below and, in tests, on CPU ops over gloo.
 """
 from __future__ import annotations
 
@@ -28,12 +30,11 @@ import ctypes as C
 from . import native
 
 
-
 def route_and_sample(ops, world: int, group=None) -> None:
     """One exchange round; ops provides pack/alloc/unpack_sample/scatter."""
     import torch
     import torch.distributed as dist
-    XREC = ops.rec_bytes                                # bytes per exchanged span record
+    XREC = ops.rec_bytes                                # bytes per exchanged record
     send, counts, pos = ops.pack(world)                 # counts: int64 tensor [world] on ops.device
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=group)
@@ -48,8 +49,14 @@ def route_and_sample(ops, world: int, group=None) -> None:
     ops.scatter(back, pos)
 
 
+OWNER_COLS = (("trace_id", 16), ("start_ns", 8), ("end_ns", 8), ("status", 1), ("resource", 4), ("res_svc", 4),
+              ("res_svc_str", 4), ("route_match", 8), ("svc_match", 8))
+
+
 class DeviceExchange:
     """Device ops for route_and_sample over one HBM-resident batch."""
+
+    seed = 0x5EED
 
     def __init__(self, engine, db, stream=None):
         import torch
@@ -105,33 +112,22 @@ class DeviceExchange:
         if n <= self._recv_cap and self._x is not None:
             return self._x
         cap = max(int(n * 1.25), 1024)
-        d = self.device
-        x = {"trace_id": torch.empty(2 * cap, dtype=torch.int64, device=d),
-             "start_ns": torch.empty(cap, dtype=torch.int64, device=d),
-             "end_ns": torch.empty(cap, dtype=torch.int64, device=d),
-             "status": torch.empty(cap, dtype=torch.uint8, device=d),
-             "resource": torch.empty(cap, dtype=torch.int32, device=d),
-             "res_svc": torch.empty(cap, dtype=torch.int32, device=d),
-             "res_svc_str": torch.empty(cap, dtype=torch.int32, device=d),
-             "route_match": torch.empty(cap, dtype=torch.int64, device=d),
-             "attr_match": torch.empty(cap, dtype=torch.int64, device=d),
-             "keep": torch.empty(cap, dtype=torch.uint8, device=d),
-             "status_word": torch.zeros(4, dtype=torch.int32, device=d)}
+        x = {k: torch.empty(cap * w + 16, dtype=torch.uint8, device=self.device) for k, w in OWNER_COLS}
+        x["keep"] = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        x["status_word"] = torch.zeros(16, dtype=torch.uint8, device=self.device)
         self._x, self._recv_cap = x, cap
         return x
 
     def unpack_sample(self, recv, n):
         x = self._ensure(n)
         p = {k: v.data_ptr() for k, v in x.items()}
-        native.check(self.L.ose_shard_unpack(recv.data_ptr(), n, self.rec_bytes, p["trace_id"], p["start_ns"], p["end_ns"],
-                                             p["status"], p["resource"], p["res_svc"], p["res_svc_str"],
-                                             p["route_match"], p["attr_match"], self._s()))
+        native.check(self.L.ose_shard_unpack(recv.data_ptr(), n, self.rec_bytes,
+                                             *[p[k] for k, _ in OWNER_COLS], self._s()))
         cols = native.Columns()
         cols.n_spans = n
         cols.n_resources = n
-        for f in ("trace_id", "start_ns", "end_ns", "status", "resource", "res_svc", "res_svc_str", "route_match",
-                  "attr_match"):
-            setattr(cols, f, p[f])
+        for k, _ in OWNER_COLS:
+            setattr(cols, k, p[k])
         outs = native.Outputs()
         outs.keep = p["keep"]
         outs.device_status = p["status_word"]
@@ -140,9 +136,59 @@ class DeviceExchange:
                                                native.GROUP_TRACE_ID, C.byref(rnd), self._s()))
         return x["keep"]
 
-    seed = 0x5EED
-
     def scatter(self, back, pos):
         native.check(self.L.ose_shard_scatter_keep(back.data_ptr(), pos.data_ptr(), self.n,
                                                    self.db.outs.keep, self._s()))
 
+
+class NcclComm:
+    """An RCCL communicator created by the engine library (ose_nccl_comm_init);
+    the unique id is broadcast once over an existing torch.distributed group."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        import torch
+        import torch.distributed as dist
+        self.L = native.lib()
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            buf = (C.c_uint8 * 128)()
+            native.check(self.L.ose_nccl_unique_id(buf, 128))
+            uid = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+        if world > 1:
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+            t = uid.to(dev)
+            dist.broadcast(t, 0, group=group)
+            uid = t.cpu()
+        ub = (C.c_uint8 * 128)(*uid.tolist())
+        h = C.c_void_p()
+        native.check(self.L.ose_nccl_comm_init(C.byref(h), world, ub, rank))
+        self.h, self.rank, self.world = h, rank, world
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ose_nccl_comm_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+
+class NcclExchange:
+    """The product round: ``ose_exchange_sample`` (one C-ABI call per step)."""
+
+    seed = 0x5EED
+
+    def __init__(self, engine, db, comm: NcclComm, stream=None):
+        self.eng, self.db, self.comm, self.stream = engine, db, comm, stream
+        self.L = native.lib()
+        self.stats = (C.c_uint64 * 3)()
+
+    def round(self):
+        rnd = native.Rand(self.seed, 0.0)
+        s = None if self.stream is None else C.c_void_p(self.stream)
+        native.check(self.L.ose_exchange_sample(self.eng.h, C.byref(self.db.cols), C.byref(self.db.outs),
+                                                self.comm.h, self.comm.rank, self.comm.world, C.byref(rnd), s,
+                                                self.stats))
+
+    def allreduce_counters(self, local_ptr: int, node_ptr: int, n: int):
+        s = None if self.stream is None else C.c_void_p(self.stream)
+        native.check(self.L.ose_allreduce_counters(local_ptr, node_ptr, n, self.comm.h, s))

@@ -42,7 +42,7 @@ STAGE_SAMPLE = 0x1
 STAGE_TEMPLATE = 0x2
 STAGE_SIZE = 0x4
 STAGE_APPLY_KEEP = 0x8
-XREC_BYTES = 64
+XREC_BYTES = 56
 
 GROUP_TRACE_ID = 0
 GROUP_BATCH = 1
@@ -69,7 +69,7 @@ class Columns(C.Structure):
     _fields_ = [
         ("n_spans", C.c_uint64), ("n_resources", C.c_uint32), ("n_scopes", C.c_uint32),
         ("n_attrsets", C.c_uint32), ("_pad", C.c_uint32), ("arena_bytes", C.c_uint64),
-    ] + [(f, _p) for f in COLUMN_FIELDS]
+    ] + [(f, _p) for f in COLUMN_FIELDS] + [("svc_match", _p)]
 
 
 class Outputs(C.Structure):
@@ -127,6 +127,12 @@ def lib() -> C.CDLL:
         "ose_shard_unpack": (C.c_int, [_p, C.c_uint64, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
         "ose_shard_record_bytes": (C.c_uint32, [_p]),
         "ose_shard_scatter_keep": (C.c_int, [_p, _p, C.c_uint64, _p, _p]),
+        "ose_nccl_unique_id": (C.c_int, [_p, C.c_size_t]),
+        "ose_nccl_comm_init": (C.c_int, [C.POINTER(_p), C.c_int, _p, C.c_int]),
+        "ose_nccl_comm_destroy": (None, [_p]),
+        "ose_exchange_sample": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(Outputs), _p, C.c_int, C.c_int,
+                                          C.POINTER(Rand), _p, _p]),
+        "ose_allreduce_counters": (C.c_int, [_p, _p, C.c_uint64, _p, _p]),
         "ose_profile_enable": (C.c_int, [_p, C.c_int]),
         "ose_profile_read": (C.c_int, [_p, C.c_char_p, C.c_size_t]),
         # host layer (odigos_amd/csrc/host.cpp)

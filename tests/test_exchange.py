@@ -1,11 +1,16 @@
 """Trace-id exchange across GPUs (odigos_amd/exchange.py).
 
-CPU: the exchange protocol (route_and_sample) on world_size 2 and 3 over
-gloo, with the numpy record emulation and the oracle as the SAMPLE stage:
-every rank's keep bytes equal the oracle run on the concatenated global
-batch, for traces that straddle ranks.
+CPU: the partial records (numpy restatement) fold to the same decisions as
+the spans they replace (oracle on the expanded records vs oracle on the
+spans, zero starts included); the exchange protocol (route_and_sample) on
+world_size 2 and 3 over gloo, with the numpy records and the oracle as the
+owner's SAMPLE stage: every rank's keep bytes equal the oracle run on the
+concatenated global batch, for traces that straddle ranks.
 GPU (@gpu): the pack / unpack / scatter kernels against the numpy
-emulation, and the full round on one GPU over RCCL (world 1).
+restatement (bytes exact); the owner path on one GPU at 2 x 10M spans (two
+split-mode sources, both owners, decisions against the oracle on the
+global batch); the round over RCCL at world 1 through torch.distributed and
+through the C ABI (ose_exchange_sample).
 """
 import os
 import socket
@@ -14,7 +19,8 @@ import numpy as np
 import pytest
 
 from odigos_amd import native
-from tests.exchange_emul import CpuOps, HostCols, endpoint_bits, owners, pack, rec_bytes, synthetic_global_batch, unpack
+from tests.exchange_emul import (REC_BYTES, CpuOps, HostCols, endpoint_bits, expand_for_oracle, owners, pack,
+                                 synthetic_global_batch, unpack)
 from tests.workloads import c3_sampling_config
 
 CFG = c3_sampling_config()
@@ -39,29 +45,77 @@ def test_owner_hash_matches_abi():
         assert list(got) == want
 
 
-def test_pack_unpack_roundtrip():
+def test_record_bytes_abi():
+    assert REC_BYTES == native.XREC_BYTES == 56
+
+
+def test_pack_records_and_positions():
     tid, start, end, status, svc, svc_str, ep = synthetic_global_batch(1, 2000, 5)
     rec, counts, pos = pack(tid, start, end, status, svc, svc_str, ep, 4, cfg=CFG)
-    assert counts.sum() == 2000
-    assert rec.itemsize == rec_bytes(CFG) == 48
-    hc = unpack(rec.view(np.uint8), CFG)
-    a = hc.a
-    np.testing.assert_array_equal(a["start_ns"][pos], start)
-    np.testing.assert_array_equal(a["trace_id"].reshape(-1, 2)[pos], tid)
-    # buckets are contiguous and in batch order inside a bucket
-    own = owners(tid[:, 0], tid[:, 1], 4)
+    assert counts.sum() == len(rec) < 2000            # records fold several spans
+    r = rec.view(np.dtype([("hi", "<u8"), ("lo", "<u8"), ("rest", "V40")]))
+    np.testing.assert_array_equal(r["hi"][pos], tid[:, 0])
+    np.testing.assert_array_equal(r["lo"][pos], tid[:, 1])
+    # buckets are contiguous and keep source order inside a bucket
+    own = owners(rec["hi"], rec["lo"], 4)
+    assert np.all(np.diff(own) >= 0)
     for d in range(4):
-        p = pos[own == d]
-        assert np.all(np.diff(p) == 1)
+        p = pos[owners(tid[:, 0], tid[:, 1], 4) == d]
+        assert np.all(np.diff(p) >= 0)
+    # no record crosses a 64-span step
+    for k in range(0, 2000, 64):
+        if k:
+            assert pos[k] != pos[k - 1]
 
 
-def _oracle_keep(glob):
+def _oracle_keep(glob, cfg=CFG):
     from odigos_amd.batch import HostOutputs
     from tests.oracle_lib import SamplingOracle
     hc = HostCols(*glob)
     ho = HostOutputs(hc.cols)
-    assert SamplingOracle(CFG).process(hc.cols, ho.outs, native.GROUP_TRACE_ID, SEED, 4) == 0
+    assert SamplingOracle(cfg).process(hc.cols, ho.outs, native.GROUP_TRACE_ID, SEED, 4) == 0
     return ho.view("keep", np.uint8)[: hc.cols.n_spans].copy()
+
+
+def _fractional(cfg):
+    import copy
+    cfg = copy.deepcopy(cfg)
+    for k, r in enumerate(cfg["endpoint_rules"]):
+        r["rule_details"]["fallback_sampling_ratio"] = 33.3 + k
+    return cfg
+
+
+@pytest.mark.parametrize("seed,world", [(5, 1), (6, 3), (7, 8)])
+def test_records_fold_like_spans(seed, world):
+    # the owner's fold over the records (expanded for the oracle) decides every
+    # trace exactly as the oracle over the original spans (zero starts reset
+    # minStart inside and across records; fractional ratios)
+    from odigos_amd.batch import HostOutputs
+    from tests.oracle_lib import SamplingOracle
+    cfg = _fractional(CFG)
+    glob = synthetic_global_batch(1, 6000, seed)
+    rec, counts, pos = pack(*glob, world, cfg=cfg)
+    hc, main = expand_for_oracle(rec.view(np.uint8), cfg)
+    ho = HostOutputs(hc.cols)
+    assert SamplingOracle(cfg).process(hc.cols, ho.outs, native.GROUP_TRACE_ID, SEED, 2) == 0
+    keep_rec = ho.view("keep", np.uint8)[main]
+    np.testing.assert_array_equal(keep_rec[pos], _oracle_keep(glob, cfg))
+
+
+def test_unpack_columns():
+    glob = synthetic_global_batch(1, 3000, 9)
+    rec, counts, pos = pack(*glob, 2, cfg=CFG)
+    hc = unpack(rec.view(np.uint8))
+    a = hc.a
+    n = len(rec)
+    assert np.all(a["res_svc_str"][:n] == 0xFFFFFFFF)
+    assert np.all(a["resource"][:n] == np.arange(n))
+    flags = (rec["w6"] >> np.uint64(24)).astype(np.int64)
+    lat = (flags & 2) != 0
+    np.testing.assert_array_equal(a["end_ns"][:n][~lat], 0)
+    np.testing.assert_array_equal(a["svc_match"][:n], rec["svcb"])
+    reset_first = lat & ((flags & 4) != 0) & (rec["m"] != np.uint64(2**64 - 1))
+    np.testing.assert_array_equal((a["status"][:n] & 0x80) != 0, reset_first)
 
 
 def _rank_main(rank, world, m, port, q):
@@ -77,7 +131,7 @@ def _rank_main(rank, world, m, port, q):
         ops = CpuOps(local, CFG, SEED)
         route_and_sample(ops, world)
         want = _oracle_keep(glob)[lo:hi]
-        q.put((rank, bool(np.array_equal(ops.keep, want)), int((ops.keep != want).sum())))
+        q.put((rank, bool(np.array_equal(ops.keep, want)), int((ops.keep != want).sum()), ops.records_sent))
     finally:
         dist.destroy_process_group()
 
@@ -94,7 +148,9 @@ def test_exchange_protocol_gloo(world):
     res = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
-    assert all(ok for _, ok, _ in res), res
+    assert all(ok for _, ok, _, _ in res), res
+    # partial records: fewer records than spans cross the exchange
+    assert sum(r for _, _, _, r in res) < world * 3000
 
 
 def test_straddling_traces_exist():
@@ -107,7 +163,7 @@ def test_straddling_traces_exist():
 
 # ---------------- GPU ----------------
 
-def _shard_vs_emulation(cfg, with_attr):
+def _shard_vs_emulation(cfg, with_attr, world=3):
     import ctypes as C
     import torch
     from odigos_amd.batch import DeviceBatch, Engine, Generator
@@ -116,16 +172,18 @@ def _shard_vs_emulation(cfg, with_attr):
     attr = None
     if with_attr:
         attr = np.random.default_rng(7).integers(0, 2**62, size=n, dtype=np.int64).astype(np.uint64)
+        attr &= np.uint64(1)   # one span_attribute rule: bit 0
         g.cols.attr_match = attr.ctypes.data
+    st = g.array("start_ns").view(np.uint64)
+    st[np.random.default_rng(8).random(len(st)) < 0.02] = 0   # zero starts: records with a reset
     eng = Engine({"odigossampling": cfg})
     db = DeviceBatch(g.cols)
-    world = 3
-    rb = native.lib().ose_shard_record_bytes(eng.h)
-    assert rb == rec_bytes(cfg) == (56 if with_attr else 48)
+    L = native.lib()
+    rb = L.ose_shard_record_bytes(eng.h)
+    assert rb == REC_BYTES
     send = torch.empty(n * rb, dtype=torch.uint8, device="cuda")
     counts = torch.zeros(world, dtype=torch.int64, device="cuda")
     pos = torch.empty(n, dtype=torch.int32, device="cuda")
-    L = native.lib()
     native.check(L.ose_shard_pack(eng.h, C.byref(db.cols), world, send.data_ptr(), counts.data_ptr(), pos.data_ptr(), None))
     torch.cuda.synchronize()
     tid = g.array("trace_id").view(np.uint64).reshape(-1, 2)[:n]
@@ -136,47 +194,160 @@ def _shard_vs_emulation(cfg, with_attr):
     arena = g.array("arena")
     rb_ = [bytes(arena[o:o + ln]) for o, ln in route]
     ep = endpoint_bits(cfg, rsvc[res], rb_)
-    rec, cnt, p = pack(tid, g.array("start_ns").view(np.uint64)[:n], g.array("end_ns").view(np.uint64)[:n],
-                       g.array("status")[:n], rsvc[res], rstr[res], ep, world, attr, cfg=cfg)
+    rec, cnt, p = pack(tid, st[:n], g.array("end_ns").view(np.uint64)[:n], g.array("status")[:n], rsvc[res], rstr[res],
+                       ep, world, attr, cfg=cfg)
+    R = len(rec)
     np.testing.assert_array_equal(counts.cpu().numpy(), cnt)
     np.testing.assert_array_equal(pos.cpu().numpy(), p)
-    np.testing.assert_array_equal(send.cpu().numpy(), rec.view(np.uint8))
+    np.testing.assert_array_equal(send[: R * rb].cpu().numpy(), rec.view(np.uint8))
     # unpack
-    cols = {k: torch.empty(n * w, dtype=torch.uint8, device="cuda") for k, w in
-            (("trace_id", 16), ("start_ns", 8), ("end_ns", 8), ("status", 1), ("resource", 4), ("res_svc", 4),
-             ("res_svc_str", 4), ("route_match", 8), ("attr_match", 8))}
-    native.check(L.ose_shard_unpack(send.data_ptr(), n, rb, *[cols[k].data_ptr() for k in
-                                    ("trace_id", "start_ns", "end_ns", "status", "resource", "res_svc", "res_svc_str",
-                                     "route_match", "attr_match")], None))
+    from odigos_amd.exchange import OWNER_COLS
+    cols = {k: torch.empty(R * w, dtype=torch.uint8, device="cuda") for k, w in OWNER_COLS}
+    native.check(L.ose_shard_unpack(send.data_ptr(), R, rb, *[cols[k].data_ptr() for k, _ in OWNER_COLS], None))
     torch.cuda.synchronize()
-    hc = unpack(rec.view(np.uint8), cfg)
+    hc = unpack(rec.view(np.uint8))
     for k in cols:
         np.testing.assert_array_equal(cols[k].cpu().numpy(), hc.a[k].view(np.uint8)[: cols[k].numel()])
+    return R, n
 
 
 @pytest.mark.gpu
 def test_gpu_shard_kernels_vs_emulation():
-    _shard_vs_emulation(CFG, False)
+    R, n = _shard_vs_emulation(CFG, False)
+    assert R < n / 2
 
 
 @pytest.mark.gpu
 def test_gpu_shard_kernels_with_attr_bits():
-    # span_attribute rules: 56-byte records carry the attr_match bits
+    # span_attribute rules: their bits ride in the record's rule word
     cfg = dict(CFG)
     cfg["global_rules"] = list(CFG.get("global_rules") or []) + [
         {"name": "attr", "type": "span_attribute",
          "rule_details": {"service_name": "svc-attr", "attribute_key": "env", "condition_type": "string",
                           "operation": "equals", "expected_value": "prod", "sampling_ratio": 50.0}}]
-    _shard_vs_emulation(cfg, True)
+    _shard_vs_emulation(cfg, True, world=8)
+
+
+def _owner_path(sources, cfg):
+    """The whole exchange on one GPU: pack every source batch for len(sources)
+    owners, hand each owner its buckets in source-rank order, unpack + SAMPLE
+    there, send the keep bytes back and scatter them."""
+    import ctypes as C
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine
+    from odigos_amd.exchange import DeviceExchange
+    W = len(sources)
+    eng = Engine({"odigossampling": cfg})
+    L = native.lib()
+    dbs, packs = [], []
+    for g in sources:
+        db = DeviceBatch(g.cols)
+        n = g.cols.n_spans
+        send = torch.empty(max(n, 1) * REC_BYTES, dtype=torch.uint8, device="cuda")
+        counts = torch.zeros(W, dtype=torch.int64, device="cuda")
+        pos = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+        native.check(L.ose_shard_pack(eng.h, C.byref(db.cols), W, send.data_ptr(), counts.data_ptr(), pos.data_ptr(), None))
+        c = counts.cpu().numpy()
+        packs.append((send, np.concatenate([[0], np.cumsum(c)]), pos))
+        dbs.append(db)
+    backs = [torch.empty(max(int(p[1][-1]), 1), dtype=torch.uint8, device="cuda") for p in packs]
+    records = 0
+    for o in range(W):
+        parts = [p[0][p[1][o] * REC_BYTES: p[1][o + 1] * REC_BYTES] for p in packs]
+        recv = torch.cat(parts)
+        k = recv.numel() // REC_BYTES
+        records += k
+        ex = DeviceExchange.receiver(eng, REC_BYTES)
+        keep_x = ex.unpack_sample(recv, k)
+        off = 0
+        for s, p in enumerate(packs):
+            m = int(p[1][o + 1] - p[1][o])
+            backs[s][p[1][o]: p[1][o + 1]] = keep_x[off: off + m]
+            off += m
+    for s, (db, p) in enumerate(zip(dbs, packs)):
+        native.check(L.ose_shard_scatter_keep(backs[s].data_ptr(), p[2].data_ptr(), db.cols.n_spans, db.outs.keep, None))
+    torch.cuda.synchronize()
+    return [db.out_numpy("keep", n=db.cols.n_spans) for db in dbs], records
+
+
+def _concat_keep_oracle(sources, cfg, threads=16):
+    """The oracle on the global batch: the sources concatenated in rank order."""
+    import ctypes as C
+    from odigos_amd.batch import HostOutputs
+    from tests.oracle_lib import SamplingOracle
+    keeps = []
+    # one concatenated column set (resources renumbered per source)
+    cat = {}
+    for f, dt in (("trace_id", np.uint64), ("start_ns", np.uint64), ("end_ns", np.uint64), ("status", np.uint8),
+                  ("route", np.uint32)):
+        cat[f] = np.concatenate([g.array(f).view(dt)[: (g.cols.n_spans * (2 if f in ("trace_id", "route") else 1))]
+                                 for g in sources])
+    roff = np.cumsum([0] + [g.cols.n_resources for g in sources])
+    aoff = np.cumsum([0] + [g.cols.arena_bytes for g in sources])
+    cat["resource"] = np.concatenate([g.array("resource").view(np.uint32)[: g.cols.n_spans] + np.uint32(roff[k])
+                                      for k, g in enumerate(sources)])
+    rt = cat["route"].reshape(-1, 2).copy()
+    base = np.concatenate([np.full(g.cols.n_spans, aoff[k], np.uint64) for k, g in enumerate(sources)])
+    rt[:, 0] = (rt[:, 0].astype(np.uint64) + base * (rt[:, 1] > 0)).astype(np.uint32)
+    cat["route"] = rt.reshape(-1)
+    cat["arena"] = np.concatenate([g.array("arena")[: g.cols.arena_bytes] for g in sources] + [np.zeros(64, np.uint8)])
+    for f in ("res_svc", "res_svc_str"):
+        cat[f] = np.concatenate([g.array(f).view(np.uint32)[: g.cols.n_resources] for g in sources])
+    assert cat["arena"].size < 2**32
+    cols = native.Columns()
+    cols.n_spans = sum(g.cols.n_spans for g in sources)
+    cols.n_resources = int(roff[-1])
+    cols.arena_bytes = int(aoff[-1])
+    for f, a in cat.items():
+        setattr(cols, f, a.ctypes.data)
+    ho = HostOutputs(cols)
+    assert SamplingOracle(cfg).process(cols, ho.outs, native.GROUP_TRACE_ID, SEED, threads) == 0
+    keep = ho.view("keep", np.uint8)[: cols.n_spans]
+    off = 0
+    for g in sources:
+        keeps.append(keep[off: off + g.cols.n_spans].copy())
+        off += g.cols.n_spans
+    return keeps
+
+
+@pytest.mark.gpu
+def test_gpu_owner_path_2x10M():
+    # two split-mode sources of a 20M-span fused batch (the ResourceSpans of a
+    # trace land on both): each owner folds the records it receives in source
+    # order; every span's decision equals the oracle on the global batch
+    from odigos_amd.batch import Generator
+    sources = [Generator("fused", seed=0x0D160074, n_spans=20_000_000, threads=16, rank=r, world=2) for r in range(2)]
+    assert min(g.cols.n_spans for g in sources) > 9_000_000
+    got, records = _owner_path(sources, CFG)
+    want = _concat_keep_oracle(sources, CFG)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+    assert records < 0.6 * sum(g.cols.n_spans for g in sources)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [3, 8])
+def test_gpu_owner_path_zero_starts(world):
+    from odigos_amd.batch import Generator
+    cfg = _fractional(CFG)
+    sources = [Generator("zipf", seed=0x0D160075 + world, n_spans=400_000, rank=r, world=world) for r in range(world)]
+    for k, g in enumerate(sources):
+        st = g.array("start_ns").view(np.uint64)
+        st[np.random.default_rng(k).random(len(st)) < 0.01] = 0
+    got, _ = _owner_path(sources, cfg)
+    want = _concat_keep_oracle(sources, cfg)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
 
 
 @pytest.mark.gpu
 def test_gpu_exchange_round_world1():
-    # the full round on one GPU over RCCL: keep equals the direct SAMPLE stage
+    # the full round on one GPU over RCCL: through torch.distributed
+    # (route_and_sample) and through the C ABI (ose_exchange_sample)
     import torch
     import torch.distributed as dist
     from odigos_amd.batch import DeviceBatch, Engine, Generator, HostOutputs
-    from odigos_amd.exchange import DeviceExchange, route_and_sample
+    from odigos_amd.exchange import DeviceExchange, NcclComm, NcclExchange, route_and_sample
     from tests.oracle_lib import SamplingOracle
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_free_port())
@@ -184,13 +355,27 @@ def test_gpu_exchange_round_world1():
     try:
         g = Generator("fused", seed=0x0D160064, n_spans=200_000, shuffle=True)
         eng = Engine({"odigossampling": CFG})
+        ho = HostOutputs(g.cols)
+        assert SamplingOracle(CFG).process(g.cols, ho.outs, native.GROUP_TRACE_ID, 0x5EED, 8) == 0
+        n = g.cols.n_spans
         db = DeviceBatch(g.cols)
         ex = DeviceExchange(eng, db, stream=torch.cuda.current_stream().cuda_stream)
         route_and_sample(ex, 1)
         torch.cuda.synchronize()
-        ho = HostOutputs(g.cols)
-        assert SamplingOracle(CFG).process(g.cols, ho.outs, native.GROUP_TRACE_ID, ex.seed, 8) == 0
-        n = g.cols.n_spans
         np.testing.assert_array_equal(db.out_numpy("keep")[:n], ho.view("keep", np.uint8)[:n])
+        db2 = DeviceBatch(g.cols)
+        comm = NcclComm(0, 1)
+        nx = NcclExchange(eng, db2, comm, stream=torch.cuda.current_stream().cuda_stream)
+        nx.round()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(db2.out_numpy("keep")[:n], ho.view("keep", np.uint8)[:n])
+        assert nx.stats[2] == n and 0 < nx.stats[0] == nx.stats[1] < n
+        # node counters: all-reduce of a local vector over one rank is the identity
+        loc = torch.arange(1, 9, dtype=torch.int64, device="cuda")
+        node = torch.zeros(8, dtype=torch.int64, device="cuda")
+        nx.allreduce_counters(loc.data_ptr(), node.data_ptr(), 8)
+        torch.cuda.synchronize()
+        assert node.tolist() == list(range(1, 9))
+        comm.close()
     finally:
         dist.destroy_process_group()

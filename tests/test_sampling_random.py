@@ -328,16 +328,19 @@ def test_gpu_sampling_parity_full_c5():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shuffle", [False, True])
-def test_gpu_sample_and_template_one_call(shuffle):
+@pytest.mark.parametrize("workload,shuffle", [("fused", False), ("fused", True), ("zipf", False), ("zipf", True)])
+def test_gpu_sample_and_template_one_call(workload, shuffle):
     # SAMPLE | TEMPLATE in one call queues the URL launches between SAMPLE's
-    # fast path and its (host-gated) slow path and per-trace compaction
-    # (engine.cpp run_stages): keep, per-trace records and URL outputs must
-    # all match the oracle, with and without repeated trace ids
+    # fast path and its host-gated rest: trace_long_kernel (Zipf: runs longer
+    # than the fast pass walks), the slow path (shuffled: repeated trace
+    # ids) and per-trace compaction (engine.cpp run_stages).  Keep, per-trace
+    # records and URL outputs must all match the oracle.
     import torch
     from odigos_amd.batch import DeviceBatch, Engine
     from tests.oracle_lib import UrlOracle
-    g = Generator("fused", seed=0x0D160044, n_spans=200_000, shuffle=shuffle)
+    g = Generator(workload, seed=0x0D160044, n_spans=400_000 if workload == "zipf" else 200_000, shuffle=shuffle)
+    if workload == "zipf":
+        inject_zero_starts(g, 0.01, 3)
     eng = Engine({"odigossampling": CFG, "odigosurltemplate": {}})
     db = DeviceBatch(g.cols)
     eng.process_device(db, native.STAGE_SAMPLE | native.STAGE_TEMPLATE, native.GROUP_TRACE_ID, seed=SEED)
@@ -350,6 +353,8 @@ def test_gpu_sample_and_template_one_call(shuffle):
     assert int(db.out_numpy("trace_count", np.uint32)[0]) == t
     np.testing.assert_array_equal(db.out_numpy("trace_first_span", np.uint32)[:t], ho.view("trace_first_span", np.uint32)[:t])
     np.testing.assert_array_equal(db.out_numpy("trace_keep")[:t], ho.view("trace_keep", np.uint8)[:t])
+    np.testing.assert_array_equal(db.out_numpy("trace_level")[:t], ho.view("trace_level", np.uint8)[:t])
+    np.testing.assert_array_equal(db.out_numpy("trace_ratio", np.float64)[:t], ho.view("trace_ratio", np.float64)[:t])
     uo = HostOutputs(g.cols)
     assert UrlOracle({}).process(g.cols, uo.outs, nthreads=8) == 0
     np.testing.assert_array_equal(db.out_numpy("url_out")[:n], uo.view("url_out", np.uint8)[:n])
