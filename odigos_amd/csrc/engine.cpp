@@ -195,6 +195,8 @@ Engine::~Engine() {
     if (w->dev) (void)hipFree(w->dev);
     if (w->table) (void)hipFree(w->table);
     if (w->fp_table) (void)hipFree(w->fp_table);
+    if (w->runs) (void)hipFree(w->runs);
+    if (w->run_count) (void)hipFree(w->run_count);
     if (w->pending) (void)hipEventDestroy(w->pending);
     if (w->dup_host) (void)hipHostFree(w->dup_host);
     if (w->dup_ready) (void)hipEventDestroy(w->dup_ready);

@@ -38,6 +38,10 @@ struct Workspace {
   uint64_t fp_slots_cap = 0;
   uint32_t epoch = 0;
   int reserve_table(uint64_t n_spans);
+  uint32_t* runs = nullptr;        // run-list path: kMaxRuns run heads per table slot
+  uint32_t* run_count = nullptr;
+  uint64_t runs_slots = 0;
+  int reserve_runs();
   // SAMPLE + TEMPLATE in one call: the fast path's dup flag is copied here and
   // read by the host after the URL launches are queued (run_stages), so the
   // slow-path launches are only queued when a trace id repeats

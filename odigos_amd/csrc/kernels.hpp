@@ -116,12 +116,26 @@ struct TraceKernelArgs {
   uint32_t* long_runs;        // [n_spans / 64 + 1]
   uint32_t long_steps;        // hand-off distance in 64-span steps (kLongSteps)
   uint32_t win_per_wave;      // 64-span windows whose run heads one wave owns (kWinPerWave)
+  // run-list path (repeated trace ids, before the sort-based fallback):
+  // trace_runs_kernel lists each trace's runs in its exact-table slot,
+  // trace_fold_kernel folds the runs of every trace with 2..kMaxRuns runs
+  uint32_t* run_count;        // [table slots] runs listed per slot
+  uint32_t* runs;             // [table slots * kMaxRuns] run-head positions
+  uint32_t* overflow;         // set when a trace needs the sort-based path
+  uint64_t* win_first;        // [n_windows] heads that start a trace (first run only)
+  uint32_t* head_slot;        // [n_spans] exact-table slot of each run head
 };
+constexpr uint32_t kMaxRuns = 8;          // runs per trace the run-list path folds
+constexpr uint32_t kMaxFoldSpans = 4096;  // spans per trace one lane folds
+constexpr uint32_t kMaxFoldSlots = 8;     // latency services per trace one lane folds
 constexpr uint32_t kWinPerWave = 16;   // tools/gpu_wpw.sh: C5 0.97 -> 0.83 ms, C3 2.03 -> 1.99 ms, C4 unchanged
 constexpr uint32_t kLongSteps = 4;   // tools/gpu_long_iter.sh: C5 16 -> 4 steps 2.75 -> 2.13 ms, C3 unchanged
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs = 0);
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st);   // slow path, gated on *dup
+void launch_trace_runs(const TraceKernelArgs& a, hipStream_t st);           // run-list path (gated on *dup)
+void launch_trace_fold(const TraceKernelArgs& a, hipStream_t st);
+void launch_trace_first_select(const TraceKernelArgs& a, hipStream_t st);   // win_first -> win_heads unless *overflow
 
 // Slow path (runs only when *dup != 0; every launch checks the flag first).
 struct TraceSortArgs {

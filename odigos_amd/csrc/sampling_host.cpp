@@ -179,6 +179,7 @@ size_t sampling_scratch_bytes(uint64_t n) {
   s = align_up(s + 4 * 256 * T, 256);  // hist offsets
   s = align_up(s + 8 * htiles, 256);   // scan status (hist)
   s = align_up(s + 4 * (N / 64 + 1), 256);   // long runs
+  s = align_up(s + 8 * W, 256);        // win_first (run-list path)
   return s + 256;
 }
 
@@ -187,6 +188,20 @@ size_t Engine::workspace_bytes(uint64_t n_spans) const {
   if (has_sampling) s = std::max(s, sampling_scratch_bytes(n_spans));
   if (has_traffic) s = std::max(s, size_scratch_bytes(n_spans, n_spans));
   return s;
+}
+
+// Run lists of the run-list path (allocated the first time a batch repeats
+// a trace id; sized like the exact table).
+int Workspace::reserve_runs() {
+  if (runs && runs_slots >= table_slots_cap) return 0;
+  if (runs) HIP_TRY(hipFree(runs));
+  if (run_count) HIP_TRY(hipFree(run_count));
+  runs = run_count = nullptr;
+  runs_slots = 0;
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&runs), table_slots_cap * kMaxRuns * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&run_count), table_slots_cap * sizeof(uint32_t)));
+  runs_slots = table_slots_cap;
+  return 0;
 }
 
 int Workspace::reserve_table(uint64_t n_spans) {
@@ -259,7 +274,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     off = align_up(off + bytes, 256);
     return p;
   };
-  uint32_t* misc = reinterpret_cast<uint32_t*>(base);   // [0] dup, [2] scan counter (windows), [4] scan counter (hist), [12] long runs
+  uint32_t* misc = reinterpret_cast<uint32_t*>(base);   // [0] dup, [2] scan counter (windows), [4] scan counter (hist), [12] long runs, [14] run-list overflow
   uint64_t* win_heads = reinterpret_cast<uint64_t*>(take(8 * W));
   uint32_t* win_base = reinterpret_cast<uint32_t*>(take(4 * W));
   uint64_t* wstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)wtiles));
@@ -273,6 +288,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   uint32_t* hoff = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
   uint64_t* hstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)htiles));
   uint32_t* long_runs = reinterpret_cast<uint32_t*>(take(4 * (N / 64 + 1)));
+  uint64_t* win_first = reinterpret_cast<uint64_t*>(take(8 * W));
   if (off > need) return fail(OSE_EINVAL, "internal: trace workspace layout exceeds its bound");
   uint32_t* err = o->device_status ? o->device_status : misc + 8;
   HIP_TRY(hipMemsetAsync(base, 0, 64, st));
@@ -338,21 +354,40 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // (they would all return at once: the fast path left *dup clear)
   auto rest = [=](bool run_slow) -> int {
   if (run_slow) {
-    // slow path: every launch returns at once unless the fast path set *dup
+    // repeated trace ids: the run-list path (every launch returns at once
+    // unless the fast path set *dup), then the sort-based path, which runs
+    // only when some trace overflowed the run-list path
+    int rr = ws->reserve_runs();
+    if (rr) return rr;
+    uint32_t* overflow = misc + 14;
+    TraceKernelArgs rl = a;
+    rl.run_count = ws->run_count;
+    rl.runs = ws->runs;
+    rl.overflow = overflow;
+    rl.win_first = win_first;
+    rl.head_slot = key;
+    Engine::Timed tr{};
+    e->prof_begin("trace_run_list", st, tr);
+    launch_trace_runs(rl, st);
+    HIP_TRY(hipGetLastError());
+    launch_trace_fold(rl, st);
+    HIP_TRY(hipGetLastError());
+    launch_trace_first_select(rl, st);
+    HIP_TRY(hipGetLastError());
+    e->prof_end(tr, st);
     Engine::Timed ts{};
     e->prof_begin("trace_sort_path", st, ts);
     TraceSortArgs s{};
     s.n_spans = n;
     s.n_tiles = (uint32_t)T;
-    s.gate = misc;
+    s.gate = overflow;
     s.tid = c->trace_id;
     s.table = a.table;
     s.table_mask = a.table_mask;
     s.epoch = a.epoch;
     s.key = key;
     s.error = err;
-    launch_trace_insert_exact(a, st);
-    HIP_TRY(hipGetLastError());
+    // (the run-list kernel already put every run head in the exact table)
     launch_trace_key(s, st);
     HIP_TRY(hipGetLastError());
     int bits = 1;
@@ -378,7 +413,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
       sa.n = 256 * T;
       sa.n_tiles = htiles;
       sa.popcount = 0;
-      sa.gate = misc;
+      sa.gate = overflow;
       sa.in = hist;
       sa.out = hoff;
       sa.counter = misc + 4;
@@ -394,6 +429,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
       vin = vbuf[pass & 1];
     }
     TraceKernelArgs b = a;
+    b.dup = overflow;   // perm-mode evaluation is gated on this word
     b.mode = kTracePerm;
     b.long_runs = nullptr;   // the sorted pass walks every run itself
     b.perm = vin;

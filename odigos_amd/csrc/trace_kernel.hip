@@ -308,7 +308,8 @@ __device__ __forceinline__ void decide(const Cfg& c, uint32_t err, uint64_t ep, 
 // store READY; readers poll the state and read the key with sc1 loads
 // (MI355X_MICROARCH.md "Valid forms": sc1 payload + drained flag).  A lane
 // that finds the key ready and equal is a second run of that trace_id.
-__device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint64_t lo, uint32_t pos) {
+__device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint64_t lo, uint32_t pos,
+                                    uint64_t* slot_out = nullptr) {
   const uint32_t busy = (a.epoch << 2) | 1u, ready = (a.epoch << 2) | 2u;
   uint64_t h = tid_hash(hi, lo) & a.table_mask;
   uint32_t probes = 0, spins = 0;
@@ -322,8 +323,10 @@ __device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint6
         __hip_atomic_store(&s->hi, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->lo, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->first, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.run_count) __hip_atomic_store(&a.run_count[h], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&s->state, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (slot_out) *slot_out = h;
         return;
       }
       continue;   // lost the race for this slot: look at it again
@@ -341,6 +344,7 @@ __device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint6
     if (h2 == hi && l2 == lo) {
       atomicMin(&s->first, pos);
       atomicOr(a.dup, 1u);
+      if (slot_out) *slot_out = h;
       return;
     }
     h = (h + 1) & a.table_mask;
@@ -992,6 +996,153 @@ __global__ __launch_bounds__(256) void trace_insert_exact_kernel(TraceKernelArgs
   }
 }
 
+// ---- run-list path ---------------------------------------------------------
+// A batch with repeated trace ids (resource-shuffled input, or the records a
+// trace's owner GPU receives from several sources) usually holds each trace
+// in a few runs.  trace_runs_kernel inserts every run head (the window head
+// masks of the fast pass) into the exact table and lists the run in the
+// trace's slot; trace_fold_kernel then folds, for every trace with 2 or
+// more runs, its runs in batch order on one lane (exactly the fold
+// trace_eval_kernel does over a contiguous trace), decides and writes keep
+// over all its runs.  Traces with more than kMaxRuns runs, more than
+// kMaxFoldSpans spans or more than kMaxFoldSlots latency services set
+// *overflow, and the sort-based path (gated on it) recomputes the batch.
+__global__ __launch_bounds__(256) void trace_runs_kernel(TraceKernelArgs a) {
+  if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  const int lane = threadIdx.x & 63;
+  for (uint64_t w = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWave; w < a.n_windows;
+       w += (uint64_t)gridDim.x * (256 / kWave)) {
+    const uint64_t heads = a.win_heads[w];
+    const uint64_t p = w * kWave + lane;
+    if (!((heads >> lane) & 1) || p >= a.n_spans) continue;
+    const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
+    uint64_t slot = ~0ull;
+    table_insert(a, hi, lo, (uint32_t)p, &slot);
+    if (slot == ~0ull) {   // table full / spin gave up: error already flagged
+      atomicOr(a.overflow, 1u);
+      continue;
+    }
+    const uint32_t k = atomicAdd(&a.run_count[slot], 1u);
+    if (k < kMaxRuns) a.runs[slot * kMaxRuns + k] = (uint32_t)p;
+    else atomicOr(a.overflow, 1u);
+    a.head_slot[p] = (uint32_t)slot;
+  }
+}
+
+// end of the run starting at head position p: the next head after it
+__device__ __forceinline__ uint64_t run_end(const TraceKernelArgs& a, uint64_t p) {
+  uint64_t w = p / kWave;
+  uint64_t m = a.win_heads[w] & ~lanemask_le((int)(p % kWave));
+  while (!m) {
+    if (++w >= a.n_windows) return a.n_spans;
+    m = a.win_heads[w];
+  }
+  return w * kWave + (uint64_t)ffs64(m);
+}
+
+__global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a) {
+  if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
+  {
+    const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
+    for (uint32_t k = threadIdx.x * 16; k < nb; k += kTThreads * 16)
+      *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
+    __syncthreads();
+  }
+  const Cfg c = load_cfg(cfg_lds);
+  const uint32_t nsvc = c.h->n_services;
+  const bool want_route = c.h->n_lat && !a.route_match && a.route;
+  const int lane = threadIdx.x & 63;
+  for (uint64_t w = ((uint64_t)blockIdx.x * kTThreads + threadIdx.x) / kWave; w < a.n_windows;
+       w += (uint64_t)gridDim.x * kTWaves) {
+    const uint64_t heads = a.win_heads[w];
+    const uint64_t p = w * kWave + lane;
+    const bool head = ((heads >> lane) & 1) && p < a.n_spans;
+    uint32_t slot = 0, nr = 0;
+    bool first = false;
+    if (head) {
+      slot = a.head_slot[p];
+      first = a.table[slot].first == (uint32_t)p;
+      nr = __hip_atomic_load(&a.run_count[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint64_t fm = __ballot(first);
+    if (lane == 0) a.win_first[w] = fm;
+    if (!first || nr < 2 || nr > kMaxRuns) continue;   // one run: the fast pass decided it
+    // the trace's runs in batch order
+    uint32_t rs[kMaxRuns];
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxRuns; k++) rs[k] = k < nr ? a.runs[(uint64_t)slot * kMaxRuns + k] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t k = 1; k < kMaxRuns; k++)   // insertion sort, unrolled (nr <= 8)
+#pragma unroll
+      for (uint32_t j = k; j > 0; j--)
+        if (rs[j - 1] > rs[j]) { const uint32_t t = rs[j]; rs[j] = rs[j - 1]; rs[j - 1] = t; }
+    uint32_t err = 0, nslots = 0;
+    uint64_t ep = 0, svcb = 0, spans = 0;
+    uint32_t ks[kMaxFoldSlots];
+    Lat ls[kMaxFoldSlots];
+    bool over = false;
+    for (uint32_t r = 0; r < nr && !over; r++) {
+      const uint64_t s0 = rs[r], s1 = run_end(a, s0);
+      spans += s1 - s0;
+      if (spans > kMaxFoldSpans) { over = true; break; }
+      for (uint64_t q = s0; q < s1; q++) {
+        const uint32_t res = a.resource[q], stt = a.status[q];
+        err |= (stt & ~kStatusReset) == OSE_STATUS_ERROR;
+        const uint32_t sv = a.res_svc[res];
+        if (a.svc_match) {
+          svcb |= a.svc_match[q];
+        } else {
+          const uint32_t ss = a.res_svc_str[res];
+          if (ss < nsvc) svcb |= c.svc_bits[ss];
+          if (a.attr_match) svcb |= a.attr_match[q] << c.h->attr_shift;
+        }
+        if (sv >= nsvc) continue;
+        const uint32_t slt = c.svc_slot[sv];
+        if (slt == kNoSlot) continue;
+        ep |= a.route_match ? a.route_match[q] & c.slot_rules[slt]
+                            : (want_route ? endpoint_bits(c, slt, a.arena, a.route[q]) : 0ull);
+        const uint64_t st = a.start ? a.start[q] : 0, en = a.end ? a.end[q] : 0;
+        const Lat v{(st == 0 || (stt & kStatusReset)) ? 3u : 2u, st == 0 ? kInf : st, en};
+        uint32_t k = 0;
+        while (k < nslots && ks[k] != slt) k++;
+        if (k == nslots) {
+          if (nslots == kMaxFoldSlots) { over = true; break; }
+          ks[nslots] = slt;
+          ls[nslots] = Lat{0u, kInf, 0ull};
+          nslots++;
+        }
+        ls[k] = lat_comb(ls[k], v);
+      }
+    }
+    if (over) {
+      atomicOr(a.overflow, 1u);
+      continue;
+    }
+    uint64_t lsat = 0;
+    for (uint32_t k = 0; k < nslots; k++)
+      if (ls[k].f & 2u) lsat |= latency_satisfied(c, ks[k], ep, ls[k].m, ls[k].e);
+    const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
+    uint8_t dk = 0, dl = 0;
+    double dr = 0;
+    decide(c, err, ep, lsat, svcb, trace_uniform(hi, lo, a.seed), dk, dl, dr);
+    write_rec(a, p, dk, dl, dr);
+    for (uint32_t r = 0; r < nr; r++) {
+      const uint64_t s0 = rs[r], s1 = run_end(a, s0);
+      for (uint64_t q = s0; q < s1; q++) a.keep[q] = dk;
+    }
+  }
+}
+
+// the per-trace outputs list first runs only, unless the sort-based path
+// (gated on *overflow) rewrites the head masks itself
+__global__ __launch_bounds__(256) void trace_first_select_kernel(TraceKernelArgs a) {
+  if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  if (__hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < a.n_windows; w += (uint64_t)gridDim.x * 256)
+    a.win_heads[w] = a.win_first[w];
+}
+
 // key[i] = first run-head position of span i's trace_id (read-only probe of
 // the table the fast path filled).
 __global__ __launch_bounds__(256) void trace_key_kernel(TraceSortArgs a) {
@@ -1383,6 +1534,18 @@ void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st) {
   if (a.n_spans)
     hipLaunchKernelGGL(trace_insert_exact_kernel, dim3((uint32_t)std::min<uint64_t>((a.n_spans + 255) / 256, kGatedBlocks)),
                        dim3(256), 0, st, a);
+}
+void launch_trace_runs(const TraceKernelArgs& a, hipStream_t st) {
+  const uint64_t blocks = std::min<uint64_t>((a.n_windows + 3) / 4, kGatedBlocks);
+  hipLaunchKernelGGL(trace_runs_kernel, dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(256), 0, st, a);
+}
+void launch_trace_fold(const TraceKernelArgs& a, hipStream_t st) {
+  const uint64_t blocks = std::min<uint64_t>((a.n_windows + kTWaves - 1) / kTWaves, kGatedBlocks);
+  hipLaunchKernelGGL(trace_fold_kernel, dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(kTThreads), 0, st, a);
+}
+void launch_trace_first_select(const TraceKernelArgs& a, hipStream_t st) {
+  const uint64_t blocks = std::min<uint64_t>((a.n_windows + 255) / 256, kGatedBlocks);
+  hipLaunchKernelGGL(trace_first_select_kernel, dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(256), 0, st, a);
 }
 void launch_trace_key(const TraceSortArgs& a, hipStream_t st) {
   const uint64_t blocks = std::min<uint64_t>((a.n_spans + 255) / 256, kGatedBlocks);
