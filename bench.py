@@ -55,7 +55,9 @@ FUSED_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "re
 SAMPLE_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc", "res_svc_str")
 URL_KERNELS = ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel")
 TRACE_KERNELS = ("trace_eval_kernel", "trace_long_kernel")
-SLOW_KERNELS = ("trace_sort_path",)   # the repeated-trace-id path, timed as one span of launches
+# the repeated-trace-id paths, each timed as one span of launches (run lists,
+# then the sort path for traces that overflow them)
+SLOW_KERNELS = ("trace_run_list", "trace_sort_path")
 SIZE_KERNELS = ("size_span_kernel", "size_scope_kernel", "size_res_kernel")
 PER_TRACE_OUTS = ("trace_count", "trace_first_span", "trace_keep", "trace_level", "trace_ratio")
 
@@ -73,19 +75,19 @@ WORKLOADS = {
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
     "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000, per_gpu=True,
                  cfg=None, stages="SAMPLE|TEMPLATE", null_columns=("res_url_ok",), null_outputs=PER_TRACE_OUTS,
-                 fields=SAMPLE_FIELDS + ("kind", "url_flags", "path"), kernels=TRACE_KERNELS + URL_KERNELS,
+                 fields=SAMPLE_FIELDS + ("kind", "url_flags", "path"), kernels=TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS,
                  metric_config="C5: odigossampling + odigosurltemplate on Zipf(1.1) trace sizes (1 to 50k "
                                "spans/trace), 1M distinct routes, 64-bit user ids in paths, 50M spans per GPU"),
     "fused": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False,
                   cfg=None, stages="SAMPLE|TEMPLATE|SIZE", null_columns=("res_url_ok",),
                   null_outputs=PER_TRACE_OUTS + ("res_bytes",), fields=FUSED_FIELDS,
-                  kernels=TRACE_KERNELS + URL_KERNELS + SIZE_KERNELS,
+                  kernels=TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS + SIZE_KERNELS,
                   metric_config="C4: fused odigossampling -> odigosurltemplate -> odigostrafficmetrics, 100M spans "
                                 "in total (all on one GPU at N=1; ~100M/N per GPU, trace-id all-to-all over RCCL "
                                 "at N>1)"),
     "owner": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False, sources=8,
                   cfg=None, stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
-                  fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
+                  fields=SAMPLE_FIELDS, kernels=("shard_unpack",) + TRACE_KERNELS + SLOW_KERNELS,
                   metric_config="C4 owner side on one GPU: the records trace owner 0 of 8 receives "
                                 "(8 source shards of the 100M-span C4 batch, rank order), unpack + SAMPLE"),
 }

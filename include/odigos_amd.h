@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define OSE_ABI_VERSION 2
+#define OSE_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------- */
 #define OSE_OK        0
@@ -155,8 +155,10 @@ typedef struct ose_columns {
                                   instead of route/arena (set by ose_shard_unpack)               */
   const uint64_t* attr_match;  /* bit k = the span meets the k-th span_attribute rule (in level order):
                                   its resource's AsString(service.name) is the rule's service_name and
-                                  its attribute satisfies the condition (spanattribute.go:126-320,
-                                  evaluated by the shim); required when such rules are configured */
+                                  its attribute satisfies the condition (spanattribute.go:126-320).
+                                  With attr_type set, only the bits of the rules the engine leaves to
+                                  the shim (ose_engine_info.attr_host_rules: "json" conditions) are
+                                  read (NULL when there are none); without it every bit is read   */
 
   /* per resource */
   const uint32_t* res_svc;      /* ose_engine_service_id(AsString(service.name)) or OSE_NONE */
@@ -176,7 +178,30 @@ typedef struct ose_columns {
    * service rules) of the spans a partial record folds; when non-NULL the
    * engine reads it instead of res_svc_str / attr_match                   */
   const uint64_t* svc_match;
+
+  /* per span x attribute key, optional: the span_attribute rules with
+   * string / number / boolean conditions are evaluated on the GPU from the
+   * span's value of the rule's attribute_key (spanattribute.go:136-230).
+   * Key k is the k-th distinct attribute_key of those rules in level order
+   * (ose_engine_attr_key).  Key-major: entry [k * n_spans + i] is
+   * Attributes().Get(key k) of span i (the first entry with that key):
+   *   attr_type  OSE_ATTR_* (OSE_ATTR_ABSENT when the key is not found)
+   *   attr_val   STR: ose_strref {off, len} into the arena (as a u64, off in
+   *              the low half); INT: the int64; DOUBLE: the float64 bits;
+   *              BOOL: 0 / 1; other types: 0                               */
+  uint32_t n_attr_keys;
+  uint32_t _pad2;
+  const uint8_t* attr_type;
+  const uint64_t* attr_val;
 } ose_columns;
+
+/* pcommon.ValueType of an attribute value in attr_type */
+#define OSE_ATTR_ABSENT 0u
+#define OSE_ATTR_STR    1u
+#define OSE_ATTR_INT    2u
+#define OSE_ATTR_DOUBLE 3u
+#define OSE_ATTR_BOOL   4u
+#define OSE_ATTR_OTHER  5u   /* map, slice, bytes, empty */
 
 /* ---- results -----------------------------------------------------------
  * Any pointer may be NULL when its stage is not requested.                 */
@@ -235,8 +260,16 @@ typedef struct ose_engine_info {
   uint32_t max_template_name;   /* longest "{name}" body the templater can emit */
   int64_t inverse_sampling;     /* odigostrafficmetrics int64(1/sampling_ratio) */
   double traffic_sampling_ratio;
+  uint32_t n_attr_rules;        /* span_attribute rules (attr_match bits) */
+  uint32_t n_attr_keys;         /* attribute keys the GPU-evaluated ones read */
+  uint64_t attr_host_rules;     /* bit k: rule k is evaluated by the shim into
+                                   attr_match even when attr_type is given */
 } ose_engine_info;
 int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info);
+
+/* Attribute key k (< n_attr_keys) of the attr_type / attr_val columns; the
+ * bytes stay valid for the engine's lifetime.                               */
+int ose_engine_attr_key(const ose_engine* eng, uint32_t k, const char** key, uint32_t* len);
 
 /* Pinned host staging: the engine owns the memory (cgo: no Go pointers are
  * retained).  dims->n_spans, n_resources, n_scopes, n_attrsets and

@@ -22,6 +22,7 @@ COLUMN_LAYOUT = {
     "route_match": ("span", 8), "attr_match": ("span", 8),
     "res_svc": ("res", 4), "res_svc_str": ("res", 4), "res_url_ok": ("res", 1), "res_attrset": ("res", 4),
     "res_size": ("res", 4), "scope_size": ("scope", 4), "scope_resource": ("scope", 4),
+    "attr_type": ("span_key", 1), "attr_val": ("span_key", 8),
 }
 OUTPUT_LAYOUT = {
     "keep": ("span", 1), "trace_count": ("one", 4), "trace_first_span": ("span", 4), "trace_keep": ("span", 1),
@@ -33,7 +34,7 @@ OUTPUT_LAYOUT = {
 
 def _count(cols, dim: str) -> int:
     return {"span": cols.n_spans, "res": cols.n_resources, "scope": cols.n_scopes, "arena": cols.arena_bytes,
-            "attrset": cols.n_attrsets, "one": 1}[dim]
+            "attrset": cols.n_attrsets, "one": 1, "span_key": cols.n_spans * cols.n_attr_keys}[dim]
 
 
 def default_tmpl_cap(cols) -> int:
@@ -118,7 +119,7 @@ class DeviceBatch:
         import torch
         self.torch = torch
         self.cols = native.Columns()
-        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes"):
+        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys"):
             setattr(self.cols, f, getattr(host_cols, f))
         self.t = {}
         for name, (dim, size) in COLUMN_LAYOUT.items():
@@ -206,8 +207,8 @@ class Engine:
 
 class PinnedBatch:
     """An engine-owned pinned host batch (ose_batch_acquire) for the
-    synchronous drop-in path ose_process: H2D of the columns, the stages,
-    D2H of the results — what a cgo shim calls per ConsumeTraces."""
+    synchronous drop-in call ose_process: H2D of the columns, the stages,
+    D2H of the results — what the cgo shim calls per ConsumeTraces."""
 
     def __init__(self, engine: "Engine", dims: native.Columns):
         self.L = engine.L
@@ -217,64 +218,19 @@ class PinnedBatch:
         self.h = h
         self.cols = self.L.ose_batch_columns(h).contents
         self.outs = self.L.ose_batch_outputs(h).contents
-        self.cap = {f: getattr(dims, f) for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes")}
 
-    def fill(self, src: native.Columns, span_lo: int = 0, span_hi: int | None = None):
-        """Copies the spans [span_lo, span_hi) of a generated batch (whole
-        resources expected: the columns are copied as they are, resource,
-        scope and arena references rebased to the slice)."""
-        n_all = src.n_spans
-        span_hi = n_all if span_hi is None else span_hi
-        n = span_hi - span_lo
-        assert n <= self.cap["n_spans"]
-        self.cols.n_spans = n
-        self.cols.n_attrsets = src.n_attrsets
+    def fill(self, src: native.Columns):
+        """Copies a host batch of the acquired dimensions into the pinned
+        columns (the shim's fillColumns step); columns the source lacks are
+        NULLed, which tells ose_process they are absent."""
         for f, (dim, size) in COLUMN_LAYOUT.items():
-            if dim != "span" or not getattr(src, f) or not getattr(self.cols, f):
+            if dim in ("attrset", "one"):
                 continue
-            C.memmove(getattr(self.cols, f), getattr(src, f) + span_lo * size, n * size)
-        if n_all == n:   # whole batch: per-resource/scope columns and the arena as they are
-            self.cols.n_resources, self.cols.n_scopes = src.n_resources, src.n_scopes
-            self.cols.arena_bytes = src.arena_bytes
-            for f, (dim, size) in COLUMN_LAYOUT.items():
-                if dim in ("res", "scope", "arena") and getattr(src, f) and getattr(self.cols, f):
-                    C.memmove(getattr(self.cols, f), getattr(src, f), _count(src, dim) * size)
-            return
-        # a slice: rebase resource / scope indices and the arena
-        res = np.ctypeslib.as_array((C.c_uint32 * n).from_address(getattr(self.cols, "resource")))
-        r0, r1 = int(res[0]), int(res[-1]) + 1
-        res -= np.uint32(r0)
-        sc = np.ctypeslib.as_array((C.c_uint32 * n).from_address(getattr(self.cols, "scope")))
-        s0, s1 = int(sc[0]), int(sc[-1]) + 1
-        sc -= np.uint32(s0)
-        self.cols.n_resources, self.cols.n_scopes = r1 - r0, s1 - s0
-        for f, (dim, size) in COLUMN_LAYOUT.items():
-            if dim == "res" and getattr(src, f) and getattr(self.cols, f):
-                C.memmove(getattr(self.cols, f), getattr(src, f) + r0 * size, (r1 - r0) * size)
-            if dim == "scope" and getattr(src, f) and getattr(self.cols, f):
-                C.memmove(getattr(self.cols, f), getattr(src, f) + s0 * size, (s1 - s0) * size)
-        if self.cols.scope_resource:
-            srr = np.ctypeslib.as_array((C.c_uint32 * (s1 - s0)).from_address(self.cols.scope_resource))
-            srr -= np.uint32(r0)
-        lo, hi = None, None
-        for f in ("path", "route"):
-            if not getattr(self.cols, f):
-                continue
-            ref = np.ctypeslib.as_array((C.c_uint32 * (2 * n)).from_address(getattr(self.cols, f))).reshape(-1, 2)
-            m = ref[:, 1] > 0
-            if m.any():
-                a, b = int(ref[m, 0].min()), int((ref[m, 0] + ref[m, 1]).max())
-                lo = a if lo is None else min(lo, a)
-                hi = b if hi is None else max(hi, b)
-        lo, hi = (lo or 0), (hi or 0)
-        self.cols.arena_bytes = hi - lo
-        if hi > lo:
-            C.memmove(self.cols.arena, src.arena + lo, hi - lo)
-        for f in ("path", "route"):
-            if getattr(self.cols, f):
-                ref = np.ctypeslib.as_array((C.c_uint32 * (2 * n)).from_address(getattr(self.cols, f))).reshape(-1, 2)
-                m = ref[:, 1] > 0
-                ref[m, 0] -= np.uint32(lo)
+            dst, srcp = getattr(self.cols, f, None), getattr(src, f, None)
+            if dst and srcp:
+                C.memmove(dst, srcp, _count(src, dim) * size)
+            elif dst:
+                setattr(self.cols, f, None)
 
     def process(self, stages: int, group_mode: int = native.GROUP_TRACE_ID, seed: int = 0, traffic_u: float = 0.0):
         rnd = native.Rand(seed, traffic_u)

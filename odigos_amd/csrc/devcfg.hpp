@@ -98,3 +98,35 @@ struct SampCfgDev {
 };
 
 }  // namespace ose
+
+namespace ose {
+
+// span_attribute rules evaluated on the GPU (attr_kernel.hip; the rule
+// semantics of internal/sampling/spanattribute.go:136-230).  One entry per
+// rule with a string / number / boolean condition, in level order; `bit` is
+// the rule's attr_match bit, `key` its attr_type / attr_val column.
+enum : uint32_t { kAttrCondStr = 0, kAttrCondNum = 1, kAttrCondBool = 2 };
+enum : uint32_t {
+  kAttrOpNever = 0,   // an operation the condition type has no case for
+  kAttrOpExists, kAttrOpEq, kAttrOpNe, kAttrOpContains, kAttrOpNotContains, kAttrOpRegex,
+  kAttrOpGt, kAttrOpLt, kAttrOpGe, kAttrOpLe
+};
+struct AttrRuleDev {
+  uint32_t bit, key, svc, cond, op;
+  uint32_t exp_off, exp_len;   // expected_value bytes (string conditions), bytes section
+  uint32_t dfa_off;            // regex: DfaDev byte offset; 0 = regexp.Compile failed (never matches)
+  uint32_t num_ok;             // strconv.ParseFloat(expected_value) succeeded
+  uint32_t bool_ok, bool_val;  // strconv.ParseBool(expected_value)
+  uint32_t _pad;
+  double num;
+};
+struct AttrCfgDev {
+  uint32_t n_rules;
+  uint32_t n_keys;
+  uint32_t rules_off;          // AttrRuleDev[n_rules]
+  uint32_t bytes_off;
+  uint32_t total_bytes;
+  uint32_t _pad[3];
+};
+
+}  // namespace ose

@@ -17,6 +17,7 @@
 #include "devcfg.hpp"
 #include "engine_internal.hpp"
 #include "kernels.hpp"
+#include "blob.hpp"
 #include "regex_dfa.hpp"
 
 namespace ose {
@@ -33,49 +34,6 @@ int fail(int code, const std::string& msg) {
     hipError_t _e = (expr);                                                             \
     if (_e != hipSuccess) return fail(OSE_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
   } while (0)
-
-namespace {
-
-// ---------------- blob builder ----------------
-struct Blob {
-  std::vector<uint8_t> b;
-  uint32_t align() {
-    while (b.size() % 16) b.push_back(0);
-    return (uint32_t)b.size();
-  }
-  template <typename T>
-  uint32_t put(const T* p, size_t n) {
-    uint32_t off = align();
-    const uint8_t* s = reinterpret_cast<const uint8_t*>(p);
-    b.insert(b.end(), s, s + n * sizeof(T));
-    return off;
-  }
-  template <typename T>
-  T* at(uint32_t off) { return reinterpret_cast<T*>(b.data() + off); }
-};
-
-uint32_t put_dfa(Blob& bl, const Dfa& d) {
-  DfaDev h{};
-  h.nclasses = d.nclasses;
-  h.nstates = d.nstates;
-  h.start = d.start;
-  h.match = d.match;
-  h.hi_n = (uint32_t)d.hi_lo.size();
-  std::memcpy(h.ascii, d.ascii_class, 128);
-  uint32_t off = bl.put(&h, 1);
-  std::vector<uint32_t> hr;
-  for (size_t k = 0; k < d.hi_lo.size(); k++) { hr.push_back(d.hi_lo[k]); hr.push_back(d.hi_hi[k]); hr.push_back(d.hi_cls[k]); }
-  uint32_t hoff = bl.put(hr.data(), hr.size());
-  uint32_t toff = bl.put(d.trans.data(), d.trans.size());
-  uint32_t aoff = bl.put(d.accept_end.data(), d.accept_end.size());
-  DfaDev* hp = bl.at<DfaDev>(off);
-  hp->hi_off = hoff;
-  hp->trans_off = toff;
-  hp->acc_off = aoff;
-  return off;
-}
-
-}  // namespace
 
 // odigosurltemplate tables: newUrlTemplateProcessor (processor.go:27-69)
 // groups rules by segment count keeping config order; custom ids default
@@ -186,17 +144,20 @@ int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32
 // ---------------- engine ----------------
 Engine::~Engine() {
   release_exchange_scratch(this);
+  release_batch_pool(this);
   for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto s : streams) (void)hipStreamDestroy(s);
   for (auto ev : event_pool) (void)hipEventDestroy(ev);
   if (url_blob_dev) (void)hipFree(url_blob_dev);
   if (sampling_blob_dev) (void)hipFree(sampling_blob_dev);
+  if (attr_blob_dev) (void)hipFree(attr_blob_dev);
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
     if (w->table) (void)hipFree(w->table);
     if (w->fp_table) (void)hipFree(w->fp_table);
     if (w->runs) (void)hipFree(w->runs);
     if (w->run_count) (void)hipFree(w->run_count);
+    if (w->attr_bits) (void)hipFree(w->attr_bits);
     if (w->pending) (void)hipEventDestroy(w->pending);
     if (w->dup_host) (void)hipHostFree(w->dup_host);
     if (w->dup_ready) (void)hipEventDestroy(w->dup_ready);
@@ -529,6 +490,8 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
   }
   int rc = e->build_sampling_tables();
   if (rc) { delete e; return rc; }
+  rc = e->build_attr_tables();
+  if (rc) { delete e; return rc; }
   rc = ensure_device();
   if (rc) { delete e; return rc; }
   if (e->has_url) {
@@ -537,6 +500,10 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
   }
   if (e->has_sampling) {
     rc = upload(e->sampling_blob_host, &e->sampling_blob_dev);
+    if (rc) { delete e; return rc; }
+  }
+  if (!e->attr_blob_host.empty()) {
+    rc = upload(e->attr_blob_host, &e->attr_blob_dev);
     if (rc) { delete e; return rc; }
   }
   *out = reinterpret_cast<ose_engine*>(e);
@@ -560,6 +527,9 @@ int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info) {
   info->max_template_name = e->max_name;
   info->inverse_sampling = e->inverse;
   info->traffic_sampling_ratio = e->traffic.sampling_ratio;
+  info->n_attr_rules = e->attr_n_rules;
+  info->n_attr_keys = (uint32_t)e->attr_keys.size();
+  info->attr_host_rules = e->attr_host_rules;
   return 0;
 }
 
@@ -570,6 +540,7 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   Workspace* ws = e->acquire_ws(nullptr);
   int rc = ws->reserve(e->workspace_bytes(n_spans));
   if (!rc && e->has_sampling) rc = ws->reserve_table(n_spans);
+  if (!rc && e->attr_n_dev) rc = ws->reserve_attr(n_spans);
   e->release_ws(ws, nullptr);
   return rc;
 }

@@ -19,6 +19,7 @@ int ensure_device();
 bool stream_capturing(hipStream_t st);
 struct Engine;
 void release_exchange_scratch(const Engine* e);   // shard_host.cpp
+void release_batch_pool(Engine* e);                // batch.cpp
 
 // Device scratch for one in-flight call (look-back status words, sort
 // buffers, partial records).  Engines keep a pool so concurrent callers never
@@ -42,6 +43,9 @@ struct Workspace {
   uint32_t* run_count = nullptr;
   uint64_t runs_slots = 0;
   int reserve_runs();
+  uint64_t* attr_bits = nullptr;   // span_attribute bits evaluated on the GPU (attr_host.cpp)
+  uint64_t attr_bits_cap = 0;
+  int reserve_attr(uint64_t n_spans);
   // SAMPLE + TEMPLATE in one call: the fast path's dup flag is copied here and
   // read by the host after the URL launches are queued (run_stages), so the
   // slow-path launches are only queued when a trace id repeats
@@ -64,9 +68,18 @@ struct Engine {
   uint8_t* sampling_blob_dev = nullptr;
   std::unordered_map<std::string, uint32_t> service_ids;
   uint32_t sampling_n_lat = 0, sampling_n_attr = 0;
+  // span_attribute rules: all of them (attr_n_rules), the GPU-evaluated ones
+  // (attr_n_dev, attr_kernel.hip) and the keys those read
+  std::vector<uint8_t> attr_blob_host;
+  uint8_t* attr_blob_dev = nullptr;
+  uint32_t attr_n_rules = 0, attr_n_dev = 0;
+  uint64_t attr_host_rules = 0;
+  std::vector<std::string> attr_keys;
 
   std::mutex mu;
   std::vector<Workspace*> pool, free_ws;
+  std::vector<void*> batch_pool;   // released ose_batch slabs (batch.cpp)
+  size_t batch_pool_bytes = 0;
 
   // ose_profile_*: (kernel name, start, stop) per launch
   bool profiling = false;
@@ -85,6 +98,7 @@ struct Engine {
   hipStream_t take_stream();
   void give_stream(hipStream_t s);
   int build_sampling_tables();
+  int build_attr_tables();
   size_t workspace_bytes(uint64_t n_spans) const;
 };
 
@@ -95,6 +109,8 @@ struct Engine {
 int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
                  hipStream_t st, Workspace* ws, std::function<int()>* tail = nullptr);
 size_t sampling_scratch_bytes(uint64_t n_spans);
+// the attr_match bits the trace stage reads for this call (attr_host.cpp)
+int resolve_attr_match(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, const uint64_t** out);
 int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
              const ose_rand* rnd, hipStream_t st, Workspace* ws);
 size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources);

@@ -3,8 +3,12 @@
 #include "host.hpp"
 
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <set>
+#include <thread>
 
 #include "span_attr.hpp"
 #include "urlparse.hpp"
@@ -45,6 +49,8 @@ void HostBatch::bind() {
   cols.scope_size = scope_size.data();
   cols.scope_resource = scope_resource.data();
   cols.attr_match = attr_match.data();
+  cols.attr_type = cols.n_attr_keys ? attr_type.data() : nullptr;
+  cols.attr_val = cols.n_attr_keys ? attr_val.data() : nullptr;
   outs.keep = keep.data();
   outs.trace_count = trace_count.data();
   outs.trace_first_span = trace_first_span.data();
@@ -117,6 +123,7 @@ TracesProcessor::TracesProcessor(ProcKind k, const Json& cfg) : kind_(k), cfg_js
           if (!e.empty() && err_.empty()) err_ = e;
         }
     if (attr_preds_.size() > 64 && err_.empty()) err_ = "more than 64 span_attribute rules are not supported";
+    attr_plan_ = plan_attr_rules(sampling_);
   }
   if (err_.empty() && has_url_) {
     // newUrlTemplateProcessor errors (rule parsing, custom id regexps) are
@@ -132,7 +139,7 @@ uint32_t TracesProcessor::stages() const {
   return (has_sampling_ ? OSE_STAGE_SAMPLE : 0) | (has_url_ ? OSE_STAGE_TEMPLATE : 0) | (has_traffic_ ? OSE_STAGE_SIZE : 0);
 }
 
-int TracesProcessor::ensure_engine() {
+int TracesProcessor::ensure_engine() {   // callers hold mu_
   if (eng_) return 0;
   Json root = Json::object();
   if (kind_ == ProcKind::Pipeline) root = cfg_json_;
@@ -168,6 +175,7 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
     return r;
   };
   uint32_t scope_idx = 0;
+  std::vector<std::pair<std::vector<uint8_t>, std::vector<uint64_t>>> attr_cols(attr_plan_.keys.size());
   for (size_t ri = 0; ri < t.resource_spans.size(); ri++) {
     const ResourceSpans& rs = t.resource_spans[ri];
     const AttrMap& ra = rs.resource_attrs;
@@ -222,13 +230,35 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
         hb->scope.push_back(scope_idx);
         hb->span_size.push_back((uint32_t)sizer.span(sp));
         hb->name_len.push_back((uint32_t)sp.name.size());
+        // span_attribute: the "json" conditions are evaluated here; the
+        // others on the GPU from the span's value of each rule key
         uint64_t am = 0;
-        for (uint64_t m = attr_res; m; m &= m - 1) {
+        for (uint64_t m = attr_res & attr_plan_.host_mask; m; m &= m - 1) {
           const int k = __builtin_ctzll(m);
           if (const Value* av = sp.attrs.Get(attr_preds_[k].key()))
             if (attr_preds_[k].eval(*av)) am |= 1ull << k;
         }
         hb->attr_match.push_back(am);
+        for (size_t k = 0; k < attr_plan_.keys.size(); k++) {
+          uint8_t ty = OSE_ATTR_ABSENT;
+          uint64_t v = 0;
+          if (const Value* av = sp.attrs.Get(attr_plan_.keys[k])) {
+            switch (av->type) {
+              case Value::TStr: {
+                ty = OSE_ATTR_STR;
+                const ose_strref r = add_str(av->s);
+                v = (uint64_t)r.off | ((uint64_t)r.len << 32);
+                break;
+              }
+              case Value::TInt: ty = OSE_ATTR_INT; v = (uint64_t)av->i; break;
+              case Value::TDouble: ty = OSE_ATTR_DOUBLE; std::memcpy(&v, &av->d, 8); break;
+              case Value::TBool: ty = OSE_ATTR_BOOL; v = av->b ? 1 : 0; break;
+              default: ty = OSE_ATTR_OTHER; break;
+            }
+          }
+          attr_cols[k].first.push_back(ty);
+          attr_cols[k].second.push_back(v);
+        }
         const AttrMap& a = sp.attrs;
         // sampling: AsString(http.route) (latency.go:64-68)
         const Value* route = a.Get("http.route");
@@ -277,6 +307,12 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
   hb->cols.n_scopes = scope_idx;
   hb->cols.n_attrsets = (uint32_t)hb->attrsets.size();
   hb->cols.arena_bytes = arena.size();
+  hb->cols.n_attr_keys = (uint32_t)attr_cols.size();
+  for (auto& kc : attr_cols) {   // key-major
+    hb->attr_type.insert(hb->attr_type.end(), kc.first.begin(), kc.first.end());
+    hb->attr_val.insert(hb->attr_val.end(), kc.second.begin(), kc.second.end());
+  }
+  if (hb->attr_type.empty()) hb->attr_type.push_back(0), hb->attr_val.push_back(0);
   // outputs (vectors never empty so data() is non-null)
   size_t nn = std::max<size_t>(n, 1);
   hb->keep.assign(nn, 0);
@@ -365,24 +401,46 @@ void TracesProcessor::Apply(HostBatch& hb, Traces& td) {
     }
   }
   if (st & OSE_STAGE_SIZE) {
+    std::lock_guard<std::mutex> g(mu_);
     for (size_t a = 0; a < hb.attrsets.size(); a++)
       if (o.attrset_bytes[a]) data_size_[hb.attrsets[a]] += o.attrset_bytes[a];
     accepted_spans_ += o.accepted_spans[0];
   }
 }
 
-int TracesProcessor::ProcessTraces(Traces& td) {
-  int rc = ensure_engine();
-  if (rc) return rc;
+int TracesProcessor::ProcessTraces(Traces& td, double* phase_s) {
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now();
+  auto lap = [&](int k) {
+    if (!phase_s) return;
+    auto t = clk::now();
+    phase_s[k] += std::chrono::duration<double>(t - t0).count();
+    t0 = t;
+  };
+  ose_rand rnd{0, 0.0};
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    rc = ensure_engine();
+    if (rc) return rc;
+    rnd.seed = seed_ ^ (draws_ * 0x9E3779B97F4A7C15ull);
+    if (has_traffic_) rnd.traffic_u = next_uniform();   // rand.Float64() per call (processor.go:72)
+  }
   auto hb = Columnarize(td);
-  ose_rand rnd{seed_ ^ (draws_ * 0x9E3779B97F4A7C15ull), 0.0};
-  if (has_traffic_) rnd.traffic_u = next_uniform();   // rand.Float64() per call (processor.go:72)
+  lap(0);
   ose_columns dims = hb->cols;
   ose_batch* b = nullptr;
   rc = ose_batch_acquire(eng_, &dims, &b);
   if (rc) return rc;
   ose_columns* c = ose_batch_columns(b);
   ose_outputs* o = ose_batch_outputs(b);
+  // outputs Apply does not read are not produced (no per-trace compaction,
+  // no D2H): one decision per call in BATCH mode, keep bytes otherwise
+  o->trace_first_span = nullptr;
+  o->trace_level = nullptr;
+  o->trace_ratio = nullptr;
+  o->res_bytes = nullptr;
+  if (group_mode != OSE_GROUP_BATCH) o->trace_count = nullptr, o->trace_keep = nullptr;
   const uint64_t n = hb->cols.n_spans;
   const uint32_t R = hb->cols.n_resources, S = hb->cols.n_scopes, A = hb->cols.n_attrsets;
   auto cp = [](const void* dst, const void* src, size_t bytes) {
@@ -409,13 +467,19 @@ int TracesProcessor::ProcessTraces(Traces& td) {
   cp(c->scope_size, hb->cols.scope_size, 4 * S);
   cp(c->scope_resource, hb->cols.scope_resource, 4 * S);
   cp(c->attr_match, hb->cols.attr_match, 8 * n);
+  if (hb->cols.n_attr_keys) {
+    cp(c->attr_type, hb->cols.attr_type, (size_t)hb->cols.n_attr_keys * n);
+    cp(c->attr_val, hb->cols.attr_val, 8 * (size_t)hb->cols.n_attr_keys * n);
+  }
   std::memset(o->attrset_bytes, 0, 8 * (size_t)A);
   std::memset(o->accepted_spans, 0, 8);
+  lap(1);
   rc = ose_process(eng_, b, stages(), group_mode, &rnd);
   if (rc) { ose_batch_release(b); return rc; }
+  lap(2);
   // read back into the host batch and apply
   cp(hb->outs.keep, o->keep, n);
-  if (stages() & OSE_STAGE_SAMPLE) {
+  if ((stages() & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_BATCH) {
     cp(hb->outs.trace_count, o->trace_count, 4);
     cp(hb->outs.trace_keep, o->trace_keep, 1);
   }
@@ -427,7 +491,9 @@ int TracesProcessor::ProcessTraces(Traces& td) {
   cp(hb->outs.attrset_bytes, o->attrset_bytes, 8 * (size_t)A);
   cp(hb->outs.accepted_spans, o->accepted_spans, 8);
   ose_batch_release(b);
+  lap(3);
   Apply(*hb, td);
+  lap(4);
   return 0;
 }
 
@@ -542,6 +608,77 @@ int osehost_apply(void* p, void* hb, char** out) {
   return 0;
 }
 void osehost_batch_free(void* hb) { delete static_cast<HostBatch*>(hb); }
+
+// Drop-in timing (tools/dropin_bench.py): ConsumeTraces end to end on the
+// C++ host mirror.  traces_json is a JSON array of OTLP/JSON Traces; thread t
+// of `threads` consumes items t, t+threads, ... `reps` times each, every call
+// on a fresh copy of its item (the copy is outside the timed call).
+// out[0] wall s, [1] calls, [2] spans, [3..7] summed phase s (columnarise,
+// pinned fill, ose_process, read-back, apply), [8..11] per-call latency
+// p50/p90/p99/max s.  Returns 0 or the first failing call's code.
+int osehost_bench(void* p, const char* traces_json, uint32_t reps, uint32_t threads, double* out) {
+  auto* tp = static_cast<TracesProcessor*>(p);
+  std::vector<Traces> items;
+  try {
+    Json arr = parse_json(traces_json);
+    if (!arr.is_arr()) throw std::runtime_error("expected a JSON array of Traces");
+    for (auto& t : arr.arr) items.push_back(traces_from_json(t));
+  } catch (const std::exception& e) {
+    g_host_err = e.what();
+    return OSE_EINVAL;
+  }
+  if (threads < 1) threads = 1;
+  std::vector<std::vector<double>> lat(threads);
+  std::vector<std::array<double, 5>> ph(threads);
+  std::atomic<int> first_rc{0};
+  std::string first_err;
+  std::mutex err_mu;
+  uint64_t spans = 0;
+  for (auto& t : items)
+    for (auto& rs : t.resource_spans)
+      for (auto& ss : rs.scope_spans) spans += ss.spans.size();
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now();
+  std::vector<std::thread> th;
+  for (uint32_t w = 0; w < threads; w++)
+    th.emplace_back([&, w]() {
+      ph[w].fill(0.0);
+      for (uint32_t r = 0; r < reps; r++)
+        for (size_t i = w; i < items.size(); i += threads) {
+          Traces td = items[i];
+          auto a = clk::now();
+          int rc = tp->ProcessTraces(td, ph[w].data());
+          lat[w].push_back(std::chrono::duration<double>(clk::now() - a).count());
+          if (rc) {
+            int z = 0;
+            if (first_rc.compare_exchange_strong(z, rc)) {
+              std::lock_guard<std::mutex> g(err_mu);
+              first_err = ose_last_error();   // thread-local in the worker
+            }
+            return;
+          }
+        }
+    });
+  for (auto& x : th) x.join();
+  const double wall = std::chrono::duration<double>(clk::now() - t0).count();
+  std::vector<double> all;
+  for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double q) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, (size_t)(q * (double)all.size()))]; };
+  out[0] = wall;
+  out[1] = (double)all.size();
+  out[2] = (double)spans * reps;
+  for (int k = 0; k < 5; k++) {
+    out[3 + k] = 0;
+    for (auto& v : ph) out[3 + k] += v[k];
+  }
+  out[8] = pct(0.50);
+  out[9] = pct(0.90);
+  out[10] = pct(0.99);
+  out[11] = all.empty() ? 0.0 : all.back();
+  if (first_rc.load()) { g_host_err = first_err; return first_rc.load(); }
+  return 0;
+}
 
 char* osehost_metrics_json(void* p) { return dup_cstr(static_cast<TracesProcessor*>(p)->MetricsJson()); }
 // Traces round trip through the pdata model (fixture sanity)

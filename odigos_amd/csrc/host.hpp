@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -35,6 +36,8 @@ struct HostBatch {
   std::vector<ose_strref> path, route;
   std::vector<uint32_t> res_svc, res_svc_str, res_attrset, res_size, scope_size, scope_resource;
   std::vector<uint8_t> res_url_ok;
+  std::vector<uint8_t> attr_type;           // key-major [n_attr_keys * n]
+  std::vector<uint64_t> attr_val;
   // outputs
   std::vector<uint8_t> keep, trace_keep, trace_level, url_out, tmpl_arena;
   std::vector<uint32_t> trace_count, trace_first_span, device_status;
@@ -61,8 +64,11 @@ class TracesProcessor {
   ProcKind kind() const { return kind_; }
   uint32_t stages() const;
   // processTraces; returns 0 or an OSE_E* code (the hot path never fails in
-  // the reference; an engine failure here is surfaced, never masked)
-  int ProcessTraces(Traces& td);
+  // the reference; an engine failure here is surfaced, never masked).
+  // Re-entrant: receivers and groupbytrace call ConsumeTraces from several
+  // goroutines.  phase_s (optional, 5 entries) accumulates the seconds spent
+  // in columnarise / pinned fill / ose_process / read-back / apply.
+  int ProcessTraces(Traces& td, double* phase_s = nullptr);
   // test seams: the same steps without the device
   std::unique_ptr<HostBatch> Columnarize(const Traces& td) const;
   void Apply(HostBatch& hb, Traces& td);
@@ -80,12 +86,16 @@ class TracesProcessor {
   bool has_url_ = false, has_sampling_ = false, has_traffic_ = false;
   std::map<std::string, uint32_t> services_;
   std::vector<SpanAttrPredicate> attr_preds_;   // span_attribute rules, level order
+  AttrPlan attr_plan_;                          // which of them the GPU evaluates, from which key column
   ose_engine* eng_ = nullptr;
   uint64_t seed_ = 0x0D16A5EEDull;
   uint64_t draws_ = 0;
   // traffic metrics state (otelcol_odigos_trace_data_size / _accepted_spans)
   std::map<std::vector<std::pair<std::string, std::string>>, int64_t> data_size_;
   int64_t accepted_spans_ = 0;
+  // guards eng_ creation, the rand.Float64 stream and the traffic counters
+  // (the reference's otel counters and math/rand are goroutine-safe)
+  mutable std::mutex mu_;
   int ensure_engine();
   double next_uniform();
 };

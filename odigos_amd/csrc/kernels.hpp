@@ -278,4 +278,20 @@ void launch_size_spans(const SizeKernelArgs& a, hipStream_t st);
 void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st);
 void launch_size_resources(const SizeKernelArgs& a, hipStream_t st);
 
+// span_attribute conditions (attr_kernel.hip): out[i] = host_bits[i] &
+// host_mask | the bits of the GPU-evaluated rules the span meets.
+struct AttrArgs {
+  uint64_t n_spans;
+  const uint8_t* type;         // [n_keys * n_spans] OSE_ATTR_*
+  const uint64_t* val;         // [n_keys * n_spans]
+  const uint8_t* arena;
+  const uint32_t* resource;
+  const uint32_t* res_svc;
+  const uint64_t* host_bits;   // may be null
+  uint64_t host_mask;
+  const uint8_t* cfg;          // AttrCfgDev blob
+  uint64_t* out;
+};
+void launch_attr_eval(const AttrArgs& a, hipStream_t st);
+
 }  // namespace ose

@@ -220,6 +220,10 @@ Json value_to_json(const Value& v) {
     case Value::TStr: o.set("stringValue", Json::str(v.s)); break;
     case Value::TInt: o.set("intValue", Json::str(std::to_string(v.i))); break;
     case Value::TDouble: {
+      if (!std::isfinite(v.d)) {   // protobuf JSON mapping: "NaN", "Infinity", "-Infinity"
+        o.set("doubleValue", Json::str(v.d != v.d ? "NaN" : v.d > 0 ? "Infinity" : "-Infinity"));
+        break;
+      }
       char buf[64];
       auto r = std::to_chars(buf, buf + sizeof buf, v.d);
       o.set("doubleValue", Json::number(std::string(buf, r.ptr)));

@@ -234,8 +234,6 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
       return fail(OSE_EINVAL, "SAMPLE stage needs status, resource, res_svc, res_svc_str and keep");
     if (!c->trace_id && (group_mode == OSE_GROUP_TRACE_ID || o->trace_keep || o->trace_level || o->trace_ratio))
       return fail(OSE_EINVAL, "SAMPLE stage needs the trace_id column");
-    if (e->sampling_n_attr && !c->attr_match && !c->svc_match)
-      return fail(OSE_EINVAL, "span_attribute rules need the attr_match column");
     if (lat && (!c->start_ns || !c->end_ns || (!c->route_match && (!c->route || !c->arena))))
       return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns and route + arena (or route_match)");
   } else if (!c->res_svc_str && c->n_resources) {
@@ -321,7 +319,12 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.error = err;
   a.batch_keep = misc + kBatchKeepWord;
   a.route_match = c->route_match;
-  a.attr_match = e->sampling_n_attr ? c->attr_match : nullptr;
+  {
+    const uint64_t* am = nullptr;
+    const int ar = resolve_attr_match(e, c, ws, st, &am);
+    if (ar) return ar;
+    a.attr_match = e->sampling_n_attr ? am : nullptr;
+  }
   a.svc_match = c->svc_match;
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
   a.n_long = misc + 12;

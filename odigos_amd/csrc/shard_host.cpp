@@ -153,7 +153,6 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
     return fail(OSE_EINVAL, "ose_shard_pack needs trace_id, status, resource, res_svc, res_svc_str");
   if (n && e->sampling_n_lat && (!c->start_ns || !c->end_ns || (!c->route_match && (!c->route || !c->arena))))
     return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns and route + arena (or route_match)");
-  if (n && e->sampling_n_attr && !c->attr_match) return fail(OSE_EINVAL, "span_attribute rules need the attr_match column");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipMemsetAsync(counts, 0, 8 * (size_t)n_ranks, st));
   if (n == 0) return 0;
@@ -180,7 +179,15 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.route = c->route;
   a.arena = c->arena;
   a.route_match = c->route_match;
-  a.attr_match = e->sampling_n_attr ? c->attr_match : nullptr;
+  {
+    const uint64_t* am = nullptr;
+    rc = resolve_attr_match(e, c, ws, st, &am);
+    if (rc) {
+      e->release_ws(ws, st);
+      return rc;
+    }
+    a.attr_match = e->sampling_n_attr ? am : nullptr;
+  }
   a.res_svc = c->res_svc;
   a.res_svc_str = c->res_svc_str;
   a.cfg = e->sampling_blob_dev;

@@ -13,22 +13,76 @@ namespace ose {
 
 // ---------------- strconv ----------------
 
-// strconv.ParseFloat(s, 64): the whole string must parse; out-of-range
-// magnitudes are an error (ErrRange), underflow rounds to zero silently.
+// strconv.ParseFloat(s, 64): the whole string must be a Go float literal
+// (readFloat: optional sign, decimal or "0x" mantissa — the latter needs a
+// 'p' exponent — with '_' digit separators as underscoreOK allows; or
+// [+-]inf / [+-]infinity / nan, case-insensitive).  Out-of-range magnitudes
+// are an error (ErrRange); underflow rounds to zero silently.
 bool go_parse_float(const std::string& s, double& out) {
-  if (s.empty() || std::isspace((unsigned char)s[0])) return false;
-  // strtod extensions Go rejects: "nan(...)" payloads and "infinity" tails
-  std::string low;
-  for (char ch : s) low += (char)std::tolower((unsigned char)ch);
-  size_t k = (low[0] == '+' || low[0] == '-') ? 1 : 0;
-  const std::string body = low.substr(k);
-  if (body.find('(') != std::string::npos) return false;
-  if (body.compare(0, 3, "inf") == 0 && body != "inf" && body != "infinity") return false;
-  if (body.compare(0, 3, "nan") == 0 && (body != "nan" || k)) return false;
+  const size_t n = s.size();
+  if (n == 0) return false;
+  auto lc = [&](size_t i) { return (char)std::tolower((unsigned char)s[i]); };
+  size_t i = (s[0] == '+' || s[0] == '-') ? 1 : 0;
+  // special values
+  std::string rest;
+  for (size_t k = i; k < n; k++) rest += lc(k);
+  if (rest == "inf" || rest == "infinity") {
+    out = s[0] == '-' ? -HUGE_VAL : HUGE_VAL;
+    return true;
+  }
+  if (rest == "nan") {
+    if (i) return false;   // no sign on NaN
+    out = std::nan("");
+    return true;
+  }
+  const bool hex = i + 2 < n && s[i] == '0' && lc(i + 1) == 'x';
+  size_t p = hex ? i + 2 : i;
+  bool digits = false, dot = false, under = false;
+  for (; p < n; p++) {
+    const char c = lc(p);
+    if (c == '_') { under = true; continue; }
+    if (c == '.' && !dot) { dot = true; continue; }
+    if (std::isdigit((unsigned char)c) || (hex && c >= 'a' && c <= 'f')) { digits = true; continue; }
+    break;
+  }
+  if (!digits) return false;
+  if (p < n && lc(p) == (hex ? 'p' : 'e')) {
+    p++;
+    if (p < n && (s[p] == '+' || s[p] == '-')) p++;
+    if (p >= n || !std::isdigit((unsigned char)s[p])) return false;
+    while (p < n && (std::isdigit((unsigned char)s[p]) || s[p] == '_')) under |= s[p++] == '_';
+  } else if (hex) {
+    return false;
+  }
+  if (p != n) return false;
+  std::string lit;
+  if (under) {
+    // underscoreOK: each '_' sits between two digits (a base prefix counts as one)
+    char prev = i == 0 && !hex ? '^' : '^';
+    size_t q = i;
+    if (hex) { prev = '0'; q = i + 2; }
+    for (; q < n; q++) {
+      const char c = lc(q);
+      const bool dig = std::isdigit((unsigned char)c) || (hex && c >= 'a' && c <= 'f');
+      if (dig) prev = '0';
+      else if (c == '_') {
+        if (prev != '0') return false;
+        prev = '_';
+      } else {
+        if (prev == '_') return false;
+        prev = '!';
+      }
+    }
+    if (prev == '_') return false;
+    for (char c : s)
+      if (c != '_') lit += c;
+  } else {
+    lit = s;
+  }
   errno = 0;
   char* end = nullptr;
-  const double v = std::strtod(s.c_str(), &end);
-  if (end != s.c_str() + s.size()) return false;
+  const double v = std::strtod(lit.c_str(), &end);
+  if (end != lit.c_str() + lit.size()) return false;
   if (errno == ERANGE && std::isinf(v)) return false;
   out = v;
   return true;
@@ -492,6 +546,25 @@ bool SpanAttrPredicate::eval(const Value& attr) const {
     return false;   // "exists" / "jsonpath_exists": accepted by Validate, never satisfied (:241-315)
   }
   return false;
+}
+
+AttrPlan plan_attr_rules(const SamplingConfig& c) {
+  AttrPlan p;
+  int k = 0;
+  for (auto* lvl : {&c.global_rules, &c.service_rules, &c.endpoint_rules})
+    for (auto& r : *lvl) {
+      if (r.rtype != RuleType::SpanAttribute) continue;
+      if (r.attr.condition_type == "json") {
+        p.rule_key.push_back(-1);
+        if (k < 64) p.host_mask |= 1ull << k;
+      } else {
+        auto it = std::find(p.keys.begin(), p.keys.end(), r.attr.attribute_key);
+        if (it == p.keys.end()) it = p.keys.insert(p.keys.end(), r.attr.attribute_key);
+        p.rule_key.push_back((int)(it - p.keys.begin()));
+      }
+      k++;
+    }
+  return p;
 }
 
 }  // namespace ose

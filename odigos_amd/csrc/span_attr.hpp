@@ -50,6 +50,16 @@ class SpanAttrPredicate {
   std::vector<JsonPathStep> path_;
 };
 
+// Which span_attribute rules the engine evaluates on the GPU, and from which
+// attr_type / attr_val column (include/odigos_amd.h): every rule with a
+// string / number / boolean condition; "json" conditions stay with the shim.
+struct AttrPlan {
+  std::vector<std::string> keys;   // distinct attribute_key of the GPU rules, level order
+  std::vector<int> rule_key;       // per span_attribute rule (level order): key column, -1 = shim
+  uint64_t host_mask = 0;          // attr_match bits the shim still computes
+};
+AttrPlan plan_attr_rules(const SamplingConfig& c);
+
 // helpers exposed for tests
 bool go_parse_float(const std::string& s, double& out);
 bool go_parse_bool(const std::string& s, bool& out);

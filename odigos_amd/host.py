@@ -66,6 +66,8 @@ def attr_value(v) -> dict:
     if isinstance(v, int):
         return {"intValue": str(v)}
     if isinstance(v, float):
+        if v != v or v in (float("inf"), float("-inf")):   # protobuf JSON mapping of non-finite doubles
+            return {"doubleValue": "NaN" if v != v else ("Infinity" if v > 0 else "-Infinity")}
         return {"doubleValue": v}
     if isinstance(v, dict) and len(v) == 1 and next(iter(v)).endswith("Value"):
         return v

@@ -47,6 +47,9 @@ XREC_BYTES = 56
 GROUP_TRACE_ID = 0
 GROUP_BATCH = 1
 
+# attr_type values (include/odigos_amd.h OSE_ATTR_*)
+ATTR_ABSENT, ATTR_STR, ATTR_INT, ATTR_DOUBLE, ATTR_BOOL, ATTR_OTHER = range(6)
+
 _p = C.c_void_p
 
 
@@ -69,7 +72,8 @@ class Columns(C.Structure):
     _fields_ = [
         ("n_spans", C.c_uint64), ("n_resources", C.c_uint32), ("n_scopes", C.c_uint32),
         ("n_attrsets", C.c_uint32), ("_pad", C.c_uint32), ("arena_bytes", C.c_uint64),
-    ] + [(f, _p) for f in COLUMN_FIELDS] + [("svc_match", _p)]
+    ] + [(f, _p) for f in COLUMN_FIELDS] + [("svc_match", _p), ("n_attr_keys", C.c_uint32), ("_pad2", C.c_uint32),
+                                            ("attr_type", _p), ("attr_val", _p)]
 
 
 class Outputs(C.Structure):
@@ -85,7 +89,8 @@ class Outputs(C.Structure):
 
 class EngineInfo(C.Structure):
     _fields_ = [("stages", C.c_uint32), ("max_template_name", C.c_uint32),
-                ("inverse_sampling", C.c_int64), ("traffic_sampling_ratio", C.c_double)]
+                ("inverse_sampling", C.c_int64), ("traffic_sampling_ratio", C.c_double),
+                ("n_attr_rules", C.c_uint32), ("n_attr_keys", C.c_uint32), ("attr_host_rules", C.c_uint64)]
 
 
 _lib = None
@@ -113,6 +118,7 @@ def lib() -> C.CDLL:
         "ose_engine_destroy": (None, [_p]),
         "ose_engine_service_id": (C.c_uint32, [_p, C.c_char_p, C.c_size_t]),
         "ose_engine_get_info": (C.c_int, [_p, C.POINTER(EngineInfo)]),
+        "ose_engine_attr_key": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),
         "ose_batch_columns": (C.POINTER(Columns), [_p]),
         "ose_batch_outputs": (C.POINTER(Outputs), [_p]),
@@ -145,6 +151,7 @@ def lib() -> C.CDLL:
         "osehost_batch_columns": (C.POINTER(Columns), [_p]),
         "osehost_batch_outputs": (C.POINTER(Outputs), [_p]),
         "osehost_apply": (C.c_int, [_p, _p, C.POINTER(_p)]),
+        "osehost_bench": (C.c_int, [_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]),
         "osehost_batch_free": (None, [_p]),
         "osehost_metrics_json": (_p, [_p]),
         "osehost_roundtrip": (_p, [C.c_char_p]),

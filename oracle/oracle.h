@@ -66,19 +66,47 @@ int orc_url_process(const orc_url* u, const ose_columns* c, ose_outputs* o,
 #define ORC_RULE_ERROR    0
 #define ORC_RULE_LATENCY  1
 #define ORC_RULE_SERVICE  2
-#define ORC_RULE_ATTR     3   /* span_attribute: the per-span condition comes from
-                                 the attr_match column (bit = index among the
-                                 span_attribute rules, level order) */
+#define ORC_RULE_ATTR     3   /* span_attribute (spanattribute.go:126-320): the
+                                 per-span condition is restated here from the
+                                 attr_type / attr_val column attr_col when the
+                                 batch carries those columns and attr_col >= 0;
+                                 otherwise it is bit (index among the
+                                 span_attribute rules, level order) of attr_match */
 typedef struct orc_rule {
   int32_t level;        /* 0 global, 1 service, 2 endpoint (rule_engine.go:56-60) */
   int32_t type;         /* ORC_RULE_* */
-  uint32_t svc;         /* http_latency / service_name */
+  uint32_t svc;         /* http_latency / service_name / span_attribute service */
   uint32_t route_len;   /* http_latency http_route */
   const char* route;
   int64_t threshold;    /* http_latency threshold (ms) */
-  double ratio;         /* service_name sampling_ratio */
+  double ratio;         /* service_name / span_attribute sampling_ratio */
   double fallback;      /* fallback_sampling_ratio */
+  /* span_attribute */
+  int32_t attr_col;     /* key column of its attribute_key, -1 = from attr_match */
+  uint32_t attr_expected_len;
+  const char* attr_cond;       /* condition_type */
+  const char* attr_op;         /* operation */
+  const char* attr_expected;   /* expected_value */
 } orc_rule;
+
+/* ---- span_attribute per-span condition (oracle/span_attr.c) -------------- */
+typedef struct orc_attr_cond {
+  int cond;             /* 0 string, 1 number, 2 boolean */
+  char op[32];
+  char* expected;
+  size_t expected_len;
+  orc_re* re;           /* regex: NULL when regexp.Compile fails */
+  int num_ok, bool_ok, bool_val;
+  double num;
+} orc_attr_cond;
+int orc_attr_cond_init(orc_attr_cond* a, const char* cond, const char* op, const char* expected, size_t elen);
+void orc_attr_cond_free(orc_attr_cond* a);
+/* the condition on one span's value (attr_type / attr_val entry), given that
+ * the key was found (type != OSE_ATTR_ABSENT) */
+int orc_attr_cond_eval(const orc_attr_cond* a, uint8_t type, uint64_t val, const uint8_t* arena);
+/* strconv.ParseFloat(s, 64) / strconv.ParseBool: 1 = ok */
+int orc_go_parse_float(const char* s, size_t n, double* out);
+int orc_go_parse_bool(const char* s, size_t n, int* out);
 typedef struct orc_sampling orc_sampling;
 orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules);
 void orc_sampling_free(orc_sampling* s);

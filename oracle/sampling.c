@@ -25,6 +25,7 @@
 struct orc_sampling {
   int n;
   orc_rule* rules;   /* copies; route strings owned */
+  orc_attr_cond* conds;   /* span_attribute rules with attr_col >= 0 */
   int* lat_index;    /* index of each http_latency rule among them (route_match bit) */
   int* attr_index;   /* index of each span_attribute rule among them (attr_match bit) */
 };
@@ -35,6 +36,7 @@ orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules) {
   s->rules = (orc_rule*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(orc_rule));
   s->lat_index = (int*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(int));
   s->attr_index = (int*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(int));
+  s->conds = (orc_attr_cond*)calloc(n_rules > 0 ? (size_t)n_rules : 1, sizeof(orc_attr_cond));
   int nl = 0, na = 0;
   for (int i = 0; i < n_rules; i++) {
     s->lat_index[i] = rules[i].type == ORC_RULE_LATENCY ? nl++ : -1;
@@ -46,13 +48,22 @@ orc_sampling* orc_sampling_create(const orc_rule* rules, int n_rules) {
     if (rules[i].route_len) memcpy(r, rules[i].route, rules[i].route_len);
     r[rules[i].route_len] = 0;
     s->rules[i].route = r;
+    if (rules[i].type == ORC_RULE_ATTR && rules[i].attr_col >= 0 &&
+        orc_attr_cond_init(&s->conds[i], rules[i].attr_cond, rules[i].attr_op, rules[i].attr_expected,
+                           rules[i].attr_expected_len) != 0)
+      s->rules[i].attr_col = -1;
+    s->rules[i].attr_cond = s->rules[i].attr_op = s->rules[i].attr_expected = NULL;
   }
   return s;
 }
 
 void orc_sampling_free(orc_sampling* s) {
   if (!s) return;
-  for (int i = 0; i < s->n; i++) free((void*)s->rules[i].route);
+  for (int i = 0; i < s->n; i++) {
+    free((void*)s->rules[i].route);
+    if (s->rules[i].type == ORC_RULE_ATTR && s->rules[i].attr_col >= 0) orc_attr_cond_free(&s->conds[i]);
+  }
+  free(s->conds);
   free(s->rules);
   free(s->lat_index);
   free(s->attr_index);
@@ -141,8 +152,22 @@ static eval_t eval_service(const orc_rule* r, const trace_view* t) {
 /* SpanAttributeRule.Evaluate (spanattribute.go:126-320) over the per-span
  * condition bits: (true, true, ratio) as soon as one span of the trace meets
  * it, else (false, false, fallback) — never matched-but-unsatisfied. */
-static eval_t eval_attr(const orc_rule* r, int attr_index, const trace_view* t) {
+static eval_t eval_attr(const orc_rule* r, const orc_attr_cond* cond, int attr_index, const trace_view* t) {
   const ose_columns* c = t->c;
+  if (r->attr_col >= 0 && c->attr_type && (uint32_t)r->attr_col < c->n_attr_keys) {
+    /* spanattribute.go:127-135: resources whose AsString(service.name) is the
+     * rule's service, then Get(AttributeKey) per span */
+    const uint64_t n = c->n_spans;
+    for (uint64_t k = 0; k < t->n; k++) {
+      const uint32_t i = t->spans[k];
+      if (r->svc == OSE_NONE || c->res_svc[c->resource[i]] != r->svc) continue;
+      const uint64_t j = (uint64_t)r->attr_col * n + i;
+      const uint8_t ty = c->attr_type[j];
+      if (ty == OSE_ATTR_ABSENT) continue;
+      if (orc_attr_cond_eval(cond, ty, c->attr_val[j], c->arena)) return (eval_t){1, 1, r->ratio};
+    }
+    return (eval_t){0, 0, r->fallback};
+  }
   for (uint64_t k = 0; k < t->n; k++)
     if ((c->attr_match[t->spans[k]] >> attr_index) & 1) return (eval_t){1, 1, r->ratio};
   return (eval_t){0, 0, r->fallback};
@@ -162,7 +187,7 @@ static void evaluate_level(const orc_sampling* s, int level, const trace_view* t
     switch (r->type) {
       case ORC_RULE_ERROR: e = eval_error(r, t); break;
       case ORC_RULE_LATENCY: e = eval_latency(r, s->lat_index[k], t); break;
-      case ORC_RULE_ATTR: e = eval_attr(r, s->attr_index[k], t); break;
+      case ORC_RULE_ATTR: e = eval_attr(r, &s->conds[k], s->attr_index[k], t); break;
       default: e = eval_service(r, t); break;
     }
     if (e.satisfied) {

@@ -19,7 +19,23 @@ _L = None
 
 class OrcRule(C.Structure):
     _fields_ = [("level", C.c_int32), ("type", C.c_int32), ("svc", C.c_uint32), ("route_len", C.c_uint32),
-                ("route", C.c_char_p), ("threshold", C.c_int64), ("ratio", C.c_double), ("fallback", C.c_double)]
+                ("route", C.c_char_p), ("threshold", C.c_int64), ("ratio", C.c_double), ("fallback", C.c_double),
+                ("attr_col", C.c_int32), ("attr_expected_len", C.c_uint32), ("attr_cond", C.c_char_p),
+                ("attr_op", C.c_char_p), ("attr_expected", C.c_char_p)]
+
+
+def attr_key_columns(cfg: dict) -> list[str]:
+    """The attr_type / attr_val key columns (include/odigos_amd.h): distinct
+    attribute_key of the span_attribute rules whose condition_type is not
+    "json", in level order (global, service, endpoint), config order inside."""
+    keys = []
+    for key in ("global_rules", "service_rules", "endpoint_rules"):
+        for r in cfg.get(key) or []:
+            d = r.get("rule_details") or {}
+            if r["type"] == "span_attribute" and d.get("condition_type") != "json":
+                if d.get("attribute_key") not in keys:
+                    keys.append(d.get("attribute_key"))
+    return keys
 
 
 def lib():
@@ -41,6 +57,8 @@ def lib():
             "orc_sampling_process": (C.c_int, [_p, C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32,
                                                C.POINTER(native.Rand), C.c_int]),
             "orc_trace_uniform": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64]),
+            "orc_go_parse_float": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_double)]),
+            "orc_go_parse_bool": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
             "orc_size_process": (C.c_int, [C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32, C.c_uint32,
                                            C.POINTER(native.Outputs), C.c_int64, C.c_double, C.c_double]),
             "orc_size_process_mt": (C.c_int, [C.POINTER(native.Columns), C.POINTER(native.Outputs), C.c_uint32,
@@ -136,6 +154,7 @@ class SamplingOracle:
     def __init__(self, cfg: dict | None = None):
         cfg = cfg or {}
         self.services = intern_services(cfg)
+        keys = attr_key_columns(cfg)
         rules = []
         for level, key in enumerate(("global_rules", "service_rules", "endpoint_rules")):
             for r in cfg.get(key) or []:
@@ -143,9 +162,15 @@ class SamplingOracle:
                 if r["type"] not in self.TYPES:
                     raise ValueError(f"oracle: rule type {r['type']} not restated")
                 route = (d.get("http_route") or "").encode()
+                col, cond, op, exp = -1, b"", b"", b""
+                if r["type"] == "span_attribute" and d.get("condition_type") != "json":
+                    col = keys.index(d.get("attribute_key"))
+                    cond = (d.get("condition_type") or "").encode()
+                    op = (d.get("operation") or "").encode()
+                    exp = (d.get("expected_value") or "").encode("utf-8", "surrogateescape")
                 rules.append(OrcRule(level, self.TYPES[r["type"]], self.services.get(d.get("service_name"), native.OSE_NONE),
                                      len(route), route, int(d.get("threshold", 0)), float(d.get("sampling_ratio", 0.0)),
-                                     float(d.get("fallback_sampling_ratio", 0.0))))
+                                     float(d.get("fallback_sampling_ratio", 0.0)), col, len(exp), cond, op, exp))
         arr = (OrcRule * max(len(rules), 1))(*rules)
         self._keep = arr
         self.h = lib().orc_sampling_create(arr, len(rules))

@@ -13,6 +13,8 @@ GPU (@gpu):
   * TEMPLATE | SIZE captured into a hipGraph (torch.cuda.graph) replays to
     the same outputs as eager calls; SAMPLE by trace id refuses capture.
 """
+import ctypes as C
+import json
 import threading
 
 import numpy as np
@@ -168,3 +170,86 @@ def test_gpu_graph_capture_refuses_trace_id_sampling():
     assert SamplingOracle(c3_sampling_config()).process(g.cols, ho.outs, native.GROUP_BATCH, 0, 1) == 0
     n = g.cols.n_spans
     np.testing.assert_array_equal(db.out_numpy("keep", n=n), ho.view("keep", np.uint8)[:n])
+
+
+@pytest.mark.gpu
+def test_gpu_concurrent_pipeline_counters():
+    """odigosurltemplate + odigostrafficmetrics from 6 threads: every output
+    and the summed otel counters equal the single-threaded run's (the traffic
+    counters are shared state, processor.go:76-81)."""
+    from odigos_amd import host
+    cfg = {"odigosurltemplate": {}, "odigostrafficmetrics": {"res_attributes_keys": ["service.name", "k8s.pod.name"]}}
+    from tools.dropin_bench import batch_items
+    items = batch_items(12, 700, 0x0D16C0DE)
+    ref = host.Processor("pipeline", cfg)
+    want = [ref.consume(td) for td in items]
+    p = host.Processor("pipeline", cfg)
+    got = [None] * len(items)
+    errors = []
+
+    def worker(t):
+        try:
+            for k in range(t, len(items), 6):
+                got[k] = p.consume(items[k])
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    assert got == want
+    key = lambda m: sorted((json.dumps(d["attributes"], sort_keys=True), d["value"]) for d in m["otelcol_odigos_trace_data_size"])
+    assert key(p.metrics()) == key(ref.metrics())
+    assert p.metrics()["otelcol_odigos_accepted_spans"] == ref.metrics()["otelcol_odigos_accepted_spans"]
+
+
+@pytest.mark.gpu
+def test_gpu_host_bench_entry():
+    """osehost_bench (tools/dropin_bench.py) runs every call and times it."""
+    import ctypes as C
+    from odigos_amd import host
+    from tools.dropin_bench import per_trace_items
+    items = per_trace_items(40, 7)
+    p = host.Processor("odigossampling", c3_sampling_config())
+    out = (C.c_double * 12)()
+    rc = native.lib().osehost_bench(p.h, host.dumps(items).encode(), 3, 4, out)
+    assert rc == 0, native.lib().osehost_last_error()
+    assert int(out[1]) == 120
+    assert out[0] > 0 and 0 < out[8] <= out[9] <= out[10] <= out[11]
+    assert out[5] > 0   # ose_process time
+
+
+@pytest.mark.gpu
+def test_gpu_ose_process_pinned_pool():
+    """ose_process on engine-owned pinned batches (batch.cpp): outputs equal
+    the oracle chain; a released batch is reused by the next acquire (the
+    pool), including for a smaller batch, with the absent columns NULLed."""
+    from odigos_amd.batch import Engine, PinnedBatch
+    eng = Engine(CFG)
+    for k, n in enumerate((120_000, 90_000, 120_000)):
+        g = Generator("fused", seed=0x0D160920 + k, n_spans=n)
+        b = PinnedBatch(eng, g.cols)
+        b.fill(g.cols)
+        b.cols.res_url_ok = None
+        for f in ("trace_first_span", "trace_level", "trace_ratio", "res_bytes"):
+            setattr(b.outs, f, None)
+        A = g.cols.n_attrsets
+        np.ctypeslib.as_array((C.c_int64 * max(A, 1)).from_address(b.outs.attrset_bytes))[:] = 0
+        np.ctypeslib.as_array((C.c_int64 * 1).from_address(b.outs.accepted_spans))[:] = 0
+        b.process(STAGES, native.GROUP_TRACE_ID, seed=SEED)
+        ho = oracle_chain(g.cols)
+        keep = np.ctypeslib.as_array((C.c_uint8 * n).from_address(b.outs.keep))
+        np.testing.assert_array_equal(keep, ho.view("keep", np.uint8)[:n])
+        url = np.ctypeslib.as_array((C.c_uint8 * n).from_address(b.outs.url_out))
+        np.testing.assert_array_equal(url, ho.view("url_out", np.uint8)[:n])
+        used = int(b.outs.tmpl_arena_used[0]) if hasattr(b.outs.tmpl_arena_used, "__getitem__") else \
+            int(C.cast(b.outs.tmpl_arena_used, C.POINTER(C.c_uint64))[0])
+        assert used == int(ho.used[0])
+        arena = np.ctypeslib.as_array((C.c_uint8 * used).from_address(b.outs.tmpl_arena))
+        np.testing.assert_array_equal(arena, ho.bufs["tmpl_arena"][:used])
+        ab = np.ctypeslib.as_array((C.c_int64 * A).from_address(b.outs.attrset_bytes))
+        np.testing.assert_array_equal(ab, ho.view("attrset_bytes", np.int64)[:A])
+        b.close()

@@ -1,9 +1,13 @@
-"""odigossampling span_attribute rules (SURVEY.md §8 a-7).
+"""odigossampling span_attribute rules (SURVEY.md §8 a-7, §8f-3).
 
-The per-span condition (internal/sampling/spanattribute.go:126-320) runs in
-the host columniser (odigos_amd/csrc/span_attr.cpp) and lands in the
-attr_match column; the trace stage (GPU) and the oracle OR the bits per
-trace as service-shaped rules.
+The per-span condition (internal/sampling/spanattribute.go:126-320): string,
+number and boolean conditions run on the GPU (attr_kernel.hip) from the
+attr_type / attr_val columns the host columniser fills; "json" conditions
+run in the host columniser (odigos_amd/csrc/span_attr.cpp) into attr_match.
+The oracle restates the string / number / boolean condition on its own
+(oracle/span_attr.c, with oracle/regex.c), so the GPU path is not compared
+with the product's host predicate.  The trace stage and the oracle OR the
+bits per trace as service-shaped rules.
 
 * KATs: the 20 cases of spanattribute_test.go, transcribed as data
   (tests/golden/span_attribute_kats.json) — CPU through host columniser +
@@ -89,7 +93,7 @@ def test_kat_oracle(c):
 
 def _eval(rule, value):
     L = native.lib()
-    r = L.osehost_span_attr_eval(json.dumps(rule).encode(), json.dumps(value).encode())
+    r = L.osehost_span_attr_eval(json.dumps(rule).encode(), host.dumps(value).encode())
     if r < 0:
         raise RuntimeError(L.osehost_last_error().decode())
     return bool(r)
@@ -102,7 +106,7 @@ def _r(cond, op, exp="", path=""):
 
 S = lambda s: {"stringValue": s}  # noqa: E731
 I = lambda i: {"intValue": str(i)}  # noqa: E731
-D = lambda d: {"doubleValue": d}  # noqa: E731
+D = host.attr_value  # noqa: E731  (doubles; non-finite ones as the protobuf JSON strings)
 B = lambda b: {"boolValue": b}  # noqa: E731
 
 PRED_CASES = [
@@ -276,6 +280,142 @@ def test_rule_limit():
         Engine({"odigossampling": {"global_rules": rules}})
 
 
+# ---- strconv.ParseFloat: product (span_attr.cpp) vs oracle (span_attr.c) ----
+
+FLOATS = ["5", "+5", "-5", ".5", "5.", "+.5e-3", "1e2", "1E+2", "1e", "e1", "", " 5", "5 ", "1_000", "1__0", "_1",
+          "1_", "1_0.0_1", "1._5", "1_.5", "1e1_0", "0x1p-2", "0x1.8", "0x1.8p1", "0X1P+0", "0x_1p0", "0x1_0p0",
+          "0x", "0xp1", "0x.8p1", "0x1p", "inf", "+Inf", "-INFINITY", "infinit", "infx", "nan", "NaN", "+nan",
+          "-nan", "1e400", "-1e400", "1e-400", "4.9e-324", "0x1p-1074", "0x1p1024", "0x1.fffffffffffffp1023",
+          "9007199254740993", "0.1", "00012", "1.2.3", "--1", "+-1", "1e+", "1e-_1", "0b101", "0o17", "1f"]
+
+
+@pytest.mark.parametrize("s", FLOATS)
+def test_parse_float_product_vs_oracle(s):
+    v = C.c_double()
+    ok = orc_lib().orc_go_parse_float(s.encode(), len(s), C.byref(v))
+    if not ok:
+        # ParseFloat error: the rule never holds (spanattribute.go:185-188)
+        for op in ("equals", "not_equals", "less_than", "greater_than"):
+            assert not _eval(_r("number", op, s), D(1.0)), (s, op)
+        return
+    x = v.value
+    if x != x:   # NaN: == never holds, != always
+        assert not _eval(_r("number", "equals", s), D(1.0)) and _eval(_r("number", "not_equals", s), D(1.0))
+        return
+    val = D(x)
+    assert _eval(_r("number", "equals", s), val), s
+    assert not _eval(_r("number", "not_equals", s), val), s
+
+
+# ---- random differential: GPU kernel vs oracle restatement ---------------------
+
+def _random_attr_case(seed, n_traces=60):
+    """Rules over three keys (string / number / bool conditions, every
+    operation, regexps, unparsable expectations) and traces whose spans carry
+    those keys with every value type."""
+    import random
+    rng = random.Random(seed)
+    svcs = ["svc-a", "svc-b", "svc-c"]
+    str_rules = [("equals", "prod"), ("not_equals", "prod"), ("contains", "ro"), ("not_contains", "x"),
+                 ("exists", ""), ("regex", "^p[a-z]+d$"), ("regex", "(a|b)+c"), ("regex", "a("), ("regex", "é+"),
+                 ("contains", ""), ("equals", "")]
+    num_rules = [("equals", "5"), ("not_equals", "5"), ("greater_than", "2.5"), ("less_than", "-1e3"),
+                 ("greater_than_or_equal", "0x1p3"), ("less_than_or_equal", "1_000"), ("exists", ""),
+                 ("equals", "bogus"), ("equals", "NaN"), ("not_equals", "nan"), ("greater_than", "-Inf")]
+    bool_rules = [("equals", "true"), ("equals", "F"), ("exists", ""), ("equals", "yes")]
+    rules = []
+    for k in range(rng.randint(4, 14)):
+        cond = rng.choice(["string", "number", "boolean"])
+        op, exp = rng.choice({"string": str_rules, "number": num_rules, "boolean": bool_rules}[cond])
+        key = rng.choice(["env", "code", "flag"])
+        rules.append({"name": f"a{k}", "type": "span_attribute",
+                      "rule_details": {"service_name": rng.choice(svcs), "attribute_key": key,
+                                       "condition_type": cond, "operation": op, "expected_value": exp,
+                                       "sampling_ratio": float(rng.choice([0, 10, 35, 50, 100])),
+                                       "fallback_sampling_ratio": float(rng.choice([0, 5, 20]))}})
+    levels = {"global_rules": [], "service_rules": [], "endpoint_rules": []}
+    for r in rules:
+        levels[rng.choice(list(levels))].append(r)
+
+    def value():
+        t = rng.randrange(7)
+        if t == 0:
+            return rng.choice(["prod", "pod", "", "dev", "prxd", "abbc", "ééé", "xprodx", "p\u00e9d"])
+        if t == 1:
+            return rng.choice([5, -5, 0, 8, 1000, 1001, -1000, 2 ** 62, -(2 ** 53) - 1])
+        if t == 2:
+            return rng.choice([5.0, 2.5, 2.5000001, -1e3, float("nan"), float("inf"), -0.0, 8.0, 1e300])
+        if t == 3:
+            return rng.choice([True, False])
+        if t == 4:
+            return {"arrayValue": {"values": [{"intValue": "1"}]}}
+        if t == 5:
+            return {"bytesValue": "AAE="}
+        return None
+
+    rs = []
+    for tr in range(n_traces):
+        tid = "%032x" % rng.getrandbits(128)
+        for _ in range(rng.randint(1, 3)):
+            spans = []
+            for j in range(rng.randint(1, 4)):
+                attrs = {}
+                for key in ("env", "code", "flag"):
+                    if rng.random() < 0.6:
+                        v = value()
+                        if v is not None:
+                            attrs[key] = v
+                spans.append(host.span(name="s", trace_id=tid, span_id="%016x" % rng.getrandbits(64),
+                                       start=BASE, end=BASE + 10, attributes=attrs))
+            res = {"service.name": rng.choice(svcs + ["other"])} if rng.random() < 0.95 else {}
+            rs.append(host.resource_spans(res, spans))
+    rng.shuffle(rs)
+    return levels, host.traces(*rs)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_oracle_vs_host_predicate(seed):
+    """The oracle's restatement from the columns equals the product's host
+    predicate (span_attr.cpp, the legacy attr_match path) on every trace."""
+    cfg, td = _random_attr_case(seed)
+    proc = host.Processor("odigossampling", cfg)
+    hb = proc.columnarize(td)
+    n = hb.cols.n_spans
+    from odigos_amd.batch import HostOutputs
+    a = HostOutputs(hb.cols)
+    assert SamplingOracle(cfg).process(hb.cols, a.outs, native.GROUP_TRACE_ID, SEED) == 0
+    # the same rules with every bit from attr_match computed by the host predicate
+    bits = np.zeros(max(n, 1), dtype=np.uint64)
+    k = 0
+    for lvl in ("global_rules", "service_rules", "endpoint_rules"):
+        for r in cfg[lvl]:
+            d = r["rule_details"]
+            i = 0
+            for rs in td["resourceSpans"]:
+                svc = host.find_attr({"attributes": rs["resource"]["attributes"]}, "service.name")
+                for sc in rs["scopeSpans"]:
+                    for sp in sc["spans"]:
+                        av = host.find_attr(sp, d["attribute_key"])
+                        if svc is not None and host.as_string(svc) == d["service_name"] and av is not None \
+                                and _eval(d, av):
+                            bits[i] |= np.uint64(1 << k)
+                        i += 1
+            k += 1
+    cols = hb.cols
+    saved = (cols.attr_type, cols.attr_val, cols.attr_match)
+    cols.attr_type = cols.attr_val = None
+    cols.attr_match = bits.ctypes.data
+    b = HostOutputs(hb.cols)
+    try:
+        assert SamplingOracle(cfg).process(cols, b.outs, native.GROUP_TRACE_ID, SEED) == 0
+    finally:
+        cols.attr_type, cols.attr_val, cols.attr_match = saved
+    np.testing.assert_array_equal(a.view("keep", np.uint8)[:n], b.view("keep", np.uint8)[:n])
+    t = int(a.view("trace_count", np.uint32)[0])
+    np.testing.assert_array_equal(a.view("trace_level", np.uint8)[:t], b.view("trace_level", np.uint8)[:t])
+    np.testing.assert_array_equal(a.view("trace_ratio", np.float64)[:t], b.view("trace_ratio", np.float64)[:t])
+
+
 # ---- GPU --------------------------------------------------------------------
 
 def _gpu(cfg, td):
@@ -321,3 +461,57 @@ def test_consume_gpu():
     assert proc.consume(_trace(({"service.name": "svc"}, [{"env": "prod"}])))["resourceSpans"] == []
     out = proc.consume(_trace(({"service.name": "svc"}, [{"env": "dev"}])))
     assert len(out["resourceSpans"]) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_random_gpu_vs_oracle(seed):
+    """attr_kernel.hip + the trace stage against the oracle's restatement on
+    random rules and values, grouped by trace id."""
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine, HostOutputs
+    cfg, td = _random_attr_case(seed, n_traces=400)
+    proc = host.Processor("odigossampling", cfg)
+    hb = proc.columnarize(td)
+    n = hb.cols.n_spans
+    assert hb.cols.n_attr_keys >= 1
+    eng = Engine({"odigossampling": cfg})
+    info = eng.info()
+    assert info.n_attr_keys == hb.cols.n_attr_keys and info.attr_host_rules == 0
+    db = DeviceBatch(hb.cols)
+    eng.process_device(db, native.STAGE_SAMPLE, native.GROUP_TRACE_ID, seed=SEED)
+    torch.cuda.synchronize()
+    assert int(db.out_numpy("device_status", np.uint32)[0]) == 0
+    ho = HostOutputs(hb.cols)
+    assert SamplingOracle(cfg).process(hb.cols, ho.outs, native.GROUP_TRACE_ID, SEED) == 0
+    np.testing.assert_array_equal(db.out_numpy("keep", n=n), ho.view("keep", np.uint8)[:n])
+    t = int(ho.view("trace_count", np.uint32)[0])
+    assert int(db.out_numpy("trace_count", np.uint32)[0]) == t
+    np.testing.assert_array_equal(db.out_numpy("trace_level", n=t), ho.view("trace_level", np.uint8)[:t])
+    np.testing.assert_array_equal(db.out_numpy("trace_ratio", np.float64, n=t), ho.view("trace_ratio", np.float64)[:t])
+
+
+@pytest.mark.gpu
+def test_json_rules_stay_on_host():
+    """A json condition is the shim's (attr_host_rules); its bit and a GPU
+    rule's bit combine in one trace decision."""
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine, HostOutputs
+    cfg = {"global_rules": [
+        {"name": "j", "type": "span_attribute", "rule_details": dict(_r("json", "contains_key", path="$.a"),
+                                                                     service_name="svc", attribute_key="body",
+                                                                     sampling_ratio=40.0)},
+        {"name": "s", "type": "span_attribute", "rule_details": dict(ENV, sampling_ratio=25.0)}]}
+    td = _trace(({"service.name": "svc"}, [{"body": '{"a": 1}'}, {"env": "prod"}]),
+                ({"service.name": "svc"}, [{"body": "[]"}]))
+    proc = host.Processor("odigossampling", cfg)
+    proc.configure(SEED, native.GROUP_BATCH)
+    hb = proc.columnarize(td)
+    eng = Engine({"odigossampling": cfg})
+    assert eng.info().attr_host_rules == 1 and eng.info().n_attr_keys == 1
+    db = DeviceBatch(hb.cols)
+    eng.process_device(db, native.STAGE_SAMPLE, native.GROUP_BATCH, seed=SEED)
+    torch.cuda.synchronize()
+    ho = HostOutputs(hb.cols)
+    assert SamplingOracle(cfg).process(hb.cols, ho.outs, native.GROUP_BATCH, SEED) == 0
+    assert float(db.out_numpy("trace_ratio", np.float64)[0]) == 40.0 == float(ho.view("trace_ratio", np.float64)[0])

@@ -4,21 +4,26 @@ bench workload's kernels (written to a JSON merged into profiles/pmc_traffic.jso
 traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB counters -> bytes); FETCH_SIZE is
 doubled per MI355X_MICROARCH.md (wide reads tallied at half).  The bench line's
 kernel key is the '+'-joined kernel list of the stage."""
-import csv, glob, json, re, sys
+import csv, glob, json, sys
 from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from bench import WORKLOADS  # noqa: E402  (the bench line's kernel list is the key)
+
+# profile spans that cover several launches: the kernels they stand for
+SPAN_KERNELS = {"trace_run_list": ("trace_runs_kernel", "trace_fold_kernel", "trace_first_select_kernel"),
+                "trace_sort_path": ("trace_key_kernel", "sort_hist_kernel", "scan_u32_kernel", "sort_scatter_kernel"),
+                "shard_unpack": ("shard_unpack_kernel",)}
 
 wl, root, out = sys.argv[1], sys.argv[2], sys.argv[3]
-STAGES = {"url": ("url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel"), "sampling": ("trace_eval_kernel", "trace_long_kernel"),
-          "zipf": ("trace_eval_kernel", "trace_long_kernel"),
-          "fused": ("trace_eval_kernel", "trace_long_kernel", "url_plan_kernel", "url_scan_kernel", "url_emit_kernel", "url_emit_slow_kernel",
-                    "size_span_kernel", "size_scope_kernel", "size_res_kernel")}
-kernels = STAGES[wl]
+kernels = WORKLOADS[wl]["kernels"]
 vals = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
 for c in vals:
     for f in glob.glob(f"{root}/{c}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             for k in kernels:
-                if k in row.get("Kernel_Name", ""):
+                if any(x in row.get("Kernel_Name", "") for x in SPAN_KERNELS.get(k, (k,))):
                     vals[c][k].append(float(row["Counter_Value"]))
 spans = None
 for f in glob.glob(f"{root}/FETCH_SIZE.log"):
@@ -30,7 +35,10 @@ for k in kernels:
     fe = vals["FETCH_SIZE"][k]
     wr = vals["WRITE_SIZE"][k]
     if not fe or not wr:
-        sys.exit(f"missing counters for {k}")
+        # host-gated launches (trace_long_kernel, the repeated-trace-id
+        # paths, url_emit_slow_kernel) that this workload never queued
+        per_k[k] = {"fetch_kib": 0.0, "write_kib": 0.0, "hbm_bytes": 0.0, "launched": False}
+        continue
     # gated launches (the sort-based trace path exits at once unless the fast
     # path saw a split trace) are dispatches of the same kernel with ~no
     # traffic: average over the working dispatches only

@@ -8,6 +8,6 @@ WL=${1:-url}
 mkdir -p gpurun_out/traffic_$WL
 cd /tmp && export TMPDIR=/tmp
 for ctr in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/traffic_$WL/$ctr -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/traffic_$WL/$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 $GRAFT_REPO_ROOT/gpurun_out/traffic_$WL/$ctr.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/traffic_$WL/$ctr -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-parity > $GRAFT_REPO_ROOT/gpurun_out/traffic_$WL/$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 $GRAFT_REPO_ROOT/gpurun_out/traffic_$WL/$ctr.log; exit 1; }
 done
 python3 $GRAFT_REPO_ROOT/tools/pmc_traffic.py $WL $GRAFT_REPO_ROOT/gpurun_out/traffic_$WL $GRAFT_REPO_ROOT/gpurun_out/pmc_traffic_$WL.json
