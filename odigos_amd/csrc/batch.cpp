@@ -150,8 +150,6 @@ int Batch::build(const ose_columns& dims) {
               {o_ratio, 8 * n1, (void**)&outs_h.trace_ratio},
               {o_res, 8 * R, (void**)&outs_h.res_bytes}};
   outs_h.tmpl_arena_cap = outs_d.tmpl_arena_cap = tmpl_cap;
-  outs_h.tmpl_arena_used = &used_h;
-  outs_d.tmpl_arena_used = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(outs_d.device_status) + 8);
   set_dims(dims);
   return 0;
 }
@@ -176,6 +174,10 @@ void Batch::set_dims(const ose_columns& dims) {
     outs_h.tmpl_arena = tmpl_h_big;
     outs_d.tmpl_arena = tmpl_d_big;
   }
+  // the device's tmpl_arena_used lives in device_status's slack (read back
+  // with the counters); the shim reads used_h
+  outs_h.tmpl_arena_used = &used_h;
+  outs_d.tmpl_arena_used = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(outs_d.device_status) + 8);
   used_h = 0;
 }
 
@@ -278,6 +280,24 @@ int ose_process(ose_engine* eng, ose_batch* bb, uint32_t stage_mask, uint32_t gr
   if (!cd.attr_type || !cd.attr_val) cd.attr_type = nullptr, cd.attr_val = nullptr, cd.n_attr_keys = 0;
   if (!od.device_status || !od.attrset_bytes || !od.accepted_spans || !od.tmpl_arena)
     return fail(OSE_EINVAL, "ose_process: device_status, attrset_bytes, accepted_spans and tmpl_arena must stay set");
+  {
+    // every device pointer a kernel gets lies in this batch's device memory
+    auto inside = [&](const void* p) {
+      const uint8_t* q = static_cast<const uint8_t*>(p);
+      return !p || (q >= b->d && q < b->d + b->bytes) || (b->tmpl_d_big && q == b->tmpl_d_big);
+    };
+    bool ok = inside(od.tmpl_arena_used);
+    for (auto& f : b->fields) {
+      const uint8_t* ds = reinterpret_cast<const uint8_t*>(f.ds);
+      const uint8_t* cbase = reinterpret_cast<const uint8_t*>(&b->cols_d);
+      const void* p = (ds >= cbase && ds < cbase + sizeof(ose_columns))
+                          ? *reinterpret_cast<void* const*>(reinterpret_cast<const uint8_t*>(&cd) + (ds - cbase))
+                          : *reinterpret_cast<void* const*>(reinterpret_cast<const uint8_t*>(&od) +
+                                                            (ds - reinterpret_cast<const uint8_t*>(&b->outs_d)));
+      ok = ok && inside(p);
+    }
+    if (!ok) return fail(OSE_EINVAL, "ose_process: a device pointer of the batch lies outside its memory");
+  }
   uint32_t* status_h = b->outs_h.device_status;
   uint64_t* used_h = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(status_h) + 8);
   // the counters are ADDED to on the device: keep the caller's values for a rerun
