@@ -231,9 +231,9 @@ def test_gpu_ose_process_pinned_pool():
     eng = Engine(CFG)
     for k, n in enumerate((120_000, 90_000, 120_000)):
         g = Generator("fused", seed=0x0D160920 + k, n_spans=n)
+        g.cols.res_url_ok = None   # no include/exclude configured (fill NULLs the pinned column)
         b = PinnedBatch(eng, g.cols)
         b.fill(g.cols)
-        b.cols.res_url_ok = None
         for f in ("trace_first_span", "trace_level", "trace_ratio", "res_bytes"):
             setattr(b.outs, f, None)
         A = g.cols.n_attrsets
