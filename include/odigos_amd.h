@@ -248,6 +248,12 @@ typedef struct ose_batch ose_batch;
 int ose_engine_create(const char* cfg_json, ose_engine** out);
 void ose_engine_destroy(ose_engine* eng);
 
+/* Device selection: an engine lives on the HIP device that is current on
+ * the creating thread, and every later call on it runs there whatever
+ * thread makes it (a gateway with N GPUs creates one engine per GPU, each
+ * after ose_set_device(k) on the creating thread).                          */
+int ose_set_device(int device);
+
 /* Interned id of a service name referenced by a sampling rule, or OSE_NONE.
  * The shim uses it to fill res_svc / res_svc_str (rule_engine callers compare
  * service.name by equality only: latency.go:55, servicename.go:40).        */

@@ -198,6 +198,8 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
   int rc = ensure_device();
   if (rc) return rc;
   Engine* e = reinterpret_cast<Engine*>(eng);
+  rc = bind_device(e);
+  if (rc) return rc;
   {
     // smallest pooled batch that fits
     std::lock_guard<std::mutex> g(e->mu);
@@ -234,6 +236,7 @@ void ose_batch_release(ose_batch* bb) {
   if (!bb) return;
   Batch* b = reinterpret_cast<Batch*>(bb);
   Engine* e = b->e;
+  (void)bind_device(e);
   {
     std::lock_guard<std::mutex> g(e->mu);
     if (!b->tmpl_h_big && e->batch_pool.size() < kPoolMax && e->batch_pool_bytes + b->bytes <= kPoolBytesMax) {
@@ -250,6 +253,7 @@ int ose_process(ose_engine* eng, ose_batch* bb, uint32_t stage_mask, uint32_t gr
   Engine* e = reinterpret_cast<Engine*>(eng);
   Batch* b = reinterpret_cast<Batch*>(bb);
   if (!b->fits(b->cols_h)) return fail(OSE_EINVAL, "batch dimensions exceed the acquired capacity");
+  if (int brc = bind_device(e)) return brc;
   hipStream_t st = e->take_stream();
   if (!st) return fail(OSE_EDEVICE, "hipStreamCreate failed");
   struct GiveBack {

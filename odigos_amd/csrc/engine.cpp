@@ -288,6 +288,12 @@ int ensure_device() {
   return 0;
 }
 
+int bind_device(const Engine* e) {
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != e->device) HIP_TRY(hipSetDevice(e->device));
+  return 0;
+}
+
 int upload(const std::vector<uint8_t>& host, uint8_t** dev) {
   HIP_TRY(hipMalloc(dev, host.size()));
   HIP_TRY(hipMemcpy(*dev, host.data(), host.size(), hipMemcpyHostToDevice));
@@ -494,6 +500,7 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
   if (rc) { delete e; return rc; }
   rc = ensure_device();
   if (rc) { delete e; return rc; }
+  if (hipGetDevice(&e->device) != hipSuccess) { delete e; return fail(OSE_EDEVICE, "hipGetDevice failed"); }
   if (e->has_url) {
     rc = upload(e->url_blob_host, &e->url_blob_dev);
     if (rc) { delete e; return rc; }
@@ -510,7 +517,18 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
   return 0;
 }
 
-void ose_engine_destroy(ose_engine* eng) { delete reinterpret_cast<Engine*>(eng); }
+void ose_engine_destroy(ose_engine* eng) {
+  if (!eng) return;
+  (void)bind_device(reinterpret_cast<Engine*>(eng));
+  delete reinterpret_cast<Engine*>(eng);
+}
+
+int ose_set_device(int device) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(device));
+  return 0;
+}
 
 uint32_t ose_engine_service_id(const ose_engine* eng, const char* name, size_t len) {
   if (!eng || !name) return OSE_NONE;
@@ -537,6 +555,7 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   if (!eng) return fail(OSE_EINVAL, "NULL engine");
   (void)arena_bytes;
   Engine* e = reinterpret_cast<Engine*>(eng);
+  if (int brc = bind_device(e)) return brc;
   Workspace* ws = e->acquire_ws(nullptr);
   int rc = ws->reserve(e->workspace_bytes(n_spans));
   if (!rc && e->has_sampling) rc = ws->reserve_table(n_spans);
@@ -548,6 +567,7 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
 int ose_process_device(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, uint32_t stage_mask,
                        uint32_t group_mode, const ose_rand* rnd, void* hip_stream) {
   if (!eng) return fail(OSE_EINVAL, "NULL engine");
+  if (int brc = bind_device(reinterpret_cast<Engine*>(eng))) return brc;
   return run_stages(reinterpret_cast<Engine*>(eng), cols, outs, stage_mask, group_mode, rnd,
                     static_cast<hipStream_t>(hip_stream));
 }
@@ -561,6 +581,7 @@ int ose_profile_enable(ose_engine* eng, int on) {
 int ose_profile_read(ose_engine* eng, char* json, size_t cap) {
   if (!eng || !json) return fail(OSE_EINVAL, "NULL argument");
   Engine* e = reinterpret_cast<Engine*>(eng);
+  if (int brc = bind_device(e)) return brc;
   std::vector<Engine::Timed> ts;
   {
     std::lock_guard<std::mutex> g(e->mu);

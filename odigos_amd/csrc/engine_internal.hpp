@@ -15,6 +15,10 @@
 namespace ose {
 
 int fail(int code, const std::string& msg);
+struct Engine;
+// makes the engine's device current on the calling thread (a shim's
+// goroutines migrate across OS threads; HIP's current device is per thread)
+int bind_device(const Engine* e);
 int ensure_device();
 bool stream_capturing(hipStream_t st);
 struct Engine;
@@ -54,6 +58,7 @@ struct Workspace {
 };
 
 struct Engine {
+  int device = 0;   // the HIP device current when the engine was created; every call runs there
   UrlTemplateConfig url;
   SamplingConfig sampling;
   TrafficMetricsConfig traffic;

@@ -146,6 +146,7 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   if (!eng || !c || !send || !counts || !pack_pos) return fail(OSE_EINVAL, "NULL argument");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_pack needs odigossampling on the engine");
+  if (int brc = bind_device(e)) return brc;
   if (n_ranks == 0 || n_ranks > 64) return fail(OSE_EINVAL, "n_ranks must be in 1..64");
   const uint64_t n = c->n_spans;
   if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "more than 2^32-16 spans");
@@ -291,6 +292,7 @@ int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outp
   if (cols->n_spans && !outs->keep) return fail(OSE_EINVAL, "outs->keep is required");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "the exchange needs odigossampling on the engine");
+  if (int brc = bind_device(e)) return brc;
   const Rccl& r = rccl();
   if (!r.ok) return fail(OSE_ENOTSUP, "RCCL (librccl.so.1) is not available");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);

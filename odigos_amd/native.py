@@ -118,6 +118,7 @@ def lib() -> C.CDLL:
         "ose_engine_destroy": (None, [_p]),
         "ose_engine_service_id": (C.c_uint32, [_p, C.c_char_p, C.c_size_t]),
         "ose_engine_get_info": (C.c_int, [_p, C.POINTER(EngineInfo)]),
+        "ose_set_device": (C.c_int, [C.c_int]),
         "ose_engine_attr_key": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),
         "ose_batch_columns": (C.POINTER(Columns), [_p]),
