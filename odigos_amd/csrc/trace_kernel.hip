@@ -308,7 +308,13 @@ __device__ __forceinline__ void decide(const Cfg& c, uint32_t err, uint64_t ep, 
 // store READY; readers poll the state and read the key with sc1 loads
 // (MI355X_MICROARCH.md "Valid forms": sc1 payload + drained flag).  A lane
 // that finds the key ready and equal is a second run of that trace_id.
-__device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint64_t lo, uint32_t pos,
+// Returns kInsNew (the slot was claimed; with run lists, the run is listed
+// as the trace's first), kInsFound (the id was there: a repeated trace id)
+// or kInsFail (error flagged).  Callers gated on *dup do not set it again:
+// one word hit by every repeated head of the batch is a serialised
+// device-scope atomic per head.
+constexpr int kInsNew = 0, kInsFound = 1, kInsFail = -1;
+__device__ inline int table_insert(const TraceKernelArgs& a, uint64_t hi, uint64_t lo, uint32_t pos,
                                     uint64_t* slot_out = nullptr) {
   const uint32_t busy = (a.epoch << 2) | 1u, ready = (a.epoch << 2) | 2u;
   uint64_t h = tid_hash(hi, lo) & a.table_mask;
@@ -323,18 +329,21 @@ __device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint6
         __hip_atomic_store(&s->hi, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->lo, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->first, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (a.run_count) __hip_atomic_store(&a.run_count[h], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.run_count) {   // this run is the trace's first listed run
+          __hip_atomic_store(&a.run_count[h], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (a.runs) a.runs[h * kMaxRuns] = pos;
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&s->state, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (slot_out) *slot_out = h;
-        return;
+        return kInsNew;
       }
       continue;   // lost the race for this slot: look at it again
     }
     if ((st & 3u) != 2u) {   // another lane is publishing this slot
       if (++spins > (1u << 20)) {
         atomicOr(a.error, 1u);
-        return;
+        return kInsFail;
       }
       __builtin_amdgcn_s_sleep(1);
       continue;
@@ -343,14 +352,13 @@ __device__ inline void table_insert(const TraceKernelArgs& a, uint64_t hi, uint6
     const uint64_t l2 = __hip_atomic_load(&s->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (h2 == hi && l2 == lo) {
       atomicMin(&s->first, pos);
-      atomicOr(a.dup, 1u);
       if (slot_out) *slot_out = h;
-      return;
+      return kInsFound;
     }
     h = (h + 1) & a.table_mask;
     if (++probes > a.table_mask) {
       atomicOr(a.error, 4u);
-      return;
+      return kInsFail;
     }
   }
 }
@@ -438,7 +446,8 @@ __device__ __forceinline__ uint64_t fp_cell(const TraceKernelArgs& a, uint64_t h
   const uint64_t fp = ((splitmix64(lo ^ (hi << 1)) >> 16) | 1ull) & 0xFFFFFFFFFFFFull;
   return ((uint64_t)(a.epoch & 0xFFFFu) << 48) | fp;
 }
-__device__ inline void fp_insert_cell(const TraceKernelArgs& a, uint64_t cell, uint64_t idx) {
+// true: the fingerprint was there already (or the probe sequence ran out)
+__device__ inline bool fp_insert_cell(const TraceKernelArgs& a, uint64_t cell, uint64_t idx) {
   const uint64_t ep = cell & ~0xFFFFFFFFFFFFull, fp = cell & 0xFFFFFFFFFFFFull;
   for (uint32_t probes = 0; probes < 64; probes++) {
     uint64_t* q = &a.fp_table[idx];
@@ -447,18 +456,15 @@ __device__ inline void fp_insert_cell(const TraceKernelArgs& a, uint64_t cell, u
       if ((v & ~0xFFFFFFFFFFFFull) != ep) {
         if (__hip_atomic_compare_exchange_strong(q, &v, cell, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT))
-          return;
+          return false;
         continue;   // v now holds the current cell
       }
       break;
     }
-    if ((v & 0xFFFFFFFFFFFFull) == fp) {
-      atomicOr(a.dup, 1u);
-      return;
-    }
+    if ((v & 0xFFFFFFFFFFFFull) == fp) return true;
     idx = (idx + 1) & a.fp_mask;
   }
-  atomicOr(a.dup, 1u);   // probe sequence too long: let the exact path decide
+  return true;   // probe sequence too long: let the exact path decide
 }
 
 __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos, uint8_t keep, uint8_t level,
@@ -484,8 +490,11 @@ struct HeadQ {
 };
 __device__ void flush_heads(const TraceKernelArgs& a, HeadQ& H, uint32_t& hn, int lane) {
   __builtin_amdgcn_wave_barrier();
+  bool dup = false;
   for (uint32_t b = 0; b < hn; b += kWave)
-    if (b + lane < hn) fp_insert_cell(a, H.cell[b + lane], H.idx[b + lane]);
+    if (b + lane < hn) dup |= fp_insert_cell(a, H.cell[b + lane], H.idx[b + lane]);
+  // one *dup store per wave flush (a per-head atomic on one word serialises)
+  if (__ballot(dup) && lane == 0) atomicOr(a.dup, 1u);
   __builtin_amdgcn_wave_barrier();
   hn = 0;
 }
@@ -992,7 +1001,7 @@ __global__ __launch_bounds__(256) void trace_insert_exact_kernel(TraceKernelArgs
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < a.n_spans; p += (uint64_t)gridDim.x * 256) {
     const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
     if (p > 0 && a.tid[2 * p - 2] == hi && a.tid[2 * p - 1] == lo) continue;
-    table_insert(a, hi, lo, (uint32_t)p);
+    (void)table_insert(a, hi, lo, (uint32_t)p);   // gated on *dup: already set
   }
 }
 
@@ -1017,14 +1026,16 @@ __global__ __launch_bounds__(256) void trace_runs_kernel(TraceKernelArgs a) {
     if (!((heads >> lane) & 1) || p >= a.n_spans) continue;
     const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
     uint64_t slot = ~0ull;
-    table_insert(a, hi, lo, (uint32_t)p, &slot);
-    if (slot == ~0ull) {   // table full / spin gave up: error already flagged
+    const int ins = table_insert(a, hi, lo, (uint32_t)p, &slot);   // gated on *dup: not set again
+    if (ins == kInsFail || slot == ~0ull) {   // table full / spin gave up: error already flagged
       atomicOr(a.overflow, 1u);
       continue;
     }
-    const uint32_t k = atomicAdd(&a.run_count[slot], 1u);
-    if (k < kMaxRuns) a.runs[slot * kMaxRuns + k] = (uint32_t)p;
-    else atomicOr(a.overflow, 1u);
+    if (ins == kInsFound) {   // a later run: append (the claiming lane listed the first)
+      const uint32_t k = atomicAdd(&a.run_count[slot], 1u);
+      if (k < kMaxRuns) a.runs[slot * kMaxRuns + k] = (uint32_t)p;
+      else atomicOr(a.overflow, 1u);
+    }
     a.head_slot[p] = (uint32_t)slot;
   }
 }
