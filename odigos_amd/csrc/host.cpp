@@ -2,6 +2,8 @@
 // function reads from pdata; Apply mirrors what it writes.
 #include "host.hpp"
 
+#include "columnize.hpp"
+
 #include <algorithm>
 #include <array>
 #include <atomic>
@@ -72,31 +74,6 @@ namespace {
 
 const char* kProcType[] = {"odigossampling", "odigosurltemplate", "odigostrafficmetrics", "pipeline"};
 
-// resourceToWorkloadStringRepresentation (filtermatcher.go:30-84)
-bool workload_key(const AttrMap& attrs, std::string& key) {
-  const Value* ns = attrs.Get("k8s.namespace.name");
-  if (!ns || ns->type != Value::TStr) return false;
-  struct { const char* attr; const char* kind; } order[] = {
-      {"k8s.deployment.name", "deployment"}, {"k8s.statefulset.name", "statefulset"}, {"k8s.daemonset.name", "daemonset"}};
-  for (auto& o : order) {
-    const Value* v = attrs.Get(o.attr);
-    if (!v) continue;
-    if (v->type != Value::TStr) return false;
-    key = ns->s + "/" + o.kind + "/" + v->s;
-    return true;
-  }
-  return false;
-}
-std::set<std::string> workload_set(const MatchProperties& mp) {
-  std::set<std::string> s;
-  for (auto& w : mp.k8s_workloads) {
-    std::string k = w.kind;
-    for (auto& c : k) c = (char)std::tolower((unsigned char)c);
-    s.insert(w.namespace_ + "/" + k + "/" + w.name);   // k8sWorkloadToStringRepresentation (:21-24)
-  }
-  return s;
-}
-
 }  // namespace
 
 TracesProcessor::TracesProcessor(ProcKind k, const Json& cfg) : kind_(k), cfg_json_(cfg) {
@@ -112,23 +89,10 @@ TracesProcessor::TracesProcessor(ProcKind k, const Json& cfg) : kind_(k), cfg_js
       group_mode = OSE_GROUP_TRACE_ID;
       break;
   }
-  if (has_sampling_) services_ = intern_services(sampling_);
-  if (err_.empty() && has_sampling_) {
-    // span_attribute conditions run here, per span, into attr_match (level order)
-    for (auto* lvl : {&sampling_.global_rules, &sampling_.service_rules, &sampling_.endpoint_rules})
-      for (auto& r : *lvl)
-        if (r.rtype == RuleType::SpanAttribute) {
-          attr_preds_.emplace_back();
-          std::string e = attr_preds_.back().compile(r.attr);
-          if (!e.empty() && err_.empty()) err_ = e;
-        }
-    if (attr_preds_.size() > 64 && err_.empty()) err_ = "more than 64 span_attribute rules are not supported";
-    attr_plan_ = plan_attr_rules(sampling_);
-  }
-  if (err_.empty() && has_url_) {
-    // newUrlTemplateProcessor errors (rule parsing, custom id regexps) are
-    // create-time errors too (factory.go:37-40); decode_url_config covers them.
-  }
+  // span_attribute conditions: compiled here (json ones run in the walk);
+  // newUrlTemplateProcessor's errors are decode_url_config's (factory.go:37-40)
+  if (err_.empty())
+    err_ = ctx_.build(has_url_ ? &url_ : nullptr, has_sampling_ ? &sampling_ : nullptr, has_traffic_ ? &traffic_ : nullptr);
 }
 
 TracesProcessor::~TracesProcessor() {
@@ -164,9 +128,6 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
   hb->td = td;
   const Traces& t = hb->td;
   ProtoSizer sizer;
-  std::set<std::string> excl, incl;
-  if (url_.exclude) excl = workload_set(*url_.exclude);
-  if (url_.include) incl = workload_set(*url_.include);
   std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> attrset_ids;
   std::string arena;
   auto add_str = [&](const std::string& s) {
@@ -175,42 +136,19 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
     return r;
   };
   uint32_t scope_idx = 0;
-  std::vector<std::pair<std::vector<uint8_t>, std::vector<uint64_t>>> attr_cols(attr_plan_.keys.size());
+  const size_t nk = ctx_.attr_plan.keys.size();
+  std::vector<std::pair<std::vector<uint8_t>, std::vector<uint64_t>>> attr_cols(nk);
+  SpanCols sc;
   for (size_t ri = 0; ri < t.resource_spans.size(); ri++) {
     const ResourceSpans& rs = t.resource_spans[ri];
-    const AttrMap& ra = rs.resource_attrs;
-    // service ids (latency.go:51-56 AsString; servicename.go:38-42 Str)
-    uint32_t svc = OSE_NONE, svc_str = OSE_NONE;
-    const Value* svc_val = ra.Get("service.name");
-    const std::string svc_as = svc_val ? svc_val->AsString() : std::string();
-    uint64_t attr_res = 0;   // span_attribute rules whose service this resource is (spanattribute.go:130-132)
-    for (size_t k = 0; k < attr_preds_.size(); k++)
-      if (svc_val && attr_preds_[k].service() == svc_as) attr_res |= 1ull << k;
-    if (const Value* v = ra.Get("service.name")) {
-      auto it = services_.find(v->AsString());
-      if (it != services_.end()) svc = it->second;
-      if (v->type == Value::TStr && it != services_.end()) svc_str = it->second;
-    }
-    hb->res_svc.push_back(svc);
-    hb->res_svc_str.push_back(svc_str);
-    // include/exclude (processor.go:76-85)
-    bool ok = true;
-    if (url_.exclude || url_.include) {
-      std::string key;
-      bool has_key = workload_key(ra, key);
-      if (url_.exclude && has_key && excl.count(key)) ok = false;
-      if (url_.include && !(has_key && incl.count(key))) ok = false;
-    }
-    hb->res_url_ok.push_back(ok ? 1 : 0);
-    // attributeSetFromResource (odigostrafficmetrics/processor.go:60-69)
-    std::map<std::string, std::string> set;   // attribute.NewSet: sorted, last value wins
-    for (auto& k : traffic_.res_attributes_keys)
-      if (const Value* v = ra.Get(k)) set[k] = v->Str();
-    std::vector<std::pair<std::string, std::string>> key(set.begin(), set.end());
-    auto it = attrset_ids.find(key);
+    const ResourceCols rc = columnize_resource(ctx_, rs.resource_attrs);
+    hb->res_svc.push_back(rc.svc);
+    hb->res_svc_str.push_back(rc.svc_str);
+    hb->res_url_ok.push_back(rc.url_ok);
+    auto it = attrset_ids.find(rc.attrset);
     if (it == attrset_ids.end()) {
-      it = attrset_ids.emplace(key, (uint32_t)hb->attrsets.size()).first;
-      hb->attrsets.push_back(key);
+      it = attrset_ids.emplace(rc.attrset, (uint32_t)hb->attrsets.size()).first;
+      hb->attrsets.push_back(rc.attrset);
     }
     hb->res_attrset.push_back(it->second);
     hb->res_size.push_back((uint32_t)sizer.resource_fixed(rs));
@@ -218,83 +156,30 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
       hb->scope_size.push_back((uint32_t)sizer.scope_fixed(ss));
       hb->scope_resource.push_back((uint32_t)ri);
       for (auto& sp : ss.spans) {
-        uint64_t hi = 0, lo = 0;
-        for (int k = 0; k < 8; k++) { hi = hi << 8 | sp.trace_id[k]; lo = lo << 8 | sp.trace_id[8 + k]; }
-        hb->trace_id.push_back(hi);
-        hb->trace_id.push_back(lo);
-        hb->start.push_back(sp.start);
-        hb->end.push_back(sp.end);
-        hb->status.push_back((uint8_t)sp.status_code);
-        hb->kind.push_back((uint8_t)std::min<int32_t>(std::max<int32_t>(sp.kind, 0), 255));
+        columnize_span(ctx_, sp, rc.attr_res, sizer, sc);
+        hb->trace_id.push_back(sc.hi);
+        hb->trace_id.push_back(sc.lo);
+        hb->start.push_back(sc.start);
+        hb->end.push_back(sc.end);
+        hb->status.push_back(sc.status);
+        hb->kind.push_back(sc.kind);
         hb->resource.push_back((uint32_t)ri);
         hb->scope.push_back(scope_idx);
-        hb->span_size.push_back((uint32_t)sizer.span(sp));
-        hb->name_len.push_back((uint32_t)sp.name.size());
-        // span_attribute: the "json" conditions are evaluated here; the
-        // others on the GPU from the span's value of each rule key
-        uint64_t am = 0;
-        for (uint64_t m = attr_res & attr_plan_.host_mask; m; m &= m - 1) {
-          const int k = __builtin_ctzll(m);
-          if (const Value* av = sp.attrs.Get(attr_preds_[k].key()))
-            if (attr_preds_[k].eval(*av)) am |= 1ull << k;
-        }
-        hb->attr_match.push_back(am);
-        for (size_t k = 0; k < attr_plan_.keys.size(); k++) {
-          uint8_t ty = OSE_ATTR_ABSENT;
-          uint64_t v = 0;
-          if (const Value* av = sp.attrs.Get(attr_plan_.keys[k])) {
-            switch (av->type) {
-              case Value::TStr: {
-                ty = OSE_ATTR_STR;
-                const ose_strref r = add_str(av->s);
-                v = (uint64_t)r.off | ((uint64_t)r.len << 32);
-                break;
-              }
-              case Value::TInt: ty = OSE_ATTR_INT; v = (uint64_t)av->i; break;
-              case Value::TDouble: ty = OSE_ATTR_DOUBLE; std::memcpy(&v, &av->d, 8); break;
-              case Value::TBool: ty = OSE_ATTR_BOOL; v = av->b ? 1 : 0; break;
-              default: ty = OSE_ATTR_OTHER; break;
-            }
+        hb->span_size.push_back(sc.span_size);
+        hb->name_len.push_back(sc.name_len);
+        hb->attr_match.push_back(sc.attr_match);
+        for (size_t k = 0; k < nk; k++) {
+          uint64_t v = sc.attr_val[k];
+          if (sc.attr_type[k] == OSE_ATTR_STR) {
+            const ose_strref r = add_str(sc.attr_str[k]);
+            v = (uint64_t)r.off | ((uint64_t)r.len << 32);
           }
-          attr_cols[k].first.push_back(ty);
+          attr_cols[k].first.push_back(sc.attr_type[k]);
           attr_cols[k].second.push_back(v);
         }
-        const AttrMap& a = sp.attrs;
-        // sampling: AsString(http.route) (latency.go:64-68)
-        const Value* route = a.Get("http.route");
-        hb->route.push_back(route ? add_str(route->AsString()) : ose_strref{0, 0});
-        // urltemplate (processor.go:98-147, 235-287)
-        uint8_t f = 0;
-        ose_strref pref{0, 0};
-        const Value* m = a.Get("http.request.method");
-        if (!m) m = a.Get("http.method");
-        if (m) {
-          f |= OSE_URL_HAS_METHOD;
-          std::string method = m->AsString();
-          if (sp.name == method) f |= OSE_URL_NAME_EQ_METHOD;
-          const char* tkey = sp.kind == OSE_KIND_CLIENT ? "url.template" : "http.route";
-          if (const Value* tv = a.Get(tkey)) {
-            if (tv->type != Value::TStr) f |= OSE_URL_TGT_NONSTR;
-            else f |= tv->s.empty() ? OSE_URL_TGT_STR_EMPTY : OSE_URL_TGT_STR;
-          }
-          if (const Value* p = a.Get("url.path")) {
-            f |= OSE_URL_PATH_RAW;
-            pref = add_str(p->AsString());
-          } else if (const Value* p = a.Get("http.target")) {
-            f |= OSE_URL_PATH_TARGET;
-            pref = add_str(p->AsString());
-          } else {
-            const Value* fu = a.Get("url.full");
-            if (!fu) fu = a.Get("http.url");
-            std::string path;
-            if (fu && go_url_parse_path(fu->AsString(), path)) {
-              f |= OSE_URL_PATH_RAW;
-              pref = add_str(path);
-            }
-          }
-        }
-        hb->url_flags.push_back(f);
-        hb->path.push_back(pref);
+        hb->route.push_back(sc.has_route ? add_str(sc.route) : ose_strref{0, 0});
+        hb->url_flags.push_back(sc.url_flags);
+        hb->path.push_back((sc.url_flags & OSE_URL_PATH_MASK) != OSE_URL_PATH_NONE ? add_str(sc.path) : ose_strref{0, 0});
       }
       scope_idx++;
     }

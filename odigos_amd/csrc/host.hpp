@@ -20,6 +20,7 @@
 #include "../../include/odigos_amd.h"
 #include "config.hpp"
 #include "pdata.hpp"
+#include "columnize.hpp"
 #include "span_attr.hpp"
 
 namespace ose {
@@ -84,9 +85,7 @@ class TracesProcessor {
   SamplingConfig sampling_;
   TrafficMetricsConfig traffic_;
   bool has_url_ = false, has_sampling_ = false, has_traffic_ = false;
-  std::map<std::string, uint32_t> services_;
-  std::vector<SpanAttrPredicate> attr_preds_;   // span_attribute rules, level order
-  AttrPlan attr_plan_;                          // which of them the GPU evaluates, from which key column
+  ColumnizeCtx ctx_;   // the walk's view of the config (columnize.hpp)
   ose_engine* eng_ = nullptr;
   uint64_t seed_ = 0x0D16A5EEDull;
   uint64_t draws_ = 0;
