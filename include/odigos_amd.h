@@ -390,6 +390,33 @@ int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outp
 int ose_allreduce_counters(const int64_t* local, int64_t* node, uint64_t n, void* nccl_comm,
                            void* hip_stream);
 
+/* ---- OTLP protobuf ingest -----------------------------
+ * Replaces ptrace.ProtoUnmarshaler.UnmarshalTraces on the receive path
+ * (collector/receivers/odigosebpfreceiver/traces.go:77-88) together with the
+ * shim's columnising walk: one serialized TracesData (the body of an
+ * ExportTraceServiceRequest; concatenated messages merge) becomes the
+ * device columns this engine's stages read, for ose_process_device.
+ * The host walks the message structure (ResourceSpans / ScopeSpans headers,
+ * resource and scope contents, one header per span) while the bytes go
+ * H2D; the GPU decodes every span (ids, times, status, kind, name, the
+ * attributes the stages read, events and links for the sizes) and computes
+ * span_size as pdata's sizer does.  Spans it cannot finish exactly (a value
+ * that needs AsString or net/url.Parse, nested values, json span_attribute
+ * keys, unusual ids or fields) get a host pass; ose_otlp_host_spans says how
+ * many.  Strings are referenced in place: the arena is the message bytes,
+ * followed by the host pass's strings.  What UnmarshalTraces rejects is
+ * OSE_EINVAL.  Asynchronous work is on hip_stream; the call returns when
+ * the columns are complete on that stream.  res_attrset ids index the
+ * attribute sets ose_otlp_attrset returns ({"key": "value", ...}).         */
+typedef struct ose_otlp_batch ose_otlp_batch;
+int ose_otlp_decode(ose_engine* eng, const void* pb, size_t len, void* hip_stream, ose_otlp_batch** out);
+const ose_columns* ose_otlp_columns(const ose_otlp_batch* b);   /* device pointers */
+uint32_t ose_otlp_host_spans(const ose_otlp_batch* b);
+int ose_otlp_attrset(const ose_otlp_batch* b, uint32_t k, char* json, size_t cap);
+/* copies every column whose dst pointer is non-NULL (host or device memory) */
+int ose_otlp_download(const ose_otlp_batch* b, const ose_columns* dst);
+void ose_otlp_release(ose_otlp_batch* b);
+
 /* Message of the last failure on this thread ("" if none). */
 const char* ose_last_error(void);
 

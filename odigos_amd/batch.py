@@ -112,6 +112,25 @@ class HostOutputs:
         return self.bufs[name].view(dtype)
 
 
+def device_outputs(dims: native.Columns, device="cuda", tmpl_cap: int | None = None):
+    """ose_outputs for a batch of these dimensions, in HBM (torch tensors)."""
+    import torch
+    outs = native.Outputs()
+    o = {}
+    for name, (dim, size) in OUTPUT_LAYOUT.items():
+        n = max(_count(dims, dim) * size, 16)
+        t = torch.zeros(n + 16, dtype=torch.uint8, device=device)
+        o[name] = t
+        setattr(outs, name, t.data_ptr())
+    cap = tmpl_cap if tmpl_cap is not None else default_tmpl_cap(dims)
+    o["tmpl_arena"] = torch.zeros(cap + 16, dtype=torch.uint8, device=device)
+    outs.tmpl_arena = o["tmpl_arena"].data_ptr()
+    outs.tmpl_arena_cap = cap
+    o["used"] = torch.zeros(2, dtype=torch.int64, device=device)
+    outs.tmpl_arena_used = o["used"].data_ptr()
+    return outs, o
+
+
 class DeviceBatch:
     """Columns + outputs resident in HBM (torch uint8 tensors)."""
 
@@ -134,19 +153,7 @@ class DeviceBatch:
                 t[:n].copy_(torch.from_numpy(src))
             self.t[name] = t
             setattr(self.cols, name, t.data_ptr())
-        self.outs = native.Outputs()
-        self.o = {}
-        for name, (dim, size) in OUTPUT_LAYOUT.items():
-            n = max(_count(host_cols, dim) * size, 16)
-            t = torch.zeros(n + 16, dtype=torch.uint8, device=device)
-            self.o[name] = t
-            setattr(self.outs, name, t.data_ptr())
-        cap = tmpl_cap if tmpl_cap is not None else default_tmpl_cap(host_cols)
-        self.o["tmpl_arena"] = torch.zeros(cap + 16, dtype=torch.uint8, device=device)
-        self.outs.tmpl_arena = self.o["tmpl_arena"].data_ptr()
-        self.outs.tmpl_arena_cap = cap
-        self.o["used"] = torch.zeros(2, dtype=torch.int64, device=device)
-        self.outs.tmpl_arena_used = self.o["used"].data_ptr()
+        self.outs, self.o = device_outputs(host_cols, device, tmpl_cap)
 
     def out_numpy(self, name: str, dtype=np.uint8, n: int | None = None) -> np.ndarray:
         """Host copy of an output (the first n elements of dtype, or all)."""
@@ -239,6 +246,61 @@ class PinnedBatch:
     def close(self):
         if getattr(self, "h", None):
             self.L.ose_batch_release(self.h)
+            self.h = None
+
+    __del__ = close
+
+
+class OtlpBatch:
+    """A serialized TracesData decoded on the GPU (ose_otlp_decode): device
+    columns owned by the engine plus HBM outputs, usable wherever a
+    DeviceBatch is (Engine.process_device)."""
+
+    def __init__(self, engine: "Engine", pb: bytes, stream=None, tmpl_cap: int | None = None):
+        self.L = engine.L
+        h = C.c_void_p()
+        s = None if stream is None else C.c_void_p(stream)
+        native.check(self.L.ose_otlp_decode(engine.h, pb, len(pb), s, C.byref(h)))
+        self.h = h
+        self.cols = native.Columns.from_buffer_copy(self.L.ose_otlp_columns(h).contents)
+        self.host_spans = int(self.L.ose_otlp_host_spans(h))
+        self.outs, self.o = device_outputs(self.cols, tmpl_cap=tmpl_cap)
+
+    def attrset(self, k: int) -> dict:
+        import json
+        buf = C.create_string_buffer(1 << 16)
+        native.check(self.L.ose_otlp_attrset(self.h, k, buf, len(buf)))
+        return json.loads(buf.value.decode("utf-8", "surrogateescape"))
+
+    def download(self) -> dict:
+        """Host copies of every column (numpy), dims and the arena."""
+        c = self.cols
+        dst = native.Columns()
+        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys"):
+            setattr(dst, f, getattr(c, f))
+        out = {}
+        for name, (dim, size) in COLUMN_LAYOUT.items():
+            if not getattr(c, name):
+                continue
+            nb = _count(c, dim) * size
+            a = np.zeros(max(nb, 1) + 16, dtype=np.uint8)
+            out[name] = a
+            setattr(dst, name, a.ctypes.data)
+        native.check(self.L.ose_otlp_download(self.h, C.byref(dst)))
+        return out
+
+    def out_numpy(self, name: str, dtype=np.uint8, n: int | None = None) -> np.ndarray:
+        t = self.o[name]
+        if n is not None:
+            t = t[: n * np.dtype(dtype).itemsize]
+        return t.cpu().numpy().view(dtype)
+
+    def used(self) -> int:
+        return int(self.o["used"][0].item())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ose_otlp_release(self.h)
             self.h = None
 
     __del__ = close

@@ -145,6 +145,7 @@ int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32
 Engine::~Engine() {
   release_exchange_scratch(this);
   release_batch_pool(this);
+  release_otlp(this);
   for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto s : streams) (void)hipStreamDestroy(s);
   for (auto ev : event_pool) (void)hipEventDestroy(ev);

@@ -24,6 +24,8 @@ bool stream_capturing(hipStream_t st);
 struct Engine;
 void release_exchange_scratch(const Engine* e);   // shard_host.cpp
 void release_batch_pool(Engine* e);                // batch.cpp
+struct OtlpEngine;
+void release_otlp(Engine* e);                      // otlp_host.cpp
 
 // Device scratch for one in-flight call (look-back status words, sort
 // buffers, partial records).  Engines keep a pool so concurrent callers never
@@ -84,6 +86,8 @@ struct Engine {
   std::mutex mu;
   std::vector<Workspace*> pool, free_ws;
   std::vector<void*> batch_pool;   // released ose_batch slabs (batch.cpp)
+  OtlpEngine* otlp = nullptr;      // OTLP ingest tables, built on first use (otlp_host.cpp)
+  std::vector<void*> otlp_pool;    // released ose_otlp_batch objects
   size_t batch_pool_bytes = 0;
 
   // ose_profile_*: (kernel name, start, stop) per launch

@@ -3,6 +3,7 @@
 #include "host.hpp"
 
 #include "columnize.hpp"
+#include "otlp_pb.hpp"
 
 #include <algorithm>
 #include <array>
@@ -566,6 +567,17 @@ int osehost_bench(void* p, const char* traces_json, uint32_t reps, uint32_t thre
 }
 
 char* osehost_metrics_json(void* p) { return dup_cstr(static_cast<TracesProcessor*>(p)->MetricsJson()); }
+// OTLP protobuf -> pdata (otlp_pb.cpp) -> OTLP/JSON: the host unmarshaler
+// the ingest's host pass uses (tests); NULL + osehost_last_error on error
+char* osehost_pb_to_json(const uint8_t* pb, size_t len) {
+  Traces td;
+  std::string err;
+  if (!traces_from_protobuf(pb, len, td, err)) {
+    g_host_err = err;
+    return nullptr;
+  }
+  return dup_cstr(dump_traces(td));
+}
 // Traces round trip through the pdata model (fixture sanity)
 char* osehost_roundtrip(const char* traces_json) {
   try {

@@ -294,4 +294,79 @@ struct AttrArgs {
 };
 void launch_attr_eval(const AttrArgs& a, hipStream_t st);
 
+// OTLP protobuf ingest (otlp_kernel.hip).  Attribute keys the decoder
+// looks for, with the roles a key plays (one entry per distinct key).
+enum : uint32_t {
+  kRoleMethodNew = 1u << 0,   // http.request.method
+  kRoleMethodOld = 1u << 1,   // http.method
+  kRoleRoute = 1u << 2,       // http.route (sampling route; SERVER target)
+  kRoleUrlTmpl = 1u << 3,     // url.template (CLIENT target)
+  kRoleUrlPath = 1u << 4,     // url.path
+  kRoleTarget = 1u << 5,      // http.target
+  kRoleFull = 1u << 6,        // url.full / http.url: net/url.Parse on the host
+  kRoleHost = 1u << 7,        // a json span_attribute rule's key: host pass
+  kRoleAttr0 = 1u << 8,       // + k: GPU attribute key column k (k < kOtlpMaxAttrKeys)
+};
+constexpr uint32_t kOtlpMaxAttrKeys = 24;
+struct OtlpKeyDev {
+  uint32_t len, off, roles, _pad;
+};
+struct OtlpArgs {
+  const uint8_t* pb;            // message bytes = the arena (16-byte aligned, 16 bytes of slack)
+  uint64_t n_spans;
+  const uint64_t* span_ref;     // payload offset | length << 32
+  const OtlpKeyDev* keys;
+  const uint8_t* key_bytes;
+  uint32_t n_keys;
+  uint32_t n_attr_keys;
+  uint64_t key_lens;            // bit l: some key has length l (< 64)
+  uint64_t* tid;
+  uint64_t* start;
+  uint64_t* end;
+  uint8_t* status;
+  uint8_t* kind;
+  uint8_t* url_flags;
+  ose_strref* path;
+  ose_strref* route;
+  uint32_t* span_size;
+  uint32_t* name_len;
+  uint64_t* attr_match;         // may be null
+  uint8_t* attr_type;
+  uint64_t* attr_val;
+  uint8_t* host_flag;           // [n_spans] 1 = the host pass writes this span
+  uint32_t* host_count;         // zeroed before launch
+  uint32_t* host_list;
+  uint32_t host_cap;
+};
+struct OtlpFix {
+  uint64_t idx;
+  uint64_t hi, lo, start, end, attr_match;
+  ose_strref path, route;
+  uint32_t span_size, name_len;
+  uint8_t status, kind, url_flags, _pad[5];
+};
+struct OtlpFixArgs {
+  uint32_t n;
+  uint32_t n_attr_keys;
+  uint64_t n_spans;
+  const OtlpFix* fix;
+  const uint8_t* fix_type;      // [n * n_attr_keys]
+  const uint64_t* fix_val;
+  uint64_t* tid;
+  uint64_t* start;
+  uint64_t* end;
+  uint8_t* status;
+  uint8_t* kind;
+  uint8_t* url_flags;
+  ose_strref* path;
+  ose_strref* route;
+  uint32_t* span_size;
+  uint32_t* name_len;
+  uint64_t* attr_match;
+  uint8_t* attr_type;
+  uint64_t* attr_val;
+};
+void launch_otlp_spans(const OtlpArgs& a, hipStream_t st);
+void launch_otlp_fix(const OtlpFixArgs& a, hipStream_t st);
+
 }  // namespace ose

@@ -1,0 +1,472 @@
+// otlp_host.cpp — OTLP protobuf ingest: ose_otlp_*.
+//
+// One call turns a serialized TracesData into device columns:
+//   1. the bytes go to pinned staging and H2D (the arena: strings are
+//      referenced in place) while the host walks the structure (otlp_pb.cpp
+//      pb_walk: ResourceSpans / ScopeSpans headers, resource and scope
+//      contents, one header per span);
+//   2. per-resource and per-scope columns on the host (columnize.cpp: the
+//      service ids, include/exclude, attribute sets, the fixed sizes);
+//   3. otlp_span_kernel decodes every span on the GPU;
+//   4. the spans it lists get the host pass: pb_span + columnize_span, their
+//      strings appended after the message bytes, written by otlp_fix_kernel.
+#include <cstring>
+#include <map>
+
+#include "columnize.hpp"
+#include "engine_internal.hpp"
+#include "kernels.hpp"
+#include "otlp_pb.hpp"
+
+namespace ose {
+
+#define HIP_TRY(expr)                                                                                  \
+  do {                                                                                                 \
+    hipError_t _e = (expr);                                                                            \
+    if (_e != hipSuccess) return fail(OSE_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+size_t up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+struct DevBuf {   // grow-only device (or pinned host) buffer
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  bool host = false;
+  int need(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) { if (host) (void)hipHostFree(p); else (void)hipFree(p); }
+    p = nullptr;
+    cap = 0;
+    const size_t want = up(std::max<size_t>(bytes + bytes / 4, 1 << 20), 1 << 16);
+    if (host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault));
+    else HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p), want));
+    cap = want;
+    return 0;
+  }
+  ~DevBuf() {
+    if (p) { if (host) (void)hipHostFree(p); else (void)hipFree(p); }
+  }
+};
+}  // namespace
+
+// The engine's view for the ingest: the columniser context and the key
+// table the GPU decoder matches (built once per engine).
+struct OtlpEngine {
+  ColumnizeCtx ctx;
+  std::vector<OtlpKeyDev> keys;
+  std::string key_bytes;
+  uint64_t key_lens = 0;
+  uint8_t* keys_dev = nullptr;   // OtlpKeyDev[] then the bytes
+  uint32_t n_attr_keys = 0;
+  bool json_rules = false;
+  std::string err;
+  ~OtlpEngine() { if (keys_dev) (void)hipFree(keys_dev); }
+};
+
+struct OtlpBatchImpl {
+  Engine* e = nullptr;
+  ose_columns cols{};
+  DevBuf arena, slab, stage, fixdev;   // device arena; device columns; pinned staging; host-pass records
+  std::vector<std::vector<std::pair<std::string, std::string>>> attrsets;
+  uint32_t host_spans = 0;
+  OtlpBatchImpl() { stage.host = true; }
+};
+
+namespace {
+std::mutex g_otlp_mu;
+
+OtlpEngine* otlp_engine(Engine* e, int& rc) {
+  std::lock_guard<std::mutex> g(g_otlp_mu);
+  rc = 0;
+  if (e->otlp) return e->otlp;
+  auto* o = new OtlpEngine();
+  o->err = o->ctx.build(e->has_url ? &e->url : nullptr, e->has_sampling ? &e->sampling : nullptr,
+                        e->has_traffic ? &e->traffic : nullptr);
+  if (!o->err.empty()) { rc = fail(OSE_EINVAL, o->err); delete o; return nullptr; }
+  std::map<std::string, uint32_t> roles;
+  roles["http.request.method"] |= kRoleMethodNew;
+  roles["http.method"] |= kRoleMethodOld;
+  roles["http.route"] |= kRoleRoute;
+  roles["url.template"] |= kRoleUrlTmpl;
+  roles["url.path"] |= kRoleUrlPath;
+  roles["http.target"] |= kRoleTarget;
+  roles["url.full"] |= kRoleFull;
+  roles["http.url"] |= kRoleFull;
+  const AttrPlan& plan = o->ctx.attr_plan;
+  if (plan.keys.size() > kOtlpMaxAttrKeys) {
+    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 24 span_attribute keys");
+    delete o;
+    return nullptr;
+  }
+  o->n_attr_keys = (uint32_t)plan.keys.size();
+  for (size_t k = 0; k < plan.keys.size(); k++) roles[plan.keys[k]] |= kRoleAttr0 << k;
+  for (size_t k = 0; k < plan.rule_key.size(); k++)
+    if (plan.rule_key[k] < 0) {
+      roles[o->ctx.attr_preds[k].key()] |= kRoleHost;
+      o->json_rules = true;
+    }
+  for (auto& kv : roles) {
+    OtlpKeyDev d{(uint32_t)kv.first.size(), (uint32_t)o->key_bytes.size(), kv.second, 0};
+    o->key_bytes += kv.first;
+    o->keys.push_back(d);
+    if (kv.first.size() < 64) o->key_lens |= 1ull << kv.first.size();
+  }
+  const size_t kb = o->keys.size() * sizeof(OtlpKeyDev);
+  std::vector<uint8_t> blob(kb + o->key_bytes.size() + 16, 0);
+  std::memcpy(blob.data(), o->keys.data(), kb);
+  std::memcpy(blob.data() + kb, o->key_bytes.data(), o->key_bytes.size());
+  if (hipMalloc(reinterpret_cast<void**>(&o->keys_dev), blob.size()) != hipSuccess ||
+      hipMemcpy(o->keys_dev, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    rc = fail(OSE_EDEVICE, "OTLP ingest: key table upload failed");
+    delete o;
+    return nullptr;
+  }
+  e->otlp = o;
+  return o;
+}
+}  // namespace
+
+void release_otlp(Engine* e) {
+  for (void* p : e->otlp_pool) delete static_cast<OtlpBatchImpl*>(p);
+  e->otlp_pool.clear();
+  delete e->otlp;
+  e->otlp = nullptr;
+}
+
+namespace {
+int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchImpl* b) {
+  int rc;
+  OtlpEngine* o = otlp_engine(e, rc);
+  if (!o) return rc;
+  if (len > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: message beyond the 4 GiB arena range");
+  // 1. bytes to pinned staging and H2D, the walk meanwhile
+  const size_t pb_cap = up(len + 16, 16);
+  if ((rc = b->stage.need(pb_cap))) return rc;
+  std::memcpy(b->stage.p, pb, len);
+  std::memset(b->stage.p + len, 0, pb_cap - len);
+  const size_t fix_reserve = std::max<size_t>(1 << 16, len / 8);
+  if ((rc = b->arena.need(pb_cap + fix_reserve + 16))) return rc;
+  HIP_TRY(hipMemcpyAsync(b->arena.p, b->stage.p, pb_cap, hipMemcpyHostToDevice, st));
+  PbWalk w;
+  if (!pb_walk(pb, len, w)) return fail(OSE_EINVAL, w.err);
+  HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
+  const uint64_t n = w.span_ref.size(), R = w.res.size(), S = w.scopes.size();
+  if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: more than 2^32-16 spans");
+  const uint32_t K = o->n_attr_keys;
+  // 2. resource / scope columns on the host
+  std::vector<uint32_t> res_svc(R), res_svc_str(R), res_attrset(R), res_size(R), scope_size(S), scope_res(S);
+  std::vector<uint8_t> res_ok(R);
+  std::vector<uint64_t> attr_res(R);
+  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
+  b->attrsets.clear();
+  ProtoSizer sizer;
+  for (uint64_t r = 0; r < R; r++) {
+    const ResourceCols rc2 = columnize_resource(o->ctx, w.res[r].attrs);
+    res_svc[r] = rc2.svc;
+    res_svc_str[r] = rc2.svc_str;
+    res_ok[r] = rc2.url_ok;
+    attr_res[r] = rc2.attr_res;
+    auto it = set_ids.find(rc2.attrset);
+    if (it == set_ids.end()) {
+      it = set_ids.emplace(rc2.attrset, (uint32_t)b->attrsets.size()).first;
+      b->attrsets.push_back(rc2.attrset);
+    }
+    res_attrset[r] = it->second;
+    ResourceSpans rs;
+    rs.resource_attrs = w.res[r].attrs;
+    rs.resource_dropped = w.res[r].dropped;
+    rs.schema_url = w.res[r].schema_url;
+    res_size[r] = (uint32_t)sizer.resource_fixed(rs);
+  }
+  for (uint64_t s = 0; s < S; s++) {
+    scope_size[s] = (uint32_t)sizer.scope_fixed(w.scopes[s].meta);
+    scope_res[s] = w.scopes[s].resource;
+  }
+  // device columns: one slab
+  const uint64_t N = std::max<uint64_t>(n, 1);
+  struct Part { void** dst; size_t bytes; const void* src; };
+  ose_columns& c = b->cols;
+  c = ose_columns{};
+  uint8_t* host_flag = nullptr;
+  uint32_t* host_count = nullptr;
+  uint32_t* host_list = nullptr;
+  uint64_t* span_ref = nullptr;
+  std::vector<Part> parts = {
+      {(void**)&span_ref, 8 * N, w.span_ref.data()},
+      {(void**)&c.resource, 4 * N, w.span_res.data()},
+      {(void**)&c.scope, 4 * N, w.span_scope.data()},
+      {(void**)&c.res_svc, 4 * R, res_svc.data()},
+      {(void**)&c.res_svc_str, 4 * R, res_svc_str.data()},
+      {(void**)&c.res_url_ok, R, res_ok.data()},
+      {(void**)&c.res_attrset, 4 * R, res_attrset.data()},
+      {(void**)&c.res_size, 4 * R, res_size.data()},
+      {(void**)&c.scope_size, 4 * S, scope_size.data()},
+      {(void**)&c.scope_resource, 4 * S, scope_res.data()},
+      // outputs of the decoder
+      {(void**)&c.trace_id, 16 * N, nullptr},
+      {(void**)&c.start_ns, 8 * N, nullptr},
+      {(void**)&c.end_ns, 8 * N, nullptr},
+      {(void**)&c.status, N, nullptr},
+      {(void**)&c.kind, N, nullptr},
+      {(void**)&c.url_flags, N, nullptr},
+      {(void**)&c.path, 8 * N, nullptr},
+      {(void**)&c.route, 8 * N, nullptr},
+      {(void**)&c.span_size, 4 * N, nullptr},
+      {(void**)&c.name_len, 4 * N, nullptr},
+      {(void**)&host_flag, N, nullptr},
+      {(void**)&host_count, 16, nullptr},
+      {(void**)&host_list, 4 * N, nullptr},
+  };
+  if (o->json_rules) parts.push_back({(void**)&c.attr_match, 8 * N, nullptr});
+  if (K) {
+    parts.push_back({(void**)&c.attr_type, (size_t)K * N, nullptr});
+    parts.push_back({(void**)&c.attr_val, 8 * (size_t)K * N, nullptr});
+  }
+  size_t total = 0, inputs = 0;
+  for (auto& p : parts) {
+    total = up(total + p.bytes + 16);
+    if (p.src) inputs = total;
+  }
+  if ((rc = b->slab.need(total)) || (rc = b->stage.need(inputs))) return rc;
+  size_t off = 0;
+  for (auto& p : parts) {
+    *p.dst = b->slab.p + off;
+    if (p.src && p.bytes) std::memcpy(b->stage.p + off, p.src, p.bytes);
+    off = up(off + p.bytes + 16);
+  }
+  HIP_TRY(hipMemcpyAsync(b->slab.p, b->stage.p, inputs, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(host_count, 0, 16, st));
+  c.n_spans = n;
+  c.n_resources = (uint32_t)R;
+  c.n_scopes = (uint32_t)S;
+  c.n_attrsets = (uint32_t)b->attrsets.size();
+  c.arena = b->arena.p;
+  c.arena_bytes = len;
+  c.n_attr_keys = K;
+  if (!o->ctx.url_filter) c.res_url_ok = nullptr;
+  // 3. the GPU decoder
+  OtlpArgs a{};
+  a.pb = b->arena.p;
+  a.n_spans = n;
+  a.span_ref = span_ref;
+  a.keys = reinterpret_cast<const OtlpKeyDev*>(o->keys_dev);
+  a.key_bytes = o->keys_dev + o->keys.size() * sizeof(OtlpKeyDev);
+  a.n_keys = (uint32_t)o->keys.size();
+  a.n_attr_keys = K;
+  a.key_lens = o->key_lens;
+  a.tid = const_cast<uint64_t*>(c.trace_id);
+  a.start = const_cast<uint64_t*>(c.start_ns);
+  a.end = const_cast<uint64_t*>(c.end_ns);
+  a.status = const_cast<uint8_t*>(c.status);
+  a.kind = const_cast<uint8_t*>(c.kind);
+  a.url_flags = const_cast<uint8_t*>(c.url_flags);
+  a.path = const_cast<ose_strref*>(c.path);
+  a.route = const_cast<ose_strref*>(c.route);
+  a.span_size = const_cast<uint32_t*>(c.span_size);
+  a.name_len = const_cast<uint32_t*>(c.name_len);
+  a.attr_match = const_cast<uint64_t*>(c.attr_match);
+  a.attr_type = const_cast<uint8_t*>(c.attr_type);
+  a.attr_val = const_cast<uint64_t*>(c.attr_val);
+  a.host_flag = host_flag;
+  a.host_count = host_count;
+  a.host_list = host_list;
+  a.host_cap = (uint32_t)N;
+  Engine::Timed tm{};
+  e->prof_begin("otlp_span_kernel", st, tm);
+  launch_otlp_spans(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  // 4. the host pass
+  uint32_t cnt = 0;
+  HIP_TRY(hipMemcpyAsync(&cnt, host_count, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  b->host_spans = cnt;
+  if (!cnt) return 0;
+  std::vector<uint32_t> list(cnt);
+  HIP_TRY(hipMemcpy(list.data(), host_list, 4 * (size_t)cnt, hipMemcpyDeviceToHost));
+  std::vector<OtlpFix> fix(cnt);
+  std::vector<uint8_t> fix_type((size_t)cnt * K);
+  std::vector<uint64_t> fix_val((size_t)cnt * K);
+  std::string strs;   // appended after the message bytes
+  const size_t str_base = pb_cap;
+  auto put = [&](const std::string& s) {
+    ose_strref r{(uint32_t)(str_base + strs.size()), (uint32_t)s.size()};
+    strs += s;
+    return r;
+  };
+  SpanCols sc;
+  for (uint32_t q = 0; q < cnt; q++) {
+    const uint32_t i = list[q];
+    const uint64_t ref = w.span_ref[i];
+    Span sp;
+    if (!pb_span(pb + (uint32_t)ref, (size_t)(ref >> 32), sp)) return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
+    columnize_span(o->ctx, sp, attr_res[w.span_res[i]], sizer, sc);
+    OtlpFix& x = fix[q];
+    x = OtlpFix{};
+    x.idx = i;
+    x.hi = sc.hi;
+    x.lo = sc.lo;
+    x.start = sc.start;
+    x.end = sc.end;
+    x.attr_match = sc.attr_match;
+    x.status = sc.status;
+    x.kind = sc.kind;
+    x.url_flags = sc.url_flags;
+    x.span_size = sc.span_size;
+    x.name_len = sc.name_len;
+    for (uint32_t k = 0; k < K; k++) {
+      uint64_t v = sc.attr_val[k];
+      if (sc.attr_type[k] == OSE_ATTR_STR) {
+        const ose_strref r = put(sc.attr_str[k]);
+        v = (uint64_t)r.off | ((uint64_t)r.len << 32);
+      }
+      fix_type[(size_t)q * K + k] = sc.attr_type[k];
+      fix_val[(size_t)q * K + k] = v;
+    }
+    x.route = sc.has_route ? put(sc.route) : ose_strref{0, 0};
+    x.path = (sc.url_flags & OSE_URL_PATH_MASK) != OSE_URL_PATH_NONE ? put(sc.path) : ose_strref{0, 0};
+  }
+  if (str_base + strs.size() + 16 > b->arena.cap) {
+    // a larger arena: the message bytes move with it
+    DevBuf bigger;
+    if ((rc = bigger.need(str_base + strs.size() + 16))) return rc;
+    HIP_TRY(hipMemcpyAsync(bigger.p, b->arena.p, pb_cap, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::swap(b->arena.p, bigger.p);
+    std::swap(b->arena.cap, bigger.cap);
+    c.arena = b->arena.p;
+  }
+  c.arena_bytes = str_base + strs.size();
+  const size_t fb = up(cnt * sizeof(OtlpFix)), tb = up((size_t)cnt * K + 16), vb = up((size_t)cnt * K * 8 + 16);
+  if ((rc = b->stage.need(fb + tb + vb + strs.size() + 16))) return rc;
+  DevBuf& fixdev = b->fixdev;
+  if ((rc = fixdev.need(fb + tb + vb))) return rc;
+  std::memcpy(b->stage.p, fix.data(), cnt * sizeof(OtlpFix));
+  if (K) {
+    std::memcpy(b->stage.p + fb, fix_type.data(), (size_t)cnt * K);
+    std::memcpy(b->stage.p + fb + tb, fix_val.data(), (size_t)cnt * K * 8);
+  }
+  std::memcpy(b->stage.p + fb + tb + vb, strs.data(), strs.size());
+  HIP_TRY(hipMemcpyAsync(fixdev.p, b->stage.p, fb + tb + vb, hipMemcpyHostToDevice, st));
+  if (!strs.empty())
+    HIP_TRY(hipMemcpyAsync(b->arena.p + str_base, b->stage.p + fb + tb + vb, strs.size(), hipMemcpyHostToDevice, st));
+  OtlpFixArgs fa{};
+  fa.n = cnt;
+  fa.n_attr_keys = K;
+  fa.n_spans = n;
+  fa.fix = reinterpret_cast<const OtlpFix*>(fixdev.p);
+  fa.fix_type = fixdev.p + fb;
+  fa.fix_val = reinterpret_cast<const uint64_t*>(fixdev.p + fb + tb);
+  fa.tid = a.tid;
+  fa.start = a.start;
+  fa.end = a.end;
+  fa.status = a.status;
+  fa.kind = a.kind;
+  fa.url_flags = a.url_flags;
+  fa.path = a.path;
+  fa.route = a.route;
+  fa.span_size = a.span_size;
+  fa.name_len = a.name_len;
+  fa.attr_match = a.attr_match;
+  fa.attr_type = a.attr_type;
+  fa.attr_val = a.attr_val;
+  launch_otlp_fix(fa, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));   // fixdev and the staging are reused / freed
+  return 0;
+}
+}  // namespace
+
+}  // namespace ose
+
+using namespace ose;
+
+extern "C" {
+
+int ose_otlp_decode(ose_engine* eng, const void* pb, size_t len, void* hip_stream, ose_otlp_batch** out) {
+  if (!eng || (!pb && len) || !out) return fail(OSE_EINVAL, "NULL argument");
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  if (int rc = bind_device(e)) return rc;
+  OtlpBatchImpl* b = nullptr;
+  {
+    // released batches keep their (grow-only) buffers: no allocation per call
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->otlp_pool.empty()) {
+      b = static_cast<OtlpBatchImpl*>(e->otlp_pool.back());
+      e->otlp_pool.pop_back();
+    }
+  }
+  if (!b) b = new OtlpBatchImpl();
+  b->e = e;
+  const int rc = decode(e, static_cast<const uint8_t*>(pb), len, static_cast<hipStream_t>(hip_stream), b);
+  if (rc) {
+    delete b;
+    return rc;
+  }
+  *out = reinterpret_cast<ose_otlp_batch*>(b);
+  return 0;
+}
+
+int ose_otlp_download(const ose_otlp_batch* bb, const ose_columns* dst) {
+  if (!bb || !dst) return fail(OSE_EINVAL, "NULL argument");
+  const auto* b = reinterpret_cast<const OtlpBatchImpl*>(bb);
+  if (int rc = bind_device(b->e)) return rc;
+  const ose_columns& c = b->cols;
+  const uint64_t n = c.n_spans, R = c.n_resources, S = c.n_scopes, K = c.n_attr_keys;
+  struct F { const void* src; void* dst; size_t bytes; };
+  const F fs[] = {
+      {c.arena, (void*)dst->arena, c.arena_bytes}, {c.trace_id, (void*)dst->trace_id, 16 * n},
+      {c.start_ns, (void*)dst->start_ns, 8 * n}, {c.end_ns, (void*)dst->end_ns, 8 * n},
+      {c.status, (void*)dst->status, n}, {c.kind, (void*)dst->kind, n}, {c.resource, (void*)dst->resource, 4 * n},
+      {c.scope, (void*)dst->scope, 4 * n}, {c.url_flags, (void*)dst->url_flags, n}, {c.path, (void*)dst->path, 8 * n},
+      {c.route, (void*)dst->route, 8 * n}, {c.span_size, (void*)dst->span_size, 4 * n},
+      {c.name_len, (void*)dst->name_len, 4 * n}, {c.attr_match, (void*)dst->attr_match, 8 * n},
+      {c.res_svc, (void*)dst->res_svc, 4 * R}, {c.res_svc_str, (void*)dst->res_svc_str, 4 * R},
+      {c.res_url_ok, (void*)dst->res_url_ok, R}, {c.res_attrset, (void*)dst->res_attrset, 4 * R},
+      {c.res_size, (void*)dst->res_size, 4 * R}, {c.scope_size, (void*)dst->scope_size, 4 * S},
+      {c.scope_resource, (void*)dst->scope_resource, 4 * S}, {c.attr_type, (void*)dst->attr_type, K * n},
+      {c.attr_val, (void*)dst->attr_val, 8 * K * n},
+  };
+  for (auto& f : fs)
+    if (f.src && f.dst && f.bytes) HIP_TRY(hipMemcpy(f.dst, f.src, f.bytes, hipMemcpyDefault));
+  return 0;
+}
+
+const ose_columns* ose_otlp_columns(const ose_otlp_batch* bb) {
+  return bb ? &reinterpret_cast<const OtlpBatchImpl*>(bb)->cols : nullptr;
+}
+
+uint32_t ose_otlp_host_spans(const ose_otlp_batch* bb) {
+  return bb ? reinterpret_cast<const OtlpBatchImpl*>(bb)->host_spans : 0;
+}
+
+int ose_otlp_attrset(const ose_otlp_batch* bb, uint32_t k, char* json, size_t cap) {
+  if (!bb || !json) return fail(OSE_EINVAL, "NULL argument");
+  const auto* b = reinterpret_cast<const OtlpBatchImpl*>(bb);
+  if (k >= b->attrsets.size()) return fail(OSE_EINVAL, "attribute set index out of range");
+  Json o = Json::object();
+  for (auto& kv : b->attrsets[k]) o.set(kv.first, Json::str(kv.second));
+  std::string s;
+  dump_json(s, o);
+  if (s.size() + 1 > cap) return fail(OSE_ERANGE, "buffer too small");
+  std::memcpy(json, s.c_str(), s.size() + 1);
+  return 0;
+}
+
+void ose_otlp_release(ose_otlp_batch* bb) {
+  if (!bb) return;
+  auto* b = reinterpret_cast<OtlpBatchImpl*>(bb);
+  Engine* e = b->e;
+  (void)bind_device(e);
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->otlp_pool.size() < 16) {
+      e->otlp_pool.push_back(b);
+      return;
+    }
+  }
+  delete b;
+}
+
+}  // extern "C"

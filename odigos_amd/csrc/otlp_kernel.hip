@@ -1,0 +1,461 @@
+// otlp_kernel.hip — OTLP protobuf ingest on the GPU: the
+// Span messages of a serialized TracesData decoded straight into the
+// columns the three stages read (what ptrace.ProtoUnmarshaler.UnmarshalTraces
+// plus the shim's columnising walk produce on the CPU; collector/receivers/
+// odigosebpfreceiver/traces.go:77-88, odigos_amd/csrc/columnize.cpp).
+//
+// One lane per span walks its payload once through 16-byte vector loads
+// (ByteReader): ids, times, kind, name, status, the attributes whose keys
+// the stages read (first occurrence, as pcommon.Map.Get), and the span's
+// wire size as pdata's sizer computes it (gogo framing: ids, Status and
+// KeyValue.value always emitted; otlp_pb.hpp / pdata.cpp ProtoSizer::span).
+// Strings stay where they are: refs point into the message bytes, which are
+// the arena.  A span the lane cannot finish exactly — a value that needs
+// AsString or url.Parse, a nested ArrayValue / KeyValueList, a json
+// span_attribute key, an id of unusual length, a group or malformed field,
+// a repeated KeyValue field — is listed for the host pass (otlp_host.cpp),
+// which decodes it with the host unmarshaler and writes all its columns.
+#include <hip/hip_runtime.h>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+namespace ose {
+
+namespace {
+constexpr int kOThreads = 256;
+
+__device__ __forceinline__ uint32_t sov(uint64_t x) { return (uint32_t)((64 - __clzll(x | 1) + 6) / 7); }
+__device__ __forceinline__ uint64_t field_len(uint64_t l) { return 1 + sov(l) + l; }
+__device__ __forceinline__ uint64_t str_field(uint64_t l) { return l ? field_len(l) : 0; }
+__device__ __forceinline__ uint64_t varint_field(uint64_t v) { return v ? 1 + sov(v) : 0; }
+
+struct Rd {
+  ByteReader br;
+  uint32_t i, end;
+  bool bad;
+  __device__ Rd(const uint8_t* base, uint32_t s, uint32_t e) : br(base), i(s), end(e), bad(false) {}
+  __device__ __forceinline__ bool more() const { return !bad && i < end; }
+  __device__ uint64_t varint() {
+    uint64_t v = 0;
+    for (uint32_t s = 0; s < 64; s += 7) {
+      if (i >= end) break;
+      const uint32_t b = br.at(i++);
+      v |= (uint64_t)(b & 0x7F) << s;
+      if (b < 0x80) return v;
+    }
+    bad = true;
+    return 0;
+  }
+  __device__ uint64_t fixed(uint32_t nb) {
+    if (i + nb > end) { bad = true; return 0; }
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < nb; k++) v |= (uint64_t)br.at(i + k) << (8 * k);
+    i += nb;
+    return v;
+  }
+  // LEN payload [s, s + l)
+  __device__ bool len(uint32_t& s, uint32_t& l) {
+    const uint64_t x = varint();
+    if (bad || x > end - i) { bad = true; return false; }
+    s = i;
+    l = (uint32_t)x;
+    i += l;
+    return true;
+  }
+  // an unknown field (groups go to the host pass)
+  __device__ bool skip(uint32_t wt) {
+    uint32_t s, l;
+    switch (wt) {
+      case 0: varint(); break;
+      case 1: fixed(8); break;
+      case 2: len(s, l); break;
+      case 5: fixed(4); break;
+      default: bad = true;
+    }
+    return !bad;
+  }
+  __device__ bool tag(uint32_t& f, uint32_t& wt) {
+    const uint64_t t = varint();
+    f = (uint32_t)(t >> 3);
+    wt = (uint32_t)(t & 7);
+    if (bad || f == 0 || (t >> 3) > 0x1FFFFFFFull || wt == 3 || wt == 4) bad = true;
+    return !bad;
+  }
+};
+
+// a value of interest: AnyValue type (OSE_ATTR_* plus kNested / kAttrBytes) and payload
+constexpr uint32_t kNested = 6, kAttrBytes = 7;
+struct Val {
+  uint32_t type;   // OSE_ATTR_ABSENT when the key was not seen
+  uint32_t off, len;
+  uint64_t v;
+};
+
+// AnyValue [s, e): the last oneof field wins; returns its pdata size
+// contribution (ProtoSizer::any_value) or sets nested / bad
+__device__ uint64_t any_value(Rd& r, uint32_t s, uint32_t e, Val& out) {
+  const uint32_t save_i = r.i, save_end = r.end;
+  r.i = s;
+  r.end = e;
+  out.type = OSE_ATTR_OTHER;   // empty AnyValue: TEmpty (size 0)
+  out.off = out.len = 0;
+  out.v = 0;
+  uint64_t sz = 0;
+  uint32_t f, wt;
+  while (r.more() && r.tag(f, wt)) {
+    uint32_t ps, pl;
+    switch (f) {
+      case 1:
+        if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+        out.type = OSE_ATTR_STR; out.off = ps; out.len = pl; out.v = 0;
+        sz = field_len(pl);
+        break;
+      case 2:
+        if (wt != 0) { r.bad = true; break; }
+        out.v = r.varint() != 0; out.type = OSE_ATTR_BOOL;
+        sz = 2;
+        break;
+      case 3:
+        if (wt != 0) { r.bad = true; break; }
+        out.v = r.varint(); out.type = OSE_ATTR_INT;
+        sz = 1 + sov(out.v);
+        break;
+      case 4:
+        if (wt != 1) { r.bad = true; break; }
+        out.v = r.fixed(8); out.type = OSE_ATTR_DOUBLE;
+        sz = 9;
+        break;
+      case 5:
+      case 6:
+        if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+        out.type = kNested;
+        break;
+      case 7:
+        if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+        out.type = kAttrBytes; out.off = ps; out.len = pl;
+        sz = field_len(pl);
+        break;
+      default:
+        r.skip(wt);
+    }
+  }
+  if (out.type == OSE_ATTR_OTHER) sz = 0;
+  r.i = save_i;
+  r.end = save_end;
+  return sz;
+}
+
+// one KeyValue [s, e): key, value and its size (ProtoSizer::key_value, gogo)
+__device__ uint64_t key_value(Rd& r, uint32_t s, uint32_t e, uint32_t& ko, uint32_t& kl, Val& val) {
+  const uint32_t save_i = r.i, save_end = r.end;
+  r.i = s;
+  r.end = e;
+  uint32_t nkey = 0, nval = 0, vs = 0, vl = 0;
+  ko = kl = 0;
+  uint32_t f, wt;
+  while (r.more() && r.tag(f, wt)) {
+    uint32_t ps, pl;
+    if (f == 1) {
+      if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+      ko = ps; kl = pl; nkey++;
+    } else if (f == 2) {
+      if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+      vs = ps; vl = pl; nval++;
+    } else {
+      r.skip(wt);
+    }
+  }
+  r.i = save_i;
+  r.end = save_end;
+  if (nkey > 1 || nval > 1) { r.bad = true; return 0; }   // field merges: host pass
+  uint64_t av = 0;
+  val.type = OSE_ATTR_OTHER;
+  val.off = val.len = 0;
+  val.v = 0;
+  if (nval) av = any_value(r, vs, vs + vl, val);
+  if (val.type == kNested) r.bad = true;                   // nested sizes: host pass
+  return str_field(kl) + field_len(av);
+}
+
+// the roles of key [o, o + l) (0 = not a key of interest)
+__device__ uint32_t key_roles(const OtlpArgs& a, Rd& r, uint32_t o, uint32_t l) {
+  if (l >= 64 || !((a.key_lens >> l) & 1)) return 0;
+  uint32_t roles = 0;
+  for (uint32_t k = 0; k < a.n_keys; k++) {
+    const OtlpKeyDev kd = a.keys[k];
+    if (kd.len != l) continue;
+    uint32_t q = 0;
+    while (q < l && r.br.at(o + q) == a.key_bytes[kd.off + q]) q++;
+    if (q == l) roles |= kd.roles;
+  }
+  return roles;
+}
+
+__device__ bool same_bytes(Rd& r, uint32_t a0, uint32_t b0, uint32_t n) {
+  for (uint32_t q = 0; q < n; q++)
+    if (r.br.at(a0 + q) != r.br.at(b0 + q)) return false;
+  return true;
+}
+
+// attributes of an Event / Link: sizes only (scalar values), [s, e)
+__device__ uint64_t nested_attr(Rd& r, uint32_t s, uint32_t e) {
+  uint32_t ko, kl;
+  Val v;
+  return field_len(key_value(r, s, e, ko, kl, v));
+}
+}  // namespace
+
+__global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * kOThreads;
+  for (uint64_t i = (uint64_t)blockIdx.x * kOThreads + threadIdx.x; i < a.n_spans; i += stride) {
+    const uint64_t ref = a.span_ref[i];
+    const uint32_t s0 = (uint32_t)ref, s1 = s0 + (uint32_t)(ref >> 32);
+    Rd r(a.pb, s0, s1);
+    uint64_t hi = 0, lo = 0, start = 0, end = 0;
+    bool tid_nz = false, sid_nz = false, pid_nz = false;
+    uint32_t ts_len = 0, name_off = 0, name_len = 0, kind = 0, flags = 0;
+    uint32_t dr_attrs = 0, dr_events = 0, dr_links = 0, st_msg = 0, st_code = 0;
+    uint64_t attrs_sz = 0, events_sz = 0, links_sz = 0;
+    uint32_t found = 0;   // roles seen (first occurrence wins)
+    Val mnew{0, 0, 0, 0}, mold{0, 0, 0, 0}, route{0, 0, 0, 0}, utmpl{0, 0, 0, 0}, upath{0, 0, 0, 0},
+        target{0, 0, 0, 0};
+    bool full_seen = false, host_key = false;
+    uint32_t f, wt;
+    while (r.more() && r.tag(f, wt)) {
+      uint32_t ps, pl;
+      switch (f) {
+        case 1:   // trace_id
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          if (pl == 16) {
+            hi = lo = 0;
+            for (uint32_t k = 0; k < 8; k++) hi = hi << 8 | r.br.at(ps + k);
+            for (uint32_t k = 0; k < 8; k++) lo = lo << 8 | r.br.at(ps + 8 + k);
+            tid_nz = (hi | lo) != 0;
+          } else if (pl == 0) {
+            hi = lo = 0;
+            tid_nz = false;
+          } else {
+            r.bad = true;
+          }
+          break;
+        case 2:
+        case 4: {   // span_id / parent_span_id
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          bool nz = false;
+          if (pl == 8) {
+            for (uint32_t k = 0; k < 8; k++) nz |= r.br.at(ps + k) != 0;
+          } else if (pl != 0) {
+            r.bad = true;
+          }
+          if (f == 2) sid_nz = nz; else pid_nz = nz;
+          break;
+        }
+        case 3:
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          ts_len = pl;
+          break;
+        case 5:
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          name_off = ps;
+          name_len = pl;
+          break;
+        case 6:
+          if (wt != 0) { r.bad = true; break; }
+          kind = (uint32_t)r.varint();
+          break;
+        case 7:
+        case 8:
+          if (wt != 1) { r.bad = true; break; }
+          if (f == 7) start = r.fixed(8); else end = r.fixed(8);
+          break;
+        case 9: {   // attributes
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          uint32_t ko, kl;
+          Val v;
+          attrs_sz += field_len(key_value(r, ps, ps + pl, ko, kl, v));
+          if (r.bad) break;
+          const uint32_t roles = key_roles(a, r, ko, kl) & ~found;
+          if (!roles) break;
+          found |= roles;
+          if (roles & kRoleMethodNew) mnew = v;
+          if (roles & kRoleMethodOld) mold = v;
+          if (roles & kRoleRoute) route = v;
+          if (roles & kRoleUrlTmpl) utmpl = v;
+          if (roles & kRoleUrlPath) upath = v;
+          if (roles & kRoleTarget) target = v;
+          if (roles & kRoleFull) full_seen = true;
+          if (roles & kRoleHost) host_key = true;
+          for (uint32_t k = 0; k < a.n_attr_keys; k++)
+            if (roles & (kRoleAttr0 << k)) {
+              const uint64_t j = (uint64_t)k * a.n_spans + i;
+              uint32_t t = v.type == kAttrBytes ? OSE_ATTR_OTHER : v.type;
+              a.attr_type[j] = (uint8_t)t;
+              a.attr_val[j] = t == OSE_ATTR_STR ? ((uint64_t)v.off | ((uint64_t)v.len << 32)) : v.v;
+            }
+          break;
+        }
+        case 10: if (wt != 0) r.bad = true; else dr_attrs = (uint32_t)r.varint(); break;
+        case 11: {   // events: time, name, attributes, dropped
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          const uint32_t save_i = r.i, save_end = r.end;
+          r.i = ps;
+          r.end = ps + pl;
+          uint64_t t = 0, ea = 0;
+          uint32_t nl = 0, dr = 0, f2, w2, qs, ql;
+          while (r.more() && r.tag(f2, w2)) {
+            if (f2 == 1) { if (w2 != 1) r.bad = true; else t = r.fixed(8); }
+            else if (f2 == 2) { if (w2 != 2 || !r.len(qs, ql)) r.bad = true; else nl = ql; }
+            else if (f2 == 3) { if (w2 != 2 || !r.len(qs, ql)) r.bad = true; else ea += nested_attr(r, qs, qs + ql); }
+            else if (f2 == 4) { if (w2 != 0) r.bad = true; else dr = (uint32_t)r.varint(); }
+            else r.skip(w2);
+          }
+          r.i = save_i;
+          r.end = save_end;
+          events_sz += field_len((t ? 9 : 0) + str_field(nl) + ea + varint_field(dr));
+          break;
+        }
+        case 12: if (wt != 0) r.bad = true; else dr_events = (uint32_t)r.varint(); break;
+        case 13: {   // links: trace_id, span_id, trace_state, attributes, dropped, flags
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          const uint32_t save_i = r.i, save_end = r.end;
+          r.i = ps;
+          r.end = ps + pl;
+          uint64_t la = 0;
+          uint32_t tsl = 0, dr = 0, lf = 0, f2, w2, qs, ql;
+          bool lt = false, ls = false;
+          while (r.more() && r.tag(f2, w2)) {
+            if (f2 == 1 || f2 == 2) {
+              if (w2 != 2 || !r.len(qs, ql)) { r.bad = true; break; }
+              const uint32_t want = f2 == 1 ? 16 : 8;
+              bool nz = false;
+              if (ql == want) { for (uint32_t k = 0; k < ql; k++) nz |= r.br.at(qs + k) != 0; }
+              else if (ql != 0) r.bad = true;
+              if (f2 == 1) lt = nz; else ls = nz;
+            } else if (f2 == 3) { if (w2 != 2 || !r.len(qs, ql)) r.bad = true; else tsl = ql; }
+            else if (f2 == 4) { if (w2 != 2 || !r.len(qs, ql)) r.bad = true; else la += nested_attr(r, qs, qs + ql); }
+            else if (f2 == 5) { if (w2 != 0) r.bad = true; else dr = (uint32_t)r.varint(); }
+            else if (f2 == 6) { if (w2 != 5) r.bad = true; else lf = (uint32_t)r.fixed(4); }
+            else r.skip(w2);
+          }
+          r.i = save_i;
+          r.end = save_end;
+          links_sz += field_len((lt ? 18 : 2) + (ls ? 10 : 2) + str_field(tsl) + la + varint_field(dr) + (lf ? 5 : 0));
+          break;
+        }
+        case 14: if (wt != 0) r.bad = true; else dr_links = (uint32_t)r.varint(); break;
+        case 15: {   // status: message (2), code (3); merges
+          if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+          const uint32_t save_i = r.i, save_end = r.end;
+          r.i = ps;
+          r.end = ps + pl;
+          uint32_t f2, w2, qs, ql;
+          while (r.more() && r.tag(f2, w2)) {
+            if (f2 == 2) { if (w2 != 2 || !r.len(qs, ql)) r.bad = true; else st_msg = ql; }
+            else if (f2 == 3) { if (w2 != 0) r.bad = true; else st_code = (uint32_t)r.varint(); }
+            else r.skip(w2);
+          }
+          r.i = save_i;
+          r.end = save_end;
+          break;
+        }
+        case 16: if (wt != 5) r.bad = true; else flags = (uint32_t)r.fixed(4); break;
+        default:
+          r.skip(wt);
+      }
+    }
+    // the url path source and the values AsString would have to format
+    const Val& m = (found & kRoleMethodNew) ? mnew : mold;
+    const bool has_m = (found & (kRoleMethodNew | kRoleMethodOld)) != 0;
+    bool host = r.bad || host_key;
+    if (found & kRoleRoute) host |= route.type != OSE_ATTR_STR;
+    uint32_t uf = 0;
+    ose_strref path{0, 0};
+    if (has_m && !host) {
+      uf |= OSE_URL_HAS_METHOD;
+      if (m.type != OSE_ATTR_STR) host = true;
+      else if (m.len == name_len && same_bytes(r, m.off, name_off, name_len)) uf |= OSE_URL_NAME_EQ_METHOD;
+      const bool client = (int32_t)kind == OSE_KIND_CLIENT;
+      const Val& tv = client ? utmpl : route;
+      if (found & (client ? kRoleUrlTmpl : kRoleRoute)) {
+        if (tv.type != OSE_ATTR_STR) uf |= OSE_URL_TGT_NONSTR;
+        else uf |= tv.len == 0 ? OSE_URL_TGT_STR_EMPTY : OSE_URL_TGT_STR;
+      }
+      if (found & kRoleUrlPath) {
+        uf |= OSE_URL_PATH_RAW;
+        if (upath.type != OSE_ATTR_STR) host = true;
+        path = ose_strref{upath.off, upath.len};
+      } else if (found & kRoleTarget) {
+        uf |= OSE_URL_PATH_TARGET;
+        if (target.type != OSE_ATTR_STR) host = true;
+        path = ose_strref{target.off, target.len};
+      } else if (full_seen) {
+        host = true;   // net/url.Parse
+      }
+    }
+    if (host) {
+      a.host_flag[i] = 1;
+      const uint32_t slot = atomicAdd(a.host_count, 1u);
+      if (slot < a.host_cap) a.host_list[slot] = (uint32_t)i;
+      continue;
+    }
+    a.host_flag[i] = 0;
+    for (uint32_t k = 0; k < a.n_attr_keys; k++)   // keys this span does not carry
+      if (!(found & (kRoleAttr0 << k))) a.attr_type[(uint64_t)k * a.n_spans + i] = OSE_ATTR_ABSENT;
+    a.tid[2 * i] = hi;
+    a.tid[2 * i + 1] = lo;
+    a.start[i] = start;
+    a.end[i] = end;
+    const int32_t code = (int32_t)st_code;
+    a.status[i] = (uint8_t)(code >= 0 && code <= 2 ? code : 3);
+    const int32_t k32 = (int32_t)kind;
+    a.kind[i] = (uint8_t)(k32 < 0 ? 0 : (k32 > 255 ? 255 : k32));
+    a.url_flags[i] = (uint8_t)uf;
+    a.path[i] = path;
+    a.route[i] = (found & kRoleRoute) ? ose_strref{route.off, route.len} : ose_strref{0, 0};
+    a.name_len[i] = name_len;
+    if (a.attr_match) a.attr_match[i] = 0;
+    // ProtoSizer::span (gogo): ids, Status and KeyValue.value always emitted
+    const uint64_t st = str_field(st_msg) + varint_field((uint64_t)(int64_t)(int32_t)st_code);
+    const uint64_t sz = (tid_nz ? 18 : 2) + (sid_nz ? 10 : 2) + str_field(ts_len) + (pid_nz ? 10 : 2) +
+                        str_field(name_len) + varint_field((uint64_t)(int64_t)k32) + (start ? 9 : 0) + (end ? 9 : 0) +
+                        attrs_sz + varint_field(dr_attrs) + events_sz + varint_field(dr_events) + links_sz +
+                        varint_field(dr_links) + field_len(st) + (flags ? 6 : 0);
+    a.span_size[i] = (uint32_t)sz;
+  }
+}
+
+// host-pass results: every column of the listed spans
+__global__ __launch_bounds__(kOThreads) void otlp_fix_kernel(OtlpFixArgs a) {
+  const uint32_t q = blockIdx.x * kOThreads + threadIdx.x;
+  if (q >= a.n) return;
+  const OtlpFix& x = a.fix[q];
+  const uint64_t i = x.idx;
+  a.tid[2 * i] = x.hi;
+  a.tid[2 * i + 1] = x.lo;
+  a.start[i] = x.start;
+  a.end[i] = x.end;
+  a.status[i] = x.status;
+  a.kind[i] = x.kind;
+  a.url_flags[i] = x.url_flags;
+  a.path[i] = x.path;
+  a.route[i] = x.route;
+  a.name_len[i] = x.name_len;
+  a.span_size[i] = x.span_size;
+  if (a.attr_match) a.attr_match[i] = x.attr_match;
+  for (uint32_t k = 0; k < a.n_attr_keys; k++) {
+    a.attr_type[(uint64_t)k * a.n_spans + i] = a.fix_type[(uint64_t)q * a.n_attr_keys + k];
+    a.attr_val[(uint64_t)k * a.n_spans + i] = a.fix_val[(uint64_t)q * a.n_attr_keys + k];
+  }
+}
+
+void launch_otlp_spans(const OtlpArgs& a, hipStream_t st) {
+  const uint64_t blocks = std::min<uint64_t>((a.n_spans + kOThreads - 1) / kOThreads, 8192);
+  if (blocks) hipLaunchKernelGGL(otlp_span_kernel, dim3((uint32_t)blocks), dim3(kOThreads), 0, st, a);
+}
+void launch_otlp_fix(const OtlpFixArgs& a, hipStream_t st) {
+  const uint32_t blocks = (a.n + kOThreads - 1) / kOThreads;
+  if (blocks) hipLaunchKernelGGL(otlp_fix_kernel, dim3(blocks), dim3(kOThreads), 0, st, a);
+}
+
+}  // namespace ose
