@@ -246,6 +246,7 @@ typedef struct ose_batch ose_batch;
  * regexp to a DFA; a regexp the DFA compiler cannot express is OSE_ENOTSUP
  * (there is no host fallback).                                              */
 int ose_engine_create(const char* cfg_json, ose_engine** out);
+/* Every ose_batch and ose_otlp_batch of the engine must be released first. */
 void ose_engine_destroy(ose_engine* eng);
 
 /* Device selection: an engine lives on the HIP device that is current on

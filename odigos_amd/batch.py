@@ -258,6 +258,7 @@ class OtlpBatch:
 
     def __init__(self, engine: "Engine", pb: bytes, stream=None, tmpl_cap: int | None = None):
         self.L = engine.L
+        self.eng = engine   # the engine must outlive its batches (ose_otlp_release before ose_engine_destroy)
         h = C.c_void_p()
         s = None if stream is None else C.c_void_p(stream)
         native.check(self.L.ose_otlp_decode(engine.h, pb, len(pb), s, C.byref(h)))

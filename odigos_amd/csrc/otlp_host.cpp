@@ -272,6 +272,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   a.host_count = host_count;
   a.host_list = host_list;
   a.host_cap = (uint32_t)N;
+  (void)hipGetLastError();   // a stale error of an earlier call must not be reported as this launch's
   Engine::Timed tm{};
   e->prof_begin("otlp_span_kernel", st, tm);
   launch_otlp_spans(a, st);

@@ -401,7 +401,10 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
     }
     a.host_flag[i] = 0;
     for (uint32_t k = 0; k < a.n_attr_keys; k++)   // keys this span does not carry
-      if (!(found & (kRoleAttr0 << k))) a.attr_type[(uint64_t)k * a.n_spans + i] = OSE_ATTR_ABSENT;
+      if (!(found & (kRoleAttr0 << k))) {
+        a.attr_type[(uint64_t)k * a.n_spans + i] = OSE_ATTR_ABSENT;
+        a.attr_val[(uint64_t)k * a.n_spans + i] = 0;
+      }
     a.tid[2 * i] = hi;
     a.tid[2 * i + 1] = lo;
     a.start[i] = start;
