@@ -67,6 +67,9 @@ class Generator:
             L.osegen_columns.restype = C.POINTER(native.Columns)
             L.osegen_columns.argtypes = [C.c_void_p]
             L.osegen_free.argtypes = [C.c_void_p]
+            L.osegen_otlp.restype = C.c_void_p
+            L.osegen_otlp.argtypes = [C.POINTER(native.Columns), C.c_int, C.POINTER(C.c_uint64)]
+            L.osegen_otlp_free.argtypes = [C.c_void_p]
             Generator._L = L
         if world is None:
             self.h = Generator._L.osegen_create(workload.encode(), seed, n_spans, threads, int(shuffle))
@@ -84,6 +87,15 @@ class Generator:
         if field == "arena":
             n = (n + 15) // 16 * 16 + 16
         return host_array(getattr(self.cols, field), n)
+
+    def otlp(self, threads: int = 8) -> bytes:
+        """The batch as a serialized OTLP TracesData (gen_otlp.cpp)."""
+        n = C.c_uint64()
+        p = Generator._L.osegen_otlp(C.byref(self.cols), threads, C.byref(n))
+        try:
+            return C.string_at(p, n.value)
+        finally:
+            Generator._L.osegen_otlp_free(p)
 
     def __del__(self):
         if getattr(self, "h", None):
