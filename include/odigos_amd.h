@@ -410,6 +410,11 @@ int ose_allreduce_counters(const int64_t* local, int64_t* node, uint64_t n, void
  * the columns are complete on that stream.  res_attrset ids index the
  * attribute sets ose_otlp_attrset returns ({"key": "value", ...}).         */
 typedef struct ose_otlp_batch ose_otlp_batch;
+/* Pinned host memory for a receiver to read requests into: ose_otlp_decode
+ * copies a pinned message straight to HBM (a pageable one goes through the
+ * batch's pinned staging first).                                           */
+int ose_host_alloc(size_t bytes, void** out);
+void ose_host_free(void* p);
 int ose_otlp_decode(ose_engine* eng, const void* pb, size_t len, void* hip_stream, ose_otlp_batch** out);
 const ose_columns* ose_otlp_columns(const ose_otlp_batch* b);   /* device pointers */
 uint32_t ose_otlp_host_spans(const ose_otlp_batch* b);

@@ -268,12 +268,18 @@ class OtlpBatch:
     columns owned by the engine plus HBM outputs, usable wherever a
     DeviceBatch is (Engine.process_device)."""
 
-    def __init__(self, engine: "Engine", pb: bytes, stream=None, tmpl_cap: int | None = None):
+    def __init__(self, engine: "Engine", pb, stream=None, tmpl_cap: int | None = None, length: int | None = None):
+        """pb: the message bytes, or the address of a buffer (e.g. PinnedBuffer) with `length`."""
         self.L = engine.L
         self.eng = engine   # the engine must outlive its batches (ose_otlp_release before ose_engine_destroy)
         h = C.c_void_p()
         s = None if stream is None else C.c_void_p(stream)
-        native.check(self.L.ose_otlp_decode(engine.h, pb, len(pb), s, C.byref(h)))
+        if isinstance(pb, (bytes, bytearray)):
+            buf = C.c_char_p(bytes(pb)) if isinstance(pb, bytearray) else C.c_char_p(pb)
+            addr, n = C.cast(buf, C.c_void_p), len(pb)
+        else:
+            addr, n = C.c_void_p(int(pb)), int(length)
+        native.check(self.L.ose_otlp_decode(engine.h, addr, n, s, C.byref(h)))
         self.h = h
         self.cols = native.Columns.from_buffer_copy(self.L.ose_otlp_columns(h).contents)
         self.host_spans = int(self.L.ose_otlp_host_spans(h))
@@ -315,5 +321,23 @@ class OtlpBatch:
         if getattr(self, "h", None):
             self.L.ose_otlp_release(self.h)
             self.h = None
+
+    __del__ = close
+
+
+class PinnedBuffer:
+    """Pinned host memory from the engine library (ose_host_alloc)."""
+
+    def __init__(self, data: bytes):
+        self.L = native.lib()
+        p = C.c_void_p()
+        native.check(self.L.ose_host_alloc(len(data), C.byref(p)))
+        self.p, self.n = p.value, len(data)
+        C.memmove(self.p, data, len(data))
+
+    def close(self):
+        if getattr(self, "p", None):
+            self.L.ose_host_free(C.c_void_p(self.p))
+            self.p = None
 
     __del__ = close

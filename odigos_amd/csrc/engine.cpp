@@ -524,6 +524,17 @@ void ose_engine_destroy(ose_engine* eng) {
   delete reinterpret_cast<Engine*>(eng);
 }
 
+int ose_host_alloc(size_t bytes, void** out) {
+  if (!out) return fail(OSE_EINVAL, "NULL argument");
+  int rc = ensure_device();
+  if (rc) return rc;
+  HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return 0;
+}
+void ose_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 int ose_set_device(int device) {
   int rc = ensure_device();
   if (rc) return rc;

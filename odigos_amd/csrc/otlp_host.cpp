@@ -10,8 +10,12 @@
 //   3. otlp_span_kernel decodes every span on the GPU;
 //   4. the spans it lists get the host pass: pb_span + columnize_span, their
 //      strings appended after the message bytes, written by otlp_fix_kernel.
+#include <algorithm>
 #include <cstring>
 #include <map>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
 
 #include "columnize.hpp"
 #include "engine_internal.hpp"
@@ -135,54 +139,281 @@ void release_otlp(Engine* e) {
 }
 
 namespace {
+// memcpy over threads for large copies into pinned staging
+void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n) {
+  const size_t kChunk = size_t(64) << 20;
+  if (n < 2 * kChunk) { std::memcpy(dst, src, n); return; }
+  const int T = (int)std::min<size_t>(16, n / kChunk);
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++)
+    th.emplace_back([=]() { const size_t a = n * t / T, b = n * (t + 1) / T; std::memcpy(dst + a, src + a, b - a); });
+  std::memcpy(dst, src, n / T);
+  for (auto& x : th) x.join();
+}
+
+// The structural walk, resources split over threads.  Resource and scope
+// messages repeat across a batch (one SDK, one pod), so their columns are
+// cached by message bytes.
+struct Walked {
+  std::vector<uint64_t> span_ref;
+  std::vector<uint32_t> span_res, span_scope;
+  std::vector<uint32_t> res_svc, res_svc_str, res_attrset, res_size, scope_size, scope_res;
+  std::vector<uint8_t> res_ok;
+  std::vector<uint64_t> attr_res;
+  std::vector<std::vector<std::pair<std::string, std::string>>> sets;
+  std::string err;
+};
+struct WalkChunk {
+  std::vector<uint64_t> span_ref;
+  std::vector<uint32_t> span_res, span_scope;   // chunk-local indices
+  std::vector<uint32_t> res_svc, res_svc_str, res_set, res_size, scope_size, scope_res;
+  std::vector<uint8_t> res_ok;
+  std::vector<uint64_t> attr_res;
+  std::vector<std::vector<std::pair<std::string, std::string>>> sets;   // chunk-local first appearance
+  std::string err;
+};
+struct CachedRes {
+  uint32_t svc, svc_str, set, rpart;
+  uint8_t ok;
+  uint64_t attr_res;
+};
+uint64_t sov64(uint64_t x) { uint64_t n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
+uint64_t flen(uint64_t l) { return 1 + sov64(l) + l; }
+
+void walk_chunk(const ColumnizeCtx& ctx, const uint8_t* p, const std::vector<std::pair<size_t, size_t>>& rsl,
+                size_t r0, size_t r1, WalkChunk& c) {
+  std::unordered_map<std::string_view, CachedRes> rcache;
+  std::unordered_map<std::string_view, uint32_t> scache;
+  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
+  ProtoSizer sizer;
+  std::vector<std::pair<size_t, size_t>> resf, scopes, deprecated;
+  for (size_t r = r0; r < r1; r++) {
+    const size_t ro = rsl[r].first, rl = rsl[r].second;
+    PbReader rr(p + ro, rl);
+    resf.clear();
+    scopes.clear();
+    deprecated.clear();
+    size_t schema = 0;
+    uint32_t f, wt;
+    while (rr.more() && rr.tag(f, wt)) {
+      size_t o, l;
+      if (f == 1 || f == 2 || f == 1000 || f == 3) {
+        if (wt != 2 || !rr.bytes(o, l)) { rr.fail(); break; }
+        if (f == 1) resf.emplace_back(ro + o, l);
+        else if (f == 3) schema = l;
+        else (f == 2 ? scopes : deprecated).emplace_back(ro + o, l);
+      } else {
+        rr.skip(wt, f);
+      }
+    }
+    if (!rr.ok) { c.err = "OTLP protobuf: malformed ResourceSpans"; return; }
+    if (scopes.empty()) scopes.swap(deprecated);
+    // the resource's columns (cached by its message bytes)
+    CachedRes cr{};
+    const std::string_view key = resf.size() == 1 ? std::string_view((const char*)p + resf[0].first, resf[0].second)
+                                                  : std::string_view();
+    auto it = resf.size() <= 1 ? rcache.find(key) : rcache.end();
+    if (it != rcache.end()) {
+      cr = it->second;
+    } else {
+      AttrMap attrs;
+      uint32_t dropped = 0;
+      for (auto& x : resf)
+        if (!pb_resource(p + x.first, x.second, attrs, dropped)) { c.err = "OTLP protobuf: malformed Resource"; return; }
+      const ResourceCols rc = columnize_resource(ctx, attrs);
+      cr.svc = rc.svc;
+      cr.svc_str = rc.svc_str;
+      cr.ok = rc.url_ok;
+      cr.attr_res = rc.attr_res;
+      auto si = set_ids.find(rc.attrset);
+      if (si == set_ids.end()) {
+        si = set_ids.emplace(rc.attrset, (uint32_t)c.sets.size()).first;
+        c.sets.push_back(rc.attrset);
+      }
+      cr.set = si->second;
+      cr.rpart = (uint32_t)flen(sizer.attrs(attrs, 1) + (dropped ? 1 + sov64(dropped) : 0));   // Resource: always emitted
+      if (resf.size() <= 1) rcache.emplace(key, cr);
+    }
+    const uint32_t rloc = (uint32_t)c.res_svc.size();
+    c.res_svc.push_back(cr.svc);
+    c.res_svc_str.push_back(cr.svc_str);
+    c.res_ok.push_back(cr.ok);
+    c.attr_res.push_back(cr.attr_res);
+    c.res_set.push_back(cr.set);
+    c.res_size.push_back(cr.rpart + (uint32_t)(schema ? flen(schema) : 0));
+    for (auto& so : scopes) {
+      const uint32_t sloc = (uint32_t)c.scope_size.size();
+      PbReader sr(p + so.first, so.second);
+      size_t sschema = 0;
+      std::vector<std::pair<size_t, size_t>> scf;
+      while (sr.more() && sr.tag(f, wt)) {
+        size_t o, l;
+        if (f == 1 || f == 2 || f == 3) {
+          if (wt != 2 || !sr.bytes(o, l)) { sr.fail(); break; }
+          if (f == 1) {
+            scf.emplace_back(so.first + o, l);
+          } else if (f == 3) {
+            sschema = l;
+          } else {
+            const uint64_t off = so.first + o;
+            if (off > 0xFFFFFFFFull || l > 0xFFFFFFFFull) { c.err = "span beyond the 4 GiB arena range"; return; }
+            c.span_ref.push_back(off | ((uint64_t)l << 32));
+            c.span_res.push_back(rloc);
+            c.span_scope.push_back(sloc);
+          }
+        } else {
+          sr.skip(wt, f);
+        }
+      }
+      if (!sr.ok) { c.err = "OTLP protobuf: malformed ScopeSpans"; return; }
+      uint32_t spart;
+      const std::string_view sk = scf.size() == 1 ? std::string_view((const char*)p + scf[0].first, scf[0].second)
+                                                  : std::string_view();
+      auto si = scf.size() <= 1 ? scache.find(sk) : scache.end();
+      if (si != scache.end()) {
+        spart = si->second;
+      } else {
+        ScopeSpans meta;
+        for (auto& x : scf)
+          if (!pb_scope(p + x.first, x.second, meta)) { c.err = "OTLP protobuf: malformed InstrumentationScope"; return; }
+        spart = (uint32_t)sizer.scope_fixed(meta);   // schema_url empty here
+        if (scf.size() <= 1) scache.emplace(sk, spart);
+      }
+      c.scope_size.push_back(spart + (uint32_t)(sschema ? flen(sschema) : 0));
+      c.scope_res.push_back(rloc);
+    }
+  }
+}
+
+bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
+  // top level: the ResourceSpans fields
+  std::vector<std::pair<size_t, size_t>> rsl;
+  PbReader top(p, n);
+  uint32_t f, wt;
+  while (top.more() && top.tag(f, wt)) {
+    size_t o, l;
+    if (f == 1) {
+      if (wt != 2 || !top.bytes(o, l)) { top.fail(); break; }
+      rsl.emplace_back(o, l);
+    } else if (!top.skip(wt, f)) {
+      break;
+    }
+  }
+  if (!top.ok) { w.err = "OTLP protobuf: malformed TracesData"; return false; }
+  const size_t R = rsl.size();
+  const int T = (int)std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1u, std::thread::hardware_concurrency()), R / 512}));
+  std::vector<WalkChunk> ch((size_t)T);
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back([&, t]() { walk_chunk(ctx, p, rsl, R * t / T, R * (t + 1) / T, ch[t]); });
+    walk_chunk(ctx, p, rsl, 0, R / T, ch[0]);
+    for (auto& x : th) x.join();
+  }
+  for (auto& c : ch)
+    if (!c.err.empty()) { w.err = c.err; return false; }
+  // merge: global indices, attribute sets in first-appearance order
+  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
+  std::vector<std::vector<uint32_t>> set_map(ch.size());
+  size_t nspan = 0, nres = 0, nscope = 0;
+  for (size_t t = 0; t < ch.size(); t++) {
+    for (auto& st : ch[t].sets) {
+      auto it = set_ids.find(st);
+      if (it == set_ids.end()) {
+        it = set_ids.emplace(st, (uint32_t)w.sets.size()).first;
+        w.sets.push_back(st);
+      }
+      set_map[t].push_back(it->second);
+    }
+    nspan += ch[t].span_ref.size();
+    nres += ch[t].res_svc.size();
+    nscope += ch[t].scope_size.size();
+  }
+  w.span_ref.resize(nspan);
+  w.span_res.resize(nspan);
+  w.span_scope.resize(nspan);
+  w.res_svc.resize(nres);
+  w.res_svc_str.resize(nres);
+  w.res_attrset.resize(nres);
+  w.res_size.resize(nres);
+  w.res_ok.resize(nres);
+  w.attr_res.resize(nres);
+  w.scope_size.resize(nscope);
+  w.scope_res.resize(nscope);
+  std::vector<size_t> so(ch.size()), ro(ch.size()), co(ch.size());
+  for (size_t t = 1; t < ch.size(); t++) {
+    so[t] = so[t - 1] + ch[t - 1].span_ref.size();
+    ro[t] = ro[t - 1] + ch[t - 1].res_svc.size();
+    co[t] = co[t - 1] + ch[t - 1].scope_size.size();
+  }
+  auto place = [&](size_t t) {
+    const WalkChunk& c = ch[t];
+    for (size_t k = 0; k < c.span_ref.size(); k++) {
+      w.span_ref[so[t] + k] = c.span_ref[k];
+      w.span_res[so[t] + k] = (uint32_t)(ro[t] + c.span_res[k]);
+      w.span_scope[so[t] + k] = (uint32_t)(co[t] + c.span_scope[k]);
+    }
+    for (size_t k = 0; k < c.res_svc.size(); k++) {
+      w.res_svc[ro[t] + k] = c.res_svc[k];
+      w.res_svc_str[ro[t] + k] = c.res_svc_str[k];
+      w.res_attrset[ro[t] + k] = set_map[t][c.res_set[k]];
+      w.res_size[ro[t] + k] = c.res_size[k];
+      w.res_ok[ro[t] + k] = c.res_ok[k];
+      w.attr_res[ro[t] + k] = c.attr_res[k];
+    }
+    for (size_t k = 0; k < c.scope_size.size(); k++) {
+      w.scope_size[co[t] + k] = c.scope_size[k];
+      w.scope_res[co[t] + k] = (uint32_t)(ro[t] + c.scope_res[k]);
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < ch.size(); t++) th.emplace_back(place, t);
+    place(0);
+    for (auto& x : th) x.join();
+  }
+  return true;
+}
+}  // namespace
+
+namespace {
 int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchImpl* b) {
   int rc;
   OtlpEngine* o = otlp_engine(e, rc);
   if (!o) return rc;
   if (len > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: message beyond the 4 GiB arena range");
-  // 1. bytes to pinned staging and H2D, the walk meanwhile
+  // 1. the bytes H2D (straight from the caller's buffer when it is pinned,
+  //    else through pinned staging), the walk meanwhile
   const size_t pb_cap = up(len + 16, 16);
-  if ((rc = b->stage.need(pb_cap))) return rc;
-  std::memcpy(b->stage.p, pb, len);
-  std::memset(b->stage.p + len, 0, pb_cap - len);
   const size_t fix_reserve = std::max<size_t>(1 << 16, len / 8);
   if ((rc = b->arena.need(pb_cap + fix_reserve + 16))) return rc;
-  HIP_TRY(hipMemcpyAsync(b->arena.p, b->stage.p, pb_cap, hipMemcpyHostToDevice, st));
-  PbWalk w;
-  if (!pb_walk(pb, len, w)) return fail(OSE_EINVAL, w.err);
+  hipPointerAttribute_t pa{};
+  const bool pinned = len && hipPointerGetAttributes(&pa, pb) == hipSuccess && pa.type == hipMemoryTypeHost;
+  (void)hipGetLastError();   // an unregistered pointer is not an error here
+  if (pinned) {
+    HIP_TRY(hipMemcpyAsync(b->arena.p, pb, len, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(b->arena.p + len, 0, pb_cap - len, st));
+  } else {
+    if ((rc = b->stage.need(pb_cap))) return rc;
+    par_memcpy(b->stage.p, pb, len);
+    std::memset(b->stage.p + len, 0, pb_cap - len);
+    HIP_TRY(hipMemcpyAsync(b->arena.p, b->stage.p, pb_cap, hipMemcpyHostToDevice, st));
+  }
+  Walked w;
+  if (!walk(o->ctx, pb, len, w)) return fail(OSE_EINVAL, w.err);
   HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
-  const uint64_t n = w.span_ref.size(), R = w.res.size(), S = w.scopes.size();
+  const uint64_t n = w.span_ref.size(), R = w.res_svc.size(), S = w.scope_size.size();
   if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: more than 2^32-16 spans");
   const uint32_t K = o->n_attr_keys;
-  // 2. resource / scope columns on the host
-  std::vector<uint32_t> res_svc(R), res_svc_str(R), res_attrset(R), res_size(R), scope_size(S), scope_res(S);
-  std::vector<uint8_t> res_ok(R);
-  std::vector<uint64_t> attr_res(R);
-  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
-  b->attrsets.clear();
+  b->attrsets = std::move(w.sets);
+  std::vector<uint32_t>& res_svc = w.res_svc;
+  std::vector<uint32_t>& res_svc_str = w.res_svc_str;
+  std::vector<uint32_t>& res_attrset = w.res_attrset;
+  std::vector<uint32_t>& res_size = w.res_size;
+  std::vector<uint32_t>& scope_size = w.scope_size;
+  std::vector<uint32_t>& scope_res = w.scope_res;
+  std::vector<uint8_t>& res_ok = w.res_ok;
+  std::vector<uint64_t>& attr_res = w.attr_res;
   ProtoSizer sizer;
-  for (uint64_t r = 0; r < R; r++) {
-    const ResourceCols rc2 = columnize_resource(o->ctx, w.res[r].attrs);
-    res_svc[r] = rc2.svc;
-    res_svc_str[r] = rc2.svc_str;
-    res_ok[r] = rc2.url_ok;
-    attr_res[r] = rc2.attr_res;
-    auto it = set_ids.find(rc2.attrset);
-    if (it == set_ids.end()) {
-      it = set_ids.emplace(rc2.attrset, (uint32_t)b->attrsets.size()).first;
-      b->attrsets.push_back(rc2.attrset);
-    }
-    res_attrset[r] = it->second;
-    ResourceSpans rs;
-    rs.resource_attrs = w.res[r].attrs;
-    rs.resource_dropped = w.res[r].dropped;
-    rs.schema_url = w.res[r].schema_url;
-    res_size[r] = (uint32_t)sizer.resource_fixed(rs);
-  }
-  for (uint64_t s = 0; s < S; s++) {
-    scope_size[s] = (uint32_t)sizer.scope_fixed(w.scopes[s].meta);
-    scope_res[s] = w.scopes[s].resource;
-  }
   // device columns: one slab
   const uint64_t N = std::max<uint64_t>(n, 1);
   struct Part { void** dst; size_t bytes; const void* src; };
@@ -299,7 +530,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   SpanCols sc;
   for (uint32_t q = 0; q < cnt; q++) {
     const uint32_t i = list[q];
-    const uint64_t ref = w.span_ref[i];
+    const uint64_t ref = w.span_ref[i];   // (Walked keeps the walk's arrays)
     Span sp;
     if (!pb_span(pb + (uint32_t)ref, (size_t)(ref >> 32), sp)) return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
     columnize_span(o->ctx, sp, attr_res[w.span_res[i]], sizer, sc);
@@ -407,6 +638,55 @@ int ose_otlp_decode(ose_engine* eng, const void* pb, size_t len, void* hip_strea
   }
   *out = reinterpret_cast<ose_otlp_batch*>(b);
   return 0;
+}
+
+// Test seam (CPU): the structural walk alone, for a pipeline config
+// {"odigossampling": ..., "odigosurltemplate": ..., "odigostrafficmetrics": ...};
+// the arrays as JSON, NULL on an error (osehost_last_error)
+char* osehost_otlp_walk(const char* cfg_json, const uint8_t* pb, size_t len) {
+  try {
+    Json cfg = parse_json(cfg_json);
+    UrlTemplateConfig url;
+    SamplingConfig sampling;
+    TrafficMetricsConfig traffic;
+    std::string err;
+    const Json* ju = cfg.get("odigosurltemplate");
+    const Json* js = cfg.get("odigossampling");
+    const Json* jt = cfg.get("odigostrafficmetrics");
+    if (ju && err.empty()) err = decode_url_config(*ju, url);
+    if (js && err.empty()) err = decode_sampling_config(*js, sampling);
+    if (jt && err.empty()) err = decode_traffic_config(*jt, traffic);
+    ColumnizeCtx ctx;
+    if (err.empty()) err = ctx.build(ju ? &url : nullptr, js ? &sampling : nullptr, jt ? &traffic : nullptr);
+    Walked w;
+    if (err.empty() && !walk(ctx, pb, len, w)) err = w.err;
+    if (!err.empty()) { fail(OSE_EINVAL, err); return nullptr; }
+    auto arr = [](const auto& v) {
+      Json a = Json::array();
+      for (auto x : v) a.push(Json::number(std::to_string((uint64_t)x)));
+      return a;
+    };
+    Json o = Json::object();
+    o.set("span_ref", arr(w.span_ref));
+    o.set("span_res", arr(w.span_res));
+    o.set("span_scope", arr(w.span_scope));
+    o.set("res_svc", arr(w.res_svc));
+    o.set("res_svc_str", arr(w.res_svc_str));
+    o.set("res_attrset", arr(w.res_attrset));
+    o.set("res_size", arr(w.res_size));
+    o.set("res_ok", arr(w.res_ok));
+    o.set("scope_size", arr(w.scope_size));
+    o.set("scope_res", arr(w.scope_res));
+    o.set("n_sets", Json::number(std::to_string(w.sets.size())));
+    std::string out;
+    dump_json(out, o);
+    char* r = static_cast<char*>(std::malloc(out.size() + 1));
+    std::memcpy(r, out.c_str(), out.size() + 1);
+    return r;
+  } catch (const std::exception& ex) {
+    fail(OSE_EINVAL, ex.what());
+    return nullptr;
+  }
 }
 
 int ose_otlp_download(const ose_otlp_batch* bb, const ose_columns* dst) {

@@ -119,7 +119,9 @@ def lib() -> C.CDLL:
         "ose_engine_service_id": (C.c_uint32, [_p, C.c_char_p, C.c_size_t]),
         "ose_engine_get_info": (C.c_int, [_p, C.POINTER(EngineInfo)]),
         "ose_set_device": (C.c_int, [C.c_int]),
-        "ose_otlp_decode": (C.c_int, [_p, C.c_char_p, C.c_size_t, _p, C.POINTER(_p)]),
+        "ose_otlp_decode": (C.c_int, [_p, _p, C.c_size_t, _p, C.POINTER(_p)]),
+        "ose_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(_p)]),
+        "ose_host_free": (None, [_p]),
         "ose_otlp_columns": (C.POINTER(Columns), [_p]),
         "ose_otlp_host_spans": (C.c_uint32, [_p]),
         "ose_otlp_attrset": (C.c_int, [_p, C.c_uint32, C.c_char_p, C.c_size_t]),
@@ -163,6 +165,7 @@ def lib() -> C.CDLL:
         "osehost_metrics_json": (_p, [_p]),
         "osehost_roundtrip": (_p, [C.c_char_p]),
         "osehost_pb_to_json": (_p, [C.c_char_p, C.c_size_t]),
+        "osehost_otlp_walk": (_p, [C.c_char_p, C.c_char_p, C.c_size_t]),
         "osehost_resource_sizes": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
         "osehost_as_string": (_p, [C.c_char_p]),
         "osehost_free": (None, [_p]),

@@ -399,3 +399,52 @@ def test_gpu_decode_rejects_malformed():
     # an empty message decodes to an empty batch
     ob = OtlpBatch(eng, b"")
     assert ob.cols.n_spans == 0
+
+
+# ---- CPU: the threaded structural walk of the ingest --------------------------------
+
+def _walk(cfg, pb):
+    L = native.lib()
+    p = L.osehost_otlp_walk(json.dumps(cfg).encode(), pb, len(pb))
+    if not p:
+        return None
+    return json.loads(native.take_bytes(p).decode("ascii"))
+
+
+def _check_walk(cfg, pb):
+    w = _walk(cfg, pb)
+    td = _pb_to_json(pb)
+    _, hb = _host_columns(cfg, td)
+    c = hb.cols
+    n, R, S = c.n_spans, c.n_resources, c.n_scopes
+    assert len(w["span_ref"]) == n and len(w["res_svc"]) == R and len(w["scope_size"]) == S
+    for name, col, cnt, dt in (("span_res", "resource", n, np.uint32), ("span_scope", "scope", n, np.uint32),
+                               ("res_svc", "res_svc", R, np.uint32), ("res_svc_str", "res_svc_str", R, np.uint32),
+                               ("res_attrset", "res_attrset", R, np.uint32), ("res_size", "res_size", R, np.uint32),
+                               ("scope_size", "scope_size", S, np.uint32), ("scope_res", "scope_resource", S, np.uint32)):
+        np.testing.assert_array_equal(np.array(w[name], dtype=dt), _arr(getattr(c, col), cnt, dt), err_msg=name)
+    if cfg.get("odigosurltemplate", {}).get("exclude"):
+        np.testing.assert_array_equal(np.array(w["res_ok"], dtype=np.uint8), _arr(c.res_url_ok, R, np.uint8))
+    assert w["n_sets"] == c.n_attrsets
+    # every span reference frames a Span payload inside the message
+    refs = np.array(w["span_ref"], dtype=np.uint64)
+    assert ((refs & 0xFFFFFFFF) + (refs >> 32) <= len(pb)).all()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_walk_matches_host_columns(seed):
+    rng = random.Random(seed)
+    td = _http_traces(rng, 60, odd=0.1) if seed % 2 else _rand_traces(rng, n_res=5)
+    _check_walk([CFG, CFG_EXCLUDE][seed % 2], to_pb(td))
+
+
+def test_walk_threaded_generated_batch():
+    # enough resources for the threaded walk (>= 1024), repeated resource and
+    # scope messages (the caches)
+    from odigos_amd.batch import Generator
+    g = Generator("fused", seed=0x0D16F001, n_spans=30_000, threads=4)
+    _check_walk(CFG_EXCLUDE, g.otlp(4))
+
+
+def test_walk_rejects_malformed():
+    assert _walk(CFG, b"\x0a\x05\x12\x03\x12") is None

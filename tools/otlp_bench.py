@@ -1,0 +1,118 @@
+"""OTLP protobuf ingest timed end to end on one GPU: a
+serialized TracesData in host memory (the C4 mix as an HTTP instrumentation
+would send it, odigos_amd/csrc/gen_otlp.cpp) → ose_otlp_decode (structural
+walk on the host, H2D, the span decoder, the host pass) → the three stages
+on the decoded columns.  PCIe-inclusive by construction: not a bench.py
+`value`.  One JSON line on stdout and in --out.
+
+Legs: decode from pinned memory (ose_host_alloc: a receiver reading into
+engine buffers), decode from pageable memory, and the stages after it.
+The span decoder's roofline: message bytes read + columns written per
+launch over its HIP-event time, against 8 TB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spans", type=int, default=10_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "otlp.json"))
+    args = ap.parse_args()
+    import torch
+    from bench import NODE_KEYS, cpu_share
+    from odigos_amd import native
+    from odigos_amd.batch import Engine, Generator, OtlpBatch, PinnedBuffer
+    from tests.workloads import c3_sampling_config
+    share, nproc, model = cpu_share()
+    threads = max(1, min(16, share))
+    t = time.perf_counter()
+    g = Generator("fused", seed=0x0D16F0A1, n_spans=args.spans, threads=threads)
+    pb = g.otlp(threads)
+    print(f"generated {len(pb) / 1e9:.2f} GB for {args.spans} spans in {time.perf_counter() - t:.1f}s", flush=True)
+    cfg = {"odigossampling": c3_sampling_config(), "odigosurltemplate": {},
+           "odigostrafficmetrics": {"res_attributes_keys": NODE_KEYS}}
+    eng = Engine(cfg)
+    pin = PinnedBuffer(pb)
+    st = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE
+    sh = torch.cuda.current_stream().cuda_stream
+
+    def one(pinned: bool, stages: bool):
+        a = time.perf_counter()
+        ob = OtlpBatch(eng, pin.p, stream=sh, length=pin.n) if pinned else OtlpBatch(eng, pb, stream=sh)
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        if stages:
+            eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
+            torch.cuda.synchronize()
+        c = time.perf_counter()
+        info = (ob.cols.n_spans, ob.host_spans, int(ob.out_numpy("device_status", n=1)[0]) if stages else 0)
+        ob.close()
+        return b - a, c - b, info
+
+    for _ in range(2):
+        one(True, True)
+    res = {"metric": "OTLP protobuf ingest: host TracesData bytes -> decoded columns -> SAMPLE|TEMPLATE|SIZE",
+           "spans": args.spans, "message_bytes": len(pb), "bytes_per_span": len(pb) / args.spans,
+           "host_cpu": model, "cpu_share": share, "nproc": nproc}
+    eng.profile(True)
+    dec, stg = [], []
+    for _ in range(args.reps):
+        d, s, info = one(True, True)
+        dec.append(d)
+        stg.append(s)
+        assert info[2] == 0, "device status"
+    prof = eng.profile_read()
+    eng.profile(False)
+    n_dec = prof.get("otlp_span_kernel", {"ms": 0.0, "launches": 1})
+    k_ms = n_dec["ms"] / max(n_dec["launches"], 1)
+    stage_ms = sum(v["ms"] for k, v in prof.items() if k != "otlp_span_kernel") / args.reps
+    dp = min(dec)
+    res["decode_pinned_ms"] = dp * 1e3
+    res["stages_ms"] = min(stg) * 1e3
+    res["stages_kernel_ms"] = stage_ms
+    res["end_to_end_spans_per_s"] = args.spans / (dp + min(stg))
+    res["decode_spans_per_s"] = args.spans / dp
+    res["host_pass_spans"] = info[1]
+    res["span_kernel_ms"] = k_ms
+    # decoder roofline: the message bytes it reads + 60 B/span of columns (and flags) written
+    alg = len(pb) + 8 * args.spans + 60 * args.spans
+    res["span_kernel_roofline"] = {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9 if k_ms else 0.0,
+                                   "peak": 8000.0, "unit": "GB/s", "algorithmic_bytes": alg}
+    res["span_kernel_roofline"]["frac"] = res["span_kernel_roofline"]["achieved"] / 8000.0
+    d, _, _ = one(False, False)
+    res["decode_pageable_ms"] = d * 1e3
+    # per-call latency at the batch processor's 8192 spans
+    smallpb = Generator("fused", seed=0x0D16F0A2, n_spans=8192, threads=threads).otlp(threads)
+    spin = PinnedBuffer(smallpb)
+    lat = []
+    for k in range(220):
+        a = time.perf_counter()
+        ob = OtlpBatch(eng, spin.p, stream=sh, length=spin.n)
+        eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
+        torch.cuda.synchronize()
+        ob.close()
+        if k >= 20:
+            lat.append(time.perf_counter() - a)
+    lat.sort()
+    res["batch8192_decode_and_stages_us"] = {"p50": lat[len(lat) // 2] * 1e6, "p99": lat[int(len(lat) * 0.99)] * 1e6}
+    res["batch8192_spans_per_s"] = 8192 / lat[len(lat) // 2]
+    spin.close()
+    pin.close()
+    line = json.dumps(res)
+    Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+    Path(args.out).write_text(line + "\n")
+    print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
