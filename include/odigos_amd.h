@@ -418,6 +418,9 @@ void ose_host_free(void* p);
 int ose_otlp_decode(ose_engine* eng, const void* pb, size_t len, void* hip_stream, ose_otlp_batch** out);
 const ose_columns* ose_otlp_columns(const ose_otlp_batch* b);   /* device pointers */
 uint32_t ose_otlp_host_spans(const ose_otlp_batch* b);
+/* host wall time of the call's phases (ms): bytes in (copy / H2D issue),
+ * structural walk, columns upload, span decoder (+ sync), host pass */
+int ose_otlp_timings(const ose_otlp_batch* b, double* ms5);
 int ose_otlp_attrset(const ose_otlp_batch* b, uint32_t k, char* json, size_t cap);
 /* copies every column whose dst pointer is non-NULL (host or device memory) */
 int ose_otlp_download(const ose_otlp_batch* b, const ose_columns* dst);

@@ -92,8 +92,8 @@ class Generator:
         """The batch as a serialized OTLP TracesData (gen_otlp.cpp)."""
         n = C.c_uint64()
         p = Generator._L.osegen_otlp(C.byref(self.cols), threads, C.byref(n))
-        try:
-            return C.string_at(p, n.value)
+        try:   # (string_at takes an int size: messages above 2 GiB need the array view)
+            return C.cast(p, C.POINTER(C.c_char * n.value)).contents.raw
         finally:
             Generator._L.osegen_otlp_free(p)
 
@@ -268,8 +268,10 @@ class OtlpBatch:
     columns owned by the engine plus HBM outputs, usable wherever a
     DeviceBatch is (Engine.process_device)."""
 
-    def __init__(self, engine: "Engine", pb, stream=None, tmpl_cap: int | None = None, length: int | None = None):
-        """pb: the message bytes, or the address of a buffer (e.g. PinnedBuffer) with `length`."""
+    def __init__(self, engine: "Engine", pb, stream=None, tmpl_cap: int | None = None, length: int | None = None,
+                 outputs=None):
+        """pb: the message bytes, or the address of a buffer (e.g. PinnedBuffer) with `length`;
+        outputs: an (outs, tensors) pair from device_outputs to reuse."""
         self.L = engine.L
         self.eng = engine   # the engine must outlive its batches (ose_otlp_release before ose_engine_destroy)
         h = C.c_void_p()
@@ -283,7 +285,10 @@ class OtlpBatch:
         self.h = h
         self.cols = native.Columns.from_buffer_copy(self.L.ose_otlp_columns(h).contents)
         self.host_spans = int(self.L.ose_otlp_host_spans(h))
-        self.outs, self.o = device_outputs(self.cols, tmpl_cap=tmpl_cap)
+        t = (C.c_double * 5)()
+        native.check(self.L.ose_otlp_timings(h, t))
+        self.timings_ms = dict(zip(("bytes_in", "walk", "columns", "span_kernel", "host_pass"), list(t)))
+        self.outs, self.o = outputs if outputs is not None else device_outputs(self.cols, tmpl_cap=tmpl_cap)
 
     def attrset(self, k: int) -> dict:
         import json

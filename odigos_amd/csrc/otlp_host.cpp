@@ -11,6 +11,7 @@
 //   4. the spans it lists get the host pass: pb_span + columnize_span, their
 //      strings appended after the message bytes, written by otlp_fix_kernel.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <string_view>
@@ -74,6 +75,7 @@ struct OtlpBatchImpl {
   DevBuf arena, slab, stage, fixdev;   // device arena; device columns; pinned staging; host-pass records
   std::vector<std::vector<std::pair<std::string, std::string>>> attrsets;
   uint32_t host_spans = 0;
+  double t_ms[5] = {0, 0, 0, 0, 0};   // copy-in, walk, columns upload, span kernel (+ sync), host pass
   OtlpBatchImpl() { stage.host = true; }
 };
 
@@ -180,15 +182,41 @@ struct CachedRes {
 uint64_t sov64(uint64_t x) { uint64_t n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
 uint64_t flen(uint64_t l) { return 1 + sov64(l) + l; }
 
-void walk_chunk(const ColumnizeCtx& ctx, const uint8_t* p, const std::vector<std::pair<size_t, size_t>>& rsl,
-                size_t r0, size_t r1, WalkChunk& c) {
+// The TracesData records that start in [s, lim) (a record may run past lim:
+// *end is where the last one ends), each ResourceSpans walked in full.
+void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s, size_t lim, WalkChunk& c,
+                  size_t* end) {
   std::unordered_map<std::string_view, CachedRes> rcache;
   std::unordered_map<std::string_view, uint32_t> scache;
   std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
   ProtoSizer sizer;
-  std::vector<std::pair<size_t, size_t>> resf, scopes, deprecated;
-  for (size_t r = r0; r < r1; r++) {
-    const size_t ro = rsl[r].first, rl = rsl[r].second;
+  std::vector<std::pair<size_t, size_t>> resf, scopes, deprecated, scf;
+  const size_t est = (std::min(lim, n) - std::min(s, n)) / 128 + 16;   // spans of >= 128 bytes
+  c.span_ref.reserve(est);
+  c.span_res.reserve(est);
+  c.span_scope.reserve(est);
+  PbReader top(p, n);
+  top.i = s;
+  *end = s;
+  // The walk is a chain of lengths: each header's address depends on the
+  // last length, so without help every span costs a DRAM round trip.  The
+  // segment is prefetched line by line a few KB ahead of the walk instead.
+  size_t pf = s & ~size_t(63);
+  auto ahead = [&](size_t pos) {
+    const size_t want = std::min(n, pos + 8192);
+    for (; pf < want; pf += 64) __builtin_prefetch(p + pf, 0, 3);
+  };
+  uint32_t tf, twt;
+  while (top.i < lim && top.more() && top.tag(tf, twt)) {
+    ahead(top.i);
+    size_t ro, rl;
+    if (tf != 1) {
+      if (!top.skip(twt, tf)) break;
+      *end = top.i;
+      continue;
+    }
+    if (twt != 2 || !top.bytes(ro, rl)) { top.fail(); break; }
+    *end = top.i;
     PbReader rr(p + ro, rl);
     resf.clear();
     scopes.clear();
@@ -245,7 +273,7 @@ void walk_chunk(const ColumnizeCtx& ctx, const uint8_t* p, const std::vector<std
       const uint32_t sloc = (uint32_t)c.scope_size.size();
       PbReader sr(p + so.first, so.second);
       size_t sschema = 0;
-      std::vector<std::pair<size_t, size_t>> scf;
+      scf.clear();
       while (sr.more() && sr.tag(f, wt)) {
         size_t o, l;
         if (f == 1 || f == 2 || f == 3) {
@@ -256,6 +284,7 @@ void walk_chunk(const ColumnizeCtx& ctx, const uint8_t* p, const std::vector<std
             sschema = l;
           } else {
             const uint64_t off = so.first + o;
+            ahead(off + l);
             if (off > 0xFFFFFFFFull || l > 0xFFFFFFFFull) { c.err = "span beyond the 4 GiB arena range"; return; }
             c.span_ref.push_back(off | ((uint64_t)l << 32));
             c.span_res.push_back(rloc);
@@ -283,34 +312,72 @@ void walk_chunk(const ColumnizeCtx& ctx, const uint8_t* p, const std::vector<std
       c.scope_res.push_back(rloc);
     }
   }
+  if (!top.ok) c.err = "OTLP protobuf: malformed TracesData";
 }
 
-bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
-  // top level: the ResourceSpans fields
-  std::vector<std::pair<size_t, size_t>> rsl;
-  PbReader top(p, n);
-  uint32_t f, wt;
-  while (top.more() && top.tag(f, wt)) {
-    size_t o, l;
-    if (f == 1) {
-      if (wt != 2 || !top.bytes(o, l)) { top.fail(); break; }
-      rsl.emplace_back(o, l);
-    } else if (!top.skip(wt, f)) {
-      break;
+// A plausible record start at or after k: a TracesData field 1 (0x0A) whose
+// length varint frames a record followed by 3 more such records (or the end).
+size_t find_start(const uint8_t* p, size_t n, size_t k) {
+  for (size_t q = k; q + 2 < n; q++) {
+    if (p[q] != 0x0A) continue;
+    size_t pos = q;
+    int hops = 0;
+    bool ok = true;
+    while (hops < 4 && pos < n) {
+      PbReader r(p, n);
+      r.i = pos;
+      uint32_t f, wt;
+      size_t o, l;
+      if (!r.tag(f, wt) || f != 1 || wt != 2 || !r.bytes(o, l) || l == 0 || (p[o] != 0x0A && p[o] != 0x12)) {
+        ok = false;
+        break;
+      }
+      pos = r.i;
+      hops++;
     }
+    if (ok) return q;
   }
-  if (!top.ok) { w.err = "OTLP protobuf: malformed TracesData"; return false; }
-  const size_t R = rsl.size();
-  const int T = (int)std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1u, std::thread::hardware_concurrency()), R / 512}));
-  std::vector<WalkChunk> ch((size_t)T);
-  {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; t++) th.emplace_back([&, t]() { walk_chunk(ctx, p, rsl, R * t / T, R * (t + 1) / T, ch[t]); });
-    walk_chunk(ctx, p, rsl, 0, R / T, ch[0]);
-    for (auto& x : th) x.join();
+  return n;
+}
+
+// The walk, split over threads: the records form one chain of lengths, so
+// each thread starts at a speculated record start and walks up to the next
+// thread's; the split is exact iff every thread ends exactly where the next
+// one started (the chain from 0 is unique), else the walk runs again on one
+// thread.
+bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
+  const size_t kSeg = size_t(4) << 20;
+  int T = (int)std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1u, std::thread::hardware_concurrency()), n / kSeg}));
+  if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));   // diagnostics
+  std::vector<WalkChunk> ch;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    if (attempt) T = 1;
+    std::vector<size_t> st((size_t)T + 1, n), en((size_t)T, 0);
+    st[0] = 0;
+    for (int t = 1; t < T; t++) st[t] = find_start(p, n, n * (size_t)t / (size_t)T);
+    for (int t = T - 1; t >= 1; t--) st[t] = std::min(st[t], st[t + 1]);   // monotone
+    ch.assign((size_t)T, WalkChunk());
+    {
+      std::vector<std::thread> th;
+      for (int t = 1; t < T; t++) th.emplace_back([&, t]() { walk_segment(ctx, p, n, st[t], st[t + 1], ch[t], &en[t]); });
+      walk_segment(ctx, p, n, st[0], st[1], ch[0], &en[0]);
+      for (auto& x : th) x.join();
+    }
+    bool exact = true;
+    for (int t = 0; t < T; t++) {
+      if (!ch[t].err.empty()) {
+        if (t == 0 || attempt) { w.err = ch[t].err; return false; }
+        exact = false;   // a speculated start inside a record: redo
+      }
+      if (t + 1 < T && en[t] != st[t + 1]) exact = false;
+    }
+    if (en[T - 1] != n && ch[T - 1].err.empty()) {   // trailing bytes the segment walker did not reach
+      if (attempt || T == 1) { w.err = "OTLP protobuf: malformed TracesData"; return false; }
+      exact = false;
+    }
+    if (exact) break;
+    if (attempt) { w.err = "OTLP protobuf: malformed TracesData"; return false; }
   }
-  for (auto& c : ch)
-    if (!c.err.empty()) { w.err = c.err; return false; }
   // merge: global indices, attribute sets in first-appearance order
   std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
   std::vector<std::vector<uint32_t>> set_map(ch.size());
@@ -381,6 +448,14 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   OtlpEngine* o = otlp_engine(e, rc);
   if (!o) return rc;
   if (len > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: message beyond the 4 GiB arena range");
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now();
+  auto lap = [&](int k) {
+    const auto t = clk::now();
+    b->t_ms[k] = std::chrono::duration<double, std::milli>(t - t0).count();
+    t0 = t;
+  };
+  for (double& x : b->t_ms) x = 0;
   // 1. the bytes H2D (straight from the caller's buffer when it is pinned,
   //    else through pinned staging), the walk meanwhile
   const size_t pb_cap = up(len + 16, 16);
@@ -398,8 +473,10 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     std::memset(b->stage.p + len, 0, pb_cap - len);
     HIP_TRY(hipMemcpyAsync(b->arena.p, b->stage.p, pb_cap, hipMemcpyHostToDevice, st));
   }
+  lap(0);
   Walked w;
   if (!walk(o->ctx, pb, len, w)) return fail(OSE_EINVAL, w.err);
+  lap(1);
   HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
   const uint64_t n = w.span_ref.size(), R = w.res_svc.size(), S = w.scope_size.size();
   if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: more than 2^32-16 spans");
@@ -476,6 +553,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   c.arena_bytes = len;
   c.n_attr_keys = K;
   if (!o->ctx.url_filter) c.res_url_ok = nullptr;
+  lap(2);
   // 3. the GPU decoder
   OtlpArgs a{};
   a.pb = b->arena.p;
@@ -514,6 +592,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   HIP_TRY(hipMemcpyAsync(&cnt, host_count, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   b->host_spans = cnt;
+  lap(3);
   if (!cnt) return 0;
   std::vector<uint32_t> list(cnt);
   HIP_TRY(hipMemcpy(list.data(), host_list, 4 * (size_t)cnt, hipMemcpyDeviceToHost));
@@ -606,6 +685,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   launch_otlp_fix(fa, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));   // fixdev and the staging are reused / freed
+  lap(4);
   return 0;
 }
 }  // namespace
@@ -659,8 +739,16 @@ char* osehost_otlp_walk(const char* cfg_json, const uint8_t* pb, size_t len) {
     ColumnizeCtx ctx;
     if (err.empty()) err = ctx.build(ju ? &url : nullptr, js ? &sampling : nullptr, jt ? &traffic : nullptr);
     Walked w;
+    const auto t0 = std::chrono::steady_clock::now();
     if (err.empty() && !walk(ctx, pb, len, w)) err = w.err;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (!err.empty()) { fail(OSE_EINVAL, err); return nullptr; }
+    if (cfg.get("timing_only")) {   // diagnostics: the walk's wall time only
+      std::string out = "{\"walk_ms\":" + std::to_string(ms) + ",\"spans\":" + std::to_string(w.span_ref.size()) + "}";
+      char* r = static_cast<char*>(std::malloc(out.size() + 1));
+      std::memcpy(r, out.c_str(), out.size() + 1);
+      return r;
+    }
     auto arr = [](const auto& v) {
       Json a = Json::array();
       for (auto x : v) a.push(Json::number(std::to_string((uint64_t)x)));
@@ -716,6 +804,12 @@ int ose_otlp_download(const ose_otlp_batch* bb, const ose_columns* dst) {
 
 const ose_columns* ose_otlp_columns(const ose_otlp_batch* bb) {
   return bb ? &reinterpret_cast<const OtlpBatchImpl*>(bb)->cols : nullptr;
+}
+
+int ose_otlp_timings(const ose_otlp_batch* bb, double* ms5) {
+  if (!bb || !ms5) return fail(OSE_EINVAL, "NULL argument");
+  std::memcpy(ms5, reinterpret_cast<const OtlpBatchImpl*>(bb)->t_ms, sizeof(double) * 5);
+  return 0;
 }
 
 uint32_t ose_otlp_host_spans(const ose_otlp_batch* bb) {

@@ -124,6 +124,7 @@ def lib() -> C.CDLL:
         "ose_host_free": (None, [_p]),
         "ose_otlp_columns": (C.POINTER(Columns), [_p]),
         "ose_otlp_host_spans": (C.c_uint32, [_p]),
+        "ose_otlp_timings": (C.c_int, [_p, C.POINTER(C.c_double)]),
         "ose_otlp_attrset": (C.c_int, [_p, C.c_uint32, C.c_char_p, C.c_size_t]),
         "ose_otlp_download": (C.c_int, [_p, C.POINTER(Columns)]),
         "ose_otlp_release": (None, [_p]),
