@@ -426,6 +426,42 @@ int ose_otlp_attrset(const ose_otlp_batch* b, uint32_t k, char* json, size_t cap
 int ose_otlp_download(const ose_otlp_batch* b, const ose_columns* dst);
 void ose_otlp_release(ose_otlp_batch* b);
 
+/* ---- output side: routing + OTLP re-encode ------------
+ * ose_router replaces odigosrouterconnector's routing table
+ * (collector/connectors/odigosrouterconnector/routingmap.go:34-57
+ * BuildSignalRoutingMap, for the TRACES signal).  cfg_json is the
+ * connector's Config: {"datastreams": [{"name": ..., "sources":
+ * [{"namespace", "kind", "name"}], "destinations": [{"destinationname",
+ * "configuredsignals": ["TRACES", ...]}]}]}.  Pipelines are the data
+ * streams carrying TRACES, in order of first appearance.                    */
+typedef struct ose_router ose_router;
+int ose_router_create(const char* cfg_json, ose_router** out);
+void ose_router_destroy(ose_router* r);
+uint32_t ose_router_pipelines(const ose_router* r);
+const char* ose_router_pipeline(const ose_router* r, uint32_t k);   /* owned by r */
+
+/* Replaces the end of the gateway's traces/in pipeline: the processed
+ * ptrace.Traces leaving the three processors, odigosrouterconnector's
+ * ConsumeTraces (connector.go:174-237: each ResourceSpans copied to every
+ * pipeline its k8s workload routes to, unmatched ones to "default") and the
+ * exporters' ptrace.ProtoMarshaler.MarshalTraces.  `outs` are the outputs
+ * ose_process_device wrote for this batch with `stages` / `group_mode`
+ * (device or host memory; read on hip_stream): keep (or trace_keep[0] with
+ * OSE_GROUP_BATCH) removes spans, emptied scopes and resources, url_out /
+ * tmpl rename and template the kept spans.  With a router the outputs are
+ * its pipelines then "default" (ose_router_pipelines + 1 of them); without,
+ * one output.  Each output is a serialized TracesData, byte for byte what
+ * pdata's marshaler writes for the processed traces; n_resources == 0 means
+ * the connector would not call that pipeline.  The message bytes given to
+ * ose_otlp_decode must be unchanged until this call returns.              */
+typedef struct ose_otlp_out ose_otlp_out;
+int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* b, const ose_outputs* outs, uint32_t stages,
+                    uint32_t group_mode, const ose_router* router, void* hip_stream, ose_otlp_out** out);
+uint32_t ose_otlp_out_count(const ose_otlp_out* o);
+int ose_otlp_out_get(const ose_otlp_out* o, uint32_t k, const char** name, const uint8_t** data, uint64_t* len,
+                     uint32_t* n_resources);   /* pointers valid until release */
+void ose_otlp_out_release(ose_otlp_out* o);
+
 /* Message of the last failure on this thread ("" if none). */
 const char* ose_last_error(void);
 

@@ -263,6 +263,54 @@ class PinnedBatch:
     __del__ = close
 
 
+def take_otlp_out(L, h, copy: bool = True) -> list:
+    """The outputs of an ose_otlp_out (then released); copy=False gives the
+    byte counts instead of the bytes."""
+    try:
+        res = []
+        for k in range(L.ose_otlp_out_count(h)):
+            name, data, n, nres = C.c_char_p(), C.c_void_p(), C.c_uint64(), C.c_uint32()
+            native.check(L.ose_otlp_out_get(h, k, C.byref(name), C.byref(data), C.byref(n), C.byref(nres)))
+            if copy:
+                raw = (C.c_char * n.value).from_address(data.value).raw if n.value else b""
+            else:
+                raw = n.value
+            res.append((name.value.decode("utf-8", "surrogateescape"), raw, nres.value))
+        return res
+    finally:
+        L.ose_otlp_out_release(h)
+
+
+class Router:
+    """odigosrouterconnector's routing table (ose_router_create); `signal`
+    other than TRACES builds it through the test seam (routing KATs)."""
+
+    def __init__(self, cfg, signal: str | None = None):
+        import json
+        self.L = native.lib()
+        text = cfg if isinstance(cfg, str) else json.dumps(cfg)
+        h = C.c_void_p()
+        if signal is None:
+            native.check(self.L.ose_router_create(text.encode(), C.byref(h)))
+        else:
+            native.check(self.L.osehost_router_create_signal(text.encode(), signal.encode(), C.byref(h)))
+        self.h = h
+        self.pipelines = [self.L.ose_router_pipeline(h, k).decode() for k in range(self.L.ose_router_pipelines(h))]
+
+    def route(self, attrs: dict) -> tuple:
+        """determineRoutingPipelines on {"key": value}: (pipelines, key)."""
+        import json
+        out = json.loads(native.take_bytes(self.L.osehost_router_route(self.h, json.dumps(attrs).encode())))
+        return out["pipelines"], out["key"]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ose_router_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+
 class OtlpBatch:
     """A serialized TracesData decoded on the GPU (ose_otlp_decode): device
     columns owned by the engine plus HBM outputs, usable wherever a
@@ -277,7 +325,8 @@ class OtlpBatch:
         h = C.c_void_p()
         s = None if stream is None else C.c_void_p(stream)
         if isinstance(pb, (bytes, bytearray)):
-            buf = C.c_char_p(bytes(pb)) if isinstance(pb, bytearray) else C.c_char_p(pb)
+            self._msg = bytes(pb) if isinstance(pb, bytearray) else pb   # read again by encode()
+            buf = C.c_char_p(self._msg)
             addr, n = C.cast(buf, C.c_void_p), len(pb)
         else:
             addr, n = C.c_void_p(int(pb)), int(length)
@@ -321,6 +370,17 @@ class OtlpBatch:
 
     def used(self) -> int:
         return int(self.o["used"][0].item())
+
+    def encode(self, stages: int, group_mode: int = native.GROUP_TRACE_ID, router: "Router | None" = None,
+               stream=None, copy: bool = True) -> list:
+        """ose_otlp_encode after Engine.process_device(self, stages, group_mode):
+        [(pipeline, TracesData bytes, n_resources)] — the router's pipelines
+        then "default", or one ("", bytes, n) without a router."""
+        h = C.c_void_p()
+        s = None if stream is None else C.c_void_p(stream)
+        native.check(self.L.ose_otlp_encode(self.eng.h, self.h, C.byref(self.outs), stages, group_mode,
+                                            router.h if router is not None else None, s, C.byref(h)))
+        return take_otlp_out(self.L, h, copy)
 
     def close(self):
         if getattr(self, "h", None):

@@ -2,9 +2,10 @@
 // tests (bench/test infrastructure, part of libosegen): the resources,
 // spans, times, statuses, kinds, paths and routes of a generated batch
 // (gen_batch.cpp), written as OTLP trace.proto messages with the attributes
-// an HTTP instrumentation sets.  Encoding is canonical proto3 (defaults
-// omitted); resources are encoded in parallel chunks (TracesData is a
-// concatenation of ResourceSpans fields).
+// an HTTP instrumentation sets, encoded as pdata's marshaler writes them
+// (what a node collector's OTLP exporter sends the gateway: proto3 defaults
+// omitted, ids and Status always framed); resources are encoded in parallel
+// chunks (TracesData is a concatenation of ResourceSpans fields).
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -72,6 +73,7 @@ void encode_resources(const ose_columns* c, const std::vector<Res>& res, size_t 
       std::snprintf(name, sizeof name, "svc-%02u", svc);
       kv_str(resm, 1, "service.name", name, std::strlen(name));
       kv_str(resm, 1, "k8s.namespace.name", "default", 7);
+      kv_str(resm, 1, "k8s.deployment.name", name, std::strlen(name));   // what k8sattributes adds
       char pod[32];
       std::snprintf(pod, sizeof pod, "pod-%u", c->res_attrset[r] % 4);
       kv_str(resm, 1, "k8s.pod.name", pod, std::strlen(pod));
@@ -98,6 +100,8 @@ void encode_resources(const ose_columns* c, const std::vector<Res>& res, size_t 
         const uint64_t h2 = mix(h);
         std::memcpy(id, &h2, 8);
         put_bytes(sp, 4, id, 8);
+      } else {
+        put_bytes(sp, 4, id, 0);   // pdata frames an empty parent id
       }
       const uint8_t f = c->url_flags[i];
       const char* method = kMethod[h >> 62];
@@ -128,10 +132,12 @@ void encode_resources(const ose_columns* c, const std::vector<Res>& res, size_t 
         kv_str(sp, 9, "network.protocol.version", "1.1", 3);
         kv_str(sp, 9, "user_agent.original", kUa, sizeof kUa - 1);
       }
-      if (c->status[i]) {
+      {   // Status: non-nullable, always framed
         std::string st;
-        put_tag(st, 3, 0);
-        put_varint(st, c->status[i]);
+        if (c->status[i]) {
+          put_tag(st, 3, 0);
+          put_varint(st, c->status[i]);
+        }
         put_msg(sp, 15, st);
       }
       put_msg(sc, 2, sp);

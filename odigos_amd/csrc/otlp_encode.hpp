@@ -1,0 +1,74 @@
+// otlp_encode.hpp — SoA decisions → OTLP TracesData bytes, and the
+// odigosrouterconnector routing table.
+#pragma once
+#include <cstdint>
+#include <cstdlib>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/odigos_amd.h"
+#include "json.hpp"
+#include "pdata.hpp"
+
+namespace ose {
+
+// Where the structural walk found each message of one TracesData (offsets
+// into the message bytes; a ref is offset | length << 32).
+struct OtlpLayout {
+  static constexpr uint64_t kMulti = ~0ull;   // scope_hdr: several scope fields (merged)
+  std::vector<uint64_t> res_ref;       // ResourceSpans payload
+  std::vector<uint32_t> res_scope0;    // first scope of each resource
+  std::vector<uint64_t> scope_ref;     // ScopeSpans payload
+  std::vector<uint64_t> scope_hdr;     // its InstrumentationScope message (0: none)
+  std::vector<uint64_t> scope_schema;  // its schema_url (last occurrence; length 0: none)
+  std::vector<uint32_t> scope_span0;   // first span of each scope
+};
+
+// odigosrouterconnector: BuildSignalRoutingMap (routingmap.go:34-57) for one
+// signal, and determineRoutingPipelines (connector.go:147-172).
+struct Router {
+  std::string signal;
+  std::vector<std::string> pipelines;                                  // output order: first appearance
+  std::unordered_map<std::string, std::vector<uint32_t>> routes;       // "ns/kind/name" → pipelines
+  // NULL when the resource routes to the default pipeline; *key gets the
+  // routing key when one matched
+  const std::vector<uint32_t>* route(const AttrMap& attrs, std::string* key = nullptr) const;
+};
+// {"datastreams": [{"name", "sources": [{"namespace", "kind", "name"}],
+//   "destinations": [{"destinationname", "configuredsignals": [...]}]}]}
+std::string build_router(const Json& cfg, const std::string& signal, Router& r);
+std::string normalize_kind(const std::string& kind);
+
+// The per-span decisions the encoder applies (host memory).
+struct EncodeDecisions {
+  const uint8_t* keep = nullptr;        // NULL: every span kept
+  bool drop_all = false;                // OSE_GROUP_BATCH, the call's trace unsampled
+  const uint8_t* url_out = nullptr;     // NULL: no template stage
+  const ose_strref* tmpl = nullptr;
+  const uint8_t* tmpl_arena = nullptr;
+  uint64_t tmpl_arena_len = 0;
+  const uint32_t* span_size = nullptr;  // pdata's size of each span (NULL: trust the input's encoding)
+};
+
+struct EncodedOutput {
+  std::string name;
+  uint8_t* data = nullptr;   // malloc'd
+  uint64_t len = 0;
+  uint32_t n_resources = 0;
+};
+
+struct OtlpOut {   // ose_otlp_out
+  std::vector<EncodedOutput> outs;
+  ~OtlpOut() {
+    for (auto& o : outs) std::free(o.data);
+  }
+};
+
+// One TracesData per output (router pipelines, then the default one; one
+// output without a router).  false + err on a malformed message.
+bool encode_traces(const uint8_t* pb, size_t len, const std::vector<uint64_t>& span_ref, const OtlpLayout& lay,
+                   const EncodeDecisions& d, const Router* router, int threads, std::vector<EncodedOutput>& outs,
+                   std::string& err);
+
+}  // namespace ose

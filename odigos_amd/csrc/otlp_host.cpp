@@ -21,6 +21,7 @@
 #include "columnize.hpp"
 #include "engine_internal.hpp"
 #include "kernels.hpp"
+#include "otlp_encode.hpp"
 #include "otlp_pb.hpp"
 
 namespace ose {
@@ -76,6 +77,11 @@ struct OtlpBatchImpl {
   std::vector<std::vector<std::pair<std::string, std::string>>> attrsets;
   uint32_t host_spans = 0;
   double t_ms[5] = {0, 0, 0, 0, 0};   // copy-in, walk, columns upload, span kernel (+ sync), host pass
+  // for ose_otlp_encode: the caller's message and where its parts are
+  const uint8_t* pb = nullptr;
+  size_t pb_len = 0;
+  std::vector<uint64_t> span_ref;
+  OtlpLayout lay;
   OtlpBatchImpl() { stage.host = true; }
 };
 
@@ -163,6 +169,7 @@ struct Walked {
   std::vector<uint8_t> res_ok;
   std::vector<uint64_t> attr_res;
   std::vector<std::vector<std::pair<std::string, std::string>>> sets;
+  OtlpLayout lay;   // what the re-encoder needs (otlp_encode.cpp)
   std::string err;
 };
 struct WalkChunk {
@@ -171,6 +178,7 @@ struct WalkChunk {
   std::vector<uint32_t> res_svc, res_svc_str, res_set, res_size, scope_size, scope_res;
   std::vector<uint8_t> res_ok;
   std::vector<uint64_t> attr_res;
+  OtlpLayout lay;   // res_scope0 / scope_span0 chunk-local
   std::vector<std::vector<std::pair<std::string, std::string>>> sets;   // chunk-local first appearance
   std::string err;
 };
@@ -263,6 +271,8 @@ void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s,
       if (resf.size() <= 1) rcache.emplace(key, cr);
     }
     const uint32_t rloc = (uint32_t)c.res_svc.size();
+    c.lay.res_ref.push_back(ro | ((uint64_t)rl << 32));
+    c.lay.res_scope0.push_back((uint32_t)c.scope_size.size());
     c.res_svc.push_back(cr.svc);
     c.res_svc_str.push_back(cr.svc_str);
     c.res_ok.push_back(cr.ok);
@@ -272,8 +282,10 @@ void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s,
     for (auto& so : scopes) {
       const uint32_t sloc = (uint32_t)c.scope_size.size();
       PbReader sr(p + so.first, so.second);
-      size_t sschema = 0;
+      size_t sschema = 0, sschema_off = 0;
       scf.clear();
+      c.lay.scope_ref.push_back(so.first | ((uint64_t)so.second << 32));
+      c.lay.scope_span0.push_back((uint32_t)c.span_ref.size());
       while (sr.more() && sr.tag(f, wt)) {
         size_t o, l;
         if (f == 1 || f == 2 || f == 3) {
@@ -282,6 +294,7 @@ void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s,
             scf.emplace_back(so.first + o, l);
           } else if (f == 3) {
             sschema = l;
+            sschema_off = so.first + o;
           } else {
             const uint64_t off = so.first + o;
             ahead(off + l);
@@ -310,6 +323,10 @@ void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s,
       }
       c.scope_size.push_back(spart + (uint32_t)(sschema ? flen(sschema) : 0));
       c.scope_res.push_back(rloc);
+      c.lay.scope_hdr.push_back(scf.empty() ? 0
+                                : scf.size() == 1 ? (scf[0].first | ((uint64_t)scf[0].second << 32))
+                                                  : OtlpLayout::kMulti);
+      c.lay.scope_schema.push_back(sschema_off | ((uint64_t)sschema << 32));
     }
   }
   if (!top.ok) c.err = "OTLP protobuf: malformed TracesData";
@@ -406,6 +423,12 @@ bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
   w.attr_res.resize(nres);
   w.scope_size.resize(nscope);
   w.scope_res.resize(nscope);
+  w.lay.res_ref.resize(nres);
+  w.lay.res_scope0.resize(nres);
+  w.lay.scope_ref.resize(nscope);
+  w.lay.scope_hdr.resize(nscope);
+  w.lay.scope_schema.resize(nscope);
+  w.lay.scope_span0.resize(nscope);
   std::vector<size_t> so(ch.size()), ro(ch.size()), co(ch.size());
   for (size_t t = 1; t < ch.size(); t++) {
     so[t] = so[t - 1] + ch[t - 1].span_ref.size();
@@ -426,10 +449,16 @@ bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
       w.res_size[ro[t] + k] = c.res_size[k];
       w.res_ok[ro[t] + k] = c.res_ok[k];
       w.attr_res[ro[t] + k] = c.attr_res[k];
+      w.lay.res_ref[ro[t] + k] = c.lay.res_ref[k];
+      w.lay.res_scope0[ro[t] + k] = (uint32_t)(co[t] + c.lay.res_scope0[k]);
     }
     for (size_t k = 0; k < c.scope_size.size(); k++) {
       w.scope_size[co[t] + k] = c.scope_size[k];
       w.scope_res[co[t] + k] = (uint32_t)(ro[t] + c.scope_res[k]);
+      w.lay.scope_ref[co[t] + k] = c.lay.scope_ref[k];
+      w.lay.scope_hdr[co[t] + k] = c.lay.scope_hdr[k];
+      w.lay.scope_schema[co[t] + k] = c.lay.scope_schema[k];
+      w.lay.scope_span0[co[t] + k] = (uint32_t)(so[t] + c.lay.scope_span0[k]);
     }
   };
   {
@@ -478,7 +507,11 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   if (!walk(o->ctx, pb, len, w)) return fail(OSE_EINVAL, w.err);
   lap(1);
   HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
-  const uint64_t n = w.span_ref.size(), R = w.res_svc.size(), S = w.scope_size.size();
+  b->pb = pb;
+  b->pb_len = len;
+  b->span_ref = std::move(w.span_ref);
+  b->lay = std::move(w.lay);
+  const uint64_t n = b->span_ref.size(), R = w.res_svc.size(), S = w.scope_size.size();
   if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: more than 2^32-16 spans");
   const uint32_t K = o->n_attr_keys;
   b->attrsets = std::move(w.sets);
@@ -501,7 +534,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   uint32_t* host_list = nullptr;
   uint64_t* span_ref = nullptr;
   std::vector<Part> parts = {
-      {(void**)&span_ref, 8 * N, w.span_ref.data()},
+      {(void**)&span_ref, 8 * N, b->span_ref.data()},
       {(void**)&c.resource, 4 * N, w.span_res.data()},
       {(void**)&c.scope, 4 * N, w.span_scope.data()},
       {(void**)&c.res_svc, 4 * R, res_svc.data()},
@@ -609,7 +642,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   SpanCols sc;
   for (uint32_t q = 0; q < cnt; q++) {
     const uint32_t i = list[q];
-    const uint64_t ref = w.span_ref[i];   // (Walked keeps the walk's arrays)
+    const uint64_t ref = b->span_ref[i];
     Span sp;
     if (!pb_span(pb + (uint32_t)ref, (size_t)(ref >> 32), sp)) return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
     columnize_span(o->ctx, sp, attr_res[w.span_res[i]], sizer, sc);
@@ -826,6 +859,119 @@ int ose_otlp_attrset(const ose_otlp_batch* bb, uint32_t k, char* json, size_t ca
   dump_json(s, o);
   if (s.size() + 1 > cap) return fail(OSE_ERANGE, "buffer too small");
   std::memcpy(json, s.c_str(), s.size() + 1);
+  return 0;
+}
+
+namespace {
+int encode_threads() {
+  return (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+}
+}  // namespace
+
+int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs* outs, uint32_t stages,
+                    uint32_t group_mode, const ose_router* router, void* hip_stream, ose_otlp_out** out) {
+  if (!eng || !bb || !out) return fail(OSE_EINVAL, "NULL argument");
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  auto* b = const_cast<OtlpBatchImpl*>(reinterpret_cast<const OtlpBatchImpl*>(bb));
+  if (b->e != e) return fail(OSE_EINVAL, "the batch belongs to another engine");
+  if (int rc = bind_device(e)) return rc;
+  const bool batch_mode = (stages & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_BATCH;
+  const bool sampled = (stages & (OSE_STAGE_SAMPLE | OSE_STAGE_APPLY_KEEP)) && !batch_mode;
+  const bool tmpl = stages & OSE_STAGE_TEMPLATE;
+  if ((sampled || batch_mode || tmpl) && !outs) return fail(OSE_EINVAL, "NULL outputs");
+  if (sampled && !outs->keep) return fail(OSE_EINVAL, "keep is NULL");
+  if (batch_mode && !outs->trace_keep) return fail(OSE_EINVAL, "trace_keep is NULL");
+  if (tmpl && (!outs->url_out || !outs->tmpl || !outs->tmpl_arena || !outs->tmpl_arena_used))
+    return fail(OSE_EINVAL, "template outputs are NULL");
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  const uint64_t n = b->cols.n_spans;
+  // the decisions and the decoder's span sizes, D2H into the batch's pinned staging
+  const size_t o_keep = 0, o_url = up(n + 16), o_tmpl = o_url + up(n + 16), o_size = o_tmpl + up(8 * n + 16),
+               o_misc = o_size + up(4 * n + 16), o_arena = o_misc + 256;
+  int rc;
+  if ((rc = b->stage.need(o_arena))) return rc;
+  uint8_t* h = b->stage.p;
+  if (n) HIP_TRY(hipMemcpyAsync(h + o_size, b->cols.span_size, 4 * n, hipMemcpyDeviceToHost, st));
+  if (sampled && n) HIP_TRY(hipMemcpyAsync(h + o_keep, outs->keep, n, hipMemcpyDefault, st));
+  if (batch_mode) HIP_TRY(hipMemcpyAsync(h + o_misc + 8, outs->trace_keep, 1, hipMemcpyDefault, st));
+  if (tmpl) {
+    if (n) HIP_TRY(hipMemcpyAsync(h + o_url, outs->url_out, n, hipMemcpyDefault, st));
+    if (n) HIP_TRY(hipMemcpyAsync(h + o_tmpl, outs->tmpl, 8 * n, hipMemcpyDefault, st));
+    HIP_TRY(hipMemcpyAsync(h + o_misc, outs->tmpl_arena_used, 8, hipMemcpyDefault, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  uint64_t used = 0;
+  if (tmpl) {
+    std::memcpy(&used, h + o_misc, 8);
+    if (used > outs->tmpl_arena_cap) return fail(OSE_ERANGE, "tmpl_arena_used beyond tmpl_arena_cap");
+    if (used) {
+      if ((rc = b->stage.need(o_arena + used))) return rc;   // grow-only: earlier contents are lost
+      h = b->stage.p;
+      if (n) HIP_TRY(hipMemcpyAsync(h + o_size, b->cols.span_size, 4 * n, hipMemcpyDeviceToHost, st));
+      if (sampled && n) HIP_TRY(hipMemcpyAsync(h + o_keep, outs->keep, n, hipMemcpyDefault, st));
+      if (n) HIP_TRY(hipMemcpyAsync(h + o_url, outs->url_out, n, hipMemcpyDefault, st));
+      if (n) HIP_TRY(hipMemcpyAsync(h + o_tmpl, outs->tmpl, 8 * n, hipMemcpyDefault, st));
+      if (batch_mode) HIP_TRY(hipMemcpyAsync(h + o_misc + 8, outs->trace_keep, 1, hipMemcpyDefault, st));
+      HIP_TRY(hipMemcpyAsync(h + o_arena, outs->tmpl_arena, used, hipMemcpyDefault, st));
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+  }
+  EncodeDecisions d;
+  d.keep = sampled ? h + o_keep : nullptr;
+  d.drop_all = batch_mode && !h[o_misc + 8];
+  if (tmpl) {
+    d.url_out = h + o_url;
+    d.tmpl = reinterpret_cast<const ose_strref*>(h + o_tmpl);
+    d.tmpl_arena = h + o_arena;
+    d.tmpl_arena_len = used;
+  }
+  d.span_size = reinterpret_cast<const uint32_t*>(h + o_size);
+  auto* o = new OtlpOut();
+  std::string err;
+  if (!encode_traces(b->pb, b->pb_len, b->span_ref, b->lay, d, reinterpret_cast<const Router*>(router),
+                     encode_threads(), o->outs, err)) {
+    delete o;
+    return fail(OSE_EINVAL, err);
+  }
+  *out = reinterpret_cast<ose_otlp_out*>(o);
+  return 0;
+}
+
+// Test seam (CPU): the encoder on the host walk of `pb` with the given
+// decisions (keep / url_out / tmpl NULL when absent) and span sizes
+// computed on the host as the decoder would.
+int osehost_otlp_encode(const uint8_t* pb, size_t len, const uint8_t* keep, int drop_all, const uint8_t* url_out,
+                        const ose_strref* tmpl, const uint8_t* tmpl_arena, uint64_t tmpl_arena_len,
+                        const ose_router* router, int threads, ose_otlp_out** out) {
+  if ((!pb && len) || !out) return fail(OSE_EINVAL, "NULL argument");
+  ColumnizeCtx ctx;
+  std::string err = ctx.build(nullptr, nullptr, nullptr);
+  Walked w;
+  if (err.empty() && !walk(ctx, pb, len, w)) err = w.err;
+  if (!err.empty()) return fail(OSE_EINVAL, err);
+  std::vector<uint32_t> sizes(w.span_ref.size());
+  ProtoSizer sizer;
+  for (size_t i = 0; i < sizes.size(); i++) {
+    Span sp;
+    if (!pb_span(pb + (uint32_t)w.span_ref[i], (size_t)(w.span_ref[i] >> 32), sp))
+      return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
+    sizes[i] = (uint32_t)sizer.span(sp);
+  }
+  EncodeDecisions d;
+  d.keep = keep;
+  d.drop_all = drop_all != 0;
+  d.url_out = url_out;
+  d.tmpl = tmpl;
+  d.tmpl_arena = tmpl_arena;
+  d.tmpl_arena_len = tmpl_arena_len;
+  d.span_size = sizes.data();
+  auto* o = new OtlpOut();
+  if (!encode_traces(pb, len, w.span_ref, w.lay, d, reinterpret_cast<const Router*>(router),
+                     threads > 0 ? threads : encode_threads(), o->outs, err)) {
+    delete o;
+    return fail(OSE_EINVAL, err);
+  }
+  *out = reinterpret_cast<ose_otlp_out*>(o);
   return 0;
 }
 

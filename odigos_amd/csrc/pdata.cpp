@@ -484,4 +484,136 @@ uint64_t ProtoSizer::resource_spans(const ResourceSpans& rs) const {
   return n;
 }
 
+
+// ---------------- protobuf encoding (the sizer's fields, written) ----------------
+void ProtoWriter::varint(uint64_t v) {
+  while (v >= 0x80) { o += (char)(v | 0x80); v >>= 7; }
+  o += (char)v;
+}
+void ProtoWriter::tag(uint32_t field, uint32_t wt) { varint(((uint64_t)field << 3) | wt); }
+void ProtoWriter::bytes(uint32_t field, const void* p, size_t n) {
+  tag(field, 2);
+  varint(n);
+  o.append(static_cast<const char*>(p), n);
+}
+void ProtoWriter::str(uint32_t field, const std::string& s) {
+  if (!s.empty()) bytes(field, s.data(), s.size());
+}
+namespace {
+void put_fixed(std::string& o, uint64_t v, int n) {
+  for (int k = 0; k < n; k++) o += (char)(v >> (8 * k));
+}
+template <size_t N>
+void put_id(ProtoWriter& w, uint32_t field, const std::array<uint8_t, N>& id) {
+  const bool empty = std::all_of(id.begin(), id.end(), [](uint8_t b) { return b == 0; });
+  w.bytes(field, id.data(), empty ? 0 : N);   // gogo customtype: framed even when empty
+}
+}  // namespace
+void ProtoWriter::any_value(const Value& v) {
+  const ProtoSizer sz;
+  switch (v.type) {
+    case Value::TEmpty: return;
+    case Value::TStr: bytes(1, v.s.data(), v.s.size()); return;   // oneof: written even when ""
+    case Value::TBool: tag(2, 0); varint(v.b ? 1 : 0); return;
+    case Value::TInt: tag(3, 0); varint((uint64_t)v.i); return;
+    case Value::TDouble: {
+      tag(4, 1);
+      uint64_t bits;
+      std::memcpy(&bits, &v.d, 8);
+      put_fixed(o, bits, 8);
+      return;
+    }
+    case Value::TBytes: bytes(7, v.s.data(), v.s.size()); return;
+    case Value::TSlice: {
+      uint64_t l = 0;
+      for (auto& e : v.slice) l += field_len(sz.any_value(e));
+      tag(5, 2);
+      varint(l);
+      for (auto& e : v.slice) {   // ArrayValue.values (field 1)
+        tag(1, 2);
+        varint(sz.any_value(e));
+        any_value(e);
+      }
+      return;
+    }
+    case Value::TMap: {
+      uint64_t l = 0;
+      for (auto& kv : v.map) l += field_len(sz.key_value(kv.first, kv.second));
+      tag(6, 2);
+      varint(l);
+      for (auto& kv : v.map) {   // KeyValueList.values (field 1)
+        tag(1, 2);
+        varint(sz.key_value(kv.first, kv.second));
+        key_value(kv.first, kv.second);
+      }
+      return;
+    }
+  }
+}
+void ProtoWriter::key_value(const std::string& k, const Value& v) {
+  str(1, k);
+  tag(2, 2);   // KeyValue.value: non-nullable, always framed
+  varint(ProtoSizer().any_value(v));
+  any_value(v);
+}
+void ProtoWriter::attrs(const AttrMap& m, uint32_t field) {
+  const ProtoSizer sz;
+  for (auto& kv : m.kv) {
+    tag(field, 2);
+    varint(sz.key_value(kv.first, kv.second));
+    key_value(kv.first, kv.second);
+  }
+}
+void ProtoWriter::span(const Span& s) {
+  put_id(*this, 1, s.trace_id);
+  put_id(*this, 2, s.span_id);
+  str(3, s.trace_state);
+  put_id(*this, 4, s.parent_span_id);
+  str(5, s.name);
+  if (s.kind) { tag(6, 0); varint((uint64_t)(int64_t)s.kind); }
+  if (s.start) { tag(7, 1); put_fixed(o, s.start, 8); }
+  if (s.end) { tag(8, 1); put_fixed(o, s.end, 8); }
+  attrs(s.attrs, 9);
+  if (s.dropped_attrs) { tag(10, 0); varint(s.dropped_attrs); }
+  const ProtoSizer sz;
+  for (auto& ev : s.events) {
+    const uint64_t e = (ev.time ? 9 : 0) + str_field(ev.name) + sz.attrs(ev.attrs, 3) + varint_field(ev.dropped);
+    tag(11, 2);
+    varint(e);
+    if (ev.time) { tag(1, 1); put_fixed(o, ev.time, 8); }
+    str(2, ev.name);
+    attrs(ev.attrs, 3);
+    if (ev.dropped) { tag(4, 0); varint(ev.dropped); }
+  }
+  if (s.dropped_events) { tag(12, 0); varint(s.dropped_events); }
+  for (auto& lk : s.links) {
+    const uint64_t e = id_field(lk.trace_id, true) + id_field(lk.span_id, true) + str_field(lk.trace_state) +
+                       sz.attrs(lk.attrs, 4) + varint_field(lk.dropped) + (lk.flags ? 5 : 0);
+    tag(13, 2);
+    varint(e);
+    put_id(*this, 1, lk.trace_id);
+    put_id(*this, 2, lk.span_id);
+    str(3, lk.trace_state);
+    attrs(lk.attrs, 4);
+    if (lk.dropped) { tag(5, 0); varint(lk.dropped); }
+    if (lk.flags) { tag(6, 5); put_fixed(o, lk.flags, 4); }
+  }
+  if (s.dropped_links) { tag(14, 0); varint(s.dropped_links); }
+  tag(15, 2);   // Status: non-nullable
+  varint(str_field(s.status_message) + varint_field((uint64_t)(int64_t)s.status_code));
+  str(2, s.status_message);
+  if (s.status_code) { tag(3, 0); varint((uint64_t)(int64_t)s.status_code); }
+  if (s.flags) { tag(16, 5); put_fixed(o, s.flags, 4); }
+}
+void ProtoWriter::resource(const AttrMap& a, uint32_t dropped) {
+  attrs(a, 1);
+  if (dropped) { tag(2, 0); varint(dropped); }
+}
+void ProtoWriter::scope(const ScopeSpans& ss) {
+  str(1, ss.scope_name);
+  str(2, ss.scope_version);
+  attrs(ss.scope_attrs, 3);
+  if (ss.scope_dropped) { tag(4, 0); varint(ss.scope_dropped); }
+}
+
 }  // namespace ose

@@ -132,4 +132,23 @@ struct ProtoSizer {
   uint64_t resource_spans(const ResourceSpans& rs) const;    // full ResourceSpans body
 };
 
+// ---- protobuf encoding: what pdata's generated marshalers write ----
+// (MarshalToSizedBuffer: fields in ascending number, defaults omitted,
+// gogo's always-framed messages and ids as ProtoSizer counts them), so a
+// message's bytes are exactly ProtoSizer{gogo=true}'s length.
+struct ProtoWriter {
+  std::string& o;
+  explicit ProtoWriter(std::string& out) : o(out) {}
+  void varint(uint64_t v);
+  void tag(uint32_t field, uint32_t wt);
+  void bytes(uint32_t field, const void* p, size_t n);   // LEN field, always written
+  void str(uint32_t field, const std::string& s);        // omitted when empty
+  void any_value(const Value& v);                        // AnyValue body
+  void key_value(const std::string& k, const Value& v);  // KeyValue body
+  void attrs(const AttrMap& m, uint32_t field);
+  void span(const Span& s);                              // Span body
+  void resource(const AttrMap& attrs, uint32_t dropped); // Resource body
+  void scope(const ScopeSpans& ss);                      // InstrumentationScope body
+};
+
 }  // namespace ose

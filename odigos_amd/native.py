@@ -128,6 +128,15 @@ def lib() -> C.CDLL:
         "ose_otlp_attrset": (C.c_int, [_p, C.c_uint32, C.c_char_p, C.c_size_t]),
         "ose_otlp_download": (C.c_int, [_p, C.POINTER(Columns)]),
         "ose_otlp_release": (None, [_p]),
+        "ose_router_create": (C.c_int, [C.c_char_p, C.POINTER(_p)]),
+        "ose_router_destroy": (None, [_p]),
+        "ose_router_pipelines": (C.c_uint32, [_p]),
+        "ose_router_pipeline": (C.c_char_p, [_p, C.c_uint32]),
+        "ose_otlp_encode": (C.c_int, [_p, _p, C.POINTER(Outputs), C.c_uint32, C.c_uint32, _p, _p, C.POINTER(_p)]),
+        "ose_otlp_out_count": (C.c_uint32, [_p]),
+        "ose_otlp_out_get": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(_p),
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+        "ose_otlp_out_release": (None, [_p]),
         "ose_engine_attr_key": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),
         "ose_batch_columns": (C.POINTER(Columns), [_p]),
@@ -167,6 +176,10 @@ def lib() -> C.CDLL:
         "osehost_roundtrip": (_p, [C.c_char_p]),
         "osehost_pb_to_json": (_p, [C.c_char_p, C.c_size_t]),
         "osehost_otlp_walk": (_p, [C.c_char_p, C.c_char_p, C.c_size_t]),
+        "osehost_otlp_encode": (C.c_int, [C.c_char_p, C.c_size_t, _p, C.c_int, _p, _p, _p, C.c_uint64, _p, C.c_int,
+                                          C.POINTER(_p)]),
+        "osehost_router_create_signal": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(_p)]),
+        "osehost_router_route": (_p, [_p, C.c_char_p]),
         "osehost_resource_sizes": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
         "osehost_as_string": (_p, [C.c_char_p]),
         "osehost_free": (None, [_p]),

@@ -178,6 +178,8 @@ def to_pb(td: dict) -> bytes:
         m.resource.SetInParent()
         for d in rs["resource"].get("attributes", []):
             kv(d, m.resource.attributes.add())
+        m.resource.dropped_attributes_count = int(rs["resource"].get("droppedAttributesCount", 0))
+        m.schema_url = rs.get("schemaUrl", "")
         for ss in rs["scopeSpans"]:
             s = m.scope_spans.add()
             sc = ss.get("scope", {})
@@ -188,6 +190,8 @@ def to_pb(td: dict) -> bytes:
                 s.scope.version = sc["version"]
             for d in sc.get("attributes", []):
                 kv(d, s.scope.attributes.add())
+            s.scope.dropped_attributes_count = int(sc.get("droppedAttributesCount", 0))
+            s.schema_url = ss.get("schemaUrl", "")
             for sp in ss["spans"]:
                 p = s.spans.add()
                 p.trace_id = bytes.fromhex(sp.get("traceId", ""))

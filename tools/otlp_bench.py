@@ -6,7 +6,9 @@ on the decoded columns.  PCIe-inclusive by construction: not a bench.py
 `value`.  One JSON line on stdout and in --out.
 
 Legs: decode from pinned memory (ose_host_alloc: a receiver reading into
-engine buffers), decode from pageable memory, and the stages after it.
+engine buffers), decode from pageable memory, the stages after it, and the
+output side (ose_otlp_encode: decisions D2H, routing to data-stream
+pipelines, one TracesData per pipeline).
 The span decoder's roofline: message bytes read + columns written per
 launch over its HIP-event time, against 8 TB/s.
 """
@@ -31,7 +33,7 @@ def main():
     import torch
     from bench import NODE_KEYS, cpu_share
     from odigos_amd import native
-    from odigos_amd.batch import Engine, Generator, OtlpBatch, PinnedBuffer
+    from odigos_amd.batch import Engine, Generator, OtlpBatch, PinnedBuffer, Router
     from tests.workloads import c3_sampling_config
     share, nproc, model = cpu_share()
     threads = max(1, min(16, share))
@@ -53,6 +55,17 @@ def main():
     outs = device_outputs(dims, tmpl_cap=64 * args.spans)
     phases = []
 
+    # data streams over the generated services (k8s.deployment.name = svc-NN in
+    # namespace default): two pipelines, one of them fed twice, the rest default
+    streams = [{"name": "ds-a", "sources": [{"namespace": "default", "kind": "Deployment", "name": "svc-%02d" % k}
+                                            for k in range(0, 12)],
+                "destinations": [{"destinationname": "d1", "configuredsignals": ["TRACES"]}]},
+               {"name": "ds-b", "sources": [{"namespace": "default", "kind": "Deployment", "name": "svc-%02d" % k}
+                                            for k in range(8, 20)],
+                "destinations": [{"destinationname": "d2", "configuredsignals": ["TRACES", "LOGS"]}]}]
+    router = Router({"datastreams": streams})
+    enc = []
+
     def one(pinned: bool, stages: bool):
         a = time.perf_counter()
         ob = (OtlpBatch(eng, pin.p, stream=sh, length=pin.n, outputs=outs) if pinned
@@ -64,6 +77,9 @@ def main():
             eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
             torch.cuda.synchronize()
         c = time.perf_counter()
+        if stages:
+            out = ob.encode(st, native.GROUP_TRACE_ID, router, stream=sh, copy=False)
+            enc.append((time.perf_counter() - c, out))
         info = (ob.cols.n_spans, ob.host_spans, int(ob.out_numpy("device_status", n=1)[0]) if stages else 0)
         ob.close()
         return b - a, c - b, info
@@ -95,6 +111,12 @@ def main():
     res["decode_spans_per_s"] = args.spans / dp
     res["host_pass_spans"] = info[1]
     res["span_kernel_ms"] = k_ms
+    e_best = min(enc[2:], key=lambda x: x[0])
+    res["encode_ms"] = e_best[0] * 1e3
+    res["encode_outputs"] = [{"pipeline": p, "bytes": nb, "resources": nr} for p, nb, nr in e_best[1]]
+    out_bytes = sum(x["bytes"] for x in res["encode_outputs"])
+    res["encode_out_GBps"] = out_bytes / e_best[0] / 1e9
+    res["end_to_end_with_encode_spans_per_s"] = args.spans / (dp + min(stg) + e_best[0])
     # decoder roofline: the message bytes it reads + 60 B/span of columns (and flags) written
     alg = len(pb) + 8 * args.spans + 60 * args.spans
     res["span_kernel_roofline"] = {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9 if k_ms else 0.0,
@@ -115,11 +137,12 @@ def main():
         sph.append(ob.timings_ms)
         eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
         torch.cuda.synchronize()
+        ob.encode(st, native.GROUP_TRACE_ID, router, stream=sh, copy=False)
         ob.close()
         if k >= 20:
             lat.append(time.perf_counter() - a)
     lat.sort()
-    res["batch8192_decode_and_stages_us"] = {"p50": lat[len(lat) // 2] * 1e6, "p99": lat[int(len(lat) * 0.99)] * 1e6}
+    res["batch8192_decode_stages_encode_us"] = {"p50": lat[len(lat) // 2] * 1e6, "p99": lat[int(len(lat) * 0.99)] * 1e6}
     res["batch8192_spans_per_s"] = 8192 / lat[len(lat) // 2]
     res["batch8192_decode_phases_ms_median"] = {k: sorted(x[k] for x in sph[20:])[len(sph[20:]) // 2] for k in sph[0]}
     spin.close()
