@@ -146,6 +146,7 @@ Engine::~Engine() {
   release_exchange_scratch(this);
   release_batch_pool(this);
   release_otlp(this);
+  release_encode(this);
   for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto s : streams) (void)hipStreamDestroy(s);
   for (auto ev : event_pool) (void)hipEventDestroy(ev);

@@ -26,6 +26,7 @@ void release_exchange_scratch(const Engine* e);   // shard_host.cpp
 void release_batch_pool(Engine* e);                // batch.cpp
 struct OtlpEngine;
 void release_otlp(Engine* e);                      // otlp_host.cpp
+void release_encode(Engine* e);                    // otlp_encode.cpp
 
 // Device scratch for one in-flight call (look-back status words, sort
 // buffers, partial records).  Engines keep a pool so concurrent callers never
@@ -88,6 +89,7 @@ struct Engine {
   std::vector<void*> batch_pool;   // released ose_batch slabs (batch.cpp)
   OtlpEngine* otlp = nullptr;      // OTLP ingest tables, built on first use (otlp_host.cpp)
   std::vector<void*> otlp_pool;    // released ose_otlp_batch objects
+  std::vector<void*> enc_pool;     // encoder workspaces of released ose_otlp_out objects
   size_t batch_pool_bytes = 0;
 
   // ose_profile_*: (kernel name, start, stop) per launch

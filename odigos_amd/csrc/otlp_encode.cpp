@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <cctype>
+#include <chrono>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -31,6 +33,7 @@
 
 #include "engine_internal.hpp"
 #include "otlp_pb.hpp"
+#include "taskpool.hpp"
 
 namespace ose {
 
@@ -132,7 +135,7 @@ const std::vector<uint32_t>* Router::route(const AttrMap& attrs, std::string* ke
 
 // ---- the encoder ------------------------------------------------------------
 
-namespace {
+namespace enc {
 constexpr uint64_t kDropped = ~0ull;
 
 inline uint32_t sov64(uint64_t x) { uint32_t n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
@@ -155,14 +158,25 @@ struct ResHdr {
   bool routed = false;                        // route found (else default)
 };
 
+// One rewritten span: the source with the name field and the target
+// KeyValue replaced (a < b) or inserted (a == b) — or, in_mods, bytes
+// re-marshaled into Chunk::mods at name_a.
+struct Edit {
+  uint32_t name_a, name_b, attr_a, attr_b;
+  uint32_t meth_off, meth_len;   // the method string (in the message, or in mods)
+  uint32_t tmpl_off, tmpl_len;   // the template (in the template arena)
+  uint32_t out_len;
+  uint8_t u, client, in_mods, meth_in_mods;
+};
+
 struct Chunk {
   size_t r0 = 0, r1 = 0;
   std::unordered_map<std::string_view, ResHdr> rcache;
   std::unordered_map<std::string_view, std::string> scache;
   std::deque<ResHdr> rown;          // merged headers (several Resource fields)
   std::deque<std::string> sown;
-  std::string mods;                 // edited / re-marshaled spans, in order
-  std::vector<uint32_t> mod_len;
+  std::vector<Edit> edits;          // one per rewritten span, in order
+  std::string mods;                 // re-marshaled spans, AsString methods
   std::vector<uint64_t> out_bytes, out_res, cursor;
   std::string err;
 };
@@ -176,11 +190,12 @@ struct Enc {
   const Router* router;
   uint64_t n, R, S;
   uint32_t n_out;
-  // per resource / scope results of pass 1
-  std::vector<uint64_t> res_body, res_schema;
-  std::vector<const ResHdr*> res_hdr;
-  std::vector<uint64_t> scope_body;
-  std::vector<const std::string*> scope_hdr;
+  // per resource / scope results of pass 1 (the workspace's)
+  std::vector<uint64_t>& res_body;
+  std::vector<uint64_t>& res_schema;
+  std::vector<const ResHdr*>& res_hdr;
+  std::vector<uint64_t>& scope_body;
+  std::vector<const std::string*>& scope_hdr;
 
   uint64_t scope_end(uint64_t s) const { return s + 1 < S ? lay.scope_span0[s + 1] : n; }
   uint64_t res_scope_end(uint64_t r) const { return r + 1 < R ? lay.res_scope0[r + 1] : S; }
@@ -257,7 +272,8 @@ struct Enc {
     return &c.sown.back();
   }
 
-  // The processed span i into c.mods; false on a malformed span.
+  // The processed span i: an edit plan (or bytes in c.mods) appended to
+  // c.edits; false on a malformed span.
   bool rewrite(Chunk& c, uint64_t i) {
     const uint8_t* sp = pb + (uint32_t)span_ref[i];
     const size_t L = (size_t)(span_ref[i] >> 32);
@@ -268,14 +284,16 @@ struct Enc {
       if ((uint64_t)t.off + t.len > d.tmpl_arena_len) { c.err = "template reference beyond the template arena"; return false; }
       T = std::string_view((const char*)d.tmpl_arena + t.off, t.len);
     }
-    const size_t start = c.mods.size();
     const bool canonical = !d.span_size || d.span_size[i] == (uint32_t)L;
-    if (canonical ? !edit_in_place(c, sp, L, u, T) : !remarshal(c, sp, L, u, T)) return false;
-    c.mod_len.push_back((uint32_t)(c.mods.size() - start));
-    return true;
+    if (canonical) {
+      int rc = plan_edit(c, sp, L, u, T);
+      if (rc < 0) return false;
+      if (rc > 0) return true;
+    }
+    return remarshal(c, sp, L, u, T);
   }
 
-  // host.cpp Apply (processor.go:230-232, 259) on the decoded span
+  // host.cpp Apply (processor.go:230-232, 259) on the decoded span, written to c.mods
   bool remarshal(Chunk& c, const uint8_t* sp, size_t L, uint8_t u, std::string_view T) {
     Span s;
     if (!pb_span(sp, L, s)) { c.err = "OTLP protobuf: malformed Span"; return false; }
@@ -288,29 +306,40 @@ struct Enc {
         s.name = (m ? m->AsString() : std::string()) + " " + tmpl;
       }
     }
+    const size_t start = c.mods.size();
     ProtoWriter(c.mods).span(s);
+    Edit e{};
+    e.in_mods = 1;
+    e.name_a = (uint32_t)start;
+    e.out_len = (uint32_t)(c.mods.size() - start);
+    c.edits.push_back(e);
     return true;
   }
 
-  // The same change on bytes already in pdata's encoding: fields ascend, so
-  // the name goes at field 5's place and an appended attribute after the
-  // last field 9.
-  bool edit_in_place(Chunk& c, const uint8_t* sp, size_t L, uint8_t u, std::string_view T) {
-    struct Rec { uint32_t f; size_t a, b; };
-    thread_local std::vector<Rec> recs;
-    recs.clear();
+  // The same change on bytes already in pdata's encoding, as a plan: fields
+  // ascend, so the new name takes field 5's place (or goes before the first
+  // later field) and the target KeyValue replaces the first one with its key
+  // (Map.PutStr) or goes after the last attribute.  1 = planned, 0 = the
+  // fields are out of order (re-marshal), -1 = malformed.
+  int plan_edit(Chunk& c, const uint8_t* sp, size_t L, uint8_t u, std::string_view T) {
+    Edit e{};
+    e.u = u;
+    e.name_a = e.name_b = (uint32_t)L;
+    e.attr_a = e.attr_b = (uint32_t)L;
+    e.tmpl_off = (uint32_t)(T.data() - (const char*)d.tmpl_arena);
+    e.tmpl_len = (uint32_t)T.size();
     int32_t kind = 0;
-    size_t tgt = SIZE_MAX;   // record index of the target KeyValue
+    bool name_set = false, attr_set = false, have_new = false, have_old = false;
     const uint8_t* mnew = nullptr; size_t mnew_len = 0;
     const uint8_t* mold = nullptr; size_t mold_len = 0;
-    bool have_new = false, have_old = false;
+    uint32_t prev_f = 0;
     PbReader r(sp, L);
     uint32_t f, wt;
-    // pass over the span's fields (kind precedes the attributes)
-    std::string_view target;
     while (r.more()) {
       const size_t a = r.i;
       if (!r.tag(f, wt)) break;
+      if (f < prev_f) return 0;
+      prev_f = f;
       size_t po = 0, pl = 0;
       if (f == 6 && wt == 0) {
         kind = (int32_t)r.varint();
@@ -319,10 +348,12 @@ struct Enc {
       } else if (!r.skip(wt, f)) {
         break;
       }
-      const size_t nrec = recs.size();
-      recs.push_back(Rec{f, a, r.i});
+      if (!name_set && f >= 5) {   // the name's place
+        e.name_a = (uint32_t)a;
+        e.name_b = f == 5 ? (uint32_t)r.i : (uint32_t)a;
+        name_set = true;
+      }
       if (f == 9 && wt == 2) {
-        if (target.empty()) target = kind == OSE_KIND_CLIENT ? "url.template" : "http.route";
         // KeyValue: key (field 1), value (field 2)
         PbReader kv(sp + po, pl);
         uint32_t kf, kwt;
@@ -338,84 +369,110 @@ struct Enc {
             kv.skip(kwt, kf);
           }
         }
-        const std::string_view key((const char*)sp + po + ko, kl);
-        if ((u & OSE_OUT_SET_ATTR) && tgt == SIZE_MAX && key == target) tgt = nrec;
-        if (!have_new && key == "http.request.method") {
+        const char* key = (const char*)sp + po + ko;
+        if ((u & OSE_OUT_SET_ATTR) && !attr_set) {
+          const bool client = kind == OSE_KIND_CLIENT;
+          if (client ? (kl == 12 && std::memcmp(key, "url.template", 12) == 0)
+                     : (kl == 10 && std::memcmp(key, "http.route", 10) == 0)) {
+            e.attr_a = (uint32_t)a;
+            e.attr_b = (uint32_t)r.i;
+            attr_set = true;
+          }
+        }
+        if (!have_new && kl == 19 && std::memcmp(key, "http.request.method", 19) == 0) {
           have_new = true;
           mnew = hv ? sp + po + vo : nullptr, mnew_len = hv ? vl : 0;
-        } else if (!have_old && key == "http.method") {
+        } else if (!have_old && kl == 11 && std::memcmp(key, "http.method", 11) == 0) {
           have_old = true;
           mold = hv ? sp + po + vo : nullptr, mold_len = hv ? vl : 0;
         }
+      } else if (f > 9 && !attr_set) {   // after the last attribute
+        e.attr_a = e.attr_b = (uint32_t)a;
+        attr_set = true;
       }
     }
-    if (!r.ok || r.i != L) { c.err = "OTLP protobuf: malformed Span"; return false; }
-    if (target.empty()) target = kind == OSE_KIND_CLIENT ? "url.template" : "http.route";
-    std::string name;
+    if (!r.ok || r.i != L) { c.err = "OTLP protobuf: malformed Span"; return -1; }
+    e.client = kind == OSE_KIND_CLIENT;
+    if (!(u & OSE_OUT_RENAME)) e.name_a = e.name_b = 0;
+    if (!(u & OSE_OUT_SET_ATTR)) e.attr_a = e.attr_b = (uint32_t)L;
+    uint64_t out = L - (e.name_b - e.name_a) - (e.attr_b - e.attr_a);
     if (u & OSE_OUT_RENAME) {
+      // the method: AnyValue{string_value} in place; anything else through pdata's AsString
       const uint8_t* mv = have_new ? mnew : mold;
       const size_t ml = have_new ? mnew_len : mold_len;
+      e.meth_len = 0;
       if (have_new || have_old) {
-        // AnyValue{string_value} directly; anything else through pdata's AsString
-        uint64_t sl;
-        size_t hdr = 1;
         bool direct = false;
         if (mv && ml >= 2 && mv[0] == 0x0A) {
           PbReader vr(mv, ml);
           vr.i = 1;
-          sl = vr.varint();
-          hdr = vr.i;
-          direct = vr.ok && hdr + sl == ml;
+          const uint64_t sl = vr.varint();
+          direct = vr.ok && vr.i + sl == ml;
+          if (direct) {
+            e.meth_off = (uint32_t)(mv + vr.i - pb);
+            e.meth_len = (uint32_t)sl;
+          }
         }
-        if (direct) {
-          name.assign((const char*)mv + hdr, ml - hdr);
-        } else {
+        if (!direct) {
           Value v;
-          if (mv && !pb_any_value(mv, ml, v)) { c.err = "OTLP protobuf: malformed AnyValue"; return false; }
-          name = v.AsString();
+          if (mv && !pb_any_value(mv, ml, v)) { c.err = "OTLP protobuf: malformed AnyValue"; return -1; }
+          const std::string m = v.AsString();
+          e.meth_in_mods = 1;
+          e.meth_off = (uint32_t)c.mods.size();
+          e.meth_len = (uint32_t)m.size();
+          c.mods += m;
         }
       }
-      name += ' ';
-      name.append(T.data(), T.size());
+      out += flen((uint64_t)e.meth_len + 1 + T.size());
     }
-    // write
-    std::string& o = c.mods;
-    auto put_name = [&]() {
-      ProtoWriter(o).bytes(5, name.data(), name.size());
-    };
-    auto put_attr = [&]() {
-      const uint64_t av = flen(T.size());
-      const uint64_t kvl = flen(target.size()) + flen(av);
-      ProtoWriter w(o);
-      w.tag(9, 2);
-      w.varint(kvl);
-      w.bytes(1, target.data(), target.size());
-      w.tag(2, 2);
-      w.varint(av);
-      w.bytes(1, T.data(), T.size());
-    };
-    bool name_done = !(u & OSE_OUT_RENAME), attr_done = !(u & OSE_OUT_SET_ATTR);
-    for (size_t k = 0; k < recs.size(); k++) {
-      const Rec& x = recs[k];
-      if (!name_done && x.f >= 5) {
-        put_name();
-        name_done = true;
-        if (x.f == 5) continue;
-      }
-      if (!attr_done && k == tgt) {
-        put_attr();
-        attr_done = true;
-        continue;
-      }
-      if (!attr_done && tgt == SIZE_MAX && x.f > 9) {
-        put_attr();
-        attr_done = true;
-      }
-      o.append((const char*)sp + x.a, x.b - x.a);
+    if (u & OSE_OUT_SET_ATTR) out += flen(kv_len(e.client, T.size()));
+    if (e.name_b > e.attr_a) return 0;   // not the ascending order the plan assumes
+    e.out_len = (uint32_t)out;
+    c.edits.push_back(e);
+    return 1;
+  }
+  static uint64_t kv_len(bool client, size_t tl) {   // KeyValue{key, AnyValue{string_value}}
+    return flen(client ? 12 : 10) + flen(flen(tl));
+  }
+
+  // an edited span's bytes at w
+  uint8_t* write_edit(const Chunk& c, const Edit& e, const uint8_t* sp, size_t L, uint8_t* w) const {
+    if (e.in_mods) {
+      std::memcpy(w, c.mods.data() + e.name_a, e.out_len);
+      return w + e.out_len;
     }
-    if (!name_done) put_name();
-    if (!attr_done) put_attr();
-    return true;
+    const char* T = (const char*)d.tmpl_arena + e.tmpl_off;
+    std::memcpy(w, sp, e.name_a);
+    w += e.name_a;
+    if (e.u & OSE_OUT_RENAME) {
+      *w++ = 0x2A;
+      w = put_varint(w, (uint64_t)e.meth_len + 1 + e.tmpl_len);
+      const uint8_t* m = e.meth_in_mods ? (const uint8_t*)c.mods.data() + e.meth_off : pb + e.meth_off;
+      std::memcpy(w, m, e.meth_len);
+      w += e.meth_len;
+      *w++ = ' ';
+      std::memcpy(w, T, e.tmpl_len);
+      w += e.tmpl_len;
+    }
+    std::memcpy(w, sp + e.name_b, e.attr_a - e.name_b);
+    w += e.attr_a - e.name_b;
+    if (e.u & OSE_OUT_SET_ATTR) {
+      const size_t kl = e.client ? 12 : 10;
+      *w++ = 0x4A;
+      w = put_varint(w, kv_len(e.client, e.tmpl_len));
+      *w++ = 0x0A;
+      *w++ = (uint8_t)kl;
+      std::memcpy(w, e.client ? "url.template" : "http.route", kl);
+      w += kl;
+      *w++ = 0x12;
+      w = put_varint(w, flen(e.tmpl_len));
+      *w++ = 0x0A;
+      w = put_varint(w, e.tmpl_len);
+      std::memcpy(w, T, e.tmpl_len);
+      w += e.tmpl_len;
+    }
+    std::memcpy(w, sp + e.attr_b, L - e.attr_b);
+    return w + (L - e.attr_b);
   }
 
   // pass 1: sizes, headers, edited spans
@@ -465,7 +522,7 @@ struct Enc {
           uint64_t l = span_ref[i] >> 32;
           if (rewritten(i)) {
             if (!rewrite(c, i)) return;
-            l = c.mod_len.back();
+            l = c.edits.back().out_len;
           }
           sb += flen(l);
         }
@@ -494,7 +551,7 @@ struct Enc {
 
   // pass 2: the records at their final offsets
   void write_chunk(Chunk& c, std::vector<EncodedOutput>& outs) {
-    size_t mi = 0, moff = 0;
+    size_t ei = 0;
     for (uint64_t r = c.r0; r < c.r1; r++) {
       if (res_body[r] == kDropped) continue;
       uint32_t ks[64], nk;
@@ -517,9 +574,10 @@ struct Enc {
         for (uint64_t i = i0; i < i1; i++) {
           if (!kept(i)) continue;
           if (rewritten(i)) {
-            const uint32_t l = c.mod_len[mi++];
-            w = put_rec(w, 0x12, c.mods.data() + moff, l);
-            moff += l;
+            const Edit& ed = c.edits[ei++];
+            *w++ = 0x12;
+            w = put_varint(w, ed.out_len);
+            w = write_edit(c, ed, pb + (uint32_t)span_ref[i], span_ref[i] >> 32, w);
           } else {
             w = put_rec(w, 0x12, pb + (uint32_t)span_ref[i], span_ref[i] >> 32);
           }
@@ -538,12 +596,57 @@ struct Enc {
     }
   }
 };
-}  // namespace
+}  // namespace enc
+
+struct EncodeWork {
+  std::vector<enc::Chunk> ch;
+  std::vector<uint64_t> res_body, res_schema, scope_body;
+  std::vector<const enc::ResHdr*> res_hdr;
+  std::vector<const std::string*> scope_hdr;
+  std::vector<std::pair<uint8_t*, size_t>> bufs;   // free output buffers
+  ~EncodeWork() {
+    for (auto& b : bufs) std::free(b.first);
+  }
+};
+EncodeWork* encode_work_new() { return new EncodeWork(); }
+void encode_work_free(EncodeWork* w) { delete w; }
+
+void otlp_out_release(OtlpOut* o) {
+  if (!o) return;
+  if (o->work) {
+    for (auto& x : o->outs)
+      if (x.data) o->work->bufs.emplace_back(x.data, x.cap);
+    o->outs.clear();
+    if (o->e) {
+      std::lock_guard<std::mutex> g(o->e->mu);
+      if (o->e->enc_pool.size() < 8) {
+        o->e->enc_pool.push_back(o->work);
+        o->work = nullptr;
+      }
+    }
+    delete o->work;
+  }
+  delete o;
+}
+
+void release_encode(Engine* e) {
+  for (void* p : e->enc_pool) delete static_cast<EncodeWork*>(p);
+  e->enc_pool.clear();
+}
 
 bool encode_traces(const uint8_t* pb, size_t len, const std::vector<uint64_t>& span_ref, const OtlpLayout& lay,
-                   const EncodeDecisions& d, const Router* router, int threads, std::vector<EncodedOutput>& outs,
-                   std::string& err) {
-  Enc e{pb, len, span_ref, lay, d, router, span_ref.size(), lay.res_ref.size(), lay.scope_ref.size(), 1, {}, {}, {}, {}, {}};
+                   const EncodeDecisions& d, const Router* router, int threads, EncodeWork& w,
+                   std::vector<EncodedOutput>& outs, std::string& err, double* t_ms3) {
+  using namespace enc;
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now();
+  auto lap = [&](int k) {
+    const auto t = clk::now();
+    if (t_ms3) t_ms3[k] = std::chrono::duration<double, std::milli>(t - t0).count();
+    t0 = t;
+  };
+  Enc e{pb, len, span_ref, lay, d, router, span_ref.size(), lay.res_ref.size(), lay.scope_ref.size(), 1,
+        w.res_body, w.res_schema, w.res_hdr, w.scope_body, w.scope_hdr};
   if (router) {
     if (router->pipelines.size() > 63) { err = "router: more than 63 pipelines"; return false; }
     e.n_out = (uint32_t)router->pipelines.size() + 1;
@@ -555,8 +658,19 @@ bool encode_traces(const uint8_t* pb, size_t len, const std::vector<uint64_t>& s
   e.scope_hdr.assign(e.S, nullptr);
   // chunks of about equal span counts
   int T = std::max(1, threads);
-  T = (int)std::min<uint64_t>((uint64_t)T, std::max<uint64_t>(1, std::min<uint64_t>(e.R, e.n / 32768 + 1)));
-  std::vector<Chunk> ch((size_t)T);
+  T = (int)std::min<uint64_t>((uint64_t)T, std::max<uint64_t>(1, std::min<uint64_t>(e.R, e.n / 2048 + 1)));
+  std::vector<Chunk>& ch = w.ch;
+  if (ch.size() < (size_t)T) ch.resize((size_t)T);
+  for (int t = 0; t < T; t++) {   // keep the capacity, drop the contents
+    Chunk& c = ch[t];
+    c.rcache.clear();
+    c.scache.clear();
+    c.rown.clear();
+    c.sown.clear();
+    c.mods.clear();
+    c.edits.clear();
+    c.err.clear();
+  }
   {
     uint64_t r = 0;
     for (int t = 0; t < T; t++) {
@@ -567,35 +681,52 @@ bool encode_traces(const uint8_t* pb, size_t len, const std::vector<uint64_t>& s
       ch[t].r1 = r;
     }
   }
-  auto run = [&](auto&& fn) {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; t++) th.emplace_back([&, t]() { fn(ch[t]); });
-    fn(ch[0]);
-    for (auto& x : th) x.join();
-  };
+  auto run = [&](auto&& fn) { parallel_run(T, [&](int t) { fn(ch[t]); }); };
   run([&](Chunk& c) { e.size_chunk(c); });
-  for (auto& c : ch)
-    if (!c.err.empty()) { err = c.err; return false; }
+  for (int t = 0; t < T; t++)
+    if (!ch[t].err.empty()) { err = ch[t].err; return false; }
+  lap(0);
   outs.assign(e.n_out, EncodedOutput{});
   for (uint32_t k = 0; k < e.n_out; k++) {
     outs[k].name = router ? (k + 1 < e.n_out ? router->pipelines[k] : std::string("default")) : std::string();
     uint64_t off = 0;
-    for (auto& c : ch) {
+    for (int t = 0; t < T; t++) {
+      Chunk& c = ch[t];
       c.cursor.resize(e.n_out);
       c.cursor[k] = off;
       off += c.out_bytes[k];
       outs[k].n_resources += (uint32_t)c.out_res[k];
     }
     outs[k].len = off;
-    outs[k].data = static_cast<uint8_t*>(std::malloc(off ? off : 1));
-    if (!outs[k].data) {
-      for (auto& x : outs) std::free(x.data);
+  }
+  // buffers: the largest outputs take the largest free buffers
+  std::vector<uint32_t> order(e.n_out);
+  for (uint32_t k = 0; k < e.n_out; k++) order[k] = k;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return outs[a].len > outs[b].len; });
+  std::sort(w.bufs.begin(), w.bufs.end(), [](auto& a, auto& b) { return a.second > b.second; });
+  for (uint32_t q = 0; q < e.n_out; q++) {
+    EncodedOutput& x = outs[order[q]];
+    const size_t need = std::max<size_t>(x.len, 64);
+    if (!w.bufs.empty() && w.bufs.front().second >= need) {
+      x.data = w.bufs.front().first;
+      x.cap = w.bufs.front().second;
+      w.bufs.erase(w.bufs.begin());
+      continue;
+    }
+    const size_t cap = need + need / 8;
+    x.data = static_cast<uint8_t*>(std::malloc(cap));
+    x.cap = cap;
+    if (!x.data) {
+      for (auto& y : outs)
+        if (y.data) w.bufs.emplace_back(y.data, y.cap);
       outs.clear();
       err = "out of host memory";
       return false;
     }
   }
+  lap(1);
   run([&](Chunk& c) { e.write_chunk(c, outs); });
+  lap(2);
   return true;
 }
 
@@ -646,7 +777,14 @@ int ose_otlp_out_get(const ose_otlp_out* o, uint32_t k, const char** name, const
   return 0;
 }
 
-void ose_otlp_out_release(ose_otlp_out* o) { delete reinterpret_cast<OtlpOut*>(o); }
+void ose_otlp_out_release(ose_otlp_out* o) { otlp_out_release(reinterpret_cast<OtlpOut*>(o)); }
+
+// diagnostics: decisions D2H, sizing pass, buffers, writing pass (ms)
+int osehost_otlp_out_timings(const ose_otlp_out* o, double* ms4) {
+  if (!o || !ms4) return fail(OSE_EINVAL, "NULL argument");
+  std::memcpy(ms4, reinterpret_cast<const OtlpOut*>(o)->t_ms, sizeof(double) * 4);
+  return 0;
+}
 
 // Test seams (CPU).  A router for any signal (the KATs route logs and
 // metrics too); the routing of one resource's attributes ({"key": value})

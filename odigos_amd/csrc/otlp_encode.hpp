@@ -53,22 +53,33 @@ struct EncodeDecisions {
 
 struct EncodedOutput {
   std::string name;
-  uint8_t* data = nullptr;   // malloc'd
+  uint8_t* data = nullptr;   // malloc'd, from the workspace's buffers
+  size_t cap = 0;
   uint64_t len = 0;
   uint32_t n_resources = 0;
 };
 
+// The encoder's grow-only state (per-thread chunks, per-resource records,
+// output buffers): reused across calls so a steady stream of batches does
+// not allocate or fault in fresh pages.
+struct EncodeWork;
+EncodeWork* encode_work_new();
+void encode_work_free(EncodeWork* w);
+
+struct Engine;
 struct OtlpOut {   // ose_otlp_out
   std::vector<EncodedOutput> outs;
-  ~OtlpOut() {
-    for (auto& o : outs) std::free(o.data);
-  }
+  EncodeWork* work = nullptr;   // the outputs' buffers go back to it
+  Engine* e = nullptr;          // whose pool the workspace returns to (NULL: freed)
+  double t_ms[4] = {0, 0, 0, 0};   // decisions D2H, sizing pass, buffers, writing pass
 };
+void otlp_out_release(OtlpOut* o);
 
 // One TracesData per output (router pipelines, then the default one; one
-// output without a router).  false + err on a malformed message.
+// output without a router).  false + err on a malformed message.  t_ms3:
+// the sizing pass, buffers, writing pass.
 bool encode_traces(const uint8_t* pb, size_t len, const std::vector<uint64_t>& span_ref, const OtlpLayout& lay,
-                   const EncodeDecisions& d, const Router* router, int threads, std::vector<EncodedOutput>& outs,
-                   std::string& err);
+                   const EncodeDecisions& d, const Router* router, int threads, EncodeWork& w,
+                   std::vector<EncodedOutput>& outs, std::string& err, double* t_ms3 = nullptr);
 
 }  // namespace ose

@@ -23,6 +23,7 @@
 #include "kernels.hpp"
 #include "otlp_encode.hpp"
 #include "otlp_pb.hpp"
+#include "taskpool.hpp"
 
 namespace ose {
 
@@ -363,8 +364,8 @@ size_t find_start(const uint8_t* p, size_t n, size_t k) {
 // one started (the chain from 0 is unique), else the walk runs again on one
 // thread.
 bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
-  const size_t kSeg = size_t(4) << 20;
-  int T = (int)std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1u, std::thread::hardware_concurrency()), n / kSeg}));
+  const size_t kSeg = size_t(256) << 10;
+  int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)parallel_width(), n / kSeg}));
   if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));   // diagnostics
   std::vector<WalkChunk> ch;
   for (int attempt = 0; attempt < 2; attempt++) {
@@ -374,12 +375,7 @@ bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
     for (int t = 1; t < T; t++) st[t] = find_start(p, n, n * (size_t)t / (size_t)T);
     for (int t = T - 1; t >= 1; t--) st[t] = std::min(st[t], st[t + 1]);   // monotone
     ch.assign((size_t)T, WalkChunk());
-    {
-      std::vector<std::thread> th;
-      for (int t = 1; t < T; t++) th.emplace_back([&, t]() { walk_segment(ctx, p, n, st[t], st[t + 1], ch[t], &en[t]); });
-      walk_segment(ctx, p, n, st[0], st[1], ch[0], &en[0]);
-      for (auto& x : th) x.join();
-    }
+    parallel_run(T, [&](int t) { walk_segment(ctx, p, n, st[t], st[t + 1], ch[t], &en[t]); });
     bool exact = true;
     for (int t = 0; t < T; t++) {
       if (!ch[t].err.empty()) {
@@ -461,12 +457,7 @@ bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
       w.lay.scope_span0[co[t] + k] = (uint32_t)(so[t] + c.lay.scope_span0[k]);
     }
   };
-  {
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < ch.size(); t++) th.emplace_back(place, t);
-    place(0);
-    for (auto& x : th) x.join();
-  }
+  parallel_run((int)ch.size(), [&](int t) { place((size_t)t); });
   return true;
 }
 }  // namespace
@@ -863,9 +854,7 @@ int ose_otlp_attrset(const ose_otlp_batch* bb, uint32_t k, char* json, size_t ca
 }
 
 namespace {
-int encode_threads() {
-  return (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-}
+int encode_threads() { return parallel_width(); }
 }  // namespace
 
 int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs* outs, uint32_t stages,
@@ -884,6 +873,7 @@ int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs
   if (tmpl && (!outs->url_out || !outs->tmpl || !outs->tmpl_arena || !outs->tmpl_arena_used))
     return fail(OSE_EINVAL, "template outputs are NULL");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  const auto t_start = std::chrono::steady_clock::now();
   const uint64_t n = b->cols.n_spans;
   // the decisions and the decoder's span sizes, D2H into the batch's pinned staging
   const size_t o_keep = 0, o_url = up(n + 16), o_tmpl = o_url + up(n + 16), o_size = o_tmpl + up(8 * n + 16),
@@ -927,10 +917,20 @@ int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs
   }
   d.span_size = reinterpret_cast<const uint32_t*>(h + o_size);
   auto* o = new OtlpOut();
+  o->e = e;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->enc_pool.empty()) {
+      o->work = static_cast<EncodeWork*>(e->enc_pool.back());
+      e->enc_pool.pop_back();
+    }
+  }
+  if (!o->work) o->work = encode_work_new();
+  o->t_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   std::string err;
   if (!encode_traces(b->pb, b->pb_len, b->span_ref, b->lay, d, reinterpret_cast<const Router*>(router),
-                     encode_threads(), o->outs, err)) {
-    delete o;
+                     encode_threads(), *o->work, o->outs, err, o->t_ms + 1)) {
+    otlp_out_release(o);
     return fail(OSE_EINVAL, err);
   }
   *out = reinterpret_cast<ose_otlp_out*>(o);
@@ -966,9 +966,10 @@ int osehost_otlp_encode(const uint8_t* pb, size_t len, const uint8_t* keep, int 
   d.tmpl_arena_len = tmpl_arena_len;
   d.span_size = sizes.data();
   auto* o = new OtlpOut();
+  o->work = encode_work_new();
   if (!encode_traces(pb, len, w.span_ref, w.lay, d, reinterpret_cast<const Router*>(router),
-                     threads > 0 ? threads : encode_threads(), o->outs, err)) {
-    delete o;
+                     threads > 0 ? threads : encode_threads(), *o->work, o->outs, err, o->t_ms + 1)) {
+    otlp_out_release(o);
     return fail(OSE_EINVAL, err);
   }
   *out = reinterpret_cast<ose_otlp_out*>(o);

@@ -5,51 +5,6 @@
 
 namespace ose {
 
-uint64_t PbReader::varint() {
-  uint64_t v = 0;
-  for (uint32_t shift = 0;; shift += 7) {
-    if (shift >= 64 || i >= n) { ok = false; return 0; }   // ErrIntOverflow / io.ErrUnexpectedEOF
-    const uint8_t b = p[i++];
-    v |= (uint64_t)(b & 0x7F) << shift;
-    if (b < 0x80) return v;
-  }
-}
-
-bool PbReader::tag(uint32_t& field, uint32_t& wt) {
-  const uint64_t t = varint();
-  if (!ok) return false;
-  field = (uint32_t)(t >> 3);
-  wt = (uint32_t)(t & 7);
-  if ((t >> 3) == 0 || (t >> 3) > 0x1FFFFFFF || wt == 4) { ok = false; return false; }   // illegal tag / end group
-  return true;
-}
-
-uint64_t PbReader::fixed64() {
-  if (i + 8 > n) { ok = false; return 0; }
-  uint64_t v;
-  std::memcpy(&v, p + i, 8);
-  i += 8;
-  return v;
-}
-
-uint32_t PbReader::fixed32() {
-  if (i + 4 > n) { ok = false; return 0; }
-  uint32_t v;
-  std::memcpy(&v, p + i, 4);
-  i += 4;
-  return v;
-}
-
-bool PbReader::bytes(size_t& off, size_t& len) {
-  const uint64_t l = varint();
-  if (!ok) return false;
-  if (l > (uint64_t)INT64_MAX || l > n - i) { ok = false; return false; }   // ErrInvalidLength / EOF
-  off = i;
-  len = (size_t)l;
-  i += (size_t)l;
-  return true;
-}
-
 // skipTraces: the unknown field whose tag was just read, groups included
 bool PbReader::skip(uint32_t wt, uint32_t) {
   int depth = 0;

@@ -358,3 +358,34 @@ def test_gpu_encode_generated_batch():
     names = [sp["name"] for rs in out_td["resourceSpans"] for ss in rs["scopeSpans"] for sp in ss["spans"]]
     assert len(names) == int(keep.sum())
     ob.close()
+
+
+def test_encode_concurrent_callers():
+    """Calls from several threads at once share the host task pool (each
+    caller helps run the queued work): every result equals the serial one."""
+    import threading
+    from odigos_amd.batch import Generator
+    g = Generator("fused", seed=0x7A5C, n_spans=40_000, threads=4)
+    pb = g.otlp(4)
+    n = g.cols.n_spans
+    rng = np.random.default_rng(3)
+    keep = (rng.random(n) < 0.5).astype(np.uint8)
+    url = rng.choice(np.array([0, 1, 2, 3], dtype=np.uint8), n)
+    tmpls = ["/a/{id}"] * n
+    want = _encode_seam(pb, keep, url, tmpls, threads=8)
+    errs = []
+
+    def worker():
+        try:
+            for _ in range(3):
+                if _encode_seam(pb, keep, url, tmpls, threads=8) != want:
+                    errs.append("mismatch")
+        except Exception as ex:   # noqa: BLE001
+            errs.append(repr(ex))
+
+    th = [threading.Thread(target=worker) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
