@@ -12,6 +12,8 @@
 //      strings appended after the message bytes, written by otlp_fix_kernel.
 #include <algorithm>
 #include <chrono>
+#include <deque>
+#include <shared_mutex>
 #include <cstring>
 #include <map>
 #include <string_view>
@@ -57,6 +59,33 @@ struct DevBuf {   // grow-only device (or pinned host) buffer
 };
 }  // namespace
 
+namespace {
+struct CachedRes {
+  uint32_t svc, svc_str, set, rpart;   // set: id in ResCache::sets
+  uint8_t ok;
+  uint64_t attr_res;
+};
+
+// Resource columns by message bytes, kept across calls (a gateway sees the
+// same pods' resources batch after batch), and the attribute sets interned.
+struct ResCache {
+  static constexpr size_t kMaxEntries = size_t(1) << 16;
+  std::shared_mutex mu;
+  std::deque<std::string> keys;   // owned bytes the map's views point into
+  std::unordered_map<std::string_view, CachedRes> map;
+  std::deque<std::vector<std::pair<std::string, std::string>>> sets;   // stable addresses
+  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
+  uint32_t intern(const std::vector<std::pair<std::string, std::string>>& set) {   // under the unique lock
+    auto it = set_ids.find(set);
+    if (it != set_ids.end()) return it->second;
+    const uint32_t id = (uint32_t)sets.size();
+    sets.push_back(set);
+    set_ids.emplace(set, id);
+    return id;
+  }
+};
+}  // namespace
+
 // The engine's view for the ingest: the columniser context and the key
 // table the GPU decoder matches (built once per engine).
 struct OtlpEngine {
@@ -67,6 +96,7 @@ struct OtlpEngine {
   uint8_t* keys_dev = nullptr;   // OtlpKeyDev[] then the bytes
   uint32_t n_attr_keys = 0;
   bool json_rules = false;
+  ResCache res_cache;
   std::string err;
   ~OtlpEngine() { if (keys_dev) (void)hipFree(keys_dev); }
 };
@@ -180,24 +210,17 @@ struct WalkChunk {
   std::vector<uint8_t> res_ok;
   std::vector<uint64_t> attr_res;
   OtlpLayout lay;   // res_scope0 / scope_span0 chunk-local
-  std::vector<std::vector<std::pair<std::string, std::string>>> sets;   // chunk-local first appearance
   std::string err;
-};
-struct CachedRes {
-  uint32_t svc, svc_str, set, rpart;
-  uint8_t ok;
-  uint64_t attr_res;
 };
 uint64_t sov64(uint64_t x) { uint64_t n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
 uint64_t flen(uint64_t l) { return 1 + sov64(l) + l; }
 
 // The TracesData records that start in [s, lim) (a record may run past lim:
 // *end is where the last one ends), each ResourceSpans walked in full.
-void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s, size_t lim, WalkChunk& c,
-                  size_t* end) {
-  std::unordered_map<std::string_view, CachedRes> rcache;
+void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, size_t s, size_t lim,
+                  WalkChunk& c, size_t* end) {
+  std::unordered_map<std::string_view, CachedRes> rcache;   // this call's, by view into the message
   std::unordered_map<std::string_view, uint32_t> scache;
-  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
   ProtoSizer sizer;
   std::vector<std::pair<size_t, size_t>> resf, scopes, deprecated, scf;
   const size_t est = (std::min(lim, n) - std::min(s, n)) / 128 + 16;   // spans of >= 128 bytes
@@ -250,9 +273,20 @@ void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s,
     const std::string_view key = resf.size() == 1 ? std::string_view((const char*)p + resf[0].first, resf[0].second)
                                                   : std::string_view();
     auto it = resf.size() <= 1 ? rcache.find(key) : rcache.end();
+    bool have = false;
     if (it != rcache.end()) {
       cr = it->second;
-    } else {
+      have = true;
+    } else if (resf.size() <= 1) {
+      std::shared_lock<std::shared_mutex> g(cache.mu);
+      auto ci = cache.map.find(key);
+      if (ci != cache.map.end()) {
+        cr = ci->second;
+        have = true;
+        rcache.emplace(key, cr);
+      }
+    }
+    if (!have) {
       AttrMap attrs;
       uint32_t dropped = 0;
       for (auto& x : resf)
@@ -262,13 +296,15 @@ void walk_segment(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, size_t s,
       cr.svc_str = rc.svc_str;
       cr.ok = rc.url_ok;
       cr.attr_res = rc.attr_res;
-      auto si = set_ids.find(rc.attrset);
-      if (si == set_ids.end()) {
-        si = set_ids.emplace(rc.attrset, (uint32_t)c.sets.size()).first;
-        c.sets.push_back(rc.attrset);
-      }
-      cr.set = si->second;
       cr.rpart = (uint32_t)flen(sizer.attrs(attrs, 1) + (dropped ? 1 + sov64(dropped) : 0));   // Resource: always emitted
+      {
+        std::unique_lock<std::shared_mutex> g(cache.mu);
+        cr.set = cache.intern(rc.attrset);
+        if (resf.size() <= 1 && cache.map.size() < ResCache::kMaxEntries && !cache.map.count(key)) {
+          cache.keys.emplace_back(key);
+          cache.map.emplace(std::string_view(cache.keys.back()), cr);
+        }
+      }
       if (resf.size() <= 1) rcache.emplace(key, cr);
     }
     const uint32_t rloc = (uint32_t)c.res_svc.size();
@@ -363,7 +399,7 @@ size_t find_start(const uint8_t* p, size_t n, size_t k) {
 // thread's; the split is exact iff every thread ends exactly where the next
 // one started (the chain from 0 is unique), else the walk runs again on one
 // thread.
-bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
+bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, Walked& w) {
   const size_t kSeg = size_t(256) << 10;
   int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)parallel_width(), n / kSeg}));
   if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));   // diagnostics
@@ -375,7 +411,7 @@ bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
     for (int t = 1; t < T; t++) st[t] = find_start(p, n, n * (size_t)t / (size_t)T);
     for (int t = T - 1; t >= 1; t--) st[t] = std::min(st[t], st[t + 1]);   // monotone
     ch.assign((size_t)T, WalkChunk());
-    parallel_run(T, [&](int t) { walk_segment(ctx, p, n, st[t], st[t + 1], ch[t], &en[t]); });
+    parallel_run(T, [&](int t) { walk_segment(ctx, cache, p, n, st[t], st[t + 1], ch[t], &en[t]); });
     bool exact = true;
     for (int t = 0; t < T; t++) {
       if (!ch[t].err.empty()) {
@@ -392,18 +428,15 @@ bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
     if (attempt) { w.err = "OTLP protobuf: malformed TracesData"; return false; }
   }
   // merge: global indices, attribute sets in first-appearance order
-  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> set_ids;
-  std::vector<std::vector<uint32_t>> set_map(ch.size());
+  std::unordered_map<uint32_t, uint32_t> set_map;   // cache id -> this batch's
+  {
+    std::shared_lock<std::shared_mutex> g(cache.mu);
+    for (auto& c : ch)
+      for (uint32_t id : c.res_set)
+        if (set_map.emplace(id, (uint32_t)w.sets.size()).second) w.sets.push_back(cache.sets[id]);
+  }
   size_t nspan = 0, nres = 0, nscope = 0;
   for (size_t t = 0; t < ch.size(); t++) {
-    for (auto& st : ch[t].sets) {
-      auto it = set_ids.find(st);
-      if (it == set_ids.end()) {
-        it = set_ids.emplace(st, (uint32_t)w.sets.size()).first;
-        w.sets.push_back(st);
-      }
-      set_map[t].push_back(it->second);
-    }
     nspan += ch[t].span_ref.size();
     nres += ch[t].res_svc.size();
     nscope += ch[t].scope_size.size();
@@ -441,7 +474,7 @@ bool walk(const ColumnizeCtx& ctx, const uint8_t* p, size_t n, Walked& w) {
     for (size_t k = 0; k < c.res_svc.size(); k++) {
       w.res_svc[ro[t] + k] = c.res_svc[k];
       w.res_svc_str[ro[t] + k] = c.res_svc_str[k];
-      w.res_attrset[ro[t] + k] = set_map[t][c.res_set[k]];
+      w.res_attrset[ro[t] + k] = set_map.at(c.res_set[k]);
       w.res_size[ro[t] + k] = c.res_size[k];
       w.res_ok[ro[t] + k] = c.res_ok[k];
       w.attr_res[ro[t] + k] = c.attr_res[k];
@@ -495,7 +528,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   }
   lap(0);
   Walked w;
-  if (!walk(o->ctx, pb, len, w)) return fail(OSE_EINVAL, w.err);
+  if (!walk(o->ctx, o->res_cache, pb, len, w)) return fail(OSE_EINVAL, w.err);
   lap(1);
   HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
   b->pb = pb;
@@ -764,7 +797,8 @@ char* osehost_otlp_walk(const char* cfg_json, const uint8_t* pb, size_t len) {
     if (err.empty()) err = ctx.build(ju ? &url : nullptr, js ? &sampling : nullptr, jt ? &traffic : nullptr);
     Walked w;
     const auto t0 = std::chrono::steady_clock::now();
-    if (err.empty() && !walk(ctx, pb, len, w)) err = w.err;
+    ResCache cache;
+    if (err.empty() && !walk(ctx, cache, pb, len, w)) err = w.err;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (!err.empty()) { fail(OSE_EINVAL, err); return nullptr; }
     if (cfg.get("timing_only")) {   // diagnostics: the walk's wall time only
@@ -947,7 +981,8 @@ int osehost_otlp_encode(const uint8_t* pb, size_t len, const uint8_t* keep, int 
   ColumnizeCtx ctx;
   std::string err = ctx.build(nullptr, nullptr, nullptr);
   Walked w;
-  if (err.empty() && !walk(ctx, pb, len, w)) err = w.err;
+  ResCache cache;
+  if (err.empty() && !walk(ctx, cache, pb, len, w)) err = w.err;
   if (!err.empty()) return fail(OSE_EINVAL, err);
   std::vector<uint32_t> sizes(w.span_ref.size());
   ProtoSizer sizer;

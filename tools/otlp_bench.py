@@ -79,7 +79,7 @@ def main():
         c = time.perf_counter()
         if stages:
             out = ob.encode(st, native.GROUP_TRACE_ID, router, stream=sh, copy=False)
-            enc.append((time.perf_counter() - c, out))
+            enc.append((time.perf_counter() - c, out, ob.encode_ms))
         info = (ob.cols.n_spans, ob.host_spans, int(ob.out_numpy("device_status", n=1)[0]) if stages else 0)
         ob.close()
         return b - a, c - b, info
@@ -113,6 +113,7 @@ def main():
     res["span_kernel_ms"] = k_ms
     e_best = min(enc[2:], key=lambda x: x[0])
     res["encode_ms"] = e_best[0] * 1e3
+    res["encode_phases_ms"] = dict(zip(("decisions_d2h", "sizing", "buffers", "writing"), e_best[2]))
     res["encode_outputs"] = [{"pipeline": p, "bytes": nb, "resources": nr} for p, nb, nr in e_best[1]]
     out_bytes = sum(x["bytes"] for x in res["encode_outputs"])
     res["encode_out_GBps"] = out_bytes / e_best[0] / 1e9
@@ -130,20 +131,27 @@ def main():
     sdims = native.Columns()
     sdims.n_spans, sdims.n_resources, sdims.n_attrsets = 8192, 8192, 4096
     souts = device_outputs(sdims, tmpl_cap=64 * 8192)
-    lat, sph = [], []
+    lat, sph, leg = [], [], []
     for k in range(220):
         a = time.perf_counter()
         ob = OtlpBatch(eng, spin.p, stream=sh, length=spin.n, outputs=souts)
         sph.append(ob.timings_ms)
+        b = time.perf_counter()
         eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
         torch.cuda.synchronize()
+        c = time.perf_counter()
         ob.encode(st, native.GROUP_TRACE_ID, router, stream=sh, copy=False)
+        d = time.perf_counter()
+        sph[-1].update({"enc_" + x: v for x, v in zip(("d2h", "sizing", "buffers", "writing"), ob.encode_ms)})
         ob.close()
         if k >= 20:
             lat.append(time.perf_counter() - a)
+            leg.append(((b - a) * 1e3, (c - b) * 1e3, (d - c) * 1e3))
     lat.sort()
     res["batch8192_decode_stages_encode_us"] = {"p50": lat[len(lat) // 2] * 1e6, "p99": lat[int(len(lat) * 0.99)] * 1e6}
     res["batch8192_spans_per_s"] = 8192 / lat[len(lat) // 2]
+    res["batch8192_legs_ms_median"] = {k: sorted(x[j] for x in leg)[len(leg) // 2]
+                                       for j, k in enumerate(("decode", "stages", "encode"))}
     res["batch8192_decode_phases_ms_median"] = {k: sorted(x[k] for x in sph[20:])[len(sph[20:]) // 2] for k in sph[0]}
     spin.close()
     pin.close()
