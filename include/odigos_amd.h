@@ -462,6 +462,41 @@ int ose_otlp_out_get(const ose_otlp_out* o, uint32_t k, const char** name, const
                      uint32_t* n_resources);   /* pointers valid until release */
 void ose_otlp_out_release(ose_otlp_out* o);
 
+/* ---- groupbytrace, resident in HBM ----------------------
+ * Replaces the groupbytrace processor the gateway runs before odigossampling
+ * (opentelemetry-collector-contrib groupbytraceprocessor v0.141.0,
+ * `collector/builder-config.yaml:73`; configured by
+ * `autoscaler/controllers/actions/sampling/groupbytrace.go:3-9` and
+ * `sampling_controller.go:193-220`).  cfg_json: {"wait_duration": "30s",
+ * "num_traces": 1000000, "num_workers": 1} (the processor's keys; Go
+ * durations).  Spans wait on the GPU (span_capacity spans, arena_capacity
+ * bytes of their route / path / attribute strings) until wait_duration after
+ * their trace's first span; ose_gbt_release then returns every trace whose
+ * time has come as one device batch: each trace contiguous, its pieces (one
+ * per ResourceSpans x ScopeSpans it arrived in) in arrival order as
+ * resources with one scope each, traces in creation order.  Run the
+ * processors on it with OSE_GROUP_TRACE_ID: each trace is decided as
+ * groupbytrace's one-trace ConsumeTraces call would be.  A new trace evicts
+ * (drops) the one created num_traces creations earlier if it is still
+ * waiting.  now_ns is the caller's clock and must not go backwards.
+ * attrset_map (n_attrsets of the added batch, may be NULL = identity) maps
+ * the batch's res_attrset ids to ids stable across batches.  The released
+ * columns stay valid until the next release; OSE_ERANGE when the store is
+ * full (more spans than the capacity within one wait_duration).            */
+typedef struct ose_gbt ose_gbt;
+int ose_gbt_create(ose_engine* eng, const char* cfg_json, uint64_t span_capacity, uint64_t arena_capacity,
+                   ose_gbt** out);
+void ose_gbt_destroy(ose_gbt* g);
+int ose_gbt_add(ose_gbt* g, const ose_columns* cols_dev, const uint32_t* attrset_map, int64_t now_ns,
+                void* hip_stream);
+int ose_gbt_release(ose_gbt* g, int64_t now_ns, void* hip_stream, const ose_columns** out_dev,
+                    uint32_t* n_traces);
+/* traces waiting, spans held, traces created / released / evicted, spans
+ * released / added, string bytes held */
+int ose_gbt_stats(const ose_gbt* g, uint64_t* out8);
+/* copies every column of the last release whose dst pointer is non-NULL */
+int ose_gbt_download(const ose_gbt* g, const ose_columns* dst);
+
 /* Message of the last failure on this thread ("" if none). */
 const char* ose_last_error(void);
 

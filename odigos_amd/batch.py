@@ -316,6 +316,82 @@ class Router:
     __del__ = close
 
 
+class GroupByTrace:
+    """The GPU-resident groupbytrace store (ose_gbt_*): add device batches
+    with the caller's clock, release the traces whose wait is over as one
+    device batch (DeviceView) for Engine.process_device."""
+
+    STATS = ("waiting_traces", "held_spans", "created", "released", "evicted", "released_spans", "added_spans",
+             "held_bytes")
+
+    def __init__(self, engine: "Engine", cfg: dict, span_capacity: int, arena_capacity: int):
+        import json
+        self.L = engine.L
+        self.eng = engine
+        h = C.c_void_p()
+        native.check(self.L.ose_gbt_create(engine.h, json.dumps(cfg).encode(), span_capacity, arena_capacity,
+                                           C.byref(h)))
+        self.h = h
+
+    def add(self, cols: native.Columns, now_ns: int, attrset_map=None, stream=None):
+        m = None
+        if attrset_map is not None:
+            m = np.ascontiguousarray(attrset_map, dtype=np.uint32)
+        s = None if stream is None else C.c_void_p(stream)
+        native.check(self.L.ose_gbt_add(self.h, C.byref(cols), None if m is None else m.ctypes.data, now_ns, s))
+
+    def release(self, now_ns: int, stream=None):
+        """(columns of the released batch (device pointers), traces released)"""
+        out = C.POINTER(native.Columns)()
+        nt = C.c_uint32()
+        s = None if stream is None else C.c_void_p(stream)
+        native.check(self.L.ose_gbt_release(self.h, now_ns, s, C.byref(out), C.byref(nt)))
+        return native.Columns.from_buffer_copy(out.contents), nt.value
+
+    def stats(self) -> dict:
+        v = (C.c_uint64 * 8)()
+        native.check(self.L.ose_gbt_stats(self.h, v))
+        return dict(zip(self.STATS, list(v)))
+
+    def download(self, cols: native.Columns) -> dict:
+        """Host copies (numpy) of the last release's columns."""
+        dst = native.Columns()
+        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys"):
+            setattr(dst, f, getattr(cols, f))
+        out = {}
+        for name, (dim, size) in COLUMN_LAYOUT.items():
+            if not getattr(cols, name):
+                continue
+            nb = _count(cols, dim) * size
+            a = np.zeros(max(nb, 1) + 16, dtype=np.uint8)
+            out[name] = a
+            setattr(dst, name, a.ctypes.data)
+        native.check(self.L.ose_gbt_download(self.h, C.byref(dst)))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ose_gbt_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+
+class DeviceView:
+    """Device columns owned elsewhere (an OTLP batch, a groupbytrace release)
+    plus HBM outputs: what Engine.process_device takes."""
+
+    def __init__(self, cols: native.Columns, tmpl_cap: int | None = None):
+        self.cols = cols
+        self.outs, self.o = device_outputs(cols, tmpl_cap=tmpl_cap)
+
+    def out_numpy(self, name: str, dtype=np.uint8, n: int | None = None) -> np.ndarray:
+        t = self.o[name]
+        if n is not None:
+            t = t[: n * np.dtype(dtype).itemsize]
+        return t.cpu().numpy().view(dtype)
+
+
 class OtlpBatch:
     """A serialized TracesData decoded on the GPU (ose_otlp_decode): device
     columns owned by the engine plus HBM outputs, usable wherever a

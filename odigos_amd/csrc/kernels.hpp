@@ -369,4 +369,77 @@ struct OtlpFixArgs {
 void launch_otlp_spans(const OtlpArgs& a, hipStream_t st);
 void launch_otlp_fix(const OtlpFixArgs& a, hipStream_t st);
 
+// ---- groupbytrace store (gbt_kernel.hip) --------------------------------------
+struct GbtSlot {              // trace id -> creation number (32 B, generation-tagged)
+  uint32_t state;             // epoch << 2 | {0 empty, 1 busy, 2 ready}
+  uint32_t first;             // smallest batch position carrying the id (new ids)
+  uint64_t hi, lo;
+  uint64_t seq;               // creation number; ~0 while a new id is being numbered
+};
+struct GbtPool {              // spans waiting for release (ring of pool_cap)
+  uint64_t* tid;              // {hi, lo}
+  uint64_t *start, *end, *attr_match, *seq, *origin, *str_off;
+  uint8_t *status, *kind, *url_flags;
+  uint32_t *span_size, *name_len;
+  ose_strref *route, *path;   // relative to the span's string block
+  uint8_t* attr_type;         // key-major, [key * pool_cap + p]
+  uint64_t* attr_val;
+};
+struct GbtScopes {            // the fragment columns of each added scope (ring)
+  uint32_t *res_svc, *res_svc_str, *res_attrset, *res_size, *scope_size;
+  uint8_t* res_url_ok;
+};
+struct GbtOut {               // the released batch
+  uint64_t* tid;
+  uint64_t *start, *end, *attr_match;
+  uint8_t *status, *kind, *url_flags;
+  uint32_t *span_size, *name_len, *resource, *scope;
+  ose_strref *route, *path;
+  uint8_t* attr_type;
+  uint64_t* attr_val;
+  uint32_t *res_svc, *res_svc_str, *res_attrset, *res_size, *scope_size, *scope_resource;
+  uint8_t* res_url_ok;
+  uint8_t* arena;
+};
+struct GbtArgs {
+  GbtSlot* table;
+  uint64_t table_mask;
+  uint32_t epoch;
+  uint32_t n_attr_keys;
+  uint32_t* error;
+  uint64_t* ring_tid;         // [2 * num_traces]
+  uint64_t num_traces;
+  uint64_t live_lo, live_hi;  // rebuild range
+  // add: the batch
+  ose_columns cols;
+  uint64_t n, n_scopes;
+  uint64_t next_seq;
+  uint64_t* slot_of;
+  uint32_t *flag, *rank, *strlen, *stroff;
+  const uint32_t* attrset_map;
+  // the rings
+  GbtPool pool;
+  uint64_t pool_pos, pool_cap;
+  GbtScopes scopes;
+  uint64_t scope_pos, scope_cap;
+  uint8_t* arena_ring;
+  uint64_t arena_pos, arena_cap;
+  // release
+  uint64_t rel_lo, rel_hi;
+  uint32_t *keys, *vals;
+  const uint32_t* order;
+  GbtOut out;
+};
+void launch_gbt_rebuild(const GbtArgs& a, hipStream_t st);
+void launch_gbt_lookup(const GbtArgs& a, hipStream_t st);
+void launch_gbt_creator(const GbtArgs& a, hipStream_t st);
+void launch_gbt_assign(const GbtArgs& a, hipStream_t st);
+void launch_gbt_append(const GbtArgs& a, hipStream_t st);
+void launch_gbt_strings(const GbtArgs& a, hipStream_t st);
+void launch_gbt_scopes(const GbtArgs& a, hipStream_t st);
+void launch_gbt_flag(const GbtArgs& a, hipStream_t st);
+void launch_gbt_compact(const GbtArgs& a, hipStream_t st);
+void launch_gbt_gather(const GbtArgs& a, hipStream_t st);
+void launch_gbt_emit(const GbtArgs& a, hipStream_t st);
+
 }  // namespace ose

@@ -137,6 +137,12 @@ def lib() -> C.CDLL:
         "ose_otlp_out_get": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(_p),
                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
         "ose_otlp_out_release": (None, [_p]),
+        "ose_gbt_create": (C.c_int, [_p, C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(_p)]),
+        "ose_gbt_destroy": (None, [_p]),
+        "ose_gbt_add": (C.c_int, [_p, C.POINTER(Columns), _p, C.c_int64, _p]),
+        "ose_gbt_release": (C.c_int, [_p, C.c_int64, _p, C.POINTER(C.POINTER(Columns)), C.POINTER(C.c_uint32)]),
+        "ose_gbt_stats": (C.c_int, [_p, C.POINTER(C.c_uint64)]),
+        "ose_gbt_download": (C.c_int, [_p, C.POINTER(Columns)]),
         "ose_engine_attr_key": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),
         "ose_batch_columns": (C.POINTER(Columns), [_p]),
@@ -181,6 +187,7 @@ def lib() -> C.CDLL:
         "osehost_router_create_signal": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(_p)]),
         "osehost_router_route": (_p, [_p, C.c_char_p]),
         "osehost_otlp_out_timings": (C.c_int, [_p, C.POINTER(C.c_double)]),
+        "osehost_parse_duration": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
         "osehost_resource_sizes": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
         "osehost_as_string": (_p, [C.c_char_p]),
         "osehost_free": (None, [_p]),

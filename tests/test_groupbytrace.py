@@ -1,0 +1,234 @@
+"""GPU-resident groupbytrace (odigos_amd/csrc/gbt_{host.cpp,
+kernel.hip}, ose_gbt_*) against tests/gbt_ref.py, an independent Python
+restatement of contrib's groupbytraceprocessor v0.141.0 (parity unpinned:
+the processor is not in the reference tree).
+
+CPU: the restatement's own behaviour on hand-built sequences (split per
+resource x scope x trace, append, expiry, eviction, recreation after
+release) and Go's time.ParseDuration as the store reads wait_duration.
+GPU: batches decoded from OTLP protobuf are added with a clock; every
+release equals, column by column, the host columniser over the traces the
+restatement releases at that time (their pieces in arrival order); the
+stages on a release equal the oracle; eviction under a small num_traces;
+capacity errors.
+"""
+import ctypes as C
+import random
+
+import numpy as np
+import pytest
+
+from odigos_amd import host, native
+from tests.gbt_ref import GroupByTraceRef, split_traces
+from tests.test_otlp import CFG, SEED, _arr, _http_traces, _strings, to_pb
+
+S = 1_000_000_000   # ns
+
+
+def _tid(k):
+    return "%032x" % (k + 1)
+
+
+def _piece_spans(p):
+    return [sp["name"] for sp in p["scopeSpans"][0]["spans"]]
+
+
+# ---- CPU: the restatement -------------------------------------------------------------
+
+def test_ref_split_per_resource_scope_trace():
+    a, b = _tid(1), _tid(2)
+    rs1 = host.resource_spans({"service.name": "x"}, scopes=[
+        {"scope": {"name": "s1"}, "spans": [host.span("a1", trace_id=a), host.span("b1", trace_id=b),
+                                           host.span("a2", trace_id=a)]},
+        {"scope": {"name": "s2"}, "spans": [host.span("b2", trace_id=b)]}])
+    rs2 = host.resource_spans({"service.name": "y"}, [host.span("a3", trace_id=a)])
+    pieces = split_traces(host.traces(rs1, rs2))
+    assert [(t, _piece_spans(p)) for t, p in pieces] == [(a, ["a1", "a2"]), (b, ["b1"]), (b, ["b2"]), (a, ["a3"])]
+    assert pieces[2][1]["scopeSpans"][0]["scope"] == {"name": "s2"}
+
+
+def test_ref_expiry_append_recreate_evict():
+    g = GroupByTraceRef(30 * S, num_traces=2)
+    t = lambda *ks: host.traces(host.resource_spans({}, [host.span(f"s{k}", trace_id=_tid(k)) for k in ks]))  # noqa
+    g.consume(t(1, 2), 0)
+    g.consume(t(1), 10 * S)                       # appended, no new timer
+    assert g.release(29 * S) == []
+    out = g.release(30 * S)
+    assert [[_piece_spans(p) for p in tr] for tr in out] == [[["s1"], ["s1"]], [["s2"]]]
+    g.consume(t(1), 31 * S)                       # released: a new trace
+    g.consume(t(3, 4), 32 * S)                    # ring of 2: trace 3 evicts nothing (slot freed), 4 evicts 1
+    assert g.evicted == 1
+    out = g.release(100 * S)
+    assert [[_piece_spans(p) for p in tr] for tr in out] == [[["s3"]], [["s4"]]]
+
+
+@pytest.mark.parametrize("text,ns", [("30s", 30 * S), ("1m30s", 90 * S), ("1.5h", 5400 * S), ("500ms", 500_000_000),
+                                     ("0", 0), ("2us", 2000), ("-1s", -S), ("1h2m3.5s", 3723_500_000_000)])
+def test_parse_duration(text, ns):
+    v = C.c_int64()
+    native.check(native.lib().osehost_parse_duration(text.encode(), C.byref(v)))
+    assert v.value == ns
+
+
+@pytest.mark.parametrize("text", ["", "30", "1x", "s", ".s", "1.5"])
+def test_parse_duration_rejects(text):
+    v = C.c_int64()
+    assert native.lib().osehost_parse_duration(text.encode(), C.byref(v)) == native.OSE_EINVAL
+
+
+# ---- GPU ----------------------------------------------------------------------------
+
+def _expected_columns(traces):
+    td = host.traces(*[p for tr in traces for p in tr])
+    proc = host.Processor("pipeline", CFG)
+    return td, proc, proc.columnarize(td)
+
+
+def _compare_release(got, cols, hb, set_names):
+    """Released columns == the host columniser's on the same traces; attribute
+    sets compared by content (the store's ids are the shim's global ids)."""
+    c = hb.cols
+    n, R = c.n_spans, c.n_resources
+    assert (cols.n_spans, cols.n_resources, cols.n_scopes) == (n, R, c.n_scopes)
+    want = {"trace_id": (2 * n, np.uint64), "start_ns": (n, np.uint64), "end_ns": (n, np.uint64),
+            "status": (n, np.uint8), "kind": (n, np.uint8), "resource": (n, np.uint32), "scope": (n, np.uint32),
+            "url_flags": (n, np.uint8), "span_size": (n, np.uint32), "name_len": (n, np.uint32),
+            "res_svc": (R, np.uint32), "res_svc_str": (R, np.uint32), "res_size": (R, np.uint32),
+            "scope_size": (R, np.uint32), "scope_resource": (R, np.uint32)}
+    for name, (cnt, dt) in want.items():
+        np.testing.assert_array_equal(got[name].view(dt)[:cnt], _arr(getattr(c, name), cnt, dt), err_msg=name)
+    harena = _arr(c.arena, c.arena_bytes, np.uint8)
+    for name in ("route", "path"):
+        g = got[name].view(np.uint32).reshape(-1, 2)[:n]
+        h = _arr(getattr(c, name), 2 * n, np.uint32).reshape(-1, 2)
+        if name == "path":
+            m = (_arr(c.url_flags, n, np.uint8) & native.URL_PATH_MASK) != 0
+            g, h = g[m], h[m]
+        assert _strings(got["arena"], g) == _strings(harena, h), name
+    K = c.n_attr_keys
+    if K:
+        gt = got["attr_type"][:K * n]
+        np.testing.assert_array_equal(gt, _arr(c.attr_type, K * n, np.uint8))
+        gv = got["attr_val"].view(np.uint64)[:K * n]
+        hv = _arr(c.attr_val, K * n, np.uint64)
+        s = gt == native.ATTR_STR
+        np.testing.assert_array_equal(gv[~s], hv[~s])
+        g2 = np.stack([gv[s] & 0xFFFFFFFF, gv[s] >> 32], 1)
+        h2 = np.stack([hv[s] & 0xFFFFFFFF, hv[s] >> 32], 1)
+        assert _strings(got["arena"], g2) == _strings(harena, h2)
+    return got["res_attrset"].view(np.uint32)[:R], _arr(c.res_attrset, R, np.uint32)
+
+
+def _set_of(rs) -> tuple:
+    """attributeSetFromResource (odigostrafficmetrics/processor.go:60-69): Str() of the configured keys."""
+    d = {}
+    for k in CFG["odigostrafficmetrics"]["res_attributes_keys"]:
+        v = host.find_attr(rs.get("resource") or {}, k)
+        if v is not None:
+            d[k] = v.get("stringValue", "") if isinstance(v, dict) else ""
+    return tuple(sorted(d.items()))
+
+
+class _Shim:
+    """What a shim does around the store: decode, intern attribute sets, add."""
+
+    def __init__(self, eng, cfg, span_capacity=1 << 16, arena_capacity=1 << 22):
+        from odigos_amd.batch import GroupByTrace
+        self.eng = eng
+        self.g = GroupByTrace(eng, cfg, span_capacity, arena_capacity)
+        self.sets = {}      # frozen attribute set -> global id
+        self.names = []
+
+    def add(self, td, now):
+        from odigos_amd.batch import OtlpBatch
+        ob = OtlpBatch(self.eng, to_pb(td))
+        ids = []
+        for k in range(ob.cols.n_attrsets):
+            key = tuple(sorted(ob.attrset(k).items()))
+            if key not in self.sets:
+                self.sets[key] = len(self.names)
+                self.names.append(key)
+            ids.append(self.sets[key])
+        self.g.add(ob.cols, now, ids)
+        ob.close()
+
+
+@pytest.mark.gpu
+def test_gpu_releases_match_restatement():
+    from odigos_amd.batch import DeviceView, Engine
+    import torch
+    rng = random.Random(0x6B7)
+    eng = Engine(CFG)
+    shim = _Shim(eng, {"wait_duration": "30s"})
+    ref = GroupByTraceRef(30 * S)
+    # traces arrive in several batches (a trace's spans spread over calls)
+    pool = _http_traces(rng, 120, odd=0.05)["resourceSpans"]
+    rng.shuffle(pool)
+    batches = [pool[k:k + 25] for k in range(0, len(pool), 25)]
+    now = 0
+    released_total = 0
+    for step, rss in enumerate(batches + [[]] * 4):
+        now += rng.choice([3, 7, 11, 20]) * S
+        if rss:
+            td = host.traces(*rss)
+            shim.add(td, now)
+            ref.consume(td, now)
+        cols, ntr = shim.g.release(now)
+        want = ref.release(now)
+        assert ntr == len(want), step
+        if not want:
+            assert cols.n_spans == 0
+            continue
+        released_total += len(want)
+        td_w, proc, hb = _expected_columns(want)
+        got = shim.g.download(cols)
+        g_sets, h_sets = _compare_release(got, cols, hb, shim.names)
+        assert [shim.names[x] for x in g_sets] == [_set_of(rs) for rs in td_w["resourceSpans"]]
+        # the stages on the release: each trace decided as its own call
+        dv = DeviceView(cols)
+        st = native.STAGE_SAMPLE | native.STAGE_TEMPLATE
+        eng.process_device(dv, st, native.GROUP_TRACE_ID, seed=SEED)
+        torch.cuda.synchronize()
+        from odigos_amd.batch import HostOutputs
+        from tests.oracle_lib import SamplingOracle, UrlOracle
+        ho = HostOutputs(hb.cols)
+        assert SamplingOracle(CFG["odigossampling"]).process(hb.cols, ho.outs, native.GROUP_TRACE_ID, SEED, 4) == 0
+        assert UrlOracle(CFG["odigosurltemplate"]).process(hb.cols, ho.outs, 4) == 0
+        n = hb.cols.n_spans
+        np.testing.assert_array_equal(dv.out_numpy("keep", n=n), ho.view("keep", np.uint8)[:n])
+        np.testing.assert_array_equal(dv.out_numpy("url_out", n=n), ho.view("url_out", np.uint8)[:n])
+    st = shim.g.stats()
+    assert released_total == st["released"] > 0 and st["waiting_traces"] == 0 and st["evicted"] == 0
+    assert st["held_spans"] == 0 and st["held_bytes"] == 0   # every epoch reclaimed
+
+
+@pytest.mark.gpu
+def test_gpu_eviction_and_capacity():
+    from odigos_amd.batch import Engine
+    eng = Engine(CFG)
+    shim = _Shim(eng, {"wait_duration": "10s", "num_traces": 4}, span_capacity=2048, arena_capacity=1 << 16)
+    ref = GroupByTraceRef(10 * S, num_traces=4)
+    mk = lambda ks, tag: host.traces(host.resource_spans(  # noqa: E731
+        {"service.name": "svc-a"}, [host.span(f"{tag}{k}", kind=2, trace_id=_tid(k), attributes={"url.path": f"/u/{k}"})
+                                    for k in ks]))
+    # 5 evicts 1; then 6 evicts 2 and the returning 1 is a new trace evicting 3
+    # (an id evicted by a creation in the same batch is not covered: the store
+    # applies eviction per batch)
+    for now, ks in ((0, [1, 2, 3]), (1 * S, [4, 5]), (2 * S, [6, 1])):
+        td = mk(ks, "t%d-" % now)
+        shim.add(td, now)
+        ref.consume(td, now)
+    cols, ntr = shim.g.release(20 * S)
+    want = ref.release(20 * S)
+    assert ntr == len(want) == 4 and ref.evicted == shim.g.stats()["evicted"] == 3
+    td_w, proc, hb = _expected_columns(want)
+    _compare_release(shim.g.download(cols), cols, hb, shim.names)
+    # more spans than the store holds within one wait: OSE_ERANGE, state unchanged
+    big = host.traces(host.resource_spans({"service.name": "svc-a"},
+                                          [host.span("x", trace_id=_tid(100 + k)) for k in range(3000)]))
+    with pytest.raises(native.OseError) as ei:
+        shim.add(big, 30 * S)
+    assert ei.value.code == native.OSE_ERANGE
+    # time must not go backwards
+    with pytest.raises(native.OseError):
+        shim.add(mk([9], "z"), 25 * S)
