@@ -187,6 +187,13 @@ class Engine:
         h = C.c_void_p()
         native.check(self.L.ose_engine_create(dumps(cfg).encode(), C.byref(h)))
         self.h = h
+        # objects that must be released before the engine (the ABI's rule):
+        # a garbage cycle may finalize the engine first, so it closes them
+        import weakref
+        self._children = weakref.WeakSet()
+
+    def adopt(self, obj):
+        self._children.add(obj)
 
     def info(self) -> native.EngineInfo:
         i = native.EngineInfo()
@@ -218,6 +225,8 @@ class Engine:
 
     def close(self):
         if getattr(self, "h", None):
+            for c in list(getattr(self, "_children", ())):
+                c.close()
             self.L.ose_engine_destroy(self.h)
             self.h = None
 
@@ -235,6 +244,7 @@ class PinnedBatch:
         h = C.c_void_p()
         native.check(self.L.ose_batch_acquire(engine.h, C.byref(dims), C.byref(h)))
         self.h = h
+        engine.adopt(self)
         self.cols = self.L.ose_batch_columns(h).contents
         self.outs = self.L.ose_batch_outputs(h).contents
 
@@ -332,6 +342,7 @@ class GroupByTrace:
         native.check(self.L.ose_gbt_create(engine.h, json.dumps(cfg).encode(), span_capacity, arena_capacity,
                                            C.byref(h)))
         self.h = h
+        engine.adopt(self)
 
     def add(self, cols: native.Columns, now_ns: int, attrset_map=None, stream=None):
         m = None
@@ -413,6 +424,7 @@ class OtlpBatch:
             addr, n = C.c_void_p(int(pb)), int(length)
         native.check(self.L.ose_otlp_decode(engine.h, addr, n, s, C.byref(h)))
         self.h = h
+        engine.adopt(self)
         self.cols = native.Columns.from_buffer_copy(self.L.ose_otlp_columns(h).contents)
         self.host_spans = int(self.L.ose_otlp_host_spans(h))
         t = (C.c_double * 5)()

@@ -16,6 +16,7 @@
 // Time is the caller's clock (now_ns on every call), so releases are
 // deterministic.  The kernels are in gbt_kernel.hip.
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <deque>
@@ -115,6 +116,7 @@ struct Gbt {
   struct Epoch { int64_t t; uint64_t seq1, pool1, scope1, arena1; };
   std::deque<Epoch> epochs;
   uint32_t n_attrsets = 0;
+  int64_t last_now = INT64_MIN;   // the clock of the last successful call
   // the last release
   ose_columns out_cols{};
   // stats: created, released traces, evicted traces, released spans, added spans
@@ -171,7 +173,7 @@ GbtArgs base_args(Gbt* g) {
 }
 
 int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t now, hipStream_t st) {
-  if (!g->epochs.empty() && now < g->epochs.back().t) return fail(OSE_EINVAL, "groupbytrace: now_ns went backwards");
+  if (now < g->last_now) return fail(OSE_EINVAL, "groupbytrace: now_ns went backwards");
   const uint64_t n = c->n_spans, S = c->n_scopes;
   if (!n) return 0;
   if (g->K && c->n_attr_keys != g->K) return fail(OSE_EINVAL, "groupbytrace: the batch's attribute key columns differ from the engine's");
@@ -246,10 +248,13 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
   g->arena_end += bytes;
   g->n_attrsets = std::max<uint32_t>(g->n_attrsets, A ? max_set + 1 : 0);
   g->epochs.push_back(Gbt::Epoch{now, g->next_seq, g->pool_end, g->scope_end, g->arena_end});
+  g->last_now = now;
   return 0;
 }
 
 int gbt_release(Gbt* g, int64_t now, hipStream_t st, uint32_t* n_traces) {
+  if (now < g->last_now) return fail(OSE_EINVAL, "groupbytrace: now_ns went backwards");
+  g->last_now = now;
   ose_columns& oc = g->out_cols;
   oc = ose_columns{};
   *n_traces = 0;

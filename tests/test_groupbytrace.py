@@ -229,6 +229,8 @@ def test_gpu_eviction_and_capacity():
     with pytest.raises(native.OseError) as ei:
         shim.add(big, 30 * S)
     assert ei.value.code == native.OSE_ERANGE
-    # time must not go backwards
+    # time must not go backwards (the last successful call was the release at 20 s)
     with pytest.raises(native.OseError):
-        shim.add(mk([9], "z"), 25 * S)
+        shim.add(mk([9], "z"), 15 * S)
+    shim.add(mk([9], "z"), 25 * S)
+    assert shim.g.stats()["waiting_traces"] == 1
