@@ -178,6 +178,17 @@ class DeviceBatch:
         return int(self.o["used"][0].item())
 
 
+_ENGINES = None
+
+
+def _close_engines():
+    """atexit: engines (and the batches / stores they own) are released while
+    the HIP runtime is still up, not by finalizers during interpreter
+    teardown."""
+    for e in list(_ENGINES or ()):
+        e.close()
+
+
 class Engine:
     """ose_engine handle (product path: raises if the HIP library cannot run)."""
 
@@ -191,6 +202,12 @@ class Engine:
         # a garbage cycle may finalize the engine first, so it closes them
         import weakref
         self._children = weakref.WeakSet()
+        global _ENGINES
+        if _ENGINES is None:
+            import atexit
+            _ENGINES = weakref.WeakSet()
+            atexit.register(_close_engines)
+        _ENGINES.add(self)
 
     def adopt(self, obj):
         self._children.add(obj)

@@ -522,6 +522,7 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
 void ose_engine_destroy(ose_engine* eng) {
   if (!eng) return;
   (void)bind_device(reinterpret_cast<Engine*>(eng));
+  (void)hipDeviceSynchronize();   // nothing in flight may still use the buffers freed below
   delete reinterpret_cast<Engine*>(eng);
 }
 

@@ -338,6 +338,32 @@ struct OtlpArgs {
   uint32_t* host_list;
   uint32_t host_cap;
 };
+// ScopeSpans walked on the GPU (the host walks TracesData and ResourceSpans
+// only): pass 1 counts each scope's spans and reads its InstrumentationScope
+// and schema_url; pass 2 (after a scan of the counts) writes the span refs.
+constexpr uint64_t kOtlpScopeMulti = ~0ull;
+struct OtlpScopeArgs {
+  const uint8_t* pb;
+  uint64_t n_scopes;
+  const uint64_t* scope_ref;    // ScopeSpans payload off | len << 32
+  const uint8_t* on_host;       // 1: the host walked this scope (counts / sizes / layout preset)
+  const uint32_t* scope_res;
+  uint32_t* count;              // spans per scope
+  uint32_t* scope_size;         // pdata's fixed ScopeSpans size (scope + schema_url)
+  uint64_t* hdr;                // the InstrumentationScope message ref, 0 none, kOtlpScopeMulti several
+  uint64_t* schema;             // schema_url ref (last occurrence; length 0: none)
+  uint32_t* flags;              // 1: size left to the host (merged / unusual scope message), 2: malformed
+  const uint32_t* span0;        // pass 2: exclusive scan of count
+  uint64_t* span_ref;
+  uint32_t* span_res;
+  uint32_t* span_scope;
+  // pass 2 for the host-walked scopes: their refs, listed in scope order
+  const uint64_t* host_refs;
+  const uint64_t* host_at;      // [n_scopes] offset into host_refs (host-walked scopes)
+};
+void launch_otlp_scope_count(const OtlpScopeArgs& a, hipStream_t st);
+void launch_otlp_scope_spans(const OtlpScopeArgs& a, hipStream_t st);
+
 struct OtlpFix {
   uint64_t idx;
   uint64_t hi, lo, start, end, attr_match;

@@ -113,8 +113,18 @@ struct OtlpBatchImpl {
   size_t pb_len = 0;
   std::vector<uint64_t> span_ref;
   OtlpLayout lay;
+  // with the scopes walked on the GPU, span_ref and the scopes' span0 / hdr
+  // / schema are on the device until ose_otlp_encode (or the host pass)
+  // brings them back
+  bool layout_on_host = true;
+  DevBuf sslab;   // scope-level device arrays
+  uint64_t* d_span_ref = nullptr;
+  uint32_t *d_span_res = nullptr, *d_span0 = nullptr;
+  uint64_t *d_hdr = nullptr, *d_schema = nullptr;
+  OtlpScopeArgs sargs{};   // the GPU scope walk's arrays (pass 2 reuses them)
   OtlpBatchImpl() { stage.host = true; }
 };
+
 
 namespace {
 std::mutex g_otlp_mu;
@@ -194,7 +204,9 @@ void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n) {
 // messages repeat across a batch (one SDK, one pod), so their columns are
 // cached by message bytes.
 struct Walked {
-  std::vector<uint64_t> span_ref;
+  std::vector<uint64_t> span_ref;   // with gpu_scopes: the host-walked scopes' spans only
+  std::vector<uint8_t> scope_on_host;
+  std::vector<uint32_t> scope_count;
   std::vector<uint32_t> span_res, span_scope;
   std::vector<uint32_t> res_svc, res_svc_str, res_attrset, res_size, scope_size, scope_res;
   std::vector<uint8_t> res_ok;
@@ -210,20 +222,27 @@ struct WalkChunk {
   std::vector<uint8_t> res_ok;
   std::vector<uint64_t> attr_res;
   OtlpLayout lay;   // res_scope0 / scope_span0 chunk-local
+  // GPU-walked scopes (walk with gpu_scopes): span_ref lists only the spans
+  // of the scopes the host walked
+  std::vector<uint8_t> scope_on_host;
+  std::vector<uint32_t> scope_count;
   std::string err;
 };
+// ScopeSpans payloads up to this size are walked on the GPU (a lane per
+// scope follows its chain of span lengths); larger ones on the host
+constexpr size_t kGpuScopeBytes = size_t(64) << 10;
 uint64_t sov64(uint64_t x) { uint64_t n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
 uint64_t flen(uint64_t l) { return 1 + sov64(l) + l; }
 
 // The TracesData records that start in [s, lim) (a record may run past lim:
 // *end is where the last one ends), each ResourceSpans walked in full.
 void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, size_t s, size_t lim,
-                  WalkChunk& c, size_t* end) {
+                  WalkChunk& c, size_t* end, bool gpu_scopes) {
   std::unordered_map<std::string_view, CachedRes> rcache;   // this call's, by view into the message
   std::unordered_map<std::string_view, uint32_t> scache;
   ProtoSizer sizer;
   std::vector<std::pair<size_t, size_t>> resf, scopes, deprecated, scf;
-  const size_t est = (std::min(lim, n) - std::min(s, n)) / 128 + 16;   // spans of >= 128 bytes
+  const size_t est = gpu_scopes ? 16 : (std::min(lim, n) - std::min(s, n)) / 128 + 16;   // spans of >= 128 bytes
   c.span_ref.reserve(est);
   c.span_res.reserve(est);
   c.span_scope.reserve(est);
@@ -235,6 +254,7 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
   // segment is prefetched line by line a few KB ahead of the walk instead.
   size_t pf = s & ~size_t(63);
   auto ahead = [&](size_t pos) {
+    if (gpu_scopes) return;   // the host reads headers only: no streaming of span bytes
     const size_t want = std::min(n, pos + 8192);
     for (; pf < want; pf += 64) __builtin_prefetch(p + pf, 0, 3);
   };
@@ -249,6 +269,7 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
     }
     if (twt != 2 || !top.bytes(ro, rl)) { top.fail(); break; }
     *end = top.i;
+    if (gpu_scopes && top.i + 2 < n) __builtin_prefetch(p + top.i, 0, 3);   // the next record's header
     PbReader rr(p + ro, rl);
     resf.clear();
     scopes.clear();
@@ -323,6 +344,16 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
       scf.clear();
       c.lay.scope_ref.push_back(so.first | ((uint64_t)so.second << 32));
       c.lay.scope_span0.push_back((uint32_t)c.span_ref.size());
+      if (gpu_scopes && so.second <= kGpuScopeBytes) {   // counted, sized and listed on the GPU
+        c.scope_on_host.push_back(0);
+        c.scope_count.push_back(0);
+        c.scope_size.push_back(0);
+        c.scope_res.push_back(rloc);
+        c.lay.scope_hdr.push_back(0);
+        c.lay.scope_schema.push_back(0);
+        continue;
+      }
+      const size_t first_span = c.span_ref.size();
       while (sr.more() && sr.tag(f, wt)) {
         size_t o, l;
         if (f == 1 || f == 2 || f == 3) {
@@ -337,8 +368,10 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
             ahead(off + l);
             if (off > 0xFFFFFFFFull || l > 0xFFFFFFFFull) { c.err = "span beyond the 4 GiB arena range"; return; }
             c.span_ref.push_back(off | ((uint64_t)l << 32));
-            c.span_res.push_back(rloc);
-            c.span_scope.push_back(sloc);
+            if (!gpu_scopes) {
+              c.span_res.push_back(rloc);
+              c.span_scope.push_back(sloc);
+            }
           }
         } else {
           sr.skip(wt, f);
@@ -364,6 +397,8 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
                                 : scf.size() == 1 ? (scf[0].first | ((uint64_t)scf[0].second << 32))
                                                   : OtlpLayout::kMulti);
       c.lay.scope_schema.push_back(sschema_off | ((uint64_t)sschema << 32));
+      c.scope_on_host.push_back(1);
+      c.scope_count.push_back((uint32_t)(c.span_ref.size() - first_span));
     }
   }
   if (!top.ok) c.err = "OTLP protobuf: malformed TracesData";
@@ -399,7 +434,7 @@ size_t find_start(const uint8_t* p, size_t n, size_t k) {
 // thread's; the split is exact iff every thread ends exactly where the next
 // one started (the chain from 0 is unique), else the walk runs again on one
 // thread.
-bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, Walked& w) {
+bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, Walked& w, bool gpu_scopes = false) {
   const size_t kSeg = size_t(256) << 10;
   int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)parallel_width(), n / kSeg}));
   if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));   // diagnostics
@@ -411,7 +446,7 @@ bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, 
     for (int t = 1; t < T; t++) st[t] = find_start(p, n, n * (size_t)t / (size_t)T);
     for (int t = T - 1; t >= 1; t--) st[t] = std::min(st[t], st[t + 1]);   // monotone
     ch.assign((size_t)T, WalkChunk());
-    parallel_run(T, [&](int t) { walk_segment(ctx, cache, p, n, st[t], st[t + 1], ch[t], &en[t]); });
+    parallel_run(T, [&](int t) { walk_segment(ctx, cache, p, n, st[t], st[t + 1], ch[t], &en[t], gpu_scopes); });
     bool exact = true;
     for (int t = 0; t < T; t++) {
       if (!ch[t].err.empty()) {
@@ -442,8 +477,12 @@ bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, 
     nscope += ch[t].scope_size.size();
   }
   w.span_ref.resize(nspan);
-  w.span_res.resize(nspan);
-  w.span_scope.resize(nspan);
+  if (!gpu_scopes) {
+    w.span_res.resize(nspan);
+    w.span_scope.resize(nspan);
+  }
+  w.scope_on_host.resize(nscope);
+  w.scope_count.resize(nscope);
   w.res_svc.resize(nres);
   w.res_svc_str.resize(nres);
   w.res_attrset.resize(nres);
@@ -468,8 +507,10 @@ bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, 
     const WalkChunk& c = ch[t];
     for (size_t k = 0; k < c.span_ref.size(); k++) {
       w.span_ref[so[t] + k] = c.span_ref[k];
-      w.span_res[so[t] + k] = (uint32_t)(ro[t] + c.span_res[k]);
-      w.span_scope[so[t] + k] = (uint32_t)(co[t] + c.span_scope[k]);
+      if (!gpu_scopes) {
+        w.span_res[so[t] + k] = (uint32_t)(ro[t] + c.span_res[k]);
+        w.span_scope[so[t] + k] = (uint32_t)(co[t] + c.span_scope[k]);
+      }
     }
     for (size_t k = 0; k < c.res_svc.size(); k++) {
       w.res_svc[ro[t] + k] = c.res_svc[k];
@@ -487,7 +528,9 @@ bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, 
       w.lay.scope_ref[co[t] + k] = c.lay.scope_ref[k];
       w.lay.scope_hdr[co[t] + k] = c.lay.scope_hdr[k];
       w.lay.scope_schema[co[t] + k] = c.lay.scope_schema[k];
-      w.lay.scope_span0[co[t] + k] = (uint32_t)(so[t] + c.lay.scope_span0[k]);
+      w.lay.scope_span0[co[t] + k] = (uint32_t)(so[t] + c.lay.scope_span0[k]);   // gpu_scopes: into span_ref
+      w.scope_on_host[co[t] + k] = c.scope_on_host[k];
+      w.scope_count[co[t] + k] = c.scope_count[k];
     }
   };
   parallel_run((int)ch.size(), [&](int t) { place((size_t)t); });
@@ -496,7 +539,150 @@ bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, 
 }  // namespace
 
 namespace {
-int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchImpl* b) {
+// The GPU half of the structural walk: every ScopeSpans the host did not
+// walk is counted, sized and listed on the device (otlp_scope_*_kernel);
+// returns the span count in *n_out, or 1 in *redo when some scope needs the
+// host walk (groups or a malformed field: the caller walks on the host).
+int scope_walk_gpu(Engine* e, OtlpBatchImpl* b, Walked& w, hipStream_t st, uint64_t* n_out, bool* redo) {
+  (void)e;
+  const uint64_t S = w.scope_size.size(), H = w.span_ref.size();
+  *redo = false;
+  const uint32_t tiles = (uint32_t)((S + kScanTileItems - 1) / kScanTileItems);
+  struct Part { void** dst; size_t bytes; const void* src; };
+  uint64_t *scope_ref, *hdr, *schema, *host_at, *host_refs, *status;
+  uint8_t* on_host;
+  uint32_t *count, *scope_size, *flags, *span0, *scope_res, *words;
+  std::vector<Part> parts = {
+      {(void**)&scope_ref, 8 * S, b->lay.scope_ref.data()},
+      {(void**)&hdr, 8 * S, b->lay.scope_hdr.data()},
+      {(void**)&schema, 8 * S, b->lay.scope_schema.data()},
+      {(void**)&host_at, 8 * S, nullptr},
+      {(void**)&host_refs, 8 * H, w.span_ref.data()},
+      {(void**)&on_host, S, w.scope_on_host.data()},
+      {(void**)&count, 4 * S, w.scope_count.data()},
+      {(void**)&scope_size, 4 * S, w.scope_size.data()},
+      {(void**)&scope_res, 4 * S, w.scope_res.data()},
+      // device-only
+      {(void**)&flags, 4 * S, nullptr},
+      {(void**)&span0, 4 * S, nullptr},
+      {(void**)&status, 8 * (size_t)tiles + 64, nullptr},
+      {(void**)&words, 64, nullptr},
+  };
+  size_t total = 0, inputs = 0;
+  for (auto& p : parts) {
+    total = up(total + p.bytes + 16);
+    if (p.src || p.dst == (void**)&host_at) inputs = total;
+  }
+  int rc;
+  if ((rc = b->sslab.need(total)) || (rc = b->stage.need(inputs))) return rc;
+  size_t off = 0;
+  for (auto& p : parts) {
+    *p.dst = b->sslab.p + off;
+    if (p.src && p.bytes) std::memcpy(b->stage.p + off, p.src, p.bytes);
+    off = up(off + p.bytes + 16);
+  }
+  {   // host_at: the host-walked scopes' offsets into host_refs (the walk's span0)
+    uint64_t* ha = reinterpret_cast<uint64_t*>(b->stage.p + (reinterpret_cast<uint8_t*>(host_at) - b->sslab.p));
+    for (uint64_t q = 0; q < S; q++) ha[q] = b->lay.scope_span0[q];
+  }
+  HIP_TRY(hipMemcpyAsync(b->sslab.p, b->stage.p, inputs, hipMemcpyHostToDevice, st));
+  const size_t dev0 = reinterpret_cast<uint8_t*>(flags) - b->sslab.p;
+  HIP_TRY(hipMemsetAsync(flags, 0, total - dev0, st));   // flags, span0, scan status, words
+  OtlpScopeArgs a{};
+  a.pb = b->arena.p;
+  a.n_scopes = S;
+  a.scope_ref = scope_ref;
+  a.on_host = on_host;
+  a.scope_res = scope_res;
+  a.count = count;
+  a.scope_size = scope_size;
+  a.hdr = hdr;
+  a.schema = schema;
+  a.flags = flags;
+  a.span0 = span0;
+  a.host_refs = host_refs;
+  a.host_at = host_at;
+  b->sargs = a;
+  (void)hipGetLastError();
+  launch_otlp_scope_count(a, st);
+  HIP_TRY(hipGetLastError());
+  ScanArgs sa{};
+  sa.n = S;
+  sa.n_tiles = tiles;
+  sa.in = count;
+  sa.out = span0;
+  sa.total = words + 1;
+  sa.counter = words + 2;
+  sa.status = status;
+  sa.error = words;
+  if (S) launch_scan_u32(sa, st);
+  HIP_TRY(hipGetLastError());
+  uint32_t h[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(h, words, 8, hipMemcpyDeviceToHost, st));
+  // which scopes the host must finish (flags): copied back with the counts
+  std::vector<uint32_t> fl(S);
+  if (S) HIP_TRY(hipMemcpyAsync(fl.data(), flags, 4 * S, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (h[0]) return fail(OSE_EDEVICE, "OTLP ingest: scope scan error");
+  *n_out = h[1];
+  b->d_span0 = span0;
+  b->d_hdr = hdr;
+  b->d_schema = schema;
+  std::vector<std::pair<uint64_t, uint32_t>> patch;   // scope sizes the host computes
+  ProtoSizer sizer;
+  for (uint64_t q = 0; q < S; q++) {
+    if (!fl[q]) continue;
+    if (fl[q] & 2) { *redo = true; return 0; }
+    // a merged or unusual InstrumentationScope: pb_scope over its fields
+    const uint64_t sr = b->lay.scope_ref[q];
+    PbReader r(b->pb + (uint32_t)sr, (size_t)(sr >> 32));
+    ScopeSpans meta;
+    size_t sch = 0;
+    uint32_t f, wt;
+    while (r.more() && r.tag(f, wt)) {
+      size_t o, l;
+      if ((f == 1 || f == 2 || f == 3) && wt == 2 && r.bytes(o, l)) {
+        if (f == 1 && !pb_scope(b->pb + (uint32_t)sr + o, l, meta))
+          return fail(OSE_EINVAL, "OTLP protobuf: malformed InstrumentationScope");
+        if (f == 3) sch = l;
+      } else if (f == 1 || f == 2 || f == 3) {
+        return fail(OSE_EINVAL, "OTLP protobuf: malformed ScopeSpans");
+      } else {
+        r.skip(wt, f);
+      }
+    }
+    if (!r.ok) return fail(OSE_EINVAL, "OTLP protobuf: malformed ScopeSpans");
+    patch.emplace_back(q, (uint32_t)(sizer.scope_fixed(meta) + (sch ? flen(sch) : 0)));
+  }
+  for (auto& x : patch) HIP_TRY(hipMemcpyAsync(scope_size + x.first, &x.second, 4, hipMemcpyHostToDevice, st));
+  if (!patch.empty()) HIP_TRY(hipStreamSynchronize(st));   // the patch sources are on this stack
+  b->cols.scope_size = scope_size;
+  b->cols.scope_resource = scope_res;
+  // pass 2 writes into the span columns decode() allocates next
+  b->layout_on_host = false;
+  return 0;
+}
+
+// span refs and the scopes' span0 / header / schema refs back to the host
+// (the encoder and the host pass read them there)
+int layout_to_host(OtlpBatchImpl* b, hipStream_t st) {
+  if (b->layout_on_host) return 0;
+  const uint64_t n = b->cols.n_spans, S = b->cols.n_scopes;
+  b->span_ref.resize(n);
+  std::vector<uint32_t> span0(S);
+  if (n) HIP_TRY(hipMemcpyAsync(b->span_ref.data(), b->d_span_ref, 8 * n, hipMemcpyDeviceToHost, st));
+  if (S) {
+    HIP_TRY(hipMemcpyAsync(span0.data(), b->d_span0, 4 * S, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(b->lay.scope_hdr.data(), b->d_hdr, 8 * S, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(b->lay.scope_schema.data(), b->d_schema, 8 * S, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  for (uint64_t q = 0; q < S; q++) b->lay.scope_span0[q] = span0[q];
+  b->layout_on_host = true;
+  return 0;
+}
+
+int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchImpl* b, bool host_scopes = false) {
   int rc;
   OtlpEngine* o = otlp_engine(e, rc);
   if (!o) return rc;
@@ -527,47 +713,57 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     HIP_TRY(hipMemcpyAsync(b->arena.p, b->stage.p, pb_cap, hipMemcpyHostToDevice, st));
   }
   lap(0);
+  // 2. the walk: TracesData and ResourceSpans on the host, ScopeSpans up to
+  //    64 KB on the GPU (OSE_OTLP_HOST_SCOPES=1: all on the host, diagnostics)
+  static const bool env_host = getenv("OSE_OTLP_HOST_SCOPES") != nullptr;
+  const bool gpu_scopes = !host_scopes && !env_host;
   Walked w;
-  if (!walk(o->ctx, o->res_cache, pb, len, w)) return fail(OSE_EINVAL, w.err);
+  if (!walk(o->ctx, o->res_cache, pb, len, w, gpu_scopes)) return fail(OSE_EINVAL, w.err);
   lap(1);
   HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
   b->pb = pb;
   b->pb_len = len;
-  b->span_ref = std::move(w.span_ref);
   b->lay = std::move(w.lay);
-  const uint64_t n = b->span_ref.size(), R = w.res_svc.size(), S = w.scope_size.size();
+  b->layout_on_host = true;
+  ose_columns& c = b->cols;
+  c = ose_columns{};
+  uint64_t n = 0;
+  if (gpu_scopes) {
+    bool redo = false;
+    if ((rc = scope_walk_gpu(e, b, w, st, &n, &redo))) return rc;
+    if (redo) return decode(e, pb, len, st, b, true);   // a scope needs the host walk: all on the host
+  } else {
+    n = w.span_ref.size();
+    b->span_ref = std::move(w.span_ref);
+  }
+  const uint64_t R = w.res_svc.size(), S = b->lay.scope_ref.size();
   if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: more than 2^32-16 spans");
   const uint32_t K = o->n_attr_keys;
   b->attrsets = std::move(w.sets);
-  std::vector<uint32_t>& res_svc = w.res_svc;
-  std::vector<uint32_t>& res_svc_str = w.res_svc_str;
-  std::vector<uint32_t>& res_attrset = w.res_attrset;
-  std::vector<uint32_t>& res_size = w.res_size;
-  std::vector<uint32_t>& scope_size = w.scope_size;
-  std::vector<uint32_t>& scope_res = w.scope_res;
-  std::vector<uint8_t>& res_ok = w.res_ok;
-  std::vector<uint64_t>& attr_res = w.attr_res;
   ProtoSizer sizer;
   // device columns: one slab
   const uint64_t N = std::max<uint64_t>(n, 1);
   struct Part { void** dst; size_t bytes; const void* src; };
-  ose_columns& c = b->cols;
-  c = ose_columns{};
   uint8_t* host_flag = nullptr;
   uint32_t* host_count = nullptr;
   uint32_t* host_list = nullptr;
   uint64_t* span_ref = nullptr;
+  const ose_columns keep_scope = c;   // scope_size / scope_resource set by the GPU walk
   std::vector<Part> parts = {
-      {(void**)&span_ref, 8 * N, b->span_ref.data()},
-      {(void**)&c.resource, 4 * N, w.span_res.data()},
-      {(void**)&c.scope, 4 * N, w.span_scope.data()},
-      {(void**)&c.res_svc, 4 * R, res_svc.data()},
-      {(void**)&c.res_svc_str, 4 * R, res_svc_str.data()},
-      {(void**)&c.res_url_ok, R, res_ok.data()},
-      {(void**)&c.res_attrset, 4 * R, res_attrset.data()},
-      {(void**)&c.res_size, 4 * R, res_size.data()},
-      {(void**)&c.scope_size, 4 * S, scope_size.data()},
-      {(void**)&c.scope_resource, 4 * S, scope_res.data()},
+      {(void**)&span_ref, 8 * N, gpu_scopes ? nullptr : b->span_ref.data()},
+      {(void**)&c.resource, 4 * N, gpu_scopes ? nullptr : w.span_res.data()},
+      {(void**)&c.scope, 4 * N, gpu_scopes ? nullptr : w.span_scope.data()},
+      {(void**)&c.res_svc, 4 * R, w.res_svc.data()},
+      {(void**)&c.res_svc_str, 4 * R, w.res_svc_str.data()},
+      {(void**)&c.res_url_ok, R, w.res_ok.data()},
+      {(void**)&c.res_attrset, 4 * R, w.res_attrset.data()},
+      {(void**)&c.res_size, 4 * R, w.res_size.data()},
+  };
+  if (!gpu_scopes) {
+    parts.push_back({(void**)&c.scope_size, 4 * S, w.scope_size.data()});
+    parts.push_back({(void**)&c.scope_resource, 4 * S, w.scope_res.data()});
+  }
+  const std::vector<Part> outs = {
       // outputs of the decoder
       {(void**)&c.trace_id, 16 * N, nullptr},
       {(void**)&c.start_ns, 8 * N, nullptr},
@@ -583,6 +779,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
       {(void**)&host_count, 16, nullptr},
       {(void**)&host_list, 4 * N, nullptr},
   };
+  parts.insert(parts.end(), outs.begin(), outs.end());
   if (o->json_rules) parts.push_back({(void**)&c.attr_match, 8 * N, nullptr});
   if (K) {
     parts.push_back({(void**)&c.attr_type, (size_t)K * N, nullptr});
@@ -600,8 +797,22 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     if (p.src && p.bytes) std::memcpy(b->stage.p + off, p.src, p.bytes);
     off = up(off + p.bytes + 16);
   }
-  HIP_TRY(hipMemcpyAsync(b->slab.p, b->stage.p, inputs, hipMemcpyHostToDevice, st));
+  if (inputs) HIP_TRY(hipMemcpyAsync(b->slab.p, b->stage.p, inputs, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(host_count, 0, 16, st));
+  if (gpu_scopes) {
+    c.scope_size = keep_scope.scope_size;
+    c.scope_resource = keep_scope.scope_resource;
+    // pass 2: the span refs of every scope at their place
+    OtlpScopeArgs sa = b->sargs;
+    sa.span_ref = span_ref;
+    sa.span_res = const_cast<uint32_t*>(c.resource);
+    sa.span_scope = const_cast<uint32_t*>(c.scope);
+    launch_otlp_scope_spans(sa, st);
+    HIP_TRY(hipGetLastError());
+    b->d_span_ref = span_ref;
+    b->d_span_res = const_cast<uint32_t*>(c.resource);
+    b->span_ref.clear();
+  }
   c.n_spans = n;
   c.n_resources = (uint32_t)R;
   c.n_scopes = (uint32_t)S;
@@ -610,6 +821,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   c.arena_bytes = len;
   c.n_attr_keys = K;
   if (!o->ctx.url_filter) c.res_url_ok = nullptr;
+  std::vector<uint64_t>& attr_res = w.attr_res;
   lap(2);
   // 3. the GPU decoder
   OtlpArgs a{};
@@ -641,7 +853,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   (void)hipGetLastError();   // a stale error of an earlier call must not be reported as this launch's
   Engine::Timed tm{};
   e->prof_begin("otlp_span_kernel", st, tm);
-  launch_otlp_spans(a, st);
+  if (n) launch_otlp_spans(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
   // 4. the host pass
@@ -651,6 +863,14 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   b->host_spans = cnt;
   lap(3);
   if (!cnt) return 0;
+  std::vector<uint32_t> span_res;
+  const std::vector<uint32_t>* sres = &w.span_res;
+  if (!b->layout_on_host) {   // the spans' refs and resources from the device
+    if ((rc = layout_to_host(b, st))) return rc;
+    span_res.resize(n);
+    HIP_TRY(hipMemcpy(span_res.data(), b->d_span_res, 4 * n, hipMemcpyDeviceToHost));
+    sres = &span_res;
+  }
   std::vector<uint32_t> list(cnt);
   HIP_TRY(hipMemcpy(list.data(), host_list, 4 * (size_t)cnt, hipMemcpyDeviceToHost));
   std::vector<OtlpFix> fix(cnt);
@@ -669,7 +889,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     const uint64_t ref = b->span_ref[i];
     Span sp;
     if (!pb_span(pb + (uint32_t)ref, (size_t)(ref >> 32), sp)) return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
-    columnize_span(o->ctx, sp, attr_res[w.span_res[i]], sizer, sc);
+    columnize_span(o->ctx, sp, attr_res[(*sres)[i]], sizer, sc);
     OtlpFix& x = fix[q];
     x = OtlpFix{};
     x.idx = i;
@@ -770,6 +990,7 @@ int ose_otlp_decode(ose_engine* eng, const void* pb, size_t len, void* hip_strea
   b->e = e;
   const int rc = decode(e, static_cast<const uint8_t*>(pb), len, static_cast<hipStream_t>(hip_stream), b);
   if (rc) {
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(hip_stream));   // no copy may outlive the buffers
     delete b;
     return rc;
   }
@@ -950,6 +1171,7 @@ int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs
     d.tmpl_arena_len = used;
   }
   d.span_size = reinterpret_cast<const uint32_t*>(h + o_size);
+  if ((rc = layout_to_host(b, st))) return rc;
   auto* o = new OtlpOut();
   o->e = e;
   {

@@ -452,6 +452,120 @@ __global__ __launch_bounds__(kOThreads) void otlp_fix_kernel(OtlpFixArgs a) {
   }
 }
 
+// ---- ScopeSpans on the GPU ------------------------------------------------------
+// Pass 1, one lane per scope: the fields of its payload (otlp_pb.cpp
+// pb_walk's ScopeSpans loop): InstrumentationScope (1), spans (2),
+// schema_url (3), others skipped.  The scope's fixed size is
+// ProtoSizer::scope_fixed: the InstrumentationScope framed (always, gogo)
+// + schema_url; a merged or unusual scope message leaves it to the host.
+__global__ __launch_bounds__(kOThreads) void otlp_scope_count_kernel(OtlpScopeArgs a) {
+  const uint64_t q = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (q >= a.n_scopes || a.on_host[q]) return;
+  const uint64_t ref = a.scope_ref[q];
+  const uint32_t s0 = (uint32_t)ref, s1 = s0 + (uint32_t)(ref >> 32);
+  Rd r(a.pb, s0, s1);
+  uint32_t n = 0, nh = 0, flags = 0;
+  uint64_t hdr = 0, schema = 0;
+  uint32_t f, wt;
+  while (r.more() && r.tag(f, wt)) {
+    uint32_t ps, pl;
+    if (f == 1 || f == 2 || f == 3) {
+      if (wt != 2 || !r.len(ps, pl)) { r.bad = true; break; }
+      if (f == 1) { hdr = (uint64_t)ps | ((uint64_t)pl << 32); nh++; }
+      else if (f == 2) n++;
+      else schema = (uint64_t)ps | ((uint64_t)pl << 32);
+    } else {
+      r.skip(wt);
+    }
+  }
+  if (r.bad) {
+    a.flags[q] = 2;
+    a.count[q] = 0;
+    return;
+  }
+  // the InstrumentationScope's pdata size (name, version: last occurrence)
+  uint64_t sc = 0;
+  if (nh == 1) {
+    Rd h(a.pb, (uint32_t)hdr, (uint32_t)hdr + (uint32_t)(hdr >> 32));
+    uint32_t name = 0, version = 0;
+    uint64_t dropped = 0, attrs = 0;
+    while (h.more() && h.tag(f, wt)) {
+      uint32_t ps, pl;
+      if (f == 1 || f == 2 || f == 3) {
+        if (wt != 2 || !h.len(ps, pl)) { h.bad = true; break; }
+        if (f == 1) name = pl;
+        else if (f == 2) version = pl;
+        else {
+          uint32_t ko, kl;
+          Val v;
+          attrs += field_len(key_value(h, ps, ps + pl, ko, kl, v));
+        }
+      } else if (f == 4) {
+        if (wt != 0) { h.bad = true; break; }
+        dropped = (uint32_t)h.varint();
+      } else {
+        h.skip(wt);
+      }
+    }
+    if (h.bad) flags = 1;
+    sc = str_field(name) + str_field(version) + attrs + varint_field(dropped);
+  } else if (nh > 1) {
+    flags = 1;
+    hdr = kOtlpScopeMulti;
+  }
+  a.count[q] = n;
+  a.hdr[q] = hdr;
+  a.schema[q] = schema;
+  a.flags[q] = flags;
+  a.scope_size[q] = flags ? 0u : (uint32_t)(field_len(sc) + str_field((uint32_t)(schema >> 32)));
+}
+
+// Pass 2: every scope's span refs at their place in the batch
+__global__ __launch_bounds__(kOThreads) void otlp_scope_spans_kernel(OtlpScopeArgs a) {
+  const uint64_t q = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (q >= a.n_scopes) return;
+  uint64_t i = a.span0[q];
+  const uint32_t res = a.scope_res[q];
+  if (a.on_host[q]) {
+    const uint64_t at = a.host_at[q];
+    for (uint32_t k = 0; k < a.count[q]; k++, i++) {
+      a.span_ref[i] = a.host_refs[at + k];
+      a.span_res[i] = res;
+      a.span_scope[i] = (uint32_t)q;
+    }
+    return;
+  }
+  const uint64_t ref = a.scope_ref[q];
+  const uint32_t s0 = (uint32_t)ref, s1 = s0 + (uint32_t)(ref >> 32);
+  Rd r(a.pb, s0, s1);
+  uint32_t f, wt;
+  while (r.more() && r.tag(f, wt)) {
+    uint32_t ps, pl;
+    if (f == 1 || f == 2 || f == 3) {
+      if (wt != 2 || !r.len(ps, pl)) break;
+      if (f == 2) {
+        a.span_ref[i] = (uint64_t)ps | ((uint64_t)pl << 32);
+        a.span_res[i] = res;
+        a.span_scope[i] = (uint32_t)q;
+        i++;
+      }
+    } else {
+      r.skip(wt);
+    }
+  }
+}
+
+void launch_otlp_scope_count(const OtlpScopeArgs& a, hipStream_t st) {
+  if (a.n_scopes)
+    hipLaunchKernelGGL(otlp_scope_count_kernel, dim3((uint32_t)((a.n_scopes + kOThreads - 1) / kOThreads)),
+                       dim3(kOThreads), 0, st, a);
+}
+void launch_otlp_scope_spans(const OtlpScopeArgs& a, hipStream_t st) {
+  if (a.n_scopes)
+    hipLaunchKernelGGL(otlp_scope_spans_kernel, dim3((uint32_t)((a.n_scopes + kOThreads - 1) / kOThreads)),
+                       dim3(kOThreads), 0, st, a);
+}
+
 void launch_otlp_spans(const OtlpArgs& a, hipStream_t st) {
   const uint64_t blocks = std::min<uint64_t>((a.n_spans + kOThreads - 1) / kOThreads, 8192);
   if (blocks) hipLaunchKernelGGL(otlp_span_kernel, dim3((uint32_t)blocks), dim3(kOThreads), 0, st, a);

@@ -8,7 +8,8 @@ from odigos_amd import native
 from odigos_amd.batch import DeviceBatch, Engine, Generator
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
-g = Generator("url", 0x0D160002, n, threads=16)
+wl = os.environ.get("OSE_CLOCKS_WORKLOAD", "url")   # "url" (C2) or "fused" (C4's mix)
+g = Generator(wl, 0x0D160002, n, threads=16)
 g.cols.res_url_ok = None
 eng = Engine({"odigosurltemplate": {}})
 db = DeviceBatch(g.cols, fields=("arena", "kind", "url_flags", "path"))
