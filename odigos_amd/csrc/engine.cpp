@@ -318,16 +318,21 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   uint64_t n = c->n_spans;
   const uint32_t groups = (uint32_t)((n + kUrlGroup - 1) / kUrlGroup);
   // workspace: [0,16) scan counter, slow count, error | scan status 8t (both zeroed by one memset) |
-  // plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | slow groups 4g | dbg
+  // plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | group_scr 8g |
+  // slow groups 4g | dbg | scratch (the assembled group images)
   const uint32_t scan_tiles = (groups + kUrlScanTile - 1) / kUrlScanTile;
   const size_t off_sst = 16, zero_bytes = off_sst + 8 * (size_t)scan_tiles;
   const size_t off_len = align_up(zero_bytes, 256), off_meta = off_len + 4 * n;
   const size_t off_code = align_up(off_meta + 4 * n, 8);
   const size_t off_gsum = off_code + 8 * n, off_gbase = off_gsum + 8 * (size_t)groups;
-  const size_t off_slow = off_gbase + 8 * (size_t)groups;
+  const size_t off_gscr = off_gbase + 8 * (size_t)groups;
+  const size_t off_slow = off_gscr + 8 * (size_t)groups;
   const size_t off_dbg = align_up(off_slow + 4 * (size_t)groups, 256);
-  const size_t need = off_dbg + 256;
-  if (need > url_workspace_bytes(n)) return fail(OSE_EINVAL, "internal: URL workspace layout exceeds its bound");
+  const size_t off_scr = off_dbg + 256;
+  const size_t scr_bytes = url_scratch_bytes(n, c->arena_bytes);
+  const size_t need = off_scr + scr_bytes;
+  if (need > url_workspace_bytes(n, c->arena_bytes))
+    return fail(OSE_EINVAL, "internal: URL workspace layout exceeds its bound");
   int rc = ws->reserve(ws_off + need);
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(ws->dev) + ws_off;
@@ -351,6 +356,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.plan_code = reinterpret_cast<uint64_t*>(base + off_code);
   a.group_sum = reinterpret_cast<uint64_t*>(base + off_gsum);
   a.group_base = reinterpret_cast<uint64_t*>(base + off_gbase);
+  a.group_scr = reinterpret_cast<uint64_t*>(base + off_gscr);
+  a.scratch = base + off_scr;
   a.n_scan_tiles = scan_tiles;
   a.scan_counter = reinterpret_cast<uint32_t*>(base);
   a.scan_status = reinterpret_cast<uint64_t*>(base + off_sst);
@@ -360,6 +367,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   HIP_TRY(hipMemsetAsync(base, 0, zero_bytes, st));
   a.used = o->tmpl_arena_used;
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
+  a.scr_region = (scr_bytes / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
   if (n == 0) {
     if (o->tmpl_arena_used) HIP_TRY(hipMemsetAsync(o->tmpl_arena_used, 0, 8, st));
     return 0;
@@ -377,8 +385,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   launch_url_scan(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
-  e->prof_begin("url_emit_kernel", st, tm);
-  launch_url_emit(a, st);
+  e->prof_begin("url_copy_kernel", st, tm);
+  launch_url_copy(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
   e->prof_begin("url_emit_slow_kernel", st, tm);
@@ -390,10 +398,9 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
     HIP_TRY(hipMemcpyAsync(h, a.dbg, sizeof h, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const double wp = h[3] ? (double)h[3] : 1.0, we = h[6] ? (double)h[6] : 1.0;
-    fprintf(stderr, "url clocks/wave: plan[stage %.0f bitmaps %.0f plan %.0f] emit[stage %.0f emit %.0f]\n",
-            h[0] / wp, h[1] / wp, h[2] / wp, h[4] / we, h[5] / we);
-    fprintf(stderr, "url emit cumulative clocks/wave: counts %.0f bitmap %.0f pieces %.0f gather %.0f stores(after stage) %.0f\n",
-            h[8] / we, h[9] / we, h[10] / we, h[11] / we, h[12] / we);
+    (void)we;
+    fprintf(stderr, "url clocks/wave: plan[stage %.0f bitmaps %.0f plan %.0f assemble+store %.0f]\n", h[0] / wp,
+            h[1] / wp, h[2] / wp, h[5] / wp);
     fprintf(stderr, "url plan list clocks/wave: enumerate %.0f classify %.0f fold %.0f\n", h[13] / wp, h[14] / wp,
             h[15] / wp);
   }
@@ -411,8 +418,8 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   // one reservation for every stage of the call: a stage must not reallocate
   // scratch an earlier stage of the same call is still using on the stream
   size_t need = 0;
-  if (mask & OSE_STAGE_TEMPLATE) need = std::max(need, url_workspace_bytes(c->n_spans));
-  if (mask & OSE_STAGE_SAMPLE) need = std::max(need, e->workspace_bytes(c->n_spans));
+  if (mask & OSE_STAGE_TEMPLATE) need = std::max(need, url_workspace_bytes(c->n_spans, c->arena_bytes));
+  if (mask & OSE_STAGE_SAMPLE) need = std::max(need, e->workspace_bytes(c->n_spans, c->arena_bytes));
   if (mask & OSE_STAGE_SIZE) need = std::max(need, size_scratch_bytes(c->n_scopes, c->n_resources));
   // SAMPLE + TEMPLATE by trace id: the URL stage reads nothing SAMPLE writes,
   // so its launches are queued between SAMPLE's fast path and the rest of
@@ -434,7 +441,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
                             !capturing && !getenv("OSE_NO_DEFER_SLOW");
   const bool defer = gate_on_host && (mask & OSE_STAGE_TEMPLATE);
   const size_t url_off = defer ? (sampling_scratch_bytes(c->n_spans) + 255) / 256 * 256 : 0;
-  if (defer) need = std::max(need, url_off + url_workspace_bytes(c->n_spans));
+  if (defer) need = std::max(need, url_off + url_workspace_bytes(c->n_spans, c->arena_bytes));
   int rc = ws->reserve(need);
   std::function<int()> sample_tail;
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
@@ -567,11 +574,10 @@ int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info) {
 
 int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   if (!eng) return fail(OSE_EINVAL, "NULL engine");
-  (void)arena_bytes;
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (int brc = bind_device(e)) return brc;
   Workspace* ws = e->acquire_ws(nullptr);
-  int rc = ws->reserve(e->workspace_bytes(n_spans));
+  int rc = ws->reserve(e->workspace_bytes(n_spans, arena_bytes));
   if (!rc && e->has_sampling) rc = ws->reserve_table(n_spans);
   if (!rc && e->attr_n_dev) rc = ws->reserve_attr(n_spans);
   e->release_ws(ws, nullptr);

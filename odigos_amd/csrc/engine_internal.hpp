@@ -110,7 +110,7 @@ struct Engine {
   void give_stream(hipStream_t s);
   int build_sampling_tables();
   int build_attr_tables();
-  size_t workspace_bytes(uint64_t n_spans) const;
+  size_t workspace_bytes(uint64_t n_spans, uint64_t arena_bytes) const;   // every configured stage
 };
 
 // tail != nullptr (OSE_GROUP_TRACE_ID only): queue the fast path, then hand

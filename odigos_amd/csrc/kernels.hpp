@@ -8,10 +8,15 @@
 
 namespace ose {
 
-// odigosurltemplate: three launches on one stream (url_kernel.hip).
-//   url_plan_kernel  one wave per 64-span group: plan + output length per span
+// odigosurltemplate: four launches on one stream (url_kernel.hip).
+//   url_plan_kernel  one wave per 64-span group: plan, output length per span
+//                    and the group's template bytes, assembled in LDS and
+//                    stored to the wave's scratch region
 //   url_scan_kernel  exclusive scan of the per-group output sums
-//   url_emit_kernel  one wave per group: template bytes + refs
+//   url_copy_kernel  one wave per group: template refs, and the group's bytes
+//                    copied from scratch to their place in the output arena
+//   url_emit_slow_kernel  the groups the plan kernel could not assemble (user
+//                    rules, oversized groups), from the plan arrays
 struct UrlKernelArgs {
   uint64_t n_spans;
   uint32_t n_groups;           // ceil(n_spans / kUrlGroup)
@@ -28,8 +33,11 @@ struct UrlKernelArgs {
   const uint8_t* cfg;          // UrlCfgDev blob
   // workspace
   uint32_t* plan_len;          // [n_spans] output length
-  uint32_t* plan_meta;         // [n_spans] mode/lead/slow/url_out/field
-  uint64_t* plan_code;         // [n_spans] per-segment name ids
+  uint32_t* plan_meta;         // [n_spans] mode/lead/slow/url_out/field (slow groups only)
+  uint64_t* plan_code;         // [n_spans] per-segment name ids (slow groups only)
+  uint8_t* scratch;            // assembled group images: wave w owns [w * scr_region, +scr_region)
+  uint64_t scr_region;         // bytes per wave (multiple of 16)
+  uint64_t* group_scr;         // [n_groups] scratch offset of the group's image, ~0: slow group
   uint64_t* group_sum;         // [n_groups]
   uint64_t* group_base;        // [n_groups] exclusive prefix
   uint32_t n_scan_tiles;       // ceil(n_groups / kUrlScanTile)
@@ -37,7 +45,7 @@ struct UrlKernelArgs {
   uint64_t* scan_status;       // [n_scan_tiles], zeroed before launch
   uint32_t* error;             // bit0 look-back timeout, bit1 output overflow
   uint64_t* used;              // bytes written (optional)
-  uint32_t* slow_count;        // groups K3 left to K3s (zeroed before launch)
+  uint32_t* slow_count;        // groups the plan kernel left to K3s (zeroed before launch)
   uint32_t* slow_groups;       // [n_groups]
   uint32_t general;            // user rules or custom ids configured (selects the general kernel instances)
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
@@ -46,14 +54,26 @@ struct UrlKernelArgs {
 constexpr uint32_t kUrlGroup = 64;       // spans per wave group (url_kernel.hip kWave)
 constexpr uint32_t kUrlScanTile = 1024;  // groups per scan workgroup (url_kernel.hip kScanThreads)
 // workspace bytes the URL stage needs for n spans (engine.cpp run_url layout)
-inline size_t url_workspace_bytes(uint64_t n) {
+constexpr uint32_t kUrlMaxWaves = 4096;  // waves of the persistent plan grid (>= its resident waves)
+constexpr uint32_t kUrlWaveSlack = 8192; // scratch bytes per wave on top of its share
+// scratch for the assembled group images of a batch whose arena holds
+// arena_bytes: the path bytes bound the templates but for inserted names,
+// hence 1.25x plus a per-wave slack; a group that does not fit its wave's
+// region is emitted by url_emit_slow_kernel instead
+inline size_t url_scratch_bytes(uint64_t n, uint64_t arena_bytes) {
+  const uint64_t g = (n + kUrlGroup - 1) / kUrlGroup;
+  const uint64_t w = g < kUrlMaxWaves ? g : kUrlMaxWaves;
+  return ((arena_bytes + n + (arena_bytes + n) / 4 + 15) & ~15ull) + w * kUrlWaveSlack;
+}
+inline size_t url_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
   const uint64_t g = (n + kUrlGroup - 1) / kUrlGroup;
   const uint64_t t = (g + kUrlScanTile - 1) / kUrlScanTile;
-  return 16 + t * 8 + 256 + n * 16 + 8 + g * 20 + 512;
+  return 16 + t * 8 + 256 + n * 16 + 8 + g * 28 + 512 + 256 + url_scratch_bytes(n, arena_bytes);
 }
 void launch_url_plan(const UrlKernelArgs& a, hipStream_t st);
+uint32_t url_plan_waves(const UrlKernelArgs& a);   // waves of the plan grid (scratch regions)
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st);
-void launch_url_emit(const UrlKernelArgs& a, hipStream_t st);
+void launch_url_copy(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st);
 
 }  // namespace ose

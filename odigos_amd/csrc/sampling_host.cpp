@@ -183,8 +183,8 @@ size_t sampling_scratch_bytes(uint64_t n) {
   return s + 256;
 }
 
-size_t Engine::workspace_bytes(uint64_t n_spans) const {
-  size_t s = url_workspace_bytes(n_spans);
+size_t Engine::workspace_bytes(uint64_t n_spans, uint64_t arena_bytes) const {
+  size_t s = has_url ? url_workspace_bytes(n_spans, arena_bytes) : 0;
   if (has_sampling) s = std::max(s, sampling_scratch_bytes(n_spans));
   if (has_traffic) s = std::max(s, size_scratch_bytes(n_spans, n_spans));
   return s;

@@ -868,8 +868,142 @@ __device__ __forceinline__ uint32_t wave_first_group() { return blockIdx.x * kWa
 __device__ __forceinline__ uint32_t wave_stride() { return gridDim.x * kWaves; }
 
 // ---------------------------------------------------------------------------
-// K1: plan.  Waves are independent (no workgroup barrier after the config
-// load); per group: class bitmaps of the staged bytes, then one plan per span.
+// Output helpers shared by the plan kernel's writer and K3s.
+typedef __attribute__((address_space(3))) uint32_t lds_w32;
+struct PutOr {
+  lds_w32* img;
+  uint32_t wpos, nb;   // wpos: image offset of acc's first byte (dword aligned); nb: bytes in acc
+  uint64_t acc;
+  __device__ PutOr(lds_w32* im, uint32_t start) : img(im), wpos(start & ~3u), nb(start & 3u), acc(0) {}
+  __device__ __forceinline__ void flush() {
+    __hip_atomic_fetch_or(&img[wpos >> 2], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    acc >>= 32;
+    wpos += 4;
+    nb -= 4;
+  }
+  __device__ __forceinline__ void byte(uint32_t c) {
+    acc |= (uint64_t)(c & 0xFFu) << (8 * nb);
+    if (++nb == 4) flush();
+  }
+  __device__ __forceinline__ void word(uint32_t x, uint32_t nv) {
+    if (nv < 4) x &= (1u << (8 * nv)) - 1u;
+    acc |= (uint64_t)x << (8 * nb);
+    nb += nv;
+    if (nb >= 4) flush();
+  }
+  __device__ __forceinline__ void finish() {
+    if (nb) __hip_atomic_fetch_or(&img[wpos >> 2], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+};
+
+
+constexpr uint32_t kBNames = 1024;    // braced names for template ids 0..14, '/' at byte 0
+
+struct BracedNames {
+  __attribute__((aligned(16))) uint8_t b[kBNames + 16];
+  uint16_t off[16];
+  uint8_t len[16];
+  uint32_t ok;
+};
+
+// "{name}" for ids 0..14 (the ids a plan code can carry), once per workgroup.
+__device__ void load_braced_names(const Cfg& cfg, BracedNames& bn) {
+  if (threadIdx.x == 0) {
+    const uint32_t nn = min(cfg.h->n_names, 15u);
+    uint32_t o = 4;
+    bool ok = true;
+    bn.b[0] = '/';
+    for (uint32_t id = 0; id < nn; id++) {
+      const uint32_t l = cfg.name(id).len + 2;
+      if (o + l > kBNames || l > 255) { ok = false; break; }
+      bn.off[id] = (uint16_t)o;
+      bn.len[id] = (uint8_t)l;
+      o += l;
+    }
+    bn.ok = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  if (bn.ok && threadIdx.x < min(cfg.h->n_names, 15u)) {
+    const NameDev nm = cfg.name(threadIdx.x);
+    const uint8_t* src = cfg.blob + cfg.h->bytes_off + nm.off;
+    uint8_t* d = bn.b + bn.off[threadIdx.x];
+    d[0] = '{';
+    for (uint32_t q = 0; q < nm.len; q++) d[1 + q] = src[q];
+    d[1 + nm.len] = '}';
+  }
+  __syncthreads();
+}
+
+
+__device__ __forceinline__ uint32_t lds_word(const lds_u8* L, uint32_t p) {
+  const lds_u32* w = (const lds_u32*)(L + (p & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], p & 3);
+}
+
+
+// The columns K3s reads for one group.
+struct EmitCols {
+  uint32_t len, meta;
+  uint64_t code;
+  ose_strref pr;
+  uint64_t base, gsum;
+};
+__device__ __forceinline__ EmitCols emit_cols(const UrlKernelArgs& a, uint32_t g, int lane) {
+  EmitCols c{0, 0, 0, {0, 0}, 0, 0};
+  const uint64_t i = (uint64_t)g * kWave + lane;
+  if (g < a.n_groups) {
+    c.base = a.group_base[g];
+    c.gsum = a.group_sum[g];
+  }
+  if (i < a.n_spans) {
+    c.len = a.plan_len[i];
+    c.meta = a.plan_meta[i];
+    c.code = a.plan_code[i];
+    c.pr = a.path[i];
+  }
+  return c;
+}
+__device__ __forceinline__ bool emit_needs_path(uint32_t meta) {
+  const uint32_t mode = meta & 7u;
+  return mode == M_RULE || mode == M_DEFAULT || mode == M_ORIG;
+}
+
+// image dword k <-> global bytes [base - shift + 4k, +4); bytes outside
+// [base, base + gtotal) belong to the neighbouring groups, so partial dwords
+// at the ends are stored bytewise
+__device__ __forceinline__ void store_image(const UrlKernelArgs& a, const lds_w32* img, uint64_t base, uint32_t shift,
+                                            uint64_t gtotal) {
+  const int lane = threadIdx.x & 63;
+  uint8_t* gdst = a.out_arena + (base - shift);
+  const uint32_t nd = (uint32_t)((shift + gtotal + 3) / 4);
+  const uint64_t endb = shift + gtotal;
+  for (uint32_t k = lane; k < nd; k += kWave) {
+    const uint32_t w = img[k];
+    const uint32_t b0 = 4 * k;
+    if (b0 >= shift && b0 + 4 <= endb) {
+      *reinterpret_cast<uint32_t*>(gdst + b0) = w;
+    } else {
+      for (uint32_t q = 0; q < 4; q++)
+        if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(w >> (8 * q));
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  const uint32_t incl = wave_incl_sum_u32(v);
+  *total = lane_value(incl, kWave - 1);
+  return incl - v;
+}
+
+
+// ---------------------------------------------------------------------------
+// K1: plan and assemble.  Waves are independent (no workgroup barrier after
+// the config load); per group: class bitmaps of the staged bytes, the segment
+// list and its classification, one plan per span, then the group's template
+// bytes, written from the segment list into an LDS image (over the bitmaps,
+// which are dead by then) and stored to the wave's scratch region.  The
+// group's place in the output arena is only known after K2, so K4 moves the
+// image there; the path bytes are read from HBM once.
 constexpr uint32_t kSegCap = 192;   // per-wave segment list (C2 groups hold ~118 segments, max seen 182)
 // K1 stages each group through LDS-DMA into one of two per-wave buffers, so
 // the next group's bytes land while this one is planned without holding them
@@ -883,9 +1017,12 @@ constexpr uint32_t kPlanBmRows = kPlanStage / 32 + 3;
 struct PlanSmem {
   NamesSmem ns;
   __attribute__((aligned(16))) uint8_t stage[2][kWaves][kPlanStage + 16];
-  __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kPlanBmRows];
-  uint32_t segs[kWaves][kSegCap];
+  __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kPlanBmRows];   // class bitmaps, then the output image
+  uint32_t segs[kWaves][kSegCap];   // enumerated segments (start | len | owner lane)
+  uint32_t cls[kWaves][kSegCap];    // their classification (out_len << 8 | id + 1)
+  BracedNames bn;
 };
+constexpr uint32_t kImgCap = kRowVec * kPlanBmRows * 16;   // bytes of one wave's output image
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
@@ -954,18 +1091,20 @@ __device__ __noinline__ int classify_long(const Cfg& cfg, const LdsReader& rd, u
 // span's segments into the wave's list; the wave classifies the list 64
 // segments per step (about 2 steps for a C2 group, instead of one step per
 // segment index of the longest path); each lane then folds its own entries.
-// Entries: start 12 | len 13 before classification, then out_len << 8 | (id + 1)
-// where out_len is what the segment adds to the template ({name} or itself).
+// Entries: start 12 | len 13 | owner lane 6 before classification, then
+// out_len << 8 | (id + 1) where out_len is what the segment adds to the
+// template ({name} or itself).
 // A path whose bytes lie in 6 bitmap rows (the common case) finds its '?' cut,
 // leading '/' and segment ends in one read of those rows' slash and '?' words
 // and folds its entries (<= 8) in one read; longer paths walk the rows.
 // Returns false (nothing written) when the list would overflow.
 // cls: where the classified entries go (== segs: in place; else segs keeps
-// start | len << 12 for a fused emit)
+// the enumerated entries for the fused writer).  *big_id: some segment of
+// this lane's path took a name id the braced-name table does not hold.
 __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32, lds_cu4* bm, uint32_t* segs,
                                                 bool needs_path, uint32_t p0, uint32_t plen, uint32_t f, Plan& p,
                                                 bool tm, uint64_t* tt, uint32_t* cls = nullptr,
-                                                uint32_t* seg_off = nullptr) {
+                                                uint32_t* seg_off = nullptr, bool* big_id = nullptr) {
   if (!cls) cls = segs;
   const int lane = threadIdx.x & 63;
   uint64_t c0 = tm ? clk() : 0;
@@ -1038,28 +1177,29 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   if (nseg) {   // enumerate
     const uint32_t bend = p0 + n;
     uint32_t s = p0 + p.lead, k = 0;
+    const uint32_t own = (uint32_t)lane << 25;   // the entry's span (the fused writer's owner lane)
     if (win) {
       const uint32_t wb = p0 - b0;   // stage coordinate of window bit 0
       for (uint64_t m = sl0; m; m &= m - 1) {
         const uint32_t e = wb + (uint32_t)__builtin_ctzll(m);
-        segs[off + k++] = s | ((e - s) << 12);
+        segs[off + k++] = s | ((e - s) << 12) | own;
         s = e + 1;
       }
       for (uint64_t m = sl1; m; m &= m - 1) {
         const uint32_t e = wb + 64 + (uint32_t)__builtin_ctzll(m);
-        segs[off + k++] = s | ((e - s) << 12);
+        segs[off + k++] = s | ((e - s) << 12) | own;
         s = e + 1;
       }
       for (uint64_t m = sl2; m; m &= m - 1) {
         const uint32_t e = wb + 128 + (uint32_t)__builtin_ctzll(m);
-        segs[off + k++] = s | ((e - s) << 12);
+        segs[off + k++] = s | ((e - s) << 12) | own;
         s = e + 1;
       }
-      segs[off + k] = s | ((bend - s) << 12);
+      segs[off + k] = s | ((bend - s) << 12) | own;
     } else {
       for (; k < nseg; k++) {
         const uint32_t e = k + 1 < nseg ? first_of(bm, C_SL, s, bend) : bend;
-        segs[off + k] = s | ((e - s) << 12);
+        segs[off + k] = s | ((e - s) << 12) | own;
         s = e + 1;
       }
     }
@@ -1069,7 +1209,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   LdsReader rd0(stage32, 0);
   for (uint32_t x = lane; x < total; x += kWave) {   // classify
     const uint32_t ent = segs[x];
-    const uint32_t s = ent & 0xFFFu, L = ent >> 12;
+    const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
     int id;
     if (L <= 64) {
       const Win w = load_win<0, 2>(bm, s);
@@ -1082,6 +1222,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   }
   wave_lds_sync();
   if (tm) { const uint64_t c1 = clk(); tt[1] += c1 - c0; c0 = c1; }
+  bool big = false;
   if (nseg) {   // fold
     uint32_t l = p.lead + nseg - 1;
     bool templated = false;
@@ -1097,7 +1238,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
           if (id >= 0) {
             templated = true;
             if (id < 15) p.code |= (uint64_t)(id + 1) << (k * 4);
-            else p.slow = true;
+            else p.slow = big = true;
           }
         }
       }
@@ -1110,6 +1251,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
           templated = true;
           if (k < 16 && id < 15) p.code |= (uint64_t)(id + 1) << (k * 4);
           else p.slow = true;
+          big |= id >= 15;
         }
       }
     }
@@ -1119,6 +1261,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   }
   if (tm) tt[2] += clk() - c0;
   if (seg_off) *seg_off = off | (nseg << 16);
+  if (big_id) *big_id = big;
   return true;
 }
 
@@ -1148,6 +1291,57 @@ __device__ __forceinline__ uint32_t plan_gate(const PlanCols& c) {
   return (c.f & OSE_URL_PATH_MASK) != OSE_URL_PATH_NONE ? 2u : 0u;
 }
 
+// The group's template bytes into img from the classified segment list,
+// called by the whole wave.  Entry x of lane L's path writes '/' and then its
+// output ({name} from the braced-name table, or the segment's own staged
+// bytes) at L's output offset plus the outputs of L's earlier entries; a path
+// that neither starts with '/' nor keeps its original form (processor.go:
+// 182-185 "/" + body) drops the first separator.  M_SLASH / M_RENAME_SLASH
+// spans are a lone '/'.  Every image byte is written exactly once (byte
+// stores, 8 loads in flight per batch), so the image needs no clearing.
+// Entries are written 64 per step, one per lane: the per-byte work follows the
+// longest segment of a step, not the longest path of the group.
+__device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L, uint32_t stage_src, const uint32_t* segs,
+                                               const uint32_t* cls, const BracedNames& bn, uint32_t bn_src,
+                                               const Plan& p, uint32_t seg_off, uint32_t local) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nseg = seg_off >> 16, off = seg_off & 0xFFFFu;
+  const uint32_t pre = (p.lead || p.mode == M_ORIG) ? 1u : 0u;
+  uint32_t unused;
+  // bytes this lane's entries write, separators included; E0 = those of the lanes before
+  const uint32_t E0 = wave_excl_scan(nseg ? p.len + 1 - pre : 0u, &unused);
+  const int32_t adj = (int32_t)local - (int32_t)E0 - (int32_t)(1 - pre);
+  const uint32_t pk = ((uint32_t)adj & 0xFFFFu) | (off << 16) | (pre << 24);
+  if (p.len && (p.mode == M_SLASH || p.mode == M_RENAME_SLASH)) img[local] = '/';
+  const uint32_t total = lane_value(off + nseg, kWave - 1);
+  uint32_t carry = 0;
+  for (uint32_t x0 = 0; x0 < total; x0 += kWave) {
+    const uint32_t x = x0 + (uint32_t)lane;
+    const bool v = x < total;
+    const uint32_t ent = v ? segs[x] : 0u, c = v ? cls[x] : 0u;
+    const uint32_t opk = (uint32_t)__shfl((int)pk, (int)(ent >> 25), kWave);
+    uint32_t stot;
+    const uint32_t E = carry + wave_excl_scan(v ? (c >> 8) + 1 : 0u, &stot);
+    carry += stot;
+    if (v) {
+      const uint32_t pos = (uint32_t)(((int32_t)(opk << 16) >> 16) + (int32_t)E);
+      if (x != ((opk >> 16) & 0xFFu) || (opk >> 24)) img[pos] = '/';
+      const int id = (int)(c & 0xFFu) - 1;
+      const lds_u8* sp = L + (id >= 0 ? bn_src + bn.off[id] : stage_src + (ent & 0xFFFu));
+      const uint32_t n = id >= 0 ? (uint32_t)bn.len[id] : (ent >> 12) & 0x1FFFu;
+      lds_out_u8* dp = img + pos + 1;
+      for (uint32_t q = 0; q < n; q += 8) {
+        uint32_t b[8];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; t++) b[t] = sp[q + t];   // reads past n stay inside the stage / name table
+#pragma unroll
+        for (uint32_t t = 0; t < 8; t++)
+          if (q + t < n) dp[q + t] = (uint8_t)b[t];
+      }
+    }
+  }
+}
+
 // kMode bit 0 (kModeGeneral): user templatization rules or custom ids are
 // configured; without it the instance is compiled with neither (their loops
 // fold away, which is what keeps the default-config kernel off scratch).
@@ -1158,6 +1352,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
   __shared__ PlanSmem sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   Cfg cfg = load_cfg(a, sm.ns);
+  load_braced_names(cfg, sm.bn);   // workgroup barrier: before any wave may leave
   if (!(kMode & kModeGeneral)) {
     cfg.n_custom = 0;
     cfg.n_rules = 0;
@@ -1172,8 +1367,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
   uint32_t g = wave_first_group();
   if (g >= a.n_groups) return;
   const bool tm = (kMode & kModeDiag) && a.dbg != nullptr;
-  uint64_t t0 = 0, t_stage = 0, t_bm = 0, t_plan = 0, tt[3] = {0, 0, 0};
+  uint64_t t0 = 0, t_stage = 0, t_bm = 0, t_plan = 0, t_emit = 0, tt[3] = {0, 0, 0};
   uint32_t buf = 0;
+  const bool fused_cfg = sm.bn.ok && !(a.ablate & 2);
+  const lds_u8* L = (const lds_u8*)(void*)&sm;
+  const uint32_t bn_src = (uint32_t)((uint8_t*)sm.bn.b - (uint8_t*)&sm);
+  const uint64_t region = (uint64_t)wave_first_group() * a.scr_region;   // this wave's scratch
+  uint64_t scr_used = 0;
 
   // prologue: columns of groups g and g + stride, bytes of group g
   PlanCols cur = plan_cols(a, (uint64_t)g * kWave + lane);
@@ -1218,10 +1418,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     Plan p;
     uint32_t oflags = 0;
     // the list planner uses wave shuffles: called by the whole wave (lanes without a path add no segments)
-    bool listed = false;
+    bool listed = false, big = false;
+    uint32_t seg_off = 0;
     if (lo16 != ~0u && !(a.ablate & (1024 | 2)))
       listed = plan_group_list(cfg, stage32, (lds_cu4*)sm.bm[wv], sm.segs[wv], needs_path, cur.pr.off - lo16,
-                               cur.pr.len, cur.f, p, tm, tt);
+                               cur.pr.len, cur.f, p, tm, tt, sm.cls[wv], &seg_off, &big);
     if (gate == 1) {
       p.mode = M_RENAME_SLASH;
       p.len = 1;
@@ -1243,14 +1444,46 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
       oflags = OSE_OUT_SET_ATTR;                                                       // processor.go:259
       if ((cur.f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;     // :216-225
     }
+    const uint64_t sum = wave_sum_u64(p.len);
+    const uint64_t need = (sum + 15) & ~15ull;
+    // wave-uniform: the group is assembled here unless a user rule matched, a
+    // name id lies outside the braced table, the list planner gave up, or the
+    // image does not fit LDS or the wave's scratch region
+    const bool fast = fused_cfg && listed && __ballot(p.mode == M_RULE || big) == 0 && sum <= kImgCap &&
+                      scr_used + need <= a.scr_region;
     if (i < a.n_spans) {
       a.plan_len[i] = p.len;
-      a.plan_meta[i] = pack_meta(p.mode, p.lead, p.slow, oflags, p.field);
-      a.plan_code[i] = p.code;
+      a.url_out[i] = (uint8_t)oflags;
+      if (!fast) {
+        a.plan_meta[i] = pack_meta(p.mode, p.lead, p.slow, oflags, p.field);
+        a.plan_code[i] = p.code;
+      }
     }
-    const uint64_t sum = wave_sum_u64(p.len);
-    if (lane == 0) a.group_sum[g] = sum;
     if (tm) { const uint64_t t1 = clk(); t_plan += t1 - t0; t0 = t1; }
+    if (fast) {
+      lds_u4* img4 = (lds_u4*)sm.bm[wv];
+      const uint32_t n16 = (uint32_t)(need / 16);
+      uint32_t unused;
+      const uint32_t local = wave_excl_scan(p.len, &unused);
+      assemble_group((lds_out_u8*)sm.bm[wv], L, (uint32_t)(stage - (uint8_t*)&sm), sm.segs[wv], sm.cls[wv], sm.bn,
+                     bn_src, p, seg_off, local);
+      wave_lds_sync();
+      uint4* dst = reinterpret_cast<uint4*>(a.scratch + region + scr_used);
+      for (uint32_t k = lane; k < n16; k += kWave) {
+        const u32x4 v = img4[k];
+        dst[k] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      if (lane == 0) {
+        a.group_sum[g] = sum;
+        a.group_scr[g] = region + scr_used;
+      }
+      scr_used += need;
+    } else if (lane == 0) {
+      a.group_sum[g] = sum;
+      a.group_scr[g] = ~0ull;
+      if (sum) a.slow_groups[atomicAdd(a.slow_count, 1u)] = g;
+    }
+    if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
     if (!more) break;
     wave_lds_sync();   // every lane is done with this group's stage and bitmaps
     pf = pf2;
@@ -1264,6 +1497,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     atomicAdd((unsigned long long*)&a.dbg[1], (unsigned long long)t_bm);
     atomicAdd((unsigned long long*)&a.dbg[2], (unsigned long long)t_plan);
     atomicAdd((unsigned long long*)&a.dbg[3], 1ull);
+    atomicAdd((unsigned long long*)&a.dbg[5], (unsigned long long)t_emit);
     atomicAdd((unsigned long long*)&a.dbg[13], (unsigned long long)tt[0]);
     atomicAdd((unsigned long long*)&a.dbg[14], (unsigned long long)tt[1]);
     atomicAdd((unsigned long long*)&a.dbg[15], (unsigned long long)tt[2]);
@@ -1314,431 +1548,87 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// K3: emit.  One wave per 64-span group: the group's output bytes are
-// contiguous, so lanes assemble them in a per-wave LDS image (dword-aligned
-// to the global destination; lanes OR whole dwords in with ds_or_b32, which
-// composes the dwords two spans share) and the wave stores the image with
-// coalesced dword stores.
-typedef __attribute__((address_space(3))) uint32_t lds_w32;
-struct PutOr {
-  lds_w32* img;
-  uint32_t wpos, nb;   // wpos: image offset of acc's first byte (dword aligned); nb: bytes in acc
-  uint64_t acc;
-  __device__ PutOr(lds_w32* im, uint32_t start) : img(im), wpos(start & ~3u), nb(start & 3u), acc(0) {}
-  __device__ __forceinline__ void flush() {
-    __hip_atomic_fetch_or(&img[wpos >> 2], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    acc >>= 32;
-    wpos += 4;
-    nb -= 4;
-  }
-  __device__ __forceinline__ void byte(uint32_t c) {
-    acc |= (uint64_t)(c & 0xFFu) << (8 * nb);
-    if (++nb == 4) flush();
-  }
-  __device__ __forceinline__ void word(uint32_t x, uint32_t nv) {
-    if (nv < 4) x &= (1u << (8 * nv)) - 1u;
-    acc |= (uint64_t)x << (8 * nb);
-    nb += nv;
-    if (nb >= 4) flush();
-  }
-  __device__ __forceinline__ void finish() {
-    if (nb) __hip_atomic_fetch_or(&img[wpos >> 2], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
+// K4: template refs of every span, and the image of every group K1 assembled
+// moved from scratch to its place in the output arena.  One wave per group,
+// persistent, with the next group's columns in flight while one is copied.
+// Lane l of a round reads scratch chunk c = l + 64 r (16 bytes) and writes
+// destination dwords 4c..4c+3: dword k covers image bytes [4k - shift, +4),
+// a funnel shift of scratch dwords k-1 and k (dword 4c-1 from the lane below,
+// or from lane 63 of the previous round).  Dwords the group shares with its
+// neighbours are stored bytewise.
+struct CopyCols {
+  uint32_t len;
+  uint64_t base, gsum, so;
 };
-
-// Piece gather (the K3 fast path).  A group's output is a concatenation of
-// pieces, each a copy of LDS bytes: for M_DEFAULT the source stretch before a
-// templated segment (kept segments and the '/' separators are source bytes
-// already), then "{name}" from a braced name table; M_ORIG is "/" + body and
-// M_SLASH a lone "/".  Lanes list their span's pieces, then every lane
-// assembles an equal contiguous run of output dwords from the piece list, so
-// the per-byte work no longer follows the longest path of the group.
-// Groups with user rules, out-of-table names or >16 segments (plan `slow`)
-// take the per-span writer (emit_path).
-constexpr uint32_t kPieceCap = 448;   // per wave; a C2 group lists ~260
-constexpr uint32_t kBNames = 1024;    // braced names for template ids 0..14, '/' at byte 0
-constexpr uint32_t kSlashWords = kStage / 32 + 2;
-struct BracedNames {
-  __attribute__((aligned(16))) uint8_t b[kBNames + 16];
-  uint16_t off[16];
-  uint8_t len[16];
-  uint32_t ok;
-};
-struct EmitSmem {
-  NamesSmem ns;
-  BracedNames bn;
-  __attribute__((aligned(16))) uint8_t stage[kWaves][kStage + 16];
-  __attribute__((aligned(16))) uint32_t img[kWaves][kWaveOut / 4 + 4];
-  uint32_t slash[kWaves][kSlashWords];
-  uint32_t pdl[kWaves][kPieceCap];   // dst | len << 16 (output bytes of the group)
-  uint16_t psrc[kWaves][kPieceCap];  // source byte offset within EmitSmem
-};
-
-// "{name}" for ids 0..14 (the ids a plan code can carry), once per workgroup.
-__device__ void load_braced_names(const Cfg& cfg, BracedNames& bn) {
-  if (threadIdx.x == 0) {
-    const uint32_t nn = min(cfg.h->n_names, 15u);
-    uint32_t o = 4;
-    bool ok = true;
-    bn.b[0] = '/';
-    for (uint32_t id = 0; id < nn; id++) {
-      const uint32_t l = cfg.name(id).len + 2;
-      if (o + l > kBNames || l > 255) { ok = false; break; }
-      bn.off[id] = (uint16_t)o;
-      bn.len[id] = (uint8_t)l;
-      o += l;
-    }
-    bn.ok = ok ? 1u : 0u;
-  }
-  __syncthreads();
-  if (bn.ok && threadIdx.x < min(cfg.h->n_names, 15u)) {
-    const NameDev nm = cfg.name(threadIdx.x);
-    const uint8_t* src = cfg.blob + cfg.h->bytes_off + nm.off;
-    uint8_t* d = bn.b + bn.off[threadIdx.x];
-    d[0] = '{';
-    for (uint32_t q = 0; q < nm.len; q++) d[1 + q] = src[q];
-    d[1 + nm.len] = '}';
-  }
-  __syncthreads();
-}
-
-// first '/' in [a, e) (stage coordinates) from the slash bitmap, or e
-__device__ __forceinline__ uint32_t next_slash(const lds_u32* sl, uint32_t a, uint32_t e) {
-  while (a < e) {
-    const uint32_t r = a >> 5, sh = a & 31;
-    const uint32_t m = __builtin_amdgcn_alignbit(sl[r + 1], sl[r], sh) & (uint32_t)low_mask(e - a);
-    if (m) return a + __builtin_ctz(m);
-    a += 32;
-  }
-  return e;
-}
-
-// Appends the pieces of one lane (dst = output offset within the group) and
-// records, for every gathering lane L >= 1 whose first output byte
-// L * cb - shift this lane's output holds, the piece index (so no gathering
-// lane searches the list).  The lane tracks the next such L: one compare per
-// piece, one division per lane.
-struct PieceWriter {
-  uint32_t* pdl;
-  uint16_t* psrc;
-  uint16_t* start;
-  uint32_t idx, dst;
-  uint32_t nl, nl_byte, cb;   // next gathering lane whose first byte lies at or after dst, and that byte
-  __device__ PieceWriter(uint32_t* p, uint16_t* ps, uint16_t* st, uint32_t i, uint32_t d, uint32_t cb_, uint32_t shift)
-      : pdl(p), psrc(ps), start(st), idx(i), dst(d), cb(cb_) {
-    if (!start) {   // no start table: the gathering lanes search the list
-      nl = kWave;
-      nl_byte = ~0u;
-      return;
-    }
-    const uint32_t a = d + shift;                      // image byte of this lane's first output byte
-    uint32_t l = (uint32_t)((float)(a + cb - 1) * (1.0f / (float)cb));   // ceil(a / cb)
-    if (l * cb < a) l++;
-    if (l && (l - 1) * cb >= a) l--;
-    nl = l ? l : 1u;
-    nl_byte = nl * cb - shift;
-  }
-  __device__ __forceinline__ void put(uint32_t src, uint32_t len) {
-    pdl[idx] = dst | (len << 16);
-    psrc[idx] = (uint16_t)src;
-    dst += len;
-    while (nl_byte < dst && nl < (uint32_t)kWave) {   // the piece [dst - len, dst) holds lane nl's first byte
-      start[nl] = (uint16_t)idx;
-      nl++;
-      nl_byte += cb;
-    }
-    idx++;
-  }
-};
-
-// the last piece whose output offset is <= ob (pieces are in output order)
-__device__ __forceinline__ uint32_t find_piece(const uint32_t* pdl, uint32_t np, uint32_t ob) {
-  uint32_t lo = 0, n = np;
-  while (n > 1) {
-    const uint32_t h = n >> 1;
-    if ((pdl[lo + h] & 0xFFFFu) <= ob) lo += h;
-    n -= h;
-  }
-  return lo;
-}
-
-__device__ __forceinline__ uint32_t lds_word(const lds_u8* L, uint32_t p) {
-  const lds_u32* w = (const lds_u32*)(L + (p & ~3u));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], p & 3);
-}
-
-// The columns K3 reads for one group, loaded two groups ahead (with the
-// group's output base and size, so nothing is loaded after a stage prefetch
-// and waited for before the group is done).
-struct EmitCols {
-  uint32_t len, meta;
-  uint64_t code;
-  ose_strref pr;
-  uint64_t base, gsum;
-};
-__device__ __forceinline__ EmitCols emit_cols(const UrlKernelArgs& a, uint32_t g, int lane) {
-  EmitCols c{0, 0, 0, {0, 0}, 0, 0};
+__device__ __forceinline__ CopyCols copy_cols(const UrlKernelArgs& a, uint32_t g, int lane) {
+  CopyCols c{0, 0, 0, ~0ull};
   const uint64_t i = (uint64_t)g * kWave + lane;
-  if (g < a.n_groups) {
-    c.base = a.group_base[g];
-    c.gsum = a.group_sum[g];
-  }
-  if (i < a.n_spans) {
-    c.len = a.plan_len[i];
-    c.meta = a.plan_meta[i];
-    c.code = a.plan_code[i];
-    c.pr = a.path[i];
-  }
+  c.base = a.group_base[g];
+  c.gsum = a.group_sum[g];
+  c.so = a.group_scr[g];
+  if (i < a.n_spans) c.len = a.plan_len[i];
   return c;
 }
-__device__ __forceinline__ bool emit_needs_path(uint32_t meta) {
-  const uint32_t mode = meta & 7u;
-  return mode == M_RULE || mode == M_DEFAULT || mode == M_ORIG;
-}
-
-// image dword k <-> global bytes [base - shift + 4k, +4); bytes outside
-// [base, base + gtotal) belong to the neighbouring groups, so partial dwords
-// at the ends are stored bytewise
-__device__ __forceinline__ void store_image(const UrlKernelArgs& a, const lds_w32* img, uint64_t base, uint32_t shift,
-                                            uint64_t gtotal) {
+__global__ __launch_bounds__(kThreads) void url_copy_kernel(UrlKernelArgs a) {
   const int lane = threadIdx.x & 63;
-  uint8_t* gdst = a.out_arena + (base - shift);
-  const uint32_t nd = (uint32_t)((shift + gtotal + 3) / 4);
-  const uint64_t endb = shift + gtotal;
-  for (uint32_t k = lane; k < nd; k += kWave) {
-    const uint32_t w = img[k];
-    const uint32_t b0 = 4 * k;
-    if (b0 >= shift && b0 + 4 <= endb) {
-      *reinterpret_cast<uint32_t*>(gdst + b0) = w;
-    } else {
-      for (uint32_t q = 0; q < 4; q++)
-        if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(w >> (8 * q));
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
-  const uint32_t incl = wave_incl_sum_u32(v);
-  *total = lane_value(incl, kWave - 1);
-  return incl - v;
-}
-
-// K3: emit, piece-gather groups only (the others are listed for K3s).  One
-// wave per 64-span group, persistent, with the next group's bytes and the
-// group after's columns in flight while a group is assembled.
-template <int kMode>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void url_emit_kernel(UrlKernelArgs a) {
-  __shared__ EmitSmem sm;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  Cfg cfg = load_cfg(a, sm.ns);
-  if (!(kMode & kModeGeneral)) {
-    cfg.n_custom = 0;
-    cfg.n_rules = 0;
-    cfg.max_rule_nseg = 0;
-  }
-  if (!(kMode & kModeDiag)) {
-    cfg.ablate = 0;
-    a.ablate = 0;
-    a.dbg = nullptr;
-  }
-  load_braced_names(cfg, sm.bn);
-  const bool fast_cfg = sm.bn.ok && !(a.ablate & 2048);
-  const lds_u8* L = (const lds_u8*)(void*)&sm;
-  const uint32_t stage_src = (uint32_t)((uint8_t*)sm.stage[wv] - (uint8_t*)&sm);
-  const uint32_t bn_src = (uint32_t)((uint8_t*)sm.bn.b - (uint8_t*)&sm);
   const uint32_t stride = wave_stride();
   uint32_t g = wave_first_group();
   if (g >= a.n_groups) return;
-  const bool tm = (kMode & kModeDiag) && a.dbg != nullptr;
-  uint64_t t0 = 0, t_stage = 0, t_emit = 0, ts[5] = {0, 0, 0, 0, 0};
-  uint8_t* stage = sm.stage[wv];
-  lds_u32* stage32 = (lds_u32*)stage;
-  lds_w32* img = (lds_w32*)sm.img[wv];
-
-  EmitCols cur = emit_cols(a, g, lane);
-  EmitCols nxt = emit_cols(a, g + stride, lane);
-  bool np = emit_needs_path(cur.meta);
-  StagePf pf = stage_issue(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u);
-  stage_commit(pf, stage);
+  CopyCols cur = copy_cols(a, g, lane);
   for (;;) {
-    if (tm) t0 = clk();
-    const uint64_t i = (uint64_t)g * kWave + lane;
-    const bool valid = i < a.n_spans;
     const uint32_t g2 = g + stride;
     const bool more = g2 < a.n_groups;
-    const bool np2 = more && emit_needs_path(nxt.meta);
-    const StagePf pf2 = stage_issue(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u);
-    const EmitCols nn = emit_cols(a, g2 + stride, lane);
-    if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
-
-    const uint64_t base = cur.base, gtotal = cur.gsum;
-    const uint32_t len = cur.len, meta = cur.meta, mode = meta & 7u;
+    CopyCols nxt{};
+    if (more) nxt = copy_cols(a, g2, lane);
+    const uint64_t i = (uint64_t)g * kWave + lane;
     uint32_t unused;
-    const uint32_t local = wave_excl_scan(len, &unused);
-    const bool work = base + gtotal <= a.out_cap && !(a.ablate & 1);   // overflow: the scan flagged it
-    const uint32_t lo16 = pf.lo16;
-    const uint32_t shift = (uint32_t)(base & 3);
-    const uint32_t img_bytes = shift + (uint32_t)gtotal;
-    const uint32_t lead = (meta >> 3) & 1u, field = meta >> 7;
-    const bool slow = (meta >> 4) & 1u;
-    // piece counts: M_DEFAULT 2T+1 (T templated segments), M_ORIG 2, M_SLASH / M_RENAME_SLASH 1
-    uint32_t npc = 0;
-    bool lane_bad = false;
-    if (len) {
-      if (mode == M_DEFAULT) {
-        uint64_t x = cur.code;
-        x |= x >> 1;
-        x = (x | (x >> 2)) & 0x1111111111111111ull;
-        npc = 2 * (uint32_t)__builtin_popcountll(x) + 1;
-        lane_bad = slow || field == kNField;
-      } else if (mode == M_ORIG) {
-        npc = 2;
-        lane_bad = field == kNField;
-      } else if (mode == M_SLASH || mode == M_RENAME_SLASH) {
-        npc = 1;
-      } else {
-        lane_bad = true;   // M_RULE
-      }
-    }
-    uint32_t npieces;
-    const uint32_t poff = wave_excl_scan(npc, &npieces);
-    const bool fast = work && fast_cfg && img_bytes <= kWaveOut && lo16 != ~0u && __ballot(lane_bad) == 0 &&
-                      npieces <= kPieceCap;   // wave-uniform
-    if (tm) { const uint64_t t1 = clk(); ts[0] += t1 - t0; }
-    if (fast) {
-      const ose_strref pr = emit_needs_path(meta) ? cur.pr : ose_strref{0, 0};
-      lds_u32* sl = (lds_u32*)sm.slash[wv];
-      if (__ballot(mode == M_DEFAULT && len != 0)) {   // '/' bitmap of the staged bytes
-        const uint32_t rows = (pf.bytes + 31) / 32;
-        for (uint32_t r = lane; r < rows; r += kWave) {
-          const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
-          const u32x4 v0 = src[0], v1 = src[1];
-          const uint32_t xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-          uint32_t acc = 0;
-#pragma unroll
-          for (int d = 0; d < 8; d++) acc |= movemask4(swar_eq(xs[d], '/')) << (4 * d);
-          sm.slash[wv][r] = acc;
-        }
-        wave_lds_sync();
-      }
-      if (tm) { const uint64_t t1 = clk(); ts[1] += t1 - t0; }
-      const uint32_t nd = (img_bytes + 3) / 4;
-      const uint32_t cb = 4 * ((nd + kWave - 1) / kWave);
-      PieceWriter pw(sm.pdl[wv], sm.psrc[wv], nullptr, poff, local, cb, shift);
-      if (len) {
-        if (mode == M_DEFAULT) {
-          const uint32_t p0 = pr.off - lo16, n = field;
-          uint32_t cs = 0, s = lead;
-          const uint32_t b0 = p0 & 31, r0 = p0 >> 5;
-          if (b0 + n <= 192) {
-            // the path's '/' bits from one read of 6 slash-bitmap rows (window
-            // bit 0 = stage byte 32 r0), kept to [lead, n) of the path
-            uint32_t w[6];
-#pragma unroll
-            for (int j = 0; j < 6; j++) w[j] = sl[min(r0 + j, kSlashWords - 1)];
-            uint64_t h[3];
-#pragma unroll
-            for (int j = 0; j < 3; j++)
-              h[j] = (w[2 * j] | ((uint64_t)w[2 * j + 1] << 32)) & half_mask(b0 + lead, b0 + n, 64 * j);
-            for (uint64_t c = (a.ablate & 8192) ? 0 : cur.code; c; c >>= 4) {
-              // first '/' at path offset >= s, else n
-              const uint32_t q = b0 + s;
-              uint32_t e = n;
-#pragma unroll
-              for (int j = 2; j >= 0; j--) {
-                const uint64_t m = h[j] & ~(q > 64u * j ? low_mask(q - 64u * j) : 0ull);
-                if (m) e = 64u * j + (uint32_t)__builtin_ctzll(m) - b0;
-              }
-              const uint32_t nib = (uint32_t)(c & 15u);
-              if (nib) {
-                pw.put(stage_src + p0 + cs, s - cs);
-                pw.put(bn_src + sm.bn.off[nib - 1], sm.bn.len[nib - 1]);
-                cs = e;
-              }
-              s = e + 1;
-            }
+    const uint32_t local = wave_excl_scan(cur.len, &unused);
+    const uint64_t base = cur.base, gsum = cur.gsum;
+    if (i < a.n_spans) a.tmpl[i] = ose_strref{(uint32_t)(base + local), cur.len};
+    // K3s's groups, empty ones and an overflowing batch (the scan flagged it) copy nothing
+    if (cur.so != ~0ull && gsum != 0 && base + gsum <= a.out_cap) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.scratch + cur.so);
+      const uint32_t shift = (uint32_t)(base & 3);
+      uint8_t* gdst = a.out_arena + (base - shift);
+      const uint64_t endb = shift + gsum;
+      const uint32_t n16 = (uint32_t)((gsum + 15) / 16);
+      const uint32_t nchunk = (uint32_t)((endb + 15) / 16);   // destination chunks of 4 dwords
+      uint32_t carry = 0;
+      for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
+        const uint32_t c = c0 + (uint32_t)lane;
+        const uint4 v = c < n16 ? src[c] : make_uint4(0, 0, 0, 0);
+        uint32_t pw = (uint32_t)__shfl_up((int)v.w, 1, kWave);
+        if (lane == 0) pw = carry;
+        carry = lane_value(v.w, kWave - 1);
+        const uint32_t sh = 4 - shift;
+        const uint32_t w0 = shift ? __builtin_amdgcn_alignbyte(v.x, pw, sh) : v.x;
+        const uint32_t w1 = shift ? __builtin_amdgcn_alignbyte(v.y, v.x, sh) : v.y;
+        const uint32_t w2 = shift ? __builtin_amdgcn_alignbyte(v.z, v.y, sh) : v.z;
+        const uint32_t w3 = shift ? __builtin_amdgcn_alignbyte(v.w, v.z, sh) : v.w;
+        if (c < nchunk) {
+          const uint64_t b0 = 16ull * c;
+          if (b0 >= shift && b0 + 16 <= endb) {
+            uint32_t* d = reinterpret_cast<uint32_t*>(gdst + b0);
+            d[0] = w0;
+            d[1] = w1;
+            d[2] = w2;
+            d[3] = w3;
           } else {
-            for (uint64_t c = (a.ablate & 8192) ? 0 : cur.code; c; c >>= 4) {
-              const uint32_t e = next_slash(sl, p0 + s, p0 + n) - p0;
-              const uint32_t nib = (uint32_t)(c & 15u);
-              if (nib) {
-                pw.put(stage_src + p0 + cs, s - cs);
-                pw.put(bn_src + sm.bn.off[nib - 1], sm.bn.len[nib - 1]);
-                cs = e;
-              }
-              s = e + 1;
-            }
+            const uint32_t ws[4] = {w0, w1, w2, w3};
+#pragma unroll
+            for (uint32_t q = 0; q < 16; q++)
+              if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(ws[q >> 2] >> (8 * (q & 3)));
           }
-          pw.put(stage_src + p0 + cs, n - cs);
-        } else if (mode == M_ORIG) {
-          pw.put(bn_src, 1);
-          pw.put(stage_src + (pr.off - lo16) + lead, field - lead);
-        } else {
-          pw.put(bn_src, 1);
         }
       }
-      wave_lds_sync();
-      if (tm) { const uint64_t t1 = clk(); ts[2] += t1 - t0; }
-      // each lane assembles image dwords [lane*q, lane*q + q)
-      const uint32_t q = cb / 4, d0 = lane * q, d1 = min(nd, d0 + q);
-      if (d0 < d1 && gtotal != 0) {
-        const uint32_t* pdl = sm.pdl[wv];
-        const uint16_t* psrc = sm.psrc[wv];
-        const uint32_t ob = lane ? 4 * d0 - shift : 0u;
-        uint32_t idx = find_piece(pdl, npieces, ob);
-        uint32_t pd = pdl[idx];
-        uint32_t src = psrc[idx] + (ob - (pd & 0xFFFFu));
-        uint32_t rem = (pd >> 16) - (ob - (pd & 0xFFFFu));
-        for (uint32_t d = d0; d < d1; d++) {
-          uint32_t w = 0, have = (d == 0) ? shift : 0u;
-          while (have < 4) {
-            while (rem == 0 && idx + 1 < npieces) {
-              pd = pdl[++idx];
-              src = psrc[idx];
-              rem = pd >> 16;
-            }
-            if (rem == 0) break;   // end of the group's output
-            const uint32_t x = lds_word(L, src);
-            const uint32_t take = min(rem, 4u - have);
-            w |= (take == 4 ? x : (x & ((1u << (8 * take)) - 1u))) << (8 * have);
-            have += take;
-            src += take;
-            rem -= take;
-          }
-          img[d] = w;
-        }
-      }
-    } else if (work && lane == 0) {
-      a.slow_groups[atomicAdd(a.slow_count, 1u)] = g;
     }
-    wave_lds_sync();   // image writes and stage reads of this group are done
-    if (tm) { const uint64_t t1 = clk(); ts[3] += t1 - t0; }
-    if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
-    // The next group's stage is committed before this group's stores are
-    // issued: waiting for the prefetch (older) then never waits for them.
-    if (more) stage_commit(pf2, stage);
-    if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
-    if (valid) {
-      a.url_out[i] = (uint8_t)((meta >> 5) & 3u);
-      a.tmpl[i] = ose_strref{(uint32_t)(base + local), len};
-    }
-    if (fast) store_image(a, img, base, shift, gtotal);
-    if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; ts[4] += t1 - t0; }
     if (!more) break;
-    pf = pf2;
     cur = nxt;
-    nxt = nn;
     g = g2;
-  }
-  if (tm && lane == 0) {
-    atomicAdd((unsigned long long*)&a.dbg[4], (unsigned long long)t_stage);
-    atomicAdd((unsigned long long*)&a.dbg[5], (unsigned long long)t_emit);
-    atomicAdd((unsigned long long*)&a.dbg[6], 1ull);
-    for (int q = 0; q < 5; q++) atomicAdd((unsigned long long*)&a.dbg[8 + q], (unsigned long long)ts[q]);
   }
 }
 
-// K3s: the groups K3 listed (user rules, plan `slow`, names outside the
+// K3s: the groups K1 listed (user rules, plan `slow`, names outside the
 // braced table, an output image or a stage larger than LDS), with the
 // per-span writer (emit_path).  One wave per listed group; exits at once when
 // the list is empty.
@@ -1761,6 +1651,7 @@ __global__ __launch_bounds__(kThreads) void url_emit_slow_kernel(UrlKernelArgs a
     const uint64_t i = (uint64_t)g * kWave + lane;
     const EmitCols c = emit_cols(a, g, lane);
     const uint64_t base = c.base, gtotal = c.gsum;
+    if (base + gtotal > a.out_cap) continue;   // overflow: the scan flagged it
     const uint32_t len = c.len, meta = c.meta, mode = meta & 7u;
     uint32_t unused;
     const uint32_t local = wave_excl_scan(len, &unused);
@@ -1817,16 +1708,21 @@ static int url_mode(const UrlKernelArgs& a) {
   return (a.general ? kModeGeneral : 0) | ((a.ablate || a.dbg) ? kModeDiag : 0);
 }
 template <int M>
-static void launch_plan_mode(const UrlKernelArgs& a, hipStream_t st) {
-  static const uint32_t cap = resident_blocks(url_plan_kernel<M>, 0);
-  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
-  hipLaunchKernelGGL(url_plan_kernel<M>, dim3(blocks), dim3(kThreads), 0, st, a);
+static uint32_t plan_blocks(const UrlKernelArgs& a) {
+  static const uint32_t cap = std::min<uint32_t>(resident_blocks(url_plan_kernel<M>, 0), kUrlMaxWaves / kWaves);
+  return std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
 }
 template <int M>
-static void launch_emit_mode(const UrlKernelArgs& a, hipStream_t st) {
-  static const uint32_t cap = resident_blocks(url_emit_kernel<M>, 0);
-  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
-  hipLaunchKernelGGL(url_emit_kernel<M>, dim3(blocks), dim3(kThreads), 0, st, a);
+static void launch_plan_mode(const UrlKernelArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(url_plan_kernel<M>, dim3(plan_blocks<M>(a)), dim3(kThreads), 0, st, a);
+}
+uint32_t url_plan_waves(const UrlKernelArgs& a) {
+  switch (url_mode(a)) {
+    case 0: return plan_blocks<0>(a) * kWaves;
+    case 1: return plan_blocks<1>(a) * kWaves;
+    case 2: return plan_blocks<2>(a) * kWaves;
+    default: return plan_blocks<3>(a) * kWaves;
+  }
 }
 void launch_url_plan(const UrlKernelArgs& a, hipStream_t st) {
   switch (url_mode(a)) {
@@ -1839,13 +1735,10 @@ void launch_url_plan(const UrlKernelArgs& a, hipStream_t st) {
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(url_scan_kernel, dim3(a.n_scan_tiles), dim3(kScanThreads), 0, st, a);
 }
-void launch_url_emit(const UrlKernelArgs& a, hipStream_t st) {
-  switch (url_mode(a)) {
-    case 0: launch_emit_mode<0>(a, st); break;
-    case 1: launch_emit_mode<1>(a, st); break;
-    case 2: launch_emit_mode<2>(a, st); break;
-    default: launch_emit_mode<3>(a, st); break;
-  }
+void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
+  static const uint32_t cap = resident_blocks(url_copy_kernel, 0);
+  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL(url_copy_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
 }
 void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st) {
   // the list length is on the device: a grid for every group, blocks past it exit at once
