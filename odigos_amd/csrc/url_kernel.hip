@@ -167,6 +167,7 @@ struct Cfg {
   const uint8_t* blob;
   lds_cfg* h;             // header copy in LDS: fields are read where used, no registers held
   uint32_t n_custom, n_rules, max_rule_nseg;   // the fields every span's plan tests
+  uint32_t names_off;
   lds_u8* names;          // first kNamesLds bytes of the bytes section, staged in LDS
   uint32_t names_len;
   uint32_t ablate;        // diagnostics (UrlKernelArgs::ablate)
@@ -814,7 +815,7 @@ __device__ __forceinline__ Cfg load_cfg(const UrlKernelArgs& a, NamesSmem& ns) {
     ns.name_tab[threadIdx.x] = reinterpret_cast<const NameDev*>(a.cfg + h.names_off)[threadIdx.x];
   if (threadIdx.x == 0) ns.hdr = h;
   __syncthreads();
-  return Cfg{a.cfg, (lds_cfg*)&ns.hdr, h.n_custom, h.n_rules, h.max_rule_nseg, (lds_u8*)ns.names, names_len, a.ablate,
+  return Cfg{a.cfg, (lds_cfg*)&ns.hdr, h.n_custom, h.n_rules, h.max_rule_nseg, h.names_off, (lds_u8*)ns.names, names_len, a.ablate,
              (const __attribute__((address_space(3))) NameDev*)ns.name_tab};
 }
 
@@ -1079,6 +1080,17 @@ __device__ __forceinline__ uint64_t half_mask(uint32_t lo, uint32_t hi, uint32_t
   return low_mask(h) & ~low_mask(l);
 }
 
+// length of name `id`: the LDS table for the first kNameTab names, else a
+// call (a global load inline would make the classify loop wait for every
+// vector-memory operation in flight, the next group's stage included)
+__device__ __noinline__ uint32_t name_len_global(const uint8_t* blob, uint32_t names_off, uint32_t id) {
+  return reinterpret_cast<const NameDev*>(blob + names_off)[id].len;
+}
+__device__ __forceinline__ uint32_t name_len(const Cfg& cfg, uint32_t id) {
+  if (id < kNameTab) return cfg.name_tab[id].len;
+  return name_len_global(cfg.blob, cfg.names_off, id);
+}
+
 // getSegmentTemplatizationString for a segment longer than a 64-bit window
 // (rare: kept out of line so the list planner's registers stay small)
 __device__ __noinline__ int classify_long(const Cfg& cfg, const LdsReader& rd, uint32_t s, uint32_t L) {
@@ -1217,8 +1229,10 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
     } else {
       id = classify_long(cfg, rd0, s, L);   // segment longer than 64 bytes
     }
-    const uint32_t out = id >= 0 ? cfg.name((uint32_t)id).len + 2 : L;
-    cls[x] = (out << 8) | (uint32_t)(id + 1);
+    const uint32_t out = id >= 0 ? name_len(cfg, (uint32_t)id) + 2 : L;
+    // id + 1 in 8 bits: 255 stands for every id >= 254 (such plans are `slow`
+    // and re-classify their segments when emitted)
+    cls[x] = (out << 8) | min((uint32_t)(id + 1), 255u);
   }
   wave_lds_sync();
   if (tm) { const uint64_t c1 = clk(); tt[1] += c1 - c0; c0 = c1; }
@@ -1378,11 +1392,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
   // prologue: columns of groups g and g + stride, bytes of group g
   PlanCols cur = plan_cols(a, (uint64_t)g * kWave + lane);
   PlanCols nxt = plan_cols(a, (uint64_t)(g + stride) * kWave + lane);
+  PlanCols nn{};
   bool np = plan_gate(cur) == 2;
   StageDma pf = stage_dma(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u, sm.stage[0][wv]);
+  bool first = true;
   for (;;) {
     if (tm) t0 = clk();
     wait_dma();   // this group's bytes and the next group's columns have landed
+    // the column sets move only here, after the wait: a copy of registers
+    // whose loads are in flight would wait for every store issued since
+    if (!first) {
+      cur = nxt;
+      nxt = nn;
+    }
+    first = false;
     uint8_t* stage = sm.stage[buf][wv];
     lds_u32* stage32 = (lds_u32*)stage;
     const uint64_t i = (uint64_t)g * kWave + lane;
@@ -1392,7 +1415,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     const bool np2 = more && plan_gate(nxt) == 2;
     const StageDma pf2 =
         stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[buf ^ 1][wv]);
-    const PlanCols nn = plan_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
+    nn = plan_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
     if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
 
     const uint32_t gate = plan_gate(cur);
@@ -1488,8 +1511,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     wave_lds_sync();   // every lane is done with this group's stage and bitmaps
     pf = pf2;
     buf ^= 1;
-    cur = nxt;
-    nxt = nn;
     g = g2;
   }
   if (tm && lane == 0) {

@@ -1,0 +1,14 @@
+#!/bin/bash
+# trace_eval with a three-set prefetch ring: sampling GPU tests, C3, C5 and C4 benches
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_sampling_random.py tests/test_sampling_kats.py tests/test_exchange.py tests/test_span_attribute.py > gpurun_out/r2y_tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/r2y_tests.log
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r2y_tests.log | head -30; exit $rc; fi
+for wl in sampling zipf fused; do
+  timeout -k 10 500 python -u bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r2y_bench_$wl.log 2>&1 || { tail -30 gpurun_out/r2y_bench_$wl.log; exit 1; }
+  echo "== $wl"; grep -o '"ms_per_step": [0-9.]*' gpurun_out/r2y_bench_$wl.log
+  grep -o '"kernel_ms_each": {[^}]*}' gpurun_out/r2y_bench_$wl.log
+  grep -o '"parity_vs_oracle": [a-z]*' gpurun_out/r2y_bench_$wl.log
+done
