@@ -365,7 +365,7 @@ def main():
         for f in wl.get("null_outputs", ()):
             setattr(db.outs, f, None)    # outputs the shim does not read (per-trace diagnostics)
         n_units = gen.cols.n_spans
-        eng.reserve(n_units)
+        eng.reserve(n_units, gen.cols.arena_bytes)
         if world > 1 and stages & native.STAGE_SAMPLE:
             # fold each rank's spans into partial records, route them
             # to each trace's owner GPU (RCCL over xGMI), decide there, bring keep

@@ -133,7 +133,9 @@ typedef struct ose_columns {
   uint32_t n_scopes;
   uint32_t n_attrsets;      /* traffic-metrics attribute sets (res_attrset range) */
   uint32_t _pad;
-  uint64_t arena_bytes;
+  uint64_t arena_bytes;     /* bytes of `arena`; also sizes the TEMPLATE stage's scratch for
+                               the assembled templates (an understated value is not an error:
+                               the groups that do not fit take the slower per-span writer) */
   const uint8_t* arena;     /* all string bytes referenced by ose_strref columns */
 
   /* per span */
@@ -311,7 +313,9 @@ int ose_process_device(ose_engine* eng, const ose_columns* cols,
                        uint32_t group_mode, const ose_rand* rnd, void* hip_stream);
 
 /* Workspace pre-sizing for ose_process_device (so the timed call performs no
- * allocation; required before a hipGraph capture).                          */
+ * allocation; required before a hipGraph capture).  arena_bytes: the largest
+ * ose_columns.arena_bytes the calls will pass (the TEMPLATE stage's scratch
+ * is sized from it).                                                        */
 int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes);
 
 /* Per-kernel device time, measured with hipEvents recorded on the stream

@@ -1,0 +1,13 @@
+#!/bin/bash
+# 8-class bitmaps: URL GPU tests, C2 and C4 benches, then C3 / C5 / owner lines
+set -o pipefail
+mkdir -p gpurun_out/c2
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_url_kats.py tests/test_url_random.py tests/test_size.py > gpurun_out/c2/tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/c2/tests.log
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/c2/tests.log | head -30; exit $rc; fi
+for wl in url fused zipf sampling owner; do
+  st=20; wu=5; if [ $wl = owner ]; then st=10; wu=3; fi
+  timeout -k 10 500 python -u bench.py --workload $wl --steps $st --warmup $wu > gpurun_out/c2/bench_$wl.log 2>&1 || { tail -30 gpurun_out/c2/bench_$wl.log; exit 1; }
+  echo "== $wl"; grep -o '"ms_per_step": [0-9.]*' gpurun_out/c2/bench_$wl.log; grep -o '"frac": [0-9.]*' gpurun_out/c2/bench_$wl.log; grep -o '"kernel_ms_each": {[^}]*}' gpurun_out/c2/bench_$wl.log; grep -o '"parity_vs_oracle": [a-z]*' gpurun_out/c2/bench_$wl.log
+done
