@@ -1590,62 +1590,91 @@ __device__ __forceinline__ CopyCols copy_cols(const UrlKernelArgs& a, uint32_t g
   if (i < a.n_spans) c.len = a.plan_len[i];
   return c;
 }
+// one destination round (up to 64 chunks of 16 bytes) of a group's image: v
+// holds scratch chunk c = c0 + lane
+__device__ __forceinline__ void copy_round(uint8_t* gdst, uint32_t shift, uint64_t endb, uint32_t c0, uint32_t nchunk,
+                                           const uint4& v, uint32_t& carry) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t c = c0 + (uint32_t)lane;
+  uint32_t pw = (uint32_t)__shfl_up((int)v.w, 1, kWave);
+  if (lane == 0) pw = carry;
+  carry = lane_value(v.w, kWave - 1);
+  const uint32_t sh = 4 - shift;
+  const uint32_t w0 = shift ? __builtin_amdgcn_alignbyte(v.x, pw, sh) : v.x;
+  const uint32_t w1 = shift ? __builtin_amdgcn_alignbyte(v.y, v.x, sh) : v.y;
+  const uint32_t w2 = shift ? __builtin_amdgcn_alignbyte(v.z, v.y, sh) : v.z;
+  const uint32_t w3 = shift ? __builtin_amdgcn_alignbyte(v.w, v.z, sh) : v.w;
+  if (c < nchunk) {
+    const uint64_t b0 = 16ull * c;
+    if (b0 >= shift && b0 + 16 <= endb) {
+      uint32_t* d = reinterpret_cast<uint32_t*>(gdst + b0);
+      d[0] = w0;
+      d[1] = w1;
+      d[2] = w2;
+      d[3] = w3;
+    } else {
+      const uint32_t ws[4] = {w0, w1, w2, w3};
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++)
+        if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(ws[q >> 2] >> (8 * (q & 3)));
+    }
+  }
+}
+// A group's copy plan: nothing to copy for K3s's groups, empty ones and an
+// overflowing batch (the scan flagged it)
+struct CopyJob {
+  const uint4* src;
+  uint8_t* gdst;
+  uint32_t shift, n16, nchunk;
+  uint64_t endb;
+  bool on;
+};
+__device__ __forceinline__ CopyJob copy_job(const UrlKernelArgs& a, const CopyCols& c) {
+  CopyJob j{};
+  j.on = c.so != ~0ull && c.gsum != 0 && c.base + c.gsum <= a.out_cap;
+  if (!j.on) return j;
+  j.src = reinterpret_cast<const uint4*>(a.scratch + c.so);
+  j.shift = (uint32_t)(c.base & 3);
+  j.gdst = a.out_arena + (c.base - j.shift);
+  j.endb = j.shift + c.gsum;
+  j.n16 = (uint32_t)((c.gsum + 15) / 16);
+  j.nchunk = (uint32_t)((j.endb + 15) / 16);
+  return j;
+}
+__device__ __forceinline__ uint4 copy_load(const CopyJob& j, uint32_t c0) {
+  const uint32_t c = c0 + (threadIdx.x & 63);
+  return j.on && c < j.n16 ? j.src[c] : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void copy_rest(const CopyJob& j, uint4 v, uint32_t& carry) {
+  copy_round(j.gdst, j.shift, j.endb, 0, j.nchunk, v, carry);
+  for (uint32_t c0 = kWave; c0 < j.nchunk; c0 += kWave) {
+    v = copy_load(j, c0);
+    copy_round(j.gdst, j.shift, j.endb, c0, j.nchunk, v, carry);
+  }
+}
+// Two groups per iteration (g and g + stride): their columns are loaded
+// together and their first scratch rounds together, so a wave waits two
+// memory round trips per two groups.
 __global__ __launch_bounds__(kThreads) void url_copy_kernel(UrlKernelArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t stride = wave_stride();
-  uint32_t g = wave_first_group();
-  if (g >= a.n_groups) return;
-  CopyCols cur = copy_cols(a, g, lane);
-  for (;;) {
-    const uint32_t g2 = g + stride;
-    const bool more = g2 < a.n_groups;
-    CopyCols nxt{};
-    if (more) nxt = copy_cols(a, g2, lane);
-    const uint64_t i = (uint64_t)g * kWave + lane;
+  for (uint32_t g = wave_first_group(); g < a.n_groups; g += 2 * stride) {
+    const uint32_t gb = g + stride;
+    const bool hb = gb < a.n_groups;
+    const CopyCols A = copy_cols(a, g, lane);
+    CopyCols B{0, 0, 0, ~0ull};
+    if (hb) B = copy_cols(a, gb, lane);
     uint32_t unused;
-    const uint32_t local = wave_excl_scan(cur.len, &unused);
-    const uint64_t base = cur.base, gsum = cur.gsum;
-    if (i < a.n_spans) a.tmpl[i] = ose_strref{(uint32_t)(base + local), cur.len};
-    // K3s's groups, empty ones and an overflowing batch (the scan flagged it) copy nothing
-    if (cur.so != ~0ull && gsum != 0 && base + gsum <= a.out_cap) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.scratch + cur.so);
-      const uint32_t shift = (uint32_t)(base & 3);
-      uint8_t* gdst = a.out_arena + (base - shift);
-      const uint64_t endb = shift + gsum;
-      const uint32_t n16 = (uint32_t)((gsum + 15) / 16);
-      const uint32_t nchunk = (uint32_t)((endb + 15) / 16);   // destination chunks of 4 dwords
-      uint32_t carry = 0;
-      for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
-        const uint32_t c = c0 + (uint32_t)lane;
-        const uint4 v = c < n16 ? src[c] : make_uint4(0, 0, 0, 0);
-        uint32_t pw = (uint32_t)__shfl_up((int)v.w, 1, kWave);
-        if (lane == 0) pw = carry;
-        carry = lane_value(v.w, kWave - 1);
-        const uint32_t sh = 4 - shift;
-        const uint32_t w0 = shift ? __builtin_amdgcn_alignbyte(v.x, pw, sh) : v.x;
-        const uint32_t w1 = shift ? __builtin_amdgcn_alignbyte(v.y, v.x, sh) : v.y;
-        const uint32_t w2 = shift ? __builtin_amdgcn_alignbyte(v.z, v.y, sh) : v.z;
-        const uint32_t w3 = shift ? __builtin_amdgcn_alignbyte(v.w, v.z, sh) : v.w;
-        if (c < nchunk) {
-          const uint64_t b0 = 16ull * c;
-          if (b0 >= shift && b0 + 16 <= endb) {
-            uint32_t* d = reinterpret_cast<uint32_t*>(gdst + b0);
-            d[0] = w0;
-            d[1] = w1;
-            d[2] = w2;
-            d[3] = w3;
-          } else {
-            const uint32_t ws[4] = {w0, w1, w2, w3};
-#pragma unroll
-            for (uint32_t q = 0; q < 16; q++)
-              if (b0 + q >= shift && b0 + q < endb) gdst[b0 + q] = (uint8_t)(ws[q >> 2] >> (8 * (q & 3)));
-          }
-        }
-      }
-    }
-    if (!more) break;
-    cur = nxt;
-    g = g2;
+    const uint32_t la = wave_excl_scan(A.len, &unused), lb = wave_excl_scan(B.len, &unused);
+    const uint64_t ia = (uint64_t)g * kWave + lane, ib = (uint64_t)gb * kWave + lane;
+    const CopyJob ja = copy_job(a, A), jb = copy_job(a, B);
+    const uint4 va = copy_load(ja, 0), vb = copy_load(jb, 0);
+    if (ia < a.n_spans) a.tmpl[ia] = ose_strref{(uint32_t)(A.base + la), A.len};
+    if (hb && ib < a.n_spans) a.tmpl[ib] = ose_strref{(uint32_t)(B.base + lb), B.len};
+    uint32_t carry = 0;
+    if (ja.on) copy_rest(ja, va, carry);
+    carry = 0;
+    if (jb.on) copy_rest(jb, vb, carry);
   }
 }
 

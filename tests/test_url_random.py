@@ -156,3 +156,49 @@ def test_gpu_url_parity_full_c2():
     # BASELINE.json configs[1]: 10M spans, C2 mix, byte-exact against the oracle
     ns, used = run_gpu_vs_oracle({}, "url", 0x0D160002, 10_000_000)
     assert ns == 10_000_000 and used > 0
+
+
+def _gpu_vs_oracle_cols(g, cfg, arena_bytes=None):
+    """run_gpu_vs_oracle on prepared columns; arena_bytes overrides what the
+    device batch declares (it sizes the plan kernel's scratch)."""
+    import torch
+    eng = Engine({"odigosurltemplate": cfg})
+    db = DeviceBatch(g.cols)
+    if arena_bytes is not None:
+        db.cols.arena_bytes = arena_bytes
+    eng.process_device(db, native.STAGE_TEMPLATE)
+    torch.cuda.synchronize()
+    assert int(db.out_numpy("device_status", np.uint32)[0]) == 0
+    ho = HostOutputs(g.cols)
+    assert UrlOracle(cfg).process(g.cols, ho.outs, nthreads=8) == 0
+    ns = g.cols.n_spans
+    np.testing.assert_array_equal(db.out_numpy("url_out")[:ns], ho.view("url_out", np.uint8)[:ns])
+    gt = db.out_numpy("tmpl", np.uint32)[: 2 * ns].reshape(-1, 2)
+    ot = ho.view("tmpl", np.uint32)[: 2 * ns].reshape(-1, 2)
+    mask = ho.view("url_out", np.uint8)[:ns] != 0
+    np.testing.assert_array_equal(gt[mask], ot[mask])
+    used = db.used()
+    assert used == int(ho.used[0])
+    np.testing.assert_array_equal(db.out_numpy("tmpl_arena")[:used], ho.bufs["tmpl_arena"][:used])
+    return used
+
+
+@pytest.mark.gpu
+def test_gpu_url_parity_group_images_over_lds():
+    # every path stretched to 200 arena bytes (overlapping its neighbours'):
+    # a group's template outgrows the plan kernel's LDS image, so the group is
+    # listed for url_emit_slow_kernel and url_copy_kernel leaves its bytes alone
+    g = Generator("url", seed=0x0D160032, n_spans=20_000)
+    path = g.array("path").view(np.uint32).reshape(-1, 2)
+    has = path[:, 1] > 0
+    path[has, 1] = np.minimum(200, g.cols.arena_bytes - path[has, 0]).astype(np.uint32)
+    used = _gpu_vs_oracle_cols(g, {})
+    assert used > 0
+
+
+@pytest.mark.gpu
+def test_gpu_url_parity_scratch_regions_overflow():
+    # arena_bytes understated to 0: each plan wave's scratch region holds only
+    # a few group images, the rest fall back to the per-span writer
+    g = Generator("url", seed=0x0D160042, n_spans=2_000_000, threads=8)
+    _gpu_vs_oracle_cols(g, {}, arena_bytes=0)
