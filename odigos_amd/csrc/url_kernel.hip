@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../../include/odigos_amd.h"
 #include "device_common.hpp"
@@ -1786,8 +1787,15 @@ void launch_url_scan(const UrlKernelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(url_scan_kernel, dim3(a.n_scan_tiles), dim3(kScanThreads), 0, st, a);
 }
 void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
-  static const uint32_t cap = resident_blocks(url_copy_kernel, 0);
-  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
+  // far more workgroups than fit at once (C4 sweep, tools/gpu_r2_knob.sh:
+  // resident grid 1.01 ms, 16384 blocks 0.93, 65536 0.92): a wave's two
+  // groups are two memory round trips, and the waves waiting on them are what
+  // keeps HBM busy
+  static const uint32_t cap = [] {
+    const char* g = getenv("OSE_COPY_GRID");   // tuning
+    return g ? std::max<uint32_t>(1, (uint32_t)strtoul(g, nullptr, 0)) : 65536u;
+  }();
+  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + 2 * kWaves - 1) / (2 * kWaves));
   hipLaunchKernelGGL(url_copy_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
 }
 void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st) {
