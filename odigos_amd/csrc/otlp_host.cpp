@@ -1019,7 +1019,8 @@ char* osehost_otlp_walk(const char* cfg_json, const uint8_t* pb, size_t len) {
     Walked w;
     const auto t0 = std::chrono::steady_clock::now();
     ResCache cache;
-    if (err.empty() && !walk(ctx, cache, pb, len, w)) err = w.err;
+    const bool gpu_scopes = cfg.get("gpu_scopes") != nullptr;   // the walk ose_otlp_decode runs (ScopeSpans left to the GPU)
+    if (err.empty() && !walk(ctx, cache, pb, len, w, gpu_scopes)) err = w.err;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (!err.empty()) { fail(OSE_EINVAL, err); return nullptr; }
     if (cfg.get("timing_only")) {   // diagnostics: the walk's wall time only

@@ -452,3 +452,17 @@ def test_walk_threaded_generated_batch():
 
 def test_walk_rejects_malformed():
     assert _walk(CFG, b"\x0a\x05\x12\x03\x12") is None
+
+
+def test_walk_gpu_scopes_resources_match():
+    # the walk ose_otlp_decode runs leaves ScopeSpans to the GPU: the host
+    # lists no span, and its resource columns equal the full walk's
+    from odigos_amd.batch import Generator
+    g = Generator("fused", seed=0x0D16F002, n_spans=30_000, threads=4)
+    pb = g.otlp(4)
+    full = _walk(CFG_EXCLUDE, pb)
+    part = _walk(dict(CFG_EXCLUDE, gpu_scopes=True), pb)
+    assert len(part["span_ref"]) == 0 and len(full["span_ref"]) == 30_000
+    for k in ("res_svc", "res_svc_str", "res_attrset", "res_size", "res_ok", "n_sets"):
+        assert part[k] == full[k], k
+    assert len(part["scope_size"]) == len(full["scope_size"])
