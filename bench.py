@@ -340,7 +340,7 @@ def main():
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     total = args.spans or wl["spans"]
-    gen = db = None
+    gen = db = comm = None
     extra = {}
 
     if args.workload == "owner":
@@ -487,6 +487,9 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        if comm is not None:
+            torch.cuda.synchronize()
+            comm.close()   # the RCCL communicator goes before the process group and the HIP runtime
         dist.destroy_process_group()
 
 
