@@ -543,7 +543,23 @@ __device__ void flush_queue(const TraceKernelArgs& a, const Cfg& c, DecideQ& Q, 
 
 
 
+// kLean: the instance for the common call — batch order (kTraceRuns), no
+// owner-side record columns, no precomputed endpoint bits, no span_attribute
+// bits, no diagnostics.  Those arguments are constants in it, so their code
+// and the kernel-argument registers that hold them fold away (the general
+// instance spills ~90 scalar registers into vector lanes).
+template <bool kLean>
 __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void trace_eval_kernel(TraceKernelArgs a) {
+  if (kLean) {
+    a.mode = kTraceRuns;
+    a.svc_match = nullptr;
+    a.route_match = nullptr;
+    a.attr_match = nullptr;
+    a.perm = nullptr;
+    a.key = nullptr;
+    a.batch_keep = nullptr;
+    a.ablate = 0;
+  }
   if (a.mode == kTracePerm && __hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   __shared__ DecideQ queues[kTWaves];
   __shared__ HeadQ headqs[kTWaves];
@@ -1532,7 +1548,10 @@ void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, u
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t per_block = kTWaves * a.win_per_wave;
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
-  hipLaunchKernelGGL(trace_eval_kernel, dim3(blocks), dim3(kTThreads), 0, st, a);
+  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate)
+    hipLaunchKernelGGL(trace_eval_kernel<true>, dim3(blocks), dim3(kTThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(trace_eval_kernel<false>, dim3(blocks), dim3(kTThreads), 0, st, a);
 }
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs) {
   // known_runs: the listed-run count the host read (host-gated form); else a
