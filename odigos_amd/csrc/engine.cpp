@@ -317,9 +317,9 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   if (o->tmpl_arena_cap > 0xFFFFFFFFull) return fail(OSE_ERANGE, "tmpl_arena_cap exceeds the 32-bit offset range");
   uint64_t n = c->n_spans;
   const uint32_t groups = (uint32_t)((n + kUrlGroup - 1) / kUrlGroup);
-  // workspace: [0,16) scan counter, slow count, error | scan status 8t (both zeroed by one memset) |
-  // plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | group_scr 8g |
-  // slow groups 4g | dbg | scratch (the assembled group images)
+  // workspace: [0,16) scan counter, slow count, error, unplanned count | scan status 8t (both zeroed by
+  // one memset) | plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | group_scr 8g |
+  // slow groups 4g | unplanned groups 4g | dbg | scratch (the assembled group images)
   const uint32_t scan_tiles = (groups + kUrlScanTile - 1) / kUrlScanTile;
   const size_t off_sst = 16, zero_bytes = off_sst + 8 * (size_t)scan_tiles;
   const size_t off_len = align_up(zero_bytes, 256), off_meta = off_len + 4 * n;
@@ -327,7 +327,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   const size_t off_gsum = off_code + 8 * n, off_gbase = off_gsum + 8 * (size_t)groups;
   const size_t off_gscr = off_gbase + 8 * (size_t)groups;
   const size_t off_slow = off_gscr + 8 * (size_t)groups;
-  const size_t off_dbg = align_up(off_slow + 4 * (size_t)groups, 256);
+  const size_t off_unpl = off_slow + 4 * (size_t)groups;
+  const size_t off_dbg = align_up(off_unpl + 4 * (size_t)groups, 256);
   const size_t off_scr = off_dbg + 256;
   const size_t scr_bytes = url_scratch_bytes(n, c->arena_bytes);
   const size_t need = off_scr + scr_bytes;
@@ -364,6 +365,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.error = o->device_status ? o->device_status : reinterpret_cast<uint32_t*>(base + 8);
   a.slow_count = reinterpret_cast<uint32_t*>(base + 4);
   a.slow_groups = reinterpret_cast<uint32_t*>(base + off_slow);
+  a.unplanned_count = reinterpret_cast<uint32_t*>(base + 12);
+  a.unplanned = reinterpret_cast<uint32_t*>(base + off_unpl);
   HIP_TRY(hipMemsetAsync(base, 0, zero_bytes, st));
   a.used = o->tmpl_arena_used;
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
@@ -379,6 +382,10 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   Engine::Timed tm{};
   e->prof_begin("url_plan_kernel", st, tm);
   launch_url_plan(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
+  e->prof_begin("url_plan_slow_kernel", st, tm);
+  launch_url_plan_slow(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
   e->prof_begin("url_scan_kernel", st, tm);

@@ -12,6 +12,9 @@ namespace ose {
 //   url_plan_kernel  one wave per 64-span group: plan, output length per span
 //                    and the group's template bytes, assembled in LDS and
 //                    stored to the wave's scratch region
+//   url_plan_slow_kernel  the groups the plan kernel could not plan from its
+//                    LDS stage (byte range over the stage, segment list
+//                    overflow, a segment over 64 bytes): planned per span from HBM
 //   url_scan_kernel  exclusive scan of the per-group output sums
 //   url_copy_kernel  one wave per group: template refs, and the group's bytes
 //                    copied from scratch to their place in the output arena
@@ -47,6 +50,8 @@ struct UrlKernelArgs {
   uint64_t* used;              // bytes written (optional)
   uint32_t* slow_count;        // groups the plan kernel left to K3s (zeroed before launch)
   uint32_t* slow_groups;       // [n_groups]
+  uint32_t* unplanned_count;   // groups the plan kernel left to url_plan_slow_kernel (zeroed before launch)
+  uint32_t* unplanned;         // [n_groups]
   uint32_t general;            // user rules or custom ids configured (selects the general kernel instances)
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
   uint64_t* dbg;               // diagnostics only (ablate & 512): per-section clock sums
@@ -68,12 +73,13 @@ inline size_t url_scratch_bytes(uint64_t n, uint64_t arena_bytes) {
 inline size_t url_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
   const uint64_t g = (n + kUrlGroup - 1) / kUrlGroup;
   const uint64_t t = (g + kUrlScanTile - 1) / kUrlScanTile;
-  return 16 + t * 8 + 256 + n * 16 + 8 + g * 28 + 512 + 256 + url_scratch_bytes(n, arena_bytes);
+  return 16 + t * 8 + 256 + n * 16 + 8 + g * 32 + 512 + 256 + url_scratch_bytes(n, arena_bytes);
 }
 void launch_url_plan(const UrlKernelArgs& a, hipStream_t st);
 uint32_t url_plan_waves(const UrlKernelArgs& a);   // waves of the plan grid (scratch regions)
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_copy(const UrlKernelArgs& a, hipStream_t st);
+void launch_url_plan_slow(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st);
 
 }  // namespace ose

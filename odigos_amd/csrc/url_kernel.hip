@@ -169,6 +169,7 @@ struct Cfg {
   lds_cfg* h;             // header copy in LDS: fields are read where used, no registers held
   uint32_t n_custom, n_rules, max_rule_nseg;   // the fields every span's plan tests
   uint32_t names_off;
+  uint32_t names_tab_all;   // every name id < kNameTab (the LDS name table holds them all)
   lds_u8* names;          // first kNamesLds bytes of the bytes section, staged in LDS
   uint32_t names_len;
   uint32_t ablate;        // diagnostics (UrlKernelArgs::ablate)
@@ -693,65 +694,6 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
   return -1;
 }
 
-// phase 1 from the class bitmaps: same result as plan_path, with segment
-// ends and the cheap predicates read from the windows.  p0 = stage offset of
-// the path (rd reads relative to it).
-__device__ __noinline__ Plan plan_bits(const Cfg& cfg, LdsReader& rd, lds_cu4* bm, uint32_t p0, uint32_t plen,
-                                       uint32_t f) {
-  Plan p;
-  const uint32_t n =
-      (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET ? first_of(bm, C_QM, p0, p0 + plen) - p0 : plen;
-  p.lead = (n > 0 && rd.at(0) == '/') ? 1 : 0;
-  if (n == p.lead) {   // "" or "/" -> "/" (processor.go:156-160)
-    p.mode = M_SLASH;
-    p.len = 1;
-    return p;
-  }
-  if (cfg.n_rules) {
-    const uint32_t nseg = 1 + count_byte(rd, p.lead, n, '/');
-    if (nseg <= cfg.max_rule_nseg) {
-      const uint32_t* by_len = reinterpret_cast<const uint32_t*>(cfg.blob + cfg.h->rules_by_len_off);
-      const UrlRuleDev* rules = reinterpret_cast<const UrlRuleDev*>(cfg.blob + cfg.h->rules_off);
-      for (uint32_t r = by_len[nseg]; r < by_len[nseg + 1]; r++) {
-        int64_t l = attempt_rule(cfg, rules[r], rd, p.lead, n);
-        if (l >= 0) { p.mode = M_RULE; p.field = r; p.len = p.lead + (uint32_t)l; return p; }
-      }
-    }
-  }
-  uint32_t s = p.lead, seg = 0, l = p.lead;
-  bool templated = false;
-  for (;;) {
-    const uint32_t rem = n - s;
-    const Win w = load_win<0, 2>(bm, p0 + s);
-    const uint64_t slm = w.c[C_SL] & low_mask(rem);
-    uint32_t e;
-    int id;
-    if (slm || rem <= 64 || (cfg.ablate & 64)) {
-      const uint32_t L = slm ? (uint32_t)__builtin_ctzll(slm) : min(rem, 64u);
-      e = s + L;
-      id = classify_win(cfg, rd, w, bm, p0 + s, s, L);
-    } else {
-      id = classify_segment(cfg, rd, s, n, &e);   // segment longer than 64 bytes
-    }
-    if (seg) l += 1;
-    if (id >= 0) {
-      templated = true;
-      l += cfg.name((uint32_t)id).len + 2;
-      if (seg < 16 && id < 15) p.code |= (uint64_t)(id + 1) << (seg * 4);
-      else p.slow = true;
-    } else {
-      l += e - s;
-    }
-    seg++;
-    if (e >= n) break;
-    s = e + 1;
-  }
-  if (templated) { p.mode = M_DEFAULT; p.len = l; }
-  else { p.mode = M_ORIG; p.len = 1 + (n - p.lead); }
-  p.field = n < kNField ? n : kNField;
-  return p;
-}
-
 // Rare paths kept out of line so the hot LDS->LDS instantiation stays small:
 // a group whose bytes do not fit the stage reads HBM, a tile whose output
 // does not fit the LDS image writes HBM.
@@ -816,7 +758,8 @@ __device__ __forceinline__ Cfg load_cfg(const UrlKernelArgs& a, NamesSmem& ns) {
     ns.name_tab[threadIdx.x] = reinterpret_cast<const NameDev*>(a.cfg + h.names_off)[threadIdx.x];
   if (threadIdx.x == 0) ns.hdr = h;
   __syncthreads();
-  return Cfg{a.cfg, (lds_cfg*)&ns.hdr, h.n_custom, h.n_rules, h.max_rule_nseg, h.names_off, (lds_u8*)ns.names, names_len, a.ablate,
+  return Cfg{a.cfg, (lds_cfg*)&ns.hdr, h.n_custom, h.n_rules, h.max_rule_nseg, h.names_off, h.n_names <= kNameTab ? 1u : 0u,
+             (lds_u8*)ns.names, names_len, a.ablate,
              (const __attribute__((address_space(3))) NameDev*)ns.name_tab};
 }
 
@@ -1088,17 +1031,10 @@ __device__ __noinline__ uint32_t name_len_global(const uint8_t* blob, uint32_t n
   return reinterpret_cast<const NameDev*>(blob + names_off)[id].len;
 }
 __device__ __forceinline__ uint32_t name_len(const Cfg& cfg, uint32_t id) {
-  if (id < kNameTab) return cfg.name_tab[id].len;
+  if (cfg.names_tab_all || id < kNameTab) return cfg.name_tab[id].len;
   return name_len_global(cfg.blob, cfg.names_off, id);
 }
 
-// getSegmentTemplatizationString for a segment longer than a 64-bit window
-// (rare: kept out of line so the list planner's registers stay small)
-__device__ __noinline__ int classify_long(const Cfg& cfg, const LdsReader& rd, uint32_t s, uint32_t L) {
-  LdsReader r = rd;
-  uint32_t e;
-  return classify_segment(cfg, r, s, s + L, &e);
-}
 
 // Phase 1 for a whole group through a segment list: each lane enumerates its
 // span's segments into the wave's list; the wave classifies the list 64
@@ -1110,7 +1046,8 @@ __device__ __noinline__ int classify_long(const Cfg& cfg, const LdsReader& rd, u
 // A path whose bytes lie in 6 bitmap rows (the common case) finds its '?' cut,
 // leading '/' and segment ends in one read of those rows' slash and '?' words
 // and folds its entries (<= 8) in one read; longer paths walk the rows.
-// Returns false (nothing written) when the list would overflow.
+// Returns false when the list would overflow or a segment is longer than 64
+// bytes (the group is then planned by url_plan_slow_kernel).
 // cls: where the classified entries go (== segs: in place; else segs keeps
 // the enumerated entries for the fused writer).  *big_id: some segment of
 // this lane's path took a name id the braced-name table does not hold.
@@ -1220,15 +1157,16 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   wave_lds_sync();
   if (tm) { const uint64_t c1 = clk(); tt[0] += c1 - c0; c0 = c1; }
   LdsReader rd0(stage32, 0);
+  bool longseg = false;
   for (uint32_t x = lane; x < total; x += kWave) {   // classify
     const uint32_t ent = segs[x];
     const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
-    int id;
+    int id = -1;
     if (L <= 64) {
       const Win w = load_win<0, 2>(bm, s);
       id = classify_win(cfg, rd0, w, bm, s, s, L);
     } else {
-      id = classify_long(cfg, rd0, s, L);   // segment longer than 64 bytes
+      longseg = true;   // a segment longer than a 64-bit window: the group goes to url_plan_slow_kernel
     }
     const uint32_t out = id >= 0 ? name_len(cfg, (uint32_t)id) + 2 : L;
     // id + 1 in 8 bits: 255 stands for every id >= 254 (such plans are `slow`
@@ -1236,6 +1174,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
     cls[x] = (out << 8) | min((uint32_t)(id + 1), 255u);
   }
   wave_lds_sync();
+  if (__ballot(longseg)) return false;
   if (tm) { const uint64_t c1 = clk(); tt[1] += c1 - c0; c0 = c1; }
   bool big = false;
   if (nseg) {   // fold
@@ -1372,6 +1311,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     cfg.n_custom = 0;
     cfg.n_rules = 0;
     cfg.max_rule_nseg = 0;
+    cfg.names_tab_all = 1;   // the built-in names only
   }
   if (!(kMode & kModeDiag)) {
     cfg.ablate = 0;
@@ -1456,18 +1396,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
       p.len = 1 + cur.pr.len;
       p.field = cur.pr.len;
       oflags = OSE_OUT_SET_ATTR;
-    } else if (needs_path && !listed) {
-      if (lo16 != ~0u) {
-        LdsReader rd(stage32, cur.pr.off - lo16);
-        p = plan_bits(cfg, rd, (lds_cu4*)sm.bm[wv], cur.pr.off - lo16, cur.pr.len, cur.f);
-      } else {
-        p = plan_global(cfg, a.arena + cur.pr.off, cur.pr.len, cur.f);
-      }
     }
+    // wave-uniform: a group whose paths the list planner could not take (a
+    // byte range over the stage, a list over kSegCap, a segment over 64
+    // bytes) is planned from HBM by url_plan_slow_kernel; kept out of this
+    // kernel, whose registers the fallback calls would otherwise claim
+    const bool unplanned = __ballot(needs_path && !listed && !(a.ablate & 2)) != 0;
     if (needs_path && !(a.ablate & 2)) {
       oflags = OSE_OUT_SET_ATTR;                                                       // processor.go:259
       if ((cur.f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;     // :216-225
     }
+    if (unplanned) {
+      if (lane == 0) a.unplanned[atomicAdd(a.unplanned_count, 1u)] = g;
+    } else {
     const uint64_t sum = wave_sum_u64(p.len);
     const uint64_t need = (sum + 15) & ~15ull;
     // wave-uniform: the group is assembled here unless a user rule matched, a
@@ -1506,6 +1447,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
       a.group_sum[g] = sum;
       a.group_scr[g] = ~0ull;
       if (sum) a.slow_groups[atomicAdd(a.slow_count, 1u)] = g;
+    }
     }
     if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
     if (!more) break;
@@ -1679,6 +1621,70 @@ __global__ __launch_bounds__(kThreads) void url_copy_kernel(UrlKernelArgs a) {
   }
 }
 
+// K1b: the groups K1 listed as unplanned, one single-wave workgroup per
+// group (persistent; exits at once when the list is empty).  The group's
+// arena range is staged into a 32 KB LDS buffer (larger ranges plan from
+// HBM); every span is planned from its bytes (plan_path), then the plan
+// arrays, url_out and the group's output sum; the group is listed for K3s,
+// which emits it.  A group's wave spends its time in per-lane byte walks:
+// from LDS each step is an LDS round trip instead of an HBM one.
+constexpr uint32_t kSlowStage = 32 * 1024;
+__global__ __launch_bounds__(kWave) void url_plan_slow_kernel(UrlKernelArgs a) {
+  __shared__ NamesSmem ns;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kSlowStage + 16];
+  const uint32_t count = *a.unplanned_count;
+  if (blockIdx.x >= count) return;
+  const int lane = threadIdx.x;
+  const Cfg cfg = load_cfg(a, ns);
+  for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) {
+    const uint32_t g = a.unplanned[k];
+    const uint64_t i = (uint64_t)g * kWave + lane;
+    const PlanCols c = plan_cols(a, i);
+    const uint32_t gate = plan_gate(c);
+    // the arena bytes [lo, hi) the group's paths reference, 16-byte aligned down
+    uint32_t lo = gate == 2 ? c.pr.off : ~0u, hi = gate == 2 ? c.pr.off + c.pr.len : 0u;
+    lo = wave_min_u32(lo);
+    hi = wave_max_u32(hi);
+    const uint32_t lo16 = lo & ~15u;
+    const bool staged = lo < hi && hi - lo16 <= kSlowStage;   // wave-uniform
+    if (staged) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.arena + lo16);
+      uint4* dst = reinterpret_cast<uint4*>(stage);
+      for (uint32_t x = lane; x < (hi - lo16 + 15) / 16; x += kWave) dst[x] = src[x];
+      wave_lds_sync();
+    }
+    Plan p;
+    uint32_t oflags = 0;
+    if (gate == 1) {
+      p.mode = M_RENAME_SLASH;
+      p.len = 1;
+      oflags = OSE_OUT_RENAME;
+    } else if (gate == 2) {
+      if (staged) {
+        LdsReader rd((lds_u32*)stage, c.pr.off - lo16);
+        p = plan_path(cfg, rd, c.pr.len, c.f);
+      } else {
+        p = plan_global(cfg, a.arena + c.pr.off, c.pr.len, c.f);
+      }
+      oflags = OSE_OUT_SET_ATTR;                                                       // processor.go:259
+      if ((c.f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;       // :216-225
+    }
+    if (i < a.n_spans) {
+      a.plan_len[i] = p.len;
+      a.url_out[i] = (uint8_t)oflags;
+      a.plan_meta[i] = pack_meta(p.mode, p.lead, p.slow, oflags, p.field);
+      a.plan_code[i] = p.code;
+    }
+    const uint64_t sum = wave_sum_u64(p.len);
+    if (lane == 0) {
+      a.group_sum[g] = sum;
+      a.group_scr[g] = ~0ull;
+      if (sum) a.slow_groups[atomicAdd(a.slow_count, 1u)] = g;
+    }
+    wave_lds_sync();   // the stage is reused by the next group
+  }
+}
+
 // K3s: the groups K1 listed (user rules, plan `slow`, names outside the
 // braced table, an output image or a stage larger than LDS), with the
 // per-span writer (emit_path).  One wave per listed group; exits at once when
@@ -1797,6 +1803,20 @@ void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
   }();
   const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + 2 * kWaves - 1) / (2 * kWaves));
   hipLaunchKernelGGL(url_copy_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+}
+void launch_url_plan_slow(const UrlKernelArgs& a, hipStream_t st) {
+  // the list length is on the device: a workgroup per group up to the resident
+  // count, workgroups past the list's end exit at once
+  static const uint32_t cap = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024u;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, url_plan_slow_kernel, kWave, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 2;
+    return (uint32_t)(cus * per_cu);
+  }();
+  const uint32_t blocks = std::min<uint32_t>(cap, a.n_groups);
+  if (blocks) hipLaunchKernelGGL(url_plan_slow_kernel, dim3(blocks), dim3(kWave), 0, st, a);
 }
 void launch_url_emit_slow(const UrlKernelArgs& a, hipStream_t st) {
   // the list length is on the device: a grid for every group, blocks past it exit at once

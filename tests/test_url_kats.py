@@ -123,3 +123,34 @@ def test_default_config_and_validation():
     for cfg in bad:
         with pytest.raises(ValueError):
             host.Processor("odigosurltemplate", cfg)
+
+
+@pytest.mark.gpu
+def test_gpu_long_segments_and_wide_groups():
+    # segments longer than a 64-bit window and groups whose byte range outgrows
+    # the plan kernel's stage are planned by url_plan_slow_kernel and emitted
+    # by url_emit_slow_kernel; the result must equal the oracle's
+    import random
+    rng = random.Random(0x0D16_0A11)
+    spans = []
+    for k in range(300):
+        shape = rng.randrange(5)
+        if shape == 0:
+            path = "/" + "".join(rng.choice("abcxyz") for _ in range(rng.randrange(65, 200)))
+        elif shape == 1:
+            path = "/v1/" + "".join(rng.choice("0123456789") for _ in range(rng.randrange(65, 120))) + "/items"
+        elif shape == 2:
+            path = "/" + "ab" * rng.randrange(33, 60) + "/" + "9" * rng.randrange(7, 90)
+        elif shape == 3:
+            path = "/" + "/".join(f"seg{i}" for i in range(rng.randrange(400, 700)))   # a 3-5 KB path
+        else:
+            path = "/users/%d/orders/%s" % (rng.randrange(10**9), "".join(rng.choice("0123456789abcdef") for _ in range(32)))
+        spans.append(host.span(name="GET", kind=rng.choice([2, 3]), attributes={"http.request.method": "GET", "url.path": path}))
+    res = {"service.name": "svc", "k8s.namespace.name": "default", "k8s.deployment.name": "svc"}
+    tr = host.traces(host.resource_spans(res, spans))
+    proc = host.Processor("odigosurltemplate", {})
+    hb = proc.columnarize(tr)
+    assert UrlOracle({}).process(hb.cols, hb.outs) == 0
+    want = hb.apply()
+    got = host.Processor("odigosurltemplate", {}).consume(tr)
+    assert got == want
