@@ -972,31 +972,61 @@ constexpr uint32_t kImgCap = kRowVec * kPlanBmRows * 16;   // bytes of one wave'
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 struct StageDma {
-  uint32_t lo16, bytes;   // bytes == 0: nothing staged; lo16 == ~0u: range too large (HBM reads)
+  // per lane: a path at arena offset o sits at stage offset o - base (base is
+  // wave-uniform for a contiguous copy, per lane for a gather); bytes == 0:
+  // nothing staged; base == ~0u: the wave's paths do not fit the stage
+  uint32_t base, bytes;
 };
-// Issues the copy of the arena bytes [lo, hi) the wave's lanes reference
-// (16-byte aligned down) into `stage` by LDS-DMA (global_load_lds_dwordx4:
-// lane k's 16 bytes land at stage + 16k of each 1 KB piece).  The caller
-// waits vmcnt before reading the buffer.
-__device__ __forceinline__ StageDma stage_dma(const uint8_t* arena, uint32_t lo, uint32_t hi, uint8_t* stage) {
+// Issues the copy of the arena bytes the wave's lanes reference into `stage` by
+// LDS-DMA (global_load_lds_dwordx4: lane k's 16 bytes land at stage + 16k of
+// each 1 KB piece).  When the wave's range [min lo, max hi) fits, it is copied
+// whole (16-byte aligned down).  When it does not (paths spread through other
+// strings of the arena: C4's routes, the span messages of an OTLP-decoded
+// batch), each lane's path is gathered as its own 16-byte chunks, packed in
+// lane order: slot x of the stage takes chunk x - cs(L) of owner L, the last
+// lane whose exclusive chunk scan cs(L) <= x (binary search over shuffles).
+// The caller waits vmcnt before reading the buffer.
+__device__ __forceinline__ StageDma stage_dma(const uint8_t* arena, uint32_t lo_l, uint32_t hi_l, uint8_t* stage) {
   const int lane = threadIdx.x & 63;
-  lo = wave_min_u32(lo);
-  hi = wave_max_u32(hi);
+  const uint32_t lo = wave_min_u32(lo_l), hi = wave_max_u32(hi_l);
   StageDma sd{0, 0};
   if (lo >= hi) return sd;
-  sd.lo16 = lo & ~15u;
-  const uint32_t bytes = (hi - sd.lo16 + 15u) & ~15u;
-  if (bytes > kPlanStage) {
-    sd.lo16 = ~0u;
+  const uint32_t lo16 = lo & ~15u;
+  const uint32_t bytes = (hi - lo16 + 15u) & ~15u;
+  if (bytes <= kPlanStage) {
+    sd.base = lo16;
+    sd.bytes = bytes;
+    const uint4* src = reinterpret_cast<const uint4*>(arena + lo16) + lane;
+    const uint32_t nv = bytes / 16;
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanStage / 1024; k++)
+      if (lane + 64 * k < nv)
+        __builtin_amdgcn_global_load_lds((glb_void*)(src + 64 * k), (lds_void*)(stage + 1024 * k), 16, 0, 0);
     return sd;
   }
-  sd.bytes = bytes;
-  const uint4* src = reinterpret_cast<const uint4*>(arena + sd.lo16) + lane;
-  const uint32_t nv = bytes / 16;
+  const uint32_t nc = lo_l < hi_l ? ((hi_l + 15u) >> 4) - (lo_l >> 4) : 0u;
+  uint32_t total;
+  const uint32_t cs = wave_excl_scan(nc, &total);
+  if (total * 16 > kPlanStage) {
+    sd.base = ~0u;
+    return sd;
+  }
+  sd.base = lo_l < hi_l ? lo_l - (16 * cs + (lo_l & 15u)) : 0u;
+  sd.bytes = total * 16;
+  const uint32_t ch = (lo_l >> 4) - cs;   // chunk index of slot x, lane L: x + ch(L)
 #pragma unroll
-  for (uint32_t k = 0; k < kPlanStage / 1024; k++)
-    if (lane + 64 * k < nv)
-      __builtin_amdgcn_global_load_lds((glb_void*)(src + 64 * k), (lds_void*)(stage + 1024 * k), 16, 0, 0);
+  for (uint32_t k = 0; k < kPlanStage / 1024; k++) {
+    const uint32_t x = lane + 64 * k;
+    if (64 * k < total) {   // wave-uniform
+      uint32_t o = 0;
+#pragma unroll
+      for (uint32_t step = 32; step; step >>= 1)
+        if (__shfl(cs, (int)(o + step)) <= x) o += step;
+      const uint32_t c = (uint32_t)__shfl(ch, (int)o) + x;
+      if (x < total)
+        __builtin_amdgcn_global_load_lds((glb_void*)(arena + 16ull * c), (lds_void*)(stage + 1024 * k), 16, 0, 0);
+    }
+  }
   return sd;
 }
 __device__ __forceinline__ void wait_dma() {
@@ -1361,8 +1391,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
 
     const uint32_t gate = plan_gate(cur);
     const bool needs_path = gate == 2;
-    const uint32_t lo16 = pf.lo16;
-    if (lo16 != ~0u && pf.bytes && !(a.ablate & 4)) {
+    const uint32_t lo16 = pf.base;   // per lane (a gathered stage)
+    const bool staged = __ballot(lo16 == ~0u) == 0;
+    if (staged && pf.bytes && !(a.ablate & 4)) {
       // rows holding path bytes; when other strings of the arena fill a good
       // part of the staged range (C4), only those rows get bitmaps
       uint32_t m0 = 0, m1 = 0, m2 = 0;
@@ -1384,7 +1415,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     // the list planner uses wave shuffles: called by the whole wave (lanes without a path add no segments)
     bool listed = false, big = false;
     uint32_t seg_off = 0;
-    if (lo16 != ~0u && !(a.ablate & (1024 | 2)))
+    if (staged && !(a.ablate & (1024 | 2)))
       listed = plan_group_list(cfg, stage32, (lds_cu4*)sm.bm[wv], sm.segs[wv], needs_path, cur.pr.off - lo16,
                                cur.pr.len, cur.f, p, tm, tt, sm.cls[wv], &seg_off, &big);
     if (gate == 1) {
