@@ -402,7 +402,9 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   e->prof_end(tm, st);
   if (a.ablate & 512) {
     uint64_t h[16];
+    uint32_t cnt[4];
     HIP_TRY(hipMemcpyAsync(h, a.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(cnt, base, sizeof cnt, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const double wp = h[3] ? (double)h[3] : 1.0, we = h[6] ? (double)h[6] : 1.0;
     (void)we;
@@ -410,6 +412,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
             h[1] / wp, h[2] / wp, h[5] / wp);
     fprintf(stderr, "url plan list clocks/wave: enumerate %.0f classify %.0f fold %.0f\n", h[13] / wp, h[14] / wp,
             h[15] / wp);
+    fprintf(stderr, "url groups: %llu, slow (K3s) %u, unplanned (K1b) %u\n", (unsigned long long)((n + 63) / 64),
+            cnt[1], cnt[3]);
   }
   return 0;
 }

@@ -950,18 +950,25 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
 // group's place in the output arena is only known after K2, so K4 moves the
 // image there; the path bytes are read from HBM once.
 constexpr uint32_t kSegCap = 192;   // per-wave segment list (C2 groups hold ~118 segments, max seen 182)
-// K1 stages each group through LDS-DMA into one of two per-wave buffers, so
-// the next group's bytes land while this one is planned without holding them
-// in VGPRs (a register prefetch spilled to scratch at this kernel's VGPR
-// budget, which forced a full vmcnt wait per group).  3 KB per buffer covers
-// 99.9% of C2/C4 groups (p99 of a group's byte range is 2.9 KB); larger
-// groups plan from HBM.  2 x 3 KB stage + 12-class bitmaps + segment list per
-// wave keep three 4-wave workgroups per CU.
+// K1 stages each group through LDS-DMA into a per-wave buffer: the next
+// group's copy is issued as soon as this group's assembly is done with the
+// buffer, and waited for at the top of the next iteration.  3 KB covers 99.9%
+// of C2/C4 groups as one contiguous range (p99 of a group's byte range is
+// 2.9 KB); a wider range is gathered path by path (stage_dma), and a group
+// whose paths alone overflow goes to url_plan_slow_kernel.  One 3 KB buffer +
+// 12-class bitmaps + segment list per wave (39.7 KB per 4-wave workgroup) and
+// <= 128 VGPRs keep four workgroups per CU; a second buffer, prefetching a
+// whole group ahead, held the kernel to three (52 KB) and measured 8% slower
+// (OSE_PLAN_BUFS=2 builds that variant: C4 plan 7.45 vs 6.84 ms).
 constexpr uint32_t kPlanStage = 3 * 1024;
+#ifndef OSE_PLAN_BUFS
+#define OSE_PLAN_BUFS 1
+#endif
+constexpr uint32_t kPlanBufs = OSE_PLAN_BUFS;
 constexpr uint32_t kPlanBmRows = kPlanStage / 32 + 3;
 struct PlanSmem {
   NamesSmem ns;
-  __attribute__((aligned(16))) uint8_t stage[2][kWaves][kPlanStage + 16];
+  __attribute__((aligned(16))) uint8_t stage[kPlanBufs][kWaves][kPlanStage + 16];
   __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kPlanBmRows];   // class bitmaps, then the output image
   uint32_t segs[kWaves][kSegCap];   // enumerated segments (start | len | owner lane)
   uint32_t cls[kWaves][kSegCap];    // their classification (out_len << 8 | id + 1)
@@ -1332,7 +1339,7 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
 // bit 1 (kModeDiag): OSE_URL_ABLATE / per-section clocks.
 constexpr int kModeGeneral = 1, kModeDiag = 2;
 template <int kMode>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void url_plan_kernel(UrlKernelArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanBufs == 1 ? 4 : 3, kPlanBufs == 1 ? 4 : 3))) void url_plan_kernel(UrlKernelArgs a) {
   __shared__ PlanSmem sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   Cfg cfg = load_cfg(a, sm.ns);
@@ -1384,8 +1391,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     const bool more = g2 < a.n_groups;
     // in flight while this group is planned: bytes of the next group, columns of the one after
     const bool np2 = more && plan_gate(nxt) == 2;
-    const StageDma pf2 =
-        stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[buf ^ 1][wv]);
+    StageDma pf2{0, 0};
+    if constexpr (kPlanBufs == 2)
+      pf2 = stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[buf ^ 1][wv]);
     nn = plan_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
     if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
 
@@ -1483,8 +1491,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3, 3))
     if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
     if (!more) break;
     wave_lds_sync();   // every lane is done with this group's stage and bitmaps
+    if constexpr (kPlanBufs == 1)
+      pf2 = stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[0][wv]);
     pf = pf2;
-    buf ^= 1;
+    buf ^= kPlanBufs - 1;
     g = g2;
   }
   if (tm && lane == 0) {

@@ -13,4 +13,4 @@ done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/ga/otlp_prof -o otlp -- python3 tools/otlp_bench.py --spans 10000000 --reps 3 --out gpurun_out/ga/otlp.json > gpurun_out/ga/otlp.log 2>&1 || { tail -20 gpurun_out/ga/otlp.log; exit 1; }
 python3 -c "import json; d=json.load(open('gpurun_out/ga/otlp.json')); print('otlp stages_ms', d['stages_ms'], 'kernel', d['stages_kernel_ms'])"
-f=$(find gpurun_out/ga/otlp_prof -name '*kernel_stats.csv' | head -1); head -14 "$f" | cut -d, -f1-4
+true
