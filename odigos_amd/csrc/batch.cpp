@@ -234,6 +234,7 @@ ose_outputs* ose_batch_outputs(ose_batch* bb) { return bb ? &reinterpret_cast<Ba
 
 void ose_batch_release(ose_batch* bb) {
   if (!bb) return;
+  LastErrorScope keep;
   Batch* b = reinterpret_cast<Batch*>(bb);
   Engine* e = b->e;
   (void)bind_device(e);

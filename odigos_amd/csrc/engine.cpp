@@ -414,6 +414,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
             h[15] / wp);
     fprintf(stderr, "url groups: %llu, slow (K3s) %u, unplanned (K1b) %u\n", (unsigned long long)((n + 63) / 64),
             cnt[1], cnt[3]);
+    fprintf(stderr, "url_plan_slow_kernel slowest block clocks: config %llu whole %llu plan_path %llu\n",
+            (unsigned long long)h[8], (unsigned long long)h[9], (unsigned long long)h[10]);
   }
   return 0;
 }
@@ -539,6 +541,7 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
 
 void ose_engine_destroy(ose_engine* eng) {
   if (!eng) return;
+  LastErrorScope keep;
   (void)bind_device(reinterpret_cast<Engine*>(eng));
   (void)hipDeviceSynchronize();   // nothing in flight may still use the buffers freed below
   delete reinterpret_cast<Engine*>(eng);
@@ -552,6 +555,7 @@ int ose_host_alloc(size_t bytes, void** out) {
   return 0;
 }
 void ose_host_free(void* p) {
+  LastErrorScope keep;
   if (p) (void)hipHostFree(p);
 }
 

@@ -20,6 +20,16 @@ struct Engine;
 // goroutines migrate across OS threads; HIP's current device is per thread)
 int bind_device(const Engine* e);
 int ensure_device();
+// The release entry points return nothing, so a HIP error their clean-up
+// meets is dropped; this keeps it out of the runtime's per-thread last-error
+// slot too, where the caller's next launch check (torch's, a shim's) would
+// report it against its own work.  An error already pending on entry is left.
+struct LastErrorScope {
+  hipError_t prev = hipPeekAtLastError();
+  ~LastErrorScope() {
+    if (prev == hipSuccess) (void)hipGetLastError();
+  }
+};
 bool stream_capturing(hipStream_t st);
 struct Engine;
 void release_exchange_scratch(const Engine* e);   // shard_host.cpp

@@ -518,6 +518,7 @@ int ose_gbt_create(ose_engine* eng, const char* cfg_json, uint64_t span_capacity
 
 void ose_gbt_destroy(ose_gbt* gg) {
   if (!gg) return;
+  LastErrorScope keep;
   auto* g = reinterpret_cast<Gbt*>(gg);
   (void)bind_device(g->e);
   delete g;

@@ -749,7 +749,10 @@ int ose_router_create(const char* cfg_json, ose_router** out) {
   }
 }
 
-void ose_router_destroy(ose_router* r) { delete reinterpret_cast<Router*>(r); }
+void ose_router_destroy(ose_router* r) {
+  LastErrorScope keep;
+  delete reinterpret_cast<Router*>(r);
+}
 
 uint32_t ose_router_pipelines(const ose_router* r) {
   return r ? (uint32_t)reinterpret_cast<const Router*>(r)->pipelines.size() : 0;
@@ -777,7 +780,10 @@ int ose_otlp_out_get(const ose_otlp_out* o, uint32_t k, const char** name, const
   return 0;
 }
 
-void ose_otlp_out_release(ose_otlp_out* o) { otlp_out_release(reinterpret_cast<OtlpOut*>(o)); }
+void ose_otlp_out_release(ose_otlp_out* o) {
+  LastErrorScope keep;
+  otlp_out_release(reinterpret_cast<OtlpOut*>(o));
+}
 
 // diagnostics: decisions D2H, sizing pass, buffers, writing pass (ms)
 int osehost_otlp_out_timings(const ose_otlp_out* o, double* ms4) {

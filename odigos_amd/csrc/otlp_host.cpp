@@ -1236,6 +1236,7 @@ int osehost_otlp_encode(const uint8_t* pb, size_t len, const uint8_t* keep, int 
 
 void ose_otlp_release(ose_otlp_batch* bb) {
   if (!bb) return;
+  LastErrorScope keep;
   auto* b = reinterpret_cast<OtlpBatchImpl*>(bb);
   Engine* e = b->e;
   (void)bind_device(e);

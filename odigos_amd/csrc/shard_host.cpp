@@ -272,6 +272,7 @@ int ose_nccl_comm_init(void** comm_out, int n_ranks, const void* id, int rank) {
 }
 
 void ose_nccl_comm_destroy(void* comm) {
+  LastErrorScope keep;
   if (comm && rccl().ok) (void)rccl().comm_destroy(static_cast<ncclComm_t>(comm));
 }
 

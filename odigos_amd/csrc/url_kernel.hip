@@ -1663,50 +1663,91 @@ __global__ __launch_bounds__(kThreads) void url_copy_kernel(UrlKernelArgs a) {
 }
 
 // K1b: the groups K1 listed as unplanned, one single-wave workgroup per
-// group (persistent; exits at once when the list is empty).  The group's
-// arena range is staged into a 32 KB LDS buffer (larger ranges plan from
-// HBM); every span is planned from its bytes (plan_path), then the plan
-// arrays, url_out and the group's output sum; the group is listed for K3s,
-// which emits it.  A group's wave spends its time in per-lane byte walks:
-// from LDS each step is an LDS round trip instead of an HBM one.
-constexpr uint32_t kSlowStage = 32 * 1024;
+// group (persistent; exits at once when the list is empty).  Their paths are
+// planned in lane subsets whose 16-byte chunks fit K1's 3 KB stage: each
+// subset is gathered (stage_dma), given its row bitmaps and planned by the
+// same wave-parallel list planner as K1.  A subset the list planner refuses
+// (a segment over 64 bytes, more than kSegCap segments) and a single path
+// over 3 KB are planned per lane (plan_path from the stage, plan_global from
+// HBM): per-lane byte walks diverge across the wave, which made a lone group
+// cost ~190k clocks when every lane took that route.  The plan arrays,
+// url_out and the group's output sum are written; the group is listed for
+// K3s, which emits it.
+struct SlowPlanSmem {
+  NamesSmem ns;
+  __attribute__((aligned(16))) uint8_t stage[kPlanStage + 16];
+  __attribute__((aligned(16))) u32x4 bm[kRowVec * kPlanBmRows];
+  uint32_t segs[kSegCap];
+  uint32_t cls[kSegCap];
+};
 __global__ __launch_bounds__(kWave) void url_plan_slow_kernel(UrlKernelArgs a) {
-  __shared__ NamesSmem ns;
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kSlowStage + 16];
+  __shared__ SlowPlanSmem sm;
   const uint32_t count = *a.unplanned_count;
   if (blockIdx.x >= count) return;
   const int lane = threadIdx.x;
-  const Cfg cfg = load_cfg(a, ns);
+  const uint64_t c0 = a.dbg ? clk() : 0;
+  const Cfg cfg = load_cfg(a, sm.ns);
+  uint64_t c_plan = 0;
+  const uint64_t c1 = a.dbg ? clk() : 0;
+  lds_u32* stage32 = (lds_u32*)sm.stage;
+  uint64_t tt[3] = {0, 0, 0};
   for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) {
     const uint32_t g = a.unplanned[k];
     const uint64_t i = (uint64_t)g * kWave + lane;
     const PlanCols c = plan_cols(a, i);
     const uint32_t gate = plan_gate(c);
-    // the arena bytes [lo, hi) the group's paths reference, 16-byte aligned down
-    uint32_t lo = gate == 2 ? c.pr.off : ~0u, hi = gate == 2 ? c.pr.off + c.pr.len : 0u;
-    lo = wave_min_u32(lo);
-    hi = wave_max_u32(hi);
-    const uint32_t lo16 = lo & ~15u;
-    const bool staged = lo < hi && hi - lo16 <= kSlowStage;   // wave-uniform
-    if (staged) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.arena + lo16);
-      uint4* dst = reinterpret_cast<uint4*>(stage);
-      for (uint32_t x = lane; x < (hi - lo16 + 15) / 16; x += kWave) dst[x] = src[x];
-      wave_lds_sync();
-    }
     Plan p;
     uint32_t oflags = 0;
     if (gate == 1) {
       p.mode = M_RENAME_SLASH;
       p.len = 1;
       oflags = OSE_OUT_RENAME;
-    } else if (gate == 2) {
-      if (staged) {
-        LdsReader rd((lds_u32*)stage, c.pr.off - lo16);
-        p = plan_path(cfg, rd, c.pr.len, c.f);
-      } else {
-        p = plan_global(cfg, a.arena + c.pr.off, c.pr.len, c.f);
+    }
+    const uint32_t lo_l = c.pr.off, hi_l = c.pr.off + c.pr.len;
+    const uint32_t nc = gate == 2 && c.pr.len ? ((hi_l + 15u) >> 4) - (lo_l >> 4) : 0u;
+    bool todo = gate == 2;
+    while (__ballot(todo)) {   // wave-uniform
+      const uint64_t t = a.dbg ? clk() : 0;
+      uint32_t unused;
+      const uint32_t cs = wave_excl_scan(todo ? nc : 0u, &unused);
+      bool take = todo && cs + nc <= kPlanStage / 16;
+      const bool alone = __ballot(take) == 0;   // the first pending path alone is over 3 KB
+      if (alone) {
+        const int first = __builtin_ctzll(__ballot(todo));
+        if (lane == first) {
+          p = plan_global(cfg, a.arena + c.pr.off, c.pr.len, c.f);
+          todo = false;
+        }
+        continue;
       }
+      const StageDma sd = stage_dma(a.arena, take ? lo_l : ~0u, take ? hi_l : 0u, sm.stage);
+      wait_dma();
+      const uint32_t p0 = c.pr.off - sd.base;
+      uint32_t m0 = 0, m1 = 0, m2 = 0;
+      if (take && c.pr.len) {
+        const uint32_t rl = p0 >> 5, rh = (p0 + c.pr.len - 1) >> 5;
+        m0 = row_bits(rl, rh, 0);
+        m1 = row_bits(rl, rh, 32);
+        m2 = row_bits(rl, rh, 64);
+      }
+      build_bitmaps_rows(stage32, (lds_u4*)sm.bm, wave_or_u32(m0), wave_or_u32(m1), wave_or_u32(m2));
+      wave_lds_sync();
+      Plan q;
+      const bool listed = plan_group_list(cfg, stage32, (lds_cu4*)sm.bm, sm.segs, take, p0, c.pr.len, c.f, q, false,
+                                          tt, sm.cls);
+      if (take) {
+        if (listed) {
+          p = q;
+        } else {
+          LdsReader rd(stage32, p0);
+          p = plan_path(cfg, rd, c.pr.len, c.f);
+        }
+        todo = false;
+      }
+      wave_lds_sync();   // the stage and bitmaps are refilled for the next subset
+      if (a.dbg) c_plan += clk() - t;
+    }
+    if (gate == 2) {
       oflags = OSE_OUT_SET_ATTR;                                                       // processor.go:259
       if ((c.f & OSE_URL_NAME_EQ_METHOD) && p.len > 0) oflags |= OSE_OUT_RENAME;       // :216-225
     }
@@ -1722,7 +1763,14 @@ __global__ __launch_bounds__(kWave) void url_plan_slow_kernel(UrlKernelArgs a) {
       a.group_scr[g] = ~0ull;
       if (sum) a.slow_groups[atomicAdd(a.slow_count, 1u)] = g;
     }
-    wave_lds_sync();   // the stage is reused by the next group
+  }
+  if (a.dbg) {   // diagnostics: the slowest block's clocks (config load, whole, subset planning)
+    const uint64_t c2 = clk();
+    if (lane == 0) {
+      atomicMax((unsigned long long*)&a.dbg[8], (unsigned long long)(c1 - c0));
+      atomicMax((unsigned long long*)&a.dbg[9], (unsigned long long)(c2 - c0));
+      atomicMax((unsigned long long*)&a.dbg[10], (unsigned long long)c_plan);
+    }
   }
 }
 

@@ -35,3 +35,40 @@ def gpu_available() -> bool:
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+def _hip_runtime():
+    """The libamdhip64 this process already loaded (torch's), so its
+    per-thread last-error state is the one torch's launch checks read."""
+    import ctypes
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64.so" in line:
+                lib = ctypes.CDLL(line.split()[-1])
+                lib.hipGetErrorName.restype = ctypes.c_char_p
+                return lib
+    return None
+
+
+@pytest.fixture(autouse=True)
+def _no_sticky_hip_error(request):
+    """A GPU test must not leave a HIP error in the runtime's last-error slot:
+    torch reports it at its next launch check, inside whichever test comes
+    next."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import torch
+    if not torch.cuda.is_available():
+        yield
+        return
+    hip = _hip_runtime()
+    if hip is not None:
+        err = hip.hipGetLastError()
+        if err:   # set between tests: a finalizer (ose_*_release / destroy) of an earlier test's objects
+            pytest.fail(f"HIP error {hip.hipGetErrorName(err).decode()} ({err}) pending before this test")
+    yield
+    if hip is not None:
+        err = hip.hipGetLastError()
+        if err:
+            pytest.fail(f"HIP error {hip.hipGetErrorName(err).decode()} ({err}) left in the runtime by this test")

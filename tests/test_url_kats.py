@@ -154,3 +154,48 @@ def test_gpu_long_segments_and_wide_groups():
     want = hb.apply()
     got = host.Processor("odigosurltemplate", {}).consume(tr)
     assert got == want
+
+
+@pytest.mark.gpu
+def test_gpu_groups_over_the_stage_planned_in_subsets():
+    # 80-140 byte paths of ordinary segments: a group's paths alone outgrow the
+    # plan kernel's 3 KB stage (about 7 chunks of 16 bytes per path), so
+    # url_plan_slow_kernel plans each group in lane subsets with the list
+    # planner; a few lanes carry a 65+ byte segment, whose subset falls back
+    # to per-lane planning.  The result must equal the oracle's.
+    import random
+    import uuid
+    rng = random.Random(0x0D16_0A12)
+
+    def segment():
+        k = rng.randrange(8)
+        if k == 0:
+            return str(rng.randrange(10 ** rng.randrange(1, 12)))
+        if k == 1:
+            return str(uuid.UUID(int=rng.getrandbits(128)))
+        if k == 2:
+            return "".join(rng.choice("0123456789abcdef") for _ in range(rng.randrange(8, 40)))
+        if k == 3:
+            return "2024-%02d-%02d" % (rng.randrange(1, 13), rng.randrange(1, 29))
+        if k == 4:
+            return "user%d@example.com" % rng.randrange(1000)
+        return "".join(rng.choice("abcdefghijklmnopqrstuvwxyz-_") for _ in range(rng.randrange(2, 14)))
+
+    spans = []
+    for k in range(640):
+        parts = []
+        while sum(len(p) + 1 for p in parts) < rng.randrange(80, 140):
+            parts.append(segment())
+        if rng.random() < 0.02:
+            parts.append("z" * rng.randrange(65, 90))
+        path = "/" + "/".join(parts) + ("/" if rng.random() < 0.05 else "")
+        spans.append(host.span(name="GET", kind=rng.choice([2, 3]),
+                               attributes={"http.request.method": "GET", "url.path": path}))
+    res = {"service.name": "svc", "k8s.namespace.name": "default", "k8s.deployment.name": "svc"}
+    tr = host.traces(host.resource_spans(res, spans))
+    proc = host.Processor("odigosurltemplate", {})
+    hb = proc.columnarize(tr)
+    assert UrlOracle({}).process(hb.cols, hb.outs) == 0
+    want = hb.apply()
+    got = host.Processor("odigosurltemplate", {}).consume(tr)
+    assert got == want
