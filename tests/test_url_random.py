@@ -202,3 +202,18 @@ def test_gpu_url_parity_scratch_regions_overflow():
     # a few group images, the rest fall back to the per-span writer
     g = Generator("url", seed=0x0D160042, n_spans=2_000_000, threads=8)
     _gpu_vs_oracle_cols(g, {}, arena_bytes=0)
+
+
+@pytest.mark.gpu
+def test_gpu_url_parity_paths_spread_through_the_arena():
+    # the path refs of a C2 batch permuted across its spans: every group's
+    # paths lie anywhere in the 10 MB arena (as in an OTLP-decoded batch), so
+    # url_plan_kernel stages them by the per-lane gather, and groups whose
+    # chunks outgrow the stage go to url_plan_slow_kernel's subsets
+    g = Generator("url", seed=0x0D160052, n_spans=300_000, threads=8)
+    path = g.array("path").view(np.uint32).reshape(-1, 2)
+    has = np.flatnonzero(path[:, 1] > 0)
+    perm = np.random.default_rng(0x0D160052).permutation(has.size)
+    path[has] = path[has][perm]
+    used = _gpu_vs_oracle_cols(g, {})
+    assert used > 0
