@@ -1469,8 +1469,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
       const uint32_t n16 = (uint32_t)(need / 16);
       uint32_t unused;
       const uint32_t local = wave_excl_scan(p.len, &unused);
-      assemble_group((lds_out_u8*)sm.bm[wv], L, (uint32_t)(stage - (uint8_t*)&sm), sm.segs[wv], sm.cls[wv], sm.bn,
-                     bn_src, p, seg_off, local);
+      if (!(a.ablate & 64))   // diagnostics: OSE_URL_ABLATE 64 skips the image writes (wrong output)
+        assemble_group((lds_out_u8*)sm.bm[wv], L, (uint32_t)(stage - (uint8_t*)&sm), sm.segs[wv], sm.cls[wv], sm.bn,
+                       bn_src, p, seg_off, local);
       wave_lds_sync();
       uint4* dst = reinterpret_cast<uint4*>(a.scratch + region + scr_used);
       for (uint32_t k = lane; k < n16; k += kWave) {
