@@ -1389,7 +1389,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     const uint64_t i = (uint64_t)g * kWave + lane;
     const uint32_t g2 = g + stride;
     const bool more = g2 < a.n_groups;
-    // in flight while this group is planned: bytes of the next group, columns of the one after
+    // in flight while this group is planned: the columns of the group after
+    // the next (and, with two stage buffers, the next group's bytes)
     const bool np2 = more && plan_gate(nxt) == 2;
     StageDma pf2{0, 0};
     if constexpr (kPlanBufs == 2)
