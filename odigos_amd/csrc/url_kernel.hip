@@ -1638,10 +1638,29 @@ __device__ __forceinline__ void copy_rest(const CopyJob& j, uint4 v, uint32_t& c
     copy_round(j.gdst, j.shift, j.endb, c0, j.nchunk, v, carry);
   }
 }
+// One group per iteration at eight waves per SIMD (62 VGPRs): on one box it
+// beat the two-groups-per-iteration form below (83 VGPRs, five waves) by 3-5%
+// on C4 / C5 / C2 (tools/gpu_r2_cp.sh) -- more resident waves hide the two
+// memory round trips per group better than the explicit pairing.
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void url_copy_kernel(UrlKernelArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t stride = wave_stride();
+  for (uint32_t g = wave_first_group(); g < a.n_groups; g += stride) {
+    const CopyCols A = copy_cols(a, g, lane);
+    uint32_t unused;
+    const uint32_t la = wave_excl_scan(A.len, &unused);
+    const uint64_t ia = (uint64_t)g * kWave + lane;
+    const CopyJob ja = copy_job(a, A);
+    const uint4 va = copy_load(ja, 0);
+    if (ia < a.n_spans) a.tmpl[ia] = ose_strref{(uint32_t)(A.base + la), A.len};
+    uint32_t carry = 0;
+    if (ja.on) copy_rest(ja, va, carry);
+  }
+}
 // Two groups per iteration (g and g + stride): their columns are loaded
 // together and their first scratch rounds together, so a wave waits two
-// memory round trips per two groups.
-__global__ __launch_bounds__(kThreads) void url_copy_kernel(UrlKernelArgs a) {
+// memory round trips per two groups (kept for A/B: OSE_COPY_PAIR=1).
+__global__ __launch_bounds__(kThreads) void url_copy_pair_kernel(UrlKernelArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t stride = wave_stride();
   for (uint32_t g = wave_first_group(); g < a.n_groups; g += 2 * stride) {
@@ -1892,8 +1911,15 @@ void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
     const char* g = getenv("OSE_COPY_GRID");   // tuning
     return g ? std::max<uint32_t>(1, (uint32_t)strtoul(g, nullptr, 0)) : 65536u;
   }();
+  static const bool pair = [] {
+    const char* p = getenv("OSE_COPY_PAIR");   // A/B: the two-groups-per-iteration kernel
+    return p && strtoul(p, nullptr, 0) != 0;
+  }();
   const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + 2 * kWaves - 1) / (2 * kWaves));
-  hipLaunchKernelGGL(url_copy_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+  if (pair)
+    hipLaunchKernelGGL(url_copy_pair_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(url_copy_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
 }
 void launch_url_plan_slow(const UrlKernelArgs& a, hipStream_t st) {
   // the list length is on the device: a workgroup per group up to the resident
