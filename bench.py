@@ -378,11 +378,24 @@ def main():
             A = gen.cols.n_attrsets
             node_ctr = torch.zeros(A + 1, dtype=torch.int64, device="cuda")
 
+            # TEMPLATE reads nothing the exchange writes: it runs on a second
+            # stream while the round packs, waits for the counts, moves the
+            # records and decides on the owners (the exchange
+            # overlapped with the URL stage); SIZE | APPLY_KEEP joins both
+            side = torch.cuda.Stream()
+            side_h = side.cuda_stream
+            tmpl_st = local_st & native.STAGE_TEMPLATE
+            rest_st = local_st & ~native.STAGE_TEMPLATE
+
             def step():
+                if tmpl_st:
+                    side.wait_stream(stream)   # the previous step's SIZE has read this step's outputs
+                    eng.process_device(db, tmpl_st, native.GROUP_TRACE_ID, seed=0x5EED, stream=side_h)
                 nx.round()
-                if local_st & (native.STAGE_TEMPLATE | native.STAGE_SIZE):
-                    eng.process_device(db, local_st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
-                if local_st & native.STAGE_SIZE:
+                if tmpl_st:
+                    stream.wait_stream(side)
+                if rest_st & native.STAGE_SIZE:
+                    eng.process_device(db, rest_st, native.GROUP_TRACE_ID, seed=0x5EED, stream=sh)
                     nx.allreduce_counters(db.outs.attrset_bytes, node_ctr.data_ptr(), A)
                     nx.allreduce_counters(db.outs.accepted_spans, node_ctr.data_ptr() + 8 * A, 1)
         else:
@@ -429,7 +442,7 @@ def main():
                       "exchange_record_bytes_per_span": native.XREC_BYTES * st_[0] / max(st_[2], 1)})
         out_kernels = dict(prof)
         extra["exchange_kernels_ms"] = {k: v["ms"] / max(args.steps, 1) for k, v in out_kernels.items()
-                                        if k in ("shard_pack", "shard_unpack")}
+                                        if k in ("shard_pack", "shard_unpack", "owner_sample")}
     if args.workload == "owner":
         b_alg = None
         achieved = 0.0

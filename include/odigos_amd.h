@@ -248,7 +248,10 @@ typedef struct ose_batch ose_batch;
  * regexp to a DFA; a regexp the DFA compiler cannot express is OSE_ENOTSUP
  * (there is no host fallback).                                              */
 int ose_engine_create(const char* cfg_json, ose_engine** out);
-/* Every ose_batch and ose_otlp_batch of the engine must be released first. */
+/* The engine's batches (ose_batch, ose_otlp_batch, ose_otlp_out, ose_gbt)
+ * may be released before or after this call: each holds a reference, and
+ * the engine is freed (after a device synchronise) when the last one goes.
+ * No other call may use `eng` after it.                                     */
 void ose_engine_destroy(ose_engine* eng);
 
 /* Device selection: an engine lives on the HIP device that is current on
@@ -384,7 +387,12 @@ void ose_nccl_comm_destroy(void* comm);
  * the scatter into outs->keep.  Every rank of the communicator calls it for
  * the same round.  The calling thread waits once (the record counts size
  * the split).  stats (optional, [3]): records sent, records received, spans.
- * Rounds on one engine are serialised.                                      */
+ * Rounds on one engine are serialised, on the host and on the device (a
+ * round queued on another stream waits for the previous round's transfers).
+ * Errors this rank can see alone (arguments, columns, scratch) are returned
+ * before the first collective.  An error after it (a transfer, the owner's
+ * SAMPLE stage) leaves the peers inside a collective: as after any NCCL
+ * error, the communicator must then be destroyed by every rank.            */
 int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs,
                         void* nccl_comm, int rank, int n_ranks, const ose_rand* rnd,
                         void* hip_stream, uint64_t* stats);
@@ -500,6 +508,13 @@ int ose_gbt_release(ose_gbt* g, int64_t now_ns, void* hip_stream, const ose_colu
 int ose_gbt_stats(const ose_gbt* g, uint64_t* out8);
 /* copies every column of the last release whose dst pointer is non-NULL */
 int ose_gbt_download(const ose_gbt* g, const ose_columns* dst);
+
+/* HIP errors met by the entry points that return nothing (ose_*_release,
+ * ose_*_destroy, ose_host_free) since the library loaded: they are recorded
+ * here instead of being left in the HIP runtime's per-thread last-error
+ * slot.  Returns the count; `last` (may be NULL) receives the latest one as
+ * "entry point: hipErrorName (text)".                                        */
+uint64_t ose_dropped_errors(char* last, size_t cap);
 
 /* Message of the last failure on this thread ("" if none). */
 const char* ose_last_error(void);

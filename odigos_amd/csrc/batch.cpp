@@ -216,6 +216,7 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
         e->batch_pool.erase(e->batch_pool.begin() + (long)best);
         e->batch_pool_bytes -= b->bytes;
         b->set_dims(*dims);
+        engine_retain(e);
         *out = reinterpret_cast<ose_batch*>(b);
         return 0;
       }
@@ -225,6 +226,7 @@ int ose_batch_acquire(ose_engine* eng, const ose_columns* dims, ose_batch** out)
   b->e = e;
   rc = b->build(*dims);
   if (rc) { delete b; return rc; }
+  engine_retain(e);
   *out = reinterpret_cast<ose_batch*>(b);
   return 0;
 }
@@ -234,19 +236,21 @@ ose_outputs* ose_batch_outputs(ose_batch* bb) { return bb ? &reinterpret_cast<Ba
 
 void ose_batch_release(ose_batch* bb) {
   if (!bb) return;
-  LastErrorScope keep;
+  LastErrorScope keep("ose_batch_release");
   Batch* b = reinterpret_cast<Batch*>(bb);
   Engine* e = b->e;
   (void)bind_device(e);
-  {
+  bool pooled = false;
+  if (!e->closed.load()) {
     std::lock_guard<std::mutex> g(e->mu);
     if (!b->tmpl_h_big && e->batch_pool.size() < kPoolMax && e->batch_pool_bytes + b->bytes <= kPoolBytesMax) {
       e->batch_pool.push_back(b);
       e->batch_pool_bytes += b->bytes;
-      return;
+      pooled = true;
     }
   }
-  delete b;
+  if (!pooled) delete b;
+  engine_unref(e);
 }
 
 int ose_process(ose_engine* eng, ose_batch* bb, uint32_t stage_mask, uint32_t group_mode, const ose_rand* rnd) {

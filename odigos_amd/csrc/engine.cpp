@@ -296,6 +296,25 @@ int bind_device(const Engine* e) {
   return 0;
 }
 
+static std::mutex g_dropped_mu;
+static uint64_t g_dropped_count = 0;
+static std::string g_dropped_last;
+void note_dropped_error(const char* where, hipError_t err) {
+  std::lock_guard<std::mutex> g(g_dropped_mu);
+  g_dropped_count++;
+  g_dropped_last = std::string(where) + ": " + hipGetErrorName(err) + " (" + hipGetErrorString(err) + ")";
+}
+
+void engine_retain(Engine* e) { e->refs.fetch_add(1, std::memory_order_relaxed); }
+
+void engine_unref(Engine* e) {
+  if (e->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+  LastErrorScope keep("engine_unref");
+  (void)bind_device(e);
+  (void)hipDeviceSynchronize();   // nothing in flight may still use the buffers freed below
+  delete e;
+}
+
 int upload(const std::vector<uint8_t>& host, uint8_t** dev) {
   HIP_TRY(hipMalloc(dev, host.size()));
   HIP_TRY(hipMemcpy(*dev, host.data(), host.size(), hipMemcpyHostToDevice));
@@ -482,6 +501,12 @@ extern "C" {
 
 const char* ose_last_error(void) { return g_last_error.c_str(); }
 
+uint64_t ose_dropped_errors(char* last, size_t cap) {
+  std::lock_guard<std::mutex> g(g_dropped_mu);
+  if (last && cap) snprintf(last, cap, "%s", g_dropped_last.c_str());
+  return g_dropped_count;
+}
+
 int ose_engine_create(const char* cfg_json, ose_engine** out) {
   if (!out) return fail(OSE_EINVAL, "out is NULL");
   *out = nullptr;
@@ -541,10 +566,9 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
 
 void ose_engine_destroy(ose_engine* eng) {
   if (!eng) return;
-  LastErrorScope keep;
-  (void)bind_device(reinterpret_cast<Engine*>(eng));
-  (void)hipDeviceSynchronize();   // nothing in flight may still use the buffers freed below
-  delete reinterpret_cast<Engine*>(eng);
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  e->closed.store(true);
+  engine_unref(e);
 }
 
 int ose_host_alloc(size_t bytes, void** out) {
@@ -555,7 +579,7 @@ int ose_host_alloc(size_t bytes, void** out) {
   return 0;
 }
 void ose_host_free(void* p) {
-  LastErrorScope keep;
+  LastErrorScope keep("ose_host_free");
   if (p) (void)hipHostFree(p);
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <mutex>
@@ -20,14 +21,24 @@ struct Engine;
 // goroutines migrate across OS threads; HIP's current device is per thread)
 int bind_device(const Engine* e);
 int ensure_device();
+void engine_retain(Engine* e);
+// drops one reference; the last one synchronises the device and frees the engine
+void engine_unref(Engine* e);
 // The release entry points return nothing, so a HIP error their clean-up
-// meets is dropped; this keeps it out of the runtime's per-thread last-error
-// slot too, where the caller's next launch check (torch's, a shim's) would
-// report it against its own work.  An error already pending on entry is left.
+// meets cannot be returned; it is taken out of the runtime's per-thread
+// last-error slot (where the caller's next launch check, torch's or a
+// shim's, would report it against its own work) and recorded instead:
+// ose_dropped_errors() gives the count and the last one (the GPU tests fail
+// on any).  An error already pending on entry is left alone.
+void note_dropped_error(const char* where, hipError_t err);
 struct LastErrorScope {
-  hipError_t prev = hipPeekAtLastError();
+  const char* where;
+  hipError_t prev;
+  explicit LastErrorScope(const char* w) : where(w), prev(hipPeekAtLastError()) {}
   ~LastErrorScope() {
-    if (prev == hipSuccess) (void)hipGetLastError();
+    if (prev != hipSuccess) return;
+    const hipError_t now = hipGetLastError();
+    if (now != hipSuccess) note_dropped_error(where, now);
   }
 };
 bool stream_capturing(hipStream_t st);
@@ -71,6 +82,13 @@ struct Workspace {
 };
 
 struct Engine {
+  // Lifetime: ose_engine_destroy drops the creator's reference; every live
+  // child (ose_batch, ose_otlp_batch, ose_otlp_out, ose_gbt) holds one more,
+  // so the engine is freed when the last of them is released, in whatever
+  // order a shim's finalizers run.  Children released after the destroy are
+  // freed instead of pooled.
+  std::atomic<int> refs{1};
+  std::atomic<bool> closed{false};
   int device = 0;   // the HIP device current when the engine was created; every call runs there
   UrlTemplateConfig url;
   SamplingConfig sampling;

@@ -122,8 +122,24 @@ struct Gbt {
   // stats: created, released traces, evicted traces, released spans, added spans
   uint64_t created = 0, released = 0, evicted = 0, released_spans = 0, added_spans = 0;
 
+  // the persistent id table (gbt_kernel.hip): slots claimed since its last
+  // rebuild (live ids and tombstones), the number of the last add
+  uint64_t slots_used = 0;
+  uint32_t add_gen = 0;
+  bool table_valid = false;
+
   uint64_t evict_below() const { return next_seq > num_traces ? next_seq - num_traces : 0; }
   uint64_t live_lo() const { return std::max(rel_end, evict_below()); }
+  // traces whose wait is over at `now`: [.., expired_below(now)) (created by
+  // the calls at least wait_duration ago; the next release hands them out)
+  uint64_t expired_below(int64_t now) const {
+    uint64_t b = rel_end;
+    for (const Epoch& ep : epochs) {
+      if (ep.t + wait_ns > now) break;
+      b = std::max(b, ep.seq1);
+    }
+    return b;
+  }
 };
 
 namespace {
@@ -183,16 +199,28 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
   if (g->pool_end - g->pool_begin + n > g->pool_cap || g->scope_end - g->scope_begin + S > g->scope_cap)
     return fail(OSE_ERANGE, "groupbytrace: the store is full (spans waiting for wait_duration exceed its capacity)");
   int rc;
-  // the id table: 2x the live traces plus the batch, generation-tagged
-  const uint64_t live = g->next_seq - g->live_lo();
+  // An added span joins its id's trace only while that trace is waiting: not
+  // released, not evicted, and not past its wait_duration at `now` (contrib's
+  // timer would have sent it downstream at its deadline, and later spans of
+  // the id start a new trace; the expired one still goes out at the next
+  // release).
+  const uint64_t lo = std::max(g->live_lo(), g->expired_below(now));
+  const uint64_t live = g->next_seq - lo;
+  // the persistent id table: at least 4x the live traces plus the batch;
+  // re-inserted from the live traces when it grows, when tombstones and live
+  // ids would pass half of it, and when the epoch tag wraps
   uint64_t slots = 1024;
-  while (slots < 2 * (live + n)) slots <<= 1;
-  if (slots > g->table_slots || ++g->epoch >= (1u << 29)) {
+  while (slots < 4 * (live + n)) slots <<= 1;
+  bool rebuild = !g->table_valid || g->slots_used + n > g->table_slots / 2;
+  if (slots > g->table_slots || g->epoch + 1 >= (1u << 29)) {
     if ((rc = g->table.need(std::max(slots, g->table_slots) * sizeof(GbtSlot)))) return rc;
     g->table_slots = std::max(slots, g->table_slots);
     HIP_TRY(hipMemsetAsync(g->table.p, 0, g->table_slots * sizeof(GbtSlot), st));
-    g->epoch = 1;
+    g->epoch = 0;
+    rebuild = true;
   }
+  if (rebuild) g->epoch++;
+  g->add_gen = g->add_gen + 1 == 0 ? 1 : g->add_gen + 1;
   // scratch: slot_of (8n), flag, rank, strlen, stroff (4n each), the attribute-set map
   const size_t A = c->n_attrsets;
   if ((rc = g->scratch.need(up(8 * n) + 4 * up(4 * n + 16) + up(4 * A + 16))) || (rc = words_need(g, n))) return rc;
@@ -213,33 +241,45 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
   a.n = n;
   a.n_scopes = S;
   a.next_seq = g->next_seq;
-  a.live_lo = g->live_lo();
+  a.live_lo = lo;
   a.live_hi = g->next_seq;
+  a.add_gen = g->add_gen;
   a.pool_pos = g->pool_end;
   a.scope_pos = g->scope_end;
   a.arena_pos = g->arena_end;
+  a.arena_room = g->arena_cap - (g->arena_end - g->arena_begin);
   HIP_TRY(hipMemsetAsync(g->words.p, 0, 16, st));   // error word, totals
   uint32_t* totals = reinterpret_cast<uint32_t*>(g->words.p) + 1;   // [0] new traces, [1] string bytes
+  a.totals = totals;
   (void)hipGetLastError();
-  launch_gbt_rebuild(a, st);
+  if (rebuild) launch_gbt_rebuild(a, st);
   launch_gbt_lookup(a, st);
   launch_gbt_creator(a, st);
   HIP_TRY(hipGetLastError());
   if ((rc = scan_u32(g, a.flag, a.rank, n, totals, st))) return rc;
+  if ((rc = scan_u32(g, a.strlen, a.stroff, n, totals + 1, st))) return rc;
+  // every kernel from here stores nothing when the batch's strings do not
+  // fit the arena ring (error bit 8): a refused add leaves the store as it was
   launch_gbt_assign(a, st);
   launch_gbt_append(a, st);
   launch_gbt_scopes(a, st);
+  launch_gbt_strings(a, st);
   HIP_TRY(hipGetLastError());
-  if ((rc = scan_u32(g, a.strlen, a.stroff, n, totals + 1, st))) return rc;
   uint32_t h[4] = {0, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(h, g->words.p, 16, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  if (h[0]) return fail(OSE_EDEVICE, "groupbytrace: device table error " + std::to_string(h[0]));
-  const uint64_t created = h[1], bytes = h[2];
-  if (g->arena_end - g->arena_begin + bytes > g->arena_cap)
+  if (rebuild) g->slots_used = live;
+  g->table_valid = true;
+  if (h[0] & 8u) {
+    g->slots_used += n;   // ids the lookups claimed stay as tombstones
     return fail(OSE_ERANGE, "groupbytrace: the string arena is full (bytes waiting for wait_duration exceed its capacity)");
-  launch_gbt_strings(a, st);
-  HIP_TRY(hipGetLastError());
+  }
+  if (h[0]) {
+    g->table_valid = false;
+    return fail(OSE_EDEVICE, "groupbytrace: device table error " + std::to_string(h[0]));
+  }
+  const uint64_t created = h[1], bytes = h[2];
+  g->slots_used += created;
   g->next_seq += created;
   g->created += created;
   g->added_spans += n;
@@ -512,16 +552,19 @@ int ose_gbt_create(ose_engine* eng, const char* cfg_json, uint64_t span_capacity
     *p.dst = g->scopes.p + off;
     off = up(off + p.bytes + 16);
   }
+  engine_retain(e);   // dropped by ose_gbt_destroy
   *out = reinterpret_cast<ose_gbt*>(g);
   return 0;
 }
 
 void ose_gbt_destroy(ose_gbt* gg) {
   if (!gg) return;
-  LastErrorScope keep;
+  LastErrorScope keep("ose_gbt_destroy");
   auto* g = reinterpret_cast<Gbt*>(gg);
-  (void)bind_device(g->e);
+  Engine* e = g->e;
+  (void)bind_device(e);
   delete g;
+  engine_unref(e);
 }
 
 int ose_gbt_add(ose_gbt* gg, const ose_columns* cols, const uint32_t* attrset_map, int64_t now_ns, void* hip_stream) {

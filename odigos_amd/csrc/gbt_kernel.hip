@@ -10,10 +10,11 @@
 //   * traces are numbered in creation order (seq, 64-bit); the ring of
 //     num_traces ids (contrib's ringBuffer) is ring_tid[seq % num_traces],
 //     so a trace created num_traces creations after another evicts it;
-//   * the id -> seq table is rebuilt for every add from the live traces
-//     (generation-tagged slots, nothing to clear), then the batch's spans
-//     look themselves up; ids not found are new traces, numbered in the
-//     order of their first span in the batch;
+//   * the id -> seq table persists across adds (tombstones: an id whose
+//     trace is gone reclaims its own slot; the table is re-inserted from the
+//     live traces only when it grows or tombstones fill half of it); the
+//     batch's spans look themselves up, and ids without a live trace start
+//     new traces, numbered in the order of their first span in the batch;
 //   * spans go to a pool ring in arrival order (columns + a string block in
 //     an arena ring), scopes to a scope ring (the fragment's resource and
 //     scope columns);
@@ -43,11 +44,22 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-// Insert-or-find (the trace table's publish protocol, trace_kernel.hip):
-// a stale-epoch slot is claimed BUSY, the key and value stored with
-// agent-scope stores, drained, then READY.  Returns the slot; *fresh says
-// whether this call claimed it.  UINT64_MAX on failure (error flagged).
-__device__ uint64_t gbt_insert(const GbtArgs& a, uint64_t hi, uint64_t lo, uint64_t seq, uint32_t pos, bool* fresh) {
+// The id table persists across adds.  A slot holds an id and the creation
+// number of its newest trace; the trace is live for an added span iff that
+// number is in [live_lo, live_hi) (not released, evicted or expired).  A
+// slot whose trace is no longer live stays as a tombstone: lookups of other
+// ids probe past it, and its own id takes it back (reclaim) when it comes
+// again.  The host bumps the epoch and re-inserts the live traces only when
+// the table grows or tombstones fill half of it, so an add costs O(batch),
+// not O(traces waiting).
+//
+// Slots are published with the trace table's protocol (trace_kernel.hip): a
+// stale-epoch slot is claimed BUSY, its fields stored with agent-scope
+// stores, drained, then READY.
+
+// rebuild: one live trace per id (an id's expired instance is outside
+// [live_lo, live_hi), so each id occurs at most once; the newest wins anyway)
+__device__ void gbt_put(const GbtArgs& a, uint64_t hi, uint64_t lo, uint64_t seq) {
   const uint32_t busy = (a.epoch << 2) | 1u, ready = (a.epoch << 2) | 2u;
   uint64_t h = mix64(hi ^ mix64(lo)) & a.table_mask;
   uint32_t probes = 0, spins = 0;
@@ -61,15 +73,60 @@ __device__ uint64_t gbt_insert(const GbtArgs& a, uint64_t hi, uint64_t lo, uint6
         __hip_atomic_store(&s->hi, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->lo, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->first, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&s->state, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      continue;
+    }
+    if ((st & 3u) != 2u) {
+      if (++spins > (1u << 20)) {
+        atomicOr(a.error, 1u);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    if (__hip_atomic_load(&s->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hi &&
+        __hip_atomic_load(&s->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo) {
+      __hip_atomic_fetch_max(&s->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    h = (h + 1) & a.table_mask;
+    if (++probes > a.table_mask) {
+      atomicOr(a.error, 4u);
+      return;
+    }
+  }
+}
+
+// lookup of an added span: the slot of its id, which holds either a live
+// trace or (claimed or reclaimed for this add) kGbtUnset | add_gen with the
+// smallest batch position of the id in `first`.  UINT64_MAX on failure.
+__device__ uint64_t gbt_lookup(const GbtArgs& a, uint64_t hi, uint64_t lo, uint32_t pos) {
+  const uint32_t busy = (a.epoch << 2) | 1u, ready = (a.epoch << 2) | 2u;
+  const uint64_t mine = kGbtUnset | a.add_gen;
+  uint64_t h = mix64(hi ^ mix64(lo)) & a.table_mask;
+  uint32_t probes = 0, spins = 0;
+  for (;;) {
+    GbtSlot* s = &a.table[h];
+    const uint32_t st = __hip_atomic_load(&s->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((st >> 2) != a.epoch) {   // empty: the id is not in the table
+      uint32_t expect = st;
+      if (__hip_atomic_compare_exchange_strong(&s->state, &expect, busy, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(&s->hi, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->lo, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->seq, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&s->first, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&s->state, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *fresh = true;
         return h;
       }
-      continue;   // lost the race for this slot: look at it again
+      continue;
     }
-    if ((st & 3u) != 2u) {   // another lane is publishing this slot
+    if ((st & 3u) != 2u) {   // another lane is publishing or reclaiming this slot
       if (++spins > (1u << 20)) {
         atomicOr(a.error, 1u);
         return ~0ull;
@@ -77,45 +134,58 @@ __device__ uint64_t gbt_insert(const GbtArgs& a, uint64_t hi, uint64_t lo, uint6
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    const uint64_t h2 = __hip_atomic_load(&s->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t l2 = __hip_atomic_load(&s->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (h2 == hi && l2 == lo) {
-      *fresh = false;
+    if (__hip_atomic_load(&s->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != hi ||
+        __hip_atomic_load(&s->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != lo) {
+      h = (h + 1) & a.table_mask;   // another id (live or a tombstone)
+      if (++probes > a.table_mask) {
+        atomicOr(a.error, 4u);
+        return ~0ull;
+      }
+      continue;
+    }
+    const uint64_t seq = __hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seq == mine) {   // numbered by this add
+      atomicMin(&s->first, pos);
       return h;
     }
-    h = (h + 1) & a.table_mask;
-    if (++probes > a.table_mask) {
-      atomicOr(a.error, 4u);
-      return ~0ull;
+    if (seq < kGbtUnset && seq >= a.live_lo && seq < a.live_hi) return h;   // a live trace
+    // the id's last trace is gone (released, evicted, expired) or an earlier
+    // add failed while numbering it: the id starts a new trace in this slot
+    uint32_t expect = st;
+    if (__hip_atomic_compare_exchange_strong(&s->state, &expect, busy, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      if (__hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine) {
+        atomicMin(&s->first, pos);   // reclaimed by another lane between our reads
+      } else {
+        __hip_atomic_store(&s->seq, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s->first, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&s->state, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return h;
     }
   }
 }
 
 // ---- add -------------------------------------------------------------------
 
-// the live traces [live_lo, live_hi) back into the table
+// the live traces [live_lo, live_hi) back into a fresh epoch of the table
 __global__ __launch_bounds__(kGbtThreads) void gbt_rebuild_kernel(GbtArgs a) {
   for (uint64_t s = a.live_lo + (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x; s < a.live_hi;
        s += (uint64_t)gridDim.x * kGbtThreads) {
     const uint64_t r = s % a.num_traces;
-    bool fresh;
-    (void)gbt_insert(a, a.ring_tid[2 * r], a.ring_tid[2 * r + 1], s, ~0u, &fresh);
+    gbt_put(a, a.ring_tid[2 * r], a.ring_tid[2 * r + 1], s);
   }
 }
 
-// every span of the batch: its table slot; new ids get an unset seq and
-// the smallest position of the batch that carries them
+// every span of the batch: its table slot
 __global__ __launch_bounds__(kGbtThreads) void gbt_lookup_kernel(GbtArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
   if (i >= a.n) return;
-  const uint64_t hi = a.cols.trace_id[2 * i], lo = a.cols.trace_id[2 * i + 1];
-  bool fresh;
-  const uint64_t h = gbt_insert(a, hi, lo, kUnset, (uint32_t)i, &fresh);
-  a.slot_of[i] = h;
-  if (h != ~0ull && !fresh) atomicMin(&a.table[h].first, (uint32_t)i);
+  a.slot_of[i] = gbt_lookup(a, a.cols.trace_id[2 * i], a.cols.trace_id[2 * i + 1], (uint32_t)i);
 }
 
-// creators: the first span of each new trace
+// creators (the first span of each new trace) and each span's string block length
 __global__ __launch_bounds__(kGbtThreads) void gbt_creator_kernel(GbtArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
   if (i >= a.n) return;
@@ -123,14 +193,31 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_creator_kernel(GbtArgs a) {
   uint32_t f = 0;
   if (h != ~0ull) {
     const GbtSlot& s = a.table[h];
-    f = s.seq == kUnset && s.first == (uint32_t)i;
+    f = s.seq == (kGbtUnset | a.add_gen) && s.first == (uint32_t)i;
   }
   a.flag[i] = f;
+  const ose_columns& c = a.cols;
+  uint32_t len = 0;
+  if (c.route) len += c.route[i].len;
+  if (c.path) len += c.path[i].len;
+  for (uint32_t k = 0; k < a.n_attr_keys; k++)
+    if (c.attr_type[(uint64_t)k * a.n + i] == OSE_ATTR_STR) len += (uint32_t)(c.attr_val[(uint64_t)k * a.n + i] >> 32);
+  a.strlen[i] = len;
+}
+
+// the batch's strings do not fit the arena ring: nothing of the batch is
+// stored (no trace numbered, no ring slot overwritten) and the add fails
+__device__ __forceinline__ bool gbt_batch_refused(const GbtArgs& a) {
+  return (uint64_t)a.totals[1] > a.arena_room;
 }
 
 // new traces numbered in first-appearance order; the ring remembers their ids
 __global__ __launch_bounds__(kGbtThreads) void gbt_assign_kernel(GbtArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
+  if (gbt_batch_refused(a)) {
+    if (i == 0) atomicOr(a.error, 8u);
+    return;
+  }
   if (i >= a.n || !a.flag[i]) return;
   const uint64_t seq = a.next_seq + a.rank[i];
   a.table[a.slot_of[i]].seq = seq;
@@ -139,10 +226,10 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_assign_kernel(GbtArgs a) {
   a.ring_tid[2 * r + 1] = a.cols.trace_id[2 * i + 1];
 }
 
-// the spans into the pool ring; the length of each span's string block
+// the spans into the pool ring
 __global__ __launch_bounds__(kGbtThreads) void gbt_append_kernel(GbtArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
-  if (i >= a.n) return;
+  if (i >= a.n || gbt_batch_refused(a)) return;
   const GbtPool& P = a.pool;
   const ose_columns& c = a.cols;
   const uint64_t p = (a.pool_pos + i) % a.pool_cap;
@@ -159,12 +246,6 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_append_kernel(GbtArgs a) {
   P.name_len[p] = c.name_len ? c.name_len[i] : 0;
   P.attr_match[p] = c.attr_match ? c.attr_match[i] : 0;
   P.origin[p] = a.scope_pos + c.scope[i];
-  uint32_t len = 0;
-  if (c.route) len += c.route[i].len;
-  if (c.path) len += c.path[i].len;
-  for (uint32_t k = 0; k < a.n_attr_keys; k++)
-    if (c.attr_type[(uint64_t)k * a.n + i] == OSE_ATTR_STR) len += (uint32_t)(c.attr_val[(uint64_t)k * a.n + i] >> 32);
-  a.strlen[i] = len;
 }
 
 __device__ __forceinline__ void ring_copy(uint8_t* ring, uint64_t cap, uint64_t dst, const uint8_t* src, uint32_t n) {
@@ -179,7 +260,7 @@ __device__ __forceinline__ void ring_copy(uint8_t* ring, uint64_t cap, uint64_t 
 // the pool are relative to the block
 __global__ __launch_bounds__(kGbtThreads) void gbt_strings_kernel(GbtArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
-  if (i >= a.n) return;
+  if (i >= a.n || gbt_batch_refused(a)) return;
   const GbtPool& P = a.pool;
   const ose_columns& c = a.cols;
   const uint64_t p = (a.pool_pos + i) % a.pool_cap;
@@ -219,7 +300,7 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_strings_kernel(GbtArgs a) {
 // the batch's scopes into the scope ring, with their resource's columns
 __global__ __launch_bounds__(kGbtThreads) void gbt_scopes_kernel(GbtArgs a) {
   const uint64_t s = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
-  if (s >= a.n_scopes) return;
+  if (s >= a.n_scopes || gbt_batch_refused(a)) return;
   const ose_columns& c = a.cols;
   const GbtScopes& Q = a.scopes;
   const uint64_t q = (a.scope_pos + s) % a.scope_cap;

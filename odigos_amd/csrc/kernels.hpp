@@ -426,8 +426,10 @@ struct GbtSlot {              // trace id -> creation number (32 B, generation-t
   uint32_t state;             // epoch << 2 | {0 empty, 1 busy, 2 ready}
   uint32_t first;             // smallest batch position carrying the id (new ids)
   uint64_t hi, lo;
-  uint64_t seq;               // creation number; ~0 while a new id is being numbered
+  uint64_t seq;               // creation number of the id's newest trace; kGbtUnset | add
+                              // while add number `add` is numbering a new trace for it
 };
+constexpr uint64_t kGbtUnset = 0xFFFFFFFF00000000ull;
 struct GbtPool {              // spans waiting for release (ring of pool_cap)
   uint64_t* tid;              // {hi, lo}
   uint64_t *start, *end, *attr_match, *seq, *origin, *str_off;
@@ -461,7 +463,11 @@ struct GbtArgs {
   uint32_t* error;
   uint64_t* ring_tid;         // [2 * num_traces]
   uint64_t num_traces;
-  uint64_t live_lo, live_hi;  // rebuild range
+  uint64_t live_lo, live_hi;  // traces an added span may join (and the rebuild range)
+  uint32_t add_gen;           // number of this add (tags the ids it numbers)
+  uint32_t _pad0;
+  uint64_t arena_room;        // string bytes the arena ring can still take
+  const uint32_t* totals;     // [0] new traces, [1] string bytes of the batch (scans)
   // add: the batch
   ose_columns cols;
   uint64_t n, n_scopes;

@@ -617,7 +617,7 @@ void otlp_out_release(OtlpOut* o) {
     for (auto& x : o->outs)
       if (x.data) o->work->bufs.emplace_back(x.data, x.cap);
     o->outs.clear();
-    if (o->e) {
+    if (o->e && !o->e->closed.load()) {
       std::lock_guard<std::mutex> g(o->e->mu);
       if (o->e->enc_pool.size() < 8) {
         o->e->enc_pool.push_back(o->work);
@@ -626,6 +626,7 @@ void otlp_out_release(OtlpOut* o) {
     }
     delete o->work;
   }
+  if (o->e) engine_unref(o->e);
   delete o;
 }
 
@@ -750,7 +751,7 @@ int ose_router_create(const char* cfg_json, ose_router** out) {
 }
 
 void ose_router_destroy(ose_router* r) {
-  LastErrorScope keep;
+  LastErrorScope keep("ose_router_destroy");
   delete reinterpret_cast<Router*>(r);
 }
 
@@ -781,7 +782,7 @@ int ose_otlp_out_get(const ose_otlp_out* o, uint32_t k, const char** name, const
 }
 
 void ose_otlp_out_release(ose_otlp_out* o) {
-  LastErrorScope keep;
+  LastErrorScope keep("ose_otlp_out_release");
   otlp_out_release(reinterpret_cast<OtlpOut*>(o));
 }
 

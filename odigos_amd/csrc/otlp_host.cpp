@@ -994,6 +994,7 @@ int ose_otlp_decode(ose_engine* eng, const void* pb, size_t len, void* hip_strea
     delete b;
     return rc;
   }
+  engine_retain(e);
   *out = reinterpret_cast<ose_otlp_batch*>(b);
   return 0;
 }
@@ -1175,6 +1176,7 @@ int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs
   if ((rc = layout_to_host(b, st))) return rc;
   auto* o = new OtlpOut();
   o->e = e;
+  engine_retain(e);   // dropped by otlp_out_release
   {
     std::lock_guard<std::mutex> g(e->mu);
     if (!e->enc_pool.empty()) {
@@ -1236,18 +1238,20 @@ int osehost_otlp_encode(const uint8_t* pb, size_t len, const uint8_t* keep, int 
 
 void ose_otlp_release(ose_otlp_batch* bb) {
   if (!bb) return;
-  LastErrorScope keep;
+  LastErrorScope keep("ose_otlp_release");
   auto* b = reinterpret_cast<OtlpBatchImpl*>(bb);
   Engine* e = b->e;
   (void)bind_device(e);
-  {
+  bool pooled = false;
+  if (!e->closed.load()) {
     std::lock_guard<std::mutex> g(e->mu);
     if (e->otlp_pool.size() < 16) {
       e->otlp_pool.push_back(b);
-      return;
+      pooled = true;
     }
   }
-  delete b;
+  if (!pooled) delete b;
+  engine_unref(e);
 }
 
 }  // extern "C"

@@ -9,6 +9,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <type_traits>
@@ -71,8 +73,11 @@ int nccl_fail(const char* what, ncclResult_t rc) {
     if (_r != ncclSuccess) return nccl_fail(#expr, _r); \
   } while (0)
 
-// device scratch of one exchange round (per engine; rounds on one engine are
-// serialised by its mutex)
+// device scratch of one exchange round (per engine).  Rounds on one engine
+// are serialised on the host by `mu` and on the device by `done`: the next
+// round's stream waits for the event the previous round recorded at its end,
+// so a round queued on another stream cannot pack into `send` while the
+// previous round's transfers still read it.
 struct XBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -92,10 +97,13 @@ struct XScratch {
   std::mutex mu;
   XBuf send, recv, pos, counts, keep_back, keep_x, cols;
   uint64_t* host_counts = nullptr;   // pinned [2 * 64]
+  hipEvent_t done = nullptr;         // recorded at the end of the last round
+  bool done_set = false;
   ~XScratch() {
     for (XBuf* b : {&send, &recv, &pos, &counts, &keep_back, &keep_x, &cols})
       if (b->p) (void)hipFree(b->p);
     if (host_counts) (void)hipHostFree(host_counts);
+    if (done) (void)hipEventDestroy(done);
   }
 };
 std::mutex g_xs_mu;
@@ -108,6 +116,139 @@ XScratch* scratch_of(const Engine* e) {
   g_xs.emplace_back(e, x);
   return x;
 }
+
+// ---- transports ------------------------------------------------------------------
+// What one exchange round needs of a collective library: a variable-size
+// all-to-all of bytes, stream-ordered on `st` (rank r sends slen[p] bytes at
+// send + soff[p] to rank p and receives rlen[p] bytes from p into
+// recv + roff[p]).  The product transport is RCCL's grouped point-to-point
+// over xGMI; the test transport moves the bytes between in-process ranks.
+struct XTransport {
+  virtual ~XTransport() = default;
+  virtual int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv,
+                        const uint64_t* roff, const uint64_t* rlen, hipStream_t st) = 0;
+  // a rank that fails in the middle of a round tells its peers (the local
+  // transport unblocks them; an RCCL communicator is left to the caller)
+  virtual void abort() {}
+};
+
+struct RcclTransport final : XTransport {
+  ncclComm_t comm;
+  int n_ranks;
+  RcclTransport(ncclComm_t c, int w) : comm(c), n_ranks(w) {}
+  int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
+                const uint64_t* rlen, hipStream_t st) override {
+    const Rccl& r = rccl();
+    ncclResult_t rc = r.group_start();
+    if (rc != ncclSuccess) return nccl_fail("ncclGroupStart", rc);
+    int err = 0;
+    for (int p = 0; p < n_ranks && !err; p++) {
+      if (slen[p] && (rc = r.send(send + soff[p], slen[p], ncclUint8, p, comm, st)) != ncclSuccess)
+        err = nccl_fail("ncclSend", rc);
+      if (!err && rlen[p] && (rc = r.recv(recv + roff[p], rlen[p], ncclUint8, p, comm, st)) != ncclSuccess)
+        err = nccl_fail("ncclRecv", rc);
+    }
+    rc = r.group_end();   // the group is closed on every path, a failed enqueue included
+    if (err) return err;
+    if (rc != ncclSuccess) return nccl_fail("ncclGroupEnd", rc);
+    return 0;
+  }
+};
+
+// In-process ranks (test transport, osehost_xgroup_*): W host threads, each
+// with its own engine and stream, on one or several devices.  A phase is two
+// rendezvous: every rank publishes its send buffer and an event recorded
+// behind the data, then pulls its pieces with device-to-device copies queued
+// behind the senders' events and records a `done` event; after the second
+// rendezvous every rank's stream waits for its peers' `done`, so a send
+// buffer is reused only after every copy out of it (NCCL send semantics).
+struct LocalGroup {
+  explicit LocalGroup(int w) : n_ranks(w), slots(w) {}
+  ~LocalGroup() {
+    for (auto& s : slots) {
+      if (s.ready) (void)hipEventDestroy(s.ready);
+      if (s.done) (void)hipEventDestroy(s.done);
+    }
+  }
+  struct Slot {
+    const uint8_t* send = nullptr;
+    const uint64_t* soff = nullptr;
+    const uint64_t* slen = nullptr;
+    hipEvent_t ready = nullptr, done = nullptr;
+  };
+  const int n_ranks;
+  std::vector<Slot> slots;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  bool broken = false;
+  int barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return fail(OSE_EDEVICE, "in-process exchange group: a peer failed");
+    const uint64_t gen = generation;
+    if (++arrived == n_ranks) {
+      arrived = 0;
+      generation++;
+      cv.notify_all();
+      return 0;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen || broken; })) {
+      broken = true;
+      cv.notify_all();
+      return fail(OSE_ETIMEDOUT, "in-process exchange group: a peer never arrived");
+    }
+    return broken ? fail(OSE_EDEVICE, "in-process exchange group: a peer failed") : 0;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    broken = true;
+    cv.notify_all();
+  }
+};
+
+struct LocalTransport final : XTransport {
+  LocalGroup* g;
+  int rank;
+  LocalTransport(LocalGroup* grp, int r) : g(grp), rank(r) {}
+  void abort() override { g->abort(); }
+  int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
+                const uint64_t* rlen, hipStream_t st) override {
+    LocalGroup::Slot& me = g->slots[(size_t)rank];
+    if (!me.ready && hipEventCreateWithFlags(&me.ready, hipEventDisableTiming) != hipSuccess)
+      return fail(OSE_EDEVICE, "hipEventCreate failed");
+    if (!me.done && hipEventCreateWithFlags(&me.done, hipEventDisableTiming) != hipSuccess)
+      return fail(OSE_EDEVICE, "hipEventCreate failed");
+    me.send = send;
+    me.soff = soff;
+    me.slen = slen;
+    if (hipEventRecord(me.ready, st) != hipSuccess) return fail(OSE_EDEVICE, "hipEventRecord failed");
+    if (int rc = g->barrier()) return rc;
+    int err = 0;
+    for (int p = 0; p < g->n_ranks && !err; p++) {
+      const LocalGroup::Slot& src = g->slots[(size_t)p];
+      if (src.slen[rank] != rlen[p]) {
+        err = fail(OSE_EINVAL, "in-process exchange: send and receive sizes disagree");
+        break;
+      }
+      if (!rlen[p]) continue;
+      if (hipStreamWaitEvent(st, src.ready, 0) != hipSuccess ||
+          hipMemcpyAsync(recv + roff[p], src.send + src.soff[rank], rlen[p], hipMemcpyDeviceToDevice, st) != hipSuccess)
+        err = fail(OSE_EDEVICE, "in-process exchange: device copy failed");
+    }
+    if (!err && hipEventRecord(me.done, st) != hipSuccess) err = fail(OSE_EDEVICE, "hipEventRecord failed");
+    if (err) {
+      g->abort();
+      return err;
+    }
+    if (int rc = g->barrier()) return rc;
+    for (int p = 0; p < g->n_ranks; p++)
+      if (slen[p] && hipStreamWaitEvent(st, g->slots[(size_t)p].done, 0) != hipSuccess)
+        return fail(OSE_EDEVICE, "hipStreamWaitEvent failed");
+    return 0;
+  }
+};
+
 }  // namespace
 
 void release_exchange_scratch(const Engine* e) {
@@ -128,6 +269,127 @@ using namespace ose;
     hipError_t _e = (expr);                                                                            \
     if (_e != hipSuccess) return fail(OSE_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
   } while (0)
+
+namespace ose {
+namespace {
+// One exchange round (ose_exchange_sample).  Everything that can fail on
+// this rank alone (arguments, scratch) is checked before the first
+// collective; a failure after it leaves the peers inside a collective, so
+// the transport is told (abort) and the caller must treat the communicator
+// as unusable, as after any NCCL error.
+int exchange_round(Engine* e, const ose_columns* cols, const ose_outputs* outs, XTransport& tx, int rank, int n_ranks,
+                   const ose_rand* rnd, hipStream_t st, uint64_t* stats) {
+  if (n_ranks < 1 || n_ranks > 64 || rank < 0 || rank >= n_ranks) return fail(OSE_EINVAL, "rank / n_ranks out of range");
+  if (cols->n_spans && !outs->keep) return fail(OSE_EINVAL, "outs->keep is required");
+  if (!e->has_sampling) return fail(OSE_EINVAL, "the exchange needs odigossampling on the engine");
+  if (int brc = bind_device(e)) return brc;
+  XScratch* xs = scratch_of(e);
+  std::lock_guard<std::mutex> g(xs->mu);
+  const uint64_t n = cols->n_spans, W = (uint64_t)n_ranks;
+  int rc;
+  if ((rc = xs->send.need(std::max<uint64_t>(n, 1) * kXRecBytes)) || (rc = xs->pos.need(4 * std::max<uint64_t>(n, 1))) ||
+      (rc = xs->counts.need(16 * W)) || (rc = xs->keep_back.need(std::max<uint64_t>(n, 1))))
+    return rc;
+  if (!xs->host_counts) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&xs->host_counts), 16 * 64, hipHostMallocDefault));
+  if (!xs->done) HIP_TRY(hipEventCreateWithFlags(&xs->done, hipEventDisableTiming));
+  if (xs->done_set) HIP_TRY(hipStreamWaitEvent(st, xs->done, 0));   // the previous round left the scratch
+  uint64_t* scnt_d = xs->counts.as<uint64_t>();
+  uint64_t* rcnt_d = scnt_d + W;
+  // 1. partial records per owner
+  rc = ose_shard_pack(reinterpret_cast<ose_engine*>(e), cols, (uint32_t)W, xs->send.p, scnt_d, xs->pos.as<uint32_t>(), st);
+  if (rc) return rc;   // before any collective
+  auto abort_with = [&](int code) {
+    tx.abort();
+    return code;
+  };
+  // 2. record counts, all-to-all (one u64 per peer)
+  std::vector<uint64_t> c_off(W), c_len(W, 8);
+  for (uint64_t p = 0; p < W; p++) c_off[p] = 8 * p;
+  if ((rc = tx.alltoallv(reinterpret_cast<const uint8_t*>(scnt_d), c_off.data(), c_len.data(),
+                         reinterpret_cast<uint8_t*>(rcnt_d), c_off.data(), c_len.data(), st)))
+    return abort_with(rc);
+  if (hipMemcpyAsync(xs->host_counts, scnt_d, 16 * W, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)   // the host needs the split sizes
+    return abort_with(fail(OSE_EDEVICE, "exchange: reading the record counts failed"));
+  std::vector<uint64_t> sc(xs->host_counts, xs->host_counts + W), rcv(xs->host_counts + W, xs->host_counts + 2 * W);
+  std::vector<uint64_t> sd(W + 1, 0), rd(W + 1, 0);
+  for (uint64_t p = 0; p < W; p++) {
+    sd[p + 1] = sd[p] + sc[p];
+    rd[p + 1] = rd[p] + rcv[p];
+  }
+  const uint64_t n_recv = rd[W];
+  if (n_recv > 0xFFFFFFF0ull) return abort_with(fail(OSE_ERANGE, "more than 2^32-16 records received"));
+  // owner-side columns: trace_id 16, start 8, end 8, route_match 8, svc_match 8, resource 4, res_svc 4,
+  // res_svc_str 4, status 1 per record
+  const uint64_t R = std::max<uint64_t>(n_recv, 1);
+  const size_t o_tid = 0, o_st = align_up(o_tid + 16 * R, 256), o_en = align_up(o_st + 8 * R, 256),
+               o_rm = align_up(o_en + 8 * R, 256), o_sm = align_up(o_rm + 8 * R, 256),
+               o_res = align_up(o_sm + 8 * R, 256), o_sv = align_up(o_res + 4 * R, 256),
+               o_ss = align_up(o_sv + 4 * R, 256), o_stat = align_up(o_ss + 4 * R, 256), o_end = o_stat + R + 256;
+  if ((rc = xs->recv.need(R * kXRecBytes)) || (rc = xs->keep_x.need(R)) || (rc = xs->cols.need(o_end)))
+    return abort_with(rc);
+  // 3. the records (variable sizes per peer)
+  std::vector<uint64_t> s_off(W), s_len(W), r_off(W), r_len(W);
+  for (uint64_t p = 0; p < W; p++) {
+    s_off[p] = sd[p] * kXRecBytes;
+    s_len[p] = sc[p] * kXRecBytes;
+    r_off[p] = rd[p] * kXRecBytes;
+    r_len[p] = rcv[p] * kXRecBytes;
+  }
+  uint8_t* recvb = xs->recv.as<uint8_t>();
+  if ((rc = tx.alltoallv(xs->send.as<uint8_t>(), s_off.data(), s_len.data(), recvb, r_off.data(), r_len.data(), st)))
+    return abort_with(rc);
+  // 4. owner: unpack (source-rank order) + the SAMPLE stage by trace id
+  uint8_t* cb = xs->cols.as<uint8_t>();
+  ose_columns oc{};
+  oc.n_spans = n_recv;
+  oc.n_resources = (uint32_t)n_recv;
+  oc.trace_id = reinterpret_cast<uint64_t*>(cb + o_tid);
+  oc.start_ns = reinterpret_cast<uint64_t*>(cb + o_st);
+  oc.end_ns = reinterpret_cast<uint64_t*>(cb + o_en);
+  oc.route_match = reinterpret_cast<uint64_t*>(cb + o_rm);
+  oc.svc_match = reinterpret_cast<uint64_t*>(cb + o_sm);
+  oc.resource = reinterpret_cast<uint32_t*>(cb + o_res);
+  oc.res_svc = reinterpret_cast<uint32_t*>(cb + o_sv);
+  oc.res_svc_str = reinterpret_cast<uint32_t*>(cb + o_ss);
+  oc.status = cb + o_stat;
+  if (n_recv) {
+    Engine::Timed tm{};
+    e->prof_begin("shard_unpack", st, tm);
+    rc = ose_shard_unpack(recvb, n_recv, kXRecBytes, const_cast<uint64_t*>(oc.trace_id), const_cast<uint64_t*>(oc.start_ns),
+                          const_cast<uint64_t*>(oc.end_ns), const_cast<uint8_t*>(oc.status),
+                          const_cast<uint32_t*>(oc.resource), const_cast<uint32_t*>(oc.res_svc),
+                          const_cast<uint32_t*>(oc.res_svc_str), const_cast<uint64_t*>(oc.route_match),
+                          const_cast<uint64_t*>(oc.svc_match), st);
+    e->prof_end(tm, st);
+    if (rc) return abort_with(rc);
+    ose_outputs ox{};
+    ox.keep = xs->keep_x.as<uint8_t>();
+    ox.device_status = outs->device_status;
+    Engine::Timed to{};
+    e->prof_begin("owner_sample", st, to);
+    rc = run_stages(e, &oc, &ox, OSE_STAGE_SAMPLE, OSE_GROUP_TRACE_ID, rnd, st);
+    e->prof_end(to, st);
+    if (rc) return abort_with(rc);
+  }
+  // 5. decisions back to the sources (reverse split), 6. onto the spans
+  std::vector<uint64_t> kb_off(sd.begin(), sd.end() - 1), kx_off(rd.begin(), rd.end() - 1);
+  if ((rc = tx.alltoallv(xs->keep_x.as<uint8_t>(), kx_off.data(), rcv.data(), xs->keep_back.as<uint8_t>(), kb_off.data(),
+                         sc.data(), st)))
+    return abort_with(rc);
+  rc = ose_shard_scatter_keep(xs->keep_back.as<uint8_t>(), xs->pos.as<uint32_t>(), n, outs->keep, st);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(xs->done, st));
+  xs->done_set = true;
+  if (stats) {   // records sent, records received, spans
+    stats[0] = sd[W];
+    stats[1] = n_recv;
+    stats[2] = n;
+  }
+  return 0;
+}
+}  // namespace
+}  // namespace ose
 
 extern "C" {
 
@@ -272,7 +534,7 @@ int ose_nccl_comm_init(void** comm_out, int n_ranks, const void* id, int rank) {
 }
 
 void ose_nccl_comm_destroy(void* comm) {
-  LastErrorScope keep;
+  LastErrorScope keep("ose_nccl_comm_destroy");
   if (comm && rccl().ok) (void)rccl().comm_destroy(static_cast<ncclComm_t>(comm));
 }
 
@@ -289,109 +551,31 @@ int ose_allreduce_counters(const int64_t* local, int64_t* node, uint64_t n, void
 int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, void* nccl_comm,
                         int rank, int n_ranks, const ose_rand* rnd, void* hip_stream, uint64_t* stats) {
   if (!eng || !cols || !outs || !nccl_comm) return fail(OSE_EINVAL, "NULL argument");
-  if (n_ranks < 1 || n_ranks > 64 || rank < 0 || rank >= n_ranks) return fail(OSE_EINVAL, "rank / n_ranks out of range");
-  if (cols->n_spans && !outs->keep) return fail(OSE_EINVAL, "outs->keep is required");
-  Engine* e = reinterpret_cast<Engine*>(eng);
-  if (!e->has_sampling) return fail(OSE_EINVAL, "the exchange needs odigossampling on the engine");
-  if (int brc = bind_device(e)) return brc;
   const Rccl& r = rccl();
   if (!r.ok) return fail(OSE_ENOTSUP, "RCCL (librccl.so.1) is not available");
-  hipStream_t st = static_cast<hipStream_t>(hip_stream);
-  ncclComm_t comm = static_cast<ncclComm_t>(nccl_comm);
-  XScratch* xs = scratch_of(e);
-  std::lock_guard<std::mutex> g(xs->mu);
-  const uint64_t n = cols->n_spans, W = (uint64_t)n_ranks;
-  int rc;
-  if ((rc = xs->send.need(std::max<uint64_t>(n, 1) * kXRecBytes)) || (rc = xs->pos.need(4 * std::max<uint64_t>(n, 1))) ||
-      (rc = xs->counts.need(16 * W)) || (rc = xs->keep_back.need(std::max<uint64_t>(n, 1))))
-    return rc;
-  if (!xs->host_counts) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&xs->host_counts), 16 * 64, hipHostMallocDefault));
-  uint64_t* scnt_d = xs->counts.as<uint64_t>();
-  uint64_t* rcnt_d = scnt_d + W;
-  // 1. partial records per owner
-  rc = ose_shard_pack(eng, cols, (uint32_t)W, xs->send.p, scnt_d, xs->pos.as<uint32_t>(), st);
-  if (rc) return rc;
-  // 2. record counts, all-to-all (one u64 per peer)
-  NCCL_TRY(r.group_start());
-  for (int p = 0; p < n_ranks; p++) {
-    NCCL_TRY(r.send(scnt_d + p, 1, ncclUint64, p, comm, st));
-    NCCL_TRY(r.recv(rcnt_d + p, 1, ncclUint64, p, comm, st));
-  }
-  NCCL_TRY(r.group_end());
-  HIP_TRY(hipMemcpyAsync(xs->host_counts, scnt_d, 16 * W, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));   // the host needs the split sizes
-  std::vector<uint64_t> sc(xs->host_counts, xs->host_counts + W), rcv(xs->host_counts + W, xs->host_counts + 2 * W);
-  std::vector<uint64_t> sd(W + 1, 0), rd(W + 1, 0);
-  for (uint64_t p = 0; p < W; p++) {
-    sd[p + 1] = sd[p] + sc[p];
-    rd[p + 1] = rd[p] + rcv[p];
-  }
-  const uint64_t n_recv = rd[W];
-  if (n_recv > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "more than 2^32-16 records received");
-  // owner-side columns: trace_id 16, start 8, end 8, route_match 8, svc_match 8, resource 4, res_svc 4,
-  // res_svc_str 4, status 1 per record
-  const uint64_t R = std::max<uint64_t>(n_recv, 1);
-  const size_t o_tid = 0, o_st = align_up(o_tid + 16 * R, 256), o_en = align_up(o_st + 8 * R, 256),
-               o_rm = align_up(o_en + 8 * R, 256), o_sm = align_up(o_rm + 8 * R, 256),
-               o_res = align_up(o_sm + 8 * R, 256), o_sv = align_up(o_res + 4 * R, 256),
-               o_ss = align_up(o_sv + 4 * R, 256), o_stat = align_up(o_ss + 4 * R, 256), o_end = o_stat + R + 256;
-  if ((rc = xs->recv.need(R * kXRecBytes)) || (rc = xs->keep_x.need(R)) || (rc = xs->cols.need(o_end))) return rc;
-  // 3. the records, grouped point-to-point (variable sizes per peer)
-  uint8_t* sendb = xs->send.as<uint8_t>();
-  uint8_t* recvb = xs->recv.as<uint8_t>();
-  NCCL_TRY(r.group_start());
-  for (int p = 0; p < n_ranks; p++) {
-    if (sc[p]) NCCL_TRY(r.send(sendb + sd[p] * kXRecBytes, sc[p] * kXRecBytes, ncclUint8, p, comm, st));
-    if (rcv[p]) NCCL_TRY(r.recv(recvb + rd[p] * kXRecBytes, rcv[p] * kXRecBytes, ncclUint8, p, comm, st));
-  }
-  NCCL_TRY(r.group_end());
-  // 4. owner: unpack (source-rank order) + the SAMPLE stage by trace id
-  uint8_t* cb = xs->cols.as<uint8_t>();
-  ose_columns oc{};
-  oc.n_spans = n_recv;
-  oc.n_resources = (uint32_t)n_recv;
-  oc.trace_id = reinterpret_cast<uint64_t*>(cb + o_tid);
-  oc.start_ns = reinterpret_cast<uint64_t*>(cb + o_st);
-  oc.end_ns = reinterpret_cast<uint64_t*>(cb + o_en);
-  oc.route_match = reinterpret_cast<uint64_t*>(cb + o_rm);
-  oc.svc_match = reinterpret_cast<uint64_t*>(cb + o_sm);
-  oc.resource = reinterpret_cast<uint32_t*>(cb + o_res);
-  oc.res_svc = reinterpret_cast<uint32_t*>(cb + o_sv);
-  oc.res_svc_str = reinterpret_cast<uint32_t*>(cb + o_ss);
-  oc.status = cb + o_stat;
-  if (n_recv) {
-    Engine::Timed tm{};
-    e->prof_begin("shard_unpack", st, tm);
-    rc = ose_shard_unpack(recvb, n_recv, kXRecBytes, const_cast<uint64_t*>(oc.trace_id), const_cast<uint64_t*>(oc.start_ns),
-                          const_cast<uint64_t*>(oc.end_ns), const_cast<uint8_t*>(oc.status),
-                          const_cast<uint32_t*>(oc.resource), const_cast<uint32_t*>(oc.res_svc),
-                          const_cast<uint32_t*>(oc.res_svc_str), const_cast<uint64_t*>(oc.route_match),
-                          const_cast<uint64_t*>(oc.svc_match), st);
-    e->prof_end(tm, st);
-    if (rc) return rc;
-    ose_outputs ox{};
-    ox.keep = xs->keep_x.as<uint8_t>();
-    ox.device_status = outs->device_status;
-    rc = run_stages(e, &oc, &ox, OSE_STAGE_SAMPLE, OSE_GROUP_TRACE_ID, rnd, st);
-    if (rc) return rc;
-  }
-  // 5. decisions back to the sources (reverse split), 6. onto the spans
-  uint8_t* kx = xs->keep_x.as<uint8_t>();
-  uint8_t* kb = xs->keep_back.as<uint8_t>();
-  NCCL_TRY(r.group_start());
-  for (int p = 0; p < n_ranks; p++) {
-    if (rcv[p]) NCCL_TRY(r.send(kx + rd[p], rcv[p], ncclUint8, p, comm, st));
-    if (sc[p]) NCCL_TRY(r.recv(kb + sd[p], sc[p], ncclUint8, p, comm, st));
-  }
-  NCCL_TRY(r.group_end());
-  rc = ose_shard_scatter_keep(kb, xs->pos.as<uint32_t>(), n, outs->keep, hip_stream);
-  if (rc) return rc;
-  if (stats) {   // records sent, records received, spans
-    stats[0] = sd[W];
-    stats[1] = n_recv;
-    stats[2] = n;
-  }
+  RcclTransport tx(static_cast<ncclComm_t>(nccl_comm), n_ranks);
+  return exchange_round(reinterpret_cast<Engine*>(eng), cols, outs, tx, rank, n_ranks, rnd,
+                        static_cast<hipStream_t>(hip_stream), stats);
+}
+
+// ---- test seam: in-process ranks (no RCCL) ---------------------------------------
+int osehost_xgroup_create(int n_ranks, void** out) {
+  if (!out || n_ranks < 1 || n_ranks > 64) return fail(OSE_EINVAL, "n_ranks must be in 1..64");
+  *out = new LocalGroup(n_ranks);
   return 0;
+}
+void osehost_xgroup_destroy(void* grp) {
+  LastErrorScope keep("osehost_xgroup_destroy");
+  delete static_cast<LocalGroup*>(grp);
+}
+int osehost_exchange_sample_local(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, void* grp,
+                                  int rank, const ose_rand* rnd, void* hip_stream, uint64_t* stats) {
+  if (!eng || !cols || !outs || !grp) return fail(OSE_EINVAL, "NULL argument");
+  auto* g = static_cast<LocalGroup*>(grp);
+  if (rank < 0 || rank >= g->n_ranks) return fail(OSE_EINVAL, "rank out of range");
+  LocalTransport tx(g, rank);
+  return exchange_round(reinterpret_cast<Engine*>(eng), cols, outs, tx, rank, g->n_ranks, rnd,
+                        static_cast<hipStream_t>(hip_stream), stats);
 }
 
 }  // extern "C"

@@ -116,6 +116,7 @@ def lib() -> C.CDLL:
         "ose_last_error": (C.c_char_p, []),
         "ose_engine_create": (C.c_int, [C.c_char_p, C.POINTER(_p)]),
         "ose_engine_destroy": (None, [_p]),
+        "ose_dropped_errors": (C.c_uint64, [C.c_char_p, C.c_size_t]),
         "ose_engine_service_id": (C.c_uint32, [_p, C.c_char_p, C.c_size_t]),
         "ose_engine_get_info": (C.c_int, [_p, C.POINTER(EngineInfo)]),
         "ose_set_device": (C.c_int, [C.c_int]),
@@ -168,6 +169,10 @@ def lib() -> C.CDLL:
         "ose_profile_read": (C.c_int, [_p, C.c_char_p, C.c_size_t]),
         # host layer (odigos_amd/csrc/host.cpp)
         "osehost_last_error": (C.c_char_p, []),
+        "osehost_xgroup_create": (C.c_int, [C.c_int, C.POINTER(_p)]),
+        "osehost_xgroup_destroy": (None, [_p]),
+        "osehost_exchange_sample_local": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(Outputs), _p, C.c_int,
+                                                    C.POINTER(Rand), _p, C.POINTER(C.c_uint64)]),
         "osehost_processor_create": (_p, [C.c_char_p, C.c_char_p]),
         "osehost_processor_destroy": (None, [_p]),
         "osehost_processor_set": (None, [_p, C.c_uint64, C.c_uint32]),

@@ -62,12 +62,25 @@ def _no_sticky_hip_error(request):
     if not torch.cuda.is_available():
         yield
         return
+    import ctypes
+    from odigos_amd import native
+    L = native.lib()
+    buf = ctypes.create_string_buffer(512)
     hip = _hip_runtime()
     if hip is not None:
         err = hip.hipGetLastError()
         if err:   # set between tests: a finalizer (ose_*_release / destroy) of an earlier test's objects
             pytest.fail(f"HIP error {hip.hipGetErrorName(err).decode()} ({err}) pending before this test")
+    # errors the release entry points met (recorded, not returned): a finalizer
+    # of an earlier test's objects, or this test's own releases
+    dropped0 = L.ose_dropped_errors(buf, len(buf))
     yield
+    import gc
+    gc.collect()   # run this test's finalizers here, so their errors are charged to it
+    dropped = L.ose_dropped_errors(buf, len(buf))
+    if dropped != dropped0:
+        pytest.fail(f"{dropped - dropped0} HIP error(s) met by release entry points during this test; "
+                    f"last: {buf.value.decode()}")
     if hip is not None:
         err = hip.hipGetLastError()
         if err:

@@ -16,7 +16,11 @@ behaviour, restated here independently of the engine:
   one ptrace.Traces of its pieces in arrival order.
 
 Releases happen at the caller's clock (`release(now)` fires every timer
-with deadline <= now, in arming order).  One deliberate difference from
+with deadline <= now, in arming order).  A trace whose deadline has passed
+takes no more spans even before that call: `consume(td, now)` treats its
+id as unknown (a new trace), as contrib's timer would already have sent it.
+A trace evicted after its deadline but before the release call is dropped
+(the engine applies eviction per add).  One deliberate difference from
 the Go code, which the engine shares: a timer releases the trace instance
 it was armed for, so a trace evicted and created again is not released by
 the old instance's timer.
@@ -66,7 +70,19 @@ class GroupByTraceRef:
         self.timers = []                  # (deadline, instance) in arming order
         self.evicted = 0
 
+    def _expire(self, now: int) -> None:
+        """Timers with deadline <= now have fired: their traces no longer take
+        spans (a later span of the id starts a new trace), though they leave
+        at the next release(now) call."""
+        for d, k in self.timers:
+            if d > now:
+                break
+            t = self.inst.get(k)
+            if t is not None and self.live.get(t["tid"]) == k:
+                del self.live[t["tid"]]
+
     def consume(self, td: dict, now: int) -> None:
+        self._expire(now)
         for tid, piece in split_traces(td):
             tid = _norm(tid)
             if tid in self.live:
@@ -75,7 +91,8 @@ class GroupByTraceRef:
             self.index = (self.index + 1) % self.size
             old = self.ring[self.index]
             if old is not None and old in self.inst:   # evicted: dropped
-                del self.live[self.inst[old]["tid"]]
+                if self.live.get(self.inst[old]["tid"]) == old:
+                    del self.live[self.inst[old]["tid"]]
                 del self.inst[old]
                 self.evicted += 1
             k = self.next
@@ -94,6 +111,7 @@ class GroupByTraceRef:
             t = self.inst.pop(k, None)
             if t is None:
                 continue   # evicted earlier
-            del self.live[t["tid"]]   # its ring slot is free: the next put there evicts nothing
+            if self.live.get(t["tid"]) == k:   # (an expired trace has left `live` already)
+                del self.live[t["tid"]]
             out.append(t["pieces"])
         return out

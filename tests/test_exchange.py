@@ -379,3 +379,99 @@ def test_gpu_exchange_round_world1():
         comm.close()
     finally:
         dist.destroy_process_group()
+
+
+def _local_round(sources, cfg, rounds=1, stream_per_rank=True):
+    """ose_exchange_sample's round (exchange_round) at world len(sources) on
+    ONE GPU: one engine, stream and host thread per rank, the in-process
+    transport (osehost_xgroup_*) moving the bytes with device copies where
+    RCCL would send them over xGMI.  Returns each rank's keep bytes and
+    round stats."""
+    import ctypes as C
+    import threading
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine
+    L = native.lib()
+    W = len(sources)
+    grp = C.c_void_p()
+    native.check(L.osehost_xgroup_create(W, C.byref(grp)))
+    engs = [Engine({"odigossampling": cfg}) for _ in range(W)]
+    dbs = [DeviceBatch(g.cols) for g in sources]
+    streams = [torch.cuda.Stream() if stream_per_rank else torch.cuda.current_stream() for _ in range(W)]
+    stats = [(C.c_uint64 * 3)() for _ in range(W)]
+    errs = [None] * W
+    torch.cuda.synchronize()
+
+    def rank_main(r):
+        try:
+            rnd = native.Rand(SEED, 0.0)
+            for _ in range(rounds):
+                rc = L.osehost_exchange_sample_local(engs[r].h, C.byref(dbs[r].cols), C.byref(dbs[r].outs), grp, r,
+                                                     C.byref(rnd), C.c_void_p(streams[r].cuda_stream), stats[r])
+                if rc:
+                    errs[r] = (rc, native.last_error() if hasattr(native, "last_error") else "")
+                    return
+        except Exception as ex:   # pragma: no cover
+            errs[r] = repr(ex)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    torch.cuda.synchronize()
+    L.osehost_xgroup_destroy(grp)
+    assert all(e is None for e in errs), errs
+    keeps = [db.out_numpy("keep", n=db.cols.n_spans).copy() for db in dbs]
+    for e in engs:
+        e.close()
+    return keeps, [list(s) for s in stats]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n_total", [(2, 600_000), (3, 900_000), (8, 2_400_000)])
+def test_gpu_exchange_round_local_world(world, n_total):
+    # the product round (bucket offsets, the grouped all-to-all of counts and
+    # records, owner unpack + SAMPLE, the reverse split, the scatter) at
+    # world > 1, on split-mode C4 sources whose traces straddle ranks; every
+    # rank's keep equals the oracle on the concatenated global batch
+    from odigos_amd.batch import Generator
+    sources = [Generator("fused", seed=0x0D1600B0 + world, n_spans=n_total, threads=8, rank=r, world=world)
+               for r in range(world)]
+    got, stats = _local_round(sources, CFG, rounds=2)
+    want = _concat_keep_oracle(sources, CFG)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+    sent = sum(s[0] for s in stats)
+    recv = sum(s[1] for s in stats)
+    assert sent == recv and 0 < sent < sum(g.cols.n_spans for g in sources)
+    assert [s[2] for s in stats] == [g.cols.n_spans for g in sources]
+
+
+@pytest.mark.gpu
+def test_gpu_exchange_round_local_zipf_zero_starts():
+    # Zipf trace sizes (long traces straddle every rank), zero starts and
+    # fractional ratios through the same round at world 3, all ranks on one stream
+    from odigos_amd.batch import Generator
+    cfg = _fractional(CFG)
+    sources = [Generator("zipf", seed=0x0D1600B9, n_spans=600_000, rank=r, world=3) for r in range(3)]
+    for k, g in enumerate(sources):
+        st = g.array("start_ns").view(np.uint64)
+        st[np.random.default_rng(40 + k).random(len(st)) < 0.01] = 0
+    got, _ = _local_round(sources, cfg, stream_per_rank=True)
+    want = _concat_keep_oracle(sources, cfg)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.gpu
+def test_gpu_exchange_round_local_empty_rank():
+    # a rank with no spans still takes part in every collective
+    from odigos_amd.batch import Generator
+    sources = [Generator("fused", seed=0x0D1600BA, n_spans=200_000, rank=r, world=2) for r in range(2)]
+    sources.append(Generator("fused", seed=0x0D1600BB, n_spans=0))
+    got, stats = _local_round(sources, CFG)
+    want = _concat_keep_oracle(sources, CFG)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+    assert stats[2][0] == 0 and stats[2][2] == 0

@@ -234,3 +234,95 @@ def test_gpu_eviction_and_capacity():
         shim.add(mk([9], "z"), 15 * S)
     shim.add(mk([9], "z"), 25 * S)
     assert shim.g.stats()["waiting_traces"] == 1
+
+
+def _check_release(shim, ref, now):
+    cols, ntr = shim.g.release(now)
+    want = ref.release(now)
+    assert ntr == len(want)
+    if want:
+        td_w, proc, hb = _expected_columns(want)
+        _compare_release(shim.g.download(cols), cols, hb, shim.names)
+    else:
+        assert cols.n_spans == 0
+    return len(want)
+
+
+def _mk(ks, tag, svc="svc-a"):
+    return host.traces(host.resource_spans(
+        {"service.name": svc}, [host.span(f"{tag}{k}", kind=2, trace_id=_tid(k), attributes={"url.path": f"/u/{k}"})
+                                for k in ks]))
+
+
+@pytest.mark.gpu
+def test_gpu_late_spans_after_deadline_start_new_trace():
+    # spans of an id whose trace is past its wait_duration, added
+    # before any release call, start a new trace; the expired one goes out
+    # at the next release with only its own spans
+    from odigos_amd.batch import Engine
+    eng = Engine(CFG)
+    shim = _Shim(eng, {"wait_duration": "10s"})
+    ref = GroupByTraceRef(10 * S)
+    for now, ks, tag in ((0, [1, 2], "a"), (4 * S, [1], "b"), (11 * S, [1, 2, 3], "c"), (12 * S, [2], "d")):
+        td = _mk(ks, tag)
+        shim.add(td, now)
+        ref.consume(td, now)
+    assert _check_release(shim, ref, 12 * S) == 2          # the first instances of 1 and 2
+    assert shim.g.stats()["waiting_traces"] == 3           # 1, 2, 3 again
+    assert _check_release(shim, ref, 25 * S) == 3
+    assert shim.g.stats()["waiting_traces"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_refused_add_leaves_store_unchanged():
+    # an add whose strings overflow the arena ring is refused
+    # before any trace is numbered or ring slot written, so later adds and
+    # releases see exactly the store before it
+    from odigos_amd.batch import Engine
+    eng = Engine(CFG)
+    shim = _Shim(eng, {"wait_duration": "10s", "num_traces": 8}, span_capacity=4096, arena_capacity=3000)
+    ref = GroupByTraceRef(10 * S, num_traces=8)
+    for now, ks in ((0, [1, 2, 3]), (1 * S, [4, 5, 6, 7])):
+        td = _mk(ks, "p%d-" % now)
+        shim.add(td, now)
+        ref.consume(td, now)
+    before = shim.g.stats()
+    big = host.traces(host.resource_spans({"service.name": "svc-a"}, [
+        host.span("x", kind=2, trace_id=_tid(200 + k), attributes={"url.path": "/" + "q" * 60}) for k in range(60)]))
+    with pytest.raises(native.OseError) as ei:
+        shim.add(big, 2 * S)
+    assert ei.value.code == native.OSE_ERANGE
+    assert shim.g.stats() == before
+    # the ids of the refused batch are unknown; the waiting traces keep their ring slots
+    for now, ks in ((3 * S, [1, 8, 200]), (4 * S, [9, 10, 2])):
+        td = _mk(ks, "q%d-" % now)
+        shim.add(td, now)
+        ref.consume(td, now)
+    assert _check_release(shim, ref, 30 * S) > 0
+    assert shim.g.stats()["evicted"] == ref.evicted
+
+
+@pytest.mark.gpu
+def test_gpu_ids_return_across_many_adds():
+    # the persistent id table: ids come back after their traces were
+    # released (a tombstone reclaimed by its own id), new ids keep arriving
+    # (tombstones accumulate until the table is re-inserted), every release
+    # equal to the restatement
+    from odigos_amd.batch import Engine
+    rng = random.Random(0x6BA)
+    eng = Engine(CFG)
+    shim = _Shim(eng, {"wait_duration": "3s", "num_traces": 300}, span_capacity=1 << 15, arena_capacity=1 << 20)
+    ref = GroupByTraceRef(3 * S, num_traces=300)
+    now = 0
+    total = 0
+    for step in range(90):
+        now += S
+        ks = rng.sample(range(1, 700), 40)
+        td = _mk(ks, "s%d-" % step, svc=rng.choice(["svc-a", "svc-b"]))
+        shim.add(td, now)
+        ref.consume(td, now)
+        if step % 3 == 2:
+            total += _check_release(shim, ref, now)
+    total += _check_release(shim, ref, now + 10 * S)
+    st = shim.g.stats()
+    assert st["released"] == total and st["evicted"] == ref.evicted and st["waiting_traces"] == 0
