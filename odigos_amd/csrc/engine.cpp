@@ -324,9 +324,15 @@ int upload(const std::vector<uint8_t>& host, uint8_t** dev) {
 // Workspace layout for one call (byte offsets), see run_stages.
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st);
+
 // ws_off: the URL scratch starts this many bytes into the workspace (past a
-// SAMPLE stage's scratch whose slow path is still to be queued)
-int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws, size_t ws_off = 0) {
+// SAMPLE stage's scratch whose slow path is still to be queued).  front: only
+// plan, plan_slow and scan are queued, and the arguments of the rest go to
+// *front (run_url_back queues url_copy, fused with odigostrafficmetrics'
+// spans pass when front->fuse_size is set, and url_emit_slow).
+int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws, size_t ws_off = 0,
+            UrlKernelArgs* front = nullptr) {
   if (!e->has_url) return fail(OSE_EINVAL, "odigosurltemplate is not configured on this engine");
   if (!c->url_flags || !c->kind || !c->path || !c->arena || !o->url_out || !o->tmpl || !o->tmpl_arena)
     return fail(OSE_EINVAL, "TEMPLATE stage needs url_flags, kind, path, arena, url_out, tmpl, tmpl_arena");
@@ -390,6 +396,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.used = o->tmpl_arena_used;
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
   a.scr_region = (scr_bytes / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
+  if (front) *front = a;
   if (n == 0) {
     if (o->tmpl_arena_used) HIP_TRY(hipMemsetAsync(o->tmpl_arena_used, 0, 8, st));
     return 0;
@@ -411,6 +418,16 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   launch_url_scan(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
+  if (front) {
+    *front = a;
+    return 0;
+  }
+  return run_url_back(e, a, st);
+}
+
+int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st) {
+  if (a.n_spans == 0) return 0;
+  Engine::Timed tm{};
   e->prof_begin("url_copy_kernel", st, tm);
   launch_url_copy(a, st);
   HIP_TRY(hipGetLastError());
@@ -423,7 +440,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
     uint64_t h[16];
     uint32_t cnt[4];
     HIP_TRY(hipMemcpyAsync(h, a.dbg, sizeof h, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(cnt, base, sizeof cnt, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(cnt, a.scan_counter, sizeof cnt, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const double wp = h[3] ? (double)h[3] : 1.0, we = h[6] ? (double)h[6] : 1.0;
     (void)we;
@@ -431,7 +448,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
             h[1] / wp, h[2] / wp, h[5] / wp);
     fprintf(stderr, "url plan list clocks/wave: enumerate %.0f classify %.0f fold %.0f\n", h[13] / wp, h[14] / wp,
             h[15] / wp);
-    fprintf(stderr, "url groups: %llu, slow (K3s) %u, unplanned (K1b) %u\n", (unsigned long long)((n + 63) / 64),
+    fprintf(stderr, "url groups: %llu, slow (K3s) %u, unplanned (K1b) %u\n", (unsigned long long)((a.n_spans + 63) / 64),
             cnt[1], cnt[3]);
     fprintf(stderr, "url_plan_slow_kernel slowest block clocks: config %llu whole %llu plan_path %llu\n",
             (unsigned long long)h[8], (unsigned long long)h[9], (unsigned long long)h[10]);
@@ -446,13 +463,6 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
     return fail(OSE_EINVAL, "unknown stage bit");
   if ((mask & OSE_STAGE_APPLY_KEEP) && (mask & OSE_STAGE_SAMPLE))
     return fail(OSE_EINVAL, "OSE_STAGE_APPLY_KEEP and OSE_STAGE_SAMPLE exclude each other");
-  Workspace* ws = e->acquire_ws(st);
-  // one reservation for every stage of the call: a stage must not reallocate
-  // scratch an earlier stage of the same call is still using on the stream
-  size_t need = 0;
-  if (mask & OSE_STAGE_TEMPLATE) need = std::max(need, url_workspace_bytes(c->n_spans, c->arena_bytes));
-  if (mask & OSE_STAGE_SAMPLE) need = std::max(need, e->workspace_bytes(c->n_spans, c->arena_bytes));
-  if (mask & OSE_STAGE_SIZE) need = std::max(need, size_scratch_bytes(c->n_scopes, c->n_resources));
   // SAMPLE + TEMPLATE by trace id: the URL stage reads nothing SAMPLE writes,
   // so its launches are queued between SAMPLE's fast path and the rest of
   // SAMPLE, which is queued once the host has read the fast path's dup flag
@@ -464,16 +474,31 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   // trace-id stage keeps host state per call (table generations), so it is
   // refused there; every other stage is captured as plain launches.
   const bool capturing = stream_capturing(st);
-  if (capturing && (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID) {
-    e->return_unused_ws(ws);   // nothing was captured into it
+  if (capturing && (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID)
     return fail(OSE_ENOTSUP, "SAMPLE with OSE_GROUP_TRACE_ID cannot be captured into a hipGraph "
                              "(its trace-id tables advance a host-side generation per call)");
-  }
-  const bool gate_on_host = (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID && c->n_spans > 0 &&
-                            !capturing && !getenv("OSE_NO_DEFER_SLOW");
+  Workspace* ws = e->acquire_ws(st);
+  const uint64_t n = c->n_spans;
+  const bool gate_on_host = (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID && n > 0 && !capturing &&
+                            !getenv("OSE_NO_DEFER_SLOW");
   const bool defer = gate_on_host && (mask & OSE_STAGE_TEMPLATE);
-  const size_t url_off = defer ? (sampling_scratch_bytes(c->n_spans) + 255) / 256 * 256 : 0;
-  if (defer) need = std::max(need, url_off + url_workspace_bytes(c->n_spans, c->arena_bytes));
+  // Workspace layout, one reservation for every stage of the call (a stage
+  // must not reallocate scratch an earlier stage of the same call is still
+  // using on the stream):
+  //   [0, 256)  SAMPLE's words (the OSE_GROUP_BATCH decision SIZE reads);
+  //             its whole scratch while its slow path may still be queued
+  //   url_off   the URL stage's scratch
+  //   size_off  the size stage's sums (after the URL scratch: with TEMPLATE
+  //             its spans pass runs inside url_copy_kernel)
+  size_t need = 0;
+  if (mask & OSE_STAGE_SAMPLE) need = sampling_scratch_bytes(n);
+  const size_t url_off = (mask & OSE_STAGE_SAMPLE) ? align_up(defer ? sampling_scratch_bytes(n) : 256, 256) : 0;
+  size_t size_off = (mask & OSE_STAGE_SAMPLE) ? 256 : 0;
+  if (mask & OSE_STAGE_TEMPLATE) {
+    need = std::max(need, url_off + url_workspace_bytes(n, c->arena_bytes));
+    size_off = align_up(url_off + url_workspace_bytes(n, c->arena_bytes), 256);
+  }
+  if (mask & OSE_STAGE_SIZE) need = std::max(need, size_off + size_scratch_bytes(c->n_scopes, c->n_resources));
   int rc = ws->reserve(need);
   std::function<int()> sample_tail;
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
@@ -482,13 +507,30 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
     rc = sample_tail();
     sample_tail = nullptr;
   }
-  if (!rc && (mask & OSE_STAGE_TEMPLATE)) rc = run_url(e, c, o, st, ws, url_off);
+  UrlKernelArgs ua{};
+  const bool tmpl = !rc && (mask & OSE_STAGE_TEMPLATE);
+  if (tmpl) rc = run_url(e, c, o, st, ws, url_off, &ua);
   if (sample_tail) {
     const int trc = sample_tail();   // always drained: the host event wait must not be skipped
     if (!rc) rc = trc;
   }
-  // odigostrafficmetrics runs last, on what the earlier stages left
-  if (!rc && (mask & OSE_STAGE_SIZE)) rc = run_size(e, c, o, mask, group_mode, rnd, st, ws);
+  // odigostrafficmetrics runs last, on what the earlier stages left (the
+  // decisions are final here: SAMPLE's tail has been queued)
+  SizeKernelArgs sa{};
+  bool size_on = false;
+  if (!rc && (mask & OSE_STAGE_SIZE)) rc = prepare_size(e, c, o, mask, group_mode, rnd, st, ws, size_off, sa, size_on);
+  if (!rc && tmpl) {
+    if (size_on && n > 0 && !getenv("OSE_NO_FUSED_SIZE")) {
+      // the spans pass rides in url_copy_kernel (one walk over the spans)
+      sa.kept_partials = size_partials_of(ws, size_off, c->n_scopes, c->n_resources);
+      sa.n_kept_partials = url_copy_blocks(ua.n_groups);
+      ua.fuse_size = 1;
+      ua.size_partials = const_cast<uint32_t*>(sa.kept_partials);
+      ua.sz = sa;
+    }
+    rc = run_url_back(e, ua, st);
+  }
+  if (!rc && size_on) rc = run_size_tail(e, sa, st);
   e->release_ws(ws, st);
   return rc;
 }

@@ -150,8 +150,14 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
 size_t sampling_scratch_bytes(uint64_t n_spans);
 // the attr_match bits the trace stage reads for this call (attr_host.cpp)
 int resolve_attr_match(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, const uint64_t** out);
+// size stage scratch at workspace byte `off` (size_host.cpp)
 int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
-             const ose_rand* rnd, hipStream_t st, Workspace* ws);
+             const ose_rand* rnd, hipStream_t st, Workspace* ws, size_t off);
+struct SizeKernelArgs;
+int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
+                 const ose_rand* rnd, hipStream_t st, Workspace* ws, size_t off, SizeKernelArgs& a, bool& active);
+uint32_t* size_partials_of(Workspace* ws, size_t off, uint64_t n_scopes, uint64_t n_resources);
+int run_size_tail(Engine* e, const SizeKernelArgs& a, hipStream_t st);
 size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources);
 int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
                const ose_rand* rnd, hipStream_t st);

@@ -20,6 +20,40 @@ namespace ose {
 //                    copied from scratch to their place in the output arena
 //   url_emit_slow_kernel  the groups the plan kernel could not assemble (user
 //                    rules, oversized groups), from the plan arrays
+struct SizeKernelArgs {
+  uint64_t n_spans;
+  uint32_t n_scopes, n_resources, n_attrsets;
+  uint32_t sampled;           // SAMPLE ran in this call: keep decides which spans survive
+  uint32_t templated;         // TEMPLATE ran: url_out / tmpl grow the spans
+  uint32_t remove_empty;      // OSE_GROUP_TRACE_ID sampling: emptied scopes/resources are removed
+  const uint32_t* batch_keep; // OSE_GROUP_BATCH sampling: 0 empties the whole call (null otherwise)
+  const uint32_t* span_size;
+  const uint32_t* name_len;
+  const uint32_t* scope;
+  const uint32_t* scope_size;
+  const uint32_t* scope_resource;
+  const uint32_t* res_size;
+  const uint32_t* res_attrset;
+  const uint8_t* keep;
+  const uint8_t* url_out;
+  const uint8_t* kind;
+  const ose_strref* tmpl;
+  int64_t inverse;
+  uint64_t* scope_body;       // [S] zeroed
+  uint32_t* scope_kept;       // [S] zeroed
+  uint32_t* scope_had;        // [S] zeroed
+  uint64_t* res_body;         // [R] zeroed
+  uint32_t* res_alive;        // [R] zeroed
+  uint32_t* res_had;          // [R] zeroed
+  int64_t* attrset_bytes;     // [n_attrsets] added to
+  int64_t* accepted;          // [1] added to
+  uint64_t* res_bytes;        // [R] or null
+  // the spans pass ran fused in url_copy_kernel: the surviving spans counted
+  // per block there, summed by size_res_kernel (null: size_span_kernel counted)
+  const uint32_t* kept_partials;
+  uint32_t n_kept_partials;
+};
+
 struct UrlKernelArgs {
   uint64_t n_spans;
   uint32_t n_groups;           // ceil(n_spans / kUrlGroup)
@@ -55,7 +89,16 @@ struct UrlKernelArgs {
   uint32_t general;            // user rules or custom ids configured (selects the general kernel instances)
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
   uint64_t* dbg;               // diagnostics only (ablate & 512): per-section clock sums
+  // odigostrafficmetrics' spans pass fused into url_copy_kernel (TEMPLATE and
+  // SIZE in one call): sz as size_span_kernel would get it, sz.tmpl unused
+  // (the plan lengths are the template lengths); the kept count of block b
+  // goes to size_partials[b] (launch_url_copy's grid, <= kUrlCopyMaxBlocks)
+  uint32_t fuse_size;
+  uint32_t* size_partials;
+  SizeKernelArgs sz;
 };
+constexpr uint32_t kUrlCopyMaxBlocks = 65536;
+uint32_t url_copy_blocks(uint32_t n_groups);
 constexpr uint32_t kUrlGroup = 64;       // spans per wave group (url_kernel.hip kWave)
 constexpr uint32_t kUrlScanTile = 1024;  // groups per scan workgroup (url_kernel.hip kScanThreads)
 // workspace bytes the URL stage needs for n spans (engine.cpp run_url layout)
@@ -271,35 +314,6 @@ constexpr uint32_t kBatchKeepWord = 16;   // OSE_GROUP_BATCH decision of the SAM
 // odigostrafficmetrics (size_kernel.hip): three passes, spans -> scopes ->
 // resources, each a wave-segmented reduction (the columns are in pdata
 // order, so scope and resource indices are non-decreasing).
-struct SizeKernelArgs {
-  uint64_t n_spans;
-  uint32_t n_scopes, n_resources, n_attrsets;
-  uint32_t sampled;           // SAMPLE ran in this call: keep decides which spans survive
-  uint32_t templated;         // TEMPLATE ran: url_out / tmpl grow the spans
-  uint32_t remove_empty;      // OSE_GROUP_TRACE_ID sampling: emptied scopes/resources are removed
-  const uint32_t* batch_keep; // OSE_GROUP_BATCH sampling: 0 empties the whole call (null otherwise)
-  const uint32_t* span_size;
-  const uint32_t* name_len;
-  const uint32_t* scope;
-  const uint32_t* scope_size;
-  const uint32_t* scope_resource;
-  const uint32_t* res_size;
-  const uint32_t* res_attrset;
-  const uint8_t* keep;
-  const uint8_t* url_out;
-  const uint8_t* kind;
-  const ose_strref* tmpl;
-  int64_t inverse;
-  uint64_t* scope_body;       // [S] zeroed
-  uint32_t* scope_kept;       // [S] zeroed
-  uint32_t* scope_had;        // [S] zeroed
-  uint64_t* res_body;         // [R] zeroed
-  uint32_t* res_alive;        // [R] zeroed
-  uint32_t* res_had;          // [R] zeroed
-  int64_t* attrset_bytes;     // [n_attrsets] added to
-  int64_t* accepted;          // [1] added to
-  uint64_t* res_bytes;        // [R] or null
-};
 void launch_size_spans(const SizeKernelArgs& a, hipStream_t st);
 void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st);
 void launch_size_resources(const SizeKernelArgs& a, hipStream_t st);

@@ -183,10 +183,13 @@ size_t sampling_scratch_bytes(uint64_t n) {
   return s + 256;
 }
 
+// the workspace of a call running every configured stage (run_stages'
+// layout: SAMPLE's scratch, the URL scratch after it, the size sums after
+// that; scopes and resources bounded by the spans)
 size_t Engine::workspace_bytes(uint64_t n_spans, uint64_t arena_bytes) const {
-  size_t s = has_url ? url_workspace_bytes(n_spans, arena_bytes) : 0;
-  if (has_sampling) s = std::max(s, sampling_scratch_bytes(n_spans));
-  if (has_traffic) s = std::max(s, size_scratch_bytes(n_spans, n_spans));
+  size_t s = has_sampling ? align_up(sampling_scratch_bytes(n_spans), 256) : 0;
+  if (has_url) s = align_up(s + url_workspace_bytes(n_spans, arena_bytes), 256);
+  if (has_traffic) s += size_scratch_bytes(n_spans, n_spans);
   return s;
 }
 

@@ -18,14 +18,20 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 }  // namespace
 
 size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources) {
-  return align_up(256 + 16 * std::max<uint64_t>(n_scopes, 1), 256) + align_up(16 * std::max<uint64_t>(n_resources, 1), 256) + 256;
+  return align_up(256 + 16 * std::max<uint64_t>(n_scopes, 1), 256) + align_up(16 * std::max<uint64_t>(n_resources, 1), 256) +
+         align_up(4ull * kUrlCopyMaxBlocks, 256) + 256;
 }
 
 // dataSizesMetricsProcessor.processTraces (odigostrafficmetrics/
 // processor.go:71-84) after the stages of `mask` that ran before it in this
-// call (gateway order: sampling, then templating, then size).
-int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
-             const ose_rand* rnd, hipStream_t st, Workspace* ws) {
+// call (gateway order: sampling, then templating, then size): validation, the
+// rand gate, the zeroed per-scope / per-resource sums (the workspace from
+// byte `off`; the SAMPLE stage's words at its byte 0 hold the OSE_GROUP_BATCH
+// decision) and the arguments.  *active is false when the gate skips the
+// stage.
+int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
+                 const ose_rand* rnd, hipStream_t st, Workspace* ws, size_t off, SizeKernelArgs& a, bool& active) {
+  active = false;
   if (!e->has_traffic) return fail(OSE_EINVAL, "odigostrafficmetrics is not configured on this engine");
   if (!o->attrset_bytes || !o->accepted_spans) return fail(OSE_EINVAL, "SIZE stage needs attrset_bytes and accepted_spans");
   const uint64_t n = c->n_spans;
@@ -44,13 +50,13 @@ int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mas
   // res_bytes needs no clearing: size_res_kernel writes every entry, zeros
   // when the batch was dropped
   const uint64_t S = c->n_scopes, R = c->n_resources;
-  int rc = ws->reserve(size_scratch_bytes(S, R));
+  int rc = ws->reserve(off + size_scratch_bytes(S, R));
   if (rc) return rc;
-  uint8_t* base = static_cast<uint8_t*>(ws->dev);
+  uint8_t* base = static_cast<uint8_t*>(ws->dev) + off;
   uint8_t* sc = base + 256;
   uint8_t* rs = base + align_up(256 + 16 * std::max<uint64_t>(S, 1), 256);
   HIP_TRY(hipMemsetAsync(sc, 0, (size_t)(rs - sc) + 16 * std::max<uint64_t>(R, 1), st));   // scope and resource sums
-  SizeKernelArgs a{};
+  a = SizeKernelArgs{};
   a.n_spans = n;
   a.n_scopes = (uint32_t)S;
   a.n_resources = (uint32_t)R;
@@ -58,7 +64,8 @@ int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mas
   a.sampled = sampled;
   a.templated = templated;
   a.remove_empty = applied || (sampled && group_mode == OSE_GROUP_TRACE_ID);
-  a.batch_keep = !applied && sampled && group_mode == OSE_GROUP_BATCH ? reinterpret_cast<const uint32_t*>(base) + kBatchKeepWord : nullptr;
+  a.batch_keep = !applied && sampled && group_mode == OSE_GROUP_BATCH
+                     ? reinterpret_cast<const uint32_t*>(ws->dev) + kBatchKeepWord : nullptr;
   a.span_size = c->span_size;
   a.name_len = c->name_len;
   a.scope = c->scope;
@@ -80,11 +87,28 @@ int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mas
   a.attrset_bytes = o->attrset_bytes;
   a.accepted = o->accepted_spans;
   a.res_bytes = o->res_bytes;
+  a.kept_partials = nullptr;   // set by run_stages when url_copy_kernel runs the spans pass (size_partials_of)
+  a.n_kept_partials = 0;
+  active = true;
+  return 0;
+}
+
+uint32_t* size_partials_of(Workspace* ws, size_t off, uint64_t n_scopes, uint64_t n_resources) {
+  uint8_t* base = static_cast<uint8_t*>(ws->dev) + off;
+  uint8_t* rs = base + align_up(256 + 16 * std::max<uint64_t>(n_scopes, 1), 256);
+  return reinterpret_cast<uint32_t*>(rs + align_up(16 * std::max<uint64_t>(n_resources, 1), 256));
+}
+
+// the spans pass (unless url_copy_kernel ran it: a.kept_partials set), then
+// scopes and resources
+int run_size_tail(Engine* e, const SizeKernelArgs& a, hipStream_t st) {
   Engine::Timed tm{};
-  e->prof_begin("size_span_kernel", st, tm);
-  launch_size_spans(a, st);
-  HIP_TRY(hipGetLastError());
-  e->prof_end(tm, st);
+  if (!a.kept_partials) {
+    e->prof_begin("size_span_kernel", st, tm);
+    launch_size_spans(a, st);
+    HIP_TRY(hipGetLastError());
+    e->prof_end(tm, st);
+  }
   e->prof_begin("size_scope_kernel", st, tm);
   launch_size_scopes(a, st);
   HIP_TRY(hipGetLastError());
@@ -94,6 +118,15 @@ int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mas
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
   return 0;
+}
+
+int run_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
+             const ose_rand* rnd, hipStream_t st, Workspace* ws, size_t off) {
+  SizeKernelArgs a;
+  bool active = false;
+  int rc = prepare_size(e, c, o, mask, group_mode, rnd, st, ws, off, a, active);
+  if (rc || !active) return rc;
+  return run_size_tail(e, a, st);
 }
 
 }  // namespace ose

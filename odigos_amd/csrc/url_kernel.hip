@@ -31,6 +31,7 @@
 #include "../../include/odigos_amd.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
+#include "size_device.hpp"
 
 namespace ose {
 namespace {
@@ -1640,21 +1641,47 @@ __device__ __forceinline__ void copy_rest(const CopyJob& j, uint4 v, uint32_t& c
 }
 // One group per iteration at eight waves per SIMD (62 VGPRs): on one box it
 // beat the two-groups-per-iteration form below (83 VGPRs, five waves) by 3-5%
-// on C4 / C5 / C2 (tools/gpu_r2_cp.sh) -- more resident waves hide the two
-// memory round trips per group better than the explicit pairing.
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void url_copy_kernel(UrlKernelArgs a) {
+// on C4 / C5 / C2 (profiles/r2d_url_copy_ab.txt) -- more resident waves hide
+// the two memory round trips per group better than the explicit pairing.
+// kSize: odigostrafficmetrics' spans pass (size_device.hpp) fused in, with
+// the plan lengths as the template lengths: the span columns it reads are
+// loaded with the group's copy columns, so the pass adds no round trip and no
+// second walk over the spans (size_span_kernel is then not launched); the
+// surviving spans are counted per block into size_partials.
+template <bool kSize>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize ? 6 : 8, 8))) void url_copy_kernel(UrlKernelArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t stride = wave_stride();
+  uint32_t kept = 0;
+  const bool sz_on = kSize && !sizedev::size_batch_dropped(a.sz);
   for (uint32_t g = wave_first_group(); g < a.n_groups; g += stride) {
     const CopyCols A = copy_cols(a, g, lane);
+    const uint64_t ia = (uint64_t)g * kWave + lane;
+    sizedev::SpanCols x{};
+    if (kSize && sz_on) x = sizedev::size_span_load(a.sz, ia, false);
     uint32_t unused;
     const uint32_t la = wave_excl_scan(A.len, &unused);
-    const uint64_t ia = (uint64_t)g * kWave + lane;
     const CopyJob ja = copy_job(a, A);
     const uint4 va = copy_load(ja, 0);
     if (ia < a.n_spans) a.tmpl[ia] = ose_strref{(uint32_t)(A.base + la), A.len};
+    if (kSize && sz_on) {
+      x.tl = A.len;
+      kept += sizedev::size_span_finish(a.sz, x);
+    }
     uint32_t carry = 0;
     if (ja.on) copy_rest(ja, va, carry);
+  }
+  if (kSize) {
+    __shared__ uint32_t wk[kWaves];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o, kWave);
+    if (lane == 0) wk[threadIdx.x >> 6] = kept;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < kWaves; w++) t += wk[w];
+      a.size_partials[blockIdx.x] = t;
+    }
   }
 }
 // Two groups per iteration (g and g + stride): their columns are loaded
@@ -1902,24 +1929,30 @@ void launch_url_plan(const UrlKernelArgs& a, hipStream_t st) {
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(url_scan_kernel, dim3(a.n_scan_tiles), dim3(kScanThreads), 0, st, a);
 }
-void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
-  // far more workgroups than fit at once (C4 sweep, tools/gpu_r2_knob.sh:
+uint32_t url_copy_blocks(uint32_t n_groups) {
+  // far more workgroups than fit at once (C4 sweep, profiles/r2d_url_copy_grid_sweep.txt:
   // resident grid 1.01 ms, 16384 blocks 0.93, 65536 0.92): a wave's two
   // groups are two memory round trips, and the waves waiting on them are what
   // keeps HBM busy
   static const uint32_t cap = [] {
     const char* g = getenv("OSE_COPY_GRID");   // tuning
-    return g ? std::max<uint32_t>(1, (uint32_t)strtoul(g, nullptr, 0)) : 65536u;
+    return g ? std::min<uint32_t>(kUrlCopyMaxBlocks, std::max<uint32_t>(1, (uint32_t)strtoul(g, nullptr, 0)))
+             : kUrlCopyMaxBlocks;
   }();
+  return std::max<uint32_t>(1, std::min<uint32_t>(cap, (n_groups + 2 * kWaves - 1) / (2 * kWaves)));
+}
+void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
   static const bool pair = [] {
     const char* p = getenv("OSE_COPY_PAIR");   // A/B: the two-groups-per-iteration kernel
     return p && strtoul(p, nullptr, 0) != 0;
   }();
-  const uint32_t blocks = std::min<uint32_t>(cap, (a.n_groups + 2 * kWaves - 1) / (2 * kWaves));
-  if (pair)
+  const uint32_t blocks = url_copy_blocks(a.n_groups);
+  if (a.fuse_size)
+    hipLaunchKernelGGL(url_copy_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, a);
+  else if (pair)
     hipLaunchKernelGGL(url_copy_pair_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
   else
-    hipLaunchKernelGGL(url_copy_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(url_copy_kernel<false>, dim3(blocks), dim3(kThreads), 0, st, a);
 }
 void launch_url_plan_slow(const UrlKernelArgs& a, hipStream_t st) {
   // the list length is on the device: a workgroup per group up to the resident
