@@ -1,5 +1,6 @@
 // regex_dfa.cpp — Go RE2-syntax regexp -> DFA (see regex_dfa.hpp).
 #include "regex_dfa.hpp"
+#include "unicode_tables.hpp"
 
 #include <algorithm>
 #include <map>
@@ -60,21 +61,95 @@ Ranges negate(Ranges r) {
   if (next <= kRuneMax) o.push_back({next, kRuneMax});
   return o;
 }
-// unicode.SimpleFold restricted to ASCII-letter orbits: {k,K,U+212A}, {s,S,U+017F}
+// unicode.SimpleFold closure (regexp/syntax appendFoldedRange): every rune
+// of r brings its whole simple case-folding orbit (unicode_tables.hpp).
 void fold(Ranges& r) {
-  Ranges add;
-  for (auto& x : r) {
-    for (uint32_t c = x.first; c <= x.second && c < 0x80; c++) {
-      if (c >= 'a' && c <= 'z') add.push_back({c - 32, c - 32});
-      if (c >= 'A' && c <= 'Z') add.push_back({c + 32, c + 32});
-      if (c == 'k' || c == 'K') add.push_back({0x212A, 0x212A});
-      if (c == 's' || c == 'S') add.push_back({0x17F, 0x17F});
-    }
-    if (x.first <= 0x212A && 0x212A <= x.second) { add.push_back({'k', 'k'}); add.push_back({'K', 'K'}); }
-    if (x.first <= 0x17F && 0x17F <= x.second) { add.push_back({'s', 's'}); add.push_back({'S', 'S'}); }
-  }
-  r.insert(r.end(), add.begin(), add.end());
   normalize(r);
+  // each pass adds the next rune of every member's orbit; orbits are short
+  // cycles, so a few passes close the set
+  for (int pass = 0; pass < 8; pass++) {
+    Ranges add;
+    for (uint32_t k = 0; k < kFoldOrbitN; k++) {
+      const uint32_t c = kFoldOrbit[2 * k], nx = kFoldOrbit[2 * k + 1];
+      auto in = [&](uint32_t x) {
+        auto it = std::upper_bound(r.begin(), r.end(), std::make_pair(x, kRuneMax + 1));
+        return it != r.begin() && std::prev(it)->second >= x;
+      };
+      if (in(c) && !in(nx)) add.push_back({nx, nx});
+    }
+    if (add.empty()) break;
+    r.insert(r.end(), add.begin(), add.end());
+    normalize(r);
+  }
+}
+
+Ranges table_ranges(const UniTable& t) {
+  Ranges r;
+  for (uint32_t k = 0; k < t.n; k++) r.push_back({t.ranges[2 * k], t.ranges[2 * k + 1]});
+  return r;
+}
+// TR18 loose matching (Go 1.25 regexp/syntax): case-insensitive, spaces,
+// underscores and hyphens ignored
+std::string loose(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == ' ' || c == '_' || c == '-') continue;
+    o += (char)((c >= 'A' && c <= 'Z') ? c + 32 : c);
+  }
+  return o;
+}
+// the table of a \p{name} (Go 1.25 unicodeTable): Any, ASCII, Assigned,
+// general categories (one and two letters, LC, Cn) and their long aliases,
+// scripts.  false: no such class.
+bool unicode_class(const std::string& name, Ranges& out) {
+  static const std::pair<const char*, const char*> kAliases[] = {
+      {"casedletter", "LC"}, {"closepunctuation", "Pe"}, {"combiningmark", "M"}, {"connectorpunctuation", "Pc"},
+      {"control", "Cc"}, {"currencysymbol", "Sc"}, {"dashpunctuation", "Pd"}, {"decimalnumber", "Nd"},
+      {"enclosingmark", "Me"}, {"finalpunctuation", "Pf"}, {"format", "Cf"}, {"initialpunctuation", "Pi"},
+      {"letter", "L"}, {"letternumber", "Nl"}, {"lineseparator", "Zl"}, {"lowercaseletter", "Ll"}, {"mark", "M"},
+      {"mathsymbol", "Sm"}, {"modifierletter", "Lm"}, {"modifiersymbol", "Sk"}, {"nonspacingmark", "Mn"},
+      {"number", "N"}, {"openpunctuation", "Ps"}, {"other", "C"}, {"otherletter", "Lo"}, {"othernumber", "No"},
+      {"otherpunctuation", "Po"}, {"othersymbol", "So"}, {"paragraphseparator", "Zp"}, {"privateuse", "Co"},
+      {"punctuation", "P"}, {"separator", "Z"}, {"spaceseparator", "Zs"}, {"spacingmark", "Mc"}, {"surrogate", "Cs"},
+      {"symbol", "S"}, {"titlecaseletter", "Lt"}, {"unassigned", "Cn"}, {"uppercaseletter", "Lu"}, {"cntrl", "Cc"},
+      {"digit", "Nd"}, {"punct", "P"}};
+  std::string key = loose(name);
+  for (auto& a : kAliases)
+    if (key == a.first) key = loose(a.second);
+  out.clear();
+  if (key == "any") { out = {{0, kRuneMax}}; return true; }
+  if (key == "ascii") { out = {{0, 0x7F}}; return true; }
+  auto all_assigned = [&]() {
+    Ranges r;
+    for (uint32_t k = 0; k < kUniCategoriesN; k++) {
+      Ranges t = table_ranges(kUniCategories[k]);
+      r.insert(r.end(), t.begin(), t.end());
+    }
+    normalize(r);
+    return r;
+  };
+  if (key == "assigned") { out = all_assigned(); return true; }
+  if (key == "cn") { out = negate(all_assigned()); return true; }
+  if (key == "lc") key = "lu|ll|lt";
+  bool any = false;
+  for (uint32_t k = 0; k < kUniCategoriesN; k++) {
+    const std::string cat = loose(kUniCategories[k].name);
+    // one letter: the group (Go's unicode.C is Cc|Cf|Co|Cs: the tables have no Cn)
+    const bool hit = cat == key || (key.size() == 1 && cat[0] == key[0]) ||
+                     (key == "lu|ll|lt" && (cat == "lu" || cat == "ll" || cat == "lt"));
+    if (!hit) continue;
+    Ranges t = table_ranges(kUniCategories[k]);
+    out.insert(out.end(), t.begin(), t.end());
+    any = true;
+  }
+  if (any) { normalize(out); return true; }
+  for (uint32_t k = 0; k < kUniScriptsN; k++)
+    if (loose(kUniScripts[k].name) == key) {
+      out = table_ranges(kUniScripts[k]);
+      normalize(out);
+      return true;
+    }
+  return false;
 }
 
 enum EmptyOp : uint8_t { kBOL = 1, kEOL = 2, kBOT = 4, kEOT = 8, kWB = 16, kNWB = 32 };
@@ -107,6 +182,7 @@ class Parser {
   size_t i_ = 0;
   bool fi_ = false, fm_ = false, fs_ = false;
   int depth_ = 0;
+  Ranges uclass_;   // the set of the last \p / \P escape
 
   [[noreturn]] void syntax(const std::string& m) { throw ParseError{RegexStatus::Syntax, m}; }
   [[noreturn]] void unsupported(const std::string& m) { throw ParseError{RegexStatus::Unsupported, m}; }
@@ -132,30 +208,11 @@ class Parser {
     if (neg) t = negate(t);
     r.insert(r.end(), t.begin(), t.end());
   }
-  // Folding is only implemented for ASCII orbits ({k,K,U+212A}, {s,S,U+017F},
-  // letter pairs).  A set whose non-ASCII part is empty, only U+017F/U+212A,
-  // or everything but those two is closed under every other orbit.
-  static bool fold_safe(Ranges r) {
-    normalize(r);
-    Ranges na;
-    for (auto& x : r) if (x.second >= 0x80) na.push_back({std::max<uint32_t>(x.first, 0x80), x.second});
-    if (na.empty()) return true;
-    auto specials_only = [](const Ranges& s) {
-      for (auto& x : s) if (x.first != x.second || (x.first != 0x17F && x.first != 0x212A)) return false;
-      return true;
-    };
-    if (specials_only(na)) return true;
-    Ranges comp;
-    uint32_t next = 0x80;
-    for (auto& x : na) { if (x.first > next) comp.push_back({next, x.first - 1}); next = x.second + 1; }
-    if (next <= kRuneMax) comp.push_back({next, kRuneMax});
-    return specials_only(comp);
-  }
   static bool alnum(uint32_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
   static bool hexd(char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
   static uint32_t hexv(char c) { return c <= '9' ? c - '0' : ((c | 0x20) - 'a' + 10); }
 
-  // escape after '\'; kind: 0 rune, 1 perl class (perl,neg), 2 empty op
+  // escape after '\'; kind: 0 rune, 1 perl class (perl,neg), 2 empty op, 3 unicode class (uclass_)
   int escape(uint32_t& r, char& pk, bool& pneg, uint8_t& op, bool in_class) {
     if (eof()) syntax("trailing backslash at end of expression");
     int w;
@@ -175,8 +232,31 @@ class Parser {
       case 'B': if (!in_class) { op = kNWB; return 2; } break;
       case 'A': if (!in_class) { op = kBOT; return 2; } break;
       case 'z': if (!in_class) { op = kEOT; return 2; } break;
-      case 'p': case 'P': unsupported("unsupported: Unicode class \\p");
-      case 'Q': unsupported("unsupported: \\Q...\\E");
+      case 'p': case 'P': {   // regexp/syntax parseUnicodeClass
+        bool neg = c == 'P';
+        std::string name;
+        if (eof()) syntax("invalid character class range");
+        if (s_[i_] == '{') {
+          const size_t e = s_.find('}', i_);
+          if (e == std::string::npos) syntax("invalid character class range");
+          name = s_.substr(i_ + 1, e - i_ - 1);
+          i_ = e + 1;
+        } else {
+          int w2;
+          (void)rune(w2);
+          name = s_.substr(i_, (size_t)w2);
+          i_ += w2;
+        }
+        if (!name.empty() && name[0] == '^') {   // \p{^Greek} == \P{Greek}
+          neg = !neg;
+          name = name.substr(1);
+        }
+        Ranges t;
+        if (!unicode_class(name, t)) syntax("invalid character class range");
+        if (fi_) fold(t);   // folded, then negated (parseUnicodeClass)
+        uclass_ = neg ? negate(t) : t;
+        return 3;
+      }
       case '1': case '2': case '3': case '4': case '5': case '6': case '7':
         if (eof() || s_[i_] < '0' || s_[i_] > '7') break;
         [[fallthrough]];
@@ -255,6 +335,7 @@ class Parser {
         i_++;
         int k = escape(lo, pk, pn, op, true);
         if (k == 1) { perl(r, pk, pn); continue; }
+        if (k == 3) { r.insert(r.end(), uclass_.begin(), uclass_.end()); continue; }
       } else {
         int w;
         lo = rune(w);
@@ -276,7 +357,6 @@ class Parser {
       }
       r.push_back({lo, hi});
     }
-    if (fi_ && !fold_safe(r)) unsupported("unsupported: (?i) with non-ASCII class members");
     return chars(std::move(r), neg);
   }
 
@@ -391,6 +471,21 @@ class Parser {
         continue;
       }
       uint32_t r;
+      if (c == '\\' && i_ + 1 < s_.size() && s_[i_ + 1] == 'Q') {
+        // \Q...\E: every rune up to \E (or the end) is a literal
+        i_ += 2;
+        const size_t e = s_.find("\\E", i_);
+        const size_t stop = e == std::string::npos ? s_.size() : e;
+        while (i_ < stop) {
+          int w;
+          const uint32_t lit = rune(w);
+          i_ += w;
+          cat->sub.push_back(chars(Ranges{{lit, lit}}, false));
+        }
+        if (e != std::string::npos) i_ = e + 2;
+        last_rep = false;
+        continue;
+      }
       if (c == '\\') {
         i_++;
         char pk = 0;
@@ -398,6 +493,13 @@ class Parser {
         uint8_t op = 0;
         int k = escape(r, pk, pn, op, false);
         if (k == 1) { Ranges t; perl(t, pk, pn); cat->sub.push_back(chars(t, false)); continue; }
+        if (k == 3) {
+          auto n = std::make_unique<Node>();
+          n->kind = Node::Chars;
+          n->chars = uclass_;
+          cat->sub.push_back(std::move(n));
+          continue;
+        }
         if (k == 2) {
           auto n = std::make_unique<Node>();
           n->kind = Node::Assert;
@@ -410,7 +512,6 @@ class Parser {
         r = rune(w);
         i_ += w;
       }
-      if (fi_ && r >= 0x80) unsupported("unsupported: (?i) with non-ASCII literal");
       cat->sub.push_back(chars(Ranges{{r, r}}, false));
     }
     return cat;

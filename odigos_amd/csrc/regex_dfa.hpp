@@ -11,8 +11,11 @@
 // multi-line variants) resolved from a per-state "previous rune type" and the
 // class of the next rune, exactly as regexp.EmptyOpContext does.  Invalid
 // UTF-8 bytes are runes U+FFFD of width 1 (unicode/utf8.DecodeRune).
-// Unsupported (rejected, never approximated): \p{..}, \Q..\E, (?i) with
-// non-ASCII letters, DFAs above kMaxStates.
+// \p{..} / \P{..} (Go 1.25 names: categories, aliases, scripts, Any, ASCII,
+// Assigned, Cn, LC; loose matching), \Q..\E and (?i) simple case folding of
+// any rune use unicode_tables.cpp (generated; Unicode 13.0.0 data, the
+// reference's Go 1.25 has 15.0.0: later code points are parity unpinned).
+// Unsupported (rejected, never approximated): DFAs above kMaxStates.
 #pragma once
 #include <cstdint>
 #include <string>

@@ -23,6 +23,15 @@ extern "C" {
 
 /* ---- regexp (Go RE2 syntax subset, backtracking; oracle-private) ----- */
 typedef struct orc_re orc_re;
+/* Unicode data for \p{..} and (?i) (unicode_data.c, generated): inclusive
+ * {lo, hi} pairs; orc_fold_next: {rune, next rune of its simple-folding orbit} */
+typedef struct { const char* name; const int* r; int n; } orc_utab;
+extern const orc_utab orc_ucats[];
+extern const int orc_ucats_n;
+extern const orc_utab orc_uscripts[];
+extern const int orc_uscripts_n;
+extern const int orc_fold_next[];
+extern const int orc_fold_n;
 /* returns NULL and fills err on a syntax error the Go parser would reject */
 orc_re* orc_re_compile(const char* pattern, char* err, size_t errcap);
 /* regexp.MatchString semantics: unanchored search over the UTF-8 string */

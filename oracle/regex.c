@@ -13,8 +13,10 @@
  * Algorithm (deliberately different from the product's DFA compiler):
  * parse -> instruction program -> backtracking with a visited bitmap
  * (RE2 "BitState"), tried from every rune boundary.
- * Unsupported (rejected at compile, never guessed): \p{..} Unicode classes,
- * \Q..\E, (?i) together with non-ASCII letters in the pattern.
+ * \p{..} / \P{..} (Go 1.25 names, loose matching) and (?i) on any rune
+ * use the oracle's own generated Unicode data (unicode_data.c: Unicode
+ * 13.0.0 categories; Go 1.25 uses 15.0.0, so later code points are parity
+ * unpinned); \Q..\E quotes literals.
  */
 #include "oracle.h"
 #include <stdlib.h>
@@ -148,22 +150,21 @@ static void cls_negate(rclass* c) {
   if (next <= RUNE_MAX) cls_add(&o, next, RUNE_MAX);
   free(c->r); *c = o;
 }
-/* unicode.SimpleFold orbits restricted to ASCII letters (+ the two non-ASCII
- * members of ASCII orbits: U+212A KELVIN SIGN ~ k, U+017F LONG S ~ s). */
+static int cls_has(const rclass* c, int r);
+static int peek_rune(parser* ps, int* w);
+/* unicode.SimpleFold closure: every member brings its whole orbit
+ * (orc_fold_next lists each orbit as a cycle; repeated passes close it). */
 static void cls_fold(rclass* c) {
-  int n0 = c->n;
-  for (int i = 0; i < n0; i++) {
-    int lo = c->r[i].lo, hi = c->r[i].hi;
-    for (int r = lo; r <= hi && r < 0x80; r++) {
-      if (r >= 'a' && r <= 'z') cls_add(c, r - 32, r - 32);
-      if (r >= 'A' && r <= 'Z') cls_add(c, r + 32, r + 32);
-      if (r == 'k' || r == 'K') cls_add(c, 0x212A, 0x212A);
-      if (r == 's' || r == 'S') cls_add(c, 0x17F, 0x17F);
-    }
-    if (lo <= 0x212A && 0x212A <= hi) { cls_add(c, 'k', 'k'); cls_add(c, 'K', 'K'); }
-    if (lo <= 0x17F && 0x17F <= hi) { cls_add(c, 's', 's'); cls_add(c, 'S', 'S'); }
-  }
   cls_norm(c);
+  for (int pass = 0; pass < 8; pass++) {
+    int added = 0;
+    for (int k = 0; k < orc_fold_n; k++) {
+      int r = orc_fold_next[2 * k], nx = orc_fold_next[2 * k + 1];
+      if (cls_has(c, r) && !cls_has(c, nx)) { cls_add(c, nx, nx); added = 1; }
+    }
+    if (!added) break;
+    cls_norm(c);
+  }
 }
 static int cls_has(const rclass* c, int r) {
   int lo = 0, hi = c->n - 1;
@@ -190,6 +191,88 @@ static void add_perl_neg(rclass* c, char k, int fold) {
   cls_negate(&t);
   for (int i = 0; i < t.n; i++) cls_add(c, t.r[i].lo, t.r[i].hi);
   free(t.r);
+}
+
+/* Go 1.25 regexp/syntax unicodeTable: names compared loosely (case, ' ',
+ * '_' and '-' ignored); Any, ASCII, Assigned, Cn, LC, one-letter groups,
+ * two-letter categories with their long aliases, scripts. */
+static void loose_name(const char* s, size_t n, char* out, size_t cap) {
+  size_t k = 0;
+  for (size_t i = 0; i < n && k + 1 < cap; i++) {
+    char c = s[i];
+    if (c == ' ' || c == '_' || c == '-') continue;
+    out[k++] = (c >= 'A' && c <= 'Z') ? (char)(c + 32) : c;
+  }
+  out[k] = 0;
+}
+static void add_tab(rclass* t, const orc_utab* u) {
+  for (int i = 0; i < u->n; i++) cls_add(t, u->r[2 * i], u->r[2 * i + 1]);
+}
+static int unicode_named(rclass* t, const char* name, size_t len) {
+  static const char* const alias[][2] = {
+    {"letter", "l"}, {"casedletter", "lc"}, {"uppercaseletter", "lu"}, {"lowercaseletter", "ll"},
+    {"titlecaseletter", "lt"}, {"modifierletter", "lm"}, {"otherletter", "lo"}, {"mark", "m"},
+    {"combiningmark", "m"}, {"nonspacingmark", "mn"}, {"spacingmark", "mc"}, {"enclosingmark", "me"},
+    {"number", "n"}, {"decimalnumber", "nd"}, {"digit", "nd"}, {"letternumber", "nl"}, {"othernumber", "no"},
+    {"punctuation", "p"}, {"punct", "p"}, {"connectorpunctuation", "pc"}, {"dashpunctuation", "pd"},
+    {"openpunctuation", "ps"}, {"closepunctuation", "pe"}, {"initialpunctuation", "pi"},
+    {"finalpunctuation", "pf"}, {"otherpunctuation", "po"}, {"symbol", "s"}, {"mathsymbol", "sm"},
+    {"currencysymbol", "sc"}, {"modifiersymbol", "sk"}, {"othersymbol", "so"}, {"separator", "z"},
+    {"spaceseparator", "zs"}, {"lineseparator", "zl"}, {"paragraphseparator", "zp"}, {"other", "c"},
+    {"control", "cc"}, {"cntrl", "cc"}, {"format", "cf"}, {"surrogate", "cs"}, {"privateuse", "co"},
+    {"unassigned", "cn"}};
+  char key[64], nm[64];
+  loose_name(name, len, key, sizeof key);
+  for (size_t i = 0; i < sizeof alias / sizeof alias[0]; i++)
+    if (strcmp(key, alias[i][0]) == 0) { snprintf(key, sizeof key, "%s", alias[i][1]); break; }
+  if (strcmp(key, "any") == 0) { cls_add(t, 0, RUNE_MAX); return 1; }
+  if (strcmp(key, "ascii") == 0) { cls_add(t, 0, 0x7F); return 1; }
+  if (strcmp(key, "assigned") == 0 || strcmp(key, "cn") == 0) {
+    rclass a = {0, 0, 0};
+    for (int i = 0; i < orc_ucats_n; i++) add_tab(&a, &orc_ucats[i]);
+    if (key[0] == 'c') cls_negate(&a);
+    for (int i = 0; i < a.n; i++) cls_add(t, a.r[i].lo, a.r[i].hi);
+    free(a.r);
+    return 1;
+  }
+  int hit = 0;
+  for (int i = 0; i < orc_ucats_n; i++) {
+    loose_name(orc_ucats[i].name, strlen(orc_ucats[i].name), nm, sizeof nm);
+    int in = strcmp(nm, key) == 0 || (key[0] && !key[1] && nm[0] == key[0]) ||
+             (strcmp(key, "lc") == 0 && (!strcmp(nm, "lu") || !strcmp(nm, "ll") || !strcmp(nm, "lt")));
+    if (in) { add_tab(t, &orc_ucats[i]); hit = 1; }
+  }
+  if (hit) return 1;
+  for (int i = 0; i < orc_uscripts_n; i++) {
+    loose_name(orc_uscripts[i].name, strlen(orc_uscripts[i].name), nm, sizeof nm);
+    if (strcmp(nm, key) == 0) { add_tab(t, &orc_uscripts[i]); return 1; }
+  }
+  return 0;
+}
+/* \p / \P after the letter: the (folded under (?i), then signed) set into
+ * out; -1 on a bad name (regexp/syntax parseUnicodeClass) */
+static int parse_uclass(parser* ps, int upper, rclass* out) {
+  int neg = upper;
+  const char* nm; size_t len;
+  if (ps->p >= ps->end) { set_err(ps, "invalid character class range"); return -1; }
+  if (*ps->p == '{') {
+    const char* e = memchr(ps->p, '}', (size_t)(ps->end - ps->p));
+    if (!e) { set_err(ps, "invalid character class range"); return -1; }
+    nm = ps->p + 1; len = (size_t)(e - nm);
+    ps->p = e + 1;
+  } else {
+    int w; peek_rune(ps, &w);
+    nm = ps->p; len = (size_t)w;
+    ps->p += w;
+  }
+  if (len && nm[0] == '^') { neg = !neg; nm++; len--; }
+  rclass t = {0, 0, 0};
+  if (!unicode_named(&t, nm, len)) { free(t.r); set_err(ps, "invalid character class range"); return -1; }
+  cls_norm(&t);
+  if (ps->flag_i) cls_fold(&t);
+  if (neg) cls_negate(&t);
+  *out = t;
+  return 0;
 }
 
 static int posix_class(rclass* c, const char* name, size_t len, int neg) {
@@ -241,7 +324,8 @@ static int parse_escape(parser* ps, char* perl, int* neg, int* op, int in_class)
     case 'B': if (in_class) break; *op = E_NWB; return -3;
     case 'A': if (in_class) break; *op = E_BOT; return -3;
     case 'z': if (in_class) break; *op = E_EOT; return -3;
-    case 'p': case 'P': case 'Q': case 'C': ps->unsupported = 1; set_err(ps, "unsupported escape"); return -1;
+    case 'p': case 'P': return c == 'P' ? -5 : -4;   /* unicode class: the caller parses the name */
+    case 'C': ps->unsupported = 1; set_err(ps, "unsupported escape"); return -1;
     case '1': case '2': case '3': case '4': case '5': case '6': case '7':
       if (ps->p >= ps->end || *ps->p < '0' || *ps->p > '7') break;
       /* fallthrough */
@@ -314,6 +398,13 @@ static node* parse_class(parser* ps) {  /* after '[' */
       char perl = 0; int neg = 0, op = 0;
       lo = parse_escape(ps, &perl, &neg, &op, 1);
       if (lo == -2) { if (neg) add_perl_neg(&t, perl, ps->flag_i); else add_perl(&t, perl); continue; }
+      if (lo == -4 || lo == -5) {
+        rclass u;
+        if (parse_uclass(ps, lo == -5, &u) < 0) { free(t.r); return NULL; }
+        for (int i = 0; i < u.n; i++) cls_add(&t, u.r[i].lo, u.r[i].hi);
+        free(u.r);
+        continue;
+      }
       if (lo < 0) { free(t.r); return NULL; }
     } else {
       int w; lo = peek_rune(ps, &w); ps->p += w;
@@ -450,11 +541,30 @@ static node* parse_concat(parser* ps) {
     if (c == '.') { ps->p++; addkid(cat, mk(ps->flag_s ? N_ANY : N_ANYNL)); continue; }
     if (c == '^') { ps->p++; node* n = mk(N_ASSERT); n->assert_op = ps->flag_m ? E_BOL : E_BOT; addkid(cat, n); continue; }
     if (c == '$') { ps->p++; node* n = mk(N_ASSERT); n->assert_op = ps->flag_m ? E_EOL : E_EOT; addkid(cat, n); continue; }
+    if (c == '\\' && ps->p + 1 < ps->end && ps->p[1] == 'Q') {   /* \Q...\E: literals up to \E or the end */
+      ps->p += 2;
+      const char* e = ps->p;
+      while (e + 1 < ps->end && !(e[0] == '\\' && e[1] == 'E')) e++;
+      if (!(e + 1 < ps->end)) e = ps->end;
+      while (ps->p < e) { int w; int r = peek_rune(ps, &w); ps->p += w; addkid(cat, lit_node(ps, r)); }
+      if (e < ps->end) ps->p = e + 2;
+      continue;
+    }
     if (c == '\\') {
       ps->p++;
       char perl = 0; int neg = 0, op = 0;
       int r = parse_escape(ps, &perl, &neg, &op, 0);
       if (r == -1) { free_node(cat); return NULL; }
+      if (r == -4 || r == -5) {
+        rclass u;
+        if (parse_uclass(ps, r == -5, &u) < 0) { free_node(cat); return NULL; }
+        int ci = new_class(ps->re);
+        ps->re->cls[ci] = u;
+        node* n = mk(N_CLASS);
+        n->cls = ci;
+        addkid(cat, n);
+        continue;
+      }
       if (r == -2) {
         rclass t = {0, 0, 0};
         add_perl(&t, perl);
@@ -462,13 +572,11 @@ static node* parse_concat(parser* ps) {
         continue;
       }
       if (r == -3) { node* n = mk(N_ASSERT); n->assert_op = op; addkid(cat, n); continue; }
-      if (ps->flag_i && r >= 0x80) { ps->unsupported = 1; set_err(ps, "unsupported: (?i) with non-ASCII literal"); free_node(cat); return NULL; }
       addkid(cat, lit_node(ps, r));
       continue;
     }
     {
       int w; int r = peek_rune(ps, &w); ps->p += w;
-      if (ps->flag_i && r >= 0x80) { ps->unsupported = 1; set_err(ps, "unsupported: (?i) with non-ASCII literal"); free_node(cat); return NULL; }
       addkid(cat, lit_node(ps, r));
     }
   }

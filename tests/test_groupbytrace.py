@@ -250,7 +250,8 @@ def _check_release(shim, ref, now):
 
 def _mk(ks, tag, svc="svc-a"):
     return host.traces(host.resource_spans(
-        {"service.name": svc}, [host.span(f"{tag}{k}", kind=2, trace_id=_tid(k), attributes={"url.path": f"/u/{k}"})
+        {"service.name": svc}, [host.span(f"{tag}{k}", kind=2, trace_id=_tid(k),
+                                          attributes={"http.request.method": "GET", "url.path": f"/u/{k}"})
                                 for k in ks]))
 
 
@@ -288,7 +289,8 @@ def test_gpu_refused_add_leaves_store_unchanged():
         ref.consume(td, now)
     before = shim.g.stats()
     big = host.traces(host.resource_spans({"service.name": "svc-a"}, [
-        host.span("x", kind=2, trace_id=_tid(200 + k), attributes={"url.path": "/" + "q" * 60}) for k in range(60)]))
+        host.span("x", kind=2, trace_id=_tid(200 + k),
+                  attributes={"http.request.method": "GET", "url.path": "/" + "q" * 60}) for k in range(60)]))
     with pytest.raises(native.OseError) as ei:
         shim.add(big, 2 * S)
     assert ei.value.code == native.OSE_ERANGE
