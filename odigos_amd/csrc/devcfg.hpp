@@ -37,13 +37,12 @@ struct NameDev {
 
 // Name table order: 0 "id", 1 "date", 2 "email", 3.. custom-id names.
 enum : uint32_t { kNameId = 0, kNameDate = 1, kNameEmail = 2, kNameCustom0 = 3 };
-constexpr uint32_t kMaxRuleLen = 64;   // rules longer than this never match (paths split into > 64 segments are not rule-eligible... see engine.cpp)
 
 struct UrlCfgDev {
   uint32_t n_custom, n_rules, n_names, n_dfa;
   uint32_t max_rule_nseg;        // 0 when there are no rules
   uint32_t max_name_len;
-  uint32_t rules_by_len_off;     // uint32 [kMaxRuleLen + 2]: first rule index for nseg (rules sorted by nseg, config order within)
+  uint32_t rules_by_len_off;     // uint32 [max_rule_nseg + 2]: first rule index for nseg (rules sorted by nseg, config order within)
   uint32_t rules_off;            // UrlRuleDev[n_rules]
   uint32_t segs_off;             // UrlRuleSegDev[]
   uint32_t custom_off;           // UrlCustomDev[n_custom]

@@ -80,11 +80,13 @@ int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32
     if (!e.empty()) return fail(OSE_EINVAL, e);
     pr.nseg = (uint32_t)pr.segs.size();
     pr.order = k;
-    if (pr.nseg > kMaxRuleLen) return fail(OSE_ENOTSUP, "templatization rule has more than 64 segments");
     rules.push_back(std::move(pr));
   }
   std::stable_sort(rules.begin(), rules.end(), [](const ParsedRule& a, const ParsedRule& b) { return a.nseg < b.nseg; });
-  std::vector<uint32_t> by_len(kMaxRuleLen + 2, 0);
+  uint32_t longest = 0;
+  for (auto& r : rules) longest = std::max(longest, r.nseg);
+  // by_len[n] for n <= longest + 1 (a path with more segments than the longest rule tries none)
+  std::vector<uint32_t> by_len(longest + 2, 0);
   std::vector<UrlRuleDev> rdev;
   std::vector<UrlRuleSegDev> sdev;
   uint32_t max_nseg = 0;
@@ -111,7 +113,7 @@ int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32
     }
   }
   // by_len[n] = first rule with nseg >= n
-  for (uint32_t n = 0; n <= kMaxRuleLen + 1; n++) {
+  for (uint32_t n = 0; n <= longest + 1; n++) {
     uint32_t k = 0;
     while (k < rules.size() && rules[k].nseg < n) k++;
     by_len[n] = k;

@@ -281,7 +281,7 @@ def test_gpu_refused_add_leaves_store_unchanged():
     # releases see exactly the store before it
     from odigos_amd.batch import Engine
     eng = Engine(CFG)
-    shim = _Shim(eng, {"wait_duration": "10s", "num_traces": 8}, span_capacity=4096, arena_capacity=3000)
+    shim = _Shim(eng, {"wait_duration": "10s", "num_traces": 8}, span_capacity=4096, arena_capacity=1 << 16)
     ref = GroupByTraceRef(10 * S, num_traces=8)
     for now, ks in ((0, [1, 2, 3]), (1 * S, [4, 5, 6, 7])):
         td = _mk(ks, "p%d-" % now)
@@ -290,7 +290,7 @@ def test_gpu_refused_add_leaves_store_unchanged():
     before = shim.g.stats()
     big = host.traces(host.resource_spans({"service.name": "svc-a"}, [
         host.span("x", kind=2, trace_id=_tid(200 + k),
-                  attributes={"http.request.method": "GET", "url.path": "/" + "q" * 60}) for k in range(60)]))
+                  attributes={"http.request.method": "GET", "url.path": "/" + "q" * 999}) for k in range(80)]))
     with pytest.raises(native.OseError) as ei:
         shim.add(big, 2 * S)
     assert ei.value.code == native.OSE_ERANGE
