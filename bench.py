@@ -485,6 +485,21 @@ def main():
                      "kernel": kname, "kernel_ms": k_ms, "kernel_ms_each": per_k,
                      "algorithmic_bytes_per_launch": b_alg},
     }
+    # measured HBM stream-copy bandwidth beside the spec peak (2 x 2 GiB copy,
+    # read + written bytes over the kernel time)
+    try:
+        import ctypes as C
+        a_ = torch.empty(2 << 30, dtype=torch.uint8, device="cuda")
+        b_ = torch.empty_like(a_)
+        bw = C.c_double()
+        native.check(native.lib().osehost_stream_copy(b_.data_ptr(), a_.data_ptr(), a_.numel(), 10, C.c_void_p(sh),
+                                                      C.byref(bw)))
+        out["roofline"]["stream_copy_gbs"] = bw.value
+        out["roofline"]["frac_of_stream_copy"] = achieved / bw.value if bw.value else None
+        del a_, b_
+    except Exception as ex:   # diagnostics only
+        out["roofline"]["stream_copy_gbs"] = None
+        print("stream copy measurement failed:", ex, file=sys.stderr)
     if rank == 0 and world == 1 and args.workload != "owner":
         orc = native_oracle()
         if not args.no_cpu_baseline:

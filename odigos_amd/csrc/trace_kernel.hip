@@ -103,6 +103,25 @@ __device__ __forceinline__ void seg_or_scan(uint32_t h, uint32_t& err, uint64_t&
   seg_or_step<0x142, 0xA>(h, err, ep, sv);
   seg_or_step<0x143, 0xC>(h, err, ep, sv);
 }
+// two 64-bit words (the latency stretches' threshold bits and latency-slot bits)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_or2_step(uint32_t& h, uint64_t& x, uint64_t& y) {
+  const uint32_t oh = dpp_mov<CTRL, ROWS>(0u, h);
+  const uint64_t ox = dpp64<CTRL, ROWS>(0ull, x), oy = dpp64<CTRL, ROWS>(0ull, y);
+  if (!h) {
+    x |= ox;
+    y |= oy;
+  }
+  h |= oh;
+}
+__device__ __forceinline__ void seg_or2_scan(uint32_t h, uint64_t& x, uint64_t& y) {
+  seg_or2_step<0x111, 0xF>(h, x, y);
+  seg_or2_step<0x112, 0xF>(h, x, y);
+  seg_or2_step<0x114, 0xF>(h, x, y);
+  seg_or2_step<0x118, 0xF>(h, x, y);
+  seg_or2_step<0x142, 0xA>(h, x, y);
+  seg_or2_step<0x143, 0xC>(h, x, y);
+}
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
 #pragma unroll
@@ -716,35 +735,74 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         }
       }
     }
-    // ---- segmented OR of the flag masks (DPP scan; h = segment head) ----
+    // ---- latency state (latency.go:69-80) ----
+    // One segmented scan of the monoid over stretches: maximal runs of lanes
+    // with one trace and one latency slot (a trace's spans of a service come
+    // together, ResourceSpans by ResourceSpans).  A stretch's element is its
+    // trace's element for that slot when the slot has no other stretch in the
+    // trace within this step; the step checks that (slot bits OR-scanned per
+    // trace) and otherwise takes the per-slot scans below.  At a stretch tail
+    // the slot's rules whose threshold the duration reaches are found without
+    // the endpoint mask; ORed per trace and masked by the trace's endpoint bits
+    // at its tail, they are the per-slot result.  The carried trace (segment 0)
+    // and the trace left open at the end combine their stretches into the
+    // per-slot carry registers in lane order.
     const uint32_t hseg = mine ? (uint32_t)((segmask >> lane) & 1) : 1u;
+    // ---- segmented OR of the flag masks (DPP scan; h = segment head) ----
     seg_or_scan(hseg, err, ep, svcb);
-    // ---- latency state, one segmented scan per latency slot present ----
     uint64_t lsat = 0, n_kmask = 0;
     Lat nxt{0, kInf, 0};
     const bool carried_tail = (lane == t0 && seg0_cont) || (lane == last_own && last_open);
-    uint64_t pend = (a.ablate & 2) ? 0 : __ballot(slot != kNoSlot);
-    while (pend) {
-      const uint32_t ks = rdl(slot, ffs64(pend));
-      const bool ink = slot == ks;
-      pend &= ~__ballot(ink);
-      Lat v = ink ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
-      seg_lat_scan(hseg, v);
-      if (tail && !carried_tail && (v.f & 2u)) lsat |= latency_satisfied(c, ks, ep, v.m, v.e);
-      if (seg0_cont) {
-        const uint32_t f0 = rdl(v.f, t0);
-        if (f0 & 2u) {
-          const Lat v0{f0, rdl64(v.m, t0), rdl64(v.e, t0)};
+    const bool lat_on = !(a.ablate & 2) && __ballot(slot != kNoSlot) != 0;   // wave-uniform
+    uint64_t lraw = 0, smask = 0;
+    bool stail = false, shead = false;
+    if (lat_on) {
+      const uint32_t pslot = dpp_mov<0x138>(kNoSlot, slot);   // lane - 1's slot (wave_shr:1)
+      shead = !mine || hseg || pslot != slot;
+      const uint32_t hs = shead ? 1u : 0u;
+      stail = mine && dpp_mov<0x130>(1u, hs) != 0;            // lane + 1 starts a stretch (wave_shl:1)
+      Lat v = slot != kNoSlot ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+      seg_lat_scan(hs, v);
+      const bool lt = stail && (v.f & 2u);
+      if (lt) lraw = latency_satisfied(c, slot, ~0ull, v.m, v.e);
+      if (slot != kNoSlot) smask = 1ull << slot;
+      if (seg0_cont) {   // the carried trace's stretches, in order
+        for (uint64_t m0 = __ballot(lt && lane <= t0); m0; m0 &= m0 - 1) {
+          const int L = ffs64(m0);
+          const uint32_t ks = rdl(slot, L);
+          const Lat v0{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
           if ((uint32_t)lane == ks) cur = lat_comb(cur, v0);
           c_kmask |= 1ull << ks;
         }
       }
-      if (last_open) {
-        const uint32_t fl = rdl(v.f, last_own);
-        if (fl & 2u) {
-          if ((uint32_t)lane == ks) nxt = Lat{fl, rdl64(v.m, last_own), rdl64(v.e, last_own)};
+      if (last_open) {   // the open trace's stretches, in order
+        for (uint64_t m1 = __ballot(lt && lane >= sst_last); m1; m1 &= m1 - 1) {
+          const int L = ffs64(m1);
+          const uint32_t ks = rdl(slot, L);
+          const Lat v1{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
+          if ((uint32_t)lane == ks) nxt = lat_comb(nxt, v1);
           n_kmask |= 1ull << ks;
         }
+      }
+    }
+    if (lat_on) {
+      seg_or2_scan(hseg, lraw, smask);
+      // a slot with two stretches in a trace this step closes: per-slot scans
+      const uint64_t psm = dpp64<0x138, 0xF>(0ull, smask);   // lane - 1's inclusive slot bits
+      const bool in_closed = mine && !(seg0_cont && lane <= t0) && !(last_open && lane >= sst_last);
+      const bool rep = in_closed && shead && !hseg && slot != kNoSlot && ((psm >> slot) & 1);
+      if (__ballot(rep)) {
+        uint64_t pend = __ballot(slot != kNoSlot && in_closed);
+        while (pend) {
+          const uint32_t ks = rdl(slot, ffs64(pend));
+          const bool ink = slot == ks;
+          pend &= ~__ballot(ink);
+          Lat v = ink ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+          seg_lat_scan(hseg, v);
+          if (tail && !carried_tail && (v.f & 2u)) lsat |= latency_satisfied(c, ks, ep, v.m, v.e);
+        }
+      } else if (tail && !carried_tail) {
+        lsat = lraw & ep;
       }
     }
     // ---- the carried trace closes in this step: queue it ----

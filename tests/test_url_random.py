@@ -217,3 +217,51 @@ def test_gpu_url_parity_paths_spread_through_the_arena():
     path[has] = path[has][perm]
     used = _gpu_vs_oracle_cols(g, {})
     assert used > 0
+
+
+def _long_rule_cfg():
+    # a templatization rule of 70 segments (the reference has no limit:
+    # parseUserInputRuleString, templatize.go:97-138)
+    segs = ["seg%d" % k for k in range(70)]
+    segs[3] = "{id}"
+    segs[69] = "{last:\\d+}"
+    return {"templatization_rules": ["/" + "/".join(segs), "/users/{user}"]}
+
+
+def test_long_rule_accepted_at_creation():
+    import ctypes as C
+    import json
+    h = C.c_void_p()
+    rc = native.lib().ose_engine_create(json.dumps({"odigosurltemplate": _long_rule_cfg()}).encode(), C.byref(h))
+    assert rc in (0, native.OSE_EDEVICE), (rc, native.last_error())
+    if rc == 0:
+        native.lib().ose_engine_destroy(h)
+
+
+@pytest.mark.gpu
+def test_gpu_url_parity_rule_longer_than_64_segments():
+    import torch
+    from tests.test_unicode_regex import _cols_from_paths
+    rng = random.Random(0x0D1600D1)
+    paths = []
+    for k in range(3000):
+        segs = ["seg%d" % j for j in range(70)]
+        segs[3] = str(rng.randrange(10**6))
+        segs[69] = str(rng.randrange(10**6)) if k % 3 else "x%d" % k
+        if k % 5 == 0:
+            segs = segs[: rng.randrange(60, 75)]
+        paths.append(("/" + "/".join(segs)).encode())
+    cols, _keep = _cols_from_paths(paths)
+    cfg = _long_rule_cfg()
+    eng = Engine({"odigosurltemplate": cfg})
+    db = DeviceBatch(cols)
+    eng.process_device(db, native.STAGE_TEMPLATE)
+    torch.cuda.synchronize()
+    ho = HostOutputs(cols)
+    assert UrlOracle(cfg).process(cols, ho.outs, 4) == 0
+    n = cols.n_spans
+    np.testing.assert_array_equal(db.out_numpy("url_out", n=n), ho.view("url_out", np.uint8)[:n])
+    used = db.used()
+    assert used == int(ho.used[0])
+    np.testing.assert_array_equal(db.out_numpy("tmpl_arena", n=used), ho.bufs["tmpl_arena"][:used])
+    assert b"{last}" in ho.bufs["tmpl_arena"][:used].tobytes()
