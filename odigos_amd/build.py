@@ -55,18 +55,23 @@ def _compile_all(jobs, items):
             f.result()
 
 
-def build_product(force: bool = False, jobs: int = 8) -> Path:
+def build_product(force: bool = False, jobs: int = 8, variant: str = "", defines=()) -> Path:
+    """variant/defines: an A/B build of the same sources with extra -D flags
+    (libodigos_amd<variant>.so, loaded when OSE_LIB_VARIANT=<variant>;
+    diagnostics only — the product is the default build)."""
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    OBJDIR.mkdir(parents=True, exist_ok=True)
-    out = LIBDIR / "libodigos_amd.so"
+    objdir = OBJDIR / ("variant" + variant) if variant else OBJDIR
+    objdir.mkdir(parents=True, exist_ok=True)
+    out = LIBDIR / f"libodigos_amd{variant}.so"
+    flags = HIP_FLAGS + [f"-D{d}" for d in defines]
     headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "odigos_amd.h"]
     hdr_t = _deps_mtime(headers)
     cmds, objs = [], []
     for src in PRODUCT_SOURCES:
-        obj = OBJDIR / (src.name + ".o")
+        obj = objdir / (src.name + ".o")
         objs.append(obj)
-        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_t):
-            cmds.append([HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)])
+        if force or variant or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_t):
+            cmds.append([HIPCC, *flags, "-c", str(src), "-o", str(obj)])
     _compile_all(jobs, cmds)
     if force or cmds or not out.exists() or out.stat().st_mtime < _deps_mtime(objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(out), *map(str, objs)])
@@ -96,5 +101,9 @@ def build_all(force: bool = False, jobs: int = 8) -> None:
 
 
 if __name__ == "__main__":
+    if "--variant" in sys.argv:   # python -m odigos_amd.build --variant _b NAME=VALUE ...
+        k = sys.argv.index("--variant")
+        print("built:", build_product(variant=sys.argv[k + 1], defines=sys.argv[k + 2:]))
+        sys.exit(0)
     build_all(force="--force" in sys.argv)
     print("built:", LIBDIR / "libodigos_amd.so", LIBDIR / "libosegen.so", ORACLE / "liboracle.so")

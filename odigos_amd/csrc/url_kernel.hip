@@ -451,6 +451,12 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // ds_read_b128).  Built cooperatively, 32 bytes per lane, branch-free.
 // Classes 0-7 are read for every segment; 8-11 (the email classes) only for
 // segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
+#ifndef OSE_URL_SWZ
+#define OSE_URL_SWZ 1     // swizzled row reads in build_row (A/B: odigos_amd/build.py --variant)
+#endif
+#ifndef OSE_URL_ASM32
+#define OSE_URL_ASM32 1   // dword-packed assembly (ds_or_b32 into a zeroed image) instead of byte stores
+#endif
 enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
 constexpr uint32_t kBase = 8;
 constexpr uint32_t kRowVec = 3;   // u32x4 per row
@@ -468,7 +474,16 @@ __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t
 #pragma unroll
     for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
     const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
+#if OSE_URL_SWZ
+    // rows r and r + 8 read their two halves in opposite order: the 32-byte
+    // row stride alone puts them on the same ds_read_b128 banks (2-way)
+    const uint32_t sw = (r >> 3) & 1u;
+    const u32x4 v0 = src[sw], v1 = src[sw ^ 1u];
+    const uint32_t dsh = sw << 4;   // xs[d] is row dword d ^ 4sw: its bits go to 4d ^ 16sw
+#else
     const u32x4 v0 = src[0], v1 = src[1];
+    const uint32_t dsh = 0;
+#endif
     const uint32_t xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
     for (int d = 0; d < 8; d++) {
@@ -503,7 +518,7 @@ __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t
           ~alpha & kH,                                     // C_NAL
       };
 #pragma unroll
-      for (int c = 0; c < (int)kClasses; c++) acc[c] |= movemask4(m[c]) << (4 * d);
+      for (int c = 0; c < (int)kClasses; c++) acc[c] |= movemask4(m[c]) << ((4 * d) ^ dsh);
     }
     bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
     bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
@@ -1293,6 +1308,9 @@ __device__ __forceinline__ uint32_t plan_gate(const PlanCols& c) {
 // stores, 8 loads in flight per batch), so the image needs no clearing.
 // Entries are written 64 per step, one per lane: the per-byte work follows the
 // longest segment of a step, not the longest path of the group.
+// OSE_URL_ASM32: each entry's bytes go out as whole dwords (ds_or_b32 into an
+// image the caller zeroed; two unaligned dword reads of the source per
+// dword), about a third of the LDS instructions of the byte form.
 __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L, uint32_t stage_src, const uint32_t* segs,
                                                const uint32_t* cls, const BracedNames& bn, uint32_t bn_src,
                                                const Plan& p, uint32_t seg_off, uint32_t local) {
@@ -1304,7 +1322,14 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
   const uint32_t E0 = wave_excl_scan(nseg ? p.len + 1 - pre : 0u, &unused);
   const int32_t adj = (int32_t)local - (int32_t)E0 - (int32_t)(1 - pre);
   const uint32_t pk = ((uint32_t)adj & 0xFFFFu) | (off << 16) | (pre << 24);
-  if (p.len && (p.mode == M_SLASH || p.mode == M_RENAME_SLASH)) img[local] = '/';
+  if (p.len && (p.mode == M_SLASH || p.mode == M_RENAME_SLASH)) {
+#if OSE_URL_ASM32
+    __hip_atomic_fetch_or((lds_w32*)img + (local >> 2), (uint32_t)'/' << (8 * (local & 3)), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+    img[local] = '/';
+#endif
+  }
   const uint32_t total = lane_value(off + nseg, kWave - 1);
   uint32_t carry = 0;
   for (uint32_t x0 = 0; x0 < total; x0 += kWave) {
@@ -1317,10 +1342,27 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
     carry += stot;
     if (v) {
       const uint32_t pos = (uint32_t)(((int32_t)(opk << 16) >> 16) + (int32_t)E);
-      if (x != ((opk >> 16) & 0xFFu) || (opk >> 24)) img[pos] = '/';
+      const bool slash = x != ((opk >> 16) & 0xFFu) || (opk >> 24);
       const int id = (int)(c & 0xFFu) - 1;
-      const lds_u8* sp = L + (id >= 0 ? bn_src + bn.off[id] : stage_src + (ent & 0xFFFu));
+      const uint32_t so = id >= 0 ? bn_src + bn.off[id] : stage_src + (ent & 0xFFFu);   // the body's LDS byte offset
       const uint32_t n = id >= 0 ? (uint32_t)bn.len[id] : (ent >> 12) & 0x1FFFu;
+#if OSE_URL_ASM32
+      // output bytes [b0, b1): '/' at pos (when written), the body at pos + 1;
+      // each image dword they touch gets its bytes by one ds_or_b32 (the image
+      // was zeroed; dwords shared with the neighbouring entries get OR-ed)
+      const uint32_t b0 = slash ? pos : pos + 1, b1 = pos + 1 + n;
+      lds_w32* img32 = (lds_w32*)img;
+      for (uint32_t k = b0 >> 2; 4 * k < b1; k++) {
+        // body byte i sits at image byte pos + 1 + i: the dword's 4 bytes are body bytes 4k - pos - 1 + j
+        uint32_t w = lds_word(L, so + 4 * k - pos - 1);
+        const uint32_t lo = b0 > 4 * k ? b0 - 4 * k : 0u, hi = b1 - 4 * k < 4 ? b1 - 4 * k : 4u;
+        if (slash && pos >> 2 == k) w = (w & ~(0xFFu << (8 * (pos & 3)))) | ('/' << (8 * (pos & 3)));
+        const uint32_t mask = (hi == 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
+        __hip_atomic_fetch_or(&img32[k], w & mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#else
+      if (slash) img[pos] = '/';
+      const lds_u8* sp = L + so;
       lds_out_u8* dp = img + pos + 1;
       for (uint32_t q = 0; q < n; q += 8) {
         uint32_t b[8];
@@ -1330,6 +1372,7 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
         for (uint32_t t = 0; t < 8; t++)
           if (q + t < n) dp[q + t] = (uint8_t)b[t];
       }
+#endif
     }
   }
 }
@@ -1471,6 +1514,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
       const uint32_t n16 = (uint32_t)(need / 16);
       uint32_t unused;
       const uint32_t local = wave_excl_scan(p.len, &unused);
+#if OSE_URL_ASM32
+      for (uint32_t k = lane; k < n16; k += kWave) img4[k] = u32x4{0u, 0u, 0u, 0u};   // the bitmaps are dead here
+      wave_lds_sync();
+#endif
       if (!(a.ablate & 64))   // diagnostics: OSE_URL_ABLATE 64 skips the image writes (wrong output)
         assemble_group((lds_out_u8*)sm.bm[wv], L, (uint32_t)(stage - (uint8_t*)&sm), sm.segs[wv], sm.cls[wv], sm.bn,
                        bn_src, p, seg_off, local);

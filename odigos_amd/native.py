@@ -6,6 +6,7 @@ fails loudly; nothing here falls back to a CPU implementation.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libodigos_amd.so"
@@ -101,8 +102,12 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
-        raise RuntimeError(f"{LIB_PATH} is missing: run `python -m odigos_amd.build` (hipcc, gfx950)")
+    path = LIB_PATH
+    variant = os.environ.get("OSE_LIB_VARIANT", "")   # A/B diagnostics (odigos_amd/build.py --variant)
+    if variant:
+        path = LIB_PATH.with_name(f"libodigos_amd{variant}.so")
+    if not path.exists():
+        raise RuntimeError(f"{path} is missing: run `python -m odigos_amd.build` (hipcc, gfx950)")
     # One HIP runtime per process: torch ships its own libamdhip64 (soname
     # libamdhip64.so.7, loaded by file name from torch/lib).  Loading torch
     # first makes this library bind to that same copy instead of a second
@@ -111,7 +116,7 @@ def lib() -> C.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(str(LIB_PATH))
+    L = C.CDLL(str(path))
     sig = {
         "ose_last_error": (C.c_char_p, []),
         "ose_engine_create": (C.c_int, [C.c_char_p, C.POINTER(_p)]),
