@@ -85,6 +85,14 @@ WORKLOADS = {
                   metric_config="C4: fused odigossampling -> odigosurltemplate -> odigostrafficmetrics, 100M spans "
                                 "in total (all on one GPU at N=1; ~100M/N per GPU, trace-id all-to-all over RCCL "
                                 "at N>1)"),
+    "node8": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False, ranks=8,
+                  cfg=None, stages="SAMPLE|TEMPLATE|SIZE", null_columns=("res_url_ok",),
+                  null_outputs=PER_TRACE_OUTS + ("res_bytes",), fields=FUSED_FIELDS,
+                  kernels=("shard_pack", "shard_unpack") + TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS + SIZE_KERNELS,
+                  metric_config="diagnostic: C4 at N=8 emulated on ONE GPU -- the 8 ranks' whole steps (pack, the "
+                                "exchange round through the in-process transport, owner SAMPLE, reverse split, "
+                                "TEMPLATE on a second stream, SIZE|APPLY_KEEP), one thread, engine and stream pair "
+                                "per rank; the projected per-GPU step is the wall time / 8"),
     "owner": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False, sources=8,
                   cfg=None, stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
                   fields=SAMPLE_FIELDS, kernels=("shard_unpack",) + TRACE_KERNELS + SLOW_KERNELS,
@@ -343,7 +351,47 @@ def main():
     gen = db = comm = None
     extra = {}
 
-    if args.workload == "owner":
+    if args.workload == "node8":
+        assert world == 1, "the node8 workload emulates an 8-GPU step on one GPU"
+        import concurrent.futures as cf
+        import ctypes as C
+        W = wl["ranks"]
+        L = native.lib()
+        grp = C.c_void_p()
+        native.check(L.osehost_xgroup_create(W, C.byref(grp)))
+        engs, dbs, mains, sides, gens = [], [], [], [], []
+        for r in range(W):
+            g = Generator(wl["gen"], seed=wl["seed"], n_spans=total, threads=gen_threads, rank=r, world=W)
+            for f in wl.get("null_columns", ()):
+                setattr(g.cols, f, None)
+            d = DeviceBatch(g.cols, fields=wl.get("fields"))
+            for f in wl.get("null_outputs", ()):
+                setattr(d.outs, f, None)
+            e = eng if r == 0 else Engine(cfg)
+            e.reserve(g.cols.n_spans, g.cols.arena_bytes)
+            engs.append(e); dbs.append(d); gens.append(g)
+            mains.append(torch.cuda.Stream()); sides.append(torch.cuda.Stream())
+        n_units = sum(g.cols.n_spans for g in gens)
+        gen, db = gens[0], dbs[0]
+        stats = [(C.c_uint64 * 3)() for _ in range(W)]
+        local_st = native.STAGE_SIZE | native.STAGE_APPLY_KEEP
+        pool = cf.ThreadPoolExecutor(W)
+
+        def rank_step(r):
+            rnd = native.Rand(0x5EED, 0.0)
+            sides[r].wait_stream(mains[r])
+            engs[r].process_device(dbs[r], native.STAGE_TEMPLATE, native.GROUP_TRACE_ID, seed=0x5EED,
+                                   stream=sides[r].cuda_stream)
+            native.check(L.osehost_exchange_sample_local(engs[r].h, C.byref(dbs[r].cols), C.byref(dbs[r].outs), grp,
+                                                         r, C.byref(rnd), C.c_void_p(mains[r].cuda_stream), stats[r]))
+            mains[r].wait_stream(sides[r])
+            engs[r].process_device(dbs[r], local_st, native.GROUP_TRACE_ID, seed=0x5EED, stream=mains[r].cuda_stream)
+
+        def step():
+            for f in [pool.submit(rank_step, r) for r in range(W)]:
+                f.result()
+        extra = {"emulated_ranks": W}
+    elif args.workload == "owner":
         assert world == 1, "the owner workload emulates an 8-GPU step on one GPU"
         recv, n_rec, spans_repr, rb = build_owner_batch(eng, wl, gen_threads)
         from odigos_amd.exchange import DeviceExchange
@@ -408,7 +456,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.profile(True)
+    all_engs = engs if args.workload == "node8" else [eng]
+    for e in all_engs:
+        e.profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -416,8 +466,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    eng.profile(False)
-    prof = eng.profile_read()
+    prof = {}
+    for e in all_engs:
+        e.profile(False)
+        for k, v in e.profile_read().items():
+            acc = prof.setdefault(k, {"launches": 0, "ms": 0.0})
+            acc["launches"] += v["launches"]
+            acc["ms"] += v["ms"]
     if db is not None:
         status = int(db.out_numpy("device_status", np.uint32)[0])
         if status:
@@ -443,11 +498,22 @@ def main():
         out_kernels = dict(prof)
         extra["exchange_kernels_ms"] = {k: v["ms"] / max(args.steps, 1) for k, v in out_kernels.items()
                                         if k in ("shard_pack", "shard_unpack", "owner_sample")}
+    if args.workload == "node8":
+        st_ = [[int(x) for x in st] for st in stats]
+        extra.update({"exchange_records_sent": sum(x[0] for x in st_),
+                      "exchange_record_bytes_per_span": native.XREC_BYTES * sum(x[0] for x in st_) / max(n_units, 1),
+                      "projected_ms_per_gpu_step": elapsed / args.steps * 1e3 / W,
+                      "kernel_ms_per_gpu_step": k_ms / W,
+                      "projected_xgmi_ms": native.XREC_BYTES * max(x[0] for x in st_) * (W - 1) / W /
+                                           (7 * 153e9) * 1e3 * 2})   # records + keep bytes back, 7 links of 153 GB/s
     if args.workload == "owner":
         b_alg = None
         achieved = 0.0
     else:
-        b_alg = algorithmic_bytes(wl, gen, db, n_units, cfg)
+        if args.workload == "node8":
+            b_alg = sum(algorithmic_bytes(wl, g, d, g.cols.n_spans, cfg) for g, d in zip(gens, dbs))
+        else:
+            b_alg = algorithmic_bytes(wl, gen, db, n_units, cfg)
         achieved = b_alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
 
     traffic = None

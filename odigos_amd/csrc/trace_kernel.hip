@@ -123,10 +123,14 @@ __device__ __forceinline__ void seg_or2_scan(uint32_t h, uint64_t& x, uint64_t& 
   seg_or2_step<0x143, 0xC>(h, x, y);
 }
 
+// OR over the wave, broadcast: DPP row_shr within each 16-lane row, then the
+// four row results read out (no ds_bpermute round trips)
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, kWave);
-  return v;
+  v |= dpp64<0x111, 0xF>(0ull, v);
+  v |= dpp64<0x112, 0xF>(0ull, v);
+  v |= dpp64<0x114, 0xF>(0ull, v);
+  v |= dpp64<0x118, 0xF>(0ull, v);
+  return rdl64(v, 15) | rdl64(v, 31) | rdl64(v, 47) | rdl64(v, 63);
 }
 
 struct Cfg {
@@ -835,7 +839,14 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     const uint32_t nq = __popcll(qmask);
     if (nq) {
       if (qn + nq > kQ) flush_queue(a, c, Q, qn, lane);
-      const uint64_t hh = __shfl(r.hi, sst, kWave), hl = __shfl(r.lo, sst, kWave);
+      // the trace's first span's id (the injected uniform): in batch order and
+      // in the sorted permutation every span of a segment has that id; only a
+      // whole-batch trace (OSE_GROUP_BATCH) mixes ids
+      uint64_t hh = r.hi, hl = r.lo;
+      if (a.mode == kTraceBatch) {
+        hh = __shfl(r.hi, sst, kWave);
+        hl = __shfl(r.lo, sst, kWave);
+      }
       if ((qmask >> lane) & 1) {
         const uint32_t e = qn + __popcll(qmask & lanemask_lt(lane));
         Q.err[e] = err;

@@ -454,8 +454,11 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #ifndef OSE_URL_SWZ
 #define OSE_URL_SWZ 1     // swizzled row reads in build_row (A/B: odigos_amd/build.py --variant)
 #endif
+#ifndef OSE_URL_RDMASK
+#define OSE_URL_RDMASK 1  // bitmap rows past a segment / path are not read
+#endif
 #ifndef OSE_URL_ASM32
-#define OSE_URL_ASM32 1   // dword-packed assembly (ds_or_b32 into a zeroed image) instead of byte stores
+#define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores
 #endif
 enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
 constexpr uint32_t kBase = 8;
@@ -568,13 +571,24 @@ template <int NV>
 struct WinT {
   uint64_t c[4 * NV];
 };
+// L: the bytes the caller looks at (<= 64): rows past them are not read
+// (OSE_URL_RDMASK), so a short segment costs one or two rows of LDS reads
 template <int V0, int NV>
-__device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a) {
+__device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a, uint32_t L = 64) {
   const uint32_t r = a >> 5, sh = a & 31;
+#if OSE_URL_RDMASK
+  const bool r1 = sh + L > 32, r2 = sh + L > 64;
+#else
+  const bool r1 = true, r2 = true;
+  (void)L;
+#endif
   WinT<NV> w;
 #pragma unroll
   for (int v = 0; v < NV; v++) {
-    const u32x4 x0 = bm[kRowVec * r + V0 + v], x1 = bm[kRowVec * (r + 1) + V0 + v], x2 = bm[kRowVec * (r + 2) + V0 + v];
+    const u32x4 z{0u, 0u, 0u, 0u};
+    const u32x4 x0 = bm[kRowVec * r + V0 + v];
+    const u32x4 x1 = r1 ? bm[kRowVec * (r + 1) + V0 + v] : z;
+    const u32x4 x2 = r2 ? bm[kRowVec * (r + 2) + V0 + v] : z;
     const uint32_t w0[4] = {x0.x, x0.y, x0.z, x0.w}, w1[4] = {x1.x, x1.y, x1.z, x1.w}, w2[4] = {x2.x, x2.y, x2.z, x2.w};
 #pragma unroll
     for (int c = 0; c < 4; c++)
@@ -642,7 +656,7 @@ __device__ __forceinline__ bool email_win(uint64_t at, lds_cu4* bm, uint32_t a, 
   const uint64_t M = low_mask(L);
   const uint32_t p = (uint32_t)__builtin_ctzll(at);
   if (p == 0) return false;
-  const WinT<1> e = load_win<2, 1>(bm, a);   // BLOC, BDOM, DOT, NAL
+  const WinT<1> e = load_win<2, 1>(bm, a, L);   // BLOC, BDOM, DOT, NAL
   const uint64_t dom = M & ~low_mask(p + 1);
   if ((e.c[0] & low_mask(p)) || (e.c[1] & dom)) return false;
   const uint64_t dots = e.c[2] & dom;
@@ -1122,12 +1136,24 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   if (needs_path) {
     if (win) {
       uint32_t w[12];
+#if OSE_URL_RDMASK
+      // only the rows the path covers, and the '?' words only for http.target
+      const uint32_t nrow = (b0 + plen + 31) >> 5;
+      const bool tgt = (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET;
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        const uint32_t r = min(r0 + j, kPlanBmRows - 1);
+        w[j] = (uint32_t)j < nrow ? b32[4 * kRowVec * r + C_SL] : 0u;
+        w[6 + j] = tgt && (uint32_t)j < nrow ? b32[4 * kRowVec * r + C_QM] : 0u;
+      }
+#else
 #pragma unroll
       for (int j = 0; j < 6; j++) {
         const uint32_t r = min(r0 + j, kPlanBmRows - 1);   // rows past the path are masked off below
         w[j] = b32[4 * kRowVec * r + C_SL];
         w[6 + j] = b32[4 * kRowVec * r + C_QM];
       }
+#endif
       sl0 = w[0] | ((uint64_t)w[1] << 32);
       sl1 = w[2] | ((uint64_t)w[3] << 32);
       sl2 = w[4] | ((uint64_t)w[5] << 32);
@@ -1216,7 +1242,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
     const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
     int id = -1;
     if (L <= 64) {
-      const Win w = load_win<0, 2>(bm, s);
+      const Win w = load_win<0, 2>(bm, s, L);
       id = classify_win(cfg, rd0, w, bm, s, s, L);
     } else {
       longseg = true;   // a segment longer than a 64-bit window: the group goes to url_plan_slow_kernel
