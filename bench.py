@@ -370,7 +370,12 @@ def main():
             e = eng if r == 0 else Engine(cfg)
             e.reserve(g.cols.n_spans, g.cols.arena_bytes)
             engs.append(e); dbs.append(d); gens.append(g)
-            mains.append(torch.cuda.Stream()); sides.append(torch.cuda.Stream())
+            if os.environ.get("OSE_NODE8_ONE_STREAM") and mains:
+                # diagnostic: every rank's work on ONE stream, so each kernel's
+                # duration is uncontended and their sum / 8 is a serial per-GPU step
+                mains.append(mains[0]); sides.append(mains[0])
+            else:
+                mains.append(torch.cuda.Stream()); sides.append(torch.cuda.Stream())
         n_units = sum(g.cols.n_spans for g in gens)
         gen, db = gens[0], dbs[0]
         stats = [(C.c_uint64 * 3)() for _ in range(W)]
@@ -390,7 +395,7 @@ def main():
         def step():
             for f in [pool.submit(rank_step, r) for r in range(W)]:
                 f.result()
-        extra = {"emulated_ranks": W}
+        extra = {"emulated_ranks": W, "one_stream": bool(os.environ.get("OSE_NODE8_ONE_STREAM"))}
     elif args.workload == "owner":
         assert world == 1, "the owner workload emulates an 8-GPU step on one GPU"
         recv, n_rec, spans_repr, rb = build_owner_batch(eng, wl, gen_threads)

@@ -654,12 +654,17 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu;
     uint4 rw = make_uint4(0, 0, 0, 0);
     if (valid && work) {
-      sv = a.res_svc[r.res];
-      ss = a.res_svc_str[r.res];
+      if (a.ablate & 16) {   // diagnostics: no dependent service-id loads
+        sv = r.res % (nsvc + 1);
+        ss = sv;
+      } else {
+        sv = a.res_svc[r.res];
+        ss = a.res_svc_str[r.res];
+      }
       // route bytes only for spans of a latency-rule service (strings.HasPrefix
       // is evaluated for nothing else): one dependent LDS lookup, and the
       // random 16-byte arena reads of every other routed span are skipped
-      if (want_route && r.route.len && sv < nsvc && c.svc_slot[sv] != kNoSlot)
+      if (want_route && r.route.len && sv < nsvc && c.svc_slot[sv] != kNoSlot && !(a.ablate & 32))
         rw = head16(a.arena, r.route.off, r.route.len);
     }
     const uint64_t vmask = __ballot(valid);

@@ -452,10 +452,10 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // Classes 0-7 are read for every segment; 8-11 (the email classes) only for
 // segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
 #ifndef OSE_URL_SWZ
-#define OSE_URL_SWZ 1     // swizzled row reads in build_row (A/B: odigos_amd/build.py --variant)
+#define OSE_URL_SWZ 0     // swizzled row reads in build_row: measured slower (C4 url_plan 7.20 vs 6.87 ms with both off)
 #endif
 #ifndef OSE_URL_RDMASK
-#define OSE_URL_RDMASK 1  // bitmap rows past a segment / path are not read
+#define OSE_URL_RDMASK 0  // skip bitmap rows past a segment / path: measured slower (the extra branches cost more than the reads)
 #endif
 #ifndef OSE_URL_ASM32
 #define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores

@@ -29,10 +29,13 @@ def timeit(label, ablate, reps=5):
     pr = eng.profile_read()["trace_eval_kernel"]
     print(f"{label:44s} {pr['ms'] / pr['launches']:9.3f} ms", flush=True)
 
-timeit("C3 baseline", 0)
+timeit("C3 baseline (lean instance)", 0)
+timeit("general instance (64: unused bit)", 64)
 timeit("no table insert (1)", 1)
 timeit("no latency scans (2)", 2)
 timeit("no decide (4)", 4)
 timeit("no endpoint prefix match (8)", 8)
-timeit("no OR scan (16)", 16)
-timeit("none of them (31)", 31)
+timeit("no dependent service-id loads (16)", 16)
+timeit("no route head reads (32)", 32)
+timeit("no dependent loads (48)", 48)
+timeit("none of them (63)", 63)
