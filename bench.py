@@ -128,13 +128,16 @@ def _stages(wl):
 
 
 # ---- algorithmic bytes -------------------------------
-def algorithmic_bytes_url(gen, url_out, used, n) -> int:
+def algorithmic_bytes_url(gen, url_out, tmpl, n) -> int:
     """URL row: per span 8 B path ref + 1 B kind + 1 B url_flags read, 8 B
     template ref + 1 B url_out written; plus the path bytes of every span
-    whose path is templatized (read) and the template bytes written."""
+    whose path is templatized (read) and the template bytes written (the
+    lengths of the emitted templates: the packed arena's size, and what the
+    refs form writes)."""
     path = gen.array("path").view(np.uint32).reshape(-1, 2)[:n]
     templ_read = int(path[(url_out[:n] & 1) != 0, 1].sum())
-    return n * (8 + 1 + 1) + n * (8 + 1) + templ_read + used
+    written = int(tmpl.reshape(-1, 2)[:n][url_out[:n] != 0, 1].astype(np.int64).sum())
+    return n * (8 + 1 + 1) + n * (8 + 1) + templ_read + written
 
 
 def algorithmic_bytes_sampling(gen, n, cfg) -> int:
@@ -156,7 +159,7 @@ def algorithmic_bytes(wl, gen, db, n, cfg) -> int:
     if "SAMPLE" in st:
         b += algorithmic_bytes_sampling(gen, n, cfg)
     if "TEMPLATE" in st:
-        b += algorithmic_bytes_url(gen, db.out_numpy("url_out", n=n), db.used(), n)
+        b += algorithmic_bytes_url(gen, db.out_numpy("url_out", n=n), db.out_numpy("tmpl", np.uint32, n=2 * n), n)
     if "SIZE" in st:
         # span_size, scope, name_len per span; 8 B per scope, 12 B per resource, 8 B per attribute set
         b += n * 12 + gen.cols.n_scopes * 8 + gen.cols.n_resources * 12 + gen.cols.n_attrsets * 8
@@ -262,10 +265,19 @@ def parity_full(wl, gen, db, cfg, stages, threads, calls):
         uo = db.out_numpy("url_out", n=n)
         res["url_out"] = bool(np.array_equal(ho.view("url_out", np.uint8)[:n], uo))
         m = uo != 0
-        res["tmpl_refs"] = bool(np.array_equal(ho.view("tmpl", np.uint64)[:n][m], db.out_numpy("tmpl", np.uint64, n=n)[m]))
         used = db.used()
-        res["tmpl_arena"] = bool(used == int(ho.used[0]) and
-                                 np.array_equal(ho.bufs["tmpl_arena"][:used], db.out_numpy("tmpl_arena", n=used)))
+        if stages & native.STAGE_TEMPLATE_REFS:
+            # per span: the bytes each ref names (the arena is sparse)
+            from tests.oracle_lib import span_template_bytes
+            gb, gl = span_template_bytes(db.out_numpy("tmpl", np.uint32, n=2 * n), db.out_numpy("tmpl_arena", n=used), m)
+            ob, ol = span_template_bytes(ho.view("tmpl", np.uint32)[: 2 * n], ho.bufs["tmpl_arena"][: int(ho.used[0])], m)
+            res["tmpl_lens"] = bool(np.array_equal(gl, ol))
+            res["tmpl_bytes_per_span"] = bool(gb.size == ob.size and np.array_equal(gb, ob))
+        else:
+            res["tmpl_refs"] = bool(np.array_equal(ho.view("tmpl", np.uint64)[:n][m],
+                                                   db.out_numpy("tmpl", np.uint64, n=n)[m]))
+            res["tmpl_arena"] = bool(used == int(ho.used[0]) and
+                                     np.array_equal(ho.bufs["tmpl_arena"][:used], db.out_numpy("tmpl_arena", n=used)))
     if stages & native.STAGE_SIZE:
         A = gen.cols.n_attrsets
         # the device counters were ADDED to by every timed and warm-up call
@@ -322,6 +334,10 @@ def main():
     ap.add_argument("--spans", type=int, default=0, help="override the workload's span count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    # refs (OSE_STAGE_TEMPLATE_REFS): the templates stay where the GPU assembled
+    # them and the device-resident consumer follows the refs; packed: the
+    # compact arena a host copy needs (one more pass over the template bytes)
+    ap.add_argument("--tmpl-form", default="refs", choices=("refs", "packed"))
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -341,6 +357,9 @@ def main():
 
     wl = WORKLOADS[args.workload]
     stages = _stages(wl)
+    tform = native.STAGE_TEMPLATE_REFS if args.tmpl_form == "refs" else 0
+    if stages & native.STAGE_TEMPLATE:
+        stages |= tform
     cfg = _cfg(wl)
     share, nproc, model = cpu_share()
     gen_threads = max(1, min(16, share))
@@ -385,7 +404,7 @@ def main():
         def rank_step(r):
             rnd = native.Rand(0x5EED, 0.0)
             sides[r].wait_stream(mains[r])
-            engs[r].process_device(dbs[r], native.STAGE_TEMPLATE, native.GROUP_TRACE_ID, seed=0x5EED,
+            engs[r].process_device(dbs[r], native.STAGE_TEMPLATE | tform, native.GROUP_TRACE_ID, seed=0x5EED,
                                    stream=sides[r].cuda_stream)
             native.check(L.osehost_exchange_sample_local(engs[r].h, C.byref(dbs[r].cols), C.byref(dbs[r].outs), grp,
                                                          r, C.byref(rnd), C.c_void_p(mains[r].cuda_stream), stats[r]))
@@ -437,8 +456,8 @@ def main():
             # overlapped with the URL stage); SIZE | APPLY_KEEP joins both
             side = torch.cuda.Stream()
             side_h = side.cuda_stream
-            tmpl_st = local_st & native.STAGE_TEMPLATE
-            rest_st = local_st & ~native.STAGE_TEMPLATE
+            tmpl_st = local_st & (native.STAGE_TEMPLATE | native.STAGE_TEMPLATE_REFS)
+            rest_st = local_st & ~(native.STAGE_TEMPLATE | native.STAGE_TEMPLATE_REFS)
 
             def step():
                 if tmpl_st:
@@ -547,6 +566,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded generator, SURVEY.md §8d mix)",
         "config": {"workload": wl["metric_config"], "spans_per_gpu": n_units, "spans_total": int(total_units),
+                   "template_form": args.tmpl_form if stages & native.STAGE_TEMPLATE else None,
                    "seed": wl["seed"], "processors": list(cfg.keys()),
                    "parallelism": (f"dp{world}: trace-id all-to-all (RCCL) of sampling partials, local templating/size"
                                    if world > 1 and stages & native.STAGE_SAMPLE else

@@ -258,6 +258,8 @@ int ose_process(ose_engine* eng, ose_batch* bb, uint32_t stage_mask, uint32_t gr
   Engine* e = reinterpret_cast<Engine*>(eng);
   Batch* b = reinterpret_cast<Batch*>(bb);
   if (!b->fits(b->cols_h)) return fail(OSE_EINVAL, "batch dimensions exceed the acquired capacity");
+  if (stage_mask & OSE_STAGE_TEMPLATE_REFS)
+    return fail(OSE_EINVAL, "OSE_STAGE_TEMPLATE_REFS is for ose_process_device (ose_process copies the packed arena)");
   if (int brc = bind_device(e)) return brc;
   hipStream_t st = e->take_stream();
   if (!st) return fail(OSE_EDEVICE, "hipStreamCreate failed");

@@ -328,13 +328,20 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st);
 
+// OSE_STAGE_TEMPLATE_REFS: tmpl_arena [0, base) holds the wave regions of the
+// assembled images (the scratch the packed form keeps in the workspace, at
+// most 7/8 of the capacity), the slow groups' templates are packed after it
+static uint64_t refs_base(uint64_t n, uint64_t arena_bytes, uint64_t cap) {
+  return std::min<uint64_t>(url_scratch_bytes(n, arena_bytes), cap - cap / 8) & ~15ull;
+}
+
 // ws_off: the URL scratch starts this many bytes into the workspace (past a
 // SAMPLE stage's scratch whose slow path is still to be queued).  front: only
 // plan, plan_slow and scan are queued, and the arguments of the rest go to
 // *front (run_url_back queues url_copy, fused with odigostrafficmetrics'
 // spans pass when front->fuse_size is set, and url_emit_slow).
 int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws, size_t ws_off = 0,
-            UrlKernelArgs* front = nullptr) {
+            UrlKernelArgs* front = nullptr, bool refs = false) {
   if (!e->has_url) return fail(OSE_EINVAL, "odigosurltemplate is not configured on this engine");
   if (!c->url_flags || !c->kind || !c->path || !c->arena || !o->url_out || !o->tmpl || !o->tmpl_arena)
     return fail(OSE_EINVAL, "TEMPLATE stage needs url_flags, kind, path, arena, url_out, tmpl, tmpl_arena");
@@ -357,8 +364,8 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   const size_t off_unpl = off_slow + 4 * (size_t)groups;
   const size_t off_dbg = align_up(off_unpl + 4 * (size_t)groups, 256);
   const size_t off_scr = off_dbg + 256;
-  const size_t scr_bytes = url_scratch_bytes(n, c->arena_bytes);
-  const size_t need = off_scr + scr_bytes;
+  const size_t scr_bytes = refs ? refs_base(n, c->arena_bytes, o->tmpl_arena_cap) : url_scratch_bytes(n, c->arena_bytes);
+  const size_t need = off_scr + (refs ? 0 : scr_bytes);   // refs: the images go to tmpl_arena itself
   if (need > url_workspace_bytes(n, c->arena_bytes))
     return fail(OSE_EINVAL, "internal: URL workspace layout exceeds its bound");
   int rc = ws->reserve(ws_off + need);
@@ -386,6 +393,13 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.group_base = reinterpret_cast<uint64_t*>(base + off_gbase);
   a.group_scr = reinterpret_cast<uint64_t*>(base + off_gscr);
   a.scratch = base + off_scr;
+  if (refs) {
+    a.refs = 1;
+    a.scratch = o->tmpl_arena;
+    a.slow_base = scr_bytes;
+    a.out_arena = o->tmpl_arena + scr_bytes;
+    a.out_cap = o->tmpl_arena_cap - scr_bytes;
+  }
   a.n_scan_tiles = scan_tiles;
   a.scan_counter = reinterpret_cast<uint32_t*>(base);
   a.scan_status = reinterpret_cast<uint64_t*>(base + off_sst);
@@ -461,8 +475,10 @@ int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st) {
 int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
                const ose_rand* rnd, hipStream_t st) {
   if (!c || !o) return fail(OSE_EINVAL, "columns and outputs are required");
-  if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE | OSE_STAGE_APPLY_KEEP))
+  if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE | OSE_STAGE_APPLY_KEEP | OSE_STAGE_TEMPLATE_REFS))
     return fail(OSE_EINVAL, "unknown stage bit");
+  if ((mask & OSE_STAGE_TEMPLATE_REFS) && !(mask & OSE_STAGE_TEMPLATE))
+    return fail(OSE_EINVAL, "OSE_STAGE_TEMPLATE_REFS needs OSE_STAGE_TEMPLATE");
   if ((mask & OSE_STAGE_APPLY_KEEP) && (mask & OSE_STAGE_SAMPLE))
     return fail(OSE_EINVAL, "OSE_STAGE_APPLY_KEEP and OSE_STAGE_SAMPLE exclude each other");
   // SAMPLE + TEMPLATE by trace id: the URL stage reads nothing SAMPLE writes,
@@ -511,7 +527,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   }
   UrlKernelArgs ua{};
   const bool tmpl = !rc && (mask & OSE_STAGE_TEMPLATE);
-  if (tmpl) rc = run_url(e, c, o, st, ws, url_off, &ua);
+  if (tmpl) rc = run_url(e, c, o, st, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0);
   if (sample_tail) {
     const int trc = sample_tail();   // always drained: the host event wait must not be skipped
     if (!rc) rc = trc;
@@ -665,6 +681,11 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   if (!rc && e->attr_n_dev) rc = ws->reserve_attr(n_spans);
   e->release_ws(ws, nullptr);
   return rc;
+}
+
+uint64_t ose_template_refs_base(const ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes, uint64_t tmpl_arena_cap) {
+  (void)eng;
+  return refs_base(n_spans, arena_bytes, tmpl_arena_cap);
 }
 
 int ose_process_device(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, uint32_t stage_mask,

@@ -1598,7 +1598,8 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
   __syncthreads();
   const uint32_t tile = tile_s;
   const uint64_t k = (uint64_t)tile * kScanThreads + tid;
-  const uint64_t v = k < a.n_groups ? a.group_sum[k] : 0;
+  // refs mode: only the slow groups take room past slow_base
+  const uint64_t v = k < a.n_groups && !(a.refs && a.group_scr[k] != ~0ull) ? a.group_sum[k] : 0;
   uint64_t incl = v;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -1619,7 +1620,7 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
     if (lane == 0) {
       prefix = pfx;
       if (tile == a.n_scan_tiles - 1) {
-        if (a.used) *a.used = pfx + total;
+        if (a.used) *a.used = a.slow_base + pfx + total;
         if (pfx + total > a.out_cap) atomicOr(a.error, 2u);
       }
     }
@@ -1691,7 +1692,7 @@ struct CopyJob {
 };
 __device__ __forceinline__ CopyJob copy_job(const UrlKernelArgs& a, const CopyCols& c) {
   CopyJob j{};
-  j.on = c.so != ~0ull && c.gsum != 0 && c.base + c.gsum <= a.out_cap;
+  j.on = !a.refs && c.so != ~0ull && c.gsum != 0 && c.base + c.gsum <= a.out_cap;
   if (!j.on) return j;
   j.src = reinterpret_cast<const uint4*>(a.scratch + c.so);
   j.shift = (uint32_t)(c.base & 3);
@@ -1736,7 +1737,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize 
     const uint32_t la = wave_excl_scan(A.len, &unused);
     const CopyJob ja = copy_job(a, A);
     const uint4 va = copy_load(ja, 0);
-    if (ia < a.n_spans) a.tmpl[ia] = ose_strref{(uint32_t)(A.base + la), A.len};
+    if (ia < a.n_spans) {
+      // refs mode: a fast group's template stays in its scratch image
+      const uint64_t at = a.refs ? (A.so != ~0ull ? A.so : a.slow_base + A.base) : A.base;
+      a.tmpl[ia] = ose_strref{(uint32_t)(at + la), A.len};
+    }
     if (kSize && sz_on) {
       x.tl = A.len;
       kept += sizedev::size_span_finish(a.sz, x);
@@ -1774,7 +1779,11 @@ __global__ __launch_bounds__(kThreads) void url_copy_pair_kernel(UrlKernelArgs a
     const uint64_t ia = (uint64_t)g * kWave + lane, ib = (uint64_t)gb * kWave + lane;
     const CopyJob ja = copy_job(a, A), jb = copy_job(a, B);
     const uint4 va = copy_load(ja, 0), vb = copy_load(jb, 0);
-    if (ia < a.n_spans) a.tmpl[ia] = ose_strref{(uint32_t)(A.base + la), A.len};
+    if (ia < a.n_spans) {
+      // refs mode: a fast group's template stays in its scratch image
+      const uint64_t at = a.refs ? (A.so != ~0ull ? A.so : a.slow_base + A.base) : A.base;
+      a.tmpl[ia] = ose_strref{(uint32_t)(at + la), A.len};
+    }
     if (hb && ib < a.n_spans) a.tmpl[ib] = ose_strref{(uint32_t)(B.base + lb), B.len};
     uint32_t carry = 0;
     if (ja.on) copy_rest(ja, va, carry);
@@ -2022,7 +2031,7 @@ void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
   const uint32_t blocks = url_copy_blocks(a.n_groups);
   if (a.fuse_size)
     hipLaunchKernelGGL(url_copy_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, a);
-  else if (pair)
+  else if (pair && !a.refs)
     hipLaunchKernelGGL(url_copy_pair_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
   else
     hipLaunchKernelGGL(url_copy_kernel<false>, dim3(blocks), dim3(kThreads), 0, st, a);

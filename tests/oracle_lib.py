@@ -9,6 +9,8 @@ from odigos_amd import native
 
 import os
 
+import numpy as np
+
 # OSE_ORACLE_LIB: a host-tuned build of the same sources (bench.py builds one
 # with -march=native on the GPU box for the CPU baseline)
 ORACLE_PATH = Path(os.environ.get("OSE_ORACLE_LIB") or
@@ -190,3 +192,19 @@ def size_process(cols, res_outs, stages: int, group_mode: int, outs, inverse: in
     holds the earlier stages' results (keep / trace_keep / url_out / tmpl)."""
     return lib().orc_size_process_mt(C.byref(cols), C.byref(res_outs), stages, group_mode, C.byref(outs), inverse,
                                      ratio, traffic_u, nthreads)
+
+
+def span_template_bytes(refs: np.ndarray, arena: np.ndarray, mask: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Per-span template parity (OSE_STAGE_TEMPLATE_REFS): the bytes each
+    masked span's ref {off, len} names, concatenated in span order, and the
+    lengths.  Two arenas hold the same templates iff both results match,
+    whatever the layout (packed or sparse)."""
+    r = refs.reshape(-1, 2)[mask].astype(np.int64)
+    lens = r[:, 1]
+    total = int(lens.sum())
+    if total == 0:
+        return np.zeros(0, dtype=np.uint8), lens
+    starts = np.cumsum(lens) - lens
+    idx = np.repeat(r[:, 0] - starts, lens) + np.arange(total, dtype=np.int64)
+    assert idx.max() < arena.size, "a template ref points past the arena"
+    return arena[idx], lens
