@@ -97,14 +97,16 @@ extern "C" {
  * as if SAMPLE had run in this call with group_mode OSE_GROUP_TRACE_ID.    */
 #define OSE_STAGE_APPLY_KEEP 0x8u
 /* With OSE_STAGE_TEMPLATE, ose_process_device only: the templates stay where
- * the GPU assembled them instead of being packed.  tmpl[i] still refers into
- * tmpl_arena and its bytes are exactly the packed form's, but the arena is
- * sparse: unused bytes lie between templates, and *tmpl_arena_used is the
- * end of the highest range written (the templates of groups that took the
- * per-span writer lie past ose_template_refs_base(), packed).  It saves a
+ * the GPU assembled them (64-span groups, in the order the GPU finished
+ * them) instead of being packed in span order.  tmpl[i] still refers into
+ * tmpl_arena and its bytes are exactly the packed form's, but the arena has
+ * gaps: up to 15 bytes after each group and, per assembling wave, the unused
+ * tail of its last space chunk (at most tmpl_arena_cap / 8 in all);
+ * *tmpl_arena_used is the end of the highest range written.  It saves a
  * read and a write of every template byte when the consumer follows the
- * refs on the device (ose_otlp_encode does) instead of copying the arena
- * to the host.  Overflow (device_status bit 2) as in the packed form.      */
+ * refs on the device instead of copying the arena to the host.  Overflow
+ * (device_status bit 2, *tmpl_arena_used = the bytes needed) as in the
+ * packed form.                                                              */
 #define OSE_STAGE_TEMPLATE_REFS 0x10u
 
 /* ---- grouping of spans into "traces" for odigossampling --------------
@@ -330,15 +332,6 @@ int ose_process_device(ose_engine* eng, const ose_columns* cols,
  * ose_columns.arena_bytes the calls will pass (the TEMPLATE stage's scratch
  * is sized from it).                                                        */
 int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes);
-
-/* OSE_STAGE_TEMPLATE_REFS layout for a call on n_spans spans whose columns
- * give arena_bytes, into a tmpl_arena of tmpl_arena_cap bytes: tmpl_arena
- * [0, base) holds the assembled group images (per-wave regions), the
- * per-span writer's templates are packed from base on.  A capacity that
- * leaves the images no room is not an error (their groups take the per-span
- * writer); one that leaves the packed part too little is device_status bit 2. */
-uint64_t ose_template_refs_base(const ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes,
-                                uint64_t tmpl_arena_cap);
 
 /* Per-kernel device time, measured with hipEvents recorded on the stream
  * each kernel is launched on (diagnostics and bench.py; off by default).

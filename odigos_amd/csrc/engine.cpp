@@ -328,13 +328,6 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st);
 
-// OSE_STAGE_TEMPLATE_REFS: tmpl_arena [0, base) holds the wave regions of the
-// assembled images (the scratch the packed form keeps in the workspace, at
-// most 7/8 of the capacity), the slow groups' templates are packed after it
-static uint64_t refs_base(uint64_t n, uint64_t arena_bytes, uint64_t cap) {
-  return std::min<uint64_t>(url_scratch_bytes(n, arena_bytes), cap - cap / 8) & ~15ull;
-}
-
 // ws_off: the URL scratch starts this many bytes into the workspace (past a
 // SAMPLE stage's scratch whose slow path is still to be queued).  front: only
 // plan, plan_slow and scan are queued, and the arguments of the rest go to
@@ -351,11 +344,11 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   if (o->tmpl_arena_cap > 0xFFFFFFFFull) return fail(OSE_ERANGE, "tmpl_arena_cap exceeds the 32-bit offset range");
   uint64_t n = c->n_spans;
   const uint32_t groups = (uint32_t)((n + kUrlGroup - 1) / kUrlGroup);
-  // workspace: [0,16) scan counter, slow count, error, unplanned count | scan status 8t (both zeroed by
-  // one memset) | plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | group_scr 8g |
+  // workspace: [0,16) scan counter, slow count, error, unplanned count | [16,24) refs bump | scan status 8t
+  // (all zeroed by one memset) | plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | group_scr 8g |
   // slow groups 4g | unplanned groups 4g | dbg | scratch (the assembled group images)
   const uint32_t scan_tiles = (groups + kUrlScanTile - 1) / kUrlScanTile;
-  const size_t off_sst = 16, zero_bytes = off_sst + 8 * (size_t)scan_tiles;
+  const size_t off_bump = 16, off_sst = 24, zero_bytes = off_sst + 8 * (size_t)scan_tiles;
   const size_t off_len = align_up(zero_bytes, 256), off_meta = off_len + 4 * n;
   const size_t off_code = align_up(off_meta + 4 * n, 8);
   const size_t off_gsum = off_code + 8 * n, off_gbase = off_gsum + 8 * (size_t)groups;
@@ -364,7 +357,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   const size_t off_unpl = off_slow + 4 * (size_t)groups;
   const size_t off_dbg = align_up(off_unpl + 4 * (size_t)groups, 256);
   const size_t off_scr = off_dbg + 256;
-  const size_t scr_bytes = refs ? refs_base(n, c->arena_bytes, o->tmpl_arena_cap) : url_scratch_bytes(n, c->arena_bytes);
+  const size_t scr_bytes = url_scratch_bytes(n, c->arena_bytes);
   const size_t need = off_scr + (refs ? 0 : scr_bytes);   // refs: the images go to tmpl_arena itself
   if (need > url_workspace_bytes(n, c->arena_bytes))
     return fail(OSE_EINVAL, "internal: URL workspace layout exceeds its bound");
@@ -396,9 +389,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   if (refs) {
     a.refs = 1;
     a.scratch = o->tmpl_arena;
-    a.slow_base = scr_bytes;
-    a.out_arena = o->tmpl_arena + scr_bytes;
-    a.out_cap = o->tmpl_arena_cap - scr_bytes;
+    a.bump = reinterpret_cast<uint64_t*>(base + off_bump);
   }
   a.n_scan_tiles = scan_tiles;
   a.scan_counter = reinterpret_cast<uint32_t*>(base);
@@ -412,6 +403,10 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.used = o->tmpl_arena_used;
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
   a.scr_region = (scr_bytes / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
+  // refs: image chunks of about an eighth of the arena over the plan waves
+  // (4 KiB .. 256 KiB): a wave leaves at most one chunk's tail unused
+  a.refs_chunk = std::min<uint64_t>(256 << 10, std::max<uint64_t>(4096, o->tmpl_arena_cap / 8 /
+                                                                   std::max<uint32_t>(1, url_plan_waves(a)))) & ~15ull;
   if (front) *front = a;
   if (n == 0) {
     if (o->tmpl_arena_used) HIP_TRY(hipMemsetAsync(o->tmpl_arena_used, 0, 8, st));
@@ -681,11 +676,6 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   if (!rc && e->attr_n_dev) rc = ws->reserve_attr(n_spans);
   e->release_ws(ws, nullptr);
   return rc;
-}
-
-uint64_t ose_template_refs_base(const ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes, uint64_t tmpl_arena_cap) {
-  (void)eng;
-  return refs_base(n_spans, arena_bytes, tmpl_arena_cap);
 }
 
 int ose_process_device(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, uint32_t stage_mask,

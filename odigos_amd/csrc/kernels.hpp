@@ -87,12 +87,14 @@ struct UrlKernelArgs {
   uint32_t* unplanned_count;   // groups the plan kernel left to url_plan_slow_kernel (zeroed before launch)
   uint32_t* unplanned;         // [n_groups]
   uint32_t general;            // user rules or custom ids configured (selects the general kernel instances)
-  // OSE_STAGE_TEMPLATE_REFS: scratch is the caller's tmpl_arena, the fast
-  // groups' images stay where url_plan_kernel wrote them (their refs point
-  // there, url_copy_kernel copies nothing); out_arena / out_cap / the scan
-  // cover only the slow groups, written from slow_base on
+  // OSE_STAGE_TEMPLATE_REFS: scratch is the caller's tmpl_arena (== out_arena),
+  // the fast groups' images stay where url_plan_kernel wrote them (their refs
+  // point there, url_copy_kernel copies nothing).  A plan wave takes its
+  // image space in chunks of refs_chunk bytes from *bump (zeroed before the
+  // launch); the scan places the slow groups from the final *bump on.
   uint32_t refs;
-  uint64_t slow_base;
+  uint64_t* bump;
+  uint64_t refs_chunk;
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
   uint64_t* dbg;               // diagnostics only (ablate & 512): per-section clock sums
   // odigostrafficmetrics' spans pass fused into url_copy_kernel (TEMPLATE and

@@ -1434,8 +1434,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
   const bool fused_cfg = sm.bn.ok && !(a.ablate & 2);
   const lds_u8* L = (const lds_u8*)(void*)&sm;
   const uint32_t bn_src = (uint32_t)((uint8_t*)sm.bn.b - (uint8_t*)&sm);
-  const uint64_t region = (uint64_t)wave_first_group() * a.scr_region;   // this wave's scratch
-  uint64_t scr_used = 0;
+  // this wave's scratch: a region of the workspace, or (refs) chunks of the
+  // output arena taken as the wave goes
+  uint64_t region = a.refs ? 0 : (uint64_t)wave_first_group() * a.scr_region;
+  uint64_t scr_used = 0, scr_end = a.refs ? 0 : a.scr_region;
+  bool exhausted = false;   // refs: a chunk went past the arena, the wave takes no more
 
   // prologue: columns of groups g and g + stride, bytes of group g
   PlanCols cur = plan_cols(a, (uint64_t)g * kWave + lane);
@@ -1524,8 +1527,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     // wave-uniform: the group is assembled here unless a user rule matched, a
     // name id lies outside the braced table, the list planner gave up, or the
     // image does not fit LDS or the wave's scratch region
-    const bool fast = fused_cfg && listed && __ballot(p.mode == M_RULE || big) == 0 && sum <= kImgCap &&
-                      scr_used + need <= a.scr_region;
+    bool fast = fused_cfg && listed && __ballot(p.mode == M_RULE || big) == 0 && sum <= kImgCap;
+    if (fast && scr_used + need > scr_end) {
+      if (a.refs && !exhausted) {   // a new chunk (the rest of the current one is left unused)
+        const uint64_t csz = max(a.refs_chunk, need);
+        uint64_t at = 0;
+        if (lane == 0) at = atomicAdd((unsigned long long*)a.bump, (unsigned long long)csz);
+        at = (uint64_t)lane_value((uint32_t)at, 0) | ((uint64_t)lane_value((uint32_t)(at >> 32), 0) << 32);
+        if (at + csz <= a.out_cap) {
+          region = at;
+          scr_used = 0;
+          scr_end = csz;
+        } else {
+          fast = false;   // the arena is full: the scan flags the overflow
+          exhausted = true;
+        }
+      } else {
+        fast = false;
+      }
+    }
     if (i < a.n_spans) {
       a.plan_len[i] = p.len;
       a.url_out[i] = (uint8_t)oflags;
@@ -1598,8 +1618,10 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
   __syncthreads();
   const uint32_t tile = tile_s;
   const uint64_t k = (uint64_t)tile * kScanThreads + tid;
-  // refs mode: only the slow groups take room past slow_base
+  // refs mode: only the slow groups are placed by the scan, after the plan
+  // waves' image chunks
   const uint64_t v = k < a.n_groups && !(a.refs && a.group_scr[k] != ~0ull) ? a.group_sum[k] : 0;
+  const uint64_t sb = a.refs ? *a.bump : 0;
   uint64_t incl = v;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -1620,13 +1642,13 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
     if (lane == 0) {
       prefix = pfx;
       if (tile == a.n_scan_tiles - 1) {
-        if (a.used) *a.used = a.slow_base + pfx + total;
-        if (pfx + total > a.out_cap) atomicOr(a.error, 2u);
+        if (a.used) *a.used = sb + pfx + total;
+        if (sb + pfx + total > a.out_cap) atomicOr(a.error, 2u);
       }
     }
   }
   __syncthreads();
-  if (k < a.n_groups) a.group_base[k] = prefix + wbase + incl - v;
+  if (k < a.n_groups) a.group_base[k] = sb + prefix + wbase + incl - v;
 }
 
 // ---------------------------------------------------------------------------
@@ -1739,7 +1761,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize 
     const uint4 va = copy_load(ja, 0);
     if (ia < a.n_spans) {
       // refs mode: a fast group's template stays in its scratch image
-      const uint64_t at = a.refs ? (A.so != ~0ull ? A.so : a.slow_base + A.base) : A.base;
+      const uint64_t at = a.refs && A.so != ~0ull ? A.so : A.base;
       a.tmpl[ia] = ose_strref{(uint32_t)(at + la), A.len};
     }
     if (kSize && sz_on) {
@@ -1781,7 +1803,7 @@ __global__ __launch_bounds__(kThreads) void url_copy_pair_kernel(UrlKernelArgs a
     const uint4 va = copy_load(ja, 0), vb = copy_load(jb, 0);
     if (ia < a.n_spans) {
       // refs mode: a fast group's template stays in its scratch image
-      const uint64_t at = a.refs ? (A.so != ~0ull ? A.so : a.slow_base + A.base) : A.base;
+      const uint64_t at = a.refs && A.so != ~0ull ? A.so : A.base;
       a.tmpl[ia] = ose_strref{(uint32_t)(at + la), A.len};
     }
     if (hb && ib < a.n_spans) a.tmpl[ib] = ose_strref{(uint32_t)(B.base + lb), B.len};

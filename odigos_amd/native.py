@@ -159,7 +159,6 @@ def lib() -> C.CDLL:
         "ose_process_device": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(Outputs), C.c_uint32, C.c_uint32,
                                          C.POINTER(Rand), _p]),
         "ose_reserve": (C.c_int, [_p, C.c_uint64, C.c_uint64]),
-        "ose_template_refs_base": (C.c_uint64, [_p, C.c_uint64, C.c_uint64, C.c_uint64]),
         "ose_device_info": (C.c_int, [C.c_char_p, C.c_size_t]),
         "ose_shard_owner": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint32]),
         "ose_shard_pack": (C.c_int, [_p, C.POINTER(Columns), C.c_uint32, _p, _p, _p, _p]),
