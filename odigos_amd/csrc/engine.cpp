@@ -403,10 +403,10 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.used = o->tmpl_arena_used;
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
   a.scr_region = (scr_bytes / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
-  // refs: image chunks of about an eighth of the arena over the plan waves
-  // (4 KiB .. 256 KiB): a wave leaves at most one chunk's tail unused
-  a.refs_chunk = std::min<uint64_t>(256 << 10, std::max<uint64_t>(4096, o->tmpl_arena_cap / 8 /
-                                                                   std::max<uint32_t>(1, url_plan_waves(a)))) & ~15ull;
+  // refs: image chunks of an eighth of the arena over the plan waves (at most
+  // 256 KiB; a group larger than a chunk takes exactly its size): a wave
+  // leaves at most one chunk's tail unused
+  a.refs_chunk = std::min<uint64_t>(256 << 10, o->tmpl_arena_cap / 8 / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
   if (front) *front = a;
   if (n == 0) {
     if (o->tmpl_arena_used) HIP_TRY(hipMemsetAsync(o->tmpl_arena_used, 0, 8, st));

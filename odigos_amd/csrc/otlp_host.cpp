@@ -270,6 +270,8 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
     if (twt != 2 || !top.bytes(ro, rl)) { top.fail(); break; }
     *end = top.i;
     if (gpu_scopes && top.i + 2 < n) __builtin_prefetch(p + top.i, 0, 3);   // the next record's header
+    static const int chain_only = getenv("OSE_WALK_CHAIN_ONLY") ? atoi(getenv("OSE_WALK_CHAIN_ONLY")) : 0;   // diagnostics
+    if (chain_only == 1) continue;
     PbReader rr(p + ro, rl);
     resf.clear();
     scopes.clear();
@@ -288,6 +290,7 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
       }
     }
     if (!rr.ok) { c.err = "OTLP protobuf: malformed ResourceSpans"; return; }
+    if (chain_only == 2) continue;
     if (scopes.empty()) scopes.swap(deprecated);
     // the resource's columns (cached by its message bytes)
     CachedRes cr{};
