@@ -159,6 +159,8 @@ Engine::~Engine() {
     if (w->dev) (void)hipFree(w->dev);
     if (w->table) (void)hipFree(w->table);
     if (w->fp_table) (void)hipFree(w->fp_table);
+    if (w->dup_bkt) (void)hipFree(w->dup_bkt);
+    if (w->dup_bkt_count) (void)hipFree(w->dup_bkt_count);
     if (w->runs) (void)hipFree(w->runs);
     if (w->run_count) (void)hipFree(w->run_count);
     if (w->attr_bits) (void)hipFree(w->attr_bits);

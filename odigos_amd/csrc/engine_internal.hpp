@@ -65,6 +65,9 @@ struct Workspace {
   uint64_t table_slots_cap = 0;
   uint64_t* fp_table = nullptr;   // fast-path fingerprint cells
   uint64_t fp_slots_cap = 0;
+  uint64_t* dup_bkt = nullptr;         // bucketed duplicate detection (TraceKernelArgs::dup_bkt)
+  uint32_t* dup_bkt_count = nullptr;
+  uint32_t dup_bkt_bits = 0;
   uint32_t epoch = 0;
   int reserve_table(uint64_t n_spans);
   uint32_t* runs = nullptr;        // run-list path: kMaxRuns run heads per table slot

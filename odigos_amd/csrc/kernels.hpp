@@ -179,6 +179,12 @@ struct TraceKernelArgs {
   uint64_t* fp_table;          // fingerprint cells (fast-path duplicate detection)
   uint64_t fp_mask;
   uint32_t* dup;              // set by the fast path when a trace_id spans several runs
+  // bucketed duplicate detection (used instead of fp_table when dup_bkt is
+  // set): a run head appends its 64-bit fingerprint to bucket fp >> (64 -
+  // dup_bkt_bits); trace_dup_check_kernel looks for a repeat per bucket in LDS
+  uint32_t* dup_bkt_count;    // [1 << dup_bkt_bits], zeroed before the launch
+  uint64_t* dup_bkt;          // [(1 << dup_bkt_bits) * kDupBucketCap]
+  uint32_t dup_bkt_bits;
   const uint32_t* perm;       // kTracePerm: position -> span
   const uint32_t* key;        // kTracePerm: span -> canonical trace (first run-head position)
   uint32_t* error;            // bit0 spin timeout, bit2 trace table full
@@ -208,6 +214,8 @@ constexpr uint32_t kMaxFoldSlots = 8;     // latency services per trace one lane
 constexpr uint32_t kWinPerWave = 16;   // tools/gpu_wpw.sh: C5 0.97 -> 0.83 ms, C3 2.03 -> 1.99 ms, C4 unchanged
 constexpr uint32_t kLongSteps = 4;   // tools/gpu_long_iter.sh: C5 16 -> 4 steps 2.75 -> 2.13 ms, C3 unchanged
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
+constexpr uint32_t kDupBucketCap = 1024;   // fingerprints per bucket (more: the exact path decides)
+void launch_trace_dup_check(const TraceKernelArgs& a, hipStream_t st);
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs = 0);
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st);   // slow path, gated on *dup
 void launch_trace_runs(const TraceKernelArgs& a, hipStream_t st);           // run-list path (gated on *dup)
@@ -409,6 +417,58 @@ struct OtlpScopeArgs {
   const uint64_t* host_refs;
   const uint64_t* host_at;      // [n_scopes] offset into host_refs (host-walked scopes)
 };
+// ResourceSpans on the GPU (the host walks only the TracesData chain of
+// ResourceSpans records): each record's fields, its Resource's columns from
+// the engine's device table of resources seen before (keyed by the Resource
+// message bytes: FNV-1a 64), its ScopeSpans listed for the scope passes.
+struct ResSlotDev {          // 48 B; ready != 0: filled
+  uint64_t h;
+  uint32_t koff, klen;       // key bytes in the table's key arena
+  uint32_t svc, svc_str, set, rpart;
+  uint64_t attr_res;
+  uint32_t ok, ready;
+};
+constexpr uint32_t kResSlots = 1u << 17;
+constexpr uint32_t kResKeyBytes = 16u << 20;
+// FNV-1a over the bytes (the host fills the table with the same function)
+inline __host__ __device__ uint64_t res_key_hash_step(uint64_t h, uint32_t b) { return (h ^ b) * 0x100000001B3ull; }
+constexpr uint64_t kResHashSeed = 0xCBF29CE484222325ull;
+struct OtlpResArgs {
+  const uint8_t* pb;
+  uint64_t n_res;
+  const uint64_t* res_ref;     // ResourceSpans payload off | len << 32
+  uint32_t* flags;             // 1: resource columns from the host, 2: malformed, 4: scopes are field 1000
+  uint32_t* nscope;            // ScopeSpans per resource (field 2, or field 1000 when there is no field 2)
+  uint32_t* schema_len;        // ResourceSpans.schema_url length (last occurrence)
+  uint32_t* any_bad;           // [1] OR of flags & 2
+  const uint32_t* scope0;      // pass 2: exclusive scan of nscope
+  uint64_t* scope_ref;
+  uint32_t* scope_res;
+  // the Resource's columns
+  const ResSlotDev* table;
+  const uint8_t* keys;
+  uint32_t* res_svc;
+  uint32_t* res_svc_str;
+  uint32_t* res_set;           // the resource cache's attribute-set id (batch ids after compaction)
+  uint32_t* res_size;
+  uint8_t* res_ok;
+  uint64_t* attr_res;
+  uint32_t* miss_count;        // [1]
+  uint32_t* miss_list;         // [n_res]
+};
+void launch_otlp_res_fields(const OtlpResArgs& a, hipStream_t st);
+void launch_otlp_res_scopes(const OtlpResArgs& a, hipStream_t st);
+// the host's columns of the missed resources: fix k = {row, svc, svc_str, set, rpart, ok, attr_res}
+struct OtlpResFix {
+  uint32_t row, svc, svc_str, set, rpart, ok;
+  uint64_t attr_res;
+};
+void launch_otlp_res_fix(const OtlpResArgs& a, const OtlpResFix* fix, uint32_t n, hipStream_t st);
+// attribute-set ids of the cache -> the batch's (ascending cache id): used
+// flags, then (after an exclusive scan of them) the ids and the list
+void launch_otlp_set_mark(const uint32_t* res_set, uint64_t n_res, uint32_t* used, hipStream_t st);
+void launch_otlp_set_apply(uint32_t* res_set, uint64_t n_res, const uint32_t* used, const uint32_t* local,
+                           uint32_t n_sets, uint32_t* list, hipStream_t st);
 void launch_otlp_scope_count(const OtlpScopeArgs& a, hipStream_t st);
 void launch_otlp_scope_spans(const OtlpScopeArgs& a, hipStream_t st);
 

@@ -88,6 +88,76 @@ struct ResCache {
 
 // The engine's view for the ingest: the columniser context and the key
 // table the GPU decoder matches (built once per engine).
+// The device copy of the resource cache (ResCache) the GPU ResourceSpans
+// pass looks resources up in (otlp_res_fields_kernel): open addressing on
+// the Resource bytes' FNV-1a hash, up to 64 probes, never deleted.  A host
+// mirror takes the inserts; sync() copies what changed.  Lookups in flight
+// hold the lock shared, updates unique.
+struct DevResTable {
+  std::shared_mutex mu;
+  ResSlotDev* d_slots = nullptr;
+  uint8_t* d_keys = nullptr;
+  std::vector<ResSlotDev> slots;
+  std::vector<uint8_t> keys;
+  std::vector<uint32_t> changed;   // slots filled since the last sync
+  size_t keys_synced = 0;
+  uint32_t n = 0;
+  int ensure() {   // under the unique lock
+    if (d_slots) return 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_slots), sizeof(ResSlotDev) * kResSlots));
+    HIP_TRY(hipMemset(d_slots, 0, sizeof(ResSlotDev) * kResSlots));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_keys), kResKeyBytes));
+    slots.assign(kResSlots, ResSlotDev{});
+    return 0;
+  }
+  void insert(const uint8_t* key, uint32_t len, const CachedRes& cr) {   // under the unique lock
+    if (!d_slots || n >= kResSlots / 2 || keys.size() + len > kResKeyBytes) return;
+    uint64_t h = kResHashSeed;
+    for (uint32_t q = 0; q < len; q++) h = res_key_hash_step(h, key[q]);
+    uint32_t slot = (uint32_t)h & (kResSlots - 1);
+    for (int probe = 0; probe < 64; probe++, slot = (slot + 1) & (kResSlots - 1)) {
+      ResSlotDev& e = slots[slot];
+      if (!e.ready) {
+        e.h = h;
+        e.koff = (uint32_t)keys.size();
+        e.klen = len;
+        keys.insert(keys.end(), key, key + len);
+        e.svc = cr.svc;
+        e.svc_str = cr.svc_str;
+        e.set = cr.set;
+        e.rpart = cr.rpart;
+        e.attr_res = cr.attr_res;
+        e.ok = cr.ok;
+        e.ready = 1;
+        changed.push_back(slot);
+        n++;
+        return;
+      }
+      if (e.h == h && e.klen == len && std::memcmp(keys.data() + e.koff, key, len) == 0) return;
+    }
+  }
+  int sync(hipStream_t st) {   // under the unique lock
+    if (changed.empty()) return 0;
+    if (keys.size() > keys_synced)
+      HIP_TRY(hipMemcpyAsync(d_keys + keys_synced, keys.data() + keys_synced, keys.size() - keys_synced,
+                             hipMemcpyHostToDevice, st));
+    if (changed.size() > 256) {
+      HIP_TRY(hipMemcpyAsync(d_slots, slots.data(), sizeof(ResSlotDev) * kResSlots, hipMemcpyHostToDevice, st));
+    } else {
+      for (uint32_t k : changed)
+        HIP_TRY(hipMemcpyAsync(d_slots + k, &slots[k], sizeof(ResSlotDev), hipMemcpyHostToDevice, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));   // the sources are the mirror, which the next insert changes
+    keys_synced = keys.size();
+    changed.clear();
+    return 0;
+  }
+  ~DevResTable() {
+    if (d_slots) (void)hipFree(d_slots);
+    if (d_keys) (void)hipFree(d_keys);
+  }
+};
+
 struct OtlpEngine {
   ColumnizeCtx ctx;
   std::vector<OtlpKeyDev> keys;
@@ -97,6 +167,7 @@ struct OtlpEngine {
   uint32_t n_attr_keys = 0;
   bool json_rules = false;
   ResCache res_cache;
+  DevResTable res_dev;
   std::string err;
   ~OtlpEngine() { if (keys_dev) (void)hipFree(keys_dev); }
 };
@@ -234,10 +305,36 @@ constexpr size_t kGpuScopeBytes = size_t(64) << 10;
 uint64_t sov64(uint64_t x) { uint64_t n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
 uint64_t flen(uint64_t l) { return 1 + sov64(l) + l; }
 
+// A resource's columns from its Resource field(s) (merged as pdata merges
+// them), entered into the cache by message bytes when there is at most one
+// field.  False: a malformed Resource.
+bool resolve_resource(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p,
+                      const std::vector<std::pair<size_t, size_t>>& resf, ProtoSizer& sizer, CachedRes& cr) {
+  AttrMap attrs;
+  uint32_t dropped = 0;
+  for (auto& x : resf)
+    if (!pb_resource(p + x.first, x.second, attrs, dropped)) return false;
+  const ResourceCols rc = columnize_resource(ctx, attrs);
+  cr.svc = rc.svc;
+  cr.svc_str = rc.svc_str;
+  cr.ok = rc.url_ok;
+  cr.attr_res = rc.attr_res;
+  cr.rpart = (uint32_t)flen(sizer.attrs(attrs, 1) + (dropped ? 1 + sov64(dropped) : 0));   // Resource: always emitted
+  const std::string_view key = resf.size() == 1 ? std::string_view((const char*)p + resf[0].first, resf[0].second)
+                                                : std::string_view();
+  std::unique_lock<std::shared_mutex> g(cache.mu);
+  cr.set = cache.intern(rc.attrset);
+  if (resf.size() <= 1 && cache.map.size() < ResCache::kMaxEntries && !cache.map.count(key)) {
+    cache.keys.emplace_back(key);
+    cache.map.emplace(std::string_view(cache.keys.back()), cr);
+  }
+  return true;
+}
+
 // The TracesData records that start in [s, lim) (a record may run past lim:
 // *end is where the last one ends), each ResourceSpans walked in full.
 void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, size_t s, size_t lim,
-                  WalkChunk& c, size_t* end, bool gpu_scopes) {
+                  WalkChunk& c, size_t* end, bool gpu_scopes, bool chain = false) {
   std::unordered_map<std::string_view, CachedRes> rcache;   // this call's, by view into the message
   std::unordered_map<std::string_view, uint32_t> scache;
   ProtoSizer sizer;
@@ -270,6 +367,11 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
     if (twt != 2 || !top.bytes(ro, rl)) { top.fail(); break; }
     *end = top.i;
     if (gpu_scopes && top.i + 2 < n) __builtin_prefetch(p + top.i, 0, 3);   // the next record's header
+    if (chain) {   // the TracesData chain only: the GPU walks each record (otlp_res_fields_kernel)
+      if (ro > 0xFFFFFFFFull || rl > 0xFFFFFFFFull) { c.err = "ResourceSpans beyond the 4 GiB arena range"; return; }
+      c.lay.res_ref.push_back(ro | ((uint64_t)rl << 32));
+      continue;
+    }
     static const int chain_only = getenv("OSE_WALK_CHAIN_ONLY") ? atoi(getenv("OSE_WALK_CHAIN_ONLY")) : 0;   // diagnostics
     if (chain_only == 1) continue;
     PbReader rr(p + ro, rl);
@@ -311,24 +413,7 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
       }
     }
     if (!have) {
-      AttrMap attrs;
-      uint32_t dropped = 0;
-      for (auto& x : resf)
-        if (!pb_resource(p + x.first, x.second, attrs, dropped)) { c.err = "OTLP protobuf: malformed Resource"; return; }
-      const ResourceCols rc = columnize_resource(ctx, attrs);
-      cr.svc = rc.svc;
-      cr.svc_str = rc.svc_str;
-      cr.ok = rc.url_ok;
-      cr.attr_res = rc.attr_res;
-      cr.rpart = (uint32_t)flen(sizer.attrs(attrs, 1) + (dropped ? 1 + sov64(dropped) : 0));   // Resource: always emitted
-      {
-        std::unique_lock<std::shared_mutex> g(cache.mu);
-        cr.set = cache.intern(rc.attrset);
-        if (resf.size() <= 1 && cache.map.size() < ResCache::kMaxEntries && !cache.map.count(key)) {
-          cache.keys.emplace_back(key);
-          cache.map.emplace(std::string_view(cache.keys.back()), cr);
-        }
-      }
+      if (!resolve_resource(ctx, cache, p, resf, sizer, cr)) { c.err = "OTLP protobuf: malformed Resource"; return; }
       if (resf.size() <= 1) rcache.emplace(key, cr);
     }
     const uint32_t rloc = (uint32_t)c.res_svc.size();
@@ -430,6 +515,49 @@ size_t find_start(const uint8_t* p, size_t n, size_t k) {
     if (ok) return q;
   }
   return n;
+}
+
+// The TracesData chain alone (the ResourceSpans records), split over threads
+// as walk() does.
+bool walk_chain(const uint8_t* p, size_t n, std::vector<uint64_t>& res_ref, std::string& err) {
+  const size_t kSeg = size_t(256) << 10;
+  int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)parallel_width(), n / kSeg}));
+  if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));   // diagnostics
+  static const ColumnizeCtx no_ctx;
+  static ResCache no_cache;
+  std::vector<WalkChunk> ch;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    if (attempt) T = 1;
+    std::vector<size_t> st((size_t)T + 1, n), en((size_t)T, 0);
+    st[0] = 0;
+    for (int t = 1; t < T; t++) st[t] = find_start(p, n, n * (size_t)t / (size_t)T);
+    for (int t = T - 1; t >= 1; t--) st[t] = std::min(st[t], st[t + 1]);
+    ch.assign((size_t)T, WalkChunk());
+    parallel_run(T, [&](int t) { walk_segment(no_ctx, no_cache, p, n, st[t], st[t + 1], ch[t], &en[t], true, true); });
+    bool exact = true;
+    for (int t = 0; t < T; t++) {
+      if (!ch[t].err.empty()) {
+        if (t == 0 || attempt) { err = ch[t].err; return false; }
+        exact = false;
+      }
+      if (t + 1 < T && en[t] != st[t + 1]) exact = false;
+    }
+    if (en[T - 1] != n && ch[T - 1].err.empty()) {
+      if (attempt || T == 1) { err = "OTLP protobuf: malformed TracesData"; return false; }
+      exact = false;
+    }
+    if (exact) break;
+    if (attempt) { err = "OTLP protobuf: malformed TracesData"; return false; }
+  }
+  size_t total = 0;
+  for (auto& c : ch) total += c.lay.res_ref.size();
+  res_ref.resize(total);
+  size_t o = 0;
+  for (auto& c : ch) {
+    std::memcpy(res_ref.data() + o, c.lay.res_ref.data(), 8 * c.lay.res_ref.size());
+    o += c.lay.res_ref.size();
+  }
+  return true;
 }
 
 // The walk, split over threads: the records form one chain of lengths, so

@@ -555,6 +555,146 @@ __global__ __launch_bounds__(kOThreads) void otlp_scope_spans_kernel(OtlpScopeAr
   }
 }
 
+// ---- ResourceSpans on the GPU ------------------------------------------------------
+// Pass 1, one lane per ResourceSpans (otlp_pb.cpp pb_walk's ResourceSpans
+// loop): Resource (1), scope_spans (2), the deprecated
+// instrumentation_library_spans (1000, read only when there is no field 2),
+// schema_url (3), others skipped.  The Resource's columns come from the
+// device table when its message bytes are there (one Resource field; the
+// empty key stands for none); else the row is listed for the host.
+__global__ __launch_bounds__(kOThreads) void otlp_res_fields_kernel(OtlpResArgs a) {
+  const uint64_t r = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (r >= a.n_res) return;
+  const uint64_t ref = a.res_ref[r];
+  const uint32_t s0 = (uint32_t)ref, s1 = s0 + (uint32_t)(ref >> 32);
+  Rd rd(a.pb, s0, s1);
+  uint32_t nres = 0, nsc = 0, ndep = 0, schema = 0, ro = 0, rl = 0;
+  uint32_t f, wt;
+  while (rd.more() && rd.tag(f, wt)) {
+    uint32_t ps, pl;
+    if (f == 1 || f == 2 || f == 3 || f == 1000) {
+      if (wt != 2 || !rd.len(ps, pl)) { rd.bad = true; break; }
+      if (f == 1) { ro = ps; rl = pl; nres++; }
+      else if (f == 2) nsc++;
+      else if (f == 1000) ndep++;
+      else schema = pl;
+    } else {
+      rd.skip(wt);
+    }
+  }
+  uint32_t flags = 0;
+  if (rd.bad) {
+    a.flags[r] = 2;
+    a.nscope[r] = 0;
+    atomicOr(a.any_bad, 1u);
+    return;
+  }
+  if (!nsc && ndep) flags |= 4;
+  a.nscope[r] = nsc ? nsc : ndep;
+  a.schema_len[r] = schema;
+  bool found = false;
+  if (nres <= 1) {
+    uint64_t h = kResHashSeed;
+    for (uint32_t q = 0; q < rl; q++) h = res_key_hash_step(h, rd.br.at(ro + q));
+    for (uint32_t probe = 0, slot = (uint32_t)h & (kResSlots - 1); probe < 64; probe++, slot = (slot + 1) & (kResSlots - 1)) {
+      const ResSlotDev& e = a.table[slot];
+      if (!e.ready) break;
+      if (e.h != h || e.klen != rl) continue;
+      uint32_t q = 0;
+      while (q < rl && a.keys[e.koff + q] == rd.br.at(ro + q)) q++;
+      if (q < rl) continue;
+      a.res_svc[r] = e.svc;
+      a.res_svc_str[r] = e.svc_str;
+      a.res_set[r] = e.set;
+      a.res_ok[r] = (uint8_t)e.ok;
+      a.attr_res[r] = e.attr_res;
+      a.res_size[r] = e.rpart + (schema ? (uint32_t)field_len(schema) : 0u);
+      found = true;
+      break;
+    }
+  }
+  if (!found) {
+    flags |= 1;
+    a.miss_list[atomicAdd(a.miss_count, 1u)] = (uint32_t)r;
+  }
+  a.flags[r] = flags;
+}
+
+// Pass 2: every resource's ScopeSpans refs at their place
+__global__ __launch_bounds__(kOThreads) void otlp_res_scopes_kernel(OtlpResArgs a) {
+  const uint64_t r = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (r >= a.n_res) return;
+  const uint32_t want = (a.flags[r] & 4) ? 1000u : 2u;
+  uint64_t q = a.scope0[r];
+  const uint64_t ref = a.res_ref[r];
+  const uint32_t s0 = (uint32_t)ref, s1 = s0 + (uint32_t)(ref >> 32);
+  Rd rd(a.pb, s0, s1);
+  uint32_t f, wt;
+  while (rd.more() && rd.tag(f, wt)) {
+    uint32_t ps, pl;
+    if (f == 1 || f == 2 || f == 3 || f == 1000) {
+      if (wt != 2 || !rd.len(ps, pl)) break;
+      if (f == want) {
+        a.scope_ref[q] = (uint64_t)ps | ((uint64_t)pl << 32);
+        a.scope_res[q] = (uint32_t)r;
+        q++;
+      }
+    } else {
+      rd.skip(wt);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kOThreads) void otlp_res_fix_kernel(OtlpResArgs a, const OtlpResFix* fix, uint32_t n) {
+  const uint32_t k = blockIdx.x * kOThreads + threadIdx.x;
+  if (k >= n) return;
+  const OtlpResFix x = fix[k];
+  const uint32_t sch = a.schema_len[x.row];
+  a.res_svc[x.row] = x.svc;
+  a.res_svc_str[x.row] = x.svc_str;
+  a.res_set[x.row] = x.set;
+  a.res_ok[x.row] = (uint8_t)x.ok;
+  a.attr_res[x.row] = x.attr_res;
+  a.res_size[x.row] = x.rpart + (sch ? (uint32_t)field_len(sch) : 0u);
+}
+
+__global__ __launch_bounds__(kOThreads) void otlp_set_mark_kernel(const uint32_t* res_set, uint64_t n, uint32_t* used) {
+  const uint64_t r = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (r < n) used[res_set[r]] = 1u;   // benign race: every writer stores 1
+}
+__global__ __launch_bounds__(kOThreads) void otlp_set_apply_kernel(uint32_t* res_set, uint64_t n, const uint32_t* used,
+                                                                   const uint32_t* local, uint32_t n_sets, uint32_t* list) {
+  const uint64_t t = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (t < n) res_set[t] = local[res_set[t]];
+  if (t < n_sets && used[t]) list[local[t]] = (uint32_t)t;
+}
+
+void launch_otlp_res_fields(const OtlpResArgs& a, hipStream_t st) {
+  if (a.n_res)
+    hipLaunchKernelGGL(otlp_res_fields_kernel, dim3((uint32_t)((a.n_res + kOThreads - 1) / kOThreads)), dim3(kOThreads), 0,
+                       st, a);
+}
+void launch_otlp_res_scopes(const OtlpResArgs& a, hipStream_t st) {
+  if (a.n_res)
+    hipLaunchKernelGGL(otlp_res_scopes_kernel, dim3((uint32_t)((a.n_res + kOThreads - 1) / kOThreads)), dim3(kOThreads), 0,
+                       st, a);
+}
+void launch_otlp_res_fix(const OtlpResArgs& a, const OtlpResFix* fix, uint32_t n, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(otlp_res_fix_kernel, dim3((n + kOThreads - 1) / kOThreads), dim3(kOThreads), 0, st, a, fix, n);
+}
+void launch_otlp_set_mark(const uint32_t* res_set, uint64_t n_res, uint32_t* used, hipStream_t st) {
+  if (n_res)
+    hipLaunchKernelGGL(otlp_set_mark_kernel, dim3((uint32_t)((n_res + kOThreads - 1) / kOThreads)), dim3(kOThreads), 0, st,
+                       res_set, n_res, used);
+}
+void launch_otlp_set_apply(uint32_t* res_set, uint64_t n_res, const uint32_t* used, const uint32_t* local,
+                           uint32_t n_sets, uint32_t* list, hipStream_t st) {
+  const uint64_t m = std::max<uint64_t>(n_res, n_sets);
+  if (m)
+    hipLaunchKernelGGL(otlp_set_apply_kernel, dim3((uint32_t)((m + kOThreads - 1) / kOThreads)), dim3(kOThreads), 0, st,
+                       res_set, n_res, used, local, n_sets, list);
+}
+
 void launch_otlp_scope_count(const OtlpScopeArgs& a, hipStream_t st) {
   if (a.n_scopes)
     hipLaunchKernelGGL(otlp_scope_count_kernel, dim3((uint32_t)((a.n_scopes + kOThreads - 1) / kOThreads)),

@@ -212,14 +212,23 @@ int Workspace::reserve_table(uint64_t n_spans) {
   if (slots <= table_slots_cap) return 0;
   if (table) HIP_TRY(hipFree(table));
   if (fp_table) HIP_TRY(hipFree(fp_table));
+  if (dup_bkt) HIP_TRY(hipFree(dup_bkt));
+  if (dup_bkt_count) HIP_TRY(hipFree(dup_bkt_count));
   table = nullptr;
   fp_table = nullptr;
+  dup_bkt = nullptr;
+  dup_bkt_count = nullptr;
   table_slots_cap = 0;
   HIP_TRY(hipMalloc(&table, slots * sizeof(TraceSlot)));
   HIP_TRY(hipMemset(table, 0, slots * sizeof(TraceSlot)));
   fp_slots_cap = fp_slots(n_spans);
   HIP_TRY(hipMalloc(&fp_table, fp_slots_cap * sizeof(uint64_t)));
   HIP_TRY(hipMemset(fp_table, 0, fp_slots_cap * sizeof(uint64_t)));
+  // fingerprint buckets: half full (on average) at one run head per 4 spans
+  dup_bkt_bits = 0;
+  while ((uint64_t(kDupBucketCap) / 2 << dup_bkt_bits) < n_spans / 4) dup_bkt_bits++;
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dup_bkt), (size_t(kDupBucketCap) << dup_bkt_bits) * sizeof(uint64_t)));
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dup_bkt_count), (size_t(1) << dup_bkt_bits) * sizeof(uint32_t)));
   table_slots_cap = slots;
   epoch = 0;
   return 0;
@@ -336,11 +345,28 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.win_per_wave = kWinPerWave;
   if (const char* ww = getenv("OSE_WIN_PER_WAVE")) a.win_per_wave = std::max<uint32_t>(1, (uint32_t)strtoul(ww, nullptr, 0));   // tuning
   if (const char* ls = getenv("OSE_LONG_STEPS")) a.long_steps = std::max<uint32_t>(1, (uint32_t)strtoul(ls, nullptr, 0));   // tuning
+  // duplicate detection: fingerprint buckets checked in LDS (OSE_DUP_BUCKETS=1)
+  // or the fingerprint table
+  const char* bkt_env = getenv("OSE_DUP_BUCKETS");   // read per call (A/B and tests)
+  const bool buckets = bkt_env && strtoul(bkt_env, nullptr, 0) != 0;
+  if (buckets && a.mode == kTraceRuns && ws->dup_bkt) {
+    a.dup_bkt = ws->dup_bkt;
+    a.dup_bkt_count = ws->dup_bkt_count;
+    a.dup_bkt_bits = ws->dup_bkt_bits;
+    HIP_TRY(hipMemsetAsync(a.dup_bkt_count, 0, sizeof(uint32_t) << a.dup_bkt_bits, st));
+  }
   Engine::Timed tm{};
   e->prof_begin("trace_eval_kernel", st, tm);
   launch_trace_eval(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
+  if (a.dup_bkt) {
+    Engine::Timed td{};
+    e->prof_begin("trace_dup_check", st, td);
+    launch_trace_dup_check(a, st);
+    HIP_TRY(hipGetLastError());
+    e->prof_end(td, st);
+  }
   auto long_pass = [=](uint32_t known_runs) -> int {
     Engine::Timed tl{};
     e->prof_begin("trace_long_kernel", st, tl);

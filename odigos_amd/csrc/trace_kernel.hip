@@ -514,8 +514,20 @@ struct HeadQ {
 __device__ void flush_heads(const TraceKernelArgs& a, HeadQ& H, uint32_t& hn, int lane) {
   __builtin_amdgcn_wave_barrier();
   bool dup = false;
-  for (uint32_t b = 0; b < hn; b += kWave)
-    if (b + lane < hn) dup |= fp_insert_cell(a, H.cell[b + lane], H.idx[b + lane]);
+  if (a.dup_bkt) {   // bucketed: one returning atomic per head, the fingerprint stored after it
+    for (uint32_t b = 0; b < hn; b += kWave) {
+      if (b + lane < hn) {
+        const uint64_t h = H.cell[b + lane];
+        const uint32_t bk = (uint32_t)(h >> (64 - a.dup_bkt_bits));
+        const uint32_t at = atomicAdd(&a.dup_bkt_count[bk], 1u);
+        if (at < kDupBucketCap) a.dup_bkt[(uint64_t)bk * kDupBucketCap + at] = h | 1ull;   // (0 marks an empty set slot)
+        else dup = true;
+      }
+    }
+  } else {
+    for (uint32_t b = 0; b < hn; b += kWave)
+      if (b + lane < hn) dup |= fp_insert_cell(a, H.cell[b + lane], H.idx[b + lane]);
+  }
   // one *dup store per wave flush (a per-head atomic on one word serialises)
   if (__ballot(dup) && lane == 0) atomicOr(a.dup, 1u);
   __builtin_amdgcn_wave_barrier();
@@ -677,8 +689,12 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         if (hn + nh > kHeadQ) flush_heads(a, HQ, hn, lane);
         if (hd) {
           const uint32_t e = hn + __popcll(hmask & lanemask_lt(lane));
-          HQ.cell[e] = fp_cell(a, r.hi, r.lo);
-          HQ.idx[e] = (uint32_t)(tid_hash(r.hi, r.lo) & a.fp_mask);
+          if (a.dup_bkt) {
+            HQ.cell[e] = splitmix64(r.lo ^ (r.hi << 1));
+          } else {
+            HQ.cell[e] = fp_cell(a, r.hi, r.lo);
+            HQ.idx[e] = (uint32_t)(tid_hash(r.hi, r.lo) & a.fp_mask);
+          }
         }
         hn += nh;
       }
@@ -1627,6 +1643,43 @@ void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   else
     hipLaunchKernelGGL(trace_eval_kernel<false>, dim3(blocks), dim3(kTThreads), 0, st, a);
 }
+// One workgroup per fingerprint bucket: its entries into an LDS hash set; an
+// entry met twice (or a bucket past its capacity) sets *dup
+__global__ __launch_bounds__(256) void trace_dup_check_kernel(TraceKernelArgs a) {
+  constexpr uint32_t kSet = 2 * kDupBucketCap;
+  static_assert(kSet == 2048, "the set's hash takes 11 bits");
+  __shared__ uint64_t set[kSet];
+  __shared__ uint32_t found;
+  const uint32_t bk = blockIdx.x;
+  const uint32_t c = a.dup_bkt_count[bk];
+  if (c <= 1) return;
+  if (c > kDupBucketCap) {
+    if (threadIdx.x == 0) atomicOr(a.dup, 1u);
+    return;
+  }
+  for (uint32_t k = threadIdx.x; k < kSet; k += 256) set[k] = 0ull;
+  if (threadIdx.x == 0) found = 0;
+  __syncthreads();
+  const uint64_t* e = a.dup_bkt + (uint64_t)bk * kDupBucketCap;
+  bool hit = false;
+  for (uint32_t k = threadIdx.x; k < c; k += 256) {
+    const uint64_t v = e[k];   // never 0
+    uint32_t s = ((uint32_t)v * 0x9E3779B1u) >> (32 - 11);
+    for (uint32_t probes = 0; probes < kSet; probes++) {
+      const uint64_t old = atomicCAS((unsigned long long*)&set[s], 0ull, (unsigned long long)v);
+      if (old == 0) break;
+      if (old == v) { hit = true; break; }
+      s = (s + 1) & (kSet - 1);
+    }
+  }
+  if (hit) found = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && found) atomicOr(a.dup, 1u);
+}
+void launch_trace_dup_check(const TraceKernelArgs& a, hipStream_t st) {
+  if (a.dup_bkt) hipLaunchKernelGGL(trace_dup_check_kernel, dim3(1u << a.dup_bkt_bits), dim3(256), 0, st, a);
+}
+
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs) {
   // known_runs: the listed-run count the host read (host-gated form); else a
   // grid for the most runs the fast path can list, blocks past *n_long exit

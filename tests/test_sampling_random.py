@@ -361,3 +361,13 @@ def test_gpu_sample_and_template_one_call(workload, shuffle):
     used = db.used()
     assert used == int(uo.used[0])
     np.testing.assert_array_equal(db.out_numpy("tmpl_arena")[:used], uo.bufs["tmpl_arena"][:used])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle,n", [(False, 300_000), (True, 300_000), (False, 2_000_000), (True, 50_000)])
+def test_gpu_sampling_dup_buckets(monkeypatch, shuffle, n):
+    # the fast path's duplicate detection through fingerprint buckets checked
+    # in LDS (OSE_DUP_BUCKETS=1, read per call): the same decisions as the
+    # oracle, repeated trace ids (shuffled resources) found
+    monkeypatch.setenv("OSE_DUP_BUCKETS", "1")
+    gpu_vs_oracle(Generator("sampling", seed=0x0D1600F0 + n, n_spans=n, shuffle=shuffle))
