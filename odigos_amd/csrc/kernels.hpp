@@ -464,11 +464,14 @@ struct OtlpResFix {
   uint64_t attr_res;
 };
 void launch_otlp_res_fix(const OtlpResArgs& a, const OtlpResFix* fix, uint32_t n, hipStream_t st);
-// attribute-set ids of the cache -> the batch's (ascending cache id): used
-// flags, then (after an exclusive scan of them) the ids and the list
-void launch_otlp_set_mark(const uint32_t* res_set, uint64_t n_res, uint32_t* used, hipStream_t st);
-void launch_otlp_set_apply(uint32_t* res_set, uint64_t n_res, const uint32_t* used, const uint32_t* local,
-                           uint32_t n_sets, uint32_t* list, hipStream_t st);
+// attribute-set ids of the cache -> the batch's, in order of first appearance
+// (as the host walk numbers them): each set's first resource (first[], set
+// to ~0 before), the resources that are first of their set (is_first), and
+// after an exclusive scan of those flags (pos) the ids and the batch's list
+void launch_otlp_set_first(const uint32_t* res_set, uint64_t n_res, uint32_t* first, uint32_t* is_first,
+                           hipStream_t st);
+void launch_otlp_set_apply(uint32_t* res_set, uint64_t n_res, const uint32_t* first, const uint32_t* is_first,
+                           const uint32_t* pos, uint32_t* list, hipStream_t st);
 void launch_otlp_scope_count(const OtlpScopeArgs& a, hipStream_t st);
 void launch_otlp_scope_spans(const OtlpScopeArgs& a, hipStream_t st);
 

@@ -189,6 +189,11 @@ struct OtlpBatchImpl {
   // brings them back
   bool layout_on_host = true;
   DevBuf sslab;   // scope-level device arrays
+  DevBuf rslab, setbuf;   // resource-level device arrays; attribute-set compaction (GPU ResourceSpans walk)
+  bool res_on_device = false;   // res_scope0 / scope_ref / attr_res live on the device (rslab, sslab)
+  uint32_t* d_res_scope0 = nullptr;
+  uint64_t* d_scope_ref = nullptr;
+  uint64_t* d_attr_res = nullptr;
   uint64_t* d_span_ref = nullptr;
   uint32_t *d_span_res = nullptr, *d_span0 = nullptr;
   uint64_t *d_hdr = nullptr, *d_schema = nullptr;
@@ -674,9 +679,208 @@ namespace {
 // walk is counted, sized and listed on the device (otlp_scope_*_kernel);
 // returns the span count in *n_out, or 1 in *redo when some scope needs the
 // host walk (groups or a malformed field: the caller walks on the host).
-int scope_walk_gpu(Engine* e, OtlpBatchImpl* b, Walked& w, hipStream_t st, uint64_t* n_out, bool* redo) {
+// The GPU half of the ResourceSpans level: the host walks
+// the TracesData chain only (walk_chain), the device each record's fields
+// (otlp_res_fields_kernel), the Resource columns from the device resource
+// table; resources the table lacks are resolved on the host (pb_resource,
+// columnize_resource: the same cache as the host walk), entered into the
+// table, and their columns scattered in.  The attribute-set ids are then
+// renumbered for the batch (ascending cache id).  *redo: a malformed record
+// (the host walk reports it exactly).  Fills w.lay.res_ref and w.sets, *R,
+// *S and the args of the scope listing.
+int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len, hipStream_t st, Walked& w,
+                 uint64_t* R_out, uint64_t* S_out, OtlpResArgs* args, bool* redo) {
+  *redo = false;
+  std::string err;
+  if (!walk_chain(pb, len, w.lay.res_ref, err)) return fail(OSE_EINVAL, err);
+  HIP_TRY(hipStreamSynchronize(st));   // the staging buffer (the message's H2D) is reused below
+  const uint64_t R = w.lay.res_ref.size();
+  *R_out = R;
+  const uint64_t RN = std::max<uint64_t>(R, 1);
+  const uint32_t tiles = (uint32_t)((RN + kScanTileItems - 1) / kScanTileItems);
+  struct Part { void** dst; size_t bytes; };
+  OtlpResArgs a{};
+  uint64_t* status = nullptr;
+  uint32_t* words = nullptr;
+  const std::vector<Part> parts = {
+      {(void**)&a.res_ref, 8 * RN}, {(void**)&a.flags, 4 * RN}, {(void**)&a.nscope, 4 * RN},
+      {(void**)&a.schema_len, 4 * RN}, {(void**)&a.scope0, 4 * RN}, {(void**)&a.res_svc, 4 * RN},
+      {(void**)&a.res_svc_str, 4 * RN}, {(void**)&a.res_set, 4 * RN}, {(void**)&a.res_size, 4 * RN},
+      {(void**)&a.res_ok, RN}, {(void**)&a.attr_res, 8 * RN}, {(void**)&a.miss_list, 4 * RN},
+      {(void**)&status, 8 * (size_t)tiles + 64}, {(void**)&words, 64},
+  };
+  size_t total = 0;
+  for (auto& p : parts) total = up(total + p.bytes + 16);
+  int rc;
+  if ((rc = b->rslab.need(total)) || (rc = b->stage.need(8 * RN + 64))) return rc;
+  size_t off = 0;
+  for (auto& p : parts) {
+    *p.dst = b->rslab.p + off;
+    off = up(off + p.bytes + 16);
+  }
+  if (R) std::memcpy(b->stage.p, w.lay.res_ref.data(), 8 * R);
+  if (R) HIP_TRY(hipMemcpyAsync(const_cast<uint64_t*>(a.res_ref), b->stage.p, 8 * R, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(status, 0, reinterpret_cast<uint8_t*>(words) + 64 - reinterpret_cast<uint8_t*>(status), st));
+  a.pb = b->arena.p;
+  a.n_res = R;
+  a.any_bad = words;
+  a.miss_count = words + 1;
+  uint32_t h[4] = {0, 0, 0, 0};
+  {
+    DevResTable& t = o->res_dev;
+    {
+      std::unique_lock<std::shared_mutex> g(t.mu);
+      if ((rc = t.ensure())) return rc;
+    }
+    std::shared_lock<std::shared_mutex> g(t.mu);   // held until the lookups have run
+    a.table = t.d_slots;
+    a.keys = t.d_keys;
+    (void)hipGetLastError();
+    launch_otlp_res_fields(a, st);
+    HIP_TRY(hipGetLastError());
+    ScanArgs sa{};
+    sa.n = R;
+    sa.n_tiles = tiles;
+    sa.in = a.nscope;
+    sa.out = const_cast<uint32_t*>(a.scope0);
+    sa.total = words + 2;
+    sa.counter = words + 3;
+    sa.status = status;
+    sa.error = words + 4;
+    if (R) launch_scan_u32(sa, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h, words, 12, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  if (h[0]) { *redo = true; return 0; }
+  *S_out = h[2];
+  // the resources the table lacks: resolved on the host
+  const uint32_t nm = h[1];
+  if (nm) {
+    std::vector<uint32_t> miss(nm);
+    HIP_TRY(hipMemcpy(miss.data(), a.miss_list, 4 * (size_t)nm, hipMemcpyDeviceToHost));
+    std::vector<OtlpResFix> fix(nm);
+    std::vector<uint8_t> keyed(nm, 0);   // entered into the device table (one Resource field or none)
+    std::vector<std::pair<size_t, size_t>> key_of(nm);
+    const int T = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)parallel_width(), nm / 256));
+    std::vector<std::string> errs((size_t)T);
+    parallel_run(T, [&](int t) {
+      ProtoSizer sizer;
+      std::vector<std::pair<size_t, size_t>> resf;
+      for (uint32_t k = (uint32_t)((uint64_t)nm * t / T); k < (uint32_t)((uint64_t)nm * (t + 1) / T); k++) {
+        const uint32_t r = miss[k];
+        const uint64_t rr = w.lay.res_ref[r];
+        const size_t ro = (uint32_t)rr;
+        PbReader rd(pb + ro, (size_t)(rr >> 32));
+        resf.clear();
+        uint32_t f, wt;
+        while (rd.more() && rd.tag(f, wt)) {
+          size_t fo, fl;
+          if (f == 1 || f == 2 || f == 3 || f == 1000) {
+            if (wt != 2 || !rd.bytes(fo, fl)) { rd.fail(); break; }
+            if (f == 1) resf.emplace_back(ro + fo, fl);
+          } else {
+            rd.skip(wt, f);
+          }
+        }
+        if (!rd.ok) { errs[t] = "OTLP protobuf: malformed ResourceSpans"; return; }
+        CachedRes cr{};
+        bool have = false;
+        const std::string_view key = resf.size() == 1 ? std::string_view((const char*)pb + resf[0].first, resf[0].second)
+                                                      : std::string_view();
+        if (resf.size() <= 1) {
+          std::shared_lock<std::shared_mutex> g(o->res_cache.mu);
+          auto ci = o->res_cache.map.find(key);
+          if (ci != o->res_cache.map.end()) {
+            cr = ci->second;
+            have = true;
+          }
+        }
+        if (!have && !resolve_resource(o->ctx, o->res_cache, pb, resf, sizer, cr)) {
+          errs[t] = "OTLP protobuf: malformed Resource";
+          return;
+        }
+        fix[k] = OtlpResFix{r, cr.svc, cr.svc_str, cr.set, cr.rpart, cr.ok, cr.attr_res};
+        if (resf.size() <= 1) {
+          keyed[k] = 1;
+          key_of[k] = resf.empty() ? std::pair<size_t, size_t>(0, 0) : resf[0];
+        }
+      }
+    });
+    for (auto& e : errs)
+      if (!e.empty()) return fail(OSE_EINVAL, e);
+    if ((rc = b->fixdev.need(sizeof(OtlpResFix) * nm)) || (rc = b->stage.need(sizeof(OtlpResFix) * nm))) return rc;
+    std::memcpy(b->stage.p, fix.data(), sizeof(OtlpResFix) * nm);
+    HIP_TRY(hipMemcpyAsync(b->fixdev.p, b->stage.p, sizeof(OtlpResFix) * nm, hipMemcpyHostToDevice, st));
+    launch_otlp_res_fix(a, reinterpret_cast<const OtlpResFix*>(b->fixdev.p), nm, st);
+    HIP_TRY(hipGetLastError());
+    {   // later calls find these on the device
+      DevResTable& t = o->res_dev;
+      std::unique_lock<std::shared_mutex> g(t.mu);
+      for (uint32_t k = 0; k < nm; k++) {
+        if (!keyed[k]) continue;
+        const CachedRes cr{fix[k].svc, fix[k].svc_str, fix[k].set, fix[k].rpart, (uint8_t)fix[k].ok, fix[k].attr_res};
+        t.insert(pb + key_of[k].first, (uint32_t)key_of[k].second, cr);
+      }
+      if ((rc = t.sync(st))) return rc;
+    }
+  }
+  // the cache's attribute-set ids -> this batch's (first appearance)
+  uint32_t n_sets;
+  {
+    std::shared_lock<std::shared_mutex> g(o->res_cache.mu);
+    n_sets = (uint32_t)o->res_cache.sets.size();
+  }
+  const uint64_t NS = std::max<uint64_t>(n_sets, 1);
+  const size_t o_flag = up(4 * NS + 16), o_pos = o_flag + up(4 * RN + 16), o_list = o_pos + up(4 * RN + 16),
+               o_stat = o_list + up(4 * RN + 16), o_words = o_stat + up(8 * (size_t)tiles + 64);
+  if ((rc = b->setbuf.need(o_words + 64))) return rc;
+  uint32_t* first = reinterpret_cast<uint32_t*>(b->setbuf.p);
+  uint32_t* is_first = reinterpret_cast<uint32_t*>(b->setbuf.p + o_flag);
+  uint32_t* pos = reinterpret_cast<uint32_t*>(b->setbuf.p + o_pos);
+  uint32_t* list = reinterpret_cast<uint32_t*>(b->setbuf.p + o_list);
+  uint64_t* sstat = reinterpret_cast<uint64_t*>(b->setbuf.p + o_stat);
+  uint32_t* swords = reinterpret_cast<uint32_t*>(b->setbuf.p + o_words);
+  HIP_TRY(hipMemsetAsync(first, 0xFF, 4 * NS, st));
+  HIP_TRY(hipMemsetAsync(sstat, 0, o_words + 64 - o_stat, st));
+  launch_otlp_set_first(a.res_set, R, first, is_first, st);
+  HIP_TRY(hipGetLastError());
+  ScanArgs ss{};
+  ss.n = R;
+  ss.n_tiles = tiles;
+  ss.in = is_first;
+  ss.out = pos;
+  ss.total = swords + 1;
+  ss.counter = swords + 2;
+  ss.status = sstat;
+  ss.error = swords;
+  if (R) launch_scan_u32(ss, st);
+  HIP_TRY(hipGetLastError());
+  launch_otlp_set_apply(a.res_set, R, first, is_first, pos, list, st);
+  HIP_TRY(hipGetLastError());
+  uint32_t sw[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(sw, swords, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (sw[0]) return fail(OSE_EDEVICE, "OTLP ingest: attribute-set scan error");
+  std::vector<uint32_t> ids(sw[1]);
+  if (sw[1]) HIP_TRY(hipMemcpy(ids.data(), list, 4 * (size_t)sw[1], hipMemcpyDeviceToHost));
+  {
+    std::shared_lock<std::shared_mutex> g(o->res_cache.mu);
+    w.sets.clear();
+    for (uint32_t id : ids) w.sets.push_back(o->res_cache.sets[id]);
+  }
+  *args = a;
+  b->d_res_scope0 = const_cast<uint32_t*>(a.scope0);
+  b->d_attr_res = a.attr_res;
+  return 0;
+}
+
+// res: the GPU ResourceSpans pass ran (res_walk_gpu): its S scopes are listed
+// on the device by otlp_res_scopes_kernel, every one walked here
+int scope_walk_gpu(Engine* e, OtlpBatchImpl* b, Walked& w, hipStream_t st, uint64_t* n_out, bool* redo,
+                   OtlpResArgs* res = nullptr, uint64_t S_res = 0) {
   (void)e;
-  const uint64_t S = w.scope_size.size(), H = w.span_ref.size();
+  const uint64_t S = res ? S_res : w.scope_size.size(), H = res ? 0 : w.span_ref.size();
   *redo = false;
   const uint32_t tiles = (uint32_t)((S + kScanTileItems - 1) / kScanTileItems);
   struct Part { void** dst; size_t bytes; const void* src; };
@@ -684,15 +888,15 @@ int scope_walk_gpu(Engine* e, OtlpBatchImpl* b, Walked& w, hipStream_t st, uint6
   uint8_t* on_host;
   uint32_t *count, *scope_size, *flags, *span0, *scope_res, *words;
   std::vector<Part> parts = {
-      {(void**)&scope_ref, 8 * S, b->lay.scope_ref.data()},
-      {(void**)&hdr, 8 * S, b->lay.scope_hdr.data()},
-      {(void**)&schema, 8 * S, b->lay.scope_schema.data()},
+      {(void**)&scope_ref, 8 * S, res ? nullptr : b->lay.scope_ref.data()},
+      {(void**)&hdr, 8 * S, res ? nullptr : b->lay.scope_hdr.data()},
+      {(void**)&schema, 8 * S, res ? nullptr : b->lay.scope_schema.data()},
       {(void**)&host_at, 8 * S, nullptr},
-      {(void**)&host_refs, 8 * H, w.span_ref.data()},
-      {(void**)&on_host, S, w.scope_on_host.data()},
-      {(void**)&count, 4 * S, w.scope_count.data()},
-      {(void**)&scope_size, 4 * S, w.scope_size.data()},
-      {(void**)&scope_res, 4 * S, w.scope_res.data()},
+      {(void**)&host_refs, 8 * H, res ? nullptr : w.span_ref.data()},
+      {(void**)&on_host, S, res ? nullptr : w.scope_on_host.data()},
+      {(void**)&count, 4 * S, res ? nullptr : w.scope_count.data()},
+      {(void**)&scope_size, 4 * S, res ? nullptr : w.scope_size.data()},
+      {(void**)&scope_res, 4 * S, res ? nullptr : w.scope_res.data()},
       // device-only
       {(void**)&flags, 4 * S, nullptr},
       {(void**)&span0, 4 * S, nullptr},
@@ -702,21 +906,29 @@ int scope_walk_gpu(Engine* e, OtlpBatchImpl* b, Walked& w, hipStream_t st, uint6
   size_t total = 0, inputs = 0;
   for (auto& p : parts) {
     total = up(total + p.bytes + 16);
-    if (p.src || p.dst == (void**)&host_at) inputs = total;
+    if (!res && (p.src || p.dst == (void**)&host_at)) inputs = total;
   }
   int rc;
   if ((rc = b->sslab.need(total)) || (rc = b->stage.need(inputs))) return rc;
   size_t off = 0;
   for (auto& p : parts) {
     *p.dst = b->sslab.p + off;
-    if (p.src && p.bytes) std::memcpy(b->stage.p + off, p.src, p.bytes);
+    if (!res && p.src && p.bytes) std::memcpy(b->stage.p + off, p.src, p.bytes);
     off = up(off + p.bytes + 16);
   }
-  {   // host_at: the host-walked scopes' offsets into host_refs (the walk's span0)
+  if (!res) {   // host_at: the host-walked scopes' offsets into host_refs (the walk's span0)
     uint64_t* ha = reinterpret_cast<uint64_t*>(b->stage.p + (reinterpret_cast<uint8_t*>(host_at) - b->sslab.p));
     for (uint64_t q = 0; q < S; q++) ha[q] = b->lay.scope_span0[q];
+    HIP_TRY(hipMemcpyAsync(b->sslab.p, b->stage.p, inputs, hipMemcpyHostToDevice, st));
+  } else {
+    // the scopes of every resource at their place, none walked on the host
+    HIP_TRY(hipMemsetAsync(on_host, 0, S, st));
+    res->scope_ref = scope_ref;
+    res->scope_res = scope_res;
+    launch_otlp_res_scopes(*res, st);
+    HIP_TRY(hipGetLastError());
+    b->d_scope_ref = scope_ref;
   }
-  HIP_TRY(hipMemcpyAsync(b->sslab.p, b->stage.p, inputs, hipMemcpyHostToDevice, st));
   const size_t dev0 = reinterpret_cast<uint8_t*>(flags) - b->sslab.p;
   HIP_TRY(hipMemsetAsync(flags, 0, total - dev0, st));   // flags, span0, scan status, words
   OtlpScopeArgs a{};
@@ -761,6 +973,14 @@ int scope_walk_gpu(Engine* e, OtlpBatchImpl* b, Walked& w, hipStream_t st, uint6
   b->d_schema = schema;
   std::vector<std::pair<uint64_t, uint32_t>> patch;   // scope sizes the host computes
   ProtoSizer sizer;
+  if (res) {
+    bool any = false;
+    for (uint64_t q = 0; q < S && !any; q++) any = fl[q] != 0;
+    if (any) {   // the flagged scopes' refs
+      b->lay.scope_ref.resize(S);
+      HIP_TRY(hipMemcpy(b->lay.scope_ref.data(), scope_ref, 8 * S, hipMemcpyDeviceToHost));
+    }
+  }
   for (uint64_t q = 0; q < S; q++) {
     if (!fl[q]) continue;
     if (fl[q] & 2) { *redo = true; return 0; }
@@ -798,9 +1018,18 @@ int scope_walk_gpu(Engine* e, OtlpBatchImpl* b, Walked& w, hipStream_t st, uint6
 // (the encoder and the host pass read them there)
 int layout_to_host(OtlpBatchImpl* b, hipStream_t st) {
   if (b->layout_on_host) return 0;
-  const uint64_t n = b->cols.n_spans, S = b->cols.n_scopes;
+  const uint64_t n = b->cols.n_spans, S = b->cols.n_scopes, R = b->cols.n_resources;
   b->span_ref.resize(n);
   std::vector<uint32_t> span0(S);
+  if (b->res_on_device) {   // the ResourceSpans level was walked on the GPU too
+    b->lay.res_scope0.resize(R);
+    b->lay.scope_ref.resize(S);
+    b->lay.scope_hdr.resize(S);
+    b->lay.scope_schema.resize(S);
+    b->lay.scope_span0.resize(S);
+    if (R) HIP_TRY(hipMemcpyAsync(b->lay.res_scope0.data(), b->d_res_scope0, 4 * R, hipMemcpyDeviceToHost, st));
+    if (S) HIP_TRY(hipMemcpyAsync(b->lay.scope_ref.data(), b->d_scope_ref, 8 * S, hipMemcpyDeviceToHost, st));
+  }
   if (n) HIP_TRY(hipMemcpyAsync(b->span_ref.data(), b->d_span_ref, 8 * n, hipMemcpyDeviceToHost, st));
   if (S) {
     HIP_TRY(hipMemcpyAsync(span0.data(), b->d_span0, 4 * S, hipMemcpyDeviceToHost, st));
@@ -813,7 +1042,8 @@ int layout_to_host(OtlpBatchImpl* b, hipStream_t st) {
   return 0;
 }
 
-int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchImpl* b, bool host_scopes = false) {
+int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchImpl* b, bool host_scopes = false,
+           bool host_res = false) {
   int rc;
   OtlpEngine* o = otlp_engine(e, rc);
   if (!o) return rc;
@@ -846,28 +1076,43 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   lap(0);
   // 2. the walk: TracesData and ResourceSpans on the host, ScopeSpans up to
   //    64 KB on the GPU (OSE_OTLP_HOST_SCOPES=1: all on the host, diagnostics)
+  //    (OSE_OTLP_HOST_RESOURCES=1: ResourceSpans on the host, ScopeSpans on the
+  //    GPU; without it only the TracesData chain is walked on the host)
   static const bool env_host = getenv("OSE_OTLP_HOST_SCOPES") != nullptr;
+  const bool env_host_res = getenv("OSE_OTLP_HOST_RESOURCES") != nullptr;   // read per call (tests)
   const bool gpu_scopes = !host_scopes && !env_host;
+  const bool gpu_res = gpu_scopes && !host_res && !env_host_res;
   Walked w;
-  if (!walk(o->ctx, o->res_cache, pb, len, w, gpu_scopes)) return fail(OSE_EINVAL, w.err);
+  OtlpResArgs ra{};
+  uint64_t R = 0, S = 0;
+  if (gpu_res) {
+    bool redo = false;
+    if ((rc = res_walk_gpu(o, b, pb, len, st, w, &R, &S, &ra, &redo))) return rc;
+    if (redo) return decode(e, pb, len, st, b, false, true);   // a malformed record: the host walk reports it
+  } else {
+    if (!walk(o->ctx, o->res_cache, pb, len, w, gpu_scopes)) return fail(OSE_EINVAL, w.err);
+    HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
+    R = w.res_svc.size();
+  }
   lap(1);
-  HIP_TRY(hipStreamSynchronize(st));   // the staging buffer is reused below
   b->pb = pb;
   b->pb_len = len;
   b->lay = std::move(w.lay);
   b->layout_on_host = true;
+  b->res_on_device = gpu_res;
   ose_columns& c = b->cols;
   c = ose_columns{};
+  c.n_resources = (uint32_t)R;
   uint64_t n = 0;
   if (gpu_scopes) {
     bool redo = false;
-    if ((rc = scope_walk_gpu(e, b, w, st, &n, &redo))) return rc;
-    if (redo) return decode(e, pb, len, st, b, true);   // a scope needs the host walk: all on the host
+    if ((rc = scope_walk_gpu(e, b, w, st, &n, &redo, gpu_res ? &ra : nullptr, S))) return rc;
+    if (redo) return decode(e, pb, len, st, b, true, true);   // a scope needs the host walk: all on the host
   } else {
     n = w.span_ref.size();
     b->span_ref = std::move(w.span_ref);
   }
-  const uint64_t R = w.res_svc.size(), S = b->lay.scope_ref.size();
+  if (!gpu_res) S = b->lay.scope_ref.size();
   if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "OTLP ingest: more than 2^32-16 spans");
   const uint32_t K = o->n_attr_keys;
   b->attrsets = std::move(w.sets);
@@ -884,12 +1129,14 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
       {(void**)&span_ref, 8 * N, gpu_scopes ? nullptr : b->span_ref.data()},
       {(void**)&c.resource, 4 * N, gpu_scopes ? nullptr : w.span_res.data()},
       {(void**)&c.scope, 4 * N, gpu_scopes ? nullptr : w.span_scope.data()},
-      {(void**)&c.res_svc, 4 * R, w.res_svc.data()},
-      {(void**)&c.res_svc_str, 4 * R, w.res_svc_str.data()},
-      {(void**)&c.res_url_ok, R, w.res_ok.data()},
-      {(void**)&c.res_attrset, 4 * R, w.res_attrset.data()},
-      {(void**)&c.res_size, 4 * R, w.res_size.data()},
   };
+  if (!gpu_res) {
+    parts.push_back({(void**)&c.res_svc, 4 * R, w.res_svc.data()});
+    parts.push_back({(void**)&c.res_svc_str, 4 * R, w.res_svc_str.data()});
+    parts.push_back({(void**)&c.res_url_ok, R, w.res_ok.data()});
+    parts.push_back({(void**)&c.res_attrset, 4 * R, w.res_attrset.data()});
+    parts.push_back({(void**)&c.res_size, 4 * R, w.res_size.data()});
+  }
   if (!gpu_scopes) {
     parts.push_back({(void**)&c.scope_size, 4 * S, w.scope_size.data()});
     parts.push_back({(void**)&c.scope_resource, 4 * S, w.scope_res.data()});
@@ -930,6 +1177,13 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   }
   if (inputs) HIP_TRY(hipMemcpyAsync(b->slab.p, b->stage.p, inputs, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(host_count, 0, 16, st));
+  if (gpu_res) {   // the resource columns the GPU pass wrote
+    c.res_svc = ra.res_svc;
+    c.res_svc_str = ra.res_svc_str;
+    c.res_url_ok = ra.res_ok;
+    c.res_attrset = ra.res_set;
+    c.res_size = ra.res_size;
+  }
   if (gpu_scopes) {
     c.scope_size = keep_scope.scope_size;
     c.scope_resource = keep_scope.scope_resource;
@@ -996,6 +1250,10 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   if (!cnt) return 0;
   std::vector<uint32_t> span_res;
   const std::vector<uint32_t>* sres = &w.span_res;
+  if (gpu_res) {   // the resources' span_attribute service bits from the device
+    attr_res.resize(R);
+    if (R) HIP_TRY(hipMemcpy(attr_res.data(), b->d_attr_res, 8 * R, hipMemcpyDeviceToHost));
+  }
   if (!b->layout_on_host) {   // the spans' refs and resources from the device
     if ((rc = layout_to_host(b, st))) return rc;
     span_res.resize(n);

@@ -658,15 +658,23 @@ __global__ __launch_bounds__(kOThreads) void otlp_res_fix_kernel(OtlpResArgs a, 
   a.res_size[x.row] = x.rpart + (sch ? (uint32_t)field_len(sch) : 0u);
 }
 
-__global__ __launch_bounds__(kOThreads) void otlp_set_mark_kernel(const uint32_t* res_set, uint64_t n, uint32_t* used) {
+__global__ __launch_bounds__(kOThreads) void otlp_set_min_kernel(const uint32_t* res_set, uint64_t n, uint32_t* first) {
   const uint64_t r = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
-  if (r < n) used[res_set[r]] = 1u;   // benign race: every writer stores 1
+  if (r < n) atomicMin(&first[res_set[r]], (uint32_t)r);
 }
-__global__ __launch_bounds__(kOThreads) void otlp_set_apply_kernel(uint32_t* res_set, uint64_t n, const uint32_t* used,
-                                                                   const uint32_t* local, uint32_t n_sets, uint32_t* list) {
-  const uint64_t t = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
-  if (t < n) res_set[t] = local[res_set[t]];
-  if (t < n_sets && used[t]) list[local[t]] = (uint32_t)t;
+__global__ __launch_bounds__(kOThreads) void otlp_set_flag_kernel(const uint32_t* res_set, uint64_t n, const uint32_t* first,
+                                                                  uint32_t* is_first) {
+  const uint64_t r = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (r < n) is_first[r] = first[res_set[r]] == (uint32_t)r ? 1u : 0u;
+}
+__global__ __launch_bounds__(kOThreads) void otlp_set_apply_kernel(uint32_t* res_set, uint64_t n, const uint32_t* first,
+                                                                   const uint32_t* is_first, const uint32_t* pos,
+                                                                   uint32_t* list) {
+  const uint64_t r = (uint64_t)blockIdx.x * kOThreads + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t s = res_set[r];
+  if (is_first[r]) list[pos[r]] = s;
+  res_set[r] = pos[first[s]];
 }
 
 void launch_otlp_res_fields(const OtlpResArgs& a, hipStream_t st) {
@@ -682,17 +690,18 @@ void launch_otlp_res_scopes(const OtlpResArgs& a, hipStream_t st) {
 void launch_otlp_res_fix(const OtlpResArgs& a, const OtlpResFix* fix, uint32_t n, hipStream_t st) {
   if (n) hipLaunchKernelGGL(otlp_res_fix_kernel, dim3((n + kOThreads - 1) / kOThreads), dim3(kOThreads), 0, st, a, fix, n);
 }
-void launch_otlp_set_mark(const uint32_t* res_set, uint64_t n_res, uint32_t* used, hipStream_t st) {
-  if (n_res)
-    hipLaunchKernelGGL(otlp_set_mark_kernel, dim3((uint32_t)((n_res + kOThreads - 1) / kOThreads)), dim3(kOThreads), 0, st,
-                       res_set, n_res, used);
+void launch_otlp_set_first(const uint32_t* res_set, uint64_t n_res, uint32_t* first, uint32_t* is_first,
+                           hipStream_t st) {
+  if (!n_res) return;
+  const dim3 g((uint32_t)((n_res + kOThreads - 1) / kOThreads));
+  hipLaunchKernelGGL(otlp_set_min_kernel, g, dim3(kOThreads), 0, st, res_set, n_res, first);
+  hipLaunchKernelGGL(otlp_set_flag_kernel, g, dim3(kOThreads), 0, st, res_set, n_res, first, is_first);
 }
-void launch_otlp_set_apply(uint32_t* res_set, uint64_t n_res, const uint32_t* used, const uint32_t* local,
-                           uint32_t n_sets, uint32_t* list, hipStream_t st) {
-  const uint64_t m = std::max<uint64_t>(n_res, n_sets);
-  if (m)
-    hipLaunchKernelGGL(otlp_set_apply_kernel, dim3((uint32_t)((m + kOThreads - 1) / kOThreads)), dim3(kOThreads), 0, st,
-                       res_set, n_res, used, local, n_sets, list);
+void launch_otlp_set_apply(uint32_t* res_set, uint64_t n_res, const uint32_t* first, const uint32_t* is_first,
+                           const uint32_t* pos, uint32_t* list, hipStream_t st) {
+  if (n_res)
+    hipLaunchKernelGGL(otlp_set_apply_kernel, dim3((uint32_t)((n_res + kOThreads - 1) / kOThreads)), dim3(kOThreads), 0,
+                       st, res_set, n_res, first, is_first, pos, list);
 }
 
 void launch_otlp_scope_count(const OtlpScopeArgs& a, hipStream_t st) {

@@ -348,6 +348,32 @@ def test_gpu_decode_matches_host_columns(seed, odd, cfg):
 
 
 @pytest.mark.gpu
+def test_gpu_resource_walk_cold_warm_and_host(monkeypatch):
+    # the ResourceSpans level on the GPU (otlp_res_fields_kernel): a cold
+    # engine resolves every resource on the host and enters it in the device
+    # table, a second decode finds them all there; both equal the host
+    # columniser and the host ResourceSpans walk (OSE_OTLP_HOST_RESOURCES=1)
+    from odigos_amd.batch import Engine, OtlpBatch
+    td = _http_traces(random.Random(31), 300, odd=0.05)
+    _, hb = _host_columns(CFG, td)
+    pb = to_pb(td)
+    eng = Engine(CFG)
+    for _ in range(2):
+        ob = OtlpBatch(eng, pb)
+        _compare(ob.cols, hb.cols, ob.download())
+        ob.close()
+    monkeypatch.setenv("OSE_OTLP_HOST_RESOURCES", "1")
+    ob = OtlpBatch(eng, pb)
+    _compare(ob.cols, hb.cols, ob.download())
+    # a message of several copies (resources repeated, table hits in one call)
+    td3 = {"resourceSpans": td["resourceSpans"] * 3}
+    _, hb3 = _host_columns(CFG, td3)
+    monkeypatch.delenv("OSE_OTLP_HOST_RESOURCES")
+    ob3 = OtlpBatch(Engine(CFG), to_pb(td3))
+    _compare(ob3.cols, hb3.cols, ob3.download())
+
+
+@pytest.mark.gpu
 def test_gpu_decode_generic_traces():
     # the size test's generator: nested values, random keys, empty ids
     from odigos_amd.batch import Engine, OtlpBatch
