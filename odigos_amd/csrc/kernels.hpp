@@ -456,6 +456,32 @@ struct OtlpResArgs {
   uint32_t* miss_count;        // [1]
   uint32_t* miss_list;         // [n_res]
 };
+// The TracesData chain on the GPU: the message split into segments of
+// kChainSeg bytes; lane t speculates a record start in its segment (as the
+// host walk's find_start does) and walks the top-level fields from it until
+// the first field boundary at or past the next segment.  The host links the
+// segments (a speculated start inside a record converges to the true chain at
+// that record's end, one of the field starts listed) and otlp_chain_list
+// writes the records of each linked segment from its first true field on.
+constexpr uint32_t kChainSeg = 64u << 10;
+constexpr uint32_t kChainList = 16;   // field starts listed per segment
+constexpr uint64_t kChainNone = ~0ull;
+struct OtlpChainArgs {
+  const uint8_t* pb;
+  uint64_t n;
+  uint32_t n_seg;
+  uint64_t* start;      // [n_seg] speculated start (kChainNone: none in the segment)
+  uint64_t* end;        // [n_seg] where the walk stopped (first boundary >= next segment)
+  uint32_t* nrec;       // [n_seg] records (field 1) walked
+  uint32_t* bad;        // [n_seg] the walk met a malformed field (end = where)
+  uint64_t* list;       // [n_seg * kChainList] field starts | (field 1) << 63
+  // pass 2 (linked segments): walk from first[t] (kChainNone: skip), records to res_ref from base[t]
+  const uint64_t* first;
+  const uint32_t* base;
+  uint64_t* res_ref;
+};
+void launch_otlp_chain_seg(const OtlpChainArgs& a, hipStream_t st);
+void launch_otlp_chain_list(const OtlpChainArgs& a, hipStream_t st);
 void launch_otlp_res_fields(const OtlpResArgs& a, hipStream_t st);
 void launch_otlp_res_scopes(const OtlpResArgs& a, hipStream_t st);
 // the host's columns of the missed resources: fix k = {row, svc, svc_str, set, rpart, ok, attr_res}

@@ -189,7 +189,8 @@ struct OtlpBatchImpl {
   // brings them back
   bool layout_on_host = true;
   DevBuf sslab;   // scope-level device arrays
-  DevBuf rslab, setbuf;   // resource-level device arrays; attribute-set compaction (GPU ResourceSpans walk)
+  DevBuf rslab, setbuf, cslab;   // resource-level device arrays; attribute-set compaction; the GPU chain walk
+  uint64_t* d_res_ref = nullptr;   // the ResourceSpans refs (lay.res_ref is filled from it on demand)
   bool res_on_device = false;   // res_scope0 / scope_ref / attr_res live on the device (rslab, sslab)
   uint32_t* d_res_scope0 = nullptr;
   uint64_t* d_scope_ref = nullptr;
@@ -692,9 +693,72 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
                  uint64_t* R_out, uint64_t* S_out, OtlpResArgs* args, bool* redo) {
   *redo = false;
   std::string err;
-  if (!walk_chain(pb, len, w.lay.res_ref, err)) return fail(OSE_EINVAL, err);
-  HIP_TRY(hipStreamSynchronize(st));   // the staging buffer (the message's H2D) is reused below
-  const uint64_t R = w.lay.res_ref.size();
+  int rc;
+  // the TracesData chain: segments walked on the GPU and linked here, or
+  // (OSE_OTLP_HOST_CHAIN=1, or when the link fails) the host walk
+  std::vector<uint64_t> seg_first;
+  std::vector<uint32_t> seg_base;
+  uint64_t R = 0;
+  bool gpu_chain = len > 0 && !getenv("OSE_OTLP_HOST_CHAIN");
+  const uint32_t T = (uint32_t)((len + kChainSeg - 1) / kChainSeg);
+  OtlpChainArgs ca{};
+  if (gpu_chain) {
+    const size_t o_end = up(8 * (size_t)T + 16), o_nrec = o_end + up(8 * (size_t)T + 16),
+                 o_bad = o_nrec + up(4 * (size_t)T + 16), o_list = o_bad + up(4 * (size_t)T + 16),
+                 o_first = o_list + up(8 * (size_t)T * kChainList + 16), o_base = o_first + up(8 * (size_t)T + 16),
+                 o_total = o_base + up(4 * (size_t)T + 16);
+    if ((rc = b->cslab.need(o_total)) || (rc = b->stage.need(o_first))) return rc;
+    HIP_TRY(hipStreamSynchronize(st));   // the staging buffer (the message's H2D) is reused below
+    ca.pb = b->arena.p;
+    ca.n = len;
+    ca.n_seg = T;
+    ca.start = reinterpret_cast<uint64_t*>(b->cslab.p);
+    ca.end = reinterpret_cast<uint64_t*>(b->cslab.p + o_end);
+    ca.nrec = reinterpret_cast<uint32_t*>(b->cslab.p + o_nrec);
+    ca.bad = reinterpret_cast<uint32_t*>(b->cslab.p + o_bad);
+    ca.list = reinterpret_cast<uint64_t*>(b->cslab.p + o_list);
+    ca.first = reinterpret_cast<const uint64_t*>(b->cslab.p + o_first);
+    ca.base = reinterpret_cast<const uint32_t*>(b->cslab.p + o_base);
+    (void)hipGetLastError();
+    launch_otlp_chain_seg(ca, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(b->stage.p, b->cslab.p, o_first, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t* h_start = reinterpret_cast<const uint64_t*>(b->stage.p);
+    const uint64_t* h_end = reinterpret_cast<const uint64_t*>(b->stage.p + o_end);
+    const uint32_t* h_nrec = reinterpret_cast<const uint32_t*>(b->stage.p + o_nrec);
+    const uint32_t* h_bad = reinterpret_cast<const uint32_t*>(b->stage.p + o_bad);
+    const uint64_t* h_list = reinterpret_cast<const uint64_t*>(b->stage.p + o_list);
+    // link: the true chain enters segment t at pos; the segment's walk must
+    // have a field start there (its speculated start, or where a start
+    // inside a record converged), and counts from it
+    seg_first.assign(T, kChainNone);
+    seg_base.assign(T, 0);
+    uint64_t pos = 0;
+    for (uint32_t t = 0; t < T && gpu_chain; t++) {
+      const uint64_t s1 = std::min<uint64_t>(len, (uint64_t)t * kChainSeg + kChainSeg);
+      if (pos >= s1) continue;   // a record covers the whole segment
+      if (h_start[t] == kChainNone) { gpu_chain = false; break; }
+      uint32_t j = 0, skipped = 0;
+      while (j < kChainList && h_list[(uint64_t)t * kChainList + j] != kChainNone &&
+             (h_list[(uint64_t)t * kChainList + j] & ~(1ull << 63)) != pos) {
+        skipped += (uint32_t)(h_list[(uint64_t)t * kChainList + j] >> 63);
+        j++;
+      }
+      if (j == kChainList || h_list[(uint64_t)t * kChainList + j] == kChainNone || h_bad[t]) { gpu_chain = false; break; }
+      seg_first[t] = pos;
+      seg_base[t] = (uint32_t)R;
+      R += h_nrec[t] - skipped;
+      pos = h_end[t];
+    }
+    if (pos != len) gpu_chain = false;   // the host walk decides (and reports a malformed message)
+    if (R > 0xFFFFFFF0ull) gpu_chain = false;
+  }
+  if (!gpu_chain) {
+    if (!walk_chain(pb, len, w.lay.res_ref, err)) return fail(OSE_EINVAL, err);
+    HIP_TRY(hipStreamSynchronize(st));   // the staging buffer (the message's H2D) is reused below
+    R = w.lay.res_ref.size();
+  }
   *R_out = R;
   const uint64_t RN = std::max<uint64_t>(R, 1);
   const uint32_t tiles = (uint32_t)((RN + kScanTileItems - 1) / kScanTileItems);
@@ -711,15 +775,26 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
   };
   size_t total = 0;
   for (auto& p : parts) total = up(total + p.bytes + 16);
-  int rc;
-  if ((rc = b->rslab.need(total)) || (rc = b->stage.need(8 * RN + 64))) return rc;
+  if ((rc = b->rslab.need(total)) || (rc = b->stage.need(std::max<size_t>(8 * RN, 12 * (size_t)T) + 64))) return rc;
   size_t off = 0;
   for (auto& p : parts) {
     *p.dst = b->rslab.p + off;
     off = up(off + p.bytes + 16);
   }
-  if (R) std::memcpy(b->stage.p, w.lay.res_ref.data(), 8 * R);
-  if (R) HIP_TRY(hipMemcpyAsync(const_cast<uint64_t*>(a.res_ref), b->stage.p, 8 * R, hipMemcpyHostToDevice, st));
+  if (gpu_chain) {   // the records of the linked segments, written on the GPU
+    std::memcpy(b->stage.p, seg_first.data(), 8 * (size_t)T);
+    std::memcpy(b->stage.p + 8 * (size_t)T, seg_base.data(), 4 * (size_t)T);
+    HIP_TRY(hipMemcpyAsync(const_cast<uint64_t*>(ca.first), b->stage.p, 8 * (size_t)T, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(const_cast<uint32_t*>(ca.base), b->stage.p + 8 * (size_t)T, 4 * (size_t)T,
+                           hipMemcpyHostToDevice, st));
+    ca.res_ref = const_cast<uint64_t*>(a.res_ref);
+    launch_otlp_chain_list(ca, st);
+    HIP_TRY(hipGetLastError());
+  } else if (R) {
+    std::memcpy(b->stage.p, w.lay.res_ref.data(), 8 * R);
+    HIP_TRY(hipMemcpyAsync(const_cast<uint64_t*>(a.res_ref), b->stage.p, 8 * R, hipMemcpyHostToDevice, st));
+  }
+  b->d_res_ref = const_cast<uint64_t*>(a.res_ref);
   HIP_TRY(hipMemsetAsync(status, 0, reinterpret_cast<uint8_t*>(words) + 64 - reinterpret_cast<uint8_t*>(status), st));
   a.pb = b->arena.p;
   a.n_res = R;
@@ -757,6 +832,10 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
   // the resources the table lacks: resolved on the host
   const uint32_t nm = h[1];
   if (nm) {
+    if (w.lay.res_ref.size() != R) {   // the refs the GPU chain walk wrote
+      w.lay.res_ref.resize(R);
+      HIP_TRY(hipMemcpy(w.lay.res_ref.data(), a.res_ref, 8 * R, hipMemcpyDeviceToHost));
+    }
     std::vector<uint32_t> miss(nm);
     HIP_TRY(hipMemcpy(miss.data(), a.miss_list, 4 * (size_t)nm, hipMemcpyDeviceToHost));
     std::vector<OtlpResFix> fix(nm);
@@ -1022,6 +1101,10 @@ int layout_to_host(OtlpBatchImpl* b, hipStream_t st) {
   b->span_ref.resize(n);
   std::vector<uint32_t> span0(S);
   if (b->res_on_device) {   // the ResourceSpans level was walked on the GPU too
+    if (b->lay.res_ref.size() != R) {
+      b->lay.res_ref.resize(R);
+      if (R) HIP_TRY(hipMemcpyAsync(b->lay.res_ref.data(), b->d_res_ref, 8 * R, hipMemcpyDeviceToHost, st));
+    }
     b->lay.res_scope0.resize(R);
     b->lay.scope_ref.resize(S);
     b->lay.scope_hdr.resize(S);

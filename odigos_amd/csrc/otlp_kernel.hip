@@ -555,6 +555,82 @@ __global__ __launch_bounds__(kOThreads) void otlp_scope_spans_kernel(OtlpScopeAr
   }
 }
 
+// ---- the TracesData chain on the GPU -------------------------------------------------
+// a plausible record start at q: field 1 (0x0A) whose length frames a record
+// whose payload starts with a Resource or ScopeSpans tag, 4 such in a row (or
+// the message end) -- the host walk's find_start (otlp_host.cpp)
+__device__ bool chain_plausible(const uint8_t* pb, uint64_t n, uint32_t q) {
+  uint32_t pos = q;
+  for (int hops = 0; hops < 4 && pos < n; hops++) {
+    Rd r(pb, pos, (uint32_t)n);
+    uint32_t f, wt, ps, pl;
+    if (!r.tag(f, wt) || f != 1 || wt != 2 || !r.len(ps, pl) || pl == 0) return false;
+    const uint32_t b0 = r.br.at(ps);
+    if (b0 != 0x0A && b0 != 0x12) return false;
+    pos = r.i;
+  }
+  return true;
+}
+__global__ __launch_bounds__(kOThreads) void otlp_chain_seg_kernel(OtlpChainArgs a) {
+  const uint32_t t = blockIdx.x * kOThreads + threadIdx.x;
+  if (t >= a.n_seg) return;
+  const uint64_t s0 = (uint64_t)t * kChainSeg, s1 = min<uint64_t>(a.n, s0 + kChainSeg);
+  uint64_t c = kChainNone;
+  if (t == 0) {
+    c = 0;
+  } else {
+    ByteReader br(a.pb);
+    for (uint64_t q = s0; q < s1; q++)
+      if (br.at((uint32_t)q) == 0x0A && chain_plausible(a.pb, a.n, (uint32_t)q)) { c = q; break; }
+  }
+  a.start[t] = c;
+  a.nrec[t] = 0;
+  a.bad[t] = 0;
+  if (c == kChainNone) return;
+  Rd r(a.pb, (uint32_t)c, (uint32_t)a.n);
+  uint32_t k = 0, nrec = 0;
+  while (r.i < s1 && r.i < a.n) {
+    const uint64_t at = r.i;
+    uint32_t f, wt;
+    if (!r.tag(f, wt)) break;
+    const bool rec = f == 1 && wt == 2;
+    if (k < kChainList) a.list[(uint64_t)t * kChainList + k] = at | ((uint64_t)rec << 63);
+    k++;
+    if (!r.skip(wt)) break;
+    nrec += rec;
+  }
+  for (; k < kChainList; k++) a.list[(uint64_t)t * kChainList + k] = kChainNone;
+  a.bad[t] = r.bad ? 1u : 0u;
+  a.end[t] = r.i;
+  a.nrec[t] = nrec;
+}
+__global__ __launch_bounds__(kOThreads) void otlp_chain_list_kernel(OtlpChainArgs a) {
+  const uint32_t t = blockIdx.x * kOThreads + threadIdx.x;
+  if (t >= a.n_seg || a.first[t] == kChainNone) return;
+  const uint64_t s1 = min<uint64_t>(a.n, (uint64_t)t * kChainSeg + kChainSeg);
+  Rd r(a.pb, (uint32_t)a.first[t], (uint32_t)a.n);
+  uint64_t q = a.base[t];
+  while (r.i < s1 && r.i < a.n) {
+    uint32_t f, wt;
+    if (!r.tag(f, wt)) break;
+    if (f == 1 && wt == 2) {
+      uint32_t ps, pl;
+      if (!r.len(ps, pl)) break;
+      a.res_ref[q++] = (uint64_t)ps | ((uint64_t)pl << 32);
+    } else if (!r.skip(wt)) {
+      break;
+    }
+  }
+}
+void launch_otlp_chain_seg(const OtlpChainArgs& a, hipStream_t st) {
+  if (a.n_seg)
+    hipLaunchKernelGGL(otlp_chain_seg_kernel, dim3((a.n_seg + kOThreads - 1) / kOThreads), dim3(kOThreads), 0, st, a);
+}
+void launch_otlp_chain_list(const OtlpChainArgs& a, hipStream_t st) {
+  if (a.n_seg)
+    hipLaunchKernelGGL(otlp_chain_list_kernel, dim3((a.n_seg + kOThreads - 1) / kOThreads), dim3(kOThreads), 0, st, a);
+}
+
 // ---- ResourceSpans on the GPU ------------------------------------------------------
 // Pass 1, one lane per ResourceSpans (otlp_pb.cpp pb_walk's ResourceSpans
 // loop): Resource (1), scope_spans (2), the deprecated

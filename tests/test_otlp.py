@@ -371,6 +371,33 @@ def test_gpu_resource_walk_cold_warm_and_host(monkeypatch):
     monkeypatch.delenv("OSE_OTLP_HOST_RESOURCES")
     ob3 = OtlpBatch(Engine(CFG), to_pb(td3))
     _compare(ob3.cols, hb3.cols, ob3.download())
+    # the TracesData chain walked on the host (OSE_OTLP_HOST_CHAIN=1) equals the GPU's
+    monkeypatch.setenv("OSE_OTLP_HOST_CHAIN", "1")
+    ob4 = OtlpBatch(Engine(CFG), to_pb(td3))
+    _compare(ob4.cols, hb3.cols, ob4.download())
+
+
+@pytest.mark.gpu
+def test_gpu_chain_walk_records_over_segments():
+    # ResourceSpans records larger than the GPU chain walk's 64 KiB segments
+    # (whole segments inside one record) between small ones, and a message
+    # whose bytes end inside a record (malformed: the host walk reports it)
+    from odigos_amd.batch import Engine, OtlpBatch
+    rng = random.Random(41)
+    td = _http_traces(rng, 120)
+    rss = td["resourceSpans"]
+    big = host.resource_spans({"service.name": "big", "k8s.pod.name": "pod-0"},
+                              [sp for r in rss[:40] for ss in r["scopeSpans"] for sp in ss["spans"]] * 30)
+    td2 = host.traces(*(rss[40:80] + [big] + rss[80:] + [big]))
+    pb = to_pb(td2)
+    assert len(pb) > 3 * (64 << 10)
+    _, hb = _host_columns(CFG, td2)
+    eng = Engine(CFG)
+    ob = OtlpBatch(eng, pb)
+    _compare(ob.cols, hb.cols, ob.download())
+    with pytest.raises(native.OseError) as ei:
+        OtlpBatch(eng, pb[: len(pb) - 1000])
+    assert ei.value.code == native.OSE_EINVAL
 
 
 @pytest.mark.gpu
