@@ -290,15 +290,21 @@ class PinnedBatch:
     __del__ = close
 
 
-def take_otlp_out(L, h, copy: bool = True, timings: list | None = None) -> list:
+def take_otlp_out(L, h, copy: bool = True, timings: list | None = None, path: dict | None = None) -> list:
     """The outputs of an ose_otlp_out (then released); copy=False gives the
     byte counts instead of the bytes; `timings` receives the encoder's phase
-    times (ms: decisions D2H, sizing pass, buffers, writing pass)."""
+    times (ms: decisions D2H, sizing pass, buffers, writing pass); `path`
+    whether the GPU encoder wrote them ("gpu") and why it handed the call to
+    the host encoder ("fallback", kEncFb* bits)."""
     try:
         if timings is not None:
             t = (C.c_double * 4)()
             native.check(L.osehost_otlp_out_timings(h, t))
             timings[:] = list(t)
+        if path is not None:
+            fb = C.c_uint32()
+            path["gpu"] = bool(L.osehost_otlp_out_path(h, C.byref(fb)))
+            path["fallback"] = fb.value
         res = []
         for k in range(L.ose_otlp_out_count(h)):
             name, data, n, nres = C.c_char_p(), C.c_void_p(), C.c_uint64(), C.c_uint32()
@@ -491,7 +497,8 @@ class OtlpBatch:
         native.check(self.L.ose_otlp_encode(self.eng.h, self.h, C.byref(self.outs), stages, group_mode,
                                             router.h if router is not None else None, s, C.byref(h)))
         self.encode_ms = []
-        return take_otlp_out(self.L, h, copy, self.encode_ms)
+        self.encode_path = {}
+        return take_otlp_out(self.L, h, copy, self.encode_ms, self.encode_path)
 
     def close(self):
         if getattr(self, "h", None):

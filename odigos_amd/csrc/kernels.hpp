@@ -501,6 +501,81 @@ void launch_otlp_set_apply(uint32_t* res_set, uint64_t n_res, const uint32_t* fi
 void launch_otlp_scope_count(const OtlpScopeArgs& a, hipStream_t st);
 void launch_otlp_scope_spans(const OtlpScopeArgs& a, hipStream_t st);
 
+// OTLP re-encode on the GPU (encode_kernel.hip): the
+// sizing and writing passes of otlp_encode.cpp over the message bytes and
+// the decisions, both already in HBM.  Resources are routed on the device
+// (odigosrouterconnector's key from the Resource's attributes, looked up in
+// an FNV-1a table of the router's keys).  What the device path does not
+// write exactly as the host encoder would — a span, scope or resource whose
+// encoding is not already pdata's, a method needing AsString, fields out of
+// order, a merged Resource — sets a flag, and the call goes to the host
+// encoder instead.
+constexpr uint64_t kEncDropped = ~0ull;
+constexpr uint64_t kEncNoHdr = ~0ull;            // res_hdr / scope header: absent ("0A 00")
+constexpr uint32_t kEncTiles = 1024;             // resources per scan tile
+enum : uint32_t {
+  kEncFbSpan = 1,       // a rewritten span pdata would re-marshal, or an AsString method
+  kEncFbScope = 2,      // a scope header not in pdata's encoding / merged
+  kEncFbRes = 4,        // a resource header not in pdata's encoding / merged / malformed
+  kEncFbTmpl = 8,       // a template reference beyond the arena (the host reports it)
+  kEncFbRoute = 16,     // a routing attribute the device does not read exactly
+};
+struct EncEdit {        // one rewritten span (otlp_encode.cpp Edit)
+  uint32_t name_a, name_b, attr_a, attr_b;
+  uint32_t meth_off, meth_len;   // the method string in the message
+  uint32_t tmpl_off, tmpl_len;   // the template in the template arena
+  uint32_t out_len;              // edited span bytes
+  uint32_t flags;                // url_out | client << 8
+};
+struct EncRouteSlot {   // router key "ns/kind/name" -> pipelines; klen == ~0: empty
+  uint64_t h;
+  uint32_t koff, klen;
+  uint64_t mask;
+};
+struct EncArgs {
+  const uint8_t* pb;
+  uint64_t n_spans, n_scopes, n_res;
+  const uint64_t* span_ref;
+  const uint32_t* span_size;
+  const uint8_t* keep;           // NULL: every span kept
+  const uint8_t* url_out;        // NULL: no template stage
+  const ose_strref* tmpl;
+  const uint8_t* tmpl_arena;
+  const uint64_t* tmpl_used;
+  const uint32_t* scope_span0;
+  const uint64_t* scope_hdr;     // InstrumentationScope ref (0: none, kOtlpScopeMulti: merged)
+  const uint64_t* scope_schema;
+  const uint32_t* scope_size;    // the decoder's pdata size of the scope's fixed part
+  const uint64_t* res_ref;
+  const uint32_t* res_scope0;
+  const uint32_t* res_size;      // the decoder's pdata size of the resource's fixed part
+  uint32_t n_out;                // router pipelines + 1 (default), or 1
+  uint32_t route_bits;           // log2 of the route table's slots (0: no router)
+  const EncRouteSlot* routes;
+  const uint8_t* route_keys;
+  // sizing pass
+  uint32_t* span_out;            // framed bytes of span i in its scope (0: dropped)
+  EncEdit* edit;
+  uint64_t* scope_body;          // kEncDropped: removed
+  uint64_t* res_body;
+  uint64_t* res_rec;             // framed record bytes (0: dropped)
+  uint64_t* res_mask;            // outputs the resource goes to
+  uint64_t* res_hdr;             // Resource payload ref, kEncNoHdr: absent
+  uint64_t* res_schema;          // ResourceSpans.schema_url ref (length 0: none)
+  uint32_t* flags;               // [1] OR of kEncFb*
+  // scans: offsets per output, then the writing pass
+  uint64_t* tile_sum;            // [n_out][tiles] bytes, then [n_out][tiles] counts
+  uint64_t* off;                 // [n_out][n_res]
+  uint64_t* out_total;           // [n_out] bytes, then [n_out] resource counts
+  const uint64_t* out_base;      // [n_out]
+  uint8_t* out;
+};
+void launch_enc_spans(const EncArgs& a, hipStream_t st);
+void launch_enc_scopes(const EncArgs& a, hipStream_t st);
+void launch_enc_resources(const EncArgs& a, hipStream_t st);
+void launch_enc_scan(const EncArgs& a, hipStream_t st);
+void launch_enc_write(const EncArgs& a, hipStream_t st);
+
 struct OtlpFix {
   uint64_t idx;
   uint64_t hi, lo, start, end, attr_match;

@@ -32,6 +32,7 @@
 #include <thread>
 
 #include "engine_internal.hpp"
+#include "kernels.hpp"
 #include "otlp_pb.hpp"
 #include "taskpool.hpp"
 
@@ -61,6 +62,8 @@ std::string ci_str(const Json& o, const char* key) {
   return v && v->is_str() ? v->s : std::string();
 }
 }  // namespace
+
+void build_route_blob(Router& r);
 
 std::string build_router(const Json& cfg, const std::string& signal, Router& r) {
   r = Router{};
@@ -106,7 +109,36 @@ std::string build_router(const Json& cfg, const std::string& signal, Router& r) 
       }
     }
   }
+  build_route_blob(r);
   return "";
+}
+
+// Router::dev_blob (encode_kernel.hip route_resource)
+void build_route_blob(Router& r) {
+  r.dev_blob.clear();
+  r.route_bits = 0;
+  r.dev_slots_bytes = 0;
+  if (r.pipelines.size() > 63) return;   // the encoders refuse such a router
+  uint32_t bits = 1;
+  while ((size_t(1) << bits) < 2 * r.routes.size() + 2) bits++;
+  const size_t slots = size_t(1) << bits;
+  std::vector<EncRouteSlot> tab(slots, EncRouteSlot{0, 0, ~0u, 0});
+  std::string keys;
+  for (auto& kv : r.routes) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (unsigned char c : kv.first) h = (h ^ c) * 0x100000001b3ull;
+    uint64_t mask = 0;
+    for (uint32_t p : kv.second) mask |= 1ull << p;
+    size_t s = (size_t)h & (slots - 1);
+    while (tab[s].klen != ~0u) s = (s + 1) & (slots - 1);
+    tab[s] = EncRouteSlot{h, (uint32_t)keys.size(), (uint32_t)kv.first.size(), mask};
+    keys += kv.first;
+  }
+  r.route_bits = bits;
+  r.dev_slots_bytes = slots * sizeof(EncRouteSlot);
+  r.dev_blob.resize(r.dev_slots_bytes + keys.size() + 16, 0);
+  std::memcpy(r.dev_blob.data(), tab.data(), r.dev_slots_bytes);
+  std::memcpy(r.dev_blob.data() + r.dev_slots_bytes, keys.data(), keys.size());
 }
 
 const std::vector<uint32_t>* Router::route(const AttrMap& attrs, std::string* key) const {
@@ -603,19 +635,42 @@ struct EncodeWork {
   std::vector<uint64_t> res_body, res_schema, scope_body;
   std::vector<const enc::ResHdr*> res_hdr;
   std::vector<const std::string*> scope_hdr;
-  std::vector<std::pair<uint8_t*, size_t>> bufs;   // free output buffers
+  std::vector<std::pair<uint8_t*, size_t>> bufs;     // free output buffers
+  std::vector<std::pair<uint8_t*, size_t>> pinned;   // free pinned output buffers (the GPU encoder's)
   ~EncodeWork() {
     for (auto& b : bufs) std::free(b.first);
+    for (auto& b : pinned) (void)hipHostFree(b.first);
   }
 };
 EncodeWork* encode_work_new() { return new EncodeWork(); }
 void encode_work_free(EncodeWork* w) { delete w; }
 
+uint8_t* encode_work_pinned(EncodeWork& w, size_t need, size_t* cap) {
+  need = std::max<size_t>(need, 64);
+  size_t best = w.pinned.size();
+  for (size_t k = 0; k < w.pinned.size(); k++)
+    if (w.pinned[k].second >= need && (best == w.pinned.size() || w.pinned[k].second < w.pinned[best].second)) best = k;
+  if (best < w.pinned.size()) {
+    uint8_t* p = w.pinned[best].first;
+    *cap = w.pinned[best].second;
+    w.pinned.erase(w.pinned.begin() + (ptrdiff_t)best);
+    return p;
+  }
+  const size_t c = need + need / 8;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  *cap = c;
+  return static_cast<uint8_t*>(p);
+}
+
 void otlp_out_release(OtlpOut* o) {
   if (!o) return;
   if (o->work) {
     for (auto& x : o->outs)
-      if (x.data) o->work->bufs.emplace_back(x.data, x.cap);
+      if (x.data) (x.pinned ? o->work->pinned : o->work->bufs).emplace_back(x.data, x.cap);
     o->outs.clear();
     if (o->e && !o->e->closed.load()) {
       std::lock_guard<std::mutex> g(o->e->mu);
@@ -791,6 +846,15 @@ int osehost_otlp_out_timings(const ose_otlp_out* o, double* ms4) {
   if (!o || !ms4) return fail(OSE_EINVAL, "NULL argument");
   std::memcpy(ms4, reinterpret_cast<const OtlpOut*>(o)->t_ms, sizeof(double) * 4);
   return 0;
+}
+
+// diagnostics: 1 when the GPU encoder wrote the outputs; *fallback: why the
+// GPU encoder handed the call to the host (kEncFb* bits, 0 when it did not run)
+int osehost_otlp_out_path(const ose_otlp_out* o, uint32_t* fallback) {
+  if (!o) return fail(OSE_EINVAL, "NULL argument");
+  const OtlpOut* x = reinterpret_cast<const OtlpOut*>(o);
+  if (fallback) *fallback = x->fallback;
+  return x->gpu;
 }
 
 // Test seams (CPU).  A router for any signal (the KATs route logs and

@@ -34,6 +34,12 @@ struct Router {
   // NULL when the resource routes to the default pipeline; *key gets the
   // routing key when one matched
   const std::vector<uint32_t>* route(const AttrMap& attrs, std::string* key = nullptr) const;
+  // the routes as the GPU encoder reads them (EncRouteSlot[1 << route_bits],
+  // then the key bytes; FNV-1a 64 of the key, linear probing), built with
+  // the router
+  std::vector<uint8_t> dev_blob;
+  uint32_t route_bits = 0;
+  size_t dev_slots_bytes = 0;
 };
 // {"datastreams": [{"name", "sources": [{"namespace", "kind", "name"}],
 //   "destinations": [{"destinationname", "configuredsignals": [...]}]}]}
@@ -53,8 +59,9 @@ struct EncodeDecisions {
 
 struct EncodedOutput {
   std::string name;
-  uint8_t* data = nullptr;   // malloc'd, from the workspace's buffers
+  uint8_t* data = nullptr;   // malloc'd (or pinned), from the workspace's buffers
   size_t cap = 0;
+  bool pinned = false;       // hipHostMalloc'd (the GPU encoder's D2H target)
   uint64_t len = 0;
   uint32_t n_resources = 0;
 };
@@ -65,6 +72,9 @@ struct EncodedOutput {
 struct EncodeWork;
 EncodeWork* encode_work_new();
 void encode_work_free(EncodeWork* w);
+// a pinned host buffer of at least `need` bytes from the workspace's pool
+// (NULL when hipHostMalloc fails); it goes back to the pool with the output
+uint8_t* encode_work_pinned(EncodeWork& w, size_t need, size_t* cap);
 
 struct Engine;
 struct OtlpOut {   // ose_otlp_out
@@ -72,6 +82,8 @@ struct OtlpOut {   // ose_otlp_out
   EncodeWork* work = nullptr;   // the outputs' buffers go back to it
   Engine* e = nullptr;          // whose pool the workspace returns to (NULL: freed)
   double t_ms[4] = {0, 0, 0, 0};   // decisions D2H, sizing pass, buffers, writing pass
+  int gpu = 0;                     // 1: written by the GPU encoder (encode_kernel.hip)
+  uint32_t fallback = 0;           // why the GPU encoder handed the call to the host (kEncFb*)
 };
 void otlp_out_release(OtlpOut* o);
 

@@ -199,7 +199,12 @@ struct OtlpBatchImpl {
   uint32_t *d_span_res = nullptr, *d_span0 = nullptr;
   uint64_t *d_hdr = nullptr, *d_schema = nullptr;
   OtlpScopeArgs sargs{};   // the GPU scope walk's arrays (pass 2 reuses them)
-  OtlpBatchImpl() { stage.host = true; }
+  // the GPU encoder (encode_kernel.hip): the span refs in HBM (always), the
+  // scope level there when the GPU walked it; its workspace and outputs
+  uint64_t* d_spans = nullptr;
+  bool scopes_dev = false;
+  DevBuf eslab, eout, emisc;
+  OtlpBatchImpl() { stage.host = true; emisc.host = true; }
 };
 
 
@@ -1187,10 +1192,12 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   c = ose_columns{};
   c.n_resources = (uint32_t)R;
   uint64_t n = 0;
+  b->scopes_dev = false;
   if (gpu_scopes) {
     bool redo = false;
     if ((rc = scope_walk_gpu(e, b, w, st, &n, &redo, gpu_res ? &ra : nullptr, S))) return rc;
     if (redo) return decode(e, pb, len, st, b, true, true);   // a scope needs the host walk: all on the host
+    b->scopes_dev = true;
   } else {
     n = w.span_ref.size();
     b->span_ref = std::move(w.span_ref);
@@ -1281,6 +1288,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     b->d_span_res = const_cast<uint32_t*>(c.resource);
     b->span_ref.clear();
   }
+  b->d_spans = span_ref;
   c.n_spans = n;
   c.n_resources = (uint32_t)R;
   c.n_scopes = (uint32_t)S;
@@ -1435,6 +1443,180 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));   // fixdev and the staging are reused / freed
   lap(4);
+  return 0;
+}
+}  // namespace
+
+// ---- the GPU encoder (encode_kernel.hip) -------------------------------------------
+namespace {
+// 0 with *host false: *o holds the outputs; 0 with *host true: the host
+// encoder takes the call (o->fallback says why); else an error code
+int encode_gpu(OtlpBatchImpl* b, const ose_outputs* outs, bool sampled, bool tmpl, const Router* router,
+               hipStream_t st, OtlpOut* o, bool* host) {
+  *host = true;
+  const char* env = getenv("OSE_ENCODE_HOST");   // diagnostics: the host encoder always
+  if (env && env[0] == '1') return 0;
+  if (router && router->pipelines.size() > 63) return 0;   // the host encoder reports it
+  const uint64_t n = b->cols.n_spans, S = b->cols.n_scopes, R = b->cols.n_resources;
+  if (!b->d_spans) return 0;
+  const uint32_t n_out = router ? (uint32_t)router->pipelines.size() + 1 : 1;
+  const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (R + kEncTiles - 1) / kEncTiles);
+  // workspace
+  EncArgs a{};
+  const size_t blob = router ? router->dev_blob.size() : 0;
+  struct Part { void** dst; size_t bytes; };
+  uint64_t* flags64 = nullptr;
+  uint32_t *scope_span0 = nullptr, *res_scope0 = nullptr;
+  uint64_t *scope_hdr = nullptr, *scope_schema = nullptr, *res_ref = nullptr;
+  uint8_t* routes = nullptr;
+  uint64_t* out_base = nullptr;
+  std::vector<Part> parts = {
+      {(void**)&a.span_out, 4 * n},
+      {(void**)&a.scope_body, 8 * S},
+      {(void**)&a.res_body, 8 * R},
+      {(void**)&a.res_rec, 8 * R},
+      {(void**)&a.res_mask, 8 * R},
+      {(void**)&a.res_hdr, 8 * R},
+      {(void**)&a.res_schema, 8 * R},
+      {(void**)&flags64, 8},
+      {(void**)&a.tile_sum, 16 * (size_t)n_out * tiles},
+      {(void**)&a.off, 8 * (size_t)n_out * R},
+      {(void**)&a.out_total, 16 * (size_t)n_out},
+      {(void**)&out_base, 8 * (size_t)n_out},
+  };
+  if (tmpl) parts.push_back({(void**)&a.edit, sizeof(EncEdit) * n});
+  if (blob) parts.push_back({(void**)&routes, blob});
+  // the layout arrays the decoder left on the host go up
+  const bool up_scopes = !b->scopes_dev, up_res = !b->res_on_device;
+  if (up_scopes) {
+    parts.push_back({(void**)&scope_span0, 4 * S});
+    parts.push_back({(void**)&scope_hdr, 8 * S});
+    parts.push_back({(void**)&scope_schema, 8 * S});
+  }
+  if (up_res) {
+    parts.push_back({(void**)&res_ref, 8 * R});
+    parts.push_back({(void**)&res_scope0, 4 * R});
+  }
+  size_t total = 0;
+  for (auto& p : parts) total = up(total + p.bytes + 16);
+  int rc;
+  if ((rc = b->eslab.need(total))) return rc;
+  size_t off = 0;
+  for (auto& p : parts) {
+    *p.dst = b->eslab.p + off;
+    off = up(off + p.bytes + 16);
+  }
+  // host-side uploads through pinned staging: route table, layout, offsets
+  size_t hbytes = 64 + 16 * (size_t)n_out + 8 * (size_t)n_out + 16 + blob + 16;
+  if (up_scopes) hbytes += 20 * S + 64;
+  if (up_res) hbytes += 12 * R + 64;
+  if ((rc = b->emisc.need(hbytes))) return rc;
+  uint8_t* h = b->emisc.p;
+  size_t ho = up(64 + 16 * (size_t)n_out, 16);   // [0, 64): flags; then the totals
+  auto upload = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (!bytes) return 0;
+    std::memcpy(h + ho, src, bytes);
+    HIP_TRY(hipMemcpyAsync(dst, h + ho, bytes, hipMemcpyHostToDevice, st));
+    ho = up(ho + bytes, 16);
+    return 0;
+  };
+  if (up_scopes && (b->lay.scope_span0.size() != S || b->lay.scope_hdr.size() != S || b->lay.scope_schema.size() != S))
+    return 0;
+  if (up_res && (b->lay.res_ref.size() != R || b->lay.res_scope0.size() != R)) return 0;
+  if (blob && (rc = upload(routes, router->dev_blob.data(), blob))) return rc;
+  if (up_scopes) {
+    std::vector<uint32_t> s0(b->lay.scope_span0.begin(), b->lay.scope_span0.end());
+    if ((rc = upload(scope_span0, s0.data(), 4 * S)) || (rc = upload(scope_hdr, b->lay.scope_hdr.data(), 8 * S)) ||
+        (rc = upload(scope_schema, b->lay.scope_schema.data(), 8 * S)))
+      return rc;
+  }
+  if (up_res &&
+      ((rc = upload(res_ref, b->lay.res_ref.data(), 8 * R)) || (rc = upload(res_scope0, b->lay.res_scope0.data(), 4 * R))))
+    return rc;
+  a.pb = b->arena.p;
+  a.n_spans = n;
+  a.n_scopes = S;
+  a.n_res = R;
+  a.span_ref = b->d_spans;
+  a.span_size = b->cols.span_size;
+  a.keep = sampled ? outs->keep : nullptr;
+  if (tmpl) {
+    a.url_out = outs->url_out;
+    a.tmpl = outs->tmpl;
+    a.tmpl_arena = outs->tmpl_arena;
+    a.tmpl_used = outs->tmpl_arena_used;
+  }
+  a.scope_span0 = up_scopes ? scope_span0 : b->d_span0;
+  a.scope_hdr = up_scopes ? scope_hdr : b->d_hdr;
+  a.scope_schema = up_scopes ? scope_schema : b->d_schema;
+  a.scope_size = b->cols.scope_size;
+  a.res_ref = up_res ? res_ref : b->d_res_ref;
+  a.res_scope0 = up_res ? res_scope0 : b->d_res_scope0;
+  a.res_size = b->cols.res_size;
+  a.n_out = n_out;
+  a.route_bits = router ? router->route_bits : 0;
+  a.routes = reinterpret_cast<const EncRouteSlot*>(routes);
+  a.route_keys = routes ? routes + router->dev_slots_bytes : nullptr;
+  a.flags = reinterpret_cast<uint32_t*>(flags64);
+  a.out_base = out_base;
+  if ((n && !a.span_size) || (S && (!a.scope_span0 || !a.scope_hdr || !a.scope_schema || !a.scope_size)) ||
+      (R && (!a.res_ref || !a.res_scope0 || !a.res_size)))
+    return 0;
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now();
+  // sizing pass, offsets
+  HIP_TRY(hipMemsetAsync(flags64, 0, 8, st));
+  launch_enc_spans(a, st);
+  HIP_TRY(hipGetLastError());
+  launch_enc_scopes(a, st);
+  HIP_TRY(hipGetLastError());
+  launch_enc_resources(a, st);
+  HIP_TRY(hipGetLastError());
+  launch_enc_scan(a, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(h, flags64, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(h + 64, a.out_total, 16 * (size_t)n_out, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  uint32_t fb;
+  std::memcpy(&fb, h, 4);
+  o->fallback = fb;
+  o->t_ms[1] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  t0 = clk::now();
+  if (fb) return 0;
+  std::vector<uint64_t> tot(2 * (size_t)n_out);
+  std::memcpy(tot.data(), h + 64, 16 * (size_t)n_out);
+  std::vector<uint64_t> base(n_out);
+  uint64_t all = 0;
+  for (uint32_t k = 0; k < n_out; k++) {
+    base[k] = all;
+    all = up(all + tot[k], 16);
+  }
+  if ((rc = b->eout.need(all + 16))) return rc;
+  a.out = b->eout.p;
+  if ((rc = upload(out_base, base.data(), 8 * (size_t)n_out))) return rc;
+  // host buffers (pinned, pooled with the workspace)
+  o->outs.assign(n_out, EncodedOutput{});
+  bool oom = false;
+  for (uint32_t k = 0; k < n_out; k++) {
+    EncodedOutput& x = o->outs[k];
+    x.name = router ? (k + 1 < n_out ? router->pipelines[k] : std::string("default")) : std::string();
+    x.len = tot[k];
+    x.n_resources = (uint32_t)tot[n_out + k];
+    x.data = encode_work_pinned(*o->work, x.len, &x.cap);
+    x.pinned = true;
+    oom |= x.data == nullptr;
+  }
+  if (oom) return fail(OSE_EDEVICE, "out of pinned host memory for the encoder outputs");
+  o->t_ms[2] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  t0 = clk::now();
+  launch_enc_write(a, st);
+  HIP_TRY(hipGetLastError());
+  for (uint32_t k = 0; k < n_out; k++)
+    if (tot[k]) HIP_TRY(hipMemcpyAsync(o->outs[k].data, a.out + base[k], tot[k], hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  o->t_ms[3] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  o->gpu = 1;
+  *host = false;
   return 0;
 }
 }  // namespace
@@ -1608,6 +1790,30 @@ int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   const auto t_start = std::chrono::steady_clock::now();
   const uint64_t n = b->cols.n_spans;
+  uint32_t gpu_fallback = 0;
+  if (!batch_mode) {   // the GPU encoder (OSE_GROUP_BATCH's all-or-nothing stays with the host)
+    auto* o = new OtlpOut();
+    o->e = e;
+    engine_retain(e);   // dropped by otlp_out_release
+    {
+      std::lock_guard<std::mutex> g(e->mu);
+      if (!e->enc_pool.empty()) {
+        o->work = static_cast<EncodeWork*>(e->enc_pool.back());
+        e->enc_pool.pop_back();
+      }
+    }
+    if (!o->work) o->work = encode_work_new();
+    bool host = true;
+    const int rc = encode_gpu(b, outs, sampled, tmpl, reinterpret_cast<const Router*>(router), st, o, &host);
+    if (rc || host) {
+      gpu_fallback = o->fallback;
+      otlp_out_release(o);   // pinned buffers taken before a failure go back to the work's pool
+      if (rc) return rc;
+    } else {
+      *out = reinterpret_cast<ose_otlp_out*>(o);
+      return 0;
+    }
+  }
   // the decisions and the decoder's span sizes, D2H into the batch's pinned staging
   const size_t o_keep = 0, o_url = up(n + 16), o_tmpl = o_url + up(n + 16), o_size = o_tmpl + up(8 * n + 16),
                o_misc = o_size + up(4 * n + 16), o_arena = o_misc + 256;
@@ -1661,6 +1867,7 @@ int ose_otlp_encode(ose_engine* eng, const ose_otlp_batch* bb, const ose_outputs
     }
   }
   if (!o->work) o->work = encode_work_new();
+  o->fallback = gpu_fallback;
   o->t_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   std::string err;
   if (!encode_traces(b->pb, b->pb_len, b->span_ref, b->lay, d, reinterpret_cast<const Router*>(router),

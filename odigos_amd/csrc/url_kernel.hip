@@ -451,8 +451,8 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // ds_read_b128).  Built cooperatively, 32 bytes per lane, branch-free.
 // Classes 0-7 are read for every segment; 8-11 (the email classes) only for
 // segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
-#ifndef OSE_URL_SWZ
-#define OSE_URL_SWZ 0     // swizzled row reads in build_row: measured slower (C4 url_plan 7.20 vs 6.87 ms with both off)
+#ifndef OSE_URL_ROWMUL
+#define OSE_URL_ROWMUL 0  // A/B: the round-2 row build (a movemask multiply per class and dword): C4 url_plan 6.87 vs 6.19 ms
 #endif
 #ifndef OSE_URL_RDMASK
 #define OSE_URL_RDMASK 0  // skip bitmap rows past a segment / path: measured slower (the extra branches cost more than the reads)
@@ -468,26 +468,39 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
 typedef const __attribute__((address_space(3))) u32x4 lds_cu4;
 
-// SWAR high-bit mask (bits 7,15,23,31) -> 4-bit mask
-__device__ __forceinline__ uint32_t movemask4(uint32_t m) { return (((m >> 7) * 0x204081u) >> 21) & 0xFu; }
+// 4x4 byte transpose: out[d] byte j = in[j] byte d (v_perm_b32 picks any 4
+// bytes of the pair {hi, lo}: selector 0-3 lo's bytes, 4-7 hi's)
+__device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t* out) {
+  const uint32_t t0 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);   // a0.b0 a1.b0 a0.b1 a1.b1
+  const uint32_t t1 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);   // a0.b2 a1.b2 a0.b3 a1.b3
+  const uint32_t t2 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+  const uint32_t t3 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+  out[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+  out[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+  out[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+  out[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
 
+// One 32-byte row.  The row's bytes are regrouped so that dword d holds bytes
+// d, d + 8, d + 16, d + 24 (two 4x4 byte transposes): a class's SWAR mask of
+// dword d then has byte 8j + d's bit at bit 8j + 7, and shifting it right by
+// 7 - d puts it at bit 8j + d, its place in the row's 32-bit class word.  So
+// a class costs one shift and an OR per dword instead of a movemask (a
+// 32-bit multiply) per dword.
 __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t r) {
   {
     uint32_t acc[kClasses];
 #pragma unroll
     for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
     const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
-#if OSE_URL_SWZ
-    // rows r and r + 8 read their two halves in opposite order: the 32-byte
-    // row stride alone puts them on the same ds_read_b128 banks (2-way)
-    const uint32_t sw = (r >> 3) & 1u;
-    const u32x4 v0 = src[sw], v1 = src[sw ^ 1u];
-    const uint32_t dsh = sw << 4;   // xs[d] is row dword d ^ 4sw: its bits go to 4d ^ 16sw
-#else
     const u32x4 v0 = src[0], v1 = src[1];
-    const uint32_t dsh = 0;
+    uint32_t xs[8];
+#if OSE_URL_ROWMUL
+    xs[0] = v0.x; xs[1] = v0.y; xs[2] = v0.z; xs[3] = v0.w; xs[4] = v1.x; xs[5] = v1.y; xs[6] = v1.z; xs[7] = v1.w;
+#else
+    transpose4(v0.x, v0.z, v1.x, v1.z, xs);       // bytes d, d+8, d+16, d+24 for d = 0..3
+    transpose4(v0.y, v0.w, v1.y, v1.w, xs + 4);   // d = 4..7
 #endif
-    const uint32_t xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
     for (int d = 0; d < 8; d++) {
       const uint32_t x = xs[d];
@@ -521,7 +534,11 @@ __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t
           ~alpha & kH,                                     // C_NAL
       };
 #pragma unroll
-      for (int c = 0; c < (int)kClasses; c++) acc[c] |= movemask4(m[c]) << ((4 * d) ^ dsh);
+#if OSE_URL_ROWMUL
+      for (int c = 0; c < (int)kClasses; c++) acc[c] |= ((((m[c] >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * d);
+#else
+      for (int c = 0; c < (int)kClasses; c++) acc[c] = (acc[c] >> 1) | m[c];   // after d = 7: dword d's bits at 8j + d
+#endif
     }
     bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
     bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
@@ -1388,8 +1405,8 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       }
 #else
       if (slash) img[pos] = '/';
-      const lds_u8* sp = L + so;
       lds_out_u8* dp = img + pos + 1;
+      const lds_u8* sp = L + so;
       for (uint32_t q = 0; q < n; q += 8) {
         uint32_t b[8];
 #pragma unroll

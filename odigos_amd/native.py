@@ -199,6 +199,7 @@ def lib() -> C.CDLL:
         "osehost_router_create_signal": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(_p)]),
         "osehost_router_route": (_p, [_p, C.c_char_p]),
         "osehost_otlp_out_timings": (C.c_int, [_p, C.POINTER(C.c_double)]),
+        "osehost_otlp_out_path": (C.c_int, [_p, C.POINTER(C.c_uint32)]),
         "osehost_parse_duration": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
         "osehost_resource_sizes": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
         "osehost_as_string": (_p, [C.c_char_p]),

@@ -344,6 +344,7 @@ def test_gpu_encode_generated_batch():
     arena = ob.out_numpy("tmpl_arena", n=ob.used()).tobytes()
     assert 0 < keep.sum() < n and (url_out != 0).sum() > n // 10
     got = ob.encode(st)
+    assert ob.encode_path == {"gpu": True, "fallback": 0}   # written by the GPU encoder
     L = native.lib()
     arena_a = np.frombuffer(arena + b"\0" * 16, dtype=np.uint8).copy()
     refs_a = np.ascontiguousarray(refs)
@@ -389,3 +390,87 @@ def test_encode_concurrent_callers():
     for t in th:
         t.join()
     assert not errs
+
+
+def _routable_gpu(td, rng):
+    """_routable, plus routing attributes the device must read as the host
+    does: a second workload key (deployment wins over statefulset, either
+    wins over daemonset, whatever their order), a repeated key (the first
+    occurrence counts), a namespace that is not a string (Str() is "")."""
+    td = _routable(td, rng)
+    for rs in td["resourceSpans"]:
+        attrs = rs["resource"]["attributes"]
+        x = rng.random()
+        if x < 0.1:
+            attrs.insert(0, host.attrs({"k8s.daemonset.name": "agent"})[0])
+        elif x < 0.2:
+            attrs += host.attrs({"k8s.statefulset.name": "db"})
+        elif x < 0.3:
+            attrs.insert(0, host.attrs({"k8s.namespace.name": 7})[0])
+        elif x < 0.4:
+            attrs += host.attrs({"k8s.namespace.name": "prod"})
+    return td
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_encoder_writes_pdata_inputs(seed, monkeypatch):
+    """A batch in pdata's encoding is routed and written by the GPU encoder
+    (encode_kernel.hip: no fallback), byte for byte what the restatement
+    writes with the GPU's decisions, and what the host encoder writes
+    (OSE_ENCODE_HOST=1) — with and without a router, with SAMPLE|TEMPLATE and
+    with TEMPLATE alone."""
+    import torch
+    from odigos_amd.batch import Engine, OtlpBatch
+    rng = random.Random(0x6E0C + seed)
+    td = _roundtrip(_routable_gpu(_http_traces(rng, 200), rng))
+    streams = _streams(rng)
+    router = Router({"datastreams": streams})
+    eng = Engine(CFG)
+    pb = gg.marshal_traces(td)
+    ob = OtlpBatch(eng, pb)
+    for st in (native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE, native.STAGE_TEMPLATE):
+        eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=SEED)
+        torch.cuda.synchronize()
+        n = ob.cols.n_spans
+        url_out = ob.out_numpy("url_out", n=n)
+        refs = ob.out_numpy("tmpl", np.uint32, n=2 * n).reshape(-1, 2)
+        arena = ob.out_numpy("tmpl_arena", n=ob.used()).tobytes()
+        tmpls = [arena[o:o + ln].decode("utf-8", "surrogateescape") if u else "" for (o, ln), u in zip(refs, url_out)]
+        dec = {"keep": list(ob.out_numpy("keep", n=n))} if st & native.STAGE_SAMPLE else {}
+        for r in (router, None):
+            want = _expected(td, streams if r else None, router.pipelines if r else None, url_out=list(url_out),
+                             tmpls=tmpls, **dec)
+            got = ob.encode(st, native.GROUP_TRACE_ID, r)
+            assert ob.encode_path == {"gpu": True, "fallback": 0}
+            assert got == want
+            monkeypatch.setenv("OSE_ENCODE_HOST", "1")
+            assert ob.encode(st, native.GROUP_TRACE_ID, r) == want
+            assert ob.encode_path["gpu"] is False
+            monkeypatch.delenv("OSE_ENCODE_HOST")
+    ob.close()
+
+
+@pytest.mark.gpu
+def test_gpu_encoder_hands_other_encodings_to_the_host():
+    """google.protobuf's encoding (empty ids and Status left out) is not
+    pdata's: the GPU encoder flags the call and the host encoder re-marshals
+    it, with the same result as the restatement."""
+    import torch
+    from odigos_amd.batch import Engine, OtlpBatch
+    rng = random.Random(0x6E1F)
+    td = _roundtrip(_routable(_http_traces(rng, 50), rng))
+    eng = Engine(CFG)
+    ob = OtlpBatch(eng, to_pb(td))
+    st = native.STAGE_SAMPLE | native.STAGE_TEMPLATE
+    eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=SEED)
+    torch.cuda.synchronize()
+    n = ob.cols.n_spans
+    url_out = ob.out_numpy("url_out", n=n)
+    refs = ob.out_numpy("tmpl", np.uint32, n=2 * n).reshape(-1, 2)
+    arena = ob.out_numpy("tmpl_arena", n=ob.used()).tobytes()
+    tmpls = [arena[o:o + ln].decode("utf-8", "surrogateescape") if u else "" for (o, ln), u in zip(refs, url_out)]
+    want = _expected(td, None, None, keep=list(ob.out_numpy("keep", n=n)), url_out=list(url_out), tmpls=tmpls)
+    assert ob.encode(st) == want
+    assert ob.encode_path["gpu"] is False and ob.encode_path["fallback"] != 0
+    ob.close()
