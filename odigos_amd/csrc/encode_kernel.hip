@@ -450,29 +450,35 @@ __global__ __launch_bounds__(kEThreads) void enc_scan_apply_kernel(EncArgs a, ui
 // ---- writing -----------------------------------------------------------------------
 namespace {
 // wave-cooperative writer of one record (positions are wave-uniform)
+// Every store is checked against the record's size from the sizing pass
+// (lim): a disagreement is a bug, flagged (kEncFbWrite) instead of written
+// past the record.
 struct WaveOut {
   uint8_t* dst;
-  uint64_t pos;
+  uint64_t pos, lim;
   int lane;
+  __device__ __forceinline__ void put(uint64_t at, uint32_t b) {
+    if (at < lim) dst[at] = (uint8_t)b;
+  }
   // tag and varint v
   __device__ __forceinline__ void hdr(uint32_t tag, uint64_t v) {
     const uint32_t nb = 1 + sov(v);
     if ((uint32_t)lane < nb) {
       const uint32_t b = lane == 0 ? tag : (uint32_t)((v >> (7 * (lane - 1))) & 0x7F) | ((uint32_t)lane + 1 < nb ? 0x80u : 0u);
-      dst[pos + lane] = (uint8_t)b;
+      put(pos + lane, b);
     }
     pos += nb;
   }
   __device__ __forceinline__ void byte(uint32_t c) {
-    if (lane == 0) dst[pos] = (uint8_t)c;
+    if (lane == 0) put(pos, c);
     pos += 1;
   }
   __device__ __forceinline__ void copy(const uint8_t* src, uint64_t n) {
-    for (uint64_t x = (uint64_t)lane; x < n; x += kWave) dst[pos + x] = src[x];
+    for (uint64_t x = (uint64_t)lane; x < n; x += kWave) put(pos + x, src[x]);
     pos += n;
   }
   __device__ __forceinline__ void lit(const char* s, uint32_t n) {
-    if ((uint32_t)lane < n) dst[pos + lane] = (uint8_t)s[lane];
+    if ((uint32_t)lane < n) put(pos + lane, (uint8_t)s[lane]);
     pos += n;
   }
 };
@@ -509,8 +515,8 @@ __device__ void write_edit(const EncArgs& a, WaveOut& w, const uint8_t* sp, uint
 }
 
 // the record of resource r at dst (Enc::write_chunk)
-__device__ void write_record(const EncArgs& a, uint64_t r, uint8_t* dst) {
-  WaveOut w{dst, 0, (int)(threadIdx.x & 63)};
+__device__ void write_record(const EncArgs& a, uint64_t r, uint8_t* dst, uint64_t rec) {
+  WaveOut w{dst, 0, rec, (int)(threadIdx.x & 63)};
   w.hdr(0x0A, uni64(a.res_body[r]));
   const uint64_t h = uni64(a.res_hdr[r]);
   if (h == kEncNoHdr) {
@@ -575,6 +581,7 @@ __device__ void write_record(const EncArgs& a, uint64_t r, uint8_t* dst) {
     w.hdr(0x1A, rs >> 32);
     w.copy(a.pb + (uint32_t)rs, rs >> 32);
   }
+  if (w.pos != rec && w.lane == 0) atomicOr(a.flags, (uint32_t)kEncFbWrite);
 }
 }  // namespace
 
@@ -582,12 +589,13 @@ __device__ void write_record(const EncArgs& a, uint64_t r, uint8_t* dst) {
 __global__ __launch_bounds__(kEThreads) void enc_write_kernel(EncArgs a) {
   const uint64_t waves = (uint64_t)gridDim.x * (kEThreads / kWave);
   for (uint64_t r = uni64((uint64_t)blockIdx.x * (kEThreads / kWave) + (threadIdx.x >> 6)); r < a.n_res; r += waves) {
-    if (uni64(a.res_rec[r]) == 0) continue;
+    const uint64_t rec = uni64(a.res_rec[r]);
+    if (rec == 0) continue;
     uint64_t mask = uni64(a.res_mask[r]);
     while (mask) {
       const uint32_t k = (uint32_t)__builtin_ctzll(mask);
       mask &= mask - 1;
-      write_record(a, r, a.out + a.out_base[k] + uni64(a.off[(uint64_t)k * a.n_res + r]));
+      write_record(a, r, a.out + a.out_base[k] + uni64(a.off[(uint64_t)k * a.n_res + r]), rec);
     }
   }
 }

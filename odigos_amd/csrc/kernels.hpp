@@ -519,6 +519,7 @@ enum : uint32_t {
   kEncFbRes = 4,        // a resource header not in pdata's encoding / merged / malformed
   kEncFbTmpl = 8,       // a template reference beyond the arena (the host reports it)
   kEncFbRoute = 16,     // a routing attribute the device does not read exactly
+  kEncFbWrite = 32,     // the writing pass disagreed with the sizing pass (a bug: the call fails)
 };
 struct EncEdit {        // one rewritten span (otlp_encode.cpp Edit)
   uint32_t name_a, name_b, attr_a, attr_b;

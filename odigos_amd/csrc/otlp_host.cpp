@@ -699,12 +699,19 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
   *redo = false;
   std::string err;
   int rc;
-  // the TracesData chain: segments walked on the GPU and linked here, or
-  // (OSE_OTLP_HOST_CHAIN=1, or when the link fails) the host walk
+  // the TracesData chain: the host walk (it runs while the message's H2D
+  // copy is in flight), or (OSE_OTLP_GPU_CHAIN=1) segments walked on the GPU
+  // and linked here, the host walk when the link fails.  The GPU form
+  // measured slower (profiles/r3_otlp_gpu_resources.json host chain,
+  // r3_otlp_gpu_chain_gpu_encode.json GPU chain: 10M spans 57.8 -> 97.4 ms of
+  // walk, an 8192-span request 0.56 -> 2.06 ms of decode): it cannot
+  // start before the whole message has landed, and each lane's hops through
+  // its 64 KiB segment are dependent HBM reads.
   std::vector<uint64_t> seg_first;
   std::vector<uint32_t> seg_base;
   uint64_t R = 0;
-  bool gpu_chain = len > 0 && !getenv("OSE_OTLP_HOST_CHAIN");
+  const char* gc = getenv("OSE_OTLP_GPU_CHAIN");   // read per call (tests, A/B)
+  bool gpu_chain = len > 0 && gc && gc[0] == '1';
   const uint32_t T = (uint32_t)((len + kChainSeg - 1) / kChainSeg);
   OtlpChainArgs ca{};
   if (gpu_chain) {
@@ -1613,7 +1620,10 @@ int encode_gpu(OtlpBatchImpl* b, const ose_outputs* outs, bool sampled, bool tmp
   HIP_TRY(hipGetLastError());
   for (uint32_t k = 0; k < n_out; k++)
     if (tot[k]) HIP_TRY(hipMemcpyAsync(o->outs[k].data, a.out + base[k], tot[k], hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(h, flags64, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  std::memcpy(&fb, h, 4);
+  if (fb & kEncFbWrite) return fail(OSE_EDEVICE, "GPU encoder: a record's bytes disagree with its size");
   o->t_ms[3] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   o->gpu = 1;
   *host = false;

@@ -451,6 +451,9 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // ds_read_b128).  Built cooperatively, 32 bytes per lane, branch-free.
 // Classes 0-7 are read for every segment; 8-11 (the email classes) only for
 // segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
+#ifndef OSE_URL_DEFER
+#define OSE_URL_DEFER 1   // date / email / U+FFFD checks in a compacted second classify pass (0: inline, round 2)
+#endif
 #ifndef OSE_URL_ROWMUL
 #define OSE_URL_ROWMUL 0  // A/B: the round-2 row build (a movemask multiply per class and dword): C4 url_plan 6.87 vs 6.19 ms
 #endif
@@ -564,6 +567,11 @@ __device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t k) {
   }
   return pos;
 }
+// position of the k-th set bit of a 64-bit m (k < popcount(m))
+__device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t k) {
+  const uint32_t c = (uint32_t)__builtin_popcount((uint32_t)m);
+  return k < c ? select_bit((uint32_t)m, k) : 32 + select_bit((uint32_t)(m >> 32), k - c);
+}
 // Only the rows (bit r of the 96-bit mask {m0, m1, m2}) that hold path bytes:
 // every reader of the bitmaps masks its windows to a path's own bytes, so the
 // rows between paths (other strings of the arena) are never looked at.
@@ -645,19 +653,30 @@ constexpr uint64_t date_shape_tab(uint32_t base) {
   for (uint32_t k = 0; k < 16; k++) t |= date_shape_bits(base + k) << (4 * k);
   return t;
 }
-template <class R>
-__device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint32_t s, uint32_t L) {
+// the part of date_win that needs no byte reads: the length has a date
+// shape and the digit / dash windows fit it
+__device__ __forceinline__ uint32_t date_shape(uint32_t L) {
   constexpr uint64_t kLo = date_shape_tab(0), kHi = date_shape_tab(16);
-  const uint32_t sh = (uint32_t)(((L < 16 ? kLo : kHi) >> (4 * (L & 15))) & 15u);
+  return L >= 32 ? 0u : (uint32_t)(((L < 16 ? kLo : kHi) >> (4 * (L & 15))) & 15u);
+}
+__device__ __forceinline__ bool date_pre(uint64_t dg, uint64_t dash, uint32_t L) {
+  const uint32_t sh = date_shape(L);
   const uint32_t tsel = sh & 3u, zsel = sh >> 2;
-  if (L >= 32 || tsel == 0) return false;
+  if (tsel == 0) return false;
   const uint32_t tlen = tsel == 1 ? 0u : tsel == 2 ? 6u : 9u;
   uint64_t dm = 0x36Full;                                     // YYYY-MM-DD digits
   dm |= tsel >= 2 ? (3ull << 11) | (3ull << 14) : 0ull;       // THH:MM
   dm |= tsel == 3 ? 3ull << 17 : 0ull;                        // :SS
   const uint32_t z = 10 + tlen;
   dm |= zsel == 2 ? 0xFull << (z + 1) : 0ull;                 // +HHMM
-  if ((dg & dm) != dm || ((dash >> 4) & 1) == 0 || ((dash >> 7) & 1) == 0) return false;
+  return (dg & dm) == dm && ((dash >> 4) & 1) != 0 && ((dash >> 7) & 1) != 0;
+}
+template <class R>
+__device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint32_t s, uint32_t L) {
+  if (!date_pre(dg, dash, L)) return false;
+  const uint32_t sh = date_shape(L);
+  const uint32_t tsel = sh & 3u, zsel = sh >> 2;
+  const uint32_t tlen = tsel == 1 ? 0u : tsel == 2 ? 6u : 9u;
   // bytes 10-13 and 16-19 hold every fixed punctuation position and the zone
   const uint32_t wa = rd.word(s + 10), wb = rd.word(s + 16);
   const uint32_t c_t = wa & 0xFFu, c_c1 = (wa >> 24) & 0xFFu, c_c2 = wb & 0xFFu;
@@ -738,6 +757,34 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
       return kNameId;
   }
   if (!(cfg.ablate & 32) && any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
+  return -1;
+}
+
+// classify_win's first pass over a step's segments: the result when none of
+// the date / email / U+FFFD checks applies (*defer false), else *defer and
+// the segment is classified by classify_win in a second pass that takes
+// only such segments (about one in ten of C4's), so those divergent checks
+// run for one compacted step per group instead of in every step.  With
+// custom ids configured (checked first) nothing is deferred.
+template <class R>
+__device__ __forceinline__ int classify_fast(const Cfg& cfg, R& rd, const Win& w, lds_cu4* bm, uint32_t a, uint32_t s,
+                                             uint32_t L, bool* defer) {
+  if (cfg.n_custom || !OSE_URL_DEFER) {
+    *defer = false;
+    return classify_win(cfg, rd, w, bm, a, s, L);
+  }
+  const uint64_t M = low_mask(L);
+  const uint64_t at = w.c[C_AT] & M;
+  *defer = (w.c[C_HI] & M) != 0 || (at && (at & (at - 1)) == 0) || date_pre(w.c[C_DG], w.c[C_DASH], L);
+  if (*defer) return -1;
+  const uint64_t d = w.c[C_DG] & M, d1 = d & (d >> 1), d2 = d1 & (d1 >> 2), d7 = d2 & (d2 >> 3);
+  if ((L > 0 && (w.c[C_BNL] & M) == 0) || d7 || ((w.c[C_BHX] & M) == 0 && L >= 16 && (L & 1) == 0)) return kNameId;
+  if (L >= 36) {
+    const uint64_t hx = ~w.c[C_BHX], ds = w.c[C_DASH], sh = L - 36;
+    if (((hx & kUuidHex) == kUuidHex && (ds & kUuidDash) == kUuidDash) ||
+        (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
+      return kNameId;
+  }
   return -1;
 }
 
@@ -1254,20 +1301,42 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   if (tm) { const uint64_t c1 = clk(); tt[0] += c1 - c0; c0 = c1; }
   LdsReader rd0(stage32, 0);
   bool longseg = false;
-  for (uint32_t x = lane; x < total; x += kWave) {   // classify
+  // id + 1 in 8 bits: 255 stands for every id >= 254 (such plans are `slow`
+  // and re-classify their segments when emitted)
+  auto put_cls = [&](uint32_t x, int id, uint32_t L) {
+    const uint32_t out = id >= 0 ? name_len(cfg, (uint32_t)id) + 2 : L;
+    cls[x] = (out << 8) | min((uint32_t)(id + 1), 255u);
+  };
+  uint64_t dm0 = 0, dm1 = 0, dm2 = 0;   // deferred entries of steps 0, 1, 2 (kSegCap = 3 steps)
+  for (uint32_t x0 = 0; x0 < total; x0 += kWave) {   // classify, first pass
+    const uint32_t x = x0 + (uint32_t)lane;
+    bool defer = false;
+    if (x < total) {
+      const uint32_t ent = segs[x];
+      const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
+      int id = -1;
+      if (L <= 64) {
+        const Win w = load_win<0, 2>(bm, s, L);
+        id = classify_fast(cfg, rd0, w, bm, s, s, L, &defer);
+      } else {
+        longseg = true;   // a segment longer than a 64-bit window: the group goes to url_plan_slow_kernel
+      }
+      if (!defer) put_cls(x, id, L);
+    }
+    const uint64_t dm = __ballot(defer);
+    if (x0 == 0) dm0 = dm;
+    else if (x0 == kWave) dm1 = dm;
+    else dm2 = dm;
+  }
+  // second pass: the deferred entries, compacted (lane k takes the k-th)
+  const uint32_t n0 = (uint32_t)__popcll(dm0), n1 = (uint32_t)__popcll(dm1), nd = n0 + n1 + (uint32_t)__popcll(dm2);
+  for (uint32_t k = lane; k < nd; k += kWave) {
+    const uint32_t x = k < n0 ? select_bit64(dm0, k) : k < n0 + n1 ? kWave + select_bit64(dm1, k - n0)
+                                                                    : 2 * kWave + select_bit64(dm2, k - n0 - n1);
     const uint32_t ent = segs[x];
     const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
-    int id = -1;
-    if (L <= 64) {
-      const Win w = load_win<0, 2>(bm, s, L);
-      id = classify_win(cfg, rd0, w, bm, s, s, L);
-    } else {
-      longseg = true;   // a segment longer than a 64-bit window: the group goes to url_plan_slow_kernel
-    }
-    const uint32_t out = id >= 0 ? name_len(cfg, (uint32_t)id) + 2 : L;
-    // id + 1 in 8 bits: 255 stands for every id >= 254 (such plans are `slow`
-    // and re-classify their segments when emitted)
-    cls[x] = (out << 8) | min((uint32_t)(id + 1), 255u);
+    const Win w = load_win<0, 2>(bm, s, L);
+    put_cls(x, classify_win(cfg, rd0, w, bm, s, s, L), L);
   }
   wave_lds_sync();
   if (__ballot(longseg)) return false;

@@ -371,18 +371,19 @@ def test_gpu_resource_walk_cold_warm_and_host(monkeypatch):
     monkeypatch.delenv("OSE_OTLP_HOST_RESOURCES")
     ob3 = OtlpBatch(Engine(CFG), to_pb(td3))
     _compare(ob3.cols, hb3.cols, ob3.download())
-    # the TracesData chain walked on the host (OSE_OTLP_HOST_CHAIN=1) equals the GPU's
-    monkeypatch.setenv("OSE_OTLP_HOST_CHAIN", "1")
+    # the TracesData chain walked on the GPU (OSE_OTLP_GPU_CHAIN=1) equals the host's
+    monkeypatch.setenv("OSE_OTLP_GPU_CHAIN", "1")
     ob4 = OtlpBatch(Engine(CFG), to_pb(td3))
     _compare(ob4.cols, hb3.cols, ob4.download())
 
 
 @pytest.mark.gpu
-def test_gpu_chain_walk_records_over_segments():
+def test_gpu_chain_walk_records_over_segments(monkeypatch):
     # ResourceSpans records larger than the GPU chain walk's 64 KiB segments
     # (whole segments inside one record) between small ones, and a message
     # whose bytes end inside a record (malformed: the host walk reports it)
     from odigos_amd.batch import Engine, OtlpBatch
+    monkeypatch.setenv("OSE_OTLP_GPU_CHAIN", "1")
     rng = random.Random(41)
     td = _http_traces(rng, 120)
     rss = td["resourceSpans"]

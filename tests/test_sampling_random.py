@@ -365,9 +365,26 @@ def test_gpu_sample_and_template_one_call(workload, shuffle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shuffle,n", [(False, 300_000), (True, 300_000), (False, 2_000_000), (True, 50_000)])
-def test_gpu_sampling_dup_buckets(monkeypatch, shuffle, n):
-    # the fast path's duplicate detection through fingerprint buckets checked
-    # in LDS (OSE_DUP_BUCKETS=1, read per call): the same decisions as the
-    # oracle, repeated trace ids (shuffled resources) found
-    monkeypatch.setenv("OSE_DUP_BUCKETS", "1")
+def test_gpu_sampling_dup_table(monkeypatch, shuffle, n):
+    # the fast path's duplicate detection through the fingerprint table
+    # (OSE_DUP_BUCKETS=0, read per call; the default buckets checked in LDS
+    # run in every other sampling test): the same decisions as the oracle,
+    # repeated trace ids (shuffled resources) found
+    monkeypatch.setenv("OSE_DUP_BUCKETS", "0")
     gpu_vs_oracle(Generator("sampling", seed=0x0D1600F0 + n, n_spans=n, shuffle=shuffle))
+
+
+@pytest.mark.gpu
+def test_gpu_sampling_many_service_rules():
+    """service_name rules naming the same service share one per-trace bit
+    (the rule is matched and satisfied iff the service occurs): 130 rules
+    over 20 services, more rules than the trace stage's 64 bits, decide as
+    the oracle does rule by rule."""
+    cfg = c3_sampling_config()
+    cfg["service_rules"] = [
+        {"name": f"r{k}", "type": "service_name",
+         "rule_details": {"service_name": f"svc-{k % 20:02d}", "sampling_ratio": float((k * 37) % 101),
+                          "fallback_sampling_ratio": float(k % 7)}}
+        for k in range(130)]
+    check_interning(cfg)
+    gpu_vs_oracle(Generator("sampling", seed=0x0D1601A5, n_spans=200_000), cfg=cfg)
