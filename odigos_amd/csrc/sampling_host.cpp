@@ -228,8 +228,9 @@ int Workspace::reserve_table(uint64_t n_spans) {
   fp_slots_cap = fp_slots(n_spans);
   HIP_TRY(hipMalloc(&fp_table, fp_slots_cap * sizeof(uint64_t)));
   HIP_TRY(hipMemset(fp_table, 0, fp_slots_cap * sizeof(uint64_t)));
-  // fingerprint buckets: half full (on average) at one run head per 4 spans
-  dup_bkt_bits = 0;
+  // fingerprint buckets: half full (on average) at one run head per 4 spans;
+  // at least 2 (the bucket is the fingerprint's top dup_bkt_bits bits)
+  dup_bkt_bits = 1;
   while ((uint64_t(kDupBucketCap) / 2 << dup_bkt_bits) < n_spans / 4) dup_bkt_bits++;
   HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dup_bkt), (size_t(kDupBucketCap) << dup_bkt_bits) * sizeof(uint64_t)));
   HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dup_bkt_count), (size_t(1) << dup_bkt_bits) * sizeof(uint32_t)));
@@ -355,7 +356,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // fingerprint table
   const char* bkt_env = getenv("OSE_DUP_BUCKETS");   // read per call (A/B and tests)
   const bool buckets = !bkt_env || strtoul(bkt_env, nullptr, 0) != 0;
-  if (buckets && a.mode == kTraceRuns && ws->dup_bkt) {
+  if (buckets && a.mode == kTraceRuns && ws->dup_bkt && ws->dup_bkt_bits >= 1 && ws->dup_bkt_bits <= 32) {
     a.dup_bkt = ws->dup_bkt;
     a.dup_bkt_count = ws->dup_bkt_count;
     a.dup_bkt_bits = ws->dup_bkt_bits;

@@ -518,7 +518,7 @@ __device__ void flush_heads(const TraceKernelArgs& a, HeadQ& H, uint32_t& hn, in
     for (uint32_t b = 0; b < hn; b += kWave) {
       if (b + lane < hn) {
         const uint64_t h = H.cell[b + lane];
-        const uint32_t bk = (uint32_t)(h >> (64 - a.dup_bkt_bits));
+        const uint32_t bk = (uint32_t)(h >> (64 - a.dup_bkt_bits));   // dup_bkt_bits in [1, 32] (the host's)
         const uint32_t at = atomicAdd(&a.dup_bkt_count[bk], 1u);
         if (at < kDupBucketCap) a.dup_bkt[(uint64_t)bk * kDupBucketCap + at] = h | 1ull;   // (0 marks an empty set slot)
         else dup = true;

@@ -1608,7 +1608,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     if (unplanned) {
       if (lane == 0) a.unplanned[atomicAdd(a.unplanned_count, 1u)] = g;
     } else {
-    const uint64_t sum = wave_sum_u64(p.len);
+    // the group's output bytes and each lane's offset in its image: one DPP
+    // scan (a 64-bit shuffle reduction would be 12 dependent LDS round trips)
+    uint32_t sum32;
+    const uint32_t local = wave_excl_scan(p.len, &sum32);
+    const uint64_t sum = sum32;
     const uint64_t need = (sum + 15) & ~15ull;
     // wave-uniform: the group is assembled here unless a user rule matched, a
     // name id lies outside the braced table, the list planner gave up, or the
@@ -1644,8 +1648,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     if (fast) {
       lds_u4* img4 = (lds_u4*)sm.bm[wv];
       const uint32_t n16 = (uint32_t)(need / 16);
-      uint32_t unused;
-      const uint32_t local = wave_excl_scan(p.len, &unused);
 #if OSE_URL_ASM32
       for (uint32_t k = lane; k < n16; k += kWave) img4[k] = u32x4{0u, 0u, 0u, 0u};   // the bitmaps are dead here
       wave_lds_sync();

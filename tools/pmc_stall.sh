@@ -1,6 +1,7 @@
 #!/bin/bash
 # stall / issue breakdown of the C4 kernels (separate --pmc passes, kernel-trace only)
 set -o pipefail
+export OSE_SKIP_BUILD=1
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/pmc3
 cd /tmp && export TMPDIR=/tmp
