@@ -463,7 +463,9 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #ifndef OSE_URL_ASM32
 #define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores
 #endif
-enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
+// classes 0-5 are what the segment classifier reads (a row's first vector and
+// half of its second), 6-7 what the enumeration reads, 8-11 the email checks
+enum : uint32_t { C_BNL = 0, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_SL, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
 constexpr uint32_t kBase = 8;
 constexpr uint32_t kRowVec = 3;   // u32x4 per row
 constexpr uint32_t kBmRows = kStage / 32 + 3;
@@ -523,13 +525,13 @@ __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t
                               (swar_ge(t, '+') & ~swar_ge(t, ','))) & asc;
       const uint32_t dom = alpha | digit | dot | dash;
       const uint32_t m[kClasses] = {
-          gsl & ~g0 & asc,                                 // C_SL
           ~(print & ~alpha) & kH,                          // C_BNL: outside noLetters' class
           ~(digit | hexl) & kH,                            // C_BHX
           digit,                                           // C_DG
           gat & ~swar_ge(t, 'A') & asc,                    // C_AT
           hi,                                              // C_HI
           dash,                                            // C_DASH
+          gsl & ~g0 & asc,                                 // C_SL
           swar_ge(t, '?') & ~gat & asc,                    // C_QM
           ~(dom | extra) & kH,                             // C_BLOC: outside [A-Za-z0-9._%+-]
           ~dom & kH,                                       // C_BDOM: outside [A-Za-z0-9.-]
@@ -622,7 +624,26 @@ __device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a, uint32_t L
   }
   return w;
 }
-typedef WinT<2> Win;   // classes 0-7
+// the 64-bit windows of classes 0-5 at stage byte a (what the segment
+// classifier reads): per row one 16-byte and one 8-byte read
+struct Win {
+  uint64_t c[6];
+};
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(3))) u32x2 lds_cu2;
+__device__ __forceinline__ Win load_win6(lds_cu4* bm, uint32_t a) {
+  const uint32_t r = a >> 5, sh = a & 31;
+  const lds_cu2* b2 = (const lds_cu2*)bm;
+  const u32x4 x0 = bm[kRowVec * r], x1 = bm[kRowVec * (r + 1)], x2 = bm[kRowVec * (r + 2)];
+  const u32x2 y0 = b2[2 * (kRowVec * r + 1)], y1 = b2[2 * (kRowVec * (r + 1) + 1)], y2 = b2[2 * (kRowVec * (r + 2) + 1)];
+  const uint32_t w0[6] = {x0.x, x0.y, x0.z, x0.w, y0.x, y0.y}, w1[6] = {x1.x, x1.y, x1.z, x1.w, y1.x, y1.y},
+                 w2[6] = {x2.x, x2.y, x2.z, x2.w, y2.x, y2.y};
+  Win w;
+#pragma unroll
+  for (int c = 0; c < 6; c++)
+    w.c[c] = ((uint64_t)__builtin_amdgcn_alignbit(w2[c], w1[c], sh) << 32) | __builtin_amdgcn_alignbit(w1[c], w0[c], sh);
+  return w;
+}
 __device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
 // first byte of class c in [a, e) (stage coordinates), or e
@@ -1316,7 +1337,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
       int id = -1;
       if (L <= 64) {
-        const Win w = load_win<0, 2>(bm, s, L);
+        const Win w = load_win6(bm, s);
         id = classify_fast(cfg, rd0, w, bm, s, s, L, &defer);
       } else {
         longseg = true;   // a segment longer than a 64-bit window: the group goes to url_plan_slow_kernel
@@ -1335,7 +1356,7 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
                                                                     : 2 * kWave + select_bit64(dm2, k - n0 - n1);
     const uint32_t ent = segs[x];
     const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
-    const Win w = load_win<0, 2>(bm, s, L);
+    const Win w = load_win6(bm, s);
     put_cls(x, classify_win(cfg, rd0, w, bm, s, s, L), L);
   }
   wave_lds_sync();
