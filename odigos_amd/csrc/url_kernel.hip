@@ -451,6 +451,9 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // ds_read_b128).  Built cooperatively, 32 bytes per lane, branch-free.
 // Classes 0-7 are read for every segment; 8-11 (the email classes) only for
 // segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
+#ifndef OSE_URL_ASMTAIL
+#define OSE_URL_ASMTAIL 1 // segment bodies past kAsmHead bytes assembled in a compacted tail pass (0: in the step)
+#endif
 #ifndef OSE_URL_DEFER
 #define OSE_URL_DEFER 1   // date / email / U+FFFD checks in a compacted second classify pass (0: inline, round 2)
 #endif
@@ -1090,6 +1093,7 @@ struct PlanSmem {
   BracedNames bn;
 };
 constexpr uint32_t kImgCap = kRowVec * kPlanBmRows * 16;   // bytes of one wave's output image
+constexpr uint32_t kAsmHead = 8;   // body bytes an entry writes in its assembly step (the rest: tail pass)
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
@@ -1444,8 +1448,8 @@ __device__ __forceinline__ uint32_t plan_gate(const PlanCols& c) {
 // OSE_URL_ASM32: each entry's bytes go out as whole dwords (ds_or_b32 into an
 // image the caller zeroed; two unaligned dword reads of the source per
 // dword), about a third of the LDS instructions of the byte form.
-__device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L, uint32_t stage_src, const uint32_t* segs,
-                                               const uint32_t* cls, const BracedNames& bn, uint32_t bn_src,
+__device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L, uint32_t stage_src, uint32_t* segs,
+                                               uint32_t* cls, const BracedNames& bn, uint32_t bn_src,
                                                const Plan& p, uint32_t seg_off, uint32_t local) {
   const int lane = threadIdx.x & 63;
   const uint32_t nseg = seg_off >> 16, off = seg_off & 0xFFFFu;
@@ -1465,9 +1469,11 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
   }
   const uint32_t total = lane_value(off + nseg, kWave - 1);
   uint32_t carry = 0;
+  uint64_t tm0 = 0, tm1 = 0, tm2 = 0;   // entries whose bodies go past kAsmHead bytes, per step
   for (uint32_t x0 = 0; x0 < total; x0 += kWave) {
     const uint32_t x = x0 + (uint32_t)lane;
     const bool v = x < total;
+    bool tail = false;
     const uint32_t ent = v ? segs[x] : 0u, c = v ? cls[x] : 0u;
     const uint32_t opk = (uint32_t)__shfl((int)pk, (int)(ent >> 25), kWave);
     uint32_t stot;
@@ -1497,17 +1503,57 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       if (slash) img[pos] = '/';
       lds_out_u8* dp = img + pos + 1;
       const lds_u8* sp = L + so;
-      for (uint32_t q = 0; q < n; q += 8) {
+#if OSE_URL_ASMTAIL
+      // the first kAsmHead bytes here; a longer body's rest in the tail pass
+      // below (its source and place kept in the entry's now dead list slots)
+      const uint32_t head = min(n, kAsmHead);
+      tail = n > kAsmHead;
+      if (tail) {
+        segs[x] = so | (pos << 16);
+        cls[x] = n;
+      }
+#else
+      const uint32_t head = n;
+#endif
+      for (uint32_t q = 0; q < head; q += 8) {
         uint32_t b[8];
 #pragma unroll
         for (uint32_t t = 0; t < 8; t++) b[t] = sp[q + t];   // reads past n stay inside the stage / name table
 #pragma unroll
         for (uint32_t t = 0; t < 8; t++)
-          if (q + t < n) dp[q + t] = (uint8_t)b[t];
+          if (q + t < head) dp[q + t] = (uint8_t)b[t];
       }
 #endif
     }
+    const uint64_t tm = __ballot(tail);
+    if (x0 == 0) tm0 = tm;
+    else if (x0 == kWave) tm1 = tm;
+    else tm2 = tm;
   }
+#if OSE_URL_ASMTAIL
+  // tail pass: the bodies longer than kAsmHead (about one entry in ten on C4's
+  // mix), compacted over the lanes, so the few long segments of a group cost
+  // one pass of their own instead of lengthening every step's byte loop
+  const uint32_t n0 = (uint32_t)__popcll(tm0), n1 = (uint32_t)__popcll(tm1), nt = n0 + n1 + (uint32_t)__popcll(tm2);
+  if (nt) {
+    wave_lds_sync();
+    for (uint32_t k = lane; k < nt; k += kWave) {
+      const uint32_t x = k < n0 ? select_bit64(tm0, k) : k < n0 + n1 ? kWave + select_bit64(tm1, k - n0)
+                                                                      : 2 * kWave + select_bit64(tm2, k - n0 - n1);
+      const uint32_t sp_pos = segs[x], n = cls[x];
+      const lds_u8* sp = L + (sp_pos & 0xFFFFu);
+      lds_out_u8* dp = img + (sp_pos >> 16) + 1;
+      for (uint32_t q = kAsmHead; q < n; q += 8) {
+        uint32_t b[8];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; t++) b[t] = sp[q + t];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; t++)
+          if (q + t < n) dp[q + t] = (uint8_t)b[t];
+      }
+    }
+  }
+#endif
 }
 
 // kMode bit 0 (kModeGeneral): user templatization rules or custom ids are

@@ -11,7 +11,7 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?
 tail -3 $OUT/pytest.log
 if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)|Error" $OUT/pytest.log | head -20; exit $rc; fi
-bash tools/gpu_ab.sh r3i_ab _nodefer fused url || exit 1
+bash tools/gpu_ab.sh r3i_ab _nodefer,_notail fused url || exit 1
 OSE_CLOCKS_WORKLOAD=fused timeout -k 10 200 python -u tools/url_clocks.py 10000000 0 > $OUT/clocks_c4.log 2>&1 || { tail -5 $OUT/clocks_c4.log; exit 1; }
 tail -6 $OUT/clocks_c4.log
 timeout -k 10 300 python -u tools/otlp_bench.py --out $OUT/otlp.json > $OUT/otlp.log 2>&1 || { tail -5 $OUT/otlp.log; exit 1; }
