@@ -690,7 +690,9 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         if (hd) {
           const uint32_t e = hn + __popcll(hmask & lanemask_lt(lane));
           if (a.dup_bkt) {
-            HQ.cell[e] = splitmix64(r.lo ^ (r.hi << 1));
+            // one multiply (odd: a bijection) on the folded id; its top bits
+            // (the bucket) depend on every bit of the id
+            HQ.cell[e] = (r.lo ^ ((r.hi << 29) | (r.hi >> 35))) * 0x9E3779B97F4A7C15ull;
           } else {
             HQ.cell[e] = fp_cell(a, r.hi, r.lo);
             HQ.idx[e] = (uint32_t)(tid_hash(r.hi, r.lo) & a.fp_mask);

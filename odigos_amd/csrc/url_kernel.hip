@@ -1505,11 +1505,13 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       const lds_u8* sp = L + so;
 #if OSE_URL_ASMTAIL
       // the first kAsmHead bytes here; a longer body's rest in the tail pass
-      // below (its source and place kept in the entry's now dead list slots)
+      // below (its source and its body's place, pos + 1 — pos itself is -1
+      // for an image's first entry when its path has no leading '/' — kept
+      // in the entry's now dead list slots)
       const uint32_t head = min(n, kAsmHead);
       tail = n > kAsmHead;
       if (tail) {
-        segs[x] = so | (pos << 16);
+        segs[x] = so | ((pos + 1) << 16);
         cls[x] = n;
       }
 #else
@@ -1542,7 +1544,7 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
                                                                       : 2 * kWave + select_bit64(tm2, k - n0 - n1);
       const uint32_t sp_pos = segs[x], n = cls[x];
       const lds_u8* sp = L + (sp_pos & 0xFFFFu);
-      lds_out_u8* dp = img + (sp_pos >> 16) + 1;
+      lds_out_u8* dp = img + (sp_pos >> 16);
       for (uint32_t q = kAsmHead; q < n; q += 8) {
         uint32_t b[8];
 #pragma unroll
