@@ -452,10 +452,10 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // Classes 0-7 are read for every segment; 8-11 (the email classes) only for
 // segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
 #ifndef OSE_URL_ASMTAIL
-#define OSE_URL_ASMTAIL 1 // segment bodies past kAsmHead bytes assembled in a compacted tail pass (0: in the step)
+#define OSE_URL_ASMTAIL 0 // segment bodies past kAsmHead bytes in a compacted tail pass: measured slower (C4 url_plan 6.37 vs 6.79 ms with it, with the deferred checks)
 #endif
 #ifndef OSE_URL_DEFER
-#define OSE_URL_DEFER 1   // date / email / U+FFFD checks in a compacted second classify pass (0: inline, round 2)
+#define OSE_URL_DEFER 0   // date / email / U+FFFD checks in a compacted second classify pass: measured slower (C4 url_plan 6.55 vs 6.79 ms with it, with the tail pass)
 #endif
 #ifndef OSE_URL_ROWMUL
 #define OSE_URL_ROWMUL 0  // A/B: the round-2 row build (a movemask multiply per class and dword): C4 url_plan 6.87 vs 6.19 ms
@@ -466,9 +466,19 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #ifndef OSE_URL_ASM32
 #define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores
 #endif
+#ifndef OSE_URL_SUMDPP
+#define OSE_URL_SUMDPP 1  // the group sum from the DPP scan (0: a 64-bit shuffle reduction)
+#endif
+#ifndef OSE_URL_CLS6
+#define OSE_URL_CLS6 1    // the classifier's six classes first (one 16-byte + one 8-byte read per window row)
+#endif
+#if OSE_URL_CLS6
 // classes 0-5 are what the segment classifier reads (a row's first vector and
 // half of its second), 6-7 what the enumeration reads, 8-11 the email checks
 enum : uint32_t { C_BNL = 0, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_SL, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
+#else
+enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
+#endif
 constexpr uint32_t kBase = 8;
 constexpr uint32_t kRowVec = 3;   // u32x4 per row
 constexpr uint32_t kBmRows = kStage / 32 + 3;
@@ -527,20 +537,19 @@ __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t
       const uint32_t extra = ((swar_ge(t, '_') & ~swar_ge(t, '`')) | (swar_ge(t, '%') & ~swar_ge(t, '&')) |
                               (swar_ge(t, '+') & ~swar_ge(t, ','))) & asc;
       const uint32_t dom = alpha | digit | dot | dash;
-      const uint32_t m[kClasses] = {
-          ~(print & ~alpha) & kH,                          // C_BNL: outside noLetters' class
-          ~(digit | hexl) & kH,                            // C_BHX
-          digit,                                           // C_DG
-          gat & ~swar_ge(t, 'A') & asc,                    // C_AT
-          hi,                                              // C_HI
-          dash,                                            // C_DASH
-          gsl & ~g0 & asc,                                 // C_SL
-          swar_ge(t, '?') & ~gat & asc,                    // C_QM
-          ~(dom | extra) & kH,                             // C_BLOC: outside [A-Za-z0-9._%+-]
-          ~dom & kH,                                       // C_BDOM: outside [A-Za-z0-9.-]
-          dot,                                             // C_DOT
-          ~alpha & kH,                                     // C_NAL
-      };
+      uint32_t m[kClasses];
+      m[C_BNL] = ~(print & ~alpha) & kH;                   // outside noLetters' class
+      m[C_BHX] = ~(digit | hexl) & kH;
+      m[C_DG] = digit;
+      m[C_AT] = gat & ~swar_ge(t, 'A') & asc;
+      m[C_HI] = hi;
+      m[C_DASH] = dash;
+      m[C_SL] = gsl & ~g0 & asc;
+      m[C_QM] = swar_ge(t, '?') & ~gat & asc;
+      m[C_BLOC] = ~(dom | extra) & kH;                     // outside [A-Za-z0-9._%+-]
+      m[C_BDOM] = ~dom & kH;                               // outside [A-Za-z0-9.-]
+      m[C_DOT] = dot;
+      m[C_NAL] = ~alpha & kH;
 #pragma unroll
 #if OSE_URL_ROWMUL
       for (int c = 0; c < (int)kClasses; c++) acc[c] |= ((((m[c] >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * d);
@@ -629,6 +638,7 @@ __device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a, uint32_t L
 }
 // the 64-bit windows of classes 0-5 at stage byte a (what the segment
 // classifier reads): per row one 16-byte and one 8-byte read
+#if OSE_URL_CLS6
 struct Win {
   uint64_t c[6];
 };
@@ -647,6 +657,10 @@ __device__ __forceinline__ Win load_win6(lds_cu4* bm, uint32_t a) {
     w.c[c] = ((uint64_t)__builtin_amdgcn_alignbit(w2[c], w1[c], sh) << 32) | __builtin_amdgcn_alignbit(w1[c], w0[c], sh);
   return w;
 }
+#else
+typedef WinT<2> Win;   // classes 0-7
+__device__ __forceinline__ Win load_win6(lds_cu4* bm, uint32_t a) { return load_win<0, 2>(bm, a); }
+#endif
 __device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
 // first byte of class c in [a, e) (stage coordinates), or e
@@ -1679,9 +1693,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     } else {
     // the group's output bytes and each lane's offset in its image: one DPP
     // scan (a 64-bit shuffle reduction would be 12 dependent LDS round trips)
+#if OSE_URL_SUMDPP
     uint32_t sum32;
     const uint32_t local = wave_excl_scan(p.len, &sum32);
     const uint64_t sum = sum32;
+#else
+    const uint64_t sum = wave_sum_u64(p.len);
+#endif
     const uint64_t need = (sum + 15) & ~15ull;
     // wave-uniform: the group is assembled here unless a user rule matched, a
     // name id lies outside the braced table, the list planner gave up, or the
@@ -1717,6 +1735,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     if (fast) {
       lds_u4* img4 = (lds_u4*)sm.bm[wv];
       const uint32_t n16 = (uint32_t)(need / 16);
+#if !OSE_URL_SUMDPP
+      uint32_t unused;
+      const uint32_t local = wave_excl_scan(p.len, &unused);
+#endif
 #if OSE_URL_ASM32
       for (uint32_t k = lane; k < n16; k += kWave) img4[k] = u32x4{0u, 0u, 0u, 0u};   // the bitmaps are dead here
       wave_lds_sync();
