@@ -466,6 +466,12 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #ifndef OSE_URL_ASM32
 #define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores
 #endif
+#ifndef OSE_URL_QROWS
+#define OSE_URL_QROWS 0   // a group's last <= 16 bitmap rows built in quarter rows (four lanes per row)
+#endif
+#ifndef OSE_URL_SPEC
+#define OSE_URL_SPEC 1    // date bytes and email windows read with the main windows (no dependent LDS round trips)
+#endif
 #ifndef OSE_URL_SUMDPP
 #define OSE_URL_SUMDPP 1  // the group sum from the DPP scan (0: a 64-bit shuffle reduction)
 #endif
@@ -505,58 +511,89 @@ __device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2
 // 7 - d puts it at bit 8j + d, its place in the row's 32-bit class word.  So
 // a class costs one shift and an OR per dword instead of a movemask (a
 // 32-bit multiply) per dword.
+// the class masks of one dword (bit 7 of byte k set when byte k is in the class)
+__device__ __forceinline__ void class_masks(uint32_t x, uint32_t* m) {
+  const uint32_t hi = x & kH, asc = hi ^ kH;
+  const uint32_t t = swar_t(x), tl = t | 0x20202020u;
+  const uint32_t g0 = swar_ge(t, '0');
+  const uint32_t digit = g0 & ~swar_ge(t, '9' + 1) & asc;
+  const uint32_t ga = swar_ge(tl, 'a');
+  const uint32_t alpha = ga & ~swar_ge(tl, 'z' + 1) & asc;
+  const uint32_t hexl = ga & ~swar_ge(tl, 'f' + 1) & asc;
+  const uint32_t print = swar_ge(t, '!') & ~swar_ge(t, 127) & asc;
+  const uint32_t gat = swar_ge(t, '@');
+  const uint32_t gdot = swar_ge(t, '.'), gsl = swar_ge(t, '/');
+  const uint32_t dash = swar_ge(t, '-') & ~gdot & asc;
+  const uint32_t dot = gdot & ~gsl & asc;
+  const uint32_t extra = ((swar_ge(t, '_') & ~swar_ge(t, '`')) | (swar_ge(t, '%') & ~swar_ge(t, '&')) |
+                          (swar_ge(t, '+') & ~swar_ge(t, ','))) & asc;
+  const uint32_t dom = alpha | digit | dot | dash;
+  m[C_BNL] = ~(print & ~alpha) & kH;                   // outside noLetters' class
+  m[C_BHX] = ~(digit | hexl) & kH;
+  m[C_DG] = digit;
+  m[C_AT] = gat & ~swar_ge(t, 'A') & asc;
+  m[C_HI] = hi;
+  m[C_DASH] = dash;
+  m[C_SL] = gsl & ~g0 & asc;
+  m[C_QM] = swar_ge(t, '?') & ~gat & asc;
+  m[C_BLOC] = ~(dom | extra) & kH;                     // outside [A-Za-z0-9._%+-]
+  m[C_BDOM] = ~dom & kH;                               // outside [A-Za-z0-9.-]
+  m[C_DOT] = dot;
+  m[C_NAL] = ~alpha & kH;
+}
 __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t r) {
-  {
-    uint32_t acc[kClasses];
+  uint32_t acc[kClasses];
 #pragma unroll
-    for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
-    const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
-    const u32x4 v0 = src[0], v1 = src[1];
-    uint32_t xs[8];
+  for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
+  const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
+  const u32x4 v0 = src[0], v1 = src[1];
+  uint32_t xs[8];
 #if OSE_URL_ROWMUL
-    xs[0] = v0.x; xs[1] = v0.y; xs[2] = v0.z; xs[3] = v0.w; xs[4] = v1.x; xs[5] = v1.y; xs[6] = v1.z; xs[7] = v1.w;
+  xs[0] = v0.x; xs[1] = v0.y; xs[2] = v0.z; xs[3] = v0.w; xs[4] = v1.x; xs[5] = v1.y; xs[6] = v1.z; xs[7] = v1.w;
 #else
-    transpose4(v0.x, v0.z, v1.x, v1.z, xs);       // bytes d, d+8, d+16, d+24 for d = 0..3
-    transpose4(v0.y, v0.w, v1.y, v1.w, xs + 4);   // d = 4..7
+  transpose4(v0.x, v0.z, v1.x, v1.z, xs);       // bytes d, d+8, d+16, d+24 for d = 0..3
+  transpose4(v0.y, v0.w, v1.y, v1.w, xs + 4);   // d = 4..7
 #endif
 #pragma unroll
-    for (int d = 0; d < 8; d++) {
-      const uint32_t x = xs[d];
-      const uint32_t hi = x & kH, asc = hi ^ kH;
-      const uint32_t t = swar_t(x), tl = t | 0x20202020u;
-      const uint32_t g0 = swar_ge(t, '0');
-      const uint32_t digit = g0 & ~swar_ge(t, '9' + 1) & asc;
-      const uint32_t ga = swar_ge(tl, 'a');
-      const uint32_t alpha = ga & ~swar_ge(tl, 'z' + 1) & asc;
-      const uint32_t hexl = ga & ~swar_ge(tl, 'f' + 1) & asc;
-      const uint32_t print = swar_ge(t, '!') & ~swar_ge(t, 127) & asc;
-      const uint32_t gat = swar_ge(t, '@');
-      const uint32_t gdot = swar_ge(t, '.'), gsl = swar_ge(t, '/');
-      const uint32_t dash = swar_ge(t, '-') & ~gdot & asc;
-      const uint32_t dot = gdot & ~gsl & asc;
-      const uint32_t extra = ((swar_ge(t, '_') & ~swar_ge(t, '`')) | (swar_ge(t, '%') & ~swar_ge(t, '&')) |
-                              (swar_ge(t, '+') & ~swar_ge(t, ','))) & asc;
-      const uint32_t dom = alpha | digit | dot | dash;
-      uint32_t m[kClasses];
-      m[C_BNL] = ~(print & ~alpha) & kH;                   // outside noLetters' class
-      m[C_BHX] = ~(digit | hexl) & kH;
-      m[C_DG] = digit;
-      m[C_AT] = gat & ~swar_ge(t, 'A') & asc;
-      m[C_HI] = hi;
-      m[C_DASH] = dash;
-      m[C_SL] = gsl & ~g0 & asc;
-      m[C_QM] = swar_ge(t, '?') & ~gat & asc;
-      m[C_BLOC] = ~(dom | extra) & kH;                     // outside [A-Za-z0-9._%+-]
-      m[C_BDOM] = ~dom & kH;                               // outside [A-Za-z0-9.-]
-      m[C_DOT] = dot;
-      m[C_NAL] = ~alpha & kH;
+  for (int d = 0; d < 8; d++) {
+    uint32_t m[kClasses];
+    class_masks(xs[d], m);
 #pragma unroll
 #if OSE_URL_ROWMUL
-      for (int c = 0; c < (int)kClasses; c++) acc[c] |= ((((m[c] >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * d);
+    for (int c = 0; c < (int)kClasses; c++) acc[c] |= ((((m[c] >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * d);
 #else
-      for (int c = 0; c < (int)kClasses; c++) acc[c] = (acc[c] >> 1) | m[c];   // after d = 7: dword d's bits at 8j + d
+    for (int c = 0; c < (int)kClasses; c++) acc[c] = (acc[c] >> 1) | m[c];   // after d = 7: dword d's bits at 8j + d
 #endif
-    }
+  }
+  bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
+  bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
+  bm[kRowVec * r + 2] = u32x4{acc[8], acc[9], acc[10], acc[11]};
+}
+// A quarter of row r (bytes 8q..8q+7) per lane, the four lanes of a quad
+// together building the row: its two dwords' class bits (movemask) at
+// 8q..8q+7, ORed over the quad by two DPP steps; the quad's first lane
+// writes the row.  For the last few rows of a group (a full round would
+// leave most lanes idle).
+__device__ __forceinline__ void build_quarter_row(lds_u32* stage32, lds_u4* bm, uint32_t r, uint32_t q, bool valid) {
+  uint32_t acc[kClasses];
+#pragma unroll
+  for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
+  if (valid) {
+    const uint32_t x0 = stage32[8 * r + 2 * q], x1 = stage32[8 * r + 2 * q + 1];
+    uint32_t m0[kClasses], m1[kClasses];
+    class_masks(x0, m0);
+    class_masks(x1, m1);
+#pragma unroll
+    for (int c = 0; c < (int)kClasses; c++)
+      acc[c] = (((((m0[c] >> 7) * 0x204081u) >> 21) & 0xFu) | (((((m1[c] >> 7) * 0x204081u) >> 21) & 0xFu) << 4))
+               << (8 * q);
+  }
+#pragma unroll
+  for (int c = 0; c < (int)kClasses; c++) {
+    acc[c] |= dpp_mov<0xB1>(0u, acc[c]);   // quad_perm [1, 0, 3, 2]
+    acc[c] |= dpp_mov<0x4E>(0u, acc[c]);   // quad_perm [2, 3, 0, 1]
+  }
+  if (valid && q == 0) {
     bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
     bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
     bm[kRowVec * r + 2] = u32x4{acc[8], acc[9], acc[10], acc[11]};
@@ -593,10 +630,22 @@ __device__ __forceinline__ void build_bitmaps_rows(lds_u32* stage32, lds_u4* bm,
                                                    uint32_t m2) {
   const int lane = threadIdx.x & 63;
   const uint32_t c0 = __builtin_popcount(m0), c1 = __builtin_popcount(m1), total = c0 + c1 + __builtin_popcount(m2);
-  for (uint32_t k = lane; k < total; k += kWave) {
-    const uint32_t r = k < c0 ? select_bit(m0, k) : k < c0 + c1 ? 32 + select_bit(m1, k - c0) : 64 + select_bit(m2, k - c0 - c1);
-    build_row(stage32, bm, r);
+  auto row_of = [&](uint32_t k) {
+    return k < c0 ? select_bit(m0, k) : k < c0 + c1 ? 32 + select_bit(m1, k - c0) : 64 + select_bit(m2, k - c0 - c1);
+  };
+#if OSE_URL_QROWS
+  // full rounds while 64 rows are left; a last round of at most 16 rows in
+  // quarter rows (four lanes per row)
+  const uint32_t full = total > kWave && total - (total & ~(kWave - 1)) <= 16 ? total & ~(kWave - 1) : total;
+  for (uint32_t k = lane; k < full; k += kWave) build_row(stage32, bm, row_of(k));
+  if (full < total) {
+    const uint32_t k = full + ((uint32_t)lane >> 2);
+    const bool valid = k < total;
+    build_quarter_row(stage32, bm, valid ? row_of(k) : 0u, (uint32_t)lane & 3u, valid);
   }
+#else
+  for (uint32_t k = lane; k < total; k += kWave) build_row(stage32, bm, row_of(k));
+#endif
 }
 // bits [lo, hi] (rows) of the 32-row word starting at row w0
 __device__ __forceinline__ uint32_t row_bits(uint32_t lo, uint32_t hi, uint32_t w0) {
@@ -709,6 +758,17 @@ __device__ __forceinline__ bool date_pre(uint64_t dg, uint64_t dash, uint32_t L)
   dm |= zsel == 2 ? 0xFull << (z + 1) : 0ull;                 // +HHMM
   return (dg & dm) == dm && ((dash >> 4) & 1) != 0 && ((dash >> 7) & 1) != 0;
 }
+// date_win given bytes 10-13 (wa) and 16-19 (wb) of the segment
+__device__ __forceinline__ bool date_words(uint64_t dg, uint64_t dash, uint32_t L, uint32_t wa, uint32_t wb) {
+  if (!date_pre(dg, dash, L)) return false;
+  const uint32_t sh = date_shape(L);
+  const uint32_t tsel = sh & 3u, zsel = sh >> 2;
+  const uint32_t tlen = tsel == 1 ? 0u : tsel == 2 ? 6u : 9u;
+  const uint32_t c_t = wa & 0xFFu, c_c1 = (wa >> 24) & 0xFFu, c_c2 = wb & 0xFFu;
+  const uint32_t c_z = tlen == 0 ? c_t : tlen == 6 ? c_c2 : wb >> 24;
+  return (tlen == 0 || (c_t == 'T' && c_c1 == ':')) && (tlen != 9 || c_c2 == ':') &&
+         (zsel == 0 || (zsel == 1 ? c_z == 'Z' : (c_z == '+' || c_z == '-')));
+}
 template <class R>
 __device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint32_t s, uint32_t L) {
   if (!date_pre(dg, dash, L)) return false;
@@ -726,6 +786,19 @@ __device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint
 // emailRegex (templatize.go:70) from the class windows: exactly one '@' at p,
 // local [0,p) >= 1 byte of [A-Za-z0-9._%+-], domain (p,L) all [A-Za-z0-9.-]
 // whose last '.' is at domain index >= 1 and is followed by >= 2 letters.
+// the email check given its class windows e (BLOC, BDOM, DOT, NAL)
+__device__ __forceinline__ bool email_cls(uint64_t at, const WinT<1>& e, uint32_t L) {
+  const uint64_t M = low_mask(L);
+  const uint32_t p = (uint32_t)__builtin_ctzll(at);
+  if (p == 0) return false;
+  const uint64_t dom = M & ~low_mask(p + 1);
+  if ((e.c[0] & low_mask(p)) || (e.c[1] & dom)) return false;
+  const uint64_t dots = e.c[2] & dom;
+  if (!dots) return false;
+  const uint32_t q = 63 - (uint32_t)__builtin_clzll(dots);
+  if (q < p + 2 || L - q - 1 < 2) return false;
+  return (e.c[3] & M & ~low_mask(q + 1)) == 0;
+}
 __device__ __forceinline__ bool email_win(uint64_t at, lds_cu4* bm, uint32_t a, uint32_t L) {
   const uint64_t M = low_mask(L);
   const uint32_t p = (uint32_t)__builtin_ctzll(at);
@@ -795,6 +868,33 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
       return kNameId;
   }
   if (!(cfg.ablate & 32) && any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
+  return -1;
+}
+
+// classify_win with the date bytes and the email windows read together with
+// the main windows (every lane, whether its segment needs them or not): any
+// of a step's 64 segments taking the date or email branch made the whole wave
+// wait for those reads one after the other
+template <class R>
+__device__ __forceinline__ int classify_spec(const Cfg& cfg, R& rd, lds_cu4* bm, uint32_t a, uint32_t s, uint32_t L) {
+  const Win w = load_win6(bm, a);
+  const WinT<1> e = load_win<2, 1>(bm, a, L);
+  const uint32_t wa = rd.word(s + 10), wb = rd.word(s + 16);
+  if (cfg.n_custom) return classify_win(cfg, rd, w, bm, a, s, L);
+  const uint64_t M = low_mask(L);
+  if (date_words(w.c[C_DG], w.c[C_DASH], L, wa, wb)) return kNameDate;
+  const bool any_hi = (w.c[C_HI] & M) != 0;
+  const uint64_t at = w.c[C_AT] & M;
+  if (!any_hi && at && (at & (at - 1)) == 0 && email_cls(at, e, L)) return kNameEmail;
+  const uint64_t d = w.c[C_DG] & M, d1 = d & (d >> 1), d2 = d1 & (d1 >> 2), d7 = d2 & (d2 >> 3);
+  if ((L > 0 && (w.c[C_BNL] & M) == 0) || d7 || ((w.c[C_BHX] & M) == 0 && L >= 16 && (L & 1) == 0)) return kNameId;
+  if (L >= 36) {
+    const uint64_t hx = ~w.c[C_BHX], ds = w.c[C_DASH], sh = L - 36;
+    if (((hx & kUuidHex) == kUuidHex && (ds & kUuidDash) == kUuidDash) ||
+        (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
+      return kNameId;
+  }
+  if (any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
   return -1;
 }
 
@@ -1355,8 +1455,15 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
       const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
       int id = -1;
       if (L <= 64) {
-        const Win w = load_win6(bm, s);
-        id = classify_fast(cfg, rd0, w, bm, s, s, L, &defer);
+#if OSE_URL_SPEC
+        if (!(cfg.ablate & (8 | 16 | 32))) {
+          id = classify_spec(cfg, rd0, bm, s, s, L);
+        } else
+#endif
+        {
+          const Win w = load_win6(bm, s);
+          id = classify_fast(cfg, rd0, w, bm, s, s, L, &defer);
+        }
       } else {
         longseg = true;   // a segment longer than a 64-bit window: the group goes to url_plan_slow_kernel
       }
