@@ -466,6 +466,9 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #ifndef OSE_URL_ASM32
 #define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores
 #endif
+#ifndef OSE_COPY_PF
+#define OSE_COPY_PF 1     // url_copy_kernel loads the next group's columns while it works on this one
+#endif
 #ifndef OSE_URL_QROWS
 #define OSE_URL_QROWS 1   // a group's last <= 16 bitmap rows built in quarter rows (four lanes per row): C2 url_plan 0.753 -> 0.729 ms, C4 6.07 -> 6.05
 #endif
@@ -2031,16 +2034,33 @@ __device__ __forceinline__ void copy_rest(const CopyJob& j, uint4 v, uint32_t& c
 // second walk over the spans (size_span_kernel is then not launched); the
 // surviving spans are counted per block into size_partials.
 template <bool kSize>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize ? 6 : 8, 8))) void url_copy_kernel(UrlKernelArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize ? 5 : 6, 8))) void url_copy_kernel(UrlKernelArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t stride = wave_stride();
   uint32_t kept = 0;
   const bool sz_on = kSize && !sizedev::size_batch_dropped(a.sz);
-  for (uint32_t g = wave_first_group(); g < a.n_groups; g += stride) {
-    const CopyCols A = copy_cols(a, g, lane);
+  uint32_t g = wave_first_group();
+  // the next group's columns are loaded while this group is worked on
+  CopyCols An{0, 0, 0, ~0ull};
+  sizedev::SpanCols xn{};
+  if (OSE_COPY_PF && g < a.n_groups) {
+    An = copy_cols(a, g, lane);
+    if (kSize && sz_on) xn = sizedev::size_span_load(a.sz, (uint64_t)g * kWave + lane, false);
+  }
+  for (; g < a.n_groups; g += stride) {
     const uint64_t ia = (uint64_t)g * kWave + lane;
-    sizedev::SpanCols x{};
-    if (kSize && sz_on) x = sizedev::size_span_load(a.sz, ia, false);
+    if (!OSE_COPY_PF) {
+      An = copy_cols(a, g, lane);
+      if (kSize && sz_on) xn = sizedev::size_span_load(a.sz, ia, false);
+    }
+    const CopyCols A = An;
+    const sizedev::SpanCols x0 = xn;
+    const bool more = g + stride < a.n_groups;
+    if (OSE_COPY_PF && more) {
+      An = copy_cols(a, g + stride, lane);
+      if (kSize && sz_on) xn = sizedev::size_span_load(a.sz, (uint64_t)(g + stride) * kWave + lane, false);
+    }
+    sizedev::SpanCols x = x0;
     uint32_t unused;
     const uint32_t la = wave_excl_scan(A.len, &unused);
     const CopyJob ja = copy_job(a, A);
@@ -2056,6 +2076,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize 
     }
     uint32_t carry = 0;
     if (ja.on) copy_rest(ja, va, carry);
+    if (!more) break;
   }
   if (kSize) {
     __shared__ uint32_t wk[kWaves];
