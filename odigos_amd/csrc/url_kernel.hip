@@ -296,6 +296,15 @@ struct Put {
   }
 };
 typedef __attribute__((address_space(3))) uint8_t lds_out_u8;
+// unaligned LDS accesses (gfx950 LDS supports them: the compiler emits
+// ds_read_b64 / ds_write_b64 for 1-byte-aligned 8-byte accesses)
+typedef uint64_t __attribute__((aligned(1))) u64_ua;
+typedef uint32_t __attribute__((aligned(1))) u32_ua;
+typedef uint16_t __attribute__((aligned(1))) u16_ua;
+typedef const __attribute__((address_space(3))) u64_ua lds_u64u;
+typedef __attribute__((address_space(3))) u64_ua lds_w64u;
+typedef __attribute__((address_space(3))) u32_ua lds_w32u;
+typedef __attribute__((address_space(3))) u16_ua lds_w16u;
 
 // copies [q, n)
 template <class R, class W>
@@ -465,6 +474,9 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #endif
 #ifndef OSE_URL_ASM32
 #define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores
+#endif
+#ifndef OSE_URL_UAW
+#define OSE_URL_UAW 1     // assembly with unaligned 8-byte LDS reads and 8/4/2/1-byte stores (0: byte stores)
 #endif
 #ifndef OSE_COPY_PF
 #define OSE_COPY_PF 1     // url_copy_kernel loads the next group's columns while it works on this one
@@ -1641,6 +1653,23 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
 #else
       const uint32_t head = n;
 #endif
+#if OSE_URL_UAW
+      // gfx950 LDS takes unaligned 8-, 4- and 2-byte accesses: one 8-byte read
+      // per 8 source bytes (reads past n stay inside the stage / name table),
+      // whole 8-byte stores, and the last 1-7 bytes as a 4-, 2- and 1-byte store
+      for (uint32_t q = 0; q < head; q += 8) {
+        uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + q);
+        const uint32_t rem = head - q;
+        if (rem >= 8) {
+          *reinterpret_cast<lds_w64u*>(dp + q) = v;
+        } else {
+          uint32_t o = q;
+          if (rem & 4) { *reinterpret_cast<lds_w32u*>(dp + o) = (uint32_t)v; v >>= 32; o += 4; }
+          if (rem & 2) { *reinterpret_cast<lds_w16u*>(dp + o) = (uint16_t)v; v >>= 16; o += 2; }
+          if (rem & 1) dp[o] = (uint8_t)v;
+        }
+      }
+#else
       for (uint32_t q = 0; q < head; q += 8) {
         uint32_t b[8];
 #pragma unroll
@@ -1649,6 +1678,7 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
         for (uint32_t t = 0; t < 8; t++)
           if (q + t < head) dp[q + t] = (uint8_t)b[t];
       }
+#endif
 #endif
     }
     const uint64_t tm = __ballot(tail);
