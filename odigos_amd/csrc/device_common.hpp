@@ -8,6 +8,10 @@
 
 #include "devcfg.hpp"
 
+#ifndef OSE_LDS_WORD2
+#define OSE_LDS_WORD2 0
+#endif
+
 namespace ose {
 
 constexpr int kWave = 64;
@@ -167,9 +171,16 @@ struct LdsReader {
   uint32_t off;    // string start within the slice
   __device__ LdsReader(lds_u32* b, uint32_t o) : base(b), off(o) {}
   __device__ __forceinline__ uint32_t at(uint32_t i) const { return ((lds_u8*)base)[off + i]; }
+  // gfx950 LDS takes unaligned dword reads: one ds_read_b32 at any byte
+  // (OSE_LDS_WORD2=1: two aligned reads and a funnel shift)
   __device__ __forceinline__ uint32_t word(uint32_t i) const {
+#if OSE_LDS_WORD2
     const uint32_t p = off + i;
     return __builtin_amdgcn_alignbyte(base[(p >> 2) + 1], base[p >> 2], p & 3);
+#else
+    typedef uint32_t __attribute__((aligned(1))) u32_ua;
+    return *reinterpret_cast<const __attribute__((address_space(3))) u32_ua*>((lds_u8*)base + off + i);
+#endif
   }
   // the dword after next is loaded one step ahead so its latency overlaps
   // the caller's work on the current word (reads up to 11 bytes past i)

@@ -478,6 +478,9 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #ifndef OSE_URL_UAW
 #define OSE_URL_UAW 1     // assembly with unaligned 8-byte LDS reads and 8/4/2/1-byte stores (0: byte stores)
 #endif
+#ifndef OSE_URL_SLASH8
+#define OSE_URL_SLASH8 1  // an entry's separator stored with its body (unaligned stores)
+#endif
 #ifndef OSE_COPY_PF
 #define OSE_COPY_PF 1     // url_copy_kernel loads the next group's columns while it works on this one
 #endif
@@ -1636,6 +1639,26 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
         __hip_atomic_fetch_or(&img32[k], w & mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
 #else
+#if OSE_URL_UAW && OSE_URL_SLASH8 && !OSE_URL_ASMTAIL
+      // the separator goes out with the body: bytes [pos, pos + 1 + n) from
+      // the byte before the body, the first replaced by '/'
+      const uint32_t b0 = slash ? pos : pos + 1, nb = pos + 1 + n - b0;
+      lds_out_u8* dp = img + b0;
+      const lds_u8* sp = L + so - (slash ? 1u : 0u);
+      for (uint32_t q = 0; q < nb; q += 8) {
+        uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + q);
+        if (q == 0 && slash) v = (v & ~0xFFull) | '/';
+        const uint32_t rem = nb - q;
+        if (rem >= 8) {
+          *reinterpret_cast<lds_w64u*>(dp + q) = v;
+        } else {
+          uint32_t o = q;
+          if (rem & 4) { *reinterpret_cast<lds_w32u*>(dp + o) = (uint32_t)v; v >>= 32; o += 4; }
+          if (rem & 2) { *reinterpret_cast<lds_w16u*>(dp + o) = (uint16_t)v; v >>= 16; o += 2; }
+          if (rem & 1) dp[o] = (uint8_t)v;
+        }
+      }
+#else
       if (slash) img[pos] = '/';
       lds_out_u8* dp = img + pos + 1;
       const lds_u8* sp = L + so;
@@ -1679,6 +1702,7 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
           if (q + t < head) dp[q + t] = (uint8_t)b[t];
       }
 #endif
+#endif   // OSE_URL_SLASH8
 #endif
     }
     const uint64_t tm = __ballot(tail);
