@@ -479,7 +479,7 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 #define OSE_URL_UAW 1     // assembly with unaligned 8-byte LDS reads and 8/4/2/1-byte stores (0: byte stores)
 #endif
 #ifndef OSE_URL_SLASH8
-#define OSE_URL_SLASH8 1  // an entry's separator stored with its body (unaligned stores)
+#define OSE_URL_SLASH8 0  // 1: an entry's separator stored with its body (unaligned stores)
 #endif
 #ifndef OSE_COPY_PF
 #define OSE_COPY_PF 1     // url_copy_kernel loads the next group's columns while it works on this one
