@@ -258,7 +258,11 @@ typedef struct ose_batch ose_batch;
  * Go Config structs; absent sections are absent processors.  Validates
  * exactly as the Go Validate() does (same messages) and compiles every user
  * regexp to a DFA; a regexp the DFA compiler cannot express is OSE_ENOTSUP
- * (there is no host fallback).                                              */
+ * (there is no host fallback).  Any number of sampling rules: a rule list
+ * beyond one GPU rule table (64 http_latency rules, 64 service_name
+ * services + span_attribute rules, 12 KiB) runs as one trace-stage pass per
+ * chunk of the list with the same decisions; OSE_ENOTSUP remains for more
+ * than 64 span_attribute rules and jsonpath filters / scripts.             */
 int ose_engine_create(const char* cfg_json, ose_engine** out);
 /* The engine's batches (ose_batch, ose_otlp_batch, ose_otlp_out, ose_gbt)
  * may be released before or after this call: each holds a reference, and
@@ -359,7 +363,9 @@ int ose_profile_read(ose_engine* eng, char* json, size_t cap);
  * Record (OSE_XREC_BYTES = 56): u64 trace_id hi, lo, min start (~0 = none),
  * max end, endpoint bits, rule bits, then u64 {latency service id : 24
  * (0xFFFFFF = none) | flags : 8 (1 error, 2 latency element present, 4 a
- * zero start came first)}.
+ * zero start came first)}.  A sampling config that needs more than one
+ * rule chunk (ose_engine_create) is OSE_ENOTSUP here: a record carries one
+ * endpoint word and one rule-bit word.
  *
  * ose_shard_pack writes the records into per-owner buckets of `send`
  * (stable: source order inside a bucket), counts[n_ranks] (records per

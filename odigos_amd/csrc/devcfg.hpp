@@ -86,7 +86,8 @@ struct SampCfgDev {
   uint32_t n_lat_slots;      // distinct service names among them
   uint32_t n_services;       // interned service ids (res_svc values >= this are "no rule service")
   uint32_t n_attr;           // span_attribute rules: their bits follow the service-rule bits
-  uint32_t attr_shift;       // = number of service_name rules
+  uint32_t attr_shift;       // = number of service_name rule bits
+  uint32_t attr_base;        // attr_match bit of this table's first span_attribute rule (rule chunks)
   uint32_t rules_off;        // SampRuleDev[n_rules]
   uint32_t lat_off;          // SampLatDev[n_lat]
   uint32_t svc_slot_off;     // uint32 [n_services]: latency slot of each service, or ~0

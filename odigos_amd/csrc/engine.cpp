@@ -153,7 +153,8 @@ Engine::~Engine() {
   for (auto s : streams) (void)hipStreamDestroy(s);
   for (auto ev : event_pool) (void)hipEventDestroy(ev);
   if (url_blob_dev) (void)hipFree(url_blob_dev);
-  if (sampling_blob_dev) (void)hipFree(sampling_blob_dev);
+  for (auto* d : sampling_chunks_dev)
+    if (d) (void)hipFree(d);   // (sampling_blob_dev is the first)
   if (attr_blob_dev) (void)hipFree(attr_blob_dev);
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
@@ -164,6 +165,8 @@ Engine::~Engine() {
     if (w->runs) (void)hipFree(w->runs);
     if (w->run_count) (void)hipFree(w->run_count);
     if (w->attr_bits) (void)hipFree(w->attr_bits);
+    for (void* f : w->fold)
+      if (f) (void)hipFree(f);
     if (w->pending) (void)hipEventDestroy(w->pending);
     if (w->dup_host) (void)hipHostFree(w->dup_host);
     if (w->dup_ready) (void)hipEventDestroy(w->dup_ready);
@@ -610,8 +613,12 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
     if (rc) { delete e; return rc; }
   }
   if (e->has_sampling) {
-    rc = upload(e->sampling_blob_host, &e->sampling_blob_dev);
-    if (rc) { delete e; return rc; }
+    e->sampling_chunks_dev.assign(e->sampling_chunks_host.size(), nullptr);
+    for (size_t k = 0; k < e->sampling_chunks_host.size(); k++) {
+      rc = upload(e->sampling_chunks_host[k], &e->sampling_chunks_dev[k]);
+      if (rc) { delete e; return rc; }
+    }
+    e->sampling_blob_dev = e->sampling_chunks_dev[0];
   }
   if (!e->attr_blob_host.empty()) {
     rc = upload(e->attr_blob_host, &e->attr_blob_dev);
@@ -676,6 +683,7 @@ int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {
   int rc = ws->reserve(e->workspace_bytes(n_spans, arena_bytes));
   if (!rc && e->has_sampling) rc = ws->reserve_table(n_spans);
   if (!rc && e->attr_n_dev) rc = ws->reserve_attr(n_spans);
+  if (!rc && e->sampling_chunks_dev.size() > 1) rc = ws->reserve_fold(std::max<uint64_t>(n_spans, 1));
   e->release_ws(ws, nullptr);
   return rc;
 }

@@ -74,6 +74,9 @@ struct Workspace {
   uint32_t* run_count = nullptr;
   uint64_t runs_slots = 0;
   int reserve_runs();
+  void* fold[2] = {nullptr, nullptr};   // FoldState ping-pong of rule-chunked SAMPLE passes
+  uint64_t fold_cap = 0;
+  int reserve_fold(uint64_t n_spans);
   uint64_t* attr_bits = nullptr;   // span_attribute bits evaluated on the GPU (attr_host.cpp)
   uint64_t attr_bits_cap = 0;
   int reserve_attr(uint64_t n_spans);
@@ -103,8 +106,14 @@ struct Engine {
 
   std::vector<uint8_t> url_blob_host;
   uint8_t* url_blob_dev = nullptr;
-  std::vector<uint8_t> sampling_blob_host;
-  uint8_t* sampling_blob_dev = nullptr;
+  std::vector<uint8_t> sampling_blob_host;   // = sampling_chunks_host[0]
+  uint8_t* sampling_blob_dev = nullptr;      // = sampling_chunks_dev[0]
+  // the rule tables in consecutive chunks of the level-ordered rule list,
+  // each within the trace stage's bounds (64 latency bits, 64 service +
+  // span_attribute bits, kSampCfgLds bytes); one chunk for most configs
+  std::vector<std::vector<uint8_t>> sampling_chunks_host;
+  std::vector<uint8_t*> sampling_chunks_dev;
+  std::vector<uint8_t> sampling_chunk_attr;   // chunk has span_attribute rules
   std::unordered_map<std::string, uint32_t> service_ids;
   uint32_t sampling_n_lat = 0, sampling_n_attr = 0;
   // span_attribute rules: all of them (attr_n_rules), the GPU-evaluated ones

@@ -153,12 +153,27 @@ struct TraceRec {             // per-trace record, stored at the trace's head po
   double ratio;
 };
 enum : uint32_t { kTraceRuns = 0, kTracePerm = 1, kTraceBatch = 2 };
+// ShouldSample's walk between the passes of a rule-chunked configuration
+// (sampling_host.cpp build_sampling_tables): the level being folded, its
+// evaluateLevel accumulators and the min fallback of the closed levels
+struct FoldState {
+  double ratio;      // the open level's ratio (after kFsDone: the satisfied level's)
+  double min_fb;     // min fallback over closed matched levels (kFsHaveMin)
+  uint32_t level;    // the open level (after kFsDone: the satisfied level)
+  uint32_t flags;    // kFs*
+};
+enum : uint32_t { kFsSat = 1, kFsMatched = 2, kFsFoundFb = 4, kFsHaveMin = 8, kFsDone = 16 };
 struct TraceKernelArgs {
   uint64_t n_spans;
   uint32_t n_windows;         // ceil(n_spans / 64), >= 1
   uint32_t mode;              // kTrace*
   uint32_t n_resources;
   uint32_t epoch;             // hash table generation (>= 1)
+  // rule-chunked passes (both null: one pass, the whole rule list): the
+  // state before this chunk's rules (null in the first pass) and after them
+  // (null in the last pass, which decides), indexed by the trace's first span
+  const FoldState* fold_in;
+  FoldState* fold_out;
   const uint64_t* tid;
   const uint64_t* start;
   const uint64_t* end;

@@ -2,6 +2,9 @@
 // and the launch sequence of the trace stage (trace_kernel.hip).
 #include <algorithm>
 #include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
 #include <cstdlib>
 #include <cstring>
 
@@ -41,10 +44,16 @@ uint64_t fp_slots(uint64_t n) {
 // these ids with ose_engine_service_id.  Then lays out the device tables
 // (devcfg.hpp SampCfgDev): rules in level order global, service, endpoint
 // (rule_engine.go:56-60), config order within a level.
-int Engine::build_sampling_tables() {
-  service_ids.clear();
-  if (!has_sampling) return 0;
-  for (auto& kv : intern_services(sampling)) service_ids.emplace(kv.first, kv.second);
+namespace {
+// One chunk's device tables (devcfg.hpp SampCfgDev): the rules `pick` holds
+// (level, rule, global span_attribute index or -1), in the order given.
+struct PickedRule {
+  int level;
+  const SamplingRule* r;
+  int attr_index;
+};
+int build_sampling_blob(const std::unordered_map<std::string, uint32_t>& service_ids, const std::vector<PickedRule>& pick,
+                        std::vector<uint8_t>& b, bool& has_attr) {
   const uint32_t nsvc = (uint32_t)service_ids.size();
   std::vector<SampRuleDev> rules;
   std::vector<SampLatDev> lat;
@@ -53,24 +62,26 @@ int Engine::build_sampling_tables() {
   std::vector<uint64_t> svc_bits(std::max<uint32_t>(nsvc, 1), 0);
   std::string bytes;
   SampCfgDev h{};
-  uint32_t n_attr = 0, total_svc = 0, total_attr = 0;
-  const std::vector<SamplingRule>* levels[3] = {&sampling.global_rules, &sampling.service_rules,
-                                                &sampling.endpoint_rules};
   // A service_name rule is matched and satisfied iff some span's service is
   // the rule's (servicename.go:35-51): rules naming the same service share
   // one per-trace bit, so the bits count distinct services, not rules.
   std::map<std::string, uint32_t> svc_rule_bit;
-  for (auto* lvl : levels)
-    for (const SamplingRule& r : *lvl) {
-      if (r.rtype == RuleType::ServiceName && svc_rule_bit.emplace(r.service.service_name, total_svc).second) total_svc++;
-      total_attr += r.rtype == RuleType::SpanAttribute;
+  uint32_t n_svc_bits = 0, n_attr = 0;
+  int attr_base = -1;
+  for (const PickedRule& pr : pick) {
+    if (pr.r->rtype == RuleType::ServiceName && svc_rule_bit.emplace(pr.r->service.service_name, n_svc_bits).second)
+      n_svc_bits++;
+    if (pr.r->rtype == RuleType::SpanAttribute) {
+      if (attr_base < 0) attr_base = pr.attr_index;
+      n_attr++;
     }
-  if (total_svc + total_attr > kMaxServiceRules)
-    return fail(OSE_ENOTSUP, "service_name rules over more than 64 distinct services plus span_attribute rules are not "
-                             "supported by the GPU trace stage (64 per-trace bits)");
+  }
+  if (n_svc_bits + n_attr > kMaxServiceRules) return 1;
+  size_t k = 0;
   for (int L = 0; L < 3; L++) {
     h.level_first[L] = (uint32_t)rules.size();
-    for (const SamplingRule& r : *levels[L]) {
+    for (; k < pick.size() && pick[k].level == L; k++) {
+      const SamplingRule& r = *pick[k].r;
       SampRuleDev d{};
       switch (r.rtype) {
         case RuleType::Error:
@@ -78,8 +89,7 @@ int Engine::build_sampling_tables() {
           d.fallback = r.error.fallback_sampling_ratio;
           break;
         case RuleType::HttpLatency: {
-          if (lat.size() >= kMaxLatencyRules)
-            return fail(OSE_ENOTSUP, "more than 64 http_latency rules are not supported by the GPU trace stage");
+          if (lat.size() >= kMaxLatencyRules) return 1;
           d.type = kSampLatency;
           d.bit = (uint32_t)lat.size();
           d.fallback = r.latency.fallback_sampling_ratio;
@@ -96,30 +106,29 @@ int Engine::build_sampling_tables() {
           // Milliseconds() >= threshold  <=>  ns >= threshold * 1e6 for threshold >= 1
           // (truncation toward zero; Validate rejects threshold <= 0)
           ld.threshold_ns = r.latency.threshold <= INT64_MAX / 1000000 ? r.latency.threshold * 1000000 : INT64_MAX;
-          for (uint32_t b = 0; b < 16 && b < ld.route_len; b++) {
-            ld.pre[b / 4] |= (uint32_t)(uint8_t)r.latency.http_route[b] << (8 * (b % 4));
-            ld.msk[b / 4] |= 0xFFu << (8 * (b % 4));
+          for (uint32_t q = 0; q < 16 && q < ld.route_len; q++) {
+            ld.pre[q / 4] |= (uint32_t)(uint8_t)r.latency.http_route[q] << (8 * (q % 4));
+            ld.msk[q / 4] |= 0xFFu << (8 * (q % 4));
           }
           bytes += r.latency.http_route;
           slot_rules[ld.slot] |= 1ull << d.bit;
           lat.push_back(ld);
           break;
         }
-        case RuleType::ServiceName: {
+        case RuleType::ServiceName:
           d.type = kSampService;
           d.bit = svc_rule_bit.at(r.service.service_name);
           d.ratio = r.service.sampling_ratio;
           d.fallback = r.service.fallback_sampling_ratio;
           svc_bits[service_ids.at(r.service.service_name)] |= 1ull << d.bit;
           break;
-        }
         case RuleType::SpanAttribute:
           // the shim evaluates the per-span condition (attr_match column,
           // odigos_amd/csrc/span_attr.cpp); the trace stage ORs the bits per
           // trace: satisfied iff any span met it, never matched-but-unsatisfied
           // (spanattribute.go:126-320), i.e. a service_name-shaped rule
           d.type = kSampService;
-          d.bit = total_svc + n_attr++;
+          d.bit = n_svc_bits + (uint32_t)(pick[k].attr_index - attr_base);
           d.ratio = r.attr.sampling_ratio;
           d.fallback = r.attr.fallback_sampling_ratio;
           break;
@@ -133,14 +142,15 @@ int Engine::build_sampling_tables() {
   h.n_lat_slots = (uint32_t)slot_rules.size();
   h.n_services = nsvc;
   h.n_attr = n_attr;
-  h.attr_shift = total_svc;
+  h.attr_shift = n_svc_bits;
+  h.attr_base = attr_base < 0 ? 0u : (uint32_t)attr_base;
   if (slot_rules.empty()) slot_rules.push_back(0);
-  std::vector<uint8_t> b(sizeof(SampCfgDev), 0);
+  b.assign(sizeof(SampCfgDev), 0);
   auto put = [&](const void* p, size_t nb) {
     while (b.size() % 16) b.push_back(0);
     uint32_t off = (uint32_t)b.size();
-    const uint8_t* s = static_cast<const uint8_t*>(p);
-    b.insert(b.end(), s, s + nb);
+    const uint8_t* src = static_cast<const uint8_t*>(p);
+    b.insert(b.end(), src, src + nb);
     return off;
   };
   h.rules_off = put(rules.data(), rules.size() * sizeof(SampRuleDev));
@@ -152,13 +162,70 @@ int Engine::build_sampling_tables() {
   while (b.size() % 16) b.push_back(0);
   b.resize(b.size() + 16, 0);
   h.total_bytes = (uint32_t)b.size();
-  if (h.total_bytes > kSampCfgLds)
-    return fail(OSE_ENOTSUP, "odigossampling rule tables exceed " + std::to_string(kSampCfgLds) +
-                                 " bytes (the GPU trace stage keeps them in LDS): shorten http_route values or rules");
+  if (h.total_bytes > kSampCfgLds) return 1;
   std::memcpy(b.data(), &h, sizeof h);
-  sampling_blob_host = std::move(b);
-  sampling_n_lat = h.n_lat;
-  sampling_n_attr = h.n_attr;
+  has_attr = n_attr > 0;
+  return 0;
+}
+}  // namespace
+
+// Interns every service name a rule compares against (latency.go:55,
+// servicename.go:40, spanattribute.go:130); the shim maps resources onto
+// these ids with ose_engine_service_id.  Then lays out the device tables
+// (devcfg.hpp SampCfgDev): rules in level order global, service, endpoint
+// (rule_engine.go:56-60), config order within a level.  A rule list beyond
+// one table's bounds (64 latency bits, 64 service + span_attribute bits,
+// kSampCfgLds bytes) is cut into consecutive chunks, each as large as fits;
+// the trace stage then runs once per chunk and carries ShouldSample's walk
+// from one to the next (trace_kernel.hip decide_chunk), so every config
+// Validate accepts runs (the span_attribute bits of a span stay one 64-bit
+// attr_match word: at most 64 span_attribute rules, as columnize.cpp).
+int Engine::build_sampling_tables() {
+  service_ids.clear();
+  sampling_chunks_host.clear();
+  sampling_chunk_attr.clear();
+  if (!has_sampling) return 0;
+  for (auto& kv : intern_services(sampling)) service_ids.emplace(kv.first, kv.second);
+  const std::vector<SamplingRule>* levels[3] = {&sampling.global_rules, &sampling.service_rules,
+                                                &sampling.endpoint_rules};
+  std::vector<PickedRule> all;
+  uint32_t n_lat = 0, n_attr = 0;
+  for (int L = 0; L < 3; L++)
+    for (const SamplingRule& r : *levels[L]) {
+      all.push_back(PickedRule{L, &r, r.rtype == RuleType::SpanAttribute ? (int)n_attr : -1});
+      n_attr += r.rtype == RuleType::SpanAttribute;
+      n_lat += r.rtype == RuleType::HttpLatency;
+    }
+  if (n_attr > 64)
+    return fail(OSE_ENOTSUP, "more than 64 span_attribute rules are not supported (one 64-bit attr_match word per span)");
+  // greedy: extend the chunk while its tables fit (a rule that alone does not
+  // fit: its route bytes or the service tables exceed kSampCfgLds)
+  size_t k = 0;
+  do {
+    std::vector<PickedRule> cur;
+    std::vector<uint8_t> fitted, blob;
+    bool fitted_attr = false, attr = false;
+    if (build_sampling_blob(service_ids, cur, fitted, fitted_attr))
+      return fail(OSE_ENOTSUP, "odigossampling service tables exceed " + std::to_string(kSampCfgLds) +
+                                   " bytes (the GPU trace stage keeps them in LDS): too many distinct service names");
+    for (; k < all.size(); k++) {
+      cur.push_back(all[k]);
+      if (build_sampling_blob(service_ids, cur, blob, attr)) {
+        cur.pop_back();
+        break;
+      }
+      fitted.swap(blob);
+      fitted_attr = attr;
+    }
+    if (cur.empty() && k < all.size())
+      return fail(OSE_ENOTSUP, "odigossampling rule tables exceed " + std::to_string(kSampCfgLds) +
+                                   " bytes for one rule (the GPU trace stage keeps them in LDS): shorten its http_route");
+    sampling_chunks_host.push_back(std::move(fitted));
+    sampling_chunk_attr.push_back(fitted_attr ? 1 : 0);
+  } while (k < all.size());
+  sampling_blob_host = sampling_chunks_host[0];
+  sampling_n_lat = n_lat;
+  sampling_n_attr = n_attr;
   return 0;
 }
 
@@ -239,8 +306,24 @@ int Workspace::reserve_table(uint64_t n_spans) {
   return 0;
 }
 
-int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
-                 hipStream_t st, Workspace* ws, std::function<int()>* tail) {
+int Workspace::reserve_fold(uint64_t n_spans) {
+  if (fold_cap >= n_spans && fold[0]) return 0;
+  for (void*& f : fold) {
+    if (f) HIP_TRY(hipFree(f));
+    f = nullptr;
+  }
+  fold_cap = 0;
+  for (void*& f : fold) HIP_TRY(hipMalloc(&f, n_spans * sizeof(FoldState)));
+  fold_cap = n_spans;
+  return 0;
+}
+
+namespace {
+// One pass of the trace stage over the rule tables of `chunk`; fold_in /
+// fold_out: the FoldState before / after this chunk's rules (run_sampling)
+int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
+                      hipStream_t st, Workspace* ws, std::function<int()>* tail, uint32_t chunk,
+                      const FoldState* fold_in, FoldState* fold_out) {
   if (!e->has_sampling) return fail(OSE_EINVAL, "odigossampling is not configured on this engine");
   if (group_mode != OSE_GROUP_TRACE_ID && group_mode != OSE_GROUP_BATCH) return fail(OSE_EINVAL, "unknown group_mode");
   const uint64_t n = c->n_spans;
@@ -323,7 +406,9 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.arena = c->arena;
   a.res_svc = c->res_svc;
   a.res_svc_str = c->res_svc_str;
-  a.cfg = e->sampling_blob_dev;
+  a.cfg = e->sampling_chunks_dev[chunk];
+  a.fold_in = fold_in;
+  a.fold_out = fold_out;
   a.seed = rnd ? rnd->seed : 0;
   a.keep = o->keep;
   a.rec = per_trace ? rec : nullptr;
@@ -340,7 +425,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     const uint64_t* am = nullptr;
     const int ar = resolve_attr_match(e, c, ws, st, &am);
     if (ar) return ar;
-    a.attr_match = e->sampling_n_attr ? am : nullptr;
+    a.attr_match = e->sampling_n_attr && e->sampling_chunk_attr[chunk] ? am : nullptr;
   }
   a.svc_match = c->svc_match;
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
@@ -522,6 +607,28 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
     }
     return rest(ws->dup_host[0] != 0);
   };
+  return 0;
+}
+
+}  // namespace
+
+// The trace stage: one pass per rule chunk (build_sampling_tables); with more
+// than one, each pass but the last saves ShouldSample's walk per trace and
+// the next resumes it (ping-pong buffers: a pass's provisional fast-path
+// decisions for traces the slow path redoes never reach the state it reads).
+// Chunked passes run without the host-gated tail.
+int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
+                 hipStream_t st, Workspace* ws, std::function<int()>* tail) {
+  const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
+  if (K <= 1) return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr);
+  int rc = ws->reserve_fold(std::max<uint64_t>(c->n_spans, 1));
+  if (rc) return rc;
+  for (uint32_t k = 0; k < K; k++) {
+    const FoldState* in = k ? static_cast<const FoldState*>(ws->fold[(k - 1) & 1]) : nullptr;
+    FoldState* out = k + 1 < K ? static_cast<FoldState*>(ws->fold[k & 1]) : nullptr;
+    rc = run_sampling_pass(e, c, o, group_mode, rnd, st, ws, nullptr, k, in, out);
+    if (rc) return rc;
+  }
   return 0;
 }
 

@@ -408,6 +408,9 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   if (!eng || !c || !send || !counts || !pack_pos) return fail(OSE_EINVAL, "NULL argument");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_pack needs odigossampling on the engine");
+  if (e->sampling_chunks_dev.size() > 1)   // a partial record carries one 64-bit endpoint and service word
+    return fail(OSE_ENOTSUP, "trace-id exchange: the sampling rules need more than one rule chunk (over 64 "
+                             "http_latency rules or 64 service + span_attribute bits); shard by trace id upstream");
   if (int brc = bind_device(e)) return brc;
   if (n_ranks == 0 || n_ranks > 64) return fail(OSE_EINVAL, "n_ranks must be in 1..64");
   const uint64_t n = c->n_spans;

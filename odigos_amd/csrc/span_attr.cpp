@@ -404,59 +404,240 @@ void marshal(const JVal& v, std::string& o) {
   }
 }
 
-// jsonpath.Get on a parsed simple path; false = an error (unknown key,
-// index out of range, step on a non-container).
-bool jsonpath_get(const std::vector<JsonPathStep>& path, const JVal& root, const JVal*& out) {
-  const JVal* cur = &root;
-  for (auto& st : path) {
-    if (st.is_index) {
-      if (cur->t != JVal::Arr) return false;
-      long long i = st.index;
-      if (i < 0) i += (long long)cur->a.size();
-      if (i < 0 || i >= (long long)cur->a.size()) return false;
-      cur = &cur->a[(size_t)i];
-    } else {
-      if (cur->t != JVal::Obj) return false;
-      auto it = cur->o.find(st.key);
-      if (it == cur->o.end()) return false;
-      cur = &it->second;
+// jsonpath.Get on a plain path (Key / Index selectors only); false = an
+// error (unknown key, index out of range, step on a non-container).
+bool plain_select(const JsonPathStep& st, const JVal& cur, const JVal*& out) {
+  if (st.kind == JsonPathStep::Index) {
+    if (cur.t != JVal::Arr) return false;
+    long long i = st.index;
+    if (i < 0) i += (long long)cur.a.size();
+    if (i < 0 || i >= (long long)cur.a.size()) return false;
+    out = &cur.a[(size_t)i];
+    return true;
+  }
+  if (cur.t != JVal::Obj) return false;
+  auto it = cur.o.find(st.key);
+  if (it == cur.o.end()) return false;
+  out = &it->second;
+  return true;
+}
+
+// The children of a container in visiting order: array order, object keys
+// sorted (Go's map order is unspecified; sorted is one of its orders)
+template <class F>
+void visit_children(const JVal& v, F&& f) {
+  if (v.t == JVal::Arr)
+    for (const JVal& e : v.a) f(e);
+  else if (v.t == JVal::Obj)
+    for (const auto& kv : v.o) f(kv.second);
+}
+
+// One selector over one value: the matches it yields (an ambiguous path
+// drops the branches a plain selector fails on instead of failing)
+void select_step(const JsonPathStep& st, const JVal& v, std::vector<const JVal*>& out) {
+  switch (st.kind) {
+    case JsonPathStep::Key:
+    case JsonPathStep::Index: {
+      const JVal* r = nullptr;
+      if (plain_select(st, v, r)) out.push_back(r);
+      break;
+    }
+    case JsonPathStep::Wild:
+      visit_children(v, [&](const JVal& c) { out.push_back(&c); });
+      break;
+    case JsonPathStep::Union:
+      for (const JsonPathStep& it : st.items) select_step(it, v, out);
+      break;
+    case JsonPathStep::Slice: {
+      if (v.t != JVal::Arr) break;
+      const long long n = (long long)v.a.size();
+      long long lo = st.has_lo ? st.lo : 0, hi = st.has_hi ? st.hi : n;
+      if (lo < 0) lo += n;
+      if (hi < 0) hi += n;
+      lo = std::max(0LL, std::min(lo, n));
+      hi = std::max(0LL, std::min(hi, n));
+      if (st.step > 0)
+        for (long long k = lo; k < hi; k += st.step) out.push_back(&v.a[(size_t)k]);
+      else if (st.step < 0)
+        for (long long k = hi - 1; k >= lo; k += st.step) out.push_back(&v.a[(size_t)k]);
+      break;
+    }
+    case JsonPathStep::Descend: {
+      // `..x`: x over the value itself and every descendant, pre-order
+      std::vector<const JVal*> stack{&v};
+      while (!stack.empty()) {
+        const JVal* cur = stack.back();
+        stack.pop_back();
+        select_step(st.items[0], *cur, out);
+        std::vector<const JVal*> kids;
+        visit_children(*cur, [&](const JVal& c) { kids.push_back(&c); });
+        for (auto it = kids.rbegin(); it != kids.rend(); ++it) stack.push_back(*it);
+      }
+      break;
     }
   }
-  out = cur;
+}
+
+bool path_is_plain(const std::vector<JsonPathStep>& path) {
+  for (const JsonPathStep& st : path)
+    if (st.kind != JsonPathStep::Key && st.kind != JsonPathStep::Index) return false;
+  return true;
+}
+
+// jsonpath.Get.  A plain path yields its value or an error (false); a path
+// with an ambiguous selector never errs and yields the list of its matches
+// (`holder` keeps that list).
+bool jsonpath_get(const std::vector<JsonPathStep>& path, const JVal& root, const JVal*& out, JVal& holder) {
+  if (path_is_plain(path)) {
+    const JVal* cur = &root;
+    for (const JsonPathStep& st : path)
+      if (!plain_select(st, *cur, cur)) return false;
+    out = cur;
+    return true;
+  }
+  std::vector<const JVal*> cur{&root}, next;
+  for (const JsonPathStep& st : path) {
+    next.clear();
+    for (const JVal* v : cur) select_step(st, *v, next);
+    cur.swap(next);
+  }
+  holder = JVal{};
+  holder.t = JVal::Arr;
+  for (const JVal* v : cur) holder.a.push_back(*v);
+  out = &holder;
+  return true;
+}
+
+// A bracket item: 'key', "key" or an integer
+bool parse_bracket_item(const std::string& p, size_t& i, JsonPathStep& out) {
+  while (i < p.size() && p[i] == ' ') i++;
+  if (i < p.size() && (p[i] == '\'' || p[i] == '"')) {
+    const char q = p[i++];
+    const size_t b = i;
+    while (i < p.size() && p[i] != q) i++;
+    if (i >= p.size()) return false;
+    out.kind = JsonPathStep::Key;
+    out.key = p.substr(b, i - b);
+    i++;
+  } else {
+    const size_t b = i;
+    if (i < p.size() && p[i] == '-') i++;
+    while (i < p.size() && std::isdigit((unsigned char)p[i])) i++;
+    if (i == b || (p[b] == '-' && i == b + 1)) return false;
+    out.kind = JsonPathStep::Index;
+    out.index = std::atoll(p.substr(b, i - b).c_str());
+  }
+  while (i < p.size() && p[i] == ' ') i++;
+  return true;
+}
+
+bool parse_int_opt(const std::string& p, size_t& i, bool& has, long long& v) {
+  while (i < p.size() && p[i] == ' ') i++;
+  const size_t b = i;
+  if (i < p.size() && p[i] == '-') i++;
+  while (i < p.size() && std::isdigit((unsigned char)p[i])) i++;
+  if (i == b) {
+    has = false;
+    return true;
+  }
+  if (p[b] == '-' && i == b + 1) return false;
+  has = true;
+  v = std::atoll(p.substr(b, i - b).c_str());
+  while (i < p.size() && p[i] == ' ') i++;
+  return true;
+}
+
+// `[...]` after the '[': *, 'k', n, unions of those, a:b:c slices
+bool parse_bracket(const std::string& p, size_t& i, JsonPathStep& out) {
+  while (i < p.size() && p[i] == ' ') i++;
+  if (i < p.size() && (p[i] == '?' || p[i] == '(')) return false;   // filter / script: not restated
+  if (i < p.size() && p[i] == '*') {
+    i++;
+    while (i < p.size() && p[i] == ' ') i++;
+    out.kind = JsonPathStep::Wild;
+  } else {
+    // a slice starts with an optional integer and a ':'
+    size_t j = i;
+    bool has_lo = false;
+    long long lo = 0;
+    if (parse_int_opt(p, j, has_lo, lo) && j < p.size() && p[j] == ':') {
+      out = JsonPathStep{};
+      out.kind = JsonPathStep::Slice;
+      out.has_lo = has_lo;
+      out.lo = lo;
+      i = j + 1;
+      if (!parse_int_opt(p, i, out.has_hi, out.hi)) return false;
+      if (i < p.size() && p[i] == ':') {
+        i++;
+        bool has_step = false;
+        if (!parse_int_opt(p, i, has_step, out.step)) return false;
+        if (!has_step) out.step = 1;
+      }
+    } else {
+      JsonPathStep first;
+      if (!parse_bracket_item(p, i, first)) return false;
+      if (i < p.size() && p[i] == ',') {
+        out = JsonPathStep{};
+        out.kind = JsonPathStep::Union;
+        out.items.push_back(first);
+        while (i < p.size() && p[i] == ',') {
+          i++;
+          JsonPathStep it;
+          if (!parse_bracket_item(p, i, it)) return false;
+          out.items.push_back(it);
+        }
+      } else {
+        out = first;
+      }
+    }
+  }
+  if (i >= p.size() || p[i] != ']') return false;
+  i++;
   return true;
 }
 
 bool parse_jsonpath(const std::string& p, std::vector<JsonPathStep>& out) {
   if (p.empty() || p[0] != '$') return false;
   size_t i = 1;
+  auto name = [&](JsonPathStep& st) {
+    const size_t b = i;
+    while (i < p.size() && (std::isalnum((unsigned char)p[i]) || p[i] == '_' || p[i] == '-')) i++;
+    if (i == b) return false;
+    st.kind = JsonPathStep::Key;
+    st.key = p.substr(b, i - b);
+    return true;
+  };
   while (i < p.size()) {
-    if (p[i] == '.') {
+    JsonPathStep st;
+    if (p[i] == '.' && i + 1 < p.size() && p[i + 1] == '.') {
+      i += 2;
+      JsonPathStep sel;
+      if (i < p.size() && p[i] == '*') {
+        i++;
+        sel.kind = JsonPathStep::Wild;
+      } else if (i < p.size() && p[i] == '[') {
+        i++;
+        if (!parse_bracket(p, i, sel)) return false;
+      } else if (!name(sel)) {
+        return false;
+      }
+      st.kind = JsonPathStep::Descend;
+      st.items.push_back(sel);
+    } else if (p[i] == '.') {
       i++;
-      size_t b = i;
-      while (i < p.size() && (std::isalnum((unsigned char)p[i]) || p[i] == '_' || p[i] == '-')) i++;
-      if (i == b) return false;   // "..", ".*" and friends: not a simple path
-      out.push_back(JsonPathStep{false, p.substr(b, i - b), 0});
+      if (i < p.size() && p[i] == '*') {
+        i++;
+        st.kind = JsonPathStep::Wild;
+      } else if (!name(st)) {
+        return false;
+      }
     } else if (p[i] == '[') {
       i++;
-      if (i < p.size() && (p[i] == '\'' || p[i] == '"')) {
-        char q = p[i++];
-        size_t b = i;
-        while (i < p.size() && p[i] != q) i++;
-        if (i >= p.size()) return false;
-        out.push_back(JsonPathStep{false, p.substr(b, i - b), 0});
-        i++;
-      } else {
-        size_t b = i;
-        if (i < p.size() && p[i] == '-') i++;
-        while (i < p.size() && std::isdigit((unsigned char)p[i])) i++;
-        if (i == b || (p[b] == '-' && i == b + 1)) return false;
-        out.push_back(JsonPathStep{true, "", std::atoll(p.substr(b, i - b).c_str())});
-      }
-      if (i >= p.size() || p[i] != ']') return false;
-      i++;
+      if (!parse_bracket(p, i, st)) return false;
     } else {
       return false;
     }
+    out.push_back(std::move(st));
   }
   return true;
 }
@@ -482,7 +663,8 @@ std::string SpanAttrPredicate::compile(const SpanAttributeRule& r) {
                           op_ == "key_not_equals")) {
     if (!parse_jsonpath(r.json_path, path_))
       return "span_attribute json_path \"" + r.json_path +
-             "\" is not a simple path ($, .key, ['key'], [index]): not supported by the engine";
+             "\" is not supported by the engine ($, .key, ['key'], [index], *, [a,b], [a:b:c] and .. are; "
+             "filters and scripts are not)";
   }
   return "";
 }
@@ -528,7 +710,8 @@ bool SpanAttrPredicate::eval(const Value& attr) const {
     if (op_ == "is_invalid_json") return !ok;
     if (!ok) return false;
     const JVal* res = nullptr;
-    const bool found = jsonpath_get(path_, root, res);
+    JVal matches;
+    const bool found = jsonpath_get(path_, root, res, matches);
     if (op_ == "contains_key") return found && res->t != JVal::Null;
     if (op_ == "not_contains_key") return !found;
     if (op_ == "key_equals" || op_ == "key_not_equals") {

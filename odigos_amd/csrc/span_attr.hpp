@@ -11,9 +11,11 @@
 //                  Marshal of nested values (sorted keys, HTML escaping)
 //   strconv        ParseFloat, ParseBool, FormatFloat(v, 'f', -1, 64)
 //   regexp         the DFA compiler of regex_dfa.hpp
-//   PaesslerAG/jsonpath v0.1.1  Get on simple paths: $, .key, ['key'],
-//                  ["key"], [index]; other syntax is OSE_ENOTSUP at
-//                  engine creation (documented, parity unpinned)
+//   PaesslerAG/jsonpath v0.1.1  Get: $, .key, ['key'], ["key"], [index]
+//                  (pinned by the KATs); the ambiguous selectors *, [*],
+//                  [a,b], [a:b:c], ..  return the match list (parity
+//                  unpinned: the library is not in the reference); filters
+//                  [?(..)] and scripts [(..)] are OSE_ENOTSUP at creation
 #pragma once
 #include <memory>
 #include <string>
@@ -25,10 +27,16 @@
 
 namespace ose {
 
+// One selector of a PaesslerAG/jsonpath path: plain (Key, Index) or
+// ambiguous (Wild `*` / `[*]`, Union `[a,b]`, Slice `[a:b:c]`, Descend `..`
+// followed by its selector)
 struct JsonPathStep {
-  bool is_index = false;
+  enum Kind { Key, Index, Wild, Union, Slice, Descend } kind = Key;
   std::string key;
   long long index = 0;
+  std::vector<JsonPathStep> items;   // Union: Key / Index items; Descend: the selector after `..`
+  bool has_lo = false, has_hi = false;
+  long long lo = 0, hi = 0, step = 1;   // Slice
 };
 
 class SpanAttrPredicate {

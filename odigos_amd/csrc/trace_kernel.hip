@@ -325,6 +325,94 @@ __device__ __forceinline__ void decide(const Cfg& c, uint32_t err, uint64_t ep, 
   }
 }
 
+// One chunk of a rule-chunked configuration: the same walk as decide() over
+// this chunk's rules (level order, config order), resumed from and saved to
+// the trace's FoldState; the last pass closes the remaining levels and
+// decides.  Pass by pass it is decide() over the whole rule list.
+__device__ void decide_chunk(const TraceKernelArgs& a, const Cfg& c, uint64_t first, uint32_t err, uint64_t ep,
+                             uint64_t lsat, uint64_t svc, double u, uint8_t& keep, uint8_t& level, double& ratio_out) {
+  FoldState s = a.fold_in ? a.fold_in[first] : FoldState{0.0, 0.0, 0u, 0u};
+  auto close = [&]() {   // the end of evaluateLevel for level s.level
+    if (s.flags & kFsSat) {
+      s.flags = kFsDone | (s.flags & kFsHaveMin);
+      return;
+    }
+    if ((s.flags & kFsMatched) && (!(s.flags & kFsHaveMin) || s.ratio < s.min_fb)) {
+      s.min_fb = s.ratio;
+      s.flags |= kFsHaveMin;
+    }
+    s.flags &= kFsHaveMin;
+    s.ratio = 0;
+    s.level++;
+  };
+  for (uint32_t L = 0; L < 3 && !(s.flags & kFsDone); L++) {
+    const uint32_t k0 = c.h->level_first[L], k1 = c.h->level_first[L + 1];
+    if (k0 == k1) continue;
+    while (s.level < L && !(s.flags & kFsDone)) close();
+    if (s.flags & kFsDone) break;
+    for (uint32_t k = k0; k < k1; k++) {
+      const SampRuleDev& r = c.rules[k];
+      bool mt, st;
+      double p;
+      if (r.type == kSampError) {
+        mt = true;
+        st = err != 0;
+        p = st ? 100.0 : r.fallback;
+      } else if (r.type == kSampLatency) {
+        mt = (ep >> r.bit) & 1;
+        st = mt && ((lsat >> r.bit) & 1);
+        p = st ? 100.0 : (mt ? r.fallback : 0.0);
+      } else {
+        mt = st = (svc >> r.bit) & 1;
+        p = st ? r.ratio : r.fallback;
+      }
+      if (st) {
+        s.ratio = s.ratio > p ? s.ratio : p;
+        s.flags |= kFsSat | kFsMatched;
+      } else if (mt) {
+        s.flags |= kFsMatched;
+        if (!(s.flags & kFsFoundFb)) {
+          s.ratio = p;
+          s.flags |= kFsFoundFb;
+        } else {
+          s.ratio = s.ratio < p ? s.ratio : p;
+        }
+      }
+    }
+  }
+  if (a.fold_out) {   // more chunks follow: save the walk (this pass's keep is rewritten by the last)
+    a.fold_out[first] = s;
+    keep = 1;
+    level = 4;
+    ratio_out = 100.0;
+    return;
+  }
+  while (s.level < 3 && !(s.flags & kFsDone)) close();
+  if (s.flags & kFsDone) {
+    level = (uint8_t)s.level;
+    ratio_out = s.ratio;
+    keep = u * 100 < s.ratio;
+  } else if (s.flags & kFsHaveMin) {
+    level = 3;
+    ratio_out = s.min_fb;
+    keep = u * 100 < s.min_fb;
+  } else {
+    level = 4;
+    ratio_out = 100.0;
+    keep = 1;
+  }
+}
+// decide() or, in a rule-chunked pass, decide_chunk(); first: the trace's
+// first span in batch order (the FoldState index)
+__device__ __forceinline__ void decide_at(const TraceKernelArgs& a, const Cfg& c, uint64_t first, uint32_t err,
+                                          uint64_t ep, uint64_t lsat, uint64_t svc, double u, uint8_t& keep,
+                                          uint8_t& level, double& ratio_out) {
+  if (a.fold_in || a.fold_out)
+    decide_chunk(a, c, first, err, ep, lsat, svc, u, keep, level, ratio_out);
+  else
+    decide(c, err, ep, lsat, svc, u, keep, level, ratio_out);
+}
+
 // ---- exact trace_id table -------------------------------------------------
 // Insert protocol: CAS the state from a stale epoch to BUSY, store the key
 // with sc1 (agent-scope relaxed) stores, drain them (s_waitcnt vmcnt(0)), then
@@ -558,8 +646,8 @@ __device__ void flush_queue(const TraceKernelArgs& a, const Cfg& c, DecideQ& Q, 
     pos = Q.pos[lane];
     len = Q.len[lane];
     if (!(a.ablate & 4))
-      decide(c, Q.err[lane], Q.ep[lane], Q.lsat[lane], Q.svc[lane], trace_uniform(Q.hi[lane], Q.lo[lane], a.seed), dk,
-             dl, dr);
+      decide_at(a, c, a.mode == kTracePerm ? a.perm[pos] : (a.mode == kTraceBatch ? 0u : pos), Q.err[lane], Q.ep[lane],
+                Q.lsat[lane], Q.svc[lane], trace_uniform(Q.hi[lane], Q.lo[lane], a.seed), dk, dl, dr);
     write_rec(a, pos, dk, dl, dr);
   }
   const uint32_t mlen = wave_max_u32((uint32_t)lane < qn ? len : 0u);
@@ -594,6 +682,8 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     a.key = nullptr;
     a.batch_keep = nullptr;
     a.ablate = 0;
+    a.fold_in = nullptr;
+    a.fold_out = nullptr;
   }
   if (a.mode == kTracePerm && __hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   __shared__ DecideQ queues[kTWaves];
@@ -631,7 +721,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
   if (n == 0) {   // kTraceBatch only: one trace with no spans
     uint8_t k, l;
     double r;
-    decide(c, 0, 0, 0, batch_svc, trace_uniform(0, 0, a.seed), k, l, r);
+    decide_at(a, c, 0, 0, 0, 0, batch_svc, trace_uniform(0, 0, a.seed), k, l, r);
     if (lane == 0) {
       if (a.batch_keep) *a.batch_keep = k;
       if (a.win_heads) a.win_heads[0] = 1;
@@ -749,7 +839,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         svcb = r.svm;
       } else {
         if (a.mode != kTraceBatch && ss < nsvc) svcb = c.svc_bits[ss];
-        if (a.attr_match) svcb |= a.attr_match[r.i] << c.h->attr_shift;
+        if (a.attr_match) svcb |= (a.attr_match[r.i] >> c.h->attr_base) << c.h->attr_shift;
       }
       if (s < nsvc) {
         slot = c.svc_slot[s];
@@ -1018,7 +1108,7 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
           svc_acc |= r.svm;
         } else {
           if (ss < nsvc) svc_acc |= c.svc_bits[ss];
-          svc_acc |= r.am << c.h->attr_shift;
+          svc_acc |= (r.am >> c.h->attr_base) << c.h->attr_shift;
         }
         if (sv < nsvc) {
           slot = c.svc_slot[sv];
@@ -1079,8 +1169,9 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
         const uint4 t = reinterpret_cast<const uint4*>(a.tid)[pos];
         uint8_t dk = 0, dl = 0;
         double dr = 0;
-        decide(c, E, EP, s_l, SV, trace_uniform((uint64_t)t.x | ((uint64_t)t.y << 32), (uint64_t)t.z | ((uint64_t)t.w << 32), a.seed),
-               dk, dl, dr);
+        decide_at(a, c, pos, E, EP, s_l, SV,
+                  trace_uniform((uint64_t)t.x | ((uint64_t)t.y << 32), (uint64_t)t.z | ((uint64_t)t.w << 32), a.seed), dk,
+                  dl, dr);
         write_rec(a, pos, dk, dl, dr);
         sm.keep = dk;
       }
@@ -1214,7 +1305,7 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
         } else {
           const uint32_t ss = a.res_svc_str[res];
           if (ss < nsvc) svcb |= c.svc_bits[ss];
-          if (a.attr_match) svcb |= a.attr_match[q] << c.h->attr_shift;
+          if (a.attr_match) svcb |= (a.attr_match[q] >> c.h->attr_base) << c.h->attr_shift;
         }
         if (sv >= nsvc) continue;
         const uint32_t slt = c.svc_slot[sv];
@@ -1244,7 +1335,7 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
     const uint64_t hi = a.tid[2 * p], lo = a.tid[2 * p + 1];
     uint8_t dk = 0, dl = 0;
     double dr = 0;
-    decide(c, err, ep, lsat, svcb, trace_uniform(hi, lo, a.seed), dk, dl, dr);
+    decide_at(a, c, p, err, ep, lsat, svcb, trace_uniform(hi, lo, a.seed), dk, dl, dr);
     write_rec(a, p, dk, dl, dr);
     for (uint32_t r = 0; r < nr; r++) {
       const uint64_t s0 = rs[r], s1 = run_end(a, s0);
@@ -1462,7 +1553,7 @@ __device__ __forceinline__ XSpan x_span(const ShardArgs& a, const Cfg& c, uint64
   x.err = a.status[j] == OSE_STATUS_ERROR;
   const uint32_t ss = a.res_svc_str[res];
   x.svcb = ss < nsvc ? c.svc_bits[ss] : 0;
-  if (a.attr_match) x.svcb |= a.attr_match[j] << c.h->attr_shift;
+  if (a.attr_match) x.svcb |= (a.attr_match[j] >> c.h->attr_base) << c.h->attr_shift;
   if (x.slot != kNoSlot) {
     x.ep = a.route_match ? a.route_match[j] & c.slot_rules[x.slot] : endpoint_bits(c, x.slot, a.arena, a.route[j]);
     x.st = a.start ? a.start[j] : 0;
@@ -1640,7 +1731,7 @@ void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, u
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t per_block = kTWaves * a.win_per_wave;
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
-  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate)
+  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate && !a.fold_in && !a.fold_out)
     hipLaunchKernelGGL(trace_eval_kernel<true>, dim3(blocks), dim3(kTThreads), 0, st, a);
   else
     hipLaunchKernelGGL(trace_eval_kernel<false>, dim3(blocks), dim3(kTThreads), 0, st, a);

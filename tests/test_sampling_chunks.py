@@ -1,0 +1,155 @@
+"""odigossampling configs beyond one rule table: more than 64 http_latency
+rules, more than 64 distinct service_name services, tables beyond the LDS
+budget.  The engine cuts the level-ordered rule list into chunks and runs the
+trace stage once per chunk, carrying ShouldSample's walk per trace
+(sampling_host.cpp build_sampling_tables / run_sampling, trace_kernel.hip
+decide_chunk).  The reference accepts these configs (odigossamplingprocessor
+config.go:17-80 Validate has no rule-count bound; rule_engine.go:55-115
+folds any number of rules).
+
+CPU: the oracle against the pure-Python restatement on the wide configs.
+GPU (@gpu): the chunked HIP path against the oracle, bit-exact on keep and
+the per-trace records, through the fast path, the slow (repeated-id) path,
+the long-run kernel and batch mode.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from odigos_amd import native
+from odigos_amd.batch import Generator
+from tests.oracle_lib import intern_services, lib as orc_lib
+from tests.test_sampling_random import SEED, _arr, _group, _py_eval, gpu_vs_oracle, inject_zero_starts, oracle_run
+from tests.workloads import check_interning
+
+_ROUTES = ["/api/v1", "/api/v2", "/api", "/api/v1/", "/health", "/api/v2/", "/a", "/x", "/api/v1/users",
+           "/api/v2/orders", "/", "/api/v1/items/"]
+_THRESH = [50, 80, 100, 150, 200, 300, 500, 750, 1000, 1500, 2000, 60, 90, 120, 400, 70]
+
+
+def _lat(j, svc):
+    return {"name": f"lat-{j}", "type": "http_latency",
+            "rule_details": {"http_route": _ROUTES[(j * 5) % len(_ROUTES)], "service_name": f"svc-{svc:02d}",
+                             "threshold": _THRESH[j % len(_THRESH)],
+                             "fallback_sampling_ratio": [0, 5, 10, 25, 0, 15, 20, 12.5, 33.3, 7][j % 10]}}
+
+
+def _svc(k, name_id):
+    return {"name": f"s{k}", "type": "service_name",
+            "rule_details": {"service_name": f"svc-{name_id:02d}", "sampling_ratio": float((k * 37) % 101),
+                             "fallback_sampling_ratio": float(k % 7)}}
+
+
+def wide_latency_config():
+    """150 http_latency rules (3 chunks) at the endpoint level over services
+    0..63 (first appearance in id order), after the C3 error and service rules."""
+    svc = [_svc(k, k) for k in range(4)]
+    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}],
+            "service_rules": svc,
+            "endpoint_rules": [_lat(j, j % 64) for j in range(150)]}
+
+
+def wide_mixed_config():
+    """Chunk boundaries inside and across levels: 80 latency rules in the
+    global level (services 0..39), 100 service_name rules over services
+    40..139 (only ids < 64 occur in the generator's batches), 70 latency rules
+    in the endpoint level."""
+    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}]
+            + [_lat(j, j % 40) for j in range(80)],
+            "service_rules": [_svc(k, 40 + k) for k in range(100)],
+            "endpoint_rules": [_lat(200 + j, j % 64) for j in range(70)]}
+
+
+def long_routes_config():
+    """Tables beyond the 12 KiB LDS budget through route bytes alone: 40
+    latency rules whose http_route is ~400 bytes (the first 7 bytes match)."""
+    rules = []
+    for j in range(40):
+        r = _lat(j, j % 16)
+        r["rule_details"]["http_route"] = "/api/v1" + "/" + "z" * (380 + j)
+        rules.append(r)
+    rules += [_lat(100 + j, j % 16) for j in range(8)]
+    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}],
+            "service_rules": [], "endpoint_rules": rules}
+
+
+CONFIGS = {"latency": wide_latency_config, "mixed": wide_mixed_config, "long_routes": long_routes_config}
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_wide_config_oracle_vs_python(name):
+    cfg = CONFIGS[name]()
+    check_interning(cfg)
+    g = Generator("sampling", seed=0x0D1607A1, n_spans=2500)
+    inject_zero_starts(g, 0.03, 5)
+    cols = g.cols
+    ho = oracle_run(cols, native.GROUP_TRACE_ID, cfg=cfg)
+    traces = _group(cols, False)
+    svc_ids = intern_services(cfg)
+    res = _arr(cols.resource, C.c_uint32, cols.n_spans)
+    tid = _arr(cols.trace_id, C.c_uint64, 2 * cols.n_spans).reshape(-1, 2)
+    levels = set()
+    for t, spans in enumerate(traces):
+        u = orc_lib().orc_trace_uniform(int(tid[spans[0], 0]), int(tid[spans[0], 1]), SEED)
+        k, lvl, ratio = _py_eval(cfg, svc_ids, cols, res, spans, False, u)
+        assert ho.view("trace_level", np.uint8)[t] == lvl, t
+        assert ho.view("trace_ratio", np.float64)[t] == ratio, t
+        assert ho.view("trace_keep", np.uint8)[t] == int(k), t
+        levels.add(lvl)
+    assert len(levels) >= 2, levels
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_gpu_wide_config(name, shuffle):
+    # contiguous traces (fast path) and resource-shuffled ones (repeated ids:
+    # the run-list and sort paths redo the fast path's provisional walk)
+    g = Generator("sampling", seed=0x0D1607B1 + int(shuffle), n_spans=200_000, shuffle=shuffle)
+    inject_zero_starts(g, 0.01, 9)
+    gpu_vs_oracle(g, cfg=CONFIGS[name]())
+
+
+@pytest.mark.gpu
+def test_gpu_wide_config_long_traces():
+    # Zipf trace sizes: runs past the fast pass's windows go to trace_long_kernel
+    g = Generator("zipf", seed=0x0D1607C1, n_spans=400_000)
+    inject_zero_starts(g, 0.01, 4)
+    gpu_vs_oracle(g, cfg=wide_mixed_config(), seed=0xDEADBEEF)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 65, 5000])
+def test_gpu_wide_config_batch_mode(n):
+    if n == 0:
+        g = Generator("sampling", seed=1, n_spans=1)
+        g.cols.n_spans = 0
+    else:
+        g = Generator("sampling", seed=0x0D1607D1 + n, n_spans=n)
+    gpu_vs_oracle(g, mode=native.GROUP_BATCH, cfg=wide_latency_config())
+
+
+@pytest.mark.gpu
+def test_gpu_wide_config_large():
+    # 2M spans through three chunks, per-trace outputs off (the bench shape)
+    g = Generator("sampling", seed=0x0D1607E1, n_spans=2_000_000, threads=8)
+    gpu_vs_oracle(g, cfg=wide_latency_config(), per_trace=False)
+
+
+@pytest.mark.gpu
+def test_gpu_wide_config_exchange_refused():
+    # a partial record carries one 64-bit endpoint / service word: the
+    # trace-id exchange refuses chunked rule lists
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine
+    eng = Engine({"odigossampling": wide_latency_config()})
+    n = 1000
+    db = DeviceBatch(Generator("sampling", seed=3, n_spans=n).cols)
+    L = native.lib()
+    send = torch.empty(n * L.ose_shard_record_bytes(eng.h), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    pos = torch.empty(n, dtype=torch.int32, device="cuda")
+    with pytest.raises(native.OseError) as ei:
+        native.check(L.ose_shard_pack(eng.h, C.byref(db.cols), 2, send.data_ptr(), counts.data_ptr(), pos.data_ptr(), None))
+    assert ei.value.code == native.OSE_ENOTSUP

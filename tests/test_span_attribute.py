@@ -196,6 +196,23 @@ PRED_CASES = [
     (_r("json", "key_equals", "x", "$.b"), S('{"a":"x"}'), False),             # Get error -> continue
     (_r("json", "key_not_equals", "x", "$.b"), S('{"a":"x"}'), False),
     (_r("json", "key_not_equals", "y", "$.a"), S('{"a":"x"}'), True),
+    # ambiguous selectors: Get returns the match list and never errs (parity
+    # unpinned: PaesslerAG/jsonpath is not in the reference; object members
+    # are visited in sorted key order)
+    (_r("json", "contains_key", path="$..a"), S('{"x":{"a":1}}'), True),
+    (_r("json", "contains_key", path="$..a"), S('{"x":1}'), True),            # an empty list is not nil
+    (_r("json", "not_contains_key", path="$.x[*]"), S('{"a":1}'), False),     # no error
+    (_r("json", "key_equals", "[1,2]", "$.a[*]"), S('{"a":[1,2]}'), True),
+    (_r("json", "key_equals", "[2,1]", "$.a[1,0]"), S('{"a":[1,2]}'), True),
+    (_r("json", "key_equals", '["x"]', "$['b',1]"), S('{"b":"x"}'), True),     # the index finds no array
+    (_r("json", "key_equals", "[5,6]", "$.a[0:2]"), S('{"a":[5,6,7]}'), True),
+    (_r("json", "key_equals", "[7]", "$.a[-1:]"), S('{"a":[5,6,7]}'), True),
+    (_r("json", "key_equals", "[7,6,5]", "$.a[::-1]"), S('{"a":[5,6,7]}'), True),
+    (_r("json", "key_equals", "[5,7]", "$.a[0:3:2]"), S('{"a":[5,6,7]}'), True),
+    (_r("json", "key_equals", '["x","y"]', "$.*"), S('{"b":"y","a":"x"}'), True),
+    (_r("json", "key_equals", "[1,3]", "$..a"), S('{"a":1,"b":{"a":3}}'), True),
+    (_r("json", "key_equals", "[]", "$..q"), S('{"a":1}'), True),
+    (_r("json", "key_equals", "[1,3]", "$..a"), S('[{"a":1},{"a":3}]'), True),
 ]
 
 
@@ -206,9 +223,9 @@ def test_predicate(rule, value, want):
 
 
 def test_unsupported_jsonpath_rejected_at_creation():
-    # filters / wildcards / recursive descent are outside the restated
+    # filters and scripts (gval expressions) are outside the restated
     # jsonpath subset: the engine refuses the config instead of guessing
-    for path in ("$..a", "$.a[*]", "$.a[?(@.b==1)]"):
+    for path in ("$.a[?(@.b==1)]", "$[(@.length-1)]", "$.a[", "a.b"):
         cfg = {"global_rules": [{"name": "j", "type": "span_attribute",
                                  "rule_details": dict(_r("json", "contains_key", path=path), sampling_ratio=1.0)}]}
         with pytest.raises((ValueError, RuntimeError)):
