@@ -73,6 +73,11 @@ WORKLOADS = {
                      fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
                      metric_config="C3: trace-level sampling (1 error + 4 service + 16 latency rules), "
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
+    "sampling_wide": dict(gen="sampling", seed=0x0D160003, spans=50_000_000, per_gpu=True,
+                          cfg="wide", stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
+                          fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
+                          metric_config="diagnostic: C3's batch under 1 error + 4 service + 150 latency rules "
+                                        "(three rule chunks, one trace-stage pass each)"),
     "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000, per_gpu=True,
                  cfg=None, stages="SAMPLE|TEMPLATE", null_columns=("res_url_ok",), null_outputs=PER_TRACE_OUTS,
                  fields=SAMPLE_FIELDS + ("kind", "url_flags", "path"), kernels=TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS,
@@ -107,6 +112,9 @@ C1 = dict(gen="fused", seed=0x0D160001, spans=1_000_000)   # SURVEY.md §8d CPU 
 
 
 def _cfg(wl):
+    if wl["cfg"] == "wide":
+        from tests.workloads import wide_latency_config
+        return {"odigossampling": wide_latency_config()}
     if wl["cfg"] is not None:
         return wl["cfg"]
     from tests.workloads import c3_sampling_config

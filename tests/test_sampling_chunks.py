@@ -21,58 +21,7 @@ from odigos_amd import native
 from odigos_amd.batch import Generator
 from tests.oracle_lib import intern_services, lib as orc_lib
 from tests.test_sampling_random import SEED, _arr, _group, _py_eval, gpu_vs_oracle, inject_zero_starts, oracle_run
-from tests.workloads import check_interning
-
-_ROUTES = ["/api/v1", "/api/v2", "/api", "/api/v1/", "/health", "/api/v2/", "/a", "/x", "/api/v1/users",
-           "/api/v2/orders", "/", "/api/v1/items/"]
-_THRESH = [50, 80, 100, 150, 200, 300, 500, 750, 1000, 1500, 2000, 60, 90, 120, 400, 70]
-
-
-def _lat(j, svc):
-    return {"name": f"lat-{j}", "type": "http_latency",
-            "rule_details": {"http_route": _ROUTES[(j * 5) % len(_ROUTES)], "service_name": f"svc-{svc:02d}",
-                             "threshold": _THRESH[j % len(_THRESH)],
-                             "fallback_sampling_ratio": [0, 5, 10, 25, 0, 15, 20, 12.5, 33.3, 7][j % 10]}}
-
-
-def _svc(k, name_id):
-    return {"name": f"s{k}", "type": "service_name",
-            "rule_details": {"service_name": f"svc-{name_id:02d}", "sampling_ratio": float((k * 37) % 101),
-                             "fallback_sampling_ratio": float(k % 7)}}
-
-
-def wide_latency_config():
-    """150 http_latency rules (3 chunks) at the endpoint level over services
-    0..63 (first appearance in id order), after the C3 error and service rules."""
-    svc = [_svc(k, k) for k in range(4)]
-    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}],
-            "service_rules": svc,
-            "endpoint_rules": [_lat(j, j % 64) for j in range(150)]}
-
-
-def wide_mixed_config():
-    """Chunk boundaries inside and across levels: 80 latency rules in the
-    global level (services 0..39), 100 service_name rules over services
-    40..139 (only ids < 64 occur in the generator's batches), 70 latency rules
-    in the endpoint level."""
-    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}]
-            + [_lat(j, j % 40) for j in range(80)],
-            "service_rules": [_svc(k, 40 + k) for k in range(100)],
-            "endpoint_rules": [_lat(200 + j, j % 64) for j in range(70)]}
-
-
-def long_routes_config():
-    """Tables beyond the 12 KiB LDS budget through route bytes alone: 40
-    latency rules whose http_route is ~400 bytes (the first 7 bytes match)."""
-    rules = []
-    for j in range(40):
-        r = _lat(j, j % 16)
-        r["rule_details"]["http_route"] = "/api/v1" + "/" + "z" * (380 + j)
-        rules.append(r)
-    rules += [_lat(100 + j, j % 16) for j in range(8)]
-    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}],
-            "service_rules": [], "endpoint_rules": rules}
-
+from tests.workloads import check_interning, long_routes_config, wide_latency_config, wide_mixed_config
 
 CONFIGS = {"latency": wide_latency_config, "mixed": wide_mixed_config, "long_routes": long_routes_config}
 
