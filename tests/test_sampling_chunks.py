@@ -94,7 +94,8 @@ def test_gpu_wide_config_exchange_refused():
     from odigos_amd.batch import DeviceBatch, Engine
     eng = Engine({"odigossampling": wide_latency_config()})
     n = 1000
-    db = DeviceBatch(Generator("sampling", seed=3, n_spans=n).cols)
+    g = Generator("sampling", seed=3, n_spans=n)   # (owns the host columns)
+    db = DeviceBatch(g.cols)
     L = native.lib()
     send = torch.empty(n * L.ose_shard_record_bytes(eng.h), dtype=torch.uint8, device="cuda")
     counts = torch.zeros(2, dtype=torch.int64, device="cuda")
