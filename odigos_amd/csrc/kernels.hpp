@@ -376,11 +376,12 @@ enum : uint32_t {
   kRoleTarget = 1u << 5,      // http.target
   kRoleFull = 1u << 6,        // url.full / http.url: net/url.Parse on the host
   kRoleHost = 1u << 7,        // a json span_attribute rule's key: host pass
-  kRoleAttr0 = 1u << 8,       // + k: GPU attribute key column k (k < kOtlpMaxAttrKeys)
 };
-constexpr uint32_t kOtlpMaxAttrKeys = 24;
+constexpr uint64_t kRoleAttr0 = 1ull << 8;   // << k: GPU attribute key column k (k < kOtlpMaxAttrKeys)
+constexpr uint32_t kOtlpMaxAttrKeys = 56;
 struct OtlpKeyDev {
-  uint32_t len, off, roles, _pad;
+  uint32_t len, off;
+  uint64_t roles;
 };
 struct OtlpArgs {
   const uint8_t* pb;            // message bytes = the arena (16-byte aligned, 16 bytes of slack)

@@ -219,7 +219,7 @@ OtlpEngine* otlp_engine(Engine* e, int& rc) {
   o->err = o->ctx.build(e->has_url ? &e->url : nullptr, e->has_sampling ? &e->sampling : nullptr,
                         e->has_traffic ? &e->traffic : nullptr);
   if (!o->err.empty()) { rc = fail(OSE_EINVAL, o->err); delete o; return nullptr; }
-  std::map<std::string, uint32_t> roles;
+  std::map<std::string, uint64_t> roles;
   roles["http.request.method"] |= kRoleMethodNew;
   roles["http.method"] |= kRoleMethodOld;
   roles["http.route"] |= kRoleRoute;
@@ -230,7 +230,7 @@ OtlpEngine* otlp_engine(Engine* e, int& rc) {
   roles["http.url"] |= kRoleFull;
   const AttrPlan& plan = o->ctx.attr_plan;
   if (plan.keys.size() > kOtlpMaxAttrKeys) {
-    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 24 span_attribute keys");
+    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 56 distinct span_attribute keys");
     delete o;
     return nullptr;
   }
@@ -242,7 +242,7 @@ OtlpEngine* otlp_engine(Engine* e, int& rc) {
       o->json_rules = true;
     }
   for (auto& kv : roles) {
-    OtlpKeyDev d{(uint32_t)kv.first.size(), (uint32_t)o->key_bytes.size(), kv.second, 0};
+    OtlpKeyDev d{(uint32_t)kv.first.size(), (uint32_t)o->key_bytes.size(), kv.second};
     o->key_bytes += kv.first;
     o->keys.push_back(d);
     if (kv.first.size() < 64) o->key_lens |= 1ull << kv.first.size();

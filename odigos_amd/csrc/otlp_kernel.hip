@@ -60,9 +60,9 @@ __device__ uint64_t key_value(Rd& r, uint32_t s, uint32_t e, uint32_t& ko, uint3
 }
 
 // the roles of key [o, o + l) (0 = not a key of interest)
-__device__ uint32_t key_roles(const OtlpArgs& a, Rd& r, uint32_t o, uint32_t l) {
+__device__ uint64_t key_roles(const OtlpArgs& a, Rd& r, uint32_t o, uint32_t l) {
   if (l >= 64 || !((a.key_lens >> l) & 1)) return 0;
-  uint32_t roles = 0;
+  uint64_t roles = 0;
   for (uint32_t k = 0; k < a.n_keys; k++) {
     const OtlpKeyDev kd = a.keys[k];
     if (kd.len != l) continue;
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
     uint32_t ts_len = 0, name_off = 0, name_len = 0, kind = 0, flags = 0;
     uint32_t dr_attrs = 0, dr_events = 0, dr_links = 0, st_msg = 0, st_code = 0;
     uint64_t attrs_sz = 0, events_sz = 0, links_sz = 0;
-    uint32_t found = 0;   // roles seen (first occurrence wins)
+    uint64_t found = 0;   // roles seen (first occurrence wins)
     Val mnew{0, 0, 0, 0}, mold{0, 0, 0, 0}, route{0, 0, 0, 0}, utmpl{0, 0, 0, 0}, upath{0, 0, 0, 0},
         target{0, 0, 0, 0};
     bool full_seen = false, host_key = false;
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
           Val v;
           attrs_sz += field_len(key_value(r, ps, ps + pl, ko, kl, v));
           if (r.bad) break;
-          const uint32_t roles = key_roles(a, r, ko, kl) & ~found;
+          const uint64_t roles = key_roles(a, r, ko, kl) & ~found;
           if (!roles) break;
           found |= roles;
           if (roles & kRoleMethodNew) mnew = v;

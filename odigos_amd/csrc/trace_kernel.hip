@@ -1740,7 +1740,7 @@ void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
 // entry met twice (or a bucket past its capacity) sets *dup
 __global__ __launch_bounds__(256) void trace_dup_check_kernel(TraceKernelArgs a) {
   constexpr uint32_t kSet = 2 * kDupBucketCap;
-  static_assert(kSet == 2048, "the set's hash takes 11 bits");
+  static_assert(kSet == 2048, "the set hash takes at most 11 bits");
   __shared__ uint64_t set[kSet];
   __shared__ uint32_t found;
   const uint32_t bk = blockIdx.x;
@@ -1750,19 +1750,24 @@ __global__ __launch_bounds__(256) void trace_dup_check_kernel(TraceKernelArgs a)
     if (threadIdx.x == 0) atomicOr(a.dup, 1u);
     return;
   }
-  for (uint32_t k = threadIdx.x; k < kSet; k += 256) set[k] = 0ull;
+  // the set: the power of two >= 2c (>= 256), so a bucket of ~c entries
+  // clears ~2c slots instead of all kSet
+  uint32_t bits = 8;
+  while ((1u << bits) < 2 * c) bits++;
+  const uint32_t nset = 1u << bits;   // <= kSet (c <= kDupBucketCap)
+  for (uint32_t k = threadIdx.x; k < nset; k += 256) set[k] = 0ull;
   if (threadIdx.x == 0) found = 0;
   __syncthreads();
   const uint64_t* e = a.dup_bkt + (uint64_t)bk * kDupBucketCap;
   bool hit = false;
   for (uint32_t k = threadIdx.x; k < c; k += 256) {
     const uint64_t v = e[k];   // never 0
-    uint32_t s = ((uint32_t)v * 0x9E3779B1u) >> (32 - 11);
-    for (uint32_t probes = 0; probes < kSet; probes++) {
+    uint32_t s = ((uint32_t)v * 0x9E3779B1u) >> (32 - bits);
+    for (uint32_t probes = 0; probes < nset; probes++) {
       const uint64_t old = atomicCAS((unsigned long long*)&set[s], 0ull, (unsigned long long)v);
       if (old == 0) break;
       if (old == v) { hit = true; break; }
-      s = (s + 1) & (kSet - 1);
+      s = (s + 1) & (nset - 1);
     }
   }
   if (hit) found = 1;

@@ -50,12 +50,18 @@ CFG_JSON_RULE["odigossampling"]["endpoint_rules"].append(
     {"name": "js", "type": "span_attribute",
      "rule_details": {"service_name": "svc-a", "attribute_key": "body", "condition_type": "json",
                       "operation": "contains_key", "json_path": "$.a", "sampling_ratio": 90}})
+CFG_MANY_KEYS = json.loads(json.dumps(CFG))   # 40 distinct span_attribute keys (the decoder's key roles)
+CFG_MANY_KEYS["odigossampling"]["endpoint_rules"] += [
+    {"name": f"k{j}", "type": "span_attribute",
+     "rule_details": {"service_name": SERVICES[j % len(SERVICES)], "attribute_key": f"k{j}",
+                      "condition_type": "string", "operation": "equals", "expected_value": "v",
+                      "sampling_ratio": float(j)}} for j in range(40)]
 CFG_EXCLUDE = json.loads(json.dumps(CFG))
 CFG_EXCLUDE["odigosurltemplate"] = {"exclude": {"k8s_workloads": [{"namespace": "prod", "kind": "Deployment",
                                                                     "name": "api"}]}}
 
 
-def _http_traces(rng: random.Random, n_traces: int, odd: float = 0.0) -> dict:
+def _http_traces(rng: random.Random, n_traces: int, odd: float = 0.0, extra_keys: int = 0) -> dict:
     """HTTP-shaped traces; `odd` is the share of spans with values the GPU
     hands to the host pass (url.full, int routes, nested values, events with
     nested attributes)."""
@@ -98,6 +104,9 @@ def _http_traces(rng: random.Random, n_traces: int, odd: float = 0.0) -> dict:
                     a["body"] = rng.choice(['{"a": 1}', "[]", "{"])
                 if rng.random() < odd:
                     a["nested"] = {"arrayValue": {"values": [{"intValue": "1"}]}}
+                for j in range(extra_keys):   # span_attribute keys beyond the role word's first 24
+                    if rng.random() < 0.15:
+                        a[f"k{j}"] = rng.choice(["v", "w", 4, True])
                 name = method if rng.random() < 0.4 else rng.choice(["op", "", "GET /x"])
                 start = 1739000000000000000 + rng.randrange(10 ** 9)
                 sp = host.span(name=name, kind=kind, attributes=a, trace_id=tid,
@@ -331,12 +340,12 @@ def _compare(cols, hb_cols, got):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,odd,cfg", [(0, 0.0, "base"), (1, 0.0, "base"), (2, 0.15, "base"), (3, 0.1, "json"),
-                                          (4, 0.0, "exclude"), (5, 0.3, "json")])
+                                          (4, 0.0, "exclude"), (5, 0.3, "json"), (6, 0.0, "many_keys")])
 def test_gpu_decode_matches_host_columns(seed, odd, cfg):
     from odigos_amd.batch import Engine, OtlpBatch
-    c = {"base": CFG, "json": CFG_JSON_RULE, "exclude": CFG_EXCLUDE}[cfg]
+    c = {"base": CFG, "json": CFG_JSON_RULE, "exclude": CFG_EXCLUDE, "many_keys": CFG_MANY_KEYS}[cfg]
     rng = random.Random(seed)
-    td = _http_traces(rng, 200, odd=odd)
+    td = _http_traces(rng, 200, odd=odd, extra_keys=40 if cfg == "many_keys" else 0)
     _, hb = _host_columns(c, td)
     eng = Engine(c)
     ob = OtlpBatch(eng, to_pb(td))
