@@ -21,7 +21,7 @@ from odigos_amd import native
 from odigos_amd.batch import Generator
 from tests.oracle_lib import intern_services, lib as orc_lib
 from tests.test_sampling_random import SEED, _arr, _group, _py_eval, gpu_vs_oracle, inject_zero_starts, oracle_run
-from tests.workloads import check_interning, long_routes_config, wide_latency_config, wide_mixed_config
+from tests.workloads import check_interning, long_routes_config, wide_attr_config, wide_latency_config, wide_mixed_config
 
 CONFIGS = {"latency": wide_latency_config, "mixed": wide_mixed_config, "long_routes": long_routes_config}
 
@@ -58,6 +58,31 @@ def test_gpu_wide_config(name, shuffle):
     g = Generator("sampling", seed=0x0D1607B1 + int(shuffle), n_spans=200_000, shuffle=shuffle)
     inject_zero_starts(g, 0.01, 9)
     gpu_vs_oracle(g, cfg=CONFIGS[name]())
+
+
+def _attr_bits(g, rules, seed, p=0.02):
+    # the shim's attr_match column for json span_attribute rules: bit k = the
+    # k-th span_attribute rule in level order met by the span
+    rng = np.random.default_rng(seed)
+    n = g.cols.n_spans
+    bits = np.zeros(n, dtype=np.uint64)
+    for k in range(rules):
+        bits |= (rng.random(n) < p).astype(np.uint64) << np.uint64(k)
+    g.cols.attr_match = bits.ctypes.data
+    return bits   # (the caller keeps it alive)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_gpu_wide_config_attr_bits_across_chunks(shuffle):
+    # span_attribute bits 0..13 in one chunk, 14..39 in the next (attr_base)
+    check_interning(wide_attr_config())
+    g = Generator("sampling", seed=0x0D1607F1 + int(shuffle), n_spans=200_000, shuffle=shuffle)
+    keep_alive = _attr_bits(g, 40, seed=17)
+    ho = gpu_vs_oracle(g, cfg=wide_attr_config())
+    t = int(ho.view("trace_count", np.uint32)[0])
+    assert len(set(ho.view("trace_level", np.uint8)[:t].tolist())) >= 2
+    del keep_alive
 
 
 @pytest.mark.gpu

@@ -78,6 +78,21 @@ def wide_mixed_config():
             "endpoint_rules": [_wide_lat(200 + j, j % 64) for j in range(70)]}
 
 
+def wide_attr_config():
+    """span_attribute rules split over two rule chunks (their attr_match bits
+    0..13 in the first, 14..39 in the second): 40 latency rules (services
+    0..39), 50 service_name rules (services 40..89), 40 json span_attribute
+    rules (bits from the attr_match column), 30 latency rules."""
+    attr = [{"name": f"a{j}", "type": "span_attribute",
+             "rule_details": {"service_name": f"svc-{j % 40:02d}", "attribute_key": "body", "condition_type": "json",
+                              "operation": "is_valid_json", "sampling_ratio": float((j * 13) % 101),
+                              "fallback_sampling_ratio": float(j % 5)}} for j in range(40)]
+    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}]
+            + [_wide_lat(j, j) for j in range(40)],
+            "service_rules": [_wide_svc(k, 40 + k) for k in range(50)] + attr,
+            "endpoint_rules": [_wide_lat(300 + j, j % 64) for j in range(30)]}
+
+
 def long_routes_config():
     """Tables beyond the 12 KiB LDS budget through route bytes alone: 40
     latency rules whose http_route is ~400 bytes (the first 7 bytes match)."""
