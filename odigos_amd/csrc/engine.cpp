@@ -567,6 +567,29 @@ uint64_t ose_dropped_errors(char* last, size_t cap) {
   return g_dropped_count;
 }
 
+// Diagnostic, no device: the number of rule chunks build_sampling_tables
+// cuts the config's odigossampling rule list into (0 without the section);
+// the codes and messages of ose_engine_create's sampling checks.
+extern "C" int osehost_sampling_chunks(const char* cfg_json, uint32_t* n_chunks) {
+  if (!n_chunks) return fail(OSE_EINVAL, "n_chunks is NULL");
+  *n_chunks = 0;
+  Json root;
+  try {
+    root = parse_json(cfg_json ? cfg_json : "{}");
+  } catch (const std::exception& ex) {
+    return fail(OSE_EINVAL, ex.what());
+  }
+  const Json* j = root.is_obj() ? root.get("odigossampling") : nullptr;
+  if (!j) return 0;
+  Engine e;
+  const std::string err = decode_sampling_config(*j, e.sampling);
+  if (!err.empty()) return fail(OSE_EINVAL, err);
+  e.has_sampling = true;
+  if (const int rc = e.build_sampling_tables()) return rc;
+  *n_chunks = (uint32_t)e.sampling_chunks_host.size();
+  return 0;
+}
+
 int ose_engine_create(const char* cfg_json, ose_engine** out) {
   if (!out) return fail(OSE_EINVAL, "out is NULL");
   *out = nullptr;

@@ -175,6 +175,7 @@ def lib() -> C.CDLL:
         "ose_profile_read": (C.c_int, [_p, C.c_char_p, C.c_size_t]),
         # host layer (odigos_amd/csrc/host.cpp)
         "osehost_last_error": (C.c_char_p, []),
+        "osehost_sampling_chunks": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32)]),
         "osehost_stream_copy": (C.c_int, [_p, _p, C.c_size_t, C.c_int, _p, C.POINTER(C.c_double)]),
         "osehost_xgroup_create": (C.c_int, [C.c_int, C.POINTER(_p)]),
         "osehost_xgroup_destroy": (None, [_p]),

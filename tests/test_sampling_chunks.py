@@ -26,6 +26,45 @@ from tests.workloads import check_interning, long_routes_config, wide_attr_confi
 CONFIGS = {"latency": wide_latency_config, "mixed": wide_mixed_config, "long_routes": long_routes_config}
 
 
+def _chunks(cfg):
+    import json
+    n = C.c_uint32()
+    native.check(native.lib().osehost_sampling_chunks(json.dumps({"odigossampling": cfg}).encode(), C.byref(n)))
+    return n.value
+
+
+def test_chunk_counts():
+    # greedy chunks of the level-ordered list (no device needed)
+    from tests.workloads import c3_sampling_config
+    assert _chunks(c3_sampling_config()) == 1
+    assert _chunks(wide_latency_config()) == 3          # 150 latency rules: 64 + 64 + 22
+    assert _chunks(wide_attr_config()) == 2             # 64 service + attr bits fill the first
+    assert _chunks(wide_mixed_config()) >= 4
+    assert _chunks(long_routes_config()) >= 2           # route bytes past the 12 KiB table
+    cfg = wide_latency_config()
+    cfg["endpoint_rules"] = cfg["endpoint_rules"][:64]
+    assert _chunks(cfg) == 1
+    cfg["endpoint_rules"] = wide_latency_config()["endpoint_rules"][:65]
+    assert _chunks(cfg) == 2
+
+
+def test_chunk_refusals():
+    import json
+    n = C.c_uint32()
+    L = native.lib()
+    one = {"global_rules": [{"name": "l", "type": "http_latency",
+                             "rule_details": {"http_route": "/" + "a" * 13000, "service_name": "s", "threshold": 5,
+                                              "fallback_sampling_ratio": 1}}]}
+    assert L.osehost_sampling_chunks(json.dumps({"odigossampling": one}).encode(), C.byref(n)) == native.OSE_ENOTSUP
+    attr = {"global_rules": [{"name": f"a{j}", "type": "span_attribute",
+                              "rule_details": {"service_name": "s", "attribute_key": "k", "condition_type": "string",
+                                               "operation": "equals", "expected_value": "v", "sampling_ratio": 1}}
+                             for j in range(65)]}
+    assert L.osehost_sampling_chunks(json.dumps({"odigossampling": attr}).encode(), C.byref(n)) == native.OSE_ENOTSUP
+    attr["global_rules"].pop()
+    assert L.osehost_sampling_chunks(json.dumps({"odigossampling": attr}).encode(), C.byref(n)) == 0 and n.value == 1
+
+
 @pytest.mark.parametrize("name", sorted(CONFIGS))
 def test_wide_config_oracle_vs_python(name):
     cfg = CONFIGS[name]()
