@@ -174,6 +174,7 @@ struct TraceKernelArgs {
   // (null in the last pass, which decides), indexed by the trace's first span
   const FoldState* fold_in;
   FoldState* fold_out;
+  uint32_t force_sort;        // trace_runs_kernel: send repeated ids to the sort-based path
   const uint64_t* tid;
   const uint64_t* start;
   const uint64_t* end;

@@ -490,6 +490,10 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     rl.overflow = overflow;
     rl.win_first = win_first;
     rl.head_slot = key;
+    // OSE_FORCE_SORT=1 (read per call): repeated trace ids go straight to the
+    // sort-based path (the run-list kernel still lists the heads it keys on)
+    const char* fs_env = getenv("OSE_FORCE_SORT");
+    rl.force_sort = fs_env && strtoul(fs_env, nullptr, 0) != 0 ? 1u : 0u;
     Engine::Timed tr{};
     e->prof_begin("trace_run_list", st, tr);
     launch_trace_runs(rl, st);

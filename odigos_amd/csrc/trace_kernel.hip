@@ -1217,6 +1217,7 @@ __global__ __launch_bounds__(256) void trace_insert_exact_kernel(TraceKernelArgs
 // *overflow, and the sort-based path (gated on it) recomputes the batch.
 __global__ __launch_bounds__(256) void trace_runs_kernel(TraceKernelArgs a) {
   if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  if (a.force_sort && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.overflow, 1u);
   const int lane = threadIdx.x & 63;
   for (uint64_t w = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWave; w < a.n_windows;
        w += (uint64_t)gridDim.x * (256 / kWave)) {
@@ -1252,6 +1253,8 @@ __device__ __forceinline__ uint64_t run_end(const TraceKernelArgs& a, uint64_t p
 
 __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a) {
   if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  // the sort-based path already has the batch (it redoes every trace)
+  if (__hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
   {
     const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
