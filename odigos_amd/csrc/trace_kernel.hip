@@ -1049,6 +1049,7 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
     const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
     for (uint32_t k = threadIdx.x * 16; k < nb; k += kLThreads * 16)
       *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
+    __syncthreads();   // every wave reads the tables (n_services, n_lat below) after the copy
   }
   const Cfg c = load_cfg(cfg_lds);
   const int lane = threadIdx.x & 63;
