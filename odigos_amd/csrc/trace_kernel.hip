@@ -594,6 +594,9 @@ __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos
 // Run heads are collected per wave in LDS and inserted 64 at a time: each
 // insert is a load and a dependent CAS, so batching turns a per-step pair of
 // round trips into one pair per 64 heads.
+#ifndef OSE_FOLD_ENDS
+#define OSE_FOLD_ENDS 0   // 1: trace_fold_kernel finds run ends once, up front
+#endif
 constexpr int kHeadQ = 128;
 struct HeadQ {
   uint64_t cell[kHeadQ];
@@ -1296,8 +1299,19 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
     uint32_t ks[kMaxFoldSlots];
     Lat ls[kMaxFoldSlots];
     bool over = false;
+#if OSE_FOLD_ENDS
+    // every run's end up front: independent head-mask walks in flight
+    // together, reused by the keep writes below
+    uint32_t re[kMaxRuns];
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxRuns; k++) re[k] = k < nr ? (uint32_t)run_end(a, rs[k]) : 0u;
+#endif
     for (uint32_t r = 0; r < nr && !over; r++) {
+#if OSE_FOLD_ENDS
+      const uint64_t s0 = rs[r], s1 = re[r];
+#else
       const uint64_t s0 = rs[r], s1 = run_end(a, s0);
+#endif
       spans += s1 - s0;
       if (spans > kMaxFoldSpans) { over = true; break; }
       for (uint64_t q = s0; q < s1; q++) {
@@ -1342,7 +1356,11 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
     decide_at(a, c, p, err, ep, lsat, svcb, trace_uniform(hi, lo, a.seed), dk, dl, dr);
     write_rec(a, p, dk, dl, dr);
     for (uint32_t r = 0; r < nr; r++) {
+#if OSE_FOLD_ENDS
+      const uint64_t s0 = rs[r], s1 = re[r];
+#else
       const uint64_t s0 = rs[r], s1 = run_end(a, s0);
+#endif
       for (uint64_t q = s0; q < s1; q++) a.keep[q] = dk;
     }
   }
