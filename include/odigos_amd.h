@@ -108,6 +108,12 @@ extern "C" {
  * (device_status bit 2, *tmpl_arena_used = the bytes needed) as in the
  * packed form.                                                              */
 #define OSE_STAGE_TEMPLATE_REFS 0x10u
+/* url_out and tmpl already hold the templating results (written by an
+ * earlier call on the same batch, e.g. TEMPLATE on a second stream while the
+ * trace-id exchange runs): SIZE counts the attribute each span gains and the
+ * renamed span names as if TEMPLATE had run in this call (the traffic
+ * processor runs after the URL processor, config_builder.go:215-229).       */
+#define OSE_STAGE_APPLY_TEMPLATE 0x20u
 
 /* ---- grouping of spans into "traces" for odigossampling --------------
  * TRACE_ID: spans sharing a 128-bit trace_id form one trace (the contract
@@ -298,6 +304,17 @@ int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info);
 /* Attribute key k (< n_attr_keys) of the attr_type / attr_val columns; the
  * bytes stay valid for the engine's lifetime.                               */
 int ose_engine_attr_key(const ose_engine* eng, uint32_t k, const char** key, uint32_t* len);
+
+/* Engine options (no reference counterpart: they select the alternative
+ * implementation of an OTLP leg, for tests that check the two against each
+ * other; the defaults are the fast paths).  Set before the calls they affect,
+ * not while such a call is in flight.  value 0 clears, non-zero sets.
+ *   "otlp_gpu_chain"       walk the TracesData chain on the GPU (ose_otlp_decode)
+ *   "otlp_host_resources"  ResourceSpans on the host, ScopeSpans on the GPU
+ *   "otlp_host_scopes"     ResourceSpans and ScopeSpans on the host
+ *   "encode_host"          ose_otlp_encode always uses the host encoder
+ * OSE_EINVAL for any other name.                                            */
+int ose_engine_set_option(ose_engine* eng, const char* name, int64_t value);
 
 /* Pinned host staging: the engine owns the memory (cgo: no Go pointers are
  * retained).  dims->n_spans, n_resources, n_scopes, n_attrsets and

@@ -234,6 +234,10 @@ class Engine:
     def profile(self, on: bool = True):
         native.check(self.L.ose_profile_enable(self.h, int(on)))
 
+    def set_option(self, name: str, value: int = 1):
+        """ose_engine_set_option: the alternative OTLP legs (tests)."""
+        native.check(self.L.ose_engine_set_option(self.h, name.encode(), int(value)))
+
     def profile_read(self) -> dict:
         import json
         buf = C.create_string_buffer(1 << 16)

@@ -94,6 +94,33 @@ def build_oracle(force: bool = False) -> Path:
     return out
 
 
+# ASan + UBSan build of the host code that parses untrusted input (OTLP
+# protobuf and JSON, regexps, jsonpath, configs, URLs), driven by
+# tests/fuzz/host_fuzz.cpp (tests/test_sanitize.py): test infrastructure,
+# never loaded by the product.
+SAN_SOURCES = ["pdata", "otlp_pb", "config", "regex_dfa", "unicode_tables", "span_attr", "urlparse"]
+SAN_FLAGS = ["-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+             "-fno-omit-frame-pointer", "-pthread", f"-I{ROOT / 'include'}"]
+
+
+def build_sanitized(force: bool = False, jobs: int = 8) -> Path:
+    objdir = OBJDIR / "asan"
+    objdir.mkdir(parents=True, exist_ok=True)
+    out = objdir / "host_fuzz"
+    srcs = [CSRC / f"{n}.cpp" for n in SAN_SOURCES] + [ROOT / "tests" / "fuzz" / "host_fuzz.cpp"]
+    hdr_t = _deps_mtime(list(CSRC.glob("*.hpp")) + [ROOT / "include" / "odigos_amd.h"])
+    cmds, objs = [], []
+    for src in srcs:
+        obj = objdir / (src.name + ".o")
+        objs.append(obj)
+        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_t):
+            cmds.append(["g++", *SAN_FLAGS, "-c", str(src), "-o", str(obj)])
+    _compile_all(jobs, cmds)
+    if force or cmds or not out.exists():
+        _run(["g++", *SAN_FLAGS, "-o", str(out), *map(str, objs)])
+    return out
+
+
 def build_all(force: bool = False, jobs: int = 8) -> None:
     build_product(force, jobs)
     build_gen(force)

@@ -159,7 +159,6 @@ Engine::~Engine() {
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
     if (w->table) (void)hipFree(w->table);
-    if (w->fp_table) (void)hipFree(w->fp_table);
     if (w->dup_bkt) (void)hipFree(w->dup_bkt);
     if (w->dup_bkt_count) (void)hipFree(w->dup_bkt_count);
     if (w->runs) (void)hipFree(w->runs);
@@ -406,7 +405,9 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.unplanned = reinterpret_cast<uint32_t*>(base + off_unpl);
   HIP_TRY(hipMemsetAsync(base, 0, zero_bytes, st));
   a.used = o->tmpl_arena_used;
+#if OSE_DIAG
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
+#endif
   a.scr_region = (scr_bytes / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
   // refs: image chunks of an eighth of the arena over the plan waves (at most
   // 256 KiB; a group larger than a chunk takes exactly its size): a wave
@@ -475,12 +476,15 @@ int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st) {
 int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
                const ose_rand* rnd, hipStream_t st) {
   if (!c || !o) return fail(OSE_EINVAL, "columns and outputs are required");
-  if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE | OSE_STAGE_APPLY_KEEP | OSE_STAGE_TEMPLATE_REFS))
+  if (mask & ~(OSE_STAGE_SAMPLE | OSE_STAGE_TEMPLATE | OSE_STAGE_SIZE | OSE_STAGE_APPLY_KEEP | OSE_STAGE_TEMPLATE_REFS |
+               OSE_STAGE_APPLY_TEMPLATE))
     return fail(OSE_EINVAL, "unknown stage bit");
   if ((mask & OSE_STAGE_TEMPLATE_REFS) && !(mask & OSE_STAGE_TEMPLATE))
     return fail(OSE_EINVAL, "OSE_STAGE_TEMPLATE_REFS needs OSE_STAGE_TEMPLATE");
   if ((mask & OSE_STAGE_APPLY_KEEP) && (mask & OSE_STAGE_SAMPLE))
     return fail(OSE_EINVAL, "OSE_STAGE_APPLY_KEEP and OSE_STAGE_SAMPLE exclude each other");
+  if ((mask & OSE_STAGE_APPLY_TEMPLATE) && (mask & OSE_STAGE_TEMPLATE))
+    return fail(OSE_EINVAL, "OSE_STAGE_APPLY_TEMPLATE and OSE_STAGE_TEMPLATE exclude each other");
   // SAMPLE + TEMPLATE by trace id: the URL stage reads nothing SAMPLE writes,
   // so its launches are queued between SAMPLE's fast path and the rest of
   // SAMPLE, which is queued once the host has read the fast path's dup flag
@@ -498,7 +502,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   Workspace* ws = e->acquire_ws(st);
   const uint64_t n = c->n_spans;
   const bool gate_on_host = (mask & OSE_STAGE_SAMPLE) && group_mode == OSE_GROUP_TRACE_ID && n > 0 && !capturing &&
-                            !getenv("OSE_NO_DEFER_SLOW");
+                            !(OSE_DIAG && getenv("OSE_NO_DEFER_SLOW"));
   const bool defer = gate_on_host && (mask & OSE_STAGE_TEMPLATE);
   // Workspace layout, one reservation for every stage of the call (a stage
   // must not reallocate scratch an earlier stage of the same call is still
@@ -538,7 +542,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   bool size_on = false;
   if (!rc && (mask & OSE_STAGE_SIZE)) rc = prepare_size(e, c, o, mask, group_mode, rnd, st, ws, size_off, sa, size_on);
   if (!rc && tmpl) {
-    if (size_on && n > 0 && !getenv("OSE_NO_FUSED_SIZE")) {
+    if (size_on && n > 0 && !(OSE_DIAG && getenv("OSE_NO_FUSED_SIZE"))) {
       // the spans pass rides in url_copy_kernel (one walk over the spans)
       sa.kept_partials = size_partials_of(ws, size_off, c->n_scopes, c->n_resources);
       sa.n_kept_partials = url_copy_blocks(ua.n_groups);
@@ -696,6 +700,24 @@ int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info) {
   info->n_attr_keys = (uint32_t)e->attr_keys.size();
   info->attr_host_rules = e->attr_host_rules;
   return 0;
+}
+
+int ose_engine_set_option(ose_engine* eng, const char* name, int64_t value) {
+  if (!eng || !name) return fail(OSE_EINVAL, "NULL argument");
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  static const struct { const char* name; uint32_t bit; } kOpts[] = {
+      {"otlp_gpu_chain", Engine::kOptOtlpGpuChain},
+      {"otlp_host_resources", Engine::kOptOtlpHostResources},
+      {"otlp_host_scopes", Engine::kOptOtlpHostScopes},
+      {"encode_host", Engine::kOptEncodeHost},
+  };
+  for (const auto& o : kOpts) {
+    if (strcmp(name, o.name) != 0) continue;
+    if (value) e->options.fetch_or(o.bit);
+    else e->options.fetch_and(~o.bit);
+    return 0;
+  }
+  return fail(OSE_EINVAL, std::string("unknown engine option: ") + name);
 }
 
 int ose_reserve(ose_engine* eng, uint64_t n_spans, uint64_t arena_bytes) {

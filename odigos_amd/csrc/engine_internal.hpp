@@ -63,8 +63,6 @@ struct Workspace {
   // across calls: entries carry a generation tag, so nothing is cleared
   void* table = nullptr;
   uint64_t table_slots_cap = 0;
-  uint64_t* fp_table = nullptr;   // fast-path fingerprint cells
-  uint64_t fp_slots_cap = 0;
   uint64_t* dup_bkt = nullptr;         // bucketed duplicate detection (TraceKernelArgs::dup_bkt)
   uint32_t* dup_bkt_count = nullptr;
   uint32_t dup_bkt_bits = 0;
@@ -100,6 +98,12 @@ struct Engine {
   SamplingConfig sampling;
   TrafficMetricsConfig traffic;
   bool has_url = false, has_sampling = false, has_traffic = false;
+  // ose_engine_set_option: alternative implementations of the OTLP legs
+  // (the default path is the fast one; these select the others, for tests
+  // that compare the two)
+  enum : uint32_t { kOptOtlpGpuChain = 1, kOptOtlpHostResources = 2, kOptOtlpHostScopes = 4, kOptEncodeHost = 8 };
+  std::atomic<uint32_t> options{0};
+  bool option(uint32_t o) const { return (options.load(std::memory_order_relaxed) & o) != 0; }
   bool url_needs_resource = false;
   int64_t inverse = 1;
   uint32_t max_name = 5;

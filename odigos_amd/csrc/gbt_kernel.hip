@@ -157,8 +157,12 @@ __device__ uint64_t gbt_lookup(const GbtArgs& a, uint64_t hi, uint64_t lo, uint3
       if (__hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine) {
         atomicMin(&s->first, pos);   // reclaimed by another lane between our reads
       } else {
-        __hip_atomic_store(&s->seq, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // first before seq, drained between them: a lane that read the state
+        // as READY before this CAS may still read seq; once it sees `mine`
+        // its atomicMin must land after this store, not under it
         __hip_atomic_store(&s->first, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&s->seq, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&s->state, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -75,6 +75,18 @@ class JsonParser {
  private:
   const std::string& t_;
   size_t i_ = 0;
+  // nesting bound: the parser recurses per array / object level (deeper
+  // input is refused instead of overflowing the caller's stack; Go's
+  // encoding/json stops at 10000 levels, configs and OTLP/JSON stay far below)
+  static constexpr int kMaxDepth = 1000;
+  int depth_ = 0;
+  struct Nest {
+    JsonParser& p;
+    explicit Nest(JsonParser& q) : p(q) {
+      if (++p.depth_ > kMaxDepth) p.fail("nesting too deep");
+    }
+    ~Nest() { p.depth_--; }
+  };
   [[noreturn]] void fail(const char* m) { throw JsonError(std::string("json: ") + m + " at offset " + std::to_string(i_)); }
   void ws() { while (i_ < t_.size() && (t_[i_] == ' ' || t_[i_] == '\n' || t_[i_] == '\r' || t_[i_] == '\t')) i_++; }
   bool lit(const char* w) {
@@ -146,6 +158,7 @@ class JsonParser {
     if (i_ >= t_.size()) fail("unexpected end");
     char c = t_[i_];
     if (c == '{') {
+      Nest nest(*this);
       i_++;
       Json o = Json::object();
       ws();
@@ -166,6 +179,7 @@ class JsonParser {
       }
     }
     if (c == '[') {
+      Nest nest(*this);
       i_++;
       Json a = Json::array();
       ws();

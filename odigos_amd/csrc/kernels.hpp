@@ -6,6 +6,14 @@
 
 #include "../../include/odigos_amd.h"
 
+// OSE_DIAG=1: the diagnostics build (python -m odigos_amd.build --variant _diag
+// OSE_DIAG=1; loaded with OSE_LIB_VARIANT=_diag): ablation switches, per-section
+// clocks and tuning knobs read from the environment.  The product library is
+// built without it and reads no such variable.
+#ifndef OSE_DIAG
+#define OSE_DIAG 0
+#endif
+
 namespace ose {
 
 // odigosurltemplate: four launches on one stream (url_kernel.hip).
@@ -174,7 +182,6 @@ struct TraceKernelArgs {
   // (null in the last pass, which decides), indexed by the trace's first span
   const FoldState* fold_in;
   FoldState* fold_out;
-  uint32_t force_sort;        // trace_runs_kernel: send repeated ids to the sort-based path
   const uint64_t* tid;
   const uint64_t* start;
   const uint64_t* end;
@@ -192,11 +199,8 @@ struct TraceKernelArgs {
   // slow path
   TraceSlot* table;            // exact table (slow path)
   uint64_t table_mask;
-  uint64_t* fp_table;          // fingerprint cells (fast-path duplicate detection)
-  uint64_t fp_mask;
   uint32_t* dup;              // set by the fast path when a trace_id spans several runs
-  // bucketed duplicate detection (used instead of fp_table when dup_bkt is
-  // set): a run head appends its 64-bit fingerprint to bucket fp >> (64 -
+  // bucketed duplicate detection (kTraceRuns): a run head appends its 64-bit fingerprint to bucket fp >> (64 -
   // dup_bkt_bits); trace_dup_check_kernel looks for a repeat per bucket in LDS
   uint32_t* dup_bkt_count;    // [1 << dup_bkt_bits], zeroed before the launch
   uint64_t* dup_bkt;          // [(1 << dup_bkt_bits) * kDupBucketCap]
@@ -337,6 +341,8 @@ struct UnpackArgs {
 };
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st);
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);
+// dst[k] += src[k] (the in-process transport's counter all-reduce)
+void launch_add_i64(int64_t* dst, const int64_t* src, uint64_t n, hipStream_t st);
 uint32_t shard_owner_host(uint64_t hi, uint64_t lo, uint32_t n_ranks);
 
 // Workspace words shared between stages of one call (uint32 index into the

@@ -383,8 +383,6 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
       c.lay.res_ref.push_back(ro | ((uint64_t)rl << 32));
       continue;
     }
-    static const int chain_only = getenv("OSE_WALK_CHAIN_ONLY") ? atoi(getenv("OSE_WALK_CHAIN_ONLY")) : 0;   // diagnostics
-    if (chain_only == 1) continue;
     PbReader rr(p + ro, rl);
     resf.clear();
     scopes.clear();
@@ -403,7 +401,6 @@ void walk_segment(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, si
       }
     }
     if (!rr.ok) { c.err = "OTLP protobuf: malformed ResourceSpans"; return; }
-    if (chain_only == 2) continue;
     if (scopes.empty()) scopes.swap(deprecated);
     // the resource's columns (cached by its message bytes)
     CachedRes cr{};
@@ -533,7 +530,9 @@ size_t find_start(const uint8_t* p, size_t n, size_t k) {
 bool walk_chain(const uint8_t* p, size_t n, std::vector<uint64_t>& res_ref, std::string& err) {
   const size_t kSeg = size_t(256) << 10;
   int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)parallel_width(), n / kSeg}));
-  if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));   // diagnostics
+#if OSE_DIAG
+  if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));
+#endif
   static const ColumnizeCtx no_ctx;
   static ResCache no_cache;
   std::vector<WalkChunk> ch;
@@ -579,7 +578,9 @@ bool walk_chain(const uint8_t* p, size_t n, std::vector<uint64_t>& res_ref, std:
 bool walk(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p, size_t n, Walked& w, bool gpu_scopes = false) {
   const size_t kSeg = size_t(256) << 10;
   int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)parallel_width(), n / kSeg}));
-  if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));   // diagnostics
+#if OSE_DIAG
+  if (const char* e = getenv("OSE_WALK_THREADS")) T = std::max(1, atoi(e));
+#endif
   std::vector<WalkChunk> ch;
   for (int attempt = 0; attempt < 2; attempt++) {
     if (attempt) T = 1;
@@ -700,7 +701,7 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
   std::string err;
   int rc;
   // the TracesData chain: the host walk (it runs while the message's H2D
-  // copy is in flight), or (OSE_OTLP_GPU_CHAIN=1) segments walked on the GPU
+  // copy is in flight), or (engine option otlp_gpu_chain) segments walked on the GPU
   // and linked here, the host walk when the link fails.  The GPU form
   // measured slower (profiles/r3_otlp_gpu_resources.json host chain,
   // r3_otlp_gpu_chain_gpu_encode.json GPU chain: 10M spans 57.8 -> 97.4 ms of
@@ -710,8 +711,7 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
   std::vector<uint64_t> seg_first;
   std::vector<uint32_t> seg_base;
   uint64_t R = 0;
-  const char* gc = getenv("OSE_OTLP_GPU_CHAIN");   // read per call (tests, A/B)
-  bool gpu_chain = len > 0 && gc && gc[0] == '1';
+  bool gpu_chain = len > 0 && b->e->option(Engine::kOptOtlpGpuChain);
   const uint32_t T = (uint32_t)((len + kChainSeg - 1) / kChainSeg);
   OtlpChainArgs ca{};
   if (gpu_chain) {
@@ -1170,13 +1170,11 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   }
   lap(0);
   // 2. the walk: TracesData and ResourceSpans on the host, ScopeSpans up to
-  //    64 KB on the GPU (OSE_OTLP_HOST_SCOPES=1: all on the host, diagnostics)
-  //    (OSE_OTLP_HOST_RESOURCES=1: ResourceSpans on the host, ScopeSpans on the
+  //    64 KB on the GPU (engine option otlp_host_scopes: all on the host)
+  //    (otlp_host_resources: ResourceSpans on the host, ScopeSpans on the
   //    GPU; without it only the TracesData chain is walked on the host)
-  static const bool env_host = getenv("OSE_OTLP_HOST_SCOPES") != nullptr;
-  const bool env_host_res = getenv("OSE_OTLP_HOST_RESOURCES") != nullptr;   // read per call (tests)
-  const bool gpu_scopes = !host_scopes && !env_host;
-  const bool gpu_res = gpu_scopes && !host_res && !env_host_res;
+  const bool gpu_scopes = !host_scopes && !e->option(Engine::kOptOtlpHostScopes);
+  const bool gpu_res = gpu_scopes && !host_res && !e->option(Engine::kOptOtlpHostResources);
   Walked w;
   OtlpResArgs ra{};
   uint64_t R = 0, S = 0;
@@ -1461,8 +1459,7 @@ namespace {
 int encode_gpu(OtlpBatchImpl* b, const ose_outputs* outs, bool sampled, bool tmpl, const Router* router,
                hipStream_t st, OtlpOut* o, bool* host) {
   *host = true;
-  const char* env = getenv("OSE_ENCODE_HOST");   // diagnostics: the host encoder always
-  if (env && env[0] == '1') return 0;
+  if (b->e->option(Engine::kOptEncodeHost)) return 0;   // engine option encode_host: the host encoder always
   if (router && router->pipelines.size() > 63) return 0;   // the host encoder reports it
   const uint64_t n = b->cols.n_spans, S = b->cols.n_scopes, R = b->cols.n_resources;
   if (!b->d_spans) return 0;

@@ -29,14 +29,6 @@ uint64_t table_slots(uint64_t n) {
   while (cap < 2 * n) cap <<= 1;
   return cap;
 }
-// Fingerprint cells: sized for the run heads of groupbytrace-ordered input
-// (~1 per 4 spans or fewer) so the table stays in the 256 MiB Infinity
-// Cache; an overfull probe sequence only sends the call down the exact path.
-uint64_t fp_slots(uint64_t n) {
-  uint64_t cap = 1024;
-  while (cap < n / 4) cap <<= 1;
-  return cap;
-}
 }  // namespace
 
 // Interns every service name a rule compares against (latency.go:55,
@@ -282,19 +274,14 @@ int Workspace::reserve_table(uint64_t n_spans) {
   const uint64_t slots = table_slots(n_spans);
   if (slots <= table_slots_cap) return 0;
   if (table) HIP_TRY(hipFree(table));
-  if (fp_table) HIP_TRY(hipFree(fp_table));
   if (dup_bkt) HIP_TRY(hipFree(dup_bkt));
   if (dup_bkt_count) HIP_TRY(hipFree(dup_bkt_count));
   table = nullptr;
-  fp_table = nullptr;
   dup_bkt = nullptr;
   dup_bkt_count = nullptr;
   table_slots_cap = 0;
   HIP_TRY(hipMalloc(&table, slots * sizeof(TraceSlot)));
   HIP_TRY(hipMemset(table, 0, slots * sizeof(TraceSlot)));
-  fp_slots_cap = fp_slots(n_spans);
-  HIP_TRY(hipMalloc(&fp_table, fp_slots_cap * sizeof(uint64_t)));
-  HIP_TRY(hipMemset(fp_table, 0, fp_slots_cap * sizeof(uint64_t)));
   // fingerprint buckets: half full (on average) at one run head per 4 spans;
   // at least 2 (the bucket is the fingerprint's top dup_bkt_bits bits)
   dup_bkt_bits = 1;
@@ -354,15 +341,11 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   if (group_mode == OSE_GROUP_TRACE_ID) {
     rc = ws->reserve_table(n);
     if (rc) return rc;
-    // generation tags: 30 bits in the exact table, 16 in the fingerprint
-    // cells; a table is cleared once when its tag wraps (0 is "never used")
+    // generation tags: 30 bits in the exact table; the table is cleared once
+    // when its tag wraps (0 is "never used")
     if (++ws->epoch >= (1u << 30)) {
       HIP_TRY(hipMemsetAsync(ws->table, 0, ws->table_slots_cap * sizeof(TraceSlot), st));
       ws->epoch = 1;
-    }
-    if ((ws->epoch & 0xFFFFu) == 0) {
-      HIP_TRY(hipMemsetAsync(ws->fp_table, 0, ws->fp_slots_cap * sizeof(uint64_t), st));
-      ++ws->epoch;
     }
   }
   uint8_t* base = static_cast<uint8_t*>(ws->dev);
@@ -415,8 +398,6 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   a.win_heads = win_heads;
   a.table = static_cast<TraceSlot*>(ws->table);
   a.table_mask = ws->table_slots_cap ? ws->table_slots_cap - 1 : 0;
-  a.fp_table = ws->fp_table;
-  a.fp_mask = ws->fp_slots_cap - 1;
   a.dup = misc;
   a.error = err;
   a.batch_keep = misc + kBatchKeepWord;
@@ -428,20 +409,24 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     a.attr_match = e->sampling_n_attr && e->sampling_chunk_attr[chunk] ? am : nullptr;
   }
   a.svc_match = c->svc_match;
-  if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // diagnostics
+#if OSE_DIAG
+  if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);
+#endif
   a.n_long = misc + 12;
   a.long_runs = a.mode == kTraceRuns ? long_runs : nullptr;
   a.long_steps = kLongSteps;
   a.win_per_wave = kWinPerWave;
-  if (const char* ww = getenv("OSE_WIN_PER_WAVE")) a.win_per_wave = std::max<uint32_t>(1, (uint32_t)strtoul(ww, nullptr, 0));   // tuning
-  if (const char* ls = getenv("OSE_LONG_STEPS")) a.long_steps = std::max<uint32_t>(1, (uint32_t)strtoul(ls, nullptr, 0));   // tuning
-  // duplicate detection: fingerprint buckets checked in LDS (the default:
-  // C4 trace_eval 3.02 -> 2.87 ms + 0.06 ms of trace_dup_check, C3 1.55 ->
-  // 1.47 + 0.03, profiles/r3_dup_buckets_ab.txt), or (OSE_DUP_BUCKETS=0) the
-  // fingerprint table
-  const char* bkt_env = getenv("OSE_DUP_BUCKETS");   // read per call (A/B and tests)
-  const bool buckets = !bkt_env || strtoul(bkt_env, nullptr, 0) != 0;
-  if (buckets && a.mode == kTraceRuns && ws->dup_bkt && ws->dup_bkt_bits >= 1 && ws->dup_bkt_bits <= 32) {
+#if OSE_DIAG
+  if (const char* ww = getenv("OSE_WIN_PER_WAVE")) a.win_per_wave = std::max<uint32_t>(1, (uint32_t)strtoul(ww, nullptr, 0));
+  if (const char* ls = getenv("OSE_LONG_STEPS")) a.long_steps = std::max<uint32_t>(1, (uint32_t)strtoul(ls, nullptr, 0));
+#endif
+  // duplicate detection: fingerprint buckets checked in LDS (replaced a
+  // fingerprint table probed with a CAS per head: C4 trace_eval 3.02 -> 2.87
+  // ms + 0.06 ms of trace_dup_check, C3 1.55 -> 1.47 + 0.03,
+  // profiles/r3_dup_buckets_ab.txt)
+  if (a.mode == kTraceRuns) {
+    if (!ws->dup_bkt || ws->dup_bkt_bits < 1 || ws->dup_bkt_bits > 32)
+      return fail(OSE_EDEVICE, "trace stage: duplicate-detection buckets missing");
     a.dup_bkt = ws->dup_bkt;
     a.dup_bkt_count = ws->dup_bkt_count;
     a.dup_bkt_bits = ws->dup_bkt_bits;
@@ -490,10 +475,6 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     rl.overflow = overflow;
     rl.win_first = win_first;
     rl.head_slot = key;
-    // OSE_FORCE_SORT=1 (read per call): repeated trace ids go straight to the
-    // sort-based path (the run-list kernel still lists the heads it keys on)
-    const char* fs_env = getenv("OSE_FORCE_SORT");
-    rl.force_sort = fs_env && strtoul(fs_env, nullptr, 0) != 0 ? 1u : 0u;
     Engine::Timed tr{};
     e->prof_begin("trace_run_list", st, tr);
     launch_trace_runs(rl, st);

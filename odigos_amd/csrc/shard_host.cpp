@@ -127,6 +127,8 @@ struct XTransport {
   virtual ~XTransport() = default;
   virtual int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv,
                         const uint64_t* roff, const uint64_t* rlen, hipStream_t st) = 0;
+  // node[k] = the sum over ranks of local[k] (int64), stream-ordered on `st`
+  virtual int allreduce_i64(const int64_t* local, int64_t* node, uint64_t n, hipStream_t st) = 0;
   // a rank that fails in the middle of a round tells its peers (the local
   // transport unblocks them; an RCCL communicator is left to the caller)
   virtual void abort() {}
@@ -151,6 +153,10 @@ struct RcclTransport final : XTransport {
     rc = r.group_end();   // the group is closed on every path, a failed enqueue included
     if (err) return err;
     if (rc != ncclSuccess) return nccl_fail("ncclGroupEnd", rc);
+    return 0;
+  }
+  int allreduce_i64(const int64_t* local, int64_t* node, uint64_t n, hipStream_t st) override {
+    NCCL_TRY(rccl().all_reduce(local, node, n, ncclInt64, ncclSum, comm, st));
     return 0;
   }
 };
@@ -244,6 +250,47 @@ struct LocalTransport final : XTransport {
     if (int rc = g->barrier()) return rc;
     for (int p = 0; p < g->n_ranks; p++)
       if (slen[p] && hipStreamWaitEvent(st, g->slots[(size_t)p].done, 0) != hipSuccess)
+        return fail(OSE_EDEVICE, "hipStreamWaitEvent failed");
+    return 0;
+  }
+  // every rank publishes its vector, then adds every rank's into its own
+  // node buffer (queued behind the owners' events); a second rendezvous
+  // keeps each local vector alive until every peer's adds are queued behind
+  // this rank's `done`
+  int allreduce_i64(const int64_t* local, int64_t* node, uint64_t n, hipStream_t st) override {
+    LocalGroup::Slot& me = g->slots[(size_t)rank];
+    if (!me.ready && hipEventCreateWithFlags(&me.ready, hipEventDisableTiming) != hipSuccess)
+      return fail(OSE_EDEVICE, "hipEventCreate failed");
+    if (!me.done && hipEventCreateWithFlags(&me.done, hipEventDisableTiming) != hipSuccess)
+      return fail(OSE_EDEVICE, "hipEventCreate failed");
+    me.send = reinterpret_cast<const uint8_t*>(local);
+    me.soff = nullptr;
+    me.slen = &n;
+    if (hipEventRecord(me.ready, st) != hipSuccess) return fail(OSE_EDEVICE, "hipEventRecord failed");
+    if (int rc = g->barrier()) return rc;
+    int err = 0;
+    if (n && hipMemsetAsync(node, 0, n * sizeof(int64_t), st) != hipSuccess) err = fail(OSE_EDEVICE, "hipMemsetAsync failed");
+    for (int p = 0; p < g->n_ranks && !err; p++) {
+      const LocalGroup::Slot& src = g->slots[(size_t)p];
+      if (*src.slen != n) {
+        err = fail(OSE_EINVAL, "in-process all-reduce: vector lengths disagree");
+        break;
+      }
+      if (hipStreamWaitEvent(st, src.ready, 0) != hipSuccess) {
+        err = fail(OSE_EDEVICE, "hipStreamWaitEvent failed");
+        break;
+      }
+      launch_add_i64(node, reinterpret_cast<const int64_t*>(src.send), n, st);
+      if (hipGetLastError() != hipSuccess) err = fail(OSE_EDEVICE, "add_i64 launch failed");
+    }
+    if (!err && hipEventRecord(me.done, st) != hipSuccess) err = fail(OSE_EDEVICE, "hipEventRecord failed");
+    if (err) {
+      g->abort();
+      return err;
+    }
+    if (int rc = g->barrier()) return rc;
+    for (int p = 0; p < g->n_ranks; p++)
+      if (hipStreamWaitEvent(st, g->slots[(size_t)p].done, 0) != hipSuccess)
         return fail(OSE_EDEVICE, "hipStreamWaitEvent failed");
     return 0;
   }
@@ -546,9 +593,8 @@ int ose_allreduce_counters(const int64_t* local, int64_t* node, uint64_t n, void
   const Rccl& r = rccl();
   if (!r.ok) return fail(OSE_ENOTSUP, "RCCL (librccl.so.1) is not available");
   if (!n) return 0;
-  NCCL_TRY(r.all_reduce(local, node, n, ncclInt64, ncclSum, static_cast<ncclComm_t>(nccl_comm),
-                        static_cast<hipStream_t>(hip_stream)));
-  return 0;
+  RcclTransport tx(static_cast<ncclComm_t>(nccl_comm), 0);
+  return tx.allreduce_i64(local, node, n, static_cast<hipStream_t>(hip_stream));
 }
 
 int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outputs* outs, void* nccl_comm,
@@ -579,6 +625,14 @@ int osehost_exchange_sample_local(ose_engine* eng, const ose_columns* cols, cons
   LocalTransport tx(g, rank);
   return exchange_round(reinterpret_cast<Engine*>(eng), cols, outs, tx, rank, g->n_ranks, rnd,
                         static_cast<hipStream_t>(hip_stream), stats);
+}
+int osehost_allreduce_counters_local(const int64_t* local, int64_t* node, uint64_t n, void* grp, int rank,
+                                     void* hip_stream) {
+  if (!grp || (n && (!local || !node))) return fail(OSE_EINVAL, "NULL argument");
+  auto* g = static_cast<LocalGroup*>(grp);
+  if (rank < 0 || rank >= g->n_ranks) return fail(OSE_EINVAL, "rank out of range");
+  LocalTransport tx(g, rank);
+  return tx.allreduce_i64(local, node, n, static_cast<hipStream_t>(hip_stream));
 }
 
 }  // extern "C"

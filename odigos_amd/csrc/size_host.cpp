@@ -39,7 +39,8 @@ int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   if (c->n_scopes && (!c->scope_size || !c->scope_resource)) return fail(OSE_EINVAL, "SIZE stage needs scope_size and scope_resource");
   if (c->n_resources && (!c->res_size || !c->res_attrset)) return fail(OSE_EINVAL, "SIZE stage needs res_size and res_attrset");
   const bool applied = mask & OSE_STAGE_APPLY_KEEP;   // decisions made by an earlier call
-  const bool sampled = (mask & OSE_STAGE_SAMPLE) || applied, templated = mask & OSE_STAGE_TEMPLATE;
+  const bool sampled = (mask & OSE_STAGE_SAMPLE) || applied;
+  const bool templated = mask & (OSE_STAGE_TEMPLATE | OSE_STAGE_APPLY_TEMPLATE);   // in this call or an earlier one
   if (applied && n && !o->keep) return fail(OSE_EINVAL, "OSE_STAGE_APPLY_KEEP needs keep");
   if (templated && n && (!c->kind || !c->name_len || !o->url_out || !o->tmpl))
     return fail(OSE_EINVAL, "SIZE after TEMPLATE needs kind, name_len, url_out and tmpl");

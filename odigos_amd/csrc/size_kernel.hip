@@ -137,10 +137,7 @@ __global__ __launch_bounds__(kSThreads) void size_res_kernel(SizeKernelArgs a) {
 }  // namespace
 
 void launch_size_spans(const SizeKernelArgs& a, hipStream_t st) {
-  static const uint64_t cap = [] {
-    const char* g = getenv("OSE_SIZE_GRID");   // tuning
-    return g ? std::max<uint64_t>(1, strtoull(g, nullptr, 0)) : 1024ull;   // swept on C4: 512 0.127 ms, 1024 0.088, 2048 0.094, 8192 0.126
-  }();
+  constexpr uint64_t cap = 1024;   // swept on C4: 512 0.127 ms, 1024 0.088, 2048 0.094, 8192 0.126
   const uint64_t blocks = std::min<uint64_t>((a.n_spans + kSThreads - 1) / kSThreads, cap);
   if (blocks) hipLaunchKernelGGL(size_span_kernel, dim3((uint32_t)blocks), dim3(kSThreads), 0, st, a);
 }
@@ -150,10 +147,7 @@ void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st) {
 }
 void launch_size_resources(const SizeKernelArgs& a, hipStream_t st) {
   if (!a.n_resources && !a.kept_partials) return;
-  static const uint32_t per_thread = [] {
-    const char* g = getenv("OSE_SIZE_RES_PER_THREAD");   // tuning
-    return g ? std::max<uint32_t>(1, (uint32_t)strtoul(g, nullptr, 0)) : 16u;   // swept on C4: 4 0.058 ms, 16 0.044, 32 0.058, 64 0.102
-  }();
+  constexpr uint32_t per_thread = 16;   // swept on C4: 4 0.058 ms, 16 0.044, 32 0.058, 64 0.102
   uint32_t blocks = (a.n_resources + kSThreads * per_thread - 1) / (kSThreads * per_thread);
   if (a.kept_partials) blocks = std::max<uint32_t>(blocks, std::min<uint32_t>(64, (a.n_kept_partials + 4095) / 4096));
   if (blocks > 2048) blocks = 2048;

@@ -547,37 +547,6 @@ __device__ __forceinline__ bool head_at(const TraceKernelArgs& a, uint64_t p) { 
   return a.tid[2 * p] != a.tid[2 * p - 2] || a.tid[2 * p + 1] != a.tid[2 * p - 1];
 }
 
-// ---- fingerprint table (fast path duplicate detection) -----------------------
-// One 8-byte cell per slot: epoch (16 bits) | fingerprint (48 bits, never 0).
-// A run head claims an empty (stale-epoch) cell with one CAS; finding its own
-// fingerprint means the trace id (probably) formed an earlier run: *dup is
-// set and the exact, sort-based path recomputes every decision.  A 48-bit
-// collision between different trace ids only costs that slow path.
-__device__ __forceinline__ uint64_t fp_cell(const TraceKernelArgs& a, uint64_t hi, uint64_t lo) {
-  const uint64_t fp = ((splitmix64(lo ^ (hi << 1)) >> 16) | 1ull) & 0xFFFFFFFFFFFFull;
-  return ((uint64_t)(a.epoch & 0xFFFFu) << 48) | fp;
-}
-// true: the fingerprint was there already (or the probe sequence ran out)
-__device__ inline bool fp_insert_cell(const TraceKernelArgs& a, uint64_t cell, uint64_t idx) {
-  const uint64_t ep = cell & ~0xFFFFFFFFFFFFull, fp = cell & 0xFFFFFFFFFFFFull;
-  for (uint32_t probes = 0; probes < 64; probes++) {
-    uint64_t* q = &a.fp_table[idx];
-    uint64_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      if ((v & ~0xFFFFFFFFFFFFull) != ep) {
-        if (__hip_atomic_compare_exchange_strong(q, &v, cell, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-          return false;
-        continue;   // v now holds the current cell
-      }
-      break;
-    }
-    if ((v & 0xFFFFFFFFFFFFull) == fp) return true;
-    idx = (idx + 1) & a.fp_mask;
-  }
-  return true;   // probe sequence too long: let the exact path decide
-}
-
 __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos, uint8_t keep, uint8_t level,
                                           double ratio) {
   if (a.mode == kTraceBatch && a.batch_keep) *a.batch_keep = keep;
@@ -600,24 +569,19 @@ __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos
 constexpr int kHeadQ = 128;
 struct HeadQ {
   uint64_t cell[kHeadQ];
-  uint32_t idx[kHeadQ];
 };
 __device__ void flush_heads(const TraceKernelArgs& a, HeadQ& H, uint32_t& hn, int lane) {
   __builtin_amdgcn_wave_barrier();
   bool dup = false;
-  if (a.dup_bkt) {   // bucketed: one returning atomic per head, the fingerprint stored after it
-    for (uint32_t b = 0; b < hn; b += kWave) {
-      if (b + lane < hn) {
-        const uint64_t h = H.cell[b + lane];
-        const uint32_t bk = (uint32_t)(h >> (64 - a.dup_bkt_bits));   // dup_bkt_bits in [1, 32] (the host's)
-        const uint32_t at = atomicAdd(&a.dup_bkt_count[bk], 1u);
-        if (at < kDupBucketCap) a.dup_bkt[(uint64_t)bk * kDupBucketCap + at] = h | 1ull;   // (0 marks an empty set slot)
-        else dup = true;
-      }
+  // bucketed: one returning atomic per head, the fingerprint stored after it
+  for (uint32_t b = 0; b < hn; b += kWave) {
+    if (b + lane < hn) {
+      const uint64_t h = H.cell[b + lane];
+      const uint32_t bk = (uint32_t)(h >> (64 - a.dup_bkt_bits));   // dup_bkt_bits in [1, 32] (the host's)
+      const uint32_t at = atomicAdd(&a.dup_bkt_count[bk], 1u);
+      if (at < kDupBucketCap) a.dup_bkt[(uint64_t)bk * kDupBucketCap + at] = h | 1ull;   // (0 marks an empty set slot)
+      else dup = true;
     }
-  } else {
-    for (uint32_t b = 0; b < hn; b += kWave)
-      if (b + lane < hn) dup |= fp_insert_cell(a, H.cell[b + lane], H.idx[b + lane]);
   }
   // one *dup store per wave flush (a per-head atomic on one word serialises)
   if (__ballot(dup) && lane == 0) atomicOr(a.dup, 1u);
@@ -782,14 +746,9 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         if (hn + nh > kHeadQ) flush_heads(a, HQ, hn, lane);
         if (hd) {
           const uint32_t e = hn + __popcll(hmask & lanemask_lt(lane));
-          if (a.dup_bkt) {
-            // one multiply (odd: a bijection) on the folded id; its top bits
-            // (the bucket) depend on every bit of the id
-            HQ.cell[e] = (r.lo ^ ((r.hi << 29) | (r.hi >> 35))) * 0x9E3779B97F4A7C15ull;
-          } else {
-            HQ.cell[e] = fp_cell(a, r.hi, r.lo);
-            HQ.idx[e] = (uint32_t)(tid_hash(r.hi, r.lo) & a.fp_mask);
-          }
+          // one multiply (odd: a bijection) on the folded id; its top bits
+          // (the bucket) depend on every bit of the id
+          HQ.cell[e] = (r.lo ^ ((r.hi << 29) | (r.hi >> 35))) * 0x9E3779B97F4A7C15ull;
         }
         hn += nh;
       }
@@ -1221,7 +1180,6 @@ __global__ __launch_bounds__(256) void trace_insert_exact_kernel(TraceKernelArgs
 // *overflow, and the sort-based path (gated on it) recomputes the batch.
 __global__ __launch_bounds__(256) void trace_runs_kernel(TraceKernelArgs a) {
   if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  if (a.force_sort && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.overflow, 1u);
   const int lane = threadIdx.x & 63;
   for (uint64_t w = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWave; w < a.n_windows;
        w += (uint64_t)gridDim.x * (256 / kWave)) {
@@ -1745,6 +1703,15 @@ void launch_shard_scatter(const ShardArgs& a, hipStream_t st) {
 }
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st) {
   if (a.n) hipLaunchKernelGGL(shard_unpack_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, st, a);
+}
+namespace {
+__global__ __launch_bounds__(256) void add_i64_kernel(int64_t* dst, const int64_t* src, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] += src[i];
+}
+}  // namespace
+void launch_add_i64(int64_t* dst, const int64_t* src, uint64_t n, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(add_i64_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, dst, src, n);
 }
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st) {
   if (n) hipLaunchKernelGGL(scatter_keep_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, back, pos, n, keep);

@@ -460,49 +460,9 @@ __device__ __forceinline__ void emit_path(const Cfg& cfg, R& rd, uint32_t plen, 
 // ds_read_b128).  Built cooperatively, 32 bytes per lane, branch-free.
 // Classes 0-7 are read for every segment; 8-11 (the email classes) only for
 // segments holding exactly one '@'.  A row is 3 x 16 bytes: [0-3] [4-7] [8-11].
-#ifndef OSE_URL_ASMTAIL
-#define OSE_URL_ASMTAIL 0 // segment bodies past kAsmHead bytes in a compacted tail pass: measured slower (C4 url_plan 6.37 vs 6.79 ms with it, with the deferred checks)
-#endif
-#ifndef OSE_URL_DEFER
-#define OSE_URL_DEFER 0   // date / email / U+FFFD checks in a compacted second classify pass: measured slower (C4 url_plan 6.55 vs 6.79 ms with it, with the tail pass)
-#endif
-#ifndef OSE_URL_ROWMUL
-#define OSE_URL_ROWMUL 0  // A/B: the round-2 row build (a movemask multiply per class and dword): C4 url_plan 6.87 vs 6.19 ms
-#endif
-#ifndef OSE_URL_RDMASK
-#define OSE_URL_RDMASK 0  // skip bitmap rows past a segment / path: measured slower (the extra branches cost more than the reads)
-#endif
-#ifndef OSE_URL_ASM32
-#define OSE_URL_ASM32 0   // dword-packed assembly (ds_or_b32 into a zeroed image): measured slower than byte stores
-#endif
-#ifndef OSE_URL_UAW
-#define OSE_URL_UAW 1     // assembly with unaligned 8-byte LDS reads and 8/4/2/1-byte stores (0: byte stores)
-#endif
-#ifndef OSE_URL_SLASH8
-#define OSE_URL_SLASH8 0  // 1: an entry's separator stored with its body (unaligned stores)
-#endif
-#ifndef OSE_COPY_PF
-#define OSE_COPY_PF 1     // url_copy_kernel loads the next group's columns while it works on this one
-#endif
-#ifndef OSE_URL_QROWS
-#define OSE_URL_QROWS 1   // a group's last <= 16 bitmap rows built in quarter rows (four lanes per row): C2 url_plan 0.753 -> 0.729 ms, C4 6.07 -> 6.05
-#endif
-#ifndef OSE_URL_SPEC
-#define OSE_URL_SPEC 1    // date bytes and email windows read with the main windows (no dependent LDS round trips)
-#endif
-#ifndef OSE_URL_SUMDPP
-#define OSE_URL_SUMDPP 1  // the group sum from the DPP scan (0: a 64-bit shuffle reduction)
-#endif
-#ifndef OSE_URL_CLS6
-#define OSE_URL_CLS6 1    // the classifier's six classes first (one 16-byte + one 8-byte read per window row)
-#endif
-#if OSE_URL_CLS6
 // classes 0-5 are what the segment classifier reads (a row's first vector and
 // half of its second), 6-7 what the enumeration reads, 8-11 the email checks
 enum : uint32_t { C_BNL = 0, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_SL, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
-#else
-enum : uint32_t { C_SL = 0, C_BNL, C_BHX, C_DG, C_AT, C_HI, C_DASH, C_QM, C_BLOC, C_BDOM, C_DOT, C_NAL, kClasses };
-#endif
 constexpr uint32_t kBase = 8;
 constexpr uint32_t kRowVec = 3;   // u32x4 per row
 constexpr uint32_t kBmRows = kStage / 32 + 3;
@@ -566,22 +526,14 @@ __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t
   const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
   const u32x4 v0 = src[0], v1 = src[1];
   uint32_t xs[8];
-#if OSE_URL_ROWMUL
-  xs[0] = v0.x; xs[1] = v0.y; xs[2] = v0.z; xs[3] = v0.w; xs[4] = v1.x; xs[5] = v1.y; xs[6] = v1.z; xs[7] = v1.w;
-#else
   transpose4(v0.x, v0.z, v1.x, v1.z, xs);       // bytes d, d+8, d+16, d+24 for d = 0..3
   transpose4(v0.y, v0.w, v1.y, v1.w, xs + 4);   // d = 4..7
-#endif
 #pragma unroll
   for (int d = 0; d < 8; d++) {
     uint32_t m[kClasses];
     class_masks(xs[d], m);
 #pragma unroll
-#if OSE_URL_ROWMUL
-    for (int c = 0; c < (int)kClasses; c++) acc[c] |= ((((m[c] >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * d);
-#else
     for (int c = 0; c < (int)kClasses; c++) acc[c] = (acc[c] >> 1) | m[c];   // after d = 7: dword d's bits at 8j + d
-#endif
   }
   bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
   bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
@@ -636,11 +588,6 @@ __device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t k) {
   }
   return pos;
 }
-// position of the k-th set bit of a 64-bit m (k < popcount(m))
-__device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t k) {
-  const uint32_t c = (uint32_t)__builtin_popcount((uint32_t)m);
-  return k < c ? select_bit((uint32_t)m, k) : 32 + select_bit((uint32_t)(m >> 32), k - c);
-}
 // Only the rows (bit r of the 96-bit mask {m0, m1, m2}) that hold path bytes:
 // every reader of the bitmaps masks its windows to a path's own bytes, so the
 // rows between paths (other strings of the arena) are never looked at.
@@ -651,7 +598,6 @@ __device__ __forceinline__ void build_bitmaps_rows(lds_u32* stage32, lds_u4* bm,
   auto row_of = [&](uint32_t k) {
     return k < c0 ? select_bit(m0, k) : k < c0 + c1 ? 32 + select_bit(m1, k - c0) : 64 + select_bit(m2, k - c0 - c1);
   };
-#if OSE_URL_QROWS
   // full rounds while 64 rows are left; a last round of at most 16 rows in
   // quarter rows (four lanes per row)
   const uint32_t full = total > kWave && total - (total & ~(kWave - 1)) <= 16 ? total & ~(kWave - 1) : total;
@@ -661,9 +607,6 @@ __device__ __forceinline__ void build_bitmaps_rows(lds_u32* stage32, lds_u4* bm,
     const bool valid = k < total;
     build_quarter_row(stage32, bm, valid ? row_of(k) : 0u, (uint32_t)lane & 3u, valid);
   }
-#else
-  for (uint32_t k = lane; k < total; k += kWave) build_row(stage32, bm, row_of(k));
-#endif
 }
 // bits [lo, hi] (rows) of the 32-row word starting at row w0
 __device__ __forceinline__ uint32_t row_bits(uint32_t lo, uint32_t hi, uint32_t w0) {
@@ -677,24 +620,15 @@ template <int NV>
 struct WinT {
   uint64_t c[4 * NV];
 };
-// L: the bytes the caller looks at (<= 64): rows past them are not read
-// (OSE_URL_RDMASK), so a short segment costs one or two rows of LDS reads
 template <int V0, int NV>
-__device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a, uint32_t L = 64) {
+__device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a) {
   const uint32_t r = a >> 5, sh = a & 31;
-#if OSE_URL_RDMASK
-  const bool r1 = sh + L > 32, r2 = sh + L > 64;
-#else
-  const bool r1 = true, r2 = true;
-  (void)L;
-#endif
   WinT<NV> w;
 #pragma unroll
   for (int v = 0; v < NV; v++) {
-    const u32x4 z{0u, 0u, 0u, 0u};
     const u32x4 x0 = bm[kRowVec * r + V0 + v];
-    const u32x4 x1 = r1 ? bm[kRowVec * (r + 1) + V0 + v] : z;
-    const u32x4 x2 = r2 ? bm[kRowVec * (r + 2) + V0 + v] : z;
+    const u32x4 x1 = bm[kRowVec * (r + 1) + V0 + v];
+    const u32x4 x2 = bm[kRowVec * (r + 2) + V0 + v];
     const uint32_t w0[4] = {x0.x, x0.y, x0.z, x0.w}, w1[4] = {x1.x, x1.y, x1.z, x1.w}, w2[4] = {x2.x, x2.y, x2.z, x2.w};
 #pragma unroll
     for (int c = 0; c < 4; c++)
@@ -705,7 +639,6 @@ __device__ __forceinline__ WinT<NV> load_win(lds_cu4* bm, uint32_t a, uint32_t L
 }
 // the 64-bit windows of classes 0-5 at stage byte a (what the segment
 // classifier reads): per row one 16-byte and one 8-byte read
-#if OSE_URL_CLS6
 struct Win {
   uint64_t c[6];
 };
@@ -724,10 +657,6 @@ __device__ __forceinline__ Win load_win6(lds_cu4* bm, uint32_t a) {
     w.c[c] = ((uint64_t)__builtin_amdgcn_alignbit(w2[c], w1[c], sh) << 32) | __builtin_amdgcn_alignbit(w1[c], w0[c], sh);
   return w;
 }
-#else
-typedef WinT<2> Win;   // classes 0-7
-__device__ __forceinline__ Win load_win6(lds_cu4* bm, uint32_t a) { return load_win<0, 2>(bm, a); }
-#endif
 __device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
 // first byte of class c in [a, e) (stage coordinates), or e
@@ -821,7 +750,7 @@ __device__ __forceinline__ bool email_win(uint64_t at, lds_cu4* bm, uint32_t a, 
   const uint64_t M = low_mask(L);
   const uint32_t p = (uint32_t)__builtin_ctzll(at);
   if (p == 0) return false;
-  const WinT<1> e = load_win<2, 1>(bm, a, L);   // BLOC, BDOM, DOT, NAL
+  const WinT<1> e = load_win<2, 1>(bm, a);   // BLOC, BDOM, DOT, NAL
   const uint64_t dom = M & ~low_mask(p + 1);
   if ((e.c[0] & low_mask(p)) || (e.c[1] & dom)) return false;
   const uint64_t dots = e.c[2] & dom;
@@ -873,10 +802,10 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
     const UrlCustomDev& cu = reinterpret_cast<const UrlCustomDev*>(cfg.blob + cfg.h->custom_off)[k];
     if (dfa_match(cfg.blob, cfg.dfa_off(cu.dfa), rd, s, s + L)) return (int)cu.name;
   }
-  if (!(cfg.ablate & 8) && date_win(rd, w.c[C_DG], w.c[C_DASH], s, L)) return kNameDate;
+  if (date_win(rd, w.c[C_DG], w.c[C_DASH], s, L)) return kNameDate;
   const bool any_hi = (w.c[C_HI] & M) != 0;
   const uint64_t at = w.c[C_AT] & M;
-  if (!(cfg.ablate & 16) && !any_hi && at && (at & (at - 1)) == 0 && email_win(at, bm, a, L)) return kNameEmail;
+  if (!any_hi && at && (at & (at - 1)) == 0 && email_win(at, bm, a, L)) return kNameEmail;
   const uint64_t d = w.c[C_DG] & M, d1 = d & (d >> 1), d2 = d1 & (d1 >> 2), d7 = d2 & (d2 >> 3);
   if ((L > 0 && (w.c[C_BNL] & M) == 0) || d7 || ((w.c[C_BHX] & M) == 0 && L >= 16 && (L & 1) == 0)) return kNameId;
   if (L >= 36) {
@@ -885,7 +814,7 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
         (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
       return kNameId;
   }
-  if (!(cfg.ablate & 32) && any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
+  if (any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
   return -1;
 }
 
@@ -896,7 +825,7 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
 template <class R>
 __device__ __forceinline__ int classify_spec(const Cfg& cfg, R& rd, lds_cu4* bm, uint32_t a, uint32_t s, uint32_t L) {
   const Win w = load_win6(bm, a);
-  const WinT<1> e = load_win<2, 1>(bm, a, L);
+  const WinT<1> e = load_win<2, 1>(bm, a);
   const uint32_t wa = rd.word(s + 10), wb = rd.word(s + 16);
   if (cfg.n_custom) return classify_win(cfg, rd, w, bm, a, s, L);
   const uint64_t M = low_mask(L);
@@ -913,34 +842,6 @@ __device__ __forceinline__ int classify_spec(const Cfg& cfg, R& rd, lds_cu4* bm,
       return kNameId;
   }
   if (any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
-  return -1;
-}
-
-// classify_win's first pass over a step's segments: the result when none of
-// the date / email / U+FFFD checks applies (*defer false), else *defer and
-// the segment is classified by classify_win in a second pass that takes
-// only such segments (about one in ten of C4's), so those divergent checks
-// run for one compacted step per group instead of in every step.  With
-// custom ids configured (checked first) nothing is deferred.
-template <class R>
-__device__ __forceinline__ int classify_fast(const Cfg& cfg, R& rd, const Win& w, lds_cu4* bm, uint32_t a, uint32_t s,
-                                             uint32_t L, bool* defer) {
-  if (cfg.n_custom || !OSE_URL_DEFER) {
-    *defer = false;
-    return classify_win(cfg, rd, w, bm, a, s, L);
-  }
-  const uint64_t M = low_mask(L);
-  const uint64_t at = w.c[C_AT] & M;
-  *defer = (w.c[C_HI] & M) != 0 || (at && (at & (at - 1)) == 0) || date_pre(w.c[C_DG], w.c[C_DASH], L);
-  if (*defer) return -1;
-  const uint64_t d = w.c[C_DG] & M, d1 = d & (d >> 1), d2 = d1 & (d1 >> 2), d7 = d2 & (d2 >> 3);
-  if ((L > 0 && (w.c[C_BNL] & M) == 0) || d7 || ((w.c[C_BHX] & M) == 0 && L >= 16 && (L & 1) == 0)) return kNameId;
-  if (L >= 36) {
-    const uint64_t hx = ~w.c[C_BHX], ds = w.c[C_DASH], sh = L - 36;
-    if (((hx & kUuidHex) == kUuidHex && (ds & kUuidDash) == kUuidDash) ||
-        (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
-      return kNameId;
-  }
   return -1;
 }
 
@@ -1209,23 +1110,18 @@ constexpr uint32_t kSegCap = 192;   // per-wave segment list (C2 groups hold ~11
 // 12-class bitmaps + segment list per wave (39.7 KB per 4-wave workgroup) and
 // <= 128 VGPRs keep four workgroups per CU; a second buffer, prefetching a
 // whole group ahead, held the kernel to three (52 KB) and measured 8% slower
-// (OSE_PLAN_BUFS=2 builds that variant: C4 plan 7.45 vs 6.84 ms).
+// (C4 plan 7.45 vs 6.84 ms, round 2).
 constexpr uint32_t kPlanStage = 3 * 1024;
-#ifndef OSE_PLAN_BUFS
-#define OSE_PLAN_BUFS 1
-#endif
-constexpr uint32_t kPlanBufs = OSE_PLAN_BUFS;
 constexpr uint32_t kPlanBmRows = kPlanStage / 32 + 3;
 struct PlanSmem {
   NamesSmem ns;
-  __attribute__((aligned(16))) uint8_t stage[kPlanBufs][kWaves][kPlanStage + 16];
+  __attribute__((aligned(16))) uint8_t stage[kWaves][kPlanStage + 16];
   __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kPlanBmRows];   // class bitmaps, then the output image
   uint32_t segs[kWaves][kSegCap];   // enumerated segments (start | len | owner lane)
   uint32_t cls[kWaves][kSegCap];    // their classification (out_len << 8 | id + 1)
   BracedNames bn;
 };
 constexpr uint32_t kImgCap = kRowVec * kPlanBmRows * 16;   // bytes of one wave's output image
-constexpr uint32_t kAsmHead = 8;   // body bytes an entry writes in its assembly step (the rest: tail pass)
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
@@ -1357,24 +1253,12 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   if (needs_path) {
     if (win) {
       uint32_t w[12];
-#if OSE_URL_RDMASK
-      // only the rows the path covers, and the '?' words only for http.target
-      const uint32_t nrow = (b0 + plen + 31) >> 5;
-      const bool tgt = (f & OSE_URL_PATH_MASK) == OSE_URL_PATH_TARGET;
-#pragma unroll
-      for (int j = 0; j < 6; j++) {
-        const uint32_t r = min(r0 + j, kPlanBmRows - 1);
-        w[j] = (uint32_t)j < nrow ? b32[4 * kRowVec * r + C_SL] : 0u;
-        w[6 + j] = tgt && (uint32_t)j < nrow ? b32[4 * kRowVec * r + C_QM] : 0u;
-      }
-#else
 #pragma unroll
       for (int j = 0; j < 6; j++) {
         const uint32_t r = min(r0 + j, kPlanBmRows - 1);   // rows past the path are masked off below
         w[j] = b32[4 * kRowVec * r + C_SL];
         w[6 + j] = b32[4 * kRowVec * r + C_QM];
       }
-#endif
       sl0 = w[0] | ((uint64_t)w[1] << 32);
       sl1 = w[2] | ((uint64_t)w[3] << 32);
       sl2 = w[4] | ((uint64_t)w[5] << 32);
@@ -1464,43 +1348,18 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
     const uint32_t out = id >= 0 ? name_len(cfg, (uint32_t)id) + 2 : L;
     cls[x] = (out << 8) | min((uint32_t)(id + 1), 255u);
   };
-  uint64_t dm0 = 0, dm1 = 0, dm2 = 0;   // deferred entries of steps 0, 1, 2 (kSegCap = 3 steps)
-  for (uint32_t x0 = 0; x0 < total; x0 += kWave) {   // classify, first pass
+  for (uint32_t x0 = 0; x0 < total; x0 += kWave) {   // classify
     const uint32_t x = x0 + (uint32_t)lane;
-    bool defer = false;
     if (x < total) {
       const uint32_t ent = segs[x];
       const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
       int id = -1;
-      if (L <= 64) {
-#if OSE_URL_SPEC
-        if (!(cfg.ablate & (8 | 16 | 32))) {
-          id = classify_spec(cfg, rd0, bm, s, s, L);
-        } else
-#endif
-        {
-          const Win w = load_win6(bm, s);
-          id = classify_fast(cfg, rd0, w, bm, s, s, L, &defer);
-        }
-      } else {
+      if (L <= 64)
+        id = classify_spec(cfg, rd0, bm, s, s, L);
+      else
         longseg = true;   // a segment longer than a 64-bit window: the group goes to url_plan_slow_kernel
-      }
-      if (!defer) put_cls(x, id, L);
+      put_cls(x, id, L);
     }
-    const uint64_t dm = __ballot(defer);
-    if (x0 == 0) dm0 = dm;
-    else if (x0 == kWave) dm1 = dm;
-    else dm2 = dm;
-  }
-  // second pass: the deferred entries, compacted (lane k takes the k-th)
-  const uint32_t n0 = (uint32_t)__popcll(dm0), n1 = (uint32_t)__popcll(dm1), nd = n0 + n1 + (uint32_t)__popcll(dm2);
-  for (uint32_t k = lane; k < nd; k += kWave) {
-    const uint32_t x = k < n0 ? select_bit64(dm0, k) : k < n0 + n1 ? kWave + select_bit64(dm1, k - n0)
-                                                                    : 2 * kWave + select_bit64(dm2, k - n0 - n1);
-    const uint32_t ent = segs[x];
-    const uint32_t s = ent & 0xFFFu, L = (ent >> 12) & 0x1FFFu;
-    const Win w = load_win6(bm, s);
-    put_cls(x, classify_win(cfg, rd0, w, bm, s, s, L), L);
   }
   wave_lds_sync();
   if (__ballot(longseg)) return false;
@@ -1580,13 +1439,10 @@ __device__ __forceinline__ uint32_t plan_gate(const PlanCols& c) {
 // bytes) at L's output offset plus the outputs of L's earlier entries; a path
 // that neither starts with '/' nor keeps its original form (processor.go:
 // 182-185 "/" + body) drops the first separator.  M_SLASH / M_RENAME_SLASH
-// spans are a lone '/'.  Every image byte is written exactly once (byte
-// stores, 8 loads in flight per batch), so the image needs no clearing.
-// Entries are written 64 per step, one per lane: the per-byte work follows the
-// longest segment of a step, not the longest path of the group.
-// OSE_URL_ASM32: each entry's bytes go out as whole dwords (ds_or_b32 into an
-// image the caller zeroed; two unaligned dword reads of the source per
-// dword), about a third of the LDS instructions of the byte form.
+// spans are a lone '/'.  Every image byte is written exactly once, so the
+// image needs no clearing.  Entries are written 64 per step, one per lane:
+// the per-byte work follows the longest segment of a step, not the longest
+// path of the group.
 __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L, uint32_t stage_src, uint32_t* segs,
                                                uint32_t* cls, const BracedNames& bn, uint32_t bn_src,
                                                const Plan& p, uint32_t seg_off, uint32_t local) {
@@ -1599,20 +1455,13 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
   const int32_t adj = (int32_t)local - (int32_t)E0 - (int32_t)(1 - pre);
   const uint32_t pk = ((uint32_t)adj & 0xFFFFu) | (off << 16) | (pre << 24);
   if (p.len && (p.mode == M_SLASH || p.mode == M_RENAME_SLASH)) {
-#if OSE_URL_ASM32
-    __hip_atomic_fetch_or((lds_w32*)img + (local >> 2), (uint32_t)'/' << (8 * (local & 3)), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
     img[local] = '/';
-#endif
   }
   const uint32_t total = lane_value(off + nseg, kWave - 1);
   uint32_t carry = 0;
-  uint64_t tm0 = 0, tm1 = 0, tm2 = 0;   // entries whose bodies go past kAsmHead bytes, per step
   for (uint32_t x0 = 0; x0 < total; x0 += kWave) {
     const uint32_t x = x0 + (uint32_t)lane;
     const bool v = x < total;
-    bool tail = false;
     const uint32_t ent = v ? segs[x] : 0u, c = v ? cls[x] : 0u;
     const uint32_t opk = (uint32_t)__shfl((int)pk, (int)(ent >> 25), kWave);
     uint32_t stot;
@@ -1624,65 +1473,15 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       const int id = (int)(c & 0xFFu) - 1;
       const uint32_t so = id >= 0 ? bn_src + bn.off[id] : stage_src + (ent & 0xFFFu);   // the body's LDS byte offset
       const uint32_t n = id >= 0 ? (uint32_t)bn.len[id] : (ent >> 12) & 0x1FFFu;
-#if OSE_URL_ASM32
-      // output bytes [b0, b1): '/' at pos (when written), the body at pos + 1;
-      // each image dword they touch gets its bytes by one ds_or_b32 (the image
-      // was zeroed; dwords shared with the neighbouring entries get OR-ed)
-      const uint32_t b0 = slash ? pos : pos + 1, b1 = pos + 1 + n;
-      lds_w32* img32 = (lds_w32*)img;
-      for (uint32_t k = b0 >> 2; 4 * k < b1; k++) {
-        // body byte i sits at image byte pos + 1 + i: the dword's 4 bytes are body bytes 4k - pos - 1 + j
-        uint32_t w = lds_word(L, so + 4 * k - pos - 1);
-        const uint32_t lo = b0 > 4 * k ? b0 - 4 * k : 0u, hi = b1 - 4 * k < 4 ? b1 - 4 * k : 4u;
-        if (slash && pos >> 2 == k) w = (w & ~(0xFFu << (8 * (pos & 3)))) | ('/' << (8 * (pos & 3)));
-        const uint32_t mask = (hi == 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
-        __hip_atomic_fetch_or(&img32[k], w & mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#else
-#if OSE_URL_UAW && OSE_URL_SLASH8 && !OSE_URL_ASMTAIL
-      // the separator goes out with the body: bytes [pos, pos + 1 + n) from
-      // the byte before the body, the first replaced by '/'
-      const uint32_t b0 = slash ? pos : pos + 1, nb = pos + 1 + n - b0;
-      lds_out_u8* dp = img + b0;
-      const lds_u8* sp = L + so - (slash ? 1u : 0u);
-      for (uint32_t q = 0; q < nb; q += 8) {
-        uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + q);
-        if (q == 0 && slash) v = (v & ~0xFFull) | '/';
-        const uint32_t rem = nb - q;
-        if (rem >= 8) {
-          *reinterpret_cast<lds_w64u*>(dp + q) = v;
-        } else {
-          uint32_t o = q;
-          if (rem & 4) { *reinterpret_cast<lds_w32u*>(dp + o) = (uint32_t)v; v >>= 32; o += 4; }
-          if (rem & 2) { *reinterpret_cast<lds_w16u*>(dp + o) = (uint16_t)v; v >>= 16; o += 2; }
-          if (rem & 1) dp[o] = (uint8_t)v;
-        }
-      }
-#else
       if (slash) img[pos] = '/';
       lds_out_u8* dp = img + pos + 1;
       const lds_u8* sp = L + so;
-#if OSE_URL_ASMTAIL
-      // the first kAsmHead bytes here; a longer body's rest in the tail pass
-      // below (its source and its body's place, pos + 1 — pos itself is -1
-      // for an image's first entry when its path has no leading '/' — kept
-      // in the entry's now dead list slots)
-      const uint32_t head = min(n, kAsmHead);
-      tail = n > kAsmHead;
-      if (tail) {
-        segs[x] = so | ((pos + 1) << 16);
-        cls[x] = n;
-      }
-#else
-      const uint32_t head = n;
-#endif
-#if OSE_URL_UAW
       // gfx950 LDS takes unaligned 8-, 4- and 2-byte accesses: one 8-byte read
       // per 8 source bytes (reads past n stay inside the stage / name table),
       // whole 8-byte stores, and the last 1-7 bytes as a 4-, 2- and 1-byte store
-      for (uint32_t q = 0; q < head; q += 8) {
+      for (uint32_t q = 0; q < n; q += 8) {
         uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + q);
-        const uint32_t rem = head - q;
+        const uint32_t rem = n - q;
         if (rem >= 8) {
           *reinterpret_cast<lds_w64u*>(dp + q) = v;
         } else {
@@ -1692,57 +1491,17 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
           if (rem & 1) dp[o] = (uint8_t)v;
         }
       }
-#else
-      for (uint32_t q = 0; q < head; q += 8) {
-        uint32_t b[8];
-#pragma unroll
-        for (uint32_t t = 0; t < 8; t++) b[t] = sp[q + t];   // reads past n stay inside the stage / name table
-#pragma unroll
-        for (uint32_t t = 0; t < 8; t++)
-          if (q + t < head) dp[q + t] = (uint8_t)b[t];
-      }
-#endif
-#endif   // OSE_URL_SLASH8
-#endif
-    }
-    const uint64_t tm = __ballot(tail);
-    if (x0 == 0) tm0 = tm;
-    else if (x0 == kWave) tm1 = tm;
-    else tm2 = tm;
-  }
-#if OSE_URL_ASMTAIL
-  // tail pass: the bodies longer than kAsmHead (about one entry in ten on C4's
-  // mix), compacted over the lanes, so the few long segments of a group cost
-  // one pass of their own instead of lengthening every step's byte loop
-  const uint32_t n0 = (uint32_t)__popcll(tm0), n1 = (uint32_t)__popcll(tm1), nt = n0 + n1 + (uint32_t)__popcll(tm2);
-  if (nt) {
-    wave_lds_sync();
-    for (uint32_t k = lane; k < nt; k += kWave) {
-      const uint32_t x = k < n0 ? select_bit64(tm0, k) : k < n0 + n1 ? kWave + select_bit64(tm1, k - n0)
-                                                                      : 2 * kWave + select_bit64(tm2, k - n0 - n1);
-      const uint32_t sp_pos = segs[x], n = cls[x];
-      const lds_u8* sp = L + (sp_pos & 0xFFFFu);
-      lds_out_u8* dp = img + (sp_pos >> 16);
-      for (uint32_t q = kAsmHead; q < n; q += 8) {
-        uint32_t b[8];
-#pragma unroll
-        for (uint32_t t = 0; t < 8; t++) b[t] = sp[q + t];
-#pragma unroll
-        for (uint32_t t = 0; t < 8; t++)
-          if (q + t < n) dp[q + t] = (uint8_t)b[t];
-      }
     }
   }
-#endif
 }
 
 // kMode bit 0 (kModeGeneral): user templatization rules or custom ids are
 // configured; without it the instance is compiled with neither (their loops
 // fold away, which is what keeps the default-config kernel off scratch).
-// bit 1 (kModeDiag): OSE_URL_ABLATE / per-section clocks.
+// bit 1 (kModeDiag, OSE_DIAG builds only): OSE_URL_ABLATE / per-section clocks.
 constexpr int kModeGeneral = 1, kModeDiag = 2;
 template <int kMode>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanBufs == 1 ? 4 : 3, kPlanBufs == 1 ? 4 : 3))) void url_plan_kernel(UrlKernelArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void url_plan_kernel(UrlKernelArgs a) {
   __shared__ PlanSmem sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   Cfg cfg = load_cfg(a, sm.ns);
@@ -1763,7 +1522,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
   if (g >= a.n_groups) return;
   const bool tm = (kMode & kModeDiag) && a.dbg != nullptr;
   uint64_t t0 = 0, t_stage = 0, t_bm = 0, t_plan = 0, t_emit = 0, tt[3] = {0, 0, 0};
-  uint32_t buf = 0;
   const bool fused_cfg = sm.bn.ok && !(a.ablate & 2);
   const lds_u8* L = (const lds_u8*)(void*)&sm;
   const uint32_t bn_src = (uint32_t)((uint8_t*)sm.bn.b - (uint8_t*)&sm);
@@ -1778,7 +1536,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
   PlanCols nxt = plan_cols(a, (uint64_t)(g + stride) * kWave + lane);
   PlanCols nn{};
   bool np = plan_gate(cur) == 2;
-  StageDma pf = stage_dma(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u, sm.stage[0][wv]);
+  StageDma pf = stage_dma(a.arena, np ? cur.pr.off : ~0u, np ? cur.pr.off + cur.pr.len : 0u, sm.stage[wv]);
   bool first = true;
   for (;;) {
     if (tm) t0 = clk();
@@ -1790,17 +1548,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
       nxt = nn;
     }
     first = false;
-    uint8_t* stage = sm.stage[buf][wv];
+    uint8_t* stage = sm.stage[wv];
     lds_u32* stage32 = (lds_u32*)stage;
     const uint64_t i = (uint64_t)g * kWave + lane;
     const uint32_t g2 = g + stride;
     const bool more = g2 < a.n_groups;
-    // in flight while this group is planned: the columns of the group after
-    // the next (and, with two stage buffers, the next group's bytes)
+    // in flight while this group is planned: the columns of the group after the next
     const bool np2 = more && plan_gate(nxt) == 2;
-    StageDma pf2{0, 0};
-    if constexpr (kPlanBufs == 2)
-      pf2 = stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[buf ^ 1][wv]);
     nn = plan_cols(a, (uint64_t)(g2 + stride) * kWave + lane);
     if (tm) { const uint64_t t1 = clk(); t_stage += t1 - t0; t0 = t1; }
 
@@ -1857,13 +1611,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     } else {
     // the group's output bytes and each lane's offset in its image: one DPP
     // scan (a 64-bit shuffle reduction would be 12 dependent LDS round trips)
-#if OSE_URL_SUMDPP
     uint32_t sum32;
     const uint32_t local = wave_excl_scan(p.len, &sum32);
     const uint64_t sum = sum32;
-#else
-    const uint64_t sum = wave_sum_u64(p.len);
-#endif
     const uint64_t need = (sum + 15) & ~15ull;
     // wave-uniform: the group is assembled here unless a user rule matched, a
     // name id lies outside the braced table, the list planner gave up, or the
@@ -1899,14 +1649,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     if (fast) {
       lds_u4* img4 = (lds_u4*)sm.bm[wv];
       const uint32_t n16 = (uint32_t)(need / 16);
-#if !OSE_URL_SUMDPP
-      uint32_t unused;
-      const uint32_t local = wave_excl_scan(p.len, &unused);
-#endif
-#if OSE_URL_ASM32
-      for (uint32_t k = lane; k < n16; k += kWave) img4[k] = u32x4{0u, 0u, 0u, 0u};   // the bitmaps are dead here
-      wave_lds_sync();
-#endif
       if (!(a.ablate & 64))   // diagnostics: OSE_URL_ABLATE 64 skips the image writes (wrong output)
         assemble_group((lds_out_u8*)sm.bm[wv], L, (uint32_t)(stage - (uint8_t*)&sm), sm.segs[wv], sm.cls[wv], sm.bn,
                        bn_src, p, seg_off, local);
@@ -1930,10 +1672,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kPlanB
     if (tm) { const uint64_t t1 = clk(); t_emit += t1 - t0; t0 = t1; }
     if (!more) break;
     wave_lds_sync();   // every lane is done with this group's stage and bitmaps
-    if constexpr (kPlanBufs == 1)
-      pf2 = stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[0][wv]);
-    pf = pf2;
-    buf ^= kPlanBufs - 1;
+    pf = stage_dma(a.arena, np2 ? nxt.pr.off : ~0u, np2 ? nxt.pr.off + nxt.pr.len : 0u, sm.stage[wv]);
     g = g2;
   }
   if (tm && lane == 0) {
@@ -2097,20 +1836,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize 
   // the next group's columns are loaded while this group is worked on
   CopyCols An{0, 0, 0, ~0ull};
   sizedev::SpanCols xn{};
-  if (OSE_COPY_PF && g < a.n_groups) {
+  if (g < a.n_groups) {
     An = copy_cols(a, g, lane);
     if (kSize && sz_on) xn = sizedev::size_span_load(a.sz, (uint64_t)g * kWave + lane, false);
   }
   for (; g < a.n_groups; g += stride) {
     const uint64_t ia = (uint64_t)g * kWave + lane;
-    if (!OSE_COPY_PF) {
-      An = copy_cols(a, g, lane);
-      if (kSize && sz_on) xn = sizedev::size_span_load(a.sz, ia, false);
-    }
     const CopyCols A = An;
     const sizedev::SpanCols x0 = xn;
     const bool more = g + stride < a.n_groups;
-    if (OSE_COPY_PF && more) {
+    if (more) {
       An = copy_cols(a, g + stride, lane);
       if (kSize && sz_on) xn = sizedev::size_span_load(a.sz, (uint64_t)(g + stride) * kWave + lane, false);
     }
@@ -2145,36 +1880,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize 
     }
   }
 }
-// Two groups per iteration (g and g + stride): their columns are loaded
-// together and their first scratch rounds together, so a wave waits two
-// memory round trips per two groups (kept for A/B: OSE_COPY_PAIR=1).
-__global__ __launch_bounds__(kThreads) void url_copy_pair_kernel(UrlKernelArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t stride = wave_stride();
-  for (uint32_t g = wave_first_group(); g < a.n_groups; g += 2 * stride) {
-    const uint32_t gb = g + stride;
-    const bool hb = gb < a.n_groups;
-    const CopyCols A = copy_cols(a, g, lane);
-    CopyCols B{0, 0, 0, ~0ull};
-    if (hb) B = copy_cols(a, gb, lane);
-    uint32_t unused;
-    const uint32_t la = wave_excl_scan(A.len, &unused), lb = wave_excl_scan(B.len, &unused);
-    const uint64_t ia = (uint64_t)g * kWave + lane, ib = (uint64_t)gb * kWave + lane;
-    const CopyJob ja = copy_job(a, A), jb = copy_job(a, B);
-    const uint4 va = copy_load(ja, 0), vb = copy_load(jb, 0);
-    if (ia < a.n_spans) {
-      // refs mode: a fast group's template stays in its scratch image
-      const uint64_t at = a.refs && A.so != ~0ull ? A.so : A.base;
-      a.tmpl[ia] = ose_strref{(uint32_t)(at + la), A.len};
-    }
-    if (hb && ib < a.n_spans) a.tmpl[ib] = ose_strref{(uint32_t)(B.base + lb), B.len};
-    uint32_t carry = 0;
-    if (ja.on) copy_rest(ja, va, carry);
-    carry = 0;
-    if (jb.on) copy_rest(jb, vb, carry);
-  }
-}
-
 // K1b: the groups K1 listed as unplanned, one single-wave workgroup per
 // group (persistent; exits at once when the list is empty).  Their paths are
 // planned in lane subsets whose 16-byte chunks fit K1's 3 KB stage: each
@@ -2364,7 +2069,7 @@ static uint32_t resident_blocks(K kernel, size_t dyn_lds) {
 }  // namespace
 
 static int url_mode(const UrlKernelArgs& a) {
-  return (a.general ? kModeGeneral : 0) | ((a.ablate || a.dbg) ? kModeDiag : 0);
+  return (a.general ? kModeGeneral : 0) | ((OSE_DIAG && (a.ablate || a.dbg)) ? kModeDiag : 0);
 }
 template <int M>
 static uint32_t plan_blocks(const UrlKernelArgs& a) {
@@ -2378,17 +2083,21 @@ static void launch_plan_mode(const UrlKernelArgs& a, hipStream_t st) {
 uint32_t url_plan_waves(const UrlKernelArgs& a) {
   switch (url_mode(a)) {
     case 0: return plan_blocks<0>(a) * kWaves;
-    case 1: return plan_blocks<1>(a) * kWaves;
+#if OSE_DIAG
     case 2: return plan_blocks<2>(a) * kWaves;
-    default: return plan_blocks<3>(a) * kWaves;
+    case 3: return plan_blocks<3>(a) * kWaves;
+#endif
+    default: return plan_blocks<1>(a) * kWaves;
   }
 }
 void launch_url_plan(const UrlKernelArgs& a, hipStream_t st) {
   switch (url_mode(a)) {
     case 0: launch_plan_mode<0>(a, st); break;
-    case 1: launch_plan_mode<1>(a, st); break;
+#if OSE_DIAG
     case 2: launch_plan_mode<2>(a, st); break;
-    default: launch_plan_mode<3>(a, st); break;
+    case 3: launch_plan_mode<3>(a, st); break;
+#endif
+    default: launch_plan_mode<1>(a, st); break;
   }
 }
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st) {
@@ -2399,23 +2108,12 @@ uint32_t url_copy_blocks(uint32_t n_groups) {
   // resident grid 1.01 ms, 16384 blocks 0.93, 65536 0.92): a wave's two
   // groups are two memory round trips, and the waves waiting on them are what
   // keeps HBM busy
-  static const uint32_t cap = [] {
-    const char* g = getenv("OSE_COPY_GRID");   // tuning
-    return g ? std::min<uint32_t>(kUrlCopyMaxBlocks, std::max<uint32_t>(1, (uint32_t)strtoul(g, nullptr, 0)))
-             : kUrlCopyMaxBlocks;
-  }();
-  return std::max<uint32_t>(1, std::min<uint32_t>(cap, (n_groups + 2 * kWaves - 1) / (2 * kWaves)));
+  return std::max<uint32_t>(1, std::min<uint32_t>(kUrlCopyMaxBlocks, (n_groups + 2 * kWaves - 1) / (2 * kWaves)));
 }
 void launch_url_copy(const UrlKernelArgs& a, hipStream_t st) {
-  static const bool pair = [] {
-    const char* p = getenv("OSE_COPY_PAIR");   // A/B: the two-groups-per-iteration kernel
-    return p && strtoul(p, nullptr, 0) != 0;
-  }();
   const uint32_t blocks = url_copy_blocks(a.n_groups);
   if (a.fuse_size)
     hipLaunchKernelGGL(url_copy_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, a);
-  else if (pair && !a.refs)
-    hipLaunchKernelGGL(url_copy_pair_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
   else
     hipLaunchKernelGGL(url_copy_kernel<false>, dim3(blocks), dim3(kThreads), 0, st, a);
 }

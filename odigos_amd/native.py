@@ -44,6 +44,7 @@ STAGE_TEMPLATE = 0x2
 STAGE_SIZE = 0x4
 STAGE_APPLY_KEEP = 0x8
 STAGE_TEMPLATE_REFS = 0x10
+STAGE_APPLY_TEMPLATE = 0x20
 XREC_BYTES = 56
 
 GROUP_TRACE_ID = 0
@@ -151,6 +152,7 @@ def lib() -> C.CDLL:
         "ose_gbt_stats": (C.c_int, [_p, C.POINTER(C.c_uint64)]),
         "ose_gbt_download": (C.c_int, [_p, C.POINTER(Columns)]),
         "ose_engine_attr_key": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
+        "ose_engine_set_option": (C.c_int, [_p, C.c_char_p, C.c_int64]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),
         "ose_batch_columns": (C.POINTER(Columns), [_p]),
         "ose_batch_outputs": (C.POINTER(Outputs), [_p]),
@@ -181,6 +183,7 @@ def lib() -> C.CDLL:
         "osehost_xgroup_destroy": (None, [_p]),
         "osehost_exchange_sample_local": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(Outputs), _p, C.c_int,
                                                     C.POINTER(Rand), _p, C.POINTER(C.c_uint64)]),
+        "osehost_allreduce_counters_local": (C.c_int, [_p, _p, C.c_uint64, _p, C.c_int, _p]),
         "osehost_processor_create": (_p, [C.c_char_p, C.c_char_p]),
         "osehost_processor_destroy": (None, [_p]),
         "osehost_processor_set": (None, [_p, C.c_uint64, C.c_uint32]),

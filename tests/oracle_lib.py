@@ -208,3 +208,96 @@ def span_template_bytes(refs: np.ndarray, arena: np.ndarray, mask: np.ndarray) -
     idx = np.repeat(r[:, 0] - starts, lens) + np.arange(total, dtype=np.int64)
     assert idx.max() < arena.size, "a template ref points past the arena"
     return arena[idx], lens
+
+
+def concat_sampling_columns(sources):
+    """The sampling columns of the global batch that the split-mode sources
+    (node-collector shards, gen_batch.cpp) make concatenated in rank order:
+    resources and arena offsets renumbered per source.  Returns (cols, keep
+    alive arrays, per-source span offsets)."""
+    cat = {}
+    for f, dt in (("trace_id", np.uint64), ("start_ns", np.uint64), ("end_ns", np.uint64), ("status", np.uint8),
+                  ("route", np.uint32)):
+        cat[f] = np.concatenate([g.array(f).view(dt)[: (g.cols.n_spans * (2 if f in ("trace_id", "route") else 1))]
+                                 for g in sources])
+    roff = np.cumsum([0] + [g.cols.n_resources for g in sources])
+    aoff = np.cumsum([0] + [g.cols.arena_bytes for g in sources])
+    cat["resource"] = np.concatenate([g.array("resource").view(np.uint32)[: g.cols.n_spans] + np.uint32(roff[k])
+                                      for k, g in enumerate(sources)])
+    rt = cat["route"].reshape(-1, 2).copy()
+    base = np.concatenate([np.full(g.cols.n_spans, aoff[k], np.uint64) for k, g in enumerate(sources)])
+    rt[:, 0] = (rt[:, 0].astype(np.uint64) + base * (rt[:, 1] > 0)).astype(np.uint32)
+    cat["route"] = rt.reshape(-1)
+    cat["arena"] = np.concatenate([g.array("arena")[: g.cols.arena_bytes] for g in sources] + [np.zeros(64, np.uint8)])
+    for f in ("res_svc", "res_svc_str"):
+        cat[f] = np.concatenate([g.array(f).view(np.uint32)[: g.cols.n_resources] for g in sources])
+    assert cat["arena"].size < 2**32
+    from odigos_amd import native
+    cols = native.Columns()
+    cols.n_spans = sum(g.cols.n_spans for g in sources)
+    cols.n_resources = int(roff[-1])
+    cols.arena_bytes = int(aoff[-1])
+    for f, a in cat.items():
+        setattr(cols, f, a.ctypes.data)
+    offs = np.cumsum([0] + [g.cols.n_spans for g in sources])
+    return cols, cat, offs
+
+
+def concat_keep_oracle(sources, cfg, seed, threads=16):
+    """SAMPLE on the global batch (the sources concatenated in rank order):
+    each source's slice of the keep bytes."""
+    from odigos_amd import native
+    from odigos_amd.batch import HostOutputs
+    cols, keepalive, offs = concat_sampling_columns(sources)
+    ho = HostOutputs(cols)
+    assert SamplingOracle(cfg).process(cols, ho.outs, native.GROUP_TRACE_ID, seed, threads) == 0
+    keep = ho.view("keep", np.uint8)[: cols.n_spans]
+    del keepalive
+    return [keep[offs[k]: offs[k + 1]].copy() for k in range(len(sources))]
+
+
+def node_parity(gens, dbs, cfg, stages, threads, calls, node_counters=None):
+    """The emulated 8-GPU step against the oracle on the GLOBAL batch (the
+    sources concatenated in rank order, traces straddling ranks): SAMPLE on the
+    concatenation gives every rank's keep slice; TEMPLATE and SIZE run per
+    rank on its own spans with that keep (what SIZE | APPLY_KEEP does after
+    the exchange); the node's counters are the sums over ranks (what
+    ose_allreduce_counters yields)."""
+    from odigos_amd.batch import HostOutputs
+    keeps = concat_keep_oracle(gens, cfg["odigossampling"], 0x5EED, threads)
+    uo = UrlOracle(cfg["odigosurltemplate"]) if stages & native.STAGE_TEMPLATE else None
+    res = {"keep": True, "url_out": True, "tmpl_lens": True, "tmpl_bytes_per_span": True}
+    node_bytes = node_bytes_gpu = None
+    node_acc = node_acc_gpu = 0
+    for g, d, kp in zip(gens, dbs, keeps):
+        n = g.cols.n_spans
+        res["keep"] &= bool(np.array_equal(kp, d.out_numpy("keep", n=n)))
+        ho = HostOutputs(g.cols)
+        ho.view("keep", np.uint8)[:n] = kp
+        if uo:
+            assert uo.process(g.cols, ho.outs, threads) == 0
+            u = d.out_numpy("url_out", n=n)
+            res["url_out"] &= bool(np.array_equal(ho.view("url_out", np.uint8)[:n], u))
+            m = u != 0
+            gb, gl = span_template_bytes(d.out_numpy("tmpl", np.uint32, n=2 * n), d.out_numpy("tmpl_arena", n=d.used()), m)
+            ob, ol = span_template_bytes(ho.view("tmpl", np.uint32)[: 2 * n], ho.bufs["tmpl_arena"][: int(ho.used[0])], m)
+            res["tmpl_lens"] &= bool(np.array_equal(gl, ol))
+            res["tmpl_bytes_per_span"] &= bool(gb.size == ob.size and np.array_equal(gb, ob))
+        if stages & native.STAGE_SIZE:
+            assert size_process(g.cols, ho.outs, stages, native.GROUP_TRACE_ID, ho.outs, 1, 1.0, 0.0, threads) == 0
+            A = g.cols.n_attrsets
+            ob_ = ho.view("attrset_bytes", np.int64)[:A].copy()
+            gb_ = d.out_numpy("attrset_bytes", np.int64, n=A).copy()
+            node_bytes = ob_ if node_bytes is None else node_bytes + ob_
+            node_bytes_gpu = gb_ if node_bytes_gpu is None else node_bytes_gpu + gb_
+            node_acc += int(ho.view("accepted_spans", np.int64)[0])
+            node_acc_gpu += int(d.out_numpy("accepted_spans", np.int64, n=1)[0])
+    if stages & native.STAGE_SIZE:
+        # the device counters were ADDED to by every timed and warm-up call;
+        # node_counters: what the counter all-reduce left on a rank
+        res["attrset_bytes"] = bool(np.array_equal(calls * node_bytes, node_bytes_gpu))
+        res["accepted_spans"] = bool(calls * node_acc == node_acc_gpu)
+        if node_counters is not None:
+            res["node_allreduce"] = bool(np.array_equal(calls * node_bytes, node_counters[0]) and
+                                         calls * node_acc == node_counters[1])
+    return res

@@ -272,42 +272,8 @@ def _owner_path(sources, cfg):
 
 def _concat_keep_oracle(sources, cfg, threads=16):
     """The oracle on the global batch: the sources concatenated in rank order."""
-    import ctypes as C
-    from odigos_amd.batch import HostOutputs
-    from tests.oracle_lib import SamplingOracle
-    keeps = []
-    # one concatenated column set (resources renumbered per source)
-    cat = {}
-    for f, dt in (("trace_id", np.uint64), ("start_ns", np.uint64), ("end_ns", np.uint64), ("status", np.uint8),
-                  ("route", np.uint32)):
-        cat[f] = np.concatenate([g.array(f).view(dt)[: (g.cols.n_spans * (2 if f in ("trace_id", "route") else 1))]
-                                 for g in sources])
-    roff = np.cumsum([0] + [g.cols.n_resources for g in sources])
-    aoff = np.cumsum([0] + [g.cols.arena_bytes for g in sources])
-    cat["resource"] = np.concatenate([g.array("resource").view(np.uint32)[: g.cols.n_spans] + np.uint32(roff[k])
-                                      for k, g in enumerate(sources)])
-    rt = cat["route"].reshape(-1, 2).copy()
-    base = np.concatenate([np.full(g.cols.n_spans, aoff[k], np.uint64) for k, g in enumerate(sources)])
-    rt[:, 0] = (rt[:, 0].astype(np.uint64) + base * (rt[:, 1] > 0)).astype(np.uint32)
-    cat["route"] = rt.reshape(-1)
-    cat["arena"] = np.concatenate([g.array("arena")[: g.cols.arena_bytes] for g in sources] + [np.zeros(64, np.uint8)])
-    for f in ("res_svc", "res_svc_str"):
-        cat[f] = np.concatenate([g.array(f).view(np.uint32)[: g.cols.n_resources] for g in sources])
-    assert cat["arena"].size < 2**32
-    cols = native.Columns()
-    cols.n_spans = sum(g.cols.n_spans for g in sources)
-    cols.n_resources = int(roff[-1])
-    cols.arena_bytes = int(aoff[-1])
-    for f, a in cat.items():
-        setattr(cols, f, a.ctypes.data)
-    ho = HostOutputs(cols)
-    assert SamplingOracle(cfg).process(cols, ho.outs, native.GROUP_TRACE_ID, SEED, threads) == 0
-    keep = ho.view("keep", np.uint8)[: cols.n_spans]
-    off = 0
-    for g in sources:
-        keeps.append(keep[off: off + g.cols.n_spans].copy())
-        off += g.cols.n_spans
-    return keeps
+    from tests.oracle_lib import concat_keep_oracle
+    return concat_keep_oracle(sources, cfg, SEED, threads)
 
 
 @pytest.mark.gpu
@@ -475,3 +441,39 @@ def test_gpu_exchange_round_local_empty_rank():
     for g, w in zip(got, want):
         np.testing.assert_array_equal(g, w)
     assert stats[2][0] == 0 and stats[2][2] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n_total,one_stream", [(8, 2_400_000, False), (3, 900_000, True)])
+def test_gpu_node_step_full(world, n_total, one_stream):
+    # the whole N-GPU C4 step at world > 1 (tests/node_emul.py, what
+    # bench.py runs per rank): TEMPLATE on the side stream, the exchange
+    # round, SIZE | APPLY_KEEP on the decisions and the counter all-reduce,
+    # two steps; every rank's keep, url_out and template bytes and the node's
+    # counters against the oracle on the concatenated global batch
+    import torch
+    from odigos_amd.batch import Generator
+    from tests.node_emul import LocalNode
+    from tests.oracle_lib import node_parity
+    from tests.workloads import c3_sampling_config
+    keys = ["k8s.namespace.name", "k8s.deployment.name", "service.name"]
+    cfg = {"odigossampling": c3_sampling_config(), "odigosurltemplate": {},
+           "odigostrafficmetrics": {"res_attributes_keys": keys}}
+    gens = [Generator("fused", seed=0x0D1600C0 + world, n_spans=n_total, threads=8, rank=r, world=world)
+            for r in range(world)]
+    for g in gens:
+        g.cols.res_url_ok = None
+    tform = native.STAGE_TEMPLATE_REFS
+    node = LocalNode(cfg, gens, tmpl_form=tform, one_stream=torch.cuda.current_stream() if one_stream else None,
+                     seed=0x5EED)
+    try:
+        for _ in range(2):
+            node.step()
+        torch.cuda.synchronize()
+        stages = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | tform | native.STAGE_SIZE
+        par = node_parity(gens, node.dbs, cfg, stages, 8, 2, node.node_counters())
+        assert all(par.values()), par
+        for d in node.dbs:
+            assert int(d.out_numpy("device_status", np.uint32)[0]) == 0
+    finally:
+        node.close()

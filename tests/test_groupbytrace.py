@@ -330,3 +330,59 @@ def test_gpu_ids_return_across_many_adds():
     total += _check_release(shim, ref, now + 10 * S)
     st = shim.g.stats()
     assert st["released"] == total and st["evicted"] == ref.evicted and st["waiting_traces"] == 0
+
+
+def _mk_starts(ids, starts, svc="svc-a"):
+    return host.traces(host.resource_spans(
+        {"service.name": svc}, [host.span(f"s{st}", kind=2, trace_id=_tid(k), start=st, end=st + 5,
+                                          attributes={"http.request.method": "GET", "url.path": f"/u/{k}"})
+                                for k, st in zip(ids, starts)]))
+
+
+def _released_starts(shim, now):
+    cols, ntr = shim.g.release(now)
+    got = shim.g.download(cols)
+    return ntr, list(got["start_ns"].view(np.uint64)[:cols.n_spans]) if cols.n_spans else []
+
+
+@pytest.mark.gpu
+def test_gpu_expired_id_hand_worked():
+    # Expected output worked out by hand from contrib groupbytrace's timer
+    # semantics, not by tests/gbt_ref.py: trace 1 is past its
+    # 10 s wait at 11 s, so its spans in the 11 s batch start a new trace; new
+    # traces are numbered by first appearance in the batch (2, 1, 3) and go out
+    # in that order, each trace's spans in arrival order.
+    from odigos_amd.batch import Engine
+    shim = _Shim(Engine(CFG), {"wait_duration": "10s"})
+    shim.add(_mk_starts([1], [1]), 0)
+    shim.add(_mk_starts([2, 1, 1, 2, 3, 1], [100, 101, 102, 103, 104, 105]), 11 * S)
+    assert _released_starts(shim, 12 * S) == (1, [1])
+    assert _released_starts(shim, 25 * S) == (3, [100, 103, 101, 102, 105, 104])
+
+
+@pytest.mark.gpu
+def test_gpu_reclaimed_ids_numbered_by_first_appearance():
+    # many spans of ids whose traces were released (tombstoned
+    # slots reclaimed in the add) interleaved with new ids in one batch: the
+    # new traces are numbered, and released, in first-appearance order
+    from odigos_amd.batch import Engine
+    rng = random.Random(0xC1A1)
+    shim = _Shim(Engine(CFG), {"wait_duration": "10s", "num_traces": 1 << 14}, span_capacity=1 << 16,
+                 arena_capacity=1 << 22)
+    now = 0
+    for rnd in range(3):
+        old = list(range(1, 257))
+        shim.add(_mk_starts(old, old), now)
+        assert _released_starts(shim, now + 11 * S)[0] == 256
+        ids = [k for k in old for _ in range(8)] + [1000 + 2000 * rnd + j for j in range(1024)]
+        rng.shuffle(ids)
+        starts = [10_000 + p for p in range(len(ids))]
+        shim.add(_mk_starts(ids, starts), now + 12 * S)
+        order = list(dict.fromkeys(ids))
+        pos = {}
+        for p, k in enumerate(ids):
+            pos.setdefault(k, []).append(starts[p])
+        want = [s for k in order for s in pos[k]]
+        ntr, got = _released_starts(shim, now + 30 * S)
+        assert ntr == len(order) and got == want
+        now += 40 * S

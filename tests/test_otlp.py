@@ -357,11 +357,11 @@ def test_gpu_decode_matches_host_columns(seed, odd, cfg):
 
 
 @pytest.mark.gpu
-def test_gpu_resource_walk_cold_warm_and_host(monkeypatch):
+def test_gpu_resource_walk_cold_warm_and_host():
     # the ResourceSpans level on the GPU (otlp_res_fields_kernel): a cold
     # engine resolves every resource on the host and enters it in the device
     # table, a second decode finds them all there; both equal the host
-    # columniser and the host ResourceSpans walk (OSE_OTLP_HOST_RESOURCES=1)
+    # columniser and the host ResourceSpans walk (engine option otlp_host_resources)
     from odigos_amd.batch import Engine, OtlpBatch
     td = _http_traces(random.Random(31), 300, odd=0.05)
     _, hb = _host_columns(CFG, td)
@@ -371,28 +371,28 @@ def test_gpu_resource_walk_cold_warm_and_host(monkeypatch):
         ob = OtlpBatch(eng, pb)
         _compare(ob.cols, hb.cols, ob.download())
         ob.close()
-    monkeypatch.setenv("OSE_OTLP_HOST_RESOURCES", "1")
+    eng.set_option("otlp_host_resources", 1)
     ob = OtlpBatch(eng, pb)
     _compare(ob.cols, hb.cols, ob.download())
+    eng.set_option("otlp_host_resources", 0)
     # a message of several copies (resources repeated, table hits in one call)
     td3 = {"resourceSpans": td["resourceSpans"] * 3}
     _, hb3 = _host_columns(CFG, td3)
-    monkeypatch.delenv("OSE_OTLP_HOST_RESOURCES")
     ob3 = OtlpBatch(Engine(CFG), to_pb(td3))
     _compare(ob3.cols, hb3.cols, ob3.download())
-    # the TracesData chain walked on the GPU (OSE_OTLP_GPU_CHAIN=1) equals the host's
-    monkeypatch.setenv("OSE_OTLP_GPU_CHAIN", "1")
-    ob4 = OtlpBatch(Engine(CFG), to_pb(td3))
+    # the TracesData chain walked on the GPU (engine option otlp_gpu_chain) equals the host's
+    eng4 = Engine(CFG)
+    eng4.set_option("otlp_gpu_chain", 1)
+    ob4 = OtlpBatch(eng4, to_pb(td3))
     _compare(ob4.cols, hb3.cols, ob4.download())
 
 
 @pytest.mark.gpu
-def test_gpu_chain_walk_records_over_segments(monkeypatch):
+def test_gpu_chain_walk_records_over_segments():
     # ResourceSpans records larger than the GPU chain walk's 64 KiB segments
     # (whole segments inside one record) between small ones, and a message
     # whose bytes end inside a record (malformed: the host walk reports it)
     from odigos_amd.batch import Engine, OtlpBatch
-    monkeypatch.setenv("OSE_OTLP_GPU_CHAIN", "1")
     rng = random.Random(41)
     td = _http_traces(rng, 120)
     rss = td["resourceSpans"]
@@ -403,6 +403,7 @@ def test_gpu_chain_walk_records_over_segments(monkeypatch):
     assert len(pb) > 3 * (64 << 10)
     _, hb = _host_columns(CFG, td2)
     eng = Engine(CFG)
+    eng.set_option("otlp_gpu_chain", 1)
     ob = OtlpBatch(eng, pb)
     _compare(ob.cols, hb.cols, ob.download())
     with pytest.raises(native.OseError) as ei:

@@ -414,11 +414,11 @@ def _routable_gpu(td, rng):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(3))
-def test_gpu_encoder_writes_pdata_inputs(seed, monkeypatch):
+def test_gpu_encoder_writes_pdata_inputs(seed):
     """A batch in pdata's encoding is routed and written by the GPU encoder
     (encode_kernel.hip: no fallback), byte for byte what the restatement
     writes with the GPU's decisions, and what the host encoder writes
-    (OSE_ENCODE_HOST=1) — with and without a router, with SAMPLE|TEMPLATE and
+    (engine option encode_host) — with and without a router, with SAMPLE|TEMPLATE and
     with TEMPLATE alone."""
     import torch
     from odigos_amd.batch import Engine, OtlpBatch
@@ -444,10 +444,10 @@ def test_gpu_encoder_writes_pdata_inputs(seed, monkeypatch):
             got = ob.encode(st, native.GROUP_TRACE_ID, r)
             assert ob.encode_path == {"gpu": True, "fallback": 0}
             assert got == want
-            monkeypatch.setenv("OSE_ENCODE_HOST", "1")
+            eng.set_option("encode_host", 1)
             assert ob.encode(st, native.GROUP_TRACE_ID, r) == want
             assert ob.encode_path["gpu"] is False
-            monkeypatch.delenv("OSE_ENCODE_HOST")
+            eng.set_option("encode_host", 0)
     ob.close()
 
 

@@ -365,12 +365,10 @@ def test_gpu_sample_and_template_one_call(workload, shuffle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shuffle,n", [(False, 300_000), (True, 300_000), (False, 2_000_000), (True, 50_000)])
-def test_gpu_sampling_dup_table(monkeypatch, shuffle, n):
-    # the fast path's duplicate detection through the fingerprint table
-    # (OSE_DUP_BUCKETS=0, read per call; the default buckets checked in LDS
-    # run in every other sampling test): the same decisions as the oracle,
-    # repeated trace ids (shuffled resources) found
-    monkeypatch.setenv("OSE_DUP_BUCKETS", "0")
+def test_gpu_sampling_dup_detection(shuffle, n):
+    # the fast path's duplicate detection (fingerprint buckets checked in
+    # LDS) at several sizes: the same decisions as the oracle, repeated trace
+    # ids (shuffled resources) found
     gpu_vs_oracle(Generator("sampling", seed=0x0D1600F0 + n, n_spans=n, shuffle=shuffle))
 
 

@@ -1,0 +1,258 @@
+"""ASan + UBSan over the host code that parses untrusted input.
+
+tests/fuzz/host_fuzz.cpp is built with -fsanitize=address,undefined
+-fno-sanitize-recover=all over the product's host sources (odigos_amd/build.py
+SAN_SOURCES: the OTLP protobuf unmarshaler and walk, the OTLP/JSON parser, the
+proto sizer and marshaler, the regex and Unicode compiler, the jsonpath and
+ParseFloat code of span_attribute, the config decoders, net/url.Parse) and fed:
+- serialized TracesData (google.protobuf encoder) truncated at every offset of
+  small messages and at random offsets of large ones, bit-flipped, overwritten
+  with random bytes, and with length prefixes inflated or deflated;
+- OTLP/JSON truncated and mutated;
+- random regexps, URLs, float strings, processor configs and span_attribute
+  json rules with random jsonpaths.
+Any sanitizer report aborts the harness (the test fails on its exit status
+and on the report in stderr).  Every message the unmarshaler cannot read must
+be rejected with a status, as pdata's UnmarshalTraces rejects it: truncations
+are accepted exactly when google.protobuf accepts them, inflated lengths that
+run past their enclosing message are always rejected.
+"""
+from __future__ import annotations
+
+import json
+import random
+import subprocess
+
+import pytest
+
+from tests.test_otlp import CFG, _http_traces, to_pb
+from tests.test_size import _otlp_classes, _rand_traces
+
+
+@pytest.fixture(scope="module")
+def harness():
+    from odigos_amd.build import build_sanitized
+    try:
+        return str(build_sanitized())
+    except RuntimeError as ex:   # pragma: no cover - the image has g++ with ASan
+        pytest.skip(f"sanitizer build unavailable: {ex}")
+
+
+def _run(harness, mode, files):
+    r = subprocess.run([harness, mode, *map(str, files)], capture_output=True, text=True, timeout=600,
+                       env={"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:halt_on_error=1",
+                            "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1", "PATH": "/usr/bin:/bin"})
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0, (r.returncode, r.stderr[-4000:])
+    return r.stdout.splitlines()
+
+
+def _google_accepts(b: bytes) -> bool:
+    """google.protobuf's verdict on a TracesData (repeated ResourceSpans
+    resource_spans = 1): the top-level fields must frame, and every field-1
+    payload must parse as a ResourceSpans."""
+    rs_cls = _otlp_classes()["ResourceSpans"]
+    i = 0
+    try:
+        while i < len(b):
+            t, i = _read_varint(b, i)
+            wt = t & 7
+            if t >> 3 == 0:
+                return False
+            if wt == 0:
+                _, i = _read_varint(b, i)
+            elif wt == 1:
+                i += 8
+            elif wt == 5:
+                i += 4
+            elif wt == 2:
+                ln, i = _read_varint(b, i)
+                if i + ln > len(b):
+                    return False
+                if t >> 3 == 1:
+                    rs_cls().ParseFromString(b[i:i + ln])
+                i += ln
+            else:
+                return False
+            if i > len(b):
+                return False
+        return True
+    except Exception:
+        return False
+
+
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _read_varint(b: bytes, i: int):
+    v, s = 0, 0
+    while True:
+        c = b[i]
+        i += 1
+        v |= (c & 0x7F) << s
+        s += 7
+        if c < 0x80:
+            return v, i
+
+
+# message fields of the OTLP schema the walk descends into: TracesData.1 ->
+# ResourceSpans, ResourceSpans.2 -> ScopeSpans, ScopeSpans.2 -> Span
+_SCHEMA = {"TracesData": {1: "ResourceSpans"}, "ResourceSpans": {2: "ScopeSpans"}, "ScopeSpans": {2: "Span"}}
+
+
+def _len_fields(b: bytes, lo: int, hi: int, msg: str = "TracesData", out=None):
+    """The length prefixes of the TracesData / ResourceSpans / ScopeSpans /
+    Span messages of a well-formed message [lo, hi): (varint start, varint
+    end, payload length, enclosing end)."""
+    out = [] if out is None else out
+    i = lo
+    while i < hi:
+        t, i = _read_varint(b, i)
+        wt = t & 7
+        if wt == 0:
+            _, i = _read_varint(b, i)
+        elif wt == 1:
+            i += 8
+        elif wt == 5:
+            i += 4
+        elif wt == 2:
+            v0 = i
+            ln, i = _read_varint(b, i)
+            sub = _SCHEMA.get(msg, {}).get(t >> 3)
+            if sub:
+                out.append((v0, i, ln, hi))
+                _len_fields(b, i, i + ln, sub, out)
+            i += ln
+        else:
+            raise AssertionError("group wire type in a generated message")
+    return out
+
+
+def _messages():
+    rng = random.Random(0x5A11)
+    msgs = [to_pb(_http_traces(rng, 6, odd=0.2)), to_pb(_rand_traces(rng, n_res=2))]
+    msgs += [to_pb(_http_traces(rng, 60, odd=0.1)), to_pb(_rand_traces(rng, n_res=8))]
+    return msgs
+
+
+def test_protobuf_corruptions_rejected_cleanly(harness, tmp_path):
+    rng = random.Random(0xB17F)
+    msgs = _messages()
+    cases = []   # (bytes, kind)
+    for k, m in enumerate(msgs):
+        cases.append((m, "valid"))
+        cuts = range(len(m)) if len(m) <= 1500 else sorted(rng.sample(range(len(m)), 300))
+        cases += [(m[:c], "trunc") for c in cuts]
+        for _ in range(150):   # single-bit flips
+            p = rng.randrange(len(m))
+            cases.append((m[:p] + bytes([m[p] ^ (1 << rng.randrange(8))]) + m[p + 1:], "flip"))
+        for _ in range(60):    # overwritten runs of random bytes
+            p = rng.randrange(len(m))
+            n = rng.randrange(1, 16)
+            cases.append((m[:p] + bytes(rng.randrange(256) for _ in range(n)) + m[p + n:], "noise"))
+        fields = _len_fields(m, 0, len(m))
+        for v0, v1, ln, end in rng.sample(fields, min(len(fields), 120)):
+            payload_end = v1 + ln
+            for delta in (1, 7, 1000, 1 << 31, (1 << 63) - ln):
+                cases.append((m[:v0] + _varint(ln + delta) + m[v1:],
+                              "inflate" if payload_end + delta > end or delta >= (1 << 31) else "inflate-inside"))
+            if ln:
+                cases.append((m[:v0] + _varint(ln - 1) + m[v1:], "deflate"))
+    cases += [(bytes(rng.randrange(256) for _ in range(rng.randrange(1, 200))), "random") for _ in range(200)]
+    cases += [(b"\x0a" + _varint(1 << 62), "huge"), (b"\x0a\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\x01", "overflow"),
+              (b"\x0a\x80", "eof-varint"), (b"", "empty")]
+    files = []
+    for i, (b, _) in enumerate(cases):
+        f = tmp_path / f"m{i:05d}.pb"
+        f.write_bytes(b)
+        files.append(f)
+    out = {}
+    for s in range(0, len(files), 2000):
+        for line in _run(harness, "pb", files[s:s + 2000]):
+            name, status = line.split()[:2]
+            out[name] = status
+    assert len(out) == len(cases)
+    for f, (b, kind) in zip(files, cases):
+        st = out[str(f)]
+        if kind in ("valid", "empty"):
+            assert st == "ok", (kind, f)
+        elif kind in ("inflate", "huge", "overflow", "eof-varint"):
+            assert st == "rejected", (kind, f)
+        elif kind == "trunc":
+            assert (st == "ok") == _google_accepts(b), (kind, f, st)
+
+
+def test_json_corruptions(harness, tmp_path):
+    from odigos_amd import host
+    rng = random.Random(0x150B)
+    texts = [json.dumps(_http_traces(rng, 5, odd=0.3)), json.dumps(_rand_traces(rng, n_res=2))]
+    cases = list(texts)
+    for t in texts:
+        cases += [t[:c] for c in sorted(rng.sample(range(len(t)), 200))]
+        alphabet = '{}[]":,0123456789-eE.tfnul\\ xé'
+        for _ in range(300):
+            p = rng.randrange(len(t))
+            cases.append(t[:p] + rng.choice(alphabet) + t[p + 1:])
+        cases.append('{"resourceSpans": [' * 4000)   # deep nesting
+    files = []
+    for i, t in enumerate(cases):
+        f = tmp_path / f"j{i:05d}.json"
+        f.write_text(t, encoding="utf-8", errors="surrogateescape")
+        files.append(f)
+    lines = _run(harness, "json", files)
+    assert len(lines) == len(cases)
+    assert all(line.split()[1] == "ok" for line in lines[:len(texts)])
+    del host
+
+
+def _rand_regex(rng):
+    toks = ["a", "b", "\\d", "\\w", "\\s", ".", "*", "+", "?", "|", "(", ")", "(?:", "[", "]", "[^a-z]", "{2,5}",
+            "{3}", "{,}", "^", "$", "\\b", "\\p{Greek}", "\\pL", "\\P{Lu}", "\\Q.*\\E", "(?i)", "(?s)", "\\x{FFFD}",
+            "\\", "[[:alpha:]]", "(?P<n>", "é", "\\z", "\\A", "{", "}", "-", "/", "\\/"]
+    return "".join(rng.choice(toks) for _ in range(rng.randrange(1, 14)))
+
+
+def _rand_path(rng):
+    toks = ["$", ".", "..", "[", "]", "*", "'k'", '"k"', "a", "b", "0", "1", "-1", ":", ",", "?(", "@", ")", "(", "2:",
+            "::", "[*]", "['a','b']", "[0:2:1]", "[::-1]"]
+    return "".join(rng.choice(toks) for _ in range(rng.randrange(1, 9)))
+
+
+def test_text_parsers(harness, tmp_path):
+    rng = random.Random(0x7E57)
+    lines = []
+    for _ in range(600):
+        lines.append("regex\t" + _rand_regex(rng))
+    for _ in range(400):
+        s = "".join(rng.choice("/%:?#[]@ab09.-+~!$&'()*,;=xXé ") for _ in range(rng.randrange(0, 40)))
+        lines.append("url\t" + rng.choice(["", "http://", "https://h:80", "//", "mailto:"]) + s)
+    for _ in range(400):
+        lines.append("float\t" + "".join(rng.choice("0123456789._eEpPxX+-infINFnaNtrue") for _ in
+                                          range(rng.randrange(0, 24))))
+    base = json.dumps(CFG)
+    for _ in range(300):
+        p = rng.randrange(len(base))
+        lines.append("config\t" + base[:p] + rng.choice('{}[]":,0-9x') + base[p + 1:])
+    for _ in range(500):
+        rule = {"name": "r", "type": "span_attribute",
+                "rule_details": {"service_name": "svc", "attribute_key": "k", "condition_type": "json",
+                                 "operation": rng.choice(["is_valid_json", "is_invalid_json", "jsonpath_exists",
+                                                          "key_equals", "key_not_equals"]),
+                                 "json_path": _rand_path(rng), "expected_value": rng.choice(["1", "\"a\"", "x", ""]),
+                                 "sampling_ratio": 50, "fallback_sampling_ratio": 10}}
+        value = rng.choice(['{"a": [1, 2, {"b": null}], "k": "v"}', "[1,2,3]", '{"a":', "7", '"s"',
+                            '{"a": {"a": {"a": 1}}}', "[" * 300, '{"\\u00e9": 1.5e3}'])
+        lines.append("attr\t" + json.dumps(rule) + "\x1f" + value)
+    f = tmp_path / "lines.txt"
+    f.write_text("\n".join(line.replace("\n", " ") for line in lines) + "\n", encoding="utf-8")
+    out = _run(harness, "lines", [f])
+    assert len(out) == len(lines)

@@ -1,6 +1,8 @@
 """Ablation timings of trace_eval_kernel on the C3 batch (diagnostic).
 Each variant sets OSE_TRACE_ABLATE (read per call by sampling_host.cpp)."""
 import os, sys
+import os
+os.environ.setdefault("OSE_LIB_VARIANT", "_diag")   # the diagnostics build (OSE_DIAG=1) reads the ablation switches
 from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import torch

@@ -1,5 +1,7 @@
 """Ablation timings of the URL kernels on synthetic C2 batches (diagnostic)."""
 import sys, time
+import os
+os.environ.setdefault("OSE_LIB_VARIANT", "_diag")   # the diagnostics build (OSE_DIAG=1) reads the ablation switches
 from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import numpy as np

@@ -1,0 +1,7 @@
+#!/bin/bash
+# correctness pass + bench lines + the FOLD_ENDS A/B (owner, zipf)
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+bash tools/gpu_check.sh r4b fused node8 || exit 1
+bash tools/gpu_ab.sh r4b_fe _fe owner zipf

@@ -2,6 +2,7 @@
 # LDS bank conflicts of url_plan_kernel (diagnostic instance) with and without
 # the assembly's byte stores (OSE_URL_ABLATE 64) and the bitmap build (4)
 R=$GRAFT_REPO_ROOT
+export OSE_LIB_VARIANT=_diag   # build it first: python -m odigos_amd.build --variant _diag OSE_DIAG=1
 mkdir -p $R/gpurun_out/ldsc
 cd /tmp && export TMPDIR=/tmp
 for ab in 4096 64 4; do

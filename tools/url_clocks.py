@@ -1,6 +1,8 @@
 """Per-section shader-clock breakdown of the URL kernels (diagnostic;
 OSE_URL_ABLATE bit 512 makes the engine print the per-wave sums)."""
 import os, sys
+import os
+os.environ.setdefault("OSE_LIB_VARIANT", "_diag")   # the diagnostics build (OSE_DIAG=1) reads the ablation switches
 from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import torch
