@@ -63,7 +63,7 @@ def build_product(force: bool = False, jobs: int = 8, variant: str = "", defines
     objdir = OBJDIR / ("variant" + variant) if variant else OBJDIR
     objdir.mkdir(parents=True, exist_ok=True)
     out = LIBDIR / f"libodigos_amd{variant}.so"
-    flags = HIP_FLAGS + [f"-D{d}" for d in defines]
+    flags = HIP_FLAGS + [d if d.startswith("-") else f"-D{d}" for d in defines]   # -flags pass through
     headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "odigos_amd.h"]
     hdr_t = _deps_mtime(headers)
     cmds, objs = [], []

@@ -219,6 +219,7 @@ struct TraceKernelArgs {
   uint32_t* long_runs;        // [n_spans / 64 + 1]
   uint32_t long_steps;        // hand-off distance in 64-span steps (kLongSteps)
   uint32_t win_per_wave;      // 64-span windows whose run heads one wave owns (kWinPerWave)
+  uint32_t narrow;            // the table's flag bits fit one word (trace_eval_kernel kNarrow)
   // run-list path (repeated trace ids, before the sort-based fallback):
   // trace_runs_kernel lists each trace's runs in its exact-table slot,
   // trace_fold_kernel folds the runs of every trace with 2..kMaxRuns runs

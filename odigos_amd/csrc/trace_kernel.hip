@@ -123,6 +123,40 @@ __device__ __forceinline__ void seg_or2_scan(uint32_t h, uint64_t& x, uint64_t& 
   seg_or2_step<0x143, 0xC>(h, x, y);
 }
 
+// one 32-bit word (kNarrow: the error bit, endpoint bits and service bits packed)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_or1_step(uint32_t& h, uint32_t& x) {
+  const uint32_t oh = dpp_mov<CTRL, ROWS>(0u, h), ox = dpp_mov<CTRL, ROWS>(0u, x);
+  if (!h) x |= ox;
+  h |= oh;
+}
+__device__ __forceinline__ void seg_or1_scan(uint32_t h, uint32_t& x) {
+  seg_or1_step<0x111, 0xF>(h, x);
+  seg_or1_step<0x112, 0xF>(h, x);
+  seg_or1_step<0x114, 0xF>(h, x);
+  seg_or1_step<0x118, 0xF>(h, x);
+  seg_or1_step<0x142, 0xA>(h, x);
+  seg_or1_step<0x143, 0xC>(h, x);
+}
+// two 32-bit words (kNarrow: the latency rules and latency slots fit 32 bits)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_or2n_step(uint32_t& h, uint32_t& x, uint32_t& y) {
+  const uint32_t oh = dpp_mov<CTRL, ROWS>(0u, h), ox = dpp_mov<CTRL, ROWS>(0u, x), oy = dpp_mov<CTRL, ROWS>(0u, y);
+  if (!h) {
+    x |= ox;
+    y |= oy;
+  }
+  h |= oh;
+}
+__device__ __forceinline__ void seg_or2n_scan(uint32_t h, uint32_t& x, uint32_t& y) {
+  seg_or2n_step<0x111, 0xF>(h, x, y);
+  seg_or2n_step<0x112, 0xF>(h, x, y);
+  seg_or2n_step<0x114, 0xF>(h, x, y);
+  seg_or2n_step<0x118, 0xF>(h, x, y);
+  seg_or2n_step<0x142, 0xA>(h, x, y);
+  seg_or2n_step<0x143, 0xC>(h, x, y);
+}
+
 // OR over the wave, broadcast: DPP row_shr within each 16-lane row, then the
 // four row results read out (no ds_bpermute round trips)
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
@@ -638,7 +672,11 @@ __device__ void flush_queue(const TraceKernelArgs& a, const Cfg& c, DecideQ& Q, 
 // bits, no diagnostics.  Those arguments are constants in it, so their code
 // and the kernel-argument registers that hold them fold away (the general
 // instance spills ~90 scalar registers into vector lanes).
-template <bool kLean>
+// kNarrow (with kLean): the error bit, the endpoint bits of the latency rules
+// and the service-rule bits fit one 32-bit word (1 + n_lat + service bits <=
+// 32, n_lat_slots <= 32; the host checks): the segmented ORs scan one word
+// instead of five, the latency stretches' words two instead of four.
+template <bool kLean, bool kNarrow>
 __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void trace_eval_kernel(TraceKernelArgs a) {
   if (kLean) {
     a.mode = kTraceRuns;
@@ -828,7 +866,16 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     // per-slot carry registers in lane order.
     const uint32_t hseg = mine ? (uint32_t)((segmask >> lane) & 1) : 1u;
     // ---- segmented OR of the flag masks (DPP scan; h = segment head) ----
-    seg_or_scan(hseg, err, ep, svcb);
+    if constexpr (kNarrow) {
+      const uint32_t nsh = 1 + c.h->n_lat;   // <= 32 (host-checked)
+      uint32_t pk = err | ((uint32_t)ep << 1) | (nsh < 32 ? (uint32_t)svcb << nsh : 0u);
+      seg_or1_scan(hseg, pk);
+      err = pk & 1u;
+      ep = (pk >> 1) & (uint32_t)((1ull << c.h->n_lat) - 1);
+      svcb = nsh < 32 ? pk >> nsh : 0u;
+    } else {
+      seg_or_scan(hseg, err, ep, svcb);
+    }
     uint64_t lsat = 0, n_kmask = 0;
     Lat nxt{0, kInf, 0};
     const bool carried_tail = (lane == t0 && seg0_cont) || (lane == last_own && last_open);
@@ -865,7 +912,14 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
       }
     }
     if (lat_on) {
-      seg_or2_scan(hseg, lraw, smask);
+      if constexpr (kNarrow) {
+        uint32_t lr = (uint32_t)lraw, sm = (uint32_t)smask;
+        seg_or2n_scan(hseg, lr, sm);
+        lraw = lr;
+        smask = sm;
+      } else {
+        seg_or2_scan(hseg, lraw, smask);
+      }
       // a slot with two stretches in a trace this step closes: per-slot scans
       const uint64_t psm = dpp64<0x138, 0xF>(0ull, smask);   // lane - 1's inclusive slot bits
       const bool in_closed = mine && !(seg0_cont && lane <= t0) && !(last_open && lane >= sst_last);
@@ -1720,10 +1774,14 @@ void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, u
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t per_block = kTWaves * a.win_per_wave;
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
-  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate && !a.fold_in && !a.fold_out)
-    hipLaunchKernelGGL(trace_eval_kernel<true>, dim3(blocks), dim3(kTThreads), 0, st, a);
-  else
-    hipLaunchKernelGGL(trace_eval_kernel<false>, dim3(blocks), dim3(kTThreads), 0, st, a);
+  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate && !a.fold_in && !a.fold_out) {
+    if (a.narrow)
+      hipLaunchKernelGGL((trace_eval_kernel<true, true>), dim3(blocks), dim3(kTThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((trace_eval_kernel<true, false>), dim3(blocks), dim3(kTThreads), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((trace_eval_kernel<false, false>), dim3(blocks), dim3(kTThreads), 0, st, a);
+  }
 }
 // One workgroup per fingerprint bucket: its entries into an LDS hash set; an
 // entry met twice (or a bucket past its capacity) sets *dup

@@ -1621,11 +1621,28 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     bool fast = fused_cfg && listed && __ballot(p.mode == M_RULE || big) == 0 && sum <= kImgCap;
     if (fast && scr_used + need > scr_end) {
       if (a.refs && !exhausted) {   // a new chunk (the rest of the current one is left unused)
-        const uint64_t csz = max(a.refs_chunk, need);
-        uint64_t at = 0;
-        if (lane == 0) at = atomicAdd((unsigned long long*)a.bump, (unsigned long long)csz);
+        // the bump moves only by space that fits the arena: a full chunk, else
+        // exactly this image, else nothing (the chunks the waves hold never
+        // pass out_cap, so *used overstates nothing and a batch the packed
+        // form fits is not refused for a chunk's unused tail)
+        uint64_t csz = max(a.refs_chunk, need), at = ~0ull;
+        if (lane == 0) {
+          unsigned long long cur = __hip_atomic_load((unsigned long long*)a.bump, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+          for (;;) {
+            const uint64_t take = cur + csz <= a.out_cap ? csz : cur + need <= a.out_cap ? need : 0;
+            if (!take) break;
+            if (__hip_atomic_compare_exchange_strong((unsigned long long*)a.bump, &cur, cur + take, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+              at = cur;
+              csz = take;
+              break;
+            }
+          }
+        }
         at = (uint64_t)lane_value((uint32_t)at, 0) | ((uint64_t)lane_value((uint32_t)(at >> 32), 0) << 32);
-        if (at + csz <= a.out_cap) {
+        csz = (uint64_t)lane_value((uint32_t)csz, 0) | ((uint64_t)lane_value((uint32_t)(csz >> 32), 0) << 32);
+        if (at != ~0ull) {
           region = at;
           scr_used = 0;
           scr_end = csz;

@@ -19,6 +19,6 @@ tail -1 $OUT/smoke.log
 for wl in "$@"; do
   timeout -k 10 600 python -u bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_$wl.log 2>&1 || { tail -30 $OUT/bench_$wl.log; exit 1; }
   echo "$wl $(grep -o '"ms_per_step": [0-9.]*\|"frac": [0-9.]*\|"parity_vs_oracle": [a-z]*\|"projected_ms_per_gpu_step": [0-9.]*' $OUT/bench_$wl.log | tr '\n' ' ')"
-  grep -o '"parity": {[^}]*}' $OUT/bench_$wl.log
-  grep -o '"kernel_ms_each": {[^}]*}' $OUT/bench_$wl.log
+  grep -o '"parity": {[^}]*}' $OUT/bench_$wl.log || true
+  grep -o '"kernel_ms_each": {[^}]*}' $OUT/bench_$wl.log || true
 done
