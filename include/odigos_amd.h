@@ -100,13 +100,16 @@ extern "C" {
  * the GPU assembled them (64-span groups, in the order the GPU finished
  * them) instead of being packed in span order.  tmpl[i] still refers into
  * tmpl_arena and its bytes are exactly the packed form's, but the arena has
- * gaps: up to 15 bytes after each group and, per assembling wave, the unused
- * tail of its last space chunk (at most tmpl_arena_cap / 8 in all);
- * *tmpl_arena_used is the end of the highest range written.  It saves a
- * read and a write of every template byte when the consumer follows the
- * refs on the device instead of copying the arena to the host.  Overflow
- * (device_status bit 2, *tmpl_arena_used = the bytes needed) as in the
- * packed form.                                                              */
+ * gaps: up to 15 bytes after each group, per assembling wave the unused
+ * tail of its last space chunk (at most tmpl_arena_cap / 8 in all), and
+ * chunk tails a wave left for a group image that did not fit (at most 1/7 of
+ * the bytes used); *tmpl_arena_used is the end of the highest range
+ * written.  It saves a read and a write of every template byte when the
+ * consumer follows the refs on the device instead of copying the arena to
+ * the host.  Overflow: device_status bit 2 and *tmpl_arena_used = an arena
+ * size a retry of the same batch fits (the templates as 16-byte aligned
+ * images, plus a third for chunk tails, plus 16 bytes per assembling wave),
+ * so a shim that retries with that capacity succeeds, as in the packed form. */
 #define OSE_STAGE_TEMPLATE_REFS 0x10u
 /* url_out and tmpl already hold the templating results (written by an
  * earlier call on the same batch, e.g. TEMPLATE on a second stream while the
@@ -210,7 +213,9 @@ typedef struct ose_columns {
    *              the low half); INT: the int64; DOUBLE: the float64 bits;
    *              BOOL: 0 / 1; other types: 0                               */
   uint32_t n_attr_keys;
-  uint32_t _pad2;
+  uint32_t match_planes;   /* route_match / svc_match hold this many planes of n_spans words,
+                              plane k for rule chunk k (K = (ose_shard_record_bytes - 40) / 16; what
+                              ose_shard_unpack writes); 0 or 1: one plane                 */
   const uint8_t* attr_type;
   const uint64_t* attr_val;
 } ose_columns;
@@ -377,25 +382,27 @@ int ose_profile_read(ose_engine* eng, char* json, size_t cap);
  * the records in (source rank, source order), i.e. in global batch order,
  * so decisions equal the single-GPU ones.
  *
- * Record (OSE_XREC_BYTES = 56): u64 trace_id hi, lo, min start (~0 = none),
- * max end, endpoint bits, rule bits, then u64 {latency service id : 24
+ * Record (ose_shard_record_bytes = 40 + 16 per rule chunk): u64 trace_id
+ * hi, lo, min start (~0 = none), max end, {latency service id : 24
  * (0xFFFFFF = none) | flags : 8 (1 error, 2 latency element present, 4 a
- * zero start came first)}.  A sampling config that needs more than one
- * rule chunk (ose_engine_create) is OSE_ENOTSUP here: a record carries one
- * endpoint word and one rule-bit word.
+ * zero start came first)}, then per rule chunk (K of them:
+ * a rule list beyond one GPU table) the endpoint bits and the rule bits
+ * under that chunk's tables.  A record's stretch has one latency service
+ * (a service with an http_latency rule in any chunk).
  *
  * ose_shard_pack writes the records into per-owner buckets of `send`
  * (stable: source order inside a bucket), counts[n_ranks] (records per
  * owner) and pack_pos[n_spans] (the slot of each span's record);
  * ose_shard_unpack turns received records into owner-side columns for
  * ose_process_device(SAMPLE, OSE_GROUP_TRACE_ID): one span and one
- * resource per record, svc_match set, status bit 7 marking a record whose
+ * resource per record, svc_match set (route_match and svc_match: one
+ * plane of n words per rule chunk, cols.match_planes), status bit 7 marking a record whose
  * zero start came first; the keep bytes go back with the reverse split and
  * ose_shard_scatter_keep puts them on the original spans.  All pointers
  * are device pointers; calls are asynchronous on hip_stream.
  * ose_exchange_sample runs the whole round over an RCCL communicator.      */
-#define OSE_XREC_BYTES 56u
-uint32_t ose_shard_record_bytes(const ose_engine* eng);   /* OSE_XREC_BYTES, 0 without odigossampling */
+#define OSE_XREC_BYTES 56u   /* a config of one rule chunk; 40 + 16 per chunk */
+uint32_t ose_shard_record_bytes(const ose_engine* eng);   /* 40 + 16 * rule chunks, 0 without odigossampling */
 uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks);
 int ose_shard_pack(ose_engine* eng, const ose_columns* cols, uint32_t n_ranks, void* send,
                    uint64_t* counts, uint32_t* pack_pos, void* hip_stream);

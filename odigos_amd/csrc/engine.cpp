@@ -155,6 +155,7 @@ Engine::~Engine() {
   if (url_blob_dev) (void)hipFree(url_blob_dev);
   for (auto* d : sampling_chunks_dev)
     if (d) (void)hipFree(d);   // (sampling_blob_dev is the first)
+  if (shard_tables_dev) (void)hipFree(shard_tables_dev);
   if (attr_blob_dev) (void)hipFree(attr_blob_dev);
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
@@ -348,11 +349,12 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   if (o->tmpl_arena_cap > 0xFFFFFFFFull) return fail(OSE_ERANGE, "tmpl_arena_cap exceeds the 32-bit offset range");
   uint64_t n = c->n_spans;
   const uint32_t groups = (uint32_t)((n + kUrlGroup - 1) / kUrlGroup);
-  // workspace: [0,16) scan counter, slow count, error, unplanned count | [16,24) refs bump | scan status 8t
+  // workspace: [0,16) scan counter, slow count, error, unplanned count | [16,24) refs bump | [24,32) refs
+  // slow groups aligned | scan status 8t
   // (all zeroed by one memset) | plan_len 4n | plan_meta 4n | plan_code 8n | group_sum 8g | group_base 8g | group_scr 8g |
   // slow groups 4g | unplanned groups 4g | dbg | scratch (the assembled group images)
   const uint32_t scan_tiles = (groups + kUrlScanTile - 1) / kUrlScanTile;
-  const size_t off_bump = 16, off_sst = 24, zero_bytes = off_sst + 8 * (size_t)scan_tiles;
+  const size_t off_bump = 16, off_asum = 24, off_sst = 32, zero_bytes = off_sst + 8 * (size_t)scan_tiles;
   const size_t off_len = align_up(zero_bytes, 256), off_meta = off_len + 4 * n;
   const size_t off_code = align_up(off_meta + 4 * n, 8);
   const size_t off_gsum = off_code + 8 * n, off_gbase = off_gsum + 8 * (size_t)groups;
@@ -394,6 +396,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
     a.refs = 1;
     a.scratch = o->tmpl_arena;
     a.bump = reinterpret_cast<uint64_t*>(base + off_bump);
+    a.slow_aligned = reinterpret_cast<uint64_t*>(base + off_asum);
   }
   a.n_scan_tiles = scan_tiles;
   a.scan_counter = reinterpret_cast<uint32_t*>(base);
@@ -411,8 +414,9 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   a.scr_region = (scr_bytes / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
   // refs: image chunks of an eighth of the arena over the plan waves (at most
   // 256 KiB; a group larger than a chunk takes exactly its size): a wave
-  // leaves at most one chunk's tail unused
-  a.refs_chunk = std::min<uint64_t>(256 << 10, o->tmpl_arena_cap / 8 / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
+  // leaves at most one chunk's tail unused (url_refs_chunk)
+  a.plan_waves = url_plan_waves(a);
+  a.refs_chunk = url_refs_chunk(o->tmpl_arena_cap, a.plan_waves);
   if (front) *front = a;
   if (n == 0) {
     if (o->tmpl_arena_used) HIP_TRY(hipMemsetAsync(o->tmpl_arena_used, 0, 8, st));
@@ -646,6 +650,12 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
       if (rc) { delete e; return rc; }
     }
     e->sampling_blob_dev = e->sampling_chunks_dev[0];
+    const size_t K = e->sampling_chunks_dev.size(), L = e->sampling_lat_svc.size();
+    std::vector<uint8_t> st(8 * K + 4 * L);
+    std::memcpy(st.data(), e->sampling_chunks_dev.data(), 8 * K);
+    std::memcpy(st.data() + 8 * K, e->sampling_lat_svc.data(), 4 * L);
+    rc = upload(st, &e->shard_tables_dev);
+    if (rc) { delete e; return rc; }
   }
   if (!e->attr_blob_host.empty()) {
     rc = upload(e->attr_blob_host, &e->attr_blob_dev);

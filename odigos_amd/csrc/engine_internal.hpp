@@ -118,6 +118,11 @@ struct Engine {
   std::vector<std::vector<uint8_t>> sampling_chunks_host;
   std::vector<uint8_t*> sampling_chunks_dev;
   std::vector<uint8_t> sampling_chunk_attr;   // chunk has span_attribute rules
+  // trace-id exchange tables (shard_host.cpp): bit s of sampling_lat_svc =
+  // service s has an http_latency rule in some chunk; on the device, the K
+  // chunk table pointers then those words (ShardArgs::cfgs, ::lat_svc)
+  std::vector<uint32_t> sampling_lat_svc;
+  uint8_t* shard_tables_dev = nullptr;
   std::unordered_map<std::string, uint32_t> service_ids;
   uint32_t sampling_n_lat = 0, sampling_n_attr = 0;
   // span_attribute rules: all of them (attr_n_rules), the GPU-evaluated ones

@@ -102,7 +102,9 @@ struct UrlKernelArgs {
   // launch); the scan places the slow groups from the final *bump on.
   uint32_t refs;
   uint64_t* bump;
-  uint64_t refs_chunk;
+  uint64_t refs_chunk;          // url_refs_chunk()
+  uint32_t plan_waves;          // url_plan_waves()
+  uint64_t* slow_aligned;       // refs: sum of the scan-placed groups' sizes rounded up to 16 (zeroed)
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
   uint64_t* dbg;               // diagnostics only (ablate & 512): per-section clock sums
   // odigostrafficmetrics' spans pass fused into url_copy_kernel (TEMPLATE and
@@ -136,6 +138,9 @@ inline size_t url_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
 }
 void launch_url_plan(const UrlKernelArgs& a, hipStream_t st);
 uint32_t url_plan_waves(const UrlKernelArgs& a);   // waves of the plan grid (scratch regions)
+// refs form: the image chunk size for an arena of `cap` bytes over `waves`
+// plan waves (0: every group image takes exactly its size)
+uint64_t url_refs_chunk(uint64_t cap, uint32_t waves);
 void launch_url_scan(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_copy(const UrlKernelArgs& a, hipStream_t st);
 void launch_url_plan_slow(const UrlKernelArgs& a, hipStream_t st);
@@ -314,22 +319,32 @@ struct ShardArgs {
   const ose_strref* route;
   const uint8_t* arena;
   const uint64_t* route_match;
+  uint64_t rm_stride;         // route_match: plane k (rule chunk k) at k * rm_stride (0: one plane)
   const uint64_t* attr_match;
   const uint32_t* res_svc;
   const uint32_t* res_svc_str;
-  const uint8_t* cfg;         // SampCfgDev blob
+  const uint8_t* const* cfgs;  // [n_chunks] SampCfgDev blobs (device array of the rule chunks' tables)
+  uint32_t n_chunks;
+  const uint32_t* lat_svc;    // bit s: service s has an http_latency rule in some chunk
   uint32_t* hist;             // [n_ranks * n_tiles] counts, then offsets (second buffer)
   uint32_t* hoff;
   uint64_t* counts;           // [n_ranks] zeroed before launch
-  uint8_t* send;              // [records * kXRecBytes], records <= n
+  uint8_t* send;              // [records * x_rec_bytes(n_chunks)], records <= n
   uint32_t* pack_pos;         // [n] slot of each span's record
 };
-constexpr uint32_t kXRecBytes = 56;   // partial record (trace_kernel.hip "trace-id exchange")
+// Partial record (trace_kernel.hip "trace-id exchange"): u64 words hi, lo,
+// min start, max end, {latency service 24 | flags 8}, then per rule chunk
+// the endpoint bits and the rule bits of that chunk's tables.
+constexpr uint32_t kXFixedWords = 5;
+constexpr uint32_t kXRecBytes = 8 * (kXFixedWords + 2);   // a one-chunk config (OSE_XREC_BYTES)
+constexpr uint32_t x_rec_words(uint32_t n_chunks) { return kXFixedWords + 2 * n_chunks; }
+constexpr uint32_t x_rec_bytes(uint32_t n_chunks) { return 8 * x_rec_words(n_chunks); }
 void launch_shard_hist(const ShardArgs& a, hipStream_t st);
 void launch_shard_scatter(const ShardArgs& a, hipStream_t st);
 struct UnpackArgs {
   const uint8_t* recv;
   uint64_t n;
+  uint32_t n_chunks;          // route_match / svc_match: n_chunks planes of n words
   uint64_t* tid;
   uint64_t* start;
   uint64_t* end;

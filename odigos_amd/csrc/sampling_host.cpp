@@ -190,6 +190,12 @@ int Engine::build_sampling_tables() {
     }
   if (n_attr > 64)
     return fail(OSE_ENOTSUP, "more than 64 span_attribute rules are not supported (one 64-bit attr_match word per span)");
+  sampling_lat_svc.assign(std::max<size_t>(1, (service_ids.size() + 31) / 32), 0u);
+  for (const PickedRule& pr : all)
+    if (pr.r->rtype == RuleType::HttpLatency) {
+      const uint32_t s = service_ids.at(pr.r->latency.service_name);
+      sampling_lat_svc[s >> 5] |= 1u << (s & 31);
+    }
   // greedy: extend the chunk while its tables fit (a rule that alone does not
   // fit: its route bytes or the service tables exceed kSampCfgLds)
   size_t k = 0;
@@ -401,14 +407,18 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   a.dup = misc;
   a.error = err;
   a.batch_keep = misc + kBatchKeepWord;
-  a.route_match = c->route_match;
+  // match planes (an owner's unpacked records): this chunk's plane
+  const uint64_t plane = c->match_planes > 1 ? (uint64_t)chunk * n : 0;
+  if (c->match_planes > 1 && c->match_planes != e->sampling_chunks_dev.size())
+    return fail(OSE_EINVAL, "cols->match_planes must be 1 or the engine's rule chunks");
+  a.route_match = c->route_match ? c->route_match + plane : nullptr;
   {
     const uint64_t* am = nullptr;
     const int ar = resolve_attr_match(e, c, ws, st, &am);
     if (ar) return ar;
     a.attr_match = e->sampling_n_attr && e->sampling_chunk_attr[chunk] ? am : nullptr;
   }
-  a.svc_match = c->svc_match;
+  a.svc_match = c->svc_match ? c->svc_match + plane : nullptr;
 #if OSE_DIAG
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);
 #endif

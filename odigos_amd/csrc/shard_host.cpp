@@ -333,8 +333,10 @@ int exchange_round(Engine* e, const ose_columns* cols, const ose_outputs* outs, 
   XScratch* xs = scratch_of(e);
   std::lock_guard<std::mutex> g(xs->mu);
   const uint64_t n = cols->n_spans, W = (uint64_t)n_ranks;
+  const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
+  const uint64_t RB = x_rec_bytes(K);   // record bytes: one endpoint and one rule word per rule chunk
   int rc;
-  if ((rc = xs->send.need(std::max<uint64_t>(n, 1) * kXRecBytes)) || (rc = xs->pos.need(4 * std::max<uint64_t>(n, 1))) ||
+  if ((rc = xs->send.need(std::max<uint64_t>(n, 1) * RB)) || (rc = xs->pos.need(4 * std::max<uint64_t>(n, 1))) ||
       (rc = xs->counts.need(16 * W)) || (rc = xs->keep_back.need(std::max<uint64_t>(n, 1))))
     return rc;
   if (!xs->host_counts) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&xs->host_counts), 16 * 64, hipHostMallocDefault));
@@ -366,22 +368,22 @@ int exchange_round(Engine* e, const ose_columns* cols, const ose_outputs* outs, 
   }
   const uint64_t n_recv = rd[W];
   if (n_recv > 0xFFFFFFF0ull) return abort_with(fail(OSE_ERANGE, "more than 2^32-16 records received"));
-  // owner-side columns: trace_id 16, start 8, end 8, route_match 8, svc_match 8, resource 4, res_svc 4,
+  // owner-side columns: trace_id 16, start 8, end 8, route_match 8 K, svc_match 8 K, resource 4, res_svc 4,
   // res_svc_str 4, status 1 per record
   const uint64_t R = std::max<uint64_t>(n_recv, 1);
   const size_t o_tid = 0, o_st = align_up(o_tid + 16 * R, 256), o_en = align_up(o_st + 8 * R, 256),
-               o_rm = align_up(o_en + 8 * R, 256), o_sm = align_up(o_rm + 8 * R, 256),
-               o_res = align_up(o_sm + 8 * R, 256), o_sv = align_up(o_res + 4 * R, 256),
+               o_rm = align_up(o_en + 8 * R, 256), o_sm = align_up(o_rm + 8 * R * K, 256),
+               o_res = align_up(o_sm + 8 * R * K, 256), o_sv = align_up(o_res + 4 * R, 256),
                o_ss = align_up(o_sv + 4 * R, 256), o_stat = align_up(o_ss + 4 * R, 256), o_end = o_stat + R + 256;
-  if ((rc = xs->recv.need(R * kXRecBytes)) || (rc = xs->keep_x.need(R)) || (rc = xs->cols.need(o_end)))
+  if ((rc = xs->recv.need(R * RB)) || (rc = xs->keep_x.need(R)) || (rc = xs->cols.need(o_end)))
     return abort_with(rc);
   // 3. the records (variable sizes per peer)
   std::vector<uint64_t> s_off(W), s_len(W), r_off(W), r_len(W);
   for (uint64_t p = 0; p < W; p++) {
-    s_off[p] = sd[p] * kXRecBytes;
-    s_len[p] = sc[p] * kXRecBytes;
-    r_off[p] = rd[p] * kXRecBytes;
-    r_len[p] = rcv[p] * kXRecBytes;
+    s_off[p] = sd[p] * RB;
+    s_len[p] = sc[p] * RB;
+    r_off[p] = rd[p] * RB;
+    r_len[p] = rcv[p] * RB;
   }
   uint8_t* recvb = xs->recv.as<uint8_t>();
   if ((rc = tx.alltoallv(xs->send.as<uint8_t>(), s_off.data(), s_len.data(), recvb, r_off.data(), r_len.data(), st)))
@@ -391,6 +393,7 @@ int exchange_round(Engine* e, const ose_columns* cols, const ose_outputs* outs, 
   ose_columns oc{};
   oc.n_spans = n_recv;
   oc.n_resources = (uint32_t)n_recv;
+  oc.match_planes = K;   // route_match / svc_match: plane k for rule chunk k
   oc.trace_id = reinterpret_cast<uint64_t*>(cb + o_tid);
   oc.start_ns = reinterpret_cast<uint64_t*>(cb + o_st);
   oc.end_ns = reinterpret_cast<uint64_t*>(cb + o_en);
@@ -403,7 +406,7 @@ int exchange_round(Engine* e, const ose_columns* cols, const ose_outputs* outs, 
   if (n_recv) {
     Engine::Timed tm{};
     e->prof_begin("shard_unpack", st, tm);
-    rc = ose_shard_unpack(recvb, n_recv, kXRecBytes, const_cast<uint64_t*>(oc.trace_id), const_cast<uint64_t*>(oc.start_ns),
+    rc = ose_shard_unpack(recvb, n_recv, (uint32_t)RB, const_cast<uint64_t*>(oc.trace_id), const_cast<uint64_t*>(oc.start_ns),
                           const_cast<uint64_t*>(oc.end_ns), const_cast<uint8_t*>(oc.status),
                           const_cast<uint32_t*>(oc.resource), const_cast<uint32_t*>(oc.res_svc),
                           const_cast<uint32_t*>(oc.res_svc_str), const_cast<uint64_t*>(oc.route_match),
@@ -447,7 +450,7 @@ uint32_t ose_shard_owner(uint64_t tid_hi, uint64_t tid_lo, uint32_t n_ranks) {
 uint32_t ose_shard_record_bytes(const ose_engine* eng) {
   const Engine* e = reinterpret_cast<const Engine*>(eng);
   if (!e || !e->has_sampling) return 0;
-  return kXRecBytes;
+  return x_rec_bytes((uint32_t)e->sampling_chunks_dev.size());
 }
 
 int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void* send, uint64_t* counts,
@@ -455,9 +458,6 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   if (!eng || !c || !send || !counts || !pack_pos) return fail(OSE_EINVAL, "NULL argument");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_pack needs odigossampling on the engine");
-  if (e->sampling_chunks_dev.size() > 1)   // a partial record carries one 64-bit endpoint and service word
-    return fail(OSE_ENOTSUP, "trace-id exchange: the sampling rules need more than one rule chunk (over 64 "
-                             "http_latency rules or 64 service + span_attribute bits); shard by trace id upstream");
   if (int brc = bind_device(e)) return brc;
   if (n_ranks == 0 || n_ranks > 64) return fail(OSE_EINVAL, "n_ranks must be in 1..64");
   const uint64_t n = c->n_spans;
@@ -492,6 +492,9 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.route = c->route;
   a.arena = c->arena;
   a.route_match = c->route_match;
+  a.rm_stride = c->match_planes > 1 ? n : 0;
+  if (c->route_match && c->match_planes > 1 && c->match_planes != e->sampling_chunks_dev.size())
+    return fail(OSE_EINVAL, "cols->match_planes must be 1 or the engine's rule chunks");
   {
     const uint64_t* am = nullptr;
     rc = resolve_attr_match(e, c, ws, st, &am);
@@ -503,7 +506,9 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   }
   a.res_svc = c->res_svc;
   a.res_svc_str = c->res_svc_str;
-  a.cfg = e->sampling_blob_dev;
+  a.cfgs = reinterpret_cast<const uint8_t* const*>(e->shard_tables_dev);
+  a.n_chunks = (uint32_t)e->sampling_chunks_dev.size();
+  a.lat_svc = reinterpret_cast<const uint32_t*>(e->shard_tables_dev + 8 * e->sampling_chunks_dev.size());
   a.hist = reinterpret_cast<uint32_t*>(base + off_hist);
   a.hoff = reinterpret_cast<uint32_t*>(base + off_hoff);
   a.counts = counts;
@@ -539,11 +544,13 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
 int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t* trace_id, uint64_t* start_ns,
                      uint64_t* end_ns, uint8_t* status, uint32_t* resource, uint32_t* res_svc, uint32_t* res_svc_str,
                      uint64_t* route_match, uint64_t* svc_match, void* hip_stream) {
-  if (rec_bytes != kXRecBytes) return fail(OSE_EINVAL, "rec_bytes must be ose_shard_record_bytes()");
+  if (rec_bytes < x_rec_bytes(1) || (rec_bytes - 8 * kXFixedWords) % 16)
+    return fail(OSE_EINVAL, "rec_bytes must be ose_shard_record_bytes()");
+  const uint32_t K = (rec_bytes - 8 * kXFixedWords) / 16;   // rule chunks: route_match / svc_match hold K planes
   if (n && (!recv || !trace_id || !start_ns || !end_ns || !status || !resource || !res_svc || !res_svc_str ||
             !route_match || !svc_match))
     return fail(OSE_EINVAL, "NULL argument");
-  UnpackArgs a{static_cast<const uint8_t*>(recv), n, trace_id, start_ns, end_ns, status, resource, res_svc, res_svc_str,
+  UnpackArgs a{static_cast<const uint8_t*>(recv), n, K, trace_id, start_ns, end_ns, status, resource, res_svc, res_svc_str,
                route_match, svc_match};
   launch_shard_unpack(a, static_cast<hipStream_t>(hip_stream));
   HIP_TRY(hipGetLastError());

@@ -1542,65 +1542,72 @@ __global__ __launch_bounds__(kTThreads) void trace_compact_kernel(TraceCompactAr
 
 // ---- trace-id exchange ---------------------------------------------------------
 // Partial records (include/odigos_amd.h "trace-id exchange"): the source
-// folds each stretch of its batch that shares a trace id and a latency slot
-// (and lies in one 64-span step) into one 56-byte record, so the owner GPU
+// folds each stretch of its batch that shares a trace id and a latency
+// service (and lies in one 64-span step) into one record, so the owner GPU
 // receives one record per stretch instead of one per span.  The record is
 // the stretch's share of what trace_eval_kernel combines per trace: the
-// error bit, the endpoint (HasPrefix) bits, the service_name /
-// span_attribute bits and the latency monoid element (reset, min start after
-// the last reset, max end) of its slot.  The owner folds records in
-// (source rank, source order), which is the global batch order restricted
-// to the trace, so the fold equals the single-GPU one (the monoid is
-// associative, the rest are ORs).
+// error bit, the latency monoid element (reset, min start after the last
+// reset, max end) of its service, and per rule chunk the endpoint
+// (HasPrefix) bits and the service_name / span_attribute bits of that
+// chunk's tables.  The owner folds records in (source rank, source order),
+// which is the global batch order restricted to the trace, so the fold
+// equals the single-GPU one (the monoid is associative, the rest are ORs),
+// chunk by chunk.
 constexpr uint32_t kXNone = 0xFFFFFFu;   // 24-bit "no latency service"
-constexpr uint32_t kXWords = 7;
 constexpr uint32_t kXErr = 1u, kXLat = 2u, kXReset = 4u;
 __device__ __forceinline__ uint32_t shard_owner(uint64_t hi, uint64_t lo, uint32_t n) {
   return (uint32_t)((tid_hash(hi, lo) >> 32) % n);
 }
 
-// one span of a 64-span step: its trace id and latency slot (the record
-// boundary test) and, with `full`, its contributions
+// one span of a 64-span step: its trace id and latency service (the record
+// boundary test) and, with `full`, its chunk-independent contributions
 struct XSpan {
   bool valid;
   uint64_t hi, lo;
-  uint32_t slot, sv, err;
-  uint64_t ep, svcb, st, en;
+  uint32_t sv, res, err;
+  uint64_t st, en;
 };
-__device__ __forceinline__ XSpan x_span(const ShardArgs& a, const Cfg& c, uint64_t j, bool full) {
+__device__ __forceinline__ XSpan x_span(const ShardArgs& a, uint32_t nsvc, uint64_t j, bool full) {
   XSpan x{};
   x.valid = j < a.n_spans;
-  x.slot = kNoSlot;
   x.sv = kXNone;
   if (!x.valid) return x;
   const uint4 t = reinterpret_cast<const uint4*>(a.tid)[j];
   x.hi = (uint64_t)t.x | ((uint64_t)t.y << 32);
   x.lo = (uint64_t)t.z | ((uint64_t)t.w << 32);
-  const uint32_t nsvc = c.h->n_services;
-  const uint32_t res = a.resource[j];
-  const uint32_t s = a.res_svc[res];
-  if (s < nsvc && c.svc_slot[s] != kNoSlot) {
-    x.slot = c.svc_slot[s];
-    x.sv = s;
-  }
+  x.res = a.resource[j];
+  const uint32_t s = a.res_svc[x.res];
+  if (s < nsvc && ((a.lat_svc[s >> 5] >> (s & 31)) & 1u)) x.sv = s;
   if (!full) return x;
   x.err = a.status[j] == OSE_STATUS_ERROR;
-  const uint32_t ss = a.res_svc_str[res];
-  x.svcb = ss < nsvc ? c.svc_bits[ss] : 0;
-  if (a.attr_match) x.svcb |= (a.attr_match[j] >> c.h->attr_base) << c.h->attr_shift;
-  if (x.slot != kNoSlot) {
-    x.ep = a.route_match ? a.route_match[j] & c.slot_rules[x.slot] : endpoint_bits(c, x.slot, a.arena, a.route[j]);
+  if (x.sv != kXNone) {
     x.st = a.start ? a.start[j] : 0;
     x.en = a.end ? a.end[j] : 0;
   }
   return x;
 }
+// the span's endpoint bits and rule bits under rule chunk k's tables
+__device__ __forceinline__ void x_chunk(const ShardArgs& a, const Cfg& c, const XSpan& x, uint64_t j, uint32_t k,
+                                        uint64_t& ep, uint64_t& svcb) {
+  ep = svcb = 0;
+  if (!x.valid) return;
+  const uint32_t nsvc = c.h->n_services;
+  const uint32_t ss = a.res_svc_str[x.res];
+  svcb = ss < nsvc ? c.svc_bits[ss] : 0;
+  if (a.attr_match && c.h->n_attr) svcb |= (a.attr_match[j] >> c.h->attr_base) << c.h->attr_shift;
+  if (x.sv != kXNone) {
+    const uint32_t slot = c.svc_slot[x.sv];
+    if (slot != kNoSlot)
+      ep = a.route_match ? a.route_match[(uint64_t)k * a.rm_stride + j] & c.slot_rules[slot]
+                         : endpoint_bits(c, slot, a.arena, a.route[j]);
+  }
+}
 // record heads of the step (lane 0 always starts one) and tails (where a
 // record's folded value sits after the inclusive segmented scans)
 __device__ __forceinline__ void x_bounds(const XSpan& x, int lane, uint64_t& heads, uint64_t& tails) {
   const uint64_t ph = __shfl_up(x.hi, 1, kWave), pl = __shfl_up(x.lo, 1, kWave);
-  const uint32_t ps = __shfl_up(x.slot, 1, kWave);
-  const bool head = x.valid && (lane == 0 || ph != x.hi || pl != x.lo || ps != x.slot);
+  const uint32_t ps = __shfl_up(x.sv, 1, kWave);
+  const bool head = x.valid && (lane == 0 || ph != x.hi || pl != x.lo || ps != x.sv);
   const uint64_t vm = __ballot(x.valid);
   heads = __ballot(head);
   const uint64_t nxt = (heads | ~vm) >> 1 | (1ull << 63);   // bit l: span l+1 starts a record or is past the end
@@ -1614,12 +1621,12 @@ __global__ __launch_bounds__(kSortThreads) void shard_hist_kernel(ShardArgs a) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t < 64) hist[t] = 0;
   __syncthreads();
-  const Cfg c = load_cfg(a.cfg);
+  const uint32_t nsvc = load_cfg(a.cfgs[0]).h->n_services;
   const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
   for (int r = 0; r < kXRounds; r++) {
     const uint64_t base = b + ((uint64_t)r * (kSortThreads / kWave) + wv) * kWave;
     if (base >= a.n_spans) break;   // wave-uniform
-    const XSpan x = x_span(a, c, base + lane, false);
+    const XSpan x = x_span(a, nsvc, base + lane, false);
     uint64_t heads, tails;
     x_bounds(x, lane, heads, tails);
     if ((tails >> lane) & 1) atomicAdd(&hist[shard_owner(x.hi, x.lo, a.n_ranks)], 1u);
@@ -1645,7 +1652,8 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     for (int k = 0; k < kW; k++) wcnt[k][t] = 0;
   }
   __syncthreads();
-  const Cfg c = load_cfg(a.cfg);
+  const uint32_t nsvc = load_cfg(a.cfgs[0]).h->n_services;
+  const uint32_t words = x_rec_words(a.n_chunks);
   const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
   for (int r = 0; r < kXRounds; r++) {
     const uint64_t base = b + ((uint64_t)r * kW + wv) * kWave;
@@ -1653,17 +1661,17 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     XSpan x{};
     uint64_t heads = 0, tails = 0;
     if (live) {
-      x = x_span(a, c, base + lane, true);
+      x = x_span(a, nsvc, base + lane, true);
       x_bounds(x, lane, heads, tails);
     }
     const bool tail = (tails >> lane) & 1;
     // fold each record (inclusive segmented scans; invalid lanes are lone segments)
     const uint32_t h = x.valid ? (uint32_t)((heads >> lane) & 1) : 1u;
     uint32_t err = x.err;
-    uint64_t ep = x.ep, svcb = x.svcb;
-    Lat v = x.slot != kNoSlot ? Lat{x.st == 0 ? 3u : 2u, x.st == 0 ? kInf : x.st, x.en} : Lat{0u, kInf, 0ull};
+    Lat v = x.sv != kXNone ? Lat{x.st == 0 ? 3u : 2u, x.st == 0 ? kInf : x.st, x.en} : Lat{0u, kInf, 0ull};
     if (live) {
-      seg_or_scan(h, err, ep, svcb);
+      uint64_t z0 = 0, z1 = 0;
+      seg_or_scan(h, err, z0, z1);
       seg_lat_scan(h, v);
     }
     // rank among this wave's records with the same owner
@@ -1689,17 +1697,30 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     }
     __syncthreads();
     uint32_t pos = 0;
+    uint64_t* rec = nullptr;
     if (tail) {
       pos = goff[d] + woff[wv][d] + rank;
-      uint64_t* rec = reinterpret_cast<uint64_t*>(a.send) + (uint64_t)pos * kXWords;
+      rec = reinterpret_cast<uint64_t*>(a.send) + (uint64_t)pos * words;
       const uint32_t flags = (err ? kXErr : 0u) | ((v.f & 2u) ? kXLat : 0u) | ((v.f & 1u) ? kXReset : 0u);
       rec[0] = x.hi;
       rec[1] = x.lo;
       rec[2] = v.m;
       rec[3] = v.e;
-      rec[4] = ep;
-      rec[5] = svcb;
-      rec[6] = (uint64_t)((x.slot != kNoSlot ? x.sv : kXNone) | (flags << 24));
+      rec[4] = (uint64_t)(x.sv | (flags << 24));
+    }
+    // per rule chunk: the endpoint and rule bits under that chunk's tables
+    for (uint32_t k = 0; k < a.n_chunks; k++) {
+      const Cfg c = load_cfg(a.cfgs[k]);
+      uint64_t ep = 0, svcb = 0;
+      if (live) {
+        x_chunk(a, c, x, base + lane, k, ep, svcb);
+        uint32_t z = 0;
+        seg_or_scan(h, z, ep, svcb);
+      }
+      if (tail) {
+        rec[kXFixedWords + 2 * k] = ep;
+        rec[kXFixedWords + 2 * k + 1] = svcb;
+      }
     }
     // every span learns its record's slot from the record's tail lane
     const int tl = ffs64(tails & ~lanemask_lt(lane));
@@ -1710,14 +1731,15 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
 
 // Records -> the owner's SAMPLE columns: one "span" per record with its own
 // resource.  The record's latency element becomes start / end plus status
-// bit 7 (kStatusReset) when a zero start came before its min start; the
-// endpoint bits go to route_match, the rule bits to svc_match.
+// bit 7 (kStatusReset) when a zero start came before its min start; chunk
+// k's endpoint bits go to plane k of route_match, its rule bits to plane k
+// of svc_match.
 __global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
-  const uint64_t* rec = reinterpret_cast<const uint64_t*>(a.recv) + i * kXWords;
-  const uint64_t m = rec[2], e = rec[3], w6 = rec[6];
-  const uint32_t sv = (uint32_t)(w6 & kXNone), flags = (uint32_t)(w6 >> 24) & 0xFFu;
+  const uint64_t* rec = reinterpret_cast<const uint64_t*>(a.recv) + i * x_rec_words(a.n_chunks);
+  const uint64_t m = rec[2], e = rec[3], w4 = rec[4];
+  const uint32_t sv = (uint32_t)(w4 & kXNone), flags = (uint32_t)(w4 >> 24) & 0xFFu;
   const bool lat = flags & kXLat;
   a.tid[2 * i] = rec[0];
   a.tid[2 * i + 1] = rec[1];
@@ -1725,8 +1747,10 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
   a.end[i] = lat ? e : 0;
   a.status[i] = (uint8_t)(((flags & kXErr) ? OSE_STATUS_ERROR : 0u) |
                           ((lat && (flags & kXReset) && m != kInf) ? kStatusReset : 0u));
-  a.route_match[i] = rec[4];
-  a.svc_match[i] = rec[5];
+  for (uint32_t k = 0; k < a.n_chunks; k++) {
+    a.route_match[k * a.n + i] = rec[kXFixedWords + 2 * k];
+    a.svc_match[k * a.n + i] = rec[kXFixedWords + 2 * k + 1];
+  }
   a.res_svc[i] = lat && sv != kXNone ? sv : 0xFFFFFFFFu;
   a.res_svc_str[i] = 0xFFFFFFFFu;
   a.resource[i] = (uint32_t)i;   // one "resource" per record carries its latency service

@@ -32,6 +32,7 @@
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "size_device.hpp"
+#include "url_classes.hpp"
 
 namespace ose {
 namespace {
@@ -470,103 +471,47 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
 typedef const __attribute__((address_space(3))) u32x4 lds_cu4;
 
-// 4x4 byte transpose: out[d] byte j = in[j] byte d (v_perm_b32 picks any 4
-// bytes of the pair {hi, lo}: selector 0-3 lo's bytes, 4-7 hi's)
-__device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t* out) {
-  const uint32_t t0 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);   // a0.b0 a1.b0 a0.b1 a1.b1
-  const uint32_t t1 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);   // a0.b2 a1.b2 a0.b3 a1.b3
-  const uint32_t t2 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
-  const uint32_t t3 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
-  out[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
-  out[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
-  out[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
-  out[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
-}
-
-// One 32-byte row.  The row's bytes are regrouped so that dword d holds bytes
-// d, d + 8, d + 16, d + 24 (two 4x4 byte transposes): a class's SWAR mask of
-// dword d then has byte 8j + d's bit at bit 8j + 7, and shifting it right by
-// 7 - d puts it at bit 8j + d, its place in the row's 32-bit class word.  So
-// a class costs one shift and an OR per dword instead of a movemask (a
-// 32-bit multiply) per dword.
-// the class masks of one dword (bit 7 of byte k set when byte k is in the class)
-__device__ __forceinline__ void class_masks(uint32_t x, uint32_t* m) {
-  const uint32_t hi = x & kH, asc = hi ^ kH;
-  const uint32_t t = swar_t(x), tl = t | 0x20202020u;
-  const uint32_t g0 = swar_ge(t, '0');
-  const uint32_t digit = g0 & ~swar_ge(t, '9' + 1) & asc;
-  const uint32_t ga = swar_ge(tl, 'a');
-  const uint32_t alpha = ga & ~swar_ge(tl, 'z' + 1) & asc;
-  const uint32_t hexl = ga & ~swar_ge(tl, 'f' + 1) & asc;
-  const uint32_t print = swar_ge(t, '!') & ~swar_ge(t, 127) & asc;
-  const uint32_t gat = swar_ge(t, '@');
-  const uint32_t gdot = swar_ge(t, '.'), gsl = swar_ge(t, '/');
-  const uint32_t dash = swar_ge(t, '-') & ~gdot & asc;
-  const uint32_t dot = gdot & ~gsl & asc;
-  const uint32_t extra = ((swar_ge(t, '_') & ~swar_ge(t, '`')) | (swar_ge(t, '%') & ~swar_ge(t, '&')) |
-                          (swar_ge(t, '+') & ~swar_ge(t, ','))) & asc;
-  const uint32_t dom = alpha | digit | dot | dash;
-  m[C_BNL] = ~(print & ~alpha) & kH;                   // outside noLetters' class
-  m[C_BHX] = ~(digit | hexl) & kH;
-  m[C_DG] = digit;
-  m[C_AT] = gat & ~swar_ge(t, 'A') & asc;
-  m[C_HI] = hi;
-  m[C_DASH] = dash;
-  m[C_SL] = gsl & ~g0 & asc;
-  m[C_QM] = swar_ge(t, '?') & ~gat & asc;
-  m[C_BLOC] = ~(dom | extra) & kH;                     // outside [A-Za-z0-9._%+-]
-  m[C_BDOM] = ~dom & kH;                               // outside [A-Za-z0-9.-]
-  m[C_DOT] = dot;
-  m[C_NAL] = ~alpha & kH;
-}
+// One 32-byte row: the class words from two nibble-lookup codes per byte and
+// a bit-matrix transpose (url_classes.hpp; tests/lut_check.cpp checks them on
+// the host).  C_* above is uc::BNL.. in the same order.
+static_assert(C_BNL == uc::BNL && C_DG == uc::DG && C_HI == uc::HI && C_QM == uc::QM && C_NAL == uc::NAL &&
+                  kClasses == uc::kN,
+              "class order");
 __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t r) {
-  uint32_t acc[kClasses];
-#pragma unroll
-  for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
   const lds_cu4* src = (lds_cu4*)(stage32 + 8 * r);
   const u32x4 v0 = src[0], v1 = src[1];
-  uint32_t xs[8];
-  transpose4(v0.x, v0.z, v1.x, v1.z, xs);       // bytes d, d+8, d+16, d+24 for d = 0..3
-  transpose4(v0.y, v0.w, v1.y, v1.w, xs + 4);   // d = 4..7
-#pragma unroll
-  for (int d = 0; d < 8; d++) {
-    uint32_t m[kClasses];
-    class_masks(xs[d], m);
-#pragma unroll
-    for (int c = 0; c < (int)kClasses; c++) acc[c] = (acc[c] >> 1) | m[c];   // after d = 7: dword d's bits at 8j + d
-  }
-  bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
-  bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
-  bm[kRowVec * r + 2] = u32x4{acc[8], acc[9], acc[10], acc[11]};
+  const uint32_t x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t w[kClasses];
+  uc::row_classes(x, w);
+  bm[kRowVec * r] = u32x4{w[0], w[1], w[2], w[3]};
+  bm[kRowVec * r + 1] = u32x4{w[4], w[5], w[6], w[7]};
+  bm[kRowVec * r + 2] = u32x4{w[8], w[9], w[10], w[11]};
 }
-// A quarter of row r (bytes 8q..8q+7) per lane, the four lanes of a quad
-// together building the row: its two dwords' class bits (movemask) at
-// 8q..8q+7, ORed over the quad by two DPP steps; the quad's first lane
-// writes the row.  For the last few rows of a group (a full round would
-// leave most lanes idle).
+// A quarter of row r (bytes 8q..8q+7, one 8 x 8 block) per lane, the four
+// lanes of a quad together building the row: each lane's transposed block
+// is broadcast over the quad (DPP quad_perm) and every lane assembles the
+// plane words with the 4 x 4 byte transposes; the quad's first lane writes
+// the row.  For the last few rows of a group (a full round would leave most
+// lanes idle).
 __device__ __forceinline__ void build_quarter_row(lds_u32* stage32, lds_u4* bm, uint32_t r, uint32_t q, bool valid) {
-  uint32_t acc[kClasses];
-#pragma unroll
-  for (int c = 0; c < (int)kClasses; c++) acc[c] = 0;
+  uint32_t P0 = 0, P1 = 0, Q0 = 0, Q1 = 0;
   if (valid) {
-    const uint32_t x0 = stage32[8 * r + 2 * q], x1 = stage32[8 * r + 2 * q + 1];
-    uint32_t m0[kClasses], m1[kClasses];
-    class_masks(x0, m0);
-    class_masks(x1, m1);
-#pragma unroll
-    for (int c = 0; c < (int)kClasses; c++)
-      acc[c] = (((((m0[c] >> 7) * 0x204081u) >> 21) & 0xFu) | (((((m1[c] >> 7) * 0x204081u) >> 21) & 0xFu) << 4))
-               << (8 * q);
+    uc::codes(stage32[8 * r + 2 * q], P0, Q0);
+    uc::codes(stage32[8 * r + 2 * q + 1], P1, Q1);
+    uc::xpose8(P0, P1);
+    uc::xpose8(Q0, Q1);
   }
-#pragma unroll
-  for (int c = 0; c < (int)kClasses; c++) {
-    acc[c] |= dpp_mov<0xB1>(0u, acc[c]);   // quad_perm [1, 0, 3, 2]
-    acc[c] |= dpp_mov<0x4E>(0u, acc[c]);   // quad_perm [2, 3, 0, 1]
-  }
+  uint32_t p[8], q8[8];
+  uc::xpose4(dpp_mov<0x00>(0u, P0), dpp_mov<0x55>(0u, P0), dpp_mov<0xAA>(0u, P0), dpp_mov<0xFF>(0u, P0), p);
+  uc::xpose4(dpp_mov<0x00>(0u, P1), dpp_mov<0x55>(0u, P1), dpp_mov<0xAA>(0u, P1), dpp_mov<0xFF>(0u, P1), p + 4);
+  uc::xpose4(dpp_mov<0x00>(0u, Q0), dpp_mov<0x55>(0u, Q0), dpp_mov<0xAA>(0u, Q0), dpp_mov<0xFF>(0u, Q0), q8);
+  uc::xpose4(dpp_mov<0x00>(0u, Q1), dpp_mov<0x55>(0u, Q1), dpp_mov<0xAA>(0u, Q1), dpp_mov<0xFF>(0u, Q1), q8 + 4);
   if (valid && q == 0) {
-    bm[kRowVec * r] = u32x4{acc[0], acc[1], acc[2], acc[3]};
-    bm[kRowVec * r + 1] = u32x4{acc[4], acc[5], acc[6], acc[7]};
-    bm[kRowVec * r + 2] = u32x4{acc[8], acc[9], acc[10], acc[11]};
+    uint32_t w[kClasses];
+    uc::derive(p, q8, w);
+    bm[kRowVec * r] = u32x4{w[0], w[1], w[2], w[3]};
+    bm[kRowVec * r + 1] = u32x4{w[4], w[5], w[6], w[7]};
+    bm[kRowVec * r + 2] = u32x4{w[8], w[9], w[10], w[11]};
   }
 }
 __device__ __forceinline__ void build_bitmaps(lds_u32* stage32, lds_u4* bm, uint32_t bytes) {
@@ -1709,7 +1654,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 // chained with the decoupled look-back (device_common.hpp).
 constexpr int kScanThreads = 1024;
 __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a) {
-  __shared__ uint64_t wsum[kScanThreads / kWave];
+  __shared__ uint64_t wsum[kScanThreads / kWave], wsum_a[kScanThreads / kWave];
   __shared__ uint64_t prefix;
   __shared__ uint32_t tile_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1728,6 +1673,9 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
     if (lane >= o) incl += t;
   }
   if (lane == kWave - 1) wsum[wv] = incl;
+  // refs: the scan-placed groups as images would take them (16-byte aligned)
+  const uint64_t va = a.refs ? wave_sum_u64((v + 15) & ~15ull) : 0;
+  if (a.refs && lane == 0) wsum_a[wv] = va;
   __syncthreads();
   uint64_t wbase = 0, total = 0;
 #pragma unroll
@@ -1737,12 +1685,28 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
     total += x;
   }
   if (wv == 0) {
+    if (a.refs && lane == 0) {   // before the tile's aggregate is published (lookback_prefix's release)
+      uint64_t ta = 0;
+      for (int w = 0; w < kScanThreads / kWave; w++) ta += wsum_a[w];
+      if (ta) atomicAdd((unsigned long long*)a.slow_aligned, (unsigned long long)ta);
+    }
     const uint64_t pfx = lookback_prefix(a.scan_status, tile, total, a.error);
     if (lane == 0) {
       prefix = pfx;
       if (tile == a.n_scan_tiles - 1) {
-        if (a.used) *a.used = sb + pfx + total;
-        if (sb + pfx + total > a.out_cap) atomicOr(a.error, 2u);
+        const bool over = sb + pfx + total > a.out_cap;
+        uint64_t used = sb + pfx + total;
+        if (over && a.refs) {
+          // what a retry needs: every group as an image (X, with the bump's
+          // chunk tails of this call counted in) in chunks of the retry's
+          // arena: X * 4/3 + 16 per plan wave covers 8X/7 + cap/8
+          // (url_refs_chunk)
+          const uint64_t X = sb + __hip_atomic_load((unsigned long long*)a.slow_aligned, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+          used = X + (X + 2) / 3 + 16ull * a.plan_waves;
+        }
+        if (a.used) *a.used = used;
+        if (over) atomicOr(a.error, 2u);
       }
     }
   }
@@ -2096,6 +2060,16 @@ static uint32_t plan_blocks(const UrlKernelArgs& a) {
 template <int M>
 static void launch_plan_mode(const UrlKernelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(url_plan_kernel<M>, dim3(plan_blocks<M>(a)), dim3(kThreads), 0, st, a);
+}
+// An eighth of the arena over the plan waves, at most 256 KiB; below eight
+// LDS images per chunk, none (exact reservations).  A wave abandons a chunk
+// only when the next image (<= kImgCap) does not fit it, so an abandoned
+// chunk is at least 7/8 used, and a wave's last chunk leaves at most one
+// chunk unused: images X fit an arena of 8X/7 + cap/8, which is what the
+// overflow report (url_scan_kernel) rests on.
+uint64_t url_refs_chunk(uint64_t cap, uint32_t waves) {
+  const uint64_t c = std::min<uint64_t>(256 << 10, cap / 8 / std::max<uint32_t>(1, waves)) & ~15ull;
+  return c >= 8 * (uint64_t)kImgCap ? c : 0;
 }
 uint32_t url_plan_waves(const UrlKernelArgs& a) {
   switch (url_mode(a)) {

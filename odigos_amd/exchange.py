@@ -112,11 +112,18 @@ class DeviceExchange:
         if n <= self._recv_cap and self._x is not None:
             return self._x
         cap = max(int(n * 1.25), 1024)
-        x = {k: torch.empty(cap * w + 16, dtype=torch.uint8, device=self.device) for k, w in OWNER_COLS}
+        planes = self.planes()   # route_match / svc_match: one plane per rule chunk
+        x = {k: torch.empty(cap * w * (planes if k in ("route_match", "svc_match") else 1) + 16, dtype=torch.uint8,
+                            device=self.device) for k, w in OWNER_COLS}
         x["keep"] = torch.empty(cap, dtype=torch.uint8, device=self.device)
         x["status_word"] = torch.zeros(16, dtype=torch.uint8, device=self.device)
         self._x, self._recv_cap = x, cap
         return x
+
+    def planes(self):
+        """rule chunks of the engine's sampling config (records carry one
+        endpoint and one rule word per chunk: 40 + 16 per chunk bytes)"""
+        return (self.rec_bytes - 40) // 16
 
     def unpack_sample(self, recv, n):
         x = self._ensure(n)
@@ -126,6 +133,7 @@ class DeviceExchange:
         cols = native.Columns()
         cols.n_spans = n
         cols.n_resources = n
+        cols.match_planes = self.planes()
         for k, _ in OWNER_COLS:
             setattr(cols, k, p[k])
         outs = native.Outputs()

@@ -75,7 +75,7 @@ class Columns(C.Structure):
     _fields_ = [
         ("n_spans", C.c_uint64), ("n_resources", C.c_uint32), ("n_scopes", C.c_uint32),
         ("n_attrsets", C.c_uint32), ("_pad", C.c_uint32), ("arena_bytes", C.c_uint64),
-    ] + [(f, _p) for f in COLUMN_FIELDS] + [("svc_match", _p), ("n_attr_keys", C.c_uint32), ("_pad2", C.c_uint32),
+    ] + [(f, _p) for f in COLUMN_FIELDS] + [("svc_match", _p), ("n_attr_keys", C.c_uint32), ("match_planes", C.c_uint32),
                                             ("attr_type", _p), ("attr_val", _p)]
 
 

@@ -23,8 +23,10 @@ NONE24 = 0xFFFFFF
 INF = np.uint64(0xFFFFFFFFFFFFFFFF)
 XERR, XLAT, XRESET = 1, 2, 4
 STEP = 64
-XDT = np.dtype([("hi", "<u8"), ("lo", "<u8"), ("m", "<u8"), ("e", "<u8"), ("ep", "<u8"), ("svcb", "<u8"),
-                ("w6", "<u8")])
+# a record of a one-chunk config: the fixed words, then the chunk's endpoint
+# and rule words (a K-chunk config appends one (ep, svcb) pair per chunk)
+XDT = np.dtype([("hi", "<u8"), ("lo", "<u8"), ("m", "<u8"), ("e", "<u8"), ("w4", "<u8"), ("ep", "<u8"),
+                ("svcb", "<u8")])
 REC_BYTES = XDT.itemsize   # 56
 
 
@@ -136,8 +138,8 @@ def pack(tid: np.ndarray, start, end, status, svc, svc_str, ep, world: int, attr
                 e = max(e, end[i])
         flags = (XERR if np.any(status[a:b] == native.STATUS_ERROR) else 0) | (XLAT if f & 2 else 0) | \
             (XRESET if f & 1 else 0)
-        recs[k] = (hi[a], lo[a], m, e, np.bitwise_or.reduce(ep[a:b]), np.bitwise_or.reduce(svcb[a:b]),
-                   (int(svc[a]) if slot[a] >= 0 else NONE24) | (flags << 24))
+        recs[k] = (hi[a], lo[a], m, e, (int(svc[a]) if slot[a] >= 0 else NONE24) | (flags << 24),
+                   np.bitwise_or.reduce(ep[a:b]), np.bitwise_or.reduce(svcb[a:b]))
     own = owners(recs["hi"], recs["lo"], world)
     order = np.argsort(own, kind="stable")
     slot_of_rec = np.empty(len(starts), dtype=np.int64)
@@ -174,8 +176,8 @@ class HostCols:
 def unpack(recv: np.ndarray) -> HostCols:
     """The owner-side columns ose_shard_unpack writes (one span per record)."""
     r = recv.view(XDT)
-    flags = (r["w6"] >> np.uint64(24)).astype(np.int64) & 0xFF
-    sv = (r["w6"] & np.uint64(NONE24)).astype(np.int64)
+    flags = (r["w4"] >> np.uint64(24)).astype(np.int64) & 0xFF
+    sv = (r["w4"] & np.uint64(NONE24)).astype(np.int64)
     lat = (flags & XLAT) != 0
     start = np.where(lat & (r["m"] != INF), r["m"], np.uint64(0))
     end = np.where(lat, r["e"], np.uint64(0))
@@ -205,8 +207,8 @@ def expand_for_oracle(recv: np.ndarray, cfg: dict):
 
     amask = (1 << 64) - 1
     for k in range(len(r)):
-        h, l, m, e, ep, sb, w6 = (int(x) for x in r[k])
-        flags, sv = (w6 >> 24) & 0xFF, w6 & NONE24
+        h, l, m, e, w4, ep, sb = (int(x) for x in r[k])
+        flags, sv = (w4 >> 24) & 0xFF, w4 & NONE24
         lat = bool(flags & XLAT)
         s = sv if lat else 0xFFFFFFFF
         if lat and (flags & XRESET) and m != int(INF):

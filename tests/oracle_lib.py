@@ -231,6 +231,8 @@ def concat_sampling_columns(sources):
     cat["arena"] = np.concatenate([g.array("arena")[: g.cols.arena_bytes] for g in sources] + [np.zeros(64, np.uint8)])
     for f in ("res_svc", "res_svc_str"):
         cat[f] = np.concatenate([g.array(f).view(np.uint32)[: g.cols.n_resources] for g in sources])
+    if all(getattr(g, "attr_bits", None) is not None for g in sources):   # the shim's span_attribute bits
+        cat["attr_match"] = np.concatenate([np.asarray(g.attr_bits, np.uint64)[: g.cols.n_spans] for g in sources])
     assert cat["arena"].size < 2**32
     from odigos_amd import native
     cols = native.Columns()

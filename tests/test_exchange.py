@@ -110,7 +110,7 @@ def test_unpack_columns():
     n = len(rec)
     assert np.all(a["res_svc_str"][:n] == 0xFFFFFFFF)
     assert np.all(a["resource"][:n] == np.arange(n))
-    flags = (rec["w6"] >> np.uint64(24)).astype(np.int64)
+    flags = (rec["w4"] >> np.uint64(24)).astype(np.int64)
     lat = (flags & 2) != 0
     np.testing.assert_array_equal(a["end_ns"][:n][~lat], 0)
     np.testing.assert_array_equal(a["svc_match"][:n], rec["svcb"])

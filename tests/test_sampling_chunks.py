@@ -151,19 +151,23 @@ def test_gpu_wide_config_large():
 
 
 @pytest.mark.gpu
-def test_gpu_wide_config_exchange_refused():
-    # a partial record carries one 64-bit endpoint / service word: the
-    # trace-id exchange refuses chunked rule lists
-    import torch
-    from odigos_amd.batch import DeviceBatch, Engine
-    eng = Engine({"odigossampling": wide_latency_config()})
-    n = 1000
-    g = Generator("sampling", seed=3, n_spans=n)   # (owns the host columns)
-    db = DeviceBatch(g.cols)
-    L = native.lib()
-    send = torch.empty(n * L.ose_shard_record_bytes(eng.h), dtype=torch.uint8, device="cuda")
-    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
-    pos = torch.empty(n, dtype=torch.int32, device="cuda")
-    with pytest.raises(native.OseError) as ei:
-        native.check(L.ose_shard_pack(eng.h, C.byref(db.cols), 2, send.data_ptr(), counts.data_ptr(), pos.data_ptr(), None))
-    assert ei.value.code == native.OSE_ENOTSUP
+@pytest.mark.parametrize("name", ["attr", "latency", "long_routes", "mixed"])
+def test_gpu_wide_config_exchange_world3(name):
+    # chunked rule lists through the trace-id exchange (ose_exchange_sample's
+    # round at world 3, in-process transport): a record carries one endpoint
+    # and one rule word per rule chunk, the owner runs every chunk's pass on
+    # its plane; traces straddle ranks, and every rank's keep equals the
+    # oracle on the concatenated global batch
+    from tests.test_exchange import _concat_keep_oracle, _local_round
+    cfg = wide_attr_config() if name == "attr" else CONFIGS[name]()
+    sources = [Generator("sampling", seed=0x0D160811, n_spans=600_000, rank=r, world=3) for r in range(3)]
+    for r, g in enumerate(sources):
+        inject_zero_starts(g, 0.01, 30 + r)
+        if name == "attr":
+            g.attr_bits = _attr_bits(g, 40, seed=50 + r)
+    assert _chunks(cfg) >= 2
+    got, stats = _local_round(sources, cfg)
+    want = _concat_keep_oracle(sources, cfg)
+    for gk, wk in zip(got, want):
+        np.testing.assert_array_equal(gk, wk)
+    assert sum(s[0] for s in stats) == sum(s[1] for s in stats) > 0

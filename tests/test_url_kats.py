@@ -199,3 +199,17 @@ def test_gpu_groups_over_the_stage_planned_in_subsets():
     want = hb.apply()
     got = host.Processor("odigosurltemplate", {}).consume(tr)
     assert got == want
+
+
+def test_url_class_words_host(tmp_path):
+    # the lookup + bit-transpose class words of url_plan_kernel's bitmaps
+    # (odigos_amd/csrc/url_classes.hpp, compiled for the host) against per-byte
+    # predicates of templatize.go's character classes: every byte value at
+    # every row position, then random rows (tests/lut_check.cpp)
+    import subprocess
+    from pathlib import Path
+    src = Path(__file__).with_name("lut_check.cpp")
+    exe = tmp_path / "lut_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), str(src)], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-2000:]
