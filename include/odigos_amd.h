@@ -107,9 +107,9 @@ extern "C" {
  * written.  It saves a read and a write of every template byte when the
  * consumer follows the refs on the device instead of copying the arena to
  * the host.  Overflow: device_status bit 2 and *tmpl_arena_used = an arena
- * size a retry of the same batch fits (the templates as 16-byte aligned
- * images, plus a third for chunk tails, plus 16 bytes per assembling wave),
- * so a shim that retries with that capacity succeeds, as in the packed form. */
+ * size for the retry (twice the templates as 16-byte aligned group images,
+ * plus one image per assembling wave, ~4.6 KiB: room for the chunk tails the
+ * retry's waves leave), as the packed form reports the bytes it needs.      */
 #define OSE_STAGE_TEMPLATE_REFS 0x10u
 /* url_out and tmpl already hold the templating results (written by an
  * earlier call on the same batch, e.g. TEMPLATE on a second stream while the

@@ -428,13 +428,11 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   a.win_per_wave = kWinPerWave;
   {
     // the error bit, the endpoint bits and the service (+ span_attribute)
-    // bits in one word: trace_eval_kernel's kNarrow instance
+    // bits in one word: trace_eval_kernel's kNarrow instance (C4 trace_eval
+    // 2.79 -> 2.65 ms, C3 1.41 -> 1.35 ms: profiles/r4e_narrow_ab.txt)
     const SampCfgDev* h = reinterpret_cast<const SampCfgDev*>(e->sampling_chunks_host[chunk].data());
     const uint32_t svc_bits = h->attr_shift + (a.attr_match ? h->n_attr : 0);
     a.narrow = 1 + h->n_lat + svc_bits <= 32 && h->n_lat_slots <= 32 ? 1u : 0u;
-#ifdef OSE_AB_NO_NARROW   // temporary A/B switch (removed after the measurement)
-    a.narrow = 0;
-#endif
   }
 #if OSE_DIAG
   if (const char* ww = getenv("OSE_WIN_PER_WAVE")) a.win_per_wave = std::max<uint32_t>(1, (uint32_t)strtoul(ww, nullptr, 0));

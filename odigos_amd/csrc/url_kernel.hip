@@ -1566,31 +1566,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     bool fast = fused_cfg && listed && __ballot(p.mode == M_RULE || big) == 0 && sum <= kImgCap;
     if (fast && scr_used + need > scr_end) {
       if (a.refs && !exhausted) {   // a new chunk (the rest of the current one is left unused)
-        // the bump moves only by space that fits the arena: a full chunk, else
-        // exactly this image, else nothing (the chunks the waves hold never
-        // pass out_cap, so *used overstates nothing and a batch the packed
-        // form fits is not refused for a chunk's unused tail)
-        uint64_t csz = max(a.refs_chunk, need), at = ~0ull;
-        if (lane == 0) {
-          unsigned long long cur = __hip_atomic_load((unsigned long long*)a.bump, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-          for (;;) {
-            const uint64_t take = cur + csz <= a.out_cap ? csz : cur + need <= a.out_cap ? need : 0;
-            if (!take) break;
-            if (__hip_atomic_compare_exchange_strong((unsigned long long*)a.bump, &cur, cur + take, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-              at = cur;
-              csz = take;
-              break;
-            }
-          }
-        }
+        // one fetch-add per chunk (a compare-and-swap loop that moved the
+        // bump only by space that fits measured 12x slower on C4: 4096 waves
+        // retrying one address); a chunk that ends past out_cap is used up
+        // to out_cap, and the scan counts the bump only up to out_cap
+        const uint64_t csz = max(a.refs_chunk, need);
+        uint64_t at = 0;
+        if (lane == 0) at = atomicAdd((unsigned long long*)a.bump, (unsigned long long)csz);
         at = (uint64_t)lane_value((uint32_t)at, 0) | ((uint64_t)lane_value((uint32_t)(at >> 32), 0) << 32);
-        csz = (uint64_t)lane_value((uint32_t)csz, 0) | ((uint64_t)lane_value((uint32_t)(csz >> 32), 0) << 32);
-        if (at != ~0ull) {
+        const uint64_t avail = at < a.out_cap ? min(csz, a.out_cap - at) : 0;
+        if (avail >= need) {
           region = at;
           scr_used = 0;
-          scr_end = csz;
+          scr_end = avail;
         } else {
           fast = false;   // the arena is full: the scan flags the overflow
           exhausted = true;
@@ -1665,7 +1653,7 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
   // refs mode: only the slow groups are placed by the scan, after the plan
   // waves' image chunks
   const uint64_t v = k < a.n_groups && !(a.refs && a.group_scr[k] != ~0ull) ? a.group_sum[k] : 0;
-  const uint64_t sb = a.refs ? *a.bump : 0;
+  const uint64_t sb = a.refs ? min(*a.bump, a.out_cap) : 0;   // chunks past out_cap are used up to it
   uint64_t incl = v;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -1697,13 +1685,12 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
         const bool over = sb + pfx + total > a.out_cap;
         uint64_t used = sb + pfx + total;
         if (over && a.refs) {
-          // what a retry needs: every group as an image (X, with the bump's
-          // chunk tails of this call counted in) in chunks of the retry's
-          // arena: X * 4/3 + 16 per plan wave covers 8X/7 + cap/8
-          // (url_refs_chunk)
+          // what a retry needs: every group as a 16-byte aligned image (X,
+          // with the bump's chunk tails of this call counted in), twice over
+          // for the tails the retry's waves leave, plus an image per wave
           const uint64_t X = sb + __hip_atomic_load((unsigned long long*)a.slow_aligned, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-          used = X + (X + 2) / 3 + 16ull * a.plan_waves;
+          used = 2 * X + (uint64_t)kImgCap * a.plan_waves;
         }
         if (a.used) *a.used = used;
         if (over) atomicOr(a.error, 2u);
@@ -2061,15 +2048,11 @@ template <int M>
 static void launch_plan_mode(const UrlKernelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(url_plan_kernel<M>, dim3(plan_blocks<M>(a)), dim3(kThreads), 0, st, a);
 }
-// An eighth of the arena over the plan waves, at most 256 KiB; below eight
-// LDS images per chunk, none (exact reservations).  A wave abandons a chunk
-// only when the next image (<= kImgCap) does not fit it, so an abandoned
-// chunk is at least 7/8 used, and a wave's last chunk leaves at most one
-// chunk unused: images X fit an arena of 8X/7 + cap/8, which is what the
-// overflow report (url_scan_kernel) rests on.
+// An eighth of the arena over the plan waves, at most 256 KiB (a group
+// larger than a chunk takes exactly its size): a wave leaves at most one
+// chunk's tail unused at the end
 uint64_t url_refs_chunk(uint64_t cap, uint32_t waves) {
-  const uint64_t c = std::min<uint64_t>(256 << 10, cap / 8 / std::max<uint32_t>(1, waves)) & ~15ull;
-  return c >= 8 * (uint64_t)kImgCap ? c : 0;
+  return std::min<uint64_t>(256 << 10, cap / 8 / std::max<uint32_t>(1, waves)) & ~15ull;
 }
 uint32_t url_plan_waves(const UrlKernelArgs& a) {
   switch (url_mode(a)) {
