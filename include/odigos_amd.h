@@ -153,7 +153,9 @@ typedef struct ose_columns {
   uint32_t n_resources;
   uint32_t n_scopes;
   uint32_t n_attrsets;      /* traffic-metrics attribute sets (res_attrset range) */
-  uint32_t _pad;
+  uint32_t attr_match_words; /* 64-bit words of attr_match per span, word-major: word w of span i at
+                                attr_match[w * n_spans + i] (bits 64w..64w+63); 0 or 1: one word.
+                                ose_engine_info.n_attr_rules > 64 needs (n_attr_rules + 63) / 64 */
   uint64_t arena_bytes;     /* bytes of `arena`; also sizes the TEMPLATE stage's scratch for
                                the assembled templates (an understated value is not an error:
                                the groups that do not fit take the slower per-span writer) */
@@ -176,7 +178,8 @@ typedef struct ose_columns {
                                   of the r-th http_latency rule) for the rules of the span's service
                                   (latency.go:64-68, 97-100); when non-NULL the engine reads it
                                   instead of route/arena (set by ose_shard_unpack)               */
-  const uint64_t* attr_match;  /* bit k = the span meets the k-th span_attribute rule (in level order):
+  const uint64_t* attr_match;  /* bit k = the span meets the k-th span_attribute rule (in level order;
+                                  beyond 64 rules, in word k / 64: attr_match_words):
                                   its resource's AsString(service.name) is the rule's service_name and
                                   its attribute satisfies the condition (spanattribute.go:126-320).
                                   With attr_type set, only the bits of the rules the engine leaves to
@@ -302,9 +305,14 @@ typedef struct ose_engine_info {
   uint32_t n_attr_rules;        /* span_attribute rules (attr_match bits) */
   uint32_t n_attr_keys;         /* attribute keys the GPU-evaluated ones read */
   uint64_t attr_host_rules;     /* bit k: rule k is evaluated by the shim into
-                                   attr_match even when attr_type is given */
+                                   attr_match even when attr_type is given (rules
+                                   0..63; all of them: ose_engine_attr_host_rules) */
 } ose_engine_info;
 int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info);
+/* The shim-evaluated span_attribute rules as (n_attr_rules + 63) / 64 words
+ * (bit k of word w: rule 64w + k); writes min(cap, that) words and returns
+ * that count (0 without span_attribute rules).                             */
+uint32_t ose_engine_attr_host_rules(const ose_engine* eng, uint64_t* words, uint32_t cap);
 
 /* Attribute key k (< n_attr_keys) of the attr_type / attr_val columns; the
  * bytes stay valid for the engine's lifetime.                               */

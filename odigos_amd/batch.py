@@ -19,7 +19,7 @@ COLUMN_LAYOUT = {
     "trace_id": ("span", 16), "start_ns": ("span", 8), "end_ns": ("span", 8), "status": ("span", 1),
     "kind": ("span", 1), "resource": ("span", 4), "scope": ("span", 4), "url_flags": ("span", 1),
     "path": ("span", 8), "route": ("span", 8), "span_size": ("span", 4), "name_len": ("span", 4),
-    "route_match": ("span", 8), "attr_match": ("span", 8),
+    "route_match": ("span", 8), "attr_match": ("span_words", 8),
     "res_svc": ("res", 4), "res_svc_str": ("res", 4), "res_url_ok": ("res", 1), "res_attrset": ("res", 4),
     "res_size": ("res", 4), "scope_size": ("scope", 4), "scope_resource": ("scope", 4),
     "attr_type": ("span_key", 1), "attr_val": ("span_key", 8),
@@ -34,7 +34,8 @@ OUTPUT_LAYOUT = {
 
 def _count(cols, dim: str) -> int:
     return {"span": cols.n_spans, "res": cols.n_resources, "scope": cols.n_scopes, "arena": cols.arena_bytes,
-            "attrset": cols.n_attrsets, "one": 1, "span_key": cols.n_spans * cols.n_attr_keys}[dim]
+            "attrset": cols.n_attrsets, "one": 1, "span_key": cols.n_spans * cols.n_attr_keys,
+            "span_words": cols.n_spans * max(1, cols.attr_match_words)}[dim]
 
 
 def default_tmpl_cap(cols) -> int:
@@ -150,7 +151,7 @@ class DeviceBatch:
         import torch
         self.torch = torch
         self.cols = native.Columns()
-        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys"):
+        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys", "attr_match_words"):
             setattr(self.cols, f, getattr(host_cols, f))
         self.t = {}
         for name, (dim, size) in COLUMN_LAYOUT.items():
@@ -394,7 +395,7 @@ class GroupByTrace:
     def download(self, cols: native.Columns) -> dict:
         """Host copies (numpy) of the last release's columns."""
         dst = native.Columns()
-        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys"):
+        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys", "attr_match_words"):
             setattr(dst, f, getattr(cols, f))
         out = {}
         for name, (dim, size) in COLUMN_LAYOUT.items():
@@ -469,7 +470,7 @@ class OtlpBatch:
         """Host copies of every column (numpy), dims and the arena."""
         c = self.cols
         dst = native.Columns()
-        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys"):
+        for f in ("n_spans", "n_resources", "n_scopes", "n_attrsets", "arena_bytes", "n_attr_keys", "attr_match_words"):
             setattr(dst, f, getattr(c, f))
         out = {}
         for name, (dim, size) in COLUMN_LAYOUT.items():

@@ -45,12 +45,16 @@ uint32_t op_code(const std::string& cond, const std::string& op) {
 int Engine::build_attr_tables() {
   attr_keys.clear();
   attr_host_rules = 0;
+  attr_host_words.clear();
+  attr_words = 1;
   attr_n_rules = attr_n_dev = 0;
   if (!has_sampling) return 0;
   const AttrPlan plan = plan_attr_rules(sampling);
   attr_keys = plan.keys;
-  attr_host_rules = plan.host_mask;
+  attr_host_words = plan.host_mask;
+  attr_host_rules = attr_host_words.empty() ? 0 : attr_host_words[0];
   attr_n_rules = (uint32_t)plan.rule_key.size();
+  attr_words = std::max<uint32_t>(1, (attr_n_rules + 63) / 64);
   Blob bl;
   AttrCfgDev h{};
   bl.put(&h, 1);
@@ -120,7 +124,7 @@ int Workspace::reserve_attr(uint64_t n) {
   if (attr_bits) HIP_TRY(hipFree(attr_bits));
   attr_bits = nullptr;
   attr_bits_cap = 0;
-  const uint64_t want = std::max<uint64_t>(n, 1 << 16);
+  const uint64_t want = std::max<uint64_t>(n, 1 << 16);   // (n = spans x attr_match words)
   HIP_TRY(hipMalloc(reinterpret_cast<void**>(&attr_bits), want * 8));
   attr_bits_cap = want;
   return 0;
@@ -128,7 +132,8 @@ int Workspace::reserve_attr(uint64_t n) {
 
 // The attr_match bits for this call: evaluated here from attr_type /
 // attr_val when the caller passes them (ORed with the shim's bits of the
-// "json" rules), else the caller's attr_match as is.
+// "json" rules), else the caller's attr_match as is.  Either way
+// e->attr_words words per span, word-major (ose_columns.attr_match_words).
 int resolve_attr_match(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, const uint64_t** out) {
   *out = nullptr;
   if (!e->attr_n_rules) return 0;
@@ -137,23 +142,31 @@ int resolve_attr_match(Engine* e, const ose_columns* c, Workspace* ws, hipStream
     *out = c->attr_match;
     return 0;
   }
-  if (c->attr_type && c->attr_val && e->attr_n_dev) {
+  const uint32_t W = e->attr_words;
+  const bool gpu_eval = c->attr_type && c->attr_val && e->attr_n_dev;
+  const bool reads_cols = c->attr_match && (!gpu_eval || e->attr_host_rules_any());   // attr_match is read
+  if (reads_cols && std::max<uint32_t>(1, c->attr_match_words) != W)
+    return fail(OSE_EINVAL, "attr_match carries " + std::to_string(std::max<uint32_t>(1, c->attr_match_words)) +
+                                " words per span; the engine's " + std::to_string(e->attr_n_rules) +
+                                " span_attribute rules need " + std::to_string(W) + " (ose_columns.attr_match_words)");
+  if (gpu_eval) {
     if (c->n_attr_keys < e->attr_keys.size())
       return fail(OSE_EINVAL, "attr_type / attr_val carry fewer keys than the engine's span_attribute rules read");
-    if (e->attr_host_rules && !c->attr_match)
+    if (e->attr_host_rules_any() && !c->attr_match)
       return fail(OSE_EINVAL, "span_attribute rules with json conditions need the attr_match column");
     if (!c->resource || !c->res_svc) return fail(OSE_EINVAL, "span_attribute rules need resource and res_svc");
-    int rc = ws->reserve_attr(n);
+    int rc = ws->reserve_attr(n * W);
     if (rc) return rc;
     AttrArgs a{};
     a.n_spans = n;
+    a.words = W;
     a.type = c->attr_type;
     a.val = c->attr_val;
     a.arena = c->arena;
     a.resource = c->resource;
     a.res_svc = c->res_svc;
-    a.host_bits = e->attr_host_rules ? c->attr_match : nullptr;
-    a.host_mask = e->attr_host_rules;
+    a.host_bits = e->attr_host_rules_any() ? c->attr_match : nullptr;
+    a.host_mask = reinterpret_cast<const uint64_t*>(e->attr_host_mask_dev);
     a.cfg = e->attr_blob_dev;
     a.out = ws->attr_bits;
     Engine::Timed tm{};

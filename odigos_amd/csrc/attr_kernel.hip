@@ -92,17 +92,22 @@ __global__ __launch_bounds__(kAThreads) void attr_eval_kernel(AttrArgs a) {
   const uint32_t nr = h->n_rules;
   const uint64_t stride = (uint64_t)gridDim.x * kAThreads;
   for (uint64_t i = (uint64_t)blockIdx.x * kAThreads + threadIdx.x; i < a.n_spans; i += stride) {
-    uint64_t bits = a.host_bits ? (a.host_bits[i] & a.host_mask) : 0;
     const uint32_t svc = a.res_svc[a.resource[i]];
-    for (uint32_t k = 0; k < nr; k++) {
-      const AttrRuleDev& r = rules[k];
-      if (svc != r.svc) continue;
-      const uint64_t j = (uint64_t)r.key * a.n_spans + i;
-      const uint32_t t = a.type[j];
-      if (t == OSE_ATTR_ABSENT) continue;   // Get(key) not found (:136-138)
-      if (eval_rule(r, a.cfg, t, a.val[j], a.arena)) bits |= 1ull << r.bit;
+    // word w holds the bits of rules 64w..64w+63; the device rules are in
+    // level order (increasing bit), so word w's are a contiguous stretch
+    uint32_t k = 0;
+    for (uint32_t w = 0; w < a.words; w++) {
+      uint64_t bits = a.host_bits ? (a.host_bits[(uint64_t)w * a.n_spans + i] & a.host_mask[w]) : 0;
+      for (; k < nr && rules[k].bit < 64 * (w + 1); k++) {
+        const AttrRuleDev& r = rules[k];
+        if (svc != r.svc) continue;
+        const uint64_t j = (uint64_t)r.key * a.n_spans + i;
+        const uint32_t t = a.type[j];
+        if (t == OSE_ATTR_ABSENT) continue;   // Get(key) not found (:136-138)
+        if (eval_rule(r, a.cfg, t, a.val[j], a.arena)) bits |= 1ull << (r.bit % 64);
+      }
+      a.out[(uint64_t)w * a.n_spans + i] = bits;
     }
-    a.out[i] = bits;
   }
 }
 

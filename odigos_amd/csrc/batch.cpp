@@ -67,7 +67,8 @@ struct Batch {
   }
   bool fits(const ose_columns& x) const {
     return x.n_spans <= cap.n_spans && x.n_resources <= cap.n_resources && x.n_scopes <= cap.n_scopes &&
-           x.n_attrsets <= cap.n_attrsets && x.arena_bytes <= cap.arena_bytes && x.n_attr_keys <= cap.n_attr_keys;
+           x.n_attrsets <= cap.n_attrsets && x.arena_bytes <= cap.arena_bytes && x.n_attr_keys <= cap.n_attr_keys &&
+           std::max<uint32_t>(1, x.attr_match_words) <= cap.attr_match_words;
   }
   int build(const ose_columns& dims);
   void set_dims(const ose_columns& dims);
@@ -81,6 +82,7 @@ int Batch::build(const ose_columns& dims) {
   cap.n_attrsets = dims.n_attrsets;
   cap.arena_bytes = dims.arena_bytes;
   cap.n_attr_keys = dims.n_attr_keys;
+  cap.attr_match_words = std::max<uint32_t>(1, dims.attr_match_words);
   const uint64_t n = cap.n_spans, R = cap.n_resources, S = cap.n_scopes, A = cap.n_attrsets, K = cap.n_attr_keys;
   const uint64_t n1 = std::max<uint64_t>(n, 1);   // BATCH mode: one trace even with no spans
   // every template fits in 2x the input bytes + 8 per span; capped at the
@@ -113,7 +115,7 @@ int Batch::build(const ose_columns& dims) {
   IN(route, 8 * n);
   IN(span_size, 4 * n);
   IN(name_len, 4 * n);   // route_match stays NULL: host batches carry route bytes
-  IN(attr_match, 8 * n);
+  IN(attr_match, 8 * n * cap.attr_match_words);   // word-major planes of the call's n_spans
   IN(res_svc, 4 * R);
   IN(res_svc_str, 4 * R);
   IN(res_url_ok, R);
@@ -164,6 +166,7 @@ void Batch::set_dims(const ose_columns& dims) {
     c->n_attrsets = dims.n_attrsets;
     c->arena_bytes = dims.arena_bytes;
     c->n_attr_keys = dims.n_attr_keys;
+    c->attr_match_words = std::max<uint32_t>(1, dims.attr_match_words);
   }
   // every pointer back to the slab (the shim NULLs columns it does not fill)
   for (auto& f : fields) {

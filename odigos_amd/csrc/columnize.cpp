@@ -53,7 +53,6 @@ std::string ColumnizeCtx::build(const UrlTemplateConfig* url, const SamplingConf
           std::string e = attr_preds.back().compile(r.attr);
           if (!e.empty()) return e;
         }
-    if (attr_preds.size() > 64) return "more than 64 span_attribute rules are not supported";
     attr_plan = plan_attr_rules(*sampling);
   }
   return "";
@@ -66,8 +65,9 @@ ResourceCols columnize_resource(const ColumnizeCtx& c, const AttrMap& ra) {
   if (sv) {
     const std::string as = sv->AsString();
     // span_attribute rules whose service this resource is (spanattribute.go:130-132)
+    r.attr_res.assign((c.attr_preds.size() + 63) / 64, 0);
     for (size_t k = 0; k < c.attr_preds.size(); k++)
-      if (c.attr_preds[k].service() == as) r.attr_res |= 1ull << k;
+      if (c.attr_preds[k].service() == as) r.attr_res[k / 64] |= 1ull << (k % 64);
     auto it = c.services.find(as);
     if (it != c.services.end()) {
       r.svc = it->second;
@@ -89,7 +89,8 @@ ResourceCols columnize_resource(const ColumnizeCtx& c, const AttrMap& ra) {
   return r;
 }
 
-void columnize_span(const ColumnizeCtx& c, const Span& sp, uint64_t attr_res, const ProtoSizer& sizer, SpanCols& o) {
+void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uint64_t>& attr_res, const ProtoSizer& sizer,
+                    SpanCols& o) {
   o.hi = o.lo = 0;
   for (int k = 0; k < 8; k++) { o.hi = o.hi << 8 | sp.trace_id[k]; o.lo = o.lo << 8 | sp.trace_id[8 + k]; }
   o.start = sp.start;
@@ -99,12 +100,14 @@ void columnize_span(const ColumnizeCtx& c, const Span& sp, uint64_t attr_res, co
   o.span_size = (uint32_t)sizer.span(sp);
   o.name_len = (uint32_t)sp.name.size();
   // span_attribute: the "json" conditions here, the others from the key columns on the GPU
-  o.attr_match = 0;
-  for (uint64_t m = attr_res & c.attr_plan.host_mask; m; m &= m - 1) {
-    const int k = __builtin_ctzll(m);
-    if (const Value* av = sp.attrs.Get(c.attr_preds[k].key()))
-      if (c.attr_preds[k].eval(*av)) o.attr_match |= 1ull << k;
-  }
+  const size_t W = std::max<size_t>(1, (c.attr_preds.size() + 63) / 64);
+  o.attr_match.assign(W, 0);
+  for (size_t w = 0; w < attr_res.size() && w < c.attr_plan.host_mask.size(); w++)
+    for (uint64_t m = attr_res[w] & c.attr_plan.host_mask[w]; m; m &= m - 1) {
+      const size_t k = 64 * w + (size_t)__builtin_ctzll(m);
+      if (const Value* av = sp.attrs.Get(c.attr_preds[k].key()))
+        if (c.attr_preds[k].eval(*av)) o.attr_match[w] |= 1ull << (k % 64);
+    }
   const size_t nk = c.attr_plan.keys.size();
   o.attr_type.assign(nk, OSE_ATTR_ABSENT);
   o.attr_val.assign(nk, 0);

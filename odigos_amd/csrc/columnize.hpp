@@ -39,7 +39,7 @@ struct ColumnizeCtx {
 struct ResourceCols {
   uint32_t svc = OSE_NONE, svc_str = OSE_NONE;
   uint8_t url_ok = 1;
-  uint64_t attr_res = 0;
+  std::vector<uint64_t> attr_res;   // span_attribute rules whose service this resource is (64 per word)
   std::vector<std::pair<std::string, std::string>> attrset;   // attribute.NewSet: sorted, last value wins
 };
 ResourceCols columnize_resource(const ColumnizeCtx& c, const AttrMap& ra);
@@ -49,14 +49,15 @@ struct SpanCols {
   uint64_t hi = 0, lo = 0, start = 0, end = 0;
   uint8_t status = 0, kind = 0, url_flags = 0;
   uint32_t span_size = 0, name_len = 0;
-  uint64_t attr_match = 0;                    // bits of the shim-evaluated (json) rules
+  std::vector<uint64_t> attr_match;           // bits of the shim-evaluated (json) rules (64 per word)
   bool has_route = false;
   std::string route, path;                    // AsString(http.route); the url path source
   std::vector<uint8_t> attr_type;             // per GPU key column
   std::vector<uint64_t> attr_val;             // STR values: placeholder, see attr_str
   std::vector<std::string> attr_str;          // STR values' bytes (per key; empty otherwise)
 };
-void columnize_span(const ColumnizeCtx& c, const Span& sp, uint64_t attr_res, const ProtoSizer& sizer, SpanCols& out);
+void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uint64_t>& attr_res, const ProtoSizer& sizer,
+                    SpanCols& out);
 
 // ptrace.StatusCode as the status column: 0/1/2 as they are, anything else
 // (not a valid code) 3 — only == OSE_STATUS_ERROR matters to the rules, and

@@ -157,6 +157,7 @@ Engine::~Engine() {
     if (d) (void)hipFree(d);   // (sampling_blob_dev is the first)
   if (shard_tables_dev) (void)hipFree(shard_tables_dev);
   if (attr_blob_dev) (void)hipFree(attr_blob_dev);
+  if (attr_host_mask_dev) (void)hipFree(attr_host_mask_dev);
   for (auto* w : pool) {
     if (w->dev) (void)hipFree(w->dev);
     if (w->table) (void)hipFree(w->table);
@@ -660,6 +661,10 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
   if (!e->attr_blob_host.empty()) {
     rc = upload(e->attr_blob_host, &e->attr_blob_dev);
     if (rc) { delete e; return rc; }
+    std::vector<uint8_t> hm(8 * std::max<size_t>(e->attr_words, 1), 0);
+    std::memcpy(hm.data(), e->attr_host_words.data(), 8 * std::min<size_t>(e->attr_host_words.size(), e->attr_words));
+    rc = upload(hm, &e->attr_host_mask_dev);
+    if (rc) { delete e; return rc; }
   }
   *out = reinterpret_cast<ose_engine*>(e);
   return 0;
@@ -710,6 +715,15 @@ int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info) {
   info->n_attr_keys = (uint32_t)e->attr_keys.size();
   info->attr_host_rules = e->attr_host_rules;
   return 0;
+}
+
+uint32_t ose_engine_attr_host_rules(const ose_engine* eng, uint64_t* words, uint32_t cap) {
+  if (!eng) return 0;
+  const Engine* e = reinterpret_cast<const Engine*>(eng);
+  if (!e->attr_n_rules) return 0;
+  const uint32_t W = e->attr_words;
+  for (uint32_t w = 0; w < W && w < cap && words; w++) words[w] = w < e->attr_host_words.size() ? e->attr_host_words[w] : 0;
+  return W;
 }
 
 int ose_engine_set_option(ose_engine* eng, const char* name, int64_t value) {

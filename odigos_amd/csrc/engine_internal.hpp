@@ -130,7 +130,15 @@ struct Engine {
   std::vector<uint8_t> attr_blob_host;
   uint8_t* attr_blob_dev = nullptr;
   uint32_t attr_n_rules = 0, attr_n_dev = 0;
-  uint64_t attr_host_rules = 0;
+  uint64_t attr_host_rules = 0;              // rules 0..63 of attr_host_words (ose_engine_info)
+  std::vector<uint64_t> attr_host_words;     // the shim-evaluated rules, one bit per rule
+  uint32_t attr_words = 1;                   // attr_match words per span: (attr_n_rules + 63) / 64, >= 1
+  uint8_t* attr_host_mask_dev = nullptr;     // attr_host_words on the device (AttrArgs::host_mask)
+  bool attr_host_rules_any() const {
+    for (uint64_t w : attr_host_words)
+      if (w) return true;
+    return false;
+  }
   std::vector<std::string> attr_keys;
 
   std::mutex mu;

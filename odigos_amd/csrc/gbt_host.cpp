@@ -176,6 +176,7 @@ GbtArgs base_args(Gbt* g) {
   a.table_mask = g->table_slots - 1;
   a.epoch = g->epoch;
   a.n_attr_keys = g->K;
+  a.attr_words = g->e->attr_words;
   a.error = reinterpret_cast<uint32_t*>(g->words.p);
   a.ring_tid = reinterpret_cast<uint64_t*>(g->ring.p);
   a.num_traces = g->num_traces;
@@ -193,6 +194,8 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
   const uint64_t n = c->n_spans, S = c->n_scopes;
   if (!n) return 0;
   if (g->K && c->n_attr_keys != g->K) return fail(OSE_EINVAL, "groupbytrace: the batch's attribute key columns differ from the engine's");
+  if (c->attr_match && std::max<uint32_t>(1, c->attr_match_words) != g->e->attr_words)
+    return fail(OSE_EINVAL, "groupbytrace: attr_match_words differs from the engine's span_attribute rule words");
   if (!c->trace_id || !c->start_ns || !c->end_ns || !c->status || !c->kind || !c->scope || !c->scope_resource ||
       !c->res_svc || !c->res_attrset || (g->K && (!c->attr_type || !c->attr_val)))
     return fail(OSE_EINVAL, "groupbytrace: a required column is NULL");
@@ -403,7 +406,7 @@ int gbt_release(Gbt* g, int64_t now, hipStream_t st, uint32_t* n_traces) {
     GbtOut& O = a.out;
     std::vector<Part> parts = {
         {(void**)&O.tid, 16 * M}, {(void**)&O.start, 8 * M}, {(void**)&O.end, 8 * M},
-        {(void**)&O.attr_match, 8 * M}, {(void**)&O.status, M}, {(void**)&O.kind, M},
+        {(void**)&O.attr_match, 8 * M * g->e->attr_words}, {(void**)&O.status, M}, {(void**)&O.kind, M},
         {(void**)&O.url_flags, M}, {(void**)&O.span_size, 4 * M}, {(void**)&O.name_len, 4 * M},
         {(void**)&O.resource, 4 * M}, {(void**)&O.scope, 4 * M}, {(void**)&O.route, 8 * M},
         {(void**)&O.path, 8 * M}, {(void**)&O.attr_type, K * M + 16}, {(void**)&O.attr_val, 8 * K * M + 16},
@@ -454,6 +457,7 @@ int gbt_release(Gbt* g, int64_t now, hipStream_t st, uint32_t* n_traces) {
     oc.span_size = O.span_size;
     oc.name_len = O.name_len;
     oc.attr_match = O.attr_match;
+    oc.attr_match_words = g->e->attr_words;
     oc.res_svc = O.res_svc;
     oc.res_svc_str = O.res_svc_str;
     oc.res_url_ok = O.res_url_ok;
@@ -521,7 +525,7 @@ int ose_gbt_create(ose_engine* eng, const char* cfg_json, uint64_t span_capacity
   struct Part { void** dst; size_t bytes; };
   std::vector<Part> parts = {
       {(void**)&g->P.tid, 16 * C}, {(void**)&g->P.start, 8 * C}, {(void**)&g->P.end, 8 * C},
-      {(void**)&g->P.attr_match, 8 * C}, {(void**)&g->P.seq, 8 * C}, {(void**)&g->P.origin, 8 * C},
+      {(void**)&g->P.attr_match, 8 * C * g->e->attr_words}, {(void**)&g->P.seq, 8 * C}, {(void**)&g->P.origin, 8 * C},
       {(void**)&g->P.str_off, 8 * C}, {(void**)&g->P.status, C}, {(void**)&g->P.kind, C},
       {(void**)&g->P.url_flags, C}, {(void**)&g->P.span_size, 4 * C}, {(void**)&g->P.name_len, 4 * C},
       {(void**)&g->P.route, 8 * C}, {(void**)&g->P.path, 8 * C}, {(void**)&g->P.attr_type, K * C + 16},
@@ -611,7 +615,8 @@ int ose_gbt_download(const ose_gbt* gg, const ose_columns* dst) {
       {c.status, (void*)dst->status, n}, {c.kind, (void*)dst->kind, n}, {c.resource, (void*)dst->resource, 4 * n},
       {c.scope, (void*)dst->scope, 4 * n}, {c.url_flags, (void*)dst->url_flags, n}, {c.path, (void*)dst->path, 8 * n},
       {c.route, (void*)dst->route, 8 * n}, {c.span_size, (void*)dst->span_size, 4 * n},
-      {c.name_len, (void*)dst->name_len, 4 * n}, {c.attr_match, (void*)dst->attr_match, 8 * n},
+      {c.name_len, (void*)dst->name_len, 4 * n},
+      {c.attr_match, (void*)dst->attr_match, 8 * n * std::max<uint32_t>(1, c.attr_match_words)},
       {c.res_svc, (void*)dst->res_svc, 4 * R}, {c.res_svc_str, (void*)dst->res_svc_str, 4 * R},
       {c.res_url_ok, (void*)dst->res_url_ok, R}, {c.res_attrset, (void*)dst->res_attrset, 4 * R},
       {c.res_size, (void*)dst->res_size, 4 * R}, {c.scope_size, (void*)dst->scope_size, 4 * S},

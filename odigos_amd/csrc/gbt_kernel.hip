@@ -248,7 +248,8 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_append_kernel(GbtArgs a) {
   P.url_flags[p] = c.url_flags ? c.url_flags[i] : 0;
   P.span_size[p] = c.span_size ? c.span_size[i] : 0;
   P.name_len[p] = c.name_len ? c.name_len[i] : 0;
-  P.attr_match[p] = c.attr_match ? c.attr_match[i] : 0;
+  for (uint32_t w = 0; w < a.attr_words; w++)
+    P.attr_match[w * a.pool_cap + p] = c.attr_match ? c.attr_match[w * a.n + i] : 0;
   P.origin[p] = a.scope_pos + c.scope[i];
 }
 
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_gather_kernel(GbtArgs a) {
   O.url_flags[j] = P.url_flags[p];
   O.span_size[j] = P.span_size[p];
   O.name_len[j] = P.name_len[p];
-  O.attr_match[j] = P.attr_match[p];
+  for (uint32_t w = 0; w < a.attr_words; w++) O.attr_match[w * a.n + j] = P.attr_match[w * a.pool_cap + p];
   uint32_t head = 1;
   if (j > 0) {
     const uint64_t q = (a.pool_pos + a.order[j - 1]) % a.pool_cap;

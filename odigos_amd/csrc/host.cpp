@@ -52,6 +52,7 @@ void HostBatch::bind() {
   cols.scope_size = scope_size.data();
   cols.scope_resource = scope_resource.data();
   cols.attr_match = attr_match.data();
+  cols.attr_match_words = attr_words;
   cols.attr_type = cols.n_attr_keys ? attr_type.data() : nullptr;
   cols.attr_val = cols.n_attr_keys ? attr_val.data() : nullptr;
   outs.keep = keep.data();
@@ -168,7 +169,7 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
         hb->scope.push_back(scope_idx);
         hb->span_size.push_back(sc.span_size);
         hb->name_len.push_back(sc.name_len);
-        hb->attr_match.push_back(sc.attr_match);
+        hb->attr_match.insert(hb->attr_match.end(), sc.attr_match.begin(), sc.attr_match.end());   // span-major here
         for (size_t k = 0; k < nk; k++) {
           uint64_t v = sc.attr_val[k];
           if (sc.attr_type[k] == OSE_ATTR_STR) {
@@ -226,6 +227,17 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
     if (v->empty()) v->push_back(0);
   for (auto* v : {&hb->status, &hb->kind, &hb->url_flags, &hb->res_url_ok})
     if (v->empty()) v->push_back(0);
+  {
+    // attr_match: span-major while built, word-major in the columns (ose_columns.attr_match_words)
+    const size_t n = hb->start.size(), W = std::max<size_t>(1, (ctx_.attr_preds.size() + 63) / 64);
+    if (W > 1) {
+      std::vector<uint64_t> t(n * W);
+      for (size_t i = 0; i < n; i++)
+        for (size_t w = 0; w < W; w++) t[w * n + i] = hb->attr_match[i * W + w];
+      hb->attr_match.swap(t);
+    }
+    hb->attr_words = (uint32_t)W;
+  }
   for (auto* v : {&hb->trace_id, &hb->start, &hb->end, &hb->attr_match})
     if (v->empty()) v->push_back(0);
   if (hb->path.empty()) hb->path.push_back(ose_strref{0, 0});
@@ -352,7 +364,7 @@ int TracesProcessor::ProcessTraces(Traces& td, double* phase_s) {
   cp(c->res_size, hb->cols.res_size, 4 * R);
   cp(c->scope_size, hb->cols.scope_size, 4 * S);
   cp(c->scope_resource, hb->cols.scope_resource, 4 * S);
-  cp(c->attr_match, hb->cols.attr_match, 8 * n);
+  cp(c->attr_match, hb->cols.attr_match, 8 * n * std::max<uint32_t>(1, hb->cols.attr_match_words));
   if (hb->cols.n_attr_keys) {
     cp(c->attr_type, hb->cols.attr_type, (size_t)hb->cols.n_attr_keys * n);
     cp(c->attr_val, hb->cols.attr_val, 8 * (size_t)hb->cols.n_attr_keys * n);

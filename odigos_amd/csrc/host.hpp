@@ -32,6 +32,7 @@ struct HostBatch {
   ose_outputs outs{};
   std::vector<uint8_t> arena;               // 16-byte aligned via arena_storage
   std::vector<uint64_t> trace_id, start, end, attr_match;
+  uint32_t attr_words = 1;   // attr_match words per span (word-major)
   std::vector<uint8_t> status, kind, url_flags;
   std::vector<uint32_t> resource, scope, span_size, name_len;
   std::vector<ose_strref> path, route;

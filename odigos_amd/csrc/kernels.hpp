@@ -216,6 +216,8 @@ struct TraceKernelArgs {
   uint32_t* batch_keep;       // kTraceBatch: the call's decision (read by the SIZE stage)
   const uint64_t* route_match;// optional precomputed endpoint bits (ose_columns.route_match)
   const uint64_t* attr_match; // span_attribute bits (null when no such rule)
+  uint64_t attr_stride;       // attr_match: word w of span i at [w * attr_stride + i]
+  uint32_t attr_words;
   const uint64_t* svc_match;  // owner-side records: OR of service_name + span_attribute rule bits (replaces both)
   uint32_t ablate;            // diagnostics only (OSE_TRACE_ABLATE, tools/ablate_trace.py): skip parts
   // kTraceRuns: runs still open kLongSteps steps past their owner's windows
@@ -321,6 +323,8 @@ struct ShardArgs {
   const uint64_t* route_match;
   uint64_t rm_stride;         // route_match: plane k (rule chunk k) at k * rm_stride (0: one plane)
   const uint64_t* attr_match;
+  uint64_t attr_stride;       // attr_match: word w of span i at [w * attr_stride + i]
+  uint32_t attr_words;
   const uint32_t* res_svc;
   const uint32_t* res_svc_str;
   const uint8_t* const* cfgs;  // [n_chunks] SampCfgDev blobs (device array of the rule chunks' tables)
@@ -381,8 +385,9 @@ struct AttrArgs {
   const uint8_t* arena;
   const uint32_t* resource;
   const uint32_t* res_svc;
+  uint32_t words;              // attr_match words per span (word-major planes of n_spans)
   const uint64_t* host_bits;   // may be null
-  uint64_t host_mask;
+  const uint64_t* host_mask;   // [words] the shim-evaluated rules
   const uint8_t* cfg;          // AttrCfgDev blob
   uint64_t* out;
 };
@@ -691,7 +696,7 @@ struct GbtArgs {
   uint64_t num_traces;
   uint64_t live_lo, live_hi;  // traces an added span may join (and the rebuild range)
   uint32_t add_gen;           // number of this add (tags the ids it numbers)
-  uint32_t _pad0;
+  uint32_t attr_words;        // attr_match words per span (word-major: batch, pool and released planes)
   uint64_t arena_room;        // string bytes the arena ring can still take
   const uint32_t* totals;     // [0] new traces, [1] string bytes of the batch (scans)
   // add: the batch

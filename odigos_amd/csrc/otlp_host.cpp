@@ -234,6 +234,12 @@ OtlpEngine* otlp_engine(Engine* e, int& rc) {
     delete o;
     return nullptr;
   }
+  if (plan.rule_key.size() > 64) {   // the decoder's per-resource rule word and attr_match are one 64-bit word
+    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 64 span_attribute rules (columnise with ose_batch_* / "
+                           "ose_process_device, whose attr_match takes any number of words)");
+    delete o;
+    return nullptr;
+  }
   o->n_attr_keys = (uint32_t)plan.keys.size();
   for (size_t k = 0; k < plan.keys.size(); k++) roles[plan.keys[k]] |= kRoleAttr0 << k;
   for (size_t k = 0; k < plan.rule_key.size(); k++)
@@ -329,7 +335,7 @@ bool resolve_resource(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p
   cr.svc = rc.svc;
   cr.svc_str = rc.svc_str;
   cr.ok = rc.url_ok;
-  cr.attr_res = rc.attr_res;
+  cr.attr_res = rc.attr_res.empty() ? 0 : rc.attr_res[0];   // <= 64 rules here (otlp_engine)
   cr.rpart = (uint32_t)flen(sizer.attrs(attrs, 1) + (dropped ? 1 + sov64(dropped) : 0));   // Resource: always emitted
   const std::string_view key = resf.size() == 1 ? std::string_view((const char*)p + resf[0].first, resf[0].second)
                                                 : std::string_view();
@@ -1369,12 +1375,14 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     return r;
   };
   SpanCols sc;
+  std::vector<uint64_t> res_words;
   for (uint32_t q = 0; q < cnt; q++) {
     const uint32_t i = list[q];
     const uint64_t ref = b->span_ref[i];
     Span sp;
     if (!pb_span(pb + (uint32_t)ref, (size_t)(ref >> 32), sp)) return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
-    columnize_span(o->ctx, sp, attr_res[(*sres)[i]], sizer, sc);
+    res_words.assign(1, attr_res[(*sres)[i]]);
+    columnize_span(o->ctx, sp, res_words, sizer, sc);
     OtlpFix& x = fix[q];
     x = OtlpFix{};
     x.idx = i;
@@ -1382,7 +1390,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     x.lo = sc.lo;
     x.start = sc.start;
     x.end = sc.end;
-    x.attr_match = sc.attr_match;
+    x.attr_match = sc.attr_match.empty() ? 0 : sc.attr_match[0];
     x.status = sc.status;
     x.kind = sc.kind;
     x.url_flags = sc.url_flags;

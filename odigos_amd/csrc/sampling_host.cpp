@@ -188,8 +188,6 @@ int Engine::build_sampling_tables() {
       n_attr += r.rtype == RuleType::SpanAttribute;
       n_lat += r.rtype == RuleType::HttpLatency;
     }
-  if (n_attr > 64)
-    return fail(OSE_ENOTSUP, "more than 64 span_attribute rules are not supported (one 64-bit attr_match word per span)");
   sampling_lat_svc.assign(std::max<size_t>(1, (service_ids.size() + 31) / 32), 0u);
   for (const PickedRule& pr : all)
     if (pr.r->rtype == RuleType::HttpLatency) {
@@ -417,6 +415,8 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     const int ar = resolve_attr_match(e, c, ws, st, &am);
     if (ar) return ar;
     a.attr_match = e->sampling_n_attr && e->sampling_chunk_attr[chunk] ? am : nullptr;
+    a.attr_stride = n;
+    a.attr_words = e->attr_words;
   }
   a.svc_match = c->svc_match ? c->svc_match + plane : nullptr;
 #if OSE_DIAG

@@ -503,6 +503,8 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
       return rc;
     }
     a.attr_match = e->sampling_n_attr ? am : nullptr;
+    a.attr_stride = n;
+    a.attr_words = e->attr_words;
   }
   a.res_svc = c->res_svc;
   a.res_svc_str = c->res_svc_str;

@@ -737,9 +737,10 @@ AttrPlan plan_attr_rules(const SamplingConfig& c) {
   for (auto* lvl : {&c.global_rules, &c.service_rules, &c.endpoint_rules})
     for (auto& r : *lvl) {
       if (r.rtype != RuleType::SpanAttribute) continue;
+      if ((size_t)k / 64 >= p.host_mask.size()) p.host_mask.push_back(0);
       if (r.attr.condition_type == "json") {
         p.rule_key.push_back(-1);
-        if (k < 64) p.host_mask |= 1ull << k;
+        p.host_mask[k / 64] |= 1ull << (k % 64);
       } else {
         auto it = std::find(p.keys.begin(), p.keys.end(), r.attr.attribute_key);
         if (it == p.keys.end()) it = p.keys.insert(p.keys.end(), r.attr.attribute_key);

@@ -64,7 +64,8 @@ class SpanAttrPredicate {
 struct AttrPlan {
   std::vector<std::string> keys;   // distinct attribute_key of the GPU rules, level order
   std::vector<int> rule_key;       // per span_attribute rule (level order): key column, -1 = shim
-  uint64_t host_mask = 0;          // attr_match bits the shim still computes
+  std::vector<uint64_t> host_mask; // attr_match bits the shim still computes ((rules + 63) / 64 words)
+  bool host(size_t k) const { return k / 64 < host_mask.size() && ((host_mask[k / 64] >> (k % 64)) & 1); }
 };
 AttrPlan plan_attr_rules(const SamplingConfig& c);
 

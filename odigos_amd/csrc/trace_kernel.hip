@@ -188,6 +188,20 @@ __device__ __forceinline__ Cfg load_cfg(const uint8_t* b) {
   return c;
 }
 
+// The span_attribute bits of span j under a rule chunk's tables: its rules'
+// attr_match bits [attr_base, attr_base + n_attr) (one 64-bit window: a
+// chunk holds at most 64 service + span_attribute bits; attr_match is
+// word-major, `words` planes of `stride` spans), placed after the chunk's
+// service-rule bits
+__device__ __forceinline__ uint64_t chunk_attr_bits(const uint64_t* am, uint64_t stride, uint32_t words,
+                                                    const SampCfgDev* h, uint64_t j) {
+  const uint32_t b = h->attr_base, w0 = b >> 6, sh = b & 63, na = h->n_attr;
+  if (!na) return 0;
+  uint64_t x = am[(uint64_t)w0 * stride + j] >> sh;
+  if (sh && w0 + 1 < words) x |= am[(uint64_t)(w0 + 1) * stride + j] << (64 - sh);
+  return (na >= 64 ? x : x & ((1ull << na) - 1)) << h->attr_shift;
+}
+
 struct Lat {
   uint32_t f;
   uint64_t m, e;
@@ -839,7 +853,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         svcb = r.svm;
       } else {
         if (a.mode != kTraceBatch && ss < nsvc) svcb = c.svc_bits[ss];
-        if (a.attr_match) svcb |= (a.attr_match[r.i] >> c.h->attr_base) << c.h->attr_shift;
+        if (a.attr_match) svcb |= chunk_attr_bits(a.attr_match, a.attr_stride, a.attr_words, c.h, r.i);
       }
       if (s < nsvc) {
         slot = c.svc_slot[s];
@@ -1031,7 +1045,7 @@ struct LongRaw {
   uint64_t st, en, am, rm, svm;
   ose_strref rt;
 };
-__device__ __forceinline__ LongRaw long_raw(const TraceKernelArgs& a, uint64_t p, uint64_t hi) {
+__device__ __forceinline__ LongRaw long_raw(const TraceKernelArgs& a, const SampCfgDev* h, uint64_t p, uint64_t hi) {
   LongRaw r{};
   if (p >= hi) return r;
   r.res = a.resource[p];
@@ -1040,7 +1054,7 @@ __device__ __forceinline__ LongRaw long_raw(const TraceKernelArgs& a, uint64_t p
     r.st = a.start[p];
     r.en = a.end[p];
   }
-  if (a.attr_match) r.am = a.attr_match[p];
+  if (a.attr_match) r.am = chunk_attr_bits(a.attr_match, a.attr_stride, a.attr_words, h, p);
   if (a.svc_match) r.svm = a.svc_match[p];
   if (a.route_match) r.rm = a.route_match[p];
   else if (a.route) r.rt = a.route[p];
@@ -1102,7 +1116,7 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
     uint32_t err = 0;
     uint64_t ep_acc = 0, svc_acc = 0, kmask = 0;
     Lat cur{0, kInf, 0};   // lane k: latency slot k
-    LongRaw nx = long_raw(a, lo + lane, hi);
+    LongRaw nx = long_raw(a, c.h, lo + lane, hi);
     for (uint64_t base = lo; base < hi; base += kWave) {
       const uint64_t p = base + lane;
       const bool valid = p < hi;
@@ -1115,7 +1129,7 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
         if (want_route && r.rt.len && sv < nsvc && c.svc_slot[sv] != kNoSlot)
           rw = head16(a.arena, r.rt.off, r.rt.len);
       }
-      if (base + kWave < hi) nx = long_raw(a, p + kWave, hi);
+      if (base + kWave < hi) nx = long_raw(a, c.h, p + kWave, hi);
       uint32_t slot = kNoSlot;
       uint64_t st = 0, en = 0;
       const uint32_t rst = (r.status & kStatusReset) ? 1u : 0u;
@@ -1125,7 +1139,7 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
           svc_acc |= r.svm;
         } else {
           if (ss < nsvc) svc_acc |= c.svc_bits[ss];
-          svc_acc |= (r.am >> c.h->attr_base) << c.h->attr_shift;
+          svc_acc |= r.am;
         }
         if (sv < nsvc) {
           slot = c.svc_slot[sv];
@@ -1335,7 +1349,7 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
         } else {
           const uint32_t ss = a.res_svc_str[res];
           if (ss < nsvc) svcb |= c.svc_bits[ss];
-          if (a.attr_match) svcb |= (a.attr_match[q] >> c.h->attr_base) << c.h->attr_shift;
+          if (a.attr_match) svcb |= chunk_attr_bits(a.attr_match, a.attr_stride, a.attr_words, c.h, q);
         }
         if (sv >= nsvc) continue;
         const uint32_t slt = c.svc_slot[sv];
@@ -1594,7 +1608,7 @@ __device__ __forceinline__ void x_chunk(const ShardArgs& a, const Cfg& c, const 
   const uint32_t nsvc = c.h->n_services;
   const uint32_t ss = a.res_svc_str[x.res];
   svcb = ss < nsvc ? c.svc_bits[ss] : 0;
-  if (a.attr_match && c.h->n_attr) svcb |= (a.attr_match[j] >> c.h->attr_base) << c.h->attr_shift;
+  if (a.attr_match) svcb |= chunk_attr_bits(a.attr_match, a.attr_stride, a.attr_words, c.h, j);
   if (x.sv != kXNone) {
     const uint32_t slot = c.svc_slot[x.sv];
     if (slot != kNoSlot)

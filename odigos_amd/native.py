@@ -74,7 +74,7 @@ COLUMN_FIELDS = [
 class Columns(C.Structure):
     _fields_ = [
         ("n_spans", C.c_uint64), ("n_resources", C.c_uint32), ("n_scopes", C.c_uint32),
-        ("n_attrsets", C.c_uint32), ("_pad", C.c_uint32), ("arena_bytes", C.c_uint64),
+        ("n_attrsets", C.c_uint32), ("attr_match_words", C.c_uint32), ("arena_bytes", C.c_uint64),
     ] + [(f, _p) for f in COLUMN_FIELDS] + [("svc_match", _p), ("n_attr_keys", C.c_uint32), ("match_planes", C.c_uint32),
                                             ("attr_type", _p), ("attr_val", _p)]
 
@@ -152,6 +152,7 @@ def lib() -> C.CDLL:
         "ose_gbt_stats": (C.c_int, [_p, C.POINTER(C.c_uint64)]),
         "ose_gbt_download": (C.c_int, [_p, C.POINTER(Columns)]),
         "ose_engine_attr_key": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
+        "ose_engine_attr_host_rules": (C.c_uint32, [_p, C.POINTER(C.c_uint64), C.c_uint32]),
         "ose_engine_set_option": (C.c_int, [_p, C.c_char_p, C.c_int64]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),
         "ose_batch_columns": (C.POINTER(Columns), [_p]),

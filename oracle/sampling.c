@@ -168,8 +168,10 @@ static eval_t eval_attr(const orc_rule* r, const orc_attr_cond* cond, int attr_i
     }
     return (eval_t){0, 0, r->fallback};
   }
+  /* bit attr_index of the span's attr_match words (word-major planes, ose_columns.attr_match_words) */
+  const uint64_t plane = (uint64_t)(attr_index / 64) * c->n_spans;
   for (uint64_t k = 0; k < t->n; k++)
-    if ((c->attr_match[t->spans[k]] >> attr_index) & 1) return (eval_t){1, 1, r->ratio};
+    if ((c->attr_match[plane + t->spans[k]] >> (attr_index % 64)) & 1) return (eval_t){1, 1, r->ratio};
   return (eval_t){0, 0, r->fallback};
 }
 

@@ -231,14 +231,19 @@ def concat_sampling_columns(sources):
     cat["arena"] = np.concatenate([g.array("arena")[: g.cols.arena_bytes] for g in sources] + [np.zeros(64, np.uint8)])
     for f in ("res_svc", "res_svc_str"):
         cat[f] = np.concatenate([g.array(f).view(np.uint32)[: g.cols.n_resources] for g in sources])
+    W = 1
     if all(getattr(g, "attr_bits", None) is not None for g in sources):   # the shim's span_attribute bits
-        cat["attr_match"] = np.concatenate([np.asarray(g.attr_bits, np.uint64)[: g.cols.n_spans] for g in sources])
+        # word-major planes: plane w of the global batch is the sources' planes w, concatenated
+        planes = [np.asarray(g.attr_bits, np.uint64).reshape(-1, g.cols.n_spans) for g in sources]
+        W = planes[0].shape[0]
+        cat["attr_match"] = np.concatenate([np.concatenate([p[w] for p in planes]) for w in range(W)])
     assert cat["arena"].size < 2**32
     from odigos_amd import native
     cols = native.Columns()
     cols.n_spans = sum(g.cols.n_spans for g in sources)
     cols.n_resources = int(roff[-1])
     cols.arena_bytes = int(aoff[-1])
+    cols.attr_match_words = W
     for f, a in cat.items():
         setattr(cols, f, a.ctypes.data)
     offs = np.cumsum([0] + [g.cols.n_spans for g in sources])

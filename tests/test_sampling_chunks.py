@@ -21,7 +21,8 @@ from odigos_amd import native
 from odigos_amd.batch import Generator
 from tests.oracle_lib import intern_services, lib as orc_lib
 from tests.test_sampling_random import SEED, _arr, _group, _py_eval, gpu_vs_oracle, inject_zero_starts, oracle_run
-from tests.workloads import check_interning, long_routes_config, wide_attr_config, wide_latency_config, wide_mixed_config
+from tests.workloads import (check_interning, long_routes_config, wide_attr100_config, wide_attr_config,
+                             wide_latency_config, wide_mixed_config)
 
 CONFIGS = {"latency": wide_latency_config, "mixed": wide_mixed_config, "long_routes": long_routes_config}
 
@@ -59,10 +60,14 @@ def test_chunk_refusals():
     attr = {"global_rules": [{"name": f"a{j}", "type": "span_attribute",
                               "rule_details": {"service_name": "s", "attribute_key": "k", "condition_type": "string",
                                                "operation": "equals", "expected_value": "v", "sampling_ratio": 1}}
-                             for j in range(65)]}
-    assert L.osehost_sampling_chunks(json.dumps({"odigossampling": attr}).encode(), C.byref(n)) == native.OSE_ENOTSUP
-    attr["global_rules"].pop()
+                             for j in range(64)]}
     assert L.osehost_sampling_chunks(json.dumps({"odigossampling": attr}).encode(), C.byref(n)) == 0 and n.value == 1
+    # past 64 span_attribute rules: more chunks, attr_match in more words
+    for k in (65, 130, 200):
+        attr["global_rules"] = [dict(attr["global_rules"][0], name=f"a{j}") for j in range(k)]
+        assert L.osehost_sampling_chunks(json.dumps({"odigossampling": attr}).encode(), C.byref(n)) == 0
+        assert n.value == (k + 63) // 64
+    assert _chunks(wide_attr100_config()) == 3        # 40 service + 24 attr bits, 64 attr, 12 attr
 
 
 @pytest.mark.parametrize("name", sorted(CONFIGS))
@@ -101,13 +106,16 @@ def test_gpu_wide_config(name, shuffle):
 
 def _attr_bits(g, rules, seed, p=0.02):
     # the shim's attr_match column for json span_attribute rules: bit k = the
-    # k-th span_attribute rule in level order met by the span
+    # k-th span_attribute rule in level order met by the span; past 64 rules
+    # word k // 64 (word-major planes, ose_columns.attr_match_words)
     rng = np.random.default_rng(seed)
     n = g.cols.n_spans
-    bits = np.zeros(n, dtype=np.uint64)
+    W = max(1, (rules + 63) // 64)
+    bits = np.zeros((W, n), dtype=np.uint64)
     for k in range(rules):
-        bits |= (rng.random(n) < p).astype(np.uint64) << np.uint64(k)
+        bits[k // 64] |= (rng.random(n) < p).astype(np.uint64) << np.uint64(k % 64)
     g.cols.attr_match = bits.ctypes.data
+    g.cols.attr_match_words = W
     return bits   # (the caller keeps it alive)
 
 
@@ -119,6 +127,20 @@ def test_gpu_wide_config_attr_bits_across_chunks(shuffle):
     g = Generator("sampling", seed=0x0D1607F1 + int(shuffle), n_spans=200_000, shuffle=shuffle)
     keep_alive = _attr_bits(g, 40, seed=17)
     ho = gpu_vs_oracle(g, cfg=wide_attr_config())
+    t = int(ho.view("trace_count", np.uint32)[0])
+    assert len(set(ho.view("trace_level", np.uint8)[:t].tolist())) >= 2
+    del keep_alive
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_gpu_attr_rules_past_64(shuffle):
+    # 100 span_attribute rules: attr_match in two words, the middle rule
+    # chunk's bits straddling them (attr_base 24: words 0 and 1)
+    check_interning(wide_attr100_config())
+    g = Generator("sampling", seed=0x0D160801 + int(shuffle), n_spans=300_000, shuffle=shuffle)
+    keep_alive = _attr_bits(g, 100, seed=23, p=0.01)
+    ho = gpu_vs_oracle(g, cfg=wide_attr100_config())
     t = int(ho.view("trace_count", np.uint32)[0])
     assert len(set(ho.view("trace_level", np.uint8)[:t].tolist())) >= 2
     del keep_alive
@@ -151,7 +173,7 @@ def test_gpu_wide_config_large():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["attr", "latency", "long_routes", "mixed"])
+@pytest.mark.parametrize("name", ["attr", "attr100", "latency", "long_routes", "mixed"])
 def test_gpu_wide_config_exchange_world3(name):
     # chunked rule lists through the trace-id exchange (ose_exchange_sample's
     # round at world 3, in-process transport): a record carries one endpoint
@@ -159,12 +181,12 @@ def test_gpu_wide_config_exchange_world3(name):
     # its plane; traces straddle ranks, and every rank's keep equals the
     # oracle on the concatenated global batch
     from tests.test_exchange import _concat_keep_oracle, _local_round
-    cfg = wide_attr_config() if name == "attr" else CONFIGS[name]()
+    cfg = {"attr": wide_attr_config, "attr100": wide_attr100_config}.get(name, CONFIGS.get(name))()
     sources = [Generator("sampling", seed=0x0D160811, n_spans=600_000, rank=r, world=3) for r in range(3)]
     for r, g in enumerate(sources):
         inject_zero_starts(g, 0.01, 30 + r)
-        if name == "attr":
-            g.attr_bits = _attr_bits(g, 40, seed=50 + r)
+        if name in ("attr", "attr100"):
+            g.attr_bits = _attr_bits(g, 40 if name == "attr" else 100, seed=50 + r, p=0.01)
     assert _chunks(cfg) >= 2
     got, stats = _local_round(sources, cfg)
     want = _concat_keep_oracle(sources, cfg)

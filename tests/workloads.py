@@ -93,6 +93,22 @@ def wide_attr_config():
             "endpoint_rules": [_wide_lat(300 + j, j % 64) for j in range(30)]}
 
 
+def wide_attr100_config():
+    """More than 64 span_attribute rules (attr_match in two 64-bit words): 40
+    service_name rules (services 0..39), then 100 json span_attribute rules
+    over services 0..63 in the service level (their bits 0..99: chunk cuts at
+    24 and 88, the middle chunk's bits straddle the two words), 20 latency
+    rules at the endpoint level."""
+    attr = [{"name": f"a{j}", "type": "span_attribute",
+             "rule_details": {"service_name": f"svc-{(40 + j) % 64:02d}", "attribute_key": "body",
+                              "condition_type": "json", "operation": "is_valid_json",
+                              "sampling_ratio": float((j * 29) % 101), "fallback_sampling_ratio": float(j % 9)}}
+            for j in range(100)]
+    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}],
+            "service_rules": [_wide_svc(k, k) for k in range(40)] + attr,
+            "endpoint_rules": [_wide_lat(500 + j, j % 64) for j in range(20)]}
+
+
 def long_routes_config():
     """Tables beyond the 12 KiB LDS budget through route bytes alone: 40
     latency rules whose http_route is ~400 bytes (the first 7 bytes match)."""
