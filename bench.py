@@ -75,9 +75,11 @@ WORKLOADS = {
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
     "sampling_wide": dict(gen="sampling", seed=0x0D160003, spans=50_000_000, per_gpu=True,
                           cfg="wide", stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
-                          fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
+                          fields=SAMPLE_FIELDS,
+                          kernels=("shard_pack", "owner_fold", "shard_unpack") + TRACE_KERNELS + SLOW_KERNELS,
                           metric_config="diagnostic: C3's batch under 1 error + 4 service + 150 latency rules "
-                                        "(three rule chunks, one trace-stage pass each)"),
+                                        "(three rule chunks: one pass over the columns into partial records "
+                                        "carrying every chunk's words, decided by the owner fold)"),
     "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000, per_gpu=True,
                  cfg=None, stages="SAMPLE|TEMPLATE", null_columns=("res_url_ok",), null_outputs=PER_TRACE_OUTS,
                  fields=SAMPLE_FIELDS + ("kind", "url_flags", "path"), kernels=TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS,
@@ -93,16 +95,17 @@ WORKLOADS = {
     "node8": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False, ranks=8,
                   cfg=None, stages="SAMPLE|TEMPLATE|SIZE", null_columns=("res_url_ok",),
                   null_outputs=PER_TRACE_OUTS + ("res_bytes",), fields=FUSED_FIELDS,
-                  kernels=("shard_pack", "shard_unpack") + TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS + SIZE_KERNELS,
+                  kernels=("shard_pack", "owner_fold", "shard_unpack") + TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS + SIZE_KERNELS,
                   metric_config="diagnostic: C4 at N=8 emulated on ONE GPU -- the 8 ranks' whole steps (pack, the "
                                 "exchange round through the in-process transport, owner SAMPLE, reverse split, "
                                 "TEMPLATE on a second stream, SIZE|APPLY_KEEP), one thread, engine and stream pair "
                                 "per rank; the projected per-GPU step is the wall time / 8"),
     "owner": dict(gen="fused", seed=0x0D160004, spans=100_000_000, per_gpu=False, sources=8,
                   cfg=None, stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
-                  fields=SAMPLE_FIELDS, kernels=("shard_unpack",) + TRACE_KERNELS + SLOW_KERNELS,
+                  fields=SAMPLE_FIELDS, kernels=("owner_fold", "shard_unpack") + TRACE_KERNELS + SLOW_KERNELS,
                   metric_config="C4 owner side on one GPU: the records trace owner 0 of 8 receives "
-                                "(8 source shards of the 100M-span C4 batch, rank order), unpack + SAMPLE"),
+                                "(8 source shards of the 100M-span C4 batch, rank order), decided by ose_shard_decide "
+                                "(the bucketed fold; unpack + SAMPLE when it overflows)"),
 }
 
 # node-collector res_attributes_keys (autoscaler/controllers/nodecollector/collectorconfig/ownmetrics-ui.go:33-47)
@@ -408,7 +411,7 @@ def main():
         eng.reserve(max(n_rec, 1))
 
         def step():
-            ex.unpack_sample(recv, n_rec)
+            ex.decide(recv, n_rec)
     else:
         if wl["per_gpu"]:
             gen = Generator(wl["gen"], seed=wl["seed"] + rank, n_spans=total, threads=gen_threads)
@@ -506,7 +509,7 @@ def main():
                       "exchange_record_bytes_per_span": native.XREC_BYTES * st_[0] / max(st_[2], 1)})
         out_kernels = dict(prof)
         extra["exchange_kernels_ms"] = {k: v["ms"] / max(args.steps, 1) for k, v in out_kernels.items()
-                                        if k in ("shard_pack", "shard_unpack", "owner_sample")}
+                                        if k in ("shard_pack", "owner_fold", "shard_unpack", "owner_sample")}
     if args.workload == "node8":
         st_ = [[int(x) for x in st] for st in stats]
         extra.update({"exchange_records_sent": sum(x[0] for x in st_),

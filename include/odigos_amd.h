@@ -418,6 +418,18 @@ int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t*
                      uint64_t* start_ns, uint64_t* end_ns, uint8_t* status, uint32_t* resource,
                      uint32_t* res_svc, uint32_t* res_svc_str, uint64_t* route_match,
                      uint64_t* svc_match, void* hip_stream);
+/* The owner's decisions for n received records (recv: the records of every
+ * source in source-rank order, as the all-to-all delivers them): keep[i] for
+ * record i.  The records are bucketed by trace-id hash and each bucket's
+ * traces are grouped, put in batch order and folded in LDS; a bucket past
+ * 512 records or a trace with more than 8 latency services sends the batch
+ * through ose_shard_unpack + ose_process_device(SAMPLE) instead (same
+ * decisions).  device_status (optional) as ose_outputs.device_status.  The
+ * calling thread waits once (the fold's overflow word).  Replaces, with
+ * ose_exchange_sample, the per-trace consumer behind the loadbalancing
+ * exporter (collectorconfig/traces.go:26-84).                             */
+int ose_shard_decide(ose_engine* eng, const void* recv, uint64_t n, uint32_t rec_bytes, uint8_t* keep,
+                     uint32_t* device_status, const ose_rand* rnd, void* hip_stream);
 int ose_shard_scatter_keep(const uint8_t* keep_back, const uint32_t* pack_pos, uint64_t n,
                            uint8_t* keep, void* hip_stream);
 
@@ -432,8 +444,8 @@ void ose_nccl_comm_destroy(void* comm);
 
 /* One exchange round for this rank's batch (device columns, as
  * ose_process_device): pack, all-to-all of the record counts, grouped
- * send/recv of the records over xGMI, unpack + the SAMPLE stage by trace id
- * for the traces this rank owns, the reverse split of the keep bytes and
+ * send/recv of the records over xGMI, ose_shard_decide for the traces this
+ * rank owns, the reverse split of the keep bytes and
  * the scatter into outs->keep.  Every rank of the communicator calls it for
  * the same round.  The calling thread waits once (the record counts size
  * the split).  stats (optional, [3]): records sent, records received, spans.

@@ -311,7 +311,7 @@ void launch_trace_compact(const TraceCompactArgs& a, hipStream_t st);
 // Trace-id exchange (ose_shard_*; trace_kernel.hip).
 struct ShardArgs {
   uint64_t n_spans;
-  uint32_t n_tiles;           // ceil(n / kSortTile)
+  uint32_t n_tiles;           // wave chunks: ceil(n / kXChunk)
   uint32_t n_ranks;           // <= 64
   const uint64_t* tid;
   const uint64_t* start;
@@ -332,18 +332,21 @@ struct ShardArgs {
   const uint32_t* lat_svc;    // bit s: service s has an http_latency rule in some chunk
   uint32_t* hist;             // [n_ranks * n_tiles] counts, then offsets (second buffer)
   uint32_t* hoff;
-  uint64_t* counts;           // [n_ranks] zeroed before launch
+  uint64_t* counts;           // [n_ranks] records per owner (shard_counts_kernel)
   uint8_t* send;              // [records * x_rec_bytes(n_chunks)], records <= n
   uint32_t* pack_pos;         // [n] slot of each span's record
 };
 // Partial record (trace_kernel.hip "trace-id exchange"): u64 words hi, lo,
 // min start, max end, {latency service 24 | flags 8}, then per rule chunk
 // the endpoint bits and the rule bits of that chunk's tables.
+constexpr uint32_t kXSteps = 16;                        // 64-span steps of one packing wave's chunk
+constexpr uint32_t kXChunk = kXSteps * 64;              // spans per packing wave
 constexpr uint32_t kXFixedWords = 5;
 constexpr uint32_t kXRecBytes = 8 * (kXFixedWords + 2);   // a one-chunk config (OSE_XREC_BYTES)
 constexpr uint32_t x_rec_words(uint32_t n_chunks) { return kXFixedWords + 2 * n_chunks; }
 constexpr uint32_t x_rec_bytes(uint32_t n_chunks) { return 8 * x_rec_words(n_chunks); }
 void launch_shard_hist(const ShardArgs& a, hipStream_t st);
+void launch_shard_counts(const ShardArgs& a, hipStream_t st);
 void launch_shard_scatter(const ShardArgs& a, hipStream_t st);
 struct UnpackArgs {
   const uint8_t* recv;
@@ -360,7 +363,38 @@ struct UnpackArgs {
   uint64_t* svc_match;
 };
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st);
+// Owner-side decisions straight from the received records (ose_shard_decide;
+// trace_kernel.hip "owner side"): records bucketed by trace-id hash, one
+// workgroup per bucket groups, orders and folds its traces in LDS.
+constexpr uint32_t kOwnerCap = 256;   // records one bucket holds (a fuller bucket: the general path)
+constexpr uint32_t kOwnerAvg = 80;    // records per bucket the host sizes the bucket count for
+constexpr uint32_t kOwnerSlotWords = 8;   // a bucket slot: hi, lo, min start, max end, {w4 | index << 32}, chunk 0's words, 0
+struct OwnerArgs {
+  const uint8_t* recv;        // n records of x_rec_words(n_chunks) words, in (source rank, source order)
+  uint64_t n;
+  uint32_t words;
+  uint32_t n_buckets;
+  uint32_t* bkt_count;        // [n_buckets], zeroed before the bucket pass
+  uint64_t* bkt_rec;          // [n_buckets * kOwnerCap * kOwnerSlotWords] the records' slots
+  const uint8_t* const* cfgs; // [n_chunks] SampCfgDev blobs
+  uint32_t n_chunks;
+  uint32_t cfg_lds_bytes;     // dynamic LDS: the largest chunk table without its route bytes (16-aligned)
+  uint64_t seed;
+  uint8_t* keep;              // [n] per record
+  uint32_t* overflow;         // set: a bucket past kOwnerCap records
+  uint64_t* clocks;           // OSE_DIAG builds: per-phase clocks of owner_fold_kernel (OSE_OWNER_CLOCKS), else null
+};
+void launch_owner_bucket(const OwnerArgs& a, hipStream_t st);
+void launch_owner_fold(const OwnerArgs& a, hipStream_t st);
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);
+// the in-process transport's pieces of one phase, moved by one launch
+struct PeerCopies {
+  const uint8_t* src[64];
+  uint8_t* dst[64];
+  uint64_t len[64];
+  uint32_t n;
+};
+void launch_peer_copies(const PeerCopies& c, uint64_t max_len, hipStream_t st);
 // dst[k] += src[k] (the in-process transport's counter all-reduce)
 void launch_add_i64(int64_t* dst, const int64_t* src, uint64_t n, hipStream_t st);
 uint32_t shard_owner_host(uint64_t hi, uint64_t lo, uint32_t n_ranks);

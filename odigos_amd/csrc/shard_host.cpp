@@ -11,11 +11,14 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <type_traits>
 #include <vector>
 
+#include "devcfg.hpp"
 #include "engine_internal.hpp"
 #include "kernels.hpp"
 
@@ -95,14 +98,17 @@ struct XBuf {
 };
 struct XScratch {
   std::mutex mu;
-  XBuf send, recv, pos, counts, keep_back, keep_x, cols;
+  XBuf send, recv, pos, counts, keep_back, keep_x, cols, bkt;
   uint64_t* host_counts = nullptr;   // pinned [2 * 64]
+  uint32_t* host_flag = nullptr;     // pinned: the owner fold's overflow word
+  bool last_general = false;         // the last owner_decide took the general path (osehost_owner_last_general)
   hipEvent_t done = nullptr;         // recorded at the end of the last round
   bool done_set = false;
   ~XScratch() {
-    for (XBuf* b : {&send, &recv, &pos, &counts, &keep_back, &keep_x, &cols})
+    for (XBuf* b : {&send, &recv, &pos, &counts, &keep_back, &keep_x, &cols, &bkt})
       if (b->p) (void)hipFree(b->p);
     if (host_counts) (void)hipHostFree(host_counts);
+    if (host_flag) (void)hipHostFree(host_flag);
     if (done) (void)hipEventDestroy(done);
   }
 };
@@ -230,7 +236,12 @@ struct LocalTransport final : XTransport {
     me.slen = slen;
     if (hipEventRecord(me.ready, st) != hipSuccess) return fail(OSE_EDEVICE, "hipEventRecord failed");
     if (int rc = g->barrier()) return rc;
+    // every peer's piece in one copy launch behind the peers' events (as
+    // RCCL's grouped send/recv moves them in one fused launch), not one
+    // hipMemcpyAsync per peer
     int err = 0;
+    PeerCopies pc{};
+    uint64_t max_len = 0;
     for (int p = 0; p < g->n_ranks && !err; p++) {
       const LocalGroup::Slot& src = g->slots[(size_t)p];
       if (src.slen[rank] != rlen[p]) {
@@ -238,9 +249,19 @@ struct LocalTransport final : XTransport {
         break;
       }
       if (!rlen[p]) continue;
-      if (hipStreamWaitEvent(st, src.ready, 0) != hipSuccess ||
-          hipMemcpyAsync(recv + roff[p], src.send + src.soff[rank], rlen[p], hipMemcpyDeviceToDevice, st) != hipSuccess)
-        err = fail(OSE_EDEVICE, "in-process exchange: device copy failed");
+      if (hipStreamWaitEvent(st, src.ready, 0) != hipSuccess) {
+        err = fail(OSE_EDEVICE, "hipStreamWaitEvent failed");
+        break;
+      }
+      pc.src[pc.n] = src.send + src.soff[rank];
+      pc.dst[pc.n] = recv + roff[p];
+      pc.len[pc.n] = rlen[p];
+      max_len = std::max(max_len, rlen[p]);
+      pc.n++;
+    }
+    if (!err) {
+      launch_peer_copies(pc, max_len, st);
+      if (hipGetLastError() != hipSuccess) err = fail(OSE_EDEVICE, "in-process exchange: device copy failed");
     }
     if (!err && hipEventRecord(me.done, st) != hipSuccess) err = fail(OSE_EDEVICE, "hipEventRecord failed");
     if (err) {
@@ -319,6 +340,149 @@ using namespace ose;
 
 namespace ose {
 namespace {
+// The owner's decisions for n received records (keep per record, recv in
+// (source rank, source order)): the bucketed fold (owner_fold_kernel), or,
+// when a bucket or a trace overflows it, the records unpacked into span
+// columns and the general SAMPLE stage (run lists, then the sort path).
+// The host waits once, for the fold's overflow word.
+int owner_decide(Engine* e, XScratch* xs, const uint8_t* recvb, uint64_t n_recv, uint32_t K, uint8_t* keep,
+                 uint32_t* device_status, const ose_rand* rnd, hipStream_t st) {
+  if (!n_recv) return 0;
+  const uint64_t RB = x_rec_bytes(K);
+  const uint64_t B = std::max<uint64_t>(1, (n_recv + kOwnerAvg - 1) / kOwnerAvg);
+  const size_t off_rec = align_up(64 + 4 * B, 256);
+  int rc;
+  if ((rc = xs->bkt.need(off_rec + 8 * kOwnerSlotWords * B * kOwnerCap))) return rc;
+  if (!xs->host_flag) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&xs->host_flag), 64, hipHostMallocDefault));
+  uint8_t* bb = xs->bkt.as<uint8_t>();
+  OwnerArgs oa{};
+  oa.recv = recvb;
+  oa.n = n_recv;
+  oa.words = x_rec_words(K);
+  oa.n_buckets = (uint32_t)B;
+  oa.overflow = reinterpret_cast<uint32_t*>(bb);
+  oa.bkt_count = reinterpret_cast<uint32_t*>(bb + 64);
+  oa.bkt_rec = reinterpret_cast<uint64_t*>(bb + off_rec);
+  oa.cfgs = reinterpret_cast<const uint8_t* const*>(e->shard_tables_dev);
+  oa.n_chunks = K;
+  for (const auto& blob : e->sampling_chunks_host)   // the tables the fold reads: everything before the route bytes
+    oa.cfg_lds_bytes = std::max(oa.cfg_lds_bytes,
+                                (reinterpret_cast<const SampCfgDev*>(blob.data())->bytes_off + 15u) & ~15u);
+  oa.seed = rnd ? rnd->seed : 0;
+  oa.keep = keep;
+  HIP_TRY(hipMemsetAsync(bb, 0, 64 + 4 * B, st));
+#if OSE_DIAG
+  static uint64_t* clocks = nullptr;   // per-phase ticks (OSE_OWNER_CLOCKS), printed after the call
+  if (getenv("OSE_OWNER_CLOCKS")) {
+    if (!clocks) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&clocks), 64));
+    HIP_TRY(hipMemsetAsync(clocks, 0, 64, st));
+    oa.clocks = clocks;
+  }
+#endif
+  Engine::Timed tf{};
+  e->prof_begin("owner_fold", st, tf);
+  launch_owner_bucket(oa, st);
+  launch_owner_fold(oa, st);
+  e->prof_end(tf, st);
+  HIP_TRY(hipGetLastError());
+#if OSE_DIAG
+  if (oa.clocks) {
+    uint64_t h[8];
+    HIP_TRY(hipMemcpyAsync(h, oa.clocks, 64, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    fprintf(stderr, "owner_fold clocks (10 ns ticks summed over workgroups): load %llu group %llu sort %llu fold %llu "
+            "keep %llu; records %llu buckets %llu\n", (unsigned long long)h[0], (unsigned long long)h[1],
+            (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4], (unsigned long long)n_recv,
+            (unsigned long long)B);
+  }
+#endif
+  HIP_TRY(hipMemcpyAsync(xs->host_flag, oa.overflow, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  xs->last_general = *xs->host_flag != 0;
+  if (!xs->last_general) return 0;
+  // the general path: owner-side columns (trace_id 16, start 8, end 8, route_match 8 K, svc_match 8 K,
+  // resource 4, res_svc 4, res_svc_str 4, status 1 per record)
+  const uint64_t R = n_recv;
+  const size_t o_tid = 0, o_st = align_up(o_tid + 16 * R, 256), o_en = align_up(o_st + 8 * R, 256),
+               o_rm = align_up(o_en + 8 * R, 256), o_sm = align_up(o_rm + 8 * R * K, 256),
+               o_res = align_up(o_sm + 8 * R * K, 256), o_sv = align_up(o_res + 4 * R, 256),
+               o_ss = align_up(o_sv + 4 * R, 256), o_stat = align_up(o_ss + 4 * R, 256), o_end = o_stat + R + 256;
+  if ((rc = xs->cols.need(o_end))) return rc;
+  uint8_t* cb = xs->cols.as<uint8_t>();
+  ose_columns oc{};
+  oc.n_spans = n_recv;
+  oc.n_resources = (uint32_t)n_recv;
+  oc.match_planes = K;   // route_match / svc_match: plane k for rule chunk k
+  oc.trace_id = reinterpret_cast<uint64_t*>(cb + o_tid);
+  oc.start_ns = reinterpret_cast<uint64_t*>(cb + o_st);
+  oc.end_ns = reinterpret_cast<uint64_t*>(cb + o_en);
+  oc.route_match = reinterpret_cast<uint64_t*>(cb + o_rm);
+  oc.svc_match = reinterpret_cast<uint64_t*>(cb + o_sm);
+  oc.resource = reinterpret_cast<uint32_t*>(cb + o_res);
+  oc.res_svc = reinterpret_cast<uint32_t*>(cb + o_sv);
+  oc.res_svc_str = reinterpret_cast<uint32_t*>(cb + o_ss);
+  oc.status = cb + o_stat;
+  Engine::Timed tm{};
+  e->prof_begin("shard_unpack", st, tm);
+  rc = ose_shard_unpack(recvb, n_recv, (uint32_t)RB, const_cast<uint64_t*>(oc.trace_id), const_cast<uint64_t*>(oc.start_ns),
+                        const_cast<uint64_t*>(oc.end_ns), const_cast<uint8_t*>(oc.status),
+                        const_cast<uint32_t*>(oc.resource), const_cast<uint32_t*>(oc.res_svc),
+                        const_cast<uint32_t*>(oc.res_svc_str), const_cast<uint64_t*>(oc.route_match),
+                        const_cast<uint64_t*>(oc.svc_match), st);
+  e->prof_end(tm, st);
+  if (rc) return rc;
+  ose_outputs ox{};
+  ox.keep = keep;
+  ox.device_status = device_status;
+  Engine::Timed to{};
+  e->prof_begin("owner_sample", st, to);
+  rc = run_stages(e, &oc, &ox, OSE_STAGE_SAMPLE, OSE_GROUP_TRACE_ID, rnd, st);
+  e->prof_end(to, st);
+  return rc;
+}
+
+}  // namespace
+
+// SAMPLE for a rule-chunked configuration on one GPU: the exchange's two
+// halves back to back with one rank.  ose_shard_pack folds the spans into
+// partial records that carry every chunk's endpoint and rule words (one
+// pass over the columns, instead of one trace stage per chunk), the records
+// are decided as an owner decides them (owner_decide: the bucketed fold,
+// which walks ShouldSample chunk by chunk), and keep goes back onto the
+// spans.  The host waits twice: for the record count and for the fold's
+// overflow word.
+int sample_by_records(Engine* e, const ose_columns* c, const ose_outputs* o, const ose_rand* rnd, hipStream_t st) {
+  const uint64_t n = c->n_spans;
+  if (!n) return 0;
+  if (!o->keep) return fail(OSE_EINVAL, "SAMPLE stage needs keep");
+  XScratch* xs = scratch_of(e);
+  std::lock_guard<std::mutex> g(xs->mu);
+  const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
+  const uint64_t RB = x_rec_bytes(K);
+  int rc;
+  if ((rc = xs->send.need(n * RB)) || (rc = xs->pos.need(4 * n)) || (rc = xs->counts.need(16)) ||
+      (rc = xs->keep_x.need(n)))
+    return rc;
+  if (!xs->host_counts) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&xs->host_counts), 16 * 64, hipHostMallocDefault));
+  if (!xs->done) HIP_TRY(hipEventCreateWithFlags(&xs->done, hipEventDisableTiming));
+  if (xs->done_set) HIP_TRY(hipStreamWaitEvent(st, xs->done, 0));
+  uint64_t* cnt_d = xs->counts.as<uint64_t>();
+  rc = ose_shard_pack(reinterpret_cast<ose_engine*>(e), c, 1, xs->send.p, cnt_d, xs->pos.as<uint32_t>(), st);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(xs->host_counts, cnt_d, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint64_t R = xs->host_counts[0];
+  if (R > n) return fail(OSE_EDEVICE, "internal: more records than spans");
+  rc = owner_decide(e, xs, xs->send.as<uint8_t>(), R, K, xs->keep_x.as<uint8_t>(), o->device_status, rnd, st);
+  if (rc) return rc;
+  launch_scatter_keep(xs->keep_x.as<uint8_t>(), xs->pos.as<uint32_t>(), n, o->keep, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(xs->done, st));
+  xs->done_set = true;
+  return 0;
+}
+
+namespace {
 // One exchange round (ose_exchange_sample).  Everything that can fail on
 // this rank alone (arguments, scratch) is checked before the first
 // collective; a failure after it leaves the peers inside a collective, so
@@ -368,15 +532,8 @@ int exchange_round(Engine* e, const ose_columns* cols, const ose_outputs* outs, 
   }
   const uint64_t n_recv = rd[W];
   if (n_recv > 0xFFFFFFF0ull) return abort_with(fail(OSE_ERANGE, "more than 2^32-16 records received"));
-  // owner-side columns: trace_id 16, start 8, end 8, route_match 8 K, svc_match 8 K, resource 4, res_svc 4,
-  // res_svc_str 4, status 1 per record
   const uint64_t R = std::max<uint64_t>(n_recv, 1);
-  const size_t o_tid = 0, o_st = align_up(o_tid + 16 * R, 256), o_en = align_up(o_st + 8 * R, 256),
-               o_rm = align_up(o_en + 8 * R, 256), o_sm = align_up(o_rm + 8 * R * K, 256),
-               o_res = align_up(o_sm + 8 * R * K, 256), o_sv = align_up(o_res + 4 * R, 256),
-               o_ss = align_up(o_sv + 4 * R, 256), o_stat = align_up(o_ss + 4 * R, 256), o_end = o_stat + R + 256;
-  if ((rc = xs->recv.need(R * RB)) || (rc = xs->keep_x.need(R)) || (rc = xs->cols.need(o_end)))
-    return abort_with(rc);
+  if ((rc = xs->recv.need(R * RB)) || (rc = xs->keep_x.need(R))) return abort_with(rc);
   // 3. the records (variable sizes per peer)
   std::vector<uint64_t> s_off(W), s_len(W), r_off(W), r_len(W);
   for (uint64_t p = 0; p < W; p++) {
@@ -388,40 +545,9 @@ int exchange_round(Engine* e, const ose_columns* cols, const ose_outputs* outs, 
   uint8_t* recvb = xs->recv.as<uint8_t>();
   if ((rc = tx.alltoallv(xs->send.as<uint8_t>(), s_off.data(), s_len.data(), recvb, r_off.data(), r_len.data(), st)))
     return abort_with(rc);
-  // 4. owner: unpack (source-rank order) + the SAMPLE stage by trace id
-  uint8_t* cb = xs->cols.as<uint8_t>();
-  ose_columns oc{};
-  oc.n_spans = n_recv;
-  oc.n_resources = (uint32_t)n_recv;
-  oc.match_planes = K;   // route_match / svc_match: plane k for rule chunk k
-  oc.trace_id = reinterpret_cast<uint64_t*>(cb + o_tid);
-  oc.start_ns = reinterpret_cast<uint64_t*>(cb + o_st);
-  oc.end_ns = reinterpret_cast<uint64_t*>(cb + o_en);
-  oc.route_match = reinterpret_cast<uint64_t*>(cb + o_rm);
-  oc.svc_match = reinterpret_cast<uint64_t*>(cb + o_sm);
-  oc.resource = reinterpret_cast<uint32_t*>(cb + o_res);
-  oc.res_svc = reinterpret_cast<uint32_t*>(cb + o_sv);
-  oc.res_svc_str = reinterpret_cast<uint32_t*>(cb + o_ss);
-  oc.status = cb + o_stat;
-  if (n_recv) {
-    Engine::Timed tm{};
-    e->prof_begin("shard_unpack", st, tm);
-    rc = ose_shard_unpack(recvb, n_recv, (uint32_t)RB, const_cast<uint64_t*>(oc.trace_id), const_cast<uint64_t*>(oc.start_ns),
-                          const_cast<uint64_t*>(oc.end_ns), const_cast<uint8_t*>(oc.status),
-                          const_cast<uint32_t*>(oc.resource), const_cast<uint32_t*>(oc.res_svc),
-                          const_cast<uint32_t*>(oc.res_svc_str), const_cast<uint64_t*>(oc.route_match),
-                          const_cast<uint64_t*>(oc.svc_match), st);
-    e->prof_end(tm, st);
-    if (rc) return abort_with(rc);
-    ose_outputs ox{};
-    ox.keep = xs->keep_x.as<uint8_t>();
-    ox.device_status = outs->device_status;
-    Engine::Timed to{};
-    e->prof_begin("owner_sample", st, to);
-    rc = run_stages(e, &oc, &ox, OSE_STAGE_SAMPLE, OSE_GROUP_TRACE_ID, rnd, st);
-    e->prof_end(to, st);
-    if (rc) return abort_with(rc);
-  }
+  // 4. owner: the decisions for the received records (source-rank order)
+  rc = owner_decide(e, xs, recvb, n_recv, K, xs->keep_x.as<uint8_t>(), outs->device_status, rnd, st);
+  if (rc) return abort_with(rc);
   // 5. decisions back to the sources (reverse split), 6. onto the spans
   std::vector<uint64_t> kb_off(sd.begin(), sd.end() - 1), kx_off(rd.begin(), rd.end() - 1);
   if ((rc = tx.alltoallv(xs->keep_x.as<uint8_t>(), kx_off.data(), rcv.data(), xs->keep_back.as<uint8_t>(), kb_off.data(),
@@ -469,7 +595,7 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipMemsetAsync(counts, 0, 8 * (size_t)n_ranks, st));
   if (n == 0) return 0;
-  const uint32_t T = (uint32_t)((n + kSortTile - 1) / kSortTile);
+  const uint32_t T = (uint32_t)((n + kXChunk - 1) / kXChunk);   // packing waves
   const uint64_t H = (uint64_t)n_ranks * T;
   const uint32_t htiles = (uint32_t)((H + kScanTileItems - 1) / kScanTileItems);
   Workspace* ws = e->acquire_ws(st);
@@ -535,6 +661,7 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
     sa.status = reinterpret_cast<uint64_t*>(base + off_st);
     sa.error = err;
     launch_scan_u32(sa, st);
+    launch_shard_counts(a, st);
     launch_shard_scatter(a, st);
     e->prof_end(tm, st);
     if (hipGetLastError() != hipSuccess) rc = fail(OSE_EDEVICE, "shard pack launch failed");
@@ -556,6 +683,28 @@ int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t*
                route_match, svc_match};
   launch_shard_unpack(a, static_cast<hipStream_t>(hip_stream));
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int ose_shard_decide(ose_engine* eng, const void* recv, uint64_t n, uint32_t rec_bytes, uint8_t* keep,
+                     uint32_t* device_status, const ose_rand* rnd, void* hip_stream) {
+  if (!eng) return fail(OSE_EINVAL, "NULL engine");
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_decide needs odigossampling on the engine");
+  const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
+  if (rec_bytes != x_rec_bytes(K)) return fail(OSE_EINVAL, "rec_bytes must be ose_shard_record_bytes(eng)");
+  if (n > 0xFFFFFFF0ull) return fail(OSE_ERANGE, "more than 2^32-16 records");
+  if (n && (!recv || !keep)) return fail(OSE_EINVAL, "NULL argument");
+  if (int brc = bind_device(e)) return brc;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  XScratch* xs = scratch_of(e);
+  std::lock_guard<std::mutex> g(xs->mu);
+  if (!xs->done) HIP_TRY(hipEventCreateWithFlags(&xs->done, hipEventDisableTiming));
+  if (xs->done_set) HIP_TRY(hipStreamWaitEvent(st, xs->done, 0));
+  const int rc = owner_decide(e, xs, static_cast<const uint8_t*>(recv), n, K, keep, device_status, rnd, st);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(xs->done, st));
+  xs->done_set = true;
   return 0;
 }
 
@@ -617,6 +766,15 @@ int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outp
 }
 
 // ---- test seam: in-process ranks (no RCCL) ---------------------------------------
+// test hook: 1 when the engine's last owner decision (ose_shard_decide or
+// the round's) fell back to the general path
+uint32_t osehost_owner_last_general(ose_engine* eng) {
+  if (!eng) return 0;
+  XScratch* xs = scratch_of(reinterpret_cast<Engine*>(eng));
+  std::lock_guard<std::mutex> g(xs->mu);
+  return xs->last_general ? 1u : 0u;
+}
+
 int osehost_xgroup_create(int n_ranks, void** out) {
   if (!out || n_ranks < 1 || n_ranks > 64) return fail(OSE_EINVAL, "n_ranks must be in 1..64");
   *out = new LocalGroup(n_ranks);

@@ -373,30 +373,29 @@ __device__ __forceinline__ void decide(const Cfg& c, uint32_t err, uint64_t ep, 
   }
 }
 
-// One chunk of a rule-chunked configuration: the same walk as decide() over
-// this chunk's rules (level order, config order), resumed from and saved to
-// the trace's FoldState; the last pass closes the remaining levels and
-// decides.  Pass by pass it is decide() over the whole rule list.
-__device__ void decide_chunk(const TraceKernelArgs& a, const Cfg& c, uint64_t first, uint32_t err, uint64_t ep,
-                             uint64_t lsat, uint64_t svc, double u, uint8_t& keep, uint8_t& level, double& ratio_out) {
-  FoldState s = a.fold_in ? a.fold_in[first] : FoldState{0.0, 0.0, 0u, 0u};
-  auto close = [&]() {   // the end of evaluateLevel for level s.level
-    if (s.flags & kFsSat) {
-      s.flags = kFsDone | (s.flags & kFsHaveMin);
-      return;
-    }
-    if ((s.flags & kFsMatched) && (!(s.flags & kFsHaveMin) || s.ratio < s.min_fb)) {
-      s.min_fb = s.ratio;
-      s.flags |= kFsHaveMin;
-    }
-    s.flags &= kFsHaveMin;
-    s.ratio = 0;
-    s.level++;
-  };
+// ShouldSample's walk (decide()) split at rule-chunk boundaries: walk_chunk
+// takes one chunk's rules (level order, config order) from the state s (the
+// open level, its evaluateLevel accumulators, the min fallback of the closed
+// levels) and leaves it there; walk_finish closes the remaining levels and
+// decides.  Chunk by chunk it is decide() over the whole rule list.
+__device__ __forceinline__ void walk_close(FoldState& s) {   // the end of evaluateLevel for level s.level
+  if (s.flags & kFsSat) {
+    s.flags = kFsDone | (s.flags & kFsHaveMin);
+    return;
+  }
+  if ((s.flags & kFsMatched) && (!(s.flags & kFsHaveMin) || s.ratio < s.min_fb)) {
+    s.min_fb = s.ratio;
+    s.flags |= kFsHaveMin;
+  }
+  s.flags &= kFsHaveMin;
+  s.ratio = 0;
+  s.level++;
+}
+__device__ void walk_chunk(const Cfg& c, FoldState& s, uint32_t err, uint64_t ep, uint64_t lsat, uint64_t svc) {
   for (uint32_t L = 0; L < 3 && !(s.flags & kFsDone); L++) {
     const uint32_t k0 = c.h->level_first[L], k1 = c.h->level_first[L + 1];
     if (k0 == k1) continue;
-    while (s.level < L && !(s.flags & kFsDone)) close();
+    while (s.level < L && !(s.flags & kFsDone)) walk_close(s);
     if (s.flags & kFsDone) break;
     for (uint32_t k = k0; k < k1; k++) {
       const SampRuleDev& r = c.rules[k];
@@ -428,14 +427,9 @@ __device__ void decide_chunk(const TraceKernelArgs& a, const Cfg& c, uint64_t fi
       }
     }
   }
-  if (a.fold_out) {   // more chunks follow: save the walk (this pass's keep is rewritten by the last)
-    a.fold_out[first] = s;
-    keep = 1;
-    level = 4;
-    ratio_out = 100.0;
-    return;
-  }
-  while (s.level < 3 && !(s.flags & kFsDone)) close();
+}
+__device__ __forceinline__ void walk_finish(FoldState& s, double u, uint8_t& keep, uint8_t& level, double& ratio_out) {
+  while (s.level < 3 && !(s.flags & kFsDone)) walk_close(s);
   if (s.flags & kFsDone) {
     level = (uint8_t)s.level;
     ratio_out = s.ratio;
@@ -449,6 +443,23 @@ __device__ void decide_chunk(const TraceKernelArgs& a, const Cfg& c, uint64_t fi
     ratio_out = 100.0;
     keep = 1;
   }
+}
+
+// One chunk of a rule-chunked configuration in a pass per chunk: the walk
+// resumed from and saved to the trace's FoldState (first: the trace's first
+// span); the last pass decides.
+__device__ void decide_chunk(const TraceKernelArgs& a, const Cfg& c, uint64_t first, uint32_t err, uint64_t ep,
+                             uint64_t lsat, uint64_t svc, double u, uint8_t& keep, uint8_t& level, double& ratio_out) {
+  FoldState s = a.fold_in ? a.fold_in[first] : FoldState{0.0, 0.0, 0u, 0u};
+  walk_chunk(c, s, err, ep, lsat, svc);
+  if (a.fold_out) {   // more chunks follow: save the walk (this pass's keep is rewritten by the last)
+    a.fold_out[first] = s;
+    keep = 1;
+    level = 4;
+    ratio_out = 100.0;
+    return;
+  }
+  walk_finish(s, u, keep, level, ratio_out);
 }
 // decide() or, in a rule-chunked pass, decide_chunk(); first: the trace's
 // first span in batch order (the FoldState index)
@@ -1574,30 +1585,51 @@ __device__ __forceinline__ uint32_t shard_owner(uint64_t hi, uint64_t lo, uint32
 }
 
 // one span of a 64-span step: its trace id and latency service (the record
-// boundary test) and, with `full`, its chunk-independent contributions
+// boundary test) and, with `full`, its chunk-independent contributions.
+// XRaw holds the span's column loads, issued one step ahead of their use
+// (a wave walks its chunk's steps in order, two steps of loads in flight).
+struct XRaw {
+  uint4 t;
+  uint32_t res, status;
+  uint64_t st, en;
+  ose_strref rt;
+};
+__device__ __forceinline__ XRaw x_load(const ShardArgs& a, uint64_t j, bool full) {
+  XRaw r{};
+  if (j >= a.n_spans) return r;
+  r.t = reinterpret_cast<const uint4*>(a.tid)[j];
+  r.res = a.resource[j];
+  if (!full) return r;
+  r.status = a.status[j];
+  if (a.start) r.st = a.start[j];
+  if (a.end) r.en = a.end[j];
+  if (a.route && !a.route_match) r.rt = a.route[j];
+  return r;
+}
 struct XSpan {
   bool valid;
   uint64_t hi, lo;
   uint32_t sv, res, err;
   uint64_t st, en;
+  ose_strref rt;
 };
-__device__ __forceinline__ XSpan x_span(const ShardArgs& a, uint32_t nsvc, uint64_t j, bool full) {
+__device__ __forceinline__ XSpan x_span(const ShardArgs& a, uint32_t nsvc, const XRaw& r, uint64_t j, bool full) {
   XSpan x{};
   x.valid = j < a.n_spans;
   x.sv = kXNone;
   if (!x.valid) return x;
-  const uint4 t = reinterpret_cast<const uint4*>(a.tid)[j];
-  x.hi = (uint64_t)t.x | ((uint64_t)t.y << 32);
-  x.lo = (uint64_t)t.z | ((uint64_t)t.w << 32);
-  x.res = a.resource[j];
+  x.hi = (uint64_t)r.t.x | ((uint64_t)r.t.y << 32);
+  x.lo = (uint64_t)r.t.z | ((uint64_t)r.t.w << 32);
+  x.res = r.res;
   const uint32_t s = a.res_svc[x.res];
   if (s < nsvc && ((a.lat_svc[s >> 5] >> (s & 31)) & 1u)) x.sv = s;
   if (!full) return x;
-  x.err = a.status[j] == OSE_STATUS_ERROR;
+  x.err = r.status == OSE_STATUS_ERROR;
   if (x.sv != kXNone) {
-    x.st = a.start ? a.start[j] : 0;
-    x.en = a.end ? a.end[j] : 0;
+    x.st = r.st;
+    x.en = r.en;
   }
+  x.rt = r.rt;
   return x;
 }
 // the span's endpoint bits and rule bits under rule chunk k's tables
@@ -1613,7 +1645,7 @@ __device__ __forceinline__ void x_chunk(const ShardArgs& a, const Cfg& c, const 
     const uint32_t slot = c.svc_slot[x.sv];
     if (slot != kNoSlot)
       ep = a.route_match ? a.route_match[(uint64_t)k * a.rm_stride + j] & c.slot_rules[slot]
-                         : endpoint_bits(c, slot, a.arena, a.route[j]);
+                         : endpoint_bits(c, slot, a.arena, x.rt);
   }
 }
 // record heads of the step (lane 0 always starts one) and tails (where a
@@ -1628,92 +1660,87 @@ __device__ __forceinline__ void x_bounds(const XSpan& x, int lane, uint64_t& hea
   tails = vm & nxt;
 }
 
-constexpr int kXRounds = kSortTile / kSortThreads;   // 64-span steps per wave per tile
-
+// Each wave packs one chunk of kXSteps consecutive 64-span steps, with no
+// block barriers: shard_hist_kernel counts the chunk's records per owner,
+// a scan over (owner, chunk) gives every (owner, chunk) its first slot, and
+// shard_scatter_kernel writes the records in source order (chunks, steps,
+// lanes), each wave advancing its own per-owner offsets (lane d: owner d).
+// The first form interleaved a block's four waves step by step and ranked
+// their records per owner through LDS with two block barriers per step.
 __global__ __launch_bounds__(kSortThreads) void shard_hist_kernel(ShardArgs a) {
-  __shared__ uint32_t hist[64];
+  __shared__ uint32_t hist[kSortThreads / kWave][64];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (t < 64) hist[t] = 0;
-  __syncthreads();
+  const uint32_t ch = blockIdx.x * (kSortThreads / kWave) + wv;
+  if (ch >= a.n_tiles) return;   // wave-uniform; no block barriers below
+  hist[wv][lane] = 0;
+  __builtin_amdgcn_wave_barrier();
   const uint32_t nsvc = load_cfg(a.cfgs[0]).h->n_services;
-  const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
-  for (int r = 0; r < kXRounds; r++) {
-    const uint64_t base = b + ((uint64_t)r * (kSortThreads / kWave) + wv) * kWave;
+  const uint64_t b0 = (uint64_t)ch * kXChunk;
+  XRaw nx = x_load(a, b0 + lane, false);
+  for (uint32_t s = 0; s < kXSteps; s++) {
+    const uint64_t base = b0 + (uint64_t)s * kWave;
     if (base >= a.n_spans) break;   // wave-uniform
-    const XSpan x = x_span(a, nsvc, base + lane, false);
+    const XRaw cur = nx;
+    if (s + 1 < kXSteps) nx = x_load(a, base + kWave + lane, false);
+    const XSpan x = x_span(a, nsvc, cur, base + lane, false);
     uint64_t heads, tails;
     x_bounds(x, lane, heads, tails);
-    if ((tails >> lane) & 1) atomicAdd(&hist[shard_owner(x.hi, x.lo, a.n_ranks)], 1u);
+    if ((tails >> lane) & 1) atomicAdd(&hist[wv][shard_owner(x.hi, x.lo, a.n_ranks)], 1u);
   }
-  __syncthreads();
-  if ((uint32_t)t < a.n_ranks) {
-    a.hist[(uint64_t)t * a.n_tiles + blockIdx.x] = hist[t];
-    if (hist[t]) atomicAdd((unsigned long long*)&a.counts[t], (unsigned long long)hist[t]);
-  }
+  __builtin_amdgcn_wave_barrier();
+  if ((uint32_t)lane < a.n_ranks) a.hist[(uint64_t)lane * a.n_tiles + ch] = hist[wv][lane];
+}
+// records per owner from the scanned (owner, chunk) offsets (a device-scope
+// atomic per wave and owner on n_ranks words serialised the count pass)
+__global__ __launch_bounds__(64) void shard_counts_kernel(ShardArgs a) {
+  const uint32_t d = threadIdx.x;
+  if (d >= a.n_ranks) return;
+  const uint64_t T = a.n_tiles;
+  const uint32_t lo = a.hoff[d * T];
+  const uint32_t hi = d + 1 < a.n_ranks ? a.hoff[(d + 1) * T] : a.hoff[d * T + T - 1] + a.hist[d * T + T - 1];
+  a.counts[d] = hi - lo;
 }
 
-// Stable bucketing of the records by owner (records keep source order inside
-// a bucket: tiles in order, rounds in order, waves in order, lanes in order)
-// and the records themselves; pack_pos[span] = its record's slot in `send`.
+// The records in source order; pack_pos[span] = its record's slot in `send`.
 __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a) {
-  constexpr int kW = kSortThreads / kWave;
-  __shared__ uint32_t goff[64], run[64];
-  __shared__ uint32_t wcnt[kW][64], woff[kW][64];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (t < 64) {
-    goff[t] = (uint32_t)t < a.n_ranks ? a.hoff[(uint64_t)t * a.n_tiles + blockIdx.x] : 0;
-    run[t] = 0;
-    for (int k = 0; k < kW; k++) wcnt[k][t] = 0;
-  }
-  __syncthreads();
+  const uint32_t ch = blockIdx.x * (kSortThreads / kWave) + wv;
+  if (ch >= a.n_tiles) return;   // wave-uniform; no block barriers below
+  uint32_t off = (uint32_t)lane < a.n_ranks ? a.hoff[(uint64_t)lane * a.n_tiles + ch] : 0u;
   const uint32_t nsvc = load_cfg(a.cfgs[0]).h->n_services;
   const uint32_t words = x_rec_words(a.n_chunks);
-  const uint64_t b = (uint64_t)blockIdx.x * kSortTile;
-  for (int r = 0; r < kXRounds; r++) {
-    const uint64_t base = b + ((uint64_t)r * kW + wv) * kWave;
-    const bool live = base < a.n_spans;   // wave-uniform; dead waves still take the barriers
-    XSpan x{};
-    uint64_t heads = 0, tails = 0;
-    if (live) {
-      x = x_span(a, nsvc, base + lane, true);
-      x_bounds(x, lane, heads, tails);
-    }
+  const uint64_t b0 = (uint64_t)ch * kXChunk;
+  XRaw nx = x_load(a, b0 + lane, true);
+  for (uint32_t s = 0; s < kXSteps; s++) {
+    const uint64_t base = b0 + (uint64_t)s * kWave;
+    if (base >= a.n_spans) break;   // wave-uniform
+    const XRaw cur = nx;
+    if (s + 1 < kXSteps) nx = x_load(a, base + kWave + lane, true);
+    const XSpan x = x_span(a, nsvc, cur, base + lane, true);
+    uint64_t heads, tails;
+    x_bounds(x, lane, heads, tails);
     const bool tail = (tails >> lane) & 1;
     // fold each record (inclusive segmented scans; invalid lanes are lone segments)
     const uint32_t h = x.valid ? (uint32_t)((heads >> lane) & 1) : 1u;
     uint32_t err = x.err;
     Lat v = x.sv != kXNone ? Lat{x.st == 0 ? 3u : 2u, x.st == 0 ? kInf : x.st, x.en} : Lat{0u, kInf, 0ull};
-    if (live) {
+    {
       uint64_t z0 = 0, z1 = 0;
       seg_or_scan(h, err, z0, z1);
       seg_lat_scan(h, v);
     }
-    // rank among this wave's records with the same owner
+    // slot: the owner's running offset + rank among this step's records of that owner
     const uint32_t d = tail ? shard_owner(x.hi, x.lo, a.n_ranks) : 0u;
-    uint64_t peers = __ballot(tail);
-#pragma unroll
-    for (int bit = 0; bit < 6; bit++) {
-      const uint64_t bal = __ballot((d >> bit) & 1u);
-      peers &= ((d >> bit) & 1u) ? bal : ~bal;
+    uint32_t pos = __shfl(off, (int)d, kWave);
+    uint64_t mine = 0;
+    for (uint32_t o = 0; o < a.n_ranks; o++) {
+      const uint64_t bo = __ballot(tail && d == o);
+      if (d == o) mine = bo;
+      if ((uint32_t)lane == o) off += (uint32_t)__popcll(bo);
     }
-    const uint32_t rank = __popcll(peers & lanemask_lt(lane));
-    const uint32_t cnt = __popcll(peers);
-    if (tail && rank == cnt - 1) wcnt[wv][d] = cnt;
-    __syncthreads();
-    if (t < 64) {
-      uint32_t acc = run[t];
-      for (int k2 = 0; k2 < kW; k2++) {
-        woff[k2][t] = acc;
-        acc += wcnt[k2][t];
-        wcnt[k2][t] = 0;
-      }
-      run[t] = acc;
-    }
-    __syncthreads();
-    uint32_t pos = 0;
+    pos += (uint32_t)__popcll(mine & lanemask_lt(lane));
     uint64_t* rec = nullptr;
     if (tail) {
-      pos = goff[d] + woff[wv][d] + rank;
       rec = reinterpret_cast<uint64_t*>(a.send) + (uint64_t)pos * words;
       const uint32_t flags = (err ? kXErr : 0u) | ((v.f & 2u) ? kXLat : 0u) | ((v.f & 1u) ? kXReset : 0u);
       rec[0] = x.hi;
@@ -1726,11 +1753,9 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     for (uint32_t k = 0; k < a.n_chunks; k++) {
       const Cfg c = load_cfg(a.cfgs[k]);
       uint64_t ep = 0, svcb = 0;
-      if (live) {
-        x_chunk(a, c, x, base + lane, k, ep, svcb);
-        uint32_t z = 0;
-        seg_or_scan(h, z, ep, svcb);
-      }
+      x_chunk(a, c, x, base + lane, k, ep, svcb);
+      uint32_t z = 0;
+      seg_or_scan(h, z, ep, svcb);
       if (tail) {
         rec[kXFixedWords + 2 * k] = ep;
         rec[kXFixedWords + 2 * k + 1] = svcb;
@@ -1770,6 +1795,244 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
   a.resource[i] = (uint32_t)i;   // one "resource" per record carries its latency service
 }
 
+// ---- owner side: decisions from the received records ------------------------------
+// A rank receives each trace it owns as pieces, one record per source
+// stretch, in (source rank, source order) = global batch order.
+// owner_bucket_kernel reads the records in order (coalesced) and moves each
+// into a 64-byte slot of its trace-id hash bucket (one atomic per record;
+// the slot keeps the record's index, since order inside a bucket is lost
+// here).  One workgroup per bucket (owner_fold_kernel):
+//   1. loads the bucket's slots (one round trip: slot t by thread t,
+//      issued with the count, not after it) into LDS and groups them by
+//      trace id with an LDS hash table (exact 128-bit compare): group = the
+//      entry that claimed the trace's slot;
+//   2. sorts the keys (group : 8 | record index : 32 | entry : 8) with a
+//      bitonic sort in LDS: every trace's records become adjacent and in
+//      batch order;
+//   3. folds each trace on one lane: the error bit, then chunk by chunk the
+//      endpoint and rule words, the latency monoid of each latency service
+//      (lat_comb in order: the zero-start reset is order-dependent; services
+//      taken one at a time in increasing id, so no per-lane arrays, which
+//      would live in scratch) and ShouldSample's walk (walk_chunk), and
+//      writes keep on every record of the trace.
+// This replaces unpacking into span columns and the general run-list path
+// (an exact table in HBM, run lists, one lane chasing a trace's runs through
+// the head masks).  Only a bucket past kOwnerCap records sets *overflow,
+// and the host then runs the general path on the whole batch.
+// Measured forms (owner workload): an index per slot with the records read
+// through it (two more dependent round trips per workgroup) and persistent
+// workgroups with the rule tables in LDS were slower (profiles/r4*_owner*).
+constexpr uint32_t kOwnerTable = 2 * kOwnerCap;   // LDS hash slots: load <= 1/2
+constexpr uint32_t kOwnerNone = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t owner_bucket_of(uint64_t h, uint32_t n_buckets) {
+  return (uint32_t)(((h & 0xFFFFFFFFull) * n_buckets) >> 32);   // the low half: owner = high half mod N
+}
+__global__ __launch_bounds__(256) void owner_bucket_kernel(OwnerArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t* r = reinterpret_cast<const uint64_t*>(a.recv) + i * a.words;
+  const uint64_t hi = r[0], lo = r[1], m = r[2], e = r[3], w4 = r[4], ep = r[kXFixedWords], sv = r[kXFixedWords + 1];
+  const uint32_t b = owner_bucket_of(tid_hash(hi, lo), a.n_buckets);
+  const uint32_t at = atomicAdd(&a.bkt_count[b], 1u);
+  if (at >= kOwnerCap) return;
+  uint4* d = reinterpret_cast<uint4*>(a.bkt_rec + ((uint64_t)b * kOwnerCap + at) * kOwnerSlotWords);
+  d[0] = make_uint4((uint32_t)hi, (uint32_t)(hi >> 32), (uint32_t)lo, (uint32_t)(lo >> 32));
+  d[1] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), (uint32_t)e, (uint32_t)(e >> 32));
+  d[2] = make_uint4((uint32_t)w4, (uint32_t)i, (uint32_t)ep, (uint32_t)(ep >> 32));
+  d[3] = make_uint4((uint32_t)sv, (uint32_t)(sv >> 32), 0u, 0u);
+}
+
+// One chunk's share of a trace's fold: the chunk's endpoint and rule words
+// ORed over the trace's entries [k, e) of the sorted keys, the latency
+// element of each latency service (in batch order; services one at a time
+// in increasing id), ShouldSample's walk over the chunk's rules
+__device__ void owner_chunk(const Cfg& c, const uint64_t* s_key, const uint32_t* s_w4, const uint64_t* s_m,
+                            const uint64_t* s_e, const uint64_t* s_ep, const uint64_t* s_sv, uint32_t k, uint32_t e,
+                            uint32_t err, bool any_lat, FoldState& s) {
+  uint64_t ep = 0, svc = 0;
+  for (uint32_t j = k; j < e; j++) {
+    const uint32_t x = (uint32_t)s_key[j] & 255u;
+    ep |= s_ep[x];
+    svc |= s_sv[x];
+  }
+  uint64_t lsat = 0;
+  const uint32_t nsvc = c.h->n_services;
+  uint32_t last = 0;
+  bool first = true;
+  while (any_lat) {
+    uint32_t nxt = kXNone;
+    for (uint32_t j = k; j < e; j++) {
+      const uint32_t w4 = s_w4[(uint32_t)s_key[j] & 255u];
+      const uint32_t sv = w4 & kXNone;
+      if (((w4 >> 24) & kXLat) && sv != kXNone && (first || sv > last) && sv < nxt) nxt = sv;
+    }
+    if (nxt == kXNone) break;
+    Lat l{0u, kInf, 0ull};
+    for (uint32_t j = k; j < e; j++) {
+      const uint32_t x = (uint32_t)s_key[j] & 255u;
+      const uint32_t w4 = s_w4[x];
+      if ((w4 & kXNone) != nxt || !((w4 >> 24) & kXLat)) continue;
+      l = lat_comb(l, Lat{2u | (((w4 >> 24) & kXReset) ? 1u : 0u), s_m[x], s_e[x]});
+    }
+    if (nxt < nsvc) {
+      const uint32_t slot = c.svc_slot[nxt];
+      if (slot != kNoSlot) lsat |= latency_satisfied(c, slot, ep, l.m, l.e);
+    }
+    last = nxt;
+    first = false;
+  }
+  walk_chunk(c, s, err, ep, lsat, svc);
+}
+
+// OSE_DIAG: wall-clock ticks per phase, summed over workgroups (thread 0
+// after a barrier; the diagnostic instance adds barriers between phases)
+#if OSE_DIAG
+#define OWNER_TICK(ph)                                                                       \
+  do {                                                                                       \
+    if (a.clocks) {                                                                          \
+      __syncthreads();                                                                       \
+      if (t == 0) {                                                                          \
+        const uint64_t now = wall_clock64();                                                 \
+        atomicAdd((unsigned long long*)&a.clocks[ph], (unsigned long long)(now - tick));     \
+        tick = now;                                                                          \
+      }                                                                                      \
+    }                                                                                        \
+  } while (0)
+#else
+#define OWNER_TICK(ph) \
+  do {                 \
+  } while (0)
+#endif
+
+// One workgroup per bucket; thread t holds entry t.  The rule tables of the
+// chunk being walked are copied into LDS without their route bytes (the
+// endpoint bits came with the records): every lookup of latency_satisfied
+// and walk_chunk is then a ds_read, not a dependent L2 round trip (with the
+// tables in HBM the fold was 89% of the kernel's clocks).
+__device__ __forceinline__ void owner_cfg_copy(const OwnerArgs& a, uint8_t* dst, uint32_t ck, uint32_t t) {
+  const uint8_t* src = a.cfgs[ck];
+  const uint32_t nb = (reinterpret_cast<const SampCfgDev*>(src)->bytes_off + 15u) & ~15u;   // <= cfg_lds_bytes
+  for (uint32_t k = t * 16; k < nb; k += 256 * 16)
+    *reinterpret_cast<uint4*>(dst + k) = *reinterpret_cast<const uint4*>(src + k);
+}
+__global__ __launch_bounds__(256) void owner_fold_kernel(OwnerArgs a) {
+  static_assert(kOwnerCap == 256, "one entry per thread; 8-bit entry and group indices");
+  extern __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[];
+  __shared__ uint64_t s_hi[kOwnerCap], s_lo[kOwnerCap], s_key[kOwnerCap];
+  __shared__ uint64_t s_m[kOwnerCap], s_e[kOwnerCap], s_ep[kOwnerCap], s_sv[kOwnerCap];
+  __shared__ uint32_t s_w4[kOwnerCap], s_tab[kOwnerTable];
+  const uint32_t t = threadIdx.x, b = blockIdx.x;
+  uint64_t tick = OSE_DIAG ? wall_clock64() : 0;
+  (void)tick;
+  // the slot load does not wait for the count: slot t is read whether or not
+  // it is filled (a bucket's slots are contiguous; unfilled ones are ignored)
+  const uint4* sl = reinterpret_cast<const uint4*>(a.bkt_rec + ((uint64_t)b * kOwnerCap + t) * kOwnerSlotWords);
+  const uint4 q0 = sl[0], q1 = sl[1], q2 = sl[2], q3 = sl[3];
+  const uint32_t cnt = a.bkt_count[b];
+  if (cnt == 0) return;   // block-uniform
+  if (cnt > kOwnerCap) {
+    if (t == 0) atomicOr(a.overflow, 1u);
+    return;
+  }
+  owner_cfg_copy(a, cfg_lds, 0, t);
+  s_tab[t] = kOwnerNone;
+  s_tab[t + 256] = kOwnerNone;
+  uint32_t ri = 0;
+  if (t < cnt) {
+    s_hi[t] = (uint64_t)q0.x | ((uint64_t)q0.y << 32);
+    s_lo[t] = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+    s_m[t] = (uint64_t)q1.x | ((uint64_t)q1.y << 32);
+    s_e[t] = (uint64_t)q1.z | ((uint64_t)q1.w << 32);
+    s_w4[t] = q2.x;
+    ri = q2.y;
+    s_ep[t] = (uint64_t)q2.z | ((uint64_t)q2.w << 32);
+    s_sv[t] = (uint64_t)q3.x | ((uint64_t)q3.y << 32);
+  }
+  uint32_t P = 1;
+  while (P < cnt) P <<= 1;
+  __syncthreads();
+  OWNER_TICK(0);
+  // 1. group by trace id; key = group : 8 | record index : 32 | entry : 8
+  if (t < P) {
+    uint64_t key = ~0ull;   // padding sorts last
+    if (t < cnt) {
+      const uint64_t hi = s_hi[t], lo = s_lo[t];
+      uint32_t slot = ((uint32_t)(tid_hash(hi, lo) >> 32) * 0x9E3779B1u) >> 23;   // 9 bits: kOwnerTable
+      uint32_t g = t;
+      for (;;) {   // the table never fills (cnt <= kOwnerTable / 2)
+        const uint32_t prev = atomicCAS(&s_tab[slot], kOwnerNone, t);
+        if (prev == kOwnerNone) break;
+        if (s_hi[prev] == hi && s_lo[prev] == lo) {
+          g = prev;
+          break;
+        }
+        slot = (slot + 1) & (kOwnerTable - 1);
+      }
+      key = ((uint64_t)g << 40) | ((uint64_t)ri << 8) | t;
+    }
+    s_key[t] = key;
+  }
+  __syncthreads();
+  OWNER_TICK(1);
+  // 2. bitonic sort of s_key[0, P) ascending: a trace's records adjacent, in batch order
+  for (uint32_t size = 2; size <= P; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      if (t < P / 2) {
+        const uint32_t i0 = 2 * t - (t & (stride - 1)), i1 = i0 + stride;
+        const bool up = (i0 & size) == 0;
+        const uint64_t x = s_key[i0], y = s_key[i1];
+        if ((x > y) == up) {
+          s_key[i0] = y;
+          s_key[i1] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  OWNER_TICK(2);
+  // 3. the trace whose first entry (in sorted order) is t
+  bool hv = false, hlat = false;
+  uint32_t he = 0, herr = 0, g = 0;
+  if (t < cnt) {
+    g = (uint32_t)(s_key[t] >> 40);
+    if (t == 0 || (uint32_t)(s_key[t - 1] >> 40) != g) {
+      uint32_t lat = 0;
+      for (uint32_t j = t; j < cnt; j++) {
+        if (j > t && (uint32_t)(s_key[j] >> 40) != g) break;
+        const uint32_t fl = s_w4[(uint32_t)s_key[j] & 255u] >> 24;
+        herr |= fl & kXErr;
+        lat |= fl & kXLat;
+        he = j + 1;
+      }
+      hv = true;
+      hlat = lat != 0;
+    }
+  }
+  FoldState fs{0.0, 0.0, 0u, 0u};
+  const uint64_t* R = reinterpret_cast<const uint64_t*>(a.recv);
+  for (uint32_t ck = 0; ck < a.n_chunks; ck++) {
+    if (ck) {   // chunk ck's tables and words of entry t (block-uniform loop)
+      __syncthreads();
+      owner_cfg_copy(a, cfg_lds, ck, t);
+      if (t < cnt) {
+        const uint64_t* r = R + (uint64_t)ri * a.words + kXFixedWords + 2 * ck;
+        s_ep[t] = r[0];
+        s_sv[t] = r[1];
+      }
+      __syncthreads();
+    }
+    if (hv) owner_chunk(load_cfg(cfg_lds), s_key, s_w4, s_m, s_e, s_ep, s_sv, t, he, herr, hlat, fs);
+  }
+  OWNER_TICK(3);
+  if (hv) {
+    uint8_t dk = 0, dl = 0;
+    double dr = 0;
+    walk_finish(fs, trace_uniform(s_hi[g], s_lo[g], a.seed), dk, dl, dr);
+    for (uint32_t j = t; j < he; j++) a.keep[(s_key[j] >> 8) & 0xFFFFFFFFull] = dk;
+  }
+  OWNER_TICK(4);
+}
+
 __global__ __launch_bounds__(256) void scatter_keep_kernel(const uint8_t* back, const uint32_t* pos, uint64_t n,
                                                            uint8_t* keep) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1788,10 +2051,15 @@ uint32_t shard_owner_host(uint64_t hi, uint64_t lo, uint32_t n) {
   return (uint32_t)((sm(hi ^ sm(lo)) >> 32) % n);
 }
 void launch_shard_hist(const ShardArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(shard_hist_kernel, dim3(a.n_tiles), dim3(kSortThreads), 0, st, a);
+  const uint32_t waves = kSortThreads / kWave;
+  hipLaunchKernelGGL(shard_hist_kernel, dim3((a.n_tiles + waves - 1) / waves), dim3(kSortThreads), 0, st, a);
+}
+void launch_shard_counts(const ShardArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(shard_counts_kernel, dim3(1), dim3(64), 0, st, a);
 }
 void launch_shard_scatter(const ShardArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(shard_scatter_kernel, dim3(a.n_tiles), dim3(kSortThreads), 0, st, a);
+  const uint32_t waves = kSortThreads / kWave;
+  hipLaunchKernelGGL(shard_scatter_kernel, dim3((a.n_tiles + waves - 1) / waves), dim3(kSortThreads), 0, st, a);
 }
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st) {
   if (a.n) hipLaunchKernelGGL(shard_unpack_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, st, a);
@@ -1801,9 +2069,43 @@ __global__ __launch_bounds__(256) void add_i64_kernel(int64_t* dst, const int64_
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) dst[i] += src[i];
 }
+// the in-process transport's phase: every peer's piece in one launch
+// (blockIdx.y = piece; 16-, 8- or 1-byte moves by the pieces' alignment)
+__global__ __launch_bounds__(256) void peer_copy_kernel(PeerCopies c) {
+  const uint32_t p = blockIdx.y;
+  const uint8_t* src = c.src[p];
+  uint8_t* dst = c.dst[p];
+  const uint64_t len = c.len[p];
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, step = (uint64_t)gridDim.x * 256;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst);
+  uint64_t done = 0;
+  if ((al & 15) == 0) {
+    const uint64_t m = len / 16;
+    for (uint64_t i = t0; i < m; i += step)
+      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    done = m * 16;
+  } else if ((al & 7) == 0) {
+    const uint64_t m = len / 8;
+    for (uint64_t i = t0; i < m; i += step)
+      reinterpret_cast<uint64_t*>(dst)[i] = reinterpret_cast<const uint64_t*>(src)[i];
+    done = m * 8;
+  }
+  for (uint64_t i = done + t0; i < len; i += step) dst[i] = src[i];
+}
 }  // namespace
+void launch_peer_copies(const PeerCopies& c, uint64_t max_len, hipStream_t st) {
+  if (!c.n || !max_len) return;
+  const uint32_t bx = (uint32_t)std::min<uint64_t>((max_len + 4095) / 4096, 1024);
+  hipLaunchKernelGGL(peer_copy_kernel, dim3(bx, c.n), dim3(256), 0, st, c);
+}
 void launch_add_i64(int64_t* dst, const int64_t* src, uint64_t n, hipStream_t st) {
   if (n) hipLaunchKernelGGL(add_i64_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, dst, src, n);
+}
+void launch_owner_bucket(const OwnerArgs& a, hipStream_t st) {
+  if (a.n) hipLaunchKernelGGL(owner_bucket_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, st, a);
+}
+void launch_owner_fold(const OwnerArgs& a, hipStream_t st) {
+  if (a.n) hipLaunchKernelGGL(owner_fold_kernel, dim3(a.n_buckets), dim3(256), a.cfg_lds_bytes, st, a);
 }
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st) {
   if (n) hipLaunchKernelGGL(scatter_keep_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, back, pos, n, keep);

@@ -10,8 +10,10 @@ traces.go:26-84).  Here, per step:
    endpoint and rule bits and the latency monoid element of the stretch) and
    buckets them by owner = hash(trace id) mod world, keeping source order;
 2. an all-to-all of the record counts, then of the records (RCCL over xGMI);
-3. ``ose_shard_unpack`` + the SAMPLE stage on the received records, folded in
-   (source rank, source order) = global batch order;
+3. ``ose_shard_decide`` on the received records: bucketed by trace-id hash,
+   each bucket's traces grouped and folded in LDS in (source rank, source
+   order) = global batch order (``ose_shard_unpack`` + the SAMPLE stage is
+   the general path it falls back to, and stays callable);
 4. the reverse all-to-all of the keep bytes and ``ose_shard_scatter_keep``.
 
 Two drivers of the same round:
@@ -31,7 +33,7 @@ from . import native
 
 
 def route_and_sample(ops, world: int, group=None) -> None:
-    """One exchange round; ops provides pack/alloc/unpack_sample/scatter."""
+    """One exchange round; ops provides pack/alloc/decide/scatter."""
     import torch
     import torch.distributed as dist
     XREC = ops.rec_bytes                                # bytes per exchanged record
@@ -43,7 +45,7 @@ def route_and_sample(ops, world: int, group=None) -> None:
     n_send, n_recv = sum(sc), sum(rc)
     recv = ops.alloc(n_recv * XREC)
     dist.all_to_all_single(recv, send[: n_send * XREC], [c * XREC for c in rc], [c * XREC for c in sc], group=group)
-    keep_x = ops.unpack_sample(recv, n_recv)            # uint8 [n_recv]
+    keep_x = ops.decide(recv, n_recv)                   # uint8 [n_recv]
     back = ops.alloc(n_send)
     dist.all_to_all_single(back, keep_x[:n_recv], sc, rc, group=group)
     ops.scatter(back, pos)
@@ -78,7 +80,7 @@ class DeviceExchange:
 
     @classmethod
     def receiver(cls, engine, rec_bytes, stream=None):
-        """Owner-side ops only (unpack_sample), for a batch of records that
+        """Owner-side ops only (decide, unpack_sample), for a batch of records that
         arrived without a local source batch (bench.py's owner workload)."""
         import torch
         self = cls.__new__(cls)
@@ -125,7 +127,16 @@ class DeviceExchange:
         endpoint and one rule word per chunk: 40 + 16 per chunk bytes)"""
         return (self.rec_bytes - 40) // 16
 
+    def decide(self, recv, n):
+        """The owner's decisions, one keep byte per record (ose_shard_decide)."""
+        x = self._ensure(n)
+        native.check(self.L.ose_shard_decide(self.eng.h, recv.data_ptr(), n, self.rec_bytes, x["keep"].data_ptr(),
+                                             x["status_word"].data_ptr(), C.byref(native.Rand(self.seed, 0.0)),
+                                             self._s()))
+        return x["keep"]
+
     def unpack_sample(self, recv, n):
+        """The general path: records unpacked into span columns + the SAMPLE stage."""
         x = self._ensure(n)
         p = {k: v.data_ptr() for k, v in x.items()}
         native.check(self.L.ose_shard_unpack(recv.data_ptr(), n, self.rec_bytes,

@@ -166,6 +166,7 @@ def lib() -> C.CDLL:
         "ose_shard_owner": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint32]),
         "ose_shard_pack": (C.c_int, [_p, C.POINTER(Columns), C.c_uint32, _p, _p, _p, _p]),
         "ose_shard_unpack": (C.c_int, [_p, C.c_uint64, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+        "ose_shard_decide": (C.c_int, [_p, _p, C.c_uint64, C.c_uint32, _p, _p, _p, _p]),
         "ose_shard_record_bytes": (C.c_uint32, [_p]),
         "ose_shard_scatter_keep": (C.c_int, [_p, _p, C.c_uint64, _p, _p]),
         "ose_nccl_unique_id": (C.c_int, [_p, C.c_size_t]),
@@ -181,6 +182,7 @@ def lib() -> C.CDLL:
         "osehost_sampling_chunks": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32)]),
         "osehost_stream_copy": (C.c_int, [_p, _p, C.c_size_t, C.c_int, _p, C.POINTER(C.c_double)]),
         "osehost_xgroup_create": (C.c_int, [C.c_int, C.POINTER(_p)]),
+        "osehost_owner_last_general": (C.c_uint32, [_p]),
         "osehost_xgroup_destroy": (None, [_p]),
         "osehost_exchange_sample_local": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(Outputs), _p, C.c_int,
                                                     C.POINTER(Rand), _p, C.POINTER(C.c_uint64)]),

@@ -254,7 +254,7 @@ class CpuOps:
     def alloc(self, nbytes):
         return self.torch.empty(nbytes, dtype=self.torch.uint8)
 
-    def unpack_sample(self, recv, n):
+    def decide(self, recv, n):
         from odigos_amd.batch import HostOutputs
         from tests.oracle_lib import SamplingOracle
         hc, main = expand_for_oracle(recv.numpy()[: n * REC_BYTES].copy(), self.cfg)

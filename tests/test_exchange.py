@@ -228,10 +228,11 @@ def test_gpu_shard_kernels_with_attr_bits():
     _shard_vs_emulation(cfg, True, world=8)
 
 
-def _owner_path(sources, cfg):
+def _owner_path(sources, cfg, general=False):
     """The whole exchange on one GPU: pack every source batch for len(sources)
-    owners, hand each owner its buckets in source-rank order, unpack + SAMPLE
-    there, send the keep bytes back and scatter them."""
+    owners, hand each owner its buckets in source-rank order, decide there
+    (ose_shard_decide; general: unpack + SAMPLE), send the keep bytes back
+    and scatter them."""
     import ctypes as C
     import torch
     from odigos_amd.batch import DeviceBatch, Engine
@@ -258,7 +259,7 @@ def _owner_path(sources, cfg):
         k = recv.numel() // REC_BYTES
         records += k
         ex = DeviceExchange.receiver(eng, REC_BYTES)
-        keep_x = ex.unpack_sample(recv, k)
+        keep_x = ex.unpack_sample(recv, k) if general else ex.decide(recv, k)
         off = 0
         for s, p in enumerate(packs):
             m = int(p[1][o + 1] - p[1][o])
@@ -304,6 +305,98 @@ def test_gpu_owner_path_zero_starts(world):
     want = _concat_keep_oracle(sources, cfg)
     for g, w in zip(got, want):
         np.testing.assert_array_equal(g, w)
+
+
+def _owner_recvs(sources, cfg):
+    """Pack every source for len(sources) owners; each owner's received
+    records (the source buckets in rank order) and the engine."""
+    import ctypes as C
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine
+    W = len(sources)
+    eng = Engine({"odigossampling": cfg})
+    L = native.lib()
+    rb = int(L.ose_shard_record_bytes(eng.h))
+    packs = []
+    for g in sources:
+        db = DeviceBatch(g.cols)
+        n = g.cols.n_spans
+        send = torch.empty(max(n, 1) * rb, dtype=torch.uint8, device="cuda")
+        counts = torch.zeros(W, dtype=torch.int64, device="cuda")
+        pos = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+        native.check(L.ose_shard_pack(eng.h, C.byref(db.cols), W, send.data_ptr(), counts.data_ptr(), pos.data_ptr(), None))
+        packs.append((send, np.concatenate([[0], np.cumsum(counts.cpu().numpy())])))
+    recvs = [torch.cat([p[0][p[1][o] * rb: p[1][o + 1] * rb] for p in packs]) for o in range(W)]
+    return eng, recvs, rb
+
+
+def _decide_both(eng, recv, rb):
+    """ose_shard_decide's keep and the general path's on the same records,
+    and whether the former fell back to the general path."""
+    from odigos_amd.exchange import DeviceExchange
+    import torch
+    k = recv.numel() // rb
+    ex = DeviceExchange.receiver(eng, rb)
+    fold = ex.decide(recv, k)[:k].cpu().numpy().copy()
+    torch.cuda.synchronize()
+    general = bool(native.lib().osehost_owner_last_general(eng.h))
+    ref = ex.unpack_sample(recv, k)[:k].cpu().numpy().copy()
+    return fold, ref, general
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["fused", "fractional", "zipf", "latency_chunks", "attr100_chunks"])
+def test_gpu_owner_decide_vs_general(case):
+    # the owner's bucketed fold (ose_shard_decide: records bucketed by trace
+    # hash, grouped, ordered and folded in LDS) against the general path
+    # (unpack + the SAMPLE stage, itself checked against the oracle by the
+    # tests above) on the same received records, byte for byte
+    from odigos_amd.batch import Generator
+    from tests.test_sampling_chunks import CONFIGS, _attr_bits, _chunks
+    from tests.test_sampling_random import inject_zero_starts
+    from tests.workloads import wide_attr100_config
+    if case in ("fused", "fractional"):
+        cfg = CFG if case == "fused" else _fractional(CFG)
+        sources = [Generator("fused", seed=0x0D1600D1, n_spans=1_000_000, rank=r, world=4) for r in range(4)]
+    elif case == "zipf":
+        cfg = _fractional(CFG)
+        sources = [Generator("zipf", seed=0x0D1600D2, n_spans=300_000, rank=r, world=3) for r in range(3)]
+    else:
+        cfg = CONFIGS["latency"]() if case == "latency_chunks" else wide_attr100_config()
+        assert _chunks(cfg) >= 2
+        sources = [Generator("sampling", seed=0x0D1600D3, n_spans=400_000, rank=r, world=3) for r in range(3)]
+        for r, g in enumerate(sources):
+            if case == "attr100_chunks":
+                g.attr_bits = _attr_bits(g, 100, seed=60 + r, p=0.01)
+    for r, g in enumerate(sources):
+        inject_zero_starts(g, 0.01, 40 + r)
+    eng, recvs, rb = _owner_recvs(sources, cfg)
+    paths = []
+    for recv in recvs:
+        fold, ref, general = _decide_both(eng, recv, rb)
+        np.testing.assert_array_equal(fold, ref)
+        paths.append(general)
+    if case != "zipf":
+        assert not any(paths), paths   # these batches stay on the fold
+
+
+@pytest.mark.gpu
+def test_gpu_owner_decide_overflow_falls_back():
+    # a trace received as 600 pieces overflows its bucket (512 records): the
+    # whole batch takes the general path, with the same decisions
+    import torch
+    from odigos_amd.batch import Generator
+    sources = [Generator("fused", seed=0x0D1600D4, n_spans=200_000, rank=r, world=2) for r in range(2)]
+    eng, recvs, rb = _owner_recvs(sources, CFG)
+    recv = recvs[0]
+    one = recv[:rb]
+    big = torch.cat([recv[: 100 * rb], one.repeat(600), recv[100 * rb:]])
+    fold, ref, general = _decide_both(eng, big, rb)
+    assert general
+    np.testing.assert_array_equal(fold, ref)
+    fold, ref, general = _decide_both(eng, recv, rb)
+    assert not general
+    np.testing.assert_array_equal(fold, ref)
 
 
 @pytest.mark.gpu
