@@ -75,11 +75,9 @@ WORKLOADS = {
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
     "sampling_wide": dict(gen="sampling", seed=0x0D160003, spans=50_000_000, per_gpu=True,
                           cfg="wide", stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
-                          fields=SAMPLE_FIELDS,
-                          kernels=("shard_pack", "owner_fold", "shard_unpack") + TRACE_KERNELS + SLOW_KERNELS,
+                          fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
                           metric_config="diagnostic: C3's batch under 1 error + 4 service + 150 latency rules "
-                                        "(three rule chunks: one pass over the columns into partial records "
-                                        "carrying every chunk's words, decided by the owner fold)"),
+                                        "(three rule chunks, one trace-stage pass each)"),
     "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000, per_gpu=True,
                  cfg=None, stages="SAMPLE|TEMPLATE", null_columns=("res_url_ok",), null_outputs=PER_TRACE_OUTS,
                  fields=SAMPLE_FIELDS + ("kind", "url_flags", "path"), kernels=TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS,

@@ -44,9 +44,6 @@ struct LastErrorScope {
 bool stream_capturing(hipStream_t st);
 struct Engine;
 void release_exchange_scratch(const Engine* e);   // shard_host.cpp
-// SAMPLE of a rule-chunked configuration on one GPU through partial records
-// (shard_host.cpp; run_sampling decides when it applies)
-int sample_by_records(Engine* e, const ose_columns* c, const ose_outputs* o, const ose_rand* rnd, hipStream_t st);
 void release_batch_pool(Engine* e);                // batch.cpp
 struct OtlpEngine;
 void release_otlp(Engine* e);                      // otlp_host.cpp

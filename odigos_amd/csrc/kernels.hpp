@@ -330,6 +330,8 @@ struct ShardArgs {
   const uint8_t* const* cfgs;  // [n_chunks] SampCfgDev blobs (device array of the rule chunks' tables)
   uint32_t n_chunks;
   const uint32_t* lat_svc;    // bit s: service s has an http_latency rule in some chunk
+  uint32_t cfg_lds_bytes;     // the chunk tables copied into LDS by shard_scatter_kernel (sum of their 16-aligned
+                              // sizes), 0: read from HBM
   uint32_t* hist;             // [n_ranks * n_tiles] counts, then offsets (second buffer)
   uint32_t* hoff;
   uint64_t* counts;           // [n_ranks] records per owner (shard_counts_kernel)

@@ -624,13 +624,9 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
                  hipStream_t st, Workspace* ws, std::function<int()>* tail) {
   const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
   if (K <= 1) return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr);
-  // one pass over the columns into partial records carrying every chunk's
-  // words, decided by the owner fold (sample_by_records); the pass-per-chunk
-  // form below stays for what records do not give: per-trace outputs,
-  // OSE_GROUP_BATCH, and the owner-side record columns themselves (svc_match)
-  const bool per_trace = o->trace_count || o->trace_first_span || o->trace_keep || o->trace_level || o->trace_ratio;
-  if (group_mode == OSE_GROUP_TRACE_ID && !per_trace && !c->svc_match && c->n_spans)
-    return sample_by_records(e, c, o, rnd, st);
+  // (one pass over the columns into partial records carrying every chunk's
+  // words, decided by the owner fold, measured slower on sampling_wide:
+  // 9.72 ms against 7.65, profiles/r4_owner_fold_forms.txt)
   int rc = ws->reserve_fold(std::max<uint64_t>(c->n_spans, 1));
   if (rc) return rc;
   for (uint32_t k = 0; k < K; k++) {

@@ -441,48 +441,6 @@ int owner_decide(Engine* e, XScratch* xs, const uint8_t* recvb, uint64_t n_recv,
   return rc;
 }
 
-}  // namespace
-
-// SAMPLE for a rule-chunked configuration on one GPU: the exchange's two
-// halves back to back with one rank.  ose_shard_pack folds the spans into
-// partial records that carry every chunk's endpoint and rule words (one
-// pass over the columns, instead of one trace stage per chunk), the records
-// are decided as an owner decides them (owner_decide: the bucketed fold,
-// which walks ShouldSample chunk by chunk), and keep goes back onto the
-// spans.  The host waits twice: for the record count and for the fold's
-// overflow word.
-int sample_by_records(Engine* e, const ose_columns* c, const ose_outputs* o, const ose_rand* rnd, hipStream_t st) {
-  const uint64_t n = c->n_spans;
-  if (!n) return 0;
-  if (!o->keep) return fail(OSE_EINVAL, "SAMPLE stage needs keep");
-  XScratch* xs = scratch_of(e);
-  std::lock_guard<std::mutex> g(xs->mu);
-  const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
-  const uint64_t RB = x_rec_bytes(K);
-  int rc;
-  if ((rc = xs->send.need(n * RB)) || (rc = xs->pos.need(4 * n)) || (rc = xs->counts.need(16)) ||
-      (rc = xs->keep_x.need(n)))
-    return rc;
-  if (!xs->host_counts) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&xs->host_counts), 16 * 64, hipHostMallocDefault));
-  if (!xs->done) HIP_TRY(hipEventCreateWithFlags(&xs->done, hipEventDisableTiming));
-  if (xs->done_set) HIP_TRY(hipStreamWaitEvent(st, xs->done, 0));
-  uint64_t* cnt_d = xs->counts.as<uint64_t>();
-  rc = ose_shard_pack(reinterpret_cast<ose_engine*>(e), c, 1, xs->send.p, cnt_d, xs->pos.as<uint32_t>(), st);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(xs->host_counts, cnt_d, 8, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  const uint64_t R = xs->host_counts[0];
-  if (R > n) return fail(OSE_EDEVICE, "internal: more records than spans");
-  rc = owner_decide(e, xs, xs->send.as<uint8_t>(), R, K, xs->keep_x.as<uint8_t>(), o->device_status, rnd, st);
-  if (rc) return rc;
-  launch_scatter_keep(xs->keep_x.as<uint8_t>(), xs->pos.as<uint32_t>(), n, o->keep, st);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(xs->done, st));
-  xs->done_set = true;
-  return 0;
-}
-
-namespace {
 // One exchange round (ose_exchange_sample).  Everything that can fail on
 // this rank alone (arguments, scratch) is checked before the first
 // collective; a failure after it leaves the peers inside a collective, so
@@ -637,6 +595,11 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.cfgs = reinterpret_cast<const uint8_t* const*>(e->shard_tables_dev);
   a.n_chunks = (uint32_t)e->sampling_chunks_dev.size();
   a.lat_svc = reinterpret_cast<const uint32_t*>(e->shard_tables_dev + 8 * e->sampling_chunks_dev.size());
+  {
+    uint32_t lb = 0;   // the chunk tables in LDS when they fit 64 KiB (else read from HBM)
+    for (const auto& blob : e->sampling_chunks_host) lb += (reinterpret_cast<const SampCfgDev*>(blob.data())->total_bytes + 15u) & ~15u;
+    a.cfg_lds_bytes = lb <= 65536 ? lb : 0;
+  }
   a.hist = reinterpret_cast<uint32_t*>(base + off_hist);
   a.hoff = reinterpret_cast<uint32_t*>(base + off_hoff);
   a.counts = counts;

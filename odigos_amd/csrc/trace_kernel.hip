@@ -1702,8 +1702,23 @@ __global__ __launch_bounds__(64) void shard_counts_kernel(ShardArgs a) {
 }
 
 // The records in source order; pack_pos[span] = its record's slot in `send`.
+// The rule chunks' tables are copied into LDS first (cfg_lds_bytes, when
+// they fit): the endpoint tests and service lookups of every span are then
+// ds_reads, as in trace_eval_kernel.
 __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xcfg[];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (a.cfg_lds_bytes) {
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < a.n_chunks; k++) {
+      const uint8_t* src = a.cfgs[k];
+      const uint32_t nb = (reinterpret_cast<const SampCfgDev*>(src)->total_bytes + 15u) & ~15u;
+      for (uint32_t q = (uint32_t)t * 16; q < nb; q += kSortThreads * 16)
+        *reinterpret_cast<uint4*>(xcfg + off + q) = *reinterpret_cast<const uint4*>(src + q);
+      off += nb;
+    }
+    __syncthreads();
+  }
   const uint32_t ch = blockIdx.x * (kSortThreads / kWave) + wv;
   if (ch >= a.n_tiles) return;   // wave-uniform; no block barriers below
   uint32_t off = (uint32_t)lane < a.n_ranks ? a.hoff[(uint64_t)lane * a.n_tiles + ch] : 0u;
@@ -1750,8 +1765,10 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
       rec[4] = (uint64_t)(x.sv | (flags << 24));
     }
     // per rule chunk: the endpoint and rule bits under that chunk's tables
+    uint32_t coff = 0;
     for (uint32_t k = 0; k < a.n_chunks; k++) {
-      const Cfg c = load_cfg(a.cfgs[k]);
+      const Cfg c = load_cfg(a.cfg_lds_bytes ? xcfg + coff : a.cfgs[k]);
+      coff += (c.h->total_bytes + 15u) & ~15u;
       uint64_t ep = 0, svcb = 0;
       x_chunk(a, c, x, base + lane, k, ep, svcb);
       uint32_t z = 0;
@@ -1819,9 +1836,12 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(UnpackArgs a) {
 // (an exact table in HBM, run lists, one lane chasing a trace's runs through
 // the head masks).  Only a bucket past kOwnerCap records sets *overflow,
 // and the host then runs the general path on the whole batch.
-// Measured forms (owner workload): an index per slot with the records read
-// through it (two more dependent round trips per workgroup) and persistent
-// workgroups with the rule tables in LDS were slower (profiles/r4*_owner*).
+// Measured forms (owner workload, profiles/r4_owner_fold_forms.txt): an
+// index per slot with the records read through it (two more dependent round
+// trips per workgroup), persistent workgroups, the rule tables read from
+// HBM (the fold phase 89% of the clocks), and per-trace member lists built
+// by a scan and an insertion sort instead of the bitonic sort, with the
+// traces' lanes packed into the first waves, were slower.
 constexpr uint32_t kOwnerTable = 2 * kOwnerCap;   // LDS hash slots: load <= 1/2
 constexpr uint32_t kOwnerNone = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t owner_bucket_of(uint64_t h, uint32_t n_buckets) {
@@ -2059,7 +2079,8 @@ void launch_shard_counts(const ShardArgs& a, hipStream_t st) {
 }
 void launch_shard_scatter(const ShardArgs& a, hipStream_t st) {
   const uint32_t waves = kSortThreads / kWave;
-  hipLaunchKernelGGL(shard_scatter_kernel, dim3((a.n_tiles + waves - 1) / waves), dim3(kSortThreads), 0, st, a);
+  hipLaunchKernelGGL(shard_scatter_kernel, dim3((a.n_tiles + waves - 1) / waves), dim3(kSortThreads), a.cfg_lds_bytes, st,
+                     a);
 }
 void launch_shard_unpack(const UnpackArgs& a, hipStream_t st) {
   if (a.n) hipLaunchKernelGGL(shard_unpack_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, st, a);
