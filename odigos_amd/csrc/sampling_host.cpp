@@ -376,7 +376,14 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   uint64_t* win_first = reinterpret_cast<uint64_t*>(take(8 * W));
   if (off > need) return fail(OSE_EINVAL, "internal: trace workspace layout exceeds its bound");
   uint32_t* err = o->device_status ? o->device_status : misc + 8;
-  HIP_TRY(hipMemsetAsync(base, 0, 64, st));
+  // a later rule-chunk pass keeps the first pass's *dup (misc[0]): the batch's
+  // trace-id layout is the same, so it neither registers run heads nor checks
+  // buckets again
+  const bool reuse_dup = chunk > 0 && group_mode == OSE_GROUP_TRACE_ID;
+  if (reuse_dup)
+    HIP_TRY(hipMemsetAsync(base + 4, 0, 60, st));
+  else
+    HIP_TRY(hipMemsetAsync(base, 0, 64, st));
 
   TraceKernelArgs a{};
   a.n_spans = n;
@@ -442,7 +449,7 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   // fingerprint table probed with a CAS per head: C4 trace_eval 3.02 -> 2.87
   // ms + 0.06 ms of trace_dup_check, C3 1.55 -> 1.47 + 0.03,
   // profiles/r3_dup_buckets_ab.txt)
-  if (a.mode == kTraceRuns) {
+  if (a.mode == kTraceRuns && !reuse_dup) {
     if (!ws->dup_bkt || ws->dup_bkt_bits < 1 || ws->dup_bkt_bits > 32)
       return fail(OSE_EDEVICE, "trace stage: duplicate-detection buckets missing");
     a.dup_bkt = ws->dup_bkt;
@@ -619,7 +626,8 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
 // than one, each pass but the last saves ShouldSample's walk per trace and
 // the next resumes it (ping-pong buffers: a pass's provisional fast-path
 // decisions for traces the slow path redoes never reach the state it reads).
-// Chunked passes run without the host-gated tail.
+// Each pass takes its slow paths host-gated; a later pass reuses the first pass's
+// duplicate detection (run_sampling_pass).
 int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
                  hipStream_t st, Workspace* ws, std::function<int()>* tail) {
   const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
@@ -632,7 +640,12 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   for (uint32_t k = 0; k < K; k++) {
     const FoldState* in = k ? static_cast<const FoldState*>(ws->fold[(k - 1) & 1]) : nullptr;
     FoldState* out = k + 1 < K ? static_cast<FoldState*>(ws->fold[k & 1]) : nullptr;
-    rc = run_sampling_pass(e, c, o, group_mode, rnd, st, ws, nullptr, k, in, out);
+    // each pass's slow paths host-gated as in a one-table call (the host waits
+    // for the pass's flags; the run-list and sort launches are queued only
+    // for a batch with repeated trace ids)
+    std::function<int()> pass_tail;
+    rc = run_sampling_pass(e, c, o, group_mode, rnd, st, ws, &pass_tail, k, in, out);
+    if (!rc && pass_tail) rc = pass_tail();
     if (rc) return rc;
   }
   return 0;

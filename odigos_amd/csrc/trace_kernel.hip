@@ -622,9 +622,6 @@ __device__ __forceinline__ void write_rec(const TraceKernelArgs& a, uint64_t pos
 // Run heads are collected per wave in LDS and inserted 64 at a time: each
 // insert is a load and a dependent CAS, so batching turns a per-step pair of
 // round trips into one pair per 64 heads.
-#ifndef OSE_FOLD_ENDS
-#define OSE_FOLD_ENDS 0   // 1: trace_fold_kernel finds run ends once, up front
-#endif
 constexpr int kHeadQ = 128;
 struct HeadQ {
   uint64_t cell[kHeadQ];
@@ -701,7 +698,10 @@ __device__ void flush_queue(const TraceKernelArgs& a, const Cfg& c, DecideQ& Q, 
 // and the service-rule bits fit one 32-bit word (1 + n_lat + service bits <=
 // 32, n_lat_slots <= 32; the host checks): the segmented ORs scan one word
 // instead of five, the latency stretches' words two instead of four.
-template <bool kLean, bool kNarrow>
+// kChunk (with kLean): one pass of a rule-chunked configuration, the walk
+// resumed from fold_in and saved to fold_out (decide_chunk) — the lean
+// instance's loads and scans instead of the general instance's.
+template <bool kLean, bool kNarrow, bool kChunk>
 __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void trace_eval_kernel(TraceKernelArgs a) {
   if (kLean) {
     a.mode = kTraceRuns;
@@ -712,8 +712,10 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     a.key = nullptr;
     a.batch_keep = nullptr;
     a.ablate = 0;
-    a.fold_in = nullptr;
-    a.fold_out = nullptr;
+    if (!kChunk) {
+      a.fold_in = nullptr;
+      a.fold_out = nullptr;
+    }
   }
   if (a.mode == kTracePerm && __hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   __shared__ DecideQ queues[kTWaves];
@@ -804,7 +806,9 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     const bool in_range = base < range_end;
     if (in_range) {
       if (lane == 0 && a.win_heads) a.win_heads[base / kWave] = hmask;
-      if (a.mode == kTraceRuns && !(a.ablate & 1) && hmask) {
+      // (no dup_bkt: a later rule-chunk pass, whose batch layout the first
+      // pass already checked — *dup carries that pass's answer)
+      if (a.mode == kTraceRuns && !(a.ablate & 1) && a.dup_bkt && hmask) {
         const uint32_t nh = __popcll(hmask);
         if (hn + nh > kHeadQ) flush_heads(a, HQ, hn, lane);
         if (hd) {
@@ -816,6 +820,9 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
         hn += nh;
       }
     }
+    // (the service ids loaded a step ahead too, the resource index two steps
+    // ahead: C3 -1 %, C4 -1.3 %, C5 +13 % — skipped steps then load every
+    // column; profiles/r4q_te_pipe_ab.txt)
     if (base + kWave < n) nx = load_raw(a, base + kWave, lane, work);   // prefetch the next step
     uint64_t own;
     if (in_range) {
@@ -1039,7 +1046,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     }
   }
   flush_queue(a, c, Q, qn, lane);
-  flush_heads(a, HQ, hn, lane);
+  if (a.dup_bkt) flush_heads(a, HQ, hn, lane);
 }
 
 // ---- long runs ------------------------------------------------------------------
@@ -1336,19 +1343,8 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
     uint32_t ks[kMaxFoldSlots];
     Lat ls[kMaxFoldSlots];
     bool over = false;
-#if OSE_FOLD_ENDS
-    // every run's end up front: independent head-mask walks in flight
-    // together, reused by the keep writes below
-    uint32_t re[kMaxRuns];
-#pragma unroll
-    for (uint32_t k = 0; k < kMaxRuns; k++) re[k] = k < nr ? (uint32_t)run_end(a, rs[k]) : 0u;
-#endif
     for (uint32_t r = 0; r < nr && !over; r++) {
-#if OSE_FOLD_ENDS
-      const uint64_t s0 = rs[r], s1 = re[r];
-#else
       const uint64_t s0 = rs[r], s1 = run_end(a, s0);
-#endif
       spans += s1 - s0;
       if (spans > kMaxFoldSpans) { over = true; break; }
       for (uint64_t q = s0; q < s1; q++) {
@@ -1393,11 +1389,7 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
     decide_at(a, c, p, err, ep, lsat, svcb, trace_uniform(hi, lo, a.seed), dk, dl, dr);
     write_rec(a, p, dk, dl, dr);
     for (uint32_t r = 0; r < nr; r++) {
-#if OSE_FOLD_ENDS
-      const uint64_t s0 = rs[r], s1 = re[r];
-#else
       const uint64_t s0 = rs[r], s1 = run_end(a, s0);
-#endif
       for (uint64_t q = s0; q < s1; q++) a.keep[q] = dk;
     }
   }
@@ -2135,13 +2127,18 @@ void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, u
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t per_block = kTWaves * a.win_per_wave;
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
-  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate && !a.fold_in && !a.fold_out) {
-    if (a.narrow)
-      hipLaunchKernelGGL((trace_eval_kernel<true, true>), dim3(blocks), dim3(kTThreads), 0, st, a);
+  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate) {
+    const bool chunk = a.fold_in || a.fold_out;
+    if (a.narrow && chunk)
+      hipLaunchKernelGGL((trace_eval_kernel<true, true, true>), dim3(blocks), dim3(kTThreads), 0, st, a);
+    else if (a.narrow)
+      hipLaunchKernelGGL((trace_eval_kernel<true, true, false>), dim3(blocks), dim3(kTThreads), 0, st, a);
+    else if (chunk)
+      hipLaunchKernelGGL((trace_eval_kernel<true, false, true>), dim3(blocks), dim3(kTThreads), 0, st, a);
     else
-      hipLaunchKernelGGL((trace_eval_kernel<true, false>), dim3(blocks), dim3(kTThreads), 0, st, a);
+      hipLaunchKernelGGL((trace_eval_kernel<true, false, false>), dim3(blocks), dim3(kTThreads), 0, st, a);
   } else {
-    hipLaunchKernelGGL((trace_eval_kernel<false, false>), dim3(blocks), dim3(kTThreads), 0, st, a);
+    hipLaunchKernelGGL((trace_eval_kernel<false, false, false>), dim3(blocks), dim3(kTThreads), 0, st, a);
   }
 }
 // One workgroup per fingerprint bucket: its entries into an LDS hash set; an
