@@ -275,8 +275,11 @@ typedef struct ose_batch ose_batch;
  * (there is no host fallback).  Any number of sampling rules: a rule list
  * beyond one GPU rule table (64 http_latency rules, 64 service_name
  * services + span_attribute rules, 12 KiB) runs as one trace-stage pass per
- * chunk of the list with the same decisions; OSE_ENOTSUP remains for more
- * than 64 span_attribute rules and jsonpath filters / scripts.             */
+ * chunk of the list with the same decisions (an http_route longer than a
+ * table: a chunk of its own, its bytes past the LDS copy read from HBM);
+ * OSE_ENOTSUP remains for jsonpath filters / scripts, regexps whose DFA
+ * exceeds 4096 states, and per-service tables over 12 KiB (about a
+ * thousand distinct service names among the sampling rules).               */
 int ose_engine_create(const char* cfg_json, ose_engine** out);
 /* The engine's batches (ose_batch, ose_otlp_batch, ose_otlp_out, ose_gbt)
  * may be released before or after this call: each holds a reference, and

@@ -45,7 +45,7 @@ struct PickedRule {
   int attr_index;
 };
 int build_sampling_blob(const std::unordered_map<std::string, uint32_t>& service_ids, const std::vector<PickedRule>& pick,
-                        std::vector<uint8_t>& b, bool& has_attr) {
+                        std::vector<uint8_t>& b, bool& has_attr, bool spill = false) {
   const uint32_t nsvc = (uint32_t)service_ids.size();
   std::vector<SampRuleDev> rules;
   std::vector<SampLatDev> lat;
@@ -154,7 +154,10 @@ int build_sampling_blob(const std::unordered_map<std::string, uint32_t>& service
   while (b.size() % 16) b.push_back(0);
   b.resize(b.size() + 16, 0);
   h.total_bytes = (uint32_t)b.size();
-  if (h.total_bytes > kSampCfgLds) return 1;
+  // the trace kernels copy the table into LDS: all of it, or with spill
+  // (a chunk of one rule whose http_route alone does not fit) everything but
+  // the route bytes past kSampCfgLds, which they read from HBM
+  if (h.total_bytes > kSampCfgLds && !(spill && h.bytes_off + 16 <= kSampCfgLds)) return 1;
   std::memcpy(b.data(), &h, sizeof h);
   has_attr = n_attr > 0;
   return 0;
@@ -167,7 +170,9 @@ int build_sampling_blob(const std::unordered_map<std::string, uint32_t>& service
 // (devcfg.hpp SampCfgDev): rules in level order global, service, endpoint
 // (rule_engine.go:56-60), config order within a level.  A rule list beyond
 // one table's bounds (64 latency bits, 64 service + span_attribute bits,
-// kSampCfgLds bytes) is cut into consecutive chunks, each as large as fits;
+// kSampCfgLds bytes) is cut into consecutive chunks, each as large as fits
+// (a rule whose route alone does not fit: a chunk of its own whose route
+// bytes past kSampCfgLds the kernels read from HBM);
 // the trace stage then runs once per chunk and carries ShouldSample's walk
 // from one to the next (trace_kernel.hip decide_chunk), so every config
 // Validate accepts runs (the span_attribute bits of a span stay one 64-bit
@@ -213,9 +218,15 @@ int Engine::build_sampling_tables() {
       fitted.swap(blob);
       fitted_attr = attr;
     }
-    if (cur.empty() && k < all.size())
-      return fail(OSE_ENOTSUP, "odigossampling rule tables exceed " + std::to_string(kSampCfgLds) +
-                                   " bytes for one rule (the GPU trace stage keeps them in LDS): shorten its http_route");
+    if (cur.empty() && k < all.size()) {
+      // one rule whose http_route alone overflows the LDS table: its own
+      // chunk, the route bytes past kSampCfgLds read from HBM by the kernels
+      cur.push_back(all[k]);
+      if (build_sampling_blob(service_ids, cur, fitted, fitted_attr, true))
+        return fail(OSE_ENOTSUP, "odigossampling rule tables exceed " + std::to_string(kSampCfgLds) +
+                                     " bytes before their route bytes (the GPU trace stage keeps them in LDS)");
+      k++;
+    }
     sampling_chunks_host.push_back(std::move(fitted));
     sampling_chunk_attr.push_back(fitted_attr ? 1 : 0);
   } while (k < all.size());

@@ -597,7 +597,8 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.lat_svc = reinterpret_cast<const uint32_t*>(e->shard_tables_dev + 8 * e->sampling_chunks_dev.size());
   {
     uint32_t lb = 0;   // the chunk tables in LDS when they fit 64 KiB (else read from HBM)
-    for (const auto& blob : e->sampling_chunks_host) lb += (reinterpret_cast<const SampCfgDev*>(blob.data())->total_bytes + 15u) & ~15u;
+    for (const auto& blob : e->sampling_chunks_host)
+      lb += (std::min<uint32_t>(reinterpret_cast<const SampCfgDev*>(blob.data())->total_bytes, kSampCfgLds) + 15u) & ~15u;
     a.cfg_lds_bytes = lb <= 65536 ? lb : 0;
   }
   a.hist = reinterpret_cast<uint32_t*>(base + off_hist);

@@ -175,8 +175,18 @@ struct Cfg {
   const uint64_t* slot_rules;
   const uint64_t* svc_bits;
   const uint8_t* bytes;
+  const uint8_t* gbytes;   // the route bytes in HBM (a table whose routes spill past the LDS copy)
+  uint32_t lds_end;        // route bytes [0, lds_end) of the bytes section are in `bytes`
 };
-__device__ __forceinline__ Cfg load_cfg(const uint8_t* b) {
+// the bytes of a rule table a kernel copies into LDS: a table longer than
+// kSampCfgLds is one whose route bytes spill (one rule with a very long
+// http_route: build_sampling_tables), read from HBM past that point
+__device__ __forceinline__ uint32_t cfg_lds_copy_bytes(const uint8_t* g) {
+  const uint32_t t = reinterpret_cast<const SampCfgDev*>(g)->total_bytes;
+  return t < kSampCfgLds ? t : kSampCfgLds;
+}
+// b: the table (in LDS or HBM); g: the same table in HBM
+__device__ __forceinline__ Cfg load_cfg(const uint8_t* b, const uint8_t* g = nullptr) {
   Cfg c;
   c.h = reinterpret_cast<const SampCfgDev*>(b);
   c.rules = reinterpret_cast<const SampRuleDev*>(b + c.h->rules_off);
@@ -185,6 +195,8 @@ __device__ __forceinline__ Cfg load_cfg(const uint8_t* b) {
   c.slot_rules = reinterpret_cast<const uint64_t*>(b + c.h->slot_rules_off);
   c.svc_bits = reinterpret_cast<const uint64_t*>(b + c.h->svc_bits_off);
   c.bytes = b + c.h->bytes_off;
+  c.gbytes = g ? g + c.h->bytes_off : c.bytes;
+  c.lds_end = g ? cfg_lds_copy_bytes(g) - c.h->bytes_off : 0xFFFFFFFFu;
   return c;
 }
 
@@ -281,7 +293,8 @@ __device__ __forceinline__ uint64_t endpoint_bits_w(const Cfg& c, uint32_t slot,
     if (!head_ok) continue;
     if (L.route_len > 16) {
       ose_strref tail{rt.off + 16, rt.len - 16};
-      if (!route_has_prefix(arena, tail, c.bytes + L.route_off + 16, L.route_len - 16)) continue;
+      const uint8_t* pre = (L.route_off + L.route_len <= c.lds_end ? c.bytes : c.gbytes) + L.route_off + 16;
+      if (!route_has_prefix(arena, tail, pre, L.route_len - 16)) continue;
     }
     ep |= 1ull << k;
   }
@@ -728,7 +741,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
   {
     // the rule tables (<= kSampCfgLds bytes, checked by the host) live in LDS:
     // every lookup below is a ds_read instead of a dependent L2 round trip
-    const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
+    const uint32_t nb = cfg_lds_copy_bytes(a.cfg);
     for (uint32_t k = threadIdx.x * 16; k < nb; k += kTThreads * 16)
       *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
     __syncthreads();
@@ -736,7 +749,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
   const uint64_t wpw = a.win_per_wave;
   const uint64_t w0 = ((uint64_t)blockIdx.x * kTWaves + wv) * wpw;   // first owned window
   if (w0 >= a.n_windows) return;
-  const Cfg c = load_cfg(cfg_lds);
+  const Cfg c = load_cfg(cfg_lds, a.cfg);
   const uint64_t n = a.n_spans;
   const uint32_t nsvc = c.h->n_services;
 
@@ -1094,12 +1107,12 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
   __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
   __shared__ LongSmem sm;
   {
-    const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
+    const uint32_t nb = cfg_lds_copy_bytes(a.cfg);
     for (uint32_t k = threadIdx.x * 16; k < nb; k += kLThreads * 16)
       *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
     __syncthreads();   // every wave reads the tables (n_services, n_lat below) after the copy
   }
-  const Cfg c = load_cfg(cfg_lds);
+  const Cfg c = load_cfg(cfg_lds, a.cfg);
   const int lane = threadIdx.x & 63;
   const uint32_t wv = threadIdx.x >> 6;
   const uint64_t n = a.n_spans;
@@ -1305,12 +1318,12 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
   if (__hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
   {
-    const uint32_t nb = reinterpret_cast<const SampCfgDev*>(a.cfg)->total_bytes;
+    const uint32_t nb = cfg_lds_copy_bytes(a.cfg);
     for (uint32_t k = threadIdx.x * 16; k < nb; k += kTThreads * 16)
       *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
     __syncthreads();
   }
-  const Cfg c = load_cfg(cfg_lds);
+  const Cfg c = load_cfg(cfg_lds, a.cfg);
   const uint32_t nsvc = c.h->n_services;
   const bool want_route = c.h->n_lat && !a.route_match && a.route;
   const int lane = threadIdx.x & 63;
@@ -1704,7 +1717,7 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     uint32_t off = 0;
     for (uint32_t k = 0; k < a.n_chunks; k++) {
       const uint8_t* src = a.cfgs[k];
-      const uint32_t nb = (reinterpret_cast<const SampCfgDev*>(src)->total_bytes + 15u) & ~15u;
+      const uint32_t nb = (cfg_lds_copy_bytes(src) + 15u) & ~15u;
       for (uint32_t q = (uint32_t)t * 16; q < nb; q += kSortThreads * 16)
         *reinterpret_cast<uint4*>(xcfg + off + q) = *reinterpret_cast<const uint4*>(src + q);
       off += nb;
@@ -1759,8 +1772,8 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     // per rule chunk: the endpoint and rule bits under that chunk's tables
     uint32_t coff = 0;
     for (uint32_t k = 0; k < a.n_chunks; k++) {
-      const Cfg c = load_cfg(a.cfg_lds_bytes ? xcfg + coff : a.cfgs[k]);
-      coff += (c.h->total_bytes + 15u) & ~15u;
+      const Cfg c = a.cfg_lds_bytes ? load_cfg(xcfg + coff, a.cfgs[k]) : load_cfg(a.cfgs[k]);
+      coff += (cfg_lds_copy_bytes(a.cfgs[k]) + 15u) & ~15u;
       uint64_t ep = 0, svcb = 0;
       x_chunk(a, c, x, base + lane, k, ep, svcb);
       uint32_t z = 0;

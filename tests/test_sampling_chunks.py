@@ -56,7 +56,10 @@ def test_chunk_refusals():
     one = {"global_rules": [{"name": "l", "type": "http_latency",
                              "rule_details": {"http_route": "/" + "a" * 13000, "service_name": "s", "threshold": 5,
                                               "fallback_sampling_ratio": 1}}]}
-    assert L.osehost_sampling_chunks(json.dumps({"odigossampling": one}).encode(), C.byref(n)) == native.OSE_ENOTSUP
+    # a route longer than the 12 KiB LDS table: its own chunk, the bytes past
+    # the table read from HBM
+    assert L.osehost_sampling_chunks(json.dumps({"odigossampling": one}).encode(), C.byref(n)) == 0 and n.value == 1
+    assert _chunks(_long_route_config()) == 3
     attr = {"global_rules": [{"name": f"a{j}", "type": "span_attribute",
                               "rule_details": {"service_name": "s", "attribute_key": "k", "condition_type": "string",
                                                "operation": "equals", "expected_value": "v", "sampling_ratio": 1}}
@@ -68,6 +71,103 @@ def test_chunk_refusals():
         assert L.osehost_sampling_chunks(json.dumps({"odigossampling": attr}).encode(), C.byref(n)) == 0
         assert n.value == (k + 63) // 64
     assert _chunks(wide_attr100_config()) == 3        # 40 service + 24 attr bits, 64 attr, 12 attr
+
+
+LONG_PRE = "/" + "a" * 13000
+
+
+def _long_route_config():
+    # C3's rules with an http_latency rule whose route alone overflows the LDS
+    # rule table, between two ordinary ones (three chunks: before, the long
+    # rule, after)
+    from tests.workloads import c3_sampling_config
+    cfg = c3_sampling_config()
+    ep = cfg["endpoint_rules"]
+    ep.insert(8, {"name": "long", "type": "http_latency",
+                  "rule_details": {"http_route": LONG_PRE, "service_name": "svc-02", "threshold": 1,
+                                   "fallback_sampling_ratio": 3}})
+    return cfg
+
+
+def _with_long_routes(g, seed, frac=0.05):
+    """Points a fraction of the spans' routes at 13 KB strings: the long rule's
+    prefix exactly, the prefix and more, one differing in its last byte, one
+    differing early, one a byte short.  Returns the new arena (keep it alive)."""
+    rng = np.random.default_rng(seed)
+    variants = [LONG_PRE, LONG_PRE + "/x", LONG_PRE[:-1] + "b", "/b" + LONG_PRE[2:], LONG_PRE[:-1]]
+    arena = g.array("arena")
+    used = int(g.cols.arena_bytes)
+    offs, blob = [], bytearray()
+    base = (used + 15) // 16 * 16
+    for v in variants:
+        offs.append(base + len(blob))
+        blob += v.encode()
+        blob += b"\0" * ((-len(blob)) % 16)
+    new = np.zeros(base + len(blob) + 32, dtype=np.uint8)
+    new[:used] = arena[:used]
+    new[base:base + len(blob)] = np.frombuffer(bytes(blob), dtype=np.uint8)
+    route = g.array("route").view(np.uint32).reshape(-1, 2)
+    pick = np.nonzero(rng.random(g.cols.n_spans) < frac)[0]
+    which = rng.integers(0, len(variants), size=len(pick))
+    route[pick, 0] = np.array(offs, dtype=np.uint32)[which]
+    route[pick, 1] = np.array([len(v) for v in variants], dtype=np.uint32)[which]
+    g.cols.arena = new.ctypes.data
+    g.cols.arena_bytes = base + len(blob)
+    return new
+
+
+def test_long_route_oracle_vs_python():
+    # the oracle against the Python restatement with the 13 KB rule and routes
+    # that match it, extend it or differ past the LDS part
+    cfg = _long_route_config()
+    g = Generator("sampling", seed=0x0D160841, n_spans=4000)
+    inject_zero_starts(g, 0.03, 7)
+    keep = _with_long_routes(g, 3, frac=0.2)
+    cols = g.cols
+    ho = oracle_run(cols, native.GROUP_TRACE_ID, cfg=cfg)
+    traces = _group(cols, False)
+    svc_ids = intern_services(cfg)
+    res = _arr(cols.resource, C.c_uint32, cols.n_spans)
+    tid = _arr(cols.trace_id, C.c_uint64, 2 * cols.n_spans).reshape(-1, 2)
+    hits = 0
+    for t, spans in enumerate(traces):
+        u = orc_lib().orc_trace_uniform(int(tid[spans[0], 0]), int(tid[spans[0], 1]), SEED)
+        k, lvl, ratio = _py_eval(cfg, svc_ids, cols, res, spans, False, u)
+        assert ho.view("trace_level", np.uint8)[t] == lvl, t
+        assert ho.view("trace_ratio", np.float64)[t] == ratio, t
+        hits += ratio == 3.0 or (lvl == 2 and ratio == 100.0)
+    assert hits > 0
+    del keep
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_gpu_route_past_the_lds_table(shuffle):
+    # a 13 KB http_route (Validate accepts it): the rule's chunk keeps its
+    # tables in LDS and reads the route bytes past kSampCfgLds from HBM; spans
+    # carrying the exact prefix, longer routes, and routes differing only
+    # past the LDS part decide as the oracle does
+    cfg = _long_route_config()
+    g = Generator("sampling", seed=0x0D160821 + int(shuffle), n_spans=200_000, shuffle=shuffle)
+    inject_zero_starts(g, 0.01, 11)
+    g.keep_arena = _with_long_routes(g, 12)
+    gpu_vs_oracle(g, cfg=cfg)
+
+
+@pytest.mark.gpu
+def test_gpu_route_past_the_lds_table_exchange_world3():
+    # the same rule through the trace-id exchange: the pack's endpoint test
+    # reads the spilled route bytes from HBM too
+    from tests.test_exchange import _concat_keep_oracle, _local_round
+    cfg = _long_route_config()
+    sources = [Generator("sampling", seed=0x0D160831, n_spans=300_000, rank=r, world=3) for r in range(3)]
+    for r, g in enumerate(sources):
+        inject_zero_starts(g, 0.01, 40 + r)
+        g.keep_arena = _with_long_routes(g, 20 + r)
+    got, _ = _local_round(sources, cfg)
+    want = _concat_keep_oracle(sources, cfg)
+    for gk, wk in zip(got, want):
+        np.testing.assert_array_equal(gk, wk)
 
 
 @pytest.mark.parametrize("name", sorted(CONFIGS))
