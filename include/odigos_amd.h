@@ -278,7 +278,7 @@ typedef struct ose_batch ose_batch;
  * chunk of the list with the same decisions (an http_route longer than a
  * table: a chunk of its own, its bytes past the LDS copy read from HBM);
  * OSE_ENOTSUP remains for jsonpath filters / scripts, regexps whose DFA
- * exceeds 4096 states, and per-service tables over 12 KiB (about a
+ * exceeds 65279 states, and per-service tables over 12 KiB (about a
  * thousand distinct service names among the sampling rules).               */
 int ose_engine_create(const char* cfg_json, ose_engine** out);
 /* The engine's batches (ose_batch, ose_otlp_batch, ose_otlp_out, ose_gbt)

@@ -29,7 +29,9 @@ enum class RegexStatus { Ok, Syntax, Unsupported, TooLarge };
 RegexStatus regex_syntax_check(const std::string& pattern, std::string& err);
 
 struct Dfa {
-  static constexpr uint32_t kMaxStates = 4096;
+  // state ids are uint16: the cap leaves room for the states one more row
+  // can add (at most 256 classes) after the last check (compile_dfa)
+  static constexpr uint32_t kMaxStates = 65535 - 256;
   uint8_t ascii_class[128];               // class of runes 0..127
   std::vector<uint32_t> hi_lo, hi_hi;     // non-ASCII rune ranges [lo,hi] ...
   std::vector<uint8_t> hi_cls;            // ... and their class (sorted by lo)
