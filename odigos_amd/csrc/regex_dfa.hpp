@@ -13,8 +13,9 @@
 // UTF-8 bytes are runes U+FFFD of width 1 (unicode/utf8.DecodeRune).
 // \p{..} / \P{..} (Go 1.25 names: categories, aliases, scripts, Any, ASCII,
 // Assigned, Cn, LC; loose matching), \Q..\E and (?i) simple case folding of
-// any rune use unicode_tables.cpp (generated; Unicode 13.0.0 data, the
-// reference's Go 1.25 has 15.0.0: later code points are parity unpinned).
+// any rune use unicode_tables.cpp (generated from ICU 70: Unicode 14.0.0
+// data; the reference's Go 1.25 has 15.0.0: the code points assigned in 15.0
+// are parity unpinned).
 // Unsupported (rejected, never approximated): DFAs above kMaxStates.
 #pragma once
 #include <cstdint>

@@ -3,20 +3,57 @@
 compiler (regex_dfa.cpp) needs for Go regexp's \\p{..} classes and (?i)
 folding of non-ASCII runes.
 
-Source data (no network here): Python's unicodedata (Unicode 13.0.0) for
-the general categories and the case mappings, the `regex` module for the
-Script property (its own, newer Unicode: intersected with the code points
-unicodedata knows as assigned, except for scripts unicodedata has no
-character of).  Go 1.25's unicode package is Unicode 15.0.0: code points
-assigned in 14.0 and 15.0 are parity unpinned.
+Source data (no network here): the image's ICU 70 (libicuuc.so.70,
+Unicode 14.0.0, through ctypes) for the general categories, the Script
+property and the simple case mappings; the `regex` module (its own, newer
+Unicode) only for scripts ICU 70 does not know (Kawi, Nag_Mundari: 15.0).
+Without ICU: Python's unicodedata (13.0.0) and the `regex` module, as
+before round 4.  Go 1.25's unicode package is Unicode 15.0.0: code points
+assigned in 15.0 are parity unpinned.
 
 Run: python3 tools/gen_unicode_tables.py > odigos_amd/csrc/unicode_tables.cpp
      python3 tools/gen_unicode_tables.py --c > oracle/unicode_data.c   (the oracle's own copy)
 """
+import ctypes as C
 import sys
 import unicodedata
 
 import regex
+
+ICU_PATH = "/usr/lib/x86_64-linux-gnu/libicuuc.so.70"
+# UCharCategory (uchar.h) -> Go / Unicode two-letter names; 0 is unassigned
+ICU_CATS = [None, "Lu", "Ll", "Lt", "Lm", "Lo", "Mn", "Me", "Mc", "Nd", "Nl", "No", "Zs", "Zl", "Zp", "Cc", "Cf",
+            "Co", "Cs", "Pd", "Ps", "Pe", "Pc", "Po", "Sm", "Sc", "Sk", "So", "Pi", "Pf"]
+
+
+class Icu:
+    def __init__(self, path=ICU_PATH, ver=70):
+        L = C.CDLL(path)
+        def fn(name, res, args):
+            f = getattr(L, "%s_%d" % (name, ver))
+            f.restype, f.argtypes = res, args
+            return f
+        self.char_type = fn("u_charType", C.c_int8, [C.c_int32])
+        self.get_script = fn("uscript_getScript", C.c_int, [C.c_int32, C.POINTER(C.c_int)])
+        self.script_name = fn("uscript_getName", C.c_char_p, [C.c_int])
+        self.tolower = fn("u_tolower", C.c_int32, [C.c_int32])
+        self.toupper = fn("u_toupper", C.c_int32, [C.c_int32])
+        self.totitle = fn("u_totitle", C.c_int32, [C.c_int32])
+        self.fold = fn("u_foldCase", C.c_int32, [C.c_int32, C.c_uint32])
+        v = (C.c_uint8 * 4)()
+        fn("u_getUnicodeVersion", None, [C.POINTER(C.c_uint8)])(v)
+        self.version = "%d.%d.%d" % (v[0], v[1], v[2])
+
+    def script(self, c):
+        e = C.c_int(0)
+        return self.script_name(self.get_script(c, C.byref(e))).decode()
+
+
+def load_icu():
+    try:
+        return Icu()
+    except (OSError, AttributeError):
+        return None
 
 MAX = 0x10FFFF
 CATS = ["Cc", "Cf", "Co", "Cs", "Ll", "Lm", "Lo", "Lt", "Lu", "Mc", "Me", "Mn", "Nd", "Nl", "No", "Pc", "Pd", "Pe",
@@ -54,10 +91,12 @@ def ranges(cps):
 
 
 def main():
+    icu = None if "--no-icu" in sys.argv else load_icu()
+    version = icu.version if icu else unicodedata.unidata_version
     cat_of = {}
     for c in range(MAX + 1):
-        g = unicodedata.category(chr(c))
-        if g != "Cn":
+        g = ICU_CATS[icu.char_type(c)] if icu else unicodedata.category(chr(c))
+        if g is not None and g != "Cn":
             cat_of[c] = g
     assigned = sorted(cat_of)
     tables = {}
@@ -68,7 +107,16 @@ def main():
     base = [c for c in range(MAX + 1) if not 0xD800 <= c <= 0xDFFF]
     scripts = {}
     aset = set(assigned)
+    icu_sc = {}
+    if icu:
+        for c in range(MAX + 1):
+            if 0xD800 <= c <= 0xDFFF:
+                continue
+            icu_sc.setdefault(icu.script(c), []).append(c)
     for s in SCRIPTS:
+        if s in icu_sc:
+            scripts[s] = ranges([c for c in icu_sc[s] if c in aset or s in ("Common", "Inherited")])
+            continue
         pat = regex.compile(r"\p{Script=%s}" % s)
         cps = [base[m.start()] for m in pat.finditer(text)]
         mine = [c for c in cps if c in aset]
@@ -92,10 +140,14 @@ def main():
     for c in assigned:
         if c in (0x130, 0x131):
             continue
-        ch = chr(c)
-        for m in (ch.lower(), ch.upper(), ch.casefold()):
-            if len(m) == 1 and ord(m) != c and ord(m) not in (0x130, 0x131):
-                union(c, ord(m))
+        if icu:   # simple (single-rune) mappings and simple case folding
+            maps = [icu.tolower(c), icu.toupper(c), icu.totitle(c), icu.fold(c, 0)]
+        else:
+            ch = chr(c)
+            maps = [ord(m) for m in (ch.lower(), ch.upper(), ch.casefold()) if len(m) == 1]
+        for m in maps:
+            if m != c and m not in (0x130, 0x131):
+                union(c, m)
     classes = {}
     nodes = set(parent) | set(parent.values())
     for c in nodes:
@@ -112,9 +164,9 @@ def main():
     w = sys.stdout.write
     if "--c" in sys.argv:   # oracle/unicode_data.c: plain C, the oracle's own data (test infrastructure)
         w("/* unicode_data.c — GENERATED by tools/gen_unicode_tables.py --c; do not edit.\n")
-        w(" * Test infrastructure: the oracle's Unicode data (unicodedata %s categories, the regex\n"
-          " * module's Script property on those code points, simple case-folding orbits). */\n"
-          % unicodedata.unidata_version)
+        w(" * Test infrastructure: the oracle's Unicode data (Unicode %s categories, scripts and\n"
+          " * simple case-folding orbits; the regex module's Script property for scripts ICU lacks). */\n"
+          % version)
         w('#include "oracle.h"\n\n')
         for kind, d in (("cat", tables), ("sc", scripts)):
             for nm, rs in d.items():
@@ -132,8 +184,9 @@ def main():
         w("const int orc_fold_n = %d;\n" % len(orbit))
         return
     w("// unicode_tables.cpp — GENERATED by tools/gen_unicode_tables.py; do not edit.\n")
-    w("// General categories: Python unicodedata %s; scripts: the regex module's Script\n" % unicodedata.unidata_version)
-    w("// property restricted to those code points; simple case-folding orbits.\n")
+    w("// General categories, scripts and simple case mappings: Unicode %s (%s); scripts ICU does\n"
+      % (version, "ICU" if icu else "Python unicodedata"))
+    w("// not know: the regex module's Script property; simple case-folding orbits.\n")
     w("// Go 1.25 (the reference's regexp) uses Unicode 15.0.0: later code points are parity unpinned.\n")
     w('#include "unicode_tables.hpp"\n\nnamespace ose {\nnamespace {\n')
     names = []
