@@ -130,6 +130,17 @@ int Workspace::reserve_attr(uint64_t n) {
   return 0;
 }
 
+int Workspace::reserve_ep_planes(uint64_t words) {
+  if (ep_planes && ep_planes_cap >= words) return 0;
+  if (captured) return fail(OSE_ENOMEM, "endpoint-plane workspace too small inside a hipGraph capture");
+  if (ep_planes) HIP_TRY(hipFree(ep_planes));
+  ep_planes = nullptr;
+  ep_planes_cap = 0;
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ep_planes), std::max<uint64_t>(words, 1) * 8));
+  ep_planes_cap = std::max<uint64_t>(words, 1);
+  return 0;
+}
+
 // The attr_match bits for this call: evaluated here from attr_type /
 // attr_val when the caller passes them (ORed with the shim's bits of the
 // "json" rules), else the caller's attr_match as is.  Either way

@@ -166,6 +166,7 @@ Engine::~Engine() {
     if (w->runs) (void)hipFree(w->runs);
     if (w->run_count) (void)hipFree(w->run_count);
     if (w->attr_bits) (void)hipFree(w->attr_bits);
+    if (w->ep_planes) (void)hipFree(w->ep_planes);
     for (void* f : w->fold)
       if (f) (void)hipFree(f);
     if (w->pending) (void)hipEventDestroy(w->pending);

@@ -78,6 +78,9 @@ struct Workspace {
   uint64_t* attr_bits = nullptr;   // span_attribute bits evaluated on the GPU (attr_host.cpp)
   uint64_t attr_bits_cap = 0;
   int reserve_attr(uint64_t n_spans);
+  uint64_t* ep_planes = nullptr;   // endpoint bits per rule chunk of a config with spilled route bytes
+  uint64_t ep_planes_cap = 0;      // (words)
+  int reserve_ep_planes(uint64_t words);
   // SAMPLE + TEMPLATE in one call: the fast path's dup flag is copied here and
   // read by the host after the URL launches are queued (run_stages), so the
   // slow-path launches are only queued when a trace id repeats
@@ -125,6 +128,10 @@ struct Engine {
   uint8_t* shard_tables_dev = nullptr;
   std::unordered_map<std::string, uint32_t> service_ids;
   uint32_t sampling_n_lat = 0, sampling_n_attr = 0;
+  // a chunk table past kSampCfgLds (a route longer than the LDS table): the
+  // trace stage and the pack then take every chunk's endpoint bits as
+  // precomputed planes (spill_endpoint_planes)
+  bool sampling_spill = false;
   // span_attribute rules: all of them (attr_n_rules), the GPU-evaluated ones
   // (attr_n_dev, attr_kernel.hip) and the keys those read
   std::vector<uint8_t> attr_blob_host;
@@ -188,6 +195,9 @@ int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
 uint32_t* size_partials_of(Workspace* ws, size_t off, uint64_t n_scopes, uint64_t n_resources);
 int run_size_tail(Engine* e, const SizeKernelArgs& a, hipStream_t st);
 size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources);
+// every rule chunk's endpoint bits of the spans as planes of n words (a
+// config with spilled route bytes: Engine::sampling_spill), sampling_host.cpp
+int spill_endpoint_planes(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, const uint64_t** out);
 int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t mask, uint32_t group_mode,
                const ose_rand* rnd, hipStream_t st);
 

@@ -389,6 +389,10 @@ struct OwnerArgs {
 void launch_owner_bucket(const OwnerArgs& a, hipStream_t st);
 void launch_owner_fold(const OwnerArgs& a, hipStream_t st);
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);
+// endpoint bits of every span under one rule chunk's tables in HBM (a chunk
+// whose route bytes spill past the LDS copy): out[j] for span j
+void launch_endpoint_plane(const uint8_t* cfg, const uint32_t* resource, const uint32_t* res_svc, const ose_strref* route,
+                           const uint8_t* arena, uint64_t n, uint64_t* out, hipStream_t st);
 // the in-process transport's pieces of one phase, moved by one launch
 struct PeerCopies {
   const uint8_t* src[64];

@@ -232,6 +232,9 @@ int Engine::build_sampling_tables() {
   } while (k < all.size());
   sampling_blob_host = sampling_chunks_host[0];
   sampling_n_lat = n_lat;
+  sampling_spill = false;
+  for (const auto& blob : sampling_chunks_host)
+    sampling_spill |= reinterpret_cast<const SampCfgDev*>(blob.data())->total_bytes > kSampCfgLds;
   sampling_n_attr = n_attr;
   return 0;
 }
@@ -639,9 +642,37 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
 // decisions for traces the slow path redoes never reach the state it reads).
 // Each pass takes its slow paths host-gated; a later pass reuses the first pass's
 // duplicate detection (run_sampling_pass).
+// A chunk whose http_route bytes spill past the kernels' LDS copy of its
+// table: the endpoint bits of every chunk are computed first from the tables
+// in HBM (endpoint_plane_kernel), and the trace stage / the pack take them as
+// route_match planes, so no kernel reads route bytes past its LDS copy.
+int spill_endpoint_planes(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, const uint64_t** out) {
+  const uint64_t n = c->n_spans, K = e->sampling_chunks_dev.size();
+  if (!c->resource || !c->res_svc || !c->route || !c->arena)
+    return fail(OSE_EINVAL, "http_latency rules need resource, res_svc, route and arena");
+  int rc = ws->reserve_ep_planes(n * K);
+  if (rc) return rc;
+  for (uint64_t k = 0; k < K; k++)
+    launch_endpoint_plane(e->sampling_chunks_dev[k], c->resource, c->res_svc, c->route, c->arena, n, ws->ep_planes + k * n,
+                          st);
+  HIP_TRY(hipGetLastError());
+  *out = ws->ep_planes;
+  return 0;
+}
+
 int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
                  hipStream_t st, Workspace* ws, std::function<int()>* tail) {
   const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
+  ose_columns cs;
+  if (e->sampling_spill && !c->route_match && e->sampling_n_lat && c->n_spans) {
+    const uint64_t* planes = nullptr;
+    const int rc = spill_endpoint_planes(e, c, ws, st, &planes);
+    if (rc) return rc;
+    cs = *c;
+    cs.route_match = planes;
+    cs.match_planes = K;
+    c = &cs;
+  }
   if (K <= 1) return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr);
   // (one pass over the columns into partial records carrying every chunk's
   // words, decided by the owner fold, measured slower on sampling_wide:

@@ -577,8 +577,20 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.arena = c->arena;
   a.route_match = c->route_match;
   a.rm_stride = c->match_planes > 1 ? n : 0;
-  if (c->route_match && c->match_planes > 1 && c->match_planes != e->sampling_chunks_dev.size())
+  if (e->sampling_spill && !c->route_match && e->sampling_n_lat) {   // route bytes past an LDS table: planes first
+    const uint64_t* planes = nullptr;
+    rc = spill_endpoint_planes(e, c, ws, st, &planes);
+    if (rc) {
+      e->release_ws(ws, st);
+      return rc;
+    }
+    a.route_match = planes;
+    a.rm_stride = n;
+  }
+  if (c->route_match && c->match_planes > 1 && c->match_planes != e->sampling_chunks_dev.size()) {
+    e->release_ws(ws, st);
     return fail(OSE_EINVAL, "cols->match_planes must be 1 or the engine's rule chunks");
+  }
   {
     const uint64_t* am = nullptr;
     rc = resolve_attr_match(e, c, ws, st, &am);

@@ -175,18 +175,17 @@ struct Cfg {
   const uint64_t* slot_rules;
   const uint64_t* svc_bits;
   const uint8_t* bytes;
-  const uint8_t* gbytes;   // the route bytes in HBM (a table whose routes spill past the LDS copy)
-  uint32_t lds_end;        // route bytes [0, lds_end) of the bytes section are in `bytes`
 };
 // the bytes of a rule table a kernel copies into LDS: a table longer than
 // kSampCfgLds is one whose route bytes spill (one rule with a very long
-// http_route: build_sampling_tables), read from HBM past that point
+// http_route: build_sampling_tables); the endpoint bits of such a chunk come
+// precomputed (endpoint_plane_kernel), so its route bytes are never read
+// from the LDS copy
 __device__ __forceinline__ uint32_t cfg_lds_copy_bytes(const uint8_t* g) {
   const uint32_t t = reinterpret_cast<const SampCfgDev*>(g)->total_bytes;
   return t < kSampCfgLds ? t : kSampCfgLds;
 }
-// b: the table (in LDS or HBM); g: the same table in HBM
-__device__ __forceinline__ Cfg load_cfg(const uint8_t* b, const uint8_t* g = nullptr) {
+__device__ __forceinline__ Cfg load_cfg(const uint8_t* b) {
   Cfg c;
   c.h = reinterpret_cast<const SampCfgDev*>(b);
   c.rules = reinterpret_cast<const SampRuleDev*>(b + c.h->rules_off);
@@ -195,8 +194,6 @@ __device__ __forceinline__ Cfg load_cfg(const uint8_t* b, const uint8_t* g = nul
   c.slot_rules = reinterpret_cast<const uint64_t*>(b + c.h->slot_rules_off);
   c.svc_bits = reinterpret_cast<const uint64_t*>(b + c.h->svc_bits_off);
   c.bytes = b + c.h->bytes_off;
-  c.gbytes = g ? g + c.h->bytes_off : c.bytes;
-  c.lds_end = g ? cfg_lds_copy_bytes(g) - c.h->bytes_off : 0xFFFFFFFFu;
   return c;
 }
 
@@ -293,8 +290,7 @@ __device__ __forceinline__ uint64_t endpoint_bits_w(const Cfg& c, uint32_t slot,
     if (!head_ok) continue;
     if (L.route_len > 16) {
       ose_strref tail{rt.off + 16, rt.len - 16};
-      const uint8_t* pre = (L.route_off + L.route_len <= c.lds_end ? c.bytes : c.gbytes) + L.route_off + 16;
-      if (!route_has_prefix(arena, tail, pre, L.route_len - 16)) continue;
+      if (!route_has_prefix(arena, tail, c.bytes + L.route_off + 16, L.route_len - 16)) continue;
     }
     ep |= 1ull << k;
   }
@@ -749,7 +745,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
   const uint64_t wpw = a.win_per_wave;
   const uint64_t w0 = ((uint64_t)blockIdx.x * kTWaves + wv) * wpw;   // first owned window
   if (w0 >= a.n_windows) return;
-  const Cfg c = load_cfg(cfg_lds, a.cfg);
+  const Cfg c = load_cfg(cfg_lds);
   const uint64_t n = a.n_spans;
   const uint32_t nsvc = c.h->n_services;
 
@@ -1112,7 +1108,7 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
       *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
     __syncthreads();   // every wave reads the tables (n_services, n_lat below) after the copy
   }
-  const Cfg c = load_cfg(cfg_lds, a.cfg);
+  const Cfg c = load_cfg(cfg_lds);
   const int lane = threadIdx.x & 63;
   const uint32_t wv = threadIdx.x >> 6;
   const uint64_t n = a.n_spans;
@@ -1323,7 +1319,7 @@ __global__ __launch_bounds__(kTThreads) void trace_fold_kernel(TraceKernelArgs a
       *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
     __syncthreads();
   }
-  const Cfg c = load_cfg(cfg_lds, a.cfg);
+  const Cfg c = load_cfg(cfg_lds);
   const uint32_t nsvc = c.h->n_services;
   const bool want_route = c.h->n_lat && !a.route_match && a.route;
   const int lane = threadIdx.x & 63;
@@ -1772,8 +1768,8 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
     // per rule chunk: the endpoint and rule bits under that chunk's tables
     uint32_t coff = 0;
     for (uint32_t k = 0; k < a.n_chunks; k++) {
-      const Cfg c = a.cfg_lds_bytes ? load_cfg(xcfg + coff, a.cfgs[k]) : load_cfg(a.cfgs[k]);
-      coff += (cfg_lds_copy_bytes(a.cfgs[k]) + 15u) & ~15u;
+      const Cfg c = load_cfg(a.cfg_lds_bytes ? xcfg + coff : a.cfgs[k]);
+      coff += ((c.h->total_bytes < kSampCfgLds ? c.h->total_bytes : kSampCfgLds) + 15u) & ~15u;
       uint64_t ep = 0, svcb = 0;
       x_chunk(a, c, x, base + lane, k, ep, svcb);
       uint32_t z = 0;
@@ -2058,6 +2054,24 @@ __global__ __launch_bounds__(256) void owner_fold_kernel(OwnerArgs a) {
   OWNER_TICK(4);
 }
 
+// The endpoint bits of every span under one rule chunk's tables read from
+// HBM (a chunk whose route bytes spill past the kernels' LDS copy): the
+// plane the trace stage and the pack then take as route_match
+__global__ __launch_bounds__(256) void endpoint_plane_kernel(const uint8_t* cfg, const uint32_t* resource,
+                                                             const uint32_t* res_svc, const ose_strref* route,
+                                                             const uint8_t* arena, uint64_t n, uint64_t* out) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const Cfg c = load_cfg(cfg);
+  const uint32_t sv = res_svc[resource[j]];
+  uint64_t ep = 0;
+  if (sv < c.h->n_services) {
+    const uint32_t slot = c.svc_slot[sv];
+    if (slot != kNoSlot) ep = endpoint_bits(c, slot, arena, route[j]);
+  }
+  out[j] = ep;
+}
+
 __global__ __launch_bounds__(256) void scatter_keep_kernel(const uint8_t* back, const uint32_t* pos, uint64_t n,
                                                            uint8_t* keep) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -2132,6 +2146,11 @@ void launch_owner_bucket(const OwnerArgs& a, hipStream_t st) {
 }
 void launch_owner_fold(const OwnerArgs& a, hipStream_t st) {
   if (a.n) hipLaunchKernelGGL(owner_fold_kernel, dim3(a.n_buckets), dim3(256), a.cfg_lds_bytes, st, a);
+}
+void launch_endpoint_plane(const uint8_t* cfg, const uint32_t* resource, const uint32_t* res_svc, const ose_strref* route,
+                           const uint8_t* arena, uint64_t n, uint64_t* out, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(endpoint_plane_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, cfg, resource,
+                            res_svc, route, arena, n, out);
 }
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st) {
   if (n) hipLaunchKernelGGL(scatter_keep_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, back, pos, n, keep);

@@ -118,12 +118,11 @@ def test_unpack_columns():
     np.testing.assert_array_equal((a["status"][:n] & 0x80) != 0, reset_first)
 
 
-def _rank_main(rank, world, m, port, q):
+def _rank_main(rank, world, m, store_file, q):
     import torch.distributed as dist
     from odigos_amd.exchange import route_and_sample
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a file rendezvous: no port to race for with tests running in parallel
+    dist.init_process_group("gloo", init_method="file://" + store_file, rank=rank, world_size=world)
     try:
         glob = synthetic_global_batch(world, m, 11)
         lo, hi = rank * m, (rank + 1) * m
@@ -141,8 +140,9 @@ def test_exchange_protocol_gloo(world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, 3000, port, q)) for r in range(world)]
+    import tempfile
+    store = os.path.join(tempfile.mkdtemp(prefix="ose_gloo_"), "store")
+    procs = [ctx.Process(target=_rank_main, args=(r, world, 3000, store, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
