@@ -551,8 +551,10 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   if (n && e->sampling_n_lat && (!c->start_ns || !c->end_ns || (!c->route_match && (!c->route || !c->arena))))
     return fail(OSE_EINVAL, "http_latency rules need start_ns, end_ns and route + arena (or route_match)");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
-  HIP_TRY(hipMemsetAsync(counts, 0, 8 * (size_t)n_ranks, st));
-  if (n == 0) return 0;
+  if (n == 0) {   // (otherwise shard_counts_kernel writes every owner's count)
+    HIP_TRY(hipMemsetAsync(counts, 0, 8 * (size_t)n_ranks, st));
+    return 0;
+  }
   const uint32_t T = (uint32_t)((n + kXChunk - 1) / kXChunk);   // packing waves
   const uint64_t H = (uint64_t)n_ranks * T;
   const uint32_t htiles = (uint32_t)((H + kScanTileItems - 1) / kScanTileItems);
