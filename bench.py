@@ -55,6 +55,7 @@ FUSED_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "re
 SAMPLE_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc", "res_svc_str")
 URL_KERNELS = ("url_plan_kernel", "url_plan_slow_kernel", "url_scan_kernel", "url_copy_kernel", "url_emit_slow_kernel")
 TRACE_KERNELS = ("trace_eval_kernel", "trace_dup_check", "trace_long_kernel")
+MULTI_KERNELS = ("trace_multi_kernel", "trace_dup_check")   # rule-chunked lists in one pass
 # the repeated-trace-id paths, each timed as one span of launches (run lists,
 # then the sort path for traces that overflow them)
 SLOW_KERNELS = ("trace_run_list", "trace_sort_path")
@@ -75,9 +76,9 @@ WORKLOADS = {
                                    "50M spans / ~5M traces per GPU, grouped by trace_id"),
     "sampling_wide": dict(gen="sampling", seed=0x0D160003, spans=50_000_000, per_gpu=True,
                           cfg="wide", stages="SAMPLE", null_columns=(), null_outputs=PER_TRACE_OUTS,
-                          fields=SAMPLE_FIELDS, kernels=TRACE_KERNELS + SLOW_KERNELS,
+                          fields=SAMPLE_FIELDS, kernels=MULTI_KERNELS[:1] + TRACE_KERNELS + SLOW_KERNELS,
                           metric_config="diagnostic: C3's batch under 1 error + 4 service + 150 latency rules "
-                                        "(three rule chunks, one trace-stage pass each)"),
+                                        "(three rule chunks, evaluated in one trace-stage pass)"),
     "zipf": dict(gen="zipf", seed=0x0D160005, spans=50_000_000, per_gpu=True,
                  cfg=None, stages="SAMPLE|TEMPLATE", null_columns=("res_url_ok",), null_outputs=PER_TRACE_OUTS,
                  fields=SAMPLE_FIELDS + ("kind", "url_flags", "path"), kernels=TRACE_KERNELS + SLOW_KERNELS + URL_KERNELS,

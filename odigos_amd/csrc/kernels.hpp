@@ -48,7 +48,6 @@ struct SizeKernelArgs {
   const ose_strref* tmpl;
   int64_t inverse;
   uint64_t* scope_body;       // [S] zeroed
-  uint32_t* scope_kept;       // [S] zeroed
   uint32_t* scope_had;        // [S] zeroed
   uint64_t* res_body;         // [R] zeroed
   uint32_t* res_alive;        // [R] zeroed
@@ -227,6 +226,11 @@ struct TraceKernelArgs {
   uint32_t long_steps;        // hand-off distance in 64-span steps (kLongSteps)
   uint32_t win_per_wave;      // 64-span windows whose run heads one wave owns (kWinPerWave)
   uint32_t narrow;            // the table's flag bits fit one word (trace_eval_kernel kNarrow)
+  // every rule chunk in one pass (trace_multi_kernel): n_multi (2..kMaxMulti)
+  // chunk tables, copied into cfg_lds_bytes of dynamic LDS (0: one table, a.cfg)
+  const uint8_t* const* cfgs;
+  uint32_t n_multi;
+  uint32_t cfg_lds_bytes;
   // run-list path (repeated trace ids, before the sort-based fallback):
   // trace_runs_kernel lists each trace's runs in its exact-table slot,
   // trace_fold_kernel folds the runs of every trace with 2..kMaxRuns runs
@@ -242,6 +246,9 @@ constexpr uint32_t kMaxFoldSlots = 8;     // latency services per trace one lane
 constexpr uint32_t kWinPerWave = 16;   // tools/gpu_wpw.sh: C5 0.97 -> 0.83 ms, C3 2.03 -> 1.99 ms, C4 unchanged
 constexpr uint32_t kLongSteps = 4;   // tools/gpu_long_iter.sh: C5 16 -> 4 steps 2.75 -> 2.13 ms, C3 unchanged
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
+// rule chunks one trace_multi_kernel pass evaluates, and their LDS budget
+constexpr uint32_t kMaxMulti = 3;
+constexpr uint32_t kMultiCfgLds = 24576;
 constexpr uint32_t kDupBucketCap = 1024;   // fingerprints per bucket (more: the exact path decides)
 void launch_trace_dup_check(const TraceKernelArgs& a, hipStream_t st);
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs = 0);

@@ -324,11 +324,30 @@ int Workspace::reserve_fold(uint64_t n_spans) {
 }
 
 namespace {
+// LDS bytes of every chunk's table (trace_multi_kernel's copy)
+uint32_t multi_cfg_bytes(const Engine* e) {
+  uint32_t t = 0;
+  for (const auto& h : e->sampling_chunks_host) {
+    const uint32_t nb = std::min<uint32_t>(reinterpret_cast<const SampCfgDev*>(h.data())->total_bytes, kSampCfgLds);
+    t += (nb + 15u) & ~15u;
+  }
+  return t;
+}
+// trace_multi_kernel takes the call: 2..kMaxMulti chunks whose tables fit
+// kMultiCfgLds together, no span_attribute rules, no spilled routes, spans
+// grouped by trace id in batch order with their own route columns
+bool multi_pass(const Engine* e, const ose_columns* c, uint32_t group_mode) {
+  const size_t K = e->sampling_chunks_host.size();
+  return K >= 2 && K <= kMaxMulti && group_mode == OSE_GROUP_TRACE_ID && c->n_spans && !e->sampling_n_attr &&
+         !e->sampling_spill && !c->route_match && !c->svc_match && multi_cfg_bytes(e) <= kMultiCfgLds;
+}
+
 // One pass of the trace stage over the rule tables of `chunk`; fold_in /
 // fold_out: the FoldState before / after this chunk's rules (run_sampling)
 int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
                       hipStream_t st, Workspace* ws, std::function<int()>* tail, uint32_t chunk,
-                      const FoldState* fold_in, FoldState* fold_out) {
+                      const FoldState* fold_in, FoldState* fold_out, uint32_t multi = 0,
+                      std::function<int()> redo = nullptr) {
   if (!e->has_sampling) return fail(OSE_EINVAL, "odigossampling is not configured on this engine");
   if (group_mode != OSE_GROUP_TRACE_ID && group_mode != OSE_GROUP_BATCH) return fail(OSE_EINVAL, "unknown group_mode");
   const uint64_t n = c->n_spans;
@@ -444,7 +463,12 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   if (const char* ab = getenv("OSE_TRACE_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);
 #endif
   a.n_long = misc + 12;
-  a.long_runs = a.mode == kTraceRuns ? long_runs : nullptr;
+  a.long_runs = a.mode == kTraceRuns && !multi ? long_runs : nullptr;
+  if (multi) {   // every chunk in one pass (run_sampling checked the conditions)
+    a.n_multi = multi;
+    a.cfgs = reinterpret_cast<const uint8_t* const*>(e->shard_tables_dev);
+    a.cfg_lds_bytes = multi_cfg_bytes(e);
+  }
   a.long_steps = kLongSteps;
   a.win_per_wave = kWinPerWave;
   {
@@ -472,7 +496,7 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     HIP_TRY(hipMemsetAsync(a.dup_bkt_count, 0, sizeof(uint32_t) << a.dup_bkt_bits, st));
   }
   Engine::Timed tm{};
-  e->prof_begin("trace_eval_kernel", st, tm);
+  e->prof_begin(multi ? "trace_multi_kernel" : "trace_eval_kernel", st, tm);
   launch_trace_eval(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
@@ -616,6 +640,21 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   return 0;
   };
   if (group_mode != OSE_GROUP_TRACE_ID) return rest(false);
+  if (multi) {
+    // the one-pass form decides batches without repeated trace ids; one with
+    // them (*dup) is redone pass per chunk, whose slow paths handle it
+    if (!ws->dup_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ws->dup_host), 64, hipHostMallocDefault));
+    if (!ws->dup_ready) HIP_TRY(hipEventCreateWithFlags(&ws->dup_ready, hipEventDisableTiming));
+    HIP_TRY(hipMemcpyAsync(ws->dup_host, misc, 64, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(ws->dup_ready, st));
+    auto finish = [rest, redo, ws]() -> int {
+      HIP_TRY(hipEventSynchronize(ws->dup_ready));
+      return ws->dup_host[0] ? redo() : rest(false);
+    };
+    if (!tail) return finish();
+    *tail = finish;
+    return 0;
+  }
   if (!tail) return rest(true);
   if (!ws->dup_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ws->dup_host), 64, hipHostMallocDefault));
   if (!ws->dup_ready) HIP_TRY(hipEventCreateWithFlags(&ws->dup_ready, hipEventDisableTiming));
@@ -677,20 +716,28 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // (one pass over the columns into partial records carrying every chunk's
   // words, decided by the owner fold, measured slower on sampling_wide:
   // 9.72 ms against 7.65, profiles/r4_owner_fold_forms.txt)
+  // one pass per chunk; each pass's slow paths host-gated as in a one-table
+  // call (the host waits for the pass's flags; the run-list and sort launches
+  // are queued only for a batch with repeated trace ids)
+  auto per_chunk = [=]() -> int {
   int rc = ws->reserve_fold(std::max<uint64_t>(c->n_spans, 1));
   if (rc) return rc;
   for (uint32_t k = 0; k < K; k++) {
     const FoldState* in = k ? static_cast<const FoldState*>(ws->fold[(k - 1) & 1]) : nullptr;
     FoldState* out = k + 1 < K ? static_cast<FoldState*>(ws->fold[k & 1]) : nullptr;
-    // each pass's slow paths host-gated as in a one-table call (the host waits
-    // for the pass's flags; the run-list and sort launches are queued only
-    // for a batch with repeated trace ids)
     std::function<int()> pass_tail;
     rc = run_sampling_pass(e, c, o, group_mode, rnd, st, ws, &pass_tail, k, in, out);
     if (!rc && pass_tail) rc = pass_tail();
     if (rc) return rc;
   }
   return 0;
+  };
+  // every chunk in one pass over the columns (trace_multi_kernel; sampling_wide
+  // 5.55 -> see DESIGN §4.2); a batch with repeated trace ids falls back to the
+  // passes per chunk
+  if (multi_pass(e, c, group_mode))
+    return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr, K, per_chunk);
+  return per_chunk();
 }
 
 }  // namespace ose

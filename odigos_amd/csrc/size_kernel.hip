@@ -67,7 +67,7 @@ __global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a)
   if (valid) {
     r = a.scope_resource[s];
     had = a.scope_had[s];
-    alive = !a.remove_empty || !had || a.scope_kept[s];   // an emptied ScopeSpans is removed
+    alive = !a.remove_empty || !had || a.scope_body[s] != 0;   // an emptied ScopeSpans is removed
     if (alive) contrib = field_len((uint64_t)a.scope_size[s] + a.scope_body[s]);
   }
   uint64_t v = contrib;

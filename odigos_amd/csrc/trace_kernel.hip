@@ -321,6 +321,29 @@ __device__ __forceinline__ uint64_t latency_satisfied(const Cfg& c, uint32_t slo
   return sat;
 }
 
+// A latency slot with two or more stretches in one closed trace (rep: a
+// stretch head whose slot the trace already had): the OR of its stretches'
+// results (lsat = lraw & ep, set by the caller) is not the trace's, so that
+// slot's monoid is scanned over the whole trace and its rules' bits replaced
+// at the trace's tail.  Only the repeated slots are rescanned (a step with
+// one repeat used to rescan every slot of its closed traces).
+__device__ __forceinline__ void rep_slots(const Cfg& c, bool rep, uint32_t slot, uint32_t hseg, bool ttail, uint64_t st,
+                                       uint64_t en, uint32_t rst, uint64_t ep, uint64_t& lsat) {
+  // the trace's repeated slots (a segmented OR of the rep lanes' slot bits)
+  uint32_t rlo = rep && slot < 32 ? 1u << slot : 0u, rhi = rep && slot >= 32 && slot != kNoSlot ? 1u << (slot - 32) : 0u;
+  seg_or2n_scan(hseg, rlo, rhi);
+  const uint64_t rm = (uint64_t)rlo | ((uint64_t)rhi << 32);
+  for (uint64_t pend = __ballot(rep); pend;) {
+    const uint32_t ks = rdl(slot, ffs64(pend));
+    const bool ink = slot == ks;
+    pend &= ~__ballot(ink);
+    Lat v = ink ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+    seg_lat_scan(hseg, v);
+    if (ttail && ((rm >> ks) & 1))
+      lsat = (lsat & ~c.slot_rules[ks]) | ((v.f & 2u) ? latency_satisfied(c, ks, ep, v.m, v.e) : 0ull);
+  }
+}
+
 // ShouldSample's level walk (rule_engine.go:55-83) over evaluateLevel's fold
 // (rule_engine.go:89-115).  level: 0..2 satisfied level, 3 min fallback, 4 none.
 __device__ __forceinline__ void decide(const Cfg& c, uint32_t err, uint64_t ep, uint64_t lsat, uint64_t svc, double u,
@@ -965,19 +988,8 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
       const uint64_t psm = dpp64<0x138, 0xF>(0ull, smask);   // lane - 1's inclusive slot bits
       const bool in_closed = mine && !(seg0_cont && lane <= t0) && !(last_open && lane >= sst_last);
       const bool rep = in_closed && shead && !hseg && slot != kNoSlot && ((psm >> slot) & 1);
-      if (__ballot(rep)) {
-        uint64_t pend = __ballot(slot != kNoSlot && in_closed);
-        while (pend) {
-          const uint32_t ks = rdl(slot, ffs64(pend));
-          const bool ink = slot == ks;
-          pend &= ~__ballot(ink);
-          Lat v = ink ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
-          seg_lat_scan(hseg, v);
-          if (tail && !carried_tail && (v.f & 2u)) lsat |= latency_satisfied(c, ks, ep, v.m, v.e);
-        }
-      } else if (tail && !carried_tail) {
-        lsat = lraw & ep;
-      }
+      if (tail && !carried_tail) lsat = lraw & ep;
+      if (__ballot(rep)) rep_slots(c, rep, slot, hseg, tail && !carried_tail, st, en, rst, ep, lsat);
     }
     // ---- the carried trace closes in this step: queue it ----
     const bool cont_close = seg0_cont && !(single && cont_next);
@@ -1056,6 +1068,300 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
   }
   flush_queue(a, c, Q, qn, lane);
   if (a.dup_bkt) flush_heads(a, HQ, hn, lane);
+}
+
+// ---- rule-chunked lists in one pass ---------------------------------------------
+// A rule list cut into K (2..kMaxMulti) chunks — no span_attribute rules, no
+// spilled routes, grouped by trace id — in one pass over the columns instead
+// of one per chunk: every chunk's table sits in LDS, each step evaluates each
+// chunk's endpoint, service and latency words exactly as trace_eval_kernel
+// does for one table, and a closed trace is queued with all K; the flush
+// walks the chunks in order (walk_chunk, then walk_finish: decide() over the
+// whole list, rule_engine.go:55-115).  Duplicate detection is the lean
+// instance's; a batch whose trace ids repeat is redone by the pass-per-chunk
+// path (run_sampling).  No long-run hand-off: a run's owner wave follows it.
+template <int K>
+struct MultiQ {
+  uint64_t hi[kQ], lo[kQ];
+  uint32_t pos[kQ], len[kQ], err[kQ];
+  uint64_t ep[K][kQ], lsat[K][kQ], svc[K][kQ];
+};
+
+template <int K>
+__device__ __forceinline__ void flush_multi(const TraceKernelArgs& a, const uint8_t* lds, const uint32_t (&coff)[K],
+                                            MultiQ<K>& Q, uint32_t& qn, int lane) {
+  if (!qn) return;
+  __builtin_amdgcn_wave_barrier();
+  uint8_t dk = 0, dl = 0;
+  double dr = 0;
+  uint32_t pos = 0, len = 0;
+  if ((uint32_t)lane < qn) {
+    pos = Q.pos[lane];
+    len = Q.len[lane];
+    FoldState s{0.0, 0.0, 0u, 0u};
+    const uint32_t err = Q.err[lane];
+#pragma unroll
+    for (int k = 0; k < K; k++) walk_chunk(load_cfg(lds + coff[k]), s, err, Q.ep[k][lane], Q.lsat[k][lane], Q.svc[k][lane]);
+    walk_finish(s, trace_uniform(Q.hi[lane], Q.lo[lane], a.seed), dk, dl, dr);
+    write_rec(a, pos, dk, dl, dr);
+  }
+  const uint32_t mlen = wave_max_u32((uint32_t)lane < qn ? len : 0u);
+  if (mlen <= 32) {
+    if ((uint32_t)lane < qn)
+      for (uint32_t q = 0; q < len; q++) a.keep[pos + q] = dk;
+  } else {
+    for (uint32_t e = 0; e < qn; e++) write_keep_range(a, rdl(pos, e), rdl(len, e), (uint8_t)rdl(dk, e), lane);
+  }
+  __builtin_amdgcn_wave_barrier();
+  qn = 0;
+}
+
+template <int K>
+__global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4))) void trace_multi_kernel(TraceKernelArgs a) {
+  extern __shared__ uint4 multi_cfg4[];
+  uint8_t* mcfg = reinterpret_cast<uint8_t*>(multi_cfg4);
+  __shared__ MultiQ<K> queues[kTWaves];
+  __shared__ HeadQ headqs[kTWaves];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = threadIdx.x >> 6;
+  MultiQ<K>& Q = queues[wv];
+  HeadQ& HQ = headqs[wv];
+  uint32_t coff[K];
+  {
+    // every chunk's table (each <= kSampCfgLds, together <= kMultiCfgLds:
+    // the host checks) into LDS
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint8_t* g = a.cfgs[k];
+      const uint32_t nb = cfg_lds_copy_bytes(g);
+      for (uint32_t x = threadIdx.x * 16; x < nb; x += kTThreads * 16)
+        *reinterpret_cast<uint4*>(mcfg + o + x) = *reinterpret_cast<const uint4*>(g + x);
+      coff[k] = o;
+      o += (nb + 15u) & ~15u;
+    }
+    __syncthreads();
+  }
+  const uint64_t wpw = a.win_per_wave;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * kTWaves + wv) * wpw;   // first owned window
+  if (w0 >= a.n_windows) return;
+  const uint64_t n = a.n_spans;
+  const uint32_t nsvc = load_cfg(mcfg).h->n_services;   // (the service ids are the engine's: every chunk's)
+
+  const uint64_t range_end = min((w0 + wpw) * kWave, n);
+  uint32_t qn = 0, hn = 0;
+  bool started = false, open = false;
+  uint32_t c_err = 0;
+  uint64_t c_pos = 0, c_hi = 0, c_lo = 0;
+  uint64_t c_ep[K], c_svc[K], c_kmask[K];
+  Lat cur[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    c_ep[k] = c_svc[k] = c_kmask[k] = 0;
+    cur[k] = Lat{0, kInf, 0};
+  }
+  uint64_t base = w0 * kWave;
+  StepRaw nx = load_raw(a, base, lane);
+  for (;;) {
+    StepRaw r = nx;
+    const bool valid = base + lane < n;
+    const bool hd = step_head(a, r, base, lane);
+    const bool work = started || __ballot(hd) != 0;   // wave-uniform: this step is evaluated
+    if (work && !r.full) r = load_raw(a, base, lane);
+    uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu;
+    uint4 rw = make_uint4(0, 0, 0, 0);
+    if (valid && work) {
+      sv = a.res_svc[r.res];
+      ss = a.res_svc_str[r.res];
+      if (r.route.len && sv < nsvc) {
+        // route bytes only for a service with latency rules in some chunk
+        bool need = false;
+#pragma unroll
+        for (int k = 0; k < K; k++) need |= load_cfg(mcfg + coff[k]).svc_slot[sv] != kNoSlot;
+        if (need) rw = head16(a.arena, r.route.off, r.route.len);
+      }
+    }
+    const uint64_t vmask = __ballot(valid);
+    const uint64_t hmask = __ballot(hd);
+    const bool in_range = base < range_end;
+    if (in_range) {
+      if (lane == 0 && a.win_heads) a.win_heads[base / kWave] = hmask;
+      if (hmask) {
+        const uint32_t nh = __popcll(hmask);
+        if (hn + nh > kHeadQ) flush_heads(a, HQ, hn, lane);
+        if (hd) {
+          const uint32_t e = hn + __popcll(hmask & lanemask_lt(lane));
+          HQ.cell[e] = (r.lo ^ ((r.hi << 29) | (r.hi >> 35))) * 0x9E3779B97F4A7C15ull;
+        }
+        hn += nh;
+      }
+    }
+    if (base + kWave < n) nx = load_raw(a, base + kWave, lane, work);   // prefetch the next step
+    uint64_t own;
+    if (in_range) {
+      if (!started) {
+        if (!hmask) {   // still inside a trace an earlier wave owns
+          base += kWave;
+          if (base >= range_end) break;
+          continue;
+        }
+        started = true;
+        own = vmask & ~lanemask_lt(ffs64(hmask));
+      } else {
+        own = vmask;
+      }
+    } else {
+      if (!open) break;
+      own = vmask & (hmask ? lanemask_lt(ffs64(hmask)) : ~0ull);
+    }
+    const uint64_t segmask = (hmask & own) | (open ? 1ull : 0ull);
+    const int last_own = fls64(own);
+    bool cont_next = false;
+    if (last_own == 63 && base + kWave < n) {
+      bool h = false;
+      if (lane == 63) h = r.ph != r.hi || r.pl != r.lo;   // lane 63 loaded the next step's first id
+      cont_next = !rdl((uint32_t)h, 63);
+    }
+    const bool mine = (own >> lane) & 1;
+    const int sst = mine ? fls64(segmask & lanemask_le(lane)) : lane;
+    const bool tail = mine && (lane == last_own || ((segmask >> (lane + 1)) & 1));
+    const uint64_t tails = __ballot(tail);
+    const int t0 = ffs64(tails);
+    const bool seg0_cont = open;
+    const bool single = t0 == last_own;
+    const bool last_open = cont_next && !(single && seg0_cont);
+    const int sst_last = rdl((uint32_t)sst, last_own);
+    const uint32_t hseg = mine ? (uint32_t)((segmask >> lane) & 1) : 1u;
+    const uint32_t rst = (r.status & kStatusReset) ? 1u : 0u;
+    uint32_t err = mine && (r.status & ~kStatusReset) == OSE_STATUS_ERROR ? 1u : 0u;
+    seg_or1_scan(hseg, err);
+    const bool carried_tail = (lane == t0 && seg0_cont) || (lane == last_own && last_open);
+    const bool in_closed = mine && !(seg0_cont && lane <= t0) && !(last_open && lane >= sst_last);
+    // ---- queue entries: the carried trace (if it closes), then this step's traces ----
+    const bool cont_close = seg0_cont && !(single && cont_next);
+    const uint64_t qmask = __ballot(tail && !carried_tail);
+    const uint32_t ncl = cont_close ? 1u : 0u, nq = __popcll(qmask);
+    if (qn + ncl + nq > (uint32_t)kQ) flush_multi<K>(a, mcfg, coff, Q, qn, lane);
+    const uint32_t qcl = qn;
+    const uint32_t qe = qn + ncl + __popcll(qmask & lanemask_lt(lane));
+    const bool queued = (qmask >> lane) & 1;
+    if (cont_close && lane == 0) {
+      Q.err[qcl] = c_err | rdl(err, t0);
+      Q.hi[qcl] = c_hi;
+      Q.lo[qcl] = c_lo;
+      Q.pos[qcl] = (uint32_t)c_pos;
+      Q.len[qcl] = (uint32_t)(base + t0 + 1 - c_pos);
+    }
+    if (queued) {
+      Q.err[qe] = err;
+      Q.hi[qe] = r.hi;
+      Q.lo[qe] = r.lo;
+      Q.pos[qe] = (uint32_t)(base + sst);
+      Q.len[qe] = (uint32_t)(lane - sst + 1);
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const Cfg c = load_cfg(mcfg + coff[k]);
+      // ---- per-span contributions under chunk k's tables ----
+      uint32_t slot = kNoSlot;
+      uint64_t ep = 0, svcb = 0, st = 0, en = 0;
+      if (mine) {
+        if (ss < nsvc) svcb = c.svc_bits[ss];
+        if (sv < nsvc) {
+          slot = c.svc_slot[sv];
+          if (slot != kNoSlot) {
+            ep = endpoint_bits_w(c, slot, a.arena, r.route, rw);
+            st = r.start;
+            en = r.end;
+          }
+        }
+      }
+      seg_or2_scan(hseg, ep, svcb);
+      // ---- latency state (trace_eval_kernel's, per chunk) ----
+      uint64_t lsat = 0, n_kmask = 0;
+      Lat nxt{0, kInf, 0};
+      if (__ballot(slot != kNoSlot)) {
+        const uint32_t pslot = dpp_mov<0x138>(kNoSlot, slot);
+        const bool shead = !mine || hseg || pslot != slot;
+        const uint32_t hs = shead ? 1u : 0u;
+        const bool stail = mine && dpp_mov<0x130>(1u, hs) != 0;
+        Lat v = slot != kNoSlot ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+        seg_lat_scan(hs, v);
+        const bool lt = stail && (v.f & 2u);
+        uint64_t lraw = 0, smask = 0;
+        if (lt) lraw = latency_satisfied(c, slot, ~0ull, v.m, v.e);
+        if (slot != kNoSlot) smask = 1ull << slot;
+        if (seg0_cont) {
+          for (uint64_t m0 = __ballot(lt && lane <= t0); m0; m0 &= m0 - 1) {
+            const int L = ffs64(m0);
+            const uint32_t ks = rdl(slot, L);
+            const Lat v0{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
+            if ((uint32_t)lane == ks) cur[k] = lat_comb(cur[k], v0);
+            c_kmask[k] |= 1ull << ks;
+          }
+        }
+        if (last_open) {
+          for (uint64_t m1 = __ballot(lt && lane >= sst_last); m1; m1 &= m1 - 1) {
+            const int L = ffs64(m1);
+            const uint32_t ks = rdl(slot, L);
+            const Lat v1{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
+            if ((uint32_t)lane == ks) nxt = lat_comb(nxt, v1);
+            n_kmask |= 1ull << ks;
+          }
+        }
+        seg_or2_scan(hseg, lraw, smask);
+        const uint64_t psm = dpp64<0x138, 0xF>(0ull, smask);
+        const bool rep = in_closed && shead && !hseg && slot != kNoSlot && ((psm >> slot) & 1);
+        if (tail && !carried_tail) lsat = lraw & ep;
+        if (__ballot(rep)) rep_slots(c, rep, slot, hseg, tail && !carried_tail, st, en, rst, ep, lsat);
+      }
+      // ---- chunk k's words of the queued traces ----
+      if (cont_close) {
+        const uint64_t EP = c_ep[k] | rdl64(ep, t0);
+        const uint64_t SV = c_svc[k] | rdl64(svcb, t0);
+        uint64_t s_l = 0;
+        if ((c_kmask[k] >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, cur[k].m, cur[k].e);
+        s_l = wave_or64(s_l);
+        if (lane == 0) {
+          Q.ep[k][qcl] = EP;
+          Q.lsat[k][qcl] = s_l;
+          Q.svc[k][qcl] = SV;
+        }
+        cur[k] = Lat{0, kInf, 0};
+        c_kmask[k] = 0;
+      }
+      if (queued) {
+        Q.ep[k][qe] = ep;
+        Q.lsat[k][qe] = lsat;
+        Q.svc[k][qe] = svcb;
+      }
+      // ---- carry into the next step ----
+      if (last_open) {
+        c_ep[k] = rdl64(ep, last_own);
+        c_svc[k] = rdl64(svcb, last_own);
+        cur[k] = nxt;
+        c_kmask[k] = n_kmask;
+      } else if (seg0_cont && single && cont_next) {
+        c_ep[k] |= rdl64(ep, t0);
+        c_svc[k] |= rdl64(svcb, t0);
+      }
+    }
+    qn += ncl + nq;
+    if (cont_close) open = false;
+    if (last_open) {
+      open = true;
+      c_pos = base + sst_last;
+      c_hi = rdl64(r.hi, sst_last);
+      c_lo = rdl64(r.lo, sst_last);
+      c_err = rdl(err, last_own);
+    } else if (seg0_cont && single && cont_next) {
+      c_err |= rdl(err, t0);
+    }
+    base += kWave;
+    if (!open && base >= range_end) break;
+  }
+  flush_multi<K>(a, mcfg, coff, Q, qn, lane);
+  flush_heads(a, HQ, hn, lane);
 }
 
 // ---- long runs ------------------------------------------------------------------
@@ -2159,6 +2465,13 @@ void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, u
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
   const uint32_t per_block = kTWaves * a.win_per_wave;
   const uint32_t blocks = (a.n_windows + per_block - 1) / per_block;
+  if (a.n_multi) {   // every rule chunk in one pass (run_sampling checks the conditions)
+    if (a.n_multi == 2)
+      hipLaunchKernelGGL((trace_multi_kernel<2>), dim3(blocks), dim3(kTThreads), a.cfg_lds_bytes, st, a);
+    else
+      hipLaunchKernelGGL((trace_multi_kernel<3>), dim3(blocks), dim3(kTThreads), a.cfg_lds_bytes, st, a);
+    return;
+  }
   if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate) {
     const bool chunk = a.fold_in || a.fold_out;
     if (a.narrow && chunk)

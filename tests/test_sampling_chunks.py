@@ -22,9 +22,10 @@ from odigos_amd.batch import Generator
 from tests.oracle_lib import intern_services, lib as orc_lib
 from tests.test_sampling_random import SEED, _arr, _group, _py_eval, gpu_vs_oracle, inject_zero_starts, oracle_run
 from tests.workloads import (check_interning, long_routes_config, wide_attr100_config, wide_attr_config,
-                             wide_latency_config, wide_mixed_config)
+                             wide_latency2_config, wide_latency_config, wide_mixed_config)
 
-CONFIGS = {"latency": wide_latency_config, "mixed": wide_mixed_config, "long_routes": long_routes_config}
+CONFIGS = {"latency": wide_latency_config, "latency2": wide_latency2_config, "mixed": wide_mixed_config,
+           "long_routes": long_routes_config}
 
 
 def _chunks(cfg):
@@ -39,6 +40,7 @@ def test_chunk_counts():
     from tests.workloads import c3_sampling_config
     assert _chunks(c3_sampling_config()) == 1
     assert _chunks(wide_latency_config()) == 3          # 150 latency rules: 64 + 64 + 22
+    assert _chunks(wide_latency2_config()) == 2
     assert _chunks(wide_attr_config()) == 2             # 64 service + attr bits fill the first
     assert _chunks(wide_mixed_config()) >= 4
     assert _chunks(long_routes_config()) >= 2           # route bytes past the 12 KiB table
@@ -202,6 +204,39 @@ def test_gpu_wide_config(name, shuffle):
     g = Generator("sampling", seed=0x0D1607B1 + int(shuffle), n_spans=200_000, shuffle=shuffle)
     inject_zero_starts(g, 0.01, 9)
     gpu_vs_oracle(g, cfg=CONFIGS[name]())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["latency", "latency2"])
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_gpu_multi_chunk_pass(name, shuffle):
+    # 2 and 3 rule chunks without span_attribute rules: every chunk in one
+    # pass over the columns (trace_multi_kernel); a batch with repeated trace
+    # ids is then redone pass per chunk (trace_eval_kernel, the slow paths)
+    g = Generator("sampling", seed=0x0D160901 + int(shuffle), n_spans=300_000, shuffle=shuffle)
+    inject_zero_starts(g, 0.01, 7)
+    ran = set()
+    ho = gpu_vs_oracle(g, cfg=CONFIGS[name](), kernels=ran)
+    assert "trace_multi_kernel" in ran, ran
+    assert ("trace_eval_kernel" in ran) == shuffle, ran
+    t = int(ho.view("trace_count", np.uint32)[0])
+    assert len(set(ho.view("trace_level", np.uint8)[:t].tolist())) >= 2
+
+
+@pytest.mark.gpu
+def test_gpu_multi_chunk_pass_edges():
+    # batches of one span, one step, a ragged last step and one long trace
+    # followed by its owner wave (no long-run hand-off in the one-pass form)
+    from tests.workloads import wide_latency_config
+    for n in (1, 63, 64, 65, 1000):
+        ran = set()
+        gpu_vs_oracle(Generator("sampling", seed=0x0D160911 + n, n_spans=n), cfg=wide_latency_config(), kernels=ran)
+        assert "trace_multi_kernel" in ran
+    g = Generator("zipf", seed=0x0D160921, n_spans=200_000)
+    inject_zero_starts(g, 0.01, 4)
+    ran = set()
+    gpu_vs_oracle(g, cfg=wide_latency_config(), kernels=ran)
+    assert "trace_multi_kernel" in ran
 
 
 def _attr_bits(g, rules, seed, p=0.02):

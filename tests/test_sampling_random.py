@@ -181,7 +181,8 @@ def test_oracle_levels_cover_all_outcomes():
 
 
 # ---------------- GPU parity ----------------
-def gpu_vs_oracle(g, mode=native.GROUP_TRACE_ID, cfg=CFG, per_trace=True, seed=SEED):
+def gpu_vs_oracle(g, mode=native.GROUP_TRACE_ID, cfg=CFG, per_trace=True, seed=SEED, kernels=None):
+    """kernels: a set the names of the launches the call profiled are added to"""
     import torch
     from odigos_amd.batch import DeviceBatch, Engine
     eng = Engine({"odigossampling": cfg})
@@ -189,8 +190,12 @@ def gpu_vs_oracle(g, mode=native.GROUP_TRACE_ID, cfg=CFG, per_trace=True, seed=S
     if not per_trace:
         for f in ("trace_count", "trace_first_span", "trace_keep", "trace_level", "trace_ratio"):
             setattr(db.outs, f, None)
+    if kernels is not None:
+        eng.profile(True)
     eng.process_device(db, native.STAGE_SAMPLE, mode, seed=seed)
     torch.cuda.synchronize()
+    if kernels is not None:
+        kernels.update(eng.profile_read())
     assert int(db.out_numpy("device_status", np.uint32)[0]) == 0
     ho = oracle_run(g.cols, mode, seed=seed, cfg=cfg)
     n = g.cols.n_spans

@@ -67,6 +67,13 @@ def wide_latency_config():
             "endpoint_rules": [_wide_lat(j, j % 64) for j in range(150)]}
 
 
+def wide_latency2_config():
+    """100 http_latency rules (2 chunks: 64 + 36) over services 0..63."""
+    cfg = wide_latency_config()
+    cfg["endpoint_rules"] = cfg["endpoint_rules"][:100]
+    return cfg
+
+
 def wide_mixed_config():
     """Chunk boundaries inside and across levels: 80 latency rules in the
     global level (services 0..39), 100 service_name rules over services
