@@ -653,9 +653,26 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
     }
     e->sampling_blob_dev = e->sampling_chunks_dev[0];
     const size_t K = e->sampling_chunks_dev.size(), L = e->sampling_lat_svc.size();
-    std::vector<uint8_t> st(8 * K + 4 * L);
+    // then trace_multi_kernel's latency-service ids: [n_services] the index of
+    // each service among those with http_latency rules in any chunk (or
+    // 0xFFFFFFFF), [64] the service of each index
+    const size_t S = e->service_ids.size();
+    std::vector<uint32_t> gof(S, 0xFFFFFFFFu), gsvc(64, 0);
+    uint32_t ng = 0;
+    for (size_t v = 0; v < S; v++)
+      if ((e->sampling_lat_svc[v >> 5] >> (v & 31)) & 1u) {
+        if (ng < 64) {
+          gof[v] = ng;
+          gsvc[ng] = (uint32_t)v;
+        }
+        ng++;
+      }
+    e->sampling_n_lat_svc = ng;
+    std::vector<uint8_t> st(8 * K + 4 * L + 4 * S + 4 * 64);
     std::memcpy(st.data(), e->sampling_chunks_dev.data(), 8 * K);
     std::memcpy(st.data() + 8 * K, e->sampling_lat_svc.data(), 4 * L);
+    if (S) std::memcpy(st.data() + 8 * K + 4 * L, gof.data(), 4 * S);
+    std::memcpy(st.data() + 8 * K + 4 * L + 4 * S, gsvc.data(), 4 * 64);
     rc = upload(st, &e->shard_tables_dev);
     if (rc) { delete e; return rc; }
   }

@@ -230,7 +230,8 @@ struct TraceKernelArgs {
   // chunk tables, copied into cfg_lds_bytes of dynamic LDS (0: one table, a.cfg)
   const uint8_t* const* cfgs;
   uint32_t n_multi;
-  uint32_t cfg_lds_bytes;
+  uint32_t cfg_lds_bytes;     // the tables, then the latency-service ids (lat_gslot)
+  const uint32_t* lat_gslot;  // [n_services] index among the latency services, [64] their service ids
   // run-list path (repeated trace ids, before the sort-based fallback):
   // trace_runs_kernel lists each trace's runs in its exact-table slot,
   // trace_fold_kernel folds the runs of every trace with 2..kMaxRuns runs

@@ -122,6 +122,25 @@ __device__ __forceinline__ void seg_or2_scan(uint32_t h, uint64_t& x, uint64_t& 
   seg_or2_step<0x142, 0xA>(h, x, y);
   seg_or2_step<0x143, 0xC>(h, x, y);
 }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_or3_step(uint32_t& h, uint64_t& x, uint64_t& y, uint64_t& z) {
+  const uint32_t oh = dpp_mov<CTRL, ROWS>(0u, h);
+  const uint64_t ox = dpp64<CTRL, ROWS>(0ull, x), oy = dpp64<CTRL, ROWS>(0ull, y), oz = dpp64<CTRL, ROWS>(0ull, z);
+  if (!h) {
+    x |= ox;
+    y |= oy;
+    z |= oz;
+  }
+  h |= oh;
+}
+__device__ __forceinline__ void seg_or_scan3(uint32_t h, uint64_t& x, uint64_t& y, uint64_t& z) {
+  seg_or3_step<0x111, 0xF>(h, x, y, z);
+  seg_or3_step<0x112, 0xF>(h, x, y, z);
+  seg_or3_step<0x114, 0xF>(h, x, y, z);
+  seg_or3_step<0x118, 0xF>(h, x, y, z);
+  seg_or3_step<0x142, 0xA>(h, x, y, z);
+  seg_or3_step<0x143, 0xC>(h, x, y, z);
+}
 
 // one 32-bit word (kNarrow: the error bit, endpoint bits and service bits packed)
 template <int CTRL, int ROWS>
@@ -1127,9 +1146,11 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
   MultiQ<K>& Q = queues[wv];
   HeadQ& HQ = headqs[wv];
   uint32_t coff[K];
+  const uint32_t nsvc = reinterpret_cast<const SampCfgDev*>(a.cfgs[0])->n_services;   // (the engine's: every chunk's)
+  const uint32_t* gslot_of;   // LDS: latency-service index of each service, then the service of each index
   {
-    // every chunk's table (each <= kSampCfgLds, together <= kMultiCfgLds:
-    // the host checks) into LDS
+    // every chunk's table (each <= kSampCfgLds, together <= kMultiCfgLds with
+    // the latency-service ids: the host checks) into LDS
     uint32_t o = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -1140,26 +1161,26 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
       coff[k] = o;
       o += (nb + 15u) & ~15u;
     }
+    uint32_t* gl = reinterpret_cast<uint32_t*>(mcfg + o);
+    for (uint32_t x = threadIdx.x; x < nsvc + 64; x += kTThreads) gl[x] = a.lat_gslot[x];
+    gslot_of = gl;
     __syncthreads();
   }
+  const uint32_t* gsvc = gslot_of + nsvc;
   const uint64_t wpw = a.win_per_wave;
   const uint64_t w0 = ((uint64_t)blockIdx.x * kTWaves + wv) * wpw;   // first owned window
   if (w0 >= a.n_windows) return;
   const uint64_t n = a.n_spans;
-  const uint32_t nsvc = load_cfg(mcfg).h->n_services;   // (the service ids are the engine's: every chunk's)
 
   const uint64_t range_end = min((w0 + wpw) * kWave, n);
   uint32_t qn = 0, hn = 0;
   bool started = false, open = false;
   uint32_t c_err = 0;
-  uint64_t c_pos = 0, c_hi = 0, c_lo = 0;
-  uint64_t c_ep[K], c_svc[K], c_kmask[K];
-  Lat cur[K];
+  uint64_t c_pos = 0, c_hi = 0, c_lo = 0, c_kmask = 0;
+  Lat cur{0, kInf, 0};   // lane g: the open trace's latency monoid for latency service g
+  uint64_t c_ep[K], c_svc[K];
 #pragma unroll
-  for (int k = 0; k < K; k++) {
-    c_ep[k] = c_svc[k] = c_kmask[k] = 0;
-    cur[k] = Lat{0, kInf, 0};
-  }
+  for (int k = 0; k < K; k++) c_ep[k] = c_svc[k] = 0;
   uint64_t base = w0 * kWave;
   StepRaw nx = load_raw(a, base, lane);
   for (;;) {
@@ -1168,17 +1189,15 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
     const bool hd = step_head(a, r, base, lane);
     const bool work = started || __ballot(hd) != 0;   // wave-uniform: this step is evaluated
     if (work && !r.full) r = load_raw(a, base, lane);
-    uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu;
+    uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu, gs0 = kNoSlot;
     uint4 rw = make_uint4(0, 0, 0, 0);
     if (valid && work) {
       sv = a.res_svc[r.res];
       ss = a.res_svc_str[r.res];
-      if (r.route.len && sv < nsvc) {
-        // route bytes only for a service with latency rules in some chunk
-        bool need = false;
-#pragma unroll
-        for (int k = 0; k < K; k++) need |= load_cfg(mcfg + coff[k]).svc_slot[sv] != kNoSlot;
-        if (need) rw = head16(a.arena, r.route.off, r.route.len);
+      if (sv < nsvc) {
+        gs0 = gslot_of[sv];
+        // route bytes only for a service with latency rules (in some chunk)
+        if (gs0 != kNoSlot && r.route.len) rw = head16(a.arena, r.route.off, r.route.len);
       }
     }
     const uint64_t vmask = __ballot(valid);
@@ -1233,18 +1252,112 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
     const int sst_last = rdl((uint32_t)sst, last_own);
     const uint32_t hseg = mine ? (uint32_t)((segmask >> lane) & 1) : 1u;
     const uint32_t rst = (r.status & kStatusReset) ? 1u : 0u;
-    uint32_t err = mine && (r.status & ~kStatusReset) == OSE_STATUS_ERROR ? 1u : 0u;
-    seg_or1_scan(hseg, err);
     const bool carried_tail = (lane == t0 && seg0_cont) || (lane == last_own && last_open);
+    const bool ttail = tail && !carried_tail;   // the tail of a trace that opens and closes in this step
     const bool in_closed = mine && !(seg0_cont && lane <= t0) && !(last_open && lane >= sst_last);
-    // ---- queue entries: the carried trace (if it closes), then this step's traces ----
+
+    // ---- per-span words of every chunk ----
+    const uint32_t gs = mine ? gs0 : kNoSlot;
+    uint32_t err = mine && (r.status & ~kStatusReset) == OSE_STATUS_ERROR ? 1u : 0u;
+    uint64_t st = 0, en = 0;
+    if (gs != kNoSlot) {
+      st = r.start;
+      en = r.end;
+    }
+    uint64_t ep[K], svcb[K], lsat[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const Cfg c = load_cfg(mcfg + coff[k]);
+      ep[k] = svcb[k] = lsat[k] = 0;
+      if (mine && ss < nsvc) svcb[k] = c.svc_bits[ss];
+      if (gs != kNoSlot) {
+        const uint32_t slot = c.svc_slot[sv];
+        if (slot != kNoSlot) ep[k] = endpoint_bits_w(c, slot, a.arena, r.route, rw);
+      }
+    }
+    // ---- latency state, once for every chunk: stretches of one trace and
+    // one latency service (a chunk's slots are its services with rules: the
+    // same stretches); the stretch tails' threshold tests per chunk ----
+    uint64_t n_kmask = 0, smask = 0;
+    Lat nxt{0, kInf, 0};
+    bool rep = false;
+    if (__ballot(gs != kNoSlot)) {
+      const uint32_t pgs = dpp_mov<0x138>(kNoSlot, gs);
+      const bool shead = !mine || hseg || pgs != gs;
+      const uint32_t hs = shead ? 1u : 0u;
+      const bool stail = mine && dpp_mov<0x130>(1u, hs) != 0;
+      Lat v = gs != kNoSlot ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+      seg_lat_scan(hs, v);
+      const bool lt = stail && (v.f & 2u);
+      if (lt) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          const Cfg c = load_cfg(mcfg + coff[k]);
+          const uint32_t slot = c.svc_slot[sv];
+          if (slot != kNoSlot) lsat[k] = latency_satisfied(c, slot, ~0ull, v.m, v.e);   // (ORed over the trace below)
+        }
+      }
+      if (gs != kNoSlot) smask = 1ull << gs;
+      if (seg0_cont) {   // the carried trace's stretches, in order
+        for (uint64_t m0 = __ballot(lt && lane <= t0); m0; m0 &= m0 - 1) {
+          const int L = ffs64(m0);
+          const uint32_t ks = rdl(gs, L);
+          const Lat v0{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
+          if ((uint32_t)lane == ks) cur = lat_comb(cur, v0);
+          c_kmask |= 1ull << ks;
+        }
+      }
+      if (last_open) {   // the open trace's stretches, in order
+        for (uint64_t m1 = __ballot(lt && lane >= sst_last); m1; m1 &= m1 - 1) {
+          const int L = ffs64(m1);
+          const uint32_t ks = rdl(gs, L);
+          const Lat v1{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
+          if ((uint32_t)lane == ks) nxt = lat_comb(nxt, v1);
+          n_kmask |= 1ull << ks;
+        }
+      }
+      uint32_t slo = (uint32_t)smask, shi = (uint32_t)(smask >> 32);
+      seg_or2n_scan(hseg, slo, shi);
+      const uint64_t psm = dpp64<0x138, 0xF>(0ull, (uint64_t)slo | ((uint64_t)shi << 32));   // lane - 1's inclusive bits
+      rep = in_closed && shead && !hseg && gs != kNoSlot && ((psm >> gs) & 1);
+    }
+    // ---- segmented ORs per trace: error, then each chunk's words ----
+    seg_or1_scan(hseg, err);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      seg_or_scan3(hseg, ep[k], svcb[k], lsat[k]);
+      lsat[k] = ttail ? lsat[k] & ep[k] : 0ull;
+    }
+    if (__ballot(rep)) {
+      // a latency service with two or more stretches in a closed trace: its
+      // monoid over the whole trace, and its rules' bits replaced per chunk
+      uint32_t rlo = rep && gs < 32 ? 1u << gs : 0u, rhi = rep && gs >= 32 && gs != kNoSlot ? 1u << (gs - 32) : 0u;
+      seg_or2n_scan(hseg, rlo, rhi);
+      const uint64_t rm = (uint64_t)rlo | ((uint64_t)rhi << 32);
+      for (uint64_t pend = __ballot(rep); pend;) {
+        const uint32_t ks = rdl(gs, ffs64(pend));
+        const bool ink = gs == ks;
+        pend &= ~__ballot(ink);
+        Lat w = ink ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
+        seg_lat_scan(hseg, w);
+        if (ttail && ((rm >> ks) & 1)) {
+#pragma unroll
+          for (int k = 0; k < K; k++) {
+            const Cfg c = load_cfg(mcfg + coff[k]);
+            const uint32_t slot = c.svc_slot[gsvc[ks]];
+            if (slot != kNoSlot)
+              lsat[k] = (lsat[k] & ~c.slot_rules[slot]) | ((w.f & 2u) ? latency_satisfied(c, slot, ep[k], w.m, w.e) : 0ull);
+          }
+        }
+      }
+    }
+    // ---- queue the carried trace (if it closes) and this step's traces ----
     const bool cont_close = seg0_cont && !(single && cont_next);
-    const uint64_t qmask = __ballot(tail && !carried_tail);
+    const uint64_t qmask = __ballot(ttail);
     const uint32_t ncl = cont_close ? 1u : 0u, nq = __popcll(qmask);
     if (qn + ncl + nq > (uint32_t)kQ) flush_multi<K>(a, mcfg, coff, Q, qn, lane);
     const uint32_t qcl = qn;
     const uint32_t qe = qn + ncl + __popcll(qmask & lanemask_lt(lane));
-    const bool queued = (qmask >> lane) & 1;
     if (cont_close && lane == 0) {
       Q.err[qcl] = c_err | rdl(err, t0);
       Q.hi[qcl] = c_hi;
@@ -1252,7 +1365,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
       Q.pos[qcl] = (uint32_t)c_pos;
       Q.len[qcl] = (uint32_t)(base + t0 + 1 - c_pos);
     }
-    if (queued) {
+    if (ttail) {
       Q.err[qe] = err;
       Q.hi[qe] = r.hi;
       Q.lo[qe] = r.lo;
@@ -1261,99 +1374,49 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const Cfg c = load_cfg(mcfg + coff[k]);
-      // ---- per-span contributions under chunk k's tables ----
-      uint32_t slot = kNoSlot;
-      uint64_t ep = 0, svcb = 0, st = 0, en = 0;
-      if (mine) {
-        if (ss < nsvc) svcb = c.svc_bits[ss];
-        if (sv < nsvc) {
-          slot = c.svc_slot[sv];
-          if (slot != kNoSlot) {
-            ep = endpoint_bits_w(c, slot, a.arena, r.route, rw);
-            st = r.start;
-            en = r.end;
-          }
-        }
-      }
-      seg_or2_scan(hseg, ep, svcb);
-      // ---- latency state (trace_eval_kernel's, per chunk) ----
-      uint64_t lsat = 0, n_kmask = 0;
-      Lat nxt{0, kInf, 0};
-      if (__ballot(slot != kNoSlot)) {
-        const uint32_t pslot = dpp_mov<0x138>(kNoSlot, slot);
-        const bool shead = !mine || hseg || pslot != slot;
-        const uint32_t hs = shead ? 1u : 0u;
-        const bool stail = mine && dpp_mov<0x130>(1u, hs) != 0;
-        Lat v = slot != kNoSlot ? Lat{(st == 0 || rst) ? 3u : 2u, st == 0 ? kInf : st, en} : Lat{0u, kInf, 0ull};
-        seg_lat_scan(hs, v);
-        const bool lt = stail && (v.f & 2u);
-        uint64_t lraw = 0, smask = 0;
-        if (lt) lraw = latency_satisfied(c, slot, ~0ull, v.m, v.e);
-        if (slot != kNoSlot) smask = 1ull << slot;
-        if (seg0_cont) {
-          for (uint64_t m0 = __ballot(lt && lane <= t0); m0; m0 &= m0 - 1) {
-            const int L = ffs64(m0);
-            const uint32_t ks = rdl(slot, L);
-            const Lat v0{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
-            if ((uint32_t)lane == ks) cur[k] = lat_comb(cur[k], v0);
-            c_kmask[k] |= 1ull << ks;
-          }
-        }
-        if (last_open) {
-          for (uint64_t m1 = __ballot(lt && lane >= sst_last); m1; m1 &= m1 - 1) {
-            const int L = ffs64(m1);
-            const uint32_t ks = rdl(slot, L);
-            const Lat v1{rdl(v.f, L), rdl64(v.m, L), rdl64(v.e, L)};
-            if ((uint32_t)lane == ks) nxt = lat_comb(nxt, v1);
-            n_kmask |= 1ull << ks;
-          }
-        }
-        seg_or2_scan(hseg, lraw, smask);
-        const uint64_t psm = dpp64<0x138, 0xF>(0ull, smask);
-        const bool rep = in_closed && shead && !hseg && slot != kNoSlot && ((psm >> slot) & 1);
-        if (tail && !carried_tail) lsat = lraw & ep;
-        if (__ballot(rep)) rep_slots(c, rep, slot, hseg, tail && !carried_tail, st, en, rst, ep, lsat);
-      }
-      // ---- chunk k's words of the queued traces ----
       if (cont_close) {
-        const uint64_t EP = c_ep[k] | rdl64(ep, t0);
-        const uint64_t SV = c_svc[k] | rdl64(svcb, t0);
+        const Cfg c = load_cfg(mcfg + coff[k]);
+        const uint64_t EP = c_ep[k] | rdl64(ep[k], t0);
         uint64_t s_l = 0;
-        if ((c_kmask[k] >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, cur[k].m, cur[k].e);
+        if ((c_kmask >> lane) & 1) {
+          const uint32_t slot = c.svc_slot[gsvc[lane]];
+          if (slot != kNoSlot) s_l = latency_satisfied(c, slot, EP, cur.m, cur.e);
+        }
         s_l = wave_or64(s_l);
         if (lane == 0) {
           Q.ep[k][qcl] = EP;
           Q.lsat[k][qcl] = s_l;
-          Q.svc[k][qcl] = SV;
+          Q.svc[k][qcl] = c_svc[k] | rdl64(svcb[k], t0);
         }
-        cur[k] = Lat{0, kInf, 0};
-        c_kmask[k] = 0;
       }
-      if (queued) {
-        Q.ep[k][qe] = ep;
-        Q.lsat[k][qe] = lsat;
-        Q.svc[k][qe] = svcb;
+      if (ttail) {
+        Q.ep[k][qe] = ep[k];
+        Q.lsat[k][qe] = lsat[k];
+        Q.svc[k][qe] = svcb[k];
       }
       // ---- carry into the next step ----
       if (last_open) {
-        c_ep[k] = rdl64(ep, last_own);
-        c_svc[k] = rdl64(svcb, last_own);
-        cur[k] = nxt;
-        c_kmask[k] = n_kmask;
+        c_ep[k] = rdl64(ep[k], last_own);
+        c_svc[k] = rdl64(svcb[k], last_own);
       } else if (seg0_cont && single && cont_next) {
-        c_ep[k] |= rdl64(ep, t0);
-        c_svc[k] |= rdl64(svcb, t0);
+        c_ep[k] |= rdl64(ep[k], t0);
+        c_svc[k] |= rdl64(svcb[k], t0);
       }
     }
     qn += ncl + nq;
-    if (cont_close) open = false;
+    if (cont_close) {
+      open = false;
+      cur = Lat{0, kInf, 0};
+      c_kmask = 0;
+    }
     if (last_open) {
       open = true;
       c_pos = base + sst_last;
       c_hi = rdl64(r.hi, sst_last);
       c_lo = rdl64(r.lo, sst_last);
       c_err = rdl(err, last_own);
+      cur = nxt;
+      c_kmask = n_kmask;
     } else if (seg0_cont && single && cont_next) {
       c_err |= rdl(err, t0);
     }

@@ -22,10 +22,10 @@ from odigos_amd.batch import Generator
 from tests.oracle_lib import intern_services, lib as orc_lib
 from tests.test_sampling_random import SEED, _arr, _group, _py_eval, gpu_vs_oracle, inject_zero_starts, oracle_run
 from tests.workloads import (check_interning, long_routes_config, wide_attr100_config, wide_attr_config,
-                             wide_latency2_config, wide_latency_config, wide_mixed_config)
+                             wide_latency2_config, wide_latency_config, wide_latency_split_config, wide_mixed_config)
 
-CONFIGS = {"latency": wide_latency_config, "latency2": wide_latency2_config, "mixed": wide_mixed_config,
-           "long_routes": long_routes_config}
+CONFIGS = {"latency": wide_latency_config, "latency2": wide_latency2_config, "latency_split": wide_latency_split_config,
+           "mixed": wide_mixed_config, "long_routes": long_routes_config}
 
 
 def _chunks(cfg):
@@ -41,6 +41,7 @@ def test_chunk_counts():
     assert _chunks(c3_sampling_config()) == 1
     assert _chunks(wide_latency_config()) == 3          # 150 latency rules: 64 + 64 + 22
     assert _chunks(wide_latency2_config()) == 2
+    assert _chunks(wide_latency_split_config()) == 2
     assert _chunks(wide_attr_config()) == 2             # 64 service + attr bits fill the first
     assert _chunks(wide_mixed_config()) >= 4
     assert _chunks(long_routes_config()) >= 2           # route bytes past the 12 KiB table
@@ -207,7 +208,7 @@ def test_gpu_wide_config(name, shuffle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["latency", "latency2"])
+@pytest.mark.parametrize("name", ["latency", "latency2", "latency_split"])
 @pytest.mark.parametrize("shuffle", [False, True])
 def test_gpu_multi_chunk_pass(name, shuffle):
     # 2 and 3 rule chunks without span_attribute rules: every chunk in one

@@ -74,6 +74,16 @@ def wide_latency2_config():
     return cfg
 
 
+def wide_latency_split_config():
+    """2 chunks whose latency services differ: 70 global-level rules over
+    services 0..9 (the first chunk takes 64), then 12 endpoint-level rules over
+    services 14..25, which have rules in the second chunk only."""
+    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}]
+            + [_wide_lat(j, j % 10) for j in range(70)],
+            "service_rules": [_wide_svc(k, 10 + k) for k in range(4)],
+            "endpoint_rules": [_wide_lat(400 + j, 14 + j) for j in range(12)]}
+
+
 def wide_mixed_config():
     """Chunk boundaries inside and across levels: 80 latency rules in the
     global level (services 0..39), 100 service_name rules over services
