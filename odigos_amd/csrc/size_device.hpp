@@ -110,7 +110,7 @@ __device__ __forceinline__ uint32_t size_span_finish(const SizeKernelArgs& a, co
   const bool tail = wave_seg_sum(s, x.valid, v, c);
   // a scope keeps a span iff its body sum is non-zero (a kept span adds its
   // framed size, >= 2 bytes): no per-scope kept count (C4 url_copy 0.80 ->
-  // 0.77 ms, profiles/r5a_size_nokept_ab.txt); "had spans" by an atomic OR
+  // 0.77 ms, profiles/r4za_size_nokept_ab.txt); "had spans" by an atomic OR
   if (tail) {
     if (v) atomicAdd((unsigned long long*)&a.scope_body[s], (unsigned long long)v);
     atomicOr(&a.scope_had[s], 1u);

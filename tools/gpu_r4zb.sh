@@ -3,7 +3,7 @@
 # size suites, then sampling_wide / sampling / fused bench lines
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/${TAG:-r5b}
+OUT=$R/gpurun_out/${TAG:-r4zb}
 mkdir -p $OUT
 cd $R
 export OSE_SKIP_BUILD=1

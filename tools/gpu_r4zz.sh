@@ -1,11 +1,11 @@
 #!/bin/bash
-# round-5 closing pass: GPU suite, smoke, the driver's default bench line
+# round-4 closing pass (after the one-pass rule chunks): GPU suite, smoke, the driver's default bench line
 # (cpu baseline included), every other workload's line
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export OSE_SKIP_BUILD=1
-OUT=$R/gpurun_out/r5z; mkdir -p $OUT
+OUT=$R/gpurun_out/r4zz; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
