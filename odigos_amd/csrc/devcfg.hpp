@@ -79,6 +79,14 @@ struct SampLatDev {      // one http_latency rule (latency.go:12-17)
   uint32_t pre[4];       // first 16 prefix bytes, little-endian dwords, zero-padded
   uint32_t msk[4];       // byte mask of the prefix within those 16 bytes
 };
+// trace_multi_kernel's flush: each rule chunk's rules by what matches them
+// (a chunk of at most 128 rules), so a trace's walk visits only its matched
+// rules — an unmatched rule leaves evaluateLevel's state as it is
+struct SampWalkDev {
+  uint64_t err[2];          // the error rules (always matched), by rule index
+  uint64_t svc[64][2];      // the service rules of each service bit
+  uint8_t lat_rule[64];     // the rule of each latency bit
+};
 struct SampCfgDev {
   uint32_t n_rules;
   uint32_t level_first[4];   // rules of level L: [level_first[L], level_first[L+1])

@@ -668,11 +668,30 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
         ng++;
       }
     e->sampling_n_lat_svc = ng;
-    std::vector<uint8_t> st(8 * K + 4 * L + 4 * S + 4 * 64);
+    // then each chunk's SampWalkDev (chunks of <= 128 rules; trace_multi_kernel)
+    std::vector<SampWalkDev> walks(K);
+    e->sampling_walk_ok = true;
+    for (size_t k = 0; k < K; k++) {
+      SampWalkDev& w = walks[k];
+      std::memset(&w, 0, sizeof w);
+      const uint8_t* b = e->sampling_chunks_host[k].data();
+      const SampCfgDev* h = reinterpret_cast<const SampCfgDev*>(b);
+      if (h->n_rules > 128) e->sampling_walk_ok = false;
+      const SampRuleDev* rules = reinterpret_cast<const SampRuleDev*>(b + h->rules_off);
+      for (uint32_t r = 0; r < h->n_rules && r < 128; r++) {
+        const uint64_t bit = 1ull << (r & 63);
+        if (rules[r].type == kSampError) w.err[r >> 6] |= bit;
+        else if (rules[r].type == kSampLatency) w.lat_rule[rules[r].bit & 63] = (uint8_t)r;
+        else w.svc[rules[r].bit & 63][r >> 6] |= bit;
+      }
+    }
+    const size_t wo = align_up(8 * K + 4 * L + 4 * S + 4 * 64, 16);
+    std::vector<uint8_t> st(wo + K * sizeof(SampWalkDev));
     std::memcpy(st.data(), e->sampling_chunks_dev.data(), 8 * K);
     std::memcpy(st.data() + 8 * K, e->sampling_lat_svc.data(), 4 * L);
     if (S) std::memcpy(st.data() + 8 * K + 4 * L, gof.data(), 4 * S);
     std::memcpy(st.data() + 8 * K + 4 * L + 4 * S, gsvc.data(), 4 * 64);
+    std::memcpy(st.data() + wo, walks.data(), K * sizeof(SampWalkDev));
     rc = upload(st, &e->shard_tables_dev);
     if (rc) { delete e; return rc; }
   }

@@ -129,6 +129,7 @@ struct Engine {
   std::unordered_map<std::string, uint32_t> service_ids;
   uint32_t sampling_n_lat = 0, sampling_n_attr = 0;
   uint32_t sampling_n_lat_svc = 0;   // services with http_latency rules (trace_multi_kernel takes <= 64)
+  bool sampling_walk_ok = false;     // every chunk has <= 128 rules (SampWalkDev, trace_multi_kernel)
   // a chunk table past kSampCfgLds (a route longer than the LDS table): the
   // trace stage and the pack then take every chunk's endpoint bits as
   // precomputed planes (spill_endpoint_planes)

@@ -175,6 +175,7 @@ struct FoldState {
   uint32_t flags;    // kFs*
 };
 enum : uint32_t { kFsSat = 1, kFsMatched = 2, kFsFoundFb = 4, kFsHaveMin = 8, kFsDone = 16 };
+struct SampWalkDev;   // devcfg.hpp
 struct TraceKernelArgs {
   uint64_t n_spans;
   uint32_t n_windows;         // ceil(n_spans / 64), >= 1
@@ -232,6 +233,7 @@ struct TraceKernelArgs {
   uint32_t n_multi;
   uint32_t cfg_lds_bytes;     // the tables, then the latency-service ids (lat_gslot)
   const uint32_t* lat_gslot;  // [n_services] index among the latency services, [64] their service ids
+  const SampWalkDev* walks;   // [n_multi] each chunk's rules by what matches them
   // run-list path (repeated trace ids, before the sort-based fallback):
   // trace_runs_kernel lists each trace's runs in its exact-table slot,
   // trace_fold_kernel folds the runs of every trace with 2..kMaxRuns runs

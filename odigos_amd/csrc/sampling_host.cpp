@@ -331,7 +331,8 @@ uint32_t multi_cfg_bytes(const Engine* e) {
     const uint32_t nb = std::min<uint32_t>(reinterpret_cast<const SampCfgDev*>(h.data())->total_bytes, kSampCfgLds);
     t += (nb + 15u) & ~15u;
   }
-  return t + (uint32_t)align_up(4 * e->service_ids.size() + 4 * 64, 16);
+  return t + (uint32_t)align_up(4 * e->service_ids.size() + 4 * 64, 16) +
+         (uint32_t)(e->sampling_chunks_host.size() * sizeof(SampWalkDev));
 }
 // trace_multi_kernel takes the call: 2..kMaxMulti chunks whose tables fit
 // kMultiCfgLds together, no span_attribute rules, no spilled routes, spans
@@ -339,7 +340,7 @@ uint32_t multi_cfg_bytes(const Engine* e) {
 bool multi_pass(const Engine* e, const ose_columns* c, uint32_t group_mode) {
   const size_t K = e->sampling_chunks_host.size();
   return K >= 2 && K <= kMaxMulti && group_mode == OSE_GROUP_TRACE_ID && c->n_spans && !e->sampling_n_attr &&
-         e->sampling_n_lat_svc <= 64 &&
+         e->sampling_n_lat_svc <= 64 && e->sampling_walk_ok &&
          !e->sampling_spill && !c->route_match && !c->svc_match && multi_cfg_bytes(e) <= kMultiCfgLds;
 }
 
@@ -471,6 +472,9 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     a.cfg_lds_bytes = multi_cfg_bytes(e);
     a.lat_gslot = reinterpret_cast<const uint32_t*>(e->shard_tables_dev + 8 * e->sampling_chunks_dev.size() +
                                                     4 * e->sampling_lat_svc.size());
+    a.walks = reinterpret_cast<const SampWalkDev*>(
+        e->shard_tables_dev + align_up(8 * e->sampling_chunks_dev.size() + 4 * e->sampling_lat_svc.size() +
+                                           4 * e->service_ids.size() + 4 * 64, 16));
   }
   a.long_steps = kLongSteps;
   a.win_per_wave = kWinPerWave;

@@ -479,6 +479,59 @@ __device__ void walk_chunk(const Cfg& c, FoldState& s, uint32_t err, uint64_t ep
     }
   }
 }
+// walk_chunk over the matched rules only (trace_multi_kernel: a chunk of at
+// most 128 rules, SampWalkDev): an unmatched rule changes nothing, and a
+// level is closed when a matched rule of a later level comes (or by the
+// next chunk / walk_finish) — the same state as walk_chunk leaves
+__device__ __forceinline__ void walk_sparse(const Cfg& c, const SampWalkDev& W, FoldState& s, uint32_t err, uint64_t ep,
+                                            uint64_t lsat, uint64_t svc) {
+  uint64_t m[2] = {W.err[0], W.err[1]};
+  for (uint64_t b = ep; b; b &= b - 1) {
+    const uint32_t r = W.lat_rule[ffs64(b)];
+    m[r >> 6] |= 1ull << (r & 63);
+  }
+  for (uint64_t b = svc; b; b &= b - 1) {
+    const int x = ffs64(b);
+    m[0] |= W.svc[x][0];
+    m[1] |= W.svc[x][1];
+  }
+  const uint32_t lf1 = c.h->level_first[1], lf2 = c.h->level_first[2];
+  for (int w = 0; w < 2; w++) {
+    for (uint64_t mm = m[w]; mm && !(s.flags & kFsDone); mm &= mm - 1) {
+      const uint32_t k = (uint32_t)(w * 64 + ffs64(mm));
+      const uint32_t L = (k >= lf1 ? 1u : 0u) + (k >= lf2 ? 1u : 0u);
+      while (s.level < L && !(s.flags & kFsDone)) walk_close(s);
+      if (s.flags & kFsDone) break;
+      const SampRuleDev& r = c.rules[k];
+      bool mt, st;
+      double p;
+      if (r.type == kSampError) {
+        mt = true;
+        st = err != 0;
+        p = st ? 100.0 : r.fallback;
+      } else if (r.type == kSampLatency) {
+        mt = (ep >> r.bit) & 1;
+        st = mt && ((lsat >> r.bit) & 1);
+        p = st ? 100.0 : (mt ? r.fallback : 0.0);
+      } else {
+        mt = st = (svc >> r.bit) & 1;
+        p = st ? r.ratio : r.fallback;
+      }
+      if (st) {
+        s.ratio = s.ratio > p ? s.ratio : p;
+        s.flags |= kFsSat | kFsMatched;
+      } else if (mt) {
+        s.flags |= kFsMatched;
+        if (!(s.flags & kFsFoundFb)) {
+          s.ratio = p;
+          s.flags |= kFsFoundFb;
+        } else {
+          s.ratio = s.ratio < p ? s.ratio : p;
+        }
+      }
+    }
+  }
+}
 __device__ __forceinline__ void walk_finish(FoldState& s, double u, uint8_t& keep, uint8_t& level, double& ratio_out) {
   while (s.level < 3 && !(s.flags & kFsDone)) walk_close(s);
   if (s.flags & kFsDone) {
@@ -1108,7 +1161,7 @@ struct MultiQ {
 
 template <int K>
 __device__ __forceinline__ void flush_multi(const TraceKernelArgs& a, const uint8_t* lds, const uint32_t (&coff)[K],
-                                            MultiQ<K>& Q, uint32_t& qn, int lane) {
+                                            const SampWalkDev* walks, MultiQ<K>& Q, uint32_t& qn, int lane) {
   if (!qn) return;
   __builtin_amdgcn_wave_barrier();
   uint8_t dk = 0, dl = 0;
@@ -1120,7 +1173,8 @@ __device__ __forceinline__ void flush_multi(const TraceKernelArgs& a, const uint
     FoldState s{0.0, 0.0, 0u, 0u};
     const uint32_t err = Q.err[lane];
 #pragma unroll
-    for (int k = 0; k < K; k++) walk_chunk(load_cfg(lds + coff[k]), s, err, Q.ep[k][lane], Q.lsat[k][lane], Q.svc[k][lane]);
+    for (int k = 0; k < K; k++)
+      walk_sparse(load_cfg(lds + coff[k]), walks[k], s, err, Q.ep[k][lane], Q.lsat[k][lane], Q.svc[k][lane]);
     walk_finish(s, trace_uniform(Q.hi[lane], Q.lo[lane], a.seed), dk, dl, dr);
     write_rec(a, pos, dk, dl, dr);
   }
@@ -1148,6 +1202,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
   uint32_t coff[K];
   const uint32_t nsvc = reinterpret_cast<const SampCfgDev*>(a.cfgs[0])->n_services;   // (the engine's: every chunk's)
   const uint32_t* gslot_of;   // LDS: latency-service index of each service, then the service of each index
+  const SampWalkDev* wlk;     // LDS: each chunk's rules by what matches them
   {
     // every chunk's table (each <= kSampCfgLds, together <= kMultiCfgLds with
     // the latency-service ids: the host checks) into LDS
@@ -1164,6 +1219,12 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
     uint32_t* gl = reinterpret_cast<uint32_t*>(mcfg + o);
     for (uint32_t x = threadIdx.x; x < nsvc + 64; x += kTThreads) gl[x] = a.lat_gslot[x];
     gslot_of = gl;
+    o += ((nsvc + 64) * 4 + 15u) & ~15u;
+    // each chunk's SampWalkDev (16-byte multiples)
+    const uint4* wg = reinterpret_cast<const uint4*>(a.walks);
+    uint4* wl = reinterpret_cast<uint4*>(mcfg + o);
+    for (uint32_t x = threadIdx.x; x < K * sizeof(SampWalkDev) / 16; x += kTThreads) wl[x] = wg[x];
+    wlk = reinterpret_cast<const SampWalkDev*>(mcfg + o);
     __syncthreads();
   }
   const uint32_t* gsvc = gslot_of + nsvc;
@@ -1355,7 +1416,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
     const bool cont_close = seg0_cont && !(single && cont_next);
     const uint64_t qmask = __ballot(ttail);
     const uint32_t ncl = cont_close ? 1u : 0u, nq = __popcll(qmask);
-    if (qn + ncl + nq > (uint32_t)kQ) flush_multi<K>(a, mcfg, coff, Q, qn, lane);
+    if (qn + ncl + nq > (uint32_t)kQ) flush_multi<K>(a, mcfg, coff, wlk, Q, qn, lane);
     const uint32_t qcl = qn;
     const uint32_t qe = qn + ncl + __popcll(qmask & lanemask_lt(lane));
     if (cont_close && lane == 0) {
@@ -1423,7 +1484,7 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
     base += kWave;
     if (!open && base >= range_end) break;
   }
-  flush_multi<K>(a, mcfg, coff, Q, qn, lane);
+  flush_multi<K>(a, mcfg, coff, wlk, Q, qn, lane);
   flush_heads(a, HQ, hn, lane);
 }
 

@@ -225,6 +225,24 @@ def test_gpu_multi_chunk_pass(name, shuffle):
 
 
 @pytest.mark.gpu
+def test_gpu_multi_chunk_pass_many_rules():
+    # a chunk of more than 128 rules (150 service_name rules sharing 4 service
+    # bits, then 100 latency rules): the pass per chunk decides it
+    cfg = wide_latency2_config()
+    cfg["service_rules"] = [_wide_svc_rule(k) for k in range(150)]
+    assert _chunks(cfg) == 2
+    g = Generator("sampling", seed=0x0D160931, n_spans=200_000)
+    ran = set()
+    gpu_vs_oracle(g, cfg=cfg, kernels=ran)
+    assert "trace_multi_kernel" not in ran and "trace_eval_kernel" in ran, ran
+
+
+def _wide_svc_rule(k):
+    from tests.workloads import _wide_svc
+    return _wide_svc(k, k % 4)
+
+
+@pytest.mark.gpu
 def test_gpu_multi_chunk_pass_edges():
     # batches of one span, one step, a ragged last step and one long trace
     # followed by its owner wave (no long-run hand-off in the one-pass form)
