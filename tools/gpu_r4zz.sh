@@ -5,7 +5,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export OSE_SKIP_BUILD=1
-OUT=$R/gpurun_out/r4zz; mkdir -p $OUT
+OUT=$R/gpurun_out/${TAG:-r4zz}; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
