@@ -580,6 +580,41 @@ def main():
     except Exception as ex:   # diagnostics only
         out["roofline"]["stream_copy_gbs"] = None
         print("stream copy measurement failed:", ex, file=sys.stderr)
+    if world > 1 and not args.no_parity:
+        # every rank's outputs against the oracle: split workloads (C4) on rank 0
+        # over the W sources concatenated in rank order (the global batch the
+        # trace-id exchange decides), per-GPU workloads on each rank's own batch
+        # (tests/dist_parity.py; the checker only, after the timed region)
+        from tests import dist_parity
+        if rank == 0:
+            native_oracle()
+        n = gen.cols.n_spans
+        if not wl["per_gpu"]:
+            A = gen.cols.n_attrsets
+            has_t = bool(stages & native.STAGE_TEMPLATE)
+            has_s = bool(stages & native.STAGE_SIZE)
+            dig = dist_parity.output_digest(
+                n, stages, keep=db.out_numpy("keep", n=n),
+                url_out=db.out_numpy("url_out", n=n) if has_t else None,
+                tmpl=db.out_numpy("tmpl", np.uint32, n=2 * n) if has_t else None,
+                tmpl_arena=db.out_numpy("tmpl_arena", n=db.used()) if has_t else None,
+                attrset_bytes=db.out_numpy("attrset_bytes", np.int64, n=A) if has_s else None,
+                accepted_spans=int(db.out_numpy("accepted_spans", np.int64, n=1)[0]) if has_s else None,
+                node_counters=(node_ctr[:A].cpu().numpy(), int(node_ctr[A].item())) if has_s else None)
+
+            def regen(s):
+                g = Generator(wl["gen"], seed=wl["seed"], n_spans=total, threads=gen_threads, rank=s, world=world)
+                for f in wl.get("null_columns", ()):
+                    setattr(g.cols, f, None)
+                return g
+            par = dist_parity.split_parity(rank, world, dig, regen, cfg, stages, args.steps + args.warmup, share,
+                                           own_source=gen)
+        else:
+            par = dist_parity.local_parity(rank, world, parity_full(wl, gen, db, cfg, stages, share,
+                                                                   args.steps + args.warmup))
+        if rank == 0:
+            out["parity_vs_oracle"] = all(par.values())
+            out["parity"] = par
     if rank == 0 and world == 1 and args.workload != "owner":
         orc = native_oracle()
         if not args.no_cpu_baseline:

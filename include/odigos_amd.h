@@ -218,7 +218,9 @@ typedef struct ose_columns {
   uint32_t n_attr_keys;
   uint32_t match_planes;   /* route_match / svc_match hold this many planes of n_spans words,
                               plane k for rule chunk k (K = (ose_shard_record_bytes - 40) / 16; what
-                              ose_shard_unpack writes); 0 or 1: one plane                 */
+                              ose_shard_unpack writes); 0 or 1: one plane, accepted only by
+                              an engine with one rule chunk (OSE_EINVAL otherwise: the bits
+                              are chunk-local rule indices)                             */
   const uint8_t* attr_type;
   const uint64_t* attr_val;
 } ose_columns;
@@ -425,7 +427,7 @@ int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t*
  * source in source-rank order, as the all-to-all delivers them): keep[i] for
  * record i.  The records are bucketed by trace-id hash and each bucket's
  * traces are grouped, put in batch order and folded in LDS; a bucket past
- * 512 records or a trace with more than 8 latency services sends the batch
+ * 256 records (kOwnerCap) sends the batch
  * through ose_shard_unpack + ose_process_device(SAMPLE) instead (same
  * decisions).  device_status (optional) as ose_outputs.device_status.  The
  * calling thread waits once (the fold's overflow word).  Replaces, with
@@ -464,7 +466,9 @@ int ose_exchange_sample(ose_engine* eng, const ose_columns* cols, const ose_outp
 
 /* Node-wide odigostrafficmetrics counters: node[k] = sum over the ranks of
  * local[k] (int64 ncclAllReduce; the counters of processor.go:76-81 summed
- * over the node's GPUs, as a scrape would sum the gateway replicas).       */
+ * over the node's GPUs, as a scrape would sum the gateway replicas).
+ * local and node may be the same buffer for the RCCL transport (in-place
+ * ncclAllReduce); the in-process test transport refuses that (OSE_EINVAL). */
 int ose_allreduce_counters(const int64_t* local, int64_t* node, uint64_t n, void* nccl_comm,
                            void* hip_stream);
 

@@ -449,8 +449,12 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   a.batch_keep = misc + kBatchKeepWord;
   // match planes (an owner's unpacked records): this chunk's plane
   const uint64_t plane = c->match_planes > 1 ? (uint64_t)chunk * n : 0;
-  if (c->match_planes > 1 && c->match_planes != e->sampling_chunks_dev.size())
-    return fail(OSE_EINVAL, "cols->match_planes must be 1 or the engine's rule chunks");
+  // the bits in route_match / svc_match are chunk-local rule indices: with
+  // more than one chunk every chunk needs its own plane (plane 0 reused for
+  // chunk k > 0 would test chunk k's rules against chunk 0's bits)
+  if ((c->route_match || c->svc_match) && (e->sampling_chunks_dev.size() > 1 || c->match_planes > 1) &&
+      c->match_planes != e->sampling_chunks_dev.size())
+    return fail(OSE_EINVAL, "cols->match_planes must equal the engine's rule chunks when route_match / svc_match are set");
   a.route_match = c->route_match ? c->route_match + plane : nullptr;
   {
     const uint64_t* am = nullptr;
@@ -709,17 +713,20 @@ int spill_endpoint_planes(Engine* e, const ose_columns* c, Workspace* ws, hipStr
 int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t group_mode, const ose_rand* rnd,
                  hipStream_t st, Workspace* ws, std::function<int()>* tail) {
   const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
-  ose_columns cs;
-  if (e->sampling_spill && !c->route_match && e->sampling_n_lat && c->n_spans) {
+  if (K > 1 && c->svc_match && c->match_planes != K)
+    return fail(OSE_EINVAL, "cols->match_planes must equal the engine's rule chunks when svc_match is set");
+  ose_columns cs = *c;
+  // (a batch without route bytes has no endpoint bits to spill: the trace
+  // stage reads a missing route column as "no routes")
+  if (e->sampling_spill && !c->route_match && c->route && e->sampling_n_lat && c->n_spans) {
     const uint64_t* planes = nullptr;
     const int rc = spill_endpoint_planes(e, c, ws, st, &planes);
     if (rc) return rc;
-    cs = *c;
     cs.route_match = planes;
     cs.match_planes = K;
-    c = &cs;
   }
-  if (K <= 1) return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr);
+  c = nullptr;   // below: the (possibly replaced) copy cs, captured by value
+  if (K <= 1) return run_sampling_pass(e, &cs, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr);
   // (one pass over the columns into partial records carrying every chunk's
   // words, decided by the owner fold, measured slower on sampling_wide:
   // 9.72 ms against 7.65, profiles/r4_owner_fold_forms.txt)
@@ -727,6 +734,7 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // call (the host waits for the pass's flags; the run-list and sort launches
   // are queued only for a batch with repeated trace ids)
   auto per_chunk = [=]() -> int {
+  const ose_columns* c = &cs;   // the lambda's own copy of the columns (it may run after run_sampling returns)
   int rc = ws->reserve_fold(std::max<uint64_t>(c->n_spans, 1));
   if (rc) return rc;
   for (uint32_t k = 0; k < K; k++) {
@@ -742,8 +750,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // every chunk in one pass over the columns (trace_multi_kernel; sampling_wide
   // 5.55 -> see DESIGN §4.2); a batch with repeated trace ids falls back to the
   // passes per chunk
-  if (multi_pass(e, c, group_mode))
-    return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr, K, per_chunk);
+  if (multi_pass(e, &cs, group_mode))
+    return run_sampling_pass(e, &cs, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr, K, per_chunk);
   return per_chunk();
 }
 

@@ -186,6 +186,7 @@ struct LocalGroup {
     const uint8_t* send = nullptr;
     const uint64_t* soff = nullptr;
     const uint64_t* slen = nullptr;
+    uint64_t n = 0;   // allreduce_i64: the vector length, by value (a peer may read it after this rank returned)
     hipEvent_t ready = nullptr, done = nullptr;
   };
   const int n_ranks;
@@ -284,16 +285,19 @@ struct LocalTransport final : XTransport {
       return fail(OSE_EDEVICE, "hipEventCreate failed");
     if (!me.done && hipEventCreateWithFlags(&me.done, hipEventDisableTiming) != hipSuccess)
       return fail(OSE_EDEVICE, "hipEventCreate failed");
+    if (n && static_cast<const void*>(local) == static_cast<const void*>(node))
+      return fail(OSE_EINVAL, "in-process all-reduce: local and node must not alias");
     me.send = reinterpret_cast<const uint8_t*>(local);
     me.soff = nullptr;
-    me.slen = &n;
+    me.slen = nullptr;
+    me.n = n;
     if (hipEventRecord(me.ready, st) != hipSuccess) return fail(OSE_EDEVICE, "hipEventRecord failed");
     if (int rc = g->barrier()) return rc;
     int err = 0;
     if (n && hipMemsetAsync(node, 0, n * sizeof(int64_t), st) != hipSuccess) err = fail(OSE_EDEVICE, "hipMemsetAsync failed");
     for (int p = 0; p < g->n_ranks && !err; p++) {
       const LocalGroup::Slot& src = g->slots[(size_t)p];
-      if (*src.slen != n) {
+      if (src.n != n) {
         err = fail(OSE_EINVAL, "in-process all-reduce: vector lengths disagree");
         break;
       }
@@ -579,7 +583,12 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.arena = c->arena;
   a.route_match = c->route_match;
   a.rm_stride = c->match_planes > 1 ? n : 0;
-  if (e->sampling_spill && !c->route_match && e->sampling_n_lat) {   // route bytes past an LDS table: planes first
+  if (c->route_match && e->sampling_chunks_dev.size() > 1 && c->match_planes != e->sampling_chunks_dev.size()) {
+    // chunk-local rule bits: one plane per chunk, never plane 0 for every chunk
+    e->release_ws(ws, st);
+    return fail(OSE_EINVAL, "cols->match_planes must equal the engine's rule chunks when route_match is set");
+  }
+  if (e->sampling_spill && !c->route_match && c->route && e->sampling_n_lat) {   // route bytes past an LDS table: planes first
     const uint64_t* planes = nullptr;
     rc = spill_endpoint_planes(e, c, ws, st, &planes);
     if (rc) {

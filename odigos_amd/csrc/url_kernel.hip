@@ -471,9 +471,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
 typedef const __attribute__((address_space(3))) u32x4 lds_cu4;
 
-// One 32-byte row: the class words from two nibble-lookup codes per byte and
-// a bit-matrix transpose (url_classes.hpp; tests/lut_check.cpp checks them on
-// the host).  C_* above is uc::BNL.. in the same order.
+// One 32-byte row: the class words as boolean functions of the row's 8 bit
+// planes (url_classes.hpp; tests/lut_check.cpp checks them on the host).
+// C_* above is uc::BNL.. in the same order.
 static_assert(C_BNL == uc::BNL && C_DG == uc::DG && C_HI == uc::HI && C_QM == uc::QM && C_NAL == uc::NAL &&
                   kClasses == uc::kN,
               "class order");
@@ -490,25 +490,22 @@ __device__ __forceinline__ void build_row(lds_u32* stage32, lds_u4* bm, uint32_t
 // A quarter of row r (bytes 8q..8q+7, one 8 x 8 block) per lane, the four
 // lanes of a quad together building the row: each lane's transposed block
 // is broadcast over the quad (DPP quad_perm) and every lane assembles the
-// plane words with the 4 x 4 byte transposes; the quad's first lane writes
-// the row.  For the last few rows of a group (a full round would leave most
-// lanes idle).
+// plane words with the 4 x 4 byte transposes; the quad's first lane derives
+// and writes the row.  For the last few rows of a group (a full round would
+// leave most lanes idle).
 __device__ __forceinline__ void build_quarter_row(lds_u32* stage32, lds_u4* bm, uint32_t r, uint32_t q, bool valid) {
-  uint32_t P0 = 0, P1 = 0, Q0 = 0, Q1 = 0;
+  uint32_t B0 = 0, B1 = 0;
   if (valid) {
-    uc::codes(stage32[8 * r + 2 * q], P0, Q0);
-    uc::codes(stage32[8 * r + 2 * q + 1], P1, Q1);
-    uc::xpose8(P0, P1);
-    uc::xpose8(Q0, Q1);
+    B0 = stage32[8 * r + 2 * q];
+    B1 = stage32[8 * r + 2 * q + 1];
+    uc::xpose8(B0, B1);
   }
-  uint32_t p[8], q8[8];
-  uc::xpose4(dpp_mov<0x00>(0u, P0), dpp_mov<0x55>(0u, P0), dpp_mov<0xAA>(0u, P0), dpp_mov<0xFF>(0u, P0), p);
-  uc::xpose4(dpp_mov<0x00>(0u, P1), dpp_mov<0x55>(0u, P1), dpp_mov<0xAA>(0u, P1), dpp_mov<0xFF>(0u, P1), p + 4);
-  uc::xpose4(dpp_mov<0x00>(0u, Q0), dpp_mov<0x55>(0u, Q0), dpp_mov<0xAA>(0u, Q0), dpp_mov<0xFF>(0u, Q0), q8);
-  uc::xpose4(dpp_mov<0x00>(0u, Q1), dpp_mov<0x55>(0u, Q1), dpp_mov<0xAA>(0u, Q1), dpp_mov<0xFF>(0u, Q1), q8 + 4);
+  uint32_t p[8];
+  uc::xpose4(dpp_mov<0x00>(0u, B0), dpp_mov<0x55>(0u, B0), dpp_mov<0xAA>(0u, B0), dpp_mov<0xFF>(0u, B0), p);
+  uc::xpose4(dpp_mov<0x00>(0u, B1), dpp_mov<0x55>(0u, B1), dpp_mov<0xAA>(0u, B1), dpp_mov<0xFF>(0u, B1), p + 4);
   if (valid && q == 0) {
     uint32_t w[kClasses];
-    uc::derive(p, q8, w);
+    uc::derive_planes(p, w);
     bm[kRowVec * r] = u32x4{w[0], w[1], w[2], w[3]};
     bm[kRowVec * r + 1] = u32x4{w[4], w[5], w[6], w[7]};
     bm[kRowVec * r + 2] = u32x4{w[8], w[9], w[10], w[11]};

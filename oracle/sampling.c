@@ -119,7 +119,7 @@ static eval_t eval_latency(const orc_rule* r, int lat_index, const trace_view* t
     if (c->route_match) {   /* precomputed HasPrefix bits (ose_columns.route_match) */
       if ((c->route_match[i] >> lat_index) & 1) endpoint_found = 1;
     } else {
-      ose_strref rt = c->route[i];   /* AsString(http.route); absent == "" here */
+      ose_strref rt = c->route ? c->route[i] : (ose_strref){0, 0};   /* AsString(http.route); absent == "" here (no column: every span absent) */
       if (rt.len >= r->route_len && memcmp(c->arena + rt.off, r->route, r->route_len) == 0)
         endpoint_found = 1;   /* strings.HasPrefix (latency.go:97-100) */
     }

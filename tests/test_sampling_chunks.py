@@ -347,3 +347,52 @@ def test_gpu_wide_config_exchange_world3(name):
     for gk, wk in zip(got, want):
         np.testing.assert_array_equal(gk, wk)
     assert sum(s[0] for s in stats) == sum(s[1] for s in stats) > 0
+
+
+@pytest.mark.gpu
+def test_gpu_match_planes_checked_against_chunks():
+    # route_match / svc_match bits are chunk-local rule indices: an engine with
+    # K > 1 chunks refuses caller planes unless match_planes == K (plane 0 read
+    # for every chunk would decide chunks 1..K-1 on chunk 0's bits); with a
+    # spilled route the engine builds K route planes itself, so a caller's
+    # one-plane svc_match is refused rather than read past its end
+    import torch
+    from odigos_amd.batch import DeviceBatch, Engine
+    for cfg in (_long_route_config(), wide_latency_config()):
+        eng = Engine({"odigossampling": cfg})
+        assert _chunks(cfg) > 1
+        g = Generator("sampling", seed=0x0D160851, n_spans=5000)
+        db = DeviceBatch(g.cols)
+        n = g.cols.n_spans
+        plane = torch.zeros(8 * n, dtype=torch.uint8, device="cuda")
+        for field in ("svc_match", "route_match"):
+            for planes in (0, 1):
+                setattr(db.cols, field, plane.data_ptr())
+                db.cols.match_planes = planes
+                with pytest.raises(native.OseError) as ei:
+                    eng.process_device(db, native.STAGE_SAMPLE, native.GROUP_TRACE_ID)
+                assert ei.value.code == native.OSE_EINVAL
+                setattr(db.cols, field, 0)
+        db.cols.match_planes = 0
+        eng.process_device(db, native.STAGE_SAMPLE, native.GROUP_TRACE_ID)
+        torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_spilled_route_config_without_route_column():
+    # a batch without an http.route column (and no route_match) is refused the
+    # same way whether or not the config spills a route past the LDS table:
+    # http_latency rules need the route bytes (no spill-specific failure)
+    from odigos_amd.batch import DeviceBatch, Engine
+    from tests.workloads import c3_sampling_config
+    msgs = []
+    for cfg in (c3_sampling_config(), _long_route_config()):
+        g = Generator("sampling", seed=0x0D160861, n_spans=20_000)
+        g.cols.route = None
+        eng = Engine({"odigossampling": cfg})
+        db = DeviceBatch(g.cols)
+        with pytest.raises(native.OseError) as ei:
+            eng.process_device(db, native.STAGE_SAMPLE, native.GROUP_TRACE_ID)
+        assert ei.value.code == native.OSE_EINVAL
+        msgs.append(str(ei.value))
+    assert msgs[0] == msgs[1]
