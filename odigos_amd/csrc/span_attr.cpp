@@ -404,6 +404,313 @@ void marshal(const JVal& v, std::string& o) {
   }
 }
 
+}  // namespace
+
+// ---------------- gval expressions of jsonpath filters / scripts ----------------
+// PaesslerAG/jsonpath v0.1.1 evaluates `[?(expr)]` and `[(expr)]` with gval's
+// full language; the engine restates the part a sampling rule can use
+// (parity unpinned: neither library is in the reference):
+//   literals      numbers (strconv float64), 'str' / "str", true, false, null
+//   paths         @ (the current value) and $ (the document) followed by
+//                 jsonpath selectors; a plain path that fails is an error,
+//                 an ambiguous one yields its match list
+//   operators     ! and unary -, * / %, + - (+ also joins two strings),
+//                 < <= > >= (two numbers or two strings), == != (same type
+//                 and value; containers by their JSON encoding), =~ (a
+//                 string against a regexp: regexp.MatchString), && ||
+//                 (short-circuit), parentheses
+// An error anywhere (a missing key, an operator on the wrong types) makes a
+// filter skip the element and a script select nothing.  A filter keeps the
+// elements (array order) or member values (sorted keys) whose result is
+// truthy: true, a non-zero number, a non-empty string, a container; a
+// script's result selects an array index (an integral number) or an object
+// key (a string).
+struct JsonExpr {
+  enum Op { Lit, Path, Not, Neg, Mul, Div, Mod, Add, Sub, Lt, Le, Gt, Ge, Eq, Ne, Match, And, Or } op = Lit;
+  JVal lit;
+  bool root = false;                    // Path: from $ (else @)
+  std::vector<JsonPathStep> steps;      // Path
+  std::shared_ptr<const JsonExpr> l, r;
+  std::shared_ptr<Dfa> re;              // Match with a literal pattern
+  bool re_ok = false;
+};
+
+namespace {
+
+struct EV {
+  bool ok = false;
+  JVal v;
+};
+
+bool truthy(const EV& e) {
+  if (!e.ok) return false;
+  switch (e.v.t) {
+    case JVal::Null: return false;
+    case JVal::Bool: return e.v.b;
+    case JVal::Num: return e.v.n != 0;
+    case JVal::Str: return !e.v.s.empty();
+    default: return true;
+  }
+}
+
+void marshal(const JVal& v, std::string& o);
+void select_step(const JsonPathStep& st, const JVal& v, std::vector<const JVal*>& out, const JVal& root);
+bool plain_select(const JsonPathStep& st, const JVal& cur, const JVal*& out);
+bool path_is_plain(const std::vector<JsonPathStep>& path);
+
+EV eval_expr(const JsonExpr& x, const JVal& cur, const JVal& root) {
+  EV r;
+  auto num = [&](double d) { r.ok = true; r.v.t = JVal::Num; r.v.n = d; return r; };
+  auto boolean = [&](bool b) { r.ok = true; r.v.t = JVal::Bool; r.v.b = b; return r; };
+  switch (x.op) {
+    case JsonExpr::Lit: r.ok = true; r.v = x.lit; return r;
+    case JsonExpr::Path: {
+      const JVal& base = x.root ? root : cur;
+      if (path_is_plain(x.steps)) {
+        const JVal* c = &base;
+        for (const JsonPathStep& st : x.steps)
+          if (!plain_select(st, *c, c)) return r;
+        r.ok = true;
+        r.v = *c;
+        return r;
+      }
+      std::vector<const JVal*> a{&base}, b;
+      for (const JsonPathStep& st : x.steps) {
+        b.clear();
+        for (const JVal* v : a) select_step(st, *v, b, root);
+        a.swap(b);
+      }
+      r.ok = true;
+      r.v.t = JVal::Arr;
+      for (const JVal* v : a) r.v.a.push_back(*v);
+      return r;
+    }
+    case JsonExpr::Not: return boolean(!truthy(eval_expr(*x.l, cur, root)));
+    case JsonExpr::Neg: {
+      EV a = eval_expr(*x.l, cur, root);
+      if (!a.ok || a.v.t != JVal::Num) return r;
+      return num(-a.v.n);
+    }
+    case JsonExpr::And: {
+      if (!truthy(eval_expr(*x.l, cur, root))) return boolean(false);
+      return boolean(truthy(eval_expr(*x.r, cur, root)));
+    }
+    case JsonExpr::Or: {
+      if (truthy(eval_expr(*x.l, cur, root))) return boolean(true);
+      return boolean(truthy(eval_expr(*x.r, cur, root)));
+    }
+    default: break;
+  }
+  EV a = eval_expr(*x.l, cur, root), b = eval_expr(*x.r, cur, root);
+  if (!a.ok || !b.ok) return r;
+  const bool nn = a.v.t == JVal::Num && b.v.t == JVal::Num, ss = a.v.t == JVal::Str && b.v.t == JVal::Str;
+  switch (x.op) {
+    case JsonExpr::Mul: return nn ? num(a.v.n * b.v.n) : r;
+    case JsonExpr::Div: return nn ? num(a.v.n / b.v.n) : r;
+    case JsonExpr::Mod: return nn ? num(std::fmod(a.v.n, b.v.n)) : r;
+    case JsonExpr::Sub: return nn ? num(a.v.n - b.v.n) : r;
+    case JsonExpr::Add:
+      if (nn) return num(a.v.n + b.v.n);
+      if (ss) {
+        r.ok = true;
+        r.v.t = JVal::Str;
+        r.v.s = a.v.s + b.v.s;
+      }
+      return r;
+    case JsonExpr::Lt: return nn ? boolean(a.v.n < b.v.n) : ss ? boolean(a.v.s < b.v.s) : r;
+    case JsonExpr::Le: return nn ? boolean(a.v.n <= b.v.n) : ss ? boolean(a.v.s <= b.v.s) : r;
+    case JsonExpr::Gt: return nn ? boolean(a.v.n > b.v.n) : ss ? boolean(a.v.s > b.v.s) : r;
+    case JsonExpr::Ge: return nn ? boolean(a.v.n >= b.v.n) : ss ? boolean(a.v.s >= b.v.s) : r;
+    case JsonExpr::Eq:
+    case JsonExpr::Ne: {
+      bool eq;
+      if (a.v.t != b.v.t) eq = false;
+      else if (nn) eq = a.v.n == b.v.n;
+      else if (ss) eq = a.v.s == b.v.s;
+      else if (a.v.t == JVal::Bool) eq = a.v.b == b.v.b;
+      else if (a.v.t == JVal::Null) eq = true;
+      else {
+        std::string ma, mb;
+        marshal(a.v, ma);
+        marshal(b.v, mb);
+        eq = ma == mb;
+      }
+      return boolean(x.op == JsonExpr::Eq ? eq : !eq);
+    }
+    case JsonExpr::Match: {
+      if (!ss) return r;
+      if (x.re) {
+        if (!x.re_ok) return r;
+        return boolean(dfa_match(*x.re, reinterpret_cast<const uint8_t*>(a.v.s.data()), a.v.s.size()));
+      }
+      Dfa d;
+      std::string err;
+      if (compile_dfa(b.v.s, d, err) != RegexStatus::Ok) return r;
+      return boolean(dfa_match(d, reinterpret_cast<const uint8_t*>(a.v.s.data()), a.v.s.size()));
+    }
+    default: return r;
+  }
+}
+
+bool parse_path_steps(const std::string& p, size_t& i, std::vector<JsonPathStep>& out, bool in_expr);
+
+// recursive descent over gval's precedence: || < && < comparisons < + - < * / % < unary
+struct ExprParser {
+  const std::string& p;
+  size_t i;
+  std::string err;
+  ExprParser(const std::string& s, size_t at) : p(s), i(at) {}
+  void ws() {
+    while (i < p.size() && (p[i] == ' ' || p[i] == '\t')) i++;
+  }
+  bool eat(const char* t) {
+    ws();
+    const size_t n = std::strlen(t);
+    if (p.compare(i, n, t) != 0) return false;
+    i += n;
+    return true;
+  }
+  using P = std::shared_ptr<JsonExpr>;
+  static P bin(JsonExpr::Op op, P l, P r) {
+    auto x = std::make_shared<JsonExpr>();
+    x->op = op;
+    x->l = l;
+    x->r = r;
+    return x;
+  }
+  P orx() {
+    P l = andx();
+    while (l && eat("||")) {
+      P r = andx();
+      if (!r) return nullptr;
+      l = bin(JsonExpr::Or, l, r);
+    }
+    return l;
+  }
+  P andx() {
+    P l = cmp();
+    while (l && eat("&&")) {
+      P r = cmp();
+      if (!r) return nullptr;
+      l = bin(JsonExpr::And, l, r);
+    }
+    return l;
+  }
+  P cmp() {
+    P l = add();
+    if (!l) return nullptr;
+    static const struct { const char* t; JsonExpr::Op op; } ops[] = {
+        {"==", JsonExpr::Eq}, {"!=", JsonExpr::Ne}, {"=~", JsonExpr::Match}, {"<=", JsonExpr::Le},
+        {">=", JsonExpr::Ge}, {"<", JsonExpr::Lt}, {">", JsonExpr::Gt}};
+    for (const auto& o : ops) {
+      if (eat(o.t)) {
+        P r = add();
+        if (!r) return nullptr;
+        P x = bin(o.op, l, r);
+        if (o.op == JsonExpr::Match && r->op == JsonExpr::Lit && r->lit.t == JVal::Str) {
+          x->re = std::make_shared<Dfa>();
+          std::string e;
+          const RegexStatus st = compile_dfa(r->lit.s, *x->re, e);
+          if (st == RegexStatus::Ok) x->re_ok = true;
+          else if (st != RegexStatus::Syntax) {   // a pattern the DFA compiler cannot take: refuse
+            err = "regexp in a jsonpath filter: " + e;
+            return nullptr;
+          }
+        }
+        return x;
+      }
+    }
+    return l;
+  }
+  P add() {
+    P l = mul();
+    for (;;) {
+      if (!l) return nullptr;
+      ws();
+      if (i < p.size() && (p[i] == '+' || p[i] == '-')) {
+        const JsonExpr::Op op = p[i] == '+' ? JsonExpr::Add : JsonExpr::Sub;
+        i++;
+        P r = mul();
+        if (!r) return nullptr;
+        l = bin(op, l, r);
+      } else {
+        return l;
+      }
+    }
+  }
+  P mul() {
+    P l = unary();
+    for (;;) {
+      if (!l) return nullptr;
+      ws();
+      if (i < p.size() && (p[i] == '*' || p[i] == '/' || p[i] == '%')) {
+        const JsonExpr::Op op = p[i] == '*' ? JsonExpr::Mul : p[i] == '/' ? JsonExpr::Div : JsonExpr::Mod;
+        i++;
+        P r = unary();
+        if (!r) return nullptr;
+        l = bin(op, l, r);
+      } else {
+        return l;
+      }
+    }
+  }
+  P unary() {
+    ws();
+    if (i < p.size() && p[i] == '!' && !(i + 1 < p.size() && p[i + 1] == '=')) {
+      i++;
+      P a = unary();
+      return a ? bin(JsonExpr::Not, a, nullptr) : nullptr;
+    }
+    if (i < p.size() && p[i] == '-') {
+      i++;
+      P a = unary();
+      return a ? bin(JsonExpr::Neg, a, nullptr) : nullptr;
+    }
+    return primary();
+  }
+  P primary() {
+    ws();
+    if (i >= p.size()) return nullptr;
+    auto x = std::make_shared<JsonExpr>();
+    const char c = p[i];
+    if (c == '(') {
+      i++;
+      P e = orx();
+      if (!e || !eat(")")) return nullptr;
+      return e;
+    }
+    if (c == '@' || c == '$') {
+      i++;
+      x->op = JsonExpr::Path;
+      x->root = c == '$';
+      if (!parse_path_steps(p, i, x->steps, true)) return nullptr;
+      return x;
+    }
+    if (c == '\'' || c == '"') {
+      const size_t b = ++i;
+      while (i < p.size() && p[i] != c) i++;
+      if (i >= p.size()) return nullptr;
+      x->lit.t = JVal::Str;
+      x->lit.s = p.substr(b, i - b);
+      i++;
+      return x;
+    }
+    if (p.compare(i, 4, "true") == 0) { i += 4; x->lit.t = JVal::Bool; x->lit.b = true; return x; }
+    if (p.compare(i, 5, "false") == 0) { i += 5; x->lit.t = JVal::Bool; x->lit.b = false; return x; }
+    if (p.compare(i, 4, "null") == 0) { i += 4; x->lit.t = JVal::Null; return x; }
+    if (std::isdigit((unsigned char)c) || c == '.') {
+      const size_t b = i;
+      while (i < p.size() && (std::isalnum((unsigned char)p[i]) || p[i] == '.' || p[i] == '_' ||
+                              ((p[i] == '+' || p[i] == '-') && (p[i - 1] == 'e' || p[i - 1] == 'E'))))
+        i++;
+      x->lit.t = JVal::Num;
+      if (!go_parse_float(p.substr(b, i - b), x->lit.n)) return nullptr;
+      return x;
+    }
+    return nullptr;
+  }
+};
+
 // jsonpath.Get on a plain path (Key / Index selectors only); false = an
 // error (unknown key, index out of range, step on a non-container).
 bool plain_select(const JsonPathStep& st, const JVal& cur, const JVal*& out) {
@@ -434,8 +741,30 @@ void visit_children(const JVal& v, F&& f) {
 
 // One selector over one value: the matches it yields (an ambiguous path
 // drops the branches a plain selector fails on instead of failing)
-void select_step(const JsonPathStep& st, const JVal& v, std::vector<const JVal*>& out) {
+void select_step(const JsonPathStep& st, const JVal& v, std::vector<const JVal*>& out, const JVal& root) {
   switch (st.kind) {
+    case JsonPathStep::Filter:
+      visit_children(v, [&](const JVal& c) {
+        if (truthy(eval_expr(*st.expr, c, root))) out.push_back(&c);
+      });
+      break;
+    case JsonPathStep::Script: {
+      const EV e = eval_expr(*st.expr, v, root);
+      if (!e.ok) break;
+      JsonPathStep sel;
+      if (e.v.t == JVal::Num && std::floor(e.v.n) == e.v.n && std::fabs(e.v.n) < 9.0e15) {
+        sel.kind = JsonPathStep::Index;
+        sel.index = (long long)e.v.n;
+      } else if (e.v.t == JVal::Str) {
+        sel.kind = JsonPathStep::Key;
+        sel.key = e.v.s;
+      } else {
+        break;
+      }
+      const JVal* r = nullptr;
+      if (plain_select(sel, v, r)) out.push_back(r);
+      break;
+    }
     case JsonPathStep::Key:
     case JsonPathStep::Index: {
       const JVal* r = nullptr;
@@ -446,7 +775,7 @@ void select_step(const JsonPathStep& st, const JVal& v, std::vector<const JVal*>
       visit_children(v, [&](const JVal& c) { out.push_back(&c); });
       break;
     case JsonPathStep::Union:
-      for (const JsonPathStep& it : st.items) select_step(it, v, out);
+      for (const JsonPathStep& it : st.items) select_step(it, v, out, root);
       break;
     case JsonPathStep::Slice: {
       if (v.t != JVal::Arr) break;
@@ -468,7 +797,7 @@ void select_step(const JsonPathStep& st, const JVal& v, std::vector<const JVal*>
       while (!stack.empty()) {
         const JVal* cur = stack.back();
         stack.pop_back();
-        select_step(st.items[0], *cur, out);
+        select_step(st.items[0], *cur, out, root);
         std::vector<const JVal*> kids;
         visit_children(*cur, [&](const JVal& c) { kids.push_back(&c); });
         for (auto it = kids.rbegin(); it != kids.rend(); ++it) stack.push_back(*it);
@@ -498,7 +827,7 @@ bool jsonpath_get(const std::vector<JsonPathStep>& path, const JVal& root, const
   std::vector<const JVal*> cur{&root}, next;
   for (const JsonPathStep& st : path) {
     next.clear();
-    for (const JVal* v : cur) select_step(st, *v, next);
+    for (const JVal* v : cur) select_step(st, *v, next, root);
     cur.swap(next);
   }
   holder = JVal{};
@@ -550,7 +879,23 @@ bool parse_int_opt(const std::string& p, size_t& i, bool& has, long long& v) {
 // `[...]` after the '[': *, 'k', n, unions of those, a:b:c slices
 bool parse_bracket(const std::string& p, size_t& i, JsonPathStep& out) {
   while (i < p.size() && p[i] == ' ') i++;
-  if (i < p.size() && (p[i] == '?' || p[i] == '(')) return false;   // filter / script: not restated
+  if (i < p.size() && (p[i] == '?' || p[i] == '(')) {   // filter [?(expr)] / script [(expr)]
+    const bool filter = p[i] == '?';
+    if (filter) i++;
+    if (i >= p.size() || p[i] != '(') return false;
+    i++;
+    ExprParser ep(p, i);
+    auto e = ep.orx();
+    if (!e || !ep.eat(")")) return false;
+    i = ep.i;
+    while (i < p.size() && p[i] == ' ') i++;
+    out = JsonPathStep{};
+    out.kind = filter ? JsonPathStep::Filter : JsonPathStep::Script;
+    out.expr = e;
+    if (i >= p.size() || p[i] != ']') return false;
+    i++;
+    return true;
+  }
   if (i < p.size() && p[i] == '*') {
     i++;
     while (i < p.size() && p[i] == ' ') i++;
@@ -596,18 +941,20 @@ bool parse_bracket(const std::string& p, size_t& i, JsonPathStep& out) {
   return true;
 }
 
-bool parse_jsonpath(const std::string& p, std::vector<JsonPathStep>& out) {
-  if (p.empty() || p[0] != '$') return false;
-  size_t i = 1;
+// The selectors after `$` / `@`.  A whole path (in_expr false) must be
+// consumed to its end; inside an expression the steps end at the first byte
+// that starts no selector, and a name takes no '-' (the minus operator).
+bool parse_path_steps(const std::string& p, size_t& i, std::vector<JsonPathStep>& out, bool in_expr) {
   auto name = [&](JsonPathStep& st) {
     const size_t b = i;
-    while (i < p.size() && (std::isalnum((unsigned char)p[i]) || p[i] == '_' || p[i] == '-')) i++;
+    while (i < p.size() && (std::isalnum((unsigned char)p[i]) || p[i] == '_' || (!in_expr && p[i] == '-'))) i++;
     if (i == b) return false;
     st.kind = JsonPathStep::Key;
     st.key = p.substr(b, i - b);
     return true;
   };
   while (i < p.size()) {
+    if (in_expr && p[i] != '.' && p[i] != '[') return true;
     JsonPathStep st;
     if (p[i] == '.' && i + 1 < p.size() && p[i + 1] == '.') {
       i += 2;
@@ -642,6 +989,12 @@ bool parse_jsonpath(const std::string& p, std::vector<JsonPathStep>& out) {
   return true;
 }
 
+bool parse_jsonpath(const std::string& p, std::vector<JsonPathStep>& out) {
+  if (p.empty() || p[0] != '$') return false;
+  size_t i = 1;
+  return parse_path_steps(p, i, out, false) && i == p.size();
+}
+
 }  // namespace
 
 std::string SpanAttrPredicate::compile(const SpanAttributeRule& r) {
@@ -663,8 +1016,8 @@ std::string SpanAttrPredicate::compile(const SpanAttributeRule& r) {
                           op_ == "key_not_equals")) {
     if (!parse_jsonpath(r.json_path, path_))
       return "span_attribute json_path \"" + r.json_path +
-             "\" is not supported by the engine ($, .key, ['key'], [index], *, [a,b], [a:b:c] and .. are; "
-             "filters and scripts are not)";
+             "\" is not a jsonpath the engine parses ($, .key, ['key'], [index], *, [a,b], [a:b:c], .., "
+             "[?(expr)] and [(expr)])";
   }
   return "";
 }

@@ -15,7 +15,10 @@
 //                  (pinned by the KATs); the ambiguous selectors *, [*],
 //                  [a,b], [a:b:c], ..  return the match list (parity
 //                  unpinned: the library is not in the reference); filters
-//                  [?(..)] and scripts [(..)] are OSE_ENOTSUP at creation
+//                  [?(..)] and scripts [(..)] evaluate a gval expression
+//                  subset (literals, @ / $ paths, ! - * / % + - < <= > >=
+//                  == != =~ && ||, parentheses), restated from gval's
+//                  published grammar (parity unpinned, see span_attr.cpp)
 #pragma once
 #include <memory>
 #include <string>
@@ -27,11 +30,14 @@
 
 namespace ose {
 
+struct JsonExpr;   // a filter / script expression (span_attr.cpp)
+
 // One selector of a PaesslerAG/jsonpath path: plain (Key, Index) or
 // ambiguous (Wild `*` / `[*]`, Union `[a,b]`, Slice `[a:b:c]`, Descend `..`
-// followed by its selector)
+// followed by its selector, Filter `[?(expr)]`, Script `[(expr)]`)
 struct JsonPathStep {
-  enum Kind { Key, Index, Wild, Union, Slice, Descend } kind = Key;
+  enum Kind { Key, Index, Wild, Union, Slice, Descend, Filter, Script } kind = Key;
+  std::shared_ptr<const JsonExpr> expr;   // Filter / Script
   std::string key;
   long long index = 0;
   std::vector<JsonPathStep> items;   // Union: Key / Index items; Descend: the selector after `..`

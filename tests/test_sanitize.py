@@ -223,7 +223,8 @@ def _rand_regex(rng):
 
 def _rand_path(rng):
     toks = ["$", ".", "..", "[", "]", "*", "'k'", '"k"', "a", "b", "0", "1", "-1", ":", ",", "?(", "@", ")", "(", "2:",
-            "::", "[*]", "['a','b']", "[0:2:1]", "[::-1]"]
+            "::", "[*]", "['a','b']", "[0:2:1]", "[::-1]", "==", "&&", "||", "<", "!", "=~", "'x'", "+",
+            "[?(@.a==1)]", "[?(@ =~ 'k.*')]", "[(1+1)]", "[?($.k)]"]
     return "".join(rng.choice(toks) for _ in range(rng.randrange(1, 9)))
 
 

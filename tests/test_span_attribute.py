@@ -213,6 +213,26 @@ PRED_CASES = [
     (_r("json", "key_equals", "[1,3]", "$..a"), S('{"a":1,"b":{"a":3}}'), True),
     (_r("json", "key_equals", "[]", "$..q"), S('{"a":1}'), True),
     (_r("json", "key_equals", "[1,3]", "$..a"), S('[{"a":1},{"a":3}]'), True),
+    # filters [?(expr)] and scripts [(expr)]: a gval expression subset
+    # (parity unpinned: gval and PaesslerAG/jsonpath are not in the reference)
+    (_r("json", "key_equals", '[{"b":1}]', "$.a[?(@.b==1)]"), S('{"a":[{"b":1},{"b":2},{"c":1}]}'), True),
+    (_r("json", "key_equals", "[2,3]", "$.a[?(@ > 1)]"), S('{"a":[1,2,3]}'), True),
+    (_r("json", "key_equals", '["x"]', "$.a[?(@.n >= 2 && @.n < 3)].s"),
+     S('{"a":[{"n":1,"s":"w"},{"n":2,"s":"x"},{"n":3,"s":"y"}]}'), True),
+    (_r("json", "key_equals", '["w","y"]', "$.a[?(@.n == 1 || @.n > 2)].s"),
+     S('{"a":[{"n":1,"s":"w"},{"n":2,"s":"x"},{"n":3,"s":"y"}]}'), True),
+    (_r("json", "key_equals", '[{"k":"v"}]', "$.a[?(@.k)]"), S('{"a":[{"k":"v"},{"j":1},{"k":""}]}'), True),
+    (_r("json", "key_equals", '[{"j":1}]', "$.a[?(!@.k)]"), S('{"a":[{"k":"v"},{"j":1}]}'), True),
+    (_r("json", "key_equals", '["prod-1"]', "$.e[?(@ =~ '^prod-')]"), S('{"e":["dev","prod-1"]}'), True),
+    (_r("json", "key_equals", "[3]", "$.a[?(@ * 2 - 1 == 5)]"), S('{"a":[1,2,3]}'), True),
+    (_r("json", "key_equals", '["ab"]', "$.a[?(@ + 'b' == 'abb')]"), S('{"a":["ab","b"]}'), True),
+    (_r("json", "key_equals", "[1]", "$.a[?(@.x == $.want)].y"), S('{"want":"q","a":[{"x":"q","y":1},{"x":"r","y":2}]}'), True),
+    (_r("json", "key_equals", "[2]", "$.o[?(@ > 1)]"), S('{"o":{"p":1,"q":2}}'), True),     # member values, sorted keys
+    (_r("json", "key_equals", "[]", "$.a[?(@.b == 'x')]"), S('{"a":[{"b":1}]}'), True),     # mixed types: not equal
+    (_r("json", "contains_key", path="$.a[?(@.b==9)]"), S('{"a":[{"b":1}]}'), True),       # an empty list is not nil
+    (_r("json", "key_equals", "[7]", "$.a[(1+1)]"), S('{"a":[5,6,7]}'), True),              # script: an index
+    (_r("json", "key_equals", "[5]", "$[(@.k)]"), S('{"k":"z","z":5}'), True),               # script: a key
+    (_r("json", "key_equals", "[]", "$.a[(9)]"), S('{"a":[5]}'), True),
 ]
 
 
@@ -223,9 +243,8 @@ def test_predicate(rule, value, want):
 
 
 def test_unsupported_jsonpath_rejected_at_creation():
-    # filters and scripts (gval expressions) are outside the restated
-    # jsonpath subset: the engine refuses the config instead of guessing
-    for path in ("$.a[?(@.b==1)]", "$[(@.length-1)]", "$.a[", "a.b"):
+    # paths the engine cannot parse are refused at creation instead of guessed
+    for path in ("$.a[?(@.b==)]", "$[(@.length-1]", "$.a[?(@.b ~ 1)]", "$.a[", "a.b"):
         cfg = {"global_rules": [{"name": "j", "type": "span_attribute",
                                  "rule_details": dict(_r("json", "contains_key", path=path), sampling_ratio=1.0)}]}
         with pytest.raises((ValueError, RuntimeError)):
