@@ -480,7 +480,8 @@ struct OtlpArgs {
   ose_strref* route;
   uint32_t* span_size;
   uint32_t* name_len;
-  uint64_t* attr_match;         // may be null
+  uint64_t* attr_match;         // may be null; attr_words word-major planes of n_spans
+  uint32_t attr_words;
   uint8_t* attr_type;
   uint64_t* attr_val;
   uint8_t* host_flag;           // [n_spans] 1 = the host pass writes this span
@@ -673,7 +674,7 @@ void launch_enc_write(const EncArgs& a, hipStream_t st);
 
 struct OtlpFix {
   uint64_t idx;
-  uint64_t hi, lo, start, end, attr_match;
+  uint64_t hi, lo, start, end;
   ose_strref path, route;
   uint32_t span_size, name_len;
   uint8_t status, kind, url_flags, _pad[5];
@@ -683,6 +684,8 @@ struct OtlpFixArgs {
   uint32_t n_attr_keys;
   uint64_t n_spans;
   const OtlpFix* fix;
+  uint32_t attr_words;          // attr_match words per span (fix_attr: [n * attr_words])
+  const uint64_t* fix_attr;
   const uint8_t* fix_type;      // [n * n_attr_keys]
   const uint64_t* fix_val;
   uint64_t* tid;

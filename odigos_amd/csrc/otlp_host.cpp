@@ -165,6 +165,7 @@ struct OtlpEngine {
   uint64_t key_lens = 0;
   uint8_t* keys_dev = nullptr;   // OtlpKeyDev[] then the bytes
   uint32_t n_attr_keys = 0;
+  uint32_t attr_words = 1;   // attr_match words per span
   bool json_rules = false;
   ResCache res_cache;
   DevResTable res_dev;
@@ -234,12 +235,18 @@ OtlpEngine* otlp_engine(Engine* e, int& rc) {
     delete o;
     return nullptr;
   }
-  if (plan.rule_key.size() > 64) {   // the decoder's per-resource rule word and attr_match are one 64-bit word
-    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 64 span_attribute rules (columnise with ose_batch_* / "
-                           "ose_process_device, whose attr_match takes any number of words)");
+  // the per-resource rule word the decoder caches holds the json (host-pass)
+  // rules only, one bit each; the GPU-evaluated rules need no resource word,
+  // and attr_match carries every rule's bit in (rules + 63) / 64 words
+  size_t n_host_rules = 0;
+  for (int rk : plan.rule_key) n_host_rules += rk < 0;
+  if (n_host_rules > 64) {
+    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 64 span_attribute rules with json conditions (columnise with "
+                           "ose_batch_* / ose_process_device, whose attr_match takes any number of words)");
     delete o;
     return nullptr;
   }
+  o->attr_words = (uint32_t)std::max<size_t>(1, (plan.rule_key.size() + 63) / 64);
   o->n_attr_keys = (uint32_t)plan.keys.size();
   for (size_t k = 0; k < plan.keys.size(); k++) roles[plan.keys[k]] |= kRoleAttr0 << k;
   for (size_t k = 0; k < plan.rule_key.size(); k++)
@@ -322,6 +329,26 @@ constexpr size_t kGpuScopeBytes = size_t(64) << 10;
 uint64_t sov64(uint64_t x) { uint64_t n = 1; while (x >= 0x80) { x >>= 7; n++; } return n; }
 uint64_t flen(uint64_t l) { return 1 + sov64(l) + l; }
 
+// The json (host-pass) span_attribute rules of a resource as one word: bit j
+// for the j-th host rule in rule order (words: the resource's bits of every
+// rule, 64 per word; ColumnizeCtx::attr_plan.host_mask marks the host rules)
+uint64_t host_rule_word(const AttrPlan& p, const std::vector<uint64_t>& words) {
+  uint64_t out = 0;
+  uint32_t j = 0;
+  for (size_t w = 0; w < p.host_mask.size(); w++)
+    for (uint64_t m = p.host_mask[w]; m; m &= m - 1, j++)
+      if (w < words.size() && ((words[w] >> __builtin_ctzll(m)) & 1)) out |= 1ull << j;
+  return out;
+}
+// ... and back to the rule-indexed words columnize_span takes
+void host_rule_words(const AttrPlan& p, uint64_t word, std::vector<uint64_t>& out) {
+  out.assign(std::max<size_t>(1, p.host_mask.size()), 0);
+  uint32_t j = 0;
+  for (size_t w = 0; w < p.host_mask.size(); w++)
+    for (uint64_t m = p.host_mask[w]; m; m &= m - 1, j++)
+      if ((word >> j) & 1) out[w] |= 1ull << __builtin_ctzll(m);
+}
+
 // A resource's columns from its Resource field(s) (merged as pdata merges
 // them), entered into the cache by message bytes when there is at most one
 // field.  False: a malformed Resource.
@@ -335,7 +362,7 @@ bool resolve_resource(const ColumnizeCtx& ctx, ResCache& cache, const uint8_t* p
   cr.svc = rc.svc;
   cr.svc_str = rc.svc_str;
   cr.ok = rc.url_ok;
-  cr.attr_res = rc.attr_res.empty() ? 0 : rc.attr_res[0];   // <= 64 rules here (otlp_engine)
+  cr.attr_res = host_rule_word(ctx.attr_plan, rc.attr_res);   // <= 64 json rules (otlp_engine)
   cr.rpart = (uint32_t)flen(sizer.attrs(attrs, 1) + (dropped ? 1 + sov64(dropped) : 0));   // Resource: always emitted
   const std::string_view key = resf.size() == 1 ? std::string_view((const char*)p + resf[0].first, resf[0].second)
                                                 : std::string_view();
@@ -1259,7 +1286,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
       {(void**)&host_list, 4 * N, nullptr},
   };
   parts.insert(parts.end(), outs.begin(), outs.end());
-  if (o->json_rules) parts.push_back({(void**)&c.attr_match, 8 * N, nullptr});
+  if (o->json_rules) parts.push_back({(void**)&c.attr_match, 8 * N * (size_t)o->attr_words, nullptr});
   if (K) {
     parts.push_back({(void**)&c.attr_type, (size_t)K * N, nullptr});
     parts.push_back({(void**)&c.attr_val, 8 * (size_t)K * N, nullptr});
@@ -1307,6 +1334,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   c.arena = b->arena.p;
   c.arena_bytes = len;
   c.n_attr_keys = K;
+  c.attr_match_words = o->attr_words;
   if (!o->ctx.url_filter) c.res_url_ok = nullptr;
   std::vector<uint64_t>& attr_res = w.attr_res;
   lap(2);
@@ -1319,6 +1347,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   a.key_bytes = o->keys_dev + o->keys.size() * sizeof(OtlpKeyDev);
   a.n_keys = (uint32_t)o->keys.size();
   a.n_attr_keys = K;
+  a.attr_words = o->attr_words;
   a.key_lens = o->key_lens;
   a.tid = const_cast<uint64_t*>(c.trace_id);
   a.start = const_cast<uint64_t*>(c.start_ns);
@@ -1367,6 +1396,8 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   std::vector<OtlpFix> fix(cnt);
   std::vector<uint8_t> fix_type((size_t)cnt * K);
   std::vector<uint64_t> fix_val((size_t)cnt * K);
+  const uint32_t AW = o->json_rules ? o->attr_words : 0;   // attr_match words the host pass writes per span
+  std::vector<uint64_t> fix_attr((size_t)cnt * AW);
   std::string strs;   // appended after the message bytes
   const size_t str_base = pb_cap;
   auto put = [&](const std::string& s) {
@@ -1381,8 +1412,9 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     const uint64_t ref = b->span_ref[i];
     Span sp;
     if (!pb_span(pb + (uint32_t)ref, (size_t)(ref >> 32), sp)) return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
-    res_words.assign(1, attr_res[(*sres)[i]]);
+    host_rule_words(o->ctx.attr_plan, attr_res[(*sres)[i]], res_words);
     columnize_span(o->ctx, sp, res_words, sizer, sc);
+    for (uint32_t w = 0; w < AW; w++) fix_attr[(size_t)q * AW + w] = w < sc.attr_match.size() ? sc.attr_match[w] : 0;
     OtlpFix& x = fix[q];
     x = OtlpFix{};
     x.idx = i;
@@ -1390,7 +1422,6 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     x.lo = sc.lo;
     x.start = sc.start;
     x.end = sc.end;
-    x.attr_match = sc.attr_match.empty() ? 0 : sc.attr_match[0];
     x.status = sc.status;
     x.kind = sc.kind;
     x.url_flags = sc.url_flags;
@@ -1420,21 +1451,25 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   }
   c.arena_bytes = str_base + strs.size();
   const size_t fb = up(cnt * sizeof(OtlpFix)), tb = up((size_t)cnt * K + 16), vb = up((size_t)cnt * K * 8 + 16);
-  if ((rc = b->stage.need(fb + tb + vb + strs.size() + 16))) return rc;
+  const size_t ab = up((size_t)cnt * AW * 8 + 16), fixb = fb + tb + vb + ab;
+  if ((rc = b->stage.need(fixb + strs.size() + 16))) return rc;
   DevBuf& fixdev = b->fixdev;
-  if ((rc = fixdev.need(fb + tb + vb))) return rc;
+  if ((rc = fixdev.need(fixb))) return rc;
   std::memcpy(b->stage.p, fix.data(), cnt * sizeof(OtlpFix));
   if (K) {
     std::memcpy(b->stage.p + fb, fix_type.data(), (size_t)cnt * K);
     std::memcpy(b->stage.p + fb + tb, fix_val.data(), (size_t)cnt * K * 8);
   }
-  std::memcpy(b->stage.p + fb + tb + vb, strs.data(), strs.size());
-  HIP_TRY(hipMemcpyAsync(fixdev.p, b->stage.p, fb + tb + vb, hipMemcpyHostToDevice, st));
+  std::memcpy(b->stage.p + fb + tb + vb, fix_attr.data(), (size_t)cnt * AW * 8);
+  std::memcpy(b->stage.p + fixb, strs.data(), strs.size());
+  HIP_TRY(hipMemcpyAsync(fixdev.p, b->stage.p, fixb, hipMemcpyHostToDevice, st));
   if (!strs.empty())
-    HIP_TRY(hipMemcpyAsync(b->arena.p + str_base, b->stage.p + fb + tb + vb, strs.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(b->arena.p + str_base, b->stage.p + fixb, strs.size(), hipMemcpyHostToDevice, st));
   OtlpFixArgs fa{};
   fa.n = cnt;
   fa.n_attr_keys = K;
+  fa.attr_words = AW;
+  fa.fix_attr = reinterpret_cast<const uint64_t*>(fixdev.p + fb + tb + vb);
   fa.n_spans = n;
   fa.fix = reinterpret_cast<const OtlpFix*>(fixdev.p);
   fa.fix_type = fixdev.p + fb;
@@ -1744,7 +1779,7 @@ int ose_otlp_download(const ose_otlp_batch* bb, const ose_columns* dst) {
       {c.status, (void*)dst->status, n}, {c.kind, (void*)dst->kind, n}, {c.resource, (void*)dst->resource, 4 * n},
       {c.scope, (void*)dst->scope, 4 * n}, {c.url_flags, (void*)dst->url_flags, n}, {c.path, (void*)dst->path, 8 * n},
       {c.route, (void*)dst->route, 8 * n}, {c.span_size, (void*)dst->span_size, 4 * n},
-      {c.name_len, (void*)dst->name_len, 4 * n}, {c.attr_match, (void*)dst->attr_match, 8 * n},
+      {c.name_len, (void*)dst->name_len, 4 * n}, {c.attr_match, (void*)dst->attr_match, 8 * n * std::max<uint32_t>(1, c.attr_match_words)},
       {c.res_svc, (void*)dst->res_svc, 4 * R}, {c.res_svc_str, (void*)dst->res_svc_str, 4 * R},
       {c.res_url_ok, (void*)dst->res_url_ok, R}, {c.res_attrset, (void*)dst->res_attrset, 4 * R},
       {c.res_size, (void*)dst->res_size, 4 * R}, {c.scope_size, (void*)dst->scope_size, 4 * S},

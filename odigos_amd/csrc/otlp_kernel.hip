@@ -298,7 +298,8 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
     a.path[i] = path;
     a.route[i] = (found & kRoleRoute) ? ose_strref{route.off, route.len} : ose_strref{0, 0};
     a.name_len[i] = name_len;
-    if (a.attr_match) a.attr_match[i] = 0;
+    if (a.attr_match)
+      for (uint32_t w = 0; w < a.attr_words; w++) a.attr_match[(uint64_t)w * a.n_spans + i] = 0;
     // ProtoSizer::span (gogo): ids, Status and KeyValue.value always emitted
     const uint64_t st = str_field(st_msg) + varint_field((uint64_t)(int64_t)(int32_t)st_code);
     const uint64_t sz = (tid_nz ? 18 : 2) + (sid_nz ? 10 : 2) + str_field(ts_len) + (pid_nz ? 10 : 2) +
@@ -326,7 +327,8 @@ __global__ __launch_bounds__(kOThreads) void otlp_fix_kernel(OtlpFixArgs a) {
   a.route[i] = x.route;
   a.name_len[i] = x.name_len;
   a.span_size[i] = x.span_size;
-  if (a.attr_match) a.attr_match[i] = x.attr_match;
+  if (a.attr_match)
+    for (uint32_t w = 0; w < a.attr_words; w++) a.attr_match[(uint64_t)w * a.n_spans + i] = a.fix_attr[(uint64_t)q * a.attr_words + w];
   for (uint32_t k = 0; k < a.n_attr_keys; k++) {
     a.attr_type[(uint64_t)k * a.n_spans + i] = a.fix_type[(uint64_t)q * a.n_attr_keys + k];
     a.attr_val[(uint64_t)k * a.n_spans + i] = a.fix_val[(uint64_t)q * a.n_attr_keys + k];

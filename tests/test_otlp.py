@@ -56,6 +56,15 @@ CFG_MANY_KEYS["odigossampling"]["endpoint_rules"] += [
      "rule_details": {"service_name": SERVICES[j % len(SERVICES)], "attribute_key": f"k{j}",
                       "condition_type": "string", "operation": "equals", "expected_value": "v",
                       "sampling_ratio": float(j)}} for j in range(40)]
+# past 64 span_attribute rules (attr_match in two words): 70 string rules over
+# the 40 keys, and the json rule after them (its bit in the second word)
+CFG_MANY_RULES = json.loads(json.dumps(CFG_JSON_RULE))
+_js = CFG_MANY_RULES["odigossampling"]["endpoint_rules"].pop()
+CFG_MANY_RULES["odigossampling"]["endpoint_rules"] += [
+    {"name": f"m{j}", "type": "span_attribute",
+     "rule_details": {"service_name": SERVICES[j % len(SERVICES)], "attribute_key": f"k{j % 40}",
+                      "condition_type": "string", "operation": "equals" if j % 2 else "contains",
+                      "expected_value": "v", "sampling_ratio": float(j)}} for j in range(70)] + [_js]
 CFG_EXCLUDE = json.loads(json.dumps(CFG))
 CFG_EXCLUDE["odigosurltemplate"] = {"exclude": {"k8s_workloads": [{"namespace": "prod", "kind": "Deployment",
                                                                     "name": "api"}]}}
@@ -335,21 +344,26 @@ def _compare(cols, hb_cols, got):
         h2 = np.stack([hv[s] & 0xFFFFFFFF, hv[s] >> 32], 1)
         assert _strings(garena, g2) == _strings(harena, h2)
     if got.get("attr_match") is not None and hb_cols.attr_match:
-        np.testing.assert_array_equal(got["attr_match"].view(np.uint64)[:n], _arr(hb_cols.attr_match, n, np.uint64))
+        W = max(1, hb_cols.attr_match_words)
+        assert max(1, cols.attr_match_words) == W
+        np.testing.assert_array_equal(got["attr_match"].view(np.uint64)[:W * n],
+                                      _arr(hb_cols.attr_match, W * n, np.uint64))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,odd,cfg", [(0, 0.0, "base"), (1, 0.0, "base"), (2, 0.15, "base"), (3, 0.1, "json"),
-                                          (4, 0.0, "exclude"), (5, 0.3, "json"), (6, 0.0, "many_keys")])
+                                          (4, 0.0, "exclude"), (5, 0.3, "json"), (6, 0.0, "many_keys"),
+                                          (7, 0.1, "many_rules")])
 def test_gpu_decode_matches_host_columns(seed, odd, cfg):
     from odigos_amd.batch import Engine, OtlpBatch
-    c = {"base": CFG, "json": CFG_JSON_RULE, "exclude": CFG_EXCLUDE, "many_keys": CFG_MANY_KEYS}[cfg]
+    c = {"base": CFG, "json": CFG_JSON_RULE, "exclude": CFG_EXCLUDE, "many_keys": CFG_MANY_KEYS,
+         "many_rules": CFG_MANY_RULES}[cfg]
     rng = random.Random(seed)
-    td = _http_traces(rng, 200, odd=odd, extra_keys=40 if cfg == "many_keys" else 0)
+    td = _http_traces(rng, 200, odd=odd, extra_keys=40 if cfg in ("many_keys", "many_rules") else 0)
     _, hb = _host_columns(c, td)
     eng = Engine(c)
     ob = OtlpBatch(eng, to_pb(td))
-    if odd == 0.0 and cfg != "json":
+    if odd == 0.0 and cfg not in ("json", "many_rules"):
         assert ob.host_spans == 0
     else:
         assert ob.host_spans > 0
@@ -424,15 +438,16 @@ def test_gpu_decode_generic_traces():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["base", "json"])
+@pytest.mark.parametrize("cfg", ["base", "json", "many_rules"])
 def test_gpu_stages_on_decoded_columns(cfg):
     """SAMPLE|TEMPLATE|SIZE on the decoded columns equals the oracle chain on
-    the host columniser's batch (decisions, templates, counters)."""
+    the host columniser's batch (decisions, templates, counters); many_rules:
+    71 span_attribute rules, attr_match in two words."""
     import torch
     from odigos_amd.batch import Engine, HostOutputs, OtlpBatch
     from tests.oracle_lib import SamplingOracle, UrlOracle, size_process
-    c = {"base": CFG, "json": CFG_JSON_RULE}[cfg]
-    td = _http_traces(random.Random(77), 400, odd=0.05)
+    c = {"base": CFG, "json": CFG_JSON_RULE, "many_rules": CFG_MANY_RULES}[cfg]
+    td = _http_traces(random.Random(77), 400, odd=0.05, extra_keys=40 if cfg == "many_rules" else 0)
     _, hb = _host_columns(c, td)
     eng = Engine(c)
     ob = OtlpBatch(eng, to_pb(td))
