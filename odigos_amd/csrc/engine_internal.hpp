@@ -80,6 +80,10 @@ struct Workspace {
   int reserve_attr(uint64_t n_spans);
   uint64_t* ep_planes = nullptr;   // endpoint bits per rule chunk of a config with spilled route bytes
   uint64_t ep_planes_cap = 0;      // (words)
+  // the caller's columns with the spilled endpoint planes substituted: the
+  // SAMPLE stage's host-gated tail reads them after run_sampling returned,
+  // so they live with the workspace the call holds, not on its stack
+  ose_columns spill_cols{};
   int reserve_ep_planes(uint64_t words);
   // SAMPLE + TEMPLATE in one call: the fast path's dup flag is copied here and
   // read by the host after the URL launches are queued (run_stages), so the

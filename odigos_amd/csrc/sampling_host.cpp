@@ -715,18 +715,18 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   const uint32_t K = (uint32_t)e->sampling_chunks_dev.size();
   if (K > 1 && c->svc_match && c->match_planes != K)
     return fail(OSE_EINVAL, "cols->match_planes must equal the engine's rule chunks when svc_match is set");
-  ose_columns cs = *c;
   // (a batch without route bytes has no endpoint bits to spill: the trace
-  // stage reads a missing route column as "no routes")
+  // stage refuses a missing route column)
   if (e->sampling_spill && !c->route_match && c->route && e->sampling_n_lat && c->n_spans) {
     const uint64_t* planes = nullptr;
     const int rc = spill_endpoint_planes(e, c, ws, st, &planes);
     if (rc) return rc;
-    cs.route_match = planes;
-    cs.match_planes = K;
+    ws->spill_cols = *c;
+    ws->spill_cols.route_match = planes;
+    ws->spill_cols.match_planes = K;
+    c = &ws->spill_cols;   // outlives this call's stack: the tails below read it later
   }
-  c = nullptr;   // below: the (possibly replaced) copy cs, captured by value
-  if (K <= 1) return run_sampling_pass(e, &cs, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr);
+  if (K <= 1) return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr);
   // (one pass over the columns into partial records carrying every chunk's
   // words, decided by the owner fold, measured slower on sampling_wide:
   // 9.72 ms against 7.65, profiles/r4_owner_fold_forms.txt)
@@ -734,7 +734,6 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // call (the host waits for the pass's flags; the run-list and sort launches
   // are queued only for a batch with repeated trace ids)
   auto per_chunk = [=]() -> int {
-  const ose_columns* c = &cs;   // the lambda's own copy of the columns (it may run after run_sampling returns)
   int rc = ws->reserve_fold(std::max<uint64_t>(c->n_spans, 1));
   if (rc) return rc;
   for (uint32_t k = 0; k < K; k++) {
@@ -750,8 +749,8 @@ int run_sampling(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   // every chunk in one pass over the columns (trace_multi_kernel; sampling_wide
   // 5.55 -> see DESIGN §4.2); a batch with repeated trace ids falls back to the
   // passes per chunk
-  if (multi_pass(e, &cs, group_mode))
-    return run_sampling_pass(e, &cs, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr, K, per_chunk);
+  if (multi_pass(e, c, group_mode))
+    return run_sampling_pass(e, c, o, group_mode, rnd, st, ws, tail, 0, nullptr, nullptr, K, per_chunk);
   return per_chunk();
 }
 

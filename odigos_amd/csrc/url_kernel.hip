@@ -161,6 +161,12 @@ __device__ bool has_fffd(R& rd, uint32_t s, uint32_t e) {
   return false;
 }
 
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 constexpr uint32_t kNameTab = 64;
 // The header is copied into registers once per workgroup: read through the
 // blob pointer the compiler cannot prove it unclobbered by the kernel's own
@@ -516,38 +522,30 @@ __device__ __forceinline__ void build_bitmaps(lds_u32* stage32, lds_u4* bm, uint
   const uint32_t rows = (bytes + 31) / 32;
   for (uint32_t r = lane; r < rows; r += kWave) build_row(stage32, bm, r);
 }
-// position of the k-th set bit of m (k < popcount(m))
-__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t k) {
-  uint32_t pos = 0;
-#pragma unroll
-  for (uint32_t w = 16; w; w >>= 1) {
-    const uint32_t c = __builtin_popcount(m & ((1u << w) - 1u));
-    if (k >= c) {
-      k -= c;
-      m >>= w;
-      pos += w;
-    }
-  }
-  return pos;
-}
 // Only the rows (bit r of the 96-bit mask {m0, m1, m2}) that hold path bytes:
 // every reader of the bitmaps masks its windows to a path's own bytes, so the
-// rows between paths (other strings of the arena) are never looked at.
+// rows between paths (other strings of the arena) are never looked at.  The
+// k-th set row is found through a list in LDS (`list`, >= 96 words of the
+// wave's free segment list): lane L enters rows L and 64 + L at their rank
+// among the set rows (mbcnt), then lane k reads entry k.  (Selecting the k-th
+// set bit per lane with a popcount bisection cost about 75 vector
+// instructions per row, half of building the row.)
 __device__ __forceinline__ void build_bitmaps_rows(lds_u32* stage32, lds_u4* bm, uint32_t m0, uint32_t m1,
-                                                   uint32_t m2) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t c0 = __builtin_popcount(m0), c1 = __builtin_popcount(m1), total = c0 + c1 + __builtin_popcount(m2);
-  auto row_of = [&](uint32_t k) {
-    return k < c0 ? select_bit(m0, k) : k < c0 + c1 ? 32 + select_bit(m1, k - c0) : 64 + select_bit(m2, k - c0 - c1);
-  };
+                                                   uint32_t m2, uint32_t* list) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t c01 = __builtin_popcount(m0) + __builtin_popcount(m1), total = c01 + __builtin_popcount(m2);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi(m1, __builtin_amdgcn_mbcnt_lo(m0, 0u));   // set rows < lane
+  if ((((lane < 32 ? m0 : m1) >> (lane & 31)) & 1u) != 0) list[below] = lane;
+  if (lane < 32 && ((m2 >> lane) & 1u) != 0) list[c01 + __builtin_amdgcn_mbcnt_lo(m2, 0u)] = 64 + lane;
+  wave_lds_sync();
   // full rounds while 64 rows are left; a last round of at most 16 rows in
   // quarter rows (four lanes per row)
   const uint32_t full = total > kWave && total - (total & ~(kWave - 1)) <= 16 ? total & ~(kWave - 1) : total;
-  for (uint32_t k = lane; k < full; k += kWave) build_row(stage32, bm, row_of(k));
+  for (uint32_t k = lane; k < full; k += kWave) build_row(stage32, bm, list[k]);
   if (full < total) {
-    const uint32_t k = full + ((uint32_t)lane >> 2);
+    const uint32_t k = full + (lane >> 2);
     const bool valid = k < total;
-    build_quarter_row(stage32, bm, valid ? row_of(k) : 0u, (uint32_t)lane & 3u, valid);
+    build_quarter_row(stage32, bm, valid ? list[k] : 0u, lane & 3u, valid);
   }
 }
 // bits [lo, hi] (rows) of the 32-row word starting at row w0
@@ -647,17 +645,6 @@ __device__ __forceinline__ bool date_pre(uint64_t dg, uint64_t dash, uint32_t L)
   dm |= zsel == 2 ? 0xFull << (z + 1) : 0ull;                 // +HHMM
   return (dg & dm) == dm && ((dash >> 4) & 1) != 0 && ((dash >> 7) & 1) != 0;
 }
-// date_win given bytes 10-13 (wa) and 16-19 (wb) of the segment
-__device__ __forceinline__ bool date_words(uint64_t dg, uint64_t dash, uint32_t L, uint32_t wa, uint32_t wb) {
-  if (!date_pre(dg, dash, L)) return false;
-  const uint32_t sh = date_shape(L);
-  const uint32_t tsel = sh & 3u, zsel = sh >> 2;
-  const uint32_t tlen = tsel == 1 ? 0u : tsel == 2 ? 6u : 9u;
-  const uint32_t c_t = wa & 0xFFu, c_c1 = (wa >> 24) & 0xFFu, c_c2 = wb & 0xFFu;
-  const uint32_t c_z = tlen == 0 ? c_t : tlen == 6 ? c_c2 : wb >> 24;
-  return (tlen == 0 || (c_t == 'T' && c_c1 == ':')) && (tlen != 9 || c_c2 == ':') &&
-         (zsel == 0 || (zsel == 1 ? c_z == 'Z' : (c_z == '+' || c_z == '-')));
-}
 template <class R>
 __device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint32_t s, uint32_t L) {
   if (!date_pre(dg, dash, L)) return false;
@@ -675,19 +662,6 @@ __device__ __forceinline__ bool date_win(R& rd, uint64_t dg, uint64_t dash, uint
 // emailRegex (templatize.go:70) from the class windows: exactly one '@' at p,
 // local [0,p) >= 1 byte of [A-Za-z0-9._%+-], domain (p,L) all [A-Za-z0-9.-]
 // whose last '.' is at domain index >= 1 and is followed by >= 2 letters.
-// the email check given its class windows e (BLOC, BDOM, DOT, NAL)
-__device__ __forceinline__ bool email_cls(uint64_t at, const WinT<1>& e, uint32_t L) {
-  const uint64_t M = low_mask(L);
-  const uint32_t p = (uint32_t)__builtin_ctzll(at);
-  if (p == 0) return false;
-  const uint64_t dom = M & ~low_mask(p + 1);
-  if ((e.c[0] & low_mask(p)) || (e.c[1] & dom)) return false;
-  const uint64_t dots = e.c[2] & dom;
-  if (!dots) return false;
-  const uint32_t q = 63 - (uint32_t)__builtin_clzll(dots);
-  if (q < p + 2 || L - q - 1 < 2) return false;
-  return (e.c[3] & M & ~low_mask(q + 1)) == 0;
-}
 __device__ __forceinline__ bool email_win(uint64_t at, lds_cu4* bm, uint32_t a, uint32_t L) {
   const uint64_t M = low_mask(L);
   const uint32_t p = (uint32_t)__builtin_ctzll(at);
@@ -760,10 +734,42 @@ __device__ __forceinline__ int classify_win(const Cfg& cfg, R& rd, const Win& w,
   return -1;
 }
 
-// classify_win with the date bytes and the email windows read together with
-// the main windows (every lane, whether its segment needs them or not): any
-// of a step's 64 segments taking the date or email branch made the whole wave
-// wait for those reads one after the other
+// datesRegex as one expression (no early exit): the length's shape, the
+// digit and dash windows, and bytes 10-13 (wa) / 16-19 (wb) of the segment
+__device__ __forceinline__ bool date_flat(uint64_t dg, uint64_t dash, uint32_t L, uint32_t wa, uint32_t wb) {
+  const uint32_t sh = date_shape(L);
+  const uint32_t tsel = sh & 3u, zsel = sh >> 2;
+  const uint32_t tlen = tsel == 1 ? 0u : tsel == 2 ? 6u : 9u;
+  uint64_t dm = 0x36Full;                                     // YYYY-MM-DD digits
+  dm |= tsel >= 2 ? (3ull << 11) | (3ull << 14) : 0ull;       // THH:MM
+  dm |= tsel == 3 ? 3ull << 17 : 0ull;                        // :SS
+  dm |= zsel == 2 ? 0xFull << (11 + tlen) : 0ull;             // +HHMM
+  const uint32_t c_t = wa & 0xFFu, c_c1 = (wa >> 24) & 0xFFu, c_c2 = wb & 0xFFu;
+  const uint32_t c_z = tlen == 0 ? c_t : tlen == 6 ? c_c2 : wb >> 24;
+  const bool zone = zsel == 0 ? true : zsel == 1 ? c_z == 'Z' : (c_z == '+') | (c_z == '-');
+  return (tsel != 0) & ((dg & dm) == dm) & ((((dash >> 4) & (dash >> 7)) & 1) != 0) &
+         ((tlen == 0) | ((c_t == 'T') & (c_c1 == ':'))) & ((tlen != 9) | (c_c2 == ':')) & zone;
+}
+// emailRegex as one expression, given that the segment holds exactly one '@'
+// (at) and no byte >= 0x80; e: the BLOC, BDOM, DOT, NAL windows
+__device__ __forceinline__ bool email_flat(uint64_t at, const WinT<1>& e, uint32_t L) {
+  const uint64_t M = low_mask(L);
+  const uint32_t p = (uint32_t)__builtin_ctzll(at | (1ull << 63));
+  const uint64_t dom = M & ~low_mask(p + 1);
+  const uint64_t dots = e.c[2] & dom;
+  const uint32_t q = 63 - (uint32_t)__builtin_clzll(dots | 1ull);
+  return (p != 0) & ((e.c[0] & low_mask(p)) == 0) & ((e.c[1] & dom) == 0) & (dots != 0) & (q >= p + 2) &
+         (L >= q + 3) & ((e.c[3] & M & ~low_mask(q + 1)) == 0);
+}
+
+// classify_win for the default configuration (no custom ids), without
+// branches: every predicate of getSegmentTemplatizationString is evaluated
+// for every lane from its windows and the date bytes, and the first that
+// holds in templatize.go's order (date, email, the ID rules) names the
+// segment.  The short-circuit form compiled to nested exec-mask branches
+// (about 300 scalar instructions per 64-segment step, more than its vector
+// work) although nearly every branch was taken by some lane of the step.
+// Only the U+FFFD walk stays a loop, entered when some lane needs it.
 template <class R>
 __device__ __forceinline__ int classify_spec(const Cfg& cfg, R& rd, lds_cu4* bm, uint32_t a, uint32_t s, uint32_t L) {
   const Win w = load_win6(bm, a);
@@ -771,20 +777,20 @@ __device__ __forceinline__ int classify_spec(const Cfg& cfg, R& rd, lds_cu4* bm,
   const uint32_t wa = rd.word(s + 10), wb = rd.word(s + 16);
   if (cfg.n_custom) return classify_win(cfg, rd, w, bm, a, s, L);
   const uint64_t M = low_mask(L);
-  if (date_words(w.c[C_DG], w.c[C_DASH], L, wa, wb)) return kNameDate;
-  const bool any_hi = (w.c[C_HI] & M) != 0;
+  const bool date = date_flat(w.c[C_DG], w.c[C_DASH], L, wa, wb);
+  const uint64_t hm = w.c[C_HI] & M;
   const uint64_t at = w.c[C_AT] & M;
-  if (!any_hi && at && (at & (at - 1)) == 0 && email_cls(at, e, L)) return kNameEmail;
+  const bool email = (hm == 0) & (at != 0) & ((at & (at - 1)) == 0) & email_flat(at, e, L);
   const uint64_t d = w.c[C_DG] & M, d1 = d & (d >> 1), d2 = d1 & (d1 >> 2), d7 = d2 & (d2 >> 3);
-  if ((L > 0 && (w.c[C_BNL] & M) == 0) || d7 || ((w.c[C_BHX] & M) == 0 && L >= 16 && (L & 1) == 0)) return kNameId;
-  if (L >= 36) {
-    const uint64_t hx = ~w.c[C_BHX], ds = w.c[C_DASH], sh = L - 36;
-    if (((hx & kUuidHex) == kUuidHex && (ds & kUuidDash) == kUuidDash) ||
-        (((hx >> sh) & kUuidHex) == kUuidHex && ((ds >> sh) & kUuidDash) == kUuidDash))
-      return kNameId;
-  }
-  if (any_hi && has_fffd_win(rd, w.c[C_HI] & M, s, L)) return kNameId;
-  return -1;
+  const uint64_t hx = ~w.c[C_BHX], ds = w.c[C_DASH], sh = L >= 36 ? L - 36 : 0;
+  const bool uuid = (L >= 36) & ((((hx & kUuidHex) == kUuidHex) & ((ds & kUuidDash) == kUuidDash)) |
+                                 ((((hx >> sh) & kUuidHex) == kUuidHex) & (((ds >> sh) & kUuidDash) == kUuidDash)));
+  const bool idp = ((L > 0) & ((w.c[C_BNL] & M) == 0)) | (d7 != 0) |
+                   (((w.c[C_BHX] & M) == 0) & (L >= 16) & ((L & 1) == 0)) | uuid;
+  int id = date ? (int)kNameDate : email ? (int)kNameEmail : idp ? (int)kNameId : -1;
+  const bool fffd = (hm != 0) & (id < 0);
+  if (__ballot(fffd) != 0 && fffd && has_fffd_win(rd, hm, s, L)) id = kNameId;
+  return id;
 }
 
 // Rare paths kept out of line so the hot LDS->LDS instantiation stays small:
@@ -810,11 +816,6 @@ __device__ __forceinline__ uint32_t pack_meta(uint32_t mode, uint32_t lead, bool
 constexpr uint32_t kNamesLds = 512;
 constexpr uint32_t kWaveOut = 4 * 1024;   // per-wave LDS image of one group's output
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Copies the arena bytes [lo, hi) the wave's 64 lanes reference (16-byte
 // aligned down) into the wave's LDS slice.  Returns the aligned start (and
@@ -1287,7 +1288,9 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   // id + 1 in 8 bits: 255 stands for every id >= 254 (such plans are `slow`
   // and re-classify their segments when emitted)
   auto put_cls = [&](uint32_t x, int id, uint32_t L) {
-    const uint32_t out = id >= 0 ? name_len(cfg, (uint32_t)id) + 2 : L;
+    const uint32_t nl = cfg.names_tab_all ? (uint32_t)cfg.name_tab[id >= 0 ? id : 0].len
+                                          : (id >= 0 ? name_len(cfg, (uint32_t)id) : 0u);
+    const uint32_t out = id >= 0 ? nl + 2 : L;
     cls[x] = (out << 8) | min((uint32_t)(id + 1), 255u);
   };
   for (uint32_t x0 = 0; x0 < total; x0 += kWave) {   // classify
@@ -1413,8 +1416,11 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       const uint32_t pos = (uint32_t)(((int32_t)(opk << 16) >> 16) + (int32_t)E);
       const bool slash = x != ((opk >> 16) & 0xFFu) || (opk >> 24);
       const int id = (int)(c & 0xFFu) - 1;
-      const uint32_t so = id >= 0 ? bn_src + bn.off[id] : stage_src + (ent & 0xFFFu);   // the body's LDS byte offset
-      const uint32_t n = id >= 0 ? (uint32_t)bn.len[id] : (ent >> 12) & 0x1FFFu;
+      // both candidates read unconditionally (a branch on id >= 0 cost the
+      // step its exec-mask bookkeeping)
+      const uint32_t idc = id >= 0 ? (uint32_t)id : 0u, boff = bn.off[idc], blen = bn.len[idc];
+      const uint32_t so = id >= 0 ? bn_src + boff : stage_src + (ent & 0xFFFu);   // the body's LDS byte offset
+      const uint32_t n = id >= 0 ? blen : (ent >> 12) & 0x1FFFu;
       if (slash) img[pos] = '/';
       lds_out_u8* dp = img + pos + 1;
       const lds_u8* sp = L + so;
@@ -1517,7 +1523,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
       m0 = wave_or_u32(m0);
       m1 = wave_or_u32(m1);
       m2 = wave_or_u32(m2);
-      build_bitmaps_rows(stage32, (lds_u4*)sm.bm[wv], m0, m1, m2);
+      build_bitmaps_rows(stage32, (lds_u4*)sm.bm[wv], m0, m1, m2, sm.segs[wv]);
       wave_lds_sync();
     }
     if (tm) { const uint64_t t1 = clk(); t_bm += t1 - t0; t0 = t1; }
@@ -1913,7 +1919,7 @@ __global__ __launch_bounds__(kWave) void url_plan_slow_kernel(UrlKernelArgs a) {
         m1 = row_bits(rl, rh, 32);
         m2 = row_bits(rl, rh, 64);
       }
-      build_bitmaps_rows(stage32, (lds_u4*)sm.bm, wave_or_u32(m0), wave_or_u32(m1), wave_or_u32(m2));
+      build_bitmaps_rows(stage32, (lds_u4*)sm.bm, wave_or_u32(m0), wave_or_u32(m1), wave_or_u32(m2), sm.segs);
       wave_lds_sync();
       Plan q;
       const bool listed = plan_group_list(cfg, stage32, (lds_cu4*)sm.bm, sm.segs, take, p0, c.pr.len, c.f, q, false,
