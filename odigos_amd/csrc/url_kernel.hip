@@ -1061,7 +1061,8 @@ struct PlanSmem {
   __attribute__((aligned(16))) uint8_t stage[kWaves][kPlanStage + 16];
   __attribute__((aligned(16))) u32x4 bm[kWaves][kRowVec * kPlanBmRows];   // class bitmaps, then the output image
   uint32_t segs[kWaves][kSegCap];   // enumerated segments (start | len | owner lane)
-  uint32_t cls[kWaves][kSegCap];    // their classification (out_len << 8 | id + 1)
+  uint32_t cls[kWaves][kSegCap + 8];   // their classification (out_len << 8 | id + 1); 8 entries of
+                                        // padding for the fold's fixed 8-entry read
   BracedNames bn;
 };
 constexpr uint32_t kImgCap = kRowVec * kPlanBmRows * 16;   // bytes of one wave's output image
@@ -1313,22 +1314,25 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   if (nseg) {   // fold
     uint32_t l = p.lead + nseg - 1;
     bool templated = false;
-    if (nseg <= 8) {   // one read of the (at most 8) entries
+    if (nseg <= 8) {   // one read of the (at most 8) entries, folded without branches
+      // (entries past the list are read from the list's padding and masked)
       uint32_t r[8];
 #pragma unroll
-      for (uint32_t k = 0; k < 8; k++) r[k] = cls[min(off + k, kSegCap - 1)];
+      for (uint32_t k = 0; k < 8; k++) r[k] = cls[off + k];
+      uint32_t any = 0, bigm = 0, code = 0;
 #pragma unroll
       for (uint32_t k = 0; k < 8; k++) {
-        if (k < nseg) {
-          const int id = (int)(r[k] & 0xFFu) - 1;
-          l += r[k] >> 8;
-          if (id >= 0) {
-            templated = true;
-            if (id < 15) p.code |= (uint64_t)(id + 1) << (k * 4);
-            else p.slow = big = true;
-          }
-        }
+        const uint32_t v = k < nseg ? r[k] : 0u;
+        const uint32_t id1 = v & 0xFFu;   // id + 1 (0: the segment stays)
+        l += v >> 8;
+        any |= id1;
+        bigm |= id1 > 15 ? 1u : 0u;
+        code |= (id1 <= 15 ? id1 : 0u) << (4 * k);   // 8 nibbles: the low 32 bits of the code
       }
+      templated = any != 0;
+      big = bigm != 0;
+      p.slow = big;
+      p.code = code;
     } else {
       for (uint32_t k = 0; k < nseg; k++) {
         const uint32_t r = cls[off + k];
@@ -1425,18 +1429,23 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       lds_out_u8* dp = img + pos + 1;
       const lds_u8* sp = L + so;
       // gfx950 LDS takes unaligned 8-, 4- and 2-byte accesses: one 8-byte read
-      // per 8 source bytes (reads past n stay inside the stage / name table),
-      // whole 8-byte stores, and the last 1-7 bytes as a 4-, 2- and 1-byte store
-      for (uint32_t q = 0; q < n; q += 8) {
-        uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + q);
-        const uint32_t rem = n - q;
-        if (rem >= 8) {
-          *reinterpret_cast<lds_w64u*>(dp + q) = v;
+      // per 8 source bytes (reads past n stay inside the stage / name table)
+      // and whole 8-byte stores, then the last 1-7 bytes once after the loop:
+      // two overlapping 4- or 2-byte stores (both inside the entry) or one
+      // byte (the tail's branches were inside every iteration before)
+      const uint32_t nf = n & ~7u, rem = n & 7u;
+      for (uint32_t q = 0; q < nf; q += 8)
+        *reinterpret_cast<lds_w64u*>(dp + q) = *reinterpret_cast<const lds_u64u*>(sp + q);
+      if (rem) {
+        const uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + nf);
+        if (rem >= 4) {
+          *reinterpret_cast<lds_w32u*>(dp + nf) = (uint32_t)v;
+          *reinterpret_cast<lds_w32u*>(dp + n - 4) = (uint32_t)(v >> (8 * (rem - 4)));
+        } else if (rem >= 2) {
+          *reinterpret_cast<lds_w16u*>(dp + nf) = (uint16_t)v;
+          *reinterpret_cast<lds_w16u*>(dp + n - 2) = (uint16_t)(v >> (8 * (rem - 2)));
         } else {
-          uint32_t o = q;
-          if (rem & 4) { *reinterpret_cast<lds_w32u*>(dp + o) = (uint32_t)v; v >>= 32; o += 4; }
-          if (rem & 2) { *reinterpret_cast<lds_w16u*>(dp + o) = (uint16_t)v; v >>= 16; o += 2; }
-          if (rem & 1) dp[o] = (uint8_t)v;
+          dp[nf] = (uint8_t)v;
         }
       }
     }
@@ -1867,7 +1876,7 @@ struct SlowPlanSmem {
   __attribute__((aligned(16))) uint8_t stage[kPlanStage + 16];
   __attribute__((aligned(16))) u32x4 bm[kRowVec * kPlanBmRows];
   uint32_t segs[kSegCap];
-  uint32_t cls[kSegCap];
+  uint32_t cls[kSegCap + 8];   // (8 entries of padding: the fold reads 8)
 };
 __global__ __launch_bounds__(kWave) void url_plan_slow_kernel(UrlKernelArgs a) {
   __shared__ SlowPlanSmem sm;
