@@ -47,10 +47,8 @@ struct SizeKernelArgs {
   const uint8_t* kind;
   const ose_strref* tmpl;
   int64_t inverse;
-  uint64_t* scope_body;       // [S] zeroed
-  uint32_t* scope_had;        // [S] zeroed
-  uint64_t* res_body;         // [R] zeroed
-  uint32_t* res_alive;        // [R] zeroed
+  uint64_t* scope_body;       // [S] zeroed: body bytes | runs that added << kSumBits (size_device.hpp)
+  uint64_t* res_body;         // [R] zeroed: body bytes | alive scopes << kSumBits
   uint32_t* res_had;          // [R] zeroed
   int64_t* attrset_bytes;     // [n_attrsets] added to
   int64_t* accepted;          // [1] added to

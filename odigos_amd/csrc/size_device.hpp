@@ -21,6 +21,14 @@ __device__ __forceinline__ uint32_t sov(uint64_t x) {
 }
 __device__ __forceinline__ uint64_t field_len(uint64_t l) { return 1 + sov(l) + l; }
 
+// The per-scope and per-resource sums carry a count in their top bits: the
+// byte sum in the low kSumBits (a batch's arena offsets are 32-bit, so no
+// scope or resource body reaches 2^40 bytes) and, above it, the number of
+// runs that added to a scope (> 0: the scope had spans) or of alive scopes
+// a resource holds -- one atomic per run instead of a sum and a flag.
+constexpr uint32_t kSumBits = 40;
+constexpr uint64_t kSumMask = (1ull << kSumBits) - 1;
+
 // One DPP step of the segmented sum: (h, v, c) elements, earlier + later =
 // (h_e | h_l, h_l ? (v_l, c_l) : (v_e + v_l, c_e + c_l)); a source lane
 // outside the row yields the identity (0, 0, 0).
@@ -110,11 +118,10 @@ __device__ __forceinline__ uint32_t size_span_finish(const SizeKernelArgs& a, co
   const bool tail = wave_seg_sum(s, x.valid, v, c);
   // a scope keeps a span iff its body sum is non-zero (a kept span adds its
   // framed size, >= 2 bytes): no per-scope kept count (C4 url_copy 0.80 ->
-  // 0.77 ms, profiles/r4za_size_nokept_ab.txt); "had spans" by an atomic OR
-  if (tail) {
-    if (v) atomicAdd((unsigned long long*)&a.scope_body[s], (unsigned long long)v);
-    atomicOr(&a.scope_had[s], 1u);
-  }
+  // 0.77 ms, profiles/r4za_size_nokept_ab.txt); "had spans" is the run count
+  // in the sum's top bits (one atomic per run; an atomic OR on a flag word
+  // beside it before)
+  if (tail) atomicAdd((unsigned long long*)&a.scope_body[s], (unsigned long long)(v + (1ull << kSumBits)));
   return x.valid ? x.kept : 0u;
 }
 

@@ -80,9 +80,7 @@ int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.tmpl = o->tmpl;
   a.inverse = e->inverse;
   a.scope_body = reinterpret_cast<uint64_t*>(sc);
-  a.scope_had = reinterpret_cast<uint32_t*>(sc + 12 * S);
   a.res_body = reinterpret_cast<uint64_t*>(rs);
-  a.res_alive = reinterpret_cast<uint32_t*>(rs + 8 * R);
   a.res_had = reinterpret_cast<uint32_t*>(rs + 12 * R);
   a.attrset_bytes = o->attrset_bytes;
   a.accepted = o->accepted_spans;

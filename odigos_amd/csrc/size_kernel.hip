@@ -66,9 +66,11 @@ __global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a)
   uint64_t contrib = 0;
   if (valid) {
     r = a.scope_resource[s];
-    had = a.scope_had[s];
-    alive = !a.remove_empty || !had || a.scope_body[s] != 0;   // an emptied ScopeSpans is removed
-    if (alive) contrib = field_len((uint64_t)a.scope_size[s] + a.scope_body[s]);
+    const uint64_t sb = a.scope_body[s];
+    const uint64_t body = sb & kSumMask;
+    had = (sb >> kSumBits) != 0;   // some run of spans added to it
+    alive = !a.remove_empty || !had || body != 0;   // an emptied ScopeSpans is removed
+    if (alive) contrib = field_len((uint64_t)a.scope_size[s] + body);
   }
   uint64_t v = contrib;
   uint32_t c = alive;
@@ -85,9 +87,8 @@ __global__ __launch_bounds__(kSThreads) void size_scope_kernel(SizeKernelArgs a)
   const uint32_t h = (hadm & upto & (~0ull << start)) ? 1u : 0u;
   // (plain stores for the runs inside a wave measured slower: C4 0.23 ->
   // 0.32 ms; these atomics resolve in L2)
-  if (tail) {
-    if (v) atomicAdd((unsigned long long*)&a.res_body[r], (unsigned long long)v);
-    if (c) atomicAdd(&a.res_alive[r], c);
+  if (tail) {   // the body sum and the alive scopes' count in one word (kSumBits)
+    if (v | c) atomicAdd((unsigned long long*)&a.res_body[r], (unsigned long long)(v + ((uint64_t)c << kSumBits)));
     if (h) a.res_had[r] = 1;
   }
 }
@@ -104,8 +105,9 @@ __global__ __launch_bounds__(kSThreads) void size_res_kernel(SizeKernelArgs a) {
     for (uint32_t k = threadIdx.x; k < a.n_attrsets; k += kSThreads) hist[k] = 0;
   __syncthreads();
   for (uint32_t r = blockIdx.x * kSThreads + threadIdx.x; r < a.n_resources; r += gridDim.x * kSThreads) {
-    const bool removed = a.remove_empty && a.res_had[r] && !a.res_alive[r];
-    const uint64_t size = removed ? 0 : (uint64_t)a.res_size[r] + a.res_body[r];
+    const uint64_t rb = a.res_body[r];
+    const bool removed = a.remove_empty && a.res_had[r] && (rb >> kSumBits) == 0;   // no alive scope left
+    const uint64_t size = removed ? 0 : (uint64_t)a.res_size[r] + (rb & kSumMask);
     if (a.res_bytes) a.res_bytes[r] = size;
     if (removed) continue;
     const long long add = (long long)size * a.inverse;

@@ -363,65 +363,72 @@ __device__ __forceinline__ void rep_slots(const Cfg& c, bool rep, uint32_t slot,
   }
 }
 
+// uniform (scalar) copies of a rule's fields: the rule table lives in LDS,
+// so its fields arrive in vector registers although every lane reads the
+// same rule; branching on the vector copy cost exec-mask bookkeeping per rule
+__device__ __forceinline__ uint32_t sgpr(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ double sgpr(double x) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  return __builtin_bit_cast(double, (uint64_t)sgpr((uint32_t)b) | ((uint64_t)sgpr((uint32_t)(b >> 32)) << 32));
+}
+
 // ShouldSample's level walk (rule_engine.go:55-83) over evaluateLevel's fold
 // (rule_engine.go:89-115).  level: 0..2 satisfied level, 3 min fallback, 4 none.
+// Without branches on per-trace values (the lanes of a flush decide 64
+// traces together): every level is folded, the first satisfied one is kept
+// (the early return of ShouldSample), and the min fallback of the matched
+// levels is only read when no level was satisfied.  The rule fields are
+// scalar, so the per-type cases are scalar branches.
 __device__ __forceinline__ void decide(const Cfg& c, uint32_t err, uint64_t ep, uint64_t lsat, uint64_t svc, double u,
                               uint8_t& keep, uint8_t& level, double& ratio_out) {
-  bool have_min = false;
-  double min_fb = 0;
+  bool have_min = false, done = false;
+  double min_fb = 0, out_ratio = 100.0;
+  uint32_t out_level = 4;
   for (int L = 0; L < 3; L++) {
     double ratio = 0;
     bool sat = false, matched = false, found_fb = false;
-    for (uint32_t k = c.h->level_first[L]; k < c.h->level_first[L + 1]; k++) {
+    const uint32_t k0 = sgpr(c.h->level_first[L]), k1 = sgpr(c.h->level_first[L + 1]);
+    for (uint32_t k = k0; k < k1; k++) {
       const SampRuleDev& r = c.rules[k];
+      const uint32_t type = sgpr(r.type), bit = sgpr(r.bit);
       bool mt, st;
       double p;
-      if (r.type == kSampError) {            // error.go:29-44
+      if (type == kSampError) {            // error.go:29-44
         mt = true;
         st = err != 0;
-        p = st ? 100.0 : r.fallback;
-      } else if (r.type == kSampLatency) {   // latency.go:84-95
-        mt = (ep >> r.bit) & 1;
-        st = mt && ((lsat >> r.bit) & 1);
-        p = st ? 100.0 : (mt ? r.fallback : 0.0);
-      } else {                               // servicename.go:35-51
-        mt = st = (svc >> r.bit) & 1;
-        p = st ? r.ratio : r.fallback;
+        p = st ? 100.0 : sgpr(r.fallback);
+      } else if (type == kSampLatency) {   // latency.go:84-95
+        mt = (ep >> bit) & 1;
+        st = mt & (((lsat >> bit) & 1) != 0);
+        p = st ? 100.0 : (mt ? sgpr(r.fallback) : 0.0);
+      } else {                             // servicename.go:35-51
+        mt = st = (svc >> bit) & 1;
+        p = st ? sgpr(r.ratio) : sgpr(r.fallback);
       }
-      if (st) {
-        sat = true;
-        ratio = ratio > p ? ratio : p;
-        matched = true;
-      } else if (mt) {
-        matched = true;
-        if (!found_fb) {
-          ratio = p;
-          found_fb = true;
-        } else {
-          ratio = ratio < p ? ratio : p;
-        }
-      }
+      // evaluateLevel: satisfied rules raise the ratio to their max; matched
+      // unsatisfied ones take the first fallback, then the min of fallbacks
+      const double rmax = ratio > p ? ratio : p;
+      const double rfb = found_fb ? (ratio < p ? ratio : p) : p;
+      ratio = st ? rmax : (mt ? rfb : ratio);
+      found_fb |= !st & mt;
+      sat |= st;
+      matched |= mt;
     }
-    if (sat) {
-      level = (uint8_t)L;
-      ratio_out = ratio;
-      keep = u * 100 < ratio;
-      return;
-    }
-    if (matched && (!have_min || ratio < min_fb)) {
-      min_fb = ratio;
-      have_min = true;
-    }
+    const bool take = sat & !done;
+    out_level = take ? (uint32_t)L : out_level;
+    out_ratio = take ? ratio : out_ratio;
+    done |= sat;
+    const bool upd = matched & (!have_min | (ratio < min_fb));
+    min_fb = upd ? ratio : min_fb;
+    have_min |= matched;
   }
-  if (have_min) {
-    level = 3;
-    ratio_out = min_fb;
-    keep = u * 100 < min_fb;
-  } else {
-    level = 4;
-    ratio_out = 100.0;
-    keep = 1;
+  if (!done) {
+    out_level = have_min ? 3u : 4u;
+    out_ratio = have_min ? min_fb : 100.0;
   }
+  level = (uint8_t)out_level;
+  ratio_out = out_ratio;
+  keep = out_level == 4 ? 1 : (u * 100 < out_ratio);
 }
 
 // ShouldSample's walk (decide()) split at rule-chunk boundaries: walk_chunk
