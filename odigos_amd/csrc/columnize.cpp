@@ -111,7 +111,7 @@ void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uin
   const size_t nk = c.attr_plan.keys.size();
   o.attr_type.assign(nk, OSE_ATTR_ABSENT);
   o.attr_val.assign(nk, 0);
-  o.attr_str.assign(nk, std::string());
+  o.attr_str.assign(nk, std::string_view());
   for (size_t k = 0; k < nk; k++) {
     const Value* av = sp.attrs.Get(c.attr_plan.keys[k]);
     if (!av) continue;
@@ -127,10 +127,20 @@ void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uin
   // sampling: AsString(http.route) (latency.go:64-68)
   const Value* route = a.Get("http.route");
   o.has_route = route != nullptr;
-  o.route = route ? route->AsString() : std::string();
+  if (route && route->type == Value::TStr) {
+    o.route = route->s;
+  } else {
+    o.route_own = route ? route->AsString() : std::string();
+    o.route = o.route_own;
+  }
+  auto as_view = [&](const Value* v) -> std::string_view {
+    if (v->type == Value::TStr) return v->s;
+    o.path_own = v->AsString();
+    return o.path_own;
+  };
   // urltemplate (processor.go:98-147, 235-287)
   uint8_t f = 0;
-  o.path.clear();
+  o.path = std::string_view();
   const Value* m = a.Get("http.request.method");
   if (!m) m = a.Get("http.method");
   if (m) {
@@ -143,17 +153,18 @@ void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uin
     }
     if (const Value* p = a.Get("url.path")) {
       f |= OSE_URL_PATH_RAW;
-      o.path = p->AsString();
+      o.path = as_view(p);
     } else if (const Value* p = a.Get("http.target")) {
       f |= OSE_URL_PATH_TARGET;
-      o.path = p->AsString();
+      o.path = as_view(p);
     } else {
       const Value* fu = a.Get("url.full");
       if (!fu) fu = a.Get("http.url");
       std::string path;
       if (fu && go_url_parse_path(fu->AsString(), path)) {
         f |= OSE_URL_PATH_RAW;
-        o.path = std::move(path);
+        o.path_own = std::move(path);
+        o.path = o.path_own;
       }
     }
   }

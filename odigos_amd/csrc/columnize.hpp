@@ -4,6 +4,7 @@
 // the OTLP protobuf ingest (otlp_host.cpp: resources on the host, the spans
 // the GPU decoder hands back for a host pass).
 #pragma once
+#include <string_view>
 #include <cstdint>
 #include <map>
 #include <set>
@@ -44,17 +45,22 @@ struct ResourceCols {
 };
 ResourceCols columnize_resource(const ColumnizeCtx& c, const AttrMap& ra);
 
-// per-span columns; strings are returned as values (the caller places them)
+// per-span columns; strings are returned as views (the caller places them):
+// into the span's own values when they are Str, else into the owned
+// conversions below (AsString of a non-Str route, a path parsed from url.full),
+// so the common case copies no string.  Views are valid while the span and
+// this SpanCols are.
 struct SpanCols {
   uint64_t hi = 0, lo = 0, start = 0, end = 0;
   uint8_t status = 0, kind = 0, url_flags = 0;
   uint32_t span_size = 0, name_len = 0;
   std::vector<uint64_t> attr_match;           // bits of the shim-evaluated (json) rules (64 per word)
   bool has_route = false;
-  std::string route, path;                    // AsString(http.route); the url path source
+  std::string_view route, path;               // AsString(http.route); the url path source
+  std::string route_own, path_own;            // their storage when converted
   std::vector<uint8_t> attr_type;             // per GPU key column
   std::vector<uint64_t> attr_val;             // STR values: placeholder, see attr_str
-  std::vector<std::string> attr_str;          // STR values' bytes (per key; empty otherwise)
+  std::vector<std::string_view> attr_str;     // STR values' bytes (per key; empty otherwise)
 };
 void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uint64_t>& attr_res, const ProtoSizer& sizer,
                     SpanCols& out);

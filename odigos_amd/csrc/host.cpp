@@ -10,10 +10,13 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <set>
+#include <string_view>
 #include <thread>
 
 #include "span_attr.hpp"
+#include "taskpool.hpp"
 #include "urlparse.hpp"
 
 namespace ose {
@@ -125,80 +128,172 @@ double TracesProcessor::next_uniform() {
   return (double)(z >> 11) * 0x1.0p-53;
 }
 
-std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const {
+// The columns of a batch: presized, then filled by resource ranges in
+// parallel on the host task pool (taskpool.hpp) when the batch is large
+// enough to pay for it.  Each range writes its spans' columns in place and
+// its strings into a range-local arena and interns its attribute sets
+// locally; the merge concatenates the arenas (shifting the ranges' string
+// refs) and renumbers the attribute sets in first-appearance order, so the
+// result is the one a sequential walk gives.  keep_copy: the batch keeps a
+// copy of the traces (the test seam's apply reads it); ProcessTraces
+// applies the outputs to its own traces and passes false.
+std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td, bool keep_copy) const {
   auto hb = std::make_unique<HostBatch>();
-  hb->td = td;
-  const Traces& t = hb->td;
-  ProtoSizer sizer;
-  std::map<std::vector<std::pair<std::string, std::string>>, uint32_t> attrset_ids;
-  std::string arena;
-  auto add_str = [&](const std::string& s) {
-    ose_strref r{(uint32_t)arena.size(), (uint32_t)s.size()};
-    arena += s;
-    return r;
-  };
-  uint32_t scope_idx = 0;
-  const size_t nk = ctx_.attr_plan.keys.size();
-  std::vector<std::pair<std::vector<uint8_t>, std::vector<uint64_t>>> attr_cols(nk);
-  SpanCols sc;
-  for (size_t ri = 0; ri < t.resource_spans.size(); ri++) {
-    const ResourceSpans& rs = t.resource_spans[ri];
-    const ResourceCols rc = columnize_resource(ctx_, rs.resource_attrs);
-    hb->res_svc.push_back(rc.svc);
-    hb->res_svc_str.push_back(rc.svc_str);
-    hb->res_url_ok.push_back(rc.url_ok);
-    auto it = attrset_ids.find(rc.attrset);
-    if (it == attrset_ids.end()) {
-      it = attrset_ids.emplace(rc.attrset, (uint32_t)hb->attrsets.size()).first;
-      hb->attrsets.push_back(rc.attrset);
-    }
-    hb->res_attrset.push_back(it->second);
-    hb->res_size.push_back((uint32_t)sizer.resource_fixed(rs));
-    for (auto& ss : rs.scope_spans) {
-      hb->scope_size.push_back((uint32_t)sizer.scope_fixed(ss));
-      hb->scope_resource.push_back((uint32_t)ri);
-      for (auto& sp : ss.spans) {
-        columnize_span(ctx_, sp, rc.attr_res, sizer, sc);
-        hb->trace_id.push_back(sc.hi);
-        hb->trace_id.push_back(sc.lo);
-        hb->start.push_back(sc.start);
-        hb->end.push_back(sc.end);
-        hb->status.push_back(sc.status);
-        hb->kind.push_back(sc.kind);
-        hb->resource.push_back((uint32_t)ri);
-        hb->scope.push_back(scope_idx);
-        hb->span_size.push_back(sc.span_size);
-        hb->name_len.push_back(sc.name_len);
-        hb->attr_match.insert(hb->attr_match.end(), sc.attr_match.begin(), sc.attr_match.end());   // span-major here
-        for (size_t k = 0; k < nk; k++) {
-          uint64_t v = sc.attr_val[k];
-          if (sc.attr_type[k] == OSE_ATTR_STR) {
-            const ose_strref r = add_str(sc.attr_str[k]);
-            v = (uint64_t)r.off | ((uint64_t)r.len << 32);
-          }
-          attr_cols[k].first.push_back(sc.attr_type[k]);
-          attr_cols[k].second.push_back(v);
-        }
-        hb->route.push_back(sc.has_route ? add_str(sc.route) : ose_strref{0, 0});
-        hb->url_flags.push_back(sc.url_flags);
-        hb->path.push_back((sc.url_flags & OSE_URL_PATH_MASK) != OSE_URL_PATH_NONE ? add_str(sc.path) : ose_strref{0, 0});
-      }
-      scope_idx++;
-    }
+  if (keep_copy) hb->td = td;
+  const Traces& t = keep_copy ? hb->td : td;
+  const size_t R = t.resource_spans.size();
+  std::vector<uint64_t> span0(R + 1, 0), scope0(R + 1, 0);
+  for (size_t ri = 0; ri < R; ri++) {
+    uint64_t ns = 0;
+    for (auto& ss : t.resource_spans[ri].scope_spans) ns += ss.spans.size();
+    span0[ri + 1] = span0[ri] + ns;
+    scope0[ri + 1] = scope0[ri] + t.resource_spans[ri].scope_spans.size();
   }
-  size_t n = hb->kind.size();
-  hb->arena.assign(arena.begin(), arena.end());
-  hb->arena.resize(((arena.size() + 15) / 16) * 16 + 16, 0);
+  const size_t N = span0[R], S = scope0[R];
+  const size_t nk = ctx_.attr_plan.keys.size(), W = std::max<size_t>(1, (ctx_.attr_preds.size() + 63) / 64);
+  hb->trace_id.resize(2 * N);
+  hb->start.resize(N);
+  hb->end.resize(N);
+  hb->status.resize(N);
+  hb->kind.resize(N);
+  hb->resource.resize(N);
+  hb->scope.resize(N);
+  hb->span_size.resize(N);
+  hb->name_len.resize(N);
+  hb->url_flags.resize(N);
+  hb->path.resize(N);
+  hb->route.resize(N);
+  hb->attr_match.assign(W * N, 0);   // word-major (ose_columns.attr_match_words)
+  hb->attr_words = (uint32_t)W;
+  hb->attr_type.resize(nk * N);      // key-major
+  hb->attr_val.resize(nk * N);
+  hb->res_svc.resize(R);
+  hb->res_svc_str.resize(R);
+  hb->res_url_ok.resize(R);
+  hb->res_attrset.resize(R);
+  hb->res_size.resize(R);
+  hb->scope_size.resize(S);
+  hb->scope_resource.resize(S);
+  using AttrSet = std::vector<std::pair<std::string, std::string>>;
+  struct Range {
+    size_t r0 = 0, r1 = 0;
+    std::string arena;
+    std::vector<AttrSet> sets;       // local first-appearance order
+    std::map<AttrSet, uint32_t> ids;
+  };
+  // ranges of about equal span counts; one range below a few thousand spans
+  const int width = N >= 4096 ? std::min<int>(parallel_width(), (int)std::min<size_t>(R, N / 2048)) : 1;
+  const int nr = std::max(1, width);
+  std::vector<Range> rg((size_t)nr);
+  for (int k = 0, ri = 0; k < nr; k++) {
+    rg[k].r0 = (size_t)ri;
+    const uint64_t goal = N * (uint64_t)(k + 1) / (uint64_t)nr;
+    while ((size_t)ri < R && (span0[ri + 1] <= goal || k == nr - 1)) ri++;
+    rg[k].r1 = (size_t)ri;
+  }
+  auto fill = [&](int k) {
+    Range& g = rg[(size_t)k];
+    ProtoSizer sizer;
+    SpanCols sc;
+    auto add_str = [&](std::string_view v) {
+      ose_strref r{(uint32_t)g.arena.size(), (uint32_t)v.size()};
+      g.arena.append(v.data(), v.size());
+      return r;
+    };
+    for (size_t ri = g.r0; ri < g.r1; ri++) {
+      const ResourceSpans& rs = t.resource_spans[ri];
+      const ResourceCols rc = columnize_resource(ctx_, rs.resource_attrs);
+      hb->res_svc[ri] = rc.svc;
+      hb->res_svc_str[ri] = rc.svc_str;
+      hb->res_url_ok[ri] = rc.url_ok;
+      auto it = g.ids.find(rc.attrset);
+      if (it == g.ids.end()) {
+        it = g.ids.emplace(rc.attrset, (uint32_t)g.sets.size()).first;
+        g.sets.push_back(rc.attrset);
+      }
+      hb->res_attrset[ri] = it->second;   // local id until the merge
+      hb->res_size[ri] = (uint32_t)sizer.resource_fixed(rs);
+      uint64_t i = span0[ri], sidx = scope0[ri];
+      for (auto& ss : rs.scope_spans) {
+        hb->scope_size[sidx] = (uint32_t)sizer.scope_fixed(ss);
+        hb->scope_resource[sidx] = (uint32_t)ri;
+        for (auto& sp : ss.spans) {
+          columnize_span(ctx_, sp, rc.attr_res, sizer, sc);
+          hb->trace_id[2 * i] = sc.hi;
+          hb->trace_id[2 * i + 1] = sc.lo;
+          hb->start[i] = sc.start;
+          hb->end[i] = sc.end;
+          hb->status[i] = sc.status;
+          hb->kind[i] = sc.kind;
+          hb->resource[i] = (uint32_t)ri;
+          hb->scope[i] = (uint32_t)sidx;
+          hb->span_size[i] = sc.span_size;
+          hb->name_len[i] = sc.name_len;
+          for (size_t w = 0; w < W && w < sc.attr_match.size(); w++) hb->attr_match[w * N + i] = sc.attr_match[w];
+          for (size_t q = 0; q < nk; q++) {
+            uint64_t v = sc.attr_val[q];
+            if (sc.attr_type[q] == OSE_ATTR_STR) {
+              const ose_strref r = add_str(sc.attr_str[q]);
+              v = (uint64_t)r.off | ((uint64_t)r.len << 32);
+            }
+            hb->attr_type[q * N + i] = sc.attr_type[q];
+            hb->attr_val[q * N + i] = v;
+          }
+          // absent strings: {~0, 0} until the merge makes them {0, 0} (a
+          // present empty string keeps its place, as in a sequential walk)
+          hb->route[i] = sc.has_route ? add_str(sc.route) : ose_strref{~0u, 0};
+          hb->url_flags[i] = sc.url_flags;
+          hb->path[i] = (sc.url_flags & OSE_URL_PATH_MASK) != OSE_URL_PATH_NONE ? add_str(sc.path) : ose_strref{~0u, 0};
+          i++;
+        }
+        sidx++;
+      }
+    }
+  };
+  if (nr > 1) parallel_run(nr, fill);
+  else fill(0);
+  // merge: attribute sets in first-appearance order, arenas concatenated
+  std::map<AttrSet, uint32_t> gid;
+  std::vector<uint64_t> abase((size_t)nr + 1, 0);
+  std::vector<std::vector<uint32_t>> remap((size_t)nr);
+  for (int k = 0; k < nr; k++) {
+    for (auto& set : rg[k].sets) {
+      auto it = gid.find(set);
+      if (it == gid.end()) {
+        it = gid.emplace(set, (uint32_t)hb->attrsets.size()).first;
+        hb->attrsets.push_back(set);
+      }
+      remap[k].push_back(it->second);
+    }
+    abase[k + 1] = abase[k] + rg[k].arena.size();
+  }
+  const size_t abytes = abase[nr];
+  hb->arena.resize(((abytes + 15) / 16) * 16 + 16, 0);
+  auto place = [&](int k) {
+    Range& g = rg[(size_t)k];
+    if (!g.arena.empty()) std::memcpy(hb->arena.data() + abase[k], g.arena.data(), g.arena.size());
+    for (size_t ri = g.r0; ri < g.r1; ri++) hb->res_attrset[ri] = remap[k][hb->res_attrset[ri]];
+    const uint32_t base = (uint32_t)abase[k];
+    for (uint64_t i = span0[g.r0]; i < span0[g.r1]; i++) {
+      ose_strref& rt = hb->route[i];
+      rt = rt.off == ~0u ? ose_strref{0, 0} : ose_strref{rt.off + base, rt.len};
+      ose_strref& pt = hb->path[i];
+      pt = pt.off == ~0u ? ose_strref{0, 0} : ose_strref{pt.off + base, pt.len};
+      if (base)
+        for (size_t q = 0; q < nk; q++)
+          if (hb->attr_type[q * N + i] == OSE_ATTR_STR) hb->attr_val[q * N + i] += base;   // off in the low half
+    }
+  };
+  if (nr > 1) parallel_run(nr, place);
+  else place(0);
+  const std::string_view arena(reinterpret_cast<const char*>(hb->arena.data()), abytes);
+  size_t n = N;
   hb->cols.n_spans = n;
-  hb->cols.n_resources = (uint32_t)t.resource_spans.size();
-  hb->cols.n_scopes = scope_idx;
+  hb->cols.n_resources = (uint32_t)R;
+  hb->cols.n_scopes = (uint32_t)S;
   hb->cols.n_attrsets = (uint32_t)hb->attrsets.size();
   hb->cols.arena_bytes = arena.size();
-  hb->cols.n_attr_keys = (uint32_t)attr_cols.size();
-  for (auto& kc : attr_cols) {   // key-major
-    hb->attr_type.insert(hb->attr_type.end(), kc.first.begin(), kc.first.end());
-    hb->attr_val.insert(hb->attr_val.end(), kc.second.begin(), kc.second.end());
-  }
+  hb->cols.n_attr_keys = (uint32_t)nk;
   if (hb->attr_type.empty()) hb->attr_type.push_back(0), hb->attr_val.push_back(0);
   // outputs (vectors never empty so data() is non-null)
   size_t nn = std::max<size_t>(n, 1);
@@ -227,17 +322,6 @@ std::unique_ptr<HostBatch> TracesProcessor::Columnarize(const Traces& td) const 
     if (v->empty()) v->push_back(0);
   for (auto* v : {&hb->status, &hb->kind, &hb->url_flags, &hb->res_url_ok})
     if (v->empty()) v->push_back(0);
-  {
-    // attr_match: span-major while built, word-major in the columns (ose_columns.attr_match_words)
-    const size_t n = hb->start.size(), W = std::max<size_t>(1, (ctx_.attr_preds.size() + 63) / 64);
-    if (W > 1) {
-      std::vector<uint64_t> t(n * W);
-      for (size_t i = 0; i < n; i++)
-        for (size_t w = 0; w < W; w++) t[w * n + i] = hb->attr_match[i * W + w];
-      hb->attr_match.swap(t);
-    }
-    hb->attr_words = (uint32_t)W;
-  }
   for (auto* v : {&hb->trace_id, &hb->start, &hb->end, &hb->attr_match})
     if (v->empty()) v->push_back(0);
   if (hb->path.empty()) hb->path.push_back(ose_strref{0, 0});
@@ -252,50 +336,101 @@ void TracesProcessor::Apply(HostBatch& hb, Traces& td) {
   // odigossampling: drop the spans of unsampled traces.  With one trace per
   // call (OSE_GROUP_BATCH) this is exactly ResourceSpans().RemoveIf(true)
   // (processor.go:23-25); per trace_id, emptied scopes/resources go too.
-  std::vector<uint8_t> keep;
+  // Resources are independent: ranges of them are applied in parallel on the
+  // host task pool for a large batch (as Columnarize fills them).
   const bool sampled = st & OSE_STAGE_SAMPLE;
-  if (sampled) keep.assign(o.keep, o.keep + hb.cols.n_spans);
-  size_t i = 0;
-  for (auto& rs : td.resource_spans) {
-    for (auto& ss : rs.scope_spans) {
-      for (auto& sp : ss.spans) {
-        bool kept = !sampled || keep[i];
-        if (kept && (st & OSE_STAGE_TEMPLATE) && o.url_out[i]) {
-          std::string tmpl(reinterpret_cast<const char*>(o.tmpl_arena) + o.tmpl[i].off, o.tmpl[i].len);
-          if (o.url_out[i] & OSE_OUT_SET_ATTR)
-            sp.attrs.PutStr(sp.kind == OSE_KIND_CLIENT ? "url.template" : "http.route", tmpl);   // processor.go:259
-          if (o.url_out[i] & OSE_OUT_RENAME) {
-            const Value* m = sp.attrs.Get("http.request.method");
-            if (!m) m = sp.attrs.Get("http.method");
-            sp.name = (m ? m->AsString() : std::string()) + " " + tmpl;   // processor.go:230-232
+  const bool by_trace = sampled && group_mode != OSE_GROUP_BATCH;
+  const size_t R = td.resource_spans.size();
+  std::vector<uint64_t> span0(R + 1, 0);
+  for (size_t ri = 0; ri < R; ri++) {
+    uint64_t ns = 0;
+    for (auto& ss : td.resource_spans[ri].scope_spans) ns += ss.spans.size();
+    span0[ri + 1] = span0[ri] + ns;
+  }
+  const uint64_t N = span0[R];
+  std::vector<uint8_t> drop_res(R, 0);
+  auto apply_range = [&](size_t r0, size_t r1) {
+    for (size_t ri = r0; ri < r1; ri++) {
+      ResourceSpans& rs = td.resource_spans[ri];
+      uint64_t i = span0[ri];
+      bool had = false;
+      uint64_t empty_before = 0;   // scopes (first 64) that had no spans before the removal
+      bool many_scopes = rs.scope_spans.size() > 64;
+      std::vector<uint8_t> empty_v;
+      if (many_scopes) empty_v.assign(rs.scope_spans.size(), 0);
+      for (size_t si = 0; si < rs.scope_spans.size(); si++) {
+        ScopeSpans& ss = rs.scope_spans[si];
+        const bool shad = !ss.spans.empty();
+        had |= shad;
+        if (!shad) {
+          if (many_scopes) empty_v[si] = 1;
+          else empty_before |= 1ull << si;
+        }
+        size_t w = 0;
+        for (size_t q = 0; q < ss.spans.size(); q++, i++) {
+          Span& sp = ss.spans[q];
+          const bool kept = !sampled || o.keep[i];
+          if (kept && (st & OSE_STAGE_TEMPLATE) && o.url_out[i]) {
+            const std::string tmpl(reinterpret_cast<const char*>(o.tmpl_arena) + o.tmpl[i].off, o.tmpl[i].len);
+            if (o.url_out[i] & OSE_OUT_SET_ATTR)
+              sp.attrs.PutStr(sp.kind == OSE_KIND_CLIENT ? "url.template" : "http.route", tmpl);   // processor.go:259
+            if (o.url_out[i] & OSE_OUT_RENAME) {
+              const Value* m = sp.attrs.Get("http.request.method");
+              if (!m) m = sp.attrs.Get("http.method");
+              sp.name = (m ? m->AsString() : std::string()) + " " + tmpl;   // processor.go:230-232
+            }
+          }
+          if (by_trace) {   // RemoveIf, keeping order
+            if (kept) {
+              if (w != q) ss.spans[w] = std::move(sp);
+              w++;
+            }
           }
         }
-        i++;
+        if (by_trace) ss.spans.resize(w);
+      }
+      if (by_trace) {
+        size_t w = 0;
+        for (size_t q = 0; q < rs.scope_spans.size(); q++) {
+          ScopeSpans& ss = rs.scope_spans[q];
+          // an emptied scope goes; a scope that never had spans stays
+          const bool was_empty = many_scopes ? empty_v[q] != 0 : ((empty_before >> q) & 1) != 0;
+          const bool keep_scope = !ss.spans.empty() || was_empty;
+          if (keep_scope) {
+            if (w != q) rs.scope_spans[w] = std::move(ss);
+            w++;
+          }
+        }
+        rs.scope_spans.resize(w);
+        if (had && rs.scope_spans.empty()) drop_res[ri] = 1;
       }
     }
+  };
+  const int nr = N >= 4096 ? std::max(1, std::min<int>(parallel_width(), (int)std::min<uint64_t>(R, N / 2048))) : 1;
+  if (nr > 1) {
+    std::vector<size_t> cut((size_t)nr + 1, R);
+    cut[0] = 0;
+    for (int k = 1, ri = 0; k < nr; k++) {
+      const uint64_t goal = N * (uint64_t)k / (uint64_t)nr;
+      while ((size_t)ri < R && span0[ri + 1] <= goal) ri++;
+      cut[k] = (size_t)ri;
+    }
+    parallel_run(nr, [&](int k) { apply_range(cut[k], cut[k + 1]); });
+  } else {
+    apply_range(0, R);
   }
   if (sampled) {
     if (group_mode == OSE_GROUP_BATCH) {
       // one decision for the whole call, spanless resources included
       if (!o.trace_keep[0]) td.resource_spans.clear();
     } else {
-      size_t k = 0;
-      std::vector<ResourceSpans> rout;
-      for (auto& rs : td.resource_spans) {
-        bool had = false;
-        std::vector<ScopeSpans> sout;
-        for (auto& ss : rs.scope_spans) {
-          bool shad = !ss.spans.empty();
-          had |= shad;
-          std::vector<Span> kept;
-          for (auto& sp : ss.spans) { if (keep[k]) kept.push_back(std::move(sp)); k++; }
-          ss.spans = std::move(kept);
-          if (!shad || !ss.spans.empty()) sout.push_back(std::move(ss));
-        }
-        rs.scope_spans = std::move(sout);
-        if (!had || !rs.scope_spans.empty()) rout.push_back(std::move(rs));
+      size_t w = 0;
+      for (size_t ri = 0; ri < R; ri++) {
+        if (drop_res[ri]) continue;
+        if (w != ri) td.resource_spans[w] = std::move(td.resource_spans[ri]);
+        w++;
       }
-      td.resource_spans = std::move(rout);
+      td.resource_spans.resize(w);
     }
   }
   if (st & OSE_STAGE_SIZE) {
@@ -489,7 +624,7 @@ int osehost_consume(void* p, const char* traces_json, char** out) {
 void* osehost_columnarize(void* p, const char* traces_json) {
   auto* tp = static_cast<TracesProcessor*>(p);
   try {
-    return tp->Columnarize(traces_from_json(parse_json(traces_json))).release();
+    return tp->Columnarize(traces_from_json(parse_json(traces_json)), true).release();   // osehost_apply reads the copy
   } catch (const std::exception& e) {
     g_host_err = e.what();
     return nullptr;

@@ -72,7 +72,7 @@ class TracesProcessor {
   // in columnarise / pinned fill / ose_process / read-back / apply.
   int ProcessTraces(Traces& td, double* phase_s = nullptr);
   // test seams: the same steps without the device
-  std::unique_ptr<HostBatch> Columnarize(const Traces& td) const;
+  std::unique_ptr<HostBatch> Columnarize(const Traces& td, bool keep_copy = false) const;
   void Apply(HostBatch& hb, Traces& td);
   std::string MetricsJson() const;
   void set_seed(uint64_t s) { seed_ = s; }

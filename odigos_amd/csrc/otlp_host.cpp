@@ -1400,7 +1400,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   std::vector<uint64_t> fix_attr((size_t)cnt * AW);
   std::string strs;   // appended after the message bytes
   const size_t str_base = pb_cap;
-  auto put = [&](const std::string& s) {
+  auto put = [&](std::string_view s) {
     ose_strref r{(uint32_t)(str_base + strs.size()), (uint32_t)s.size()};
     strs += s;
     return r;

@@ -117,6 +117,35 @@ def consume_leg(ptype: str, cfg: dict, group_mode: int, items: list[dict], threa
             "phase_us_per_call": {k: v / calls * 1e6 for k, v in ph.items()}}
 
 
+def batch_parity(cfg: dict, items: list[dict], seed: int = 0x0D16B0B0) -> bool:
+    """ConsumeTraces on the device path against the CPU oracle on the same
+    batches: each item through a fresh pipeline processor (its first call
+    samples with `seed`), and through the host seam (columnarize -> the
+    oracle chain -> apply); the resulting traces must be equal (test
+    infrastructure: the oracle only checks)."""
+    from odigos_amd import host, native
+    from tests.oracle_lib import SamplingOracle, UrlOracle, size_process
+    stages = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE
+    for td in items:
+        ref = host.Processor("pipeline", cfg)
+        ref.configure(seed, native.GROUP_TRACE_ID)
+        hb = ref.columnarize(td)
+        o = hb.outs
+        assert SamplingOracle(cfg["odigossampling"]).process(hb.cols, o, native.GROUP_TRACE_ID, seed) == 0
+        assert UrlOracle(cfg["odigosurltemplate"]).process(hb.cols, o) == 0
+        assert size_process(hb.cols, o, stages, native.GROUP_TRACE_ID, o, 1, 1.0, 0.0) == 0
+        want = hb.apply()
+        p = host.Processor("pipeline", cfg)
+        p.configure(seed, native.GROUP_TRACE_ID)
+        got = p.consume(td)
+        ok = got == want
+        p.close()
+        ref.close()
+        if not ok:
+            return False
+    return True
+
+
 def process_leg(n_spans: int, reps: int, threads: int) -> dict:
     from odigos_amd import native
     from odigos_amd.batch import Engine, Generator, PinnedBatch
@@ -179,6 +208,7 @@ def main():
     ap.add_argument("--batches", type=int, default=16)
     ap.add_argument("--process-spans", default="1000000,10000000,50000000")
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--batch-only", action="store_true", help="only the 8192-span pipeline leg (and its parity)")
     args = ap.parse_args()
     sys.path.insert(0, str(ROOT))
     from bench import NODE_KEYS, cpu_share
@@ -186,20 +216,22 @@ def main():
     res = {"metric": "drop-in ConsumeTraces end to end (C ABI, pinned H2D + kernels + D2H + apply)",
            "host_cpu": model, "cpu_share": share, "nproc": nproc}
     t = time.perf_counter()
-    pt = per_trace_items(args.traces, 0x0D16D001)
+    pt = per_trace_items(args.traces, 0x0D16D001) if not args.batch_only else []
     res["consume_per_trace"] = []
-    for th in ((1, 8) if args.quick else (1, 8, 16)):
+    for th in (() if args.batch_only else (1, 8) if args.quick else (1, 8, 16)):
         res["consume_per_trace"].append(consume_leg("odigossampling", c3_sampling_config(), native.GROUP_BATCH, pt, th, 2))
         print(f"per-trace threads={th} {time.perf_counter() - t:.1f}s {res['consume_per_trace'][-1]}", flush=True)
     pipe = {"odigossampling": c3_sampling_config(), "odigosurltemplate": {},
             "odigostrafficmetrics": {"res_attributes_keys": NODE_KEYS}}
     bi = batch_items(args.batches, 8192, 0x0D16D002)
+    res["consume_batch_parity_vs_oracle"] = batch_parity(pipe, bi[:2])
+    print(f"batch parity {res['consume_batch_parity_vs_oracle']}", flush=True)
     res["consume_batch"] = []
     for th in (1, 8):
         res["consume_batch"].append(consume_leg("pipeline", pipe, native.GROUP_TRACE_ID, bi, th, 2))
         print(f"batch threads={th} {time.perf_counter() - t:.1f}s {res['consume_batch'][-1]}", flush=True)
     res["process_pinned"] = []
-    for n in args.process_spans.split(","):
+    for n in ([] if args.batch_only else args.process_spans.split(",")):
         if n:
             res["process_pinned"].append(process_leg(int(n), 3, max(1, min(16, share))))
             print(f"process {n} {time.perf_counter() - t:.1f}s {res['process_pinned'][-1]}", flush=True)
