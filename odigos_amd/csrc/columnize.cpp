@@ -123,9 +123,39 @@ void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uin
       default: o.attr_type[k] = OSE_ATTR_OTHER; break;
     }
   }
-  const AttrMap& a = sp.attrs;
+  // the keys the processors read, picked up in one pass over the span's
+  // attributes (each the first of its key, as pcommon.Map.Get finds it)
+  const Value *route = nullptr, *method = nullptr, *method_old = nullptr, *url_tmpl = nullptr, *url_path = nullptr,
+              *target = nullptr, *url_full = nullptr, *http_url = nullptr;
+  auto first = [](const Value*& slot, const Value& v) {
+    if (!slot) slot = &v;
+  };
+  for (auto& e : sp.attrs.kv) {
+    const std::string& k = e.first;
+    switch (k.size()) {
+      case 8:
+        if (k == "url.path") first(url_path, e.second);
+        else if (k == "url.full") first(url_full, e.second);
+        else if (k == "http.url") first(http_url, e.second);
+        break;
+      case 10:
+        if (k == "http.route") first(route, e.second);
+        break;
+      case 11:
+        if (k == "http.method") first(method_old, e.second);
+        else if (k == "http.target") first(target, e.second);
+        break;
+      case 12:
+        if (k == "url.template") first(url_tmpl, e.second);
+        break;
+      case 19:
+        if (k == "http.request.method") first(method, e.second);
+        break;
+      default:
+        break;
+    }
+  }
   // sampling: AsString(http.route) (latency.go:64-68)
-  const Value* route = a.Get("http.route");
   o.has_route = route != nullptr;
   if (route && route->type == Value::TStr) {
     o.route = route->s;
@@ -141,25 +171,22 @@ void columnize_span(const ColumnizeCtx& c, const Span& sp, const std::vector<uin
   // urltemplate (processor.go:98-147, 235-287)
   uint8_t f = 0;
   o.path = std::string_view();
-  const Value* m = a.Get("http.request.method");
-  if (!m) m = a.Get("http.method");
+  const Value* m = method ? method : method_old;
   if (m) {
     f |= OSE_URL_HAS_METHOD;
-    if (sp.name == m->AsString()) f |= OSE_URL_NAME_EQ_METHOD;
-    const char* tkey = sp.kind == OSE_KIND_CLIENT ? "url.template" : "http.route";
-    if (const Value* tv = a.Get(tkey)) {
+    if (m->type == Value::TStr ? sp.name == m->s : sp.name == m->AsString()) f |= OSE_URL_NAME_EQ_METHOD;
+    if (const Value* tv = sp.kind == OSE_KIND_CLIENT ? url_tmpl : route) {
       if (tv->type != Value::TStr) f |= OSE_URL_TGT_NONSTR;
       else f |= tv->s.empty() ? OSE_URL_TGT_STR_EMPTY : OSE_URL_TGT_STR;
     }
-    if (const Value* p = a.Get("url.path")) {
+    if (const Value* p = url_path) {
       f |= OSE_URL_PATH_RAW;
       o.path = as_view(p);
-    } else if (const Value* p = a.Get("http.target")) {
+    } else if (const Value* p = target) {
       f |= OSE_URL_PATH_TARGET;
       o.path = as_view(p);
     } else {
-      const Value* fu = a.Get("url.full");
-      if (!fu) fu = a.Get("http.url");
+      const Value* fu = url_full ? url_full : http_url;
       std::string path;
       if (fu && go_url_parse_path(fu->AsString(), path)) {
         f |= OSE_URL_PATH_RAW;

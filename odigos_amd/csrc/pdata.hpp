@@ -8,6 +8,7 @@
 #include <array>
 #include <cstdint>
 #include <string>
+#include <string_view>
 #include <utility>
 #include <vector>
 
@@ -39,15 +40,19 @@ struct Value {
 // appends.
 struct AttrMap {
   std::vector<KV> kv;
-  const Value* Get(const std::string& k) const {
+  const Value* Get(std::string_view k) const {
     for (auto& e : kv)
       if (e.first == k) return &e.second;
     return nullptr;
   }
-  void PutStr(const std::string& k, const std::string& v) {
+  void PutStr(std::string_view k, std::string_view v) {
     for (auto& e : kv)
-      if (e.first == k) { e.second = Value::str(v); return; }
-    kv.emplace_back(k, Value::str(v));
+      if (e.first == k) {
+        if (e.second.type == Value::TStr) e.second.s.assign(v.data(), v.size());   // the string's buffer reused
+        else e.second = Value::str(std::string(v));
+        return;
+      }
+    kv.emplace_back(std::string(k), Value::str(std::string(v)));
   }
 };
 

@@ -1592,7 +1592,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
           scr_used = 0;
           scr_end = avail;
         } else {
-          fast = false;   // the arena is full: the scan flags the overflow
+          // the arena is full for this group: hand the chunk back when no
+          // wave has reserved after it (the bump still ends at this chunk),
+          // so the space stays for the groups the scan places; otherwise the
+          // scan counts it up to out_cap
+          if (lane == 0) atomicCAS((unsigned long long*)a.bump, (unsigned long long)(at + csz), (unsigned long long)at);
+          fast = false;
           exhausted = true;
         }
       } else {
