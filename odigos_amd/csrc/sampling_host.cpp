@@ -481,7 +481,10 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
                                            4 * e->service_ids.size() + 4 * 64, 16));
   }
   a.long_steps = kLongSteps;
-  a.win_per_wave = kWinPerWave;
+  // kWinPerWave windows per wave on large batches; a small one (the drop-in's
+  // 8192-span calls: 128 windows) spreads over at least ~4096 waves, one
+  // window each, instead of 8 waves walking 16 windows each (112 us -> ~)
+  a.win_per_wave = (uint32_t)std::min<uint64_t>(kWinPerWave, std::max<uint64_t>(1, a.n_windows / 4096));
   {
     // the error bit, the endpoint bits and the service (+ span_attribute)
     // bits in one word: trace_eval_kernel's kNarrow instance (C4 trace_eval
