@@ -279,9 +279,10 @@ typedef struct ose_batch ose_batch;
  * services + span_attribute rules, 12 KiB) runs as one trace-stage pass per
  * chunk of the list with the same decisions (an http_route longer than a
  * table: a chunk of its own, its bytes past the LDS copy read from HBM);
- * OSE_ENOTSUP remains for jsonpath filters / scripts, regexps whose DFA
- * exceeds 65279 states, and per-service tables over 12 KiB (about a
- * thousand distinct service names among the sampling rules).               */
+ * more than about 500 distinct service names among the rules: each chunk
+ * indexes its own rules' services (ose_shard_pack / ose_shard_decide then
+ * return OSE_ENOTSUP).  OSE_ENOTSUP remains for regexps whose DFA exceeds
+ * 65279 states.                                                             */
 int ose_engine_create(const char* cfg_json, ose_engine** out);
 /* The engine's batches (ose_batch, ose_otlp_batch, ose_otlp_out, ose_gbt)
  * may be released before or after this call: each holds a reference, and

@@ -155,6 +155,8 @@ Engine::~Engine() {
   if (url_blob_dev) (void)hipFree(url_blob_dev);
   for (auto* d : sampling_chunks_dev)
     if (d) (void)hipFree(d);   // (sampling_blob_dev is the first)
+  for (auto* d : sampling_svc_map_dev)
+    if (d) (void)hipFree(d);
   if (shard_tables_dev) (void)hipFree(shard_tables_dev);
   if (attr_blob_dev) (void)hipFree(attr_blob_dev);
   if (attr_host_mask_dev) (void)hipFree(attr_host_mask_dev);
@@ -167,6 +169,7 @@ Engine::~Engine() {
     if (w->run_count) (void)hipFree(w->run_count);
     if (w->attr_bits) (void)hipFree(w->attr_bits);
     if (w->ep_planes) (void)hipFree(w->ep_planes);
+    if (w->svc_local) (void)hipFree(w->svc_local);
     for (void* f : w->fold)
       if (f) (void)hipFree(f);
     if (w->pending) (void)hipEventDestroy(w->pending);
@@ -652,6 +655,14 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
       if (rc) { delete e; return rc; }
     }
     e->sampling_blob_dev = e->sampling_chunks_dev[0];
+    e->sampling_svc_map_dev.assign(e->sampling_svc_map_host.size(), nullptr);
+    for (size_t k = 0; k < e->sampling_svc_map_host.size(); k++) {
+      const auto& m = e->sampling_svc_map_host[k];
+      std::vector<uint8_t> raw(reinterpret_cast<const uint8_t*>(m.data()),
+                               reinterpret_cast<const uint8_t*>(m.data()) + 4 * m.size());
+      rc = upload(raw, reinterpret_cast<uint8_t**>(&e->sampling_svc_map_dev[k]));
+      if (rc) { delete e; return rc; }
+    }
     const size_t K = e->sampling_chunks_dev.size(), L = e->sampling_lat_svc.size();
     // then trace_multi_kernel's latency-service ids: [n_services] the index of
     // each service among those with http_latency rules in any chunk (or

@@ -84,6 +84,13 @@ struct Workspace {
   // SAMPLE stage's host-gated tail reads them after run_sampling returned,
   // so they live with the workspace the call holds, not on its stack
   ose_columns spill_cols{};
+  // chunk-local service ids of the resources (Engine::sampling_local_svc):
+  // res_svc then res_svc_str, 2 * svc_local_cap words, and the columns that
+  // point at them
+  uint32_t* svc_local = nullptr;
+  uint64_t svc_local_cap = 0;
+  ose_columns local_cols{};
+  int reserve_svc_local(uint64_t n_resources);
   int reserve_ep_planes(uint64_t words);
   // SAMPLE + TEMPLATE in one call: the fast path's dup flag is copied here and
   // read by the host after the URL launches are queued (run_stages), so the
@@ -138,6 +145,15 @@ struct Engine {
   // trace stage and the pack then take every chunk's endpoint bits as
   // precomputed planes (spill_endpoint_planes)
   bool sampling_spill = false;
+  // more interned services than one chunk's dense service tables (12 B per
+  // service) fit beside its rules in the LDS budget: each chunk's tables then
+  // index chunk-local ids (the services its rules name, n_services of its
+  // SampCfgDev), and the trace stage translates the resources' service ids
+  // for each chunk's pass (svc_translate_kernel; the trace kernels are
+  // unchanged).  Map: [chunk][global id] -> local id or 0xFFFFFFFF.
+  bool sampling_local_svc = false;
+  std::vector<std::vector<uint32_t>> sampling_svc_map_host;
+  std::vector<uint32_t*> sampling_svc_map_dev;
   // span_attribute rules: all of them (attr_n_rules), the GPU-evaluated ones
   // (attr_n_dev, attr_kernel.hip) and the keys those read
   std::vector<uint8_t> attr_blob_host;

@@ -399,6 +399,9 @@ void launch_owner_fold(const OwnerArgs& a, hipStream_t st);
 void launch_scatter_keep(const uint8_t* back, const uint32_t* pos, uint64_t n, uint8_t* keep, hipStream_t st);
 // endpoint bits of every span under one rule chunk's tables in HBM (a chunk
 // whose route bytes spill past the LDS copy): out[j] for span j
+// out[r] = map[in[r]] (0xFFFFFFFF for ids >= n_global), for res_svc and res_svc_str
+void launch_svc_translate(const uint32_t* map, uint32_t n_global, const uint32_t* in1, const uint32_t* in2, uint32_t* out1,
+                          uint32_t* out2, uint64_t n, hipStream_t st);
 void launch_endpoint_plane(const uint8_t* cfg, const uint32_t* resource, const uint32_t* res_svc, const ose_strref* route,
                            const uint8_t* arena, uint64_t n, uint64_t* out, hipStream_t st);
 // the in-process transport's pieces of one phase, moved by one launch

@@ -200,18 +200,38 @@ int Engine::build_sampling_tables() {
       sampling_lat_svc[s >> 5] |= 1u << (s & 31);
     }
   // greedy: extend the chunk while its tables fit (a rule that alone does not
-  // fit: its route bytes or the service tables exceed kSampCfgLds)
+  // fit: its route bytes or the service tables exceed kSampCfgLds).  The
+  // service tables are dense over every interned id while that fits beside a
+  // rule; past it (about a thousand services) each chunk indexes the
+  // services its own rules name (sampling_local_svc).
+  sampling_svc_map_host.clear();
+  sampling_local_svc = service_ids.size() * 12 > kSampCfgLds / 2;
+  // a chunk's local ids: its rules' services in first-appearance order
+  auto local_ids = [&](const std::vector<PickedRule>& cur) {
+    std::unordered_map<std::string, uint32_t> loc;
+    for (const PickedRule& pr : cur) {
+      const std::string* nm = pr.r->rtype == RuleType::HttpLatency   ? &pr.r->latency.service_name
+                              : pr.r->rtype == RuleType::ServiceName ? &pr.r->service.service_name
+                                                                     : nullptr;
+      if (nm) loc.emplace(*nm, (uint32_t)loc.size());
+    }
+    return loc;
+  };
+  auto blob_of = [&](const std::vector<PickedRule>& cur, std::vector<uint8_t>& b, bool& a, bool spill) {
+    return sampling_local_svc ? build_sampling_blob(local_ids(cur), cur, b, a, spill)
+                              : build_sampling_blob(service_ids, cur, b, a, spill);
+  };
   size_t k = 0;
   do {
     std::vector<PickedRule> cur;
     std::vector<uint8_t> fitted, blob;
     bool fitted_attr = false, attr = false;
-    if (build_sampling_blob(service_ids, cur, fitted, fitted_attr))
+    if (blob_of(cur, fitted, fitted_attr, false))
       return fail(OSE_ENOTSUP, "odigossampling service tables exceed " + std::to_string(kSampCfgLds) +
                                    " bytes (the GPU trace stage keeps them in LDS): too many distinct service names");
     for (; k < all.size(); k++) {
       cur.push_back(all[k]);
-      if (build_sampling_blob(service_ids, cur, blob, attr)) {
+      if (blob_of(cur, blob, attr, false)) {
         cur.pop_back();
         break;
       }
@@ -222,10 +242,19 @@ int Engine::build_sampling_tables() {
       // one rule whose http_route alone overflows the LDS table: its own
       // chunk, the route bytes past kSampCfgLds read from HBM by the kernels
       cur.push_back(all[k]);
-      if (build_sampling_blob(service_ids, cur, fitted, fitted_attr, true))
+      if (blob_of(cur, fitted, fitted_attr, true))
         return fail(OSE_ENOTSUP, "odigossampling rule tables exceed " + std::to_string(kSampCfgLds) +
                                      " bytes before their route bytes (the GPU trace stage keeps them in LDS)");
       k++;
+    }
+    if (sampling_local_svc) {
+      const auto loc = local_ids(cur);
+      std::vector<uint32_t> map(std::max<size_t>(service_ids.size(), 1), 0xFFFFFFFFu);
+      for (const auto& kv : service_ids) {
+        auto it = loc.find(kv.first);
+        if (it != loc.end()) map[kv.second] = it->second;
+      }
+      sampling_svc_map_host.push_back(std::move(map));
     }
     sampling_chunks_host.push_back(std::move(fitted));
     sampling_chunk_attr.push_back(fitted_attr ? 1 : 0);
@@ -323,6 +352,9 @@ int Workspace::reserve_fold(uint64_t n_spans) {
   return 0;
 }
 
+int local_service_ids(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, uint32_t chunk,
+                      const uint32_t** out);
+
 namespace {
 // LDS bytes of every chunk's table (trace_multi_kernel's copy)
 uint32_t multi_cfg_bytes(const Engine* e) {
@@ -340,6 +372,7 @@ uint32_t multi_cfg_bytes(const Engine* e) {
 bool multi_pass(const Engine* e, const ose_columns* c, uint32_t group_mode) {
   const size_t K = e->sampling_chunks_host.size();
   return K >= 2 && K <= kMaxMulti && group_mode == OSE_GROUP_TRACE_ID && c->n_spans && !e->sampling_n_attr &&
+         !e->sampling_local_svc &&
          e->sampling_n_lat_svc <= 64 && e->sampling_walk_ok &&
          !e->sampling_spill && !c->route_match && !c->svc_match && multi_cfg_bytes(e) <= kMultiCfgLds;
 }
@@ -435,6 +468,13 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   a.arena = c->arena;
   a.res_svc = c->res_svc;
   a.res_svc_str = c->res_svc_str;
+  if (e->sampling_local_svc && c->n_resources && c->res_svc && c->res_svc_str) {   // this chunk's service ids
+    const uint32_t* loc = nullptr;
+    const int lr = local_service_ids(e, c, ws, st, chunk, &loc);
+    if (lr) return lr;
+    a.res_svc = loc;
+    a.res_svc_str = loc + ws->svc_local_cap;
+  }
   a.cfg = e->sampling_chunks_dev[chunk];
   a.fold_in = fold_in;
   a.fold_out = fold_out;
@@ -699,15 +739,44 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
 // table: the endpoint bits of every chunk are computed first from the tables
 // in HBM (endpoint_plane_kernel), and the trace stage / the pack take them as
 // route_match planes, so no kernel reads route bytes past its LDS copy.
+// Chunk-local service ids of the batch's resources for rule chunk `chunk`
+// (Engine::sampling_local_svc): out = res_svc, out + svc_local_cap =
+// res_svc_str, both translated through the chunk's map.
+int local_service_ids(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, uint32_t chunk,
+                      const uint32_t** out) {
+  const uint64_t R = c->n_resources;
+  int rc = ws->reserve_svc_local(std::max<uint64_t>(R, 1));
+  if (rc) return rc;
+  launch_svc_translate(e->sampling_svc_map_dev[chunk], (uint32_t)e->service_ids.size(), c->res_svc, c->res_svc_str,
+                       ws->svc_local, ws->svc_local + ws->svc_local_cap, R, st);
+  HIP_TRY(hipGetLastError());
+  *out = ws->svc_local;
+  return 0;
+}
+int Workspace::reserve_svc_local(uint64_t n_resources) {
+  if (svc_local && svc_local_cap >= n_resources) return 0;
+  if (svc_local) HIP_TRY(hipFree(svc_local));
+  svc_local = nullptr;
+  svc_local_cap = 0;
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&svc_local), 2 * n_resources * sizeof(uint32_t)));
+  svc_local_cap = n_resources;
+  return 0;
+}
+
 int spill_endpoint_planes(Engine* e, const ose_columns* c, Workspace* ws, hipStream_t st, const uint64_t** out) {
   const uint64_t n = c->n_spans, K = e->sampling_chunks_dev.size();
   if (!c->resource || !c->res_svc || !c->route || !c->arena)
     return fail(OSE_EINVAL, "http_latency rules need resource, res_svc, route and arena");
   int rc = ws->reserve_ep_planes(n * K);
   if (rc) return rc;
-  for (uint64_t k = 0; k < K; k++)
-    launch_endpoint_plane(e->sampling_chunks_dev[k], c->resource, c->res_svc, c->route, c->arena, n, ws->ep_planes + k * n,
-                          st);
+  for (uint64_t k = 0; k < K; k++) {
+    const uint32_t* sv = c->res_svc;
+    if (e->sampling_local_svc) {
+      rc = local_service_ids(e, c, ws, st, (uint32_t)k, &sv);
+      if (rc) return rc;
+    }
+    launch_endpoint_plane(e->sampling_chunks_dev[k], c->resource, sv, c->route, c->arena, n, ws->ep_planes + k * n, st);
+  }
   HIP_TRY(hipGetLastError());
   *out = ws->ep_planes;
   return 0;

@@ -543,6 +543,9 @@ uint32_t ose_shard_record_bytes(const ose_engine* eng) {
 
 int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void* send, uint64_t* counts,
                    uint32_t* pack_pos, void* hip_stream) {
+  if (eng && reinterpret_cast<Engine*>(eng)->sampling_local_svc)
+    return fail(OSE_ENOTSUP, "trace-id exchange: an odigossampling config naming more services than one rule table's "
+                             "dense service tables hold (chunk-local service ids run on one GPU only)");
   if (!eng || !c || !send || !counts || !pack_pos) return fail(OSE_EINVAL, "NULL argument");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_pack needs odigossampling on the engine");
@@ -675,6 +678,9 @@ int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t*
 
 int ose_shard_decide(ose_engine* eng, const void* recv, uint64_t n, uint32_t rec_bytes, uint8_t* keep,
                      uint32_t* device_status, const ose_rand* rnd, void* hip_stream) {
+  if (eng && reinterpret_cast<Engine*>(eng)->sampling_local_svc)
+    return fail(OSE_ENOTSUP, "trace-id exchange: an odigossampling config naming more services than one rule table's "
+                             "dense service tables hold (chunk-local service ids run on one GPU only)");
   if (!eng) return fail(OSE_EINVAL, "NULL engine");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_decide needs odigossampling on the engine");

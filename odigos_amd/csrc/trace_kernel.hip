@@ -2655,6 +2655,21 @@ __global__ __launch_bounds__(256) void trace_dup_check_kernel(TraceKernelArgs a)
   __syncthreads();
   if (threadIdx.x == 0 && found) atomicOr(a.dup, 1u);
 }
+// Chunk-local service ids (sampling_host.cpp local_service_ids)
+__global__ __launch_bounds__(256) void svc_translate_kernel(const uint32_t* map, uint32_t n_global, const uint32_t* in1,
+                                                            const uint32_t* in2, uint32_t* out1, uint32_t* out2,
+                                                            uint64_t n) {
+  const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t a = in1[r], b = in2[r];
+  out1[r] = a < n_global ? map[a] : 0xFFFFFFFFu;
+  out2[r] = b < n_global ? map[b] : 0xFFFFFFFFu;
+}
+void launch_svc_translate(const uint32_t* map, uint32_t n_global, const uint32_t* in1, const uint32_t* in2, uint32_t* out1,
+                          uint32_t* out2, uint64_t n, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(svc_translate_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, map, n_global, in1,
+                            in2, out1, out2, n);
+}
 void launch_trace_dup_check(const TraceKernelArgs& a, hipStream_t st) {
   if (a.dup_bkt) hipLaunchKernelGGL(trace_dup_check_kernel, dim3(1u << a.dup_bkt_bits), dim3(256), 0, st, a);
 }

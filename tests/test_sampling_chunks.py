@@ -21,11 +21,12 @@ from odigos_amd import native
 from odigos_amd.batch import Generator
 from tests.oracle_lib import intern_services, lib as orc_lib
 from tests.test_sampling_random import SEED, _arr, _group, _py_eval, gpu_vs_oracle, inject_zero_starts, oracle_run
-from tests.workloads import (check_interning, long_routes_config, wide_attr100_config, wide_attr_config,
-                             wide_latency2_config, wide_latency_config, wide_latency_split_config, wide_mixed_config)
+from tests.workloads import (check_interning, long_routes_config, many_services_config, wide_attr100_config,
+                             wide_attr_config, wide_latency2_config, wide_latency_config, wide_latency_split_config,
+                             wide_mixed_config)
 
 CONFIGS = {"latency": wide_latency_config, "latency2": wide_latency2_config, "latency_split": wide_latency_split_config,
-           "mixed": wide_mixed_config, "long_routes": long_routes_config}
+           "mixed": wide_mixed_config, "long_routes": long_routes_config, "many_services": many_services_config}
 
 
 def _chunks(cfg):
@@ -74,6 +75,11 @@ def test_chunk_refusals():
         assert L.osehost_sampling_chunks(json.dumps({"odigossampling": attr}).encode(), C.byref(n)) == 0
         assert n.value == (k + 63) // 64
     assert _chunks(wide_attr100_config()) == 3        # 40 service + 24 attr bits, 64 attr, 12 attr
+    # 1200 services: dense service tables (14.4 KB) no longer fit a chunk, so
+    # each chunk indexes the services its rules name (no refusal); 64
+    # service bits per chunk bound the count from below
+    for n in (600, 1200, 5000):
+        assert _chunks(many_services_config(n)) >= (n + 63) // 64
 
 
 LONG_PRE = "/" + "a" * 13000
@@ -347,6 +353,27 @@ def test_gpu_wide_config_exchange_world3(name):
     for gk, wk in zip(got, want):
         np.testing.assert_array_equal(gk, wk)
     assert sum(s[0] for s in stats) == sum(s[1] for s in stats) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 65, 5000])
+def test_gpu_many_services_batch_mode(n):
+    # one decision per call over chunk-local service ids (every resource's
+    # service, spanless ones included: servicename.go:38-47)
+    g = Generator("sampling", seed=0x0D160951 + n, n_spans=n)
+    gpu_vs_oracle(g, native.GROUP_BATCH, cfg=many_services_config())
+
+
+@pytest.mark.gpu
+def test_gpu_many_services_exchange_refused():
+    # the trace-id exchange keeps global service ids in its records: a config
+    # past the dense service tables is refused there, not decided wrongly
+    from tests.test_exchange import _local_round
+    sources = [Generator("sampling", seed=0x0D160961, n_spans=2000, rank=r, world=2) for r in range(2)]
+    with pytest.raises(AssertionError) as ei:   # _local_round asserts every rank returned 0
+        _local_round(sources, many_services_config())
+    msg = str(ei.value)
+    assert "(-95, " in msg and "trace-id exchange" in msg
 
 
 @pytest.mark.gpu

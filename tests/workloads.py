@@ -95,6 +95,19 @@ def wide_mixed_config():
             "endpoint_rules": [_wide_lat(200 + j, j % 64) for j in range(70)]}
 
 
+def many_services_config(n_services=1200):
+    """More distinct service names than dense per-service tables fit beside
+    a rule table in LDS (12 B per service): 64 global-level http_latency
+    rules over services 0..63, one service_name rule per service 0..n-1 (the
+    generator's batches hold ids < 64 only), 24 endpoint-level http_latency
+    rules over services 10..33.  Each rule chunk then indexes its own
+    services (chunk-local ids)."""
+    return {"global_rules": [{"name": "errors", "type": "error", "rule_details": {"fallback_sampling_ratio": 10}}]
+            + [_wide_lat(j, j) for j in range(64)],
+            "service_rules": [_wide_svc(k, k) for k in range(n_services)],
+            "endpoint_rules": [_wide_lat(300 + j, 10 + j) for j in range(24)]}
+
+
 def wide_attr_config():
     """span_attribute rules split over two rule chunks (their attr_match bits
     0..13 in the first, 14..39 in the second): 40 latency rules (services
