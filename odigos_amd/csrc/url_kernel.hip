@@ -1289,8 +1289,11 @@ __device__ __forceinline__ bool plan_group_list(const Cfg& cfg, lds_u32* stage32
   // id + 1 in 8 bits: 255 stands for every id >= 254 (such plans are `slow`
   // and re-classify their segments when emitted)
   auto put_cls = [&](uint32_t x, int id, uint32_t L) {
-    const uint32_t nl = cfg.names_tab_all ? (uint32_t)cfg.name_tab[id >= 0 ? id : 0].len
-                                          : (id >= 0 ? name_len(cfg, (uint32_t)id) : 0u);
+    // without custom ids a segment's id is a built-in name ("id", "date",
+    // "email": engine.cpp's name table): its length without an LDS read
+    const uint32_t nl = cfg.n_custom == 0 ? (id <= 0 ? 2u : id == 1 ? 4u : 5u)
+                        : cfg.names_tab_all ? (uint32_t)cfg.name_tab[id >= 0 ? id : 0].len
+                                            : (id >= 0 ? name_len(cfg, (uint32_t)id) : 0u);
     const uint32_t out = id >= 0 ? nl + 2 : L;
     cls[x] = (out << 8) | min((uint32_t)(id + 1), 255u);
   };
@@ -1394,7 +1397,7 @@ __device__ __forceinline__ uint32_t plan_gate(const PlanCols& c) {
 // path of the group.
 __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L, uint32_t stage_src, uint32_t* segs,
                                                uint32_t* cls, const BracedNames& bn, uint32_t bn_src,
-                                               const Plan& p, uint32_t seg_off, uint32_t local) {
+                                               const Plan& p, uint32_t seg_off, uint32_t local, bool builtin) {
   const int lane = threadIdx.x & 63;
   const uint32_t nseg = seg_off >> 16, off = seg_off & 0xFFFFu;
   const uint32_t pre = (p.lead || p.mode == M_ORIG) ? 1u : 0u;
@@ -1422,7 +1425,11 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       const int id = (int)(c & 0xFFu) - 1;
       // both candidates read unconditionally (a branch on id >= 0 cost the
       // step its exec-mask bookkeeping)
-      const uint32_t idc = id >= 0 ? (uint32_t)id : 0u, boff = bn.off[idc], blen = bn.len[idc];
+      // builtin (no custom ids): "{id}" "{date}" "{email}" at 4, 8 and 14 of
+      // the braced table (load_braced_names), no LDS read
+      const uint32_t idc = id >= 0 ? (uint32_t)id : 0u;
+      const uint32_t boff = builtin ? (idc == 0 ? 4u : idc == 1 ? 8u : 14u) : (uint32_t)bn.off[idc];
+      const uint32_t blen = builtin ? (idc == 0 ? 4u : idc == 1 ? 6u : 7u) : (uint32_t)bn.len[idc];
       const uint32_t so = id >= 0 ? bn_src + boff : stage_src + (ent & 0xFFFu);   // the body's LDS byte offset
       const uint32_t n = id >= 0 ? blen : (ent >> 12) & 0x1FFFu;
       if (slash) img[pos] = '/';
@@ -1618,7 +1625,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
       const uint32_t n16 = (uint32_t)(need / 16);
       if (!(a.ablate & 64))   // diagnostics: OSE_URL_ABLATE 64 skips the image writes (wrong output)
         assemble_group((lds_out_u8*)sm.bm[wv], L, (uint32_t)(stage - (uint8_t*)&sm), sm.segs[wv], sm.cls[wv], sm.bn,
-                       bn_src, p, seg_off, local);
+                       bn_src, p, seg_off, local, cfg.n_custom == 0);
       wave_lds_sync();
       uint4* dst = reinterpret_cast<uint4*>(a.scratch + region + scr_used);
       for (uint32_t k = lane; k < n16; k += kWave) {
