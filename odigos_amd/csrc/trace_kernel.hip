@@ -822,7 +822,9 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(4, 4)
     a.perm = nullptr;
     a.key = nullptr;
     a.batch_keep = nullptr;
-    a.ablate = 0;
+#if !OSE_DIAG
+    a.ablate = 0;   // (diagnostics builds keep OSE_TRACE_ABLATE for the lean instances too)
+#endif
     if (!kChunk) {
       a.fold_in = nullptr;
       a.fold_out = nullptr;
@@ -2603,7 +2605,7 @@ void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((trace_multi_kernel<3>), dim3(blocks), dim3(kTThreads), a.cfg_lds_bytes, st, a);
     return;
   }
-  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && !a.ablate) {
+  if (a.mode == kTraceRuns && !a.svc_match && !a.route_match && !a.attr_match && (OSE_DIAG || !a.ablate)) {
     const bool chunk = a.fold_in || a.fold_out;
     if (a.narrow && chunk)
       hipLaunchKernelGGL((trace_eval_kernel<true, true, true>), dim3(blocks), dim3(kTThreads), 0, st, a);

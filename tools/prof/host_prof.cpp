@@ -44,12 +44,23 @@ int main(int argc, char** argv) {
     auto b = clk::now();
     const uint64_t n = hb->cols.n_spans;
     spans += n;
+    // templates as long as the paths (the span's own path bytes, copied into
+    // the template arena: heap-sized strings like real templates), renames
+    // where the span's name is its method
+    size_t need = 16;
+    for (uint64_t i = 0; i < n; i++) need += hb->path[i].len;
+    if (hb->tmpl_arena.size() < need + 16) { hb->tmpl_arena.resize(need + 16); hb->bind(); }
+    uint32_t at = 0;
     for (uint64_t i = 0; i < n; i++) {
       hb->outs.keep[i] = (uint8_t)(((hb->trace_id[2 * i] >> 7) % keep_mod) == 0);
-      hb->outs.url_out[i] = (hb->url_flags[i] & OSE_URL_PATH_MASK) ? OSE_OUT_SET_ATTR : 0;
-      hb->outs.tmpl[i] = ose_strref{0, 7};
+      const bool has_path = (hb->url_flags[i] & OSE_URL_PATH_MASK) != 0;
+      hb->outs.url_out[i] = has_path ? (uint8_t)(OSE_OUT_SET_ATTR | ((hb->url_flags[i] & OSE_URL_NAME_EQ_METHOD) ? OSE_OUT_RENAME : 0)) : 0;
+      const ose_strref pr = hb->path[i];
+      if (pr.len) memcpy(hb->outs.tmpl_arena + at, hb->arena.data() + pr.off, pr.len);
+      hb->outs.tmpl[i] = has_path && pr.len ? ose_strref{at, pr.len} : ose_strref{0, 7};
+      at += pr.len;
     }
-    memcpy(hb->outs.tmpl_arena, tmpl, 7);
+    (void)tmpl;
     auto c = clk::now();
     tp.Apply(*hb, td);
     auto d = clk::now();
