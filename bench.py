@@ -59,7 +59,7 @@ MULTI_KERNELS = ("trace_multi_kernel", "trace_dup_check")   # rule-chunked lists
 # the repeated-trace-id paths, each timed as one span of launches (run lists,
 # then the sort path for traces that overflow them)
 SLOW_KERNELS = ("trace_run_list", "trace_sort_path")
-SIZE_KERNELS = ("size_span_kernel", "size_scope_kernel", "size_res_kernel")
+SIZE_KERNELS = ("size_span_kernel", "size_tail_kernel", "size_fix_kernel")
 PER_TRACE_OUTS = ("trace_count", "trace_first_span", "trace_keep", "trace_level", "trace_ratio")
 
 WORKLOADS = {

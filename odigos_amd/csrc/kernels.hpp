@@ -28,6 +28,11 @@ namespace ose {
 //                    copied from scratch to their place in the output arena
 //   url_emit_slow_kernel  the groups the plan kernel could not assemble (user
 //                    rules, oversized groups), from the plan arrays
+struct SizePart {            // one resource run's share of a 64-scope window
+  uint32_t r;                 // the resource
+  uint32_t ch;                // alive scopes (bits 0-29) | had spans << 30 | whole side << 31
+  uint64_t v;                 // framed scope bytes
+};
 struct SizeKernelArgs {
   uint64_t n_spans;
   uint32_t n_scopes, n_resources, n_attrsets;
@@ -48,13 +53,17 @@ struct SizeKernelArgs {
   const ose_strref* tmpl;
   int64_t inverse;
   uint64_t* scope_body;       // [S] zeroed: body bytes | runs that added << kSumBits (size_device.hpp)
-  uint64_t* res_body;         // [R] zeroed: body bytes | alive scopes << kSumBits
-  uint32_t* res_had;          // [R] zeroed
+  // the fused scopes + resources pass (size_tail_kernel): per 64-scope window
+  // its first and last resource run's partial sums, and whether the window
+  // holds the end of a run that began in an earlier window (size_fix_kernel)
+  SizePart* parts;            // [2 * n_swin], written every call
+  uint32_t* fix;              // [n_swin], written every call
+  uint32_t n_swin;            // ceil(n_scopes / 64)
   int64_t* attrset_bytes;     // [n_attrsets] added to
   int64_t* accepted;          // [1] added to
   uint64_t* res_bytes;        // [R] or null
   // the spans pass ran fused in url_copy_kernel: the surviving spans counted
-  // per block there, summed by size_res_kernel (null: size_span_kernel counted)
+  // per block there, summed by size_tail_kernel (null: size_span_kernel counted)
   const uint32_t* kept_partials;
   uint32_t n_kept_partials;
 };
@@ -424,8 +433,11 @@ constexpr uint32_t kBatchKeepWord = 16;   // OSE_GROUP_BATCH decision of the SAM
 // resources, each a wave-segmented reduction (the columns are in pdata
 // order, so scope and resource indices are non-decreasing).
 void launch_size_spans(const SizeKernelArgs& a, hipStream_t st);
-void launch_size_scopes(const SizeKernelArgs& a, hipStream_t st);
-void launch_size_resources(const SizeKernelArgs& a, hipStream_t st);
+// scopes and resources in one pass (size_tail_kernel: every resource whose
+// scopes lie in one 64-scope window is finished there), then the resources
+// whose scopes span windows (size_fix_kernel)
+void launch_size_tail(const SizeKernelArgs& a, hipStream_t st);
+void launch_size_fix(const SizeKernelArgs& a, hipStream_t st);
 
 // span_attribute conditions (attr_kernel.hip): out[i] = host_bits[i] &
 // host_mask | the bits of the GPU-evaluated rules the span meets.

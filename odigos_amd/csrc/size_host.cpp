@@ -17,9 +17,26 @@ namespace {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 }  // namespace
 
+// [256 | scope sums 8·S | window parts 32·W | window fix flags 4·W | kept
+// partials 4·kUrlCopyMaxBlocks | 256], W = the 64-scope windows
+namespace {
+struct SizeLayout {
+  size_t scope, parts, fix, partials, end;
+};
+SizeLayout size_layout(uint64_t n_scopes) {
+  const uint64_t W = (std::max<uint64_t>(n_scopes, 1) + 63) / 64;
+  SizeLayout L;
+  L.scope = 256;
+  L.parts = align_up(L.scope + 8 * std::max<uint64_t>(n_scopes, 1), 256);
+  L.fix = align_up(L.parts + 32 * W, 256);
+  L.partials = align_up(L.fix + 4 * W, 256);
+  L.end = align_up(L.partials + 4ull * kUrlCopyMaxBlocks, 256) + 256;
+  return L;
+}
+}  // namespace
 size_t size_scratch_bytes(uint64_t n_scopes, uint64_t n_resources) {
-  return align_up(256 + 16 * std::max<uint64_t>(n_scopes, 1), 256) + align_up(16 * std::max<uint64_t>(n_resources, 1), 256) +
-         align_up(4ull * kUrlCopyMaxBlocks, 256) + 256;
+  (void)n_resources;   // the resources are finished in the scopes pass (no per-resource words)
+  return size_layout(n_scopes).end;
 }
 
 // dataSizesMetricsProcessor.processTraces (odigostrafficmetrics/
@@ -48,15 +65,16 @@ int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   const double ratio = e->traffic.sampling_ratio;
   const double u = rnd ? rnd->traffic_u : 0.0;
   if (!(ratio != 0 && u < ratio)) return 0;
-  // res_bytes needs no clearing: size_res_kernel writes every entry, zeros
-  // when the batch was dropped
+  // res_bytes needs no clearing: size_tail_kernel / size_fix_kernel write
+  // every entry, zeros when the batch was dropped; the window parts and flags
+  // are written every call
   const uint64_t S = c->n_scopes, R = c->n_resources;
   int rc = ws->reserve(off + size_scratch_bytes(S, R));
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(ws->dev) + off;
-  uint8_t* sc = base + 256;
-  uint8_t* rs = base + align_up(256 + 16 * std::max<uint64_t>(S, 1), 256);
-  HIP_TRY(hipMemsetAsync(sc, 0, (size_t)(rs - sc) + 16 * std::max<uint64_t>(R, 1), st));   // scope and resource sums
+  const SizeLayout L = size_layout(S);
+  uint8_t* sc = base + L.scope;
+  HIP_TRY(hipMemsetAsync(sc, 0, 8 * std::max<uint64_t>(S, 1), st));   // scope sums
   a = SizeKernelArgs{};
   a.n_spans = n;
   a.n_scopes = (uint32_t)S;
@@ -80,8 +98,9 @@ int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
   a.tmpl = o->tmpl;
   a.inverse = e->inverse;
   a.scope_body = reinterpret_cast<uint64_t*>(sc);
-  a.res_body = reinterpret_cast<uint64_t*>(rs);
-  a.res_had = reinterpret_cast<uint32_t*>(rs + 12 * R);
+  a.parts = reinterpret_cast<SizePart*>(base + L.parts);
+  a.fix = reinterpret_cast<uint32_t*>(base + L.fix);
+  a.n_swin = (uint32_t)((S + 63) / 64);
   a.attrset_bytes = o->attrset_bytes;
   a.accepted = o->accepted_spans;
   a.res_bytes = o->res_bytes;
@@ -92,9 +111,8 @@ int prepare_size(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t
 }
 
 uint32_t* size_partials_of(Workspace* ws, size_t off, uint64_t n_scopes, uint64_t n_resources) {
-  uint8_t* base = static_cast<uint8_t*>(ws->dev) + off;
-  uint8_t* rs = base + align_up(256 + 16 * std::max<uint64_t>(n_scopes, 1), 256);
-  return reinterpret_cast<uint32_t*>(rs + align_up(16 * std::max<uint64_t>(n_resources, 1), 256));
+  (void)n_resources;
+  return reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws->dev) + off + size_layout(n_scopes).partials);
 }
 
 // the spans pass (unless url_copy_kernel ran it: a.kept_partials set), then
@@ -107,12 +125,12 @@ int run_size_tail(Engine* e, const SizeKernelArgs& a, hipStream_t st) {
     HIP_TRY(hipGetLastError());
     e->prof_end(tm, st);
   }
-  e->prof_begin("size_scope_kernel", st, tm);
-  launch_size_scopes(a, st);
+  e->prof_begin("size_tail_kernel", st, tm);
+  launch_size_tail(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
-  e->prof_begin("size_res_kernel", st, tm);
-  launch_size_resources(a, st);
+  e->prof_begin("size_fix_kernel", st, tm);
+  launch_size_fix(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
   return 0;

@@ -153,6 +153,43 @@ def main():
     res["batch8192_legs_ms_median"] = {k: sorted(x[j] for x in leg)[len(leg) // 2]
                                        for j, k in enumerate(("decode", "stages", "encode"))}
     res["batch8192_decode_phases_ms_median"] = {k: sorted(x[k] for x in sph[20:])[len(sph[20:]) // 2] for k in sph[0]}
+    # the same 8192-span request from several callers at once (a receiver's
+    # concurrent export requests): one stream and one set of outputs per
+    # caller, the engine and router shared; whole-job spans/s
+    import threading
+    for callers in (1, 4, 8):
+        per = 120
+        ready = threading.Barrier(callers + 1)
+        errs = []
+
+        def caller(k):
+            try:
+                cs = torch.cuda.Stream()
+                ch = cs.cuda_stream
+                co = device_outputs(sdims, tmpl_cap=64 * 8192)
+                ready.wait()
+                for _ in range(per):
+                    ob = OtlpBatch(eng, spin.p, stream=ch, length=spin.n, outputs=co)
+                    eng.process_device(ob, st, native.GROUP_TRACE_ID, seed=0x5EED, stream=ch)
+                    ob.encode(st, native.GROUP_TRACE_ID, router, stream=ch, copy=False)
+                    ob.close()
+                cs.synchronize()
+            except Exception as ex:   # pragma: no cover
+                errs.append(repr(ex))
+
+        th = [threading.Thread(target=caller, args=(k,)) for k in range(callers)]
+        for t_ in th:
+            t_.start()
+        ready.wait()
+        a = time.perf_counter()
+        for t_ in th:
+            t_.join()
+        wall = time.perf_counter() - a
+        assert not errs, errs
+        res.setdefault("batch8192_callers", []).append(
+            {"callers": callers, "calls": callers * per, "wall_s": wall,
+             "spans_per_s": callers * per * 8192 / wall, "calls_per_s": callers * per / wall})
+        print(f"otlp 8192-span calls, {callers} callers: {callers * per * 8192 / wall / 1e6:.1f} M spans/s", flush=True)
     spin.close()
     pin.close()
     line = json.dumps(res)
