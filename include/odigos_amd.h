@@ -282,7 +282,7 @@ typedef struct ose_batch ose_batch;
  * more than about 500 distinct service names among the rules: each chunk
  * indexes its own rules' services (ose_shard_pack / ose_shard_decide then
  * return OSE_ENOTSUP).  OSE_ENOTSUP remains for regexps whose DFA exceeds
- * 65279 states.                                                             */
+ * about two million states (or 256 MiB of transitions).                     */
 int ose_engine_create(const char* cfg_json, ose_engine** out);
 /* The engine's batches (ose_batch, ose_otlp_batch, ose_otlp_out, ose_gbt)
  * may be released before or after this call: each holds a reference, and

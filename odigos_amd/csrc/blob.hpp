@@ -35,11 +35,19 @@ inline uint32_t put_dfa(Blob& bl, const Dfa& d) {
   h.match = d.match;
   h.hi_n = (uint32_t)d.hi_lo.size();
   std::memcpy(h.ascii, d.ascii_class, 128);
+  h.wide = d.nstates > 65535 ? 1u : 0u;
   uint32_t off = bl.put(&h, 1);
   std::vector<uint32_t> hr;
   for (size_t k = 0; k < d.hi_lo.size(); k++) { hr.push_back(d.hi_lo[k]); hr.push_back(d.hi_hi[k]); hr.push_back(d.hi_cls[k]); }
   uint32_t hoff = bl.put(hr.data(), hr.size());
-  uint32_t toff = bl.put(d.trans.data(), d.trans.size());
+  h.wide = d.nstates > 65535 ? 1u : 0u;
+  uint32_t toff;
+  if (h.wide) {
+    toff = bl.put(d.trans.data(), d.trans.size());
+  } else {
+    std::vector<uint16_t> t16(d.trans.begin(), d.trans.end());
+    toff = bl.put(t16.data(), t16.size());
+  }
   uint32_t aoff = bl.put(d.accept_end.data(), d.accept_end.size());
   DfaDev* hp = bl.at<DfaDev>(off);
   hp->hi_off = hoff;

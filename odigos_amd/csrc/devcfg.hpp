@@ -11,8 +11,9 @@ struct DfaDev {
   uint32_t nclasses, nstates, start, match;
   uint32_t hi_n;        // number of non-ASCII ranges
   uint32_t hi_off;      // uint32 triplets {lo, hi, cls}
-  uint32_t trans_off;   // uint16 [nstates][nclasses]
+  uint32_t trans_off;   // [nstates][nclasses]: uint16, or uint32 when wide
   uint32_t acc_off;     // uint8  [nstates]
+  uint32_t wide;        // more than 65535 states: uint32 state ids
   uint8_t ascii[128];   // class of runes 0..127
 };
 

@@ -272,6 +272,8 @@ template <class Reader>
 __device__ inline bool dfa_match(const uint8_t* blob, uint32_t dfa_off, Reader& rd, uint32_t s, uint32_t e) {
   const DfaDev* d = reinterpret_cast<const DfaDev*>(blob + dfa_off);
   const uint16_t* trans = reinterpret_cast<const uint16_t*>(blob + d->trans_off);
+  const uint32_t* trans32 = reinterpret_cast<const uint32_t*>(blob + d->trans_off);
+  const bool wide = d->wide != 0;
   const uint32_t ncls = d->nclasses, match = d->match;
   uint32_t st = d->start;
   uint32_t i = s;
@@ -294,7 +296,7 @@ __device__ inline bool dfa_match(const uint8_t* blob, uint32_t dfa_off, Reader& 
         else { cls = hr[3 * m + 2]; break; }
       }
     }
-    st = trans[st * ncls + cls];
+    st = wide ? trans32[st * ncls + cls] : (uint32_t)trans[st * ncls + cls];
   }
   const uint8_t* acc = blob + d->acc_off;
   return st == match || acc[st];

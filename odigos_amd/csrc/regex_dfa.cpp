@@ -789,15 +789,19 @@ RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) 
     return id;
   };
   uint32_t start = intern(Key{{}, kTypeBot});
-  std::vector<uint16_t> trans;
+  std::vector<uint32_t> trans;
   std::vector<uint8_t> acc_end;
   trans.resize(ncls);  // row for MATCH
   for (uint32_t c = 0; c < ncls; c++) trans[c] = kMatch;
   acc_end.push_back(1);
   for (uint32_t s = 1; s < states.size(); s++) {
-    if (states.size() > Dfa::kMaxStates) { err = "regexp DFA exceeds " + std::to_string(Dfa::kMaxStates) + " states"; return RegexStatus::TooLarge; }
+    if (states.size() > Dfa::kMaxStates || (uint64_t)states.size() * ncls * 4 > Dfa::kMaxTableBytes) {
+      err = "regexp DFA exceeds " + std::to_string(Dfa::kMaxStates) + " states or " +
+            std::to_string(Dfa::kMaxTableBytes >> 20) + " MiB of transitions";
+      return RegexStatus::TooLarge;
+    }
     Key cur = states[s];
-    std::vector<uint16_t> row(ncls);
+    std::vector<uint32_t> row(ncls);
     for (uint32_t c = 0; c < ncls; c++) {
       std::vector<int> set = cur.set;
       set.push_back(nfa.start);
@@ -812,7 +816,7 @@ RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) 
       std::sort(next.begin(), next.end());
       next.erase(std::unique(next.begin(), next.end()), next.end());
       uint32_t t = intern(Key{std::move(next), cls_type[c]});
-      row[c] = (uint16_t)t;
+      row[c] = t;
     }
     trans.insert(trans.end(), row.begin(), row.end());
     {

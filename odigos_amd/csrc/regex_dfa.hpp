@@ -16,7 +16,8 @@
 // any rune use unicode_tables.cpp (generated from ICU 70: Unicode 14.0.0
 // data; the reference's Go 1.25 has 15.0.0: the code points assigned in 15.0
 // are parity unpinned).
-// Unsupported (rejected, never approximated): DFAs above kMaxStates.
+// Unsupported (rejected, never approximated): DFAs above kMaxStates (about
+// two million states) or kMaxTableBytes of transitions.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -30,9 +31,12 @@ enum class RegexStatus { Ok, Syntax, Unsupported, TooLarge };
 RegexStatus regex_syntax_check(const std::string& pattern, std::string& err);
 
 struct Dfa {
-  // state ids are uint16: the cap leaves room for the states one more row
-  // can add (at most 256 classes) after the last check (compile_dfa)
-  static constexpr uint32_t kMaxStates = 65535 - 256;
+  // state ids: uint16 on the device up to 65535 states, uint32 beyond
+  // (DfaDev::wide); the cap bounds the subset construction's time and the
+  // table (kMaxTableBytes), with room for the states one more row can add
+  // (at most 256 classes) after the last check (compile_dfa)
+  static constexpr uint32_t kMaxStates = (1u << 21) - 256;
+  static constexpr uint64_t kMaxTableBytes = 256ull << 20;
   uint8_t ascii_class[128];               // class of runes 0..127
   std::vector<uint32_t> hi_lo, hi_hi;     // non-ASCII rune ranges [lo,hi] ...
   std::vector<uint8_t> hi_cls;            // ... and their class (sorted by lo)
@@ -40,7 +44,7 @@ struct Dfa {
   uint32_t nstates = 0;
   uint32_t start = 0;
   uint32_t match = 0;                     // absorbing "matched" state
-  std::vector<uint16_t> trans;            // [nstates][nclasses]
+  std::vector<uint32_t> trans;            // [nstates][nclasses]
   std::vector<uint8_t> accept_end;        // state accepts at end of text
 };
 

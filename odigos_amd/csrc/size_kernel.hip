@@ -63,13 +63,12 @@ __global__ __launch_bounds__(kSThreads) void size_span_kernel(SizeKernelArgs a) 
 // emptied resource is removed, into res_bytes and, times inverse, into its
 // attribute set's sum (LDS when the sets fit, else global).
 __device__ __forceinline__ void size_finish_res(const SizeKernelArgs& a, unsigned long long* hist, bool lds, uint32_t r,
-                                                uint64_t body, uint32_t alive, bool had) {
+                                                uint64_t body, uint32_t alive, bool had, uint32_t rsz, uint32_t set) {
   const bool removed = a.remove_empty && had && alive == 0;   // no alive scope left
-  const uint64_t size = removed ? 0 : (uint64_t)a.res_size[r] + body;
+  const uint64_t size = removed ? 0 : (uint64_t)rsz + body;
   if (a.res_bytes) a.res_bytes[r] = size;
   if (removed) return;
   const long long add = (long long)size * a.inverse;
-  const uint32_t set = a.res_attrset[r];
   if (lds) atomicAdd(&hist[set], (unsigned long long)add);
   else atomicAdd((unsigned long long*)&a.attrset_bytes[set], (unsigned long long)add);
 }
@@ -104,7 +103,7 @@ __global__ __launch_bounds__(kSThreads) void size_tail_kernel(SizeKernelArgs a) 
   const uint32_t S = a.n_scopes, R = a.n_resources;
   if (S == 0) {   // no scopes: every resource keeps its fixed size
     for (uint64_t r = (uint64_t)blockIdx.x * kSThreads + threadIdx.x; r < R; r += gstride)
-      size_finish_res(a, hist, lds, (uint32_t)r, 0, 0, false);
+      size_finish_res(a, hist, lds, (uint32_t)r, 0, 0, false, a.res_size[r], a.res_attrset[r]);
   }
   for (uint64_t t0 = (uint64_t)blockIdx.x * kSThreads; t0 < S; t0 += gstride) {
     const uint64_t s = t0 + threadIdx.x;
@@ -121,6 +120,13 @@ __global__ __launch_bounds__(kSThreads) void size_tail_kernel(SizeKernelArgs a) 
       alive = !a.remove_empty || !had || body != 0;    // an emptied ScopeSpans is removed
       if (alive) contrib = field_len((uint64_t)a.scope_size[s] + body);
       if (lane == 0 && s > 0) nb = a.scope_resource[s - 1];
+    }
+    // the resource's fixed size and attribute set, read with the scope's
+    // columns (a run's tail lane finishes its own resource)
+    uint32_t rsz = 0, rset = 0;
+    if (valid) {
+      rsz = a.res_size[r];
+      rset = a.res_attrset[r];
     }
     const uint64_t vmask = __ballot(valid);            // window lanes [0, lastv]
     if (!vmask) continue;                              // a window past the last scope (wave-uniform)
@@ -147,14 +153,14 @@ __global__ __launch_bounds__(kSThreads) void size_tail_kernel(SizeKernelArgs a) 
     const bool single = end0 == lastv;
     // runs with a side outside the window: the first (head missing), the last (tail missing)
     const bool cut = tail && ((start == 0 && !whole_head) || (lane == lastv && !whole_tail));
-    if (tail && !cut) size_finish_res(a, hist, lds, r, v, c, h != 0);
+    if (tail && !cut) size_finish_res(a, hist, lds, r, v, c, h != 0, rsz, rset);
     if (valid && head) {
       // resources with no scope between the previous run's and this one
       const uint32_t prev = lane ? pr : (s0 == 0 ? 0xFFFFFFFFu : before);
-      for (uint32_t g = prev + 1; g < r; g++) size_finish_res(a, hist, lds, g, 0, 0, false);
+      for (uint32_t g = prev + 1; g < r; g++) size_finish_res(a, hist, lds, g, 0, 0, false, a.res_size[g], a.res_attrset[g]);
     }
     if (valid && s + 1 == S)   // resources after the last scope
-      for (uint32_t g = r + 1; g < R; g++) size_finish_res(a, hist, lds, g, 0, 0, false);
+      for (uint32_t g = r + 1; g < R; g++) size_finish_res(a, hist, lds, g, 0, 0, false, a.res_size[g], a.res_attrset[g]);
     // the window's part slots and fix flag
     const uint64_t w = s0 >> 6;
     const uint32_t ch0 = (uint32_t)__builtin_amdgcn_readlane((int)(c | (h << 30)), end0);
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(kSThreads) void size_fix_kernel(SizeKernelArgs a) {
     // window k is this run alone and the run began before it: keep walking
     if (fp.r != r || (fp.ch >> 31)) break;
   }
-  size_finish_res(a, nullptr, false, r, body, alive, had);
+  size_finish_res(a, nullptr, false, r, body, alive, had, a.res_size[r], a.res_attrset[r]);
 }
 }  // namespace
 
@@ -224,7 +230,10 @@ void launch_size_spans(const SizeKernelArgs& a, hipStream_t st) {
 void launch_size_tail(const SizeKernelArgs& a, hipStream_t st) {
   // grid-stride over 256-scope tiles (fewer per-block attribute-set flushes)
   uint64_t blocks = ((uint64_t)a.n_scopes + kSThreads - 1) / kSThreads;
-  if (blocks > 4096) blocks = 4096;
+#ifndef OSE_SIZE_TAIL_CAP
+#define OSE_SIZE_TAIL_CAP 4096
+#endif
+  if (blocks > OSE_SIZE_TAIL_CAP) blocks = OSE_SIZE_TAIL_CAP;
   if (a.kept_partials) blocks = std::max<uint64_t>(blocks, std::min<uint32_t>(64, (a.n_kept_partials + 4095) / 4096));
   if (!blocks && a.n_resources) blocks = std::min<uint64_t>(((uint64_t)a.n_resources + kSThreads - 1) / kSThreads, 1024);
   if (blocks) hipLaunchKernelGGL(size_tail_kernel, dim3((uint32_t)blocks), dim3(kSThreads), 0, st, a);

@@ -1,6 +1,7 @@
 """Regexps whose DFA has thousands of states (custom ids, templatization
-rules, span_attribute regex conditions): the DFA compiler takes up to 65279
-states (uint16 state ids), 4096 before round 4.  The DFA is checked against
+rules, span_attribute regex conditions): the DFA compiler takes up to about
+two million states (uint16 state ids up to 65535, uint32 beyond; 65279 in
+round 4, 4096 before).  The DFA is checked against
 the oracle's Pike VM (oracle/regex.c, no state bound) on the host and, on
 the GPU, through URL templatization against the oracle chain."""
 import ctypes as C
@@ -39,9 +40,19 @@ def test_large_dfa_vs_oracle(pattern):
         assert _dfa(pattern, b) == orc.match(b), (pattern, s)
 
 
+def test_wide_dfa_vs_oracle():
+    # 2^18 states: uint32 state ids (refused before round 5)
+    pattern = r"(a|b)*a(a|b){17}"
+    rng = random.Random(17)
+    orc = Regex(pattern)
+    for s in _ab_strings(rng, 12):
+        b = s.encode()
+        assert _dfa(pattern, b) == orc.match(b), (pattern, s)
+
+
 def test_dfa_state_bound_still_refuses():
-    # 2^18 states: past the uint16 state ids, refused (never approximated)
-    assert native.lib().osehost_regex_match(r"(a|b)*a(a|b){17}".encode(), b"ab", 2) == -2   # too large
+    # 2^22 states: past the state bound, refused (never approximated)
+    assert native.lib().osehost_regex_match(r"(a|b)*a(a|b){21}".encode(), b"ab", 2) == -2   # too large
 
 
 def test_engine_accepts_large_dfa_custom_id():
@@ -59,8 +70,15 @@ LARGE_URL_CFG = {
 }
 
 
+WIDE_URL_CFG = {
+    "custom_ids": [{"regexp": r"^(?:a|b)*a(?:a|b){16}$", "template_name": "ab"}],   # 2^17 states: uint32 ids
+    "templatization_rules": [r"/s/{seq:^[ab]*b[ab]{16}$}/{rest}"],
+}
+
+
 @pytest.mark.gpu
-def test_gpu_url_parity_large_dfa():
+@pytest.mark.parametrize("cfg", [LARGE_URL_CFG, WIDE_URL_CFG], ids=["uint16", "uint32"])
+def test_gpu_url_parity_large_dfa(cfg):
     import torch
     from odigos_amd.batch import DeviceBatch, Engine, HostOutputs
     from tests.oracle_lib import UrlOracle
@@ -72,12 +90,12 @@ def test_gpu_url_parity_large_dfa():
             segs = ["s"] + segs[:2]
         paths.append(("/" + "/".join(segs)).encode())
     cols, _keep = _cols_from_paths(paths)
-    eng = Engine({"odigosurltemplate": LARGE_URL_CFG})
+    eng = Engine({"odigosurltemplate": cfg})
     db = DeviceBatch(cols)
     eng.process_device(db, native.STAGE_TEMPLATE)
     torch.cuda.synchronize()
     ho = HostOutputs(cols)
-    assert UrlOracle(LARGE_URL_CFG).process(cols, ho.outs, 4) == 0
+    assert UrlOracle(cfg).process(cols, ho.outs, 4) == 0
     n = cols.n_spans
     np.testing.assert_array_equal(db.out_numpy("url_out", n=n), ho.view("url_out", np.uint8)[:n])
     used = db.used()

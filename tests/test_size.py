@@ -428,3 +428,57 @@ def test_reference_traffic_kat_gpu():
         proc.consume(_reference_case())
         ms.append(proc.metrics())
     _check_reference_metrics(ms[0], ms[1])
+
+
+def _window_edge_case(rng):
+    """Resources whose scopes cross 64-scope windows (one with 150 scopes,
+    some spanless), runs of spanless resources and scopes, a resource with no
+    scopes at the end: the fused scopes + resources pass's part slots, fix
+    walk and gap handling."""
+    def spans_of(k):
+        out = []
+        for _ in range(k):
+            tid = "%032x" % rng.choice([1, 2, 3, 4])
+            out.append(host.span(name="GET", kind=2, trace_id=tid, span_id="%016x" % rng.getrandbits(64),
+                                 start=1739000000000000000 + rng.randrange(10**9), end=1739000002000000000,
+                                 status=rng.choice([0, 2]),
+                                 attributes={"http.request.method": "GET", "url.path": "/user/%d" % rng.randrange(10**6)}))
+        return out
+    rss = []
+    for r in range(12):
+        n_sc = [150, 0, 3, 70, 0, 0, 1, 64, 2, 130, 1, 0][r]
+        scopes = [{"scope": {"name": "lib%d" % q}, "spans": spans_of(rng.choice([0, 0, 1, 2, 3]))} for q in range(n_sc)]
+        rss.append(host.resource_spans({"service.name": "svc-%02d" % (r % 8), "k8s.namespace.name": "ns%d" % (r % 2)},
+                                       scopes=scopes))
+    return host.traces(*rss)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [native.GROUP_TRACE_ID, native.GROUP_BATCH])
+def test_gpu_size_pipeline_cases_vs_oracle(mode):
+    # ConsumeTraces through all three processors on the GPU against the same
+    # calls through the oracle: spanless scopes and resources, emptied ones
+    # removed, resources whose scopes cross 64-scope windows
+    cfg = _pipeline_cfg()
+    stages = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE
+    rng = random.Random(7 + mode)
+    cases = [_pipeline_case(rng, k) for k in range(30)] + [_window_edge_case(rng) for _ in range(6)]
+    for case, td in enumerate(cases):
+        seed = 0x0D17 + case
+        ref = host.Processor("pipeline", cfg)
+        ref.configure(seed, mode)
+        hb = ref.columnarize(td)
+        o = hb.outs
+        assert SamplingOracle(cfg["odigossampling"]).process(hb.cols, o, mode, seed) == 0
+        assert UrlOracle({}).process(hb.cols, o) == 0
+        assert size_process(hb.cols, o, stages, mode, o, 1, 1.0, 0.0) == 0
+        want = hb.apply()
+        wm = ref.metrics()
+        ref.close()
+        p = host.Processor("pipeline", cfg)
+        p.configure(seed, mode)
+        got = p.consume(td)
+        gm = p.metrics()
+        p.close()
+        assert got == want, case
+        assert gm == wm, case
