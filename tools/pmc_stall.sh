@@ -12,4 +12,4 @@ for ctrs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d $R/gpurun_out/pmc3/p$i -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --spans $N > $R/gpurun_out/pmc3/p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $R/gpurun_out/pmc3/p$i.log; exit 1; }
 done
-for k in url_plan_kernel trace_eval_kernel url_copy_kernel size_span_kernel; do echo "== $k"; python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc3 $k; done
+for k in url_plan_kernel trace_eval_kernel url_copy_kernel size_tail_kernel; do echo "== $k"; python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc3 $k; done
