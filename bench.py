@@ -54,7 +54,7 @@ FUSED_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "kind", "re
                 "scope_resource")
 SAMPLE_FIELDS = ("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc", "res_svc_str")
 URL_KERNELS = ("url_plan_kernel", "url_plan_slow_kernel", "url_scan_kernel", "url_copy_kernel", "url_emit_slow_kernel")
-TRACE_KERNELS = ("trace_eval_kernel", "trace_dup_check", "trace_long_kernel")
+TRACE_KERNELS = ("trace_eval_kernel", "trace_dup_check", "trace_long_kernel")   # trace_long_kernel: its HIP-event bracket holds trace_long_plan_kernel too
 MULTI_KERNELS = ("trace_multi_kernel", "trace_dup_check")   # rule-chunked lists in one pass
 # the repeated-trace-id paths, each timed as one span of launches (run lists,
 # then the sort path for traces that overflow them)

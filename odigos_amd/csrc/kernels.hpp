@@ -229,8 +229,15 @@ struct TraceKernelArgs {
   uint32_t ablate;            // diagnostics only (OSE_TRACE_ABLATE, tools/ablate_trace.py): skip parts
   // kTraceRuns: runs still open kLongSteps steps past their owner's windows
   // are listed here (head positions) and decided by trace_long_kernel
-  uint32_t* n_long;
+  uint32_t* n_long;           // [0] runs listed, [1] pieces, [3] piece partials (trace_long_plan_kernel)
   uint32_t* long_runs;        // [n_spans / 64 + 1]
+  // trace_long_plan_kernel cuts each listed run into pieces of at most
+  // kLongPiece spans (one workgroup each): per run {end, pieces, first
+  // partial, pieces done}, per piece {run, index}, per piece of a run of
+  // several a partial (kLongPartBytes)
+  uint4* long_meta;           // [n_spans / 64 + 1]
+  uint2* long_pieces;         // [long_piece_cap(n_spans)]
+  uint8_t* long_part;         // [long_part_cap(n_spans)][kLongPartBytes]
   uint32_t long_steps;        // hand-off distance in 64-span steps (kLongSteps)
   uint32_t win_per_wave;      // 64-span windows whose run heads one wave owns (kWinPerWave)
   uint32_t narrow;            // the table's flag bits fit one word (trace_eval_kernel kNarrow)
@@ -254,6 +261,13 @@ constexpr uint32_t kMaxRuns = 8;          // runs per trace the run-list path fo
 constexpr uint32_t kMaxFoldSpans = 4096;  // spans per trace one lane folds
 constexpr uint32_t kMaxFoldSlots = 8;     // latency services per trace one lane folds
 constexpr uint32_t kWinPerWave = 16;   // tools/gpu_wpw.sh: C5 0.97 -> 0.83 ms, C3 2.03 -> 1.99 ms, C4 unchanged
+#ifndef OSE_LONG_PIECE
+#define OSE_LONG_PIECE 2048
+#endif
+constexpr uint32_t kLongPiece = OSE_LONG_PIECE;   // spans of a long run one wave folds
+constexpr uint32_t kLongPartBytes = 1344;    // a piece's partial: m[64], e[64], f[64], ep, svc, kmask, err
+inline uint64_t long_piece_cap(uint64_t n) { return n / 64 + 1 + n / kLongPiece + 1; }
+inline uint64_t long_part_cap(uint64_t n) { return 2 * (n / kLongPiece) + 2; }   // pieces of runs of > kLongPiece spans
 constexpr uint32_t kLongSteps = 4;   // tools/gpu_long_iter.sh: C5 16 -> 4 steps 2.75 -> 2.13 ms, C3 unchanged
 void launch_trace_eval(const TraceKernelArgs& a, hipStream_t st);
 // rule chunks one trace_multi_kernel pass evaluates, and their LDS budget

@@ -289,6 +289,9 @@ size_t sampling_scratch_bytes(uint64_t n) {
   s = align_up(s + 4 * 256 * T, 256);  // hist offsets
   s = align_up(s + 8 * htiles, 256);   // scan status (hist)
   s = align_up(s + 4 * (N / 64 + 1), 256);   // long runs
+  s = align_up(s + 16 * (N / 64 + 1), 256);  // long-run meta
+  s = align_up(s + 8 * long_piece_cap(N), 256);   // long-run pieces
+  s = align_up(s + (size_t)kLongPartBytes * long_part_cap(N), 256);   // piece partials
   s = align_up(s + 8 * W, 256);        // win_first (run-list path)
   return s + 256;
 }
@@ -427,7 +430,7 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     off = align_up(off + bytes, 256);
     return p;
   };
-  uint32_t* misc = reinterpret_cast<uint32_t*>(base);   // [0] dup, [2] scan counter (windows), [4] scan counter (hist), [12] long runs, [14] run-list overflow
+  uint32_t* misc = reinterpret_cast<uint32_t*>(base);   // [0] dup, [2] scan counter (windows), [4] scan counter (hist), [12] long runs, [13] their pieces, [14] run-list overflow, [15] piece partials
   uint64_t* win_heads = reinterpret_cast<uint64_t*>(take(8 * W));
   uint32_t* win_base = reinterpret_cast<uint32_t*>(take(4 * W));
   uint64_t* wstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)wtiles));
@@ -441,6 +444,9 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   uint32_t* hoff = reinterpret_cast<uint32_t*>(take(4 * 256 * T));
   uint64_t* hstatus = reinterpret_cast<uint64_t*>(take(8 * (size_t)htiles));
   uint32_t* long_runs = reinterpret_cast<uint32_t*>(take(4 * (N / 64 + 1)));
+  uint4* long_meta = reinterpret_cast<uint4*>(take(16 * (N / 64 + 1)));
+  uint2* long_pieces = reinterpret_cast<uint2*>(take(8 * long_piece_cap(N)));
+  uint8_t* long_part = take((size_t)kLongPartBytes * long_part_cap(N));
   uint64_t* win_first = reinterpret_cast<uint64_t*>(take(8 * W));
   if (off > need) return fail(OSE_EINVAL, "internal: trace workspace layout exceeds its bound");
   uint32_t* err = o->device_status ? o->device_status : misc + 8;
@@ -510,6 +516,9 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
 #endif
   a.n_long = misc + 12;
   a.long_runs = a.mode == kTraceRuns && !multi ? long_runs : nullptr;
+  a.long_meta = long_meta;
+  a.long_pieces = long_pieces;
+  a.long_part = long_part;
   if (multi) {   // every chunk in one pass (run_sampling checked the conditions)
     a.n_multi = multi;
     a.cfgs = reinterpret_cast<const uint8_t* const*>(e->shard_tables_dev);
@@ -564,7 +573,7 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   auto long_pass = [=](uint32_t known_runs) -> int {
     Engine::Timed tl{};
     e->prof_begin("trace_long_kernel", st, tl);
-    launch_trace_long(a, st, known_runs);
+    launch_trace_long(a, st, known_runs);   // (trace_long_plan_kernel, then the pieces)
     HIP_TRY(hipGetLastError());
     e->prof_end(tl, st);
     return 0;

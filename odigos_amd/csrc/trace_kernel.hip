@@ -1499,13 +1499,22 @@ __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(2, 4)
 
 // ---- long runs ------------------------------------------------------------------
 // A run the fast path listed (kTraceRuns; still open long_steps steps past
-// its owner's windows) is one trace: a workgroup finds its end from the
-// window head masks, its 8 waves fold contiguous 64-span-step pieces of it
-// (per-span contributions exactly as trace_eval_kernel computes them; the
-// latency monoid reduced in lane order, then piece order), wave 0 combines
-// the pieces and decides, and the workgroup writes the run's keep bytes.
-// Workgroups take the listed runs in turn (persistent grid).
-// the columns of one span of a long run (loaded one step ahead)
+// its owner's windows) is one trace.  Zipf run lengths put most of a batch's
+// spans in a few runs, so a run is not one workgroup's work (one workgroup
+// per run: C5 0.98 ms, most of it the few workgroups holding 50k-span runs):
+//  - trace_long_plan_kernel finds each run's end from the window head masks
+//    and cuts it into pieces of at most kLongPiece spans;
+//  - trace_long_kernel's waves take the pieces in turn, each on its own (no
+//    workgroup barrier): a piece's per-span contributions exactly as
+//    trace_eval_kernel computes them, the latency monoid reduced in lane
+//    order, then step order; a one-piece run is decided there, a piece of a
+//    longer run leaves its partial in long_part;
+//  - trace_long_decide_kernel combines each longer run's partials in piece
+//    order, decides, and writes the run's keep bytes.
+// The partials cross workgroups (and XCDs) through the kernel boundary: a
+// release / acquire pair per piece inside one kernel writes back the L2 each
+// time (2.8 ms at 1024-span pieces).  C5: 0.98 -> 0.66 ms (profiles/r5l_long_pieces.txt).
+// the columns of one span of a long run (loaded two steps ahead)
 struct LongRaw {
   uint32_t res, status;
   uint64_t st, en, am, rm, svm;
@@ -1526,21 +1535,111 @@ __device__ __forceinline__ LongRaw long_raw(const TraceKernelArgs& a, const Samp
   else if (a.route) r.rt = a.route[p];
   return r;
 }
+
+// one wave per listed run: its end (the first head after it), its pieces;
+// a workgroup's 16 runs take their piece and partial ranges with one atomic
+// each (per-wave atomics on two counters serialised 0.1 ms on C5)
+constexpr int kPlanWaves = 16;
+__global__ __launch_bounds__(kPlanWaves * kWave) void trace_long_plan_kernel(TraceKernelArgs a) {
+  __shared__ uint32_t s_np[kPlanWaves];
+  __shared__ uint32_t s_q, s_p;
+  const uint32_t nl = __hip_atomic_load(a.n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = threadIdx.x >> 6;
+  for (uint32_t r0 = blockIdx.x * kPlanWaves; r0 < nl; r0 += gridDim.x * kPlanWaves) {
+    const uint32_t r = r0 + wv;
+    uint64_t pos = 0, end = a.n_spans;
+    uint32_t np = 0;
+    if (r < nl) {
+      pos = a.long_runs[r];
+      const uint32_t w0 = (uint32_t)(pos / kWave);
+      const uint64_t m0 = a.win_heads[w0] & ~lanemask_le((int)(pos % kWave));
+      if (m0) {
+        end = (uint64_t)w0 * kWave + ffs64(m0);
+      } else {
+        for (uint64_t wb = (uint64_t)w0 + 1; wb < a.n_windows; wb += kWave) {
+          const uint64_t w = wb + lane;
+          const uint64_t h = w < a.n_windows ? a.win_heads[w] : 0ull;
+          const uint64_t b = __ballot(h != 0);
+          if (b) {
+            const int l = (int)ffs64(b);
+            end = (wb + l) * kWave + ffs64(rdl64(h, l));
+            break;
+          }
+        }
+      }
+      np = (uint32_t)((end - pos + kLongPiece - 1) / kLongPiece);
+    }
+    if (lane == 0) s_np[wv] = np;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tq = 0, tp = 0;
+      for (int w = 0; w < kPlanWaves; w++) {
+        tq += s_np[w];
+        tp += s_np[w] > 1 ? s_np[w] : 0u;
+      }
+      s_q = tq ? atomicAdd(a.n_long + 1, tq) : 0u;
+      s_p = tp ? atomicAdd(a.n_long + 3, tp) : 0u;
+    }
+    __syncthreads();
+    if (r < nl) {
+      uint32_t q0 = s_q, pb = s_p;
+      for (uint32_t w = 0; w < wv; w++) {
+        q0 += s_np[w];
+        pb += s_np[w] > 1 ? s_np[w] : 0u;
+      }
+      if (lane == 0) a.long_meta[r] = make_uint4((uint32_t)end, np, np > 1 ? pb : 0u, 0u);
+      for (uint32_t k = lane; k < np; k += kWave) a.long_pieces[q0 + k] = make_uint2(r, k);
+    }
+    __syncthreads();   // s_np / s_q / s_p are read before the next round's writes
+  }
+}
+
 constexpr int kLWaves = 8;
 constexpr int kLThreads = kLWaves * kWave;
-struct LongSmem {
-  uint64_t ep[kLWaves], svc[kLWaves], kmask[kLWaves];
-  uint32_t err[kLWaves];
-  uint64_t lm[kLWaves][kWave], le[kLWaves][kWave];
-  uint32_t lf[kLWaves][kWave];
-  uint32_t end_win;
-  uint32_t keep;
+struct LongPart {   // kLongPartBytes
+  uint64_t m[kWave], e[kWave];
+  uint32_t f[kWave];
+  uint64_t ep, svc, kmask;
+  uint32_t err;
+  uint32_t _pad[9];   // 21 cache lines
 };
+static_assert(sizeof(LongPart) == kLongPartBytes, "long-run partial layout");
+// keep bytes [x0, x1) = k, 16-byte stores in the aligned middle
+__device__ __forceinline__ void long_keep_fill(uint8_t* keep, uint64_t x0, uint64_t x1, uint8_t k, int lane) {
+  const uint64_t b = reinterpret_cast<uintptr_t>(keep);
+  const uint64_t a0 = min(x1, ((b + x0 + 15) & ~15ull) - b), a1 = max(a0, ((b + x1) & ~15ull) - b);
+  for (uint64_t x = x0 + lane; x < a0; x += kWave) keep[x] = k;
+  const uint32_t k4 = k * 0x01010101u;
+  for (uint64_t x = a0 + 16ull * lane; x < a1; x += 16ull * kWave) *reinterpret_cast<uint4*>(keep + x) = make_uint4(k4, k4, k4, k4);
+  for (uint64_t x = a1 + lane; x < x1; x += kWave) keep[x] = k;
+}
+// a long run's decision (wave-wide: lane k holds latency slot k's monoid)
+// and its keep bytes
+__device__ __forceinline__ void long_decide(const TraceKernelArgs& a, const Cfg& c, int lane, uint64_t pos, uint64_t end,
+                                            uint32_t E, uint64_t EP, uint64_t SV, uint64_t K, const Lat& tot) {
+  uint64_t s_l = 0;
+  if ((K >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, tot.m, tot.e);
+  s_l = wave_or64(s_l);
+  uint32_t dk32 = 0;
+  if (lane == 0) {
+    const uint4 t = reinterpret_cast<const uint4*>(a.tid)[pos];
+    uint8_t dk = 0, dl = 0;
+    double dr = 0;
+    decide_at(a, c, pos, E, EP, s_l, SV,
+              trace_uniform((uint64_t)t.x | ((uint64_t)t.y << 32), (uint64_t)t.z | ((uint64_t)t.w << 32), a.seed), dk, dl,
+              dr);
+    write_rec(a, pos, dk, dl, dr);
+    dk32 = dk;
+  }
+  long_keep_fill(a.keep, pos, end, (uint8_t)rdl(dk32, 0), lane);
+}
+// Each wave takes pieces in turn, on its own (no workgroup barrier after
+// the table copy): a piece's latency chain overlaps the other waves' folds
 __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a) {
-  const uint32_t nl = __hip_atomic_load(a.n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (blockIdx.x >= nl) return;
+  const uint32_t npieces = __hip_atomic_load(a.n_long + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x * kLWaves >= npieces) return;
   __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
-  __shared__ LongSmem sm;
   {
     const uint32_t nb = cfg_lds_copy_bytes(a.cfg);
     for (uint32_t k = threadIdx.x * 16; k < nb; k += kLThreads * 16)
@@ -1549,53 +1648,39 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
   }
   const Cfg c = load_cfg(cfg_lds);
   const int lane = threadIdx.x & 63;
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint64_t n = a.n_spans;
   const uint32_t nsvc = c.h->n_services;
   const bool want_route = c.h->n_lat && !a.route_match && a.route;
-  for (uint32_t r = blockIdx.x; r < nl; r += gridDim.x) {
-    const uint64_t pos = a.long_runs[r];
-    // ---- run end: the first head after pos (window head masks of the fast path)
-    if (threadIdx.x == 0) sm.end_win = 0xFFFFFFFFu;
-    __syncthreads();
-    const uint32_t w0 = (uint32_t)(pos / kWave);
-    const uint64_t m0 = a.win_heads[w0] & ~lanemask_le((int)(pos % kWave));
-    uint64_t end;
-    if (m0) {
-      end = (uint64_t)w0 * kWave + ffs64(m0);
-    } else {
-      for (uint32_t wb = w0 + 1; wb < a.n_windows; wb += kLThreads) {
-        const uint32_t w = wb + threadIdx.x;
-        if (w < a.n_windows && a.win_heads[w]) atomicMin(&sm.end_win, w);
-        __syncthreads();
-        const uint32_t found = sm.end_win;
-        __syncthreads();   // every thread has read it before the next round's atomics
-        if (found != 0xFFFFFFFFu) break;
-      }
-      const uint32_t we = sm.end_win;
-      end = we == 0xFFFFFFFFu ? n : (uint64_t)we * kWave + ffs64(a.win_heads[we]);
-    }
-    // ---- this wave's piece [lo, hi) of [pos, end), whole 64-span steps
-    const uint64_t steps = (end - pos + kWave - 1) / kWave;
-    const uint64_t per = (steps + kLWaves - 1) / kLWaves;
-    const uint64_t lo = pos + (uint64_t)wv * per * kWave, hi = min(end, lo + per * kWave);
+  const uint32_t stride = gridDim.x * kLWaves;
+  for (uint32_t q = blockIdx.x * kLWaves + (threadIdx.x >> 6); q < npieces; q += stride) {
+    const uint2 pk = a.long_pieces[q];
+    const uint4 meta = a.long_meta[pk.x];   // {end, pieces, first partial, pieces done}
+    const uint64_t pos = a.long_runs[pk.x], end = meta.x;
+    const uint64_t lo = pos + (uint64_t)pk.y * kLongPiece, hi = min(end, lo + kLongPiece);
     uint32_t err = 0;
     uint64_t ep_acc = 0, svc_acc = 0, kmask = 0;
     Lat cur{0, kInf, 0};   // lane k: latency slot k
-    LongRaw nx = long_raw(a, c.h, lo + lane, hi);
+    // two steps of columns in flight, the service ids of the next step
+    // gathered a step ahead: a step's route head waits on nothing of its own
+    LongRaw r0 = long_raw(a, c.h, lo + lane, hi), r1 = long_raw(a, c.h, lo + kWave + lane, hi);
+    uint32_t nsv = 0xFFFFFFFFu, nss = 0xFFFFFFFFu;
+    if (lo + lane < hi) {
+      nsv = a.res_svc[r0.res];
+      nss = a.res_svc_str[r0.res];
+    }
     for (uint64_t base = lo; base < hi; base += kWave) {
       const uint64_t p = base + lane;
       const bool valid = p < hi;
-      const LongRaw r = nx;
-      uint32_t sv = 0xFFFFFFFFu, ss = 0xFFFFFFFFu;
+      const LongRaw r = r0;
+      const uint32_t sv = nsv, ss = nss;
       uint4 rw = make_uint4(0, 0, 0, 0);
-      if (valid) {   // this step's dependent loads, then the next step's columns
-        sv = a.res_svc[r.res];
-        ss = a.res_svc_str[r.res];
-        if (want_route && r.rt.len && sv < nsvc && c.svc_slot[sv] != kNoSlot)
-          rw = head16(a.arena, r.rt.off, r.rt.len);
+      if (valid && want_route && r.rt.len && sv < nsvc && c.svc_slot[sv] != kNoSlot)
+        rw = head16(a.arena, r.rt.off, r.rt.len);
+      r0 = r1;
+      if (base + 2 * kWave < hi) r1 = long_raw(a, c.h, p + 2 * kWave, hi);
+      if (p + kWave < hi) {
+        nsv = a.res_svc[r0.res];
+        nss = a.res_svc_str[r0.res];
       }
-      if (base + kWave < hi) nx = long_raw(a, c.h, p + kWave, hi);
       uint32_t slot = kNoSlot;
       uint64_t st = 0, en = 0;
       const uint32_t rst = (r.status & kStatusReset) ? 1u : 0u;
@@ -1635,48 +1720,68 @@ __global__ __launch_bounds__(kLThreads) void trace_long_kernel(TraceKernelArgs a
         kmask |= 1ull << ks;
       }
     }
-    err = __ballot(err != 0) ? 1u : 0u;
-    ep_acc = wave_or64(ep_acc);
-    svc_acc = wave_or64(svc_acc);
-    sm.lf[wv][lane] = cur.f;
-    sm.lm[wv][lane] = cur.m;
-    sm.le[wv][lane] = cur.e;
-    if (lane == 0) {
-      sm.err[wv] = err;
-      sm.ep[wv] = ep_acc;
-      sm.svc[wv] = svc_acc;
-      sm.kmask[wv] = kmask;
-    }
-    __syncthreads();
-    if (wv == 0) {
-      uint32_t E = 0;
-      uint64_t EP = 0, SV = 0, K = 0;
-      Lat tot{0, kInf, 0};
-      for (int w = 0; w < kLWaves; w++) {
-        E |= sm.err[w];
-        EP |= sm.ep[w];
-        SV |= sm.svc[w];
-        K |= sm.kmask[w];
-        if ((sm.kmask[w] >> lane) & 1) tot = lat_comb(tot, Lat{sm.lf[w][lane], sm.lm[w][lane], sm.le[w][lane]});
-      }
-      uint64_t s_l = 0;
-      if ((K >> lane) & 1) s_l = latency_satisfied(c, (uint32_t)lane, EP, tot.m, tot.e);
-      s_l = wave_or64(s_l);
+    uint32_t E = __ballot(err != 0) ? 1u : 0u;
+    uint64_t EP = wave_or64(ep_acc), SV = wave_or64(svc_acc), K = kmask;
+    Lat tot = cur;
+    if (meta.y > 1) {   // trace_long_decide_kernel combines the run's partials
+      LongPart* part = reinterpret_cast<LongPart*>(a.long_part + (size_t)kLongPartBytes * (meta.z + pk.y));
+      part->m[lane] = tot.m;
+      part->e[lane] = tot.e;
+      part->f[lane] = tot.f;
       if (lane == 0) {
-        const uint4 t = reinterpret_cast<const uint4*>(a.tid)[pos];
-        uint8_t dk = 0, dl = 0;
-        double dr = 0;
-        decide_at(a, c, pos, E, EP, s_l, SV,
-                  trace_uniform((uint64_t)t.x | ((uint64_t)t.y << 32), (uint64_t)t.z | ((uint64_t)t.w << 32), a.seed), dk,
-                  dl, dr);
-        write_rec(a, pos, dk, dl, dr);
-        sm.keep = dk;
+        part->ep = EP;
+        part->svc = SV;
+        part->kmask = K;
+        part->err = E;
+      }
+      continue;
+    }
+    long_decide(a, c, lane, pos, end, E, EP, SV, K, tot);
+  }
+}
+
+// one wave per run of several pieces: its partials in piece order, the
+// decision, the run's keep bytes
+__global__ __launch_bounds__(kPlanWaves * kWave) void trace_long_decide_kernel(TraceKernelArgs a) {
+  const uint32_t nl = __hip_atomic_load(a.n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x * kPlanWaves >= nl) return;
+  __shared__ __attribute__((aligned(16))) uint8_t cfg_lds[kSampCfgLds];
+  {
+    const uint32_t nb = cfg_lds_copy_bytes(a.cfg);
+    for (uint32_t k = threadIdx.x * 16; k < nb; k += kPlanWaves * kWave * 16)
+      *reinterpret_cast<uint4*>(cfg_lds + k) = *reinterpret_cast<const uint4*>(a.cfg + k);
+    __syncthreads();
+  }
+  const Cfg c = load_cfg(cfg_lds);
+  const int lane = threadIdx.x & 63;
+  for (uint32_t r = blockIdx.x * kPlanWaves + (threadIdx.x >> 6); r < nl; r += gridDim.x * kPlanWaves) {
+    const uint4 meta = a.long_meta[r];
+    if (meta.y <= 1) continue;
+    uint32_t E = 0;
+    uint64_t EP = 0, SV = 0, K = 0;
+    Lat tot{0, kInf, 0};
+    const LongPart* pp = reinterpret_cast<const LongPart*>(a.long_part + (size_t)kLongPartBytes * meta.z);
+    for (uint32_t k0 = 0; k0 < meta.y; k0 += 4) {   // piece order, 4 partials' loads in flight
+      uint64_t kk[4], m[4], e[4];
+      uint32_t f[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const LongPart& q = pp[k0 + j < meta.y ? k0 + j : k0];
+        kk[j] = k0 + j < meta.y ? q.kmask : 0ull;
+        E |= q.err;
+        EP |= q.ep;
+        SV |= q.svc;
+        f[j] = q.f[lane];
+        m[j] = q.m[lane];
+        e[j] = q.e[lane];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        K |= kk[j];
+        if ((kk[j] >> lane) & 1) tot = lat_comb(tot, Lat{f[j], m[j], e[j]});
       }
     }
-    __syncthreads();
-    const uint8_t k = (uint8_t)sm.keep;
-    for (uint64_t q = pos + threadIdx.x; q < end; q += kLThreads) a.keep[q] = k;
-    __syncthreads();
+    long_decide(a, c, lane, a.long_runs[r], meta.x, E, EP, SV, K, tot);
   }
 }
 
@@ -2677,11 +2782,17 @@ void launch_trace_dup_check(const TraceKernelArgs& a, hipStream_t st) {
 }
 
 void launch_trace_long(const TraceKernelArgs& a, hipStream_t st, uint32_t known_runs) {
-  // known_runs: the listed-run count the host read (host-gated form); else a
-  // grid for the most runs the fast path can list, blocks past *n_long exit
+  // known_runs: the listed-run count the host read (host-gated form); else
+  // grids for the most runs the fast path can list, workgroups past the
+  // device counts exit
   const uint64_t most = known_runs ? known_runs : a.n_spans / ((uint64_t)a.long_steps * kWave) + 1;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(most, 1024);
-  hipLaunchKernelGGL(trace_long_kernel, dim3(blocks), dim3(kLThreads), 0, st, a);
+  hipLaunchKernelGGL(trace_long_plan_kernel, dim3((uint32_t)std::min<uint64_t>((most + kPlanWaves - 1) / kPlanWaves, 1024)),
+                     dim3(kPlanWaves * kWave), 0, st, a);
+  const uint64_t pieces = most + a.n_spans / kLongPiece + 1;
+  hipLaunchKernelGGL(trace_long_kernel, dim3((uint32_t)std::min<uint64_t>((pieces + kLWaves - 1) / kLWaves, 1024)),
+                     dim3(kLThreads), 0, st, a);
+  hipLaunchKernelGGL(trace_long_decide_kernel, dim3((uint32_t)std::min<uint64_t>((most + kPlanWaves - 1) / kPlanWaves, 1024)),
+                     dim3(kPlanWaves * kWave), 0, st, a);
 }
 void launch_trace_insert_exact(const TraceKernelArgs& a, hipStream_t st) {
   if (a.n_spans)

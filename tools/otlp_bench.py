@@ -157,7 +157,7 @@ def main():
     # concurrent export requests): one stream and one set of outputs per
     # caller, the engine and router shared; whole-job spans/s
     import threading
-    for callers in (1, 4, 8):
+    for callers in (1, 4, 8, 16):
         per = 120
         ready = threading.Barrier(callers + 1)
         errs = []
