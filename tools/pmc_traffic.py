@@ -14,17 +14,32 @@ from bench import WORKLOADS  # noqa: E402  (the bench line's kernel list is the 
 # profile spans that cover several launches: the kernels they stand for
 SPAN_KERNELS = {"trace_run_list": ("trace_runs_kernel", "trace_fold_kernel", "trace_first_select_kernel"),
                 "trace_sort_path": ("trace_key_kernel", "sort_hist_kernel", "scan_u32_kernel", "sort_scatter_kernel"),
-                "shard_unpack": ("shard_unpack_kernel",)}
+                "shard_unpack": ("shard_unpack_kernel",),
+                "trace_long_kernel": ("trace_long_plan_kernel", "trace_long_kernel", "trace_long_decide_kernel")}
 
 wl, root, out = sys.argv[1], sys.argv[2], sys.argv[3]
 kernels = WORKLOADS[wl]["kernels"]
-vals = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+vals = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}   # (span, kernel) -> values
 for c in vals:
     for f in glob.glob(f"{root}/{c}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
+            name = row.get("Kernel_Name", "")
             for k in kernels:
-                if any(x in row.get("Kernel_Name", "") for x in SPAN_KERNELS.get(k, (k,))):
-                    vals[c][k].append(float(row["Counter_Value"]))
+                # the longest sub-kernel name contained in the row's (trace_long_kernel
+                # is also a substring of nothing else; keep the match exact per span)
+                subs = [x for x in SPAN_KERNELS.get(k, (k,)) if x in name]
+                if subs:
+                    vals[c][(k, max(subs, key=len))].append(float(row["Counter_Value"]))
+
+
+def mean_kib(xs):
+    # gated launches (the sort-based trace path exits at once unless the fast
+    # path saw a split trace) are dispatches of the same kernel with ~no
+    # traffic: average over the working dispatches only
+    xs = [x for x in xs if x > 0.01 * max(xs)] or xs
+    return sum(xs) / len(xs)
+
+
 spans = None
 for f in glob.glob(f"{root}/FETCH_SIZE.log"):
     for line in open(f):
@@ -32,19 +47,16 @@ for f in glob.glob(f"{root}/FETCH_SIZE.log"):
             spans = json.loads(line)["config"]["spans_per_gpu"]
 per_k = {}
 for k in kernels:
-    fe = vals["FETCH_SIZE"][k]
-    wr = vals["WRITE_SIZE"][k]
+    subs = SPAN_KERNELS.get(k, (k,))
+    fe = [vals["FETCH_SIZE"][(k, x)] for x in subs if vals["FETCH_SIZE"][(k, x)]]
+    wr = [vals["WRITE_SIZE"][(k, x)] for x in subs if vals["WRITE_SIZE"][(k, x)]]
     if not fe or not wr:
         # host-gated launches (trace_long_kernel, the repeated-trace-id
         # paths, url_emit_slow_kernel) that this workload never queued
         per_k[k] = {"fetch_kib": 0.0, "write_kib": 0.0, "hbm_bytes": 0.0, "launched": False}
         continue
-    # gated launches (the sort-based trace path exits at once unless the fast
-    # path saw a split trace) are dispatches of the same kernel with ~no
-    # traffic: average over the working dispatches only
-    fe = [x for x in fe if x > 0.01 * max(fe)] or fe
-    wr = [x for x in wr if x > 0.01 * max(wr)] or wr
-    fkb, wkb = sum(fe) / len(fe), sum(wr) / len(wr)
+    # a span's launches per step: the sum of its kernels' per-dispatch means
+    fkb, wkb = sum(mean_kib(x) for x in fe), sum(mean_kib(x) for x in wr)
     per_k[k] = {"fetch_kib": fkb, "write_kib": wkb, "hbm_bytes": (2 * fkb + wkb) * 1024}
 ent = {"spans": spans, "hbm_bytes_per_launch": sum(v["hbm_bytes"] for v in per_k.values()),
        "per_kernel": per_k, "method": "2*FETCH_SIZE + WRITE_SIZE, KiB, mean per dispatch"}
