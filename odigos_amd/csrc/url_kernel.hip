@@ -1636,6 +1636,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         a.group_sum[g] = sum;
         a.group_scr[g] = region + scr_used;
       }
+      // refs form: the image stays where it is, so the group's template refs
+      // are known here (url_copy_kernel writes only the other groups')
+      if (a.refs && i < a.n_spans) a.tmpl[i] = ose_strref{(uint32_t)(region + scr_used + local), p.len};
       scr_used += need;
     } else if (lane == 0) {
       a.group_sum[g] = sum;
@@ -1846,8 +1849,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize 
     const uint32_t la = wave_excl_scan(A.len, &unused);
     const CopyJob ja = copy_job(a, A);
     const uint4 va = copy_load(ja, 0);
-    if (ia < a.n_spans) {
-      // refs mode: a fast group's template stays in its scratch image
+    if (ia < a.n_spans && !(a.refs && A.so != ~0ull)) {
+      // refs mode: a fast group's template stays in its scratch image (its
+      // refs were written by url_plan_kernel)
       const uint64_t at = a.refs && A.so != ~0ull ? A.so : A.base;
       a.tmpl[ia] = ose_strref{(uint32_t)(at + la), A.len};
     }
