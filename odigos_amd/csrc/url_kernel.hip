@@ -1825,6 +1825,25 @@ template <bool kSize>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kSize ? 5 : 6, 8))) void url_copy_kernel(UrlKernelArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t stride = wave_stride();
+  if (!kSize && a.refs) {
+    // refs form without the size pass: url_plan_kernel wrote the refs of the
+    // groups it assembled; a wave looks at 64 groups' image offsets at once
+    // and writes the refs of the others (their bytes are placed at the
+    // scanned group base by url_emit_slow_kernel)
+    for (uint64_t g0 = (uint64_t)wave_first_group() * kWave; g0 < a.n_groups; g0 += (uint64_t)stride * kWave) {
+      const uint64_t gg = g0 + lane;
+      const bool other = gg < a.n_groups && a.group_scr[gg] == ~0ull;
+      for (uint64_t m = __ballot(other); m; m &= m - 1) {
+        const uint32_t g = (uint32_t)(g0 + __builtin_ctzll(m));
+        const CopyCols A = copy_cols(a, g, lane);
+        uint32_t unused;
+        const uint32_t la = wave_excl_scan(A.len, &unused);
+        const uint64_t ia = (uint64_t)g * kWave + lane;
+        if (ia < a.n_spans) a.tmpl[ia] = ose_strref{(uint32_t)(A.base + la), A.len};
+      }
+    }
+    return;
+  }
   uint32_t kept = 0;
   const bool sz_on = kSize && !sizedev::size_batch_dropped(a.sz);
   uint32_t g = wave_first_group();
