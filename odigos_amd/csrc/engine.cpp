@@ -175,6 +175,8 @@ Engine::~Engine() {
     if (w->pending) (void)hipEventDestroy(w->pending);
     if (w->dup_host) (void)hipHostFree(w->dup_host);
     if (w->dup_ready) (void)hipEventDestroy(w->dup_ready);
+    if (w->fork) (void)hipEventDestroy(w->fork);
+    if (w->join) (void)hipEventDestroy(w->join);
     delete w;
   }
 }
@@ -532,18 +534,45 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   if (mask & OSE_STAGE_SIZE) need = std::max(need, size_off + size_scratch_bytes(c->n_scopes, c->n_resources));
   int rc = ws->reserve(need);
   std::function<int()> sample_tail;
+  UrlKernelArgs ua{};
+  // SAMPLE + TEMPLATE (deferred slow path: the URL scratch lies past the
+  // trace stage's): the URL planning kernels (plan, slow plan, scan) need
+  // nothing from SAMPLE, so they run on a second stream beside the trace
+  // stage; the two are latency-bound at four waves per SIMD each and fit a
+  // CU together (LDS 2 x 39.7 + 2 x 29.7 KB).  The copy / size launches that
+  // read the final keep bytes wait for both.
+  hipStream_t ust = nullptr;
+  static const bool one_stream = getenv("OSE_ONE_STREAM") != nullptr;   // per-kernel profiling: no overlap
+  if (!one_stream && !rc && defer) {
+    if (!ws->fork) (void)hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming);
+    if (!ws->join) (void)hipEventCreateWithFlags(&ws->join, hipEventDisableTiming);
+    if (ws->fork && ws->join) ust = e->take_stream();
+    if (ust && (hipEventRecord(ws->fork, st) != hipSuccess || hipStreamWaitEvent(ust, ws->fork, 0) != hipSuccess)) {
+      e->give_stream(ust);
+      ust = nullptr;
+    }
+  }
+  const bool tmpl = !rc && (mask & OSE_STAGE_TEMPLATE);
+  if (ust && tmpl) rc = run_url(e, c, o, ust, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0);
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
   if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws, gate_on_host ? &sample_tail : nullptr);
   if (sample_tail && !defer) {
     rc = sample_tail();
     sample_tail = nullptr;
   }
-  UrlKernelArgs ua{};
-  const bool tmpl = !rc && (mask & OSE_STAGE_TEMPLATE);
-  if (tmpl) rc = run_url(e, c, o, st, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0);
+  if (!ust && tmpl && !rc) rc = run_url(e, c, o, st, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0);
   if (sample_tail) {
     const int trc = sample_tail();   // always drained: the host event wait must not be skipped
     if (!rc) rc = trc;
+  }
+  if (ust) {   // join: everything below runs on the caller's stream after both
+    const hipError_t je = hipEventRecord(ws->join, ust);
+    const hipError_t jw = je == hipSuccess ? hipStreamWaitEvent(st, ws->join, 0) : je;
+    if (jw != hipSuccess) {   // cannot order the streams: wait for the URL work on the host
+      (void)hipStreamSynchronize(ust);
+      if (!rc) rc = fail(OSE_EDEVICE, std::string("URL stream join: ") + hipGetErrorString(jw));
+    }
+    e->give_stream(ust);
   }
   // odigostrafficmetrics runs last, on what the earlier stages left (the
   // decisions are final here: SAMPLE's tail has been queued)

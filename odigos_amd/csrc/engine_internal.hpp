@@ -97,6 +97,9 @@ struct Workspace {
   // slow-path launches are only queued when a trace id repeats
   uint32_t* dup_host = nullptr;   // pinned
   hipEvent_t dup_ready = nullptr;
+  // SAMPLE + TEMPLATE: the URL planning kernels run on a second stream
+  // beside the trace stage (run_stages): fork and join events
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 struct Engine {

@@ -11,7 +11,8 @@ from odigos_amd.batch import DeviceBatch, Engine, Generator
 from tests.workloads import c3_sampling_config
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 50_000_000
-g = Generator("sampling", 0x0D160003, n, threads=16)
+wl = os.environ.get("OSE_ABLATE_WORKLOAD", "sampling")   # "sampling" (C3) or "zipf" (C5)
+g = Generator(wl, 0x0D160003 if wl == "sampling" else 0x0D160005, n, threads=16)
 eng = Engine({"odigossampling": c3_sampling_config()})
 db = DeviceBatch(g.cols, fields=("arena", "trace_id", "start_ns", "end_ns", "status", "resource", "route", "res_svc", "res_svc_str"))
 for f in ("trace_count", "trace_first_span", "trace_keep", "trace_level", "trace_ratio"):
