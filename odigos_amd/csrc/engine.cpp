@@ -342,9 +342,9 @@ int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st);
 
 // ws_off: the URL scratch starts this many bytes into the workspace (past a
 // SAMPLE stage's scratch whose slow path is still to be queued).  front: only
-// plan, plan_slow and scan are queued, and the arguments of the rest go to
-// *front (run_url_back queues url_copy, fused with odigostrafficmetrics'
-// spans pass when front->fuse_size is set, and url_emit_slow).
+// plan, plan_slow, scan and emit_slow are queued, and the arguments of the
+// rest go to *front (run_url_back queues url_copy, fused with
+// odigostrafficmetrics' spans pass when front->fuse_size is set).
 int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws, size_t ws_off = 0,
             UrlKernelArgs* front = nullptr, bool refs = false) {
   if (!e->has_url) return fail(OSE_EINVAL, "odigosurltemplate is not configured on this engine");
@@ -446,6 +446,14 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
   launch_url_scan(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
+  // the groups url_plan_kernel did not assemble, written at their scanned
+  // bases: nothing here reads SAMPLE's keep bytes or url_copy_kernel's
+  // output, so it runs with the front (beside the trace stage when the
+  // URL front has its own stream)
+  e->prof_begin("url_emit_slow_kernel", st, tm);
+  launch_url_emit_slow(a, st);
+  HIP_TRY(hipGetLastError());
+  e->prof_end(tm, st);
   if (front) {
     *front = a;
     return 0;
@@ -458,10 +466,6 @@ int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st) {
   Engine::Timed tm{};
   e->prof_begin("url_copy_kernel", st, tm);
   launch_url_copy(a, st);
-  HIP_TRY(hipGetLastError());
-  e->prof_end(tm, st);
-  e->prof_begin("url_emit_slow_kernel", st, tm);
-  launch_url_emit_slow(a, st);
   HIP_TRY(hipGetLastError());
   e->prof_end(tm, st);
   if (a.ablate & 512) {
