@@ -547,7 +547,10 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   // read the final keep bytes wait for both.
   hipStream_t ust = nullptr;
   static const bool one_stream = getenv("OSE_ONE_STREAM") != nullptr;   // per-kernel profiling: no overlap
-  if (!one_stream && !rc && defer) {
+  // (a small batch's kernels are launch-bound: a fork only adds two events
+  // and a stream hand-off to each call of a request-sized batch)
+  constexpr uint64_t kForkSpans = 1u << 20;
+  if (!one_stream && !rc && defer && n >= kForkSpans) {
     if (!ws->fork) (void)hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming);
     if (!ws->join) (void)hipEventCreateWithFlags(&ws->join, hipEventDisableTiming);
     if (ws->fork && ws->join) ust = e->take_stream();
