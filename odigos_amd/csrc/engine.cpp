@@ -346,7 +346,7 @@ int run_url_back(Engine* e, const UrlKernelArgs& a, hipStream_t st);
 // rest go to *front (run_url_back queues url_copy, fused with
 // odigostrafficmetrics' spans pass when front->fuse_size is set).
 int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t st, Workspace* ws, size_t ws_off = 0,
-            UrlKernelArgs* front = nullptr, bool refs = false) {
+            UrlKernelArgs* front = nullptr, bool refs = false, uint32_t grid_mult = 1) {
   if (!e->has_url) return fail(OSE_EINVAL, "odigosurltemplate is not configured on this engine");
   if (!c->url_flags || !c->kind || !c->path || !c->arena || !o->url_out || !o->tmpl || !o->tmpl_arena)
     return fail(OSE_EINVAL, "TEMPLATE stage needs url_flags, kind, path, arena, url_out, tmpl, tmpl_arena");
@@ -418,6 +418,7 @@ int run_url(Engine* e, const ose_columns* c, const ose_outputs* o, hipStream_t s
 #if OSE_DIAG
   if (const char* ab = getenv("OSE_URL_ABLATE")) a.ablate = (uint32_t)strtoul(ab, nullptr, 0);   // tools/ablate_url.py
 #endif
+  a.plan_grid_mult = refs ? grid_mult : 1u;
   a.scr_region = (scr_bytes / std::max<uint32_t>(1, url_plan_waves(a))) & ~15ull;
   // refs: image chunks of an eighth of the arena over the plan waves (at most
   // 256 KiB; a group larger than a chunk takes exactly its size): a wave
@@ -550,6 +551,13 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   // (a small batch's kernels are launch-bound: a fork only adds two events
   // and a stream hand-off to each call of a request-sized batch)
   constexpr uint64_t kForkSpans = 1u << 20;
+  // the plan grid beside the trace stage: 16x the resident workgroups
+  // (C4 7.80 -> 7.62 ms, C5 3.49 -> 3.26; 4x: 7.88 / 3.27; alone, C2, the
+  // resident grid stays: 16x there is 0.64 -> 2.0 ms, profiles/r5g_plan_grid_ab.txt)
+#ifndef OSE_FORK_PLAN_MULT
+#define OSE_FORK_PLAN_MULT 16
+#endif
+  constexpr uint32_t kForkPlanMult = OSE_FORK_PLAN_MULT;
   if (!one_stream && !rc && defer && n >= kForkSpans) {
     if (!ws->fork) (void)hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming);
     if (!ws->join) (void)hipEventCreateWithFlags(&ws->join, hipEventDisableTiming);
@@ -560,7 +568,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
     }
   }
   const bool tmpl = !rc && (mask & OSE_STAGE_TEMPLATE);
-  if (ust && tmpl) rc = run_url(e, c, o, ust, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0);
+  if (ust && tmpl) rc = run_url(e, c, o, ust, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0, kForkPlanMult);
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
   if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws, gate_on_host ? &sample_tail : nullptr);
   if (sample_tail && !defer) {

@@ -111,6 +111,7 @@ struct UrlKernelArgs {
   uint64_t refs_chunk;          // url_refs_chunk()
   uint32_t plan_waves;          // url_plan_waves()
   uint64_t* slow_aligned;       // refs: sum of the scan-placed groups' sizes rounded up to 16 (zeroed)
+  uint32_t plan_grid_mult;     // refs form beside the trace stage: plan workgroups = resident x this (run_stages)
   uint32_t ablate;             // diagnostics only (OSE_URL_ABLATE): 1 skip emission, 2 skip planning, 4 skip bitmaps
   uint64_t* dbg;               // diagnostics only (ablate & 512): per-section clock sums
   // odigostrafficmetrics' spans pass fused into url_copy_kernel (TEMPLATE and

@@ -2088,7 +2088,12 @@ static int url_mode(const UrlKernelArgs& a) {
 }
 template <int M>
 static uint32_t plan_blocks(const UrlKernelArgs& a) {
-  static const uint32_t cap = std::min<uint32_t>(resident_blocks(url_plan_kernel<M>, 0), kUrlMaxWaves / kWaves);
+  static const uint32_t res = resident_blocks(url_plan_kernel<M>, 0);
+  // beside the trace stage (refs form: no per-wave scratch regions) the grid
+  // is several times the resident one, so the dispatcher interleaves its
+  // workgroups with the trace stage's instead of the plan grid holding every
+  // CU's LDS until it drains (run_stages)
+  const uint32_t cap = a.refs && a.plan_grid_mult > 1 ? res * a.plan_grid_mult : std::min<uint32_t>(res, kUrlMaxWaves / kWaves);
   return std::min<uint32_t>(cap, (a.n_groups + kWaves - 1) / kWaves);
 }
 template <int M>
