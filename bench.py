@@ -507,7 +507,7 @@ def main():
     # serialises them for per-kernel profiles), so their HIP-event brackets
     # overlap and the roofline's time base is the step
     overlapped = (args.workload not in ("node8", "owner") and world == 1 and stages & native.STAGE_SAMPLE
-                  and stages & native.STAGE_TEMPLATE and not os.environ.get("OSE_ONE_STREAM"))
+                  and stages & native.STAGE_TEMPLATE and n_units >= (1 << 20) and not os.environ.get("OSE_ONE_STREAM"))
     if world > 1 and stages & native.STAGE_SAMPLE:
         st_ = [int(x) for x in nx.stats]
         extra.update({"exchange_records_sent": st_[0], "exchange_records_received": st_[1],
