@@ -136,3 +136,48 @@ def test_gpu_refs_refused_by_host_path():
         pb.process(REFS)
     with pytest.raises(native.OseError):   # REFS without TEMPLATE
         eng.process_device(DeviceBatch(g.cols), native.STAGE_TEMPLATE_REFS)
+
+
+@pytest.mark.gpu
+def test_gpu_forked_refs_equal_packed_and_overflow_retry():
+    # SAMPLE | TEMPLATE on 1M+ spans: the URL planning runs on a second stream
+    # beside the trace stage, in the refs form with a plan grid 16x the
+    # resident one (engine.cpp run_stages).  Its decisions, counters and
+    # templates equal the packed form's, and an arena too small for the
+    # larger grid's chunks reports a capacity whose retry fits.
+    import torch
+    cfg = {"odigossampling": c3_sampling_config(), "odigosurltemplate": {},
+           "odigostrafficmetrics": {"res_attributes_keys": ["service.name"]}}
+    g = Generator("fused", seed=0x0D1600ED, n_spans=1_200_000, threads=8)
+    eng = Engine(cfg)
+    st = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE
+    out = {}
+    for name, extra in (("packed", 0), ("refs", native.STAGE_TEMPLATE_REFS)):
+        db = DeviceBatch(g.cols)
+        eng.process_device(db, st | extra, seed=13)
+        torch.cuda.synchronize()
+        assert int(db.out_numpy("device_status", np.uint32)[0]) == 0
+        ns = g.cols.n_spans
+        t = db.out_numpy("tmpl", np.uint32)[: 2 * ns]
+        m = db.out_numpy("url_out")[:ns] != 0
+        out[name] = (db.out_numpy("keep")[:ns].copy(), db.out_numpy("url_out")[:ns].copy(),
+                     db.out_numpy("attrset_bytes", np.int64).copy(), db.out_numpy("accepted_spans", np.int64).copy(),
+                     span_template_bytes(t, db.out_numpy("tmpl_arena")[: db.used()], m))
+    for a, b in zip(out["packed"][:4], out["refs"][:4]):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(out["packed"][4], out["refs"][4]):   # template bytes, lengths
+        np.testing.assert_array_equal(a, b)
+    small = DeviceBatch(g.cols, tmpl_cap=1 << 16)
+    eng.process_device(small, st | native.STAGE_TEMPLATE_REFS, seed=13)
+    torch.cuda.synchronize()
+    assert int(small.out_numpy("device_status", np.uint32)[0]) & 2
+    need = small.used()
+    retry = DeviceBatch(g.cols, tmpl_cap=need)
+    eng.process_device(retry, st | native.STAGE_TEMPLATE_REFS, seed=13)
+    torch.cuda.synchronize()
+    assert int(retry.out_numpy("device_status", np.uint32)[0]) == 0
+    ns = g.cols.n_spans
+    t = retry.out_numpy("tmpl", np.uint32)[: 2 * ns]
+    m = retry.out_numpy("url_out")[:ns] != 0
+    for a, b in zip(span_template_bytes(t, retry.out_numpy("tmpl_arena")[: retry.used()], m), out["packed"][4]):
+        np.testing.assert_array_equal(a, b)
