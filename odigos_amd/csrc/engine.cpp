@@ -568,6 +568,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
     }
   }
   const bool tmpl = !rc && (mask & OSE_STAGE_TEMPLATE);
+  ws->beside_url = ust && tmpl;
   if (ust && tmpl) rc = run_url(e, c, o, ust, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0, kForkPlanMult);
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
   if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws, gate_on_host ? &sample_tail : nullptr);
@@ -606,6 +607,7 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
     rc = run_url_back(e, ua, st);
   }
   if (!rc && size_on) rc = run_size_tail(e, sa, st);
+  ws->beside_url = false;
   e->release_ws(ws, st);
   return rc;
 }

@@ -100,6 +100,7 @@ struct Workspace {
   // SAMPLE + TEMPLATE: the URL planning kernels run on a second stream
   // beside the trace stage (run_stages): fork and join events
   hipEvent_t fork = nullptr, join = nullptr;
+  bool beside_url = false;   // this call's trace stage runs beside the forked URL planning
 };
 
 struct Engine {

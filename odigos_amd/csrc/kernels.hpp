@@ -261,6 +261,10 @@ struct TraceKernelArgs {
 constexpr uint32_t kMaxRuns = 8;          // runs per trace the run-list path folds
 constexpr uint32_t kMaxFoldSpans = 4096;  // spans per trace one lane folds
 constexpr uint32_t kMaxFoldSlots = 8;     // latency services per trace one lane folds
+#ifndef OSE_WPW_BESIDE
+#define OSE_WPW_BESIDE 64
+#endif
+constexpr uint32_t kWinPerWaveBeside = OSE_WPW_BESIDE;   // beside the forked URL planning (sampling_host.cpp)
 constexpr uint32_t kWinPerWave = 16;   // tools/gpu_wpw.sh: C5 0.97 -> 0.83 ms, C3 2.03 -> 1.99 ms, C4 unchanged
 #ifndef OSE_LONG_PIECE
 #define OSE_LONG_PIECE 2048

@@ -533,7 +533,12 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
   // kWinPerWave windows per wave on large batches; a small one (the drop-in's
   // 8192-span calls: 128 windows) spreads over at least ~4096 waves, one
   // window each, instead of 8 waves walking 16 windows each (112 us -> ~)
-  a.win_per_wave = (uint32_t)std::min<uint64_t>(kWinPerWave, std::max<uint64_t>(1, a.n_windows / 4096));
+  // beside the URL planning (run_stages' fork) a wave takes kWinPerWaveBeside
+  // windows: fewer, longer trace workgroups interleave better with the plan
+  // grid's (C4 7.63 -> 7.47 ms, C5 3.26 -> 3.12; alone, C3, 16 stays best:
+  // profiles/r5w_win_per_wave_ab.txt)
+  const uint64_t wpw_cap = ws->beside_url ? kWinPerWaveBeside : kWinPerWave;
+  a.win_per_wave = (uint32_t)std::min<uint64_t>(wpw_cap, std::max<uint64_t>(1, a.n_windows / 4096));
   {
     // the error bit, the endpoint bits and the service (+ span_attribute)
     // bits in one word: trace_eval_kernel's kNarrow instance (C4 trace_eval
