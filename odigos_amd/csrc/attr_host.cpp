@@ -106,8 +106,11 @@ int Engine::build_attr_tables() {
   h.bytes_off = bl.put(bytes.data(), bytes.size());
   for (auto& rd : dfas) {
     const uint32_t off = put_dfa(bl, rd.second);
+    if (bl.overflow) break;
     bl.at<AttrRuleDev>(h.rules_off)[rd.first].dfa_off = off;
   }
+  bl.align();
+  if (bl.overflow) return fail(OSE_ENOTSUP, "span_attribute device tables exceed 4 GiB (the regex rules' DFAs together)");
   // expected-value offsets are relative to the bytes section
   for (size_t q = 0; q < rules.size(); q++) bl.at<AttrRuleDev>(h.rules_off)[q].exp_off += h.bytes_off;
   bl.align();

@@ -10,15 +10,26 @@
 
 namespace ose {
 
+// Section offsets (and DfaDev's trans_off / acc_off) are uint32: a blob
+// that would pass kMaxBytes appends nothing more and sets `overflow`, which
+// the table builders turn into OSE_ENOTSUP (sixteen 256 MiB DFAs would
+// otherwise wrap the offsets and point the kernels at the wrong tables).
 struct Blob {
+  static constexpr uint64_t kMaxBytes = 0xFFFFFFFFull - 64;
   std::vector<uint8_t> b;
+  bool overflow = false;
   uint32_t align() {
     while (b.size() % 16) b.push_back(0);
-    return (uint32_t)b.size();
+    if (b.size() > kMaxBytes) overflow = true;
+    return overflow ? 0u : (uint32_t)b.size();
   }
   template <typename T>
   uint32_t put(const T* p, size_t n) {
     uint32_t off = align();
+    if (overflow || (uint64_t)b.size() + (uint64_t)n * sizeof(T) > kMaxBytes) {
+      overflow = true;
+      return 0;
+    }
     const uint8_t* s = reinterpret_cast<const uint8_t*>(p);
     b.insert(b.end(), s, s + n * sizeof(T));
     return off;
@@ -49,6 +60,7 @@ inline uint32_t put_dfa(Blob& bl, const Dfa& d) {
     toff = bl.put(t16.data(), t16.size());
   }
   uint32_t aoff = bl.put(d.accept_end.data(), d.accept_end.size());
+  if (bl.overflow) return 0;
   DfaDev* hp = bl.at<DfaDev>(off);
   hp->hi_off = hoff;
   hp->trans_off = toff;

@@ -8,8 +8,8 @@
 
 #include "devcfg.hpp"
 
-#ifndef OSE_LDS_WORD2
-#define OSE_LDS_WORD2 0
+#ifndef OSE_LDS_WORD1
+#define OSE_LDS_WORD1 0
 #endif
 
 namespace ose {
@@ -171,15 +171,18 @@ struct LdsReader {
   uint32_t off;    // string start within the slice
   __device__ LdsReader(lds_u32* b, uint32_t o) : base(b), off(o) {}
   __device__ __forceinline__ uint32_t at(uint32_t i) const { return ((lds_u8*)base)[off + i]; }
-  // gfx950 LDS takes unaligned dword reads: one ds_read_b32 at any byte
-  // (OSE_LDS_WORD2=1: two aligned reads and a funnel shift)
+  // two aligned reads and a funnel shift: gfx950 takes a misaligned
+  // ds_read_b32 but replays it (64 cycles per wave instruction, PMC
+  // SQ_LDS_UNALIGNED_STALL), which cost url_plan_kernel more LDS cycles
+  // than all its aligned accesses (OSE_LDS_WORD1=1 builds the single
+  // misaligned read, diagnostics only)
   __device__ __forceinline__ uint32_t word(uint32_t i) const {
-#if OSE_LDS_WORD2
-    const uint32_t p = off + i;
-    return __builtin_amdgcn_alignbyte(base[(p >> 2) + 1], base[p >> 2], p & 3);
-#else
+#if OSE_LDS_WORD1
     typedef uint32_t __attribute__((aligned(1))) u32_ua;
     return *reinterpret_cast<const __attribute__((address_space(3))) u32_ua*>((lds_u8*)base + off + i);
+#else
+    const uint32_t p = off + i;
+    return __builtin_amdgcn_alignbyte(base[(p >> 2) + 1], base[p >> 2], p & 3);
 #endif
   }
   // the dword after next is loaded one step ahead so its latency overlaps

@@ -136,6 +136,7 @@ int build_url_blob(const UrlTemplateConfig& c, std::vector<uint8_t>& out, uint32
   h.dfa_off = bl.put(dfa_offs.data(), dfa_offs.size());
   h.bytes_off = bl.put(bytes.data(), bytes.size());
   bl.align();
+  if (bl.overflow) return fail(OSE_ENOTSUP, "odigosurltemplate device tables exceed 4 GiB (the regexps' DFAs together)");
   bl.b.resize(bl.b.size() + 16, 0);
   h.total_bytes = (uint32_t)bl.b.size();
   std::memcpy(bl.b.data(), &h, sizeof h);

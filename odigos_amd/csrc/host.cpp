@@ -882,3 +882,16 @@ extern "C" int osehost_regex_match(const char* pattern, const char* s, size_t n)
   if (st != ose::RegexStatus::Ok) { g_host_err = err; return -2; }
   return ose::dfa_match(d, reinterpret_cast<const uint8_t*>(s), n) ? 1 : 0;
 }
+
+// The host matcher (HostRegexp) with the given full-DFA caps; *lazy = 1 when
+// the pattern went to the lazy DFA.  1 / 0, -1 syntax, -2 unsupported.
+extern "C" int osehost_regex_match_host(const char* pattern, const char* s, size_t n, uint32_t max_states,
+                                        uint64_t max_bytes, int* lazy) {
+  ose::HostRegexp re;
+  std::string err;
+  ose::RegexStatus st = re.compile(pattern, err, max_states, max_bytes);
+  if (st == ose::RegexStatus::Syntax) { g_host_err = err; return -1; }
+  if (st != ose::RegexStatus::Ok) { g_host_err = err; return -2; }
+  if (lazy) *lazy = re.lazy() ? 1 : 0;
+  return re.match(reinterpret_cast<const uint8_t*>(s), n) ? 1 : 0;
+}

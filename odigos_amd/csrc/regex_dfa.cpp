@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 
 namespace ose {
@@ -693,7 +694,31 @@ RegexStatus regex_syntax_check(const std::string& pattern, std::string& err) {
   }
 }
 
-RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) {
+namespace {
+
+// The NFA and its rune equivalence classes: what the subset construction
+// (compile_dfa) and the lazy DFA (LazyDfa) share.
+struct Prepared {
+  Nfa nfa;
+  uint32_t ncls = 0;
+  uint32_t ascii[128];
+  std::vector<uint32_t> hi_lo, hi_hi, hi_cls;   // non-ASCII ranges, sorted
+  std::vector<int> cls_type;                    // EmptyOpContext type per class
+  std::vector<std::vector<uint8_t>> cls_in;     // [class][rangeset] membership
+  uint32_t cls(uint32_t r) const {
+    if (r < 0x80) return ascii[r];
+    size_t lo = 0, hi = hi_lo.size();
+    while (lo < hi) {
+      size_t m = (lo + hi) / 2;
+      if (r < hi_lo[m]) hi = m;
+      else if (r > hi_hi[m]) lo = m + 1;
+      else return hi_cls[m];
+    }
+    return 0;
+  }
+};
+
+RegexStatus prepare(const std::string& pattern, Prepared& P, std::string& err) {
   NodeP root;
   Compiler cc;
   try {
@@ -710,7 +735,8 @@ RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) 
     err = "error parsing regexp: " + e.msg + ": `" + pattern + "`";
     return e.st;
   }
-  const Nfa& nfa = cc.nfa;
+  P.nfa = std::move(cc.nfa);
+  const Nfa& nfa = P.nfa;
 
   // rune equivalence classes: boundaries of every set, plus '\n' and the word
   // chars so that each class has one EmptyOpContext type.
@@ -722,7 +748,6 @@ RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) 
   // elementary intervals [cuts[k], cuts[k+1]) -> signature -> class
   std::map<std::vector<uint8_t>, uint32_t> sig2cls;
   std::vector<uint32_t> iv_cls;
-  std::vector<int> cls_type;
   auto rtype = [](uint32_t r) {
     if (r == '\n') return kTypeNL;
     if ((r >= '0' && r <= '9') || (r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z') || r == '_') return kTypeWord;
@@ -742,45 +767,90 @@ RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) 
     if (it == sig2cls.end()) {
       c = (uint32_t)sig2cls.size();
       sig2cls.emplace(sig, c);
-      cls_type.push_back(rtype(lo));
+      P.cls_type.push_back(rtype(lo));
     } else {
       c = it->second;
     }
     iv_cls.push_back(c);
   }
-  uint32_t ncls = (uint32_t)sig2cls.size();
-  if (ncls > 255) { err = "regexp needs more than 255 rune classes"; return RegexStatus::TooLarge; }
-  out = Dfa{};
-  out.nclasses = ncls;
+  P.ncls = (uint32_t)sig2cls.size();
   for (size_t k = 0; k + 1 < cuts.size(); k++) {
     uint32_t lo = cuts[k], hi = cuts[k + 1] - 1;
     if (lo < 0x80) {
-      for (uint32_t r = lo; r <= std::min<uint32_t>(hi, 0x7F); r++) out.ascii_class[r] = (uint8_t)iv_cls[k];
+      for (uint32_t r = lo; r <= std::min<uint32_t>(hi, 0x7F); r++) P.ascii[r] = iv_cls[k];
     } else {
-      if (!out.hi_lo.empty() && out.hi_cls.back() == iv_cls[k] && out.hi_hi.back() + 1 == lo) out.hi_hi.back() = hi;
-      else { out.hi_lo.push_back(lo); out.hi_hi.push_back(hi); out.hi_cls.push_back((uint8_t)iv_cls[k]); }
+      if (!P.hi_lo.empty() && P.hi_cls.back() == iv_cls[k] && P.hi_hi.back() + 1 == lo) P.hi_hi.back() = hi;
+      else { P.hi_lo.push_back(lo); P.hi_hi.push_back(hi); P.hi_cls.push_back(iv_cls[k]); }
     }
   }
   // set membership per class (any interval of the class is representative)
-  std::vector<std::vector<uint8_t>> cls_in(ncls, std::vector<uint8_t>(nfa.sets.size()));
+  P.cls_in.assign(P.ncls, std::vector<uint8_t>(nfa.sets.size()));
   for (auto& kv : sig2cls)
-    for (size_t si = 0; si < nfa.sets.size(); si++) cls_in[kv.second][si] = kv.first[si];
+    for (size_t si = 0; si < nfa.sets.size(); si++) P.cls_in[kv.second][si] = kv.first[si];
+  return RegexStatus::Ok;
+}
 
-  // subset construction.  DFA state = (sorted Rune-inst set before closure,
-  // type of previous rune).  The start inst is re-injected at every position
-  // (unanchored search).  MATCH is absorbing.
-  struct Key {
-    std::vector<int> set;
-    int prev;
-    bool operator<(const Key& o) const { return prev != o.prev ? prev < o.prev : set < o.set; }
-  };
-  std::map<Key, uint32_t> ids;
-  std::vector<Key> states;
-  std::vector<char> seen(nfa.prog.size(), 0);
+// DFA state = (sorted Rune-inst set before closure, type of previous rune).
+// The start inst is re-injected at every position (unanchored search); MATCH
+// is absorbing.
+struct StateKey {
+  std::vector<int> set;
+  int prev;
+  bool operator<(const StateKey& o) const { return prev != o.prev ? prev < o.prev : set < o.set; }
+};
+
+// One transition of the subset construction: true = the closure before the
+// rune already matched (the MATCH sink), else `next` is the successor.
+bool subset_step(const Prepared& P, const StateKey& cur, uint32_t c, StateKey& next, std::vector<char>& seen) {
+  std::vector<int> set = cur.set;
+  set.push_back(P.nfa.start);
+  bool match = false;
+  closure(P.nfa, set, context(cur.prev, P.cls_type[c]), seen, match);
+  if (match) return true;
+  next.set.clear();
+  for (int pc : set) {
+    const Inst& in = P.nfa.prog[pc];
+    if (P.cls_in[c][in.ranges]) next.set.push_back(in.out);
+  }
+  std::sort(next.set.begin(), next.set.end());
+  next.set.erase(std::unique(next.set.begin(), next.set.end()), next.set.end());
+  next.prev = P.cls_type[c];
+  return false;
+}
+
+bool subset_accepts_end(const Prepared& P, const StateKey& cur, std::vector<char>& seen) {
+  std::vector<int> set = cur.set;
+  set.push_back(P.nfa.start);
+  bool match = false;
+  closure(P.nfa, set, context(cur.prev, kTypeBot), seen, match);
+  return match;
+}
+
+}  // namespace
+
+RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err, uint32_t max_states,
+                        uint64_t max_table_bytes) {
+  max_states = std::min(max_states, Dfa::kMaxStates);
+  max_table_bytes = std::min(max_table_bytes, Dfa::kMaxTableBytes);
+  Prepared P;
+  const RegexStatus pst = prepare(pattern, P, err);
+  if (pst != RegexStatus::Ok) return pst;
+  const uint32_t ncls = P.ncls;
+  if (ncls > 255) { err = "regexp needs more than 255 rune classes"; return RegexStatus::TooLarge; }
+  out = Dfa{};
+  out.nclasses = ncls;
+  for (int r = 0; r < 128; r++) out.ascii_class[r] = (uint8_t)P.ascii[r];
+  out.hi_lo = P.hi_lo;
+  out.hi_hi = P.hi_hi;
+  out.hi_cls.assign(P.hi_cls.begin(), P.hi_cls.end());
+
+  std::map<StateKey, uint32_t> ids;
+  std::vector<StateKey> states;
+  std::vector<char> seen(P.nfa.prog.size(), 0);
   const uint32_t kMatch = 0;
   // state 0 = MATCH sink
-  states.push_back(Key{{}, -1});
-  auto intern = [&](Key k) -> uint32_t {
+  states.push_back(StateKey{{}, -1});
+  auto intern = [&](StateKey k) -> uint32_t {
     auto it = ids.find(k);
     if (it != ids.end()) return it->second;
     uint32_t id = (uint32_t)states.size();
@@ -788,44 +858,25 @@ RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) 
     states.push_back(std::move(k));
     return id;
   };
-  uint32_t start = intern(Key{{}, kTypeBot});
+  uint32_t start = intern(StateKey{{}, kTypeBot});
   std::vector<uint32_t> trans;
   std::vector<uint8_t> acc_end;
   trans.resize(ncls);  // row for MATCH
   for (uint32_t c = 0; c < ncls; c++) trans[c] = kMatch;
   acc_end.push_back(1);
+  StateKey next;
   for (uint32_t s = 1; s < states.size(); s++) {
-    if (states.size() > Dfa::kMaxStates || (uint64_t)states.size() * ncls * 4 > Dfa::kMaxTableBytes) {
-      err = "regexp DFA exceeds " + std::to_string(Dfa::kMaxStates) + " states or " +
-            std::to_string(Dfa::kMaxTableBytes >> 20) + " MiB of transitions";
+    if (states.size() > max_states || (uint64_t)states.size() * ncls * 4 > max_table_bytes) {
+      err = "regexp DFA exceeds " + std::to_string(max_states) + " states or " +
+            std::to_string(max_table_bytes >> 20) + " MiB of transitions";
       return RegexStatus::TooLarge;
     }
-    Key cur = states[s];
+    StateKey cur = states[s];
     std::vector<uint32_t> row(ncls);
-    for (uint32_t c = 0; c < ncls; c++) {
-      std::vector<int> set = cur.set;
-      set.push_back(nfa.start);
-      bool match = false;
-      closure(nfa, set, context(cur.prev, cls_type[c]), seen, match);
-      if (match) { row[c] = kMatch; continue; }
-      std::vector<int> next;
-      for (int pc : set) {
-        const Inst& in = nfa.prog[pc];
-        if (cls_in[c][in.ranges]) next.push_back(in.out);
-      }
-      std::sort(next.begin(), next.end());
-      next.erase(std::unique(next.begin(), next.end()), next.end());
-      uint32_t t = intern(Key{std::move(next), cls_type[c]});
-      row[c] = t;
-    }
+    for (uint32_t c = 0; c < ncls; c++)
+      row[c] = subset_step(P, cur, c, next, seen) ? kMatch : intern(next);
     trans.insert(trans.end(), row.begin(), row.end());
-    {
-      std::vector<int> set = cur.set;
-      set.push_back(nfa.start);
-      bool match = false;
-      closure(nfa, set, context(cur.prev, kTypeBot), seen, match);
-      acc_end.push_back(match ? 1 : 0);
-    }
+    acc_end.push_back(subset_accepts_end(P, cur, seen) ? 1 : 0);
   }
   out.nstates = (uint32_t)states.size();
   out.start = start;
@@ -833,6 +884,111 @@ RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err) 
   out.trans = std::move(trans);
   out.accept_end = std::move(acc_end);
   return RegexStatus::Ok;
+}
+
+// ---------------- lazy DFA ----------------
+struct LazyDfa::Impl {
+  Prepared P;
+  uint64_t max_bytes = 0;
+  std::mutex mu;
+  std::map<StateKey, uint32_t> ids;
+  std::vector<StateKey> states;     // 0 = MATCH sink
+  std::vector<uint32_t> trans;      // [state][class], kUnknown until computed
+  std::vector<int8_t> acc;          // accept at end of text: -1 unknown
+  std::vector<char> seen;
+  uint64_t flushes = 0;
+  static constexpr uint32_t kUnknown = 0xFFFFFFFFu;
+  void reset() {
+    ids.clear();
+    states.assign(1, StateKey{{}, -1});
+    trans.assign(P.ncls, 0u);
+    acc.assign(1, 1);
+  }
+  uint32_t intern(StateKey k) {
+    auto it = ids.find(k);
+    if (it != ids.end()) return it->second;
+    const uint32_t id = (uint32_t)states.size();
+    ids.emplace(k, id);
+    states.push_back(std::move(k));
+    trans.resize(trans.size() + P.ncls, kUnknown);
+    acc.push_back(-1);
+    return id;
+  }
+};
+
+LazyDfa::LazyDfa() = default;
+LazyDfa::~LazyDfa() = default;
+
+RegexStatus LazyDfa::compile(const std::string& pattern, std::string& err, uint64_t max_cache_bytes) {
+  auto im = std::make_unique<Impl>();
+  const RegexStatus st = prepare(pattern, im->P, err);
+  if (st != RegexStatus::Ok) return st;
+  im->max_bytes = std::max<uint64_t>(max_cache_bytes, (uint64_t)im->P.ncls * 4 * 16);
+  im->seen.assign(im->P.nfa.prog.size(), 0);
+  im->reset();
+  impl_ = std::move(im);
+  return RegexStatus::Ok;
+}
+
+uint64_t LazyDfa::cache_flushes() const { return impl_ ? impl_->flushes : 0; }
+
+bool LazyDfa::match(const uint8_t* s, size_t n) const {
+  if (!impl_) return false;
+  Impl& m = *impl_;
+  std::lock_guard<std::mutex> lk(m.mu);
+  const uint32_t ncls = m.P.ncls;
+  uint32_t st = m.intern(StateKey{{}, kTypeBot});
+  StateKey next;
+  size_t i = 0;
+  while (i < n) {
+    int w;
+    const uint32_t r = decode(s + i, n - i, w);
+    i += (size_t)w;
+    const uint32_t c = m.P.cls(r);
+    uint32_t t = m.trans[(size_t)st * ncls + c];
+    if (t == Impl::kUnknown) {
+      if (subset_step(m.P, m.states[st], c, next, m.seen)) return true;   // the MATCH sink
+      // the cache holds at most max_bytes of transitions: when the next state
+      // would pass it, drop every state but the one being entered (RE2's
+      // lazy DFA does the same); the work per input rune stays bounded by the
+      // NFA's size, so the match is linear in the input
+      if (m.ids.find(next) == m.ids.end() && (uint64_t)(m.states.size() + 1) * ncls * 4 > m.max_bytes) {
+        m.reset();
+        m.flushes++;
+        st = m.intern(next);
+        continue;
+      }
+      t = m.intern(next);
+      m.trans[(size_t)st * ncls + c] = t;
+    }
+    if (t == 0) return true;
+    st = t;
+  }
+  if (m.acc[st] < 0) m.acc[st] = subset_accepts_end(m.P, m.states[st], m.seen) ? 1 : 0;
+  return m.acc[st] != 0;
+}
+
+// ---------------- host matcher ----------------
+RegexStatus HostRegexp::compile(const std::string& pattern, std::string& err, uint32_t max_states,
+                                uint64_t max_bytes) {
+  full_ = false;
+  lazy_.reset();
+  RegexStatus st = compile_dfa(pattern, dfa_, err, max_states, max_bytes);
+  if (st == RegexStatus::Ok) {
+    full_ = true;
+    return st;
+  }
+  if (st != RegexStatus::TooLarge) return st;
+  auto lz = std::make_shared<LazyDfa>();
+  err.clear();
+  st = lz->compile(pattern, err, max_bytes);
+  if (st == RegexStatus::Ok) lazy_ = std::move(lz);
+  return st;
+}
+
+bool HostRegexp::match(const uint8_t* s, size_t n) const {
+  if (full_) return dfa_match(dfa_, s, n);
+  return lazy_ && lazy_->match(s, n);
 }
 
 bool dfa_match(const Dfa& d, const uint8_t* s, size_t n) {

@@ -16,10 +16,15 @@
 // any rune use unicode_tables.cpp (generated from ICU 70: Unicode 14.0.0
 // data; the reference's Go 1.25 has 15.0.0: the code points assigned in 15.0
 // are parity unpinned).
-// Unsupported (rejected, never approximated): DFAs above kMaxStates (about
-// two million states) or kMaxTableBytes of transitions.
+// The device tables are bounded: a DFA above kMaxStates (about two million
+// states) or kMaxTableBytes of transitions is TooLarge for the kernels.  On
+// the host (span_attribute json filters, the shim's predicates) HostRegexp
+// takes any such pattern with a lazy DFA (the subset construction run on
+// demand over the input, its state cache bounded and flushed as RE2's is):
+// linear in the input, like Go's regexp, and never refused for its size.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -48,10 +53,42 @@ struct Dfa {
   std::vector<uint8_t> accept_end;        // state accepts at end of text
 };
 
-RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err);
+// max_states / max_table_bytes lower the caps (never above Dfa's).
+RegexStatus compile_dfa(const std::string& pattern, Dfa& out, std::string& err,
+                        uint32_t max_states = Dfa::kMaxStates, uint64_t max_table_bytes = Dfa::kMaxTableBytes);
 
 // Host-side evaluation of a compiled DFA (used by the engine's self-check
 // and unit tests; the kernels implement the same loop).
 bool dfa_match(const Dfa& d, const uint8_t* s, size_t n);
+
+// regexp.MatchString by a lazily built DFA whose transition cache holds at
+// most max_cache_bytes (dropped whole when full).  match() is thread-safe
+// (one mutex: the cache is shared).  Any number of rune classes.
+class LazyDfa {
+ public:
+  LazyDfa();
+  ~LazyDfa();
+  RegexStatus compile(const std::string& pattern, std::string& err, uint64_t max_cache_bytes = 4ull << 20);
+  bool match(const uint8_t* s, size_t n) const;
+  uint64_t cache_flushes() const;   // for tests
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
+// Host matcher: the full DFA when it stays within (max_states,
+// max_table_bytes), else a LazyDfa with a max_table_bytes cache.  Returns
+// Syntax / Unsupported as compile_dfa does; never TooLarge.
+class HostRegexp {
+ public:
+  RegexStatus compile(const std::string& pattern, std::string& err, uint32_t max_states = 65535,
+                      uint64_t max_table_bytes = 16ull << 20);
+  bool match(const uint8_t* s, size_t n) const;
+  bool lazy() const { return lazy_ != nullptr; }
+ private:
+  Dfa dfa_{};
+  bool full_ = false;
+  std::shared_ptr<LazyDfa> lazy_;
+};
 
 }  // namespace ose

@@ -8,6 +8,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <unordered_map>
 
 namespace ose {
 
@@ -431,11 +433,30 @@ struct JsonExpr {
   bool root = false;                    // Path: from $ (else @)
   std::vector<JsonPathStep> steps;      // Path
   std::shared_ptr<const JsonExpr> l, r;
-  std::shared_ptr<Dfa> re;              // Match with a literal pattern
+  std::shared_ptr<HostRegexp> re;       // Match with a literal pattern
   bool re_ok = false;
 };
 
 namespace {
+
+// Patterns met at run time (a filter's `=~` whose right side is not a
+// literal): at most kDynCache per thread, the cache dropped whole when full;
+// nullptr for a pattern regexp.Compile rejects (or one the parser cannot
+// take).  The full DFA is capped at 4096 states / 1 MiB and the lazy DFA's
+// cache at 1 MiB, so one evaluation costs O(pattern + input).
+constexpr size_t kDynCache = 64;
+const HostRegexp* dynamic_regexp(const std::string& pattern) {
+  thread_local std::unordered_map<std::string, std::unique_ptr<HostRegexp>> cache;
+  auto it = cache.find(pattern);
+  if (it != cache.end()) return it->second.get();
+  if (cache.size() >= kDynCache) cache.clear();
+  auto re = std::make_unique<HostRegexp>();
+  std::string err;
+  const bool ok = re->compile(pattern, err, 4096, 1ull << 20) == RegexStatus::Ok;
+  auto& slot = cache[pattern];
+  if (ok) slot = std::move(re);
+  return slot.get();
+}
 
 struct EV {
   bool ok = false;
@@ -541,12 +562,15 @@ EV eval_expr(const JsonExpr& x, const JVal& cur, const JVal& root) {
       if (!ss) return r;
       if (x.re) {
         if (!x.re_ok) return r;
-        return boolean(dfa_match(*x.re, reinterpret_cast<const uint8_t*>(a.v.s.data()), a.v.s.size()));
+        return boolean(x.re->match(reinterpret_cast<const uint8_t*>(a.v.s.data()), a.v.s.size()));
       }
-      Dfa d;
-      std::string err;
-      if (compile_dfa(b.v.s, d, err) != RegexStatus::Ok) return r;
-      return boolean(dfa_match(d, reinterpret_cast<const uint8_t*>(a.v.s.data()), a.v.s.size()));
+      // a pattern taken from the span's own JSON: compiled with small caps
+      // (a lazy DFA past them, so a pathological pattern costs bounded time
+      // and memory per evaluation and still decides as Go's regexp would),
+      // and cached per thread by pattern
+      const HostRegexp* re = dynamic_regexp(b.v.s);
+      if (!re) return r;   // regexp.Compile error: gval's =~ fails, the operand is an error
+      return boolean(re->match(reinterpret_cast<const uint8_t*>(a.v.s.data()), a.v.s.size()));
     }
     default: return r;
   }
@@ -608,11 +632,11 @@ struct ExprParser {
         if (!r) return nullptr;
         P x = bin(o.op, l, r);
         if (o.op == JsonExpr::Match && r->op == JsonExpr::Lit && r->lit.t == JVal::Str) {
-          x->re = std::make_shared<Dfa>();
+          x->re = std::make_shared<HostRegexp>();
           std::string e;
-          const RegexStatus st = compile_dfa(r->lit.s, *x->re, e);
+          const RegexStatus st = x->re->compile(r->lit.s, e);
           if (st == RegexStatus::Ok) x->re_ok = true;
-          else if (st != RegexStatus::Syntax) {   // a pattern the DFA compiler cannot take: refuse
+          else if (st != RegexStatus::Syntax) {   // syntax Go accepts but the parser does not: refuse
             err = "regexp in a jsonpath filter: " + e;
             return nullptr;
           }
@@ -1005,7 +1029,7 @@ std::string SpanAttrPredicate::compile(const SpanAttributeRule& r) {
   expected_ = r.expected_value;
   if (cond_ == "string" && op_ == "regex") {
     std::string err;
-    RegexStatus st = compile_dfa(expected_, re_, err);
+    RegexStatus st = re_.compile(expected_, err);
     if (st == RegexStatus::Ok) re_ok_ = true;
     else if (st == RegexStatus::Syntax) re_ok_ = false;   // regexp.Compile error: the span is skipped (:171-174)
     else return "span_attribute regex not supported by the DFA compiler: " + err;
@@ -1032,7 +1056,7 @@ bool SpanAttrPredicate::eval(const Value& attr) const {
     if (op_ == "not_equals") return v != expected_;
     if (op_ == "contains") return v.find(expected_) != std::string::npos;
     if (op_ == "not_contains") return v.find(expected_) == std::string::npos;
-    if (op_ == "regex") return re_ok_ && dfa_match(re_, reinterpret_cast<const uint8_t*>(v.data()), v.size());
+    if (op_ == "regex") return re_ok_ && re_.match(reinterpret_cast<const uint8_t*>(v.data()), v.size());
     return false;
   }
   if (cond_ == "number") {
@@ -1084,6 +1108,27 @@ bool SpanAttrPredicate::eval(const Value& attr) const {
   return false;
 }
 
+// A string "regex" rule whose DFA passes the device tables' bounds
+// (Dfa::kMaxStates / kMaxTableBytes) is evaluated by the shim like a json
+// rule (SpanAttrPredicate's HostRegexp takes it with a lazy DFA) instead of
+// refusing the config; the answer per pattern is kept for the process.
+bool regex_fits_device(const std::string& pattern) {
+  static std::mutex mu;
+  static std::map<std::string, bool> known;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = known.find(pattern);
+    if (it != known.end()) return it->second;
+  }
+  Dfa d;
+  std::string err;
+  const bool fits = compile_dfa(pattern, d, err) != RegexStatus::TooLarge;
+  std::lock_guard<std::mutex> lk(mu);
+  if (known.size() > 4096) known.clear();
+  known[pattern] = fits;
+  return fits;
+}
+
 AttrPlan plan_attr_rules(const SamplingConfig& c) {
   AttrPlan p;
   int k = 0;
@@ -1091,7 +1136,9 @@ AttrPlan plan_attr_rules(const SamplingConfig& c) {
     for (auto& r : *lvl) {
       if (r.rtype != RuleType::SpanAttribute) continue;
       if ((size_t)k / 64 >= p.host_mask.size()) p.host_mask.push_back(0);
-      if (r.attr.condition_type == "json") {
+      const bool host_regex = r.attr.condition_type == "string" && r.attr.operation == "regex" &&
+                              !regex_fits_device(r.attr.expected_value);
+      if (r.attr.condition_type == "json" || host_regex) {
         p.rule_key.push_back(-1);
         p.host_mask[k / 64] |= 1ull << (k % 64);
       } else {

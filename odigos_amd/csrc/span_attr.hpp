@@ -10,7 +10,7 @@
 //   encoding/json  Unmarshal validity (RFC 8259; numbers must fit float64),
 //                  Marshal of nested values (sorted keys, HTML escaping)
 //   strconv        ParseFloat, ParseBool, FormatFloat(v, 'f', -1, 64)
-//   regexp         the DFA compiler of regex_dfa.hpp
+//   regexp         regex_dfa.hpp's HostRegexp (full DFA, lazy DFA past its caps)
 //   PaesslerAG/jsonpath v0.1.1  Get: $, .key, ['key'], ["key"], [index]
 //                  (pinned by the KATs); the ambiguous selectors *, [*],
 //                  [a,b], [a:b:c], ..  return the match list (parity
@@ -57,7 +57,7 @@ class SpanAttrPredicate {
  private:
   std::string service_, key_, cond_, op_, expected_;
   bool re_ok_ = false;
-  Dfa re_;
+  HostRegexp re_;
   bool num_ok_ = false;
   double num_ = 0;
   bool bool_ok_ = false, bool_ = false;

@@ -936,7 +936,8 @@ struct PutOr {
 };
 
 
-constexpr uint32_t kBNames = 1024;    // braced names for template ids 0..14, '/' at byte 0
+constexpr uint32_t kBNames = 1024;    // braced names for template ids 0..14, each after a '/'
+typedef __attribute__((address_space(3))) uint16_t lds_w16;
 
 struct BracedNames {
   __attribute__((aligned(16))) uint8_t b[kBNames + 16];
@@ -945,19 +946,22 @@ struct BracedNames {
   uint32_t ok;
 };
 
-// "{name}" for ids 0..14 (the ids a plan code can carry), once per workgroup.
+// "{name}" for ids 0..14 (the ids a plan code can carry), once per workgroup,
+// as "/{id}/{date}/{email}/...": the byte before every name is '/' (the
+// assembly copies an entry's separator with its body).
 __device__ void load_braced_names(const Cfg& cfg, BracedNames& bn) {
   if (threadIdx.x == 0) {
     const uint32_t nn = min(cfg.h->n_names, 15u);
-    uint32_t o = 4;
+    uint32_t o = 1;
     bool ok = true;
     bn.b[0] = '/';
     for (uint32_t id = 0; id < nn; id++) {
       const uint32_t l = cfg.name(id).len + 2;
-      if (o + l > kBNames || l > 255) { ok = false; break; }
+      if (o + l + 1 > kBNames || l > 255) { ok = false; break; }
       bn.off[id] = (uint16_t)o;
       bn.len[id] = (uint8_t)l;
-      o += l;
+      bn.b[o + l] = '/';
+      o += l + 1;
     }
     bn.ok = ok ? 1u : 0u;
   }
@@ -1410,6 +1414,8 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
     img[local] = '/';
   }
   const uint32_t total = lane_value(off + nseg, kWave - 1);
+  const lds_u32* Lw = (const lds_u32*)L;
+  lds_w32* img32 = (lds_w32*)img;
   uint32_t carry = 0;
   for (uint32_t x0 = 0; x0 < total; x0 += kWave) {
     const uint32_t x = x0 + (uint32_t)lane;
@@ -1421,40 +1427,53 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
     carry += stot;
     if (v) {
       const uint32_t pos = (uint32_t)(((int32_t)(opk << 16) >> 16) + (int32_t)E);
-      const bool slash = x != ((opk >> 16) & 0xFFu) || (opk >> 24);
+      const bool first = x == ((opk >> 16) & 0xFFu);
+      const bool slash = !first || (opk >> 24);
       const int id = (int)(c & 0xFFu) - 1;
       // both candidates read unconditionally (a branch on id >= 0 cost the
       // step its exec-mask bookkeeping)
-      // builtin (no custom ids): "{id}" "{date}" "{email}" at 4, 8 and 14 of
+      // builtin (no custom ids): "{id}" "{date}" "{email}" at 1, 6 and 13 of
       // the braced table (load_braced_names), no LDS read
       const uint32_t idc = id >= 0 ? (uint32_t)id : 0u;
-      const uint32_t boff = builtin ? (idc == 0 ? 4u : idc == 1 ? 8u : 14u) : (uint32_t)bn.off[idc];
+      const uint32_t boff = builtin ? (idc == 0 ? 1u : idc == 1 ? 6u : 13u) : (uint32_t)bn.off[idc];
       const uint32_t blen = builtin ? (idc == 0 ? 4u : idc == 1 ? 6u : 7u) : (uint32_t)bn.len[idc];
       const uint32_t so = id >= 0 ? bn_src + boff : stage_src + (ent & 0xFFFu);   // the body's LDS byte offset
       const uint32_t n = id >= 0 ? blen : (ent >> 12) & 0x1FFFu;
-      if (slash) img[pos] = '/';
-      lds_out_u8* dp = img + pos + 1;
-      const lds_u8* sp = L + so;
-      // gfx950 LDS takes unaligned 8-, 4- and 2-byte accesses: one 8-byte read
-      // per 8 source bytes (reads past n stay inside the stage / name table)
-      // and whole 8-byte stores, then the last 1-7 bytes once after the loop:
-      // two overlapping 4- or 2-byte stores (both inside the entry) or one
-      // byte (the tail's branches were inside every iteration before)
-      const uint32_t nf = n & ~7u, rem = n & 7u;
-      for (uint32_t q = 0; q < nf; q += 8)
-        *reinterpret_cast<lds_w64u*>(dp + q) = *reinterpret_cast<const lds_u64u*>(sp + q);
-      if (rem) {
-        const uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + nf);
-        if (rem >= 4) {
-          *reinterpret_cast<lds_w32u*>(dp + nf) = (uint32_t)v;
-          *reinterpret_cast<lds_w32u*>(dp + n - 4) = (uint32_t)(v >> (8 * (rem - 4)));
-        } else if (rem >= 2) {
-          *reinterpret_cast<lds_w16u*>(dp + nf) = (uint16_t)v;
-          *reinterpret_cast<lds_w16u*>(dp + n - 2) = (uint16_t)(v >> (8 * (rem - 2)));
-        } else {
-          dp[nf] = (uint8_t)v;
-        }
+      // output bytes [o0, o1): the separator (when written) and the body.
+      // The byte before a body in LDS is '/' (a segment follows a '/' of
+      // its path; the braced table puts one before every name), so the
+      // separator comes with the body; only a path's first entry can lack
+      // it, and gets its '/' stored after.  Every LDS access is naturally
+      // aligned: gfx950 replays a misaligned access at 64 cycles per wave
+      // instruction (the unaligned 8-byte copy this replaced spent about
+      // two thirds of the kernel's LDS cycles in that replay).  Whole
+      // dwords of the range are written as funnel-shifted aligned source
+      // reads; the 0-3 bytes at either end as byte / short stores.
+      const uint32_t o0 = slash ? pos : pos + 1, o1 = pos + 1 + n;
+      const uint32_t sa = slash ? so - 1 : so;   // source of output byte o0
+      const uint32_t delta = sa - o0;            // source = output + delta (mod 2^32)
+      const uint32_t A0 = (o0 + 3) & ~3u, B0 = o1 & ~3u, hend = min(A0, o1);
+      const uint32_t h = __builtin_amdgcn_alignbyte(Lw[(sa >> 2) + 1], Lw[sa >> 2], sa & 3u);
+      const uint32_t a2 = (o0 + 1) & ~1u;
+      const bool h16 = a2 + 2 <= hend;
+      const uint32_t nx = h16 ? a2 + 2 : a2;
+      if ((o0 & 1u) && o0 < hend) img[o0] = (uint8_t)h;
+      if (h16) *reinterpret_cast<lds_w16*>(img + a2) = (uint16_t)(h >> (8 * (a2 - o0)));
+      if (nx < hend) img[nx] = (uint8_t)(h >> (8 * (nx - o0)));
+      const uint32_t sh = delta & 3u;
+      uint32_t q = (A0 + delta) >> 2;
+      uint32_t w0 = Lw[q];
+      for (uint32_t d = A0; d < B0; d += 4) {
+        const uint32_t w1 = Lw[++q];
+        img32[d >> 2] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        w0 = w1;
       }
+      if (B0 >= A0 && B0 < o1) {   // tail [B0, o1): 1-3 bytes
+        const uint32_t t = __builtin_amdgcn_alignbyte(Lw[q + 1], w0, sh), tl = o1 - B0;
+        if (tl >= 2) *reinterpret_cast<lds_w16*>(img + B0) = (uint16_t)t;
+        if (tl & 1u) img[B0 + (tl & 2u)] = (uint8_t)(t >> (8 * (tl & 2u)));
+      }
+      if (slash && first) img[pos] = '/';
     }
   }
 }

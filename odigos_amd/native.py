@@ -212,6 +212,8 @@ def lib() -> C.CDLL:
         "osehost_as_string": (_p, [C.c_char_p]),
         "osehost_free": (None, [_p]),
         "osehost_regex_match": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+        "osehost_regex_match_host": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint64,
+                                               C.POINTER(C.c_int)]),
         "osehost_span_attr_eval": (C.c_int, [C.c_char_p, C.c_char_p]),
     }
     for name, (res, args) in sig.items():

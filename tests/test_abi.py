@@ -35,3 +35,14 @@ def test_no_device_is_loud():
         return
     h = C.c_void_p()
     assert native.lib().ose_engine_create(b'{"odigosurltemplate": {}}', C.byref(h)) == native.OSE_EDEVICE
+
+
+def test_blob_offsets_guarded(tmp_path):
+    # device-table sections past 4 GiB are refused (blob.hpp), never wrapped
+    import subprocess
+    from pathlib import Path
+    src = Path(__file__).with_name("blob_check.cpp")
+    exe = tmp_path / "blob_check"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", str(exe), str(src)], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout

@@ -131,3 +131,84 @@ def test_unsupported_is_reported_not_guessed():
     # what the DFA compiler still refuses is a DFA over its state budget
     assert native.lib().osehost_regex_match(r"\p{Greek}".encode(), b"", 0) == 0
     assert native.lib().osehost_regex_match(r"(a|b)*a(a|b){20}".encode(), b"", 0) == -2
+
+
+def _host(pattern, s: bytes, max_states=65535, max_bytes=16 << 20):
+    import ctypes
+    lazy = ctypes.c_int(-1)
+    r = native.lib().osehost_regex_match_host(pattern.encode(), s, len(s), max_states, max_bytes, ctypes.byref(lazy))
+    assert r >= 0, (pattern, r)
+    return bool(r), lazy.value
+
+
+@pytest.mark.parametrize("pattern", PATTERNS + [p for p, _, _ in NON_ASCII])
+def test_lazy_dfa_equals_full_dfa(pattern):
+    # HostRegexp forced onto the lazy DFA (a 1-state cap sends every pattern
+    # there; a 4 KiB cache makes the larger ones flush it mid-string) decides
+    # as the full DFA does
+    rng = random.Random(hash(pattern) & 0xFFF)
+    strings = _rand_strings(rng, 200) + [s for p, s, _ in NON_ASCII if p == pattern]
+    for s in strings:
+        want = _dfa(pattern, s)
+        got, lazy = _host(pattern, s, max_states=1, max_bytes=4096)
+        assert lazy == 1 and got == want, (pattern, s)
+        got2, lazy2 = _host(pattern, s)
+        assert lazy2 == 0 and got2 == want, (pattern, s)
+
+
+def test_lazy_dfa_takes_what_the_device_refuses():
+    # a DFA of ~2^21 states: refused for the device tables, decided on the
+    # host by the lazy DFA in time linear in the input (the oracle's
+    # backtracker is the reference answer)
+    import time
+    pat = r"(a|b)*a(a|b){20}"
+    assert native.lib().osehost_regex_match(pat.encode(), b"", 0) == -2
+    rng = random.Random(7)
+    orc = Regex(pat)
+    t0 = time.time()
+    for k in range(60):
+        s = "".join(rng.choice("ab") for _ in range(rng.randrange(0, 200))).encode()
+        got, lazy = _host(pat, s)
+        assert lazy == 1 and got == orc.match(s), s
+    assert time.time() - t0 < 30
+    # a long input through a flushing cache stays linear
+    s = ("ab" * 50_000).encode()
+    t0 = time.time()
+    got, lazy = _host(pat, s, max_bytes=64 << 10)
+    assert lazy == 1 and got is True
+    assert time.time() - t0 < 20
+
+
+def test_span_attribute_oversize_regex_runs_on_the_host():
+    # a span_attribute "regex" rule whose DFA passes the device bounds is a
+    # host (shim-evaluated) rule instead of an engine refusal
+    import json
+    rule = {"service_name": "s", "attribute_key": "k", "condition_type": "string", "operation": "regex",
+            "expected_value": r"(a|b)*a(a|b){20}"}
+    v_yes = json.dumps({"stringValue": "b" * 5 + "a" + "b" * 20})
+    v_no = json.dumps({"stringValue": "b" * 30})
+    assert native.lib().osehost_span_attr_eval(json.dumps(rule).encode(), v_yes.encode()) == 1
+    assert native.lib().osehost_span_attr_eval(json.dumps(rule).encode(), v_no.encode()) == 0
+
+
+def test_jsonpath_dynamic_pattern_bounded():
+    # `=~` against a pattern taken from the span's JSON (not a literal):
+    # a pathological pattern is matched by the bounded lazy DFA, as Go's
+    # linear-time regexp would, in bounded time per evaluation
+    import json
+    import time
+    rule = {"service_name": "s", "attribute_key": "k", "condition_type": "json", "operation": "contains_key",
+            "json_path": "$.items[?(@.v =~ @.p)]"}
+    items = [{"v": "b" * 5 + "a" + "b" * 20, "p": r"(a|b)*a(a|b){20}"}]
+    v = json.dumps({"stringValue": json.dumps({"items": items})})
+    t0 = time.time()
+    for _ in range(20):
+        assert native.lib().osehost_span_attr_eval(json.dumps(rule).encode(), v.encode()) == 1
+    assert time.time() - t0 < 20
+    # key_equals on the filtered values: the element passes only when its
+    # value matches its own pattern
+    rule = dict(rule, operation="key_equals", json_path="$.items[?(@.v =~ @.p)].v",
+                expected_value=json.dumps([items[0]["v"]]))
+    assert native.lib().osehost_span_attr_eval(json.dumps(rule).encode(), v.encode()) == 1
+    v = json.dumps({"stringValue": json.dumps({"items": [{"v": "b" * 40, "p": items[0]["p"]}]})})
+    assert native.lib().osehost_span_attr_eval(json.dumps(rule).encode(), v.encode()) == 0
