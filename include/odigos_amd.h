@@ -319,6 +319,14 @@ int ose_engine_get_info(const ose_engine* eng, ose_engine_info* info);
  * (bit k of word w: rule 64w + k); writes min(cap, that) words and returns
  * that count (0 without span_attribute rules).                             */
 uint32_t ose_engine_attr_host_rules(const ose_engine* eng, uint64_t* words, uint32_t cap);
+/* How often the SAMPLE stage left its fast path since the engine was created
+ * (diagnostics and tests; no reference counterpart): counts[0] = calls whose
+ * batch repeated a trace id (the run-list path ran), counts[1] = calls some
+ * trace of which overflowed the run lists and was decided by the radix sort
+ * by trace id, counts[2] = long-run passes (traces still open 4 steps past
+ * their first window).  Synchronises the engine's device.  Writes
+ * min(cap, 3) counters and returns 3.                                      */
+uint32_t ose_engine_path_counts(ose_engine* eng, uint64_t* counts, uint32_t cap);
 
 /* Attribute key k (< n_attr_keys) of the attr_type / attr_val columns; the
  * bytes stay valid for the engine's lifetime.                               */

@@ -239,6 +239,12 @@ class Engine:
         """ose_engine_set_option: the alternative OTLP legs (tests)."""
         native.check(self.L.ose_engine_set_option(self.h, name.encode(), int(value)))
 
+    def path_counts(self) -> dict:
+        """ose_engine_path_counts: how often SAMPLE left its fast path."""
+        c = (C.c_uint64 * 3)()
+        self.L.ose_engine_path_counts(self.h, c, 3)
+        return {"run_list": int(c[0]), "sort": int(c[1]), "long_runs": int(c[2])}
+
     def profile_read(self) -> dict:
         import json
         buf = C.create_string_buffer(1 << 16)

@@ -159,6 +159,7 @@ Engine::~Engine() {
   for (auto* d : sampling_svc_map_dev)
     if (d) (void)hipFree(d);
   if (shard_tables_dev) (void)hipFree(shard_tables_dev);
+  if (path_count_dev) (void)hipFree(path_count_dev);
   if (attr_blob_dev) (void)hipFree(attr_blob_dev);
   if (attr_host_mask_dev) (void)hipFree(attr_host_mask_dev);
   for (auto* w : pool) {
@@ -761,8 +762,32 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
     rc = upload(hm, &e->attr_host_mask_dev);
     if (rc) { delete e; return rc; }
   }
+  {
+    hipError_t he = hipMalloc(reinterpret_cast<void**>(&e->path_count_dev), 64);
+    if (he == hipSuccess) he = hipMemset(e->path_count_dev, 0, 64);
+    if (he != hipSuccess) {
+      delete e;
+      return fail(OSE_EDEVICE, std::string("path counters: ") + hipGetErrorString(he));
+    }
+  }
   *out = reinterpret_cast<ose_engine*>(e);
   return 0;
+}
+
+uint32_t ose_engine_path_counts(ose_engine* eng, uint64_t* counts, uint32_t cap) {
+  if (!eng) return 0;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  uint64_t c[3] = {0, 0, e->long_run_passes.load()};
+  if (e->path_count_dev && bind_device(e) == 0) {
+    LastErrorScope keep("ose_engine_path_counts");
+    // counters the queued work has not reached yet are not counted: the
+    // device is synchronised first
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(c, e->path_count_dev, 16, hipMemcpyDeviceToHost) != hipSuccess)
+      c[0] = c[1] = 0;
+  }
+  for (uint32_t k = 0; k < 3 && k < cap && counts; k++) counts[k] = c[k];
+  return 3;
 }
 
 void ose_engine_destroy(ose_engine* eng) {

@@ -141,6 +141,10 @@ struct Engine {
   // chunk table pointers then those words (ShardArgs::cfgs, ::lat_svc)
   std::vector<uint32_t> sampling_lat_svc;
   uint8_t* shard_tables_dev = nullptr;
+  // which slow paths the trace stage took (ose_engine_path_counts): [0] run
+  // lists, [1] the radix sort (device counters), [2] long-run passes (host)
+  unsigned long long* path_count_dev = nullptr;
+  std::atomic<uint64_t> long_run_passes{0};
   std::unordered_map<std::string, uint32_t> service_ids;
   uint32_t sampling_n_lat = 0, sampling_n_attr = 0;
   uint32_t sampling_n_lat_svc = 0;   // services with http_latency rules (trace_multi_kernel takes <= 64)

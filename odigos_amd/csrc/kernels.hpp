@@ -255,6 +255,7 @@ struct TraceKernelArgs {
   uint32_t* run_count;        // [table slots] runs listed per slot
   uint32_t* runs;             // [table slots * kMaxRuns] run-head positions
   uint32_t* overflow;         // set when a trace needs the sort-based path
+  unsigned long long* path_count;   // engine counters (ose_engine_path_counts): [0] += 1 per run-list pass
   uint64_t* win_first;        // [n_windows] heads that start a trace (first run only)
   uint32_t* head_slot;        // [n_spans] exact-table slot of each run head
 };
@@ -303,6 +304,7 @@ struct TraceSortArgs {
   uint32_t* hist;             // [256 * n_tiles] digit-major
   uint32_t* key;              // canonical key per span (trace_key kernel output)
   uint32_t* error;
+  unsigned long long* path_count;   // [1] += 1 per call the sort path decided (gate open)
   // sort_hist_kernel zeroes the following scan's tile counter and look-back
   // status (only when the gate is open: no memset launches per closed call)
   uint32_t* scan_counter;

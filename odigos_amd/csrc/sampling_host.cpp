@@ -576,6 +576,7 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     e->prof_end(td, st);
   }
   auto long_pass = [=](uint32_t known_runs) -> int {
+    e->long_run_passes.fetch_add(1, std::memory_order_relaxed);
     Engine::Timed tl{};
     e->prof_begin("trace_long_kernel", st, tl);
     launch_trace_long(a, st, known_runs);   // (trace_long_plan_kernel, then the pieces)
@@ -604,6 +605,7 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     rl.run_count = ws->run_count;
     rl.runs = ws->runs;
     rl.overflow = overflow;
+    rl.path_count = e->path_count_dev;
     rl.win_first = win_first;
     rl.head_slot = key;
     Engine::Timed tr{};
@@ -627,6 +629,7 @@ int run_sampling_pass(Engine* e, const ose_columns* c, const ose_outputs* o, uin
     s.epoch = a.epoch;
     s.key = key;
     s.error = err;
+    s.path_count = e->path_count_dev;
     // (the run-list kernel already put every run head in the exact table)
     launch_trace_key(s, st);
     HIP_TRY(hipGetLastError());

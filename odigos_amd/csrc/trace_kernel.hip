@@ -1819,6 +1819,7 @@ __global__ __launch_bounds__(256) void trace_insert_exact_kernel(TraceKernelArgs
 // *overflow, and the sort-based path (gated on it) recomputes the batch.
 __global__ __launch_bounds__(256) void trace_runs_kernel(TraceKernelArgs a) {
   if (__hip_atomic_load(a.dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  if (a.path_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.path_count, 1ull);
   const int lane = threadIdx.x & 63;
   for (uint64_t w = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWave; w < a.n_windows;
        w += (uint64_t)gridDim.x * (256 / kWave)) {
@@ -1961,6 +1962,7 @@ __global__ __launch_bounds__(256) void trace_first_select_kernel(TraceKernelArgs
 // the table the fast path filled).
 __global__ __launch_bounds__(256) void trace_key_kernel(TraceSortArgs a) {
   if (gated(a.gate)) return;
+  if (a.path_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.path_count + 1, 1ull);
   const uint32_t ready = (a.epoch << 2) | 2u;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n_spans; i += (uint64_t)gridDim.x * 256) {
     const uint64_t hi = a.tid[2 * i], lo = a.tid[2 * i + 1];

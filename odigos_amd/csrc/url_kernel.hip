@@ -34,6 +34,10 @@
 #include "size_device.hpp"
 #include "url_classes.hpp"
 
+#ifndef OSE_ASM_BATCH
+#define OSE_ASM_BATCH 0
+#endif
+
 namespace ose {
 namespace {
 
@@ -1414,8 +1418,6 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
     img[local] = '/';
   }
   const uint32_t total = lane_value(off + nseg, kWave - 1);
-  const lds_u32* Lw = (const lds_u32*)L;
-  lds_w32* img32 = (lds_w32*)img;
   uint32_t carry = 0;
   for (uint32_t x0 = 0; x0 < total; x0 += kWave) {
     const uint32_t x = x0 + (uint32_t)lane;
@@ -1427,8 +1429,7 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
     carry += stot;
     if (v) {
       const uint32_t pos = (uint32_t)(((int32_t)(opk << 16) >> 16) + (int32_t)E);
-      const bool first = x == ((opk >> 16) & 0xFFu);
-      const bool slash = !first || (opk >> 24);
+      const bool slash = x != ((opk >> 16) & 0xFFu) || (opk >> 24);
       const int id = (int)(c & 0xFFu) - 1;
       // both candidates read unconditionally (a branch on id >= 0 cost the
       // step its exec-mask bookkeeping)
@@ -1439,41 +1440,47 @@ __device__ __forceinline__ void assemble_group(lds_out_u8* img, const lds_u8* L,
       const uint32_t blen = builtin ? (idc == 0 ? 4u : idc == 1 ? 6u : 7u) : (uint32_t)bn.len[idc];
       const uint32_t so = id >= 0 ? bn_src + boff : stage_src + (ent & 0xFFFu);   // the body's LDS byte offset
       const uint32_t n = id >= 0 ? blen : (ent >> 12) & 0x1FFFu;
-      // output bytes [o0, o1): the separator (when written) and the body.
-      // The byte before a body in LDS is '/' (a segment follows a '/' of
-      // its path; the braced table puts one before every name), so the
-      // separator comes with the body; only a path's first entry can lack
-      // it, and gets its '/' stored after.  Every LDS access is naturally
-      // aligned: gfx950 replays a misaligned access at 64 cycles per wave
-      // instruction (the unaligned 8-byte copy this replaced spent about
-      // two thirds of the kernel's LDS cycles in that replay).  Whole
-      // dwords of the range are written as funnel-shifted aligned source
-      // reads; the 0-3 bytes at either end as byte / short stores.
-      const uint32_t o0 = slash ? pos : pos + 1, o1 = pos + 1 + n;
-      const uint32_t sa = slash ? so - 1 : so;   // source of output byte o0
-      const uint32_t delta = sa - o0;            // source = output + delta (mod 2^32)
-      const uint32_t A0 = (o0 + 3) & ~3u, B0 = o1 & ~3u, hend = min(A0, o1);
-      const uint32_t h = __builtin_amdgcn_alignbyte(Lw[(sa >> 2) + 1], Lw[sa >> 2], sa & 3u);
-      const uint32_t a2 = (o0 + 1) & ~1u;
-      const bool h16 = a2 + 2 <= hend;
-      const uint32_t nx = h16 ? a2 + 2 : a2;
-      if ((o0 & 1u) && o0 < hend) img[o0] = (uint8_t)h;
-      if (h16) *reinterpret_cast<lds_w16*>(img + a2) = (uint16_t)(h >> (8 * (a2 - o0)));
-      if (nx < hend) img[nx] = (uint8_t)(h >> (8 * (nx - o0)));
-      const uint32_t sh = delta & 3u;
-      uint32_t q = (A0 + delta) >> 2;
-      uint32_t w0 = Lw[q];
-      for (uint32_t d = A0; d < B0; d += 4) {
-        const uint32_t w1 = Lw[++q];
-        img32[d >> 2] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        w0 = w1;
+      // gfx950 LDS takes misaligned 8-, 4- and 2-byte accesses: one 8-byte
+      // read per 8 source bytes (reads past n stay inside the stage / name
+      // table) and whole 8-byte stores, then the last 1-7 bytes once after
+      // the loop: two overlapping 4- or 2-byte stores (both inside the entry)
+      // or one byte.  The hardware replays each misaligned access (PMC
+      // SQ_LDS_UNALIGNED_STALL, two thirds of this kernel's LDS cycles on
+      // C2), yet an all-aligned form (funnel-shifted dword copies, byte and
+      // short stores at the ends) measured 5 % slower on C2 and C4, and
+      // reading the first 16 bytes before any store 1-3 % slower: the LDS
+      // pipe (21 % busy) is not what bounds this kernel, its instruction
+      // latency chains are (profiles/r6e_asm_aligned_ab.txt,
+      // r6f_asm_details_ab.txt).
+      if (slash) img[pos] = '/';
+      lds_out_u8* dp = img + pos + 1;
+      const lds_u8* sp = L + so;
+      const uint32_t nf = n & ~7u, rem = n & 7u;
+#if OSE_ASM_BATCH   // diagnostics A/B: the first 16 bytes read before any store
+      const uint64_t u0 = *reinterpret_cast<const lds_u64u*>(sp), u1 = *reinterpret_cast<const lds_u64u*>(sp + 8);
+      const uint64_t ut = *reinterpret_cast<const lds_u64u*>(sp + nf);
+      if (nf > 0) *reinterpret_cast<lds_w64u*>(dp) = u0;
+      if (nf > 8) *reinterpret_cast<lds_w64u*>(dp + 8) = u1;
+      for (uint32_t q = 16; q < nf; q += 8)
+        *reinterpret_cast<lds_w64u*>(dp + q) = *reinterpret_cast<const lds_u64u*>(sp + q);
+      if (rem) {
+        const uint64_t v = ut;
+#else
+      for (uint32_t q = 0; q < nf; q += 8)
+        *reinterpret_cast<lds_w64u*>(dp + q) = *reinterpret_cast<const lds_u64u*>(sp + q);
+      if (rem) {
+        const uint64_t v = *reinterpret_cast<const lds_u64u*>(sp + nf);
+#endif
+        if (rem >= 4) {
+          *reinterpret_cast<lds_w32u*>(dp + nf) = (uint32_t)v;
+          *reinterpret_cast<lds_w32u*>(dp + n - 4) = (uint32_t)(v >> (8 * (rem - 4)));
+        } else if (rem >= 2) {
+          *reinterpret_cast<lds_w16u*>(dp + nf) = (uint16_t)v;
+          *reinterpret_cast<lds_w16u*>(dp + n - 2) = (uint16_t)(v >> (8 * (rem - 2)));
+        } else {
+          dp[nf] = (uint8_t)v;
+        }
       }
-      if (B0 >= A0 && B0 < o1) {   // tail [B0, o1): 1-3 bytes
-        const uint32_t t = __builtin_amdgcn_alignbyte(Lw[q + 1], w0, sh), tl = o1 - B0;
-        if (tl >= 2) *reinterpret_cast<lds_w16*>(img + B0) = (uint16_t)t;
-        if (tl & 1u) img[B0 + (tl & 2u)] = (uint8_t)(t >> (8 * (tl & 2u)));
-      }
-      if (slash && first) img[pos] = '/';
     }
   }
 }
@@ -1647,6 +1654,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
                        bn_src, p, seg_off, local, cfg.n_custom == 0);
       wave_lds_sync();
       uint4* dst = reinterpret_cast<uint4*>(a.scratch + region + scr_used);
+      // two 1 KiB rows of the image per round: both reads in flight before
+      // the stores (the image is at most kImgCap bytes, < 5 rows)
+      // (two rows per round, both reads before the stores, measured 2 %
+      // slower on C4: profiles/r6f_asm_details_ab.txt)
       for (uint32_t k = lane; k < n16; k += kWave) {
         const u32x4 v = img4[k];
         dst[k] = make_uint4(v.x, v.y, v.z, v.w);

@@ -181,8 +181,9 @@ def test_oracle_levels_cover_all_outcomes():
 
 
 # ---------------- GPU parity ----------------
-def gpu_vs_oracle(g, mode=native.GROUP_TRACE_ID, cfg=CFG, per_trace=True, seed=SEED, kernels=None):
-    """kernels: a set the names of the launches the call profiled are added to"""
+def gpu_vs_oracle(g, mode=native.GROUP_TRACE_ID, cfg=CFG, per_trace=True, seed=SEED, kernels=None, paths=None):
+    """kernels: a set the names of the launches the call profiled are added to;
+    paths: a dict that receives the engine's slow-path counts after the call"""
     import torch
     from odigos_amd.batch import DeviceBatch, Engine
     eng = Engine({"odigossampling": cfg})
@@ -196,6 +197,8 @@ def gpu_vs_oracle(g, mode=native.GROUP_TRACE_ID, cfg=CFG, per_trace=True, seed=S
     torch.cuda.synchronize()
     if kernels is not None:
         kernels.update(eng.profile_read())
+    if paths is not None:
+        paths.update(eng.path_counts())
     assert int(db.out_numpy("device_status", np.uint32)[0]) == 0
     ho = oracle_run(g.cols, mode, seed=seed, cfg=cfg)
     n = g.cols.n_spans
@@ -322,7 +325,55 @@ def test_gpu_sampling_long_runs_split(seed):
 def test_gpu_sampling_long_runs_slow_path():
     # shuffled Zipf traces: split runs send the batch down the sort-based
     # path, which must overwrite the long-run decisions of the fast pass
-    gpu_vs_oracle(Generator("zipf", seed=0x0D160305, n_spans=300_000, shuffle=True))
+    paths = {}
+    gpu_vs_oracle(Generator("zipf", seed=0x0D160305, n_spans=300_000, shuffle=True), paths=paths)
+    # a Zipf trace of more than 4096 spans in several runs overflows the run
+    # lists: the radix sort by trace id decided this batch
+    assert paths["run_list"] == 1 and paths["sort"] == 1, paths
+
+
+def interleave(g, period):
+    """The sampling columns of the spans reordered by residue mod `period`
+    (spans 0, p, 2p, ..., then 1, p+1, ...): a trace of at least `period`
+    spans becomes `period` runs scattered through the batch.  resource
+    stays in place (it must stay non-decreasing), so a span takes the
+    resource of its new position: a different but valid batch."""
+    import ctypes as C
+    n = g.cols.n_spans
+    order = np.concatenate([np.arange(k, n, period) for k in range(period)])   # new p <- old order[p]
+    for name, ctype, w in (("trace_id", C.c_uint64, 2), ("start_ns", C.c_uint64, 1), ("end_ns", C.c_uint64, 1),
+                           ("status", C.c_uint8, 1), ("route", C.c_uint32, 2)):
+        a = _arr(getattr(g.cols, name), ctype, w * n).reshape(n, w)
+        a[:] = a[order].copy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("period,n", [(9, 5000), (16, 100_000), (33, 300_000)])
+def test_gpu_sampling_sort_path_decides(period, n):
+    # SURVEY §8 a-1 / north_star's "LDS radix sort by trace_id": traces cut
+    # into more than 8 runs (traces of >= period spans) overflow the run-list path (trace_fold_kernel),
+    # so the batch is decided by the stable radix sort by first run head and
+    # trace_eval_kernel over the sorted permutation; keep, trace order,
+    # levels and ratios equal the oracle, and the engine's counters show the
+    # sort path ran
+    g = Generator("sampling", seed=0x0D160503 + period, n_spans=n)
+    interleave(g, period)
+    paths = {}
+    gpu_vs_oracle(g, paths=paths)
+    assert paths["run_list"] == 1 and paths["sort"] == 1, paths
+
+
+@pytest.mark.gpu
+def test_gpu_sampling_run_list_without_sort():
+    # a trace split into 2 runs stays on the run-list path: no sort
+    g = Generator("sampling", seed=0x0D160603, n_spans=20_000)
+    import ctypes as C
+    n = g.cols.n_spans
+    tid = _arr(g.cols.trace_id, C.c_uint64, 2 * n).reshape(n, 2)
+    tid[n - 1] = tid[0]   # the first trace reappears as the batch's last span
+    paths = {}
+    gpu_vs_oracle(g, paths=paths)
+    assert paths["run_list"] == 1 and paths["sort"] == 0, paths
 
 
 @pytest.mark.gpu
