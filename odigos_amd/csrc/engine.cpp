@@ -158,6 +158,7 @@ Engine::~Engine() {
     if (d) (void)hipFree(d);   // (sampling_blob_dev is the first)
   for (auto* d : sampling_svc_map_dev)
     if (d) (void)hipFree(d);
+  if (sampling_svc_maps_dev) (void)hipFree(sampling_svc_maps_dev);
   if (shard_tables_dev) (void)hipFree(shard_tables_dev);
   if (path_count_dev) (void)hipFree(path_count_dev);
   if (attr_blob_dev) (void)hipFree(attr_blob_dev);
@@ -709,6 +710,12 @@ int ose_engine_create(const char* cfg_json, ose_engine** out) {
       std::vector<uint8_t> raw(reinterpret_cast<const uint8_t*>(m.data()),
                                reinterpret_cast<const uint8_t*>(m.data()) + 4 * m.size());
       rc = upload(raw, reinterpret_cast<uint8_t**>(&e->sampling_svc_map_dev[k]));
+      if (rc) { delete e; return rc; }
+    }
+    if (!e->sampling_svc_map_dev.empty()) {
+      std::vector<uint8_t> raw(sizeof(uint32_t*) * e->sampling_svc_map_dev.size());
+      std::memcpy(raw.data(), e->sampling_svc_map_dev.data(), raw.size());
+      rc = upload(raw, reinterpret_cast<uint8_t**>(&e->sampling_svc_maps_dev));
       if (rc) { delete e; return rc; }
     }
     const size_t K = e->sampling_chunks_dev.size(), L = e->sampling_lat_svc.size();

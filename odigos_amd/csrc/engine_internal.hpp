@@ -162,6 +162,7 @@ struct Engine {
   bool sampling_local_svc = false;
   std::vector<std::vector<uint32_t>> sampling_svc_map_host;
   std::vector<uint32_t*> sampling_svc_map_dev;
+  uint32_t** sampling_svc_maps_dev = nullptr;   // the K map pointers on the device (ShardArgs / OwnerArgs::svc_maps)
   // span_attribute rules: all of them (attr_n_rules), the GPU-evaluated ones
   // (attr_n_dev, attr_kernel.hip) and the keys those read
   std::vector<uint8_t> attr_blob_host;

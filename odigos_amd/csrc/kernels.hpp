@@ -368,6 +368,9 @@ struct ShardArgs {
   const uint8_t* const* cfgs;  // [n_chunks] SampCfgDev blobs (device array of the rule chunks' tables)
   uint32_t n_chunks;
   const uint32_t* lat_svc;    // bit s: service s has an http_latency rule in some chunk
+  uint32_t n_global_svc;      // services the engine interned (res_svc / res_svc_str / lat_svc index them)
+  const uint32_t* const* svc_maps;   // [n_chunks] global -> chunk-local service id (0xFFFFFFFF: not in the
+                                     // chunk), or null when every chunk indexes global ids (dense tables)
   uint32_t cfg_lds_bytes;     // the chunk tables copied into LDS by shard_scatter_kernel (sum of their 16-aligned
                               // sizes), 0: read from HBM
   uint32_t* hist;             // [n_ranks * n_tiles] counts, then offsets (second buffer)
@@ -418,6 +421,8 @@ struct OwnerArgs {
   uint64_t* bkt_rec;          // [n_buckets * kOwnerCap * kOwnerSlotWords] the records' slots
   const uint8_t* const* cfgs; // [n_chunks] SampCfgDev blobs
   uint32_t n_chunks;
+  const uint32_t* const* svc_maps;   // as ShardArgs::svc_maps (records carry global service ids)
+  uint32_t n_global_svc;
   uint32_t cfg_lds_bytes;     // dynamic LDS: the largest chunk table without its route bytes (16-aligned)
   uint64_t seed;
   uint8_t* keep;              // [n] per record

@@ -369,6 +369,8 @@ int owner_decide(Engine* e, XScratch* xs, const uint8_t* recvb, uint64_t n_recv,
   oa.bkt_rec = reinterpret_cast<uint64_t*>(bb + off_rec);
   oa.cfgs = reinterpret_cast<const uint8_t* const*>(e->shard_tables_dev);
   oa.n_chunks = K;
+  oa.n_global_svc = (uint32_t)e->service_ids.size();
+  oa.svc_maps = e->sampling_local_svc ? e->sampling_svc_maps_dev : nullptr;
   for (const auto& blob : e->sampling_chunks_host)   // the tables the fold reads: everything before the route bytes
     oa.cfg_lds_bytes = std::max(oa.cfg_lds_bytes,
                                 (reinterpret_cast<const SampCfgDev*>(blob.data())->bytes_off + 15u) & ~15u);
@@ -543,9 +545,6 @@ uint32_t ose_shard_record_bytes(const ose_engine* eng) {
 
 int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void* send, uint64_t* counts,
                    uint32_t* pack_pos, void* hip_stream) {
-  if (eng && reinterpret_cast<Engine*>(eng)->sampling_local_svc)
-    return fail(OSE_ENOTSUP, "trace-id exchange: an odigossampling config naming more services than one rule table's "
-                             "dense service tables hold (chunk-local service ids run on one GPU only)");
   if (!eng || !c || !send || !counts || !pack_pos) return fail(OSE_EINVAL, "NULL argument");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_pack needs odigossampling on the engine");
@@ -621,6 +620,9 @@ int ose_shard_pack(ose_engine* eng, const ose_columns* c, uint32_t n_ranks, void
   a.cfgs = reinterpret_cast<const uint8_t* const*>(e->shard_tables_dev);
   a.n_chunks = (uint32_t)e->sampling_chunks_dev.size();
   a.lat_svc = reinterpret_cast<const uint32_t*>(e->shard_tables_dev + 8 * e->sampling_chunks_dev.size());
+  // records carry global service ids; chunk-local tables map them per chunk
+  a.n_global_svc = (uint32_t)e->service_ids.size();
+  a.svc_maps = e->sampling_local_svc ? e->sampling_svc_maps_dev : nullptr;
   {
     uint32_t lb = 0;   // the chunk tables in LDS when they fit 64 KiB (else read from HBM)
     for (const auto& blob : e->sampling_chunks_host)
@@ -678,9 +680,6 @@ int ose_shard_unpack(const void* recv, uint64_t n, uint32_t rec_bytes, uint64_t*
 
 int ose_shard_decide(ose_engine* eng, const void* recv, uint64_t n, uint32_t rec_bytes, uint8_t* keep,
                      uint32_t* device_status, const ose_rand* rnd, void* hip_stream) {
-  if (eng && reinterpret_cast<Engine*>(eng)->sampling_local_svc)
-    return fail(OSE_ENOTSUP, "trace-id exchange: an odigossampling config naming more services than one rule table's "
-                             "dense service tables hold (chunk-local service ids run on one GPU only)");
   if (!eng) return fail(OSE_EINVAL, "NULL engine");
   Engine* e = reinterpret_cast<Engine*>(eng);
   if (!e->has_sampling) return fail(OSE_EINVAL, "ose_shard_decide needs odigossampling on the engine");

@@ -2168,7 +2168,7 @@ __device__ __forceinline__ XSpan x_span(const ShardArgs& a, uint32_t nsvc, const
   x.hi = (uint64_t)r.t.x | ((uint64_t)r.t.y << 32);
   x.lo = (uint64_t)r.t.z | ((uint64_t)r.t.w << 32);
   x.res = r.res;
-  const uint32_t s = a.res_svc[x.res];
+  const uint32_t s = a.res_svc[x.res];   // global id (nsvc = the engine's interned services)
   if (s < nsvc && ((a.lat_svc[s >> 5] >> (s & 31)) & 1u)) x.sv = s;
   if (!full) return x;
   x.err = r.status == OSE_STATUS_ERROR;
@@ -2185,11 +2185,16 @@ __device__ __forceinline__ void x_chunk(const ShardArgs& a, const Cfg& c, const 
   ep = svcb = 0;
   if (!x.valid) return;
   const uint32_t nsvc = c.h->n_services;
-  const uint32_t ss = a.res_svc_str[x.res];
+  // chunk-local tables: global ids through the chunk's map (ids past the
+  // engine's services and ids the chunk does not name map to none)
+  const uint32_t* map = a.svc_maps ? a.svc_maps[k] : nullptr;
+  const uint32_t sg = a.res_svc_str[x.res];
+  const uint32_t ss = map ? (sg < a.n_global_svc ? map[sg] : kXNone) : sg;
   svcb = ss < nsvc ? c.svc_bits[ss] : 0;
   if (a.attr_match) svcb |= chunk_attr_bits(a.attr_match, a.attr_stride, a.attr_words, c.h, j);
-  if (x.sv != kXNone) {
-    const uint32_t slot = c.svc_slot[x.sv];
+  const uint32_t sv = map && x.sv != kXNone ? map[x.sv] : x.sv;
+  if (sv < nsvc) {
+    const uint32_t slot = c.svc_slot[sv];
     if (slot != kNoSlot)
       ep = a.route_match ? a.route_match[(uint64_t)k * a.rm_stride + j] & c.slot_rules[slot]
                          : endpoint_bits(c, slot, a.arena, x.rt);
@@ -2221,7 +2226,7 @@ __global__ __launch_bounds__(kSortThreads) void shard_hist_kernel(ShardArgs a) {
   if (ch >= a.n_tiles) return;   // wave-uniform; no block barriers below
   hist[wv][lane] = 0;
   __builtin_amdgcn_wave_barrier();
-  const uint32_t nsvc = load_cfg(a.cfgs[0]).h->n_services;
+  const uint32_t nsvc = a.n_global_svc;
   const uint64_t b0 = (uint64_t)ch * kXChunk;
   XRaw nx = x_load(a, b0 + lane, false);
   for (uint32_t s = 0; s < kXSteps; s++) {
@@ -2269,7 +2274,7 @@ __global__ __launch_bounds__(kSortThreads) void shard_scatter_kernel(ShardArgs a
   const uint32_t ch = blockIdx.x * (kSortThreads / kWave) + wv;
   if (ch >= a.n_tiles) return;   // wave-uniform; no block barriers below
   uint32_t off = (uint32_t)lane < a.n_ranks ? a.hoff[(uint64_t)lane * a.n_tiles + ch] : 0u;
-  const uint32_t nsvc = load_cfg(a.cfgs[0]).h->n_services;
+  const uint32_t nsvc = a.n_global_svc;
   const uint32_t words = x_rec_words(a.n_chunks);
   const uint64_t b0 = (uint64_t)ch * kXChunk;
   XRaw nx = x_load(a, b0 + lane, true);
@@ -2413,9 +2418,9 @@ __global__ __launch_bounds__(256) void owner_bucket_kernel(OwnerArgs a) {
 // ORed over the trace's entries [k, e) of the sorted keys, the latency
 // element of each latency service (in batch order; services one at a time
 // in increasing id), ShouldSample's walk over the chunk's rules
-__device__ void owner_chunk(const Cfg& c, const uint64_t* s_key, const uint32_t* s_w4, const uint64_t* s_m,
-                            const uint64_t* s_e, const uint64_t* s_ep, const uint64_t* s_sv, uint32_t k, uint32_t e,
-                            uint32_t err, bool any_lat, FoldState& s) {
+__device__ void owner_chunk(const Cfg& c, const uint32_t* map, uint32_t n_global, const uint64_t* s_key,
+                            const uint32_t* s_w4, const uint64_t* s_m, const uint64_t* s_e, const uint64_t* s_ep,
+                            const uint64_t* s_sv, uint32_t k, uint32_t e, uint32_t err, bool any_lat, FoldState& s) {
   uint64_t ep = 0, svc = 0;
   for (uint32_t j = k; j < e; j++) {
     const uint32_t x = (uint32_t)s_key[j] & 255u;
@@ -2441,8 +2446,11 @@ __device__ void owner_chunk(const Cfg& c, const uint64_t* s_key, const uint32_t*
       if ((w4 & kXNone) != nxt || !((w4 >> 24) & kXLat)) continue;
       l = lat_comb(l, Lat{2u | (((w4 >> 24) & kXReset) ? 1u : 0u), s_m[x], s_e[x]});
     }
-    if (nxt < nsvc) {
-      const uint32_t slot = c.svc_slot[nxt];
+    // the record's latency service is a global id; a chunk-local table
+    // takes it through the chunk's map
+    const uint32_t sl = map ? (nxt < n_global ? map[nxt] : kXNone) : nxt;
+    if (sl < nsvc) {
+      const uint32_t slot = c.svc_slot[sl];
       if (slot != kNoSlot) lsat |= latency_satisfied(c, slot, ep, l.m, l.e);
     }
     last = nxt;
@@ -2588,7 +2596,9 @@ __global__ __launch_bounds__(256) void owner_fold_kernel(OwnerArgs a) {
       }
       __syncthreads();
     }
-    if (hv) owner_chunk(load_cfg(cfg_lds), s_key, s_w4, s_m, s_e, s_ep, s_sv, t, he, herr, hlat, fs);
+    if (hv)
+      owner_chunk(load_cfg(cfg_lds), a.svc_maps ? a.svc_maps[ck] : nullptr, a.n_global_svc, s_key, s_w4, s_m, s_e,
+                  s_ep, s_sv, t, he, herr, hlat, fs);
   }
   OWNER_TICK(3);
   if (hv) {

@@ -365,15 +365,43 @@ def test_gpu_many_services_batch_mode(n):
 
 
 @pytest.mark.gpu
-def test_gpu_many_services_exchange_refused():
-    # the trace-id exchange keeps global service ids in its records: a config
-    # past the dense service tables is refused there, not decided wrongly
-    from tests.test_exchange import _local_round
-    sources = [Generator("sampling", seed=0x0D160961, n_spans=2000, rank=r, world=2) for r in range(2)]
-    with pytest.raises(AssertionError) as ei:   # _local_round asserts every rank returned 0
-        _local_round(sources, many_services_config())
-    msg = str(ei.value)
-    assert "(-95, " in msg and "trace-id exchange" in msg
+@pytest.mark.parametrize("world,n_services", [(2, 1200), (3, 1200), (3, 5000)])
+def test_gpu_many_services_exchange(world, n_services):
+    # a config past the dense service tables (chunk-local service ids, 19+
+    # rule chunks) through ose_exchange_sample's round (in-process transport):
+    # records carry global service ids, the pack and the owner fold map them
+    # through each chunk's table (ShardArgs / OwnerArgs::svc_maps); traces
+    # straddle ranks, zero starts reset minStart, and every rank's keep equals
+    # the oracle on the concatenated global batch.  The same config decides
+    # at N = 1 (test_gpu_many_services_config), so no config is refused at
+    # N > 1 that N = 1 runs.
+    from tests.test_exchange import _concat_keep_oracle, _local_round
+    cfg = many_services_config(n_services)
+    sources = [Generator("sampling", seed=0x0D160961 + world, n_spans=400_000, rank=r, world=world)
+               for r in range(world)]
+    for r, g in enumerate(sources):
+        inject_zero_starts(g, 0.01, 70 + r)
+    got, stats = _local_round(sources, cfg)
+    want = _concat_keep_oracle(sources, cfg)
+    for gk, wk in zip(got, want):
+        np.testing.assert_array_equal(gk, wk)
+    assert sum(s[0] for s in stats) == sum(s[1] for s in stats) > 0
+
+
+@pytest.mark.gpu
+def test_gpu_many_services_owner_general_path():
+    # the owner's general path (records unpacked into columns, then the SAMPLE
+    # stage, which translates the records' global ids per chunk) on the same
+    # records as the bucketed fold: byte-identical keep
+    from tests.test_exchange import _decide_both, _owner_recvs
+    sources = [Generator("sampling", seed=0x0D160971, n_spans=300_000, rank=r, world=3) for r in range(3)]
+    for r, g in enumerate(sources):
+        inject_zero_starts(g, 0.01, 80 + r)
+    eng, recvs, rb = _owner_recvs(sources, many_services_config())
+    for recv in recvs:
+        fold, ref, general = _decide_both(eng, recv, rb)
+        np.testing.assert_array_equal(fold, ref)
+        assert not general
 
 
 @pytest.mark.gpu
