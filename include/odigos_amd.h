@@ -552,6 +552,31 @@ int ose_otlp_out_get(const ose_otlp_out* o, uint32_t k, const char** name, const
                      uint32_t* n_resources);   /* pointers valid until release */
 void ose_otlp_out_release(ose_otlp_out* o);
 
+/* ---- the OTLP path for concurrent callers -------------------------------
+ * A receiver's concurrent export requests (each a serialized TracesData)
+ * processed as one device batch per wave of calls: ose_otlp_pipeline_consume
+ * runs decode -> `stages` (OSE_GROUP_TRACE_ID) -> route + re-encode for its
+ * request together with the requests other threads hand in meanwhile, and
+ * returns this request's outputs (the form ose_otlp_encode returns: the
+ * router's pipelines then "default"; release with ose_otlp_out_release).
+ * Each output is byte for byte what ose_otlp_encode writes for the request's
+ * resources.  Differences from one call per request: spans of one trace that
+ * arrive in concurrent requests are decided together (as groupbytrace hands
+ * a whole trace to odigossampling); the traffic gate draws once per batch;
+ * the odigostrafficmetrics counters are kept by the pipeline, summed over
+ * its requests, and read (and reset) with ose_otlp_pipeline_counters:
+ * {"accepted_spans": n, "data_size": [[{attributes}, bytes], ...], plus the
+ * batching statistics}.  max_batch_bytes bounds a batch's message bytes (0:
+ * 64 MiB; a larger request runs alone).  The router (may be NULL) must
+ * outlive the pipeline; the pipeline holds a reference on the engine.     */
+typedef struct ose_otlp_pipeline ose_otlp_pipeline;
+int ose_otlp_pipeline_create(ose_engine* eng, const ose_router* router, uint32_t stages, uint64_t max_batch_bytes,
+                             ose_otlp_pipeline** out);
+int ose_otlp_pipeline_consume(ose_otlp_pipeline* p, const void* pb, size_t len, const ose_rand* rnd,
+                              ose_otlp_out** out);
+int ose_otlp_pipeline_counters(ose_otlp_pipeline* p, char* json, size_t cap);
+void ose_otlp_pipeline_destroy(ose_otlp_pipeline* p);
+
 /* ---- groupbytrace, resident in HBM ----------------------
  * Replaces the groupbytrace processor the gateway runs before odigossampling
  * (opentelemetry-collector-contrib groupbytraceprocessor v0.141.0,

@@ -519,6 +519,54 @@ class OtlpBatch:
     __del__ = close
 
 
+class OtlpPipeline:
+    """ose_otlp_pipeline: an OTLP receiver's concurrent requests (serialized
+    TracesData) coalesced into one device batch per wave of calls; consume()
+    is called from any number of threads and returns the request's outputs
+    as OtlpBatch.encode does."""
+
+    def __init__(self, eng: "Engine", router: "Router | None" = None,
+                 stages: int = native.STAGE_SAMPLE | native.STAGE_TEMPLATE | native.STAGE_SIZE,
+                 max_batch_bytes: int = 0):
+        self.L = native.lib()
+        self.eng, self.router = eng, router   # both outlive the pipeline
+        h = C.c_void_p()
+        native.check(self.L.ose_otlp_pipeline_create(eng.h, router.h if router is not None else None, stages,
+                                                     max_batch_bytes, C.byref(h)))
+        self.h = h
+
+    def consume(self, data, length: int | None = None, seed: int = 0x5EED, traffic_u: float = 0.0,
+                copy: bool = True, path: dict | None = None) -> list:
+        """data: bytes, or the address of `length` bytes (pinned or not)."""
+        rnd = native.Rand(seed, traffic_u)
+        if isinstance(data, (bytes, bytearray)):
+            buf = C.create_string_buffer(bytes(data), len(data))
+            ptr, n = C.cast(buf, C.c_void_p), len(data)
+        else:
+            ptr, n = C.c_void_p(data), int(length)
+        h = C.c_void_p()
+        native.check(self.L.ose_otlp_pipeline_consume(self.h, ptr, n, C.byref(rnd), C.byref(h)))
+        return take_otlp_out(self.L, h, copy, None, path)
+
+    def counters(self) -> dict:
+        """the traffic counters and batching statistics since the last read"""
+        import json
+        buf = C.create_string_buffer(1 << 20)
+        native.check(self.L.ose_otlp_pipeline_counters(self.h, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
+    def hold(self, n: int):
+        """test seam: batches run only once n requests joined them"""
+        native.check(self.L.osehost_otlp_pipeline_hold(self.h, n))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ose_otlp_pipeline_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+
 class PinnedBuffer:
     """Pinned host memory from the engine library (ose_host_alloc)."""
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <cstdint>
 #include <cstdlib>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -84,6 +85,9 @@ struct OtlpOut {   // ose_otlp_out
   double t_ms[4] = {0, 0, 0, 0};   // decisions D2H, sizing pass, buffers, writing pass
   int gpu = 0;                     // 1: written by the GPU encoder (encode_kernel.hip)
   uint32_t fallback = 0;           // why the GPU encoder handed the call to the host (kEncFb*)
+  // one request's slice of a coalesced batch (otlp_pipeline.cpp): the data
+  // pointers are into the batch's outputs, which `hold` keeps alive
+  std::shared_ptr<OtlpOut> hold;
 };
 void otlp_out_release(OtlpOut* o);
 

@@ -1500,7 +1500,7 @@ namespace {
 // 0 with *host false: *o holds the outputs; 0 with *host true: the host
 // encoder takes the call (o->fallback says why); else an error code
 int encode_gpu(OtlpBatchImpl* b, const ose_outputs* outs, bool sampled, bool tmpl, const Router* router,
-               hipStream_t st, OtlpOut* o, bool* host) {
+               hipStream_t st, OtlpOut* o, bool* host, std::vector<uint64_t>* res_off = nullptr) {
   *host = true;
   if (b->e->option(Engine::kOptEncodeHost)) return 0;   // engine option encode_host: the host encoder always
   if (router && router->pipelines.size() > 63) return 0;   // the host encoder reports it
@@ -1664,12 +1664,50 @@ int encode_gpu(OtlpBatchImpl* b, const ose_outputs* outs, bool sampled, bool tmp
   HIP_TRY(hipStreamSynchronize(st));
   std::memcpy(&fb, h, 4);
   if (fb & kEncFbWrite) return fail(OSE_EDEVICE, "GPU encoder: a record's bytes disagree with its size");
+  if (res_off) {   // each output's offset of every resource's record (the scan the writer used)
+    res_off->resize((size_t)n_out * R);
+    if (R) HIP_TRY(hipMemcpy(res_off->data(), a.off, 8 * (size_t)n_out * R, hipMemcpyDeviceToHost));
+  }
   o->t_ms[3] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   o->gpu = 1;
   *host = false;
   return 0;
 }
 }  // namespace
+
+// The GPU encoder for the OTLP pipeline (otlp_pipeline.cpp): *out holds the
+// batch's outputs and res_off every output's per-resource record offsets
+// (n_out x R); *gpu false when the GPU encoder declined the batch (nothing
+// in *out), the caller then takes its requests one by one.
+int otlp_encode_gpu_offsets(Engine* e, ose_otlp_batch* bb, const ose_outputs* outs, uint32_t stages,
+                            const Router* router, hipStream_t st, OtlpOut** out, std::vector<uint64_t>& res_off,
+                            bool* gpu) {
+  auto* b = reinterpret_cast<OtlpBatchImpl*>(bb);
+  *gpu = false;
+  *out = nullptr;
+  auto* o = new OtlpOut();
+  o->e = e;
+  engine_retain(e);
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->enc_pool.empty()) {
+      o->work = static_cast<EncodeWork*>(e->enc_pool.back());
+      e->enc_pool.pop_back();
+    }
+  }
+  if (!o->work) o->work = encode_work_new();
+  const bool sampled = stages & (OSE_STAGE_SAMPLE | OSE_STAGE_APPLY_KEEP);
+  const bool tmpl = stages & OSE_STAGE_TEMPLATE;
+  bool host = true;
+  const int rc = encode_gpu(b, outs, sampled, tmpl, router, st, o, &host, &res_off);
+  if (rc || host) {
+    otlp_out_release(o);
+    return rc;
+  }
+  *gpu = true;
+  *out = o;
+  return 0;
+}
 
 }  // namespace ose
 

@@ -153,6 +153,11 @@ def lib() -> C.CDLL:
         "ose_gbt_download": (C.c_int, [_p, C.POINTER(Columns)]),
         "ose_engine_attr_key": (C.c_int, [_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
         "ose_engine_attr_host_rules": (C.c_uint32, [_p, C.POINTER(C.c_uint64), C.c_uint32]),
+        "ose_otlp_pipeline_create": (C.c_int, [_p, _p, C.c_uint32, C.c_uint64, C.POINTER(_p)]),
+        "ose_otlp_pipeline_consume": (C.c_int, [_p, C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(_p)]),
+        "ose_otlp_pipeline_counters": (C.c_int, [_p, C.c_char_p, C.c_size_t]),
+        "ose_otlp_pipeline_destroy": (None, [_p]),
+        "osehost_otlp_pipeline_hold": (C.c_int, [_p, C.c_uint32]),
         "ose_engine_path_counts": (C.c_uint32, [_p, C.POINTER(C.c_uint64), C.c_uint32]),
         "ose_engine_set_option": (C.c_int, [_p, C.c_char_p, C.c_int64]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),

@@ -190,6 +190,41 @@ def main():
             {"callers": callers, "calls": callers * per, "wall_s": wall,
              "spans_per_s": callers * per * 8192 / wall, "calls_per_s": callers * per / wall})
         print(f"otlp 8192-span calls, {callers} callers: {callers * per * 8192 / wall / 1e6:.1f} M spans/s", flush=True)
+    # the same requests through ose_otlp_pipeline: concurrent callers'
+    # requests coalesced into one device batch per wave of calls
+    from odigos_amd.batch import OtlpPipeline
+    pipe = OtlpPipeline(eng, router, st)
+    for callers in (1, 4, 8, 16):
+        per = 150 if callers > 1 else 120
+        ready = threading.Barrier(callers + 1)
+        errs = []
+
+        def pcaller(k):
+            try:
+                ready.wait()
+                for _ in range(per):
+                    pipe.consume(spin.p, spin.n, seed=0x5EED, copy=False)
+            except Exception as ex:   # pragma: no cover
+                errs.append(repr(ex))
+
+        th = [threading.Thread(target=pcaller, args=(k,)) for k in range(callers)]
+        for t_ in th:
+            t_.start()
+        pipe.counters()
+        ready.wait()
+        a = time.perf_counter()
+        for t_ in th:
+            t_.join()
+        wall = time.perf_counter() - a
+        assert not errs, errs
+        cnt = pipe.counters()
+        res.setdefault("pipeline8192_callers", []).append(
+            {"callers": callers, "calls": callers * per, "wall_s": wall,
+             "spans_per_s": callers * per * 8192 / wall, "calls_per_s": callers * per / wall,
+             "batches": cnt["batches"], "largest_batch": cnt["largest_batch"], "alone": cnt["alone"]})
+        print(f"otlp pipeline 8192-span requests, {callers} callers: {callers * per * 8192 / wall / 1e6:.1f} M spans/s "
+              f"({cnt['batches']} batches, largest {cnt['largest_batch']})", flush=True)
+    pipe.close()
     spin.close()
     pin.close()
     line = json.dumps(res)
