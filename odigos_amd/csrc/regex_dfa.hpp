@@ -81,8 +81,8 @@ class LazyDfa {
 // Syntax / Unsupported as compile_dfa does; never TooLarge.
 class HostRegexp {
  public:
-  RegexStatus compile(const std::string& pattern, std::string& err, uint32_t max_states = 65535,
-                      uint64_t max_table_bytes = 16ull << 20);
+  RegexStatus compile(const std::string& pattern, std::string& err, uint32_t max_states = 16384,
+                      uint64_t max_table_bytes = 4ull << 20);
   bool match(const uint8_t* s, size_t n) const;
   bool lazy() const { return lazy_ != nullptr; }
  private:

@@ -133,7 +133,7 @@ def test_unsupported_is_reported_not_guessed():
     assert native.lib().osehost_regex_match(r"(a|b)*a(a|b){20}".encode(), b"", 0) == -2
 
 
-def _host(pattern, s: bytes, max_states=65535, max_bytes=16 << 20):
+def _host(pattern, s: bytes, max_states=16384, max_bytes=4 << 20):
     import ctypes
     lazy = ctypes.c_int(-1)
     r = native.lib().osehost_regex_match_host(pattern.encode(), s, len(s), max_states, max_bytes, ctypes.byref(lazy))
@@ -168,7 +168,7 @@ def test_lazy_dfa_takes_what_the_device_refuses():
     t0 = time.time()
     for k in range(60):
         s = "".join(rng.choice("ab") for _ in range(rng.randrange(0, 200))).encode()
-        got, lazy = _host(pat, s)
+        got, lazy = _host(pat, s, max_states=1024, max_bytes=1 << 20)
         assert lazy == 1 and got == orc.match(s), s
     assert time.time() - t0 < 30
     # a long input through a flushing cache stays linear
