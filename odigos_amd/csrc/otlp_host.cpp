@@ -167,6 +167,12 @@ struct OtlpEngine {
   uint32_t n_attr_keys = 0;
   uint32_t attr_words = 1;   // attr_match words per span
   bool json_rules = false;
+  // more than 64 shim-evaluated (json / oversize-regex) span_attribute rules:
+  // the per-resource cached word cannot hold their bits, so the host pass
+  // takes each span's from its resource's service id (AsString(service.name):
+  // the rules whose service it is, spanattribute.go:130-132), [svc][word]
+  bool wide_host_rules = false;
+  std::vector<std::vector<uint64_t>> host_rules_by_svc;
   ResCache res_cache;
   DevResTable res_dev;
   std::string err;
@@ -230,25 +236,29 @@ OtlpEngine* otlp_engine(Engine* e, int& rc) {
   roles["url.full"] |= kRoleFull;
   roles["http.url"] |= kRoleFull;
   const AttrPlan& plan = o->ctx.attr_plan;
-  if (plan.keys.size() > kOtlpMaxAttrKeys) {
-    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 56 distinct span_attribute keys");
-    delete o;
-    return nullptr;
-  }
-  // the per-resource rule word the decoder caches holds the json (host-pass)
-  // rules only, one bit each; the GPU-evaluated rules need no resource word,
-  // and attr_match carries every rule's bit in (rules + 63) / 64 words
+  // the per-resource rule word the decoder caches holds the shim-evaluated
+  // rules only, one bit each; past 64 of them the host pass takes the bits
+  // from the resource's service id instead (wide_host_rules)
   size_t n_host_rules = 0;
   for (int rk : plan.rule_key) n_host_rules += rk < 0;
   if (n_host_rules > 64) {
-    rc = fail(OSE_ENOTSUP, "OTLP ingest: more than 64 span_attribute rules with json conditions (columnise with "
-                           "ose_batch_* / ose_process_device, whose attr_match takes any number of words)");
-    delete o;
-    return nullptr;
+    o->wide_host_rules = true;
+    o->host_rules_by_svc.assign(std::max<size_t>(o->ctx.services.size(), 1),
+                                std::vector<uint64_t>(std::max<size_t>(plan.host_mask.size(), 1), 0));
+    for (size_t k = 0; k < plan.rule_key.size() && k < o->ctx.attr_preds.size(); k++) {
+      if (plan.rule_key[k] >= 0) continue;
+      auto it = o->ctx.services.find(o->ctx.attr_preds[k].service());
+      if (it != o->ctx.services.end() && it->second < o->host_rules_by_svc.size())
+        o->host_rules_by_svc[it->second][k / 64] |= 1ull << (k % 64);
+    }
   }
   o->attr_words = (uint32_t)std::max<size_t>(1, (plan.rule_key.size() + 63) / 64);
   o->n_attr_keys = (uint32_t)plan.keys.size();
-  for (size_t k = 0; k < plan.keys.size(); k++) roles[plan.keys[k]] |= kRoleAttr0 << k;
+  // key columns past kOtlpMaxAttrKeys have no role bit: a span that carries
+  // such a key takes the host pass (which fills every key column), and the
+  // GPU decoder writes the others ABSENT for every span it finishes
+  for (size_t k = 0; k < plan.keys.size(); k++)
+    roles[plan.keys[k]] |= k < kOtlpMaxAttrKeys ? kRoleAttr0 << k : (uint64_t)kRoleHost;
   for (size_t k = 0; k < plan.rule_key.size(); k++)
     if (plan.rule_key[k] < 0) {
       roles[o->ctx.attr_preds[k].key()] |= kRoleHost;
@@ -337,7 +347,7 @@ uint64_t host_rule_word(const AttrPlan& p, const std::vector<uint64_t>& words) {
   uint32_t j = 0;
   for (size_t w = 0; w < p.host_mask.size(); w++)
     for (uint64_t m = p.host_mask[w]; m; m &= m - 1, j++)
-      if (w < words.size() && ((words[w] >> __builtin_ctzll(m)) & 1)) out |= 1ull << j;
+      if (j < 64 && w < words.size() && ((words[w] >> __builtin_ctzll(m)) & 1)) out |= 1ull << j;
   return out;
 }
 // ... and back to the rule-indexed words columnize_span takes
@@ -346,7 +356,7 @@ void host_rule_words(const AttrPlan& p, uint64_t word, std::vector<uint64_t>& ou
   uint32_t j = 0;
   for (size_t w = 0; w < p.host_mask.size(); w++)
     for (uint64_t m = p.host_mask[w]; m; m &= m - 1, j++)
-      if ((word >> j) & 1) out[w] |= 1ull << __builtin_ctzll(m);
+      if (j < 64 && ((word >> j) & 1)) out[w] |= 1ull << __builtin_ctzll(m);
 }
 
 // A resource's columns from its Resource field(s) (merged as pdata merges
@@ -1381,9 +1391,18 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   if (!cnt) return 0;
   std::vector<uint32_t> span_res;
   const std::vector<uint32_t>* sres = &w.span_res;
-  if (gpu_res) {   // the resources' span_attribute service bits from the device
+  if (gpu_res && !o->wide_host_rules) {   // the resources' span_attribute service bits from the device
     attr_res.resize(R);
     if (R) HIP_TRY(hipMemcpy(attr_res.data(), b->d_attr_res, 8 * R, hipMemcpyDeviceToHost));
+  }
+  std::vector<uint32_t> res_svc_h;   // wide_host_rules: the resources' service ids
+  if (o->wide_host_rules) {
+    if (gpu_res) {
+      res_svc_h.resize(R);
+      if (R) HIP_TRY(hipMemcpy(res_svc_h.data(), c.res_svc, 4 * R, hipMemcpyDeviceToHost));
+    } else {
+      res_svc_h = w.res_svc;
+    }
   }
   if (!b->layout_on_host) {   // the spans' refs and resources from the device
     if ((rc = layout_to_host(b, st))) return rc;
@@ -1412,7 +1431,13 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
     const uint64_t ref = b->span_ref[i];
     Span sp;
     if (!pb_span(pb + (uint32_t)ref, (size_t)(ref >> 32), sp)) return fail(OSE_EINVAL, "OTLP protobuf: malformed Span");
-    host_rule_words(o->ctx.attr_plan, attr_res[(*sres)[i]], res_words);
+    if (o->wide_host_rules) {
+      const uint32_t sv = res_svc_h[(*sres)[i]];
+      if (sv < o->host_rules_by_svc.size()) res_words = o->host_rules_by_svc[sv];
+      else res_words.assign(std::max<size_t>(1, o->ctx.attr_plan.host_mask.size()), 0);
+    } else {
+      host_rule_words(o->ctx.attr_plan, attr_res[(*sres)[i]], res_words);
+    }
     columnize_span(o->ctx, sp, res_words, sizer, sc);
     for (uint32_t w = 0; w < AW; w++) fix_attr[(size_t)q * AW + w] = w < sc.attr_match.size() ? sc.attr_match[w] : 0;
     OtlpFix& x = fix[q];

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
           if (roles & kRoleTarget) target = v;
           if (roles & kRoleFull) full_seen = true;
           if (roles & kRoleHost) host_key = true;
-          for (uint32_t k = 0; k < a.n_attr_keys; k++)
+          for (uint32_t k = 0; k < a.n_attr_keys && k < kOtlpMaxAttrKeys; k++)
             if (roles & (kRoleAttr0 << k)) {
               const uint64_t j = (uint64_t)k * a.n_spans + i;
               uint32_t t = v.type == kAttrBytes ? OSE_ATTR_OTHER : v.type;
@@ -281,8 +281,8 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
       continue;
     }
     a.host_flag[i] = 0;
-    for (uint32_t k = 0; k < a.n_attr_keys; k++)   // keys this span does not carry
-      if (!(found & (kRoleAttr0 << k))) {
+    for (uint32_t k = 0; k < a.n_attr_keys; k++)   // keys this span does not carry (keys past
+      if (k >= kOtlpMaxAttrKeys || !(found & (kRoleAttr0 << k))) {   // kOtlpMaxAttrKeys send it to the host)
         a.attr_type[(uint64_t)k * a.n_spans + i] = OSE_ATTR_ABSENT;
         a.attr_val[(uint64_t)k * a.n_spans + i] = 0;
       }

@@ -65,6 +65,23 @@ CFG_MANY_RULES["odigossampling"]["endpoint_rules"] += [
      "rule_details": {"service_name": SERVICES[j % len(SERVICES)], "attribute_key": f"k{j % 40}",
                       "condition_type": "string", "operation": "equals" if j % 2 else "contains",
                       "expected_value": "v", "sampling_ratio": float(j)}} for j in range(70)] + [_js]
+# past the decoder's 56 key roles: 62 distinct string keys (keys 56.. send the
+# spans that carry them to the host pass, the others are decoded ABSENT)
+CFG_WIDE_KEYS = json.loads(json.dumps(CFG))
+CFG_WIDE_KEYS["odigossampling"]["endpoint_rules"] += [
+    {"name": f"w{j}", "type": "span_attribute",
+     "rule_details": {"service_name": SERVICES[j % len(SERVICES)], "attribute_key": f"k{j}",
+                      "condition_type": "string", "operation": "equals", "expected_value": "v",
+                      "sampling_ratio": float(j % 100)}} for j in range(60)]
+# past 64 shim-evaluated rules: 70 json rules over two keys and every
+# service (their bits from the resource's service id in the host pass)
+CFG_WIDE_JSON = json.loads(json.dumps(CFG_JSON_RULE))
+CFG_WIDE_JSON["odigossampling"]["service_rules"] += [
+    {"name": f"j{j}", "type": "span_attribute",
+     "rule_details": {"service_name": SERVICES[j % len(SERVICES)], "attribute_key": "body" if j % 3 else "k1",
+                      "condition_type": "json", "operation": ["is_valid_json", "is_invalid_json", "contains_key"][j % 3],
+                      "json_path": "$.a", "sampling_ratio": float((j * 7) % 101), "fallback_sampling_ratio": float(j % 4)}}
+    for j in range(70)]
 CFG_EXCLUDE = json.loads(json.dumps(CFG))
 CFG_EXCLUDE["odigosurltemplate"] = {"exclude": {"k8s_workloads": [{"namespace": "prod", "kind": "Deployment",
                                                                     "name": "api"}]}}
@@ -353,17 +370,18 @@ def _compare(cols, hb_cols, got):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,odd,cfg", [(0, 0.0, "base"), (1, 0.0, "base"), (2, 0.15, "base"), (3, 0.1, "json"),
                                           (4, 0.0, "exclude"), (5, 0.3, "json"), (6, 0.0, "many_keys"),
-                                          (7, 0.1, "many_rules")])
+                                          (7, 0.1, "many_rules"), (8, 0.0, "wide_keys"), (9, 0.1, "wide_json")])
 def test_gpu_decode_matches_host_columns(seed, odd, cfg):
     from odigos_amd.batch import Engine, OtlpBatch
     c = {"base": CFG, "json": CFG_JSON_RULE, "exclude": CFG_EXCLUDE, "many_keys": CFG_MANY_KEYS,
-         "many_rules": CFG_MANY_RULES}[cfg]
+         "many_rules": CFG_MANY_RULES, "wide_keys": CFG_WIDE_KEYS, "wide_json": CFG_WIDE_JSON}[cfg]
     rng = random.Random(seed)
-    td = _http_traces(rng, 200, odd=odd, extra_keys=40 if cfg in ("many_keys", "many_rules") else 0)
+    td = _http_traces(rng, 200, odd=odd, extra_keys={"many_keys": 40, "many_rules": 40, "wide_keys": 62,
+                                                     "wide_json": 4}.get(cfg, 0))
     _, hb = _host_columns(c, td)
     eng = Engine(c)
     ob = OtlpBatch(eng, to_pb(td))
-    if odd == 0.0 and cfg not in ("json", "many_rules"):
+    if odd == 0.0 and cfg not in ("json", "many_rules", "wide_keys", "wide_json"):
         assert ob.host_spans == 0
     else:
         assert ob.host_spans > 0
@@ -438,16 +456,20 @@ def test_gpu_decode_generic_traces():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["base", "json", "many_rules"])
+@pytest.mark.parametrize("cfg", ["base", "json", "many_rules", "wide_keys", "wide_json"])
 def test_gpu_stages_on_decoded_columns(cfg):
     """SAMPLE|TEMPLATE|SIZE on the decoded columns equals the oracle chain on
     the host columniser's batch (decisions, templates, counters); many_rules:
-    71 span_attribute rules, attr_match in two words."""
+    71 span_attribute rules, attr_match in two words; wide_keys: 62 attribute
+    keys (past the decoder's 56 key roles); wide_json: 71 json rules (past the
+    64 the per-resource word holds)."""
     import torch
     from odigos_amd.batch import Engine, HostOutputs, OtlpBatch
     from tests.oracle_lib import SamplingOracle, UrlOracle, size_process
-    c = {"base": CFG, "json": CFG_JSON_RULE, "many_rules": CFG_MANY_RULES}[cfg]
-    td = _http_traces(random.Random(77), 400, odd=0.05, extra_keys=40 if cfg == "many_rules" else 0)
+    c = {"base": CFG, "json": CFG_JSON_RULE, "many_rules": CFG_MANY_RULES, "wide_keys": CFG_WIDE_KEYS,
+         "wide_json": CFG_WIDE_JSON}[cfg]
+    td = _http_traces(random.Random(77), 400, odd=0.05,
+                      extra_keys={"many_rules": 40, "wide_keys": 62, "wide_json": 4}.get(cfg, 0))
     _, hb = _host_columns(c, td)
     eng = Engine(c)
     ob = OtlpBatch(eng, to_pb(td))
