@@ -1,27 +1,30 @@
 // url_kernel.hip — odigosurltemplate on CDNA4 (gfx950).
 //
-// One launch templatizes a whole batch in a single pass over HBM.  A
-// workgroup (4 waves) owns a tile of 1024 consecutive spans; each wave
-// processes 4 groups of 64 consecutive spans (one span per lane) on its own,
-// with no workgroup barrier until the tile scan:
-//   stage    the group's path bytes (the arena range its 64 spans reference)
-//            are copied HBM -> the wave's LDS slice with coalesced 16-byte
-//            loads; all per-byte work below reads LDS.
-//   phase 1  each lane plans its span: what the reference does with it
-//            (processor.go:235-287 enhanceSpan/processSpan), the
-//            templatization rules with the same segment count in config order
-//            (processor.go:149-171, templatize.go:192-237), else a
-//            per-segment classification (templatize.go:242-269).  The cheap
-//            pass reads 4 bytes per step and keeps only AND/OR/run
-//            accumulators (noLetters, hex, \d{7,}, '@' count, non-ASCII);
-//            email, UTF-8 (U+FFFD), date and UUID checks run as second
-//            passes only on the segments the cheap pass flags; compiled DFAs
-//            handle custom_ids / rule regexps.  Plans go to LDS.
-//   scan     workgroup scan of output lengths + decoupled look-back across
-//            tiles gives every span its offset in the compact output arena.
-//   phase 2  groups are re-staged (L2-resident by now) and lanes write their
-//            templates into an LDS image of the tile's output, stored to HBM
-//            with coalesced dword stores.
+// One wave per 64-span group; a persistent grid of four 4-wave workgroups per
+// CU (16x that beside the trace stage), waves independent after the config
+// load:
+//   url_plan_kernel   per group: the arena bytes its paths reference are
+//                     staged into a 3 KiB per-wave LDS buffer by LDS-DMA
+//                     (global_load_lds_dwordx4; paths gathered as 16-byte
+//                     chunks when the range is wider), the next group's copy
+//                     in flight while this one is planned; 12 bit-sliced
+//                     class bitmaps of the staged rows (url_classes.hpp);
+//                     the segment list (enumerated from the slash / '?' rows)
+//                     classified 64 segments per step, branch-free
+//                     (templatize.go:242-269), each lane folding its span's
+//                     plan (processor.go:149-186); then the group's template
+//                     bytes assembled into an LDS image over the dead bitmaps
+//                     and stored to the wave's scratch region (refs form: to
+//                     its place in the output arena, the refs written here).
+//                     Groups it cannot take (user-rule matches, name ids past
+//                     the braced table, a list or image overflow) are listed.
+//   url_plan_slow_kernel  the groups whose paths overflow the stage or hold a
+//                     segment over 64 bytes, planned in stage-sized subsets.
+//   url_scan_kernel   exclusive scan of the group sums (decoupled look-back).
+//   url_emit_slow_kernel  the listed groups, written per span at their bases.
+//   url_copy_kernel   template refs of the other groups and the images moved
+//                     to the compact output arena (with SIZE: the fused spans
+//                     pass of odigostrafficmetrics).
 // Byte-identical to the oracle (oracle/url.c) including the compact arena.
 #include <hip/hip_runtime.h>
 
@@ -43,7 +46,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr uint32_t kStage = 4 * 1024;            // per-wave LDS copy of one group's bytes
+constexpr uint32_t kStage = 4 * 1024;            // per-wave LDS copy of one group's bytes (slow kernels)
 
 enum : uint32_t { M_NONE = 0, M_RENAME_SLASH, M_SLASH, M_RULE, M_DEFAULT, M_ORIG };
 
