@@ -716,7 +716,14 @@ int osehost_bench(void* p, const char* traces_json, uint32_t reps, uint32_t thre
   using clk = std::chrono::steady_clock;
   // every call's Traces is copied before the clock starts (by the thread that
   // makes the call, as a receiver allocates the pdata it hands on) and
-  // destroyed after it stops: the copy and the teardown are the caller's
+  // destroyed after it stops: the copy and the teardown are the caller's.
+  // The copies held at once are bounded (about 1M spans per thread): reps
+  // beyond that are dropped, and out[1] / out[2] count the calls made.
+  {
+    const uint64_t per_rep = std::max<uint64_t>(1, (spans + threads - 1) / threads);
+    const uint64_t budget = 1ull << 20;
+    reps = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(reps, budget / per_rep));
+  }
   std::vector<std::vector<Traces>> work(threads);
   std::atomic<uint32_t> ready{0};
   std::atomic<bool> go{false};

@@ -1747,10 +1747,14 @@ __global__ __launch_bounds__(kScanThreads) void url_scan_kernel(UrlKernelArgs a)
         if (over && a.refs) {
           // what a retry needs: every group as a 16-byte aligned image (X,
           // with the bump's chunk tails of this call counted in), twice over
-          // for the tails the retry's waves leave, plus an image per wave
+          // for the tails the retry's waves leave (a wave leaves at most one
+          // chunk's tail, and chunks are an eighth of the arena over the
+          // waves: the tails stay under C'/8, inside 2X), plus an image per
+          // resident wave (not per wave of an oversubscribed grid beside the
+          // trace stage, 16x the resident one)
           const uint64_t X = sb + __hip_atomic_load((unsigned long long*)a.slow_aligned, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-          used = 2 * X + (uint64_t)kImgCap * a.plan_waves;
+          used = 2 * X + (uint64_t)kImgCap * min(a.plan_waves, kUrlMaxWaves);
         }
         if (a.used) *a.used = used;
         if (over) atomicOr(a.error, 2u);

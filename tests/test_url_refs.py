@@ -167,6 +167,24 @@ def test_gpu_forked_refs_equal_packed_and_overflow_retry():
         np.testing.assert_array_equal(a, b)
     for a, b in zip(out["packed"][4], out["refs"][4]):   # template bytes, lengths
         np.testing.assert_array_equal(a, b)
+    # both forms ran forked (URL planning beside the trace stage): a fork or
+    # join ordering fault would corrupt them alike, so the forked result is
+    # also checked against the oracle chain on the whole batch
+    from tests.oracle_lib import SamplingOracle, size_process
+    ns = g.cols.n_spans
+    ho = HostOutputs(g.cols)
+    assert SamplingOracle(cfg["odigossampling"]).process(g.cols, ho.outs, native.GROUP_TRACE_ID, 13, 8) == 0
+    assert UrlOracle(cfg["odigosurltemplate"]).process(g.cols, ho.outs, 8) == 0
+    assert size_process(g.cols, ho.outs, st, native.GROUP_TRACE_ID, ho.outs, 1, 1.0, 0.0, 8) == 0
+    A = g.cols.n_attrsets
+    np.testing.assert_array_equal(out["refs"][0], ho.view("keep", np.uint8)[:ns])
+    np.testing.assert_array_equal(out["refs"][1], ho.view("url_out", np.uint8)[:ns])
+    np.testing.assert_array_equal(out["refs"][2][:A], ho.view("attrset_bytes", np.int64)[:A])
+    assert int(out["refs"][3][0]) == int(ho.view("accepted_spans", np.int64)[0])
+    hm = ho.view("url_out", np.uint8)[:ns] != 0
+    want_t = span_template_bytes(ho.view("tmpl", np.uint32)[: 2 * ns], ho.bufs["tmpl_arena"][: int(ho.used[0])], hm)
+    for a, b in zip(want_t, out["refs"][4]):
+        np.testing.assert_array_equal(a, b)
     small = DeviceBatch(g.cols, tmpl_cap=1 << 16)
     eng.process_device(small, st | native.STAGE_TEMPLATE_REFS, seed=13)
     torch.cuda.synchronize()
