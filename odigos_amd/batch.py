@@ -559,6 +559,10 @@ class OtlpPipeline:
         """test seam: batches run only once n requests joined them"""
         native.check(self.L.osehost_otlp_pipeline_hold(self.h, n))
 
+    def tune(self, max_running: int, window_us: int = 200, target: int = 16):
+        """diagnostics: batches on the GPU at once, the batching window"""
+        native.check(self.L.osehost_otlp_pipeline_tune(self.h, max_running, window_us, target))
+
     def close(self):
         if getattr(self, "h", None):
             self.L.ose_otlp_pipeline_destroy(self.h)

@@ -33,6 +33,7 @@
 // same calls, with the same results a single call would have.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <map>
@@ -152,19 +153,26 @@ struct Pipeline {
   const Router* router = nullptr;
   uint32_t stages = 0;
   size_t max_bytes = 0;
-  int max_running = 2;
+  int max_running = 4;
   std::mutex mu;
   std::condition_variable cv;
   std::vector<std::unique_ptr<Slot>> slots;
   int filling = -1;
   int running = 0;
   size_t hold = 0;   // test seam (osehost_otlp_pipeline_hold): a leader waits for this many requests
+  // batching window: under load (the last batch held several requests) a
+  // leader whose slot is free still waits up to window_us for requests to
+  // join, until the batch holds target requests; at low load it runs at once
+  uint32_t window_us = 200;
+  size_t target = 8;
+  size_t last_q = 0;
   std::mutex single_mu;   // requests that run alone share one slot
   std::unique_ptr<Slot> single;
   std::mutex cmu;   // counters
   std::map<std::string, int64_t> set_bytes;
   int64_t accepted = 0;
   uint64_t n_batches = 0, n_requests = 0, n_singles = 0, max_batch = 0;
+  double t_ms[5] = {0, 0, 0, 0, 0};   // batches: wait (window + copies), decode + stages, encode, slices, total
 };
 
 namespace {
@@ -215,10 +223,12 @@ int run_front(Pipeline* p, Slot& s, const uint8_t* pb, size_t len, const ose_ran
   return ose_process_device(eng, c, &outs, p->stages, OSE_GROUP_TRACE_ID, &rnd, s.st);
 }
 
-// the device status word and the traffic counters after the stages
-int collect_counters(Pipeline* p, Slot& s, ose_otlp_batch* bb) {
-  const ose_columns* c = ose_otlp_columns(bb);
-  const uint32_t sets = c->n_attrsets;
+// the device status word and the traffic counters after the stages: the
+// copies are queued behind the stages (issue_counters) and read once the
+// encoder has synchronised the stream (take_counters), so they cost no wait
+// of their own
+int issue_counters(Slot& s, ose_otlp_batch* bb) {
+  const uint32_t sets = ose_otlp_columns(bb)->n_attrsets;
   const size_t need = 8 * (4 + (size_t)sets);
   if (need > s.host_misc_cap) {
     if (s.host_misc) (void)hipHostFree(s.host_misc);
@@ -229,7 +239,11 @@ int collect_counters(Pipeline* p, Slot& s, ose_otlp_batch* bb) {
   }
   PIPE_TRY(hipMemcpyAsync(s.host_misc, s.misc.p, 32, hipMemcpyDeviceToHost, s.st));
   if (sets) PIPE_TRY(hipMemcpyAsync(s.host_misc + 4, s.sets.p, 8 * (size_t)sets, hipMemcpyDeviceToHost, s.st));
-  PIPE_TRY(hipStreamSynchronize(s.st));
+  return 0;
+}
+int take_counters(Pipeline* p, Slot& s, ose_otlp_batch* bb) {
+  PIPE_TRY(hipStreamSynchronize(s.st));   // (already synchronised by the encoder: returns at once)
+  const uint32_t sets = ose_otlp_columns(bb)->n_attrsets;
   const uint32_t status = (uint32_t)s.host_misc[2];
   if (status) return fail(OSE_EDEVICE, "OTLP pipeline: device status " + std::to_string(status));
   if (!(p->stages & OSE_STAGE_SIZE)) return 0;
@@ -253,11 +267,16 @@ void run_alone(Pipeline* p, Slot& s, Req& r, const uint8_t* pb) {
   ose_otlp_batch* bb = nullptr;
   ose_outputs outs{};
   int rc = run_front(p, s, pb, r.len, r.rnd, &bb, outs);
-  if (!rc) rc = collect_counters(p, s, bb);
+  if (!rc) rc = issue_counters(s, bb);
   ose_otlp_out* o = nullptr;
   if (!rc)
     rc = ose_otlp_encode(reinterpret_cast<ose_engine*>(p->e), bb, &outs, p->stages, OSE_GROUP_TRACE_ID,
                          reinterpret_cast<const ose_router*>(p->router), s.st, &o);
+  if (!rc) rc = take_counters(p, s, bb);
+  if (rc && o) {
+    ose_otlp_out_release(o);
+    o = nullptr;
+  }
   if (rc) r.err = ose_last_error();
   if (bb) ose_otlp_release(bb);
   r.rc = rc;
@@ -266,14 +285,12 @@ void run_alone(Pipeline* p, Slot& s, Req& r, const uint8_t* pb) {
   p->n_singles++;
 }
 
-// top-level records of a TracesData slice (each output record is one)
-uint32_t count_records(const uint8_t* d, uint64_t len) {
-  const int64_t n = count_resource_spans(d, len);
-  return n < 0 ? 0u : (uint32_t)n;
-}
+using pclk = std::chrono::steady_clock;
+double ms_since(pclk::time_point t) { return std::chrono::duration<double, std::milli>(pclk::now() - t).count(); }
 
 void run_batch(Pipeline* p, Slot& s) {
   const size_t Q = s.reqs.size();
+  const auto t0 = pclk::now();
   auto each_alone = [&]() {
     for (Req* r : s.reqs) run_alone(p, s, *r, s.msg + r->off);
   };
@@ -293,11 +310,14 @@ void run_batch(Pipeline* p, Slot& s) {
     each_alone();
     return;
   }
+  const double t_front = ms_since(t0);
+  const auto t1 = pclk::now();
   OtlpOut* whole = nullptr;
   std::vector<uint64_t> off;
   bool gpu = false;
-  rc = otlp_encode_gpu_offsets(p->e, bb, &outs, p->stages, p->router, s.st, &whole, off, &gpu);
-  if (!rc && gpu) rc = collect_counters(p, s, bb);
+  rc = issue_counters(s, bb);
+  if (!rc) rc = otlp_encode_gpu_offsets(p->e, bb, &outs, p->stages, p->router, s.st, &whole, off, &gpu);
+  if (!rc && gpu) rc = take_counters(p, s, bb);
   if (rc || !gpu) {   // an error, or a batch the GPU encoder hands to the host encoder
     if (whole) otlp_out_release(whole);
     ose_otlp_release(bb);
@@ -313,6 +333,8 @@ void run_batch(Pipeline* p, Slot& s) {
     return;
   }
   ose_otlp_release(bb);
+  const double t_enc = ms_since(t1);
+  const auto t2 = pclk::now();
   std::shared_ptr<OtlpOut> hold(whole, [](OtlpOut* o) { otlp_out_release(o); });
   const size_t n_out = whole->outs.size();
   uint64_t r0 = 0;
@@ -326,13 +348,19 @@ void run_batch(Pipeline* p, Slot& s) {
     o->outs.resize(n_out);
     for (size_t k = 0; k < n_out; k++) {
       const EncodedOutput& w = whole->outs[k];
-      const uint64_t lo = r0 < R ? off[k * R + r0] : w.len, hi = r1 < R ? off[k * R + r1] : w.len;
+      const uint64_t* ok = off.data() + k * R;
+      const uint64_t lo = r0 < R ? ok[r0] : w.len, hi = r1 < R ? ok[r1] : w.len;
       EncodedOutput& x = o->outs[k];
       x.name = w.name;
       x.data = w.data + lo;
       x.len = hi - lo;
       x.cap = 0;
-      x.n_resources = count_records(x.data, x.len);
+      // the records in the slice: resources whose record has bytes in this
+      // output (from the offsets: the output bytes are pinned memory, slow
+      // for the host to read)
+      uint32_t nr = 0;
+      for (uint64_t q = r0; q < r1; q++) nr += (q + 1 < R ? ok[q + 1] : w.len) > ok[q];
+      x.n_resources = nr;
     }
     r->out = o;
     r->rc = 0;
@@ -342,6 +370,10 @@ void run_batch(Pipeline* p, Slot& s) {
   p->n_batches++;
   p->n_requests += Q;
   p->max_batch = std::max<uint64_t>(p->max_batch, Q);
+  p->t_ms[1] += t_front;
+  p->t_ms[2] += t_enc;
+  p->t_ms[3] += ms_since(t2);
+  p->t_ms[4] += ms_since(t0);
 }
 
 int consume(Pipeline* p, const uint8_t* pb, size_t len, const ose_rand* rnd, OtlpOut** out) {
@@ -392,20 +424,34 @@ int consume(Pipeline* p, const uint8_t* pb, size_t len, const ose_rand* rnd, Otl
     break;
   }
   Slot& s = *p->slots[si];
+  // every caller copies its own bytes, outside the lock and in parallel (a
+  // leader that deferred its copy until it knew it had company measured
+  // slower: its copy then sits on the batch's critical path)
   lk.unlock();
   if (len) std::memcpy(s.msg + r.off, pb, len);
   lk.lock();
   s.copying--;
   p->cv.notify_all();
   if (s.leader == &r) {
+    const auto tw = pclk::now();
     // run when fewer than max_running batches are on the GPU; requests keep
     // joining this batch until then
     p->cv.wait(lk, [&] { return p->running < p->max_running && (s.reqs.size() >= p->hold || s.closed); });
+    if (p->window_us && p->last_q > 1 && !s.closed && s.reqs.size() < p->target) {
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(p->window_us);
+      p->cv.wait_until(lk, until, [&] { return s.closed || s.reqs.size() >= p->target; });
+    }
+    p->last_q = s.reqs.size();
     if (p->filling == si) p->filling = -1;
     s.state = Slot::Running;
     p->running++;
     p->cv.wait(lk, [&] { return s.copying == 0; });
+    const double waited = ms_since(tw);
     lk.unlock();
+    {
+      std::lock_guard<std::mutex> g(p->cmu);
+      p->t_ms[0] += waited;
+    }
     if (int brc = bind_device(p->e)) {
       for (Req* q : s.reqs) {
         q->rc = brc;
@@ -487,7 +533,9 @@ int ose_otlp_pipeline_counters(ose_otlp_pipeline* pp, char* json, size_t cap) {
     std::lock_guard<std::mutex> g(p->cmu);
     s = "{\"accepted_spans\":" + std::to_string(p->accepted) + ",\"batches\":" + std::to_string(p->n_batches) +
         ",\"batched_requests\":" + std::to_string(p->n_requests) + ",\"alone\":" + std::to_string(p->n_singles) +
-        ",\"largest_batch\":" + std::to_string(p->max_batch) + ",\"data_size\":[";
+        ",\"largest_batch\":" + std::to_string(p->max_batch) + ",\"batch_ms\":{\"wait\":" + std::to_string(p->t_ms[0]) +
+        ",\"decode_stages\":" + std::to_string(p->t_ms[1]) + ",\"encode\":" + std::to_string(p->t_ms[2]) +
+        ",\"slices\":" + std::to_string(p->t_ms[3]) + ",\"total\":" + std::to_string(p->t_ms[4]) + "},\"data_size\":[";
     bool first = true;
     for (auto& kv : p->set_bytes) {
       s += first ? "[" : ",[";
@@ -499,8 +547,26 @@ int ose_otlp_pipeline_counters(ose_otlp_pipeline* pp, char* json, size_t cap) {
     p->accepted = 0;
     p->set_bytes.clear();
     p->n_batches = p->n_requests = p->n_singles = p->max_batch = 0;
+    for (double& t : p->t_ms) t = 0;
   }
   std::memcpy(json, s.c_str(), s.size() + 1);
+  return 0;
+}
+
+// diagnostics: how many batches may be on the GPU at once (1..8; one more
+// slot fills meanwhile), the batching window and its target batch size
+int osehost_otlp_pipeline_tune(ose_otlp_pipeline* pp, uint32_t max_running, uint32_t window_us, uint32_t target) {
+  if (!pp || max_running < 1 || max_running > 8) return fail(OSE_EINVAL, "max_running must be in 1..8");
+  auto* p = reinterpret_cast<Pipeline*>(pp);
+  std::lock_guard<std::mutex> g(p->mu);
+  p->window_us = window_us;
+  p->target = std::max<uint32_t>(target, 1);
+  while (p->slots.size() < max_running + 1) {
+    p->slots.emplace_back(new Slot());
+    if (int rc = slot_init(*p->slots.back(), p->max_bytes)) return rc;
+  }
+  p->max_running = (int)max_running;
+  p->cv.notify_all();
   return 0;
 }
 

@@ -158,6 +158,7 @@ def lib() -> C.CDLL:
         "ose_otlp_pipeline_counters": (C.c_int, [_p, C.c_char_p, C.c_size_t]),
         "ose_otlp_pipeline_destroy": (None, [_p]),
         "osehost_otlp_pipeline_hold": (C.c_int, [_p, C.c_uint32]),
+        "osehost_otlp_pipeline_tune": (C.c_int, [_p, C.c_uint32, C.c_uint32, C.c_uint32]),
         "ose_engine_path_counts": (C.c_uint32, [_p, C.POINTER(C.c_uint64), C.c_uint32]),
         "ose_engine_set_option": (C.c_int, [_p, C.c_char_p, C.c_int64]),
         "ose_batch_acquire": (C.c_int, [_p, C.POINTER(Columns), C.POINTER(_p)]),

@@ -201,6 +201,7 @@ def test_gpu_pipeline_many_callers():
     reqs = [_requests(1, sizes[k % len(sizes)], 0x0D17A300 + k)[0] for k in range(24)]
     want = [_alone(eng, router, pb) for pb in reqs]
     pipe = OtlpPipeline(eng, router, max_batch_bytes=4 << 20)
+    pipe.tune(1, 500, 8)   # one batch on the GPU at a time: the others fill meanwhile
     errs = []
 
     def caller(c):

@@ -194,6 +194,10 @@ def main():
     # requests coalesced into one device batch per wave of calls
     from odigos_amd.batch import OtlpPipeline
     pipe = OtlpPipeline(eng, router, st)
+    import os
+    if os.environ.get("OSE_PIPE_RUNNING"):   # diagnostics: the product defaults otherwise (4, 200 us, 8)
+        pipe.tune(int(os.environ["OSE_PIPE_RUNNING"]), int(os.environ.get("OSE_PIPE_WINDOW_US", "200")),
+                  int(os.environ.get("OSE_PIPE_TARGET", "8")))
     for callers in (1, 4, 8, 16):
         per = 150 if callers > 1 else 120
         ready = threading.Barrier(callers + 1)
@@ -221,9 +225,10 @@ def main():
         res.setdefault("pipeline8192_callers", []).append(
             {"callers": callers, "calls": callers * per, "wall_s": wall,
              "spans_per_s": callers * per * 8192 / wall, "calls_per_s": callers * per / wall,
-             "batches": cnt["batches"], "largest_batch": cnt["largest_batch"], "alone": cnt["alone"]})
+             "batches": cnt["batches"], "largest_batch": cnt["largest_batch"], "alone": cnt["alone"],
+             "batch_ms": cnt["batch_ms"]})
         print(f"otlp pipeline 8192-span requests, {callers} callers: {callers * per * 8192 / wall / 1e6:.1f} M spans/s "
-              f"({cnt['batches']} batches, largest {cnt['largest_batch']})", flush=True)
+              f"({cnt['batches']} batches, largest {cnt['largest_batch']}, alone {cnt['alone']}, ms {cnt['batch_ms']})", flush=True)
     pipe.close()
     spin.close()
     pin.close()
