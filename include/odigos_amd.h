@@ -593,7 +593,10 @@ void ose_otlp_pipeline_destroy(ose_otlp_pipeline* p);
  * processors on it with OSE_GROUP_TRACE_ID: each trace is decided as
  * groupbytrace's one-trace ConsumeTraces call would be.  A new trace evicts
  * (drops) the one created num_traces creations earlier if it is still
- * waiting.  now_ns is the caller's clock and must not go backwards.
+ * waiting; with num_workers W > 1, the one created num_traces / W creations
+ * earlier in its own worker (worker = FNV-1 64 of the id's 16 bytes mod W, as
+ * contrib's event machine shards traces; num_traces >= W, else OSE_EINVAL).
+ * now_ns is the caller's clock and must not go backwards.
  * attrset_map (n_attrsets of the added batch, may be NULL = identity) maps
  * the batch's res_attrset ids to ids stable across batches.  The released
  * columns stay valid until the next release; OSE_ERANGE when the store is

@@ -3,7 +3,7 @@
 // v0.141.0, `collector/builder-config.yaml:73`; not in the reference tree)
 // as Odigos configures it (`autoscaler/controllers/actions/sampling/
 // groupbytrace.go:3-9`: wait_duration "30s"; num_traces and num_workers at
-// their defaults, 1,000,000 and 1):
+// their defaults, 1,000,000 and 1; other num_workers are taken too):
 //   * ConsumeTraces splits the batch per (ResourceSpans, ScopeSpans, trace
 //     id) (batchpersignal.SplitTraces) and hands each piece to the event
 //     machine in that order;
@@ -12,7 +12,11 @@
 //     arms a timer of wait_duration; later pieces append to the trace;
 //   * on expiry the trace leaves the buffer and goes downstream as one
 //     ptrace.Traces holding its pieces in arrival order; spans of that id
-//     arriving afterwards start a new trace.
+//     arriving afterwards start a new trace;
+//   * num_workers W > 1: the event machine hands a trace's events to worker
+//     fnv64(id) % W, each worker with a ring of num_traces / W ids, so a
+//     trace is evicted by the (num_traces / W)-th trace created after it in
+//     its own worker.
 // Time is the caller's clock (now_ns on every call), so releases are
 // deterministic.  The kernels are in gbt_kernel.hip.
 #include <algorithm>
@@ -102,10 +106,14 @@ struct Gbt {
   Engine* e = nullptr;
   int64_t wait_ns = 0;
   uint64_t num_traces = 1000000;
+  uint32_t W = 1;                 // num_workers
+  uint64_t ring_n = 0, wcap = 0;  // ring slots (num_traces, or the pool capacity when W > 1); num_traces / W
+  std::vector<uint64_t> wcnt;     // per worker: traces numbered
+  std::vector<uint64_t> wrel;     // per worker: its traces with seq < rel_end (released or evicted)
   uint32_t K = 0;
   uint64_t pool_cap = 0, scope_cap = 0, arena_cap = 0;
   // device state
-  DevMem table, ring, pool, scopes, arena, scratch, sortbuf, out, words;
+  DevMem table, ring, pool, scopes, arena, scratch, sortbuf, out, words, tinfo, wdev;
   uint64_t table_slots = 0;
   uint32_t epoch = 0;
   GbtPool P{};
@@ -113,7 +121,11 @@ struct Gbt {
   // host clock
   uint64_t next_seq = 0, rel_end = 0;
   uint64_t pool_begin = 0, pool_end = 0, scope_begin = 0, scope_end = 0, arena_begin = 0, arena_end = 0;
-  struct Epoch { int64_t t; uint64_t seq1, pool1, scope1, arena1; };
+  struct Epoch {
+    int64_t t;
+    uint64_t seq1, pool1, scope1, arena1;
+    std::vector<uint64_t> wcnt1;   // W > 1: the workers' counts after the call
+  };
   std::deque<Epoch> epochs;
   uint32_t n_attrsets = 0;
   int64_t last_now = INT64_MIN;   // the clock of the last successful call
@@ -128,7 +140,16 @@ struct Gbt {
   uint32_t add_gen = 0;
   bool table_valid = false;
 
-  uint64_t evict_below() const { return next_seq > num_traces ? next_seq - num_traces : 0; }
+  // one worker: the traces a ring of num_traces has evicted (W > 1: per trace, gbt_evicted)
+  uint64_t evict_below() const { return W == 1 && next_seq > num_traces ? next_seq - num_traces : 0; }
+  // W > 1: worker w's traces [0, this) are evicted
+  uint64_t w_evicted(uint32_t w) const { return wcnt[w] > wcap ? wcnt[w] - wcap : 0; }
+  uint64_t waiting() const {
+    if (W == 1) return next_seq - live_lo();
+    uint64_t n = 0;
+    for (uint32_t w = 0; w < W; w++) n += wcnt[w] - std::max(wrel[w], w_evicted(w));
+    return n;
+  }
   uint64_t live_lo() const { return std::max(rel_end, evict_below()); }
   // traces whose wait is over at `now`: [.., expired_below(now)) (created by
   // the calls at least wait_duration ago; the next release hands them out)
@@ -170,6 +191,73 @@ int words_need(Gbt* g, uint64_t n) {   // error word, scan counter, totals, one 
   return g->words.need(64 + 8 * ((n + kScanTileItems - 1) / kScanTileItems + 256 * 4 + 16));
 }
 
+// stable LSD radix sort of m (key, value) pairs on the keys' low `bits` bits
+// (the sampling stage's sort kernels: 8-bit digits, LDS histograms, look-back
+// scans); *skeys / *svals: the sorted arrays (the inputs when m <= 1 or bits == 0)
+int sort_pairs(Gbt* g, const uint32_t* keys, const uint32_t* vals, uint64_t m, int bits, hipStream_t st,
+               const uint32_t** skeys, const uint32_t** svals) {
+  *skeys = keys;
+  *svals = vals;
+  if (m <= 1 || !bits) return 0;
+  int rc;
+  const uint32_t T = (uint32_t)((m + kSortTile - 1) / kSortTile);
+  const uint32_t htiles = (uint32_t)((256ull * T + kScanTileItems - 1) / kScanTileItems);
+  if ((rc = g->sortbuf.need(4 * up(4 * m + 16) + 2 * up(4ull * 256 * T + 16))) || (rc = words_need(g, 256ull * T)))
+    return rc;
+  uint32_t* k2 = reinterpret_cast<uint32_t*>(g->sortbuf.p);
+  uint32_t* k3 = k2 + up(4 * m + 16) / 4;
+  uint32_t* v2 = k3 + up(4 * m + 16) / 4;
+  uint32_t* v3 = v2 + up(4 * m + 16) / 4;
+  uint32_t* hist = v3 + up(4 * m + 16) / 4;
+  uint32_t* hoff = hist + up(4ull * 256 * T + 16) / 4;
+  uint32_t* gate = reinterpret_cast<uint32_t*>(g->words.p) + 8;
+  HIP_TRY(hipMemsetAsync(gate, 1, 4, st));   // open
+  TraceSortArgs s{};
+  s.n_spans = m;
+  s.n_tiles = T;
+  s.gate = gate;
+  s.error = reinterpret_cast<uint32_t*>(g->words.p);
+  s.key = const_cast<uint32_t*>(keys);
+  const uint32_t* kin = keys;
+  const uint32_t* vin = vals;
+  uint32_t* kb[2] = {k2, k3};
+  uint32_t* vb[2] = {v2, v3};
+  int pass = 0;
+  for (int shift = 0; shift < bits; shift += 8, pass++) {
+    s.shift = (uint32_t)shift;
+    s.keys_in = kin;
+    s.vals_in = vin;
+    s.keys_out = kb[pass & 1];
+    s.vals_out = vb[pass & 1];
+    s.hist = hist;
+    s.scan_counter = reinterpret_cast<uint32_t*>(g->words.p) + 4;
+    s.scan_status = reinterpret_cast<uint64_t*>(g->words.p + 64);
+    s.scan_status_n = htiles;
+    launch_sort_hist(s, st);
+    HIP_TRY(hipGetLastError());
+    ScanArgs sa{};
+    sa.n = 256ull * T;
+    sa.n_tiles = htiles;
+    sa.gate = gate;
+    sa.in = hist;
+    sa.out = hoff;
+    sa.counter = s.scan_counter;
+    sa.status = s.scan_status;
+    sa.error = s.error;
+    launch_scan_u32(sa, st);
+    HIP_TRY(hipGetLastError());
+    TraceSortArgs s2 = s;
+    s2.hist = hoff;
+    launch_sort_scatter(s2, st);
+    HIP_TRY(hipGetLastError());
+    kin = kb[pass & 1];
+    vin = vb[pass & 1];
+  }
+  *skeys = kin;
+  *svals = vin;
+  return 0;
+}
+
 GbtArgs base_args(Gbt* g) {
   GbtArgs a{};
   a.table = reinterpret_cast<GbtSlot*>(g->table.p);
@@ -180,6 +268,15 @@ GbtArgs base_args(Gbt* g) {
   a.error = reinterpret_cast<uint32_t*>(g->words.p);
   a.ring_tid = reinterpret_cast<uint64_t*>(g->ring.p);
   a.num_traces = g->num_traces;
+  a.ring_n = g->ring_n;
+  a.n_workers = g->W;
+  a.worker_cap = g->wcap;
+  if (g->W > 1) {
+    a.tinfo = reinterpret_cast<uint64_t*>(g->tinfo.p);
+    a.wcnt = reinterpret_cast<const uint64_t*>(g->wdev.p);
+    a.wadd = reinterpret_cast<uint32_t*>(g->wdev.p + up(8ull * g->W));
+    a.wstart = a.wadd + up(4ull * g->W + 16) / 4;
+  }
   a.pool = g->P;
   a.pool_cap = g->pool_cap;
   a.scopes = g->Q;
@@ -187,6 +284,33 @@ GbtArgs base_args(Gbt* g) {
   a.arena_ring = g->arena.p;
   a.arena_cap = g->arena_cap;
   return a;
+}
+
+// num_workers > 1: each new trace of the add gets its worker and its number
+// within the worker (creation order), kept in tinfo; the workers' counts grow
+int number_workers(Gbt* g, GbtArgs a, uint64_t created, hipStream_t st) {
+  const uint32_t W = g->W;
+  int rc, bits = 0;
+  while (bits < 32 && ((uint64_t)(W - 1) >> bits)) bits++;
+  HIP_TRY(hipMemsetAsync(a.wadd, 0, 4ull * W, st));
+  launch_gbt_wkey(a, st);
+  HIP_TRY(hipGetLastError());
+  uint32_t* total = reinterpret_cast<uint32_t*>(g->words.p) + 3;
+  if ((rc = scan_u32(g, a.wadd, a.wstart, W, total, st))) return rc;
+  const uint32_t *skeys = nullptr, *svals = nullptr;
+  if ((rc = sort_pairs(g, a.keys, a.vals, created, bits, st, &skeys, &svals))) return rc;
+  a.keys = const_cast<uint32_t*>(skeys);
+  a.vals = const_cast<uint32_t*>(svals);
+  launch_gbt_wnum(a, created, st);
+  HIP_TRY(hipGetLastError());
+  std::vector<uint32_t> add(W);
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpyAsync(add.data(), a.wadd, 4ull * W, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&err, g->words.p, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (err) return fail(OSE_EDEVICE, "groupbytrace: device error " + std::to_string(err) + " numbering the workers' traces");
+  for (uint32_t w = 0; w < W; w++) g->wcnt[w] += add[w];
+  return 0;
 }
 
 int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t now, hipStream_t st) {
@@ -224,9 +348,13 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
   }
   if (rebuild) g->epoch++;
   g->add_gen = g->add_gen + 1 == 0 ? 1 : g->add_gen + 1;
-  // scratch: slot_of (8n), flag, rank, strlen, stroff (4n each), the attribute-set map
+  // scratch: slot_of (8n), flag, rank, strlen, stroff (4n each), the
+  // attribute-set map; W > 1: the (worker, rank) pairs (4n each)
   const size_t A = c->n_attrsets;
-  if ((rc = g->scratch.need(up(8 * n) + 4 * up(4 * n + 16) + up(4 * A + 16))) || (rc = words_need(g, n))) return rc;
+  const size_t wpairs = g->W > 1 ? 2 * up(4 * n + 16) : 0;
+  if ((rc = g->scratch.need(up(8 * n) + 4 * up(4 * n + 16) + up(4 * A + 16) + wpairs)) ||
+      (rc = words_need(g, std::max<uint64_t>(n, g->W))))
+    return rc;
   GbtArgs a = base_args(g);
   a.slot_of = reinterpret_cast<uint64_t*>(g->scratch.p);
   a.flag = reinterpret_cast<uint32_t*>(g->scratch.p + up(8 * n));
@@ -239,6 +367,12 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
     HIP_TRY(hipMemcpyAsync(dmap, attrset_map, 4 * A, hipMemcpyHostToDevice, st));
     max_set = *std::max_element(attrset_map, attrset_map + A);
     a.attrset_map = dmap;
+  }
+  if (g->W > 1) {
+    a.keys = dmap + up(4 * A + 16) / 4;
+    a.vals = a.keys + up(4 * n + 16) / 4;
+    // the workers' counts before the batch: its lookups and the rebuild skip evicted traces
+    HIP_TRY(hipMemcpyAsync(g->wdev.p, g->wcnt.data(), 8ull * g->W, hipMemcpyHostToDevice, st));
   }
   a.cols = *c;
   a.n = n;
@@ -282,6 +416,10 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
     return fail(OSE_EDEVICE, "groupbytrace: device table error " + std::to_string(h[0]));
   }
   const uint64_t created = h[1], bytes = h[2];
+  if (g->W > 1 && created && (rc = number_workers(g, a, created, st))) {
+    g->table_valid = false;
+    return rc;
+  }
   g->slots_used += created;
   g->next_seq += created;
   g->created += created;
@@ -290,7 +428,8 @@ int gbt_add(Gbt* g, const ose_columns* c, const uint32_t* attrset_map, int64_t n
   g->scope_end += S;
   g->arena_end += bytes;
   g->n_attrsets = std::max<uint32_t>(g->n_attrsets, A ? max_set + 1 : 0);
-  g->epochs.push_back(Gbt::Epoch{now, g->next_seq, g->pool_end, g->scope_end, g->arena_end});
+  g->epochs.push_back(Gbt::Epoch{now, g->next_seq, g->pool_end, g->scope_end, g->arena_end,
+                                 g->W > 1 ? g->wcnt : std::vector<uint64_t>{}});
   g->last_now = now;
   return 0;
 }
@@ -306,11 +445,26 @@ int gbt_release(Gbt* g, int64_t now, hipStream_t st, uint32_t* n_traces) {
   uint64_t b = g->rel_end;
   while (k < g->epochs.size() && g->epochs[k].t + g->wait_ns <= now) b = std::max(b, g->epochs[k++].seq1);
   const uint64_t lo = g->live_lo();
-  if (b > g->rel_end) {
-    const uint64_t ev_hi = std::min(b, g->evict_below());
-    if (ev_hi > g->rel_end) g->evicted += ev_hi - g->rel_end;   // evicted before their timer: dropped
+  const uint64_t range = b > lo ? b - lo : 0;   // the seqs the release looks at
+  uint64_t rel = range;                          // the traces it releases
+  std::vector<uint64_t> wrel1;
+  if (g->W == 1) {
+    if (b > g->rel_end) {
+      const uint64_t ev_hi = std::min(b, g->evict_below());
+      if (ev_hi > g->rel_end) g->evicted += ev_hi - g->rel_end;   // evicted before their timer: dropped
+    }
+  } else if (k) {
+    // worker w's traces in [rel_end, b) are its numbers [wrel, wrel1); those
+    // below w_evicted were evicted before their timer: dropped
+    wrel1 = g->epochs[k - 1].wcnt1;
+    uint64_t ev = 0;
+    for (uint32_t w = 0; w < g->W; w++) {
+      const uint64_t e = std::min(wrel1[w], g->w_evicted(w));
+      if (e > g->wrel[w]) ev += e - g->wrel[w];
+    }
+    g->evicted += ev;
+    rel = range - ev;
   }
-  const uint64_t rel = b > lo ? b - lo : 0;
   const uint64_t window = g->pool_end - g->pool_begin;
   int rc;
   uint64_t m = 0;
@@ -329,6 +483,7 @@ int gbt_release(Gbt* g, int64_t now, hipStream_t st, uint32_t* n_traces) {
     a.rel_hi = b;
     uint32_t* totals = reinterpret_cast<uint32_t*>(g->words.p) + 1;
     HIP_TRY(hipMemsetAsync(g->words.p, 0, 16, st));
+    if (g->W > 1) HIP_TRY(hipMemcpyAsync(g->wdev.p, g->wcnt.data(), 8ull * g->W, hipMemcpyHostToDevice, st));
     (void)hipGetLastError();
     launch_gbt_flag(a, st);
     HIP_TRY(hipGetLastError());
@@ -341,65 +496,11 @@ int gbt_release(Gbt* g, int64_t now, hipStream_t st, uint32_t* n_traces) {
     if (h[0]) return fail(OSE_EDEVICE, "groupbytrace: device error " + std::to_string(h[0]));
     m = h[1];
     // stable sort of the released spans by trace (window order = arrival order)
-    const uint32_t* order = a.vals;
     int bits = 0;
-    while (bits < 32 && ((rel - 1) >> bits)) bits++;
-    if (m > 1 && bits) {
-      const uint32_t T = (uint32_t)((m + kSortTile - 1) / kSortTile);
-      const uint32_t htiles = (uint32_t)((256ull * T + kScanTileItems - 1) / kScanTileItems);
-      if ((rc = g->sortbuf.need(4 * up(4 * m + 16) + 2 * up(4ull * 256 * T + 16))) || (rc = words_need(g, 256ull * T)))
-        return rc;
-      uint32_t* k2 = reinterpret_cast<uint32_t*>(g->sortbuf.p);
-      uint32_t* k3 = k2 + up(4 * m + 16) / 4;
-      uint32_t* v2 = k3 + up(4 * m + 16) / 4;
-      uint32_t* v3 = v2 + up(4 * m + 16) / 4;
-      uint32_t* hist = v3 + up(4 * m + 16) / 4;
-      uint32_t* hoff = hist + up(4ull * 256 * T + 16) / 4;
-      uint32_t* gate = reinterpret_cast<uint32_t*>(g->words.p) + 8;
-      HIP_TRY(hipMemsetAsync(gate, 1, 4, st));   // open
-      TraceSortArgs s{};
-      s.n_spans = m;
-      s.n_tiles = T;
-      s.gate = gate;
-      s.error = reinterpret_cast<uint32_t*>(g->words.p);
-      s.key = a.keys;
-      const uint32_t* kin = a.keys;
-      const uint32_t* vin = a.vals;
-      uint32_t* kb[2] = {k2, k3};
-      uint32_t* vb[2] = {v2, v3};
-      int pass = 0;
-      for (int shift = 0; shift < bits; shift += 8, pass++) {
-        s.shift = (uint32_t)shift;
-        s.keys_in = kin;
-        s.vals_in = vin;
-        s.keys_out = kb[pass & 1];
-        s.vals_out = vb[pass & 1];
-        s.hist = hist;
-        s.scan_counter = reinterpret_cast<uint32_t*>(g->words.p) + 4;
-        s.scan_status = reinterpret_cast<uint64_t*>(g->words.p + 64);
-        s.scan_status_n = htiles;
-        launch_sort_hist(s, st);
-        HIP_TRY(hipGetLastError());
-        ScanArgs sa{};
-        sa.n = 256ull * T;
-        sa.n_tiles = htiles;
-        sa.gate = gate;
-        sa.in = hist;
-        sa.out = hoff;
-        sa.counter = s.scan_counter;
-        sa.status = s.scan_status;
-        sa.error = s.error;
-        launch_scan_u32(sa, st);
-        HIP_TRY(hipGetLastError());
-        TraceSortArgs s2 = s;
-        s2.hist = hoff;
-        launch_sort_scatter(s2, st);
-        HIP_TRY(hipGetLastError());
-        kin = kb[pass & 1];
-        vin = vb[pass & 1];
-      }
-      order = vin;
-    }
+    while (bits < 32 && ((range - 1) >> bits)) bits++;
+    const uint32_t* order = a.vals;
+    const uint32_t* skeys = a.keys;
+    if ((rc = sort_pairs(g, a.keys, a.vals, m, bits, st, &skeys, &order))) return rc;
     // the released batch: fixed columns and fragment heads, then strings and fragments
     const uint64_t M = std::max<uint64_t>(m, 1), K = g->K;
     struct Part { void** dst; size_t bytes; };
@@ -477,6 +578,7 @@ int gbt_release(Gbt* g, int64_t now, hipStream_t st, uint32_t* n_traces) {
   g->released += rel;
   g->released_spans += m;
   g->rel_end = std::max(g->rel_end, b);
+  if (g->W > 1 && k) g->wrel = std::move(wrel1);
   if (k) {   // every span of an expired epoch belongs to a released or evicted trace
     const Gbt::Epoch& last = g->epochs[k - 1];
     g->pool_begin = last.pool1;
@@ -510,9 +612,14 @@ int ose_gbt_create(ose_engine* eng, const char* cfg_json, uint64_t span_capacity
     }
     if (!parse_go_duration(wait, g->wait_ns)) { delete g; return fail(OSE_EINVAL, "time: invalid duration \"" + wait + "\""); }
     if (const Json* nt = cfg.get("num_traces")) g->num_traces = (uint64_t)nt->i64();
-    if (const Json* nw = cfg.get("num_workers"))
-      if (nw->i64() != 1) { delete g; return fail(OSE_ENOTSUP, "groupbytrace: num_workers other than 1"); }
+    int64_t nw = 1;
+    if (const Json* w = cfg.get("num_workers")) nw = w->i64();
     if ((int64_t)g->num_traces <= 0) { delete g; return fail(OSE_EINVAL, "groupbytrace: num_traces must be positive"); }
+    if (nw <= 0 || nw > (1 << 20)) { delete g; return fail(OSE_EINVAL, "groupbytrace: num_workers must be in [1, 2^20]"); }
+    // each worker's ring holds num_traces / num_workers ids (contrib's
+    // newRingBuffer would divide by zero below one)
+    if ((uint64_t)nw > g->num_traces) { delete g; return fail(OSE_EINVAL, "groupbytrace: num_traces must be at least num_workers"); }
+    g->W = (uint32_t)nw;
   } catch (const std::exception& ex) {
     delete g;
     return fail(OSE_EINVAL, ex.what());
@@ -521,6 +628,14 @@ int ose_gbt_create(ose_engine* eng, const char* cfg_json, uint64_t span_capacity
   g->pool_cap = std::max<uint64_t>(span_capacity, 1024);
   g->scope_cap = g->pool_cap;
   g->arena_cap = std::max<uint64_t>(arena_capacity, 1 << 16);
+  // one worker: the ring is num_traces ids (every live seq is within
+  // num_traces of the newest).  W > 1: a worker's old trace can outlive
+  // num_traces newer ones of other workers, but every seq not yet released
+  // has its first span in the pool, so pool_cap slots cover them
+  g->wcap = g->num_traces / g->W;
+  g->ring_n = g->W == 1 ? g->num_traces : g->pool_cap;
+  g->wcnt.assign(g->W, 0);
+  g->wrel.assign(g->W, 0);
   const uint64_t C = g->pool_cap, K = g->K;
   struct Part { void** dst; size_t bytes; };
   std::vector<Part> parts = {
@@ -542,7 +657,8 @@ int ose_gbt_create(ose_engine* eng, const char* cfg_json, uint64_t span_capacity
   for (auto& p : sparts) stotal = up(stotal + p.bytes + 16);
   int rc;
   if ((rc = g->pool.need(total)) || (rc = g->scopes.need(stotal)) || (rc = g->arena.need(g->arena_cap)) ||
-      (rc = g->ring.need(16 * g->num_traces)) || (rc = g->words.need(1 << 16))) {
+      (rc = g->ring.need(16 * g->ring_n)) || (rc = g->words.need(1 << 16)) ||
+      (g->W > 1 && ((rc = g->tinfo.need(8 * g->ring_n)) || (rc = g->wdev.need(up(8ull * g->W) + 2 * up(4ull * g->W + 16)))))) {
     delete g;
     return rc;
   }
@@ -590,7 +706,7 @@ int ose_gbt_release(ose_gbt* gg, int64_t now_ns, void* hip_stream, const ose_col
 int ose_gbt_stats(const ose_gbt* gg, uint64_t* out8) {
   if (!gg || !out8) return fail(OSE_EINVAL, "NULL argument");
   const auto* g = reinterpret_cast<const Gbt*>(gg);
-  out8[0] = g->next_seq - g->live_lo();           // traces waiting
+  out8[0] = g->waiting();                         // traces waiting
   out8[1] = g->pool_end - g->pool_begin;          // spans held (waiting or released, not yet reclaimed)
   out8[2] = g->created;
   out8[3] = g->released;

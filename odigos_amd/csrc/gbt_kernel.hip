@@ -10,6 +10,10 @@
 //   * traces are numbered in creation order (seq, 64-bit); the ring of
 //     num_traces ids (contrib's ringBuffer) is ring_tid[seq % num_traces],
 //     so a trace created num_traces creations after another evicts it;
+//     with num_workers W > 1 each worker has its own ring of num_traces / W
+//     ids (contrib's eventMachineWorker.buffer): a trace's worker is
+//     fnv64(id) % W, its number q within the worker is kept in tinfo, and
+//     it is evicted by its worker's trace number q + num_traces / W;
 //   * the id -> seq table persists across adds (tombstones: an id whose
 //     trace is gone reclaims its own slot; the table is re-inserted from the
 //     live traces only when it grows or tombstones fill half of it); the
@@ -36,6 +40,27 @@ namespace ose {
 namespace {
 constexpr int kGbtThreads = 256;
 constexpr uint64_t kUnset = ~0ull;
+
+// contrib's workerIndexForTraceID: FNV-1 (64-bit) over the id's 16 bytes,
+// modulo the workers (ids are {hi, lo}, big-endian)
+__device__ __forceinline__ uint32_t gbt_worker(uint64_t hi, uint64_t lo, uint32_t n_workers) {
+  uint64_t h = 14695981039346656037ull;
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    h *= 1099511628211ull;
+    h ^= ((b < 8 ? hi : lo) >> (56 - 8 * (b & 7))) & 0xFFu;
+  }
+  return (uint32_t)(h % n_workers);
+}
+
+// a trace whose worker has numbered worker_cap more traces after it: the
+// last of them took its ring slot (one worker: the contiguous eviction is in
+// live_lo instead)
+__device__ __forceinline__ bool gbt_evicted(const GbtArgs& a, uint64_t seq) {
+  if (a.n_workers <= 1) return false;
+  const uint64_t t = a.tinfo[seq % a.ring_n];
+  return a.wcnt[t >> 40] > (t & ((1ull << 40) - 1)) + a.worker_cap;
+}
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -148,7 +173,7 @@ __device__ uint64_t gbt_lookup(const GbtArgs& a, uint64_t hi, uint64_t lo, uint3
       atomicMin(&s->first, pos);
       return h;
     }
-    if (seq < kGbtUnset && seq >= a.live_lo && seq < a.live_hi) return h;   // a live trace
+    if (seq < kGbtUnset && seq >= a.live_lo && seq < a.live_hi && !gbt_evicted(a, seq)) return h;   // a live trace
     // the id's last trace is gone (released, evicted, expired) or an earlier
     // add failed while numbering it: the id starts a new trace in this slot
     uint32_t expect = st;
@@ -177,7 +202,8 @@ __device__ uint64_t gbt_lookup(const GbtArgs& a, uint64_t hi, uint64_t lo, uint3
 __global__ __launch_bounds__(kGbtThreads) void gbt_rebuild_kernel(GbtArgs a) {
   for (uint64_t s = a.live_lo + (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x; s < a.live_hi;
        s += (uint64_t)gridDim.x * kGbtThreads) {
-    const uint64_t r = s % a.num_traces;
+    if (gbt_evicted(a, s)) continue;
+    const uint64_t r = s % a.ring_n;
     gbt_put(a, a.ring_tid[2 * r], a.ring_tid[2 * r + 1], s);
   }
 }
@@ -225,7 +251,7 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_assign_kernel(GbtArgs a) {
   if (i >= a.n || !a.flag[i]) return;
   const uint64_t seq = a.next_seq + a.rank[i];
   a.table[a.slot_of[i]].seq = seq;
-  const uint64_t r = seq % a.num_traces;
+  const uint64_t r = seq % a.ring_n;
   a.ring_tid[2 * r] = a.cols.trace_id[2 * i];
   a.ring_tid[2 * r + 1] = a.cols.trace_id[2 * i + 1];
 }
@@ -319,6 +345,30 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_scopes_kernel(GbtArgs a) {
   Q.scope_size[q] = c.scope_size ? c.scope_size[s] : 0;
 }
 
+// ---- per-worker numbering (num_workers > 1), after the add's kernels -------
+
+// the batch's new traces as (worker, creation rank) pairs, and how many each
+// worker gets
+__global__ __launch_bounds__(kGbtThreads) void gbt_wkey_kernel(GbtArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
+  if (i >= a.n || !a.flag[i]) return;
+  const uint32_t k = a.rank[i];
+  const uint32_t w = gbt_worker(a.cols.trace_id[2 * i], a.cols.trace_id[2 * i + 1], a.n_workers);
+  a.keys[k] = w;
+  a.vals[k] = k;
+  atomicAdd(&a.wadd[w], 1u);
+}
+
+// the pairs stably sorted by worker: the j-th is its worker's
+// (j - wstart[w])-th new trace, after the wcnt[w] it had
+__global__ __launch_bounds__(kGbtThreads) void gbt_wnum_kernel(GbtArgs a, uint64_t created) {
+  const uint64_t j = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
+  if (j >= created) return;
+  const uint32_t w = a.keys[j];
+  const uint64_t q = a.wcnt[w] + (j - a.wstart[w]);
+  a.tinfo[(a.next_seq + a.vals[j]) % a.ring_n] = (uint64_t)w << 40 | q;
+}
+
 // ---- release ---------------------------------------------------------------
 
 // the pool window's spans of released traces (seq in [rel_lo, rel_hi))
@@ -326,7 +376,7 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_flag_kernel(GbtArgs a) {
   const uint64_t w = (uint64_t)blockIdx.x * kGbtThreads + threadIdx.x;
   if (w >= a.n) return;
   const uint64_t seq = a.pool.seq[(a.pool_pos + w) % a.pool_cap];
-  a.flag[w] = seq >= a.rel_lo && seq < a.rel_hi;
+  a.flag[w] = seq >= a.rel_lo && seq < a.rel_hi && !gbt_evicted(a, seq);
 }
 
 __global__ __launch_bounds__(kGbtThreads) void gbt_compact_kernel(GbtArgs a) {
@@ -436,5 +486,9 @@ void launch_gbt_flag(const GbtArgs& a, hipStream_t st) { GBT_LAUNCH(gbt_flag_ker
 void launch_gbt_compact(const GbtArgs& a, hipStream_t st) { GBT_LAUNCH(gbt_compact_kernel, a.n); }
 void launch_gbt_gather(const GbtArgs& a, hipStream_t st) { GBT_LAUNCH(gbt_gather_kernel, a.n); }
 void launch_gbt_emit(const GbtArgs& a, hipStream_t st) { GBT_LAUNCH(gbt_emit_kernel, a.n); }
+void launch_gbt_wkey(const GbtArgs& a, hipStream_t st) { GBT_LAUNCH(gbt_wkey_kernel, a.n); }
+void launch_gbt_wnum(const GbtArgs& a, uint64_t created, hipStream_t st) {
+  if (created) hipLaunchKernelGGL(gbt_wnum_kernel, dim3(blocks_for(created)), dim3(kGbtThreads), 0, st, a, created);
+}
 
 }  // namespace ose

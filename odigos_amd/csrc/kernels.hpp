@@ -784,8 +784,18 @@ struct GbtArgs {
   uint32_t epoch;
   uint32_t n_attr_keys;
   uint32_t* error;
-  uint64_t* ring_tid;         // [2 * num_traces]
+  uint64_t* ring_tid;         // [2 * ring_n]: the id of trace seq at seq % ring_n
   uint64_t num_traces;
+  uint64_t ring_n;            // num_traces (one worker), else the pool capacity
+  // num_workers > 1 (contrib's event machine): trace seq belongs to worker
+  // fnv64(id) % n_workers, numbered q within it; tinfo[seq % ring_n] =
+  // worker << 40 | q.  It is evicted once its worker has numbered more
+  // than q + worker_cap traces (wcnt: the workers' counts the call sees)
+  uint32_t n_workers;
+  uint64_t worker_cap;
+  uint64_t* tinfo;
+  const uint64_t* wcnt;
+  uint32_t *wadd, *wstart;    // numbering: creators per worker in the batch, their exclusive scan
   uint64_t live_lo, live_hi;  // traces an added span may join (and the rebuild range)
   uint32_t add_gen;           // number of this add (tags the ids it numbers)
   uint32_t attr_words;        // attr_match words per span (word-major: batch, pool and released planes)
@@ -822,5 +832,7 @@ void launch_gbt_flag(const GbtArgs& a, hipStream_t st);
 void launch_gbt_compact(const GbtArgs& a, hipStream_t st);
 void launch_gbt_gather(const GbtArgs& a, hipStream_t st);
 void launch_gbt_emit(const GbtArgs& a, hipStream_t st);
+void launch_gbt_wkey(const GbtArgs& a, hipStream_t st);                 // creators -> (worker, rank) pairs
+void launch_gbt_wnum(const GbtArgs& a, uint64_t created, hipStream_t st);   // sorted pairs -> tinfo
 
 }  // namespace ose

@@ -13,7 +13,12 @@ behaviour, restated here independently of the engine:
   slot (evicting — dropping — the trace there) and a timer of wait_duration
   is armed;
 * when the timer fires the trace leaves the buffer and goes downstream as
-  one ptrace.Traces of its pieces in arrival order.
+  one ptrace.Traces of its pieces in arrival order;
+* num_workers W > 1: the event machine hands a trace's events to worker
+  workerIndexForTraceID(id) = FNV-1 64 of the 16 id bytes mod W, each worker
+  with its own ring buffer of num_traces // W ids (eventMachineWorker.buffer).
+  Traces released together come out in arming order here (Go's workers
+  release them concurrently).
 
 Releases happen at the caller's clock (`release(now)` fires every timer
 with deadline <= now, in arming order).  A trace whose deadline has passed
@@ -58,12 +63,26 @@ def _norm(tid: str) -> str:
     return "" if t == "0" * 32 else t
 
 
+def fnv1_64(data: bytes) -> int:
+    """hash/fnv New64 (FNV-1: multiply, then xor)"""
+    h = 0xCBF29CE484222325
+    for b in data:
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+        h ^= b
+    return h
+
+
+def worker_index(tid: str, num_workers: int) -> int:
+    return fnv1_64(bytes.fromhex(tid) if tid else bytes(16)) % num_workers
+
+
 class GroupByTraceRef:
-    def __init__(self, wait_ns: int, num_traces: int = 1_000_000):
+    def __init__(self, wait_ns: int, num_traces: int = 1_000_000, num_workers: int = 1):
         self.wait = wait_ns
-        self.size = num_traces
-        self.ring = [None] * num_traces   # instance ids
-        self.index = -1
+        self.workers = num_workers
+        self.size = num_traces // num_workers
+        self.rings = [[None] * self.size for _ in range(num_workers)]   # instance ids
+        self.index = [-1] * num_workers
         self.live = {}                    # trace id -> instance
         self.inst = {}                    # instance -> {"tid", "pieces", "deadline"}
         self.next = 0
@@ -88,8 +107,10 @@ class GroupByTraceRef:
             if tid in self.live:
                 self.inst[self.live[tid]]["pieces"].append(piece)
                 continue
-            self.index = (self.index + 1) % self.size
-            old = self.ring[self.index]
+            w = worker_index(tid, self.workers)
+            self.index[w] = (self.index[w] + 1) % self.size
+            ring = self.rings[w]
+            old = ring[self.index[w]]
             if old is not None and old in self.inst:   # evicted: dropped
                 if self.live.get(self.inst[old]["tid"]) == old:
                     del self.live[self.inst[old]["tid"]]
@@ -97,7 +118,7 @@ class GroupByTraceRef:
                 self.evicted += 1
             k = self.next
             self.next += 1
-            self.ring[self.index] = k
+            ring[self.index[w]] = k
             self.live[tid] = k
             self.inst[k] = {"tid": tid, "pieces": [piece]}
             self.timers.append((now + self.wait, k))

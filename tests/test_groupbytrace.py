@@ -9,8 +9,9 @@ release) and Go's time.ParseDuration as the store reads wait_duration.
 GPU: batches decoded from OTLP protobuf are added with a clock; every
 release equals, column by column, the host columniser over the traces the
 restatement releases at that time (their pieces in arrival order); the
-stages on a release equal the oracle; eviction under a small num_traces;
-capacity errors.
+stages on a release equal the oracle; eviction under a small num_traces,
+with one worker and with num_workers > 1 (per-worker rings); capacity
+errors.
 """
 import ctypes as C
 import random
@@ -19,7 +20,7 @@ import numpy as np
 import pytest
 
 from odigos_amd import host, native
-from tests.gbt_ref import GroupByTraceRef, split_traces
+from tests.gbt_ref import GroupByTraceRef, fnv1_64, split_traces, worker_index
 from tests.test_otlp import CFG, SEED, _arr, _http_traces, _strings, to_pb
 
 S = 1_000_000_000   # ns
@@ -60,6 +61,29 @@ def test_ref_expiry_append_recreate_evict():
     assert g.evicted == 1
     out = g.release(100 * S)
     assert [[_piece_spans(p) for p in tr] for tr in out] == [[["s3"]], [["s4"]]]
+
+
+def test_ref_fnv1_64_go_vectors():
+    # hash/fnv's golden64 vectors (FNV-1), the hash contrib's
+    # workerIndexForTraceID takes of the 16 id bytes
+    for data, h in ((b"", 0xCBF29CE484222325), (b"a", 0xAF63BD4C8601B7BE), (b"ab", 0x08326707B4EB37B8),
+                    (b"abc", 0xD8DCCA186BAFADCB)):
+        assert fnv1_64(data) == h
+
+
+def test_ref_workers_have_their_own_rings():
+    # num_workers 2, num_traces 5: two rings of 2; a worker's ids evict only each other
+    g = GroupByTraceRef(30 * S, num_traces=5, num_workers=2)
+    ids = [_tid(k) for k in range(40)]
+    w0 = [t for t in ids if worker_index(t, 2) == 0][:3]
+    w1 = [t for t in ids if worker_index(t, 2) == 1][:1]
+    assert len(w0) == 3 and len(w1) == 1
+    mk = lambda ts: host.traces(host.resource_spans({}, [host.span(t, trace_id=t) for t in ts]))  # noqa: E731
+    g.consume(mk([w1[0], w0[0], w0[1]]), 0)
+    g.consume(mk([w0[2]]), S)   # worker 0's ring of 2 is full: w0[0] goes
+    assert g.evicted == 1
+    out = g.release(40 * S)
+    assert [_piece_spans(tr[0]) for tr in out] == [[w1[0]], [w0[1]], [w0[2]]]
 
 
 @pytest.mark.parametrize("text,ns", [("30s", 30 * S), ("1m30s", 90 * S), ("1.5h", 5400 * S), ("500ms", 500_000_000),
@@ -386,3 +410,53 @@ def test_gpu_reclaimed_ids_numbered_by_first_appearance():
         ntr, got = _released_starts(shim, now + 30 * S)
         assert ntr == len(order) and got == want
         now += 40 * S
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workers,num_traces,per_batch", [(3, 13, 6), (300, 600, 160)])
+def test_gpu_num_workers_rings(workers, num_traces, per_batch):
+    # num_workers > 1: each worker's ring of num_traces // workers ids evicts
+    # only its own traces (worker = FNV-1 of the id mod workers).  Batches
+    # hold one span per id: first the ids coming back to a waiting trace, then
+    # those coming back to a gone one (evicted, expired or released), then
+    # new ids — so no creation in a batch evicts a trace an id of the same
+    # batch joins after it (the store applies eviction per add, DESIGN.md
+    # §4.7); every release equals the restatement's.  300 workers: the
+    # per-worker numbering sorts on 9-bit keys (two radix passes).
+    from odigos_amd.batch import Engine
+    rng = random.Random(0x3C0 + workers)
+    cfg = {"wait_duration": "5s", "num_traces": num_traces, "num_workers": workers}
+    shim = _Shim(Engine(CFG), cfg, span_capacity=1 << 15, arena_capacity=1 << 21)
+    ref = GroupByTraceRef(5 * S, num_traces=num_traces, num_workers=workers)
+    seen, nxt, now, total = [], 1, 0, 0
+    for step in range(30):
+        now += S
+        back = rng.sample(seen, min(len(seen), per_batch // 3))
+        ref._expire(now)
+        waiting = lambda k: ref.live.get(_tid(k)) in ref.inst  # noqa: E731
+        back = [k for k in back if waiting(k)] + [k for k in back if not waiting(k)]
+        fresh = list(range(nxt, nxt + per_batch))
+        nxt += per_batch
+        seen += fresh
+        td = _mk(back + fresh, "w%d-" % step, svc=rng.choice(["svc-a", "svc-b"]))
+        shim.add(td, now)
+        ref.consume(td, now)
+        if step % 2 == 1:
+            total += _check_release(shim, ref, now)
+    assert ref.evicted > 0
+    # (the store counts a dropped trace when a release passes it)
+    assert shim.g.stats()["waiting_traces"] == sum(1 for v in ref.live.values() if v in ref.inst)
+    total += _check_release(shim, ref, now + 10 * S)
+    st = shim.g.stats()
+    assert st["released"] == total and st["evicted"] == ref.evicted and st["waiting_traces"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_num_workers_validation():
+    from odigos_amd.batch import Engine, GroupByTrace
+    eng = Engine(CFG)
+    for cfg in ({"num_workers": 0}, {"num_workers": -2}, {"num_traces": 3, "num_workers": 4}):
+        with pytest.raises(native.OseError) as ei:
+            GroupByTrace(eng, dict(cfg, wait_duration="1s"), 1 << 12, 1 << 16)
+        assert ei.value.code == native.OSE_EINVAL
+    GroupByTrace(eng, {"wait_duration": "1s", "num_traces": 4, "num_workers": 4}, 1 << 12, 1 << 16)
