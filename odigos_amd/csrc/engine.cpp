@@ -557,13 +557,21 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   // the plan grid beside the trace stage: 16x the resident workgroups
   // (C4 7.80 -> 7.62 ms, C5 3.49 -> 3.26; 4x: 7.88 / 3.27; alone, C2, the
   // resident grid stays: 16x there is 0.64 -> 2.0 ms, profiles/r5g_plan_grid_ab.txt)
-#ifndef OSE_FORK_PLAN_MULT
-#define OSE_FORK_PLAN_MULT 16
-#endif
-  constexpr uint32_t kForkPlanMult = OSE_FORK_PLAN_MULT;
+  // The plan grid (refs form): more workgroups than fit at once, so the
+  // dispatcher balances the groups' uneven cost (a persistent grid's waves
+  // each take a fixed 1/4096 of the groups and the last ones finish late)
+  // and, beside the trace stage, interleaves the two kernels' workgroups; a
+  // wave's start costs about what a few groups do, so each wave keeps ~19
+  // groups: serialised, C4 url_plan 4.30 (resident grid) -> 4.09 (2x) ->
+  // 3.92 (4x) -> 3.82 (8x) -> 3.80 ms (16x, the multiplier this rule gives
+  // it), C2 0.531 -> 0.520 (2x, its rule) -> 0.542 (4x) -> 0.935 (8x) -> 1.90
+  // (16x) (profiles/r6s_plan_grid_serial_ab.txt)
+  const uint32_t plan_groups = (uint32_t)((n + kUrlGroup - 1) / kUrlGroup);
   if (!one_stream && !rc && defer && n >= kForkSpans) {
     if (!ws->fork) (void)hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming);
     if (!ws->join) (void)hipEventCreateWithFlags(&ws->join, hipEventDisableTiming);
+    // (the fork stream's priority, high or low, measured no different:
+    // profiles/r6u_url_stream_priority_ab.txt)
     if (ws->fork && ws->join) ust = e->take_stream();
     if (ust && (hipEventRecord(ws->fork, st) != hipSuccess || hipStreamWaitEvent(ust, ws->fork, 0) != hipSuccess)) {
       e->give_stream(ust);
@@ -572,14 +580,16 @@ int run_stages(Engine* e, const ose_columns* c, const ose_outputs* o, uint32_t m
   }
   const bool tmpl = !rc && (mask & OSE_STAGE_TEMPLATE);
   ws->beside_url = ust && tmpl;
-  if (ust && tmpl) rc = run_url(e, c, o, ust, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0, kForkPlanMult);
+  if (ust && tmpl)
+    rc = run_url(e, c, o, ust, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0, url_plan_grid_mult(plan_groups, true));
   // gateway pipeline order: odigossampling (-24) before odigosurltemplate (1)
   if (!rc && (mask & OSE_STAGE_SAMPLE)) rc = run_sampling(e, c, o, group_mode, rnd, st, ws, gate_on_host ? &sample_tail : nullptr);
   if (sample_tail && !defer) {
     rc = sample_tail();
     sample_tail = nullptr;
   }
-  if (!ust && tmpl && !rc) rc = run_url(e, c, o, st, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0);
+  if (!ust && tmpl && !rc)
+    rc = run_url(e, c, o, st, ws, url_off, &ua, (mask & OSE_STAGE_TEMPLATE_REFS) != 0, url_plan_grid_mult(plan_groups));
   if (sample_tail) {
     const int trc = sample_tail();   // always drained: the host event wait must not be skipped
     if (!rc) rc = trc;

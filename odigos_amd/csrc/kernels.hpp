@@ -143,6 +143,17 @@ inline size_t url_workspace_bytes(uint64_t n, uint64_t arena_bytes) {
   const uint64_t t = (g + kUrlScanTile - 1) / kUrlScanTile;
   return 16 + t * 8 + 256 + n * 16 + 8 + g * 32 + 512 + 256 + url_scratch_bytes(n, arena_bytes);
 }
+// refs form: the plan grid in multiples of the resident one, from the batch's
+// groups (engine.cpp run_stages); OSE_PLAN_GRID_OLD builds: 16 beside the
+// trace stage, 1 otherwise (A/B)
+#ifndef OSE_PLAN_GRID_OLD
+#define OSE_PLAN_GRID_OLD 0
+#endif
+inline uint32_t url_plan_grid_mult(uint32_t n_groups, bool forked = false) {
+  if (OSE_PLAN_GRID_OLD) return forked ? 16u : 1u;
+  const uint32_t m = n_groups / (kUrlMaxWaves * 19u);
+  return m < 1 ? 1u : m > 16 ? 16u : m;
+}
 void launch_url_plan(const UrlKernelArgs& a, hipStream_t st);
 uint32_t url_plan_waves(const UrlKernelArgs& a);   // waves of the plan grid (scratch regions)
 // refs form: the image chunk size for an arena of `cap` bytes over `waves`
