@@ -738,8 +738,10 @@ namespace {
 // renumbered for the batch (ascending cache id).  *redo: a malformed record
 // (the host walk reports it exactly).  Fills w.lay.res_ref and w.sets, *R,
 // *S and the args of the scope listing.
+// msg_in_stage: the message's H2D copy reads b->stage (a pageable caller
+// buffer went through it), so the stage is reused only after that copy
 int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len, hipStream_t st, Walked& w,
-                 uint64_t* R_out, uint64_t* S_out, OtlpResArgs* args, bool* redo) {
+                 uint64_t* R_out, uint64_t* S_out, OtlpResArgs* args, bool* redo, bool msg_in_stage) {
   *redo = false;
   std::string err;
   int rc;
@@ -811,7 +813,10 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
   }
   if (!gpu_chain) {
     if (!walk_chain(pb, len, w.lay.res_ref, err)) return fail(OSE_EINVAL, err);
-    HIP_TRY(hipStreamSynchronize(st));   // the staging buffer (the message's H2D) is reused below
+    // the staging buffer is reused below: wait for the message's H2D when it
+    // came through it (a pinned caller buffer is copied from directly, and
+    // the resource pass queues behind that copy on the stream)
+    if (msg_in_stage) HIP_TRY(hipStreamSynchronize(st));
     R = w.lay.res_ref.size();
   }
   *R_out = R;
@@ -1223,7 +1228,7 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   uint64_t R = 0, S = 0;
   if (gpu_res) {
     bool redo = false;
-    if ((rc = res_walk_gpu(o, b, pb, len, st, w, &R, &S, &ra, &redo))) return rc;
+    if ((rc = res_walk_gpu(o, b, pb, len, st, w, &R, &S, &ra, &redo, !pinned))) return rc;
     if (redo) return decode(e, pb, len, st, b, false, true);   // a malformed record: the host walk reports it
   } else {
     if (!walk(o->ctx, o->res_cache, pb, len, w, gpu_scopes)) return fail(OSE_EINVAL, w.err);
