@@ -211,7 +211,8 @@ struct OtlpBatchImpl {
   uint64_t* d_spans = nullptr;
   bool scopes_dev = false;
   DevBuf eslab, eout, emisc;
-  OtlpBatchImpl() { stage.host = true; emisc.host = true; }
+  DevBuf seth;   // pinned: the resource pass's attribute-set scan words and ids (read after the scope pass's wait)
+  OtlpBatchImpl() { stage.host = true; emisc.host = true; seth.host = true; }
 };
 
 
@@ -997,20 +998,26 @@ int res_walk_gpu(OtlpEngine* o, OtlpBatchImpl* b, const uint8_t* pb, size_t len,
   HIP_TRY(hipGetLastError());
   launch_otlp_set_apply(a.res_set, R, first, is_first, pos, list, st);
   HIP_TRY(hipGetLastError());
-  uint32_t sw[2] = {0, 0};
-  HIP_TRY(hipMemcpyAsync(sw, swords, 8, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (sw[0]) return fail(OSE_EDEVICE, "OTLP ingest: attribute-set scan error");
-  std::vector<uint32_t> ids(sw[1]);
-  if (sw[1]) HIP_TRY(hipMemcpy(ids.data(), list, 4 * (size_t)sw[1], hipMemcpyDeviceToHost));
-  {
-    std::shared_lock<std::shared_mutex> g(o->res_cache.mu);
-    w.sets.clear();
-    for (uint32_t id : ids) w.sets.push_back(o->res_cache.sets[id]);
-  }
+  // the scan's words and the batch's set ids come back behind the scope
+  // pass, whose wait the host makes anyway (res_sets_finish)
+  if ((rc = b->seth.need(4 * (RN + 2)))) return rc;
+  uint32_t* hs = reinterpret_cast<uint32_t*>(b->seth.p);
+  HIP_TRY(hipMemcpyAsync(hs, swords, 8, hipMemcpyDeviceToHost, st));
+  if (R) HIP_TRY(hipMemcpyAsync(hs + 2, list, 4 * R, hipMemcpyDeviceToHost, st));
   *args = a;
   b->d_res_scope0 = const_cast<uint32_t*>(a.scope0);
   b->d_attr_res = a.attr_res;
+  return 0;
+}
+
+// the batch's attribute sets from res_walk_gpu's copies (first appearance)
+int res_sets_finish(OtlpEngine* o, OtlpBatchImpl* b, Walked& w, hipStream_t st) {
+  HIP_TRY(hipStreamSynchronize(st));   // (the scope pass has waited already: returns at once)
+  const uint32_t* hs = reinterpret_cast<const uint32_t*>(b->seth.p);
+  if (hs[0]) return fail(OSE_EDEVICE, "OTLP ingest: attribute-set scan error");
+  std::shared_lock<std::shared_mutex> g(o->res_cache.mu);
+  w.sets.clear();
+  for (uint32_t k = 0; k < hs[1]; k++) w.sets.push_back(o->res_cache.sets[hs[2 + k]]);
   return 0;
 }
 
@@ -1248,7 +1255,12 @@ int decode(Engine* e, const uint8_t* pb, size_t len, hipStream_t st, OtlpBatchIm
   b->scopes_dev = false;
   if (gpu_scopes) {
     bool redo = false;
-    if ((rc = scope_walk_gpu(e, b, w, st, &n, &redo, gpu_res ? &ra : nullptr, S))) return rc;
+    rc = scope_walk_gpu(e, b, w, st, &n, &redo, gpu_res ? &ra : nullptr, S);
+    if (gpu_res) {   // (also before an error return or a redo: no copy into seth may stay in flight)
+      const int src = res_sets_finish(o, b, w, st);
+      if (!rc) rc = src;
+    }
+    if (rc) return rc;
     if (redo) return decode(e, pb, len, st, b, true, true);   // a scope needs the host walk: all on the host
     b->scopes_dev = true;
   } else {
