@@ -26,6 +26,12 @@ namespace ose {
 namespace {
 using namespace pbdev;
 constexpr int kOThreads = 256;
+#ifndef OSE_SPAN_STAGE
+#define OSE_SPAN_STAGE 1
+#endif
+#ifndef OSE_SPAN_KEYS_LDS
+#define OSE_SPAN_KEYS_LDS 1
+#endif
 
 // one KeyValue [s, e): key, value and its size (ProtoSizer::key_value, gogo)
 __device__ uint64_t key_value(Rd& r, uint32_t s, uint32_t e, uint32_t& ko, uint32_t& kl, Val& val) {
@@ -59,15 +65,21 @@ __device__ uint64_t key_value(Rd& r, uint32_t s, uint32_t e, uint32_t& ko, uint3
   return str_field(kl) + field_len(av);
 }
 
+// the key table the span decoder compares against: OtlpArgs' (HBM) or a
+// workgroup's LDS copy of it
+struct KeyTab {
+  const OtlpKeyDev* keys;
+  const uint8_t* bytes;
+};
 // the roles of key [o, o + l) (0 = not a key of interest)
-__device__ uint64_t key_roles(const OtlpArgs& a, Rd& r, uint32_t o, uint32_t l) {
+__device__ uint64_t key_roles(const OtlpArgs& a, const KeyTab& kt, Rd& r, uint32_t o, uint32_t l) {
   if (l >= 64 || !((a.key_lens >> l) & 1)) return 0;
   uint64_t roles = 0;
   for (uint32_t k = 0; k < a.n_keys; k++) {
-    const OtlpKeyDev kd = a.keys[k];
+    const OtlpKeyDev kd = kt.keys[k];
     if (kd.len != l) continue;
     uint32_t q = 0;
-    while (q < l && r.br.at(o + q) == a.key_bytes[kd.off + q]) q++;
+    while (q < l && r.br.at(o + q) == kt.bytes[kd.off + q]) q++;
     if (q == l) roles |= kd.roles;
   }
   return roles;
@@ -87,12 +99,12 @@ __device__ uint64_t nested_attr(Rd& r, uint32_t s, uint32_t e) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
-  const uint64_t stride = (uint64_t)gridDim.x * kOThreads;
-  for (uint64_t i = (uint64_t)blockIdx.x * kOThreads + threadIdx.x; i < a.n_spans; i += stride) {
-    const uint64_t ref = a.span_ref[i];
+// span i: every byte read goes through `base` (the arena, or a wave's LDS
+// copy of the arena bytes its spans cover); offsets stay arena offsets
+__device__ __forceinline__ void decode_span(const OtlpArgs& a, const KeyTab& kt, uint64_t i, uint64_t ref, const uint8_t* base) {
+  {
     const uint32_t s0 = (uint32_t)ref, s1 = s0 + (uint32_t)(ref >> 32);
-    Rd r(a.pb, s0, s1);
+    Rd r(base, s0, s1);
     uint64_t hi = 0, lo = 0, start = 0, end = 0;
     bool tid_nz = false, sid_nz = false, pid_nz = false;
     uint32_t ts_len = 0, name_off = 0, name_len = 0, kind = 0, flags = 0;
@@ -156,7 +168,7 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
           Val v;
           attrs_sz += field_len(key_value(r, ps, ps + pl, ko, kl, v));
           if (r.bad) break;
-          const uint64_t roles = key_roles(a, r, ko, kl) & ~found;
+          const uint64_t roles = key_roles(a, kt, r, ko, kl) & ~found;
           if (!roles) break;
           found |= roles;
           if (roles & kRoleMethodNew) mnew = v;
@@ -278,7 +290,7 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
       a.host_flag[i] = 1;
       const uint32_t slot = atomicAdd(a.host_count, 1u);
       if (slot < a.host_cap) a.host_list[slot] = (uint32_t)i;
-      continue;
+      return;
     }
     a.host_flag[i] = 0;
     for (uint32_t k = 0; k < a.n_attr_keys; k++)   // keys this span does not carry (keys past
@@ -307,6 +319,72 @@ __global__ __launch_bounds__(kOThreads) void otlp_span_kernel(OtlpArgs a) {
                         attrs_sz + varint_field(dr_attrs) + events_sz + varint_field(dr_events) + links_sz +
                         varint_field(dr_links) + field_len(st) + (flags ? 6 : 0);
     a.span_size[i] = (uint32_t)sz;
+  }
+}
+
+// one lane per span, arena bytes read from HBM through the lane's 16-byte
+// reader (batches above kSpanStageMax spans)
+// the key table into LDS when it fits (every attribute key is compared
+// byte by byte against the keys of its length)
+constexpr uint32_t kKeyLds = 128, kKeyBytesLds = 4096;
+__device__ __forceinline__ KeyTab stage_keys(const OtlpArgs& a, OtlpKeyDev* s_keys, uint32_t* s_kb) {
+  KeyTab kt{a.keys, a.key_bytes};
+  if (!OSE_SPAN_KEYS_LDS || a.n_keys == 0 || a.n_keys > kKeyLds) return kt;
+  const OtlpKeyDev last = a.keys[a.n_keys - 1];   // keys are appended in order: last.off + last.len bytes
+  const uint32_t nkb = last.off + last.len;
+  if (nkb > kKeyBytesLds) return kt;
+  for (uint32_t k = threadIdx.x; k < a.n_keys; k += blockDim.x) s_keys[k] = a.keys[k];
+  for (uint32_t c = threadIdx.x; c < (nkb + 3) / 4; c += blockDim.x) {
+    const uint8_t* p = a.key_bytes + 4 * c;   // the key blob has 16 bytes of slack
+    s_kb[c] = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+  }
+  __syncthreads();
+  return KeyTab{s_keys, reinterpret_cast<const uint8_t*>(s_kb)};
+}
+
+__global__ __launch_bounds__(kWave) void otlp_span_kernel(OtlpArgs a) {
+  __shared__ OtlpKeyDev s_keys[kKeyLds];
+  __shared__ uint32_t s_kb[kKeyBytesLds / 4];
+  const KeyTab kt = stage_keys(a, s_keys, s_kb);
+  const uint64_t stride = (uint64_t)gridDim.x * kWave;
+  for (uint64_t i = (uint64_t)blockIdx.x * kWave + threadIdx.x; i < a.n_spans; i += stride)
+    decode_span(a, kt, i, a.span_ref[i], a.pb);
+}
+
+// One wave per workgroup.  Each round the wave copies the arena bytes its 64
+// spans cover (consecutive spans sit back to back in the message) into LDS
+// with coalesced 16-byte loads, then every lane parses its span from there:
+// the lane's ~20 dependent chunk reads become LDS round trips instead of HBM
+// ones.  A round whose spans cover more than kSpanStage bytes reads the arena.
+// The 24 KB per wave caps residency, so only batches that cannot fill the
+// chip anyway (<= kSpanStageMax spans: a pipeline request batch) take it;
+// measured in profiles/r6sx_otlp_span_kernel_ab.txt.
+constexpr uint32_t kSpanStage = 24576;
+constexpr uint64_t kSpanStageMax = 65536;
+__global__ __launch_bounds__(kWave) void otlp_span_lds_kernel(OtlpArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 stage[kSpanStage / 16];
+  __shared__ OtlpKeyDev s_keys[kKeyLds];
+  __shared__ uint32_t s_kb[kKeyBytesLds / 4];
+  const KeyTab kt = stage_keys(a, s_keys, s_kb);
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kWave; i0 < a.n_spans; i0 += (uint64_t)gridDim.x * kWave) {
+    const uint64_t i = i0 + lane;
+    const bool live = i < a.n_spans;
+    const uint64_t ref = live ? a.span_ref[i] : 0;
+    const uint32_t s0 = (uint32_t)ref, s1 = s0 + (uint32_t)(ref >> 32);
+    const uint32_t lo = wave_min_u32(live ? s0 : 0xFFFFFFFFu) & ~15u;
+    const uint32_t hi = wave_max_u32(live ? s1 : 0u);
+    // chunks [lo, hi) plus one: ByteReader::word reads up to 3 bytes past a string
+    const uint32_t nchunk = ((hi + 15u) >> 4) - (lo >> 4) + 1u;
+    const uint8_t* base = a.pb;
+    if (nchunk <= kSpanStage / 16) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.pb + lo);
+      for (uint32_t c = lane; c < nchunk; c += kWave) stage[c] = src[c];
+      __syncthreads();
+      base = reinterpret_cast<const uint8_t*>(stage) - lo;
+    }
+    if (live) decode_span(a, kt, i, ref, base);
+    __syncthreads();
   }
 }
 
@@ -675,8 +753,12 @@ void launch_otlp_scope_spans(const OtlpScopeArgs& a, hipStream_t st) {
 }
 
 void launch_otlp_spans(const OtlpArgs& a, hipStream_t st) {
-  const uint64_t blocks = std::min<uint64_t>((a.n_spans + kOThreads - 1) / kOThreads, 8192);
-  if (blocks) hipLaunchKernelGGL(otlp_span_kernel, dim3((uint32_t)blocks), dim3(kOThreads), 0, st, a);
+  const uint64_t blocks = std::min<uint64_t>((a.n_spans + kWave - 1) / kWave, 32768);
+  if (!blocks) return;
+  if (OSE_SPAN_STAGE && a.n_spans <= kSpanStageMax)
+    hipLaunchKernelGGL(otlp_span_lds_kernel, dim3((uint32_t)blocks), dim3(kWave), 0, st, a);
+  else
+    hipLaunchKernelGGL(otlp_span_kernel, dim3((uint32_t)blocks), dim3(kWave), 0, st, a);
 }
 void launch_otlp_fix(const OtlpFixArgs& a, hipStream_t st) {
   const uint32_t blocks = (a.n + kOThreads - 1) / kOThreads;
