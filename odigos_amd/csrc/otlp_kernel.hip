@@ -29,12 +29,15 @@ constexpr int kOThreads = 256;
 #ifndef OSE_SPAN_STAGE
 #define OSE_SPAN_STAGE 1
 #endif
+#ifndef OSE_SPAN_WAVES
+#define OSE_SPAN_WAVES 0
+#endif
 #ifndef OSE_SPAN_KEYS_LDS
 #define OSE_SPAN_KEYS_LDS 1
 #endif
 
 // one KeyValue [s, e): key, value and its size (ProtoSizer::key_value, gogo)
-__device__ uint64_t key_value(Rd& r, uint32_t s, uint32_t e, uint32_t& ko, uint32_t& kl, Val& val) {
+__device__ OSE_PB_INL uint64_t key_value(Rd& r, uint32_t s, uint32_t e, uint32_t& ko, uint32_t& kl, Val& val) {
   const uint32_t save_i = r.i, save_end = r.end;
   r.i = s;
   r.end = e;
@@ -72,7 +75,7 @@ struct KeyTab {
   const uint8_t* bytes;
 };
 // the roles of key [o, o + l) (0 = not a key of interest)
-__device__ uint64_t key_roles(const OtlpArgs& a, const KeyTab& kt, Rd& r, uint32_t o, uint32_t l) {
+__device__ OSE_PB_INL uint64_t key_roles(const OtlpArgs& a, const KeyTab& kt, Rd& r, uint32_t o, uint32_t l) {
   if (l >= 64 || !((a.key_lens >> l) & 1)) return 0;
   uint64_t roles = 0;
   for (uint32_t k = 0; k < a.n_keys; k++) {
@@ -85,14 +88,14 @@ __device__ uint64_t key_roles(const OtlpArgs& a, const KeyTab& kt, Rd& r, uint32
   return roles;
 }
 
-__device__ bool same_bytes(Rd& r, uint32_t a0, uint32_t b0, uint32_t n) {
+__device__ OSE_PB_INL bool same_bytes(Rd& r, uint32_t a0, uint32_t b0, uint32_t n) {
   for (uint32_t q = 0; q < n; q++)
     if (r.br.at(a0 + q) != r.br.at(b0 + q)) return false;
   return true;
 }
 
 // attributes of an Event / Link: sizes only (scalar values), [s, e)
-__device__ uint64_t nested_attr(Rd& r, uint32_t s, uint32_t e) {
+__device__ OSE_PB_INL uint64_t nested_attr(Rd& r, uint32_t s, uint32_t e) {
   uint32_t ko, kl;
   Val v;
   return field_len(key_value(r, s, e, ko, kl, v));
@@ -258,7 +261,7 @@ __device__ __forceinline__ void decode_span(const OtlpArgs& a, const KeyTab& kt,
       }
     }
     // the url path source and the values AsString would have to format
-    const Val& m = (found & kRoleMethodNew) ? mnew : mold;
+    const Val m = (found & kRoleMethodNew) ? mnew : mold;
     const bool has_m = (found & (kRoleMethodNew | kRoleMethodOld)) != 0;
     bool host = r.bad || host_key;
     if (found & kRoleRoute) host |= route.type != OSE_ATTR_STR;
@@ -269,7 +272,7 @@ __device__ __forceinline__ void decode_span(const OtlpArgs& a, const KeyTab& kt,
       if (m.type != OSE_ATTR_STR) host = true;
       else if (m.len == name_len && same_bytes(r, m.off, name_off, name_len)) uf |= OSE_URL_NAME_EQ_METHOD;
       const bool client = (int32_t)kind == OSE_KIND_CLIENT;
-      const Val& tv = client ? utmpl : route;
+      const Val tv = client ? utmpl : route;
       if (found & (client ? kRoleUrlTmpl : kRoleRoute)) {
         if (tv.type != OSE_ATTR_STR) uf |= OSE_URL_TGT_NONSTR;
         else uf |= tv.len == 0 ? OSE_URL_TGT_STR_EMPTY : OSE_URL_TGT_STR;
@@ -342,7 +345,11 @@ __device__ __forceinline__ KeyTab stage_keys(const OtlpArgs& a, OtlpKeyDev* s_ke
   return KeyTab{s_keys, reinterpret_cast<const uint8_t*>(s_kb)};
 }
 
+#if OSE_SPAN_WAVES
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(OSE_SPAN_WAVES))) void otlp_span_kernel(OtlpArgs a) {
+#else
 __global__ __launch_bounds__(kWave) void otlp_span_kernel(OtlpArgs a) {
+#endif
   __shared__ OtlpKeyDev s_keys[kKeyLds];
   __shared__ uint32_t s_kb[kKeyBytesLds / 4];
   const KeyTab kt = stage_keys(a, s_keys, s_kb);
@@ -381,7 +388,8 @@ __global__ __launch_bounds__(kWave) void otlp_span_lds_kernel(OtlpArgs a) {
       const uint4* src = reinterpret_cast<const uint4*>(a.pb + lo);
       for (uint32_t c = lane; c < nchunk; c += kWave) stage[c] = src[c];
       __syncthreads();
-      base = reinterpret_cast<const uint8_t*>(stage) - lo;
+      // (integer arithmetic: the result points below the LDS array)
+      base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uint64_t>(static_cast<const void*>(stage)) - lo);
     }
     if (live) decode_span(a, kt, i, ref, base);
     __syncthreads();

@@ -8,13 +8,21 @@
 #include "../../include/odigos_amd.h"
 #include "device_common.hpp"
 
+#ifndef OSE_PB_NO_FORCE
+#define OSE_PB_INL __forceinline__
+#define OSE_PB_LOOP _Pragma("nounroll")
+#else
+#define OSE_PB_INL
+#define OSE_PB_LOOP
+#endif
+
 namespace ose {
 namespace pbdev {
 
 __device__ __forceinline__ uint32_t sov(uint64_t x) { return (uint32_t)((64 - __clzll(x | 1) + 6) / 7); }
 __device__ __forceinline__ uint64_t field_len(uint64_t l) { return 1 + sov(l) + l; }
 __device__ __forceinline__ uint64_t str_field(uint64_t l) { return l ? field_len(l) : 0; }
-__device__ __forceinline__ uint64_t varint_field(uint64_t v) { return v ? 1 + sov(v) : 0; }
+__device__ OSE_PB_INL uint64_t varint_field(uint64_t v) { return v ? 1 + sov(v) : 0; }
 
 struct Rd {
   ByteReader br;
@@ -22,8 +30,9 @@ struct Rd {
   bool bad;
   __device__ Rd(const uint8_t* base, uint32_t s, uint32_t e) : br(base), i(s), end(e), bad(false) {}
   __device__ __forceinline__ bool more() const { return !bad && i < end; }
-  __device__ uint64_t varint() {
+  __device__ OSE_PB_INL uint64_t varint() {
     uint64_t v = 0;
+    OSE_PB_LOOP
     for (uint32_t s = 0; s < 64; s += 7) {
       if (i >= end) break;
       const uint32_t b = br.at(i++);
@@ -33,15 +42,16 @@ struct Rd {
     bad = true;
     return 0;
   }
-  __device__ uint64_t fixed(uint32_t nb) {
+  __device__ OSE_PB_INL uint64_t fixed(uint32_t nb) {
     if (i + nb > end) { bad = true; return 0; }
     uint64_t v = 0;
+    OSE_PB_LOOP
     for (uint32_t k = 0; k < nb; k++) v |= (uint64_t)br.at(i + k) << (8 * k);
     i += nb;
     return v;
   }
   // LEN payload [s, s + l)
-  __device__ bool len(uint32_t& s, uint32_t& l) {
+  __device__ OSE_PB_INL bool len(uint32_t& s, uint32_t& l) {
     const uint64_t x = varint();
     if (bad || x > end - i) { bad = true; return false; }
     s = i;
@@ -50,7 +60,7 @@ struct Rd {
     return true;
   }
   // an unknown field (groups go to the host pass)
-  __device__ bool skip(uint32_t wt) {
+  __device__ OSE_PB_INL bool skip(uint32_t wt) {
     uint32_t s, l;
     switch (wt) {
       case 0: varint(); break;
@@ -61,7 +71,7 @@ struct Rd {
     }
     return !bad;
   }
-  __device__ bool tag(uint32_t& f, uint32_t& wt) {
+  __device__ OSE_PB_INL bool tag(uint32_t& f, uint32_t& wt) {
     const uint64_t t = varint();
     f = (uint32_t)(t >> 3);
     wt = (uint32_t)(t & 7);
@@ -80,7 +90,7 @@ struct Val {
 
 // AnyValue [s, e): the last oneof field wins; returns its pdata size
 // contribution (ProtoSizer::any_value) or sets nested / bad
-__device__ inline uint64_t any_value(Rd& r, uint32_t s, uint32_t e, Val& out) {
+__device__ OSE_PB_INL uint64_t any_value(Rd& r, uint32_t s, uint32_t e, Val& out) {
   const uint32_t save_i = r.i, save_end = r.end;
   r.i = s;
   r.end = e;
