@@ -29,8 +29,10 @@ constexpr int kOThreads = 256;
 #ifndef OSE_SPAN_STAGE
 #define OSE_SPAN_STAGE 1
 #endif
+// waves per SIMD the HBM-read span kernel is compiled for: 3 (<= 168 VGPRs,
+// a few spills) beats 2 (184 VGPRs) and 4 (117 spilled VGPRs), r6sv
 #ifndef OSE_SPAN_WAVES
-#define OSE_SPAN_WAVES 0
+#define OSE_SPAN_WAVES 3
 #endif
 #ifndef OSE_SPAN_KEYS_LDS
 #define OSE_SPAN_KEYS_LDS 1
