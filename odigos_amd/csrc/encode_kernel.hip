@@ -30,6 +30,12 @@ namespace ose {
 namespace {
 using namespace pbdev;
 constexpr int kEThreads = 256;
+// the per-record passes' (spans, scopes, resources, write) workgroup size: one
+// wave (a request's few records over more CUs; r6se / r6sg)
+#ifndef OSE_ETHREADS
+#define OSE_ETHREADS 64
+#endif
+constexpr int kERec = OSE_ETHREADS;
 
 __device__ __forceinline__ bool eq_lit(ByteReader& br, uint32_t o, uint32_t n, const char* lit, uint32_t ln) {
   if (n != ln) return false;
@@ -50,10 +56,10 @@ __device__ __forceinline__ void flag(const EncArgs& a, uint32_t f) { atomicOr(a.
 // Enc::rewrite / plan_edit (otlp_encode.cpp) for the spans whose encoding is
 // pdata's; a span that is not (span_size != its length) is re-marshaled by
 // the host encoder, so it flags the call.
-__global__ __launch_bounds__(kEThreads) void enc_span_kernel(EncArgs a) {
-  const uint64_t stride = (uint64_t)gridDim.x * kEThreads;
+__global__ __launch_bounds__(kERec) void enc_span_kernel(EncArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * kERec;
   uint32_t fb = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * kEThreads + threadIdx.x; i < a.n_spans; i += stride) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kERec + threadIdx.x; i < a.n_spans; i += stride) {
     if (a.keep && !a.keep[i]) {
       a.span_out[i] = 0;
       continue;
@@ -187,8 +193,8 @@ __global__ __launch_bounds__(kEThreads) void enc_span_kernel(EncArgs a) {
 // Enc::size_chunk's scope loop: header (pdata always writes the
 // InstrumentationScope, "0A 00" when empty), spans, schema_url; a scope whose
 // spans were all dropped is removed.
-__global__ __launch_bounds__(kEThreads) void enc_scope_kernel(EncArgs a) {
-  const uint64_t s = (uint64_t)blockIdx.x * kEThreads + threadIdx.x;
+__global__ __launch_bounds__(kERec) void enc_scope_kernel(EncArgs a) {
+  const uint64_t s = (uint64_t)blockIdx.x * kERec + threadIdx.x;
   if (s >= a.n_scopes) return;
   const uint64_t i0 = a.scope_span0[s], i1 = s + 1 < a.n_scopes ? a.scope_span0[s + 1] : a.n_spans;
   const uint64_t h = a.scope_hdr[s];
@@ -310,8 +316,8 @@ __device__ uint64_t route_resource(const EncArgs& a, uint32_t s, uint32_t e, boo
 }  // namespace
 
 // Enc::size_chunk's resource loop, and its outputs (Enc::outputs_of)
-__global__ __launch_bounds__(kEThreads) void enc_res_kernel(EncArgs a) {
-  const uint64_t rr = (uint64_t)blockIdx.x * kEThreads + threadIdx.x;
+__global__ __launch_bounds__(kERec) void enc_res_kernel(EncArgs a) {
+  const uint64_t rr = (uint64_t)blockIdx.x * kERec + threadIdx.x;
   if (rr >= a.n_res) return;
   const uint64_t ref = a.res_ref[rr];
   const uint32_t ro = (uint32_t)ref, rl = (uint32_t)(ref >> 32);
@@ -586,9 +592,9 @@ __device__ void write_record(const EncArgs& a, uint64_t r, uint8_t* dst, uint64_
 }  // namespace
 
 // a wave per resource (grid-stride), its record to every output it routes to
-__global__ __launch_bounds__(kEThreads) void enc_write_kernel(EncArgs a) {
-  const uint64_t waves = (uint64_t)gridDim.x * (kEThreads / kWave);
-  for (uint64_t r = uni64((uint64_t)blockIdx.x * (kEThreads / kWave) + (threadIdx.x >> 6)); r < a.n_res; r += waves) {
+__global__ __launch_bounds__(kERec) void enc_write_kernel(EncArgs a) {
+  const uint64_t waves = (uint64_t)gridDim.x * (kERec / kWave);
+  for (uint64_t r = uni64((uint64_t)blockIdx.x * (kERec / kWave) + (threadIdx.x >> 6)); r < a.n_res; r += waves) {
     const uint64_t rec = uni64(a.res_rec[r]);
     if (rec == 0) continue;
     uint64_t mask = uni64(a.res_mask[r]);
@@ -602,18 +608,21 @@ __global__ __launch_bounds__(kEThreads) void enc_write_kernel(EncArgs a) {
 
 // ---- launchers ---------------------------------------------------------------------
 namespace {
+// blocks of kERec threads for n threads' work, at most cap x (kEThreads / kERec) (the
+// same resident thread count whatever the block size)
 inline uint32_t grid_of(uint64_t n, uint32_t cap) {
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + kEThreads - 1) / kEThreads, cap));
+  const uint64_t c = cap == ~0u ? cap : (uint64_t)cap * (kEThreads / kERec);
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + kERec - 1) / kERec, c));
 }
 }  // namespace
 void launch_enc_spans(const EncArgs& a, hipStream_t st) {
-  if (a.n_spans) hipLaunchKernelGGL(enc_span_kernel, dim3(grid_of(a.n_spans, 8192)), dim3(kEThreads), 0, st, a);
+  if (a.n_spans) hipLaunchKernelGGL(enc_span_kernel, dim3(grid_of(a.n_spans, 8192)), dim3(kERec), 0, st, a);
 }
 void launch_enc_scopes(const EncArgs& a, hipStream_t st) {
-  if (a.n_scopes) hipLaunchKernelGGL(enc_scope_kernel, dim3(grid_of(a.n_scopes, ~0u)), dim3(kEThreads), 0, st, a);
+  if (a.n_scopes) hipLaunchKernelGGL(enc_scope_kernel, dim3(grid_of(a.n_scopes, ~0u)), dim3(kERec), 0, st, a);
 }
 void launch_enc_resources(const EncArgs& a, hipStream_t st) {
-  if (a.n_res) hipLaunchKernelGGL(enc_res_kernel, dim3(grid_of(a.n_res, ~0u)), dim3(kEThreads), 0, st, a);
+  if (a.n_res) hipLaunchKernelGGL(enc_res_kernel, dim3(grid_of(a.n_res, ~0u)), dim3(kERec), 0, st, a);
 }
 void launch_enc_scan(const EncArgs& a, hipStream_t st) {
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (a.n_res + kEncTiles - 1) / kEncTiles);
@@ -622,7 +631,7 @@ void launch_enc_scan(const EncArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(enc_scan_apply_kernel, dim3(tiles, a.n_out), dim3(kEThreads), 0, st, a, tiles);
 }
 void launch_enc_write(const EncArgs& a, hipStream_t st) {
-  if (a.n_res) hipLaunchKernelGGL(enc_write_kernel, dim3(grid_of(a.n_res * kWave, 16384)), dim3(kEThreads), 0, st, a);
+  if (a.n_res) hipLaunchKernelGGL(enc_write_kernel, dim3(grid_of(a.n_res * kWave, 16384)), dim3(kERec), 0, st, a);
 }
 
 }  // namespace ose
